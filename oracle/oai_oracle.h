@@ -1,0 +1,129 @@
+/*
+ * CPU ORACLE — TEST INFRASTRUCTURE ONLY.
+ *
+ * Plain-C restatement of the reference's LTE PDSCH transmit path
+ * (erlgo/openair4G openair1/PHY), used exclusively as the parity checker by
+ * tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg.  Nothing in
+ * the product library (openair4g_amd/) links or calls it.
+ *
+ * Pinning:
+ *   - IDFT/OFDM: checked bit-exactly against the reference's own lte_dfts.c,
+ *     compiled unmodified from /root/reference into oracle/_ref (Makefile here).
+ *   - get_G / TBS plumbing: REFERENCE_DATA/pdsch.txt known answers.
+ *   - CRC-24A/B: published CRC-catalogue check values (CRC-24/LTE-A, -B).
+ *   - Turbo encoder, sub-block interleaver, rate matcher, scrambling and the
+ *     RE mapper: the reference TUs are unbuildable here (they include
+ *     PHY/defs.h -> openair2/COMMON/platform_constants.h:40 -> asn1c-generated
+ *     asn1_constants.h, and the SSE encoder needs the missing
+ *     lte_interleaver.h blob).  These stages are pinned by an independent
+ *     36.212 textbook model (tests/spec_model.py) plus structural properties;
+ *     DESIGN.md records them as "parity pinned to spec, not to reference output".
+ */
+#ifndef OAI_ORACLE_H
+#define OAI_ORACLE_H
+#include <stdint.h>
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define ORC_LTE_NULL 2
+#define ORC_NSOFT 1827072
+
+/* ---- CRC (crc_byte.c:98-153) ---- */
+void     orc_crc_init(void);
+uint32_t orc_crc24a(const uint8_t *in, int bitlen); /* returns crc<<8 like the reference */
+uint32_t orc_crc24b(const uint8_t *in, int bitlen);
+
+/* ---- segmentation (lte_segmentation.c:39-170) ---- */
+int orc_segmentation(const uint8_t *b, uint8_t **c, uint32_t B, uint32_t *C, uint32_t *Cplus,
+                     uint32_t *Cminus, uint32_t *Kplus, uint32_t *Kminus, uint32_t *F);
+
+/* ---- turbo encoder (3gpplte_sse.c:380-476 / 3gpplte.c:116-230) ---- */
+void orc_turbo_encode(const uint8_t *c, uint16_t nbytes, uint8_t *d /* 3K+12 */, uint16_t f1, uint16_t f2);
+
+/* ---- sub-block interleaver (lte_rate_matching.c:51-130); d must have 96 bytes of
+ *      LTE_NULL readable in front of it ---- */
+uint32_t orc_subblock_interleave(uint32_t D, uint8_t *d, uint8_t *w);
+
+/* ---- rate matching (lte_rate_matching.c:464-634) ---- */
+uint32_t orc_rate_match(uint32_t RTC, uint32_t G, const uint8_t *w, uint8_t *e, uint8_t C,
+                        uint32_t Nsoft, uint8_t Mdlharq, uint8_t Kmimo, uint8_t rvidx, uint8_t Qm,
+                        uint8_t Nl, uint8_t r);
+
+/* ---- Gold sequence / scrambling (lte_gold.c:151-177, dlsch_scrambling.c:51-97) ---- */
+uint32_t orc_gold_generic(uint32_t *x1, uint32_t *x2, uint8_t reset);
+void     orc_scramble(uint8_t *e, int G, uint32_t c_init);
+
+/* ---- MCS / G (lte_mcs.c:45-368) ---- */
+uint8_t orc_get_Qm(uint8_t mcs);
+int     orc_get_G(uint16_t N_RB_DL, uint8_t Ncp, uint8_t mode1_flag, uint8_t frame_type, uint16_t nb_rb,
+                  const uint32_t *rb_alloc, uint8_t Qm, uint8_t Nl, uint8_t num_pdcch_symbols,
+                  uint8_t subframe);
+
+/* ---- frame parameters (lte_parms.c:31-145) ---- */
+typedef struct {
+  uint16_t N_RB_DL;
+  uint16_t Nid_cell;
+  uint8_t Ncp;            /* 0 = normal */
+  uint8_t nushift;
+  uint8_t mode1_flag;
+  uint8_t nb_antennas_tx;
+  uint8_t frame_type;     /* 0 = FDD, 1 = TDD */
+  uint8_t symbols_per_tti;
+  uint8_t log2_symbol_size;
+  uint16_t ofdm_symbol_size;
+  uint16_t first_carrier_offset;
+  uint16_t nb_prefix_samples;
+  uint16_t nb_prefix_samples0;
+  uint32_t samples_per_tti;
+} orc_frame_t;
+int orc_init_frame(orc_frame_t *fp, uint16_t N_RB_DL, uint16_t Nid_cell, uint8_t Ncp, uint8_t nb_antennas_tx,
+                   uint8_t mode1_flag, uint8_t frame_type);
+
+/* ---- modulation + RE mapping (dlsch_modulation.c:139-1493) ----
+ * mimo_mode: 0 = SISO, 1 = ALAMOUTI (not restated), 2 = LARGE_CDD */
+typedef struct {
+  const uint8_t *e;
+  uint8_t mcs;
+  uint8_t mimo_mode;
+  uint8_t Nlayers;
+  uint32_t rb_alloc[4];
+} orc_cw_t;
+int orc_modulation(int32_t **txdataF, int16_t amp, uint32_t subframe, const orc_frame_t *fp,
+                   uint8_t num_pdcch_symbols, const orc_cw_t *cw0, const orc_cw_t *cw1,
+                   int16_t sqrt_rho_a, int16_t sqrt_rho_b);
+
+/* ---- fixed-point IDFT (lte_dfts.c:1597-2866) and OFDM modulation (ofdm_mod.c:47-229) ---- */
+void orc_idft(int log2n, const int16_t *x, int16_t *y, int scale);
+void orc_twiddle(int N, int m, int16_t *re, int16_t *im);
+void orc_ofdm_mod(const int32_t *input, int32_t *output, uint8_t log2fftsize, uint8_t nb_symbols,
+                  uint16_t nb_prefix_samples);
+void orc_normal_prefix_mod(const int32_t *txdataF, int32_t *txdata, uint8_t nsymb, const orc_frame_t *fp);
+
+/* ---- whole-subframe TX (dlsim.c:2567-2699 minus DCI/pilots) ----
+ * payload[cw] holds TBS/8 bytes (+3 bytes of room; the CRC is appended in place as in the
+ * reference).  txdata[ant] receives samples_per_tti int32 samples.  Returns 0 on success. */
+typedef struct {
+  orc_frame_t fp;
+  uint8_t n_cw;
+  uint8_t mimo_mode;
+  uint8_t num_pdcch_symbols;
+  uint8_t subframe;
+  uint16_t rnti;
+  int16_t amp;
+  int16_t sqrt_rho_a, sqrt_rho_b;
+  uint8_t Kmimo, Mdlharq;
+  uint32_t rb_alloc[4];
+  uint16_t nb_rb;
+  uint8_t mcs[2];
+  uint8_t rvidx[2];
+  uint8_t q[2];            /* scrambling codeword index (dlsim.c:2646 passes 0) */
+  uint32_t TBS[2];
+} orc_tx_cfg_t;
+int orc_tx_subframe(const orc_tx_cfg_t *cfg, uint8_t *payload[2], int32_t **txdataF, int32_t **txdata,
+                    uint8_t *e_out[2] /* optional: scrambled e bytes per cw */);
+
+#ifdef __cplusplus
+}
+#endif
+#endif
