@@ -1,0 +1,229 @@
+/*
+ * openair4g_amd — MI355X-native LTE PDSCH transmit path, C ABI.
+ *
+ * Two surfaces:
+ *
+ *  1. Drop-in entry points mirroring the reference call surface of the DLSCH transmit path
+ *     (erlgo/openair4G openair1/PHY).  Same argument meaning, same in-place side effects on
+ *     caller-owned buffers, same return conventions; host buffers in, host buffers out, the
+ *     arithmetic runs on the GPU.  The reference passes its own LTE_DL_FRAME_PARMS /
+ *     LTE_eNB_DLSCH_t; here the fields the path touches are mirrored in oai4g_frame_parms_t /
+ *     oai4g_dlsch_t (the reference-side shim that fills them is in INTEGRATION.md).
+ *
+ *  2. A batched, device-resident API (oai4g_tx_*) that runs whole subframes
+ *     (encode -> rate-match -> scramble -> modulate/map -> IDFT + CP) for many subframes per
+ *     launch, with payloads already in HBM.  This is the throughput path.
+ *
+ * Every entry point that computes returns/records an error if the HIP runtime or a gfx950
+ * device is unavailable: there is no CPU fallback.  oai4g_last_error() gives the message.
+ */
+#ifndef OAI4G_H
+#define OAI4G_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define OAI4G_LTE_NULL 2                    /* PHY/CODING/defs.h:53 */
+#define OAI4G_NSOFT 1827072                 /* PHY/LTE_TRANSPORT/defs.h:62 */
+#define OAI4G_MAX_SEGMENTS 16               /* PHY/LTE_TRANSPORT/defs.h:67 */
+#define OAI4G_MAX_CHANNEL_BITS (14 * 1200 * 6)
+#define OAI4G_D_BYTES (96 + 12 + 3 + 3 * 6144)
+#define OAI4G_W_BYTES (3 * 6144 + 96)
+
+/* MIMO_mode_t subset (PHY/impl_defs_lte.h) */
+enum { OAI4G_SISO = 0, OAI4G_ALAMOUTI = 1, OAI4G_LARGE_CDD = 2 };
+/* Extension_t (PHY/MODULATION/defs.h) */
+enum { OAI4G_CYCLIC_PREFIX = 0, OAI4G_CYCLIC_SUFFIX = 1, OAI4G_ZEROS = 2, OAI4G_NONE = 3 };
+
+/* Fields of LTE_DL_FRAME_PARMS (PHY/impl_defs_lte.h:470-572) used on this path. */
+typedef struct {
+  uint16_t N_RB_DL;
+  uint16_t Nid_cell;
+  uint8_t Ncp;              /* 0 = normal CP, 1 = extended */
+  uint8_t nushift;          /* Nid_cell % 6 */
+  uint8_t mode1_flag;       /* 1 = single-port CRS (TM1) */
+  uint8_t nb_antennas_tx;
+  uint8_t frame_type;       /* 0 = FDD, 1 = TDD */
+  uint8_t symbols_per_tti;
+  uint8_t log2_symbol_size;
+  uint8_t pad0;
+  uint16_t ofdm_symbol_size;
+  uint16_t first_carrier_offset;
+  uint16_t nb_prefix_samples;
+  uint16_t nb_prefix_samples0;
+  uint32_t samples_per_tti;
+} oai4g_frame_parms_t;
+
+/* LTE_DL_eNB_HARQ_t (PHY/LTE_TRANSPORT/defs.h:104-169), path fields only. */
+typedef struct {
+  uint32_t TBS;
+  uint32_t B;
+  uint8_t *b;
+  uint8_t *c[OAI4G_MAX_SEGMENTS];
+  uint32_t RTC[OAI4G_MAX_SEGMENTS];
+  uint8_t round;
+  uint8_t mcs;
+  uint8_t rvidx;
+  uint8_t mimo_mode;
+  uint32_t rb_alloc[4];
+  uint16_t nb_rb;
+  uint8_t *e;                              /* OAI4G_MAX_CHANNEL_BITS bytes */
+  uint8_t *d[OAI4G_MAX_SEGMENTS];          /* OAI4G_D_BYTES; first 96 = LTE_NULL */
+  uint8_t *w[OAI4G_MAX_SEGMENTS];          /* OAI4G_W_BYTES */
+  uint32_t C, Cminus, Cplus, Kminus, Kplus, F;
+  uint8_t Nl;
+  uint8_t Nlayers;
+  uint8_t first_layer;
+} oai4g_dl_harq_t;
+
+/* LTE_eNB_DLSCH_t (PHY/LTE_TRANSPORT/defs.h:240-274), path fields only. */
+typedef struct {
+  uint16_t rnti;
+  uint8_t current_harq_pid;
+  uint8_t Mdlharq;
+  uint8_t Kmimo;
+  int16_t sqrt_rho_a;
+  int16_t sqrt_rho_b;
+  oai4g_dl_harq_t *harq_processes[8];
+} oai4g_dlsch_t;
+
+/* ---------------- library / device ---------------- */
+int oai4g_init(void);                       /* idempotent; 0 on success, <0 if no usable GPU */
+const char *oai4g_last_error(void);
+int oai4g_device_name(char *buf, int len);
+
+/* ---------------- parameter helpers (host-side, scalar) ---------------- */
+/* init_frame_parms (PHY/INIT/lte_parms.c:31), osf = 1 */
+int oai4g_init_frame_parms(oai4g_frame_parms_t *fp, uint16_t N_RB_DL, uint16_t Nid_cell, uint8_t Ncp,
+                           uint8_t nb_antennas_tx, uint8_t mode1_flag, uint8_t frame_type);
+/* get_Qm (lte_mcs.c:45), get_G (lte_mcs.c:336) */
+uint8_t oai4g_get_Qm(uint8_t mcs);
+int oai4g_get_G(const oai4g_frame_parms_t *fp, uint16_t nb_rb, const uint32_t *rb_alloc, uint8_t mod_order,
+                uint8_t Nl, uint8_t num_pdcch_symbols, int frame, uint8_t subframe);
+/* new_eNB_dlsch / free_eNB_dlsch (dlsch_coding.c:120 / :85) */
+oai4g_dlsch_t *oai4g_new_dlsch(uint8_t Kmimo, uint8_t Mdlharq, uint8_t N_RB_DL);
+void oai4g_free_dlsch(oai4g_dlsch_t *dlsch);
+/* lte_gold_generic (PHY/LTE_REFSIG/lte_gold.c:151): scalar 32-bit LFSR helper, host-side */
+uint32_t oai4g_lte_gold_generic(uint32_t *x1, uint32_t *x2, uint8_t reset);
+
+/* ---------------- drop-in entry points (GPU compute on host buffers) ---------------- */
+/* crc24a / crc24b (PHY/CODING/crc_byte.c:117 / :135): returns crc << 8 */
+uint32_t oai4g_crc24a(const uint8_t *in, int bitlen);
+uint32_t oai4g_crc24b(const uint8_t *in, int bitlen);
+/* lte_segmentation (PHY/CODING/lte_segmentation.c:39) */
+int oai4g_lte_segmentation(const uint8_t *input_buffer, uint8_t **output_buffers, uint32_t B, uint32_t *C,
+                           uint32_t *Cplus, uint32_t *Cminus, uint32_t *Kplus, uint32_t *Kminus, uint32_t *F);
+/* threegpplte_turbo_encoder (PHY/CODING/3gpplte_sse.c:380, decl CODING/defs.h:315) */
+void oai4g_threegpplte_turbo_encoder(const uint8_t *input, uint16_t input_length_bytes, uint8_t *output,
+                                     uint8_t F, uint16_t interleaver_f1, uint16_t interleaver_f2);
+/* sub_block_interleaving_turbo (lte_rate_matching.c:51, decl CODING/defs.h:112).
+ * d points at &d[96] of a buffer whose 96 preceding bytes are readable (LTE_NULL). */
+uint32_t oai4g_sub_block_interleaving_turbo(uint32_t D, uint8_t *d, uint8_t *w);
+/* lte_rate_matching_turbo (lte_rate_matching.c:464, decl CODING/defs.h:191) */
+uint32_t oai4g_lte_rate_matching_turbo(uint32_t RTC, uint32_t G, const uint8_t *w, uint8_t *e, uint8_t C,
+                                       uint32_t Nsoft, uint8_t Mdlharq, uint8_t Kmimo, uint8_t rvidx,
+                                       uint8_t Qm, uint8_t Nl, uint8_t r, uint8_t nb_rb, uint8_t m);
+/* dlsch_encoding (PHY/LTE_TRANSPORT/dlsch_coding.c:254, decl proto.h:110) */
+int oai4g_dlsch_encoding(uint8_t *a, const oai4g_frame_parms_t *frame_parms, uint8_t num_pdcch_symbols,
+                         oai4g_dlsch_t *dlsch, int frame, uint8_t subframe);
+/* dlsch_scrambling (PHY/LTE_TRANSPORT/dlsch_scrambling.c:51, decl proto.h:1600) */
+void oai4g_dlsch_scrambling(const oai4g_frame_parms_t *frame_parms, int mbsfn_flag, oai4g_dlsch_t *dlsch, int G,
+                            uint8_t q, uint8_t Ns);
+/* dlsch_modulation (PHY/LTE_TRANSPORT/dlsch_modulation.c:1181, decl proto.h:197).
+ * txdataF[aa] is the caller's whole-frame grid as in the reference (indexed by
+ * ofdm_symbol_size*(l + subframe_offset*nsymb)).  Returns REs allocated, or -1. */
+int oai4g_dlsch_modulation(int32_t **txdataF, int16_t amp, uint32_t subframe_offset,
+                           const oai4g_frame_parms_t *frame_parms, uint8_t num_pdcch_symbols,
+                           oai4g_dlsch_t *dlsch0, oai4g_dlsch_t *dlsch1);
+/* PHY_ofdm_mod (PHY/MODULATION/ofdm_mod.c:85, decl MODULATION/defs.h:48); CYCLIC_PREFIX only */
+void oai4g_PHY_ofdm_mod(const int32_t *input, int32_t *output, uint8_t log2fftsize, uint8_t nb_symbols,
+                        uint16_t nb_prefix_samples, int etype);
+/* normal_prefix_mod (ofdm_mod.c:47, decl MODULATION/defs.h:88) */
+void oai4g_normal_prefix_mod(const int32_t *txdataF, int32_t *txdata, uint8_t nsymb,
+                             const oai4g_frame_parms_t *frame_parms);
+/* do_OFDM_mod (ofdm_mod.c:233, decl MODULATION/defs.h:90); PMCH subframes not supported */
+void oai4g_do_OFDM_mod(int32_t **txdataF, int32_t **txdata, uint32_t frame, uint16_t next_slot,
+                       const oai4g_frame_parms_t *frame_parms);
+/* idft64..idft2048 (PHY/TOOLS/lte_dfts.c:1856-2866, decl TOOLS/defs.h:555): y = IDFT(x) */
+int oai4g_idft(int log2n, const int16_t *x, int16_t *y, int scale);
+void oai4g_idft2048(const int16_t *x, int16_t *y, int scale);
+void oai4g_idft1024(const int16_t *x, int16_t *y, int scale);
+void oai4g_idft256(const int16_t *x, int16_t *y, int scale);
+void oai4g_idft128(const int16_t *x, int16_t *y, int scale);
+void oai4g_idft64(const int16_t *x, int16_t *y, int scale);
+
+/* ---------------- batched device-resident transmit path ---------------- */
+/* Plain-old-data parameter block: what rank 0 broadcasts (RCCL) to the other ranks. */
+typedef struct {
+  uint16_t N_RB_DL;
+  uint16_t Nid_cell;
+  uint8_t Ncp;
+  uint8_t nb_antennas_tx;
+  uint8_t mode1_flag;
+  uint8_t frame_type;
+  uint8_t n_cw;               /* 1 (TM1) or 2 (TM3) */
+  uint8_t mimo_mode;          /* OAI4G_SISO or OAI4G_LARGE_CDD */
+  uint8_t num_pdcch_symbols;
+  uint8_t Kmimo;
+  uint8_t Mdlharq;
+  uint8_t first_subframe;     /* subframe index of batch element 0 */
+  uint8_t subframe_step;      /* 0: every element uses first_subframe; 1: consecutive subframes */
+  uint8_t pad0;
+  uint16_t rnti;
+  int16_t amp;
+  int16_t sqrt_rho_a;
+  int16_t sqrt_rho_b;
+  uint32_t rb_alloc[4];
+  uint16_t nb_rb;
+  uint8_t mcs[2];
+  uint8_t rvidx[2];
+  uint8_t q[2];               /* scrambling codeword index q (dlsim passes 0) */
+  uint32_t TBS[2];
+  uint32_t payload_stride;    /* bytes between consecutive transport blocks in the payload buffer */
+  uint32_t reserved[8];
+} oai4g_tx_params_t;
+
+typedef struct oai4g_tx_config oai4g_tx_config_t;
+
+/* Derive every per-configuration table (segmentation, rate-matching geometry, RE maps,
+ * QAM/twiddle/Gold tables) and upload it to the current device.  NULL on error. */
+oai4g_tx_config_t *oai4g_tx_config_create(const oai4g_tx_params_t *p);
+void oai4g_tx_config_destroy(oai4g_tx_config_t *cfg);
+/* Derived sizes */
+uint32_t oai4g_tx_G(const oai4g_tx_config_t *cfg, int cw, int subframe);
+uint32_t oai4g_tx_ebits_words(const oai4g_tx_config_t *cfg);        /* per codeword per subframe */
+uint32_t oai4g_tx_iq_samples(const oai4g_tx_config_t *cfg);         /* per antenna per subframe */
+size_t oai4g_tx_workspace_bytes(const oai4g_tx_config_t *cfg, int n_sf);
+
+/* Run n_sf subframes.  All pointers are device pointers:
+ *   d_payload : [n_sf][n_cw][payload_stride] bytes, TBS/8 valid bytes each (not modified)
+ *   d_work    : oai4g_tx_workspace_bytes() bytes (packed scrambled e bits)
+ *   d_iq      : [n_sf][nb_antennas_tx][samples_per_tti] int32 (int16 I, int16 Q)
+ * stream is a hipStream_t (NULL = default stream).  Asynchronous. */
+int oai4g_tx_batch(const oai4g_tx_config_t *cfg, int n_sf, const uint8_t *d_payload, void *d_work,
+                   int32_t *d_iq, void *stream);
+/* Same, but records HIP events around each kernel on `stream`, synchronizes, and returns the
+ * two kernel durations in ms (kernel_ms[0] = encode/RM/scramble, [1] = modulate/IDFT/CP). */
+int oai4g_tx_batch_timed(const oai4g_tx_config_t *cfg, int n_sf, const uint8_t *d_payload, void *d_work,
+                         int32_t *d_iq, void *stream, float *kernel_ms);
+/* Stage entry for parity tests: run only the encoder kernel (payload -> packed e bits). */
+int oai4g_tx_encode(const oai4g_tx_config_t *cfg, int n_sf, const uint8_t *d_payload, void *d_work, void *stream);
+
+/* ---------------- device memory helpers (for hosts without another allocator) ---------------- */
+void *oai4g_dev_alloc(size_t bytes);
+void oai4g_dev_free(void *p);
+int oai4g_memcpy_h2d(void *dst, const void *src, size_t bytes);
+int oai4g_memcpy_d2h(void *dst, const void *src, size_t bytes);
+int oai4g_memset_d(void *dst, int value, size_t bytes);
+int oai4g_sync(void);
+/* Deterministic device-side payload generator (splitmix64 of (seed, byte index)). */
+int oai4g_fill_payload(uint8_t *d_payload, size_t bytes, uint64_t seed, void *stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

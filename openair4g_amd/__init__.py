@@ -1,0 +1,479 @@
+"""openair4g_amd — MI355X-native LTE PDSCH transmit path (host side).
+
+This module is the Python mirror of the C ABI in ``include/oai4g.h``: ctypes bindings for
+the drop-in entry points (``dlsch_encoding``, ``dlsch_scrambling``, ``dlsch_modulation``,
+``PHY_ofdm_mod`` and their callees, named as in openair1/PHY) and for the batched,
+device-resident transmit path (``TxPipeline``).  All arithmetic runs in the gfx950 kernels
+of ``lib/libopenair4g_amd.so``; if that library or a gfx950 device is missing every compute
+entry point raises ``OAI4GError`` — there is no CPU fallback.
+"""
+import ctypes
+import os
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "lib", "libopenair4g_amd.so")
+
+LTE_NULL = 2
+NSOFT = 1827072
+MAX_SEGMENTS = 16
+MAX_CHANNEL_BITS = 14 * 1200 * 6
+D_BYTES = 96 + 12 + 3 + 3 * 6144
+W_BYTES = 3 * 6144 + 96
+SISO, ALAMOUTI, LARGE_CDD = 0, 1, 2
+CYCLIC_PREFIX = 0
+
+
+class OAI4GError(RuntimeError):
+    pass
+
+
+u8p = ctypes.POINTER(ctypes.c_uint8)
+
+
+class FrameParms(ctypes.Structure):
+    """oai4g_frame_parms_t — LTE_DL_FRAME_PARMS subset (PHY/impl_defs_lte.h:470-572)."""
+    _fields_ = [("N_RB_DL", ctypes.c_uint16), ("Nid_cell", ctypes.c_uint16), ("Ncp", ctypes.c_uint8),
+                ("nushift", ctypes.c_uint8), ("mode1_flag", ctypes.c_uint8), ("nb_antennas_tx", ctypes.c_uint8),
+                ("frame_type", ctypes.c_uint8), ("symbols_per_tti", ctypes.c_uint8),
+                ("log2_symbol_size", ctypes.c_uint8), ("pad0", ctypes.c_uint8),
+                ("ofdm_symbol_size", ctypes.c_uint16), ("first_carrier_offset", ctypes.c_uint16),
+                ("nb_prefix_samples", ctypes.c_uint16), ("nb_prefix_samples0", ctypes.c_uint16),
+                ("samples_per_tti", ctypes.c_uint32)]
+
+
+class DlHarq(ctypes.Structure):
+    """oai4g_dl_harq_t — LTE_DL_eNB_HARQ_t subset (PHY/LTE_TRANSPORT/defs.h:104-169)."""
+    _fields_ = [("TBS", ctypes.c_uint32), ("B", ctypes.c_uint32), ("b", u8p), ("c", u8p * MAX_SEGMENTS),
+                ("RTC", ctypes.c_uint32 * MAX_SEGMENTS), ("round", ctypes.c_uint8), ("mcs", ctypes.c_uint8),
+                ("rvidx", ctypes.c_uint8), ("mimo_mode", ctypes.c_uint8), ("rb_alloc", ctypes.c_uint32 * 4),
+                ("nb_rb", ctypes.c_uint16), ("e", u8p), ("d", u8p * MAX_SEGMENTS), ("w", u8p * MAX_SEGMENTS),
+                ("C", ctypes.c_uint32), ("Cminus", ctypes.c_uint32), ("Cplus", ctypes.c_uint32),
+                ("Kminus", ctypes.c_uint32), ("Kplus", ctypes.c_uint32), ("F", ctypes.c_uint32),
+                ("Nl", ctypes.c_uint8), ("Nlayers", ctypes.c_uint8), ("first_layer", ctypes.c_uint8)]
+
+
+class Dlsch(ctypes.Structure):
+    """oai4g_dlsch_t — LTE_eNB_DLSCH_t subset (PHY/LTE_TRANSPORT/defs.h:240-274)."""
+    _fields_ = [("rnti", ctypes.c_uint16), ("current_harq_pid", ctypes.c_uint8), ("Mdlharq", ctypes.c_uint8),
+                ("Kmimo", ctypes.c_uint8), ("sqrt_rho_a", ctypes.c_int16), ("sqrt_rho_b", ctypes.c_int16),
+                ("harq_processes", ctypes.POINTER(DlHarq) * 8)]
+
+
+class TxParams(ctypes.Structure):
+    """oai4g_tx_params_t — the POD parameter block rank 0 broadcasts to the other ranks."""
+    _fields_ = [("N_RB_DL", ctypes.c_uint16), ("Nid_cell", ctypes.c_uint16), ("Ncp", ctypes.c_uint8),
+                ("nb_antennas_tx", ctypes.c_uint8), ("mode1_flag", ctypes.c_uint8), ("frame_type", ctypes.c_uint8),
+                ("n_cw", ctypes.c_uint8), ("mimo_mode", ctypes.c_uint8), ("num_pdcch_symbols", ctypes.c_uint8),
+                ("Kmimo", ctypes.c_uint8), ("Mdlharq", ctypes.c_uint8), ("first_subframe", ctypes.c_uint8),
+                ("subframe_step", ctypes.c_uint8), ("pad0", ctypes.c_uint8), ("rnti", ctypes.c_uint16),
+                ("amp", ctypes.c_int16), ("sqrt_rho_a", ctypes.c_int16), ("sqrt_rho_b", ctypes.c_int16),
+                ("rb_alloc", ctypes.c_uint32 * 4), ("nb_rb", ctypes.c_uint16), ("mcs", ctypes.c_uint8 * 2),
+                ("rvidx", ctypes.c_uint8 * 2), ("q", ctypes.c_uint8 * 2), ("TBS", ctypes.c_uint32 * 2),
+                ("payload_stride", ctypes.c_uint32), ("reserved", ctypes.c_uint32 * 8)]
+
+    def to_bytes(self):
+        return bytes(ctypes.string_at(ctypes.addressof(self), ctypes.sizeof(self)))
+
+    @classmethod
+    def from_bytes(cls, b):
+        p = cls()
+        ctypes.memmove(ctypes.addressof(p), bytes(b), ctypes.sizeof(cls))
+        return p
+
+
+_lib = None
+
+_SIGS = {
+    "oai4g_init": (ctypes.c_int, []),
+    "oai4g_last_error": (ctypes.c_char_p, []),
+    "oai4g_device_name": (ctypes.c_int, [ctypes.c_char_p, ctypes.c_int]),
+    "oai4g_init_frame_parms": (ctypes.c_int, [ctypes.POINTER(FrameParms), ctypes.c_uint16, ctypes.c_uint16,
+                                              ctypes.c_uint8, ctypes.c_uint8, ctypes.c_uint8, ctypes.c_uint8]),
+    "oai4g_get_Qm": (ctypes.c_uint8, [ctypes.c_uint8]),
+    "oai4g_get_G": (ctypes.c_int, [ctypes.POINTER(FrameParms), ctypes.c_uint16, ctypes.POINTER(ctypes.c_uint32),
+                                   ctypes.c_uint8, ctypes.c_uint8, ctypes.c_uint8, ctypes.c_int, ctypes.c_uint8]),
+    "oai4g_new_dlsch": (ctypes.POINTER(Dlsch), [ctypes.c_uint8, ctypes.c_uint8, ctypes.c_uint8]),
+    "oai4g_free_dlsch": (None, [ctypes.POINTER(Dlsch)]),
+    "oai4g_lte_gold_generic": (ctypes.c_uint32, [ctypes.POINTER(ctypes.c_uint32), ctypes.POINTER(ctypes.c_uint32),
+                                                 ctypes.c_uint8]),
+    "oai4g_crc24a": (ctypes.c_uint32, [ctypes.c_void_p, ctypes.c_int]),
+    "oai4g_crc24b": (ctypes.c_uint32, [ctypes.c_void_p, ctypes.c_int]),
+    "oai4g_lte_segmentation": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(u8p), ctypes.c_uint32]
+                               + [ctypes.POINTER(ctypes.c_uint32)] * 6),
+    "oai4g_threegpplte_turbo_encoder": (None, [ctypes.c_void_p, ctypes.c_uint16, ctypes.c_void_p, ctypes.c_uint8,
+                                               ctypes.c_uint16, ctypes.c_uint16]),
+    "oai4g_sub_block_interleaving_turbo": (ctypes.c_uint32, [ctypes.c_uint32, ctypes.c_void_p, ctypes.c_void_p]),
+    "oai4g_lte_rate_matching_turbo": (ctypes.c_uint32, [ctypes.c_uint32, ctypes.c_uint32, ctypes.c_void_p,
+                                                        ctypes.c_void_p] + [ctypes.c_uint8] + [ctypes.c_uint32]
+                                      + [ctypes.c_uint8] * 8),
+    "oai4g_dlsch_encoding": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(FrameParms), ctypes.c_uint8,
+                                            ctypes.POINTER(Dlsch), ctypes.c_int, ctypes.c_uint8]),
+    "oai4g_dlsch_scrambling": (None, [ctypes.POINTER(FrameParms), ctypes.c_int, ctypes.POINTER(Dlsch), ctypes.c_int,
+                                      ctypes.c_uint8, ctypes.c_uint8]),
+    "oai4g_dlsch_modulation": (ctypes.c_int, [ctypes.POINTER(ctypes.c_void_p), ctypes.c_int16, ctypes.c_uint32,
+                                              ctypes.POINTER(FrameParms), ctypes.c_uint8, ctypes.POINTER(Dlsch),
+                                              ctypes.POINTER(Dlsch)]),
+    "oai4g_PHY_ofdm_mod": (None, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint8, ctypes.c_uint8, ctypes.c_uint16,
+                                  ctypes.c_int]),
+    "oai4g_normal_prefix_mod": (None, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint8, ctypes.POINTER(FrameParms)]),
+    "oai4g_do_OFDM_mod": (None, [ctypes.POINTER(ctypes.c_void_p), ctypes.POINTER(ctypes.c_void_p), ctypes.c_uint32,
+                                 ctypes.c_uint16, ctypes.POINTER(FrameParms)]),
+    "oai4g_idft": (ctypes.c_int, [ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int]),
+    "oai4g_idft2048": (None, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int]),
+    "oai4g_idft1024": (None, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int]),
+    "oai4g_idft256": (None, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int]),
+    "oai4g_idft128": (None, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int]),
+    "oai4g_idft64": (None, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int]),
+    "oai4g_tx_config_create": (ctypes.c_void_p, [ctypes.POINTER(TxParams)]),
+    "oai4g_tx_config_destroy": (None, [ctypes.c_void_p]),
+    "oai4g_tx_G": (ctypes.c_uint32, [ctypes.c_void_p, ctypes.c_int, ctypes.c_int]),
+    "oai4g_tx_ebits_words": (ctypes.c_uint32, [ctypes.c_void_p]),
+    "oai4g_tx_iq_samples": (ctypes.c_uint32, [ctypes.c_void_p]),
+    "oai4g_tx_workspace_bytes": (ctypes.c_size_t, [ctypes.c_void_p, ctypes.c_int]),
+    "oai4g_tx_batch": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p,
+                                      ctypes.c_void_p, ctypes.c_void_p]),
+    "oai4g_tx_batch_timed": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p,
+                                            ctypes.c_void_p, ctypes.c_void_p, ctypes.POINTER(ctypes.c_float)]),
+    "oai4g_tx_encode": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p,
+                                       ctypes.c_void_p]),
+    "oai4g_dev_alloc": (ctypes.c_void_p, [ctypes.c_size_t]),
+    "oai4g_dev_free": (None, [ctypes.c_void_p]),
+    "oai4g_memcpy_h2d": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t]),
+    "oai4g_memcpy_d2h": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t]),
+    "oai4g_memset_d": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_size_t]),
+    "oai4g_sync": (ctypes.c_int, []),
+    "oai4g_fill_payload": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_uint64, ctypes.c_void_p]),
+}
+
+
+def load_library(path=LIB_PATH):
+    """Load the HIP library (raises OAI4GError if it is not built)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(path):
+        raise OAI4GError(f"HIP library not built: {path} (run __graft_entry__.build())")
+    lib = ctypes.CDLL(path)
+    for name, (res, args) in _SIGS.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    _lib = lib
+    return lib
+
+
+def exported_symbols():
+    return sorted(_SIGS)
+
+
+def lib():
+    return load_library()
+
+
+def init():
+    """Initialise the device (raises if no gfx950 GPU: no CPU fallback)."""
+    L = lib()
+    if L.oai4g_init() != 0:
+        raise OAI4GError(L.oai4g_last_error().decode())
+    return L
+
+
+def _check(ok):
+    if not ok:
+        raise OAI4GError(lib().oai4g_last_error().decode())
+
+
+def _ptr(a):
+    return ctypes.c_void_p(a.ctypes.data)
+
+
+def device_name():
+    L = init()
+    buf = ctypes.create_string_buffer(256)
+    _check(L.oai4g_device_name(buf, 256) == 0)
+    return buf.value.decode()
+
+
+# ------------------------------------------------------------------------------------------
+# drop-in entry points (host numpy buffers in/out, GPU compute)
+# ------------------------------------------------------------------------------------------
+def frame_parms(N_RB_DL, Nid_cell=0, Ncp=0, nb_antennas_tx=1, mode1_flag=1, frame_type=0):
+    fp = FrameParms()
+    _check(lib().oai4g_init_frame_parms(ctypes.byref(fp), N_RB_DL, Nid_cell, Ncp, nb_antennas_tx, mode1_flag,
+                                        frame_type) == 0)
+    return fp
+
+
+def get_G(fp, nb_rb, rb_alloc, Qm, Nl, num_pdcch, subframe):
+    ra = (ctypes.c_uint32 * 4)(*rb_alloc)
+    return lib().oai4g_get_G(ctypes.byref(fp), nb_rb, ra, Qm, Nl, num_pdcch, 0, subframe)
+
+
+def crc24a(data, bitlen):
+    init()
+    a = np.ascontiguousarray(data, dtype=np.uint8)
+    return int(lib().oai4g_crc24a(_ptr(a), bitlen))
+
+
+def crc24b(data, bitlen):
+    init()
+    a = np.ascontiguousarray(data, dtype=np.uint8)
+    return int(lib().oai4g_crc24b(_ptr(a), bitlen))
+
+
+def turbo_encode(c, f1, f2):
+    """threegpplte_turbo_encoder: c (K/8 bytes) -> d (3K+12 bytes)."""
+    init()
+    c = np.ascontiguousarray(c, dtype=np.uint8)
+    K = 8 * len(c)
+    d = np.zeros(3 * K + 12, dtype=np.uint8)
+    lib().oai4g_threegpplte_turbo_encoder(_ptr(c), len(c), _ptr(d), 0, f1, f2)
+    _check(True)
+    return d
+
+
+def subblock_interleave(d_full, D):
+    """sub_block_interleaving_turbo: d_full = 96-byte NULL prefix + d.  Returns (R, w)."""
+    init()
+    d_full = np.ascontiguousarray(d_full, dtype=np.uint8)
+    R = (D + 31) >> 5
+    w = np.zeros(3 * 32 * R, dtype=np.uint8)
+    dptr = ctypes.c_void_p(d_full.ctypes.data + 96)
+    rtc = lib().oai4g_sub_block_interleaving_turbo(D, dptr, _ptr(w))
+    if rtc == 0:
+        _check(False)
+    return rtc, w
+
+
+def rate_match(RTC, G, w, C, r, Qm, rvidx=0, Nl=1, Kmimo=1, Mdlharq=8, Nsoft=NSOFT):
+    init()
+    w = np.ascontiguousarray(w, dtype=np.uint8)
+    e = np.zeros(G + 64, dtype=np.uint8)
+    E = lib().oai4g_lte_rate_matching_turbo(RTC, G, _ptr(w), _ptr(e), C, Nsoft, Mdlharq, Kmimo, rvidx, Qm, Nl, r,
+                                            0, 0)
+    return e[:E]
+
+
+def idft(x, scale=1):
+    """x: complex int16 pairs as int16 array of length 2N."""
+    init()
+    x = np.ascontiguousarray(x, dtype=np.int16)
+    n = len(x) // 2
+    y = np.zeros_like(x)
+    _check(lib().oai4g_idft(int(n).bit_length() - 1, _ptr(x), _ptr(y), scale) == 0)
+    return y
+
+
+def ofdm_mod(grid, log2n, nb_symbols, cp):
+    """PHY_ofdm_mod (CYCLIC_PREFIX): grid int32[nb_symbols*N] -> int32[nb_symbols*(N+cp)]."""
+    init()
+    grid = np.ascontiguousarray(grid, dtype=np.int32)
+    N = 1 << log2n
+    out = np.zeros(nb_symbols * (N + cp), dtype=np.int32)
+    lib().oai4g_PHY_ofdm_mod(_ptr(grid), _ptr(out), log2n, nb_symbols, cp, CYCLIC_PREFIX)
+    return out
+
+
+def normal_prefix_mod(txdataF, fp, nsymb=7, out=None):
+    init()
+    txdataF = np.ascontiguousarray(txdataF, dtype=np.int32)
+    if out is None:
+        out = np.zeros(fp.samples_per_tti, dtype=np.int32)
+    lib().oai4g_normal_prefix_mod(_ptr(txdataF), _ptr(out), nsymb, ctypes.byref(fp))
+    return out
+
+
+class DlschHandle:
+    """Owns an oai4g_dlsch_t (new_eNB_dlsch) and exposes its HARQ-0 buffers as numpy views."""
+
+    def __init__(self, Kmimo=1, Mdlharq=8, N_RB_DL=100):
+        init()
+        self.ptr = lib().oai4g_new_dlsch(Kmimo, Mdlharq, N_RB_DL)
+        if not self.ptr:
+            raise OAI4GError("new_dlsch failed")
+        self.d = self.ptr.contents
+        self.h = self.d.harq_processes[0].contents
+
+    def close(self):
+        if self.ptr:
+            lib().oai4g_free_dlsch(self.ptr)
+            self.ptr = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def view(self, field, n, r=None):
+        p = getattr(self.h, field) if r is None else getattr(self.h, field)[r]
+        return np.ctypeslib.as_array(p, shape=(n,))
+
+
+def dlsch_encoding(a, fp, num_pdcch, dl, subframe):
+    return lib().oai4g_dlsch_encoding(_ptr(a), ctypes.byref(fp), num_pdcch, dl.ptr, 0, subframe)
+
+
+def dlsch_scrambling(fp, dl, G, q, Ns):
+    lib().oai4g_dlsch_scrambling(ctypes.byref(fp), 0, dl.ptr, G, q, Ns)
+
+
+def dlsch_modulation(txdataF, amp, subframe, fp, num_pdcch, dl0, dl1=None):
+    """txdataF: list of int32 arrays (one per antenna), modified in place."""
+    arr = (ctypes.c_void_p * len(txdataF))(*[a.ctypes.data for a in txdataF])
+    return lib().oai4g_dlsch_modulation(arr, amp, subframe, ctypes.byref(fp), num_pdcch, dl0.ptr,
+                                        dl1.ptr if dl1 is not None else None)
+
+
+# ------------------------------------------------------------------------------------------
+# configurations (BASELINE.json configs) and the batched pipeline
+# ------------------------------------------------------------------------------------------
+FULL_ALLOC_100 = (0xFFFFFFFF, 0xFFFFFFFF, 0xFFFFFFFF, 0xF)
+FULL_ALLOC_6 = (0x3F, 0, 0, 0)
+FULL_ALLOC_15 = (0x7FFF, 0, 0, 0)
+FULL_ALLOC_50 = (0xFFFFFFFF, 0x3FFFF, 0, 0)
+
+# TBS from 3GPP TS 36.213 Table 7.1.7.2.1-1 for the configurations exercised here
+TBS_TABLE = {(9, 6): 936, (4, 6): 408, (16, 100): 30576, (19, 100): 36696, (9, 100): 15840, (28, 100): 75376,
+             (5, 50): 4392, (15, 50): 14112, (26, 50): 30576}
+
+CONFIGS = {
+    # C1: dlsim 1.4 MHz SISO QPSK (MCS 9), 3 PDCCH symbols
+    "C1": dict(N_RB_DL=6, nb_antennas_tx=1, mode1_flag=1, n_cw=1, mimo_mode=SISO, num_pdcch_symbols=3,
+               mcs=(9, 0), rb_alloc=FULL_ALLOC_6, nb_rb=6, Kmimo=1),
+    # C2: dlsim 20 MHz SISO 16-QAM (MCS 16)
+    "C2": dict(N_RB_DL=100, nb_antennas_tx=1, mode1_flag=1, n_cw=1, mimo_mode=SISO, num_pdcch_symbols=1,
+               mcs=(16, 0), rb_alloc=FULL_ALLOC_100, nb_rb=100, Kmimo=1),
+    # C3: dlsim 20 MHz 2x2 TM3 (LARGE_CDD) 64-QAM, MCS 19 on both codewords (highest the reference encodes)
+    "C3": dict(N_RB_DL=100, nb_antennas_tx=2, mode1_flag=0, n_cw=2, mimo_mode=LARGE_CDD, num_pdcch_symbols=1,
+               mcs=(19, 19), rb_alloc=FULL_ALLOC_100, nb_rb=100, Kmimo=2),
+}
+
+
+def make_params(name="C3", subframe=7, subframe_step=0, rnti=0x1234, Nid_cell=0, **over):
+    c = dict(CONFIGS[name])
+    c.update(over)
+    p = TxParams()
+    p.N_RB_DL = c["N_RB_DL"]
+    p.Nid_cell = Nid_cell
+    p.Ncp = 0
+    p.nb_antennas_tx = c["nb_antennas_tx"]
+    p.mode1_flag = c["mode1_flag"]
+    p.frame_type = 0
+    p.n_cw = c["n_cw"]
+    p.mimo_mode = c["mimo_mode"]
+    p.num_pdcch_symbols = c["num_pdcch_symbols"]
+    p.Kmimo = c["Kmimo"]
+    p.Mdlharq = 8
+    p.first_subframe = subframe
+    p.subframe_step = subframe_step
+    p.rnti = rnti
+    p.amp = 512
+    p.sqrt_rho_a = 8192
+    p.sqrt_rho_b = 8192
+    for i in range(4):
+        p.rb_alloc[i] = c["rb_alloc"][i]
+    p.nb_rb = c["nb_rb"]
+    tbs = c.get("TBS")
+    for cw in range(p.n_cw):
+        p.mcs[cw] = c["mcs"][cw]
+        p.rvidx[cw] = 0
+        p.q[cw] = 0
+        p.TBS[cw] = tbs[cw] if tbs else TBS_TABLE[(c["mcs"][cw], c["nb_rb"])]
+    maxA = max(p.TBS[cw] // 8 for cw in range(p.n_cw))
+    p.payload_stride = (maxA + 3 + 15) & ~15
+    return p
+
+
+class TxPipeline:
+    """Batched device-resident transmit path for one configuration (oai4g_tx_*)."""
+
+    def __init__(self, params, n_sf, alloc=True):
+        self.L = init()
+        self.params = params
+        self.n_sf = n_sf
+        self.cfg = self.L.oai4g_tx_config_create(ctypes.byref(params))
+        if not self.cfg:
+            raise OAI4GError(self.L.oai4g_last_error().decode())
+        self.n_cw = params.n_cw
+        self.n_ant = params.nb_antennas_tx
+        self.spt = self.L.oai4g_tx_iq_samples(self.cfg)
+        self.ebits_words = self.L.oai4g_tx_ebits_words(self.cfg)
+        self.payload_bytes = n_sf * self.n_cw * params.payload_stride
+        self.work_bytes = self.L.oai4g_tx_workspace_bytes(self.cfg, n_sf)
+        self.iq_samples = n_sf * self.n_ant * self.spt
+        self.d_payload = self.d_work = self.d_iq = None
+        if alloc:
+            self.d_payload = self._alloc(self.payload_bytes)
+            self.d_work = self._alloc(self.work_bytes)
+            self.d_iq = self._alloc(self.iq_samples * 4)
+
+    def _alloc(self, n):
+        p = self.L.oai4g_dev_alloc(n)
+        if not p:
+            raise OAI4GError(self.L.oai4g_last_error().decode())
+        return p
+
+    def G(self, cw, subframe):
+        return self.L.oai4g_tx_G(self.cfg, cw, subframe)
+
+    def fill_payload(self, seed):
+        _check(self.L.oai4g_fill_payload(self.d_payload, self.payload_bytes, seed, None) == 0)
+
+    def upload_payload(self, payload):
+        payload = np.ascontiguousarray(payload, dtype=np.uint8)
+        assert payload.nbytes == self.payload_bytes
+        _check(self.L.oai4g_memcpy_h2d(self.d_payload, _ptr(payload), payload.nbytes) == 0)
+
+    def download_payload(self):
+        out = np.empty(self.payload_bytes, dtype=np.uint8)
+        _check(self.L.oai4g_memcpy_d2h(_ptr(out), self.d_payload, out.nbytes) == 0)
+        return out.reshape(self.n_sf, self.n_cw, self.params.payload_stride)
+
+    def run(self, stream=None):
+        _check(self.L.oai4g_tx_batch(self.cfg, self.n_sf, self.d_payload, self.d_work, self.d_iq, stream) == 0)
+
+    def run_timed(self, stream=None):
+        ms = (ctypes.c_float * 2)()
+        _check(self.L.oai4g_tx_batch_timed(self.cfg, self.n_sf, self.d_payload, self.d_work, self.d_iq, stream,
+                                           ms) == 0)
+        return ms[0], ms[1]
+
+    def encode_only(self, stream=None):
+        _check(self.L.oai4g_tx_encode(self.cfg, self.n_sf, self.d_payload, self.d_work, stream) == 0)
+
+    def sync(self):
+        _check(self.L.oai4g_sync() == 0)
+
+    def ebits(self):
+        out = np.empty(self.work_bytes // 4, dtype=np.uint32)
+        _check(self.L.oai4g_memcpy_d2h(_ptr(out), self.d_work, out.nbytes) == 0)
+        return out.reshape(self.n_sf, self.n_cw, self.ebits_words)
+
+    def iq(self):
+        out = np.empty(self.iq_samples, dtype=np.int32)
+        _check(self.L.oai4g_memcpy_d2h(_ptr(out), self.d_iq, out.nbytes) == 0)
+        return out.reshape(self.n_sf, self.n_ant, self.spt)
+
+    def close(self):
+        for p in (self.d_payload, self.d_work, self.d_iq):
+            if p:
+                self.L.oai4g_dev_free(p)
+        self.d_payload = self.d_work = self.d_iq = None
+        if self.cfg:
+            self.L.oai4g_tx_config_destroy(self.cfg)
+            self.cfg = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def unpack_bits(words, nbits):
+    """Packed LSB-first uint32 words -> uint8 bit array."""
+    b = np.unpackbits(np.ascontiguousarray(words, dtype="<u4").view(np.uint8), bitorder="little")
+    return b[:nbits]

@@ -1,0 +1,60 @@
+"""Build the in-tree HIP shared library (gfx950) and the CPU oracle.
+
+The product library is compiled with hipcc straight into openair4g_amd/lib/ so that it
+travels with the repository snapshot to the GPU box.  No JIT, no cache outside the tree.
+"""
+import os
+import subprocess
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(HERE)
+CSRC = os.path.join(HERE, "csrc")
+LIBDIR = os.path.join(HERE, "lib")
+LIB = os.path.join(LIBDIR, "libopenair4g_amd.so")
+SOURCES = ["oai4g_host.cpp", "oai4g_encode.hip", "oai4g_ofdm.hip"]
+EXTRA = [os.path.join(ROOT, "include", "oai4g_qpp.c")]
+HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+ARCH = os.environ.get("OAI4G_ARCH", "gfx950")
+
+
+def _newer(target, deps):
+    if not os.path.exists(target):
+        return True
+    t = os.path.getmtime(target)
+    return any(os.path.getmtime(d) > t for d in deps)
+
+
+def build_lib(force=False, verbose=False):
+    os.makedirs(LIBDIR, exist_ok=True)
+    srcs = [os.path.join(CSRC, s) for s in SOURCES]
+    deps = srcs + EXTRA + [os.path.join(CSRC, "oai4g_internal.h"), os.path.join(ROOT, "include", "oai4g.h")]
+    if not force and not _newer(LIB, deps):
+        return LIB
+    objs = []
+    for src in srcs + EXTRA:
+        obj = os.path.join(LIBDIR, os.path.basename(src) + ".o")
+        lang = ["-x", "hip"] if src.endswith((".hip", ".cpp")) else ["-x", "c"]
+        cmd = [HIPCC, f"--offload-arch={ARCH}", "-O3", "-fPIC", "-Wall", "-Wno-unused-result", "-Wno-unused-value",
+               "-I", os.path.join(ROOT, "include")] + (["-std=c++17"] if lang[1] == "hip" else []) + lang + \
+              ["-c", src, "-o", obj]
+        if verbose:
+            print(" ".join(cmd))
+        subprocess.run(cmd, check=True)
+        objs.append(obj)
+    cmd = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", LIB] + objs + ["-lpthread"]
+    if verbose:
+        print(" ".join(cmd))
+    subprocess.run(cmd, check=True)
+    return LIB
+
+
+def build_oracle(verbose=False):
+    subprocess.run(["make", "-s", "-C", os.path.join(ROOT, "oracle")], check=True,
+                   stdout=None if verbose else subprocess.DEVNULL)
+
+
+if __name__ == "__main__":
+    build_lib(force="--force" in sys.argv, verbose=True)
+    build_oracle(verbose=True)
+    print("built", LIB)

@@ -1,0 +1,1153 @@
+/*
+ * Host side of openair4g_amd: C ABI (include/oai4g.h), configuration derivation, drop-in
+ * entry points and the batched transmit path.  All arithmetic on samples / bits runs in the
+ * gfx950 kernels; this file only derives parameters (what the reference recomputes on every
+ * call: segmentation, rate-matching geometry, RE maps), moves buffers and launches.
+ */
+#include <hip/hip_runtime.h>
+#include <math.h>
+#include <pthread.h>
+#include <stdarg.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include <mutex>
+#include <vector>
+
+#include "../../include/oai4g.h"
+#include "../../include/oai4g_qpp.h"
+#include "oai4g_internal.h"
+
+/* ------------------------------------------------------------------------------------------
+ * errors
+ * ---------------------------------------------------------------------------------------- */
+static thread_local char g_err[512] = "";
+
+static void set_err(const char *fmt, ...)
+{
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(g_err, sizeof(g_err), fmt, ap);
+  va_end(ap);
+}
+
+extern "C" const char *oai4g_last_error(void) { return g_err; }
+
+#define HCK(call, ret)                                                                          \
+  do {                                                                                          \
+    hipError_t e_ = (call);                                                                     \
+    if (e_ != hipSuccess) {                                                                     \
+      set_err("%s failed: %s (%s:%d)", #call, hipGetErrorString(e_), __FILE__, __LINE__);       \
+      fprintf(stderr, "[openair4g_amd] %s\n", g_err);                                           \
+      return ret;                                                                               \
+    }                                                                                           \
+  } while (0)
+
+/* ------------------------------------------------------------------------------------------
+ * global device tables: twiddles, Gold jump-ahead
+ * ---------------------------------------------------------------------------------------- */
+static pthread_once_t g_once = PTHREAD_ONCE_INIT;
+static int g_init_status = -1;
+static char g_init_err[512] = "";
+static uint32_t *g_tw = nullptr, *g_gx1 = nullptr, *g_gx2j = nullptr;
+static uint32_t h_gx1[64], h_gx2j[64 * 32];
+
+static void twiddle_host(int N, int m, int16_t *re, int16_t *im)
+{
+  /* W_N^m in Q15: (floor(32767 cos), floor(-32767 sin)) — reproduces lte_dfts.c tw* tables */
+  double a = 2.0 * M_PI * (double)m / (double)N;
+  *re = (int16_t)floor(32767.0 * cos(a));
+  *im = (int16_t)floor(-32767.0 * sin(a));
+}
+
+static void gold_step_h(uint32_t *x1, uint32_t *x2)
+{
+  *x1 = (*x1 >> 1) ^ (*x1 >> 4);
+  *x1 = *x1 ^ (*x1 << 31) ^ (*x1 << 28);
+  *x2 = (*x2 >> 1) ^ (*x2 >> 2) ^ (*x2 >> 3) ^ (*x2 >> 4);
+  *x2 = *x2 ^ (*x2 << 31) ^ (*x2 << 30) ^ (*x2 << 29) ^ (*x2 << 28);
+}
+
+static void do_init(void)
+{
+  int n = 0;
+  hipError_t e = hipGetDeviceCount(&n);
+  if (e != hipSuccess || n == 0) {
+    snprintf(g_init_err, sizeof(g_init_err), "no HIP device available (%s)",
+             e == hipSuccess ? "0 devices" : hipGetErrorString(e));
+    g_init_status = -1;
+    return;
+  }
+  int dev = 0;
+  hipGetDevice(&dev);
+  hipDeviceProp_t prop;
+  if (hipGetDeviceProperties(&prop, dev) != hipSuccess || strncmp(prop.gcnArchName, "gfx950", 6) != 0) {
+    snprintf(g_init_err, sizeof(g_init_err), "device %d is not gfx950 (%s)", dev, prop.gcnArchName);
+    g_init_status = -2;
+    return;
+  }
+  /* twiddles */
+  std::vector<uint32_t> tw(OAI4G_TW_TOTAL);
+  const int sizes[] = {4, 6, 7, 8, 9, 10, 11};
+  for (int log2s : sizes) {
+    int N = 1 << log2s;
+    uint32_t off = oai4g_tw_offset(log2s);
+    for (int m = 0; m < N; m++) {
+      int16_t re, im;
+      twiddle_host(N, m, &re, &im);
+      tw[off + m] = (uint16_t)re | ((uint32_t)(uint16_t)im << 16);
+    }
+  }
+  /* Gold: x1 after 50+64l steps; x2 step-matrix powers M2^(50+64l) (columns) */
+  uint32_t x1 = 1u + (1u << 31), cols[32];
+  for (int b = 0; b < 32; b++) cols[b] = 1u << b;
+  int steps_done = 0;
+  for (int l = 0; l < 64; l++) {
+    int target = 50 + 64 * l;
+    while (steps_done < target) {
+      uint32_t dummy = 0;
+      gold_step_h(&x1, &dummy);
+      for (int b = 0; b < 32; b++) {
+        uint32_t z = 0;
+        gold_step_h(&z, &cols[b]);
+      }
+      steps_done++;
+    }
+    h_gx1[l] = x1;
+    for (int b = 0; b < 32; b++) h_gx2j[32 * l + b] = cols[b];
+  }
+  if (hipMalloc(&g_tw, tw.size() * 4) != hipSuccess || hipMalloc(&g_gx1, sizeof(h_gx1)) != hipSuccess ||
+      hipMalloc(&g_gx2j, sizeof(h_gx2j)) != hipSuccess ||
+      hipMemcpy(g_tw, tw.data(), tw.size() * 4, hipMemcpyHostToDevice) != hipSuccess ||
+      hipMemcpy(g_gx1, h_gx1, sizeof(h_gx1), hipMemcpyHostToDevice) != hipSuccess ||
+      hipMemcpy(g_gx2j, h_gx2j, sizeof(h_gx2j), hipMemcpyHostToDevice) != hipSuccess) {
+    snprintf(g_init_err, sizeof(g_init_err), "device table upload failed");
+    g_init_status = -3;
+    return;
+  }
+  g_init_status = 0;
+}
+
+extern "C" int oai4g_init(void)
+{
+  pthread_once(&g_once, do_init);
+  if (g_init_status != 0) {
+    set_err("openair4g_amd: %s", g_init_err);
+    fprintf(stderr, "[openair4g_amd] %s\n", g_err);
+  }
+  return g_init_status;
+}
+
+extern "C" int oai4g_device_name(char *buf, int len)
+{
+  if (oai4g_init() != 0) return -1;
+  int dev = 0;
+  hipGetDevice(&dev);
+  hipDeviceProp_t prop;
+  HCK(hipGetDeviceProperties(&prop, dev), -1);
+  snprintf(buf, len, "%s (%s, %d CUs)", prop.name, prop.gcnArchName, prop.multiProcessorCount);
+  return 0;
+}
+
+/* ------------------------------------------------------------------------------------------
+ * per-thread scratch (drop-in path): one stream + one growable device buffer
+ * ---------------------------------------------------------------------------------------- */
+struct scratch_t {
+  hipStream_t s = nullptr;
+  uint8_t *buf = nullptr;
+  size_t cap = 0;
+};
+static thread_local scratch_t g_scr;
+
+static uint8_t *scratch(size_t bytes)
+{
+  if (!g_scr.s && hipStreamCreateWithFlags(&g_scr.s, hipStreamNonBlocking) != hipSuccess) return nullptr;
+  if (bytes > g_scr.cap) {
+    if (g_scr.buf) hipFree(g_scr.buf);
+    size_t cap = bytes < (64u << 20) ? (64u << 20) : bytes;
+    if (hipMalloc(&g_scr.buf, cap) != hipSuccess) {
+      g_scr.buf = nullptr;
+      g_scr.cap = 0;
+      return nullptr;
+    }
+    g_scr.cap = cap;
+  }
+  return g_scr.buf;
+}
+
+#define NEED_INIT(ret)                    \
+  do {                                    \
+    if (oai4g_init() != 0) return ret;    \
+  } while (0)
+
+/* ------------------------------------------------------------------------------------------
+ * parameter helpers (lte_parms.c, lte_mcs.c)
+ * ---------------------------------------------------------------------------------------- */
+extern "C" int oai4g_init_frame_parms(oai4g_frame_parms_t *fp, uint16_t N_RB_DL, uint16_t Nid_cell, uint8_t Ncp,
+                                      uint8_t nb_antennas_tx, uint8_t mode1_flag, uint8_t frame_type)
+{
+  memset(fp, 0, sizeof(*fp));
+  fp->N_RB_DL = N_RB_DL;
+  fp->Nid_cell = Nid_cell;
+  fp->Ncp = Ncp;
+  fp->nushift = (uint8_t)(Nid_cell % 6);
+  fp->nb_antennas_tx = nb_antennas_tx;
+  fp->mode1_flag = mode1_flag;
+  fp->frame_type = frame_type;
+  uint16_t cp0 = Ncp ? 512 : 160, cp = Ncp ? 512 : 144;
+  fp->symbols_per_tti = Ncp ? 12 : 14;
+  int sh;
+  switch (N_RB_DL) {
+  case 100: fp->ofdm_symbol_size = 2048; fp->log2_symbol_size = 11; sh = 0; break;
+  case 50: fp->ofdm_symbol_size = 1024; fp->log2_symbol_size = 10; sh = 1; break;
+  case 25: fp->ofdm_symbol_size = 512; fp->log2_symbol_size = 9; sh = 2; break;
+  case 15: fp->ofdm_symbol_size = 256; fp->log2_symbol_size = 8; sh = 3; break;
+  case 6: fp->ofdm_symbol_size = 128; fp->log2_symbol_size = 7; sh = 4; break;
+  default: set_err("init_frame_parms: unsupported N_RB_DL %u", N_RB_DL); return -1;
+  }
+  fp->samples_per_tti = 30720u >> sh;
+  fp->first_carrier_offset = (uint16_t)(fp->ofdm_symbol_size - 6 * N_RB_DL);
+  fp->nb_prefix_samples = (uint16_t)(cp >> sh);
+  fp->nb_prefix_samples0 = (uint16_t)(cp0 >> sh);
+  return 0;
+}
+
+extern "C" uint8_t oai4g_get_Qm(uint8_t mcs) { return mcs < 10 ? 2 : (mcs < 17 ? 4 : 6); }
+
+static int rb_bit(const uint32_t *rb_alloc, int rb)
+{
+  if (rb < 32) return (rb_alloc[0] >> rb) & 1;
+  if (rb < 64) return (rb_alloc[1] >> (rb - 32)) & 1;
+  if (rb < 96) return (rb_alloc[2] >> (rb - 64)) & 1;
+  if (rb < 100) return (rb_alloc[3] >> (rb - 96)) & 1;
+  return 0;
+}
+
+/* adjust_G (lte_mcs.c:249-334) */
+static int adjust_G(const oai4g_frame_parms_t *fp, const uint32_t *rb_alloc, int Qm, int subframe)
+{
+  if (subframe != 0 && subframe != 5 && subframe != 6) return 0;
+  int re = 0, half = fp->N_RB_DL >> 1;
+  if (fp->N_RB_DL & 1) {
+    for (int rb = half - 3; rb <= half + 3; rb++)
+      if (rb_bit(rb_alloc, rb)) re += (rb == half - 3 || rb == half + 3) ? 6 : 12;
+  } else {
+    for (int rb = half - 3; rb < half + 3; rb++)
+      if (rb_bit(rb_alloc, rb)) re += 12;
+  }
+  int Ncp = fp->Ncp;
+  if (subframe == 0) {
+    if (fp->frame_type == 1)
+      return fp->mode1_flag == 0 ? (-Ncp + 14) * re * Qm / 3 : (-Ncp + 29) * re * Qm / 6;
+    return fp->mode1_flag == 0 ? (-Ncp + 17) * re * Qm / 3 : (-Ncp + 35) * re * Qm / 6;
+  }
+  if (subframe == 5) return (fp->frame_type == 0 ? 2 : 1) * re * Qm;
+  if (subframe == 6 && fp->frame_type == 1) return re * Qm;
+  return 0;
+}
+
+/* get_G (lte_mcs.c:336-368); PMCH subframes are not part of this path */
+extern "C" int oai4g_get_G(const oai4g_frame_parms_t *fp, uint16_t nb_rb, const uint32_t *rb_alloc,
+                           uint8_t mod_order, uint8_t Nl, uint8_t num_pdcch_symbols, int frame, uint8_t subframe)
+{
+  (void)frame;
+  int adj = adjust_G(fp, rb_alloc, mod_order, subframe);
+  int nd = fp->Ncp == 0 ? 11 : 9;
+  if (fp->mode1_flag == 0) return (((int)nb_rb * mod_order * ((nd - num_pdcch_symbols) * 12 + 3 * 8)) - adj) * Nl;
+  return ((int)nb_rb * mod_order * ((nd - num_pdcch_symbols) * 12 + 3 * 10)) - adj;
+}
+
+/* lte_segmentation parameter math (lte_segmentation.c:39-126) */
+static int seg_params(uint32_t B, uint32_t *C, uint32_t *Cplus, uint32_t *Cminus, uint32_t *Kplus, uint32_t *Kminus,
+                      uint32_t *F, uint32_t *L)
+{
+  uint32_t Bp;
+  if (B <= 6144) { *L = 0; *C = 1; Bp = B; }
+  else { *L = 24; *C = (B + (6144 - 24) - 1) / (6144 - 24); Bp = B + *C * 24; }
+  if (*C > OAI4G_MAX_SEGMENTS) {
+    printf("lte_segmentation.c: too many segments %u\n", *C);
+    return -1;
+  }
+  uint32_t per = Bp / *C;
+  if (per <= 40) { *Kplus = 40; *Kminus = 0; }
+  else if (per <= 512) { *Kplus = (per >> 3) << 3; *Kminus = per - 8; }
+  else if (per <= 1024) { *Kplus = ((per + 15) >> 4) << 4; *Kminus = *Kplus - 16; }
+  else if (per <= 2048) { *Kplus = ((per + 31) >> 5) << 5; *Kminus = *Kplus - 32; }
+  else if (per <= 6144) { *Kplus = ((per + 63) >> 6) << 6; *Kminus = *Kplus - 64; }
+  else {
+    printf("lte_segmentation.c: Illegal codeword size !!!\n");
+    return -1;
+  }
+  if (*C == 1) { *Cplus = 1; *Kminus = 0; *Cminus = 0; }
+  else { *Cminus = (*C * *Kplus - Bp) / (*Kplus - *Kminus); *Cplus = *C - *Cminus; }
+  *F = *Cplus * *Kplus + *Cminus * *Kminus - Bp;
+  return 0;
+}
+
+/* NULL positions of the sub-block interleaver output for block size K (by simulating
+ * sub_block_interleaving_turbo on a marker input: lte_rate_matching.c:51-130) */
+static const uint8_t k_colperm[32] = {0, 16, 8, 24, 4, 20, 12, 28, 2, 18, 10, 26, 6, 22, 14, 30,
+                                      1, 17, 9, 25, 5, 21, 13, 29, 3, 19, 11, 27, 7, 23, 15, 31};
+static int null_positions(uint32_t K, uint16_t *out, uint32_t maxn)
+{
+  uint32_t D = K + 4, R = (D + 31) >> 5, Kpi = R << 5, ND = Kpi - D;
+  std::vector<uint8_t> d(96 + 3 * D + 16, 0);
+  memset(d.data(), OAI4G_LTE_NULL, 96);
+  uint8_t *dd = d.data() + 96;
+  dd[3 * D + 2] = dd[2];
+  const uint8_t *base = dd - 3 * ND;
+  std::vector<uint8_t> w(3 * Kpi);
+  uint32_t k = 0;
+  for (uint32_t col = 0; col < 32; col++)
+    for (uint32_t row = 0; row < R; row++, k++) {
+      uint32_t j = k_colperm[col] + 32 * row;
+      w[k] = base[3 * j];
+      w[Kpi + 2 * k] = base[3 * j + 1];
+      w[Kpi + 2 * k + 1] = base[3 * j + 5];
+    }
+  if (ND > 0) w[3 * Kpi - 1] = OAI4G_LTE_NULL;
+  uint32_t n = 0;
+  for (uint32_t p = 0; p < 3 * Kpi; p++)
+    if (w[p] == OAI4G_LTE_NULL) {
+      if (n >= maxn) return -1;
+      out[n++] = (uint16_t)p;
+    }
+  return (int)n;
+}
+
+/* QAM tables (dlsch_modulation.c:79-103, 1223-1246) */
+static void qam_tables_scaled(int Qm, int16_t amp, int16_t srho_a, int16_t srho_b, int16_t *ta, int16_t *tb,
+                              int16_t *qa, int16_t *qb)
+{
+  int16_t q16[4], q64[8];
+  for (int a = -1; a <= 1; a += 2)
+    for (int b = -1; b <= 1; b += 2) {
+      q16[(1 + a) + (1 + b) / 2] = (int16_t)(-a * (20724 + b * 10362));
+      for (int c = -1; c <= 1; c += 2)
+        q64[(1 + a) * 2 + (1 + b) + (1 + c) / 2] = (int16_t)(-a * (20225 + b * (10112 + c * 5056)));
+    }
+  int16_t amp_a = (int16_t)(((int32_t)amp * srho_a) >> 13), amp_b = (int16_t)(((int32_t)amp * srho_b) >> 13);
+  for (int i = 0; i < 8; i++) {
+    int16_t v = Qm == 4 ? q16[i & 3] : q64[i];
+    ta[i] = (int16_t)(((int32_t)v * amp_a) >> 15);
+    tb[i] = (int16_t)(((int32_t)v * amp_b) >> 15);
+  }
+  *qa = (int16_t)((amp_a * 23170) >> 15);
+  *qb = (int16_t)((amp_b * 23170) >> 15);
+}
+
+/* ------------------------------------------------------------------------------------------
+ * RE map: restatement of dlsch_modulation's control flow (dlsch_modulation.c:1258-1493 and
+ * allocate_REs_in_RB :139-249, 745-748) producing, per symbol, the data-RE order.
+ * Returns REs allocated, or -1 for an unsupported mode.
+ * ---------------------------------------------------------------------------------------- */
+static int not_pilot(int pilots, int re, int nushift, int use2nd)
+{
+  int off = (pilots == 2) ? 3 : 0, v = nushift % 3;
+  if (pilots == 0) return 1;
+  if (use2nd) return (re != nushift + off) && (re != ((nushift + 6 + off) % 12));
+  return (re != v) && (re != v + 6) && (re != v + 3) && (re != v + 9);
+}
+
+static int build_remap(const oai4g_frame_parms_t *fp, const uint32_t *rb_alloc, int num_pdcch, int subframe,
+                       uint16_t *remap /* [14][N] */, uint32_t *symbase /* [14] */)
+{
+  int N = fp->ofdm_symbol_size, nsymb = fp->Ncp == 0 ? 14 : 12, half = fp->N_RB_DL >> 1;
+  int use2nd = fp->mode1_flag == 1;
+  for (int i = 0; i < 14 * N; i++) remap[i] = 0xFFFF;
+  uint32_t total = 0;
+  for (int l = 0; l < 14; l++) symbase[l] = 0;
+  for (int l = num_pdcch; l < nsymb; l++) {
+    symbase[l] = total;
+    uint32_t idx = 0;
+    int pilots;
+    if (fp->Ncp == 0) pilots = (l == 4 || l == 11) ? 2 : (l == 7 ? 1 : 0);
+    else pilots = (l == 3 || l == 9) ? 2 : (l == 6 ? 1 : 0);
+    int re_offset = fp->first_carrier_offset;
+    for (int rb = 0; rb < fp->N_RB_DL; rb++) {
+      int alloc = rb_bit(rb_alloc, rb), skip_half = 0, skip_dc = 0;
+      if (fp->N_RB_DL & 1) {
+        skip_dc = (rb == half);
+        if (subframe == 0 && rb > half - 3 && rb < half + 3 && l >= (nsymb >> 1) && l < (nsymb >> 1) + 4) alloc = 0;
+        if (subframe == 0 && rb == half - 3 && l >= (nsymb >> 1) && l < (nsymb >> 1) + 4) skip_half = 1;
+        else if (subframe == 0 && rb == half + 3 && l >= (nsymb >> 1) && l < (nsymb >> 1) + 4) skip_half = 2;
+        if (fp->frame_type == 1) {
+          if ((subframe == 0 || subframe == 5) && rb > half - 3 && rb < half + 3 && l == nsymb - 1) alloc = 0;
+          if ((subframe == 0 || subframe == 5) && rb == half - 3 && l == nsymb - 1) skip_half = 1;
+          else if ((subframe == 0 || subframe == 5) && rb == half + 3 && l == nsymb - 1) skip_half = 2;
+          if ((subframe == 1 || subframe == 6) && rb > half - 3 && rb < half + 3 && l == 2) alloc = 0;
+          if ((subframe == 1 || subframe == 6) && rb == half - 3 && l == 2) skip_half = 1;
+          else if ((subframe == 1 || subframe == 6) && rb == half + 3 && l == 2) skip_half = 2;
+        } else {
+          int ls = (nsymb >> 1) - 1, lp = (nsymb >> 1) - 2;
+          if ((subframe == 0 || subframe == 5) && rb > half - 3 && rb < half + 3 && l == ls) alloc = 0;
+          if ((subframe == 0 || subframe == 5) && rb == half - 3 && l == ls) skip_half = 1;
+          else if ((subframe == 0 || subframe == 5) && rb == half + 3 && l == ls) skip_half = 2;
+          if ((subframe == 0 || subframe == 5) && rb > half - 3 && rb < half + 3 && l == lp) alloc = 0;
+          if ((subframe == 0 || subframe == 5) && rb == half - 3 && l == lp) skip_half = 1;
+          else if ((subframe == 0 || subframe == 5) && rb == half + 3 && l == lp) skip_half = 2;
+        }
+      } else {
+        if (subframe == 0 && rb >= half - 3 && rb < half + 3 && l >= (nsymb >> 1) && l < (nsymb >> 1) + 4) alloc = 0;
+        if (fp->frame_type == 1) {
+          if ((subframe == 0 || subframe == 5) && rb >= half - 3 && rb < half + 3 && l == nsymb - 1) alloc = 0;
+          if ((subframe == 1 || subframe == 6) && rb >= half - 3 && rb < half + 3 && l == 2) alloc = 0;
+        } else {
+          if ((subframe == 0 || subframe == 5) && rb >= half - 3 && rb < half + 3 && l == (nsymb >> 1) - 2) alloc = 0;
+          if ((subframe == 0 || subframe == 5) && rb >= half - 3 && rb < half + 3 && l == (nsymb >> 1) - 1) alloc = 0;
+        }
+      }
+      if (alloc) {
+        int first = 0, last = 12, re_off = re_offset, par = 0;
+        if (skip_half == 1) last = 6;
+        else if (skip_half == 2) first = 6;
+        for (int re = first; re < last; re++) {
+          if (skip_dc && re == 6) re_off = re_off - N + 1;
+          if (!not_pilot(pilots, re, fp->nushift, use2nd)) continue;
+          int k = re_off + re;
+          if (k < 0 || k >= N) return -1;
+          remap[l * N + k] = (uint16_t)(idx | (par << 15));
+          idx++;
+          par ^= 1;
+        }
+      }
+      re_offset += 12;
+      if (re_offset >= N) re_offset = skip_dc == 0 ? 1 : 7;
+    }
+    total += idx;
+  }
+  return (int)total;
+}
+
+/* ------------------------------------------------------------------------------------------
+ * configuration
+ * ---------------------------------------------------------------------------------------- */
+struct oai4g_tx_config {
+  oai4g_tx_params_t p;
+  oai4g_frame_parms_t fp;
+  cfg_dev_t h;                      /* host mirror */
+  cfg_dev_t *d = nullptr;           /* device copy */
+  uint16_t *d_remap = nullptr;
+  std::vector<uint16_t> h_remap;
+  int re_count[10];
+};
+
+static int derive_cfg(oai4g_tx_config *cfg, const oai4g_tx_params_t *p, const uint8_t Nl[2], bool need_remap,
+                      int only_sf)
+{
+  memset(&cfg->h, 0, sizeof(cfg->h));
+  cfg->p = *p;
+  oai4g_frame_parms_t &fp = cfg->fp;
+  if (oai4g_init_frame_parms(&fp, p->N_RB_DL, p->Nid_cell, p->Ncp, p->nb_antennas_tx, p->mode1_flag,
+                             p->frame_type) != 0)
+    return -1;
+  cfg_dev_t &h = cfg->h;
+  if (p->n_cw < 1 || p->n_cw > 2) { set_err("n_cw must be 1 or 2"); return -1; }
+  if (p->mimo_mode != OAI4G_SISO && p->mimo_mode != OAI4G_LARGE_CDD) {
+    set_err("mimo_mode %u not supported (SISO and LARGE_CDD only)", p->mimo_mode);
+    return -1;
+  }
+  if (p->mimo_mode == OAI4G_LARGE_CDD && (p->nb_antennas_tx != 2 || p->n_cw != 2)) {
+    set_err("LARGE_CDD requires 2 TX antennas and 2 codewords (dlsch_modulation.c:551)");
+    return -1;
+  }
+  if (p->payload_stride % 4) { set_err("payload_stride must be a multiple of 4"); return -1; }
+  h.N_RB_DL = fp.N_RB_DL;
+  h.N = fp.ofdm_symbol_size;
+  h.log2N = fp.log2_symbol_size;
+  h.cp0 = fp.nb_prefix_samples0;
+  h.cp = fp.nb_prefix_samples;
+  h.spt = fp.samples_per_tti;
+  h.nsymb = fp.symbols_per_tti;
+  h.n_ant = fp.nb_antennas_tx;
+  h.first_carrier = fp.first_carrier_offset;
+  h.n_cw = p->n_cw;
+  h.mimo_mode = p->mimo_mode;
+  h.num_pdcch = p->num_pdcch_symbols;
+  h.rnti = p->rnti;
+  h.Nid_cell = p->Nid_cell;
+  h.first_sf = p->first_subframe % 10;
+  h.sf_step = p->subframe_step;
+  h.payload_stride = p->payload_stride;
+  uint32_t max_tb_words = 0, max_stream_words = 0, max_gw = 0, max_bits = 0;
+  bool rm_fail = false;
+  for (int cw = 0; cw < p->n_cw; cw++) {
+    cw_dev_t &c = h.cw[cw];
+    c.TBS = p->TBS[cw];
+    if (c.TBS == 0 || (c.TBS & 7)) { set_err("TBS[%d]=%u must be a positive multiple of 8", cw, c.TBS); return -1; }
+    c.A_bytes = c.TBS >> 3;
+    if (p->payload_stride < ((c.A_bytes + 3) & ~3u)) {
+      set_err("payload_stride %u < TBS/8 rounded to 4 (%u)", p->payload_stride, (c.A_bytes + 3) & ~3u);
+      return -1;
+    }
+    c.Qm = oai4g_get_Qm(p->mcs[cw]);
+    c.q = p->q[cw];
+    uint32_t C, Cp, Cm, Kp, Km, F, L;
+    if (seg_params(c.TBS + 24, &C, &Cp, &Cm, &Kp, &Km, &F, &L) < 0) { set_err("segmentation failed"); return -1; }
+    c.C = C; c.Cminus = Cm; c.Kplus = Kp; c.Kminus = Km; c.F = F; c.L = L;
+    uint32_t src = 0, maxK = 0;
+    for (uint32_t r = 0; r < C; r++) {
+      uint32_t K = r < Cm ? Km : Kp;
+      int qi = oai4g_qpp_index(K);
+      if (qi < 0) { set_err("illegal code block size %u", K); return -1; }
+      c.K[r] = K;
+      c.f1[r] = oai4g_qpp_table[qi].f1;
+      c.f2[r] = oai4g_qpp_table[qi].f2;
+      c.fill[r] = r == 0 ? F / 8 : 0;
+      c.ncopy[r] = (K - L) / 8 - c.fill[r];
+      c.src[r] = src;
+      src += c.ncopy[r];
+      maxK = K > maxK ? K : maxK;
+      /* rate matching geometry */
+      uint32_t D = K + 4, R = (D + 31) >> 5, Kpi = R << 5;
+      c.R[r] = R; c.Kpi[r] = Kpi; c.ND[r] = Kpi - D;
+      uint32_t Kw = 3 * Kpi;
+      uint32_t Nir = OAI4G_NSOFT / p->Kmimo / (p->Mdlharq < 8 ? p->Mdlharq : 8);
+      uint32_t Ncb = (Nir / C < Kw) ? Nir / C : Kw;
+      if (Ncb < Kw) {
+        printf("Exiting, RM condition (Nir %u, Nsoft %u, Kw %u\n", Nir, OAI4G_NSOFT, Kw);
+        set_err("RM condition: Ncb %u < Kw %u (the reference emits E=0, lte_rate_matching.c:518-521)", Ncb, Kw);
+        rm_fail = true;
+        Ncb = Kw;
+      }
+      c.Ncb[r] = Ncb;
+      c.kidx[r] = (C > 1 && r < Cm) ? 0 : 1;
+    }
+    if (src != (c.TBS + 24) / 8) { set_err("segmentation byte accounting mismatch"); return -1; }
+    for (int ki = 0; ki < 2; ki++) {
+      uint32_t K = ki == 0 ? (Km ? Km : Kp) : Kp;
+      int n = null_positions(K, c.nullpos[ki], OAI4G_MAX_NULLS);
+      if (n < 0) { set_err("too many NULL positions"); return -1; }
+      c.nnull[ki] = (uint32_t)n;
+    }
+    for (uint32_t r = 0; r < C; r++) {
+      uint32_t R = c.R[r], Ncb = c.Ncb[r], nn = c.nnull[c.kidx[r]];
+      const uint16_t *np = c.nullpos[c.kidx[r]];
+      uint32_t ncol8 = R << 3;
+      uint32_t k0 = R * (2 + p->rvidx[cw] * ((Ncb % ncol8 ? 1 : 0) + Ncb / ncol8) * 2);
+      uint32_t before = 0;
+      for (uint32_t i = 0; i < nn; i++)
+        if (np[i] < k0) before++;
+      c.k0c[r] = k0 - before;
+      c.Nnn[r] = Ncb - nn;
+    }
+    uint32_t nw = (maxK + 31) >> 5;
+    c.stream_words = nw + (nw >> 5) + 1;
+    uint32_t tbw = (c.A_bytes + 3 + 3) / 4 + 1;
+    max_tb_words = tbw > max_tb_words ? tbw : max_tb_words;
+    uint32_t strw = C * 3 * c.stream_words;
+    max_stream_words = strw > max_stream_words ? strw : max_stream_words;
+    for (int sf = 0; sf < 10; sf++) {
+      int G = oai4g_get_G(&fp, p->nb_rb, p->rb_alloc, (uint8_t)c.Qm, Nl[cw], p->num_pdcch_symbols, 0, (uint8_t)sf);
+      if (G <= 0 || G > OAI4G_MAX_CHANNEL_BITS) { set_err("G=%d out of range", G); return -1; }
+      c.G[sf] = (uint32_t)G;
+      uint32_t Gp = (uint32_t)G / Nl[cw] / c.Qm, GpmodC = Gp % C, off = 0;
+      for (uint32_t r = 0; r < C; r++) {
+        uint32_t E = (r < C - GpmodC) ? Nl[cw] * c.Qm * (Gp / C) : Nl[cw] * c.Qm * ((GpmodC ? 1 : 0) + Gp / C);
+        c.E[sf][r] = E;
+        c.roff[sf][r] = off;
+        off += E;
+      }
+      c.roff[sf][C] = off;
+      uint32_t gw = (off + 31) / 32;
+      max_gw = gw > max_gw ? gw : max_gw;
+      max_bits = (uint32_t)G > max_bits ? (uint32_t)G : max_bits;
+    }
+    qam_tables_scaled((int)c.Qm, p->amp, p->sqrt_rho_a, p->sqrt_rho_b, c.qam_a, c.qam_b, &c.qpsk_a, &c.qpsk_b);
+  }
+  if (max_gw > OAI4G_MAX_GOLD_WORDS) { set_err("G too large"); return -1; }
+  h.lds_tb_words = max_tb_words;
+  h.lds_stream_words = max_stream_words;
+  h.lds_gold_words = max_gw;
+  /* RE maps */
+  if (need_remap) {
+    uint32_t N = h.N;
+    cfg->h_remap.assign((size_t)10 * 14 * N, 0xFFFF);
+    for (int sf = 0; sf < 10; sf++) {
+      if (only_sf >= 0 && sf != only_sf) continue;
+      int n = build_remap(&fp, p->rb_alloc, p->num_pdcch_symbols, sf, cfg->h_remap.data() + (size_t)sf * 14 * N,
+                          h.symbase[sf]);
+      if (n < 0) { set_err("RE map construction failed"); return -1; }
+      cfg->re_count[sf] = n;
+      for (int cw = 0; cw < p->n_cw; cw++) {
+        uint32_t bits = (uint32_t)n * h.cw[cw].Qm;
+        max_bits = bits > max_bits ? bits : max_bits;
+      }
+    }
+  }
+  h.ebits_words = (max_bits + 31) / 32 + 2;
+  return rm_fail ? -2 : 0;
+}
+
+static int upload_cfg(oai4g_tx_config *cfg)
+{
+  if (!cfg->h_remap.empty()) {
+    HCK(hipMalloc(&cfg->d_remap, cfg->h_remap.size() * 2), -1);
+    HCK(hipMemcpy(cfg->d_remap, cfg->h_remap.data(), cfg->h_remap.size() * 2, hipMemcpyHostToDevice), -1);
+  }
+  cfg->h.remap = cfg->d_remap;
+  cfg->h.gold_x1 = g_gx1;
+  cfg->h.gold_x2j = g_gx2j;
+  cfg->h.tw = g_tw;
+  HCK(hipMalloc(&cfg->d, sizeof(cfg_dev_t)), -1);
+  HCK(hipMemcpy(cfg->d, &cfg->h, sizeof(cfg_dev_t), hipMemcpyHostToDevice), -1);
+  return 0;
+}
+
+static void release_cfg(oai4g_tx_config *cfg)
+{
+  if (cfg->d) hipFree(cfg->d);
+  if (cfg->d_remap) hipFree(cfg->d_remap);
+  cfg->d = nullptr;
+  cfg->d_remap = nullptr;
+}
+
+extern "C" oai4g_tx_config_t *oai4g_tx_config_create(const oai4g_tx_params_t *p)
+{
+  NEED_INIT(nullptr);
+  if (p->Ncp != 0) { set_err("batched path supports normal CP only"); return nullptr; }
+  if (p->N_RB_DL != 6 && p->N_RB_DL != 15 && p->N_RB_DL != 50 && p->N_RB_DL != 100) {
+    set_err("batched path supports N_RB_DL 6, 15, 50, 100 (IDFT 128/256/1024/2048)");
+    return nullptr;
+  }
+  oai4g_tx_config *cfg = new oai4g_tx_config();
+  uint8_t Nl[2] = {1, 1};
+  if (derive_cfg(cfg, p, Nl, true, -1) != 0 || upload_cfg(cfg) != 0) {   /* RM condition (-2) is an error here */
+    release_cfg(cfg);
+    delete cfg;
+    return nullptr;
+  }
+  return cfg;
+}
+
+extern "C" void oai4g_tx_config_destroy(oai4g_tx_config_t *cfg)
+{
+  if (!cfg) return;
+  release_cfg(cfg);
+  delete cfg;
+}
+
+extern "C" uint32_t oai4g_tx_G(const oai4g_tx_config_t *cfg, int cw, int subframe)
+{
+  return cfg->h.cw[cw].G[subframe % 10];
+}
+extern "C" uint32_t oai4g_tx_ebits_words(const oai4g_tx_config_t *cfg) { return cfg->h.ebits_words; }
+extern "C" uint32_t oai4g_tx_iq_samples(const oai4g_tx_config_t *cfg) { return cfg->h.spt; }
+extern "C" size_t oai4g_tx_workspace_bytes(const oai4g_tx_config_t *cfg, int n_sf)
+{
+  return (size_t)n_sf * cfg->h.n_cw * cfg->h.ebits_words * 4;
+}
+
+extern "C" int oai4g_tx_encode(const oai4g_tx_config_t *cfg, int n_sf, const uint8_t *d_payload, void *d_work,
+                               void *stream)
+{
+  NEED_INIT(-1);
+  HCK(oai4g_launch_encode(cfg->d, &cfg->h, n_sf, d_payload, (uint32_t *)d_work, (hipStream_t)stream), -1);
+  return 0;
+}
+
+extern "C" int oai4g_tx_batch(const oai4g_tx_config_t *cfg, int n_sf, const uint8_t *d_payload, void *d_work,
+                              int32_t *d_iq, void *stream)
+{
+  NEED_INIT(-1);
+  if (n_sf <= 0) return 0;
+  hipStream_t s = (hipStream_t)stream;
+  HCK(oai4g_launch_encode(cfg->d, &cfg->h, n_sf, d_payload, (uint32_t *)d_work, s), -1);
+  HCK(oai4g_launch_modofdm(cfg->d, &cfg->h, n_sf, (const uint32_t *)d_work, d_iq, s), -1);
+  return 0;
+}
+
+extern "C" int oai4g_tx_batch_timed(const oai4g_tx_config_t *cfg, int n_sf, const uint8_t *d_payload, void *d_work,
+                                    int32_t *d_iq, void *stream, float *kernel_ms)
+{
+  NEED_INIT(-1);
+  hipStream_t s = (hipStream_t)stream;
+  hipEvent_t ev[3];
+  for (int i = 0; i < 3; i++) HCK(hipEventCreate(&ev[i]), -1);
+  HCK(hipEventRecord(ev[0], s), -1);
+  HCK(oai4g_launch_encode(cfg->d, &cfg->h, n_sf, d_payload, (uint32_t *)d_work, s), -1);
+  HCK(hipEventRecord(ev[1], s), -1);
+  HCK(oai4g_launch_modofdm(cfg->d, &cfg->h, n_sf, (const uint32_t *)d_work, d_iq, s), -1);
+  HCK(hipEventRecord(ev[2], s), -1);
+  HCK(hipEventSynchronize(ev[2]), -1);
+  HCK(hipEventElapsedTime(&kernel_ms[0], ev[0], ev[1]), -1);
+  HCK(hipEventElapsedTime(&kernel_ms[1], ev[1], ev[2]), -1);
+  for (int i = 0; i < 3; i++) hipEventDestroy(ev[i]);
+  return 0;
+}
+
+/* ------------------------------------------------------------------------------------------
+ * device memory helpers
+ * ---------------------------------------------------------------------------------------- */
+extern "C" void *oai4g_dev_alloc(size_t bytes)
+{
+  NEED_INIT(nullptr);
+  void *p = nullptr;
+  HCK(hipMalloc(&p, bytes), nullptr);
+  return p;
+}
+extern "C" void oai4g_dev_free(void *p)
+{
+  if (p) hipFree(p);
+}
+extern "C" int oai4g_memcpy_h2d(void *dst, const void *src, size_t bytes)
+{
+  NEED_INIT(-1);
+  HCK(hipMemcpy(dst, src, bytes, hipMemcpyHostToDevice), -1);
+  return 0;
+}
+extern "C" int oai4g_memcpy_d2h(void *dst, const void *src, size_t bytes)
+{
+  NEED_INIT(-1);
+  HCK(hipMemcpy(dst, src, bytes, hipMemcpyDeviceToHost), -1);
+  return 0;
+}
+extern "C" int oai4g_memset_d(void *dst, int value, size_t bytes)
+{
+  NEED_INIT(-1);
+  HCK(hipMemset(dst, value, bytes), -1);
+  return 0;
+}
+extern "C" int oai4g_sync(void)
+{
+  NEED_INIT(-1);
+  HCK(hipDeviceSynchronize(), -1);
+  return 0;
+}
+extern "C" int oai4g_fill_payload(uint8_t *d_payload, size_t bytes, uint64_t seed, void *stream)
+{
+  NEED_INIT(-1);
+  HCK(oai4g_launch_fill(d_payload, bytes, seed, (hipStream_t)stream), -1);
+  return 0;
+}
+
+/* ------------------------------------------------------------------------------------------
+ * dlsch containers (new_eNB_dlsch / free_eNB_dlsch, dlsch_coding.c:85-220)
+ * ---------------------------------------------------------------------------------------- */
+extern "C" oai4g_dlsch_t *oai4g_new_dlsch(uint8_t Kmimo, uint8_t Mdlharq, uint8_t N_RB_DL)
+{
+  int bw_scaling = N_RB_DL == 6 ? 16 : (N_RB_DL == 25 ? 4 : (N_RB_DL == 50 ? 2 : 1));
+  oai4g_dlsch_t *d = (oai4g_dlsch_t *)calloc(1, sizeof(oai4g_dlsch_t));
+  if (!d) return nullptr;
+  d->Kmimo = Kmimo;
+  d->Mdlharq = Mdlharq;
+  d->sqrt_rho_a = 8192;
+  d->sqrt_rho_b = 8192;
+  for (int i = 0; i < Mdlharq && i < 8; i++) {
+    oai4g_dl_harq_t *h = (oai4g_dl_harq_t *)calloc(1, sizeof(oai4g_dl_harq_t));
+    d->harq_processes[i] = h;
+    h->b = (uint8_t *)calloc(OAI4G_MAX_SEGMENTS * 768 / bw_scaling + 8, 1);
+    h->e = (uint8_t *)calloc(OAI4G_MAX_CHANNEL_BITS + 64, 1);
+    h->Nl = 1;
+    for (int r = 0; r < OAI4G_MAX_SEGMENTS; r++) {
+      h->c[r] = (uint8_t *)calloc(8 + 3 + 768, 1);
+      h->d[r] = (uint8_t *)calloc(OAI4G_D_BYTES + 16, 1);
+      h->w[r] = (uint8_t *)calloc(OAI4G_W_BYTES, 1);
+      memset(h->d[r], OAI4G_LTE_NULL, 96);
+    }
+  }
+  return d;
+}
+
+extern "C" void oai4g_free_dlsch(oai4g_dlsch_t *d)
+{
+  if (!d) return;
+  for (int i = 0; i < 8; i++) {
+    oai4g_dl_harq_t *h = d->harq_processes[i];
+    if (!h) continue;
+    for (int r = 0; r < OAI4G_MAX_SEGMENTS; r++) { free(h->c[r]); free(h->d[r]); free(h->w[r]); }
+    free(h->b);
+    free(h->e);
+    free(h);
+  }
+  free(d);
+}
+
+/* lte_gold_generic (lte_gold.c:151-177): host-side scalar helper */
+extern "C" uint32_t oai4g_lte_gold_generic(uint32_t *x1, uint32_t *x2, uint8_t reset)
+{
+  if (reset) {
+    *x1 = 1u + (1u << 31);
+    *x2 = *x2 ^ ((*x2 ^ (*x2 >> 1) ^ (*x2 >> 2) ^ (*x2 >> 3)) << 31);
+    for (int n = 1; n < 50; n++) gold_step_h(x1, x2);
+  }
+  gold_step_h(x1, x2);
+  return *x1 ^ *x2;
+}
+
+/* ------------------------------------------------------------------------------------------
+ * drop-in coding entry points
+ * ---------------------------------------------------------------------------------------- */
+static uint32_t crc_dropin(const uint8_t *in, int bitlen, uint32_t poly_top)
+{
+  NEED_INIT(0);
+  uint32_t nbytes = (uint32_t)(bitlen + 7) / 8;
+  uint8_t *buf = scratch(nbytes + 64);
+  if (!buf) { set_err("scratch allocation failed"); return 0; }
+  uint32_t *d_out = (uint32_t *)(buf + ((nbytes + 15) & ~15u));
+  uint32_t out = 0;
+  HCK(hipMemcpyAsync(buf, in, nbytes, hipMemcpyHostToDevice, g_scr.s), 0);
+  HCK(oai4g_launch_crc24(buf, bitlen, poly_top, d_out, g_scr.s), 0);
+  HCK(hipMemcpyAsync(&out, d_out, 4, hipMemcpyDeviceToHost, g_scr.s), 0);
+  HCK(hipStreamSynchronize(g_scr.s), 0);
+  return out;
+}
+
+extern "C" uint32_t oai4g_crc24a(const uint8_t *in, int bitlen) { return crc_dropin(in, bitlen, 0x864cfb00u); }
+extern "C" uint32_t oai4g_crc24b(const uint8_t *in, int bitlen) { return crc_dropin(in, bitlen, 0x80006300u); }
+
+extern "C" int oai4g_lte_segmentation(const uint8_t *input_buffer, uint8_t **output_buffers, uint32_t B, uint32_t *C,
+                                      uint32_t *Cplus, uint32_t *Cminus, uint32_t *Kplus, uint32_t *Kminus,
+                                      uint32_t *F)
+{
+  uint32_t L;
+  if (seg_params(B, C, Cplus, Cminus, Kplus, Kminus, F, &L) < 0) return -1;
+  if (input_buffer && output_buffers) {
+    uint32_t k = 0, s = 0;
+    for (; k < (*F >> 3); k++) output_buffers[0][k] = 0;
+    for (uint32_t r = 0; r < *C; r++) {
+      uint32_t Kr = r < *Cminus ? *Kminus : *Kplus;
+      for (; k < ((Kr - L) >> 3); k++) output_buffers[r][k] = input_buffer[s++];
+      if (*C > 1) {
+        uint32_t crc = oai4g_crc24b(output_buffers[r], (int)(Kr - 24)) >> 8;
+        output_buffers[r][(Kr - 24) >> 3] = (uint8_t)(crc >> 16);
+        output_buffers[r][1 + ((Kr - 24) >> 3)] = (uint8_t)(crc >> 8);
+        output_buffers[r][2 + ((Kr - 24) >> 3)] = (uint8_t)crc;
+      }
+      k = 0;
+    }
+  }
+  return 0;
+}
+
+extern "C" void oai4g_threegpplte_turbo_encoder(const uint8_t *input, uint16_t input_length_bytes, uint8_t *output,
+                                                uint8_t F, uint16_t f1, uint16_t f2)
+{
+  (void)F; /* the reference's SSE encoder ignores F (3gpplte_sse.c:380-476) */
+  NEED_INIT();
+  uint32_t K = (uint32_t)input_length_bytes * 8;
+  if (oai4g_qpp_index(K) < 0) {
+    printf("Illegal frame length!\n");
+    return;
+  }
+  uint8_t *buf = scratch(1024 + 3 * 6144 + 64);
+  if (!buf) return;
+  HCK(hipMemcpyAsync(buf, input, input_length_bytes, hipMemcpyHostToDevice, g_scr.s), );
+  HCK(oai4g_launch_turbo_bytes(buf, input_length_bytes, buf + 1024, f1, f2, g_scr.s), );
+  HCK(hipMemcpyAsync(output, buf + 1024, 3 * K + 12, hipMemcpyDeviceToHost, g_scr.s), );
+  HCK(hipStreamSynchronize(g_scr.s), );
+}
+
+extern "C" uint32_t oai4g_sub_block_interleaving_turbo(uint32_t D, uint8_t *d, uint8_t *w)
+{
+  NEED_INIT(0);
+  uint32_t R = (D + 31) >> 5, Kpi = R << 5;
+  size_t dbytes = 96 + 3 * (size_t)D + 3;
+  uint8_t *buf = scratch(dbytes + 3 * Kpi + 64);
+  if (!buf) return 0;
+  HCK(hipMemcpyAsync(buf, d - 96, dbytes, hipMemcpyHostToDevice, g_scr.s), 0);
+  HCK(oai4g_launch_subblock_bytes(D, buf, buf + ((dbytes + 15) & ~(size_t)15), g_scr.s), 0);
+  HCK(hipMemcpyAsync(w, buf + ((dbytes + 15) & ~(size_t)15), 3 * Kpi, hipMemcpyDeviceToHost, g_scr.s), 0);
+  HCK(hipStreamSynchronize(g_scr.s), 0);
+  d[3 * D + 2] = d[2]; /* side effect kept (lte_rate_matching.c:75) */
+  return R;
+}
+
+extern "C" uint32_t oai4g_lte_rate_matching_turbo(uint32_t RTC, uint32_t G, const uint8_t *w, uint8_t *e, uint8_t C,
+                                                  uint32_t Nsoft, uint8_t Mdlharq, uint8_t Kmimo, uint8_t rvidx,
+                                                  uint8_t Qm, uint8_t Nl, uint8_t r, uint8_t nb_rb, uint8_t m)
+{
+  (void)nb_rb;
+  (void)m;
+  NEED_INIT(0);
+  uint32_t Kw = 3 * (RTC << 5);
+  uint32_t Nir = Nsoft / Kmimo / (Mdlharq < 8 ? Mdlharq : 8);
+  uint32_t Ncb = (Nir / C < Kw) ? Nir / C : Kw;
+  if (Ncb < Kw) {
+    printf("Exiting, RM condition (Nir %u, Nsoft %u, Kw %u\n", Nir, Nsoft, Kw);
+    return 0;
+  }
+  uint32_t Gp = G / Nl / Qm, GpmodC = Gp % C, E;
+  if (r < (C - GpmodC)) E = Nl * Qm * (Gp / C);
+  else E = Nl * Qm * ((GpmodC == 0 ? 0 : 1) + (Gp / C));
+  uint32_t ncol8 = RTC << 3;
+  uint32_t k0 = RTC * (2 + rvidx * ((Ncb % ncol8 ? 1 : 0) + Ncb / ncol8) * 2);
+  size_t woff = 0, eoff = (Ncb + 63) & ~(size_t)63, soff = eoff + ((E + 63) & ~(size_t)63);
+  uint8_t *buf = scratch(soff + 64);
+  if (!buf) return 0;
+  HCK(hipMemcpyAsync(buf + woff, w, Ncb, hipMemcpyHostToDevice, g_scr.s), 0);
+  HCK(oai4g_launch_rm_bytes(buf + woff, Ncb, k0, E, buf + eoff, (uint32_t *)(buf + soff), g_scr.s), 0);
+  HCK(hipMemcpyAsync(e, buf + eoff, E, hipMemcpyDeviceToHost, g_scr.s), 0);
+  HCK(hipStreamSynchronize(g_scr.s), 0);
+  return E;
+}
+
+/* parameter block for a single-DLSCH drop-in call */
+static void params_from_dlsch(const oai4g_frame_parms_t *fp, uint8_t num_pdcch, const oai4g_dlsch_t *d0,
+                              const oai4g_dlsch_t *d1, uint8_t subframe, oai4g_tx_params_t *p, uint8_t Nl[2])
+{
+  memset(p, 0, sizeof(*p));
+  const oai4g_dl_harq_t *h0 = d0->harq_processes[d0->current_harq_pid];
+  p->N_RB_DL = fp->N_RB_DL;
+  p->Nid_cell = fp->Nid_cell;
+  p->Ncp = fp->Ncp;
+  p->nb_antennas_tx = fp->nb_antennas_tx;
+  p->mode1_flag = fp->mode1_flag;
+  p->frame_type = fp->frame_type;
+  p->n_cw = d1 ? 2 : 1;
+  p->mimo_mode = h0->mimo_mode;
+  p->num_pdcch_symbols = num_pdcch;
+  p->Kmimo = d0->Kmimo;
+  p->Mdlharq = d0->Mdlharq;
+  p->first_subframe = subframe;
+  p->subframe_step = 0;
+  p->rnti = d0->rnti;
+  p->amp = 512;
+  p->sqrt_rho_a = d0->sqrt_rho_a;
+  p->sqrt_rho_b = d0->sqrt_rho_b;
+  memcpy(p->rb_alloc, h0->rb_alloc, sizeof(p->rb_alloc));
+  p->nb_rb = h0->nb_rb;
+  p->mcs[0] = h0->mcs;
+  p->rvidx[0] = h0->rvidx;
+  p->TBS[0] = h0->TBS;
+  Nl[0] = h0->Nl ? h0->Nl : 1;
+  Nl[1] = 1;
+  if (d1) {
+    const oai4g_dl_harq_t *h1 = d1->harq_processes[d0->current_harq_pid];
+    p->mcs[1] = h1->mcs;
+    p->rvidx[1] = h1->rvidx;
+    p->TBS[1] = h1->TBS;
+    Nl[1] = h1->Nl ? h1->Nl : 1;
+  }
+  uint32_t maxA = p->TBS[0] / 8;
+  if (d1 && p->TBS[1] / 8 > maxA) maxA = p->TBS[1] / 8;
+  p->payload_stride = (maxA + 3 + 15) & ~15u;
+}
+
+extern "C" int oai4g_dlsch_encoding(uint8_t *a, const oai4g_frame_parms_t *frame_parms, uint8_t num_pdcch_symbols,
+                                    oai4g_dlsch_t *dlsch, int frame, uint8_t subframe)
+{
+  (void)frame;
+  NEED_INIT(-1);
+  oai4g_dl_harq_t *h = dlsch->harq_processes[dlsch->current_harq_pid];
+  if (h->round != 0) {
+    set_err("dlsch_encoding: retransmission rounds re-use the stored w (not supported by the drop-in yet)");
+    return -1;
+  }
+  oai4g_tx_params_t p;
+  uint8_t Nl[2];
+  params_from_dlsch(frame_parms, num_pdcch_symbols, dlsch, nullptr, subframe, &p, Nl);
+  if (p.mimo_mode == OAI4G_ALAMOUTI || p.mimo_mode == OAI4G_LARGE_CDD) p.mimo_mode = OAI4G_SISO; /* coding only */
+  if (p.N_RB_DL != 6 && p.N_RB_DL != 15 && p.N_RB_DL != 25 && p.N_RB_DL != 50 && p.N_RB_DL != 100) return -1;
+  oai4g_tx_config cfg;
+  int rc = derive_cfg(&cfg, &p, Nl, false, -1);
+  bool rm_fail = rc == -2; /* reference: every block's rate matcher returns E = 0, e untouched */
+  if (rc != 0 && !rm_fail) return -1;
+  if (upload_cfg(&cfg) != 0) { release_cfg(&cfg); return -1; }
+  cw_dev_t &c = cfg.h.cw[0];
+  uint32_t G = c.G[subframe % 10];
+  size_t off_pay = 0, off_b = 16 * 1024, off_c = off_b + 16 * 1024, off_d = off_c + 16 * (8 + 3 + 768),
+         off_w = off_d + 16 * (size_t)OAI4G_D_BYTES, off_e = off_w + 16 * (size_t)OAI4G_W_BYTES;
+  uint8_t *buf = scratch(off_e + OAI4G_MAX_CHANNEL_BITS + 64);
+  if (!buf) { release_cfg(&cfg); return -1; }
+  HCK(hipMemcpyAsync(buf + off_pay, a, c.A_bytes, hipMemcpyHostToDevice, g_scr.s), -1);
+  enc_debug_t dbg = {buf + off_c, buf + off_d, buf + off_w, rm_fail ? nullptr : buf + off_e, buf + off_b};
+  HCK(oai4g_launch_encode_debug(cfg.d, &cfg.h, 0, subframe % 10, buf + off_pay, dbg, g_scr.s), -1);
+  std::vector<uint8_t> hb(off_e + G);
+  HCK(hipMemcpyAsync(hb.data(), buf, off_e + G, hipMemcpyDeviceToHost, g_scr.s), -1);
+  HCK(hipStreamSynchronize(g_scr.s), -1);
+  release_cfg(&cfg);
+  /* CRC appended into the caller's buffer and copied to b (dlsch_coding.c:296-305) */
+  memcpy(a + c.A_bytes, hb.data() + off_b + c.A_bytes, 3);
+  h->B = c.TBS + 24;
+  memcpy(h->b, a, c.A_bytes + 4); /* memcpy(b, a, A/8 + 4) (dlsch_coding.c:305) */
+  h->C = c.C; h->Cplus = c.C - c.Cminus; h->Cminus = c.Cminus; h->Kplus = c.Kplus; h->Kminus = c.Kminus; h->F = c.F;
+  for (uint32_t r = 0; r < c.C; r++) {
+    uint32_t K = c.K[r];
+    memcpy(h->c[r], hb.data() + off_c + r * (8 + 3 + 768), K / 8);
+    memcpy(h->d[r], hb.data() + off_d + r * (size_t)OAI4G_D_BYTES, 96 + 3 * (K + 4) + 3);
+    memcpy(h->w[r], hb.data() + off_w + r * (size_t)OAI4G_W_BYTES, 3 * c.Kpi[r]);
+    h->RTC[r] = c.R[r];
+  }
+  if (!rm_fail) memcpy(h->e, hb.data() + off_e, G);
+  return 0;
+}
+
+extern "C" void oai4g_dlsch_scrambling(const oai4g_frame_parms_t *frame_parms, int mbsfn_flag, oai4g_dlsch_t *dlsch,
+                                       int G, uint8_t q, uint8_t Ns)
+{
+  NEED_INIT();
+  uint8_t *e = dlsch->harq_processes[dlsch->current_harq_pid]->e;
+  uint32_t x2 = mbsfn_flag == 0 ? ((uint32_t)dlsch->rnti << 14) + ((uint32_t)q << 13) + ((uint32_t)(Ns >> 1) << 9) +
+                                      frame_parms->Nid_cell
+                                : ((uint32_t)(Ns >> 1) << 9) + frame_parms->Nid_cell;
+  int n = (1 + (G >> 5)) * 32; /* the reference writes past G (dlsch_scrambling.c:83-92) */
+  uint8_t *buf = scratch((size_t)n + 64);
+  if (!buf) return;
+  HCK(hipMemcpyAsync(buf, e, n, hipMemcpyHostToDevice, g_scr.s), );
+  HCK(oai4g_launch_scramble_bytes(buf, n, x2, g_gx1, g_gx2j, g_scr.s), );
+  HCK(hipMemcpyAsync(e, buf, n, hipMemcpyDeviceToHost, g_scr.s), );
+  HCK(hipStreamSynchronize(g_scr.s), );
+}
+
+extern "C" int oai4g_dlsch_modulation(int32_t **txdataF, int16_t amp, uint32_t subframe_offset,
+                                      const oai4g_frame_parms_t *frame_parms, uint8_t num_pdcch_symbols,
+                                      oai4g_dlsch_t *dlsch0, oai4g_dlsch_t *dlsch1)
+{
+  NEED_INIT(-1);
+  oai4g_tx_params_t p;
+  uint8_t Nl[2];
+  params_from_dlsch(frame_parms, num_pdcch_symbols, dlsch0, dlsch1, (uint8_t)(subframe_offset % 10), &p, Nl);
+  const oai4g_dl_harq_t *h0 = dlsch0->harq_processes[dlsch0->current_harq_pid];
+  if (h0->Nlayers > 1) return -1;
+  p.amp = amp;
+  if (p.mimo_mode == OAI4G_LARGE_CDD && !dlsch1) p.n_cw = 1;
+  if (p.mimo_mode != OAI4G_SISO && p.mimo_mode != OAI4G_LARGE_CDD) {
+    set_err("dlsch_modulation: mimo_mode %u not supported", p.mimo_mode);
+    return -1;
+  }
+  /* coding geometry is irrelevant here; use the grid-only derivation */
+  oai4g_tx_config cfg;
+  if (p.mimo_mode == OAI4G_LARGE_CDD && p.n_cw == 1) {
+    set_err("LARGE_CDD with one codeword is not supported");
+    return -1;
+  }
+  int rc = derive_cfg(&cfg, &p, Nl, true, (int)(subframe_offset % 10));
+  if (rc != 0 && rc != -2) return -1;
+  if (upload_cfg(&cfg) != 0) { release_cfg(&cfg); return -1; }
+  int sf = (int)(subframe_offset % 10);
+  uint32_t N = cfg.h.N, nsymb = cfg.h.nsymb, nant = cfg.h.n_ant;
+  size_t grid_bytes = (size_t)nant * nsymb * N * 4;
+  uint32_t n_re = (uint32_t)cfg.re_count[sf];
+  size_t e0_bytes = (size_t)n_re * cfg.h.cw[0].Qm + 64, e1_bytes = p.n_cw > 1 ? (size_t)n_re * cfg.h.cw[1].Qm + 64 : 0;
+  size_t off_e0 = (grid_bytes + 255) & ~(size_t)255, off_e1 = off_e0 + ((e0_bytes + 255) & ~(size_t)255);
+  uint8_t *buf = scratch(off_e1 + e1_bytes + 64);
+  if (!buf) { release_cfg(&cfg); return -1; }
+  size_t sym_off = (size_t)N * subframe_offset * nsymb;
+  for (uint32_t aa = 0; aa < nant; aa++)
+    HCK(hipMemcpyAsync(buf + (size_t)aa * nsymb * N * 4, txdataF[aa] + sym_off, (size_t)nsymb * N * 4,
+                       hipMemcpyHostToDevice, g_scr.s), -1);
+  HCK(hipMemcpyAsync(buf + off_e0, h0->e, (size_t)n_re * cfg.h.cw[0].Qm, hipMemcpyHostToDevice, g_scr.s), -1);
+  if (p.n_cw > 1)
+    HCK(hipMemcpyAsync(buf + off_e1, dlsch1->harq_processes[dlsch0->current_harq_pid]->e,
+                       (size_t)n_re * cfg.h.cw[1].Qm, hipMemcpyHostToDevice, g_scr.s), -1);
+  HCK(oai4g_launch_modulate_bytes(cfg.d, &cfg.h, sf, buf + off_e0, p.n_cw > 1 ? buf + off_e1 : nullptr,
+                                  (int32_t *)buf, g_scr.s), -1);
+  for (uint32_t aa = 0; aa < nant; aa++)
+    HCK(hipMemcpyAsync(txdataF[aa] + sym_off, buf + (size_t)aa * nsymb * N * 4, (size_t)nsymb * N * 4,
+                       hipMemcpyDeviceToHost, g_scr.s), -1);
+  HCK(hipStreamSynchronize(g_scr.s), -1);
+  release_cfg(&cfg);
+  return (int)n_re;
+}
+
+/* ------------------------------------------------------------------------------------------
+ * drop-in OFDM entry points
+ * ---------------------------------------------------------------------------------------- */
+static int run_ofdm(const int32_t *input, size_t in_n, int32_t *output, size_t out_lo, size_t out_n, int log2n,
+                    int nsym, const ofdm_sym_t *syms, int scale)
+{
+  NEED_INIT(-1);
+  size_t in_bytes = in_n * 4, out_off = (in_bytes + 255) & ~(size_t)255;
+  uint8_t *buf = scratch(out_off + out_n * 4 + 64);
+  if (!buf) return -1;
+  int32_t *d_in = (int32_t *)buf, *d_out = (int32_t *)(buf + out_off);
+  HCK(hipMemcpyAsync(d_in, input, in_bytes, hipMemcpyHostToDevice, g_scr.s), -1);
+  /* the output window is read-modify-write: samples outside the written symbols stay intact */
+  HCK(hipMemcpyAsync(d_out, output + out_lo, out_n * 4, hipMemcpyHostToDevice, g_scr.s), -1);
+  HCK(oai4g_launch_ofdm(d_in, d_out, log2n, nsym, syms, scale, g_tw, g_scr.s), -1);
+  HCK(hipMemcpyAsync(output + out_lo, d_out, out_n * 4, hipMemcpyDeviceToHost, g_scr.s), -1);
+  HCK(hipStreamSynchronize(g_scr.s), -1);
+  return 0;
+}
+
+static bool log2n_ok(int l) { return l == 6 || l == 7 || l == 8 || l == 10 || l == 11; }
+
+extern "C" void oai4g_PHY_ofdm_mod(const int32_t *input, int32_t *output, uint8_t log2fftsize, uint8_t nb_symbols,
+                                   uint16_t nb_prefix_samples, int etype)
+{
+  if (etype != OAI4G_CYCLIC_PREFIX) {
+    set_err("PHY_ofdm_mod: only CYCLIC_PREFIX is supported");
+    return;
+  }
+  if (!log2n_ok(log2fftsize) || nb_symbols == 0 || nb_symbols > 28) {
+    set_err("PHY_ofdm_mod: unsupported size 2^%u or symbol count %u", log2fftsize, nb_symbols);
+    return;
+  }
+  ofdm_sym_t syms[28];
+  uint32_t N = 1u << log2fftsize;
+  for (int i = 0; i < nb_symbols; i++) {
+    syms[i].in_off = (uint32_t)i * N;
+    syms[i].out_off = (uint32_t)i * N + (uint32_t)(1 + i) * nb_prefix_samples;
+    syms[i].cp = nb_prefix_samples;
+  }
+  size_t out_n = (size_t)nb_symbols * (N + nb_prefix_samples);
+  run_ofdm(input, (size_t)nb_symbols * N, output, 0, out_n, log2fftsize, nb_symbols, syms, 1);
+}
+
+/* one slot = symbol 0 with CP0, then symbols 1..nsymb-1 with CP, in a single launch */
+static void slot_syms(const oai4g_frame_parms_t *fp, uint32_t in_base, uint32_t out_base, int nsym_slot,
+                      ofdm_sym_t *syms)
+{
+  uint32_t N = fp->ofdm_symbol_size;
+  syms[0].in_off = in_base;
+  syms[0].out_off = out_base + fp->nb_prefix_samples0;
+  syms[0].cp = fp->nb_prefix_samples0;
+  for (int i = 1; i < nsym_slot; i++) {
+    syms[i].in_off = in_base + (uint32_t)i * N;
+    syms[i].out_off = out_base + N + fp->nb_prefix_samples0 + (uint32_t)(i - 1) * N + (uint32_t)i * fp->nb_prefix_samples;
+    syms[i].cp = fp->nb_prefix_samples;
+  }
+}
+
+extern "C" void oai4g_normal_prefix_mod(const int32_t *txdataF, int32_t *txdata, uint8_t nsymb,
+                                        const oai4g_frame_parms_t *fp)
+{
+  if (!log2n_ok(fp->log2_symbol_size)) { set_err("normal_prefix_mod: unsupported FFT size"); return; }
+  uint32_t N = fp->ofdm_symbol_size;
+  int short_offset = (2 * nsymb) < fp->symbols_per_tti;
+  int nslots = short_offset + 2 * nsymb / fp->symbols_per_tti;
+  ofdm_sym_t syms[28];
+  int ns = 0;
+  for (int i = 0; i < nslots; i++) {
+    int per = short_offset ? 2 : (fp->symbols_per_tti >> 1);
+    slot_syms(fp, (uint32_t)((i * N * fp->symbols_per_tti) >> 1), (uint32_t)((i * fp->samples_per_tti) >> 1), per,
+              syms + ns);
+    ns += per;
+  }
+  uint32_t in_n = 0, out_hi = 0;
+  for (int i = 0; i < ns; i++) {
+    in_n = syms[i].in_off + N > in_n ? syms[i].in_off + N : in_n;
+    out_hi = syms[i].out_off + N > out_hi ? syms[i].out_off + N : out_hi;
+  }
+  run_ofdm(txdataF, in_n, txdata, 0, out_hi, fp->log2_symbol_size, ns, syms, 1);
+}
+
+extern "C" void oai4g_do_OFDM_mod(int32_t **txdataF, int32_t **txdata, uint32_t frame, uint16_t next_slot,
+                                  const oai4g_frame_parms_t *fp)
+{
+  (void)frame;
+  uint32_t slot_offset_F = (uint32_t)next_slot * fp->ofdm_symbol_size * (fp->Ncp == 1 ? 6 : 7);
+  uint32_t slot_offset = (uint32_t)next_slot * (fp->samples_per_tti >> 1);
+  for (int aa = 0; aa < fp->nb_antennas_tx; aa++) {
+    if (fp->Ncp == 1)
+      oai4g_PHY_ofdm_mod(txdataF[aa] + slot_offset_F, txdata[aa] + slot_offset, fp->log2_symbol_size, 6,
+                         fp->nb_prefix_samples, OAI4G_CYCLIC_PREFIX);
+    else
+      oai4g_normal_prefix_mod(txdataF[aa] + slot_offset_F, txdata[aa] + slot_offset, 7, fp);
+  }
+}
+
+extern "C" int oai4g_idft(int log2n, const int16_t *x, int16_t *y, int scale)
+{
+  if (!log2n_ok(log2n)) { set_err("idft: size 2^%d not supported", log2n); return -1; }
+  ofdm_sym_t s = {0, 0, 0};
+  return run_ofdm((const int32_t *)x, (size_t)1 << log2n, (int32_t *)y, 0, (size_t)1 << log2n, log2n, 1, &s, scale);
+}
+
+extern "C" void oai4g_idft2048(const int16_t *x, int16_t *y, int scale) { oai4g_idft(11, x, y, scale); }
+extern "C" void oai4g_idft1024(const int16_t *x, int16_t *y, int scale) { oai4g_idft(10, x, y, scale); }
+extern "C" void oai4g_idft256(const int16_t *x, int16_t *y, int scale) { oai4g_idft(8, x, y, scale); }
+extern "C" void oai4g_idft128(const int16_t *x, int16_t *y, int scale) { oai4g_idft(7, x, y, scale); }
+extern "C" void oai4g_idft64(const int16_t *x, int16_t *y, int scale) { oai4g_idft(6, x, y, scale); }

@@ -1,0 +1,117 @@
+/*
+ * Internal definitions shared by the host layer (oai4g_host.cpp) and the gfx950 kernels.
+ *
+ * Device-resident configuration ("cfg_dev_t") holds everything that depends only on the
+ * cell / DLSCH parameters and the subframe index: code-block geometry, rate-matching
+ * geometry, per-symbol RE maps, QAM tables, Gold jump tables and IDFT twiddles.  It is built
+ * once per configuration on the host (the same derivations the reference re-does on every
+ * call) and read by every workgroup through scalar loads.
+ */
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/oai4g.h"
+
+#define OAI4G_MAX_CB 16
+#define OAI4G_MAX_NULLS 104
+#define OAI4G_MAX_GOLD_WORDS 4096          /* 64 lanes x 64 words: >= (14*1200*6)/32 */
+#define OAI4G_TW_TOTAL (16 + 64 + 128 + 256 + 512 + 1024 + 2048)
+
+/* twiddle table offsets (packed int16 pairs), indexed by log2 of the level size */
+static inline __host__ __device__ uint32_t oai4g_tw_offset(int log2s)
+{
+  /* 16:0, 64:16, 128:80, 256:208, 512:464, 1024:976, 2048:2000 */
+  switch (log2s) {
+  case 4: return 0;
+  case 6: return 16;
+  case 7: return 80;
+  case 8: return 208;
+  case 9: return 464;
+  case 10: return 976;
+  case 11: return 2000;
+  default: return 0;
+  }
+}
+
+struct cw_dev_t {
+  uint32_t TBS;            /* bits */
+  uint32_t A_bytes;        /* TBS/8 */
+  uint32_t C, Cminus, Kplus, Kminus, F, L;
+  uint32_t Qm;
+  uint32_t q;              /* scrambling codeword index */
+  /* per code block (segmentation, lte_segmentation.c:39-170) */
+  uint32_t K[OAI4G_MAX_CB];
+  uint32_t f1[OAI4G_MAX_CB], f2[OAI4G_MAX_CB];
+  uint32_t src[OAI4G_MAX_CB];   /* byte offset in b (= TB||CRC24A) of the first copied byte */
+  uint32_t fill[OAI4G_MAX_CB];  /* zero filler bytes at the start of the block */
+  uint32_t ncopy[OAI4G_MAX_CB]; /* bytes copied from b */
+  uint32_t crc_off[OAI4G_MAX_CB]; /* word offset of the block's streams in LDS */
+  /* per code block rate-matching geometry (lte_rate_matching.c:51-130, 464-566) */
+  uint32_t R[OAI4G_MAX_CB], Kpi[OAI4G_MAX_CB], ND[OAI4G_MAX_CB], Ncb[OAI4G_MAX_CB];
+  uint32_t Nnn[OAI4G_MAX_CB];   /* non-NULL entries of w[0..Ncb) */
+  uint32_t k0c[OAI4G_MAX_CB];   /* non-NULL entries of w[0..k0): compacted start */
+  uint32_t kidx[OAI4G_MAX_CB];  /* which null list (0: Kminus, 1: Kplus) */
+  uint32_t nnull[2];
+  uint16_t nullpos[2][OAI4G_MAX_NULLS]; /* sorted NULL positions of w for K = Kminus / Kplus */
+  /* per subframe index */
+  uint32_t G[10];
+  uint32_t E[10][OAI4G_MAX_CB];
+  uint32_t roff[10][OAI4G_MAX_CB + 1];
+  int16_t qam_a[8], qam_b[8];   /* amp_rho-scaled QAM levels (dlsch_modulation.c:1223-1246) */
+  int16_t qpsk_a, qpsk_b;
+  uint32_t stream_words;        /* LDS words per stream per block (padded) */
+};
+
+struct cfg_dev_t {
+  uint32_t N_RB_DL, N, log2N, cp0, cp, spt, nsymb, n_ant, first_carrier;
+  uint32_t n_cw, mimo_mode, num_pdcch, rnti, Nid_cell, first_sf, sf_step;
+  uint32_t payload_stride;
+  uint32_t ebits_words;         /* per codeword per subframe */
+  uint32_t lds_tb_words;        /* LDS words for TB || CRC */
+  uint32_t lds_stream_words;    /* LDS words for all block streams of one codeword */
+  uint32_t lds_gold_words;
+  uint32_t pad;
+  cw_dev_t cw[2];
+  uint32_t symbase[10][14];     /* data REs before symbol l */
+  const uint16_t *remap;        /* [10][14][N] data-RE index | parity<<15, 0xFFFF = none */
+  const uint32_t *gold_x1;      /* [64]      x1 state after 50+64l word steps */
+  const uint32_t *gold_x2j;     /* [64][32]  columns of M2^(50+64l) */
+  const uint32_t *tw;           /* OAI4G_TW_TOTAL packed twiddles */
+};
+
+/* ---------------- launch helpers implemented in the .hip files ---------------- */
+/* encoder path */
+hipError_t oai4g_launch_encode(const cfg_dev_t *d_cfg, const cfg_dev_t *h_cfg, int n_sf,
+                               const uint8_t *d_payload, uint32_t *d_ebits, hipStream_t s);
+struct enc_debug_t {
+  uint8_t *c;      /* [C][8+3+768]                         */
+  uint8_t *d;      /* [C][OAI4G_D_BYTES] (offset 96 = d[r][96]) */
+  uint8_t *w;      /* [C][OAI4G_W_BYTES]                   */
+  uint8_t *e;      /* [G] pre-scrambling rate-matcher output */
+  uint8_t *b;      /* [A/8+4] TB with CRC appended          */
+};
+hipError_t oai4g_launch_encode_debug(const cfg_dev_t *d_cfg, const cfg_dev_t *h_cfg, int cw, int sf,
+                                     const uint8_t *d_payload, enc_debug_t dbg, hipStream_t s);
+hipError_t oai4g_launch_crc24(const uint8_t *d_in, int bitlen, uint32_t poly_top, uint32_t *d_out, hipStream_t s);
+hipError_t oai4g_launch_turbo_bytes(const uint8_t *d_c, int nbytes, uint8_t *d_out, uint32_t f1, uint32_t f2,
+                                    hipStream_t s);
+hipError_t oai4g_launch_subblock_bytes(uint32_t D, const uint8_t *d_dfull, uint8_t *d_w, hipStream_t s);
+hipError_t oai4g_launch_rm_bytes(const uint8_t *d_w, uint32_t Ncb, uint32_t k0, uint32_t E, uint8_t *d_e,
+                                 uint32_t *d_status, hipStream_t s);
+hipError_t oai4g_launch_scramble_bytes(uint8_t *d_e, int n_entries, uint32_t c_init, const uint32_t *d_gold_x1,
+                                       const uint32_t *d_gold_x2j, hipStream_t s);
+hipError_t oai4g_launch_fill(uint8_t *d, size_t bytes, uint64_t seed, hipStream_t s);
+
+/* OFDM path */
+hipError_t oai4g_launch_modofdm(const cfg_dev_t *d_cfg, const cfg_dev_t *h_cfg, int n_sf, const uint32_t *d_ebits,
+                                int32_t *d_iq, hipStream_t s);
+struct ofdm_sym_t {
+  uint32_t in_off;   /* int32 index of the symbol's frequency-domain input */
+  uint32_t out_off;  /* int32 index of the symbol's time-domain body (after the CP) */
+  uint32_t cp;       /* cyclic-prefix length written in front of the body */
+};
+hipError_t oai4g_launch_ofdm(const int32_t *d_in, int32_t *d_out, int log2n, int nsym, const ofdm_sym_t *syms,
+                             int scale, const uint32_t *d_tw, hipStream_t s);
+hipError_t oai4g_launch_modulate_bytes(const cfg_dev_t *d_cfg, const cfg_dev_t *h_cfg, int sf,
+                                       const uint8_t *d_e0, const uint8_t *d_e1, int32_t *d_grid, hipStream_t s);

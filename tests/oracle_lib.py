@@ -1,0 +1,194 @@
+"""ctypes bindings to the CPU oracle (oracle/liboracle.so) — TEST INFRASTRUCTURE ONLY.
+
+Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg load this; the product
+package (openair4g_amd) never does.
+"""
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ORACLE_DIR = os.path.join(ROOT, "oracle")
+ORACLE_SO = os.path.join(ORACLE_DIR, "liboracle.so")
+REF_SO = os.path.join(ORACLE_DIR, "_ref", "libref_dfts.so")
+
+_orc = None
+
+
+class OrcFrame(ctypes.Structure):
+    _fields_ = [("N_RB_DL", ctypes.c_uint16), ("Nid_cell", ctypes.c_uint16), ("Ncp", ctypes.c_uint8),
+                ("nushift", ctypes.c_uint8), ("mode1_flag", ctypes.c_uint8), ("nb_antennas_tx", ctypes.c_uint8),
+                ("frame_type", ctypes.c_uint8), ("symbols_per_tti", ctypes.c_uint8),
+                ("log2_symbol_size", ctypes.c_uint8), ("ofdm_symbol_size", ctypes.c_uint16),
+                ("first_carrier_offset", ctypes.c_uint16), ("nb_prefix_samples", ctypes.c_uint16),
+                ("nb_prefix_samples0", ctypes.c_uint16), ("samples_per_tti", ctypes.c_uint32)]
+
+
+class OrcCw(ctypes.Structure):
+    _fields_ = [("e", ctypes.c_void_p), ("mcs", ctypes.c_uint8), ("mimo_mode", ctypes.c_uint8),
+                ("Nlayers", ctypes.c_uint8), ("rb_alloc", ctypes.c_uint32 * 4)]
+
+
+class OrcTxCfg(ctypes.Structure):
+    _fields_ = [("fp", OrcFrame), ("n_cw", ctypes.c_uint8), ("mimo_mode", ctypes.c_uint8),
+                ("num_pdcch_symbols", ctypes.c_uint8), ("subframe", ctypes.c_uint8), ("rnti", ctypes.c_uint16),
+                ("amp", ctypes.c_int16), ("sqrt_rho_a", ctypes.c_int16), ("sqrt_rho_b", ctypes.c_int16),
+                ("Kmimo", ctypes.c_uint8), ("Mdlharq", ctypes.c_uint8), ("rb_alloc", ctypes.c_uint32 * 4),
+                ("nb_rb", ctypes.c_uint16), ("mcs", ctypes.c_uint8 * 2), ("rvidx", ctypes.c_uint8 * 2),
+                ("q", ctypes.c_uint8 * 2), ("TBS", ctypes.c_uint32 * 2)]
+
+
+def build():
+    if not os.path.exists(ORACLE_SO):
+        subprocess.run(["make", "-s", "-C", ORACLE_DIR, "liboracle.so"], check=True)
+
+
+def orc():
+    global _orc
+    if _orc is None:
+        build()
+        L = ctypes.CDLL(ORACLE_SO)
+        L.orc_crc24a.restype = ctypes.c_uint32
+        L.orc_crc24b.restype = ctypes.c_uint32
+        L.orc_subblock_interleave.restype = ctypes.c_uint32
+        L.orc_rate_match.restype = ctypes.c_uint32
+        L.orc_rate_match.argtypes = [ctypes.c_uint32, ctypes.c_uint32, ctypes.c_void_p, ctypes.c_void_p,
+                                     ctypes.c_uint8, ctypes.c_uint32] + [ctypes.c_uint8] * 6
+        L.orc_gold_generic.restype = ctypes.c_uint32
+        L.orc_get_G.restype = ctypes.c_int
+        L.orc_get_G.argtypes = [ctypes.c_uint16, ctypes.c_uint8, ctypes.c_uint8, ctypes.c_uint8, ctypes.c_uint16,
+                                ctypes.c_void_p, ctypes.c_uint8, ctypes.c_uint8, ctypes.c_uint8, ctypes.c_uint8]
+        L.orc_modulation.restype = ctypes.c_int
+        L.orc_modulation.argtypes = [ctypes.c_void_p, ctypes.c_int16, ctypes.c_uint32, ctypes.POINTER(OrcFrame),
+                                     ctypes.c_uint8, ctypes.POINTER(OrcCw), ctypes.POINTER(OrcCw), ctypes.c_int16,
+                                     ctypes.c_int16]
+        L.orc_tx_subframe.restype = ctypes.c_int
+        L.orc_turbo_encode.argtypes = [ctypes.c_void_p, ctypes.c_uint16, ctypes.c_void_p, ctypes.c_uint16,
+                                       ctypes.c_uint16]
+        L.orc_scramble.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_uint32]
+        L.orc_idft.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int]
+        L.orc_ofdm_mod.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint8, ctypes.c_uint8, ctypes.c_uint16]
+        L.orc_normal_prefix_mod.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint8, ctypes.POINTER(OrcFrame)]
+        _orc = L
+    return _orc
+
+
+def ref_dfts():
+    """The reference's own lte_dfts.c (oracle/_ref), or None if it was not built here."""
+    if not os.path.exists(REF_SO):
+        return None
+    return ctypes.CDLL(REF_SO)
+
+
+def P(a):
+    return ctypes.c_void_p(a.ctypes.data)
+
+
+def frame(N_RB_DL, Nid_cell=0, Ncp=0, nb_antennas_tx=1, mode1_flag=1, frame_type=0):
+    fp = OrcFrame()
+    assert orc().orc_init_frame(ctypes.byref(fp), N_RB_DL, Nid_cell, Ncp, nb_antennas_tx, mode1_flag,
+                                frame_type) == 0
+    return fp
+
+
+def crc24a(data, bitlen):
+    a = np.ascontiguousarray(data, dtype=np.uint8)
+    return orc().orc_crc24a(P(a), bitlen)
+
+
+def crc24b(data, bitlen):
+    a = np.ascontiguousarray(data, dtype=np.uint8)
+    return orc().orc_crc24b(P(a), bitlen)
+
+
+def turbo_encode(c, f1, f2):
+    c = np.ascontiguousarray(c, dtype=np.uint8)
+    d = np.zeros(3 * 8 * len(c) + 12, dtype=np.uint8)
+    orc().orc_turbo_encode(P(c), len(c), P(d), f1, f2)
+    return d
+
+
+def subblock(d, D):
+    """d = d^(i) interleaved bytes (3D entries, no prefix).  Returns (R, w, d_with_side_effect)."""
+    buf = np.full(96 + 3 * D + 16, 2, dtype=np.uint8)
+    buf[96:96 + len(d)] = d
+    R = (D + 31) >> 5
+    w = np.zeros(3 * 32 * R, dtype=np.uint8)
+    rtc = orc().orc_subblock_interleave(D, ctypes.c_void_p(buf.ctypes.data + 96), P(w))
+    return rtc, w, buf
+
+
+def rate_match(RTC, G, w, C, r, Qm, rvidx=0, Nl=1, Kmimo=1, Mdlharq=8, Nsoft=1827072):
+    w = np.ascontiguousarray(w, dtype=np.uint8)
+    e = np.zeros(G + 64, dtype=np.uint8)
+    E = orc().orc_rate_match(RTC, G, P(w), P(e), C, Nsoft, Mdlharq, Kmimo, rvidx, Qm, Nl, r)
+    return e[:E]
+
+
+def scramble(e, G, c_init):
+    buf = np.zeros((1 + (G >> 5)) * 32 + 32, dtype=np.uint8)
+    buf[:len(e)] = e
+    orc().orc_scramble(P(buf), G, c_init)
+    return buf
+
+
+def idft(x, scale=1):
+    x = np.ascontiguousarray(x, dtype=np.int16)
+    y = np.zeros_like(x)
+    orc().orc_idft(int(len(x) // 2).bit_length() - 1, P(x), P(y), scale)
+    return y
+
+
+def get_G(N_RB_DL, Ncp, mode1_flag, frame_type, nb_rb, rb_alloc, Qm, Nl, num_pdcch, subframe):
+    ra = (ctypes.c_uint32 * 4)(*rb_alloc)
+    return orc().orc_get_G(N_RB_DL, Ncp, mode1_flag, frame_type, nb_rb, ra, Qm, Nl, num_pdcch, subframe)
+
+
+def tx_cfg_from_params(p, subframe):
+    """Oracle config mirroring an openair4g_amd.TxParams (same semantics)."""
+    c = OrcTxCfg()
+    c.fp = frame(p.N_RB_DL, p.Nid_cell, p.Ncp, p.nb_antennas_tx, p.mode1_flag, p.frame_type)
+    c.n_cw = p.n_cw
+    c.mimo_mode = p.mimo_mode
+    c.num_pdcch_symbols = p.num_pdcch_symbols
+    c.subframe = subframe
+    c.rnti = p.rnti
+    c.amp = p.amp
+    c.sqrt_rho_a = p.sqrt_rho_a
+    c.sqrt_rho_b = p.sqrt_rho_b
+    c.Kmimo = p.Kmimo
+    c.Mdlharq = p.Mdlharq
+    for i in range(4):
+        c.rb_alloc[i] = p.rb_alloc[i]
+    c.nb_rb = p.nb_rb
+    for cw in range(2):
+        c.mcs[cw] = p.mcs[cw]
+        c.rvidx[cw] = p.rvidx[cw]
+        c.q[cw] = p.q[cw]
+        c.TBS[cw] = p.TBS[cw]
+    return c
+
+
+def tx_subframe(cfg, payloads, want_e=False):
+    """Run the oracle on one subframe.  payloads: list of byte arrays (TBS/8 each).
+    Returns (txdata [n_ant][spt] int32, txdataF [n_ant][14*N], e list)."""
+    fp = cfg.fp
+    n_ant = fp.nb_antennas_tx
+    N = fp.ofdm_symbol_size
+    bufs = []
+    for cw in range(cfg.n_cw):
+        b = np.zeros(cfg.TBS[cw] // 8 + 8, dtype=np.uint8)
+        b[:cfg.TBS[cw] // 8] = payloads[cw][:cfg.TBS[cw] // 8]
+        bufs.append(b)
+    pay = (ctypes.c_void_p * 2)(*[P(b).value for b in bufs] + [None] * (2 - len(bufs)))
+    txF = [np.zeros(14 * N, dtype=np.int32) for _ in range(n_ant)]
+    txd = [np.zeros(fp.samples_per_tti, dtype=np.int32) for _ in range(n_ant)]
+    fptrs = (ctypes.c_void_p * n_ant)(*[a.ctypes.data for a in txF])
+    dptrs = (ctypes.c_void_p * n_ant)(*[a.ctypes.data for a in txd])
+    es = [np.zeros(14 * 1200 * 6 + 64, dtype=np.uint8) for _ in range(cfg.n_cw)]
+    eptrs = (ctypes.c_void_p * 2)(*[e.ctypes.data for e in es] + [None] * (2 - len(es)))
+    rc = orc().orc_tx_subframe(ctypes.byref(cfg), pay, fptrs, dptrs, eptrs if want_e else None)
+    assert rc == 0
+    return np.stack(txd), np.stack(txF), es
