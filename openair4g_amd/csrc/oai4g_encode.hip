@@ -675,11 +675,11 @@ hipError_t oai4g_launch_subblock_bytes(uint32_t D, const uint8_t *d_dfull, uint8
 
 /* lte_rate_matching_turbo on caller bytes: compaction of the non-NULL entries of w[0..Ncb)
  * (block-wide prefix count), then e[k] = compact[(start + k) mod nnz].  One workgroup. */
-__global__ void __launch_bounds__(1024) k_rm_bytes(const uint8_t *__restrict__ w, uint32_t Ncb, uint32_t k0,
+__global__ void __launch_bounds__(256) k_rm_bytes(const uint8_t *__restrict__ w, uint32_t Ncb, uint32_t k0,
                                                    uint32_t E, uint8_t *__restrict__ e, uint32_t *status)
 {
   extern __shared__ uint8_t comp[];
-  __shared__ uint32_t wsum[16];
+  __shared__ uint32_t wsum[4];
   __shared__ uint32_t s_start, s_total;
   const uint32_t tid = threadIdx.x, nth = blockDim.x;
   uint32_t per = (Ncb + nth - 1) / nth, a = tid * per, b = min(a + per, Ncb);
@@ -713,8 +713,7 @@ __global__ void __launch_bounds__(1024) k_rm_bytes(const uint8_t *__restrict__ w
 hipError_t oai4g_launch_rm_bytes(const uint8_t *d_w, uint32_t Ncb, uint32_t k0, uint32_t E, uint8_t *d_e,
                                  uint32_t *d_status, hipStream_t s)
 {
-  hipFuncSetAttribute((const void *)k_rm_bytes, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-  hipLaunchKernelGGL(k_rm_bytes, dim3(1), dim3(1024), Ncb, s, d_w, Ncb, k0, E, d_e, d_status);
+  hipLaunchKernelGGL(k_rm_bytes, dim3(1), dim3(256), (Ncb + 15) & ~15u, s, d_w, Ncb, k0, E, d_e, d_status);
   return hipGetLastError();
 }
 
