@@ -1,0 +1,64 @@
+"""Summarise a rocprofv3 session (kernel stats + FETCH_SIZE / WRITE_SIZE passes) into
+profiles/: a markdown summary and traffic_<config>.json consumed by bench.py.
+
+HBM bytes per launch follow MI355X_MICROARCH.md §HBM: FETCH_SIZE and WRITE_SIZE are KiB;
+on gfx950 FETCH_SIZE reports half the bytes of a wide streaming read, so it is doubled.
+"""
+import collections
+import csv
+import json
+import os
+import sys
+
+KMAP = {"k_encode": "encode_rm_scramble", "k_modofdm": "modulate_idft_cp"}
+
+
+def short(name):
+    for k, v in KMAP.items():
+        if name.startswith(k) or name.startswith("void " + k):
+            return v
+    return None
+
+
+def main(prof_dir, tag, config, out_dir):
+    stats = list(csv.DictReader(open(os.path.join(prof_dir, f"trace_{tag}", "run_kernel_stats.csv"))))
+    pmc = collections.defaultdict(list)
+    res = {}
+    for sub, ctr in (("fetch", "FETCH_SIZE"), ("write", "WRITE_SIZE")):
+        for r in csv.DictReader(open(os.path.join(prof_dir, f"{sub}_{tag}", "run_counter_collection.csv"))):
+            k = short(r["Kernel_Name"])
+            if k:
+                pmc[(k, ctr)].append(float(r["Counter_Value"]))
+                res[k] = {x: r[x] for x in ("Grid_Size", "Workgroup_Size", "LDS_Block_Size", "Scratch_Size",
+                                            "VGPR_Count", "SGPR_Count")}
+    traffic = {}
+    lines = [f"# rocprofv3 summary {tag} — config {config}", "",
+             "Command: `rocprofv3 --kernel-trace --stats -- python3 bench.py --steps 5 --warmup 1 --no-cpu-baseline`"
+             f" (+ separate `--pmc FETCH_SIZE` and `--pmc WRITE_SIZE` passes)", "",
+             "| kernel | calls | avg µs | min µs | max µs | % |", "|---|---|---|---|---|---|"]
+    for s in stats:
+        lines.append(f"| `{s['Name'][:70]}` | {s['Calls']} | {float(s['AverageNs'])/1e3:.1f} | "
+                     f"{float(s['MinNs'])/1e3:.1f} | {float(s['MaxNs'])/1e3:.1f} | {float(s['Percentage']):.1f} |")
+    lines += ["", "| kernel | FETCH_SIZE KiB/launch | WRITE_SIZE KiB/launch | HBM bytes/launch (2xFETCH+WRITE) | resources |",
+              "|---|---|---|---|---|"]
+    for k in sorted({k for k, _ in pmc}):
+        f = sum(pmc[(k, "FETCH_SIZE")]) / max(1, len(pmc[(k, "FETCH_SIZE")]))
+        w = sum(pmc[(k, "WRITE_SIZE")]) / max(1, len(pmc[(k, "WRITE_SIZE")]))
+        b = (2 * f + w) * 1024
+        traffic[k] = b
+        lines.append(f"| {k} | {f:.0f} | {w:.0f} | {b/1e6:.1f} MB | {res.get(k)} |")
+    os.makedirs(out_dir, exist_ok=True)
+    open(os.path.join(out_dir, f"rocprof_{tag}_{config}.md"), "w").write("\n".join(lines) + "\n")
+    json.dump(traffic, open(os.path.join(out_dir, f"traffic_{config}.json"), "w"), indent=1)
+    for s in ("trace", "fetch", "write"):
+        d = os.path.join(prof_dir, f"{s}_{tag}")
+        for fn in os.listdir(d):
+            if fn.endswith("stats.csv") or fn.endswith("counter_collection.csv"):
+                src = os.path.join(d, fn)
+                dst = os.path.join(out_dir, f"{tag}_{config}_{s}_{fn}")
+                open(dst, "w").write(open(src).read())
+    print("\n".join(lines))
+
+
+if __name__ == "__main__":
+    main(sys.argv[1], sys.argv[2], sys.argv[3], sys.argv[4] if len(sys.argv) > 4 else "profiles")
