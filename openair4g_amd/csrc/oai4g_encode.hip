@@ -62,8 +62,6 @@ static constexpr rsc_tables_t make_rsc_tables()
 
 __constant__ rsc_tables_t c_rsc = make_rsc_tables();
 
-static __constant__ uint8_t c_colperm[32] = {0, 16, 8, 24, 4, 20, 12, 28, 2, 18, 10, 26, 6, 22, 14, 30,
-                                             1, 17, 9, 25, 5, 21, 13, 29, 3, 19, 11, 27, 7, 23, 15, 31};
 
 static __device__ __forceinline__ uint32_t lsw(uint32_t w) { return w + (w >> 5); } /* stream word swizzle */
 
@@ -82,41 +80,6 @@ static __device__ __forceinline__ uint32_t crc_mulmod(uint32_t a, uint32_t b, ui
     if ((b >> i) & 1u) r ^= a;
   }
   return r;
-}
-
-/* x^(8n) mod P by square-and-multiply on x^8 */
-static __device__ __forceinline__ uint32_t crc_xpow8(uint32_t n, uint32_t poly)
-{
-  uint32_t result = 1, base = 0x100;   /* x^8 (degree < 24) */
-  while (n) {
-    if (n & 1u) result = crc_mulmod(result, base, poly);
-    base = crc_mulmod(base, base, poly);
-    n >>= 1;
-  }
-  return result;
-}
-
-/* Workgroup-cooperative CRC of buf[0..nbytes) (LDS bytes).  tab: 256-entry LDS table of the
- * 24-bit byte remainders.  Returns the 24-bit CRC in every thread.  red: >= 8 LDS words. */
-static __device__ uint32_t crc24_block(const uint8_t *buf, uint32_t nbytes, uint32_t poly, const uint32_t *tab,
-                                       uint32_t *red)
-{
-  const uint32_t tid = threadIdx.x, nth = blockDim.x;
-  uint32_t per = (nbytes + nth - 1) / nth;
-  uint32_t start = tid * per, end = min(start + per, nbytes);
-  uint32_t reg = 0;
-  for (uint32_t i = start; i < end; i++) reg = ((reg << 8) ^ tab[((reg >> 16) ^ buf[i]) & 0xffu]) & 0xffffffu;
-  if (start < nbytes && end < nbytes && reg) reg = crc_mulmod(reg, crc_xpow8(nbytes - end, poly), poly);
-  if (start >= nbytes) reg = 0;
-  /* xor-reduce: wave, then across waves */
-  for (int off = 32; off > 0; off >>= 1) reg ^= __shfl_xor(reg, off, 64);
-  __syncthreads();
-  if ((tid & 63) == 0) red[tid >> 6] = reg;
-  __syncthreads();
-  uint32_t tot = 0;
-  for (uint32_t wv = 0; wv < (nth + 63) / 64; wv++) tot ^= red[wv];
-  __syncthreads();
-  return tot;
 }
 
 static __device__ void crc_table_init(uint32_t *tab, uint32_t poly)
@@ -160,28 +123,68 @@ static __device__ void gold_generate(uint32_t *gold, uint32_t nwords, uint32_t c
 }
 
 /* ---------------------------------------------------------------------------------------
- * Turbo encoding of all code blocks of a codeword held in LDS.
- * streams: per block r, 3 streams (sys, p1, p2) of sw words each (swizzled), at
- * strm + r*3*sw.  tails: 2 words per block (6 tail bits per constituent encoder).
- * scan: 1 byte per (block, encoder, chunk).
+ * Wave-cooperative CRC-24 (crc_byte.c:98-153 restated for 64 lanes).  The message is
+ * virtually front-padded with zero bytes (which leave a zero-initialised CRC register
+ * unchanged) to 64*per bytes; lane l hashes chunk l with the byte table, then a 6-level
+ * shuffle tree combines neighbours: crc(L||R) = crc(L)*x^(8|R|) ^ crc(R) mod P.
  * ------------------------------------------------------------------------------------- */
-struct cb_geom_t {
-  uint32_t C;
-  uint32_t sw;              /* stream words per block (swizzled, padded) */
-  uint32_t K[OAI4G_MAX_CB];
-  uint32_t f1[OAI4G_MAX_CB], f2[OAI4G_MAX_CB];
+static __device__ __forceinline__ uint32_t crc_step(uint32_t reg, uint32_t byte, const uint32_t *tab)
+{
+  return ((reg << 8) & 0xffffffu) ^ tab[((reg >> 16) ^ byte) & 0xffu];
+}
+
+static __device__ uint32_t crc24_wave(const uint8_t *buf, uint32_t nbytes, uint32_t poly, const uint32_t *tab)
+{
+  const uint32_t lane = threadIdx.x & 63;
+  uint32_t per = (nbytes + 63) >> 6;
+  if (per == 0) return 0;
+  int vstart = (int)(lane * per) - (int)(per * 64 - nbytes);
+  uint32_t reg = 0;
+  for (uint32_t i = 0; i < per; i++) {
+    int idx = vstart + (int)i;
+    if (idx >= 0) reg = crc_step(reg, buf[idx], tab);
+  }
+  uint32_t m = 1;
+  for (uint32_t i = 0; i < per; i++) m = crc_step(m, 0, tab);   /* x^(8 per) mod P */
+  for (int d = 0; d < 6; d++) {
+    uint32_t other = __shfl_down(reg, 1u << d, 64);
+    if ((lane & ((2u << d) - 1u)) == 0) reg = crc_mulmod(reg, m, poly) ^ other;
+    m = crc_mulmod(m, m, poly);
+  }
+  return __shfl(reg, 0, 64);
+}
+
+/* ---------------------------------------------------------------------------------------
+ * Turbo encoding of all code blocks of a codeword held in LDS (see file header).
+ * Items: (block r, encoder e, 32-bit chunk j), flattened; ib[r] = first item of block r.
+ * ------------------------------------------------------------------------------------- */
+struct enc_tabs_t {            /* LDS copy of the RSC tables (lane-varying indices) */
+  uint8_t next[8][16];
+  uint8_t par[8][16];
+  uint8_t apow[8][8];
 };
 
-/* input word of chunk j for encoder e (0: systematic, 1: QPP-interleaved systematic) */
-static __device__ __forceinline__ uint32_t enc_input(const uint32_t *sys, uint32_t K, uint32_t f1, uint32_t f2,
-                                                     uint32_t j, int e)
+struct blk_info_t {            /* per-codeword block table in LDS */
+  uint32_t C, sw;
+  uint32_t K[OAI4G_MAX_CB], f1[OAI4G_MAX_CB], f2[OAI4G_MAX_CB];
+  uint32_t ib[OAI4G_MAX_CB + 1];   /* item base per block */
+  uint32_t inwb[OAI4G_MAX_CB];     /* interleaved-word base per block */
+};
+
+static __device__ __forceinline__ uint32_t find_block(const blk_info_t *bi, uint32_t it)
 {
-  if (e == 0) return sys[lsw(j)];
-  uint32_t k = 32 * j;
-  uint32_t n = min(32u, K - k);
-  uint64_t kk = k;
-  uint32_t pi = (uint32_t)((f1 * kk + (uint64_t)f2 * kk * kk) % K);
-  uint32_t dl = (uint32_t)((f1 + (uint64_t)f2 * (2 * kk + 1)) % K);
+  uint32_t r = 0;
+  while (r + 1 < bi->C && it >= bi->ib[r + 1]) r++;
+  return r;
+}
+
+/* interleaved input word of chunk j: bits c'_k = c_Pi(k), Pi(k) = (f1 k + f2 k^2) mod K */
+static __device__ __forceinline__ uint32_t qpp_word(const uint32_t *sys, uint32_t K, uint32_t f1, uint32_t f2,
+                                                    uint32_t j)
+{
+  uint32_t k = 32 * j, n = min(32u, K - k);
+  uint32_t pi = (((f2 * k) % K) * k + f1 * k) % K;            /* fits 32 bits for K <= 6144 */
+  uint32_t dl = (f1 + ((f2 * ((2 * k + 1) % K)) % K)) % K;     /* Pi(k+1) - Pi(k) */
   uint32_t d2 = (2u * f2) % K;
   uint32_t word = 0;
   for (uint32_t b = 0; b < n; b++) {
@@ -194,77 +197,69 @@ static __device__ __forceinline__ uint32_t enc_input(const uint32_t *sys, uint32
   return word;
 }
 
-static __device__ void turbo_encode_blocks(uint32_t *strm, uint32_t *tails, uint8_t *scan, const cb_geom_t &g)
+static __device__ void turbo_encode_blocks(uint32_t *strm, const blk_info_t *bi, uint32_t *tails, uint32_t *inw2,
+                                           uint8_t *scanA, uint8_t *scanB, const enc_tabs_t *tb)
 {
   const uint32_t tid = threadIdx.x, nth = blockDim.x;
-  /* flattened item list: for r, e, j ; per-(r,e) offsets */
-  uint32_t nitems = 0;
-  uint32_t base[OAI4G_MAX_CB];
-  for (uint32_t r = 0; r < g.C; r++) {
-    base[r] = nitems;
-    nitems += 2 * ((g.K[r] + 31) >> 5);
-  }
-  /* pass 1: zero-start exit state of every chunk */
+  const uint32_t nitems = bi->ib[bi->C], sw = bi->sw;
+  /* pass 1: chunk input words and zero-start exit states */
   for (uint32_t it = tid; it < nitems; it += nth) {
-    uint32_t r = 0;
-    while (r + 1 < g.C && it >= base[r + 1]) r++;
-    uint32_t nch = (g.K[r] + 31) >> 5, loc = it - base[r];
-    int e = loc >= nch;
-    uint32_t j = e ? loc - nch : loc;
-    const uint32_t *sys = strm + r * 3 * g.sw;
-    uint32_t u = enc_input(sys, g.K[r], g.f1[r], g.f2[r], j, e);
-    uint32_t nnib = min(32u, g.K[r] - 32 * j) >> 2;
-    uint8_t s = 0;
-    for (uint32_t q = 0; q < nnib; q++) s = c_rsc.next[s][(u >> (4 * q)) & 15u];
-    scan[it] = s;
+    uint32_t r = find_block(bi, it);
+    uint32_t K = bi->K[r], nch = (K + 31) >> 5, loc = it - bi->ib[r];
+    uint32_t e = loc >= nch, j = e ? loc - nch : loc;
+    const uint32_t *sys = strm + r * 3 * sw;
+    uint32_t u;
+    if (e) {
+      u = qpp_word(sys, K, bi->f1[r], bi->f2[r], j);
+      inw2[bi->inwb[r] + j] = u;
+    } else {
+      u = sys[lsw(j)];
+    }
+    uint32_t nnib = min(32u, K - 32 * j) >> 2;
+    uint32_t s = 0;
+    for (uint32_t q = 0; q < nnib; q++) s = tb->next[s][(u >> (4 * q)) & 15u];
+    scanA[it] = (uint8_t)s;
   }
   __syncthreads();
-  /* pass 2: segmented inclusive scan v[j] ^= A^(32*2^d) v[j-2^d] */
+  /* pass 2: segmented Hillis-Steele scan, state_after(j) = A^32 state_after(j-1) ^ s0(j) */
+  uint8_t *src = scanA, *dst = scanB;
   for (int d = 0; d < 8; d++) {
     uint32_t span = 1u << d;
-    uint8_t tmp[24];
-    int cnt = 0;
-    for (uint32_t it = tid; it < nitems; it += nth, cnt++) {
-      uint32_t r = 0;
-      while (r + 1 < g.C && it >= base[r + 1]) r++;
-      uint32_t nch = (g.K[r] + 31) >> 5, loc = it - base[r];
+    for (uint32_t it = tid; it < nitems; it += nth) {
+      uint32_t r = find_block(bi, it);
+      uint32_t nch = (bi->K[r] + 31) >> 5, loc = it - bi->ib[r];
       uint32_t j = loc >= nch ? loc - nch : loc;
-      uint8_t v = scan[it];
-      if (j >= span) v ^= c_rsc.apow[d][scan[it - span]];
-      if (cnt < 24) tmp[cnt] = v;
+      uint32_t v = src[it];
+      if (j >= span) v ^= tb->apow[d][src[it - span]];
+      dst[it] = (uint8_t)v;
     }
     __syncthreads();
-    cnt = 0;
-    for (uint32_t it = tid; it < nitems; it += nth, cnt++)
-      if (cnt < 24) scan[it] = tmp[cnt];
-    __syncthreads();
+    uint8_t *t = src; src = dst; dst = t;
   }
-  /* pass 3: re-encode each chunk from its entry state -> parity words, tails */
+  /* pass 3: re-encode from the true entry state -> parity words; tails */
   for (uint32_t it = tid; it < nitems; it += nth) {
-    uint32_t r = 0;
-    while (r + 1 < g.C && it >= base[r + 1]) r++;
-    uint32_t nch = (g.K[r] + 31) >> 5, loc = it - base[r];
-    int e = loc >= nch;
-    uint32_t j = e ? loc - nch : loc;
-    uint32_t *sys = strm + r * 3 * g.sw;
-    uint32_t u = enc_input(sys, g.K[r], g.f1[r], g.f2[r], j, e);
-    uint8_t s = j ? scan[it - 1] : 0;
-    uint32_t nnib = min(32u, g.K[r] - 32 * j) >> 2, par = 0;
+    uint32_t r = find_block(bi, it);
+    uint32_t K = bi->K[r], nch = (K + 31) >> 5, loc = it - bi->ib[r];
+    uint32_t e = loc >= nch, j = e ? loc - nch : loc;
+    uint32_t *sys = strm + r * 3 * sw;
+    uint32_t u = e ? inw2[bi->inwb[r] + j] : sys[lsw(j)];
+    uint32_t s = j ? src[it - 1] : 0;
+    uint32_t nnib = min(32u, K - 32 * j) >> 2, par = 0;
     for (uint32_t q = 0; q < nnib; q++) {
       uint32_t nib = (u >> (4 * q)) & 15u;
-      par |= (uint32_t)c_rsc.par[s][nib] << (4 * q);
-      s = c_rsc.next[s][nib];
+      par |= (uint32_t)tb->par[s][nib] << (4 * q);
+      s = tb->next[s][nib];
     }
-    sys[(1 + e) * g.sw + lsw(j)] = par;
+    sys[(1 + e) * sw + lsw(j)] = par;
     if (j == nch - 1) {
-      /* trellis termination (3gpplte_sse.c:104-109, 440-471): bits x,z per step */
-      uint32_t tb = 0;
+      /* trellis termination (3gpplte_sse.c:104-109, 440-471): (x, z) per step */
+      uint32_t tbits = 0;
       for (int stp = 0; stp < 3; stp++) {
         uint32_t z = ((s >> 2) ^ s) & 1u, x = (s ^ (s >> 1)) & 1u;
         s >>= 1;
-        tb |= (x << (2 * stp)) | (z << (2 * stp + 1));
+        tbits |= (x << (2 * stp)) | (z << (2 * stp + 1));
       }
-      tails[2 * r + e] = tb;
+      tails[2 * r + e] = tbits;
     }
   }
   __syncthreads();
@@ -276,7 +271,7 @@ static __device__ __forceinline__ uint32_t tail_bit(const uint32_t *tails, uint3
   return m < 6 ? (tails[2 * r] >> m) & 1u : (tails[2 * r + 1] >> (m - 6)) & 1u;
 }
 
-/* value of d^(s)_idx for block r: stream bit if idx < K, else tail (lte_rate_matching.c:75-110) */
+/* value of d^(s)_idx for block r: stream bit if idx < K, else tail */
 static __device__ __forceinline__ uint32_t dstream_bit(const uint32_t *blk, uint32_t sw, const uint32_t *tails,
                                                        uint32_t r, uint32_t K, uint32_t s, uint32_t idx)
 {
@@ -284,7 +279,9 @@ static __device__ __forceinline__ uint32_t dstream_bit(const uint32_t *blk, uint
   return tail_bit(tails, r, 3 * (idx - K) + s);
 }
 
-/* walker over the sub-block interleaver output w (lte_rate_matching.c:51-130) */
+static __device__ __forceinline__ uint32_t colperm(uint32_t col) { return __builtin_bitreverse32(col) >> 27; }
+
+/* ---- debug-only walker over w (reference layout dumps) ---- */
 struct wwalk_t {
   uint32_t p, region, col, row, which;
 };
@@ -302,41 +299,29 @@ static __device__ __forceinline__ void wwalk_init(wwalk_t &w, uint32_t p, uint32
   }
 }
 
-static __device__ __forceinline__ void wwalk_next(wwalk_t &w, uint32_t R)
-{
-  w.p++;
-  if (w.region == 0) {
-    if (++w.row == R) { w.row = 0; if (++w.col == 32) { w.region = 1; w.col = 0; } }
-  } else {
-    w.which ^= 1u;
-    if (w.which == 0 && ++w.row == R) { w.row = 0; if (++w.col == 32) { w.region = 0; w.col = 0; w.p = 0; } }
-  }
-}
-
 static __device__ __forceinline__ uint32_t wwalk_bit(const wwalk_t &w, const uint32_t *blk, uint32_t sw,
                                                      const uint32_t *tails, uint32_t r, uint32_t K, uint32_t ND,
                                                      uint32_t Kpi)
 {
-  uint32_t j = c_colperm[w.col] + 32 * w.row;
+  uint32_t j = colperm(w.col) + 32 * w.row;
   if (w.region == 0) return dstream_bit(blk, sw, tails, r, K, 0, j - ND);
   if (w.which == 0) return dstream_bit(blk, sw, tails, r, K, 1, j - ND);
   uint32_t j2 = (j + 1 == Kpi) ? 0 : j + 1;
   return dstream_bit(blk, sw, tails, r, K, 2, j2 - ND);
 }
 
-/* is w[p] a NULL (dummy) entry? (lte_rate_matching.c:51-130) */
 static __device__ __forceinline__ bool wwalk_null(const wwalk_t &w, uint32_t R, uint32_t ND)
 {
   if (w.row != 0) return (w.region == 1 && w.which == 1 && w.col == 31 && w.row == R - 1 && ND > 0);
-  uint32_t cp = c_colperm[w.col];
+  uint32_t cp = colperm(w.col);
   if (w.region == 0 || w.which == 0) return cp < ND;
   return (cp + 1 < ND) || (w.col == 31 && R == 1 && ND > 0);
 }
 
-/* position of the ci-th non-NULL entry of w (sorted NULL positions np[0..nn)) */
+/* position of the ci-th non-NULL entry of w (sorted NULL positions np[0..nn)); m = nulls before */
 static __device__ __forceinline__ uint32_t compact_to_pos(uint32_t ci, const uint16_t *np, uint32_t nn, uint32_t &m)
 {
-  uint32_t lo = 0, hi = nn; /* m = #{i : np[i] - i <= ci} */
+  uint32_t lo = 0, hi = nn;
   while (lo < hi) {
     uint32_t mid = (lo + hi) >> 1;
     if ((uint32_t)np[mid] - mid <= ci) lo = mid + 1;
@@ -346,43 +331,113 @@ static __device__ __forceinline__ uint32_t compact_to_pos(uint32_t ci, const uin
   return ci + lo;
 }
 
+/* 32 bits of a packed LSB-first LDS bit array starting at bit `pos` (may be negative: zeros) */
+static __device__ __forceinline__ uint32_t sx32(const uint32_t *a, int pos, bool swz)
+{
+  int wi = pos >> 5;
+  uint32_t off = (uint32_t)pos & 31u;
+  uint32_t lo = wi >= 0 ? a[swz ? lsw((uint32_t)wi) : (uint32_t)wi] : 0u;
+  if (!off) return lo;
+  uint32_t hi = wi + 1 >= 0 ? a[swz ? lsw((uint32_t)(wi + 1)) : (uint32_t)(wi + 1)] : 0u;
+  return (lo >> off) | (hi << (32 - off));
+}
+
+static __device__ __forceinline__ uint64_t spread32(uint32_t v)
+{
+  uint64_t x = v;
+  x = (x | (x << 16)) & 0x0000FFFF0000FFFFull;
+  x = (x | (x << 8)) & 0x00FF00FF00FF00FFull;
+  x = (x | (x << 4)) & 0x0F0F0F0F0F0F0F0Full;
+  x = (x | (x << 2)) & 0x3333333333333333ull;
+  x = (x | (x << 1)) & 0x5555555555555555ull;
+  return x;
+}
+
+/* OR a wave-uniform 128-bit value (nbits valid) into LDS bit array a at bit position pos.
+ * Lanes 0..4 each handle one destination word. */
+static __device__ __forceinline__ void or_bits128(uint32_t *a, uint32_t pos, uint32_t s0, uint32_t s1, uint32_t s2,
+                                                  uint32_t s3, uint32_t nbits)
+{
+  uint32_t lane = threadIdx.x & 63, off = pos & 31, nw = (off + nbits + 31) >> 5;
+  if (lane < nw) {
+    uint32_t cur = lane == 0 ? s0 : lane == 1 ? s1 : lane == 2 ? s2 : lane == 3 ? s3 : 0u;
+    uint32_t prv = lane == 0 ? 0u : lane == 1 ? s0 : lane == 2 ? s1 : lane == 3 ? s2 : s3;
+    uint32_t v = off ? (cur << off) | (prv >> (32 - off)) : cur;
+    if (v) atomicOr(&a[(pos >> 5) + lane], v);
+  }
+}
+
+/*
+ * Sub-block interleaver output w of block r as a packed bit array (NULL entries = 0)
+ * (lte_rate_matching.c:51-130).  y^(s) rows of 32 bits are bit-matrix-transposed with wave
+ * ballots: ballot((y_row >> b) & 1) is column b for 64 rows at once.
+ */
+static __device__ void build_w_bits(uint32_t *wb, const uint32_t *blk, uint32_t sw, uint32_t R, uint32_t Kpi,
+                                    uint32_t ND, uint32_t K, const uint32_t *tails, uint32_t r)
+{
+  const uint32_t tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, nwaves = blockDim.x >> 6;
+  const uint32_t nblk = (R + 63) >> 6;
+  for (uint32_t task = wave; task < 3 * nblk; task += nwaves) {
+    uint32_t s = task / nblk, bk = task - s * nblk;
+    uint32_t row = 64 * bk + lane;
+    uint32_t y = 0;
+    if (row < R) {
+      const uint32_t *st = blk + s * sw;
+      int pos = (int)(32 * row) - (int)ND + (s == 2 ? 1 : 0);
+      y = sx32(st, pos, true);
+      if (s == 2 && row == R - 1) {
+        /* j = Kpi-1 reads y^(2)_0: NULL if ND > 0, else d^(2)_0 */
+        y &= 0x7fffffffu;
+        if (ND == 0) y |= (st[lsw(0)] & 1u) << 31;
+      }
+    }
+    uint32_t nb = min(64u, R - 64 * bk);
+    for (uint32_t b = 0; b < 32; b++) {
+      uint64_t msk = __ballot((y >> b) & 1u);
+      uint32_t col = colperm(b);
+      if (s == 0) {
+        or_bits128(wb, col * R + 64 * bk, (uint32_t)msk, (uint32_t)(msk >> 32), 0, 0, nb);
+      } else {
+        uint64_t lo = spread32((uint32_t)msk) << (s - 1), hi = spread32((uint32_t)(msk >> 32)) << (s - 1);
+        or_bits128(wb, Kpi + col * 2 * R + 128 * bk, (uint32_t)lo, (uint32_t)(lo >> 32), (uint32_t)hi,
+                   (uint32_t)(hi >> 32), 2 * nb);
+      }
+    }
+  }
+  (void)K; (void)tails; (void)r;
+}
+
 /* ---------------------------------------------------------------------------------------
  * The fused encoder.
  * ------------------------------------------------------------------------------------- */
-struct enc_lds_t {
-  uint32_t *tb;     /* TB || CRC bytes */
-  uint32_t *strm;
-  uint32_t *gold;
-  uint32_t *tails;  /* 2 per block */
-  uint8_t *scan;    /* 2 * sum(K/32) bytes */
-  uint32_t *crctab; /* 256 */
-  uint32_t *red;    /* 8 */
-  uint16_t *np;     /* 2 * OAI4G_MAX_NULLS */
-};
-
 template <bool DEBUG>
 static __device__ void encode_codeword(const cfg_dev_t *__restrict__ c, uint32_t sf, uint32_t cwi,
                                        const uint8_t *__restrict__ payload, uint32_t *__restrict__ ebits,
                                        enc_debug_t dbg, uint32_t *lds_base)
 {
   const cw_dev_t &cw = c->cw[cwi];
-  const uint32_t tid = threadIdx.x, nth = blockDim.x;
+  const uint32_t tid = threadIdx.x, nth = blockDim.x, wave = tid >> 6, nwaves = nth >> 6;
   const uint32_t sfi = DEBUG ? sf : (c->first_sf + sf * c->sf_step) % 10;
-  const uint32_t C = cw.C;
-  const uint32_t sw = cw.stream_words;
-  enc_lds_t L;
-  L.tb = lds_base;
-  L.strm = L.tb + c->lds_tb_words;
-  L.gold = L.strm + c->lds_stream_words;
-  L.tails = L.gold + c->lds_gold_words;
-  L.crctab = L.tails + 2 * OAI4G_MAX_CB;
-  L.red = L.crctab + 256;
-  L.np = (uint16_t *)(L.red + 8);
-  L.scan = (uint8_t *)(L.np + 2 * OAI4G_MAX_NULLS);
-  uint8_t *tbb = (uint8_t *)L.tb;
+  const uint32_t C = cw.C, sw = cw.stream_words;
+  /* LDS carve-up */
+  uint32_t *tbw = lds_base;
+  uint32_t *strm = tbw + c->lds_tb_words;
+  uint32_t *ebuf = strm + c->lds_stream_words;
+  uint32_t *wb = ebuf + c->lds_gold_words;
+  uint32_t *inw2 = wb + c->lds_w_words;
+  uint32_t *crctab_a = inw2 + c->lds_inw_words;
+  uint32_t *crctab_b = crctab_a + 256;
+  uint32_t *tails = crctab_b + 256;
+  uint32_t *crcs = tails + 2 * OAI4G_MAX_CB;            /* [0] = CRC24A, [1+r] = CRC24B of block r */
+  blk_info_t *bi = (blk_info_t *)(crcs + OAI4G_MAX_CB + 2);
+  enc_tabs_t *tabs = (enc_tabs_t *)(bi + 1);
+  uint16_t *np = (uint16_t *)(tabs + 1);
+  uint8_t *scanA = (uint8_t *)(np + 2 * OAI4G_MAX_NULLS);
+  uint8_t *scanB = scanA + c->lds_items;
+  uint8_t *tbb = (uint8_t *)tbw;
   const uint32_t G = cw.G[sfi], Gw = (G + 31) >> 5;
 
-  /* ---- phase 0: TB bytes -> LDS, Gold words, NULL lists, CRC table ---- */
+  /* ---- phase 0: TB bytes, zeroed streams, tables, block info, Gold words ---- */
   const uint8_t *src = payload + (size_t)(DEBUG ? 0 : (sf * c->n_cw + cwi)) * c->payload_stride;
   const uint32_t Ab = cw.A_bytes;
   for (uint32_t i = tid; i < c->lds_tb_words; i += nth) {
@@ -392,43 +447,91 @@ static __device__ void encode_codeword(const cfg_dev_t *__restrict__ c, uint32_t
       uint32_t valid = Ab - 4 * i;
       if (valid < 4) v &= (1u << (8 * valid)) - 1u;
     }
-    L.tb[i] = v;
+    tbw[i] = v;
   }
-  const uint32_t c_init = (c->rnti << 14) + (cw.q << 13) + (sfi << 9) + c->Nid_cell; /* Ns>>1 = subframe */
-  gold_generate(L.gold, Gw, c_init, c->gold_x1, c->gold_x2j);
-  for (uint32_t i = tid; i < 2 * OAI4G_MAX_NULLS; i += nth) L.np[i] = cw.nullpos[i / OAI4G_MAX_NULLS][i % OAI4G_MAX_NULLS];
-  crc_table_init(L.crctab, 0x864cfbu);
+  for (uint32_t i = tid; i < c->lds_stream_words; i += nth) strm[i] = 0;
+  for (uint32_t i = tid; i < 2 * OAI4G_MAX_NULLS; i += nth) np[i] = cw.nullpos[i / OAI4G_MAX_NULLS][i % OAI4G_MAX_NULLS];
+  for (uint32_t v = tid; v < 256; v += nth) {
+    uint32_t ra = v << 16, rb = v << 16;
+    for (int i = 0; i < 8; i++) {
+      ra = (ra & 0x800000u) ? ((ra << 1) ^ 0x864cfbu) & 0xffffffu : (ra << 1) & 0xffffffu;
+      rb = (rb & 0x800000u) ? ((rb << 1) ^ 0x800063u) & 0xffffffu : (rb << 1) & 0xffffffu;
+    }
+    crctab_a[v] = ra;
+    crctab_b[v] = rb;
+  }
+  if (tid < 128) {
+    (&tabs->next[0][0])[tid] = (&c_rsc.next[0][0])[tid];
+    (&tabs->par[0][0])[tid] = (&c_rsc.par[0][0])[tid];
+    if (tid < 64) (&tabs->apow[0][0])[tid] = (&c_rsc.apow[0][0])[tid];
+  }
+  if (tid == 0) {
+    bi->C = C;
+    bi->sw = sw;
+    uint32_t it = 0, iw = 0;
+    for (uint32_t r = 0; r < C; r++) {
+      bi->K[r] = cw.K[r]; bi->f1[r] = cw.f1[r]; bi->f2[r] = cw.f2[r];
+      bi->ib[r] = it; bi->inwb[r] = iw;
+      uint32_t nch = (cw.K[r] + 31) >> 5;
+      it += 2 * nch; iw += nch;
+    }
+    bi->ib[C] = it;
+  }
+  if (DEBUG) {
+    for (uint32_t i = tid; i < Gw + 1; i += nth) ebuf[i] = 0;
+  } else {
+    const uint32_t c_init = (c->rnti << 14) + (cw.q << 13) + (sfi << 9) + c->Nid_cell; /* Ns>>1 = subframe */
+    gold_generate(ebuf, Gw, c_init, c->gold_x1, c->gold_x2j);
+    if (tid == 0) ebuf[Gw] = 0;
+  }
   __syncthreads();
 
-  /* ---- phase 1: CRC-24A (dlsch_coding.c:296-300) ---- */
-  uint32_t crc = crc24_block(tbb, Ab, 0x864cfbu, L.crctab, L.red);
+  /* ---- phase 1: CRC-24A over the TB (wave 0) and CRC-24B over every block's data bytes
+   *      excluding the TB CRC bytes (other waves); dlsch_coding.c:296-300, lte_segmentation.c:156-166 ---- */
+  const uint32_t ntask = 1 + (C > 1 ? C : 0);
+  for (uint32_t task = wave; task < ntask; task += nwaves) {
+    if (task == 0) {
+      uint32_t crc = crc24_wave(tbb, Ab, 0x864cfbu, crctab_a);
+      if ((tid & 63) == 0) crcs[0] = crc;
+    } else {
+      uint32_t r = task - 1, s0 = cw.src[r], n = cw.ncopy[r];
+      if (s0 + n > Ab) n = Ab > s0 ? Ab - s0 : 0;   /* TB CRC bytes are folded in below */
+      uint32_t crc = crc24_wave(tbb + s0, n, 0x800063u, crctab_b);
+      if ((tid & 63) == 0) crcs[1 + r] = crc;
+    }
+  }
+  __syncthreads();
   if (tid == 0) {
+    uint32_t crc = crcs[0];
     tbb[Ab] = (uint8_t)(crc >> 16);
     tbb[Ab + 1] = (uint8_t)(crc >> 8);
     tbb[Ab + 2] = (uint8_t)crc;
+    if (C > 1) {
+      /* extend the blocks whose span covers the TB CRC bytes */
+      for (uint32_t r = 0; r < C; r++) {
+        uint32_t s0 = cw.src[r], e0 = s0 + cw.ncopy[r];
+        uint32_t reg = crcs[1 + r];
+        for (uint32_t i = (s0 > Ab ? s0 : Ab); i < e0; i++) reg = crc_step(reg, tbb[i], crctab_b);
+        crcs[1 + r] = reg;
+      }
+    }
   }
   __syncthreads();
   if (DEBUG && dbg.b)
     for (uint32_t i = tid; i < Ab + 3; i += nth) dbg.b[i] = tbb[i];
 
-  /* ---- phase 2: segmentation -> per-block systematic streams (+ CRC-24B when C > 1) ---- */
-  crc_table_init(L.crctab, 0x800063u);
-  __syncthreads();
-  uint32_t crcb[OAI4G_MAX_CB];
-  for (uint32_t r = 0; r < C; r++) {
-    crcb[r] = 0;
-    if (C > 1) crcb[r] = crc24_block(tbb + cw.src[r], cw.ncopy[r], 0x800063u, L.crctab, L.red);
-  }
+  /* ---- phase 2: segmentation -> systematic streams (LSB-first words) ---- */
   for (uint32_t r = 0; r < C; r++) {
     uint32_t K = cw.K[r], nw = (K + 31) >> 5, fill = cw.fill[r], ncopy = cw.ncopy[r], s0 = cw.src[r];
-    uint32_t *sys = L.strm + r * 3 * sw;
+    uint32_t crcb = crcs[1 + r];
+    uint32_t *sys = strm + r * 3 * sw;
     for (uint32_t j = tid; j < nw; j += nth) {
       uint32_t le = 0;
       for (uint32_t q = 0; q < 4; q++) {
         uint32_t i = 4 * j + q, byte = 0;
         if (i < fill) byte = 0;
         else if (i < fill + ncopy) byte = tbb[s0 + i - fill];
-        else if (C > 1 && i < fill + ncopy + 3) byte = (crcb[r] >> (8 * (2 - (i - fill - ncopy)))) & 0xffu;
+        else if (C > 1 && i < fill + ncopy + 3) byte = (crcb >> (8 * (2 - (i - fill - ncopy)))) & 0xffu;
         le |= byte << (8 * q);
       }
       uint32_t wv = bytes_to_seq(le);
@@ -439,17 +542,13 @@ static __device__ void encode_codeword(const cfg_dev_t *__restrict__ c, uint32_t
   __syncthreads();
 
   /* ---- phase 3: turbo encoding of every block ---- */
-  cb_geom_t g;
-  g.C = C;
-  g.sw = sw;
-  for (uint32_t r = 0; r < C; r++) { g.K[r] = cw.K[r]; g.f1[r] = cw.f1[r]; g.f2[r] = cw.f2[r]; }
-  turbo_encode_blocks(L.strm, L.tails, L.scan, g);
+  turbo_encode_blocks(strm, bi, tails, inw2, scanA, scanB, tabs);
 
   if (DEBUG) {
-    /* reference-layout intermediates: c[r] bytes, d[r] (NULL prefix + 3K+12 (+side effect)), w[r] */
+    /* reference-layout intermediates: c[r] bytes, d[r] (NULL prefix + 3K+12 + side effect), w[r] */
     for (uint32_t r = 0; r < C; r++) {
       uint32_t K = cw.K[r], R = cw.R[r], Kpi = cw.Kpi[r], ND = cw.ND[r];
-      const uint32_t *blk = L.strm + r * 3 * sw;
+      const uint32_t *blk = strm + r * 3 * sw;
       if (dbg.c)
         for (uint32_t i = tid; i < K / 8; i += nth) {
           uint32_t wv = blk[lsw(i >> 2)];
@@ -461,63 +560,79 @@ static __device__ void encode_codeword(const cfg_dev_t *__restrict__ c, uint32_t
         for (uint32_t i = tid; i < 96; i += nth) d[i] = OAI4G_LTE_NULL;
         for (uint32_t i = tid; i < 3 * K + 12; i += nth) {
           uint32_t kk = i / 3, s = i - 3 * kk;
-          d[96 + i] = (uint8_t)(kk < K ? dstream_bit(blk, sw, L.tails, r, K, s, kk) : tail_bit(L.tails, r, i - 3 * K));
+          d[96 + i] = (uint8_t)(kk < K ? dstream_bit(blk, sw, tails, r, K, s, kk) : tail_bit(tails, r, i - 3 * K));
         }
-        /* d[3D+2] = d[2] (lte_rate_matching.c:75) */
-        if (tid == 0) d[96 + 3 * (K + 4) + 2] = (uint8_t)dstream_bit(blk, sw, L.tails, r, K, 2, 0);
+        if (tid == 0) d[96 + 3 * (K + 4) + 2] = (uint8_t)dstream_bit(blk, sw, tails, r, K, 2, 0);
       }
       if (dbg.w) {
         uint8_t *w = dbg.w + (size_t)r * OAI4G_W_BYTES;
         for (uint32_t p = tid; p < 3 * Kpi; p += nth) {
           wwalk_t wk;
           wwalk_init(wk, p, R, Kpi);
-          w[p] = wwalk_null(wk, R, ND) ? OAI4G_LTE_NULL : (uint8_t)wwalk_bit(wk, blk, sw, L.tails, r, K, ND, Kpi);
+          w[p] = wwalk_null(wk, R, ND) ? OAI4G_LTE_NULL : (uint8_t)wwalk_bit(wk, blk, sw, tails, r, K, ND, Kpi);
         }
       }
     }
+    if (!dbg.e) return;
   }
 
-  if (DEBUG && !dbg.e) return;
-  /* ---- phase 4: rate matching + scrambling -> packed e words ---- */
-  const uint32_t *roff = cw.roff[sfi];
-  uint32_t *eout = DEBUG ? nullptr : ebits + (size_t)(sf * c->n_cw + cwi) * c->ebits_words;
-  for (uint32_t wi = tid; wi < Gw; wi += nth) {
-    uint32_t k0 = 32 * wi;
-    uint32_t r = 0;
-    while (r + 1 < C && k0 >= roff[r + 1]) r++;
-    uint32_t out = 0;
-    uint32_t nb = min(32u, G - k0);
-    uint32_t b = 0;
-    while (b < nb && r < C) {
-      /* walk the run of bits belonging to block r */
-      uint32_t kl = k0 + b - roff[r];
-      uint32_t Er = roff[r + 1] - roff[r];
-      uint32_t run = min(nb - b, Er - kl);
-      uint32_t K = cw.K[r], R = cw.R[r], Kpi = cw.Kpi[r], ND = cw.ND[r], Nnn = cw.Nnn[r], Ncb = cw.Ncb[r];
-      const uint16_t *np = L.np + cw.kidx[r] * OAI4G_MAX_NULLS;
-      uint32_t nn = cw.nnull[cw.kidx[r]];
-      const uint32_t *blk = L.strm + r * 3 * sw;
-      uint32_t ci = (cw.k0c[r] + kl) % Nnn, m;
-      uint32_t p = compact_to_pos(ci, np, nn, m);
-      wwalk_t wk;
-      wwalk_init(wk, p, R, Kpi);
-      for (uint32_t x = 0; x < run; x++) {
-        if (x) {
-          /* advance to the next non-NULL position, wrapping at Ncb */
-          do {
-            wwalk_next(wk, R);
-            if (wk.p >= Ncb) wwalk_init(wk, 0, R, Kpi);
-          } while (wwalk_null(wk, R, ND));
-        }
-        uint32_t bit = wwalk_bit(wk, blk, sw, L.tails, r, K, ND, Kpi);
-        if (DEBUG && dbg.e) dbg.e[k0 + b + x] = (uint8_t)bit;
-        out |= bit << (b + x);
-      }
-      (void)m;
-      b += run;
-      r++;
+  /* append the 4 tail bits of each constituent stream at bit K (d^(s)_K..K+3) */
+  for (uint32_t r = tid; r < C; r += nth) {
+    uint32_t K = cw.K[r];
+    uint32_t *blk = strm + r * 3 * sw;
+    for (uint32_t s = 0; s < 3; s++) {
+      uint32_t t4 = tail_bit(tails, r, s) | (tail_bit(tails, r, 3 + s) << 1) | (tail_bit(tails, r, 6 + s) << 2) |
+                    (tail_bit(tails, r, 9 + s) << 3);
+      uint32_t w0 = K >> 5, off = K & 31;
+      blk[s * sw + lsw(w0)] |= t4 << off;
+      if (off > 28) blk[s * sw + lsw(w0 + 1)] |= t4 >> (32 - off);
     }
-    if (!DEBUG) eout[wi] = out ^ (L.gold[wi] & (nb == 32 ? 0xffffffffu : ((1u << nb) - 1u)));
+  }
+  __syncthreads();
+
+  /* ---- phase 4: per block: packed w, then word-level circular read + scramble ---- */
+  const uint32_t *roff = cw.roff[sfi];
+  for (uint32_t r = 0; r < C; r++) {
+    uint32_t K = cw.K[r], R = cw.R[r], Kpi = cw.Kpi[r], ND = cw.ND[r], Ncb = cw.Ncb[r], Nnn = cw.Nnn[r];
+    uint32_t nww = (3 * Kpi + 31) / 32 + 2;
+    for (uint32_t i = tid; i < nww; i += nth) wb[i] = 0;
+    __syncthreads();
+    build_w_bits(wb, strm + r * 3 * sw, sw, R, Kpi, ND, K, tails, r);
+    __syncthreads();
+    const uint16_t *npl = np + cw.kidx[r] * OAI4G_MAX_NULLS;
+    uint32_t nn = cw.nnull[cw.kidx[r]];
+    uint32_t E = roff[r + 1] - roff[r], base = roff[r], nwo = (E + 31) >> 5;
+    for (uint32_t i = tid; i < nwo; i += nth) {
+      uint32_t need = min(32u, E - 32 * i), got = 0, out = 0, m;
+      uint32_t p = compact_to_pos((cw.k0c[r] + 32 * i) % Nnn, npl, nn, m);
+      while (got < need) {
+        uint32_t nxt = m < nn ? (uint32_t)npl[m] : Ncb;
+        if (p == nxt) { p++; m++; continue; }          /* skip a NULL */
+        if (p >= Ncb) { p = 0; m = 0; continue; }      /* circular wrap (lte_rate_matching.c:559-566) */
+        uint32_t take = min(min(need - got, nxt - p), 32u);
+        uint32_t v = sx32(wb, (int)p, false);
+        if (take < 32) v &= (1u << take) - 1u;
+        out |= v << got;
+        got += take;
+        p += take;
+      }
+      uint32_t gpos = base + 32 * i, gw = gpos >> 5, off = gpos & 31;
+      atomicXor(&ebuf[gw], out << off);
+      if (off && (out >> (32 - off))) atomicXor(&ebuf[gw + 1], out >> (32 - off));
+    }
+    __syncthreads();
+  }
+
+  if (DEBUG) {
+    for (uint32_t k = tid; k < G; k += nth) dbg.e[k] = (uint8_t)((ebuf[k >> 5] >> (k & 31)) & 1u);
+    return;
+  }
+  uint32_t *eout = ebits + (size_t)(sf * c->n_cw + cwi) * c->ebits_words;
+  for (uint32_t i = tid; i < Gw; i += nth) {
+    uint32_t v = ebuf[i];
+    uint32_t nb = min(32u, G - 32 * i);
+    if (nb < 32) v &= (1u << nb) - 1u;
+    eout[i] = v;
   }
 }
 
@@ -539,15 +654,10 @@ __global__ void __launch_bounds__(256) k_encode_debug(const cfg_dev_t *__restric
 
 static size_t enc_lds_bytes(const cfg_dev_t *h)
 {
-  uint32_t scan_bytes = 0;
-  for (int cw = 0; cw < (int)h->n_cw; cw++) {
-    uint32_t s = 0;
-    for (uint32_t r = 0; r < h->cw[cw].C; r++) s += 2 * ((h->cw[cw].K[r] + 31) >> 5);
-    scan_bytes = s > scan_bytes ? s : scan_bytes;
-  }
-  size_t words = (size_t)h->lds_tb_words + h->lds_stream_words + h->lds_gold_words + 2 * OAI4G_MAX_CB + 256 + 8 +
-                 OAI4G_MAX_NULLS + (scan_bytes + 3) / 4 + 4;
-  return words * 4;
+  size_t words = (size_t)h->lds_tb_words + h->lds_stream_words + h->lds_gold_words + h->lds_w_words +
+                 h->lds_inw_words + 256 + 256 + 2 * OAI4G_MAX_CB + OAI4G_MAX_CB + 2;
+  size_t bytes = words * 4 + sizeof(blk_info_t) + sizeof(enc_tabs_t) + 2 * OAI4G_MAX_NULLS * 2 + 2 * h->lds_items;
+  return (bytes + 15) & ~(size_t)15;
 }
 
 hipError_t oai4g_launch_encode(const cfg_dev_t *d_cfg, const cfg_dev_t *h_cfg, int n_sf, const uint8_t *d_payload,
@@ -556,8 +666,8 @@ hipError_t oai4g_launch_encode(const cfg_dev_t *d_cfg, const cfg_dev_t *h_cfg, i
   size_t lds = enc_lds_bytes(h_cfg);
   static bool attr_set = false;
   if (!attr_set) {
-    hipFuncSetAttribute((const void *)k_encode, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-    hipFuncSetAttribute((const void *)k_encode_debug, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    (void)hipFuncSetAttribute((const void *)k_encode, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    (void)hipFuncSetAttribute((const void *)k_encode_debug, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     attr_set = true;
   }
   hipLaunchKernelGGL(k_encode, dim3(n_sf * h_cfg->n_cw), dim3(256), lds, s, d_cfg, d_payload, d_ebits);
@@ -568,7 +678,7 @@ hipError_t oai4g_launch_encode_debug(const cfg_dev_t *d_cfg, const cfg_dev_t *h_
                                      const uint8_t *d_payload, enc_debug_t dbg, hipStream_t s)
 {
   size_t lds = enc_lds_bytes(h_cfg);
-  hipFuncSetAttribute((const void *)k_encode_debug, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+  (void)hipFuncSetAttribute((const void *)k_encode_debug, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
   hipLaunchKernelGGL(k_encode_debug, dim3(1), dim3(256), lds, s, d_cfg, (uint32_t)sf, (uint32_t)cw, d_payload, dbg);
   return hipGetLastError();
 }
@@ -577,25 +687,23 @@ hipError_t oai4g_launch_encode_debug(const cfg_dev_t *d_cfg, const cfg_dev_t *h_
  * Drop-in byte-layout kernels
  * ===================================================================================== */
 
-/* crc24a/crc24b over an arbitrary bit length (crc_byte.c:117-153), one workgroup */
-__global__ void __launch_bounds__(256) k_crc24(const uint8_t *__restrict__ in, int bitlen, uint32_t poly,
-                                               uint32_t *__restrict__ out)
+/* crc24a/crc24b over an arbitrary bit length (crc_byte.c:117-153); wave 0 of one workgroup */
+__global__ void __launch_bounds__(64) k_crc24(const uint8_t *__restrict__ in, int bitlen, uint32_t poly,
+                                              uint32_t *__restrict__ out)
 {
   __shared__ uint32_t tab[256];
-  __shared__ uint32_t red[8];
   extern __shared__ uint8_t buf[];
   uint32_t nbytes = (uint32_t)bitlen / 8, rem = (uint32_t)bitlen % 8;
   for (uint32_t i = threadIdx.x; i < nbytes + (rem ? 1 : 0); i += blockDim.x) buf[i] = in[i];
   crc_table_init(tab, poly);
   __syncthreads();
-  uint32_t reg = crc24_block(buf, nbytes, poly, tab, red);
+  uint32_t reg = crc24_wave(buf, nbytes, poly, tab);
   if (threadIdx.x == 0) {
     if (rem) {
       /* crc = (crc << rem) ^ T[(byte >> (8-rem)) ^ (crc >> (32-rem))] on the <<8 register */
       uint32_t r32 = reg << 8;
       uint32_t idx = ((uint32_t)buf[nbytes] >> (8 - rem)) ^ (r32 >> (32 - rem));
-      r32 = (r32 << rem) ^ (tab[idx & 0xffu] << 8);
-      out[0] = r32;
+      out[0] = (r32 << rem) ^ (tab[idx & 0xffu] << 8);
     } else {
       out[0] = reg << 8;
     }
@@ -605,7 +713,7 @@ __global__ void __launch_bounds__(256) k_crc24(const uint8_t *__restrict__ in, i
 hipError_t oai4g_launch_crc24(const uint8_t *d_in, int bitlen, uint32_t poly_top, uint32_t *d_out, hipStream_t s)
 {
   uint32_t nbytes = (uint32_t)(bitlen + 7) / 8;
-  hipLaunchKernelGGL(k_crc24, dim3(1), dim3(256), nbytes + 4, s, d_in, bitlen, poly_top >> 8, d_out);
+  hipLaunchKernelGGL(k_crc24, dim3(1), dim3(64), nbytes + 4, s, d_in, bitlen, poly_top >> 8, d_out);
   return hipGetLastError();
 }
 
@@ -613,11 +721,25 @@ hipError_t oai4g_launch_crc24(const uint8_t *d_in, int bitlen, uint32_t poly_top
 __global__ void __launch_bounds__(256) k_turbo_bytes(const uint8_t *__restrict__ cin, uint32_t K, uint32_t f1,
                                                      uint32_t f2, uint8_t *__restrict__ dout)
 {
-  __shared__ uint32_t strm[3 * 200];
+  const uint32_t sw = 208;
+  __shared__ uint32_t strm[3 * sw];
   __shared__ uint32_t tails[2];
-  __shared__ uint8_t scan[2 * 192];
-  const uint32_t sw = 200;
+  __shared__ uint32_t inw2[192];
+  __shared__ uint8_t scanA[2 * 192], scanB[2 * 192];
+  __shared__ blk_info_t bi;
+  __shared__ enc_tabs_t tabs;
   uint32_t nw = (K + 31) >> 5;
+  for (uint32_t i = threadIdx.x; i < 3 * sw; i += blockDim.x) strm[i] = 0;
+  if (threadIdx.x < 128) {
+    (&tabs.next[0][0])[threadIdx.x] = (&c_rsc.next[0][0])[threadIdx.x];
+    (&tabs.par[0][0])[threadIdx.x] = (&c_rsc.par[0][0])[threadIdx.x];
+    if (threadIdx.x < 64) (&tabs.apow[0][0])[threadIdx.x] = (&c_rsc.apow[0][0])[threadIdx.x];
+  }
+  if (threadIdx.x == 0) {
+    bi.C = 1; bi.sw = sw; bi.K[0] = K; bi.f1[0] = f1; bi.f2[0] = f2;
+    bi.ib[0] = 0; bi.ib[1] = 2 * nw; bi.inwb[0] = 0;
+  }
+  __syncthreads();
   for (uint32_t j = threadIdx.x; j < nw; j += blockDim.x) {
     uint32_t le = 0;
     for (uint32_t q = 0; q < 4; q++) {
@@ -629,13 +751,7 @@ __global__ void __launch_bounds__(256) k_turbo_bytes(const uint8_t *__restrict__
     strm[lsw(j)] = wv;
   }
   __syncthreads();
-  cb_geom_t g;
-  g.C = 1;
-  g.sw = sw;
-  g.K[0] = K;
-  g.f1[0] = f1;
-  g.f2[0] = f2;
-  turbo_encode_blocks(strm, tails, scan, g);
+  turbo_encode_blocks(strm, &bi, tails, inw2, scanA, scanB, &tabs);
   for (uint32_t i = threadIdx.x; i < 3 * K + 12; i += blockDim.x) {
     uint32_t kk = i / 3, s = i - 3 * kk;
     dout[i] = (uint8_t)(kk < K ? dstream_bit(strm, sw, tails, 0, K, s, kk) : tail_bit(tails, 0, i - 3 * K));
@@ -657,7 +773,7 @@ __global__ void __launch_bounds__(256) k_subblock_bytes(uint32_t D, const uint8_
   const uint8_t *base = dfull + 96 - 3 * ND;
   for (uint32_t k = blockIdx.x * blockDim.x + threadIdx.x; k < Kpi; k += gridDim.x * blockDim.x) {
     uint32_t col = k / R, row = k - col * R;
-    uint32_t j = c_colperm[col] + 32 * row;
+    uint32_t j = colperm(col) + 32 * row;
     w[k] = base[3 * j];
     w[Kpi + 2 * k] = base[3 * j + 1];
     /* base[3j+5] with the d[3D+2] = d[2] alias (lte_rate_matching.c:75) */

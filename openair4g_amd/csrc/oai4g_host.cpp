@@ -470,7 +470,7 @@ static int derive_cfg(oai4g_tx_config *cfg, const oai4g_tx_params_t *p, const ui
   h.first_sf = p->first_subframe % 10;
   h.sf_step = p->subframe_step;
   h.payload_stride = p->payload_stride;
-  uint32_t max_tb_words = 0, max_stream_words = 0, max_gw = 0, max_bits = 0;
+  uint32_t max_tb_words = 0, max_stream_words = 0, max_gw = 0, max_bits = 0, max_w = 0, max_inw = 0;
   bool rm_fail = false;
   for (int cw = 0; cw < p->n_cw; cw++) {
     cw_dev_t &c = h.cw[cw];
@@ -533,7 +533,13 @@ static int derive_cfg(oai4g_tx_config *cfg, const oai4g_tx_params_t *p, const ui
       c.Nnn[r] = Ncb - nn;
     }
     uint32_t nw = (maxK + 31) >> 5;
-    c.stream_words = nw + (nw >> 5) + 1;
+    c.stream_words = (nw + 2) + ((nw + 2) >> 5) + 1;   /* + tail word + read-ahead word */
+    uint32_t inw = 0;
+    for (uint32_t r = 0; r < C; r++) inw += (c.K[r] + 31) >> 5;
+    max_inw = inw > max_inw ? inw : max_inw;
+    uint32_t wwords = 0;
+    for (uint32_t r = 0; r < C; r++) { uint32_t ww = (3 * c.Kpi[r] + 31) / 32 + 2; wwords = ww > wwords ? ww : wwords; }
+    max_w = wwords > max_w ? wwords : max_w;
     uint32_t tbw = (c.A_bytes + 3 + 3) / 4 + 1;
     max_tb_words = tbw > max_tb_words ? tbw : max_tb_words;
     uint32_t strw = C * 3 * c.stream_words;
@@ -559,7 +565,10 @@ static int derive_cfg(oai4g_tx_config *cfg, const oai4g_tx_params_t *p, const ui
   if (max_gw > OAI4G_MAX_GOLD_WORDS) { set_err("G too large"); return -1; }
   h.lds_tb_words = max_tb_words;
   h.lds_stream_words = max_stream_words;
-  h.lds_gold_words = max_gw;
+  h.lds_gold_words = max_gw + 1;
+  h.lds_w_words = max_w;
+  h.lds_inw_words = max_inw;
+  h.lds_items = 2 * max_inw;
   /* RE maps */
   if (need_remap) {
     uint32_t N = h.N;

@@ -70,8 +70,11 @@ struct cfg_dev_t {
   uint32_t ebits_words;         /* per codeword per subframe */
   uint32_t lds_tb_words;        /* LDS words for TB || CRC */
   uint32_t lds_stream_words;    /* LDS words for all block streams of one codeword */
-  uint32_t lds_gold_words;
-  uint32_t pad;
+  uint32_t lds_gold_words;      /* = e-bit staging words (Gold-prefilled) */
+  uint32_t lds_w_words;         /* packed sub-block interleaver output of one block */
+  uint32_t lds_inw_words;       /* interleaved-input words of all blocks */
+  uint32_t lds_items;           /* encoder chunk items (2 per 32-bit chunk per block) */
+  uint32_t pad[2];
   cw_dev_t cw[2];
   uint32_t symbase[10][14];     /* data REs before symbol l */
   const uint16_t *remap;        /* [10][14][N] data-RE index | parity<<15, 0xFFFF = none */

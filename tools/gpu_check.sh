@@ -12,6 +12,7 @@ step() {  # name, seconds, command...
   if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "STOP after $name (rc=$rc)"; exit $rc; fi
   return 0
 }
-step pytest_gpu 900 python -m pytest tests -m gpu -q -rf --timeout 300 ${PYTEST_ARGS}
+if [ -n "$PYTEST_K" ]; then KARG=(-k "$PYTEST_K"); else KARG=(); fi
+step pytest_gpu 900 python -m pytest tests -m gpu -q -rf --timeout 300 "${KARG[@]}"
 step smoke 300 python -c "import __graft_entry__ as g; g.smoke()"
 step bench 600 python bench.py --steps ${BENCH_STEPS:-10} --warmup 2 --cpu-seconds ${CPU_SECONDS:-8}
