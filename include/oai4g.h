@@ -213,6 +213,11 @@ int oai4g_tx_batch_timed(const oai4g_tx_config_t *cfg, int n_sf, const uint8_t *
 /* Stage entry for parity tests: run only the encoder kernel (payload -> packed e bits). */
 int oai4g_tx_encode(const oai4g_tx_config_t *cfg, int n_sf, const uint8_t *d_payload, void *d_work, void *stream);
 
+/* Diagnostics: average ms of the encoder kernel stopped after phase `stop_phase`
+ * (0 load+Gold, 1 CRC, 2 segmentation, 3 turbo, 4 w build, 99 = complete).  Outputs invalid. */
+int oai4g_diag_encode_phase_ms(const oai4g_tx_config_t *cfg, int n_sf, const uint8_t *d_payload, void *d_work,
+                               int stop_phase, int reps, float *ms);
+
 /* ---------------- device memory helpers (for hosts without another allocator) ---------------- */
 void *oai4g_dev_alloc(size_t bytes);
 void oai4g_dev_free(void *p);

@@ -138,6 +138,8 @@ _SIGS = {
                                             ctypes.c_void_p, ctypes.c_void_p, ctypes.POINTER(ctypes.c_float)]),
     "oai4g_tx_encode": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p,
                                        ctypes.c_void_p]),
+    "oai4g_diag_encode_phase_ms": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p,
+                                                  ctypes.c_int, ctypes.c_int, ctypes.POINTER(ctypes.c_float)]),
     "oai4g_dev_alloc": (ctypes.c_void_p, [ctypes.c_size_t]),
     "oai4g_dev_free": (None, [ctypes.c_void_p]),
     "oai4g_memcpy_h2d": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t]),
@@ -443,6 +445,12 @@ class TxPipeline:
 
     def encode_only(self, stream=None):
         _check(self.L.oai4g_tx_encode(self.cfg, self.n_sf, self.d_payload, self.d_work, stream) == 0)
+
+    def diag_encode_phase_ms(self, stop_phase, reps=5):
+        ms = ctypes.c_float()
+        _check(self.L.oai4g_diag_encode_phase_ms(self.cfg, self.n_sf, self.d_payload, self.d_work, stop_phase, reps,
+                                                 ctypes.byref(ms)) == 0)
+        return ms.value
 
     def sync(self):
         _check(self.L.oai4g_sync() == 0)

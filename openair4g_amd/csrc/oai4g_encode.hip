@@ -413,7 +413,7 @@ static __device__ void build_w_bits(uint32_t *wb, const uint32_t *blk, uint32_t 
 template <bool DEBUG>
 static __device__ void encode_codeword(const cfg_dev_t *__restrict__ c, uint32_t sf, uint32_t cwi,
                                        const uint8_t *__restrict__ payload, uint32_t *__restrict__ ebits,
-                                       enc_debug_t dbg, uint32_t *lds_base)
+                                       enc_debug_t dbg, uint32_t *lds_base, int stop_phase = 99)
 {
   const cw_dev_t &cw = c->cw[cwi];
   const uint32_t tid = threadIdx.x, nth = blockDim.x, wave = tid >> 6, nwaves = nth >> 6;
@@ -485,6 +485,7 @@ static __device__ void encode_codeword(const cfg_dev_t *__restrict__ c, uint32_t
     if (tid == 0) ebuf[Gw] = 0;
   }
   __syncthreads();
+  if (stop_phase <= 0) return;
 
   /* ---- phase 1: CRC-24A over the TB (wave 0) and CRC-24B over every block's data bytes
    *      excluding the TB CRC bytes (other waves); dlsch_coding.c:296-300, lte_segmentation.c:156-166 ---- */
@@ -519,6 +520,7 @@ static __device__ void encode_codeword(const cfg_dev_t *__restrict__ c, uint32_t
   __syncthreads();
   if (DEBUG && dbg.b)
     for (uint32_t i = tid; i < Ab + 3; i += nth) dbg.b[i] = tbb[i];
+  if (stop_phase <= 1) return;
 
   /* ---- phase 2: segmentation -> systematic streams (LSB-first words) ---- */
   for (uint32_t r = 0; r < C; r++) {
@@ -541,8 +543,10 @@ static __device__ void encode_codeword(const cfg_dev_t *__restrict__ c, uint32_t
   }
   __syncthreads();
 
+  if (stop_phase <= 2) return;
   /* ---- phase 3: turbo encoding of every block ---- */
   turbo_encode_blocks(strm, bi, tails, inw2, scanA, scanB, tabs);
+  if (stop_phase <= 3) return;
 
   if (DEBUG) {
     /* reference-layout intermediates: c[r] bytes, d[r] (NULL prefix + 3K+12 + side effect), w[r] */
@@ -599,6 +603,7 @@ static __device__ void encode_codeword(const cfg_dev_t *__restrict__ c, uint32_t
     __syncthreads();
     build_w_bits(wb, strm + r * 3 * sw, sw, R, Kpi, ND, K, tails, r);
     __syncthreads();
+    if (stop_phase <= 4) continue;
     const uint16_t *npl = np + cw.kidx[r] * OAI4G_MAX_NULLS;
     uint32_t nn = cw.nnull[cw.kidx[r]];
     uint32_t E = roff[r + 1] - roff[r], base = roff[r], nwo = (E + 31) >> 5;
@@ -637,12 +642,12 @@ static __device__ void encode_codeword(const cfg_dev_t *__restrict__ c, uint32_t
 }
 
 __global__ void __launch_bounds__(256) k_encode(const cfg_dev_t *__restrict__ c, const uint8_t *__restrict__ payload,
-                                                uint32_t *__restrict__ ebits)
+                                                uint32_t *__restrict__ ebits, int stop_phase)
 {
   extern __shared__ uint32_t lds_dyn[];
   uint32_t sf = blockIdx.x / c->n_cw, cwi = blockIdx.x % c->n_cw;
   enc_debug_t none = {nullptr, nullptr, nullptr, nullptr, nullptr};
-  encode_codeword<false>(c, sf, cwi, payload, ebits, none, lds_dyn);
+  encode_codeword<false>(c, sf, cwi, payload, ebits, none, lds_dyn, stop_phase);
 }
 
 __global__ void __launch_bounds__(256) k_encode_debug(const cfg_dev_t *__restrict__ c, uint32_t sf, uint32_t cwi,
@@ -660,8 +665,16 @@ static size_t enc_lds_bytes(const cfg_dev_t *h)
   return (bytes + 15) & ~(size_t)15;
 }
 
+hipError_t oai4g_launch_encode_phase(const cfg_dev_t *d_cfg, const cfg_dev_t *h_cfg, int n_sf,
+                                     const uint8_t *d_payload, uint32_t *d_ebits, int stop_phase, hipStream_t s);
 hipError_t oai4g_launch_encode(const cfg_dev_t *d_cfg, const cfg_dev_t *h_cfg, int n_sf, const uint8_t *d_payload,
                                uint32_t *d_ebits, hipStream_t s)
+{
+  return oai4g_launch_encode_phase(d_cfg, h_cfg, n_sf, d_payload, d_ebits, 99, s);
+}
+
+hipError_t oai4g_launch_encode_phase(const cfg_dev_t *d_cfg, const cfg_dev_t *h_cfg, int n_sf,
+                                     const uint8_t *d_payload, uint32_t *d_ebits, int stop_phase, hipStream_t s)
 {
   size_t lds = enc_lds_bytes(h_cfg);
   static bool attr_set = false;
@@ -670,7 +683,7 @@ hipError_t oai4g_launch_encode(const cfg_dev_t *d_cfg, const cfg_dev_t *h_cfg, i
     (void)hipFuncSetAttribute((const void *)k_encode_debug, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     attr_set = true;
   }
-  hipLaunchKernelGGL(k_encode, dim3(n_sf * h_cfg->n_cw), dim3(256), lds, s, d_cfg, d_payload, d_ebits);
+  hipLaunchKernelGGL(k_encode, dim3(n_sf * h_cfg->n_cw), dim3(256), lds, s, d_cfg, d_payload, d_ebits, stop_phase);
   return hipGetLastError();
 }
 

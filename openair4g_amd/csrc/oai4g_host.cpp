@@ -686,6 +686,28 @@ extern "C" int oai4g_tx_batch_timed(const oai4g_tx_config_t *cfg, int n_sf, cons
   return 0;
 }
 
+/* Diagnostics: time the encoder with an early exit after phase `stop_phase`
+ * (0 load/Gold, 1 CRC, 2 segmentation, 3 turbo, 4 w build, 99 full). Outputs are invalid. */
+extern "C" int oai4g_diag_encode_phase_ms(const oai4g_tx_config_t *cfg, int n_sf, const uint8_t *d_payload,
+                                          void *d_work, int stop_phase, int reps, float *ms)
+{
+  NEED_INIT(-1);
+  hipEvent_t a, b;
+  HCK(hipEventCreate(&a), -1);
+  HCK(hipEventCreate(&b), -1);
+  HCK(oai4g_launch_encode_phase(cfg->d, &cfg->h, n_sf, d_payload, (uint32_t *)d_work, stop_phase, nullptr), -1);
+  HCK(hipEventRecord(a, nullptr), -1);
+  for (int i = 0; i < reps; i++)
+    HCK(oai4g_launch_encode_phase(cfg->d, &cfg->h, n_sf, d_payload, (uint32_t *)d_work, stop_phase, nullptr), -1);
+  HCK(hipEventRecord(b, nullptr), -1);
+  HCK(hipEventSynchronize(b), -1);
+  HCK(hipEventElapsedTime(ms, a, b), -1);
+  *ms /= reps;
+  hipEventDestroy(a);
+  hipEventDestroy(b);
+  return 0;
+}
+
 /* ------------------------------------------------------------------------------------------
  * device memory helpers
  * ---------------------------------------------------------------------------------------- */

@@ -87,6 +87,8 @@ struct cfg_dev_t {
 /* encoder path */
 hipError_t oai4g_launch_encode(const cfg_dev_t *d_cfg, const cfg_dev_t *h_cfg, int n_sf,
                                const uint8_t *d_payload, uint32_t *d_ebits, hipStream_t s);
+hipError_t oai4g_launch_encode_phase(const cfg_dev_t *d_cfg, const cfg_dev_t *h_cfg, int n_sf,
+                                     const uint8_t *d_payload, uint32_t *d_ebits, int stop_phase, hipStream_t s);
 struct enc_debug_t {
   uint8_t *c;      /* [C][8+3+768]                         */
   uint8_t *d;      /* [C][OAI4G_D_BYTES] (offset 96 = d[r][96]) */
