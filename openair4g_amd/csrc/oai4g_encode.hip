@@ -68,20 +68,7 @@ static __device__ __forceinline__ uint32_t lsw(uint32_t w) { return w + (w >> 5)
 /* 4 MSB-first bytes (little-endian word) -> 32 bits LSB-first in sequence order */
 static __device__ __forceinline__ uint32_t bytes_to_seq(uint32_t le) { return __builtin_bswap32(__builtin_bitreverse32(le)); }
 
-/* ---------------------------------------------------------------------------------------
- * CRC-24 helpers: 24-bit register, MSB-first, zero init (reference returns reg << 8).
- * ------------------------------------------------------------------------------------- */
-static __device__ __forceinline__ uint32_t crc_mulmod(uint32_t a, uint32_t b, uint32_t poly)
-{
-  uint32_t r = 0;
-  for (int i = 23; i >= 0; i--) {
-    r <<= 1;
-    if (r & 0x1000000u) r ^= 0x1000000u | poly;
-    if ((b >> i) & 1u) r ^= a;
-  }
-  return r;
-}
-
+/* CRC byte table: tab[v] = v * x^24 mod P (24-bit register form of crc_byte.c:98-105) */
 static __device__ void crc_table_init(uint32_t *tab, uint32_t poly)
 {
   for (uint32_t v = threadIdx.x; v < 256; v += blockDim.x) {
@@ -123,14 +110,57 @@ static __device__ void gold_generate(uint32_t *gold, uint32_t nwords, uint32_t c
 }
 
 /* ---------------------------------------------------------------------------------------
- * Wave-cooperative CRC-24 (crc_byte.c:98-153 restated for 64 lanes).  The message is
- * virtually front-padded with zero bytes (which leave a zero-initialised CRC register
- * unchanged) to 64*per bytes; lane l hashes chunk l with the byte table, then a 6-level
- * shuffle tree combines neighbours: crc(L||R) = crc(L)*x^(8|R|) ^ crc(R) mod P.
+ * CRC-24 (crc_byte.c:98-153 restated for wavefronts).  The message is virtually
+ * front-padded with zero bytes (which leave a zero-initialised register unchanged) so that
+ * every lane hashes exactly `per` bytes; lanes are then combined pairwise up a tree:
+ * crc(L||R) = crc(L) * x^(8|R|) ^ crc(R) mod P.  The constant multipliers of every tree
+ * level come from the host as nibble tables, so a combine is 6 independent LDS lookups.
  * ------------------------------------------------------------------------------------- */
 static __device__ __forceinline__ uint32_t crc_step(uint32_t reg, uint32_t byte, const uint32_t *tab)
 {
   return ((reg << 8) & 0xffffffu) ^ tab[((reg >> 16) ^ byte) & 0xffu];
+}
+
+static __device__ __forceinline__ uint32_t crc_mul_tab(uint32_t a, const uint32_t *t /* [6][16] */)
+{
+  return t[a & 15u] ^ t[16 + ((a >> 4) & 15u)] ^ t[32 + ((a >> 8) & 15u)] ^ t[48 + ((a >> 12) & 15u)] ^
+         t[64 + ((a >> 16) & 15u)] ^ t[80 + ((a >> 20) & 15u)];
+}
+
+/* lane chunk CRC of virtual bytes [lane*per, (lane+1)*per) of a message padded to nl*per */
+static __device__ __forceinline__ uint32_t crc_chunk(const uint8_t *buf, uint32_t nbytes, uint32_t per, uint32_t lane,
+                                                     uint32_t nl, const uint32_t *tab)
+{
+  int vstart = (int)(lane * per) - (int)(per * nl - nbytes);
+  uint32_t reg = 0;
+  for (uint32_t i = 0; i < per; i++) {
+    int idx = vstart + (int)i;
+    if (idx >= 0) reg = crc_step(reg, buf[idx], tab);
+  }
+  return reg;
+}
+
+/* 6-level in-wave tree; mul = [6][6][16] tables; result valid in lane 0 */
+static __device__ __forceinline__ uint32_t crc_wave_tree(uint32_t reg, const uint32_t *mul)
+{
+  const uint32_t lane = threadIdx.x & 63;
+  for (int d = 0; d < 6; d++) {
+    uint32_t other = __shfl_down(reg, 1u << d, 64);
+    if ((lane & ((2u << d) - 1u)) == 0) reg = crc_mul_tab(reg, mul + d * 96) ^ other;
+  }
+  return reg;
+}
+
+/* generic one-wave CRC (drop-in path): multipliers computed on the fly */
+static __device__ __forceinline__ uint32_t crc_mulmod(uint32_t a, uint32_t b, uint32_t poly)
+{
+  uint32_t r = 0;
+  for (int i = 23; i >= 0; i--) {
+    r <<= 1;
+    if (r & 0x1000000u) r ^= 0x1000000u | poly;
+    if ((b >> i) & 1u) r ^= a;
+  }
+  return r;
 }
 
 static __device__ uint32_t crc24_wave(const uint8_t *buf, uint32_t nbytes, uint32_t poly, const uint32_t *tab)
@@ -138,12 +168,7 @@ static __device__ uint32_t crc24_wave(const uint8_t *buf, uint32_t nbytes, uint3
   const uint32_t lane = threadIdx.x & 63;
   uint32_t per = (nbytes + 63) >> 6;
   if (per == 0) return 0;
-  int vstart = (int)(lane * per) - (int)(per * 64 - nbytes);
-  uint32_t reg = 0;
-  for (uint32_t i = 0; i < per; i++) {
-    int idx = vstart + (int)i;
-    if (idx >= 0) reg = crc_step(reg, buf[idx], tab);
-  }
+  uint32_t reg = crc_chunk(buf, nbytes, per, lane, 64, tab);
   uint32_t m = 1;
   for (uint32_t i = 0; i < per; i++) m = crc_step(m, 0, tab);   /* x^(8 per) mod P */
   for (int d = 0; d < 6; d++) {
@@ -155,28 +180,16 @@ static __device__ uint32_t crc24_wave(const uint8_t *buf, uint32_t nbytes, uint3
 }
 
 /* ---------------------------------------------------------------------------------------
- * Turbo encoding of all code blocks of a codeword held in LDS (see file header).
- * Items: (block r, encoder e, 32-bit chunk j), flattened; ib[r] = first item of block r.
+ * Turbo encoding.  One wavefront per (block, constituent encoder) segment; lane l owns
+ * qp consecutive 32-bit chunks (qp = 1, 2 or 4).  Zero-start chunk exit states are composed
+ * lane-locally, scanned across lanes with shuffles (x -> A^(32 qp 2^d) x), and each chunk
+ * is then re-encoded from its true entry state.  No barriers, no LDS scan buffers.
  * ------------------------------------------------------------------------------------- */
 struct enc_tabs_t {            /* LDS copy of the RSC tables (lane-varying indices) */
   uint8_t next[8][16];
   uint8_t par[8][16];
   uint8_t apow[8][8];
 };
-
-struct blk_info_t {            /* per-codeword block table in LDS */
-  uint32_t C, sw;
-  uint32_t K[OAI4G_MAX_CB], f1[OAI4G_MAX_CB], f2[OAI4G_MAX_CB];
-  uint32_t ib[OAI4G_MAX_CB + 1];   /* item base per block */
-  uint32_t inwb[OAI4G_MAX_CB];     /* interleaved-word base per block */
-};
-
-static __device__ __forceinline__ uint32_t find_block(const blk_info_t *bi, uint32_t it)
-{
-  uint32_t r = 0;
-  while (r + 1 < bi->C && it >= bi->ib[r + 1]) r++;
-  return r;
-}
 
 /* interleaved input word of chunk j: bits c'_k = c_Pi(k), Pi(k) = (f1 k + f2 k^2) mod K */
 static __device__ __forceinline__ uint32_t qpp_word(const uint32_t *sys, uint32_t K, uint32_t f1, uint32_t f2,
@@ -197,72 +210,59 @@ static __device__ __forceinline__ uint32_t qpp_word(const uint32_t *sys, uint32_
   return word;
 }
 
-static __device__ void turbo_encode_blocks(uint32_t *strm, const blk_info_t *bi, uint32_t *tails, uint32_t *inw2,
-                                           uint8_t *scanA, uint8_t *scanB, const enc_tabs_t *tb)
+/* encode one segment (block r, encoder e) with the calling wavefront */
+static __device__ void turbo_segment(uint32_t *blk, uint32_t sw, uint32_t K, uint32_t f1, uint32_t f2, uint32_t e,
+                                     uint32_t *tail_out, const enc_tabs_t *tb)
 {
-  const uint32_t tid = threadIdx.x, nth = blockDim.x;
-  const uint32_t nitems = bi->ib[bi->C], sw = bi->sw;
-  /* pass 1: chunk input words and zero-start exit states */
-  for (uint32_t it = tid; it < nitems; it += nth) {
-    uint32_t r = find_block(bi, it);
-    uint32_t K = bi->K[r], nch = (K + 31) >> 5, loc = it - bi->ib[r];
-    uint32_t e = loc >= nch, j = e ? loc - nch : loc;
-    const uint32_t *sys = strm + r * 3 * sw;
-    uint32_t u;
-    if (e) {
-      u = qpp_word(sys, K, bi->f1[r], bi->f2[r], j);
-      inw2[bi->inwb[r] + j] = u;
-    } else {
-      u = sys[lsw(j)];
+  const uint32_t lane = threadIdx.x & 63;
+  const uint32_t nch = (K + 31) >> 5;
+  const uint32_t lq = nch <= 64 ? 0 : (nch <= 128 ? 1 : 2), qp = 1u << lq;
+  uint32_t u[4], s0[4];
+  uint32_t S = 0;
+#pragma unroll
+  for (int t = 0; t < 4; t++) {
+    u[t] = 0;
+    s0[t] = 0;
+    uint32_t j = lane * qp + t;
+    if (t < (int)qp && j < nch) {
+      u[t] = e ? qpp_word(blk, K, f1, f2, j) : blk[lsw(j)];
+      uint32_t nnib = min(32u, K - 32 * j) >> 2, s = 0;
+      for (uint32_t q = 0; q < nnib; q++) s = tb->next[s][(u[t] >> (4 * q)) & 15u];
+      s0[t] = s;
     }
-    uint32_t nnib = min(32u, K - 32 * j) >> 2;
-    uint32_t s = 0;
-    for (uint32_t q = 0; q < nnib; q++) s = tb->next[s][(u >> (4 * q)) & 15u];
-    scanA[it] = (uint8_t)s;
+    if (t < (int)qp) S = tb->apow[0][S] ^ s0[t];
   }
-  __syncthreads();
-  /* pass 2: segmented Hillis-Steele scan, state_after(j) = A^32 state_after(j-1) ^ s0(j) */
-  uint8_t *src = scanA, *dst = scanB;
-  for (int d = 0; d < 8; d++) {
-    uint32_t span = 1u << d;
-    for (uint32_t it = tid; it < nitems; it += nth) {
-      uint32_t r = find_block(bi, it);
-      uint32_t nch = (bi->K[r] + 31) >> 5, loc = it - bi->ib[r];
-      uint32_t j = loc >= nch ? loc - nch : loc;
-      uint32_t v = src[it];
-      if (j >= span) v ^= tb->apow[d][src[it - span]];
-      dst[it] = (uint8_t)v;
-    }
-    __syncthreads();
-    uint8_t *t = src; src = dst; dst = t;
+  /* inclusive scan over lanes: S_l ^= A^(32 qp 2^d) S_(l - 2^d) */
+#pragma unroll
+  for (int d = 0; d < 6; d++) {
+    uint32_t other = __shfl_up(S, 1u << d, 64);
+    if (lane >= (1u << d)) S ^= tb->apow[lq + d][other];
   }
-  /* pass 3: re-encode from the true entry state -> parity words; tails */
-  for (uint32_t it = tid; it < nitems; it += nth) {
-    uint32_t r = find_block(bi, it);
-    uint32_t K = bi->K[r], nch = (K + 31) >> 5, loc = it - bi->ib[r];
-    uint32_t e = loc >= nch, j = e ? loc - nch : loc;
-    uint32_t *sys = strm + r * 3 * sw;
-    uint32_t u = e ? inw2[bi->inwb[r] + j] : sys[lsw(j)];
-    uint32_t s = j ? src[it - 1] : 0;
-    uint32_t nnib = min(32u, K - 32 * j) >> 2, par = 0;
-    for (uint32_t q = 0; q < nnib; q++) {
-      uint32_t nib = (u >> (4 * q)) & 15u;
-      par |= (uint32_t)tb->par[s][nib] << (4 * q);
-      s = tb->next[s][nib];
-    }
-    sys[(1 + e) * sw + lsw(j)] = par;
-    if (j == nch - 1) {
-      /* trellis termination (3gpplte_sse.c:104-109, 440-471): (x, z) per step */
-      uint32_t tbits = 0;
-      for (int stp = 0; stp < 3; stp++) {
-        uint32_t z = ((s >> 2) ^ s) & 1u, x = (s ^ (s >> 1)) & 1u;
-        s >>= 1;
-        tbits |= (x << (2 * stp)) | (z << (2 * stp + 1));
+  uint32_t s = __shfl_up(S, 1, 64);
+  if (lane == 0) s = 0;
+#pragma unroll
+  for (int t = 0; t < 4; t++) {
+    uint32_t j = lane * qp + t;
+    if (t < (int)qp && j < nch) {
+      uint32_t nnib = min(32u, K - 32 * j) >> 2, par = 0;
+      for (uint32_t q = 0; q < nnib; q++) {
+        uint32_t nib = (u[t] >> (4 * q)) & 15u;
+        par |= (uint32_t)tb->par[s][nib] << (4 * q);
+        s = tb->next[s][nib];
       }
-      tails[2 * r + e] = tbits;
+      blk[(1 + e) * sw + lsw(j)] = par;
+      if (j == nch - 1) {
+        /* trellis termination (3gpplte_sse.c:104-109, 440-471): (x, z) per step */
+        uint32_t tbits = 0;
+        for (int stp = 0; stp < 3; stp++) {
+          uint32_t z = ((s >> 2) ^ s) & 1u, x = (s ^ (s >> 1)) & 1u;
+          s >>= 1;
+          tbits |= (x << (2 * stp)) | (z << (2 * stp + 1));
+        }
+        *tail_out = tbits;
+      }
     }
   }
-  __syncthreads();
 }
 
 /* tail bit m (0..11) of block r: t[0..5] from encoder 1, t[6..11] from encoder 2 */
@@ -318,8 +318,8 @@ static __device__ __forceinline__ bool wwalk_null(const wwalk_t &w, uint32_t R, 
   return (cp + 1 < ND) || (w.col == 31 && R == 1 && ND > 0);
 }
 
-/* position of the ci-th non-NULL entry of w (sorted NULL positions np[0..nn)); m = nulls before */
-static __device__ __forceinline__ uint32_t compact_to_pos(uint32_t ci, const uint16_t *np, uint32_t nn, uint32_t &m)
+/* position of the ci-th non-NULL entry of w (sorted NULL positions np[0..nn)) */
+static __device__ __forceinline__ uint32_t compact_to_pos(uint32_t ci, const uint16_t *np, uint32_t nn)
 {
   uint32_t lo = 0, hi = nn;
   while (lo < hi) {
@@ -327,84 +327,68 @@ static __device__ __forceinline__ uint32_t compact_to_pos(uint32_t ci, const uin
     if ((uint32_t)np[mid] - mid <= ci) lo = mid + 1;
     else hi = mid;
   }
-  m = lo;
   return ci + lo;
 }
 
-/* 32 bits of a packed LSB-first LDS bit array starting at bit `pos` (may be negative: zeros) */
-static __device__ __forceinline__ uint32_t sx32(const uint32_t *a, int pos, bool swz)
+/* 32 bits of a packed LSB-first LDS bit array (swizzled words) starting at bit `pos` (pos may be
+ * negative: zeros) */
+static __device__ __forceinline__ uint32_t sx32(const uint32_t *a, int pos)
 {
   int wi = pos >> 5;
   uint32_t off = (uint32_t)pos & 31u;
-  uint32_t lo = wi >= 0 ? a[swz ? lsw((uint32_t)wi) : (uint32_t)wi] : 0u;
+  uint32_t lo = wi >= 0 ? a[lsw((uint32_t)wi)] : 0u;
   if (!off) return lo;
-  uint32_t hi = wi + 1 >= 0 ? a[swz ? lsw((uint32_t)(wi + 1)) : (uint32_t)(wi + 1)] : 0u;
+  uint32_t hi = wi + 1 >= 0 ? a[lsw((uint32_t)(wi + 1))] : 0u;
   return (lo >> off) | (hi << (32 - off));
 }
 
-static __device__ __forceinline__ uint64_t spread32(uint32_t v)
-{
-  uint64_t x = v;
-  x = (x | (x << 16)) & 0x0000FFFF0000FFFFull;
-  x = (x | (x << 8)) & 0x00FF00FF00FF00FFull;
-  x = (x | (x << 4)) & 0x0F0F0F0F0F0F0F0Full;
-  x = (x | (x << 2)) & 0x3333333333333333ull;
-  x = (x | (x << 1)) & 0x5555555555555555ull;
-  return x;
-}
-
-/* OR a wave-uniform 128-bit value (nbits valid) into LDS bit array a at bit position pos.
- * Lanes 0..4 each handle one destination word. */
-static __device__ __forceinline__ void or_bits128(uint32_t *a, uint32_t pos, uint32_t s0, uint32_t s1, uint32_t s2,
-                                                  uint32_t s3, uint32_t nbits)
-{
-  uint32_t lane = threadIdx.x & 63, off = pos & 31, nw = (off + nbits + 31) >> 5;
-  if (lane < nw) {
-    uint32_t cur = lane == 0 ? s0 : lane == 1 ? s1 : lane == 2 ? s2 : lane == 3 ? s3 : 0u;
-    uint32_t prv = lane == 0 ? 0u : lane == 1 ? s0 : lane == 2 ? s1 : lane == 3 ? s2 : s3;
-    uint32_t v = off ? (cur << off) | (prv >> (32 - off)) : cur;
-    if (v) atomicOr(&a[(pos >> 5) + lane], v);
-  }
-}
-
 /*
- * Sub-block interleaver output w of block r as a packed bit array (NULL entries = 0)
- * (lte_rate_matching.c:51-130).  y^(s) rows of 32 bits are bit-matrix-transposed with wave
- * ballots: ballot((y_row >> b) & 1) is column b for 64 rows at once.
+ * Rate-matcher output word i of block r, traced straight back to the rows of the sub-block
+ * interleaver input (lte_rate_matching.c:51-130, 548-566): w is never built.  y[s][row] holds
+ * 32 bits of y^(s) (y^(2) pre-shifted by one for the (j+1) mod Kpi rule); w position p maps to
+ * column col, row `row` and, in the interlaced half, entry `which`; a run inside one column
+ * reads bit colperm(col) of consecutive rows.
  */
-static __device__ void build_w_bits(uint32_t *wb, const uint32_t *blk, uint32_t sw, uint32_t R, uint32_t Kpi,
-                                    uint32_t ND, uint32_t K, const uint32_t *tails, uint32_t r)
+static __device__ __forceinline__ uint32_t rm_word(const uint32_t *y, uint32_t yst, uint32_t R, uint32_t Kpi,
+                                                   uint32_t ND, uint32_t p, uint32_t need)
 {
-  const uint32_t tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, nwaves = blockDim.x >> 6;
-  const uint32_t nblk = (R + 63) >> 6;
-  for (uint32_t task = wave; task < 3 * nblk; task += nwaves) {
-    uint32_t s = task / nblk, bk = task - s * nblk;
-    uint32_t row = 64 * bk + lane;
-    uint32_t y = 0;
-    if (row < R) {
-      const uint32_t *st = blk + s * sw;
-      int pos = (int)(32 * row) - (int)ND + (s == 2 ? 1 : 0);
-      y = sx32(st, pos, true);
-      if (s == 2 && row == R - 1) {
-        /* j = Kpi-1 reads y^(2)_0: NULL if ND > 0, else d^(2)_0 */
-        y &= 0x7fffffffu;
-        if (ND == 0) y |= (st[lsw(0)] & 1u) << 31;
+  uint32_t region, col, row, which = 0;
+  if (p < Kpi) {
+    region = 0; col = p / R; row = p - col * R;
+  } else {
+    uint32_t q = p - Kpi;
+    region = 1; col = q / (2 * R);
+    uint32_t rr = q - col * 2 * R;
+    row = rr >> 1; which = rr & 1u;
+  }
+  uint32_t out = 0, got = 0;
+  while (got < need) {
+    uint32_t b = colperm(col);
+    if (region == 0) {
+      if (row == 0 && b < ND) row = 1;                        /* NULL at the column head */
+      uint32_t take = min(need - got, R - row);
+      for (uint32_t t = 0; t < take; t++) out |= ((y[lsw(row + t)] >> b) & 1u) << (got + t);
+      got += take;
+      row += take;
+      if (row == R) {
+        row = 0;
+        if (++col == 32) { region = 1; col = 0; which = 0; }
       }
-    }
-    uint32_t nb = min(64u, R - 64 * bk);
-    for (uint32_t b = 0; b < 32; b++) {
-      uint64_t msk = __ballot((y >> b) & 1u);
-      uint32_t col = colperm(b);
-      if (s == 0) {
-        or_bits128(wb, col * R + 64 * bk, (uint32_t)msk, (uint32_t)(msk >> 32), 0, 0, nb);
-      } else {
-        uint64_t lo = spread32((uint32_t)msk) << (s - 1), hi = spread32((uint32_t)(msk >> 32)) << (s - 1);
-        or_bits128(wb, Kpi + col * 2 * R + 128 * bk, (uint32_t)lo, (uint32_t)(lo >> 32), (uint32_t)hi,
-                   (uint32_t)(hi >> 32), 2 * nb);
+    } else {
+      bool isnull = which == 0 ? (row == 0 && b < ND)
+                               : ((row == 0 && b + 1 < ND) || (col == 31 && row == R - 1 && ND > 0));
+      if (!isnull) {
+        out |= ((y[(1 + which) * yst + lsw(row)] >> b) & 1u) << got;
+        got++;
+      }
+      which ^= 1u;
+      if (which == 0 && ++row == R) {
+        row = 0;
+        if (++col == 32) { region = 0; col = 0; }             /* circular wrap (Ncb = Kw) */
       }
     }
   }
-  (void)K; (void)tails; (void)r;
+  return out;
 }
 
 /* ---------------------------------------------------------------------------------------
@@ -416,7 +400,7 @@ static __device__ void encode_codeword(const cfg_dev_t *__restrict__ c, uint32_t
                                        enc_debug_t dbg, uint32_t *lds_base, int stop_phase = 99)
 {
   const cw_dev_t &cw = c->cw[cwi];
-  const uint32_t tid = threadIdx.x, nth = blockDim.x, wave = tid >> 6, nwaves = nth >> 6;
+  const uint32_t tid = threadIdx.x, nth = blockDim.x, wave = tid >> 6, lane = tid & 63, nwaves = nth >> 6;
   const uint32_t sfi = DEBUG ? sf : (c->first_sf + sf * c->sf_step) % 10;
   const uint32_t C = cw.C, sw = cw.stream_words;
   /* LDS carve-up */
@@ -424,20 +408,19 @@ static __device__ void encode_codeword(const cfg_dev_t *__restrict__ c, uint32_t
   uint32_t *strm = tbw + c->lds_tb_words;
   uint32_t *ebuf = strm + c->lds_stream_words;
   uint32_t *wb = ebuf + c->lds_gold_words;
-  uint32_t *inw2 = wb + c->lds_w_words;
-  uint32_t *crctab_a = inw2 + c->lds_inw_words;
+  uint32_t *crctab_a = wb + c->lds_w_words;
   uint32_t *crctab_b = crctab_a + 256;
-  uint32_t *tails = crctab_b + 256;
-  uint32_t *crcs = tails + 2 * OAI4G_MAX_CB;            /* [0] = CRC24A, [1+r] = CRC24B of block r */
-  blk_info_t *bi = (blk_info_t *)(crcs + OAI4G_MAX_CB + 2);
-  enc_tabs_t *tabs = (enc_tabs_t *)(bi + 1);
+  uint32_t *mul_tb = crctab_b + 256;                     /* [8][6][16] */
+  uint32_t *mul_cb = mul_tb + 8 * 96;                    /* [6][6][16] */
+  uint32_t *tails = mul_cb + 6 * 96;
+  uint32_t *crcs = tails + 2 * OAI4G_MAX_CB;             /* [0] = CRC24A, [1+r] = CRC24B of block r */
+  uint32_t *red = crcs + OAI4G_MAX_CB + 2;               /* 4 per-wave partials */
+  enc_tabs_t *tabs = (enc_tabs_t *)(red + 4);
   uint16_t *np = (uint16_t *)(tabs + 1);
-  uint8_t *scanA = (uint8_t *)(np + 2 * OAI4G_MAX_NULLS);
-  uint8_t *scanB = scanA + c->lds_items;
   uint8_t *tbb = (uint8_t *)tbw;
   const uint32_t G = cw.G[sfi], Gw = (G + 31) >> 5;
 
-  /* ---- phase 0: TB bytes, zeroed streams, tables, block info, Gold words ---- */
+  /* ---- phase 0: TB bytes, zeroed streams, tables, Gold words ---- */
   const uint8_t *src = payload + (size_t)(DEBUG ? 0 : (sf * c->n_cw + cwi)) * c->payload_stride;
   const uint32_t Ab = cw.A_bytes;
   for (uint32_t i = tid; i < c->lds_tb_words; i += nth) {
@@ -451,6 +434,8 @@ static __device__ void encode_codeword(const cfg_dev_t *__restrict__ c, uint32_t
   }
   for (uint32_t i = tid; i < c->lds_stream_words; i += nth) strm[i] = 0;
   for (uint32_t i = tid; i < 2 * OAI4G_MAX_NULLS; i += nth) np[i] = cw.nullpos[i / OAI4G_MAX_NULLS][i % OAI4G_MAX_NULLS];
+  for (uint32_t i = tid; i < 8 * 96; i += nth) mul_tb[i] = (&cw.crcmul_tb[0][0][0])[i];
+  for (uint32_t i = tid; i < 6 * 96; i += nth) mul_cb[i] = (&cw.crcmul_cb[0][0][0])[i];
   for (uint32_t v = tid; v < 256; v += nth) {
     uint32_t ra = v << 16, rb = v << 16;
     for (int i = 0; i < 8; i++) {
@@ -465,18 +450,6 @@ static __device__ void encode_codeword(const cfg_dev_t *__restrict__ c, uint32_t
     (&tabs->par[0][0])[tid] = (&c_rsc.par[0][0])[tid];
     if (tid < 64) (&tabs->apow[0][0])[tid] = (&c_rsc.apow[0][0])[tid];
   }
-  if (tid == 0) {
-    bi->C = C;
-    bi->sw = sw;
-    uint32_t it = 0, iw = 0;
-    for (uint32_t r = 0; r < C; r++) {
-      bi->K[r] = cw.K[r]; bi->f1[r] = cw.f1[r]; bi->f2[r] = cw.f2[r];
-      bi->ib[r] = it; bi->inwb[r] = iw;
-      uint32_t nch = (cw.K[r] + 31) >> 5;
-      it += 2 * nch; iw += nch;
-    }
-    bi->ib[C] = it;
-  }
   if (DEBUG) {
     for (uint32_t i = tid; i < Gw + 1; i += nth) ebuf[i] = 0;
   } else {
@@ -487,34 +460,38 @@ static __device__ void encode_codeword(const cfg_dev_t *__restrict__ c, uint32_t
   __syncthreads();
   if (stop_phase <= 0) return;
 
-  /* ---- phase 1: CRC-24A over the TB (wave 0) and CRC-24B over every block's data bytes
-   *      excluding the TB CRC bytes (other waves); dlsch_coding.c:296-300, lte_segmentation.c:156-166 ---- */
-  const uint32_t ntask = 1 + (C > 1 ? C : 0);
-  for (uint32_t task = wave; task < ntask; task += nwaves) {
-    if (task == 0) {
-      uint32_t crc = crc24_wave(tbb, Ab, 0x864cfbu, crctab_a);
-      if ((tid & 63) == 0) crcs[0] = crc;
-    } else {
-      uint32_t r = task - 1, s0 = cw.src[r], n = cw.ncopy[r];
-      if (s0 + n > Ab) n = Ab > s0 ? Ab - s0 : 0;   /* TB CRC bytes are folded in below */
-      uint32_t crc = crc24_wave(tbb + s0, n, 0x800063u, crctab_b);
-      if ((tid & 63) == 0) crcs[1 + r] = crc;
+  /* ---- phase 1: CRC-24A over the TB (dlsch_coding.c:296-300), 256 lanes ---- */
+  {
+    uint32_t reg = crc_chunk(tbb, Ab, cw.crc_per_tb, tid, nth, crctab_a);
+    reg = crc_wave_tree(reg, mul_tb);
+    if (lane == 0) red[wave] = reg;
+    __syncthreads();
+    if (tid == 0) {
+      uint32_t v01 = crc_mul_tab(red[0], mul_tb + 6 * 96) ^ red[1];
+      uint32_t v23 = crc_mul_tab(red[2], mul_tb + 6 * 96) ^ red[3];
+      uint32_t crc = crc_mul_tab(v01, mul_tb + 7 * 96) ^ v23;
+      tbb[Ab] = (uint8_t)(crc >> 16);
+      tbb[Ab + 1] = (uint8_t)(crc >> 8);
+      tbb[Ab + 2] = (uint8_t)crc;
+    }
+  }
+  /* CRC-24B of every block's data bytes (lte_segmentation.c:156-166), one wave per block;
+   * the TB-CRC bytes inside the last block are folded in once they exist */
+  if (C > 1) {
+    for (uint32_t r = wave; r < C; r += nwaves) {
+      uint32_t s0 = cw.src[r], n = cw.ncopy[r];
+      if (s0 + n > Ab) n = Ab > s0 ? Ab - s0 : 0;
+      uint32_t reg = crc_chunk(tbb + s0, n, cw.crc_per_cb, lane, 64, crctab_b);
+      reg = crc_wave_tree(reg, mul_cb);
+      if (lane == 0) crcs[1 + r] = reg;
     }
   }
   __syncthreads();
-  if (tid == 0) {
-    uint32_t crc = crcs[0];
-    tbb[Ab] = (uint8_t)(crc >> 16);
-    tbb[Ab + 1] = (uint8_t)(crc >> 8);
-    tbb[Ab + 2] = (uint8_t)crc;
-    if (C > 1) {
-      /* extend the blocks whose span covers the TB CRC bytes */
-      for (uint32_t r = 0; r < C; r++) {
-        uint32_t s0 = cw.src[r], e0 = s0 + cw.ncopy[r];
-        uint32_t reg = crcs[1 + r];
-        for (uint32_t i = (s0 > Ab ? s0 : Ab); i < e0; i++) reg = crc_step(reg, tbb[i], crctab_b);
-        crcs[1 + r] = reg;
-      }
+  if (C > 1 && tid == 0) {
+    for (uint32_t r = 0; r < C; r++) {
+      uint32_t s0 = cw.src[r], e0 = s0 + cw.ncopy[r], reg = crcs[1 + r];
+      for (uint32_t i = (s0 > Ab ? s0 : Ab); i < e0; i++) reg = crc_step(reg, tbb[i], crctab_b);
+      crcs[1 + r] = reg;
     }
   }
   __syncthreads();
@@ -525,7 +502,7 @@ static __device__ void encode_codeword(const cfg_dev_t *__restrict__ c, uint32_t
   /* ---- phase 2: segmentation -> systematic streams (LSB-first words) ---- */
   for (uint32_t r = 0; r < C; r++) {
     uint32_t K = cw.K[r], nw = (K + 31) >> 5, fill = cw.fill[r], ncopy = cw.ncopy[r], s0 = cw.src[r];
-    uint32_t crcb = crcs[1 + r];
+    uint32_t crcb = C > 1 ? crcs[1 + r] : 0;
     uint32_t *sys = strm + r * 3 * sw;
     for (uint32_t j = tid; j < nw; j += nth) {
       uint32_t le = 0;
@@ -542,10 +519,14 @@ static __device__ void encode_codeword(const cfg_dev_t *__restrict__ c, uint32_t
     }
   }
   __syncthreads();
-
   if (stop_phase <= 2) return;
-  /* ---- phase 3: turbo encoding of every block ---- */
-  turbo_encode_blocks(strm, bi, tails, inw2, scanA, scanB, tabs);
+
+  /* ---- phase 3: turbo encoding, one wave per (block, encoder) ---- */
+  for (uint32_t seg = wave; seg < 2 * C; seg += nwaves) {
+    uint32_t r = seg >> 1, e = seg & 1u;
+    turbo_segment(strm + r * 3 * sw, sw, cw.K[r], cw.f1[r], cw.f2[r], e, &tails[2 * r + e], tabs);
+  }
+  __syncthreads();
   if (stop_phase <= 3) return;
 
   if (DEBUG) {
@@ -594,33 +575,31 @@ static __device__ void encode_codeword(const cfg_dev_t *__restrict__ c, uint32_t
   }
   __syncthreads();
 
-  /* ---- phase 4: per block: packed w, then word-level circular read + scramble ---- */
+  /* ---- phase 4: per block: y^(s) row words, then word-level circular read + scramble ---- */
   const uint32_t *roff = cw.roff[sfi];
   for (uint32_t r = 0; r < C; r++) {
-    uint32_t K = cw.K[r], R = cw.R[r], Kpi = cw.Kpi[r], ND = cw.ND[r], Ncb = cw.Ncb[r], Nnn = cw.Nnn[r];
-    uint32_t nww = (3 * Kpi + 31) / 32 + 2;
-    for (uint32_t i = tid; i < nww; i += nth) wb[i] = 0;
-    __syncthreads();
-    build_w_bits(wb, strm + r * 3 * sw, sw, R, Kpi, ND, K, tails, r);
+    uint32_t R = cw.R[r], Kpi = cw.Kpi[r], ND = cw.ND[r], Nnn = cw.Nnn[r];
+    uint32_t yst = R + (R >> 5) + 2;
+    const uint32_t *blk = strm + r * 3 * sw;
+    for (uint32_t i = tid; i < 3 * R; i += nth) {
+      uint32_t s = i / R, row = i - s * R;
+      const uint32_t *st = blk + s * sw;
+      uint32_t y = sx32(st, (int)(32 * row) - (int)ND + (s == 2 ? 1 : 0));
+      if (s == 2 && row == R - 1) {
+        y &= 0x7fffffffu;                       /* j = Kpi-1 reads y^(2)_0: NULL if ND > 0 */
+        if (ND == 0) y |= (st[lsw(0)] & 1u) << 31;
+      }
+      wb[s * yst + lsw(row)] = y;
+    }
     __syncthreads();
     if (stop_phase <= 4) continue;
     const uint16_t *npl = np + cw.kidx[r] * OAI4G_MAX_NULLS;
     uint32_t nn = cw.nnull[cw.kidx[r]];
     uint32_t E = roff[r + 1] - roff[r], base = roff[r], nwo = (E + 31) >> 5;
     for (uint32_t i = tid; i < nwo; i += nth) {
-      uint32_t need = min(32u, E - 32 * i), got = 0, out = 0, m;
-      uint32_t p = compact_to_pos((cw.k0c[r] + 32 * i) % Nnn, npl, nn, m);
-      while (got < need) {
-        uint32_t nxt = m < nn ? (uint32_t)npl[m] : Ncb;
-        if (p == nxt) { p++; m++; continue; }          /* skip a NULL */
-        if (p >= Ncb) { p = 0; m = 0; continue; }      /* circular wrap (lte_rate_matching.c:559-566) */
-        uint32_t take = min(min(need - got, nxt - p), 32u);
-        uint32_t v = sx32(wb, (int)p, false);
-        if (take < 32) v &= (1u << take) - 1u;
-        out |= v << got;
-        got += take;
-        p += take;
-      }
+      uint32_t need = min(32u, E - 32 * i);
+      uint32_t p = compact_to_pos((cw.k0c[r] + 32 * i) % Nnn, npl, nn);
+      uint32_t out = rm_word(wb, yst, R, Kpi, ND, p, need);
       uint32_t gpos = base + 32 * i, gw = gpos >> 5, off = gpos & 31;
       atomicXor(&ebuf[gw], out << off);
       if (off && (out >> (32 - off))) atomicXor(&ebuf[gw + 1], out >> (32 - off));
@@ -659,9 +638,9 @@ __global__ void __launch_bounds__(256) k_encode_debug(const cfg_dev_t *__restric
 
 static size_t enc_lds_bytes(const cfg_dev_t *h)
 {
-  size_t words = (size_t)h->lds_tb_words + h->lds_stream_words + h->lds_gold_words + h->lds_w_words +
-                 h->lds_inw_words + 256 + 256 + 2 * OAI4G_MAX_CB + OAI4G_MAX_CB + 2;
-  size_t bytes = words * 4 + sizeof(blk_info_t) + sizeof(enc_tabs_t) + 2 * OAI4G_MAX_NULLS * 2 + 2 * h->lds_items;
+  size_t words = (size_t)h->lds_tb_words + h->lds_stream_words + h->lds_gold_words + h->lds_w_words + 256 + 256 +
+                 8 * 96 + 6 * 96 + 2 * OAI4G_MAX_CB + OAI4G_MAX_CB + 2 + 4;
+  size_t bytes = words * 4 + sizeof(enc_tabs_t) + 2 * OAI4G_MAX_NULLS * 2;
   return (bytes + 15) & ~(size_t)15;
 }
 
@@ -730,16 +709,13 @@ hipError_t oai4g_launch_crc24(const uint8_t *d_in, int bitlen, uint32_t poly_top
   return hipGetLastError();
 }
 
-/* threegpplte_turbo_encoder: c bytes -> d bytes (3K+12), one workgroup */
+/* threegpplte_turbo_encoder: c bytes -> d bytes (3K+12), one workgroup (waves 0/1 encode) */
 __global__ void __launch_bounds__(256) k_turbo_bytes(const uint8_t *__restrict__ cin, uint32_t K, uint32_t f1,
                                                      uint32_t f2, uint8_t *__restrict__ dout)
 {
   const uint32_t sw = 208;
   __shared__ uint32_t strm[3 * sw];
   __shared__ uint32_t tails[2];
-  __shared__ uint32_t inw2[192];
-  __shared__ uint8_t scanA[2 * 192], scanB[2 * 192];
-  __shared__ blk_info_t bi;
   __shared__ enc_tabs_t tabs;
   uint32_t nw = (K + 31) >> 5;
   for (uint32_t i = threadIdx.x; i < 3 * sw; i += blockDim.x) strm[i] = 0;
@@ -747,10 +723,6 @@ __global__ void __launch_bounds__(256) k_turbo_bytes(const uint8_t *__restrict__
     (&tabs.next[0][0])[threadIdx.x] = (&c_rsc.next[0][0])[threadIdx.x];
     (&tabs.par[0][0])[threadIdx.x] = (&c_rsc.par[0][0])[threadIdx.x];
     if (threadIdx.x < 64) (&tabs.apow[0][0])[threadIdx.x] = (&c_rsc.apow[0][0])[threadIdx.x];
-  }
-  if (threadIdx.x == 0) {
-    bi.C = 1; bi.sw = sw; bi.K[0] = K; bi.f1[0] = f1; bi.f2[0] = f2;
-    bi.ib[0] = 0; bi.ib[1] = 2 * nw; bi.inwb[0] = 0;
   }
   __syncthreads();
   for (uint32_t j = threadIdx.x; j < nw; j += blockDim.x) {
@@ -764,7 +736,9 @@ __global__ void __launch_bounds__(256) k_turbo_bytes(const uint8_t *__restrict__
     strm[lsw(j)] = wv;
   }
   __syncthreads();
-  turbo_encode_blocks(strm, &bi, tails, inw2, scanA, scanB, &tabs);
+  uint32_t wave = threadIdx.x >> 6;
+  if (wave < 2) turbo_segment(strm, sw, K, f1, f2, wave, &tails[wave], &tabs);
+  __syncthreads();
   for (uint32_t i = threadIdx.x; i < 3 * K + 12; i += blockDim.x) {
     uint32_t kk = i / 3, s = i - 3 * kk;
     dout[i] = (uint8_t)(kk < K ? dstream_bit(strm, sw, tails, 0, K, s, kk) : tail_bit(tails, 0, i - 3 * K));

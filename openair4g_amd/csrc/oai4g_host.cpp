@@ -316,6 +316,39 @@ static int null_positions(uint32_t K, uint16_t *out, uint32_t maxn)
   return (int)n;
 }
 
+/* GF(2)[x] products modulo a CRC-24 polynomial (24-bit register, x^24 implicit) */
+static uint32_t crc_mulmod_h(uint32_t a, uint32_t b, uint32_t poly)
+{
+  uint32_t r = 0;
+  for (int i = 23; i >= 0; i--) {
+    r <<= 1;
+    if (r & 0x1000000u) r ^= 0x1000000u | poly;
+    if ((b >> i) & 1u) r ^= a;
+  }
+  return r;
+}
+
+static uint32_t crc_xpow8_h(uint64_t n, uint32_t poly)   /* x^(8n) mod P */
+{
+  uint32_t result = 1, base = 0x100;
+  while (n) {
+    if (n & 1u) result = crc_mulmod_h(result, base, poly);
+    base = crc_mulmod_h(base, base, poly);
+    n >>= 1;
+  }
+  return result;
+}
+
+/* tab[d][k][v] = (v * x^(4k)) * x^(8*per*2^d) mod P, so a*m_d = xor_k tab[d][k][nibble_k(a)] */
+static void crc_mul_tables(uint32_t per, int levels, uint32_t poly, uint32_t (*tab)[6][16])
+{
+  for (int d = 0; d < levels; d++) {
+    uint32_t m = crc_xpow8_h((uint64_t)per << d, poly);
+    for (int k = 0; k < 6; k++)
+      for (uint32_t v = 0; v < 16; v++) tab[d][k][v] = crc_mulmod_h((v << (4 * k)) & 0xffffffu, m, poly);
+  }
+}
+
 /* QAM tables (dlsch_modulation.c:79-103, 1223-1246) */
 static void qam_tables_scaled(int Qm, int16_t amp, int16_t srho_a, int16_t srho_b, int16_t *ta, int16_t *tb,
                               int16_t *qa, int16_t *qb)
@@ -515,6 +548,16 @@ static int derive_cfg(oai4g_tx_config *cfg, const oai4g_tx_params_t *p, const ui
       c.kidx[r] = (C > 1 && r < Cm) ? 0 : 1;
     }
     if (src != (c.TBS + 24) / 8) { set_err("segmentation byte accounting mismatch"); return -1; }
+    c.crc_per_tb = (c.A_bytes + 255) / 256;
+    crc_mul_tables(c.crc_per_tb, 8, 0x864cfbu, c.crcmul_tb);
+    uint32_t ncb_max = 0;
+    for (uint32_t r = 0; r < C; r++) {
+      uint32_t n = c.ncopy[r];
+      if (c.src[r] + n > c.A_bytes) n = c.A_bytes > c.src[r] ? c.A_bytes - c.src[r] : 0;
+      ncb_max = n > ncb_max ? n : ncb_max;
+    }
+    c.crc_per_cb = (ncb_max + 63) / 64;
+    crc_mul_tables(c.crc_per_cb ? c.crc_per_cb : 1, 6, 0x800063u, c.crcmul_cb);
     for (int ki = 0; ki < 2; ki++) {
       uint32_t K = ki == 0 ? (Km ? Km : Kp) : Kp;
       int n = null_positions(K, c.nullpos[ki], OAI4G_MAX_NULLS);
@@ -538,7 +581,12 @@ static int derive_cfg(oai4g_tx_config *cfg, const oai4g_tx_params_t *p, const ui
     for (uint32_t r = 0; r < C; r++) inw += (c.K[r] + 31) >> 5;
     max_inw = inw > max_inw ? inw : max_inw;
     uint32_t wwords = 0;
-    for (uint32_t r = 0; r < C; r++) { uint32_t ww = (3 * c.Kpi[r] + 31) / 32 + 2; wwords = ww > wwords ? ww : wwords; }
+    for (uint32_t r = 0; r < C; r++) {
+      /* debug path: packed w; fused path: 3 padded row arrays y^(s) */
+      uint32_t ww = (3 * c.Kpi[r] + 31) / 32 + 2, R = c.R[r], yw = 3 * (R + (R >> 5) + 2);
+      ww = ww > yw ? ww : yw;
+      wwords = ww > wwords ? ww : wwords;
+    }
     max_w = wwords > max_w ? wwords : max_w;
     uint32_t tbw = (c.A_bytes + 3 + 3) / 4 + 1;
     max_tb_words = tbw > max_tb_words ? tbw : max_tb_words;

@@ -61,6 +61,11 @@ struct cw_dev_t {
   int16_t qam_a[8], qam_b[8];   /* amp_rho-scaled QAM levels (dlsch_modulation.c:1223-1246) */
   int16_t qpsk_a, qpsk_b;
   uint32_t stream_words;        /* LDS words per stream per block (padded) */
+  /* CRC tree combine (x^(8*per*2^d) mod P as 6 nibble tables of 16 entries per level) */
+  uint32_t crc_per_tb;          /* bytes per lane, 256 lanes, CRC-24A over the TB */
+  uint32_t crc_per_cb;          /* bytes per lane, 64 lanes, CRC-24B per block */
+  uint32_t crcmul_tb[8][6][16];
+  uint32_t crcmul_cb[6][6][16];
 };
 
 struct cfg_dev_t {
