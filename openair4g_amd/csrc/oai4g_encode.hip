@@ -26,6 +26,12 @@ struct rsc_tables_t {
   uint8_t next[8][16];   /* state after 4 input bits (LSB-first nibble) */
   uint8_t par[8][16];    /* 4 parity bits, LSB-first */
   uint8_t apow[8][8];    /* zero-input propagation by 32*2^d steps: apow[d][s] */
+  /* The RSC is linear and time-invariant over GF(2).  For a 32-bit input chunk u and
+   * entry state s:  parity = clmul_lo(u, hz) ^ zs[s],  exit = apow[0][s] ^ F(u) with
+   * F(u)_i = parity(u & fm[i]). */
+  uint32_t hz;           /* impulse response of the parity output (32 steps) */
+  uint32_t zs[8];        /* zero-input parity response from state s */
+  uint32_t fm[3];        /* input -> exit-state masks */
 };
 
 static constexpr uint8_t rsc_step_c(uint8_t u, uint8_t s, uint8_t *out)
@@ -57,10 +63,55 @@ static constexpr rsc_tables_t make_rsc_tables()
       }
       t.apow[d][s] = st;
     }
+  for (int s = 0; s < 8; s++) {
+    uint8_t st = (uint8_t)s;
+    uint32_t z = 0;
+    for (int k = 0; k < 32; k++) {
+      uint8_t o = 0;
+      st = rsc_step_c(k == 0 && s == 0 ? 1 : 0, st, &o);
+      z |= (uint32_t)o << k;
+    }
+    if (s == 0) t.hz = z; /* input = impulse at k = 0 from the zero state */
+    uint8_t st2 = (uint8_t)s;
+    uint32_t z2 = 0;
+    for (int k = 0; k < 32; k++) {
+      uint8_t o = 0;
+      st2 = rsc_step_c(0, st2, &o);
+      z2 |= (uint32_t)o << k;
+    }
+    t.zs[s] = z2;
+  }
+  for (int k = 0; k < 32; k++) {
+    uint8_t st = 0;
+    for (int n = 0; n < 32; n++) {
+      uint8_t o = 0;
+      st = rsc_step_c(n == k ? 1 : 0, st, &o);
+    }
+    for (int i = 0; i < 3; i++)
+      if ((st >> i) & 1) t.fm[i] |= 1u << k;
+  }
   return t;
 }
 
-__constant__ rsc_tables_t c_rsc = make_rsc_tables();
+static constexpr rsc_tables_t k_rsc = make_rsc_tables();
+
+/* truncated carry-less product u * hz (compile-time constant taps) */
+static __device__ __forceinline__ uint32_t rsc_parity_word(uint32_t u)
+{
+  uint32_t acc = 0;
+#pragma unroll
+  for (int i = 0; i < 32; i++)
+    if ((k_rsc.hz >> i) & 1u) acc ^= u << i;
+  return acc;
+}
+
+static __device__ __forceinline__ uint32_t rsc_exit_input(uint32_t u)
+{
+  return (__builtin_popcount(u & k_rsc.fm[0]) & 1u) | ((__builtin_popcount(u & k_rsc.fm[1]) & 1u) << 1) |
+         ((__builtin_popcount(u & k_rsc.fm[2]) & 1u) << 2);
+}
+
+__constant__ rsc_tables_t c_rsc = k_rsc;
 
 
 static __device__ __forceinline__ uint32_t lsw(uint32_t w) { return w + (w >> 5); } /* stream word swizzle */
@@ -189,9 +240,11 @@ struct enc_tabs_t {            /* LDS copy of the RSC tables (lane-varying indic
   uint8_t next[8][16];
   uint8_t par[8][16];
   uint8_t apow[8][8];
+  uint32_t zs[8];
 };
 
-/* interleaved input word of chunk j: bits c'_k = c_Pi(k), Pi(k) = (f1 k + f2 k^2) mod K */
+/* interleaved input word of chunk j: bits c'_k = c_Pi(k), Pi(k) = (f1 k + f2 k^2) mod K.
+ * All 32 addresses are formed first so the 32 LDS reads issue back to back. */
 static __device__ __forceinline__ uint32_t qpp_word(const uint32_t *sys, uint32_t K, uint32_t f1, uint32_t f2,
                                                     uint32_t j)
 {
@@ -199,15 +252,19 @@ static __device__ __forceinline__ uint32_t qpp_word(const uint32_t *sys, uint32_
   uint32_t pi = (((f2 * k) % K) * k + f1 * k) % K;            /* fits 32 bits for K <= 6144 */
   uint32_t dl = (f1 + ((f2 * ((2 * k + 1) % K)) % K)) % K;     /* Pi(k+1) - Pi(k) */
   uint32_t d2 = (2u * f2) % K;
-  uint32_t word = 0;
-  for (uint32_t b = 0; b < n; b++) {
-    word |= ((sys[lsw(pi >> 5)] >> (pi & 31)) & 1u) << b;
+  uint32_t pis[32];
+#pragma unroll
+  for (int b = 0; b < 32; b++) {
+    pis[b] = pi;
     pi += dl;
     if (pi >= K) pi -= K;
     dl += d2;
     if (dl >= K) dl -= K;
   }
-  return word;
+  uint32_t word = 0;
+#pragma unroll
+  for (int b = 0; b < 32; b++) word |= ((sys[lsw(pis[b] >> 5)] >> (pis[b] & 31)) & 1u) << b;
+  return n == 32 ? word : word & ((1u << n) - 1u);
 }
 
 /* encode one segment (block r, encoder e) with the calling wavefront */
@@ -217,20 +274,16 @@ static __device__ void turbo_segment(uint32_t *blk, uint32_t sw, uint32_t K, uin
   const uint32_t lane = threadIdx.x & 63;
   const uint32_t nch = (K + 31) >> 5;
   const uint32_t lq = nch <= 64 ? 0 : (nch <= 128 ? 1 : 2), qp = 1u << lq;
-  uint32_t u[4], s0[4];
+  uint32_t u[4];
   uint32_t S = 0;
 #pragma unroll
   for (int t = 0; t < 4; t++) {
     u[t] = 0;
-    s0[t] = 0;
     uint32_t j = lane * qp + t;
-    if (t < (int)qp && j < nch) {
-      u[t] = e ? qpp_word(blk, K, f1, f2, j) : blk[lsw(j)];
-      uint32_t nnib = min(32u, K - 32 * j) >> 2, s = 0;
-      for (uint32_t q = 0; q < nnib; q++) s = tb->next[s][(u[t] >> (4 * q)) & 15u];
-      s0[t] = s;
-    }
-    if (t < (int)qp) S = tb->apow[0][S] ^ s0[t];
+    if (t < (int)qp && j < nch) u[t] = e ? qpp_word(blk, K, f1, f2, j) : blk[lsw(j)];
+    /* zero-start exit state of a full chunk: A^32 contribution of the inputs (partial chunks
+     * only feed later lanes, whose values are not used) */
+    if (t < (int)qp) S = tb->apow[0][S] ^ rsc_exit_input(u[t]);
   }
   /* inclusive scan over lanes: S_l ^= A^(32 qp 2^d) S_(l - 2^d) */
 #pragma unroll
@@ -244,11 +297,13 @@ static __device__ void turbo_segment(uint32_t *blk, uint32_t sw, uint32_t K, uin
   for (int t = 0; t < 4; t++) {
     uint32_t j = lane * qp + t;
     if (t < (int)qp && j < nch) {
-      uint32_t nnib = min(32u, K - 32 * j) >> 2, par = 0;
-      for (uint32_t q = 0; q < nnib; q++) {
-        uint32_t nib = (u[t] >> (4 * q)) & 15u;
-        par |= (uint32_t)tb->par[s][nib] << (4 * q);
-        s = tb->next[s][nib];
+      uint32_t n = min(32u, K - 32 * j);
+      uint32_t par = rsc_parity_word(u[t]) ^ tb->zs[s];
+      if (n < 32) {
+        par &= (1u << n) - 1u;
+        for (uint32_t q = 0; q < (n >> 2); q++) s = tb->next[s][(u[t] >> (4 * q)) & 15u];
+      } else {
+        s = tb->apow[0][s] ^ rsc_exit_input(u[t]);
       }
       blk[(1 + e) * sw + lsw(j)] = par;
       if (j == nch - 1) {
@@ -318,8 +373,55 @@ static __device__ __forceinline__ bool wwalk_null(const wwalk_t &w, uint32_t R, 
   return (cp + 1 < ND) || (w.col == 31 && R == 1 && ND > 0);
 }
 
-/* position of the ci-th non-NULL entry of w (sorted NULL positions np[0..nn)) */
-static __device__ __forceinline__ uint32_t compact_to_pos(uint32_t ci, const uint16_t *np, uint32_t nn)
+/* bit idx of constituent stream s (tails appended at K), 0 for idx < 0 (NULL prefix) */
+static __device__ __forceinline__ uint32_t sbit(const uint32_t *st, int idx)
+{
+  uint32_t u = (uint32_t)max(idx, 0);
+  uint32_t v = (st[lsw(u >> 5)] >> (u & 31)) & 1u;
+  return idx < 0 ? 0u : v;
+}
+
+/*
+ * Word wi of the packed sub-block interleaver output w (lte_rate_matching.c:51-130): bits
+ * 32wi..32wi+31.  In the first Kpi entries (v^(0)) a word covers at most two columns (R >= 32
+ * or Kpi-aligned words), in the interlaced half 16 rows of at most two columns; each row
+ * entry is bit 32*row + colperm(col) - ND of its stream.  NULL entries read as 0 and are
+ * skipped by the rate matcher through the NULL list.
+ */
+static __device__ __forceinline__ uint32_t w_word(const uint32_t *blk, uint32_t sw, uint32_t R, uint32_t Kpi,
+                                                  uint32_t ND, uint32_t wi)
+{
+  uint32_t q = 32 * wi, v = 0;
+  if (q < Kpi) {
+    uint32_t col = q / R, row = q - col * R;
+    int b0 = (int)colperm(col) - (int)ND, b1 = (int)colperm(min(col + 1, 31u)) - (int)ND;
+#pragma unroll 8
+    for (uint32_t t = 0; t < 32; t++) {
+      uint32_t rr = row + t;
+      bool c2 = rr >= R;
+      rr = c2 ? rr - R : rr;
+      v |= sbit(blk, 32 * (int)rr + (c2 ? b1 : b0)) << t;
+    }
+  } else {
+    uint32_t e = q - Kpi, col = e / (2 * R), row = (e - col * 2 * R) >> 1;
+    int b0 = (int)colperm(col) - (int)ND, b1 = (int)colperm(min(col + 1, 31u)) - (int)ND;
+    const uint32_t *s1 = blk + sw, *s2 = blk + 2 * sw;
+#pragma unroll 4
+    for (uint32_t t = 0; t < 16; t++) {
+      uint32_t rr = row + t;
+      bool c2 = rr >= R;
+      rr = c2 ? rr - R : rr;
+      int j = 32 * (int)rr + (c2 ? b1 : b0);
+      /* v^(2)_k = y^(2)_{(pi(k)+1) mod Kpi}: the last entry wraps to y^(2)_0 */
+      int j2 = (j + (int)ND + 1 == (int)Kpi) ? -(int)ND : j + 1;
+      v |= (sbit(s1, j) << (2 * t)) | (sbit(s2, j2) << (2 * t + 1));
+    }
+  }
+  return v;
+}
+
+/* position p of the ci-th non-NULL entry of w and m = NULLs before p */
+static __device__ __forceinline__ uint32_t compact_to_pos2(uint32_t ci, const uint16_t *np, uint32_t nn, uint32_t &m)
 {
   uint32_t lo = 0, hi = nn;
   while (lo < hi) {
@@ -327,68 +429,45 @@ static __device__ __forceinline__ uint32_t compact_to_pos(uint32_t ci, const uin
     if ((uint32_t)np[mid] - mid <= ci) lo = mid + 1;
     else hi = mid;
   }
+  m = lo;
   return ci + lo;
 }
 
-/* 32 bits of a packed LSB-first LDS bit array (swizzled words) starting at bit `pos` (pos may be
- * negative: zeros) */
-static __device__ __forceinline__ uint32_t sx32(const uint32_t *a, int pos)
-{
-  int wi = pos >> 5;
-  uint32_t off = (uint32_t)pos & 31u;
-  uint32_t lo = wi >= 0 ? a[lsw((uint32_t)wi)] : 0u;
-  if (!off) return lo;
-  uint32_t hi = wi + 1 >= 0 ? a[lsw((uint32_t)(wi + 1))] : 0u;
-  return (lo >> off) | (hi << (32 - off));
-}
-
 /*
- * Rate-matcher output word i of block r, traced straight back to the rows of the sub-block
- * interleaver input (lte_rate_matching.c:51-130, 548-566): w is never built.  y[s][row] holds
- * 32 bits of y^(s) (y^(2) pre-shifted by one for the (j+1) mod Kpi rule); w position p maps to
- * column col, row `row` and, in the interlaced half, entry `which`; a run inside one column
- * reads bit colperm(col) of consecutive rows.
+ * Rate-matcher output word (lte_rate_matching.c:548-566): `need` non-NULL entries of the
+ * circular buffer w[0..Ncb) starting at position p (m NULLs before p).  Inside the buffer a
+ * 64-bit window of packed w with the (few) NULL bits squeezed out; across the wrap, bit by bit.
  */
-static __device__ __forceinline__ uint32_t rm_word(const uint32_t *y, uint32_t yst, uint32_t R, uint32_t Kpi,
-                                                   uint32_t ND, uint32_t p, uint32_t need)
+static __device__ __forceinline__ uint32_t rm_window(const uint32_t *wpk, uint32_t p, uint32_t m, uint32_t Ncb,
+                                                     const uint16_t *np, uint32_t nn, uint32_t need)
 {
-  uint32_t region, col, row, which = 0;
-  if (p < Kpi) {
-    region = 0; col = p / R; row = p - col * R;
+  uint32_t out = 0;
+  if (p + 64 <= Ncb) {
+    uint32_t wi = p >> 5, off = p & 31;
+    uint64_t x = ((uint64_t)wpk[wi + 1] << 32) | wpk[wi];
+    x >>= off;
+    if (off) x |= (uint64_t)wpk[wi + 2] << (64 - off);
+    uint32_t del = 0;
+    while (m < nn) {
+      uint32_t k = (uint32_t)np[m] - p - del;
+      if (k >= 32) break;
+      uint64_t lo = (1ull << k) - 1ull;
+      x = (x & lo) | ((x >> 1) & ~lo);
+      del++;
+      m++;
+    }
+    out = (uint32_t)x;
   } else {
-    uint32_t q = p - Kpi;
-    region = 1; col = q / (2 * R);
-    uint32_t rr = q - col * 2 * R;
-    row = rr >> 1; which = rr & 1u;
-  }
-  uint32_t out = 0, got = 0;
-  while (got < need) {
-    uint32_t b = colperm(col);
-    if (region == 0) {
-      if (row == 0 && b < ND) row = 1;                        /* NULL at the column head */
-      uint32_t take = min(need - got, R - row);
-      for (uint32_t t = 0; t < take; t++) out |= ((y[lsw(row + t)] >> b) & 1u) << (got + t);
-      got += take;
-      row += take;
-      if (row == R) {
-        row = 0;
-        if (++col == 32) { region = 1; col = 0; which = 0; }
-      }
-    } else {
-      bool isnull = which == 0 ? (row == 0 && b < ND)
-                               : ((row == 0 && b + 1 < ND) || (col == 31 && row == R - 1 && ND > 0));
-      if (!isnull) {
-        out |= ((y[(1 + which) * yst + lsw(row)] >> b) & 1u) << got;
-        got++;
-      }
-      which ^= 1u;
-      if (which == 0 && ++row == R) {
-        row = 0;
-        if (++col == 32) { region = 0; col = 0; }             /* circular wrap (Ncb = Kw) */
-      }
+    uint32_t got = 0;
+    while (got < need) {
+      if (p >= Ncb) { p = 0; m = 0; }
+      if (m < nn && np[m] == p) { p++; m++; continue; }
+      out |= ((wpk[p >> 5] >> (p & 31)) & 1u) << got;
+      got++;
+      p++;
     }
   }
-  return out;
+  return need < 32 ? out & ((1u << need) - 1u) : out;
 }
 
 /* ---------------------------------------------------------------------------------------
@@ -449,6 +528,7 @@ static __device__ void encode_codeword(const cfg_dev_t *__restrict__ c, uint32_t
     (&tabs->next[0][0])[tid] = (&c_rsc.next[0][0])[tid];
     (&tabs->par[0][0])[tid] = (&c_rsc.par[0][0])[tid];
     if (tid < 64) (&tabs->apow[0][0])[tid] = (&c_rsc.apow[0][0])[tid];
+    if (tid < 8) tabs->zs[tid] = c_rsc.zs[tid];
   }
   if (DEBUG) {
     for (uint32_t i = tid; i < Gw + 1; i += nth) ebuf[i] = 0;
@@ -575,37 +655,40 @@ static __device__ void encode_codeword(const cfg_dev_t *__restrict__ c, uint32_t
   }
   __syncthreads();
 
-  /* ---- phase 4: per block: y^(s) row words, then word-level circular read + scramble ---- */
-  const uint32_t *roff = cw.roff[sfi];
-  for (uint32_t r = 0; r < C; r++) {
-    uint32_t R = cw.R[r], Kpi = cw.Kpi[r], ND = cw.ND[r], Nnn = cw.Nnn[r];
-    uint32_t yst = R + (R >> 5) + 2;
-    const uint32_t *blk = strm + r * 3 * sw;
-    for (uint32_t i = tid; i < 3 * R; i += nth) {
-      uint32_t s = i / R, row = i - s * R;
-      const uint32_t *st = blk + s * sw;
-      uint32_t y = sx32(st, (int)(32 * row) - (int)ND + (s == 2 ? 1 : 0));
-      if (s == 2 && row == R - 1) {
-        y &= 0x7fffffffu;                       /* j = Kpi-1 reads y^(2)_0: NULL if ND > 0 */
-        if (ND == 0) y |= (st[lsw(0)] & 1u) << 31;
-      }
-      wb[s * yst + lsw(row)] = y;
-    }
-    __syncthreads();
-    if (stop_phase <= 4) continue;
-    const uint16_t *npl = np + cw.kidx[r] * OAI4G_MAX_NULLS;
-    uint32_t nn = cw.nnull[cw.kidx[r]];
-    uint32_t E = roff[r + 1] - roff[r], base = roff[r], nwo = (E + 31) >> 5;
-    for (uint32_t i = tid; i < nwo; i += nth) {
-      uint32_t need = min(32u, E - 32 * i);
-      uint32_t p = compact_to_pos((cw.k0c[r] + 32 * i) % Nnn, npl, nn);
-      uint32_t out = rm_word(wb, yst, R, Kpi, ND, p, need);
-      uint32_t gpos = base + 32 * i, gw = gpos >> 5, off = gpos & 31;
-      atomicXor(&ebuf[gw], out << off);
-      if (off && (out >> (32 - off))) atomicXor(&ebuf[gw + 1], out >> (32 - off));
-    }
-    __syncthreads();
+  /* ---- phase 4a: packed w of every block ---- */
+  const uint32_t wtot = cw.wpk_off[C];
+  for (uint32_t i = tid; i < wtot; i += nth) {
+    uint32_t r = 0;
+    while (r + 1 < C && i >= cw.wpk_off[r + 1]) r++;
+    uint32_t wi = i - cw.wpk_off[r], R = cw.R[r];
+    wb[i] = wi < 3 * R ? w_word(strm + r * 3 * sw, sw, R, cw.Kpi[r], cw.ND[r], wi) : 0u;
   }
+  __syncthreads();
+  if (stop_phase <= 4) return;
+
+  /* ---- phase 4b: rate matching of every block, XORed into the Gold words ---- */
+  const uint32_t *roff = cw.roff[sfi];
+  uint32_t nwtot = 0;
+  for (uint32_t r = 0; r < C; r++) nwtot += (roff[r + 1] - roff[r] + 31) >> 5;
+  for (uint32_t i = tid; i < nwtot; i += nth) {
+    uint32_t r = 0, acc = 0;
+    for (;;) {
+      uint32_t nwo = (roff[r + 1] - roff[r] + 31) >> 5;
+      if (r + 1 == C || i < acc + nwo) break;
+      acc += nwo;
+      r++;
+    }
+    const uint32_t k = i - acc, E = roff[r + 1] - roff[r];
+    const uint16_t *npl = np + cw.kidx[r] * OAI4G_MAX_NULLS;
+    const uint32_t nn = cw.nnull[cw.kidx[r]];
+    uint32_t need = min(32u, E - 32 * k), m;
+    uint32_t p = compact_to_pos2((cw.k0c[r] + 32 * k) % cw.Nnn[r], npl, nn, m);
+    uint32_t out = rm_window(wb + cw.wpk_off[r], p, m, cw.Ncb[r], npl, nn, need);
+    uint32_t gpos = roff[r] + 32 * k, gw = gpos >> 5, off = gpos & 31;
+    atomicXor(&ebuf[gw], out << off);
+    if (off && (out >> (32 - off))) atomicXor(&ebuf[gw + 1], out >> (32 - off));
+  }
+  __syncthreads();
 
   if (DEBUG) {
     for (uint32_t k = tid; k < G; k += nth) dbg.e[k] = (uint8_t)((ebuf[k >> 5] >> (k & 31)) & 1u);
@@ -723,6 +806,7 @@ __global__ void __launch_bounds__(256) k_turbo_bytes(const uint8_t *__restrict__
     (&tabs.next[0][0])[threadIdx.x] = (&c_rsc.next[0][0])[threadIdx.x];
     (&tabs.par[0][0])[threadIdx.x] = (&c_rsc.par[0][0])[threadIdx.x];
     if (threadIdx.x < 64) (&tabs.apow[0][0])[threadIdx.x] = (&c_rsc.apow[0][0])[threadIdx.x];
+    if (threadIdx.x < 8) tabs.zs[threadIdx.x] = c_rsc.zs[threadIdx.x];
   }
   __syncthreads();
   for (uint32_t j = threadIdx.x; j < nw; j += blockDim.x) {

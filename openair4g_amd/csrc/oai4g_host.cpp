@@ -580,13 +580,13 @@ static int derive_cfg(oai4g_tx_config *cfg, const oai4g_tx_params_t *p, const ui
     uint32_t inw = 0;
     for (uint32_t r = 0; r < C; r++) inw += (c.K[r] + 31) >> 5;
     max_inw = inw > max_inw ? inw : max_inw;
+    /* packed w of every block (3 Kpi bits = 3R words, + 2 read-ahead words each) */
     uint32_t wwords = 0;
     for (uint32_t r = 0; r < C; r++) {
-      /* debug path: packed w; fused path: 3 padded row arrays y^(s) */
-      uint32_t ww = (3 * c.Kpi[r] + 31) / 32 + 2, R = c.R[r], yw = 3 * (R + (R >> 5) + 2);
-      ww = ww > yw ? ww : yw;
-      wwords = ww > wwords ? ww : wwords;
+      c.wpk_off[r] = wwords;
+      wwords += 3 * c.R[r] + 2;
     }
+    c.wpk_off[C] = wwords;
     max_w = wwords > max_w ? wwords : max_w;
     uint32_t tbw = (c.A_bytes + 3 + 3) / 4 + 1;
     max_tb_words = tbw > max_tb_words ? tbw : max_tb_words;

@@ -52,6 +52,7 @@ struct cw_dev_t {
   uint32_t Nnn[OAI4G_MAX_CB];   /* non-NULL entries of w[0..Ncb) */
   uint32_t k0c[OAI4G_MAX_CB];   /* non-NULL entries of w[0..k0): compacted start */
   uint32_t kidx[OAI4G_MAX_CB];  /* which null list (0: Kminus, 1: Kplus) */
+  uint32_t wpk_off[OAI4G_MAX_CB + 1]; /* LDS word offset of block r's packed w (3R words + 2 pad) */
   uint32_t nnull[2];
   uint16_t nullpos[2][OAI4G_MAX_NULLS]; /* sorted NULL positions of w for K = Kminus / Kplus */
   /* per subframe index */
