@@ -141,18 +141,25 @@ static __device__ __forceinline__ void gold_step(uint32_t &x1, uint32_t &x2)
   x2 = x2 ^ (x2 << 31) ^ (x2 << 30) ^ (x2 << 29) ^ (x2 << 28);
 }
 
-static __device__ void gold_generate(uint32_t *gold, uint32_t nwords, uint32_t c_init, const uint32_t *gx1,
-                                     const uint32_t *gx2j)
+typedef const __attribute__((address_space(1))) uint32_t gu32_t;
+
+/* Gold words 0..nwords-1 (word w = state after 50+w steps): lane l jumps to word 16l with the
+ * host's M^(50+16l) tables and steps 16 words.  Needs blockDim.x == OAI4G_GOLD_LANES. */
+static __device__ __forceinline__ void gold_generate(uint32_t *gold, uint32_t nwords, uint32_t c_init,
+                                                     const uint32_t *gx1, const uint32_t *gx2j)
 {
-  uint32_t l = threadIdx.x;
-  if (l >= 64 || 64 * l >= nwords) return;
-  uint32_t x2i = c_init ^ ((c_init ^ (c_init >> 1) ^ (c_init >> 2) ^ (c_init >> 3)) << 31);
+  const uint32_t l = threadIdx.x, w0 = OAI4G_GOLD_STRIDE * l;
+  if (l >= OAI4G_GOLD_LANES || w0 >= nwords) return;
+  const uint32_t x2i = c_init ^ ((c_init ^ (c_init >> 1) ^ (c_init >> 2) ^ (c_init >> 3)) << 31);
+  gu32_t *col = (gu32_t *)(gx2j + 32 * l);
+  uint32_t cv[32];
+#pragma unroll
+  for (int b = 0; b < 32; b++) cv[b] = col[b];
   uint32_t x2 = 0;
-  const uint32_t *col = gx2j + 32 * l;
-  for (int b = 0; b < 32; b++)
-    if ((x2i >> b) & 1u) x2 ^= col[b];
-  uint32_t x1 = gx1[l];
-  uint32_t w0 = 64 * l, wend = min(w0 + 64, nwords);
+#pragma unroll
+  for (int b = 0; b < 32; b++) x2 ^= cv[b] & (0u - ((x2i >> b) & 1u));
+  uint32_t x1 = *(gu32_t *)(gx1 + l);
+  const uint32_t wend = min(w0 + OAI4G_GOLD_STRIDE, nwords);
   gold[w0] = x1 ^ x2;
   for (uint32_t w = w0 + 1; w < wend; w++) {
     gold_step(x1, x2);
@@ -268,7 +275,7 @@ static __device__ __forceinline__ uint32_t qpp_word(const uint32_t *sys, uint32_
 }
 
 /* encode one segment (block r, encoder e) with the calling wavefront */
-static __device__ void turbo_segment(uint32_t *blk, uint32_t sw, uint32_t K, uint32_t f1, uint32_t f2, uint32_t e,
+static __device__ __forceinline__ void turbo_segment(uint32_t *blk, uint32_t sw, uint32_t K, uint32_t f1, uint32_t f2, uint32_t e,
                                      uint32_t *tail_out, const enc_tabs_t *tb)
 {
   const uint32_t lane = threadIdx.x & 63;
@@ -373,48 +380,83 @@ static __device__ __forceinline__ bool wwalk_null(const wwalk_t &w, uint32_t R, 
   return (cp + 1 < ND) || (w.col == 31 && R == 1 && ND > 0);
 }
 
-/* bit idx of constituent stream s (tails appended at K), 0 for idx < 0 (NULL prefix) */
-static __device__ __forceinline__ uint32_t sbit(const uint32_t *st, int idx)
+/* 32 bits of a packed LSB-first LDS bit array (swizzled words) starting at bit `pos` (pos may be
+ * negative: zeros) */
+static __device__ __forceinline__ uint32_t sx32(const uint32_t *a, int pos)
 {
-  uint32_t u = (uint32_t)max(idx, 0);
-  uint32_t v = (st[lsw(u >> 5)] >> (u & 31)) & 1u;
-  return idx < 0 ? 0u : v;
+  int wi = pos >> 5;
+  uint32_t off = (uint32_t)pos & 31u;
+  uint32_t lo = a[lsw((uint32_t)max(wi, 0))];
+  lo = wi >= 0 ? lo : 0u;
+  uint32_t hi = a[lsw((uint32_t)max(wi + 1, 0))];
+  hi = wi + 1 >= 0 ? hi : 0u;
+  return off ? (lo >> off) | (hi << (32 - off)) : lo;
+}
+
+/* 32 bits of an unswizzled bit array starting at bit o (reads one word ahead) */
+static __device__ __forceinline__ uint32_t ext32(const uint32_t *a, uint32_t o)
+{
+  uint32_t w = o >> 5, sh = o & 31u;
+  uint32_t lo = a[w], hi = a[w + 1];
+  return sh ? (lo >> sh) | (hi << (32 - sh)) : lo;
+}
+
+static __device__ __forceinline__ uint32_t lowmask(uint32_t n) { return n >= 32 ? 0xffffffffu : (1u << n) - 1u; }
+
+/* 16 bits -> even bit positions of 32 */
+static __device__ __forceinline__ uint32_t spread16(uint32_t x)
+{
+  x &= 0xffffu;
+  x = (x | (x << 8)) & 0x00ff00ffu;
+  x = (x | (x << 4)) & 0x0f0f0f0fu;
+  x = (x | (x << 2)) & 0x33333333u;
+  x = (x | (x << 1)) & 0x55555555u;
+  return x;
+}
+
+/* 32x32 bit transpose across the 32 lanes of a half-wave: lane c ends with bit i = bit c of
+ * lane i's input */
+static __device__ __forceinline__ uint32_t transpose32(uint32_t x, uint32_t lane32)
+{
+  constexpr uint32_t m[5] = {0x0000ffffu, 0x00ff00ffu, 0x0f0f0f0fu, 0x33333333u, 0x55555555u};
+#pragma unroll
+  for (int k = 0; k < 5; k++) {
+    const uint32_t j = 16u >> k;
+    uint32_t p = __shfl_xor(x, j, 32);
+    x = (lane32 & j) ? ((x & ~m[k]) | ((p >> j) & m[k])) : ((x & m[k]) | ((p << j) & ~m[k]));
+  }
+  return x;
 }
 
 /*
- * Word wi of the packed sub-block interleaver output w (lte_rate_matching.c:51-130): bits
- * 32wi..32wi+31.  In the first Kpi entries (v^(0)) a word covers at most two columns (R >= 32
- * or Kpi-aligned words), in the interlaced half 16 rows of at most two columns; each row
- * entry is bit 32*row + colperm(col) - ND of its stream.  NULL entries read as 0 and are
- * skipped by the rate matcher through the NULL list.
+ * Word wi of the packed sub-block interleaver output w (lte_rate_matching.c:51-130) from the
+ * column-major arrays col[s][c] (R bits each: column c of y^(s), y^(2) pre-shifted by one for
+ * the (pi(k)+1) mod Kpi rule).  v^(0) is the concatenation of the permuted columns; the
+ * interlaced half takes 16 rows of v^(1)/v^(2) per word.  NULL entries read as 0 (the rate
+ * matcher skips them through the NULL list).
  */
-static __device__ __forceinline__ uint32_t w_word(const uint32_t *blk, uint32_t sw, uint32_t R, uint32_t Kpi,
-                                                  uint32_t ND, uint32_t wi)
+static __device__ __forceinline__ uint32_t w_word(const uint32_t *col, uint32_t R, uint32_t Kpi, uint32_t wi)
 {
-  uint32_t q = 32 * wi, v = 0;
+  const uint32_t RBW = (R + 31) >> 5, q = 32 * wi;
+  uint32_t v = 0, got = 0;
   if (q < Kpi) {
-    uint32_t col = q / R, row = q - col * R;
-    int b0 = (int)colperm(col) - (int)ND, b1 = (int)colperm(min(col + 1, 31u)) - (int)ND;
-#pragma unroll 8
-    for (uint32_t t = 0; t < 32; t++) {
-      uint32_t rr = row + t;
-      bool c2 = rr >= R;
-      rr = c2 ? rr - R : rr;
-      v |= sbit(blk, 32 * (int)rr + (c2 ? b1 : b0)) << t;
+    uint32_t c = q / R, o = q - c * R;
+    while (got < 32) {
+      uint32_t take = min(32 - got, R - o);
+      v |= (ext32(col + colperm(c) * RBW, o) & lowmask(take)) << got;
+      got += take;
+      c++;
+      o = 0;
     }
   } else {
-    uint32_t e = q - Kpi, col = e / (2 * R), row = (e - col * 2 * R) >> 1;
-    int b0 = (int)colperm(col) - (int)ND, b1 = (int)colperm(min(col + 1, 31u)) - (int)ND;
-    const uint32_t *s1 = blk + sw, *s2 = blk + 2 * sw;
-#pragma unroll 4
-    for (uint32_t t = 0; t < 16; t++) {
-      uint32_t rr = row + t;
-      bool c2 = rr >= R;
-      rr = c2 ? rr - R : rr;
-      int j = 32 * (int)rr + (c2 ? b1 : b0);
-      /* v^(2)_k = y^(2)_{(pi(k)+1) mod Kpi}: the last entry wraps to y^(2)_0 */
-      int j2 = (j + (int)ND + 1 == (int)Kpi) ? -(int)ND : j + 1;
-      v |= (sbit(s1, j) << (2 * t)) | (sbit(s2, j2) << (2 * t + 1));
+    uint32_t e = q - Kpi, c = e / (2 * R), row = (e - c * 2 * R) >> 1;
+    while (got < 16) {
+      uint32_t take = min(16 - got, R - row), cp = colperm(c), mk = lowmask(take);
+      uint32_t a = ext32(col + (32 + cp) * RBW, row) & mk, b = ext32(col + (64 + cp) * RBW, row) & mk;
+      v |= (spread16(a) | (spread16(b) << 1)) << (2 * got);
+      got += take;
+      c++;
+      row = 0;
     }
   }
   return v;
@@ -438,11 +480,11 @@ static __device__ __forceinline__ uint32_t compact_to_pos2(uint32_t ci, const ui
  * circular buffer w[0..Ncb) starting at position p (m NULLs before p).  Inside the buffer a
  * 64-bit window of packed w with the (few) NULL bits squeezed out; across the wrap, bit by bit.
  */
-static __device__ __forceinline__ uint32_t rm_window(const uint32_t *wpk, uint32_t p, uint32_t m, uint32_t Ncb,
+static __device__ __forceinline__ uint32_t rm_window(const uint32_t *wpk, uint32_t &p, uint32_t &m, uint32_t Ncb,
                                                      const uint16_t *np, uint32_t nn, uint32_t need)
 {
   uint32_t out = 0;
-  if (p + 64 <= Ncb) {
+  if (p + 64 <= Ncb && need == 32) {
     uint32_t wi = p >> 5, off = p & 31;
     uint64_t x = ((uint64_t)wpk[wi + 1] << 32) | wpk[wi];
     x >>= off;
@@ -457,6 +499,7 @@ static __device__ __forceinline__ uint32_t rm_window(const uint32_t *wpk, uint32
       m++;
     }
     out = (uint32_t)x;
+    p += 32 + del;
   } else {
     uint32_t got = 0;
     while (got < need) {
@@ -482,16 +525,18 @@ static __device__ void encode_codeword(const cfg_dev_t *__restrict__ c, uint32_t
   const uint32_t tid = threadIdx.x, nth = blockDim.x, wave = tid >> 6, lane = tid & 63, nwaves = nth >> 6;
   const uint32_t sfi = DEBUG ? sf : (c->first_sf + sf * c->sf_step) % 10;
   const uint32_t C = cw.C, sw = cw.stream_words;
-  /* LDS carve-up */
+  /* LDS carve-up.  Region A: TB || CRC and the CRC tables (phases 0-2), then the column-major
+   * y^(s) arrays (phase 4).  Region B: the constituent streams (phases 0-4a), then packed w. */
   uint32_t *tbw = lds_base;
-  uint32_t *strm = tbw + c->lds_tb_words;
-  uint32_t *ebuf = strm + c->lds_stream_words;
-  uint32_t *wb = ebuf + c->lds_gold_words;
-  uint32_t *crctab_a = wb + c->lds_w_words;
+  uint32_t *crctab_a = tbw + c->lds_tb_words;
   uint32_t *crctab_b = crctab_a + 256;
   uint32_t *mul_tb = crctab_b + 256;                     /* [8][6][16] */
   uint32_t *mul_cb = mul_tb + 8 * 96;                    /* [6][6][16] */
-  uint32_t *tails = mul_cb + 6 * 96;
+  uint32_t *colw = lds_base;
+  uint32_t *strm = lds_base + c->lds_a_words;
+  uint32_t *wb = strm;
+  uint32_t *ebuf = strm + c->lds_b_words;
+  uint32_t *tails = ebuf + c->lds_gold_words;
   uint32_t *crcs = tails + 2 * OAI4G_MAX_CB;             /* [0] = CRC24A, [1+r] = CRC24B of block r */
   uint32_t *red = crcs + OAI4G_MAX_CB + 2;               /* 4 per-wave partials */
   enc_tabs_t *tabs = (enc_tabs_t *)(red + 4);
@@ -655,38 +700,79 @@ static __device__ void encode_codeword(const cfg_dev_t *__restrict__ c, uint32_t
   }
   __syncthreads();
 
-  /* ---- phase 4a: packed w of every block ---- */
+  /* ---- phase 4a: y^(s) rows (32 entries each, NULL prefix of ND) transposed into column-major
+   * bit arrays, one 32x32 tile per half-wave ---- */
+  {
+    const uint32_t lane32 = tid & 31, ntask = cw.col_task[C];
+    for (uint32_t t = tid >> 5; t < ntask; t += nth >> 5) {
+      uint32_t r = 0;
+      while (r + 1 < C && t >= cw.col_task[r + 1]) r++;
+      const uint32_t R = cw.R[r], ND = cw.ND[r], RBW = (R + 31) >> 5;
+      const uint32_t tt = t - cw.col_task[r], s = tt / RBW, rb = tt - s * RBW, row = 32 * rb + lane32;
+      const uint32_t *st = strm + (r * 3 + s) * sw;
+      uint32_t y = 0;
+      if (row < R) {
+        y = sx32(st, (int)(32 * row) - (int)ND + (s == 2 ? 1 : 0));
+        if (s == 2 && row == R - 1) {
+          y &= 0x7fffffffu;                       /* j = Kpi-1 reads y^(2)_0: NULL if ND > 0 */
+          if (ND == 0) y |= (st[lsw(0)] & 1u) << 31;
+        }
+      }
+      y = transpose32(y, lane32);
+      colw[cw.col_off[r] + (32 * s + lane32) * RBW + rb] = y;
+    }
+  }
+  __syncthreads();
+
+  /* ---- phase 4b: packed w of every block (streams are dead: w overwrites them) ---- */
   const uint32_t wtot = cw.wpk_off[C];
   for (uint32_t i = tid; i < wtot; i += nth) {
     uint32_t r = 0;
     while (r + 1 < C && i >= cw.wpk_off[r + 1]) r++;
     uint32_t wi = i - cw.wpk_off[r], R = cw.R[r];
-    wb[i] = wi < 3 * R ? w_word(strm + r * 3 * sw, sw, R, cw.Kpi[r], cw.ND[r], wi) : 0u;
+    wb[i] = wi < 3 * R ? w_word(colw + cw.col_off[r], R, cw.Kpi[r], wi) : 0u;
   }
   __syncthreads();
   if (stop_phase <= 4) return;
 
-  /* ---- phase 4b: rate matching of every block, XORed into the Gold words ---- */
+  /* ---- phase 4c: rate matching (lte_rate_matching.c:548-566) of every block, XORed into the
+   * Gold-prefilled staging words; each thread walks a run of consecutive output words ---- */
   const uint32_t *roff = cw.roff[sfi];
   uint32_t nwtot = 0;
   for (uint32_t r = 0; r < C; r++) nwtot += (roff[r + 1] - roff[r] + 31) >> 5;
-  for (uint32_t i = tid; i < nwtot; i += nth) {
+  {
+    const uint32_t per = (nwtot + nth - 1) / nth, i0 = tid * per, i1 = min(i0 + per, nwtot);
     uint32_t r = 0, acc = 0;
-    for (;;) {
-      uint32_t nwo = (roff[r + 1] - roff[r] + 31) >> 5;
-      if (r + 1 == C || i < acc + nwo) break;
-      acc += nwo;
-      r++;
+    if (i0 < i1) {
+      for (;;) {
+        uint32_t nwo = (roff[r + 1] - roff[r] + 31) >> 5;
+        if (r + 1 == C || i0 < acc + nwo) break;
+        acc += nwo;
+        r++;
+      }
     }
-    const uint32_t k = i - acc, E = roff[r + 1] - roff[r];
-    const uint16_t *npl = np + cw.kidx[r] * OAI4G_MAX_NULLS;
-    const uint32_t nn = cw.nnull[cw.kidx[r]];
-    uint32_t need = min(32u, E - 32 * k), m;
-    uint32_t p = compact_to_pos2((cw.k0c[r] + 32 * k) % cw.Nnn[r], npl, nn, m);
-    uint32_t out = rm_window(wb + cw.wpk_off[r], p, m, cw.Ncb[r], npl, nn, need);
-    uint32_t gpos = roff[r] + 32 * k, gw = gpos >> 5, off = gpos & 31;
-    atomicXor(&ebuf[gw], out << off);
-    if (off && (out >> (32 - off))) atomicXor(&ebuf[gw + 1], out >> (32 - off));
+    uint32_t k = i0 - acc, p = 0, m = 0, nwo = 0, nn = 0;
+    const uint16_t *npl = np;
+    bool fresh = true;
+    for (uint32_t i = i0; i < i1; i++, k++) {
+      if (fresh) {
+        nwo = (roff[r + 1] - roff[r] + 31) >> 5;
+        npl = np + cw.kidx[r] * OAI4G_MAX_NULLS;
+        nn = cw.nnull[cw.kidx[r]];
+        p = compact_to_pos2((cw.k0c[r] + 32 * k) % cw.Nnn[r], npl, nn, m);
+        fresh = false;
+      }
+      const uint32_t E = roff[r + 1] - roff[r], need = min(32u, E - 32 * k);
+      uint32_t out = rm_window(wb + cw.wpk_off[r], p, m, cw.Ncb[r], npl, nn, need);
+      uint32_t gpos = roff[r] + 32 * k, gw = gpos >> 5, off = gpos & 31;
+      atomicXor(&ebuf[gw], out << off);
+      if (off && (out >> (32 - off))) atomicXor(&ebuf[gw + 1], out >> (32 - off));
+      if (k + 1 == nwo) {
+        r++;
+        k = (uint32_t)-1;
+        fresh = true;
+      }
+    }
   }
   __syncthreads();
 
@@ -721,8 +807,7 @@ __global__ void __launch_bounds__(256) k_encode_debug(const cfg_dev_t *__restric
 
 static size_t enc_lds_bytes(const cfg_dev_t *h)
 {
-  size_t words = (size_t)h->lds_tb_words + h->lds_stream_words + h->lds_gold_words + h->lds_w_words + 256 + 256 +
-                 8 * 96 + 6 * 96 + 2 * OAI4G_MAX_CB + OAI4G_MAX_CB + 2 + 4;
+  size_t words = (size_t)h->lds_a_words + h->lds_b_words + h->lds_gold_words + 2 * OAI4G_MAX_CB + OAI4G_MAX_CB + 2 + 4;
   size_t bytes = words * 4 + sizeof(enc_tabs_t) + 2 * OAI4G_MAX_NULLS * 2;
   return (bytes + 15) & ~(size_t)15;
 }

@@ -51,7 +51,7 @@ static pthread_once_t g_once = PTHREAD_ONCE_INIT;
 static int g_init_status = -1;
 static char g_init_err[512] = "";
 static uint32_t *g_tw = nullptr, *g_gx1 = nullptr, *g_gx2j = nullptr;
-static uint32_t h_gx1[64], h_gx2j[64 * 32];
+static uint32_t h_gx1[OAI4G_GOLD_LANES], h_gx2j[OAI4G_GOLD_LANES * 32];
 
 static void twiddle_host(int N, int m, int16_t *re, int16_t *im)
 {
@@ -99,12 +99,12 @@ static void do_init(void)
       tw[off + m] = (uint16_t)re | ((uint32_t)(uint16_t)im << 16);
     }
   }
-  /* Gold: x1 after 50+64l steps; x2 step-matrix powers M2^(50+64l) (columns) */
+  /* Gold: x1 after 50+16l steps; x2 step-matrix powers M2^(50+16l) (columns) */
   uint32_t x1 = 1u + (1u << 31), cols[32];
   for (int b = 0; b < 32; b++) cols[b] = 1u << b;
   int steps_done = 0;
-  for (int l = 0; l < 64; l++) {
-    int target = 50 + 64 * l;
+  for (int l = 0; l < OAI4G_GOLD_LANES; l++) {
+    int target = 50 + OAI4G_GOLD_STRIDE * l;
     while (steps_done < target) {
       uint32_t dummy = 0;
       gold_step_h(&x1, &dummy);
@@ -503,7 +503,7 @@ static int derive_cfg(oai4g_tx_config *cfg, const oai4g_tx_params_t *p, const ui
   h.first_sf = p->first_subframe % 10;
   h.sf_step = p->subframe_step;
   h.payload_stride = p->payload_stride;
-  uint32_t max_tb_words = 0, max_stream_words = 0, max_gw = 0, max_bits = 0, max_w = 0, max_inw = 0;
+  uint32_t max_tb_words = 0, max_stream_words = 0, max_gw = 0, max_bits = 0, max_w = 0, max_inw = 0, max_col = 0;
   bool rm_fail = false;
   for (int cw = 0; cw < p->n_cw; cw++) {
     cw_dev_t &c = h.cw[cw];
@@ -580,13 +580,22 @@ static int derive_cfg(oai4g_tx_config *cfg, const oai4g_tx_params_t *p, const ui
     uint32_t inw = 0;
     for (uint32_t r = 0; r < C; r++) inw += (c.K[r] + 31) >> 5;
     max_inw = inw > max_inw ? inw : max_inw;
-    /* packed w of every block (3 Kpi bits = 3R words, + 2 read-ahead words each) */
-    uint32_t wwords = 0;
+    /* packed w of every block (3 Kpi bits = 3R words, + 2 read-ahead words each) and the
+     * column-major y^(s) arrays (3 streams x 32 columns x ceil(R/32) words) */
+    uint32_t wwords = 0, cwords = 0, ntask = 0;
     for (uint32_t r = 0; r < C; r++) {
+      uint32_t RBW = (c.R[r] + 31) / 32;
       c.wpk_off[r] = wwords;
+      c.col_off[r] = cwords;
+      c.col_task[r] = ntask;
       wwords += 3 * c.R[r] + 2;
+      cwords += 96 * RBW;
+      ntask += 3 * RBW;
     }
     c.wpk_off[C] = wwords;
+    c.col_off[C] = cwords;
+    c.col_task[C] = ntask;
+    max_col = cwords + 1 > max_col ? cwords + 1 : max_col;
     max_w = wwords > max_w ? wwords : max_w;
     uint32_t tbw = (c.A_bytes + 3 + 3) / 4 + 1;
     max_tb_words = tbw > max_tb_words ? tbw : max_tb_words;
@@ -615,8 +624,11 @@ static int derive_cfg(oai4g_tx_config *cfg, const oai4g_tx_params_t *p, const ui
   h.lds_stream_words = max_stream_words;
   h.lds_gold_words = max_gw + 1;
   h.lds_w_words = max_w;
-  h.lds_inw_words = max_inw;
-  h.lds_items = 2 * max_inw;
+  (void)max_inw;
+  h.lds_col_words = max_col;
+  /* encoder LDS regions with phase-disjoint lifetimes (see oai4g_encode.hip) */
+  h.lds_a_words = max_tb_words + OAI4G_ENC_CRC_TABLE_WORDS > max_col ? max_tb_words + OAI4G_ENC_CRC_TABLE_WORDS : max_col;
+  h.lds_b_words = max_stream_words > max_w ? max_stream_words : max_w;
   /* RE maps */
   if (need_remap) {
     uint32_t N = h.N;

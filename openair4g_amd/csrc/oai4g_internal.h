@@ -15,7 +15,10 @@
 
 #define OAI4G_MAX_CB 16
 #define OAI4G_MAX_NULLS 104
-#define OAI4G_MAX_GOLD_WORDS 4096          /* 64 lanes x 64 words: >= (14*1200*6)/32 */
+#define OAI4G_ENC_CRC_TABLE_WORDS (256 + 256 + 8 * 96 + 6 * 96) /* byte tables A/B + tree multipliers */
+#define OAI4G_GOLD_LANES 256
+#define OAI4G_GOLD_STRIDE 16
+#define OAI4G_MAX_GOLD_WORDS (OAI4G_GOLD_LANES * OAI4G_GOLD_STRIDE) /* >= (14*1200*6)/32 */
 #define OAI4G_TW_TOTAL (16 + 64 + 128 + 256 + 512 + 1024 + 2048)
 
 /* twiddle table offsets (packed int16 pairs), indexed by log2 of the level size */
@@ -53,6 +56,8 @@ struct cw_dev_t {
   uint32_t k0c[OAI4G_MAX_CB];   /* non-NULL entries of w[0..k0): compacted start */
   uint32_t kidx[OAI4G_MAX_CB];  /* which null list (0: Kminus, 1: Kplus) */
   uint32_t wpk_off[OAI4G_MAX_CB + 1]; /* LDS word offset of block r's packed w (3R words + 2 pad) */
+  uint32_t col_off[OAI4G_MAX_CB + 1]; /* LDS word offset of block r's column arrays (96 x RBW words) */
+  uint32_t col_task[OAI4G_MAX_CB + 1];/* prefix sum of transpose tasks (3 x RBW per block) */
   uint32_t nnull[2];
   uint16_t nullpos[2][OAI4G_MAX_NULLS]; /* sorted NULL positions of w for K = Kminus / Kplus */
   /* per subframe index */
@@ -77,15 +82,16 @@ struct cfg_dev_t {
   uint32_t lds_tb_words;        /* LDS words for TB || CRC */
   uint32_t lds_stream_words;    /* LDS words for all block streams of one codeword */
   uint32_t lds_gold_words;      /* = e-bit staging words (Gold-prefilled) */
-  uint32_t lds_w_words;         /* packed sub-block interleaver output of one block */
-  uint32_t lds_inw_words;       /* interleaved-input words of all blocks */
-  uint32_t lds_items;           /* encoder chunk items (2 per 32-bit chunk per block) */
-  uint32_t pad[2];
+  uint32_t lds_w_words;         /* packed sub-block interleaver output of every block */
+  uint32_t lds_col_words;       /* column-major y^(s) arrays of every block (+1 read-ahead) */
+  uint32_t lds_a_words;         /* region A: TB + CRC tables (phases 0-2) | columns (phase 4) */
+  uint32_t lds_b_words;         /* region B: streams (phases 0-4a) | packed w (4b-4c) */
+  uint32_t pad[1];
   cw_dev_t cw[2];
   uint32_t symbase[10][14];     /* data REs before symbol l */
   const uint16_t *remap;        /* [10][14][N] data-RE index | parity<<15, 0xFFFF = none */
-  const uint32_t *gold_x1;      /* [64]      x1 state after 50+64l word steps */
-  const uint32_t *gold_x2j;     /* [64][32]  columns of M2^(50+64l) */
+  const uint32_t *gold_x1;      /* [256]     x1 state after 50+16l word steps */
+  const uint32_t *gold_x2j;     /* [256][32] columns of M2^(50+16l) */
   const uint32_t *tw;           /* OAI4G_TW_TOTAL packed twiddles */
 };
 
