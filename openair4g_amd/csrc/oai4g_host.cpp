@@ -51,6 +51,7 @@ static pthread_once_t g_once = PTHREAD_ONCE_INIT;
 static int g_init_status = -1;
 static char g_init_err[512] = "";
 static uint32_t *g_tw = nullptr, *g_gx1 = nullptr, *g_gx2j = nullptr;
+static int g_n_cu = 256;
 static uint32_t h_gx1[OAI4G_GOLD_LANES], h_gx2j[OAI4G_GOLD_LANES * 32];
 
 static void twiddle_host(int N, int m, int16_t *re, int16_t *im)
@@ -87,6 +88,7 @@ static void do_init(void)
     g_init_status = -2;
     return;
   }
+  g_n_cu = prop.multiProcessorCount > 0 ? prop.multiProcessorCount : 256;
   /* twiddles */
   std::vector<uint32_t> tw(OAI4G_TW_TOTAL);
   const int sizes[] = {4, 6, 7, 8, 9, 10, 11};
@@ -639,6 +641,10 @@ static int derive_cfg(oai4g_tx_config *cfg, const oai4g_tx_params_t *p, const ui
                           h.symbase[sf]);
       if (n < 0) { set_err("RE map construction failed"); return -1; }
       cfg->re_count[sf] = n;
+      for (int l = 0; l < 14; l++) {
+        uint32_t next = l + 1 < (int)h.nsymb ? h.symbase[sf][l + 1] : (uint32_t)n;
+        h.symnre[sf][l] = (uint16_t)(l < p->num_pdcch_symbols || l >= (int)h.nsymb ? 0 : next - h.symbase[sf][l]);
+      }
       for (int cw = 0; cw < p->n_cw; cw++) {
         uint32_t bits = (uint32_t)n * h.cw[cw].Qm;
         max_bits = bits > max_bits ? bits : max_bits;
@@ -656,6 +662,7 @@ static int upload_cfg(oai4g_tx_config *cfg)
     HCK(hipMemcpy(cfg->d_remap, cfg->h_remap.data(), cfg->h_remap.size() * 2, hipMemcpyHostToDevice), -1);
   }
   cfg->h.remap = cfg->d_remap;
+  cfg->h.n_cu = (uint32_t)g_n_cu;
   cfg->h.gold_x1 = g_gx1;
   cfg->h.gold_x2j = g_gx2j;
   cfg->h.tw = g_tw;

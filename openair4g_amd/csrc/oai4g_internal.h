@@ -89,6 +89,8 @@ struct cfg_dev_t {
   uint32_t pad[1];
   cw_dev_t cw[2];
   uint32_t symbase[10][14];     /* data REs before symbol l */
+  uint16_t symnre[10][14];      /* data REs in symbol l */
+  uint32_t n_cu;                /* compute units of the device (persistent grids) */
   const uint16_t *remap;        /* [10][14][N] data-RE index | parity<<15, 0xFFFF = none */
   const uint32_t *gold_x1;      /* [256]     x1 state after 50+16l word steps */
   const uint32_t *gold_x2j;     /* [256][32] columns of M2^(50+16l) */

@@ -7,17 +7,26 @@
  *   - QAM mapping + RE mapping + TM1/TM3 precoding (dlsch_modulation.c:139-1493) fused in
  *     front of the IDFT so the frequency grid never round-trips through HBM.
  *
- * IDFT organisation.  An N-point transform is owned by a "unit" of N/16 threads.  Thread t
- * owns the radix-16 leaf that consumes inputs x[t + (N/16) n], n = 0..15 (the digit-reversed
- * DIT leaves of the reference's recursive even/odd and mod-4 splits).  The leaf IDFT16 runs
- * in registers; each higher level (64: radix-4 with saturating Q15 products; 256/1024:
- * radix-4 with 32-bit accumulation; 128/2048: radix-2) exchanges operands through LDS,
- * stored group-major (pos = group*S + q) with one pad word per 32 to spread LDS banks.
- * The last level writes straight to global memory, producing the CP in the same pass.
+ * IDFT organisation.  An N-point transform is owned by a "unit" of T = N/16 threads.  Thread t
+ * owns the radix-16 leaf that consumes inputs x[t + T n], n = 0..15 (the digit-reversed DIT
+ * leaves of the reference's recursive even/odd and mod-4 splits).  The leaf IDFT16 runs in
+ * registers; each higher level (64: radix-4 with saturating Q15 products; 256/1024: radix-4
+ * with 32-bit accumulation; 128/2048: radix-2) exchanges operands through LDS, stored
+ * group-major (pos = group*S + q) with one pad word per 32 to spread LDS banks.  The last level
+ * writes straight to global memory, producing the CP in the same pass.
+ *
+ * The arithmetic is VALU-issue bound, so every step is shaped for instruction count:
+ * complex products are two v_dot2_i32_i16 (the reference's madd_epi16), the >>15 + packs_epi32
+ * pair is two shifts + one saturating v_cvt_pk_i16_i32, radix adds are packed saturating
+ * v_pk_add/sub_i16, and the twiddles a thread needs (a thread's twiddle indices are fixed per
+ * level) live in registers for the lifetime of a persistent workgroup.  In the fused kernel a
+ * unit transforms every antenna of one (subframe, symbol), so QAM mapping and the e-bit reads
+ * are shared between antennas.
  */
 #include "oai4g_internal.h"
 
 typedef short s16x2 __attribute__((ext_vector_type(2)));
+typedef const __attribute__((address_space(1))) uint32_t gu32_t;
 
 static __device__ __forceinline__ s16x2 u2c(uint32_t v) { return __builtin_bit_cast(s16x2, v); }
 static __device__ __forceinline__ uint32_t c2u(s16x2 v) { return __builtin_bit_cast(uint32_t, v); }
@@ -26,22 +35,35 @@ static __device__ __forceinline__ s16x2 csubs(s16x2 a, s16x2 b) { return __built
 static __device__ __forceinline__ s16x2 caddw(s16x2 a, s16x2 b) { return a + b; }
 /* sign_epi16(x,{-1,1}) + pair swap: -j*x with a wrapping negate (lte_dfts.c:1463-1466) */
 static __device__ __forceinline__ s16x2 cflip(s16x2 a) { return (s16x2){a.y, (short)(-(int)a.x)}; }
-static __device__ __forceinline__ int dot2(s16x2 a, s16x2 b) { return (int)a.x * (int)b.x + (int)a.y * (int)b.y; }
+static __device__ __forceinline__ int dot2(s16x2 a, s16x2 b) { return __builtin_amdgcn_sdot2(a, b, 0, false); }
 static __device__ __forceinline__ int wadd(int a, int b) { return (int)((unsigned)a + (unsigned)b); }
 static __device__ __forceinline__ int wsub(int a, int b) { return (int)((unsigned)a - (unsigned)b); }
-static __device__ __forceinline__ short sat16(int v) { return (short)min(max(v, -32768), 32767); }
 /* cpack: srai 15 + packs_epi32 (lte_dfts.c:123-131) */
-static __device__ __forceinline__ s16x2 cpack32(int re, int im) { return (s16x2){sat16(re >> 15), sat16(im >> 15)}; }
-/* x * conj(t), 32-bit (cmultc, lte_dfts.c:132-141) */
-static __device__ __forceinline__ void cmulc32(s16x2 x, s16x2 t, int &re, int &im)
+static __device__ __forceinline__ s16x2 cpack32(int re, int im)
 {
-  re = dot2(x, t);
-  im = dot2(x, (s16x2){(short)(-(int)t.y), t.x});
+  return __builtin_bit_cast(s16x2, __builtin_amdgcn_cvt_pk_i16(re >> 15, im >> 15));
 }
-static __device__ __forceinline__ s16x2 cmulc16(s16x2 x, s16x2 t)
+
+/* a twiddle t and its rotated companion (-t.im, t.re) for the imaginary half of x*conj(t) */
+struct twp_t {
+  s16x2 t, tn;
+};
+static __device__ __forceinline__ twp_t mk_tw(uint32_t v)
+{
+  s16x2 t = u2c(v);
+  return {t, (s16x2){(short)(-(int)t.y), t.x}};
+}
+
+/* x * conj(t), 32-bit (cmultc, lte_dfts.c:132-141) */
+static __device__ __forceinline__ void cmulc32(s16x2 x, const twp_t &w, int &re, int &im)
+{
+  re = dot2(x, w.t);
+  im = dot2(x, w.tn);
+}
+static __device__ __forceinline__ s16x2 cmulc16(s16x2 x, const twp_t &w)
 {
   int re, im;
-  cmulc32(x, t, re, im);
+  cmulc32(x, w, re, im);
   return cpack32(re, im);
 }
 
@@ -58,8 +80,9 @@ static __device__ __forceinline__ void r4inv(s16x2 p0, s16x2 p1, s16x2 p2, s16x2
 }
 
 /* ibfly4 (lte_dfts.c:795-819): 32-bit products, one cpack per output, wrapping add of x0 */
-static __device__ __forceinline__ void ibfly4(s16x2 x0, s16x2 x1, s16x2 x2, s16x2 x3, s16x2 t1, s16x2 t2,
-                                              s16x2 t3, s16x2 &y0, s16x2 &y1, s16x2 &y2, s16x2 &y3)
+static __device__ __forceinline__ void ibfly4(s16x2 x0, s16x2 x1, s16x2 x2, s16x2 x3, const twp_t &t1,
+                                              const twp_t &t2, const twp_t &t3, s16x2 &y0, s16x2 &y1, s16x2 &y2,
+                                              s16x2 &y3)
 {
   int a1r, a1i, a2r, a2i, a3r, a3i;
   cmulc32(x1, t1, a1r, a1i);
@@ -71,10 +94,10 @@ static __device__ __forceinline__ void ibfly4(s16x2 x0, s16x2 x1, s16x2 x2, s16x
   y1 = caddw(x0, cpack32(wsub(wsub(a3i, a2r), a1i), wsub(a1r, wadd(a2i, a3r))));
 }
 
-/* ibfly2 (lte_dfts.c:502-527) */
-static __device__ __forceinline__ void ibfly2(s16x2 x0, s16x2 x1, s16x2 t, s16x2 &y0, s16x2 &y1)
+/* ibfly2 (lte_dfts.c:502-527): x0 * 32767 via the same madd as the twiddled operand */
+static __device__ __forceinline__ void ibfly2(s16x2 x0, s16x2 x1, const twp_t &t, s16x2 &y0, s16x2 &y1)
 {
-  int a0r = (int)x0.x * 32767, a0i = (int)x0.y * 32767, a1r, a1i;
+  int a0r = dot2(x0, (s16x2){32767, 0}), a0i = dot2(x0, (s16x2){0, 32767}), a1r, a1i;
   cmulc32(x1, t, a1r, a1i);
   y0 = cpack32(wadd(a0r, a1r), wadd(a0i, a1i));
   y1 = cpack32(wsub(a0r, a1r), wsub(a0i, a1i));
@@ -82,97 +105,167 @@ static __device__ __forceinline__ void ibfly2(s16x2 x0, s16x2 x1, s16x2 t, s16x2
 
 static __device__ __forceinline__ s16x2 shr3(s16x2 a) { return (s16x2){(short)(a.x >> 3), (short)(a.y >> 3)}; }
 static __device__ __forceinline__ s16x2 shr1(s16x2 a) { return (s16x2){(short)(a.x >> 1), (short)(a.y >> 1)}; }
-/* mulhi_int16(a, 23170) = slli(mulhi_epi16(a, 23170), 1) (lte_dfts.c:1755) */
-static __device__ __forceinline__ short mulhi1(short v) { return (short)((((int)v * 23170) >> 16) << 1); }
-static __device__ __forceinline__ s16x2 mulhi2(s16x2 a) { return (s16x2){mulhi1(a.x), mulhi1(a.y)}; }
+/* mulhi_int16(a, 23170) = slli(mulhi_epi16(a, 23170), 1) (lte_dfts.c:1755); |result| <= 23170 */
+static __device__ __forceinline__ s16x2 mulhi2(s16x2 a)
+{
+  int pr = dot2(a, (s16x2){23170, 0}), pi = dot2(a, (s16x2){0, 23170});
+  return (s16x2){(short)((pr >> 16) << 1), (short)((pi >> 16) << 1)};
+}
 
 static __device__ __forceinline__ uint32_t lphys(uint32_t pos) { return pos + (pos >> 5); }
 
+/* ---------------------------------------------------------------------------------------
+ * Per-thread twiddle registers.  At a level with quarter size SC a thread's butterfly j
+ * (operand b = t + T j) uses index q = b mod SC; only D = min(J, SC/T) of them are distinct.
+ * ------------------------------------------------------------------------------------- */
+__host__ __device__ constexpr int tw_distinct(int T, int SC, int J) { return T >= SC ? 1 : (SC / T < J ? SC / T : J); }
+
+template <int LOG2N>
+struct idft_tw_t {
+  static constexpr int N = 1 << LOG2N, T = N >> 4;
+  static constexpr bool HAS256 = LOG2N == 8 || LOG2N >= 10, HAS1024 = LOG2N >= 10, HASR2 = LOG2N == 7 || LOG2N == 11;
+  static constexpr int D64 = tw_distinct(T, 16, 4), D256 = tw_distinct(T, 64, 4), D1024 = tw_distinct(T, 256, 4),
+                       DR2 = tw_distinct(T, N / 2, 8);
+  twp_t l16[7];                         /* W16^{0,1,2,3,4,6,9} */
+  twp_t l64[D64][3];
+  twp_t l256[HAS256 ? D256 : 1][3];
+  twp_t l1024[HAS1024 ? D1024 : 1][3];
+  twp_t r2[HASR2 ? DR2 : 1];
+
+  __device__ __forceinline__ void load(const uint32_t *tw, int t)
+  {
+    gu32_t *g = (gu32_t *)tw;
+    constexpr int i16[7] = {0, 1, 2, 3, 4, 6, 9};
+#pragma unroll
+    for (int i = 0; i < 7; i++) l16[i] = mk_tw(g[oai4g_tw_offset(4) + i16[i]]);
+#pragma unroll
+    for (int j = 0; j < D64; j++) {
+      int q = (t + T * j) & 15;
+#pragma unroll
+      for (int r = 0; r < 3; r++) l64[j][r] = mk_tw(g[oai4g_tw_offset(6) + (r + 1) * q]);
+    }
+    if constexpr (HAS256) {
+#pragma unroll
+      for (int j = 0; j < D256; j++) {
+        int q = (t + T * j) & 63;
+#pragma unroll
+        for (int r = 0; r < 3; r++) l256[j][r] = mk_tw(g[oai4g_tw_offset(8) + (r + 1) * q]);
+      }
+    }
+    if constexpr (HAS1024) {
+#pragma unroll
+      for (int j = 0; j < D1024; j++) {
+        int q = (t + T * j) & 255;
+#pragma unroll
+        for (int r = 0; r < 3; r++) l1024[j][r] = mk_tw(g[oai4g_tw_offset(10) + (r + 1) * q]);
+      }
+    }
+    if constexpr (HASR2) {
+#pragma unroll
+      for (int j = 0; j < DR2; j++) r2[j] = mk_tw(g[oai4g_tw_offset(LOG2N) + ((t + T * j) & (N / 2 - 1))]);
+    }
+  }
+};
+
 /* leaf IDFT16 in registers (lte_dfts.c:1597-1724) */
-static __device__ __forceinline__ void idft16_reg(s16x2 *x, const uint32_t *__restrict__ tw16)
+static __device__ __forceinline__ void idft16_reg(s16x2 *x, const twp_t *w16 /* W^{0,1,2,3,4,6,9} */)
 {
+  constexpr int k1[4] = {0, 1, 2, 3}, k2[4] = {0, 2, 4, 5}, k3[4] = {0, 3, 5, 6}; /* slots of k, 2k, 3k */
   s16x2 S[4][4];
 #pragma unroll
   for (int j = 0; j < 4; j++) r4inv(x[j], x[4 + j], x[8 + j], x[12 + j], S[0][j], S[1][j], S[2][j], S[3][j]);
 #pragma unroll
   for (int k = 0; k < 4; k++) {
-    s16x2 b1 = cmulc16(S[k][1], u2c(tw16[k]));
-    s16x2 b2 = cmulc16(S[k][2], u2c(tw16[2 * k]));
-    s16x2 b3 = cmulc16(S[k][3], u2c(tw16[3 * k]));
+    s16x2 b1 = cmulc16(S[k][1], w16[k1[k]]);
+    s16x2 b2 = cmulc16(S[k][2], w16[k2[k]]);
+    s16x2 b3 = cmulc16(S[k][3], w16[k3[k]]);
     r4inv(S[k][0], b1, b2, b3, x[k], x[4 + k], x[8 + k], x[12 + k]);
   }
 }
 
 /*
- * One intermediate combining level of size S = 2^LOG2S over an N = 2^LOG2N transform held in
- * LDS (group-major).  KIND: 0 = ibfly4_16 (64-level) then >>3, 1 = ibfly4 then >>1.
- * Reads all operands, barrier, writes all results, barrier.
+ * One intermediate combining level of size S = 2^LOG2S over NA transforms of N = 2^LOG2N held
+ * in LDS (group-major, NA buffers of LDSW words).  KIND: 0 = ibfly4_16 (64-level) then >>3,
+ * 1 = ibfly4 then >>1.  Reads all operands, barrier, writes all results, barrier.
  */
-template <int LOG2N, int LOG2S, int KIND>
-static __device__ __forceinline__ void idft_level_lds(uint32_t *lds, int t, const uint32_t *__restrict__ twS)
+template <int LOG2N, int LOG2S, int KIND, int NA, int D>
+static __device__ __forceinline__ void idft_level_lds(uint32_t *lds, int t, const twp_t (&tw)[D][3])
 {
-  constexpr int N = 1 << LOG2N, T = N >> 4, S = 1 << LOG2S, SC = S >> 2, GOUT = N / S;
-  s16x2 v[4][4];
-  int qq[4], gg[4];
+  constexpr int N = 1 << LOG2N, T = N >> 4, S = 1 << LOG2S, SC = S >> 2, GOUT = N / S, LDSW = N + (N >> 5);
+  s16x2 v[NA][4][4];
 #pragma unroll
   for (int j = 0; j < 4; j++) {
-    int b = t + T * j;
-    int q = b & (SC - 1), g = b / SC;
-    qq[j] = q;
-    gg[j] = g;
+    const int b = t + T * j, q = b & (SC - 1), g = b >> (LOG2S - 2);
 #pragma unroll
-    for (int r = 0; r < 4; r++) v[j][r] = u2c(lds[lphys((uint32_t)((g + GOUT * r) * SC + q))]);
+    for (int a = 0; a < NA; a++)
+#pragma unroll
+      for (int r = 0; r < 4; r++) v[a][j][r] = u2c(lds[a * LDSW + lphys((uint32_t)((g + GOUT * r) * SC + q))]);
   }
   __syncthreads();
 #pragma unroll
   for (int j = 0; j < 4; j++) {
-    int q = qq[j], g = gg[j];
-    s16x2 t1 = u2c(twS[q]), t2 = u2c(twS[2 * q]), t3 = u2c(twS[3 * q]);
-    s16x2 y0, y1, y2, y3;
-    if (KIND == 0) {
-      r4inv(v[j][0], cmulc16(v[j][1], t1), cmulc16(v[j][2], t2), cmulc16(v[j][3], t3), y0, y1, y2, y3);
-      y0 = shr3(y0); y1 = shr3(y1); y2 = shr3(y2); y3 = shr3(y3);
-    } else {
-      ibfly4(v[j][0], v[j][1], v[j][2], v[j][3], t1, t2, t3, y0, y1, y2, y3);
-      y0 = shr1(y0); y1 = shr1(y1); y2 = shr1(y2); y3 = shr1(y3);
+    const int b = t + T * j, q = b & (SC - 1), g = b >> (LOG2S - 2);
+    const twp_t *w = tw[j % D];
+    const uint32_t base = (uint32_t)(g * S + q);
+#pragma unroll
+    for (int a = 0; a < NA; a++) {
+      s16x2 y0, y1, y2, y3;
+      if (KIND == 0) {
+        r4inv(v[a][j][0], cmulc16(v[a][j][1], w[0]), cmulc16(v[a][j][2], w[1]), cmulc16(v[a][j][3], w[2]), y0, y1,
+              y2, y3);
+        y0 = shr3(y0); y1 = shr3(y1); y2 = shr3(y2); y3 = shr3(y3);
+      } else {
+        ibfly4(v[a][j][0], v[a][j][1], v[a][j][2], v[a][j][3], w[0], w[1], w[2], y0, y1, y2, y3);
+        y0 = shr1(y0); y1 = shr1(y1); y2 = shr1(y2); y3 = shr1(y3);
+      }
+      uint32_t *la = lds + a * LDSW;
+      la[lphys(base)] = c2u(y0);
+      la[lphys(base + SC)] = c2u(y1);
+      la[lphys(base + 2 * SC)] = c2u(y2);
+      la[lphys(base + 3 * SC)] = c2u(y3);
     }
-    uint32_t base = (uint32_t)(g * S + q);
-    lds[lphys(base)] = c2u(y0);
-    lds[lphys(base + SC)] = c2u(y1);
-    lds[lphys(base + 2 * SC)] = c2u(y2);
-    lds[lphys(base + 3 * SC)] = c2u(y3);
   }
   __syncthreads();
 }
 
 /*
- * Full unit IDFT.  `prod(n)` returns x[t + T n]; `cons(f, y)` stores output sample f.
- * Every thread of the workgroup must call this (it contains barriers), active or not.
+ * NA transforms by one unit.  `prod(n, x)` fills x[a] = input a at t + T n; `cons(a, f, y)`
+ * stores output sample f of transform a.  Every thread of the workgroup must call this (it
+ * contains barriers), active or not.
  */
-template <int LOG2N, class Prod, class Cons>
-static __device__ __forceinline__ void idft_unit(uint32_t *lds, int t, bool active, Prod prod, Cons cons,
-                                                 const uint32_t *__restrict__ tw, int scale)
+template <int LOG2N, int NA, class Prod, class Cons>
+static __device__ __forceinline__ void idft_unit(uint32_t *lds, int t, bool active, const idft_tw_t<LOG2N> &tw,
+                                                 Prod prod, Cons cons, int scale)
 {
-  constexpr int N = 1 << LOG2N, T = N >> 4;
-  s16x2 x[16];
+  constexpr int N = 1 << LOG2N, T = N >> 4, LDSW = N + (N >> 5);
   if (active) {
+    s16x2 x[NA][16];
 #pragma unroll
-    for (int n = 0; n < 16; n++) x[n] = prod(n);
-    idft16_reg(x, tw + oai4g_tw_offset(4));
+    for (int n = 0; n < 16; n++) {
+      s16x2 xn[NA];
+      prod(n, xn);
 #pragma unroll
-    for (int k = 0; k < 16; k++) lds[lphys((uint32_t)(t * 16 + k))] = c2u(x[k]);
+      for (int a = 0; a < NA; a++) x[a][n] = xn[a];
+    }
+#pragma unroll
+    for (int a = 0; a < NA; a++) {
+      idft16_reg(x[a], tw.l16);
+#pragma unroll
+      for (int k = 0; k < 16; k++) lds[a * LDSW + lphys((uint32_t)(t * 16 + k))] = c2u(x[a][k]);
+    }
   }
   __syncthreads();
   if constexpr (LOG2N == 6) {
     /* top-level idft64: ibfly4_16 straight to output, >>3 if scale */
-    const uint32_t *tw64 = tw + oai4g_tw_offset(6);
-    s16x2 v[4][4];
+    s16x2 v[NA][4][4];
     if (active) {
 #pragma unroll
       for (int j = 0; j < 4; j++) {
         int q = t + T * j;
 #pragma unroll
-        for (int r = 0; r < 4; r++) v[j][r] = u2c(lds[lphys((uint32_t)(r * 16 + q))]);
+        for (int a = 0; a < NA; a++)
+#pragma unroll
+          for (int r = 0; r < 4; r++) v[a][j][r] = u2c(lds[a * LDSW + lphys((uint32_t)(r * 16 + q))]);
       }
     }
     __syncthreads();
@@ -180,46 +273,56 @@ static __device__ __forceinline__ void idft_unit(uint32_t *lds, int t, bool acti
 #pragma unroll
       for (int j = 0; j < 4; j++) {
         int q = t + T * j;
-        s16x2 y[4];
-        r4inv(v[j][0], cmulc16(v[j][1], u2c(tw64[q])), cmulc16(v[j][2], u2c(tw64[2 * q])),
-              cmulc16(v[j][3], u2c(tw64[3 * q])), y[0], y[1], y[2], y[3]);
+        const twp_t *w = tw.l64[j % idft_tw_t<6>::D64];
 #pragma unroll
-        for (int m = 0; m < 4; m++) cons(q + 16 * m, scale ? shr3(y[m]) : y[m]);
+        for (int a = 0; a < NA; a++) {
+          s16x2 y[4];
+          r4inv(v[a][j][0], cmulc16(v[a][j][1], w[0]), cmulc16(v[a][j][2], w[1]), cmulc16(v[a][j][3], w[2]), y[0],
+                y[1], y[2], y[3]);
+#pragma unroll
+          for (int m = 0; m < 4; m++) cons(a, q + 16 * m, scale ? shr3(y[m]) : y[m]);
+        }
       }
     }
   } else {
-    idft_level_lds<LOG2N, 6, 0>(lds, t, tw + oai4g_tw_offset(6));
-    if constexpr (LOG2N >= 10) idft_level_lds<LOG2N, 8, 1>(lds, t, tw + oai4g_tw_offset(8));
-    if constexpr (LOG2N == 11) idft_level_lds<LOG2N, 10, 1>(lds, t, tw + oai4g_tw_offset(10));
+    idft_level_lds<LOG2N, 6, 0, NA>(lds, t, tw.l64);
+    if constexpr (LOG2N >= 10) idft_level_lds<LOG2N, 8, 1, NA>(lds, t, tw.l256);
+    if constexpr (LOG2N == 11) idft_level_lds<LOG2N, 10, 1, NA>(lds, t, tw.l1024);
     if constexpr (LOG2N == 7 || LOG2N == 11) {
       /* final radix-2 level (idft128 / idft2048): ibfly2 then mulhi scaling */
-      constexpr int SC = N >> 1;
-      const uint32_t *twN = tw + oai4g_tw_offset(LOG2N);
+      constexpr int SC = N >> 1, DR2 = idft_tw_t<LOG2N>::DR2;
       if (active) {
 #pragma unroll
         for (int j = 0; j < 8; j++) {
           int q = t + T * j;
-          s16x2 y0, y1;
-          ibfly2(u2c(lds[lphys((uint32_t)q)]), u2c(lds[lphys((uint32_t)(SC + q))]), u2c(twN[q]), y0, y1);
-          if (scale) { y0 = mulhi2(y0); y1 = mulhi2(y1); }
-          cons(q, y0);
-          cons(q + SC, y1);
+#pragma unroll
+          for (int a = 0; a < NA; a++) {
+            s16x2 y0, y1;
+            ibfly2(u2c(lds[a * LDSW + lphys((uint32_t)q)]), u2c(lds[a * LDSW + lphys((uint32_t)(SC + q))]),
+                   tw.r2[j % DR2], y0, y1);
+            if (scale) { y0 = mulhi2(y0); y1 = mulhi2(y1); }
+            cons(a, q, y0);
+            cons(a, q + SC, y1);
+          }
         }
       }
     } else {
       /* final radix-4 level (idft256 / idft1024): ibfly4 then >>1 */
       constexpr int SC = N >> 2;
-      const uint32_t *twN = tw + oai4g_tw_offset(LOG2N);
       if (active) {
 #pragma unroll
         for (int j = 0; j < 4; j++) {
           int q = t + T * j;
-          s16x2 y[4];
-          ibfly4(u2c(lds[lphys((uint32_t)q)]), u2c(lds[lphys((uint32_t)(SC + q))]),
-                 u2c(lds[lphys((uint32_t)(2 * SC + q))]), u2c(lds[lphys((uint32_t)(3 * SC + q))]), u2c(twN[q]),
-                 u2c(twN[2 * q]), u2c(twN[3 * q]), y[0], y[1], y[2], y[3]);
+          const twp_t *w = (LOG2N == 8) ? tw.l256[j % idft_tw_t<LOG2N>::D256] : tw.l1024[j % idft_tw_t<LOG2N>::D1024];
 #pragma unroll
-          for (int m = 0; m < 4; m++) cons(q + SC * m, scale ? shr1(y[m]) : y[m]);
+          for (int a = 0; a < NA; a++) {
+            s16x2 y[4];
+            ibfly4(u2c(lds[a * LDSW + lphys((uint32_t)q)]), u2c(lds[a * LDSW + lphys((uint32_t)(SC + q))]),
+                   u2c(lds[a * LDSW + lphys((uint32_t)(2 * SC + q))]),
+                   u2c(lds[a * LDSW + lphys((uint32_t)(3 * SC + q))]), w[0], w[1], w[2], y[0], y[1], y[2], y[3]);
+#pragma unroll
+            for (int m = 0; m < 4; m++) cons(a, q + SC * m, scale ? shr1(y[m]) : y[m]);
+          }
         }
       }
     }
@@ -228,6 +331,7 @@ static __device__ __forceinline__ void idft_unit(uint32_t *lds, int t, bool acti
 
 /* ======================================================================================
  * Drop-in OFDM modulation: per-symbol IDFT + CP from a frequency grid in global memory.
+ * 128-thread workgroups, 128/T units each.
  * ==================================================================================== */
 struct ofdm_args_t {
   int nsym;
@@ -236,25 +340,27 @@ struct ofdm_args_t {
 };
 
 template <int LOG2N>
-__global__ void __launch_bounds__(256) k_ofdm(const int32_t *__restrict__ in, int32_t *__restrict__ out,
+__global__ void __launch_bounds__(128) k_ofdm(const int32_t *__restrict__ in, int32_t *__restrict__ out,
                                               ofdm_args_t a, const uint32_t *__restrict__ tw)
 {
-  constexpr int N = 1 << LOG2N, T = N >> 4, UNITS = 256 / T, LDSW = N + (N >> 5);
+  constexpr int N = 1 << LOG2N, T = N >> 4, UNITS = 128 / T, LDSW = N + (N >> 5);
   __shared__ uint32_t lds_all[UNITS * LDSW];
-  int unit = threadIdx.x / T, t = threadIdx.x % T;
-  int s = blockIdx.x * UNITS + unit;
-  bool active = s < a.nsym;
+  const int unit = threadIdx.x / T, t = threadIdx.x % T;
+  const int s = blockIdx.x * UNITS + unit;
+  const bool active = s < a.nsym;
+  idft_tw_t<LOG2N> twr;
+  twr.load(tw, t);
   ofdm_sym_t d = active ? a.sym[s] : a.sym[0];
   const uint32_t *src = (const uint32_t *)in + d.in_off;
   uint32_t *dst = (uint32_t *)out + d.out_off;
-  int cp = (int)d.cp;
-  idft_unit<LOG2N>(
-      lds_all + unit * LDSW, t, active, [&](int n) { return u2c(src[t + T * n]); },
-      [&](int f, s16x2 y) {
+  const int cp = (int)d.cp;
+  idft_unit<LOG2N, 1>(
+      lds_all + unit * LDSW, t, active, twr, [&](int n, s16x2 *x) { x[0] = u2c(src[t + T * n]); },
+      [&](int, int f, s16x2 y) {
         dst[f] = c2u(y);
         if (f >= N - cp) dst[f - N] = c2u(y);
       },
-      tw, a.scale);
+      a.scale);
 }
 
 hipError_t oai4g_launch_ofdm(const int32_t *d_in, int32_t *d_out, int log2n, int nsym, const ofdm_sym_t *syms,
@@ -266,13 +372,14 @@ hipError_t oai4g_launch_ofdm(const int32_t *d_in, int32_t *d_out, int log2n, int
   a.nsym = nsym;
   a.scale = scale;
   for (int i = 0; i < nsym; i++) a.sym[i] = syms[i];
-  int units;
+  const int units = 128 / ((1 << log2n) >> 4);
+  const dim3 grid((nsym + units - 1) / units), blk(128);
   switch (log2n) {
-  case 6: units = 64; hipLaunchKernelGGL(k_ofdm<6>, dim3((nsym + units - 1) / units), dim3(256), 0, s, d_in, d_out, a, d_tw); break;
-  case 7: units = 32; hipLaunchKernelGGL(k_ofdm<7>, dim3((nsym + units - 1) / units), dim3(256), 0, s, d_in, d_out, a, d_tw); break;
-  case 8: units = 16; hipLaunchKernelGGL(k_ofdm<8>, dim3((nsym + units - 1) / units), dim3(256), 0, s, d_in, d_out, a, d_tw); break;
-  case 10: units = 4; hipLaunchKernelGGL(k_ofdm<10>, dim3((nsym + units - 1) / units), dim3(256), 0, s, d_in, d_out, a, d_tw); break;
-  case 11: units = 2; hipLaunchKernelGGL(k_ofdm<11>, dim3((nsym + units - 1) / units), dim3(256), 0, s, d_in, d_out, a, d_tw); break;
+  case 6: hipLaunchKernelGGL(k_ofdm<6>, grid, blk, 0, s, d_in, d_out, a, d_tw); break;
+  case 7: hipLaunchKernelGGL(k_ofdm<7>, grid, blk, 0, s, d_in, d_out, a, d_tw); break;
+  case 8: hipLaunchKernelGGL(k_ofdm<8>, grid, blk, 0, s, d_in, d_out, a, d_tw); break;
+  case 10: hipLaunchKernelGGL(k_ofdm<10>, grid, blk, 0, s, d_in, d_out, a, d_tw); break;
+  case 11: hipLaunchKernelGGL(k_ofdm<11>, grid, blk, 0, s, d_in, d_out, a, d_tw); break;
   default: return hipErrorInvalidValue;
   }
   return hipGetLastError();
@@ -301,14 +408,6 @@ static __device__ __forceinline__ s16x2 qam_map(uint32_t bits, uint32_t Qm, cons
   return (s16x2){tab[ir], tab[ii]};
 }
 
-static __device__ __forceinline__ uint32_t read_bits(const uint32_t *__restrict__ w, uint32_t pos)
-{
-  uint32_t wi = pos >> 5, off = pos & 31;
-  uint32_t lo = w[wi];
-  uint32_t hi = off ? w[wi + 1] : 0u;
-  return off ? ((lo >> off) | (hi << (32 - off))) : lo;
-}
-
 /* TM1 / TM3 (LARGE_CDD) precoding of one RE for antenna `ant` (dlsch_modulation.c:266-312, 733-749) */
 static __device__ __forceinline__ s16x2 precode(const cfg_dev_t *__restrict__ c, uint32_t ant, uint32_t parity,
                                                 s16x2 x0, s16x2 x1)
@@ -319,70 +418,165 @@ static __device__ __forceinline__ s16x2 precode(const cfg_dev_t *__restrict__ c,
   return (s16x2){(short)(sgn * (((int)x0.x - (int)x1.x) >> 1)), (short)(sgn * (((int)x0.y - (int)x1.y) >> 1))};
 }
 
+/* LARGE_CDD on packed lanes: floor((a+b)/2) = (a&b) + ((a^b)>>1), floor((a-b)/2) = ((a^b)>>1) - (~a&b) */
+static __device__ __forceinline__ void cdd_pair(s16x2 x0, s16x2 x1, uint32_t parity, s16x2 &y0, s16x2 &y1)
+{
+  const uint32_t a = c2u(x0), b = c2u(x1);
+  const s16x2 h = u2c(a ^ b) >> (s16x2){1, 1};
+  y0 = u2c(a & b) + h;
+  s16x2 d = h - u2c(~a & b);
+  y1 = parity ? (s16x2){0, 0} - d : d;
+}
+
 /* ======================================================================================
  * Fused: packed scrambled e bits -> QAM -> RE map -> precoding -> IDFT -> CP -> IQ.
- * One unit per (subframe, symbol, antenna).
+ * Persistent 128-thread workgroups; a unit of T threads owns one (subframe, symbol) at a time
+ * and transforms NA antenna signals (NA = 1 also serves TM1 with several antennas: the SISO
+ * precoder writes the same symbol to every antenna, so one transform is stored n_ant times).
  * ==================================================================================== */
 template <int LOG2N>
-__global__ void __launch_bounds__(256) k_modofdm(const cfg_dev_t *__restrict__ c, int n_items,
+struct modofdm_geom {
+  static constexpr int N = 1 << LOG2N, T = N >> 4, UNITS = 128 / T, LDSW = N + (N >> 5);
+  static constexpr int EW = (6 * ((N * 5) / 8)) / 32 + 4;   /* staged e-bit words per codeword */
+};
+
+template <int LOG2N, int NA>
+__global__ void __launch_bounds__(128) k_modofdm(const cfg_dev_t *__restrict__ c, int n_items,
                                                  const uint32_t *__restrict__ ebits, int32_t *__restrict__ iq)
 {
-  constexpr int N = 1 << LOG2N, T = N >> 4, UNITS = 256 / T, LDSW = N + (N >> 5);
-  __shared__ uint32_t lds_all[UNITS * LDSW];
-  int unit = threadIdx.x / T, t = threadIdx.x % T;
-  int item = blockIdx.x * UNITS + unit;
-  bool active = item < n_items;
-  uint32_t n_ant = c->n_ant, nsymb = c->nsymb;
-  uint32_t per_sf = nsymb * n_ant;
-  uint32_t it = active ? (uint32_t)item : 0u;
-  uint32_t sf = it / per_sf, rem = it % per_sf, l = rem / n_ant, ant = rem % n_ant;
-  uint32_t sfi = (c->first_sf + sf * c->sf_step) % 10;
-  const uint16_t *__restrict__ rm = c->remap + ((size_t)sfi * 14 + l) * N;
-  const cw_dev_t &cw0 = c->cw[0];
-  const cw_dev_t &cw1 = c->cw[1];
-  bool pil = pilots_of(l) != 0;
-  const int16_t *tab0 = pil ? cw0.qam_b : cw0.qam_a, *tab1 = pil ? cw1.qam_b : cw1.qam_a;
-  int16_t g0 = pil ? cw0.qpsk_b : cw0.qpsk_a, g1 = pil ? cw1.qpsk_b : cw1.qpsk_a;
-  uint32_t Qm0 = cw0.Qm, Qm1 = cw1.Qm;
-  uint32_t base_re = c->symbase[sfi][l];
-  const uint32_t *__restrict__ e0 = ebits + (size_t)(sf * c->n_cw) * c->ebits_words;
-  const uint32_t *__restrict__ e1 = e0 + c->ebits_words;
-  bool two = c->n_cw > 1;
-  /* output placement: slot = l / 7, symbol-in-slot i (normal CP) */
-  uint32_t slot = l / 7, i = l % 7;
-  uint32_t body = slot * (c->spt >> 1) + (i == 0 ? c->cp0 : (N + c->cp0) + (i - 1) * (N + c->cp) + c->cp);
-  int cp = (int)(i == 0 ? c->cp0 : c->cp);
-  uint32_t *dst = (uint32_t *)iq + ((size_t)sf * n_ant + ant) * c->spt + body;
-  idft_unit<LOG2N>(
-      lds_all + unit * LDSW, t, active,
-      [&](int n) -> s16x2 {
-        uint32_t k = (uint32_t)(t + T * n);
-        uint32_t code = rm[k];
-        if (code == 0xFFFFu) return (s16x2){0, 0};
-        uint32_t idx = (code & 0x7FFFu) + base_re;
-        s16x2 x0 = qam_map(read_bits(e0, idx * Qm0), Qm0, tab0, g0);
-        s16x2 x1 = two ? qam_map(read_bits(e1, idx * Qm1), Qm1, tab1, g1) : (s16x2){0, 0};
-        return precode(c, ant, code >> 15, x0, x1);
-      },
-      [&](int f, s16x2 y) {
-        dst[f] = c2u(y);
-        if (f >= N - cp) dst[f - N] = c2u(y);
-      },
-      c->tw, 1);
+  using G = modofdm_geom<LOG2N>;
+  constexpr int N = G::N, T = G::T, UNITS = G::UNITS, LDSW = G::LDSW, EW = G::EW;
+  __shared__ uint32_t lds_data[UNITS * NA * LDSW];
+  __shared__ uint32_t lds_e[UNITS][2][EW];
+  __shared__ uint32_t qtab[2][2][64];          /* [cw][pilot symbol][Qm bits] -> packed IQ */
+  const int unit = threadIdx.x / T, t = threadIdx.x % T;
+  idft_tw_t<LOG2N> twr;
+  twr.load(c->tw, t);
+  const uint32_t n_ant = c->n_ant, nsymb = c->nsymb, n_cw = c->n_cw;
+  const bool cdd = c->mimo_mode == OAI4G_LARGE_CDD;
+  for (uint32_t i = threadIdx.x; i < 256; i += blockDim.x) {
+    const uint32_t cw = i >> 7, pil = (i >> 6) & 1, bits = i & 63;
+    const cw_dev_t &w = c->cw[cw];
+    qtab[cw][pil][bits] = c2u(qam_map(bits, w.Qm, pil ? w.qam_b : w.qam_a, pil ? w.qpsk_b : w.qpsk_a));
+  }
+  const uint32_t Qm0 = c->cw[0].Qm, Qm1 = c->cw[1].Qm;
+  const uint32_t mask0 = (1u << Qm0) - 1u, mask1 = (1u << Qm1) - 1u;
+  __syncthreads();
+
+  for (int base = blockIdx.x * UNITS; base < n_items; base += gridDim.x * UNITS) {
+    const int item = base + unit;
+    const bool active = item < n_items;
+    const uint32_t it = active ? (uint32_t)item : 0u;
+    const uint32_t sf = it / nsymb, l = it - sf * nsymb;
+    const uint32_t sfi = (c->first_sf + sf * c->sf_step) % 10;
+    const uint32_t nre = active ? c->symnre[sfi][l] : 0u, re0 = c->symbase[sfi][l];
+    const uint32_t pil = pilots_of(l) != 0;
+    /* output placement: slot = l / 7, symbol-in-slot i (normal CP) */
+    const uint32_t slot = l / 7, si = l % 7;
+    const uint32_t body = slot * (c->spt >> 1) + (si == 0 ? c->cp0 : (N + c->cp0) + (si - 1) * (N + c->cp) + c->cp);
+    const int cp = (int)(si == 0 ? c->cp0 : c->cp);
+    uint32_t *dst0 = (uint32_t *)iq + (size_t)sf * n_ant * c->spt + body;
+
+    if (UNITS == 1 && nre == 0) {
+      /* control-region symbol: the transform of an all-zero grid is zero */
+      if (active)
+        for (uint32_t a = 0; a < n_ant; a++) {
+          uint32_t *d = dst0 + (size_t)a * c->spt - cp;   /* CP start of antenna a */
+          for (int f = t; f < N + cp; f += T) d[f] = 0u;
+        }
+      continue;
+    }
+
+    /* stage this symbol's e bits of each codeword (coalesced) */
+    const uint32_t *esf = ebits + (size_t)(sf * n_cw) * c->ebits_words;
+    const uint32_t wlo0 = (re0 * Qm0) >> 5, wlo1 = (re0 * Qm1) >> 5;
+    if (active && nre) {
+      const uint32_t cnt0 = min((uint32_t)EW, (((re0 + nre) * Qm0 + 31) >> 5) - wlo0 + 1);
+      for (uint32_t i = t; i < cnt0; i += T) lds_e[unit][0][i] = esf[wlo0 + i];
+      if (n_cw > 1) {
+        const uint32_t cnt1 = min((uint32_t)EW, (((re0 + nre) * Qm1 + 31) >> 5) - wlo1 + 1);
+        for (uint32_t i = t; i < cnt1; i += T) lds_e[unit][1][i] = esf[c->ebits_words + wlo1 + i];
+      }
+    }
+    __syncthreads();
+
+    const uint16_t *__restrict__ rm = c->remap + ((size_t)sfi * 14 + l) * N;
+    const uint32_t *e0 = lds_e[unit][0], *e1 = lds_e[unit][1];
+    const uint32_t *q0 = qtab[0][pil], *q1 = qtab[1][pil];
+    const uint32_t off0 = 32 * wlo0, off1 = 32 * wlo1;
+    idft_unit<LOG2N, NA>(
+        lds_data + unit * NA * LDSW, t, active, twr,
+        [&](int n, s16x2 *x) {
+          const uint32_t code = rm[t + T * n];
+          s16x2 x0 = {0, 0}, x1 = {0, 0};
+          if (code != 0xFFFFu) {
+            const uint32_t idx = code & 0x7FFFu;
+            const uint32_t p0 = (idx + re0) * Qm0 - off0;
+            x0 = u2c(q0[__builtin_amdgcn_alignbit(e0[(p0 >> 5) + 1], e0[p0 >> 5], p0 & 31) & mask0]);
+            if (n_cw > 1) {
+              const uint32_t p1 = (idx + re0) * Qm1 - off1;
+              x1 = u2c(q1[__builtin_amdgcn_alignbit(e1[(p1 >> 5) + 1], e1[p1 >> 5], p1 & 31) & mask1]);
+            }
+          }
+          if constexpr (NA == 2) {
+            cdd_pair(x0, x1, code >> 15 & 1u, x[0], x[1]);
+          } else {
+            x[0] = cdd ? (s16x2){(short)(((int)x0.x + (int)x1.x) >> 1), (short)(((int)x0.y + (int)x1.y) >> 1)} : x0;
+          }
+        },
+        [&](int a, int f, s16x2 y) {
+          if constexpr (NA == 2) {
+            uint32_t *d = dst0 + a * c->spt;
+            d[f] = c2u(y);
+            if (f >= N - cp) d[f - N] = c2u(y);
+          } else {
+            for (uint32_t aa = 0; aa < n_ant; aa++) {
+              uint32_t *d = dst0 + aa * c->spt;
+              d[f] = c2u(y);
+              if (f >= N - cp) d[f - N] = c2u(y);
+            }
+          }
+        },
+        1);
+    __syncthreads();
+  }
+}
+
+template <int LOG2N, int NA>
+static hipError_t launch_modofdm_t(const cfg_dev_t *d_cfg, const cfg_dev_t *h_cfg, int n_items, const uint32_t *d_ebits,
+                                   int32_t *d_iq, hipStream_t s)
+{
+  static int occ = 0;
+  if (!occ) {
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, k_modofdm<LOG2N, NA>, 128, 0) != hipSuccess || occ < 1)
+      occ = 1;
+  }
+  const int units = modofdm_geom<LOG2N>::UNITS;
+  int want = (n_items + units - 1) / units, cap = occ * (int)h_cfg->n_cu;
+  int grid = want < cap ? want : cap;
+  if (grid < 1) grid = 1;
+  hipLaunchKernelGGL((k_modofdm<LOG2N, NA>), dim3(grid), dim3(128), 0, s, d_cfg, n_items, d_ebits, d_iq);
+  return hipGetLastError();
 }
 
 hipError_t oai4g_launch_modofdm(const cfg_dev_t *d_cfg, const cfg_dev_t *h_cfg, int n_sf, const uint32_t *d_ebits,
                                 int32_t *d_iq, hipStream_t s)
 {
-  int n_items = n_sf * (int)(h_cfg->nsymb * h_cfg->n_ant);
+  const int n_items = n_sf * (int)h_cfg->nsymb;
+  /* two antenna transforms per unit only when they differ (LARGE_CDD); TM1 stores one n_ant times */
+  const bool two = h_cfg->mimo_mode == OAI4G_LARGE_CDD && h_cfg->n_ant == 2;
+  if (h_cfg->mimo_mode == OAI4G_LARGE_CDD && h_cfg->n_ant != 2) return hipErrorInvalidValue;
   switch (h_cfg->log2N) {
-  case 7: hipLaunchKernelGGL(k_modofdm<7>, dim3((n_items + 31) / 32), dim3(256), 0, s, d_cfg, n_items, d_ebits, d_iq); break;
-  case 8: hipLaunchKernelGGL(k_modofdm<8>, dim3((n_items + 15) / 16), dim3(256), 0, s, d_cfg, n_items, d_ebits, d_iq); break;
-  case 10: hipLaunchKernelGGL(k_modofdm<10>, dim3((n_items + 3) / 4), dim3(256), 0, s, d_cfg, n_items, d_ebits, d_iq); break;
-  case 11: hipLaunchKernelGGL(k_modofdm<11>, dim3((n_items + 1) / 2), dim3(256), 0, s, d_cfg, n_items, d_ebits, d_iq); break;
+  case 7: return two ? launch_modofdm_t<7, 2>(d_cfg, h_cfg, n_items, d_ebits, d_iq, s)
+                     : launch_modofdm_t<7, 1>(d_cfg, h_cfg, n_items, d_ebits, d_iq, s);
+  case 8: return two ? launch_modofdm_t<8, 2>(d_cfg, h_cfg, n_items, d_ebits, d_iq, s)
+                     : launch_modofdm_t<8, 1>(d_cfg, h_cfg, n_items, d_ebits, d_iq, s);
+  case 10: return two ? launch_modofdm_t<10, 2>(d_cfg, h_cfg, n_items, d_ebits, d_iq, s)
+                      : launch_modofdm_t<10, 1>(d_cfg, h_cfg, n_items, d_ebits, d_iq, s);
+  case 11: return two ? launch_modofdm_t<11, 2>(d_cfg, h_cfg, n_items, d_ebits, d_iq, s)
+                      : launch_modofdm_t<11, 1>(d_cfg, h_cfg, n_items, d_ebits, d_iq, s);
   default: return hipErrorInvalidValue;
   }
-  return hipGetLastError();
 }
 
 /* ======================================================================================

@@ -9,7 +9,7 @@ step() {  # name, seconds, command...
   timeout -k 10 "$secs" "$@" > "gpurun_out/$name.log" 2>&1
   local rc=$?
   echo "$name rc=$rc"; tail -n 25 "gpurun_out/$name.log"
-  if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "STOP after $name (rc=$rc)"; exit $rc; fi
+  if [ $rc -ne 0 ]; then echo "STOP after $name (rc=$rc)"; exit $rc; fi
   return 0
 }
 if [ -n "$PYTEST_K" ]; then KARG=(-k "$PYTEST_K"); else KARG=(); fi
