@@ -250,33 +250,36 @@ struct enc_tabs_t {            /* LDS copy of the RSC tables (lane-varying indic
   uint32_t zs[8];
 };
 
-/* interleaved input word of chunk j: bits c'_k = c_Pi(k), Pi(k) = (f1 k + f2 k^2) mod K.
- * All 32 addresses are formed first so the 32 LDS reads issue back to back. */
-static __device__ __forceinline__ uint32_t qpp_word(const uint32_t *sys, uint32_t K, uint32_t f1, uint32_t f2,
-                                                    uint32_t j)
+/* QPP walk start of chunk j: Pi(32j) | (Pi(32j+1) - Pi(32j) mod K) << 16 */
+static __device__ __forceinline__ uint32_t qpp_start(uint32_t K, uint32_t f1, uint32_t f2, uint32_t j)
 {
-  uint32_t k = 32 * j, n = min(32u, K - k);
+  uint32_t k = 32 * j;
   uint32_t pi = (((f2 * k) % K) * k + f1 * k) % K;            /* fits 32 bits for K <= 6144 */
   uint32_t dl = (f1 + ((f2 * ((2 * k + 1) % K)) % K)) % K;     /* Pi(k+1) - Pi(k) */
-  uint32_t d2 = (2u * f2) % K;
-  uint32_t pis[32];
+  return pi | (dl << 16);
+}
+
+/* interleaved input word of chunk j: bits c'_k = c_Pi(k), Pi(k) = (f1 k + f2 k^2) mod K walked by
+ * first and second differences (3gpplte.c:50-74), sys = swizzled systematic stream */
+static __device__ __forceinline__ uint32_t qpp_gather_word(const uint32_t *sys, uint32_t K, uint32_t start,
+                                                           uint32_t d2, uint32_t j)
+{
+  uint32_t pi = start & 0xffffu, dl = start >> 16, word = 0;
 #pragma unroll
   for (int b = 0; b < 32; b++) {
-    pis[b] = pi;
+    word |= __builtin_amdgcn_ubfe(sys[lsw(pi >> 5)], pi & 31u, 1u) << b;
     pi += dl;
-    if (pi >= K) pi -= K;
+    pi = min(pi, pi - K);
     dl += d2;
-    if (dl >= K) dl -= K;
+    dl = min(dl, dl - K);
   }
-  uint32_t word = 0;
-#pragma unroll
-  for (int b = 0; b < 32; b++) word |= ((sys[lsw(pis[b] >> 5)] >> (pis[b] & 31)) & 1u) << b;
-  return n == 32 ? word : word & ((1u << n) - 1u);
+  const uint32_t n = K - 32 * j;
+  return n >= 32 ? word : word & ((1u << n) - 1u);
 }
 
 /* encode one segment (block r, encoder e) with the calling wavefront */
-static __device__ __forceinline__ void turbo_segment(uint32_t *blk, uint32_t sw, uint32_t K, uint32_t f1, uint32_t f2, uint32_t e,
-                                     uint32_t *tail_out, const enc_tabs_t *tb)
+static __device__ __forceinline__ void turbo_segment(const uint32_t *in, bool swz_in, uint32_t *par_out, uint32_t K,
+                                                     uint32_t *tail_out, const enc_tabs_t *tb)
 {
   const uint32_t lane = threadIdx.x & 63;
   const uint32_t nch = (K + 31) >> 5;
@@ -287,7 +290,7 @@ static __device__ __forceinline__ void turbo_segment(uint32_t *blk, uint32_t sw,
   for (int t = 0; t < 4; t++) {
     u[t] = 0;
     uint32_t j = lane * qp + t;
-    if (t < (int)qp && j < nch) u[t] = e ? qpp_word(blk, K, f1, f2, j) : blk[lsw(j)];
+    if (t < (int)qp && j < nch) u[t] = in[swz_in ? lsw(j) : j];
     /* zero-start exit state of a full chunk: A^32 contribution of the inputs (partial chunks
      * only feed later lanes, whose values are not used) */
     if (t < (int)qp) S = tb->apow[0][S] ^ rsc_exit_input(u[t]);
@@ -312,7 +315,7 @@ static __device__ __forceinline__ void turbo_segment(uint32_t *blk, uint32_t sw,
       } else {
         s = tb->apow[0][s] ^ rsc_exit_input(u[t]);
       }
-      blk[(1 + e) * sw + lsw(j)] = par;
+      par_out[lsw(j)] = par;
       if (j == nch - 1) {
         /* trellis termination (3gpplte_sse.c:104-109, 440-471): (x, z) per step */
         uint32_t tbits = 0;
@@ -646,10 +649,24 @@ static __device__ void encode_codeword(const cfg_dev_t *__restrict__ c, uint32_t
   __syncthreads();
   if (stop_phase <= 2) return;
 
-  /* ---- phase 3: turbo encoding, one wave per (block, encoder) ---- */
+  /* ---- phase 3a: QPP-interleaved input words of every block (region A is free again) ---- */
+  uint32_t *ilv = lds_base;
+  {
+    const uint32_t nw = cw.ilv_off[C];
+    for (uint32_t i = tid; i < nw; i += nth) {
+      uint32_t r = 0;
+      while (r + 1 < C && i >= cw.ilv_off[r + 1]) r++;
+      const uint32_t j = i - cw.ilv_off[r], ki = cw.kidx[r];
+      ilv[i] = qpp_gather_word(strm + r * 3 * sw, cw.K[r], cw.qpp0[ki][j], cw.qpp_d2[ki], j);
+    }
+  }
+  __syncthreads();
+
+  /* ---- phase 3b: turbo encoding, one wave per (block, encoder) ---- */
   for (uint32_t seg = wave; seg < 2 * C; seg += nwaves) {
-    uint32_t r = seg >> 1, e = seg & 1u;
-    turbo_segment(strm + r * 3 * sw, sw, cw.K[r], cw.f1[r], cw.f2[r], e, &tails[2 * r + e], tabs);
+    const uint32_t r = seg >> 1, e = seg & 1u;
+    uint32_t *blk = strm + r * 3 * sw;
+    turbo_segment(e ? ilv + cw.ilv_off[r] : blk, e == 0, blk + (1 + e) * sw, cw.K[r], &tails[2 * r + e], tabs);
   }
   __syncthreads();
   if (stop_phase <= 3) return;
@@ -905,8 +922,12 @@ __global__ void __launch_bounds__(256) k_turbo_bytes(const uint8_t *__restrict__
     strm[lsw(j)] = wv;
   }
   __syncthreads();
+  __shared__ uint32_t ilv[OAI4G_MAX_CHUNKS];
+  const uint32_t d2 = (2 * f2) % K;
+  for (uint32_t j = threadIdx.x; j < nw; j += blockDim.x) ilv[j] = qpp_gather_word(strm, K, qpp_start(K, f1, f2, j), d2, j);
+  __syncthreads();
   uint32_t wave = threadIdx.x >> 6;
-  if (wave < 2) turbo_segment(strm, sw, K, f1, f2, wave, &tails[wave], &tabs);
+  if (wave < 2) turbo_segment(wave ? ilv : strm, wave == 0, strm + (1 + wave) * sw, K, &tails[wave], &tabs);
   __syncthreads();
   for (uint32_t i = threadIdx.x; i < 3 * K + 12; i += blockDim.x) {
     uint32_t kk = i / 3, s = i - 3 * kk;

@@ -550,6 +550,27 @@ static int derive_cfg(oai4g_tx_config *cfg, const oai4g_tx_params_t *p, const ui
       c.kidx[r] = (C > 1 && r < Cm) ? 0 : 1;
     }
     if (src != (c.TBS + 24) / 8) { set_err("segmentation byte accounting mismatch"); return -1; }
+    /* QPP walk tables per block size (Kminus list 0, Kplus list 1) and interleaved-word offsets */
+    for (int ki = 0; ki < 2; ki++) {
+      uint32_t K = ki == 0 ? Km : Kp;
+      if (K == 0 || (ki == 0 && !(C > 1 && Cm > 0))) continue;
+      int qi = oai4g_qpp_index(K);
+      uint64_t f1 = oai4g_qpp_table[qi].f1, f2 = oai4g_qpp_table[qi].f2;
+      for (uint32_t j = 0; j < (K + 31) / 32; j++) {
+        uint64_t k = 32 * j;
+        uint32_t pi = (uint32_t)((f1 * k + f2 * k * k) % K), pi1 = (uint32_t)((f1 * (k + 1) + f2 * (k + 1) * (k + 1)) % K);
+        c.qpp0[ki][j] = pi | (((pi1 + K - pi) % K) << 16);
+      }
+      c.qpp_d2[ki] = (uint32_t)((2 * f2) % K);
+    }
+    {
+      uint32_t o = 0;
+      for (uint32_t r = 0; r < C; r++) {
+        c.ilv_off[r] = o;
+        o += (c.K[r] + 31) / 32;
+      }
+      c.ilv_off[C] = o;
+    }
     c.crc_per_tb = (c.A_bytes + 255) / 256;
     crc_mul_tables(c.crc_per_tb, 8, 0x864cfbu, c.crcmul_tb);
     uint32_t ncb_max = 0;
@@ -630,6 +651,8 @@ static int derive_cfg(oai4g_tx_config *cfg, const oai4g_tx_params_t *p, const ui
   h.lds_col_words = max_col;
   /* encoder LDS regions with phase-disjoint lifetimes (see oai4g_encode.hip) */
   h.lds_a_words = max_tb_words + OAI4G_ENC_CRC_TABLE_WORDS > max_col ? max_tb_words + OAI4G_ENC_CRC_TABLE_WORDS : max_col;
+  for (int cw = 0; cw < p->n_cw; cw++)   /* region A also holds the interleaved words in phase 3 */
+    if (h.cw[cw].ilv_off[h.cw[cw].C] > h.lds_a_words) h.lds_a_words = h.cw[cw].ilv_off[h.cw[cw].C];
   h.lds_b_words = max_stream_words > max_w ? max_stream_words : max_w;
   /* RE maps */
   if (need_remap) {

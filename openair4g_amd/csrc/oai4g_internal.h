@@ -15,6 +15,7 @@
 
 #define OAI4G_MAX_CB 16
 #define OAI4G_MAX_NULLS 104
+#define OAI4G_MAX_CHUNKS 192                /* 6144 / 32 */
 #define OAI4G_ENC_CRC_TABLE_WORDS (256 + 256 + 8 * 96 + 6 * 96) /* byte tables A/B + tree multipliers */
 #define OAI4G_GOLD_LANES 256
 #define OAI4G_GOLD_STRIDE 16
@@ -58,6 +59,11 @@ struct cw_dev_t {
   uint32_t wpk_off[OAI4G_MAX_CB + 1]; /* LDS word offset of block r's packed w (3R words + 2 pad) */
   uint32_t col_off[OAI4G_MAX_CB + 1]; /* LDS word offset of block r's column arrays (96 x RBW words) */
   uint32_t col_task[OAI4G_MAX_CB + 1];/* prefix sum of transpose tasks (3 x RBW per block) */
+  uint32_t ilv_off[OAI4G_MAX_CB + 1]; /* LDS word offset of block r's QPP-interleaved input words */
+  /* QPP interleaver walk per 32-bit chunk j (kidx list): Pi(32j) | (Pi(32j+1)-Pi(32j) mod K) << 16,
+   * and the second difference 2 f2 mod K (3gpplte.c:50-74 restated incrementally) */
+  uint32_t qpp0[2][OAI4G_MAX_CHUNKS];
+  uint32_t qpp_d2[2];
   uint32_t nnull[2];
   uint16_t nullpos[2][OAI4G_MAX_NULLS]; /* sorted NULL positions of w for K = Kminus / Kplus */
   /* per subframe index */
