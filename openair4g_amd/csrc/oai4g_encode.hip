@@ -396,16 +396,6 @@ static __device__ __forceinline__ uint32_t sx32(const uint32_t *a, int pos)
   return off ? (lo >> off) | (hi << (32 - off)) : lo;
 }
 
-/* 32 bits of an unswizzled bit array starting at bit o (reads one word ahead) */
-static __device__ __forceinline__ uint32_t ext32(const uint32_t *a, uint32_t o)
-{
-  uint32_t w = o >> 5, sh = o & 31u;
-  uint32_t lo = a[w], hi = a[w + 1];
-  return sh ? (lo >> sh) | (hi << (32 - sh)) : lo;
-}
-
-static __device__ __forceinline__ uint32_t lowmask(uint32_t n) { return n >= 32 ? 0xffffffffu : (1u << n) - 1u; }
-
 /* 16 bits -> even bit positions of 32 */
 static __device__ __forceinline__ uint32_t spread16(uint32_t x)
 {
@@ -431,38 +421,14 @@ static __device__ __forceinline__ uint32_t transpose32(uint32_t x, uint32_t lane
   return x;
 }
 
-/*
- * Word wi of the packed sub-block interleaver output w (lte_rate_matching.c:51-130) from the
- * column-major arrays col[s][c] (R bits each: column c of y^(s), y^(2) pre-shifted by one for
- * the (pi(k)+1) mod Kpi rule).  v^(0) is the concatenation of the permuted columns; the
- * interlaced half takes 16 rows of v^(1)/v^(2) per word.  NULL entries read as 0 (the rate
- * matcher skips them through the NULL list).
- */
-static __device__ __forceinline__ uint32_t w_word(const uint32_t *col, uint32_t R, uint32_t Kpi, uint32_t wi)
+/* OR 32 bits into an LDS bit array at bit offset `bit` (LDS atomics: tiles of neighbouring
+ * columns share boundary words) */
+static __device__ __forceinline__ void or_bits(uint32_t *w, uint32_t bit, uint32_t v)
 {
-  const uint32_t RBW = (R + 31) >> 5, q = 32 * wi;
-  uint32_t v = 0, got = 0;
-  if (q < Kpi) {
-    uint32_t c = q / R, o = q - c * R;
-    while (got < 32) {
-      uint32_t take = min(32 - got, R - o);
-      v |= (ext32(col + colperm(c) * RBW, o) & lowmask(take)) << got;
-      got += take;
-      c++;
-      o = 0;
-    }
-  } else {
-    uint32_t e = q - Kpi, c = e / (2 * R), row = (e - c * 2 * R) >> 1;
-    while (got < 16) {
-      uint32_t take = min(16 - got, R - row), cp = colperm(c), mk = lowmask(take);
-      uint32_t a = ext32(col + (32 + cp) * RBW, row) & mk, b = ext32(col + (64 + cp) * RBW, row) & mk;
-      v |= (spread16(a) | (spread16(b) << 1)) << (2 * got);
-      got += take;
-      c++;
-      row = 0;
-    }
-  }
-  return v;
+  if (!v) return;
+  const uint32_t wi = bit >> 5, sh = bit & 31u;
+  atomicOr(&w[wi], v << sh);
+  if (sh && (v >> (32 - sh))) atomicOr(&w[wi + 1], v >> (32 - sh));
 }
 
 /* position p of the ci-th non-NULL entry of w and m = NULLs before p */
@@ -528,16 +494,14 @@ static __device__ void encode_codeword(const cfg_dev_t *__restrict__ c, uint32_t
   const uint32_t tid = threadIdx.x, nth = blockDim.x, wave = tid >> 6, lane = tid & 63, nwaves = nth >> 6;
   const uint32_t sfi = DEBUG ? sf : (c->first_sf + sf * c->sf_step) % 10;
   const uint32_t C = cw.C, sw = cw.stream_words;
-  /* LDS carve-up.  Region A: TB || CRC and the CRC tables (phases 0-2), then the column-major
-   * y^(s) arrays (phase 4).  Region B: the constituent streams (phases 0-4a), then packed w. */
+  /* LDS carve-up.  Region A: TB || CRC and the CRC tables (phases 0-2), the QPP-interleaved
+   * words (phase 3), packed w (phase 4).  Region B: the constituent streams. */
   uint32_t *tbw = lds_base;
   uint32_t *crctab_a = tbw + c->lds_tb_words;
   uint32_t *crctab_b = crctab_a + 256;
   uint32_t *mul_tb = crctab_b + 256;                     /* [8][6][16] */
   uint32_t *mul_cb = mul_tb + 8 * 96;                    /* [6][6][16] */
-  uint32_t *colw = lds_base;
   uint32_t *strm = lds_base + c->lds_a_words;
-  uint32_t *wb = strm;
   uint32_t *ebuf = strm + c->lds_b_words;
   uint32_t *tails = ebuf + c->lds_gold_words;
   uint32_t *crcs = tails + 2 * OAI4G_MAX_CB;             /* [0] = CRC24A, [1+r] = CRC24B of block r */
@@ -717,10 +681,18 @@ static __device__ void encode_codeword(const cfg_dev_t *__restrict__ c, uint32_t
   }
   __syncthreads();
 
-  /* ---- phase 4a: y^(s) rows (32 entries each, NULL prefix of ND) transposed into column-major
-   * bit arrays, one 32x32 tile per half-wave ---- */
+  /* ---- phase 4a: zero packed w (region A; the interleaved words are dead) ---- */
+  uint32_t *wb = lds_base;
+  for (uint32_t i = tid; i < cw.wpk_off[C]; i += nth) wb[i] = 0u;
+  __syncthreads();
+
+  /* ---- phase 4b: sub-block interleaving (lte_rate_matching.c:51-130).  Each half-wave takes a
+   * 32x32 tile of y^(s) (32 rows of 32 entries, NULL prefix of ND, y^(2) pre-shifted by one for
+   * the (pi(k)+1) mod Kpi rule), transposes it so lane c holds 32 rows of column c, and ORs that
+   * column run into packed w: column c sits at w column bitrev5(c), i.e. at bit bitrev5(c) R + row
+   * of v^(0), and interlaced (even bits v^(1), odd bits v^(2)) after Kpi. ---- */
   {
-    const uint32_t lane32 = tid & 31, ntask = cw.col_task[C];
+    const uint32_t lane32 = tid & 31, ntask = cw.col_task[C], wcol = colperm(lane32);
     for (uint32_t t = tid >> 5; t < ntask; t += nth >> 5) {
       uint32_t r = 0;
       while (r + 1 < C && t >= cw.col_task[r + 1]) r++;
@@ -736,18 +708,15 @@ static __device__ void encode_codeword(const cfg_dev_t *__restrict__ c, uint32_t
         }
       }
       y = transpose32(y, lane32);
-      colw[cw.col_off[r] + (32 * s + lane32) * RBW + rb] = y;
+      uint32_t *w = wb + cw.wpk_off[r];
+      if (s == 0) {
+        or_bits(w, wcol * R + 32 * rb, y);
+      } else {
+        const uint32_t bit = cw.Kpi[r] + 2 * (wcol * R + 32 * rb) + (s - 1);
+        or_bits(w, bit, spread16(y));
+        or_bits(w, bit + 32, spread16(y >> 16));
+      }
     }
-  }
-  __syncthreads();
-
-  /* ---- phase 4b: packed w of every block (streams are dead: w overwrites them) ---- */
-  const uint32_t wtot = cw.wpk_off[C];
-  for (uint32_t i = tid; i < wtot; i += nth) {
-    uint32_t r = 0;
-    while (r + 1 < C && i >= cw.wpk_off[r + 1]) r++;
-    uint32_t wi = i - cw.wpk_off[r], R = cw.R[r];
-    wb[i] = wi < 3 * R ? w_word(colw + cw.col_off[r], R, cw.Kpi[r], wi) : 0u;
   }
   __syncthreads();
   if (stop_phase <= 4) return;

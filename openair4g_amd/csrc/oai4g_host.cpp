@@ -505,7 +505,7 @@ static int derive_cfg(oai4g_tx_config *cfg, const oai4g_tx_params_t *p, const ui
   h.first_sf = p->first_subframe % 10;
   h.sf_step = p->subframe_step;
   h.payload_stride = p->payload_stride;
-  uint32_t max_tb_words = 0, max_stream_words = 0, max_gw = 0, max_bits = 0, max_w = 0, max_inw = 0, max_col = 0;
+  uint32_t max_tb_words = 0, max_stream_words = 0, max_gw = 0, max_bits = 0, max_w = 0, max_inw = 0;
   bool rm_fail = false;
   for (int cw = 0; cw < p->n_cw; cw++) {
     cw_dev_t &c = h.cw[cw];
@@ -604,21 +604,17 @@ static int derive_cfg(oai4g_tx_config *cfg, const oai4g_tx_params_t *p, const ui
     for (uint32_t r = 0; r < C; r++) inw += (c.K[r] + 31) >> 5;
     max_inw = inw > max_inw ? inw : max_inw;
     /* packed w of every block (3 Kpi bits = 3R words, + 2 read-ahead words each) and the
-     * column-major y^(s) arrays (3 streams x 32 columns x ceil(R/32) words) */
-    uint32_t wwords = 0, cwords = 0, ntask = 0;
+     * 32x32 transpose tiles of the sub-block interleaver (3 streams x ceil(R/32) per block) */
+    uint32_t wwords = 0, ntask = 0;
     for (uint32_t r = 0; r < C; r++) {
       uint32_t RBW = (c.R[r] + 31) / 32;
       c.wpk_off[r] = wwords;
-      c.col_off[r] = cwords;
       c.col_task[r] = ntask;
       wwords += 3 * c.R[r] + 2;
-      cwords += 96 * RBW;
       ntask += 3 * RBW;
     }
     c.wpk_off[C] = wwords;
-    c.col_off[C] = cwords;
     c.col_task[C] = ntask;
-    max_col = cwords + 1 > max_col ? cwords + 1 : max_col;
     max_w = wwords > max_w ? wwords : max_w;
     uint32_t tbw = (c.A_bytes + 3 + 3) / 4 + 1;
     max_tb_words = tbw > max_tb_words ? tbw : max_tb_words;
@@ -648,12 +644,12 @@ static int derive_cfg(oai4g_tx_config *cfg, const oai4g_tx_params_t *p, const ui
   h.lds_gold_words = max_gw + 1;
   h.lds_w_words = max_w;
   (void)max_inw;
-  h.lds_col_words = max_col;
   /* encoder LDS regions with phase-disjoint lifetimes (see oai4g_encode.hip) */
-  h.lds_a_words = max_tb_words + OAI4G_ENC_CRC_TABLE_WORDS > max_col ? max_tb_words + OAI4G_ENC_CRC_TABLE_WORDS : max_col;
+  h.lds_a_words = max_tb_words + OAI4G_ENC_CRC_TABLE_WORDS;
   for (int cw = 0; cw < p->n_cw; cw++)   /* region A also holds the interleaved words in phase 3 */
     if (h.cw[cw].ilv_off[h.cw[cw].C] > h.lds_a_words) h.lds_a_words = h.cw[cw].ilv_off[h.cw[cw].C];
-  h.lds_b_words = max_stream_words > max_w ? max_stream_words : max_w;
+  if (max_w > h.lds_a_words) h.lds_a_words = max_w;
+  h.lds_b_words = max_stream_words;
   /* RE maps */
   if (need_remap) {
     uint32_t N = h.N;

@@ -57,7 +57,6 @@ struct cw_dev_t {
   uint32_t k0c[OAI4G_MAX_CB];   /* non-NULL entries of w[0..k0): compacted start */
   uint32_t kidx[OAI4G_MAX_CB];  /* which null list (0: Kminus, 1: Kplus) */
   uint32_t wpk_off[OAI4G_MAX_CB + 1]; /* LDS word offset of block r's packed w (3R words + 2 pad) */
-  uint32_t col_off[OAI4G_MAX_CB + 1]; /* LDS word offset of block r's column arrays (96 x RBW words) */
   uint32_t col_task[OAI4G_MAX_CB + 1];/* prefix sum of transpose tasks (3 x RBW per block) */
   uint32_t ilv_off[OAI4G_MAX_CB + 1]; /* LDS word offset of block r's QPP-interleaved input words */
   /* QPP interleaver walk per 32-bit chunk j (kidx list): Pi(32j) | (Pi(32j+1)-Pi(32j) mod K) << 16,
@@ -89,10 +88,9 @@ struct cfg_dev_t {
   uint32_t lds_stream_words;    /* LDS words for all block streams of one codeword */
   uint32_t lds_gold_words;      /* = e-bit staging words (Gold-prefilled) */
   uint32_t lds_w_words;         /* packed sub-block interleaver output of every block */
-  uint32_t lds_col_words;       /* column-major y^(s) arrays of every block (+1 read-ahead) */
-  uint32_t lds_a_words;         /* region A: TB + CRC tables (phases 0-2) | columns (phase 4) */
-  uint32_t lds_b_words;         /* region B: streams (phases 0-4a) | packed w (4b-4c) */
-  uint32_t pad[1];
+  uint32_t lds_a_words;         /* region A: TB + CRC tables (0-2) | interleaved words (3) | packed w (4) */
+  uint32_t lds_b_words;         /* region B: constituent streams */
+  uint32_t pad[2];
   cw_dev_t cw[2];
   uint32_t symbase[10][14];     /* data REs before symbol l */
   uint16_t symnre[10][14];      /* data REs in symbol l */
