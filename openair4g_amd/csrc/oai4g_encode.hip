@@ -114,7 +114,6 @@ static __device__ __forceinline__ uint32_t rsc_exit_input(uint32_t u)
 __constant__ rsc_tables_t c_rsc = k_rsc;
 
 
-static __device__ __forceinline__ uint32_t lsw(uint32_t w) { return w + (w >> 5); } /* stream word swizzle */
 
 /* 4 MSB-first bytes (little-endian word) -> 32 bits LSB-first in sequence order */
 static __device__ __forceinline__ uint32_t bytes_to_seq(uint32_t le) { return __builtin_bswap32(__builtin_bitreverse32(le)); }
@@ -260,14 +259,14 @@ static __device__ __forceinline__ uint32_t qpp_start(uint32_t K, uint32_t f1, ui
 }
 
 /* interleaved input word of chunk j: bits c'_k = c_Pi(k), Pi(k) = (f1 k + f2 k^2) mod K walked by
- * first and second differences (3gpplte.c:50-74), sys = swizzled systematic stream */
+ * first and second differences (3gpplte.c:50-74) */
 static __device__ __forceinline__ uint32_t qpp_gather_word(const uint32_t *sys, uint32_t K, uint32_t start,
                                                            uint32_t d2, uint32_t j)
 {
   uint32_t pi = start & 0xffffu, dl = start >> 16, word = 0;
 #pragma unroll
   for (int b = 0; b < 32; b++) {
-    word |= __builtin_amdgcn_ubfe(sys[lsw(pi >> 5)], pi & 31u, 1u) << b;
+    word |= __builtin_amdgcn_ubfe(sys[pi >> 5], pi & 31u, 1u) << b;
     pi += dl;
     pi = min(pi, pi - K);
     dl += d2;
@@ -278,7 +277,7 @@ static __device__ __forceinline__ uint32_t qpp_gather_word(const uint32_t *sys, 
 }
 
 /* encode one segment (block r, encoder e) with the calling wavefront */
-static __device__ __forceinline__ void turbo_segment(const uint32_t *in, bool swz_in, uint32_t *par_out, uint32_t K,
+static __device__ __forceinline__ void turbo_segment(const uint32_t *in, uint32_t *par_out, uint32_t K,
                                                      uint32_t *tail_out, const enc_tabs_t *tb)
 {
   const uint32_t lane = threadIdx.x & 63;
@@ -290,7 +289,7 @@ static __device__ __forceinline__ void turbo_segment(const uint32_t *in, bool sw
   for (int t = 0; t < 4; t++) {
     u[t] = 0;
     uint32_t j = lane * qp + t;
-    if (t < (int)qp && j < nch) u[t] = in[swz_in ? lsw(j) : j];
+    if (t < (int)qp && j < nch) u[t] = in[j];
     /* zero-start exit state of a full chunk: A^32 contribution of the inputs (partial chunks
      * only feed later lanes, whose values are not used) */
     if (t < (int)qp) S = tb->apow[0][S] ^ rsc_exit_input(u[t]);
@@ -315,7 +314,7 @@ static __device__ __forceinline__ void turbo_segment(const uint32_t *in, bool sw
       } else {
         s = tb->apow[0][s] ^ rsc_exit_input(u[t]);
       }
-      par_out[lsw(j)] = par;
+      par_out[j] = par;
       if (j == nch - 1) {
         /* trellis termination (3gpplte_sse.c:104-109, 440-471): (x, z) per step */
         uint32_t tbits = 0;
@@ -340,7 +339,7 @@ static __device__ __forceinline__ uint32_t tail_bit(const uint32_t *tails, uint3
 static __device__ __forceinline__ uint32_t dstream_bit(const uint32_t *blk, uint32_t sw, const uint32_t *tails,
                                                        uint32_t r, uint32_t K, uint32_t s, uint32_t idx)
 {
-  if (idx < K) return (blk[s * sw + lsw(idx >> 5)] >> (idx & 31)) & 1u;
+  if (idx < K) return (blk[s * sw + (idx >> 5)] >> (idx & 31)) & 1u;
   return tail_bit(tails, r, 3 * (idx - K) + s);
 }
 
@@ -383,15 +382,14 @@ static __device__ __forceinline__ bool wwalk_null(const wwalk_t &w, uint32_t R, 
   return (cp + 1 < ND) || (w.col == 31 && R == 1 && ND > 0);
 }
 
-/* 32 bits of a packed LSB-first LDS bit array (swizzled words) starting at bit `pos` (pos may be
- * negative: zeros) */
+/* 32 bits of a packed LSB-first LDS bit array starting at bit `pos` (pos may be negative: zeros) */
 static __device__ __forceinline__ uint32_t sx32(const uint32_t *a, int pos)
 {
   int wi = pos >> 5;
   uint32_t off = (uint32_t)pos & 31u;
-  uint32_t lo = a[lsw((uint32_t)max(wi, 0))];
+  uint32_t lo = a[(uint32_t)max(wi, 0)];
   lo = wi >= 0 ? lo : 0u;
-  uint32_t hi = a[lsw((uint32_t)max(wi + 1, 0))];
+  uint32_t hi = a[(uint32_t)max(wi + 1, 0)];
   hi = wi + 1 >= 0 ? hi : 0u;
   return off ? (lo >> off) | (hi << (32 - off)) : lo;
 }
@@ -607,7 +605,7 @@ static __device__ void encode_codeword(const cfg_dev_t *__restrict__ c, uint32_t
       }
       uint32_t wv = bytes_to_seq(le);
       if (32 * (j + 1) > K) wv &= (1u << (K - 32 * j)) - 1u;
-      sys[lsw(j)] = wv;
+      sys[j] = wv;
     }
   }
   __syncthreads();
@@ -630,7 +628,7 @@ static __device__ void encode_codeword(const cfg_dev_t *__restrict__ c, uint32_t
   for (uint32_t seg = wave; seg < 2 * C; seg += nwaves) {
     const uint32_t r = seg >> 1, e = seg & 1u;
     uint32_t *blk = strm + r * 3 * sw;
-    turbo_segment(e ? ilv + cw.ilv_off[r] : blk, e == 0, blk + (1 + e) * sw, cw.K[r], &tails[2 * r + e], tabs);
+    turbo_segment(e ? ilv + cw.ilv_off[r] : blk, blk + (1 + e) * sw, cw.K[r], &tails[2 * r + e], tabs);
   }
   __syncthreads();
   if (stop_phase <= 3) return;
@@ -642,7 +640,7 @@ static __device__ void encode_codeword(const cfg_dev_t *__restrict__ c, uint32_t
       const uint32_t *blk = strm + r * 3 * sw;
       if (dbg.c)
         for (uint32_t i = tid; i < K / 8; i += nth) {
-          uint32_t wv = blk[lsw(i >> 2)];
+          uint32_t wv = blk[(i >> 2)];
           uint32_t byte = (wv >> (8 * (i & 3))) & 0xffu;
           dbg.c[r * (8 + 3 + 768) + i] = (uint8_t)(__builtin_bitreverse32(byte) >> 24);
         }
@@ -675,8 +673,8 @@ static __device__ void encode_codeword(const cfg_dev_t *__restrict__ c, uint32_t
       uint32_t t4 = tail_bit(tails, r, s) | (tail_bit(tails, r, 3 + s) << 1) | (tail_bit(tails, r, 6 + s) << 2) |
                     (tail_bit(tails, r, 9 + s) << 3);
       uint32_t w0 = K >> 5, off = K & 31;
-      blk[s * sw + lsw(w0)] |= t4 << off;
-      if (off > 28) blk[s * sw + lsw(w0 + 1)] |= t4 >> (32 - off);
+      blk[s * sw + w0] |= t4 << off;
+      if (off > 28) blk[s * sw + (w0 + 1)] |= t4 >> (32 - off);
     }
   }
   __syncthreads();
@@ -704,7 +702,7 @@ static __device__ void encode_codeword(const cfg_dev_t *__restrict__ c, uint32_t
         y = sx32(st, (int)(32 * row) - (int)ND + (s == 2 ? 1 : 0));
         if (s == 2 && row == R - 1) {
           y &= 0x7fffffffu;                       /* j = Kpi-1 reads y^(2)_0: NULL if ND > 0 */
-          if (ND == 0) y |= (st[lsw(0)] & 1u) << 31;
+          if (ND == 0) y |= (st[0] & 1u) << 31;
         }
       }
       y = transpose32(y, lane32);
@@ -888,7 +886,7 @@ __global__ void __launch_bounds__(256) k_turbo_bytes(const uint8_t *__restrict__
     }
     uint32_t wv = bytes_to_seq(le);
     if (32 * (j + 1) > K) wv &= (1u << (K - 32 * j)) - 1u;
-    strm[lsw(j)] = wv;
+    strm[j] = wv;
   }
   __syncthreads();
   __shared__ uint32_t ilv[OAI4G_MAX_CHUNKS];
@@ -896,7 +894,7 @@ __global__ void __launch_bounds__(256) k_turbo_bytes(const uint8_t *__restrict__
   for (uint32_t j = threadIdx.x; j < nw; j += blockDim.x) ilv[j] = qpp_gather_word(strm, K, qpp_start(K, f1, f2, j), d2, j);
   __syncthreads();
   uint32_t wave = threadIdx.x >> 6;
-  if (wave < 2) turbo_segment(wave ? ilv : strm, wave == 0, strm + (1 + wave) * sw, K, &tails[wave], &tabs);
+  if (wave < 2) turbo_segment(wave ? ilv : strm, strm + (1 + wave) * sw, K, &tails[wave], &tabs);
   __syncthreads();
   for (uint32_t i = threadIdx.x; i < 3 * K + 12; i += blockDim.x) {
     uint32_t kk = i / 3, s = i - 3 * kk;

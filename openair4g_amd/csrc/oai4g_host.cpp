@@ -599,7 +599,7 @@ static int derive_cfg(oai4g_tx_config *cfg, const oai4g_tx_params_t *p, const ui
       c.Nnn[r] = Ncb - nn;
     }
     uint32_t nw = (maxK + 31) >> 5;
-    c.stream_words = (nw + 2) + ((nw + 2) >> 5) + 1;   /* + tail word + read-ahead word */
+    c.stream_words = nw + 3;   /* + tail word + read-ahead words */
     uint32_t inw = 0;
     for (uint32_t r = 0; r < C; r++) inw += (c.K[r] + 31) >> 5;
     max_inw = inw > max_inw ? inw : max_inw;
