@@ -150,11 +150,13 @@ _SIGS = {
 }
 
 
-def load_library(path=LIB_PATH):
-    """Load the HIP library (raises OAI4GError if it is not built)."""
+def load_library(path=None):
+    """Load the HIP library (raises OAI4GError if it is not built).  OAI4G_LIB selects an
+    alternative in-tree build (kernel variants for A/B measurements)."""
     global _lib
     if _lib is not None:
         return _lib
+    path = path or os.environ.get("OAI4G_LIB") or LIB_PATH
     if not os.path.exists(path):
         raise OAI4GError(f"HIP library not built: {path} (run __graft_entry__.build())")
     lib = ctypes.CDLL(path)

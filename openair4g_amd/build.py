@@ -25,28 +25,31 @@ def _newer(target, deps):
     return any(os.path.getmtime(d) > t for d in deps)
 
 
-def build_lib(force=False, verbose=False):
-    os.makedirs(LIBDIR, exist_ok=True)
+def build_lib(force=False, verbose=False, out=None, defines=()):
+    """Compile the library; `out`/`defines` build a variant (e.g. -DOAI4G_MODOFDM_WAVES=3)."""
+    lib = out or LIB
+    libdir = os.path.dirname(lib)
+    os.makedirs(libdir, exist_ok=True)
     srcs = [os.path.join(CSRC, s) for s in SOURCES]
     deps = srcs + EXTRA + [os.path.join(CSRC, "oai4g_internal.h"), os.path.join(ROOT, "include", "oai4g.h")]
-    if not force and not _newer(LIB, deps):
-        return LIB
+    if not force and not _newer(lib, deps):
+        return lib
     objs = []
     for src in srcs + EXTRA:
-        obj = os.path.join(LIBDIR, os.path.basename(src) + ".o")
+        obj = os.path.join(libdir, os.path.basename(src) + ".o")
         lang = ["-x", "hip"] if src.endswith((".hip", ".cpp")) else ["-x", "c"]
         cmd = [HIPCC, f"--offload-arch={ARCH}", "-O3", "-fPIC", "-Wall", "-Wno-unused-result", "-Wno-unused-value",
-               "-I", os.path.join(ROOT, "include")] + (["-std=c++17"] if lang[1] == "hip" else []) + lang + \
+               "-I", os.path.join(ROOT, "include")] + list(defines) + (["-std=c++17"] if lang[1] == "hip" else []) + lang + \
               ["-c", src, "-o", obj]
         if verbose:
             print(" ".join(cmd))
         subprocess.run(cmd, check=True)
         objs.append(obj)
-    cmd = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", LIB] + objs + ["-lpthread"]
+    cmd = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", lib] + objs + ["-lpthread"]
     if verbose:
         print(" ".join(cmd))
     subprocess.run(cmd, check=True)
-    return LIB
+    return lib
 
 
 def build_oracle(verbose=False):
@@ -55,6 +58,12 @@ def build_oracle(verbose=False):
 
 
 if __name__ == "__main__":
+    if "--variant" in sys.argv:   # build.py --variant NAME -DFOO=1 ... -> variants/NAME/libopenair4g_amd.so
+        i = sys.argv.index("--variant")
+        name, defs = sys.argv[i + 1], [a for a in sys.argv[i + 2:] if a.startswith("-D")]
+        print("built", build_lib(force=True, out=os.path.join(ROOT, "variants", name, "libopenair4g_amd.so"),
+                                 defines=defs))
+        sys.exit(0)
     build_lib(force="--force" in sys.argv, verbose=True)
     build_oracle(verbose=True)
     print("built", LIB)

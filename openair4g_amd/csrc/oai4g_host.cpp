@@ -90,7 +90,7 @@ static void do_init(void)
   }
   g_n_cu = prop.multiProcessorCount > 0 ? prop.multiProcessorCount : 256;
   /* twiddles */
-  std::vector<uint32_t> tw(OAI4G_TW_TOTAL);
+  std::vector<uint32_t> tw(2 * OAI4G_TW_TOTAL);   /* t, then the rotated companions (-t.im, t.re) */
   const int sizes[] = {4, 6, 7, 8, 9, 10, 11};
   for (int log2s : sizes) {
     int N = 1 << log2s;
@@ -99,6 +99,7 @@ static void do_init(void)
       int16_t re, im;
       twiddle_host(N, m, &re, &im);
       tw[off + m] = (uint16_t)re | ((uint32_t)(uint16_t)im << 16);
+      tw[OAI4G_TW_TOTAL + off + m] = (uint16_t)(int16_t)(-im) | ((uint32_t)(uint16_t)re << 16);
     }
   }
   /* Gold: x1 after 50+16l steps; x2 step-matrix powers M2^(50+16l) (columns) */

@@ -98,7 +98,7 @@ struct cfg_dev_t {
   const uint16_t *remap;        /* [10][14][N] data-RE index | parity<<15, 0xFFFF = none */
   const uint32_t *gold_x1;      /* [256]     x1 state after 50+16l word steps */
   const uint32_t *gold_x2j;     /* [256][32] columns of M2^(50+16l) */
-  const uint32_t *tw;           /* OAI4G_TW_TOTAL packed twiddles */
+  const uint32_t *tw;           /* 2 x OAI4G_TW_TOTAL packed twiddles t, then (-t.im, t.re) */
 };
 
 /* ---------------- launch helpers implemented in the .hip files ---------------- */

@@ -27,6 +27,7 @@
 
 typedef short s16x2 __attribute__((ext_vector_type(2)));
 typedef const __attribute__((address_space(1))) uint32_t gu32_t;
+typedef const __attribute__((address_space(1))) uint16_t gu16_t;
 
 static __device__ __forceinline__ s16x2 u2c(uint32_t v) { return __builtin_bit_cast(s16x2, v); }
 static __device__ __forceinline__ uint32_t c2u(s16x2 v) { return __builtin_bit_cast(uint32_t, v); }
@@ -126,30 +127,31 @@ struct idft_tw_t {
   static constexpr bool HAS256 = LOG2N == 8 || LOG2N >= 10, HAS1024 = LOG2N >= 10, HASR2 = LOG2N == 7 || LOG2N == 11;
   static constexpr int D64 = tw_distinct(T, 16, 4), D256 = tw_distinct(T, 64, 4), D1024 = tw_distinct(T, 256, 4),
                        DR2 = tw_distinct(T, N / 2, 8);
-  twp_t l16[7];                         /* W16^{0,1,2,3,4,6,9} */
-  twp_t l64[D64][3];
-  twp_t l256[HAS256 ? D256 : 1][3];
-  twp_t l1024[HAS1024 ? D1024 : 1][3];
-  twp_t r2[HASR2 ? DR2 : 1];
+  twp_t l16[7];                         /* W16^{0,1,2,3,4,6,9}: wave-uniform (scalar loads) */
+  s16x2 l64[D64][3];                    /* per-thread twiddles; companions rebuilt at use */
+  s16x2 l256[HAS256 ? D256 : 1][3];
+  s16x2 l1024[HAS1024 ? D1024 : 1][3];
+  s16x2 r2[HASR2 ? DR2 : 1];
 
   __device__ __forceinline__ void load(const uint32_t *tw, int t)
   {
     gu32_t *g = (gu32_t *)tw;
     constexpr int i16[7] = {0, 1, 2, 3, 4, 6, 9};
 #pragma unroll
-    for (int i = 0; i < 7; i++) l16[i] = mk_tw(g[oai4g_tw_offset(4) + i16[i]]);
+    for (int i = 0; i < 7; i++)
+      l16[i] = {u2c(g[oai4g_tw_offset(4) + i16[i]]), u2c(g[OAI4G_TW_TOTAL + oai4g_tw_offset(4) + i16[i]])};
 #pragma unroll
     for (int j = 0; j < D64; j++) {
       int q = (t + T * j) & 15;
 #pragma unroll
-      for (int r = 0; r < 3; r++) l64[j][r] = mk_tw(g[oai4g_tw_offset(6) + (r + 1) * q]);
+      for (int r = 0; r < 3; r++) l64[j][r] = u2c(g[oai4g_tw_offset(6) + (r + 1) * q]);
     }
     if constexpr (HAS256) {
 #pragma unroll
       for (int j = 0; j < D256; j++) {
         int q = (t + T * j) & 63;
 #pragma unroll
-        for (int r = 0; r < 3; r++) l256[j][r] = mk_tw(g[oai4g_tw_offset(8) + (r + 1) * q]);
+        for (int r = 0; r < 3; r++) l256[j][r] = u2c(g[oai4g_tw_offset(8) + (r + 1) * q]);
       }
     }
     if constexpr (HAS1024) {
@@ -157,15 +159,17 @@ struct idft_tw_t {
       for (int j = 0; j < D1024; j++) {
         int q = (t + T * j) & 255;
 #pragma unroll
-        for (int r = 0; r < 3; r++) l1024[j][r] = mk_tw(g[oai4g_tw_offset(10) + (r + 1) * q]);
+        for (int r = 0; r < 3; r++) l1024[j][r] = u2c(g[oai4g_tw_offset(10) + (r + 1) * q]);
       }
     }
     if constexpr (HASR2) {
 #pragma unroll
-      for (int j = 0; j < DR2; j++) r2[j] = mk_tw(g[oai4g_tw_offset(LOG2N) + ((t + T * j) & (N / 2 - 1))]);
+      for (int j = 0; j < DR2; j++) r2[j] = u2c(g[oai4g_tw_offset(LOG2N) + ((t + T * j) & (N / 2 - 1))]);
     }
   }
 };
+
+static __device__ __forceinline__ twp_t tw_of(s16x2 t) { return {t, (s16x2){(short)(-(int)t.y), t.x}}; }
 
 /* leaf IDFT16 in registers (lte_dfts.c:1597-1724) */
 static __device__ __forceinline__ void idft16_reg(s16x2 *x, const twp_t *w16 /* W^{0,1,2,3,4,6,9} */)
@@ -188,44 +192,51 @@ static __device__ __forceinline__ void idft16_reg(s16x2 *x, const twp_t *w16 /* 
  * in LDS (group-major, NA buffers of LDSW words).  KIND: 0 = ibfly4_16 (64-level) then >>3,
  * 1 = ibfly4 then >>1.  Reads all operands, barrier, writes all results, barrier.
  */
-template <int LOG2N, int LOG2S, int KIND, int NA, int D>
-static __device__ __forceinline__ void idft_level_lds(uint32_t *lds, int t, const twp_t (&tw)[D][3])
+template <int LOG2N, int LOG2S, int KIND, int D>
+static __device__ __forceinline__ void idft_level_one(uint32_t *la, int t, const s16x2 (&tw)[D][3])
 {
-  constexpr int N = 1 << LOG2N, T = N >> 4, S = 1 << LOG2S, SC = S >> 2, GOUT = N / S, LDSW = N + (N >> 5);
-  s16x2 v[NA][4][4];
+  constexpr int N = 1 << LOG2N, T = N >> 4, S = 1 << LOG2S, SC = S >> 2, GOUT = N / S;
+  s16x2 v[4][4];
 #pragma unroll
   for (int j = 0; j < 4; j++) {
     const int b = t + T * j, q = b & (SC - 1), g = b >> (LOG2S - 2);
 #pragma unroll
-    for (int a = 0; a < NA; a++)
-#pragma unroll
-      for (int r = 0; r < 4; r++) v[a][j][r] = u2c(lds[a * LDSW + lphys((uint32_t)((g + GOUT * r) * SC + q))]);
+    for (int r = 0; r < 4; r++) v[j][r] = u2c(la[lphys((uint32_t)((g + GOUT * r) * SC + q))]);
   }
   __syncthreads();
 #pragma unroll
   for (int j = 0; j < 4; j++) {
     const int b = t + T * j, q = b & (SC - 1), g = b >> (LOG2S - 2);
-    const twp_t *w = tw[j % D];
+    const twp_t w[3] = {tw_of(tw[j % D][0]), tw_of(tw[j % D][1]), tw_of(tw[j % D][2])};
     const uint32_t base = (uint32_t)(g * S + q);
-#pragma unroll
-    for (int a = 0; a < NA; a++) {
-      s16x2 y0, y1, y2, y3;
-      if (KIND == 0) {
-        r4inv(v[a][j][0], cmulc16(v[a][j][1], w[0]), cmulc16(v[a][j][2], w[1]), cmulc16(v[a][j][3], w[2]), y0, y1,
-              y2, y3);
-        y0 = shr3(y0); y1 = shr3(y1); y2 = shr3(y2); y3 = shr3(y3);
-      } else {
-        ibfly4(v[a][j][0], v[a][j][1], v[a][j][2], v[a][j][3], w[0], w[1], w[2], y0, y1, y2, y3);
-        y0 = shr1(y0); y1 = shr1(y1); y2 = shr1(y2); y3 = shr1(y3);
-      }
-      uint32_t *la = lds + a * LDSW;
-      la[lphys(base)] = c2u(y0);
-      la[lphys(base + SC)] = c2u(y1);
-      la[lphys(base + 2 * SC)] = c2u(y2);
-      la[lphys(base + 3 * SC)] = c2u(y3);
+    s16x2 y0, y1, y2, y3;
+    if (KIND == 0) {
+      r4inv(v[j][0], cmulc16(v[j][1], w[0]), cmulc16(v[j][2], w[1]), cmulc16(v[j][3], w[2]), y0, y1, y2, y3);
+      y0 = shr3(y0); y1 = shr3(y1); y2 = shr3(y2); y3 = shr3(y3);
+    } else {
+      ibfly4(v[j][0], v[j][1], v[j][2], v[j][3], w[0], w[1], w[2], y0, y1, y2, y3);
+      y0 = shr1(y0); y1 = shr1(y1); y2 = shr1(y2); y3 = shr1(y3);
     }
+    la[lphys(base)] = c2u(y0);
+    la[lphys(base + SC)] = c2u(y1);
+    la[lphys(base + 2 * SC)] = c2u(y2);
+    la[lphys(base + 3 * SC)] = c2u(y3);
   }
   __syncthreads();
+}
+
+/*
+ * One intermediate combining level of size S = 2^LOG2S over NA transforms of N = 2^LOG2N held
+ * in LDS (group-major, NA buffers of LDSW words).  KIND: 0 = ibfly4_16 (64-level) then >>3,
+ * 1 = ibfly4 then >>1.  Per transform: read all operands, barrier, write all results, barrier
+ * (transforms in turn: 16 staged operands per thread instead of 16 NA).
+ */
+template <int LOG2N, int LOG2S, int KIND, int NA, int D>
+static __device__ __forceinline__ void idft_level_lds(uint32_t *lds, int t, const s16x2 (&tw)[D][3])
+{
+  constexpr int N = 1 << LOG2N, LDSW = N + (N >> 5);
+#pragma unroll
+  for (int a = 0; a < NA; a++) idft_level_one<LOG2N, LOG2S, KIND, D>(lds + a * LDSW, t, tw);
 }
 
 /*
@@ -273,7 +284,8 @@ static __device__ __forceinline__ void idft_unit(uint32_t *lds, int t, bool acti
 #pragma unroll
       for (int j = 0; j < 4; j++) {
         int q = t + T * j;
-        const twp_t *w = tw.l64[j % idft_tw_t<6>::D64];
+        const s16x2 *wt = tw.l64[j % idft_tw_t<6>::D64];
+        const twp_t w[3] = {tw_of(wt[0]), tw_of(wt[1]), tw_of(wt[2])};
 #pragma unroll
         for (int a = 0; a < NA; a++) {
           s16x2 y[4];
@@ -299,7 +311,7 @@ static __device__ __forceinline__ void idft_unit(uint32_t *lds, int t, bool acti
           for (int a = 0; a < NA; a++) {
             s16x2 y0, y1;
             ibfly2(u2c(lds[a * LDSW + lphys((uint32_t)q)]), u2c(lds[a * LDSW + lphys((uint32_t)(SC + q))]),
-                   tw.r2[j % DR2], y0, y1);
+                   tw_of(tw.r2[j % DR2]), y0, y1);
             if (scale) { y0 = mulhi2(y0); y1 = mulhi2(y1); }
             cons(a, q, y0);
             cons(a, q + SC, y1);
@@ -313,7 +325,8 @@ static __device__ __forceinline__ void idft_unit(uint32_t *lds, int t, bool acti
 #pragma unroll
         for (int j = 0; j < 4; j++) {
           int q = t + T * j;
-          const twp_t *w = (LOG2N == 8) ? tw.l256[j % idft_tw_t<LOG2N>::D256] : tw.l1024[j % idft_tw_t<LOG2N>::D1024];
+          const s16x2 *wt = (LOG2N == 8) ? tw.l256[j % idft_tw_t<LOG2N>::D256] : tw.l1024[j % idft_tw_t<LOG2N>::D1024];
+          const twp_t w[3] = {tw_of(wt[0]), tw_of(wt[1]), tw_of(wt[2])};
 #pragma unroll
           for (int a = 0; a < NA; a++) {
             s16x2 y[4];
@@ -440,8 +453,16 @@ struct modofdm_geom {
   static constexpr int EW = (6 * ((N * 5) / 8)) / 32 + 4;   /* staged e-bit words per codeword */
 };
 
+#ifndef OAI4G_MODOFDM_WAVES
+#define OAI4G_MODOFDM_WAVES 3   /* measured: 3 waves/SIMD (<=168 VGPRs) beats 2 (no cap) and 4 (spills) */
+#endif
+#if OAI4G_MODOFDM_WAVES > 0
+#define MODOFDM_ATTR __attribute__((amdgpu_waves_per_eu(OAI4G_MODOFDM_WAVES)))
+#else
+#define MODOFDM_ATTR
+#endif
 template <int LOG2N, int NA>
-__global__ void __launch_bounds__(128) k_modofdm(const cfg_dev_t *__restrict__ c, int n_items,
+__global__ void __launch_bounds__(128) MODOFDM_ATTR k_modofdm(const cfg_dev_t *__restrict__ c, int n_items,
                                                  const uint32_t *__restrict__ ebits, int32_t *__restrict__ iq)
 {
   using G = modofdm_geom<LOG2N>;
@@ -500,24 +521,25 @@ __global__ void __launch_bounds__(128) k_modofdm(const cfg_dev_t *__restrict__ c
     }
     __syncthreads();
 
-    const uint16_t *__restrict__ rm = c->remap + ((size_t)sfi * 14 + l) * N;
+    gu16_t *rm = (gu16_t *)(c->remap + ((size_t)sfi * 14 + l) * N);
     const uint32_t *e0 = lds_e[unit][0], *e1 = lds_e[unit][1];
     const uint32_t *q0 = qtab[0][pil], *q1 = qtab[1][pil];
     const uint32_t off0 = 32 * wlo0, off1 = 32 * wlo1;
     idft_unit<LOG2N, NA>(
         lds_data + unit * NA * LDSW, t, active, twr,
         [&](int n, s16x2 *x) {
+          /* branch-free so the 16 remap loads and LDS chains of a thread overlap; an RE outside
+           * the allocation reads data RE 0 (inside the staged words) and is zeroed by the select */
           const uint32_t code = rm[t + T * n];
-          s16x2 x0 = {0, 0}, x1 = {0, 0};
-          if (code != 0xFFFFu) {
-            const uint32_t idx = code & 0x7FFFu;
-            const uint32_t p0 = (idx + re0) * Qm0 - off0;
-            x0 = u2c(q0[__builtin_amdgcn_alignbit(e0[(p0 >> 5) + 1], e0[p0 >> 5], p0 & 31) & mask0]);
-            if (n_cw > 1) {
-              const uint32_t p1 = (idx + re0) * Qm1 - off1;
-              x1 = u2c(q1[__builtin_amdgcn_alignbit(e1[(p1 >> 5) + 1], e1[p1 >> 5], p1 & 31) & mask1]);
-            }
+          const bool valid = code != 0xFFFFu;
+          const uint32_t idx = valid ? (code & 0x7FFFu) : 0u;
+          const uint32_t p0 = (idx + re0) * Qm0 - off0;
+          uint32_t v0 = q0[__builtin_amdgcn_alignbit(e0[(p0 >> 5) + 1], e0[p0 >> 5], p0 & 31) & mask0], v1 = 0;
+          if (n_cw > 1) {
+            const uint32_t p1 = (idx + re0) * Qm1 - off1;
+            v1 = q1[__builtin_amdgcn_alignbit(e1[(p1 >> 5) + 1], e1[p1 >> 5], p1 & 31) & mask1];
           }
+          const s16x2 x0 = u2c(valid ? v0 : 0u), x1 = u2c(valid ? v1 : 0u);
           if constexpr (NA == 2) {
             cdd_pair(x0, x1, code >> 15 & 1u, x[0], x[1]);
           } else {
