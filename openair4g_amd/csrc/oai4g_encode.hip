@@ -486,11 +486,11 @@ static __device__ __forceinline__ uint32_t rm_window(const uint32_t *wpk, uint32
 template <bool DEBUG>
 static __device__ void encode_codeword(const cfg_dev_t *__restrict__ c, uint32_t sf, uint32_t cwi,
                                        const uint8_t *__restrict__ payload, uint32_t *__restrict__ ebits,
-                                       enc_debug_t dbg, uint32_t *lds_base, int stop_phase = 99)
+                                       enc_debug_t dbg, uint32_t *lds_base, int stop_phase = 99, uint32_t sf0 = 0)
 {
   const cw_dev_t &cw = c->cw[cwi];
   const uint32_t tid = threadIdx.x, nth = blockDim.x, wave = tid >> 6, lane = tid & 63, nwaves = nth >> 6;
-  const uint32_t sfi = DEBUG ? sf : (c->first_sf + sf * c->sf_step) % 10;
+  const uint32_t sfi = DEBUG ? sf : (c->first_sf + (sf0 + sf) * c->sf_step) % 10;
   const uint32_t C = cw.C, sw = cw.stream_words;
   /* LDS carve-up.  Region A: TB || CRC and the CRC tables (phases 0-2), the QPP-interleaved
    * words (phase 3), packed w (phase 4).  Region B: the constituent streams. */
@@ -774,12 +774,12 @@ static __device__ void encode_codeword(const cfg_dev_t *__restrict__ c, uint32_t
 }
 
 __global__ void __launch_bounds__(256) k_encode(const cfg_dev_t *__restrict__ c, const uint8_t *__restrict__ payload,
-                                                uint32_t *__restrict__ ebits, int stop_phase)
+                                                uint32_t *__restrict__ ebits, int stop_phase, uint32_t sf0)
 {
   extern __shared__ uint32_t lds_dyn[];
   uint32_t sf = blockIdx.x / c->n_cw, cwi = blockIdx.x % c->n_cw;
   enc_debug_t none = {nullptr, nullptr, nullptr, nullptr, nullptr};
-  encode_codeword<false>(c, sf, cwi, payload, ebits, none, lds_dyn, stop_phase);
+  encode_codeword<false>(c, sf, cwi, payload, ebits, none, lds_dyn, stop_phase, sf0);
 }
 
 __global__ void __launch_bounds__(256) k_encode_debug(const cfg_dev_t *__restrict__ c, uint32_t sf, uint32_t cwi,
@@ -796,17 +796,28 @@ static size_t enc_lds_bytes(const cfg_dev_t *h)
   return (bytes + 15) & ~(size_t)15;
 }
 
-hipError_t oai4g_launch_encode_phase(const cfg_dev_t *d_cfg, const cfg_dev_t *h_cfg, int n_sf,
+static hipError_t launch_encode_impl(const cfg_dev_t *d_cfg, const cfg_dev_t *h_cfg, int sf0, int n_sf,
                                      const uint8_t *d_payload, uint32_t *d_ebits, int stop_phase, hipStream_t s);
-hipError_t oai4g_launch_encode(const cfg_dev_t *d_cfg, const cfg_dev_t *h_cfg, int n_sf, const uint8_t *d_payload,
-                               uint32_t *d_ebits, hipStream_t s)
+
+/* subframes [sf0, sf0 + n_sf) of a batch whose payloads / e-bit words start at d_payload / d_ebits */
+hipError_t oai4g_launch_encode(const cfg_dev_t *d_cfg, const cfg_dev_t *h_cfg, int sf0, int n_sf,
+                               const uint8_t *d_payload, uint32_t *d_ebits, hipStream_t s)
 {
-  return oai4g_launch_encode_phase(d_cfg, h_cfg, n_sf, d_payload, d_ebits, 99, s);
+  return launch_encode_impl(d_cfg, h_cfg, sf0, n_sf, d_payload, d_ebits, 99, s);
 }
 
 hipError_t oai4g_launch_encode_phase(const cfg_dev_t *d_cfg, const cfg_dev_t *h_cfg, int n_sf,
                                      const uint8_t *d_payload, uint32_t *d_ebits, int stop_phase, hipStream_t s)
 {
+  return launch_encode_impl(d_cfg, h_cfg, 0, n_sf, d_payload, d_ebits, stop_phase, s);
+}
+
+static hipError_t launch_encode_impl(const cfg_dev_t *d_cfg, const cfg_dev_t *h_cfg, int sf0, int n_sf,
+                                     const uint8_t *d_payload, uint32_t *d_ebits, int stop_phase, hipStream_t s)
+{
+  if (n_sf <= 0) return hipSuccess;
+  d_payload += (size_t)sf0 * h_cfg->n_cw * h_cfg->payload_stride;
+  d_ebits += (size_t)sf0 * h_cfg->n_cw * h_cfg->ebits_words;
   size_t lds = enc_lds_bytes(h_cfg);
   static bool attr_set = false;
   if (!attr_set) {
@@ -814,7 +825,8 @@ hipError_t oai4g_launch_encode_phase(const cfg_dev_t *d_cfg, const cfg_dev_t *h_
     (void)hipFuncSetAttribute((const void *)k_encode_debug, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     attr_set = true;
   }
-  hipLaunchKernelGGL(k_encode, dim3(n_sf * h_cfg->n_cw), dim3(256), lds, s, d_cfg, d_payload, d_ebits, stop_phase);
+  hipLaunchKernelGGL(k_encode, dim3(n_sf * h_cfg->n_cw), dim3(256), lds, s, d_cfg, d_payload, d_ebits, stop_phase,
+                     (uint32_t)sf0);
   return hipGetLastError();
 }
 

@@ -16,6 +16,7 @@
 #define OAI4G_MAX_CB 16
 #define OAI4G_MAX_NULLS 104
 #define OAI4G_MAX_CHUNKS 192                /* 6144 / 32 */
+#define OAI4G_PIPE_MAX_CHUNKS 16
 #define OAI4G_ENC_CRC_TABLE_WORDS (256 + 256 + 8 * 96 + 6 * 96) /* byte tables A/B + tree multipliers */
 #define OAI4G_GOLD_LANES 256
 #define OAI4G_GOLD_STRIDE 16
@@ -103,7 +104,7 @@ struct cfg_dev_t {
 
 /* ---------------- launch helpers implemented in the .hip files ---------------- */
 /* encoder path */
-hipError_t oai4g_launch_encode(const cfg_dev_t *d_cfg, const cfg_dev_t *h_cfg, int n_sf,
+hipError_t oai4g_launch_encode(const cfg_dev_t *d_cfg, const cfg_dev_t *h_cfg, int sf0, int n_sf,
                                const uint8_t *d_payload, uint32_t *d_ebits, hipStream_t s);
 hipError_t oai4g_launch_encode_phase(const cfg_dev_t *d_cfg, const cfg_dev_t *h_cfg, int n_sf,
                                      const uint8_t *d_payload, uint32_t *d_ebits, int stop_phase, hipStream_t s);
@@ -127,8 +128,8 @@ hipError_t oai4g_launch_scramble_bytes(uint8_t *d_e, int n_entries, uint32_t c_i
 hipError_t oai4g_launch_fill(uint8_t *d, size_t bytes, uint64_t seed, hipStream_t s);
 
 /* OFDM path */
-hipError_t oai4g_launch_modofdm(const cfg_dev_t *d_cfg, const cfg_dev_t *h_cfg, int n_sf, const uint32_t *d_ebits,
-                                int32_t *d_iq, hipStream_t s);
+hipError_t oai4g_launch_modofdm(const cfg_dev_t *d_cfg, const cfg_dev_t *h_cfg, int sf0, int n_sf,
+                                const uint32_t *d_ebits, int32_t *d_iq, hipStream_t s);
 struct ofdm_sym_t {
   uint32_t in_off;   /* int32 index of the symbol's frequency-domain input */
   uint32_t out_off;  /* int32 index of the symbol's time-domain body (after the CP) */

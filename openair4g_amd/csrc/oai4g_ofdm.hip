@@ -463,7 +463,8 @@ struct modofdm_geom {
 #endif
 template <int LOG2N, int NA>
 __global__ void __launch_bounds__(128) MODOFDM_ATTR k_modofdm(const cfg_dev_t *__restrict__ c, int n_items,
-                                                 const uint32_t *__restrict__ ebits, int32_t *__restrict__ iq)
+                                                 const uint32_t *__restrict__ ebits, int32_t *__restrict__ iq,
+                                                 uint32_t sf0)
 {
   using G = modofdm_geom<LOG2N>;
   constexpr int N = G::N, T = G::T, UNITS = G::UNITS, LDSW = G::LDSW, EW = G::EW;
@@ -489,7 +490,7 @@ __global__ void __launch_bounds__(128) MODOFDM_ATTR k_modofdm(const cfg_dev_t *_
     const bool active = item < n_items;
     const uint32_t it = active ? (uint32_t)item : 0u;
     const uint32_t sf = it / nsymb, l = it - sf * nsymb;
-    const uint32_t sfi = (c->first_sf + sf * c->sf_step) % 10;
+    const uint32_t sfi = (c->first_sf + (sf0 + sf) * c->sf_step) % 10;
     const uint32_t nre = active ? c->symnre[sfi][l] : 0u, re0 = c->symbase[sfi][l];
     const uint32_t pil = pilots_of(l) != 0;
     /* output placement: slot = l / 7, symbol-in-slot i (normal CP) */
@@ -565,8 +566,8 @@ __global__ void __launch_bounds__(128) MODOFDM_ATTR k_modofdm(const cfg_dev_t *_
 }
 
 template <int LOG2N, int NA>
-static hipError_t launch_modofdm_t(const cfg_dev_t *d_cfg, const cfg_dev_t *h_cfg, int n_items, const uint32_t *d_ebits,
-                                   int32_t *d_iq, hipStream_t s)
+static hipError_t launch_modofdm_t(const cfg_dev_t *d_cfg, const cfg_dev_t *h_cfg, int sf0, int n_items,
+                                   const uint32_t *d_ebits, int32_t *d_iq, hipStream_t s)
 {
   static int occ = 0;
   if (!occ) {
@@ -577,26 +578,30 @@ static hipError_t launch_modofdm_t(const cfg_dev_t *d_cfg, const cfg_dev_t *h_cf
   int want = (n_items + units - 1) / units, cap = occ * (int)h_cfg->n_cu;
   int grid = want < cap ? want : cap;
   if (grid < 1) grid = 1;
-  hipLaunchKernelGGL((k_modofdm<LOG2N, NA>), dim3(grid), dim3(128), 0, s, d_cfg, n_items, d_ebits, d_iq);
+  hipLaunchKernelGGL((k_modofdm<LOG2N, NA>), dim3(grid), dim3(128), 0, s, d_cfg, n_items, d_ebits, d_iq, (uint32_t)sf0);
   return hipGetLastError();
 }
 
-hipError_t oai4g_launch_modofdm(const cfg_dev_t *d_cfg, const cfg_dev_t *h_cfg, int n_sf, const uint32_t *d_ebits,
-                                int32_t *d_iq, hipStream_t s)
+/* subframes [sf0, sf0 + n_sf) of a batch whose e-bit words / IQ start at d_ebits / d_iq */
+hipError_t oai4g_launch_modofdm(const cfg_dev_t *d_cfg, const cfg_dev_t *h_cfg, int sf0, int n_sf,
+                                const uint32_t *d_ebits, int32_t *d_iq, hipStream_t s)
 {
+  if (n_sf <= 0) return hipSuccess;
   const int n_items = n_sf * (int)h_cfg->nsymb;
+  d_ebits += (size_t)sf0 * h_cfg->n_cw * h_cfg->ebits_words;
+  d_iq += (size_t)sf0 * h_cfg->n_ant * h_cfg->spt;
   /* two antenna transforms per unit only when they differ (LARGE_CDD); TM1 stores one n_ant times */
   const bool two = h_cfg->mimo_mode == OAI4G_LARGE_CDD && h_cfg->n_ant == 2;
   if (h_cfg->mimo_mode == OAI4G_LARGE_CDD && h_cfg->n_ant != 2) return hipErrorInvalidValue;
   switch (h_cfg->log2N) {
-  case 7: return two ? launch_modofdm_t<7, 2>(d_cfg, h_cfg, n_items, d_ebits, d_iq, s)
-                     : launch_modofdm_t<7, 1>(d_cfg, h_cfg, n_items, d_ebits, d_iq, s);
-  case 8: return two ? launch_modofdm_t<8, 2>(d_cfg, h_cfg, n_items, d_ebits, d_iq, s)
-                     : launch_modofdm_t<8, 1>(d_cfg, h_cfg, n_items, d_ebits, d_iq, s);
-  case 10: return two ? launch_modofdm_t<10, 2>(d_cfg, h_cfg, n_items, d_ebits, d_iq, s)
-                      : launch_modofdm_t<10, 1>(d_cfg, h_cfg, n_items, d_ebits, d_iq, s);
-  case 11: return two ? launch_modofdm_t<11, 2>(d_cfg, h_cfg, n_items, d_ebits, d_iq, s)
-                      : launch_modofdm_t<11, 1>(d_cfg, h_cfg, n_items, d_ebits, d_iq, s);
+  case 7: return two ? launch_modofdm_t<7, 2>(d_cfg, h_cfg, sf0, n_items, d_ebits, d_iq, s)
+                     : launch_modofdm_t<7, 1>(d_cfg, h_cfg, sf0, n_items, d_ebits, d_iq, s);
+  case 8: return two ? launch_modofdm_t<8, 2>(d_cfg, h_cfg, sf0, n_items, d_ebits, d_iq, s)
+                     : launch_modofdm_t<8, 1>(d_cfg, h_cfg, sf0, n_items, d_ebits, d_iq, s);
+  case 10: return two ? launch_modofdm_t<10, 2>(d_cfg, h_cfg, sf0, n_items, d_ebits, d_iq, s)
+                      : launch_modofdm_t<10, 1>(d_cfg, h_cfg, sf0, n_items, d_ebits, d_iq, s);
+  case 11: return two ? launch_modofdm_t<11, 2>(d_cfg, h_cfg, sf0, n_items, d_ebits, d_iq, s)
+                      : launch_modofdm_t<11, 1>(d_cfg, h_cfg, sf0, n_items, d_ebits, d_iq, s);
   default: return hipErrorInvalidValue;
   }
 }
