@@ -12,7 +12,6 @@ barriers / max-reduction of the timing harness).
     python bench.py [--gpus N] [--steps K] [--warmup W] [--config C3] [--batch 2048]
 """
 import argparse
-import ctypes
 import json
 import os
 import sys
@@ -83,19 +82,13 @@ def main():
     import openair4g_amd as oai
     oai.init()
 
-    # ---- parameter block: built on rank 0, broadcast over RCCL ----
-    nbytes = ctypes.sizeof(oai.TxParams)
-    if rank == 0:
-        p0 = oai.make_params(args.config, subframe=args.subframe)
-        blob = torch.tensor(list(p0.to_bytes()), dtype=torch.uint8, device="cuda")
-    else:
-        blob = torch.zeros(nbytes, dtype=torch.uint8, device="cuda")
-    if dist is not None:
-        dist.broadcast(blob, src=0)
-    params = oai.TxParams.from_bytes(bytes(blob.cpu().numpy().tobytes()))
+    from openair4g_amd import dist as odist
+    # ---- parameter block: built on rank 0, broadcast over RCCL (the only collective) ----
+    p0 = oai.make_params(args.config, subframe=args.subframe) if rank == 0 else None
+    params = odist.broadcast_params(p0, dist, device="cuda") if dist is not None else p0
 
     pipe = oai.TxPipeline(params, args.batch)
-    pipe.fill_payload(seed=0x5EED0000 + rank)   # this rank's shard of synthetic transport blocks
+    pipe.fill_payload(seed=odist.payload_seed(0x5EED0000, rank))   # this rank's shard of synthetic TBs
     pipe.sync()
 
     for _ in range(args.warmup):

@@ -1,0 +1,133 @@
+"""Textbook 3GPP model of the PDSCH coding chain — TEST INFRASTRUCTURE ONLY.
+
+Written from the specification's definitions (bit lists, polynomials, matrices), deliberately
+unlike the oracle's implementation, to pin the oracle's coding stages where the reference's
+own translation units cannot be built here ("Oracle and pinning"):
+
+  crc24(bits, poly)       36.212 5.1.1  (CRC24A / CRC24B generator polynomials)
+  turbo_encode(c, f1, f2) 36.212 5.1.3.2 (PCCC, 8-state RSC g0 = 1+D^2+D^3, g1 = 1+D+D^3,
+                          QPP interleaver, trellis termination), returned in the reference's
+                          d layout: (x_k, z_k, z'_k) per bit, then the 12 tail bits
+  subblock(d_streams)     36.212 5.1.4.1.1 (32-column interleaver, bitrev column permutation,
+                          the pi(k) rule for d^(2)) and the bit collection w
+  rate_match(...)         36.212 5.1.4.1.2 (Ncb, E per block, k0, circular selection)
+  gold(c_init, n)         36.211 7.2 (length-31 Gold sequence, Nc = 1600)
+
+Pure Python loops: use the small sizes of the CPU suite.
+"""
+NULL = 2
+CRC24A = [24, 23, 18, 17, 14, 11, 10, 7, 6, 5, 4, 3, 1, 0]
+CRC24B = [24, 23, 6, 5, 1, 0]
+COLPERM = [0, 16, 8, 24, 4, 20, 12, 28, 2, 18, 10, 26, 6, 22, 14, 30,
+           1, 17, 9, 25, 5, 21, 13, 29, 3, 19, 11, 27, 7, 23, 15, 31]
+
+
+def bytes_to_bits(data, nbits):
+    """MSB-first bit list (a_0 is the MSB of byte 0)."""
+    return [(data[i >> 3] >> (7 - (i & 7))) & 1 for i in range(nbits)]
+
+
+def crc24(bits, taps):
+    """Parity bits p_0..p_23 of 36.212 5.1.1: a(D) D^24 mod g(D), highest power first."""
+    g = [0] * 25
+    for t in taps:
+        g[24 - t] = 1          # g[0] is the D^24 coefficient
+    reg = list(bits) + [0] * 24
+    for i in range(len(bits)):
+        if reg[i]:
+            for j in range(25):
+                reg[i + j] ^= g[j]
+    return reg[len(bits):]
+
+
+def qpp(K, f1, f2):
+    return [(f1 * i + f2 * i * i) % K for i in range(K)]
+
+
+def _rsc(bits):
+    """8-state RSC of 36.212 5.1.3.2.1: returns (z, tail_x, tail_z)."""
+    s = [0, 0, 0]                       # shift register contents D^1, D^2, D^3
+    z = []
+    for c in bits:
+        a = c ^ s[1] ^ s[2]             # feedback g0 = 1 + D^2 + D^3
+        z.append(a ^ s[0] ^ s[2])       # output g1 = 1 + D + D^3
+        s = [a, s[0], s[1]]
+    tx, tz = [], []
+    for _ in range(3):                  # termination: input = feedback, so a = 0
+        x = s[1] ^ s[2]
+        tx.append(x)
+        tz.append(s[0] ^ s[2])
+        s = [0, s[0], s[1]]
+    return z, tx, tz
+
+
+def turbo_encode(c_bits, f1, f2):
+    """d in the reference layout (3K + 12 entries)."""
+    K = len(c_bits)
+    pi = qpp(K, f1, f2)
+    z, tx, tz = _rsc(c_bits)
+    z2, tx2, tz2 = _rsc([c_bits[pi[i]] for i in range(K)])
+    d = []
+    for k in range(K):
+        d += [c_bits[k], z[k], z2[k]]
+    for i in range(3):
+        d += [tx[i], tz[i]]
+    for i in range(3):
+        d += [tx2[i], tz2[i]]
+    return d
+
+
+def streams_from_d(d, K):
+    """d^(0), d^(1), d^(2) (length D = K + 4 each) from the interleaved d layout."""
+    D = K + 4
+    return [[d[3 * k + s] for k in range(D)] for s in range(3)]
+
+
+def subblock(streams):
+    """v^(0), v^(1), v^(2) and w (36.212 5.1.4.1.1 / 5.1.4.1.2)."""
+    D = len(streams[0])
+    R = (D + 31) // 32
+    Kpi = 32 * R
+    ND = Kpi - D
+    ys = [[NULL] * ND + list(st) for st in streams]
+    v = []
+    for s in (0, 1):
+        y = ys[s]
+        v.append([y[32 * row + COLPERM[col]] for col in range(32) for row in range(R)])
+    y2 = ys[2]
+    v.append([y2[(COLPERM[k // R] + 32 * (k % R) + 1) % Kpi] for k in range(Kpi)])
+    w = list(v[0])
+    for k in range(Kpi):
+        w += [v[1][k], v[2][k]]
+    return R, w
+
+
+def rate_match(w, R, G, C, r, Qm, Nl=1, rv=0, Nsoft=1827072, Kmimo=1, Mdlharq=8):
+    """e_0..e_{E-1} of code block r; None when Ncb < Kw (the reference's limited-buffer exit)."""
+    Kw = 3 * 32 * R
+    Nir = Nsoft // (Kmimo * min(Mdlharq, 8))
+    Ncb = min(Nir // C, Kw)
+    if Ncb < Kw:
+        return None
+    Gp = G // (Nl * Qm)
+    gamma = Gp % C
+    E = Nl * Qm * (Gp // C) if r <= C - gamma - 1 else Nl * Qm * (-(-Gp // C))
+    k0 = R * (2 * (-(-Ncb // (8 * R))) * rv + 2)
+    e, j = [], 0
+    while len(e) < E:
+        x = w[(k0 + j) % Ncb]
+        if x != NULL:
+            e.append(x)
+        j += 1
+    return e
+
+
+def gold(c_init, n):
+    """c(0..n-1) of 36.211 7.2."""
+    Nc = 1600
+    x1 = [1] + [0] * 30
+    x2 = [(c_init >> i) & 1 for i in range(31)]
+    for m in range(Nc + n - 31):
+        x1.append(x1[m + 3] ^ x1[m])
+        x2.append(x2[m + 3] ^ x2[m + 2] ^ x2[m + 1] ^ x2[m])
+    return [x1[i + Nc] ^ x2[i + Nc] for i in range(n)]

@@ -1,0 +1,162 @@
+"""CPU suite: pins the oracle (test infrastructure) before it is trusted as the GPU checker.
+
+  - IDFT/OFDM: bit-exact against the reference's own lte_dfts.c outputs (tests/golden/idft_ref.npz,
+    made by tests/golden/gen_golden.py from oracle/_ref), and live against oracle/_ref when built.
+  - CRC-24A/B: the published CRC-catalogue check values (CRC-24/LTE-A 0xCDE703, CRC-24/LTE-B
+    0x23EF52 over "123456789").
+  - G: REFERENCE_DATA/pdsch.txt known answers (G 13800 / 1512 / 27600 / 41400) and SURVEY.md 8a.
+  - Turbo encoder, sub-block interleaver, rate matcher, Gold sequence: agreement with the
+    36.212 / 36.211 textbook model in tests/spec_model.py.
+  - Whole-subframe regression: the oracle reproduces tests/golden/pipeline_C1.npz.
+"""
+import os
+
+import numpy as np
+import pytest
+
+import oracle_lib as O
+import spec_model as S
+
+GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+
+
+def aligned_i16(n):
+    buf = np.zeros(n + 32, dtype=np.int16)
+    off = (-buf.ctypes.data % 64) // 2
+    return buf[off:off + n]
+
+
+# ---------------------------------------------------------------- IDFT (pinned to the reference)
+def test_idft_matches_reference_fixture():
+    z = np.load(os.path.join(GOLDEN, "idft_ref.npz"))
+    n_checked = 0
+    for key in z.files:
+        if not key.startswith("x_"):
+            continue
+        _, n, vi, scale = key.split("_")
+        y = O.idft(z[key], scale=int(scale))
+        assert np.array_equal(y, z[f"y_{n}_{vi}_{scale}"]), key
+        n_checked += 1
+    assert n_checked == 20
+
+
+@pytest.mark.skipif(O.ref_dfts() is None, reason="oracle/_ref not built (reference tree absent)")
+@pytest.mark.parametrize("log2n", [6, 7, 8, 10, 11])
+def test_idft_matches_reference_live(log2n):
+    ref = O.ref_dfts()
+    n = 1 << log2n
+    rng = np.random.default_rng(log2n)
+    for amp in (512, 4096, 32768):
+        x, y = aligned_i16(2 * n), aligned_i16(2 * n)     # the SSE code needs 16-byte alignment
+        x[:] = rng.integers(-amp, amp, 2 * n).astype(np.int16)
+        getattr(ref, f"idft{n}")(O.P(x), O.P(y), 1)
+        assert np.array_equal(O.idft(x, 1), y)
+
+
+# ---------------------------------------------------------------- CRC (catalogue check values)
+def test_crc_catalogue_check_values():
+    msg = np.frombuffer(b"123456789", dtype=np.uint8)
+    assert O.crc24a(msg, 72) >> 8 == 0xCDE703
+    assert O.crc24b(msg, 72) >> 8 == 0x23EF52
+
+
+@pytest.mark.parametrize("nbytes", [1, 3, 17, 117, 575])
+def test_crc_matches_spec_model(nbytes):
+    rng = np.random.default_rng(nbytes)
+    data = rng.integers(0, 256, nbytes, dtype=np.uint8)
+    bits = S.bytes_to_bits(data, 8 * nbytes)
+    for fn, taps in ((O.crc24a, S.CRC24A), (O.crc24b, S.CRC24B)):
+        p = S.crc24(bits, taps)
+        assert fn(data, 8 * nbytes) >> 8 == int("".join(map(str, p)), 2)
+
+
+# ---------------------------------------------------------------- G (pdsch.txt known answers)
+@pytest.mark.parametrize("N_RB,mcs,pdcch,G", [(50, 5, 2, 13800), (6, 4, 3, 1512), (50, 15, 2, 27600),
+                                               (50, 26, 2, 41400)])
+def test_get_G_reference_data(N_RB, mcs, pdcch, G):
+    """REFERENCE_DATA/pdsch.txt:7,16,24,71 (dlsim, 1 TX, full allocation, subframe 7)."""
+    fp = O.frame(N_RB)
+    Qm = O.orc().orc_get_Qm(mcs)
+    alloc = [(1 << min(32, max(0, N_RB - 32 * i))) - 1 & 0xFFFFFFFF for i in range(4)]
+    assert O.get_G(N_RB, 0, 1, 0, N_RB, alloc, Qm, 1, pdcch, 7) == G
+
+
+def test_get_G_survey_configs():
+    import openair4g_amd as oai
+    for name, G in (("C1", 1512), ("C2", 60000), ("C3", 86400)):
+        p = oai.make_params(name, subframe=7)
+        fp = O.frame(p.N_RB_DL, p.Nid_cell, p.Ncp, p.nb_antennas_tx, p.mode1_flag, p.frame_type)
+        Qm = O.orc().orc_get_Qm(p.mcs[0])
+        assert O.get_G(fp.N_RB_DL, 0, fp.mode1_flag, 0, p.nb_rb, list(p.rb_alloc), Qm, 1, p.num_pdcch_symbols,
+                       7) == G
+
+
+# ---------------------------------------------------------------- QPP table (36.212 Table 5.1.3-3)
+def test_qpp_table_is_the_spec_table():
+    sizes = list(range(40, 513, 8)) + list(range(528, 1025, 16)) + list(range(1056, 2049, 32)) + \
+        list(range(2112, 6145, 64))
+    import re
+    src = open(os.path.join(os.path.dirname(O.ORACLE_DIR), "include", "oai4g_qpp.c")).read()
+    rows = [tuple(map(int, r)) for r in re.findall(r"\{\s*(\d+)\s*,\s*(\d+)\s*,\s*(\d+)\s*\}", src)]
+    assert [r[0] for r in rows] == sizes
+    for K, f1, f2 in rows:
+        assert f1 % 2 == 1 and f2 % 2 == 0
+        assert len(set(S.qpp(K, f1, f2))) == K          # a permutation
+
+
+# ---------------------------------------------------------------- turbo encoder (36.212 5.1.3.2)
+@pytest.mark.parametrize("K,f1,f2", [(40, 3, 10), (48, 7, 12), (512, 31, 64), (1024, 31, 64), (6144, 263, 480)])
+def test_turbo_matches_spec_model(K, f1, f2):
+    rng = np.random.default_rng(K)
+    c = rng.integers(0, 256, K // 8, dtype=np.uint8)
+    d = O.turbo_encode(c, f1, f2)
+    ref = S.turbo_encode(S.bytes_to_bits(c, K), f1, f2)
+    assert d.tolist() == ref
+
+
+# ---------------------------------------------------------------- sub-block interleaver + RM
+@pytest.mark.parametrize("K,C,r,G,Qm,rv", [(40, 1, 0, 1512, 2, 0), (960, 1, 0, 1512, 2, 0),
+                                           (1024, 3, 1, 6000, 4, 0), (6144, 6, 5, 86400, 6, 0),
+                                           (6144, 5, 0, 60000, 4, 2), (512, 2, 1, 3000, 2, 3)])
+def test_subblock_and_rate_matching_match_spec_model(K, C, r, G, Qm, rv):
+    rng = np.random.default_rng(K + r)
+    d = rng.integers(0, 2, 3 * K + 12).astype(np.uint8)
+    D = K + 4
+    rtc, w, _ = O.subblock(d, D)
+    R, w_spec = S.subblock(S.streams_from_d(d.tolist(), K))
+    assert rtc == R
+    assert w.tolist() == w_spec
+    e = O.rate_match(rtc, G, w, C, r, Qm, rvidx=rv)
+    e_spec = S.rate_match(w_spec, R, G, C, r, Qm, rv=rv)
+    assert e.tolist() == e_spec
+
+
+def test_rate_matching_limited_buffer_exit():
+    """Ncb < Kw: the reference prints and returns E = 0 (lte_rate_matching.c:518-521)."""
+    d = np.zeros(3 * 6144 + 12, dtype=np.uint8)
+    rtc, w, _ = O.subblock(d, 6148)
+    # Kmimo 2, Mdlharq 8: Nir = 114192; C = 7 blocks of Kw = 18528 do not fit (C = 6 does)
+    assert len(O.rate_match(rtc, 100800, w, 7, 0, 6, Kmimo=2)) == 0
+    assert S.rate_match([0] * len(w), rtc, 100800, 7, 0, 6, Kmimo=2) is None
+    assert len(O.rate_match(rtc, 86400, w, 6, 0, 6, Kmimo=2)) == 14400
+
+
+# ---------------------------------------------------------------- Gold sequence (36.211 7.2)
+@pytest.mark.parametrize("c_init", [0x1234 << 14 | 7 << 9, 1, 0x7FFFFFFF])
+def test_gold_matches_spec_model(c_init):
+    import ctypes
+    x1, x2 = ctypes.c_uint32(0), ctypes.c_uint32(c_init)
+    words = [O.orc().orc_gold_generic(ctypes.byref(x1), ctypes.byref(x2), 1)]
+    words += [O.orc().orc_gold_generic(ctypes.byref(x1), ctypes.byref(x2), 0) for _ in range(7)]
+    c = S.gold(c_init, 256)
+    assert [(w >> b) & 1 for w in words for b in range(32)] == c
+
+
+# ---------------------------------------------------------------- whole-subframe regression
+def test_oracle_reproduces_c1_fixture():
+    import openair4g_amd as oai
+    z = np.load(os.path.join(GOLDEN, "pipeline_C1.npz"))
+    for sf in (0, 5, 7):
+        p = oai.make_params("C1", subframe=sf)
+        txd, _, _ = O.tx_subframe(O.tx_cfg_from_params(p, sf), [z[f"payload0_{sf}"]])
+        assert np.array_equal(txd, z[f"iq_{sf}"])
