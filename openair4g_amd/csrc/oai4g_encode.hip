@@ -1032,3 +1032,31 @@ hipError_t oai4g_launch_fill(uint8_t *d, size_t bytes, uint64_t seed, hipStream_
   hipLaunchKernelGGL(k_fill, dim3(1024), dim3(256), 0, s, d, bytes, seed);
   return hipGetLastError();
 }
+
+/* =======================================================================================
+ * PMC calibration (diagnostic): stream a known byte count with the access width the
+ * pipeline kernels use (4 B per lane, coalesced), mode 0 = read, 1 = write.  rocprofv3's
+ * FETCH_SIZE / WRITE_SIZE of this dispatch calibrate the counters (MI355X_MICROARCH.md:
+ * "other access widths are uncalibrated").
+ * ===================================================================================== */
+__global__ void __launch_bounds__(256) k_diag_stream(const uint32_t *__restrict__ src, uint32_t *__restrict__ dst,
+                                                     size_t n_words, int mode)
+{
+  const size_t stride = (size_t)gridDim.x * blockDim.x;
+  size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (mode == 1) {
+    for (; i < n_words; i += stride) dst[i] = (uint32_t)i;
+    return;
+  }
+  uint32_t acc = 0;
+  for (; i < n_words; i += stride) acc ^= src[i];
+  if (acc == 0x9e3779b9u) dst[0] = acc;    /* keeps the loads live; practically never stores */
+}
+
+hipError_t oai4g_launch_diag_stream(const void *src, void *dst, size_t bytes, int mode, hipStream_t s)
+{
+  hipLaunchKernelGGL(k_diag_stream, dim3(4096), dim3(256), 0, s, (const uint32_t *)src, (uint32_t *)dst, bytes / 4,
+                     mode);
+  return hipGetLastError();
+}
+

@@ -840,6 +840,14 @@ extern "C" int oai4g_diag_encode_phase_ms(const oai4g_tx_config_t *cfg, int n_sf
   return 0;
 }
 
+/* PMC calibration: stream `bytes` at 4 B per lane (mode 0 read from src, 1 write to dst) */
+extern "C" int oai4g_diag_stream(const void *d_src, void *d_dst, size_t bytes, int mode, void *stream)
+{
+  NEED_INIT(-1);
+  HCK(oai4g_launch_diag_stream(d_src, d_dst, bytes, mode, (hipStream_t)stream), -1);
+  return 0;
+}
+
 /* ------------------------------------------------------------------------------------------
  * device memory helpers
  * ---------------------------------------------------------------------------------------- */

@@ -126,6 +126,7 @@ hipError_t oai4g_launch_rm_bytes(const uint8_t *d_w, uint32_t Ncb, uint32_t k0, 
 hipError_t oai4g_launch_scramble_bytes(uint8_t *d_e, int n_entries, uint32_t c_init, const uint32_t *d_gold_x1,
                                        const uint32_t *d_gold_x2j, hipStream_t s);
 hipError_t oai4g_launch_fill(uint8_t *d, size_t bytes, uint64_t seed, hipStream_t s);
+hipError_t oai4g_launch_diag_stream(const void *src, void *dst, size_t bytes, int mode, hipStream_t s);
 
 /* OFDM path */
 hipError_t oai4g_launch_modofdm(const cfg_dev_t *d_cfg, const cfg_dev_t *h_cfg, int sf0, int n_sf,
