@@ -148,6 +148,14 @@ void oai4g_normal_prefix_mod(const int32_t *txdataF, int32_t *txdata, uint8_t ns
 /* do_OFDM_mod (ofdm_mod.c:233, decl MODULATION/defs.h:90); PMCH subframes not supported */
 void oai4g_do_OFDM_mod(int32_t **txdataF, int32_t **txdata, uint32_t frame, uint16_t next_slot,
                        const oai4g_frame_parms_t *frame_parms);
+/* generate_pilots (PHY/LTE_TRANSPORT/pilots.c:43, decl proto.h): CRS into txdataF[ant] for
+ * Ntti subframes (the reference's frame grid; overwrites the pilot REs).  The reference passes
+ * PHY_VARS_eNB for its frame parameters and Gold table; here the table is derived from fp. */
+void oai4g_generate_pilots(int32_t **txdataF, int16_t amp, const oai4g_frame_parms_t *frame_parms, uint16_t Ntti);
+/* lte_dl_cell_spec (PHY/LTE_REFSIG/lte_dl_cell_spec.c:123): CRS of port p, pilot l (0/1) of slot
+ * Ns into one OFDM symbol `output` (ofdm_symbol_size REs).  Returns 0, or -1 for a bad port. */
+int oai4g_lte_dl_cell_spec(int32_t *output, int16_t amp, const oai4g_frame_parms_t *frame_parms, uint8_t Ns,
+                           uint8_t l, uint8_t p);
 /* idft64..idft2048 (PHY/TOOLS/lte_dfts.c:1856-2866, decl TOOLS/defs.h:555): y = IDFT(x) */
 int oai4g_idft(int log2n, const int16_t *x, int16_t *y, int scale);
 void oai4g_idft2048(const int16_t *x, int16_t *y, int scale);
@@ -172,7 +180,7 @@ typedef struct {
   uint8_t Mdlharq;
   uint8_t first_subframe;     /* subframe index of batch element 0 */
   uint8_t subframe_step;      /* 0: every element uses first_subframe; 1: consecutive subframes */
-  uint8_t pad0;
+  uint8_t with_crs;           /* 1: cell-specific reference signals in the grid (pilots.c:43) */
   uint16_t rnti;
   int16_t amp;
   int16_t sqrt_rho_a;

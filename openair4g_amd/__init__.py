@@ -67,7 +67,7 @@ class TxParams(ctypes.Structure):
                 ("nb_antennas_tx", ctypes.c_uint8), ("mode1_flag", ctypes.c_uint8), ("frame_type", ctypes.c_uint8),
                 ("n_cw", ctypes.c_uint8), ("mimo_mode", ctypes.c_uint8), ("num_pdcch_symbols", ctypes.c_uint8),
                 ("Kmimo", ctypes.c_uint8), ("Mdlharq", ctypes.c_uint8), ("first_subframe", ctypes.c_uint8),
-                ("subframe_step", ctypes.c_uint8), ("pad0", ctypes.c_uint8), ("rnti", ctypes.c_uint16),
+                ("subframe_step", ctypes.c_uint8), ("with_crs", ctypes.c_uint8), ("rnti", ctypes.c_uint16),
                 ("amp", ctypes.c_int16), ("sqrt_rho_a", ctypes.c_int16), ("sqrt_rho_b", ctypes.c_int16),
                 ("rb_alloc", ctypes.c_uint32 * 4), ("nb_rb", ctypes.c_uint16), ("mcs", ctypes.c_uint8 * 2),
                 ("rvidx", ctypes.c_uint8 * 2), ("q", ctypes.c_uint8 * 2), ("TBS", ctypes.c_uint32 * 2),
@@ -120,6 +120,10 @@ _SIGS = {
     "oai4g_normal_prefix_mod": (None, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint8, ctypes.POINTER(FrameParms)]),
     "oai4g_do_OFDM_mod": (None, [ctypes.POINTER(ctypes.c_void_p), ctypes.POINTER(ctypes.c_void_p), ctypes.c_uint32,
                                  ctypes.c_uint16, ctypes.POINTER(FrameParms)]),
+    "oai4g_generate_pilots": (None, [ctypes.POINTER(ctypes.c_void_p), ctypes.c_int16, ctypes.POINTER(FrameParms),
+                                     ctypes.c_uint16]),
+    "oai4g_lte_dl_cell_spec": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int16, ctypes.POINTER(FrameParms),
+                                              ctypes.c_uint8, ctypes.c_uint8, ctypes.c_uint8]),
     "oai4g_idft": (ctypes.c_int, [ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int]),
     "oai4g_idft2048": (None, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int]),
     "oai4g_idft1024": (None, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int]),
@@ -282,6 +286,21 @@ def ofdm_mod(grid, log2n, nb_symbols, cp):
     return out
 
 
+def generate_pilots(grids, amp, fp, ntti=10):
+    """generate_pilots (pilots.c:43): CRS into the frame grids (list of int32 arrays, in place)."""
+    init()
+    ptrs = (ctypes.c_void_p * 2)(*[g.ctypes.data for g in grids] + [None] * (2 - len(grids)))
+    lib().oai4g_generate_pilots(ptrs, amp, ctypes.byref(fp), ntti)
+    return grids
+
+
+def lte_dl_cell_spec(symbol, amp, fp, Ns, l, p):
+    """lte_dl_cell_spec (lte_dl_cell_spec.c:123): CRS into one OFDM symbol (int32 array, in place)."""
+    init()
+    _check(lib().oai4g_lte_dl_cell_spec(_ptr(symbol), amp, ctypes.byref(fp), Ns, l, p) == 0)
+    return symbol
+
+
 def normal_prefix_mod(txdataF, fp, nsymb=7, out=None):
     init()
     txdataF = np.ascontiguousarray(txdataF, dtype=np.int32)
@@ -358,7 +377,7 @@ CONFIGS = {
 }
 
 
-def make_params(name="C3", subframe=7, subframe_step=0, rnti=0x1234, Nid_cell=0, **over):
+def make_params(name="C3", subframe=7, subframe_step=0, rnti=0x1234, Nid_cell=0, with_crs=0, **over):
     c = dict(CONFIGS[name])
     c.update(over)
     p = TxParams()
@@ -375,6 +394,7 @@ def make_params(name="C3", subframe=7, subframe_step=0, rnti=0x1234, Nid_cell=0,
     p.Mdlharq = 8
     p.first_subframe = subframe
     p.subframe_step = subframe_step
+    p.with_crs = with_crs
     p.rnti = rnti
     p.amp = 512
     p.sqrt_rho_a = 8192

@@ -70,6 +70,41 @@ static void gold_step_h(uint32_t *x1, uint32_t *x2)
   *x2 = *x2 ^ (*x2 << 31) ^ (*x2 << 30) ^ (*x2 << 29) ^ (*x2 << 28);
 }
 
+/* lte_gold (LTE_REFSIG/lte_gold.c:52-93): CRS Gold words [ns][pilot l][14] */
+static void lte_gold_table_h(const oai4g_frame_parms_t *fp, uint32_t t[20][2][14])
+{
+  const uint32_t Ncp = 1 - fp->Ncp, Nid = fp->Nid_cell;
+  for (uint32_t ns = 0; ns < 20; ns++)
+    for (uint32_t l = 0; l < 2; l++) {
+      uint32_t x1 = 1u + (1u << 31);
+      uint32_t x2 = Ncp + (Nid << 1) + (((1 + (Nid << 1)) * (1 + (fp->Ncp == 0 ? 4 : 3) * l + 7 * (1 + ns))) << 10);
+      x2 ^= (x2 ^ (x2 >> 1) ^ (x2 >> 2) ^ (x2 >> 3)) << 31;
+      for (int n = 1; n < 50; n++) gold_step_h(&x1, &x2);
+      for (int n = 0; n < 14; n++) {
+        gold_step_h(&x1, &x2);
+        t[ns][l][n] = x1 ^ x2;
+      }
+    }
+}
+
+/* CRS pilot RE of port p, pilot l (0: symbol 0 of the slot, 1: symbol 4 / 3), index m
+ * (lte_dl_cell_spec.c:147-200): subcarrier bin and QPSK index into qpsk[] */
+static uint32_t crs_bin(const oai4g_frame_parms_t *fp, uint32_t p, uint32_t l, uint32_t m)
+{
+  const uint32_t nu = (p == 0) ? (l == 0 ? 0 : 3) : (l == 0 ? 3 : 0);
+  uint32_t k = nu + fp->nushift;
+  if (k > 5) k -= 6;
+  k += fp->first_carrier_offset + 6 * m;
+  if (k >= fp->ofdm_symbol_size) k = k + 1 - fp->ofdm_symbol_size;     /* DC skip */
+  return k;
+}
+static uint32_t crs_qpsk(int16_t amp, uint32_t idx)
+{
+  const int16_t a = (int16_t)((amp * 23170) >> 15);                  /* ONE_OVER_SQRT2_Q15 */
+  const int16_t re = (idx & 1) ? (int16_t)-a : a, im = (idx & 2) ? (int16_t)-a : a;
+  return (uint16_t)re | ((uint32_t)(uint16_t)im << 16);
+}
+
 static void do_init(void)
 {
   int n = 0;
@@ -466,6 +501,8 @@ struct oai4g_tx_config {
   cfg_dev_t *d = nullptr;           /* device copy */
   uint16_t *d_remap = nullptr;
   std::vector<uint16_t> h_remap;
+  uint32_t *d_crs = nullptr;
+  std::vector<uint32_t> h_crs;          /* [10][4][200] packed CRS IQ */
   int re_count[10];
   /* optional pipelined batches (OAI4G_PIPE_CHUNK=n): the encoder runs on the caller's stream, the
    * modulator/IDFT on s_mod, chunk by chunk.  Off by default: measured slower on MI355X than the
@@ -668,6 +705,27 @@ static int derive_cfg(oai4g_tx_config *cfg, const oai4g_tx_params_t *p, const ui
                           h.symbase[sf]);
       if (n < 0) { set_err("RE map construction failed"); return -1; }
       cfg->re_count[sf] = n;
+      if (p->with_crs) {
+        /* pilots.c:43-168: port 0 on antenna 0; antenna 1 port 0 (mode1) or port 1 */
+        if (fp.Ncp != 0) { set_err("CRS in the batched path supports normal CP only"); return -1; }
+        uint32_t gt[20][2][14];
+        lte_gold_table_h(&fp, gt);
+        const uint32_t psym[4] = {0, 4, 7, 11};
+        const int nports = (fp.nb_antennas_tx > 1 && !fp.mode1_flag) ? 2 : 1;
+        cfg->h_crs.resize((size_t)10 * 4 * 200);
+        for (uint32_t i = 0; i < 4; i++) {
+          const uint32_t Ns = 2 * sf + (i >> 1), l = i & 1;
+          for (uint32_t m = 0; m < 2u * fp.N_RB_DL; m++) {
+            const uint32_t mp = 110 - fp.N_RB_DL + m;
+            cfg->h_crs[((size_t)sf * 4 + i) * 200 + m] = crs_qpsk(p->amp, (gt[Ns][l][mp >> 4] >> (2 * (mp & 15))) & 3);
+            for (int port = 0; port < nports; port++) {
+              uint16_t &code = cfg->h_remap[((size_t)sf * 14 + psym[i]) * N + crs_bin(&fp, port, l, m)];
+              if (code != 0xFFFF) { set_err("CRS RE collides with a PDSCH RE"); return -1; }
+              code = (uint16_t)(OAI4G_CRS_CODE | (i << 9) | ((uint32_t)port << 8) | m);
+            }
+          }
+        }
+      }
       for (int l = 0; l < 14; l++) {
         uint32_t next = l + 1 < (int)h.nsymb ? h.symbase[sf][l + 1] : (uint32_t)n;
         h.symnre[sf][l] = (uint16_t)(l < p->num_pdcch_symbols || l >= (int)h.nsymb ? 0 : next - h.symbase[sf][l]);
@@ -689,6 +747,12 @@ static int upload_cfg(oai4g_tx_config *cfg)
     HCK(hipMemcpy(cfg->d_remap, cfg->h_remap.data(), cfg->h_remap.size() * 2, hipMemcpyHostToDevice), -1);
   }
   cfg->h.remap = cfg->d_remap;
+  if (!cfg->h_crs.empty()) {
+    HCK(hipMalloc(&cfg->d_crs, cfg->h_crs.size() * 4), -1);
+    HCK(hipMemcpy(cfg->d_crs, cfg->h_crs.data(), cfg->h_crs.size() * 4, hipMemcpyHostToDevice), -1);
+  }
+  cfg->h.crs_tab = cfg->d_crs;
+  cfg->h.with_crs = cfg->d_crs ? 1u : 0u;
   cfg->h.n_cu = (uint32_t)g_n_cu;
   cfg->h.gold_x1 = g_gx1;
   cfg->h.gold_x2j = g_gx2j;
@@ -708,6 +772,8 @@ static void release_cfg(oai4g_tx_config *cfg)
   cfg->ev_done = nullptr;
   if (cfg->d) hipFree(cfg->d);
   if (cfg->d_remap) hipFree(cfg->d_remap);
+  if (cfg->d_crs) hipFree(cfg->d_crs);
+  cfg->d_crs = nullptr;
   cfg->d = nullptr;
   cfg->d_remap = nullptr;
 }
@@ -1308,6 +1374,68 @@ extern "C" void oai4g_do_OFDM_mod(int32_t **txdataF, int32_t **txdata, uint32_t 
     else
       oai4g_normal_prefix_mod(txdataF[aa] + slot_offset_F, txdata[aa] + slot_offset, 7, fp);
   }
+}
+
+/* ------------------------------------------------------------------------------------------
+ * Cell-specific reference signals (pilots.c:43-168, lte_dl_cell_spec.c:123-203)
+ * ---------------------------------------------------------------------------------------- */
+static int run_crs(int32_t *const *grids, int n_grids, size_t grid_res, const crs_job_t *jobs, int n_jobs, int16_t amp,
+                   const oai4g_frame_parms_t *fp)
+{
+  uint32_t gt[20][2][14];
+  lte_gold_table_h(fp, gt);
+  const size_t gbytes = sizeof(gt), jbytes = (size_t)n_jobs * sizeof(crs_job_t), dbytes = (size_t)n_grids * grid_res * 4;
+  uint8_t *buf = scratch(gbytes + jbytes + dbytes + 256);
+  if (!buf) return -1;
+  uint32_t *d_gold = (uint32_t *)buf;
+  crs_job_t *d_jobs = (crs_job_t *)(buf + ((gbytes + 15) & ~(size_t)15));
+  int32_t *d_grid = (int32_t *)(buf + ((gbytes + 15) & ~(size_t)15) + ((jbytes + 255) & ~(size_t)255));
+  HCK(hipMemcpyAsync(d_gold, gt, gbytes, hipMemcpyHostToDevice, g_scr.s), -1);
+  HCK(hipMemcpyAsync(d_jobs, jobs, jbytes, hipMemcpyHostToDevice, g_scr.s), -1);
+  for (int g = 0; g < n_grids; g++)
+    HCK(hipMemcpyAsync(d_grid + g * grid_res, grids[g], grid_res * 4, hipMemcpyHostToDevice, g_scr.s), -1);
+  HCK(oai4g_launch_crs(d_grid, d_jobs, n_jobs, d_gold, amp, fp->ofdm_symbol_size, fp->N_RB_DL, fp->nushift,
+                       fp->first_carrier_offset, g_scr.s), -1);
+  for (int g = 0; g < n_grids; g++)
+    HCK(hipMemcpyAsync(grids[g], d_grid + g * grid_res, grid_res * 4, hipMemcpyDeviceToHost, g_scr.s), -1);
+  HCK(hipStreamSynchronize(g_scr.s), -1);
+  return 0;
+}
+
+extern "C" void oai4g_generate_pilots(int32_t **txdataF, int16_t amp, const oai4g_frame_parms_t *fp, uint16_t Ntti)
+{
+  NEED_INIT();
+  const uint32_t N = fp->ofdm_symbol_size, Nsymb = fp->Ncp == 0 ? 14 : 12, second = fp->Ncp == 0 ? 4 : 3;
+  const int n_ant = fp->nb_antennas_tx > 1 ? 2 : 1;
+  std::vector<crs_job_t> jobs;
+  for (uint32_t tti = 0; tti < Ntti; tti++) {
+    const uint32_t base = tti * N * Nsymb, slot = (tti * 2) % 20;
+    const uint32_t sym[4] = {0, second, Nsymb >> 1, (Nsymb >> 1) + second};
+    for (int i = 0; i < 4; i++)
+      for (int a = 0; a < n_ant; a++) {
+        const size_t grid_res = (size_t)Ntti * N * Nsymb;
+        crs_job_t j;
+        j.off = (uint32_t)(a * grid_res + base + sym[i] * N);
+        j.Ns = (uint8_t)(slot + (i >> 1));
+        j.l = (uint8_t)(i & 1);
+        j.p = (uint8_t)(a == 0 || fp->mode1_flag ? 0 : 1);
+        j.pad = 0;
+        jobs.push_back(j);
+      }
+  }
+  run_crs(txdataF, n_ant, (size_t)Ntti * N * Nsymb, jobs.data(), (int)jobs.size(), amp, fp);
+}
+
+extern "C" int oai4g_lte_dl_cell_spec(int32_t *output, int16_t amp, const oai4g_frame_parms_t *fp, uint8_t Ns,
+                                      uint8_t l, uint8_t p)
+{
+  NEED_INIT(-1);
+  if (p > 1 || l > 1 || Ns >= 20) {
+    set_err("lte_dl_cell_spec: p %d, l %d -> ERROR", p, l);
+    return -1;
+  }
+  crs_job_t j = {0, Ns, l, p, 0};
+  return run_crs(&output, 1, fp->ofdm_symbol_size, &j, 1, amp, fp);
 }
 
 extern "C" int oai4g_idft(int log2n, const int16_t *x, int16_t *y, int scale)

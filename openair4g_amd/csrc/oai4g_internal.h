@@ -17,6 +17,7 @@
 #define OAI4G_MAX_NULLS 104
 #define OAI4G_MAX_CHUNKS 192                /* 6144 / 32 */
 #define OAI4G_PIPE_MAX_CHUNKS 16
+#define OAI4G_CRS_CODE 0xE000u               /* remap codes >= this (and != 0xFFFF) are CRS REs */
 #define OAI4G_ENC_CRC_TABLE_WORDS (256 + 256 + 8 * 96 + 6 * 96) /* byte tables A/B + tree multipliers */
 #define OAI4G_GOLD_LANES 256
 #define OAI4G_GOLD_STRIDE 16
@@ -96,7 +97,10 @@ struct cfg_dev_t {
   uint32_t symbase[10][14];     /* data REs before symbol l */
   uint16_t symnre[10][14];      /* data REs in symbol l */
   uint32_t n_cu;                /* compute units of the device (persistent grids) */
-  const uint16_t *remap;        /* [10][14][N] data-RE index | parity<<15, 0xFFFF = none */
+  const uint16_t *remap;        /* [10][14][N] data-RE index | parity<<15; OAI4G_CRS_CODE | pilot
+                                   symbol<<9 | port<<8 | m for a CRS RE; 0xFFFF = none */
+  uint32_t with_crs;
+  const uint32_t *crs_tab;      /* [10][4][200] packed CRS IQ of pilot symbol i (l = 0, 4, 7, 11), index m */
   const uint32_t *gold_x1;      /* [256]     x1 state after 50+16l word steps */
   const uint32_t *gold_x2j;     /* [256][32] columns of M2^(50+16l) */
   const uint32_t *tw;           /* 2 x OAI4G_TW_TOTAL packed twiddles t, then (-t.im, t.re) */
@@ -126,6 +130,14 @@ hipError_t oai4g_launch_rm_bytes(const uint8_t *d_w, uint32_t Ncb, uint32_t k0, 
 hipError_t oai4g_launch_scramble_bytes(uint8_t *d_e, int n_entries, uint32_t c_init, const uint32_t *d_gold_x1,
                                        const uint32_t *d_gold_x2j, hipStream_t s);
 hipError_t oai4g_launch_fill(uint8_t *d, size_t bytes, uint64_t seed, hipStream_t s);
+/* CRS into nsym_grids OFDM-symbol grids: job j writes grid `out + jobs[j].off` (N REs) with port
+ * jobs[j].p, pilot l of slot Ns from gold[Ns][l][14] */
+struct crs_job_t {
+  uint32_t off;
+  uint8_t Ns, l, p, pad;
+};
+hipError_t oai4g_launch_crs(int32_t *d_out, const crs_job_t *jobs, int n_jobs, const uint32_t *d_gold, int16_t amp,
+                            uint32_t N, uint32_t N_RB, uint32_t nushift, uint32_t first_carrier, hipStream_t s);
 hipError_t oai4g_launch_diag_stream(const void *src, void *dst, size_t bytes, int mode, hipStream_t s);
 
 /* OFDM path */

@@ -405,6 +405,8 @@ static __device__ __forceinline__ int pilots_of(uint32_t l)
 {
   return (l == 4 || l == 11) ? 2 : (l == 7 ? 1 : 0);  /* normal CP (dlsch_modulation.c:1268-1282) */
 }
+/* CRS-bearing symbols of a normal-CP subframe (pilots.c:43-168) */
+static __device__ __forceinline__ bool pilots_any(uint32_t l) { return l == 0 || l == 4 || l == 7 || l == 11; }
 
 /* QAM symbol from Qm bits b0..b(Qm-1) packed LSB-first in `bits` (dlsch_modulation.c:245-355). */
 static __device__ __forceinline__ s16x2 qam_map(uint32_t bits, uint32_t Qm, const int16_t *tab, int16_t gain)
@@ -499,7 +501,7 @@ __global__ void __launch_bounds__(128) MODOFDM_ATTR k_modofdm(const cfg_dev_t *_
     const int cp = (int)(si == 0 ? c->cp0 : c->cp);
     uint32_t *dst0 = (uint32_t *)iq + (size_t)sf * n_ant * c->spt + body;
 
-    if (UNITS == 1 && nre == 0) {
+    if (UNITS == 1 && nre == 0 && !(c->with_crs && pilots_any(l))) {
       /* control-region symbol: the transform of an all-zero grid is zero */
       if (active)
         for (uint32_t a = 0; a < n_ant; a++) {
@@ -523,6 +525,8 @@ __global__ void __launch_bounds__(128) MODOFDM_ATTR k_modofdm(const cfg_dev_t *_
     __syncthreads();
 
     gu16_t *rm = (gu16_t *)(c->remap + ((size_t)sfi * 14 + l) * N);
+    gu32_t *crs_tab = (gu32_t *)c->crs_tab;
+    const bool crs = c->with_crs != 0 && pilots_any(l);
     const uint32_t *e0 = lds_e[unit][0], *e1 = lds_e[unit][1];
     const uint32_t *q0 = qtab[0][pil], *q1 = qtab[1][pil];
     const uint32_t off0 = 32 * wlo0, off1 = 32 * wlo1;
@@ -532,7 +536,7 @@ __global__ void __launch_bounds__(128) MODOFDM_ATTR k_modofdm(const cfg_dev_t *_
           /* branch-free so the 16 remap loads and LDS chains of a thread overlap; an RE outside
            * the allocation reads data RE 0 (inside the staged words) and is zeroed by the select */
           const uint32_t code = rm[t + T * n];
-          const bool valid = code != 0xFFFFu;
+          const bool valid = code < OAI4G_CRS_CODE;               /* a PDSCH data RE */
           const uint32_t idx = valid ? (code & 0x7FFFu) : 0u;
           const uint32_t p0 = (idx + re0) * Qm0 - off0;
           uint32_t v0 = q0[__builtin_amdgcn_alignbit(e0[(p0 >> 5) + 1], e0[p0 >> 5], p0 & 31) & mask0], v1 = 0;
@@ -545,6 +549,15 @@ __global__ void __launch_bounds__(128) MODOFDM_ATTR k_modofdm(const cfg_dev_t *_
             cdd_pair(x0, x1, code >> 15 & 1u, x[0], x[1]);
           } else {
             x[0] = cdd ? (s16x2){(short)(((int)x0.x + (int)x1.x) >> 1), (short)(((int)x0.y + (int)x1.y) >> 1)} : x0;
+          }
+          if (crs) {
+            /* cell-specific RS (pilots.c:43-168): overwrite the antenna carrying port p */
+            const bool pil_re = code >= OAI4G_CRS_CODE && code != 0xFFFFu;
+            const uint32_t ci = (code >> 9) & 3u, m = code & 0xFFu, port = (code >> 8) & 1u;
+            const uint32_t pv = pil_re ? crs_tab[(sfi * 4 + ci) * 200 + m] : 0u;
+#pragma unroll
+            for (int a = 0; a < NA; a++)
+              if (pil_re) x[a] = (NA == 1 || (uint32_t)a == port) ? u2c(pv) : (s16x2){0, 0};
           }
         },
         [&](int a, int f, s16x2 y) {
@@ -619,7 +632,7 @@ __global__ void __launch_bounds__(256) k_modulate_bytes(const cfg_dev_t *__restr
   if (gid >= nsymb * N) return;
   uint32_t l = gid / N, k = gid % N;
   uint32_t code = c->remap[((size_t)sfi * 14 + l) * N + k];
-  if (code == 0xFFFFu) return;
+  if (code >= OAI4G_CRS_CODE) return;                 /* no data RE (CRS codes included) */
   const cw_dev_t &cw0 = c->cw[0];
   const cw_dev_t &cw1 = c->cw[1];
   bool pil = pilots_of(l) != 0;
@@ -647,3 +660,35 @@ hipError_t oai4g_launch_modulate_bytes(const cfg_dev_t *d_cfg, const cfg_dev_t *
   hipLaunchKernelGGL(k_modulate_bytes, dim3((n + 255) / 256), dim3(256), 0, s, d_cfg, sf, d_e0, d_e1, d_grid);
   return hipGetLastError();
 }
+
+/* ======================================================================================
+ * Drop-in CRS: lte_dl_cell_spec (lte_dl_cell_spec.c:123-203) for a list of OFDM symbols.
+ * Thread per (job, m); bin = first_carrier + (nu + nushift) mod 6 + 6m with the DC skip.
+ * ==================================================================================== */
+__global__ void __launch_bounds__(256) k_crs(int32_t *__restrict__ out, const crs_job_t *__restrict__ jobs,
+                                             const uint32_t *__restrict__ gold, int16_t amp, uint32_t N,
+                                             uint32_t N_RB, uint32_t nushift, uint32_t first_carrier)
+{
+  const crs_job_t j = jobs[blockIdx.y];
+  const uint32_t m = blockIdx.x * blockDim.x + threadIdx.x;
+  if (m >= 2 * N_RB) return;
+  const uint32_t nu = (j.p == 0) ? (j.l == 0 ? 0u : 3u) : (j.l == 0 ? 3u : 0u);
+  uint32_t k = nu + nushift;
+  if (k > 5) k -= 6;
+  k += first_carrier + 6 * m;
+  if (k >= N) k = k + 1 - N;
+  const uint32_t mp = 110 - N_RB + m;
+  const uint32_t idx = (gold[((uint32_t)j.Ns * 2 + j.l) * 14 + (mp >> 4)] >> (2 * (mp & 15))) & 3u;
+  const short a = (short)(((int)amp * 23170) >> 15);
+  out[j.off + k] = (int32_t)c2u((s16x2){(short)((idx & 1) ? -a : a), (short)((idx & 2) ? -a : a)});
+}
+
+hipError_t oai4g_launch_crs(int32_t *d_out, const crs_job_t *jobs, int n_jobs, const uint32_t *d_gold, int16_t amp,
+                            uint32_t N, uint32_t N_RB, uint32_t nushift, uint32_t first_carrier, hipStream_t s)
+{
+  if (n_jobs <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_crs, dim3((2 * N_RB + 255) / 256, n_jobs), dim3(256), 0, s, d_out, jobs, d_gold, amp, N, N_RB,
+                     nushift, first_carrier);
+  return hipGetLastError();
+}
+

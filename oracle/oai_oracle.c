@@ -650,6 +650,83 @@ void orc_normal_prefix_mod(const int32_t *txdataF, int32_t *txdata, uint8_t nsym
  * Whole subframe — dlsim.c:2567-2699 (dlsch_encoding dlsch_coding.c:254-419,
  * dlsch_scrambling, dlsch_modulation, do_OFDM_mod_l x2 slots).  DCI and pilots excluded.
  * ==================================================================================== */
+/* ======================================================================================
+ * Cell-specific reference signals.
+ * ==================================================================================== */
+/* lte_gold (lte_gold.c:52-93): c_init = 2^10 (7(ns+1) + l' + 1)(2 Nid + 1) + 2 Nid + N_CP with
+ * l' = 0 or 4 (3 for extended CP); words n = 0..13 after the 1600-bit warm-up */
+void orc_lte_gold_table(const orc_frame_t *fp, uint32_t table[20][2][14])
+{
+  uint32_t Ncp = 1 - fp->Ncp, Nid = fp->Nid_cell;
+  for (uint32_t ns = 0; ns < 20; ns++)
+    for (uint32_t l = 0; l < 2; l++) {
+      uint32_t x1, x2 = Ncp + (Nid << 1) + (((1 + (Nid << 1)) * (1 + ((fp->Ncp == 0) ? 4 : 3) * l + 7 * (1 + ns))) << 10);
+      /* lte_gold.c:82-91: 49 warm-up word steps, then 14 stored words; the first stored word is
+       * the state after 50 steps, which is what orc_gold_generic(reset = 1) returns */
+      table[ns][l][0] = orc_gold_generic(&x1, &x2, 1);
+      for (uint32_t n = 1; n < 14; n++) table[ns][l][n] = orc_gold_generic(&x1, &x2, 0);
+    }
+}
+
+/* lte_dl_cell_spec (lte_dl_cell_spec.c:123-203) */
+int orc_lte_dl_cell_spec(int32_t *output, int16_t amp, const orc_frame_t *fp, const uint32_t table[20][2][14],
+                         uint8_t Ns, uint8_t l, uint8_t p)
+{
+  int16_t a = (int16_t)((amp * 23170) >> 15);              /* ONE_OVER_SQRT2_Q15 */
+  int32_t qpsk[4];
+  int16_t *q = (int16_t *)qpsk;
+  q[0] = a;  q[1] = a;  q[2] = -a;  q[3] = a;  q[4] = a;  q[5] = -a;  q[6] = -a;  q[7] = -a;
+  uint32_t nu;
+  if (p == 0) nu = l == 0 ? 0 : 3;
+  else if (p == 1) nu = l == 0 ? 3 : 0;
+  else return -1;
+  uint32_t mprime = 110 - fp->N_RB_DL, k = nu + fp->nushift;
+  if (k > 5) k -= 6;
+  k += fp->first_carrier_offset;
+  for (uint32_t m = 0; m < 2u * fp->N_RB_DL; m++, mprime++) {
+    output[k] = qpsk[(table[Ns][l][mprime >> 4] >> (2 * (mprime & 15))) & 3];
+    k += 6;
+    if (k >= fp->ofdm_symbol_size) {
+      k++;                                                   /* skip DC carrier */
+      k -= fp->ofdm_symbol_size;
+    }
+  }
+  return 0;
+}
+
+/* pilots.c:43-168 for the symbols of one subframe grid: port 0 on antenna 0; antenna 1 gets
+ * port 0 too in mode1 (single-port CRS), port 1 otherwise */
+static void pilots_one(int32_t **grid, int16_t amp, const orc_frame_t *fp, const uint32_t table[20][2][14],
+                       uint32_t slot_offset)
+{
+  uint32_t N = fp->ofdm_symbol_size, Nsymb = fp->Ncp == 0 ? 14 : 12, second = fp->Ncp == 0 ? 4 : 3;
+  const uint32_t sym[4] = {0, second, Nsymb >> 1, (Nsymb >> 1) + second};
+  for (int i = 0; i < 4; i++) {
+    uint8_t Ns = (uint8_t)(slot_offset + (i >> 1)), l = (uint8_t)(i & 1);
+    orc_lte_dl_cell_spec(grid[0] + sym[i] * N, amp, fp, table, Ns, l, 0);
+    if (fp->nb_antennas_tx > 1) orc_lte_dl_cell_spec(grid[1] + sym[i] * N, amp, fp, table, Ns, l, fp->mode1_flag ? 0 : 1);
+  }
+}
+
+void orc_generate_pilots(int32_t **txdataF, int16_t amp, const orc_frame_t *fp, uint16_t Ntti)
+{
+  static uint32_t table[20][2][14];
+  orc_lte_gold_table(fp, table);
+  uint32_t Nsymb = fp->Ncp == 0 ? 14 : 12;
+  for (uint32_t tti = 0; tti < Ntti; tti++) {
+    int32_t *g[2] = {txdataF[0] + tti * fp->ofdm_symbol_size * Nsymb,
+                     fp->nb_antennas_tx > 1 ? txdataF[1] + tti * fp->ofdm_symbol_size * Nsymb : NULL};
+    pilots_one(g, amp, fp, table, (tti * 2) % 20);
+  }
+}
+
+void orc_generate_pilots_subframe(int32_t **txdataF, int16_t amp, const orc_frame_t *fp, uint8_t subframe)
+{
+  static uint32_t table[20][2][14];
+  orc_lte_gold_table(fp, table);
+  pilots_one(txdataF, amp, fp, table, (2u * subframe) % 20);
+}
+
 int orc_tx_subframe(const orc_tx_cfg_t *cfg, uint8_t *payload[2], int32_t **txdataF, int32_t **txdata,
                     uint8_t *e_out[2])
 {
@@ -692,6 +769,7 @@ int orc_tx_subframe(const orc_tx_cfg_t *cfg, uint8_t *payload[2], int32_t **txda
   memcpy(c1.rb_alloc, cfg->rb_alloc, sizeof(c1.rb_alloc));
   int N = fp->ofdm_symbol_size, nsymb = fp->symbols_per_tti;
   for (int aa = 0; aa < fp->nb_antennas_tx; aa++) memset(txdataF[aa], 0, sizeof(int32_t) * N * nsymb);
+  if (cfg->with_crs) orc_generate_pilots_subframe(txdataF, cfg->amp, fp, cfg->subframe);   /* dlsim.c:2681-2684 */
   int ret = modulation_impl(txdataF, cfg->amp, cfg->subframe, 0, fp, cfg->num_pdcch_symbols, &c0,
                             cfg->n_cw > 1 ? &c1 : NULL, cfg->sqrt_rho_a, cfg->sqrt_rho_b);
   for (int aa = 0; aa < fp->nb_antennas_tx; aa++)

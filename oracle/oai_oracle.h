@@ -100,7 +100,17 @@ void orc_ofdm_mod(const int32_t *input, int32_t *output, uint8_t log2fftsize, ui
                   uint16_t nb_prefix_samples);
 void orc_normal_prefix_mod(const int32_t *txdataF, int32_t *txdata, uint8_t nsymb, const orc_frame_t *fp);
 
-/* ---- whole-subframe TX (dlsim.c:2567-2699 minus DCI/pilots) ----
+/* ---- cell-specific reference signals (LTE_REFSIG/lte_gold.c:52-93, lte_dl_cell_spec.c:123-203,
+ *      LTE_TRANSPORT/pilots.c:43-168) ---- */
+void orc_lte_gold_table(const orc_frame_t *fp, uint32_t table[20][2][14]);
+int  orc_lte_dl_cell_spec(int32_t *output, int16_t amp, const orc_frame_t *fp, const uint32_t table[20][2][14],
+                          uint8_t Ns, uint8_t l, uint8_t p);
+/* txdataF[ant] spans Ntti subframes of nsymb * ofdm_symbol_size REs (the reference's frame grid) */
+void orc_generate_pilots(int32_t **txdataF, int16_t amp, const orc_frame_t *fp, uint16_t Ntti);
+/* the same for one subframe grid (txdataF[ant] = 14 * N REs of subframe `subframe`) */
+void orc_generate_pilots_subframe(int32_t **txdataF, int16_t amp, const orc_frame_t *fp, uint8_t subframe);
+
+/* ---- whole-subframe TX (dlsim.c:2567-2699 minus DCI; pilots when cfg->with_crs) ----
  * payload[cw] holds TBS/8 bytes (+3 bytes of room; the CRC is appended in place as in the
  * reference).  txdata[ant] receives samples_per_tti int32 samples.  Returns 0 on success. */
 typedef struct {
@@ -119,6 +129,7 @@ typedef struct {
   uint8_t rvidx[2];
   uint8_t q[2];            /* scrambling codeword index (dlsim.c:2646 passes 0) */
   uint32_t TBS[2];
+  uint8_t with_crs;        /* 1: cell-specific reference signals in the grid (generate_pilots) */
 } orc_tx_cfg_t;
 int orc_tx_subframe(const orc_tx_cfg_t *cfg, uint8_t *payload[2], int32_t **txdataF, int32_t **txdata,
                     uint8_t *e_out[2] /* optional: scrambled e bytes per cw */);

@@ -37,7 +37,7 @@ class OrcTxCfg(ctypes.Structure):
                 ("amp", ctypes.c_int16), ("sqrt_rho_a", ctypes.c_int16), ("sqrt_rho_b", ctypes.c_int16),
                 ("Kmimo", ctypes.c_uint8), ("Mdlharq", ctypes.c_uint8), ("rb_alloc", ctypes.c_uint32 * 4),
                 ("nb_rb", ctypes.c_uint16), ("mcs", ctypes.c_uint8 * 2), ("rvidx", ctypes.c_uint8 * 2),
-                ("q", ctypes.c_uint8 * 2), ("TBS", ctypes.c_uint32 * 2)]
+                ("q", ctypes.c_uint8 * 2), ("TBS", ctypes.c_uint32 * 2), ("with_crs", ctypes.c_uint8)]
 
 
 def build():
@@ -71,6 +71,9 @@ def orc():
         L.orc_idft.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int]
         L.orc_ofdm_mod.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint8, ctypes.c_uint8, ctypes.c_uint16]
         L.orc_normal_prefix_mod.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint8, ctypes.POINTER(OrcFrame)]
+        L.orc_generate_pilots.argtypes = [ctypes.c_void_p, ctypes.c_int16, ctypes.POINTER(OrcFrame), ctypes.c_uint16]
+        L.orc_generate_pilots_subframe.argtypes = [ctypes.c_void_p, ctypes.c_int16, ctypes.POINTER(OrcFrame),
+                                                   ctypes.c_uint8]
         _orc = L
     return _orc
 
@@ -168,6 +171,7 @@ def tx_cfg_from_params(p, subframe):
         c.rvidx[cw] = p.rvidx[cw]
         c.q[cw] = p.q[cw]
         c.TBS[cw] = p.TBS[cw]
+    c.with_crs = getattr(p, "with_crs", 0)
     return c
 
 
@@ -192,3 +196,13 @@ def tx_subframe(cfg, payloads, want_e=False):
     rc = orc().orc_tx_subframe(ctypes.byref(cfg), pay, fptrs, dptrs, eptrs if want_e else None)
     assert rc == 0
     return np.stack(txd), np.stack(txF), es
+
+
+def generate_pilots(fp, amp, ntti=10):
+    """Reference-layout frame grid(s) with CRS (pilots.c:43-168): [n_ant][ntti * 14 * N] int32."""
+    N = fp.ofdm_symbol_size
+    grids = [np.zeros(ntti * fp.symbols_per_tti * N, dtype=np.int32) for _ in range(fp.nb_antennas_tx)]
+    ptrs = (ctypes.c_void_p * 2)(*[g.ctypes.data for g in grids] + [None] * (2 - len(grids)))
+    orc().orc_generate_pilots(ptrs, amp, ctypes.byref(fp), ntti)
+    return grids
+

@@ -12,6 +12,7 @@ own translation units cannot be built here ("Oracle and pinning")
                           the pi(k) rule for d^(2)) and the bit collection w
   rate_match(...)         36.212 5.1.4.1.2 (Ncb, E per block, k0, circular selection)
   gold(c_init, n)         36.211 7.2 (length-31 Gold sequence, Nc = 1600)
+  crs(...)                36.211 6.10.1 (cell-specific reference signals: sequence and mapping)
 
 Pure Python loops: use the small sizes of the CPU suite.
 """
@@ -131,3 +132,27 @@ def gold(c_init, n):
         x1.append(x1[m + 3] ^ x1[m])
         x2.append(x2[m + 3] ^ x2[m + 2] ^ x2[m + 1] ^ x2[m])
     return [x1[i + Nc] ^ x2[i + Nc] for i in range(n)]
+
+
+def crs(N_RB, Nid, subframe, port, amp, N, first_carrier, Ncp=0):
+    """Cell-specific RS of one subframe, 36.211 6.10.1 (normal CP): {(l, fft_bin): (I, Q)} with the
+    QPSK amplitude (amp * 23170) >> 15.  Subcarrier k maps to bin first_carrier + k below DC and
+    to k - 6 N_RB + 1 above it (the DC bin is skipped)."""
+    a = (amp * 23170) >> 15
+    out = {}
+    nsymb = 7
+    for slot in (0, 1):
+        ns = 2 * subframe + slot
+        for lsym in (0, nsymb - 3):
+            c_init = (1 << 10) * (7 * (ns + 1) + lsym + 1) * (2 * Nid + 1) + 2 * Nid + (1 - Ncp)
+            c = gold(c_init, 4 * 110)
+            if port == 0:
+                nu = 0 if lsym == 0 else 3
+            else:
+                nu = 3 if lsym == 0 else 0
+            for m in range(2 * N_RB):
+                mp = m + 110 - N_RB
+                k = 6 * m + (nu + Nid % 6) % 6
+                fbin = first_carrier + k if k < 6 * N_RB else k - 6 * N_RB + 1
+                out[(slot * nsymb + lsym, fbin)] = (a * (1 - 2 * c[2 * mp]), a * (1 - 2 * c[2 * mp + 1]))
+    return out

@@ -196,3 +196,41 @@ def test_pipeline_full_size_c3(gpu):
     assert np.array_equal(iq1, iq2)
     # every subframe carries signal on both antennas
     assert np.all(np.abs(iq1.view(np.int16)).reshape(n_sf, -1).max(axis=1) > 0)
+
+
+# ---------------------------------------------------------------- CRS (A12)
+@pytest.mark.parametrize("name,n_sf,first,step,nid", [("C1", 10, 0, 1, 0), ("C2", 4, 4, 1, 77), ("C3", 10, 0, 1, 301)])
+def test_pipeline_with_crs_bit_exact(gpu, name, n_sf, first, step, nid):
+    p = gpu.make_params(name, subframe=first, subframe_step=step, Nid_cell=nid, with_crs=1)
+    pipe = gpu.TxPipeline(p, n_sf)
+    rng = np.random.default_rng(nid + n_sf)
+    pay = rng.integers(0, 256, size=(n_sf, p.n_cw, p.payload_stride), dtype=np.uint8)
+    pipe.upload_payload(pay)
+    pipe.run()
+    pipe.sync()
+    iq = pipe.iq()
+    for i in range(n_sf):
+        sf = (first + i * step) % 10
+        txd_o, _, _ = O.tx_subframe(O.tx_cfg_from_params(p, sf), [pay[i, cw] for cw in range(p.n_cw)])
+        assert np.array_equal(iq[i], txd_o), (name, i)
+    pipe.close()
+
+
+@pytest.mark.parametrize("N_RB,nid,n_ant,mode1", [(6, 0, 1, 1), (100, 5, 2, 0), (50, 200, 2, 1), (15, 9, 2, 0)])
+def test_generate_pilots_drop_in(gpu, N_RB, nid, n_ant, mode1):
+    fp_o = O.frame(N_RB, nid, 0, n_ant, mode1)
+    ref = O.generate_pilots(fp_o, 512, ntti=10)
+    fp = gpu.FrameParms()
+    gpu.lib().oai4g_init_frame_parms(ctypes.byref(fp), N_RB, nid, 0, n_ant, mode1, 0)
+    rng = np.random.default_rng(N_RB)
+    grids = [rng.integers(-1000, 1000, len(ref[a])).astype(np.int32) for a in range(n_ant)]
+    pre = [g.copy() for g in grids]
+    gpu.generate_pilots(grids, 512, fp, 10)
+    for a in range(n_ant):
+        pil = ref[a] != 0
+        assert np.array_equal(grids[a][pil], ref[a][pil])          # pilots overwritten (=)
+        assert np.array_equal(grids[a][~pil], pre[a][~pil])        # everything else untouched
+    sym = np.zeros(fp.ofdm_symbol_size, dtype=np.int32)
+    gpu.lte_dl_cell_spec(sym, 512, fp, 3, 1, 0)
+    N = fp.ofdm_symbol_size
+    assert np.array_equal(sym, ref[0][(1 * 14 + 11) * N:(1 * 14 + 12) * N])   # slot 3 = subframe 1, symbol 11

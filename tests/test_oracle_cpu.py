@@ -160,3 +160,21 @@ def test_oracle_reproduces_c1_fixture():
         p = oai.make_params("C1", subframe=sf)
         txd, _, _ = O.tx_subframe(O.tx_cfg_from_params(p, sf), [z[f"payload0_{sf}"]])
         assert np.array_equal(txd, z[f"iq_{sf}"])
+
+
+# ---------------------------------------------------------------- CRS (36.211 6.10.1)
+@pytest.mark.parametrize("N_RB,Nid,n_ant,mode1", [(6, 0, 1, 1), (100, 0, 2, 0), (50, 17, 2, 1), (25, 301, 2, 0)])
+def test_crs_matches_spec_model(N_RB, Nid, n_ant, mode1):
+    fp = O.frame(N_RB, Nid, 0, n_ant, mode1)
+    amp = 512
+    grids = O.generate_pilots(fp, amp, ntti=10)
+    N = fp.ofdm_symbol_size
+    for sf in (0, 3, 9):
+        for ant in range(n_ant):
+            port = 0 if (ant == 0 or mode1) else 1
+            ref = S.crs(N_RB, Nid, sf, port, amp, N, fp.first_carrier_offset)
+            g = grids[ant][sf * 14 * N:(sf + 1) * 14 * N].view(np.int16).reshape(14, N, 2)
+            nz = {(int(l), int(k)) for l, k in zip(*np.nonzero(np.any(g != 0, axis=2)))}
+            assert nz == set(ref), (sf, ant)
+            for (l, k), v in ref.items():
+                assert tuple(int(x) for x in g[l, k]) == v, (sf, ant, l, k)
