@@ -134,6 +134,17 @@ typedef struct {
 int orc_tx_subframe(const orc_tx_cfg_t *cfg, uint8_t *payload[2], int32_t **txdataF, int32_t **txdata,
                     uint8_t *e_out[2] /* optional: scrambled e bytes per cw */);
 
+/* ---- uplink turbo decoding (oai_oracle_td.c; 3gpplte_turbo_decoder_sse_16bit.c:945-1385,
+ *      lte_rate_matching.c:193-243, 688-831) ---- */
+enum { ORC_CRC24_A = 0, ORC_CRC24_B = 1, ORC_CRC16 = 2, ORC_CRC8 = 3 };
+uint8_t orc_turbo_decoder16(const int16_t *y, uint8_t *decoded_bytes, uint16_t n, uint8_t max_iterations,
+                            uint8_t crc_type, uint8_t F);
+uint32_t orc_generate_dummy_w(uint32_t D, uint8_t *w);
+int orc_rate_matching_turbo_rx(uint32_t RTC, uint32_t G, int16_t *w, const uint8_t *dummy_w, const int16_t *soft_input,
+                               uint8_t C, uint32_t Nsoft, uint8_t Mdlharq, uint8_t Kmimo, uint8_t rvidx, uint8_t clear,
+                               uint8_t Qm, uint8_t Nl, uint8_t r, uint32_t *E_out);
+void orc_sub_block_deinterleaving_turbo(uint32_t D, int16_t *d, const int16_t *w);
+
 #ifdef __cplusplus
 }
 #endif

@@ -74,6 +74,15 @@ def orc():
         L.orc_generate_pilots.argtypes = [ctypes.c_void_p, ctypes.c_int16, ctypes.POINTER(OrcFrame), ctypes.c_uint16]
         L.orc_generate_pilots_subframe.argtypes = [ctypes.c_void_p, ctypes.c_int16, ctypes.POINTER(OrcFrame),
                                                    ctypes.c_uint8]
+        L.orc_turbo_decoder16.restype = ctypes.c_uint8
+        L.orc_turbo_decoder16.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint16, ctypes.c_uint8,
+                                          ctypes.c_uint8, ctypes.c_uint8]
+        L.orc_generate_dummy_w.restype = ctypes.c_uint32
+        L.orc_rate_matching_turbo_rx.restype = ctypes.c_int
+        L.orc_rate_matching_turbo_rx.argtypes = [ctypes.c_uint32, ctypes.c_uint32, ctypes.c_void_p, ctypes.c_void_p,
+                                                 ctypes.c_void_p, ctypes.c_uint8, ctypes.c_uint32] + \
+            [ctypes.c_uint8] * 7 + [ctypes.POINTER(ctypes.c_uint32)]
+        L.orc_sub_block_deinterleaving_turbo.argtypes = [ctypes.c_uint32, ctypes.c_void_p, ctypes.c_void_p]
         _orc = L
     return _orc
 
@@ -205,4 +214,44 @@ def generate_pilots(fp, amp, ntti=10):
     ptrs = (ctypes.c_void_p * 2)(*[g.ctypes.data for g in grids] + [None] * (2 - len(grids)))
     orc().orc_generate_pilots(ptrs, amp, ctypes.byref(fp), ntti)
     return grids
+
+
+def turbo_decode(y, K, max_it=8, crc_type=0, F=0):
+    """phy_threegpplte_turbo_decoder16: y = 3K+12 int16 LLRs (positive = bit 1).
+    Returns (iterations, decoded bytes)."""
+    y = np.ascontiguousarray(y, dtype=np.int16)
+    out = np.zeros(K // 8 + 8, dtype=np.uint8)
+    it = orc().orc_turbo_decoder16(P(y), P(out), K, max_it, crc_type, F)
+    return it, out[:K // 8]
+
+
+def dummy_w(D):
+    R = (D + 31) >> 5
+    w = np.zeros(3 * 32 * R + 64, dtype=np.uint8)
+    orc().orc_generate_dummy_w(D, P(w))
+    return w
+
+
+def rate_match_rx(soft, K, G, C, r, Qm, rvidx=0, Nl=1, Kmimo=1, Mdlharq=8, w=None, clear=1, Nsoft=1827072):
+    """lte_rate_matching_turbo_rx: returns (w int16, E)."""
+    D = K + 4
+    R = (D + 31) >> 5
+    dw = dummy_w(D)
+    if w is None:
+        w = np.zeros(3 * 32 * R + 64, dtype=np.int16)
+    soft = np.ascontiguousarray(soft, dtype=np.int16)
+    E = ctypes.c_uint32()
+    rc = orc().orc_rate_matching_turbo_rx(R, G, P(w), P(dw), P(soft), C, Nsoft, Mdlharq, Kmimo, rvidx, clear, Qm, Nl,
+                                          r, ctypes.byref(E))
+    assert rc == 0
+    return w, E.value
+
+
+def subblock_deinterleave(w, K):
+    """sub_block_deinterleaving_turbo: returns d (3K+12 int16, the decoder input)."""
+    D = K + 4
+    buf = np.zeros(96 + 3 * D + 64, dtype=np.int16)
+    orc().orc_sub_block_deinterleaving_turbo(D, ctypes.c_void_p(buf.ctypes.data + 2 * 96),
+                                             P(np.ascontiguousarray(w, dtype=np.int16)))
+    return buf[96:96 + 3 * K + 12].copy()
 
