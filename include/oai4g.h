@@ -164,6 +164,29 @@ void oai4g_idft256(const int16_t *x, int16_t *y, int scale);
 void oai4g_idft128(const int16_t *x, int16_t *y, int scale);
 void oai4g_idft64(const int16_t *x, int16_t *y, int scale);
 
+/* ---------------- uplink turbo decoding ---------------- */
+enum { OAI4G_CRC24_A = 0, OAI4G_CRC24_B = 1 };
+/* phy_threegpplte_turbo_decoder16 (PHY/CODING/3gpplte_turbo_decoder_sse_16bit.c:945, decl
+ * CODING/defs.h): y = 3n+12 int16 LLRs (&d[96]), positive = bit 1.  Returns the iteration count,
+ * max_iterations+1 when no CRC check passes, 255 on bad arguments (CRC16 / CRC8 unsupported). */
+uint8_t oai4g_phy_threegpplte_turbo_decoder16(const int16_t *y, uint8_t *decoded_bytes, uint16_t n, uint16_t f1,
+                                              uint16_t f2, uint8_t max_iterations, uint8_t crc_type, uint8_t F);
+/* lte_rate_matching_turbo_rx (PHY/CODING/lte_rate_matching.c:688, decl CODING/defs.h) */
+int oai4g_lte_rate_matching_turbo_rx(uint32_t RTC, uint32_t G, int16_t *w, const uint8_t *dummy_w,
+                                     const int16_t *soft_input, uint8_t C, uint32_t Nsoft, uint8_t Mdlharq,
+                                     uint8_t Kmimo, uint8_t rvidx, uint8_t clear, uint8_t Qm, uint8_t Nl, uint8_t r,
+                                     uint32_t *E_out);
+/* sub_block_deinterleaving_turbo (lte_rate_matching.c:193): d points at &d[96] (96 writable
+ * entries before it), w holds 3*Kpi entries */
+void oai4g_sub_block_deinterleaving_turbo(uint32_t D, int16_t *d, const int16_t *w);
+/* Batched decoder, device pointers: n_cb blocks of size K, llr [n_cb][llr_stride] int16
+ * (3K+12 each), out [n_cb][out_stride] bytes (K/8 each), iters [n_cb]; scratch of
+ * oai4g_td_scratch_bytes(K, n_cb) bytes.  Asynchronous on `stream`. */
+size_t oai4g_td_scratch_bytes(uint16_t K, int n_cb);
+int oai4g_td_batch(int n_cb, uint16_t K, const int16_t *d_llr, size_t llr_stride, uint8_t *d_out, size_t out_stride,
+                   uint8_t *d_iters, uint8_t max_iterations, uint8_t crc_type, uint8_t F, void *d_scratch,
+                   void *stream);
+
 /* ---------------- batched device-resident transmit path ---------------- */
 /* Plain-old-data parameter block: what rank 0 broadcasts (RCCL) to the other ranks. */
 typedef struct {

@@ -124,6 +124,18 @@ _SIGS = {
                                      ctypes.c_uint16]),
     "oai4g_lte_dl_cell_spec": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int16, ctypes.POINTER(FrameParms),
                                               ctypes.c_uint8, ctypes.c_uint8, ctypes.c_uint8]),
+    "oai4g_phy_threegpplte_turbo_decoder16": (ctypes.c_uint8, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint16,
+                                                               ctypes.c_uint16, ctypes.c_uint16, ctypes.c_uint8,
+                                                               ctypes.c_uint8, ctypes.c_uint8]),
+    "oai4g_lte_rate_matching_turbo_rx": (ctypes.c_int, [ctypes.c_uint32, ctypes.c_uint32, ctypes.c_void_p,
+                                                        ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint8,
+                                                        ctypes.c_uint32] + [ctypes.c_uint8] * 7 +
+                                         [ctypes.POINTER(ctypes.c_uint32)]),
+    "oai4g_sub_block_deinterleaving_turbo": (None, [ctypes.c_uint32, ctypes.c_void_p, ctypes.c_void_p]),
+    "oai4g_td_scratch_bytes": (ctypes.c_size_t, [ctypes.c_uint16, ctypes.c_int]),
+    "oai4g_td_batch": (ctypes.c_int, [ctypes.c_int, ctypes.c_uint16, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p,
+                                      ctypes.c_size_t, ctypes.c_void_p, ctypes.c_uint8, ctypes.c_uint8,
+                                      ctypes.c_uint8, ctypes.c_void_p, ctypes.c_void_p]),
     "oai4g_idft": (ctypes.c_int, [ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int]),
     "oai4g_idft2048": (None, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int]),
     "oai4g_idft1024": (None, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int]),
@@ -299,6 +311,72 @@ def lte_dl_cell_spec(symbol, amp, fp, Ns, l, p):
     init()
     _check(lib().oai4g_lte_dl_cell_spec(_ptr(symbol), amp, ctypes.byref(fp), Ns, l, p) == 0)
     return symbol
+
+
+def turbo_decoder16(y, n, max_iterations=8, crc_type=0, F=0):
+    """phy_threegpplte_turbo_decoder16: y = 3n+12 int16 LLRs.  Returns (iterations, decoded bytes)."""
+    init()
+    y = np.ascontiguousarray(y, dtype=np.int16)
+    out = np.zeros(n // 8, dtype=np.uint8)
+    it = lib().oai4g_phy_threegpplte_turbo_decoder16(_ptr(y), _ptr(out), n, 0, 0, max_iterations, crc_type, F)
+    _check(it != 255)
+    return it, out
+
+
+def rate_matching_turbo_rx(RTC, G, w, dummy_w, soft, C, r, Qm, rvidx=0, clear=1, Nl=1, Kmimo=1, Mdlharq=8,
+                           Nsoft=1827072):
+    """lte_rate_matching_turbo_rx (in place on w int16).  Returns E."""
+    init()
+    E = ctypes.c_uint32()
+    soft = np.ascontiguousarray(soft, dtype=np.int16)
+    _check(lib().oai4g_lte_rate_matching_turbo_rx(RTC, G, _ptr(w), _ptr(dummy_w), _ptr(soft), C, Nsoft, Mdlharq,
+                                                  Kmimo, rvidx, clear, Qm, Nl, r, ctypes.byref(E)) == 0)
+    return E.value
+
+
+def sub_block_deinterleaving_turbo(D, w):
+    """sub_block_deinterleaving_turbo: returns the d buffer (96 + 3D + 8 int16, d = buf[96:])."""
+    init()
+    buf = np.zeros(96 + 3 * D + 8, dtype=np.int16)
+    lib().oai4g_sub_block_deinterleaving_turbo(D, ctypes.c_void_p(buf.ctypes.data + 2 * 96),
+                                               _ptr(np.ascontiguousarray(w, dtype=np.int16)))
+    return buf
+
+
+class TurboDecoderBatch:
+    """Device-resident batch of n_cb code blocks of size K (oai4g_td_batch)."""
+
+    def __init__(self, K, n_cb):
+        init()
+        self.L = lib()
+        self.K, self.n_cb = K, n_cb
+        self.llr_stride = 3 * K + 16
+        self.d_llr = self.L.oai4g_dev_alloc(n_cb * self.llr_stride * 2)
+        self.d_out = self.L.oai4g_dev_alloc(n_cb * (K // 8))
+        self.d_it = self.L.oai4g_dev_alloc(max(256, n_cb))
+        self.d_scr = self.L.oai4g_dev_alloc(self.L.oai4g_td_scratch_bytes(K, n_cb))
+        _check(all([self.d_llr, self.d_out, self.d_it, self.d_scr]))
+
+    def upload(self, llr):
+        buf = np.zeros((self.n_cb, self.llr_stride), dtype=np.int16)
+        buf[:, :3 * self.K + 12] = llr
+        _check(self.L.oai4g_memcpy_h2d(self.d_llr, _ptr(buf), buf.nbytes) == 0)
+
+    def run(self, max_iterations=8, crc_type=0, F=0, stream=None):
+        _check(self.L.oai4g_td_batch(self.n_cb, self.K, self.d_llr, self.llr_stride, self.d_out, self.K // 8,
+                                     self.d_it, max_iterations, crc_type, F, self.d_scr, stream) == 0)
+
+    def results(self):
+        _check(self.L.oai4g_sync() == 0)
+        out = np.empty((self.n_cb, self.K // 8), dtype=np.uint8)
+        it = np.empty(self.n_cb, dtype=np.uint8)
+        _check(self.L.oai4g_memcpy_d2h(_ptr(out), self.d_out, out.nbytes) == 0)
+        _check(self.L.oai4g_memcpy_d2h(_ptr(it), self.d_it, it.nbytes) == 0)
+        return it, out
+
+    def close(self):
+        for p in (self.d_llr, self.d_out, self.d_it, self.d_scr):
+            self.L.oai4g_dev_free(p)
 
 
 def normal_prefix_mod(txdataF, fp, nsymb=7, out=None):

@@ -14,6 +14,8 @@
 
 #include <mutex>
 #include <vector>
+#include <map>
+#include <mutex>
 
 #include "../../include/oai4g.h"
 #include "../../include/oai4g_qpp.h"
@@ -1436,6 +1438,137 @@ extern "C" int oai4g_lte_dl_cell_spec(int32_t *output, int16_t amp, const oai4g_
   }
   crs_job_t j = {0, Ns, l, p, 0};
   return run_crs(&output, 1, fp->ofdm_symbol_size, &j, 1, amp, fp);
+}
+
+/* ------------------------------------------------------------------------------------------
+ * Uplink turbo decoding (3gpplte_turbo_decoder_sse_16bit.c, lte_rate_matching.c)
+ * ---------------------------------------------------------------------------------------- */
+/* init_td16 (:898-943) for block size K: pi4 | pi5 | pi6 as uint16, uploaded once per K */
+static const uint16_t *td_tables(uint32_t K)
+{
+  static std::mutex mu;
+  static std::map<uint32_t, uint16_t *> cache;
+  std::lock_guard<std::mutex> lk(mu);
+  auto it = cache.find(K);
+  if (it != cache.end()) return it->second;
+  const int qi = oai4g_qpp_index(K);
+  if (qi < 0) return nullptr;
+  const uint64_t f1 = oai4g_qpp_table[qi].f1, f2 = oai4g_qpp_table[qi].f2;
+  std::vector<uint32_t> pi2(K);
+  for (uint32_t i = 0, i2 = 0; i2 < 8; i2++)
+    for (uint32_t i3 = 0, j = i2; i3 < K / 8; i3++, i++, j += 8) pi2[i] = j;
+  std::vector<uint16_t> t(3 * (size_t)K);
+  for (uint32_t i = 0; i < K; i++) {
+    const uint32_t pi = (uint32_t)((f1 * i + f2 * (uint64_t)i * i) % K), pi3 = pi2[pi];
+    t[pi2[i]] = (uint16_t)pi3;          /* pi4 */
+    t[K + pi3] = (uint16_t)pi2[i];      /* pi5 */
+    t[2 * K + pi] = (uint16_t)pi2[i];   /* pi6 */
+  }
+  uint16_t *d = nullptr;
+  if (hipMalloc(&d, t.size() * 2) != hipSuccess || hipMemcpy(d, t.data(), t.size() * 2, hipMemcpyHostToDevice) != hipSuccess) {
+    set_err("decoder table upload failed");
+    return nullptr;
+  }
+  cache[K] = d;
+  return d;
+}
+
+extern "C" size_t oai4g_td_scratch_bytes(uint16_t K, int n_cb) { return (size_t)n_cb * oai4g_td_block_bytes(K); }
+
+extern "C" int oai4g_td_batch(int n_cb, uint16_t K, const int16_t *d_llr, size_t llr_stride, uint8_t *d_out,
+                              size_t out_stride, uint8_t *d_iters, uint8_t max_iterations, uint8_t crc_type, uint8_t F,
+                              void *d_scratch, void *stream)
+{
+  NEED_INIT(-1);
+  if (crc_type > OAI4G_CRC24_B) { set_err("turbo decoder: only CRC24_A / CRC24_B are on the path"); return -1; }
+  if ((F & 7) || F + 24 > K) { set_err("turbo decoder: filler F=%u unsupported", F); return -1; }
+  const uint16_t *pi = td_tables(K);
+  if (!pi) { set_err("Illegal frame length %u", K); return -1; }
+  HCK(oai4g_launch_td16(n_cb, K, d_llr, llr_stride, d_out, out_stride, d_iters, max_iterations, crc_type, F, pi,
+                        (uint8_t *)d_scratch, (hipStream_t)stream), -1);
+  return 0;
+}
+
+extern "C" uint8_t oai4g_phy_threegpplte_turbo_decoder16(const int16_t *y, uint8_t *decoded_bytes, uint16_t n,
+                                                         uint16_t f1, uint16_t f2, uint8_t max_iterations,
+                                                         uint8_t crc_type, uint8_t F)
+{
+  NEED_INIT(255);
+  (void)f1; (void)f2;   /* the reference also selects its tables by n (:986) */
+  if (crc_type > 3) { set_err("Illegal crc length!"); return 255; }
+  if (oai4g_qpp_index(n) < 0) { set_err("Illegal frame length!"); return 255; }
+  if (crc_type > OAI4G_CRC24_B) { set_err("turbo decoder: CRC16 / CRC8 are not on the path"); return 255; }
+  const size_t ybytes = (3 * (size_t)n + 12) * 2, sbytes = oai4g_td_block_bytes(n);
+  uint8_t *buf = scratch(ybytes + 256 + (size_t)n / 8 + 256 + sbytes + 512);
+  if (!buf) return 255;
+  int16_t *d_y = (int16_t *)buf;
+  uint8_t *d_iter = buf + ((ybytes + 255) & ~(size_t)255);
+  uint8_t *d_out = d_iter + 256;
+  uint8_t *d_scr = d_out + (((size_t)n / 8 + 255) & ~(size_t)255);
+  HCK(hipMemcpyAsync(d_y, y, ybytes, hipMemcpyHostToDevice, g_scr.s), 255);
+  HCK(hipMemcpyAsync(d_out, decoded_bytes, n / 8, hipMemcpyHostToDevice, g_scr.s), 255);   /* untouched if never decided */
+  if (oai4g_td_batch(1, n, d_y, 3 * (size_t)n + 12, d_out, n / 8, d_iter, max_iterations, crc_type, F, d_scr, g_scr.s))
+    return 255;
+  uint8_t it = 0;
+  HCK(hipMemcpyAsync(decoded_bytes, d_out, n / 8, hipMemcpyDeviceToHost, g_scr.s), 255);
+  HCK(hipMemcpyAsync(&it, d_iter, 1, hipMemcpyDeviceToHost, g_scr.s), 255);
+  HCK(hipStreamSynchronize(g_scr.s), 255);
+  return it;
+}
+
+extern "C" int oai4g_lte_rate_matching_turbo_rx(uint32_t RTC, uint32_t G, int16_t *w, const uint8_t *dummy_w,
+                                                const int16_t *soft_input, uint8_t C, uint32_t Nsoft, uint8_t Mdlharq,
+                                                uint8_t Kmimo, uint8_t rvidx, uint8_t clear, uint8_t Qm, uint8_t Nl,
+                                                uint8_t r, uint32_t *E_out)
+{
+  NEED_INIT(-1);
+  if (Kmimo == 0 || Mdlharq == 0 || C == 0 || Qm == 0 || Nl == 0) return -1;
+  const uint32_t Nir = Nsoft / Kmimo / (Mdlharq < 8 ? Mdlharq : 8), Kw = 3 * (RTC << 5);
+  const uint32_t Ncb = Nir / C < Kw ? Nir / C : Kw, Gp = G / Nl / Qm, GpmodC = Gp % C;
+  const uint32_t E = r < C - GpmodC ? Nl * Qm * (Gp / C) : Nl * Qm * ((GpmodC == 0 ? 0 : 1) + Gp / C);
+  const uint32_t Ncbmod = Ncb % (RTC << 3);
+  const uint32_t k0 = RTC * (2 + (rvidx * (((Ncbmod == 0) ? 0 : 1) + (Ncb / (RTC << 3))) * 2));
+  /* compact (non-NULL) index of every w position, and of k0 */
+  std::vector<uint32_t> cidx(Ncb);
+  uint32_t nn = 0, k0c = 0;
+  for (uint32_t p = 0; p < Ncb; p++) {
+    if (p == k0) k0c = nn;
+    cidx[p] = nn;
+    if (dummy_w[p] != OAI4G_LTE_NULL) nn++;
+  }
+  if (k0 >= Ncb) k0c = 0;   /* the reference's first pass is empty; selection starts at 0 */
+  if (nn == 0 && E > 0) { set_err("rate_matching_rx: no non-NULL entries"); return -1; }
+  const size_t b_soft = (size_t)E * 2, b_w = (size_t)Ncb * 2, b_c = (size_t)Ncb * 4;
+  uint8_t *buf = scratch(b_soft + b_w + b_c + Ncb + 1024);
+  if (!buf) return -1;
+  int16_t *d_soft = (int16_t *)buf;
+  int16_t *d_w = (int16_t *)(buf + ((b_soft + 255) & ~(size_t)255));
+  uint32_t *d_c = (uint32_t *)((uint8_t *)d_w + ((b_w + 255) & ~(size_t)255));
+  uint8_t *d_dummy = (uint8_t *)d_c + ((b_c + 255) & ~(size_t)255);
+  HCK(hipMemcpyAsync(d_soft, soft_input, b_soft, hipMemcpyHostToDevice, g_scr.s), -1);
+  HCK(hipMemcpyAsync(d_w, w, b_w, hipMemcpyHostToDevice, g_scr.s), -1);
+  HCK(hipMemcpyAsync(d_c, cidx.data(), b_c, hipMemcpyHostToDevice, g_scr.s), -1);
+  HCK(hipMemcpyAsync(d_dummy, dummy_w, Ncb, hipMemcpyHostToDevice, g_scr.s), -1);
+  HCK(oai4g_launch_rm_rx(d_soft, E, d_w, d_dummy, d_c, Ncb, nn, k0c, clear == 1, g_scr.s), -1);
+  HCK(hipMemcpyAsync(w, d_w, b_w, hipMemcpyDeviceToHost, g_scr.s), -1);
+  HCK(hipStreamSynchronize(g_scr.s), -1);
+  *E_out = E;
+  return 0;
+}
+
+extern "C" void oai4g_sub_block_deinterleaving_turbo(uint32_t D, int16_t *d, const int16_t *w)
+{
+  NEED_INIT();
+  const uint32_t R = (D + 31) >> 5, Kpi = R << 5;
+  const size_t nd = 96 + 3 * (size_t)D + 8, b_d = nd * 2, b_w = 3 * (size_t)Kpi * 2;
+  uint8_t *buf = scratch(b_d + b_w + 512);
+  if (!buf) return;
+  int16_t *d_d = (int16_t *)buf, *d_w = (int16_t *)(buf + ((b_d + 255) & ~(size_t)255));
+  HCK(hipMemcpyAsync(d_d, d - 96, b_d, hipMemcpyHostToDevice, g_scr.s), );
+  HCK(hipMemcpyAsync(d_w, w, b_w, hipMemcpyHostToDevice, g_scr.s), );
+  HCK(oai4g_launch_subblock_deint(D, d_d, d_w, g_scr.s), );
+  HCK(hipMemcpyAsync(d - 96, d_d, b_d, hipMemcpyDeviceToHost, g_scr.s), );
+  HCK(hipStreamSynchronize(g_scr.s), );
 }
 
 extern "C" int oai4g_idft(int log2n, const int16_t *x, int16_t *y, int scale)

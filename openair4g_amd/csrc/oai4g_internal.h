@@ -140,6 +140,15 @@ hipError_t oai4g_launch_crs(int32_t *d_out, const crs_job_t *jobs, int n_jobs, c
                             uint32_t N, uint32_t N_RB, uint32_t nushift, uint32_t first_carrier, hipStream_t s);
 hipError_t oai4g_launch_diag_stream(const void *src, void *dst, size_t bytes, int mode, hipStream_t s);
 
+/* uplink turbo decoding (oai4g_decode.hip) */
+size_t oai4g_td_block_bytes(uint32_t K);
+hipError_t oai4g_launch_td16(int n_cb, uint32_t K, const int16_t *d_llr, size_t llr_stride, uint8_t *d_out,
+                             size_t out_stride, uint8_t *d_iters, uint32_t max_it, uint32_t crc_type, uint32_t F,
+                             const uint16_t *d_pi /* pi4 | pi5 | pi6, K each */, uint8_t *d_scratch, hipStream_t s);
+hipError_t oai4g_launch_rm_rx(const int16_t *d_soft, uint32_t E, int16_t *d_w, const uint8_t *d_dummy,
+                              const uint32_t *d_cidx, uint32_t Ncb, uint32_t Nnn, uint32_t k0c, int clear, hipStream_t s);
+hipError_t oai4g_launch_subblock_deint(uint32_t D, int16_t *d_dfull, const int16_t *d_w, hipStream_t s);
+
 /* OFDM path */
 hipError_t oai4g_launch_modofdm(const cfg_dev_t *d_cfg, const cfg_dev_t *h_cfg, int sf0, int n_sf,
                                 const uint32_t *d_ebits, int32_t *d_iq, hipStream_t s);

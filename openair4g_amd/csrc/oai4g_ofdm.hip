@@ -49,11 +49,6 @@ static __device__ __forceinline__ s16x2 cpack32(int re, int im)
 struct twp_t {
   s16x2 t, tn;
 };
-static __device__ __forceinline__ twp_t mk_tw(uint32_t v)
-{
-  s16x2 t = u2c(v);
-  return {t, (s16x2){(short)(-(int)t.y), t.x}};
-}
 
 /* x * conj(t), 32-bit (cmultc, lte_dfts.c:132-141) */
 static __device__ __forceinline__ void cmulc32(s16x2 x, const twp_t &w, int &re, int &im)
