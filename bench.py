@@ -53,6 +53,95 @@ def cpu_baseline(name, seconds, subframe):
             "sample": f"{n} subframes of {name} (sf {subframe}) through the C oracle, single thread, {dt:.1f} s"}
 
 
+C5_K, C5_CB = 5504, 8          # UL 100 PRB MCS 20: TBS 43816 -> C = 8 blocks of K = 5504
+
+
+def c5_llrs(n_cb, mode, seed):
+    """Decoder inputs (3K+12 int16 per block): "8it" = unstructured LLRs, every CRC check fails,
+    the full 8 iterations run (SURVEY 8d C5 "8 iterations fixed"); "snr" = CRC-terminated
+    codewords, BPSK amplitude 32 + Gaussian noise sigma 28 (early stop)."""
+    import numpy as np
+    rng = np.random.default_rng(seed)
+    if mode == "8it":
+        return rng.integers(-40, 41, size=(n_cb, 3 * C5_K + 12)).astype(np.int16)
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import oracle_lib as O
+    import re
+    src = open(os.path.join(ROOT, "include", "oai4g_qpp.c")).read()
+    f = {int(a): (int(b), int(c)) for a, b, c in re.findall(r"\{\s*(\d+)\s*,\s*(\d+)\s*,\s*(\d+)\s*\}", src)}
+    base = []
+    for _ in range(64):                    # 64 distinct codewords, tiled
+        c = np.zeros(C5_K // 8 + 4, dtype=np.uint8)
+        c[:(C5_K - 24) // 8] = rng.integers(0, 256, (C5_K - 24) // 8, dtype=np.uint8)
+        v = O.crc24b(c, C5_K - 24) >> 8
+        c[(C5_K - 24) // 8:(C5_K - 24) // 8 + 3] = [v >> 16, (v >> 8) & 255, v & 255]
+        d = O.turbo_encode(c[:C5_K // 8], *f[C5_K]).astype(np.float64)
+        base.append(np.clip(np.round((2 * d - 1) * 32 + rng.normal(0, 28, d.size)), -32768, 32767).astype(np.int16))
+    return np.stack([base[i % 64] for i in range(n_cb)])
+
+
+def bench_c5(args, world, rank, dist, torch):
+    """UL turbo decoding throughput (config C5): subframes of 8 code blocks, K = 5504."""
+    import numpy as np
+    import openair4g_amd as oai
+    from openair4g_amd import dist as odist
+    oai.init()
+    n_sf = args.batch
+    n_cb = n_sf * C5_CB
+    crc_type = 1                           # C > 1: per-block CRC24_B (ulsch_decoding.c)
+    llr = c5_llrs(n_cb, args.c5_mode, 0xC5 + rank)
+    dec = oai.TurboDecoderBatch(C5_K, n_cb)
+    dec.upload(llr)
+    for _ in range(args.warmup):
+        dec.run(max_iterations=8, crc_type=crc_type)
+    dec.results()
+    if dist is not None:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        dec.run(max_iterations=8, crc_type=crc_type)
+    oai.lib().oai4g_sync()
+    torch.cuda.synchronize()
+    if dist is not None:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if dist is not None:
+        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    its, _ = dec.results()
+    dec.close()
+    value = n_sf * args.steps * world / elapsed
+    per_launch_ms = elapsed * 1000.0 / args.steps
+    alg = n_cb * (2 * (3 * C5_K + 12) + C5_K // 8)          # SURVEY 8d: LLR read + bits written
+    ach = alg / (per_launch_ms * 1e-3) / 1e9
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        sys.path.insert(0, os.path.join(ROOT, "tests"))
+        import oracle_lib as O
+        n, t1 = 0, time.perf_counter()
+        while time.perf_counter() - t1 < args.cpu_seconds:
+            O.turbo_decode(llr[n % len(llr)], C5_K, max_it=8, crc_type=crc_type)
+            n += 1
+        dt = time.perf_counter() - t1
+        cpu = {"value": n / C5_CB / dt, "unit": "subframes/s", "cores": 1, "kind": "port",
+               "sample": f"{n} code blocks (K={C5_K}, mode {args.c5_mode}) through the C oracle decoder, "
+                         f"single thread, {dt:.1f} s"}
+    if rank == 0:
+        print(json.dumps({
+            "metric": "UL subframes/sec (C5 turbo decode)", "value": value, "unit": "subframes/s", "n_gpus": world,
+            "steps": args.steps, "warmup": args.warmup, "ms_per_step": per_launch_ms, "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": "int16",
+            "data": f"synthetic LLRs ({args.c5_mode})",
+            "config": {"workload": "ulsim 20 MHz MCS20 decode: 8 x K=5504, 16-bit max-log-MAP, max 8 iterations",
+                       "config_id": "C5", "subframes_per_gpu_per_step": n_sf, "code_blocks_per_step": n_cb,
+                       "mean_iterations": float(np.mean(its)), "parallelism": f"block-sharded x{world}"},
+            "roofline": {"bound": "hbm", "kernel": "k_td16", "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": ach / HBM_PEAK_GBS, "traffic": None},
+            "cpu_baseline": cpu}), flush=True)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -64,6 +153,7 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--kernel-reps", type=int, default=5, help="serial runs timed per kernel for the roofline")
+    ap.add_argument("--c5-mode", default="8it", choices=["8it", "snr"], help="C5 decoder inputs")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -78,6 +168,12 @@ def main():
         dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
     else:
         torch.cuda.set_device(0)
+
+    if args.config == "C5":
+        bench_c5(args, world, rank, dist, torch)
+        if dist is not None:
+            dist.destroy_process_group()
+        return
 
     import openair4g_amd as oai
     oai.init()
