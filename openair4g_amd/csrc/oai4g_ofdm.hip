@@ -36,7 +36,14 @@ static __device__ __forceinline__ s16x2 csubs(s16x2 a, s16x2 b) { return __built
 static __device__ __forceinline__ s16x2 caddw(s16x2 a, s16x2 b) { return a + b; }
 /* sign_epi16(x,{-1,1}) + pair swap: -j*x with a wrapping negate (lte_dfts.c:1463-1466) */
 static __device__ __forceinline__ s16x2 cflip(s16x2 a) { return (s16x2){a.y, (short)(-(int)a.x)}; }
-static __device__ __forceinline__ int dot2(s16x2 a, s16x2 b) { return __builtin_amdgcn_sdot2(a, b, 0, false); }
+/* v_dot2_i32_i16 with an inline-zero accumulator (the compiler otherwise picks the tied
+ * v_dot2c form and zeroes its accumulator with an extra v_mov per product) */
+static __device__ __forceinline__ int dot2(s16x2 a, s16x2 b)
+{
+  int r;
+  asm("v_dot2_i32_i16 %0, %1, %2, 0" : "=v"(r) : "v"(a), "v"(b));
+  return r;
+}
 static __device__ __forceinline__ int wadd(int a, int b) { return (int)((unsigned)a + (unsigned)b); }
 static __device__ __forceinline__ int wsub(int a, int b) { return (int)((unsigned)a - (unsigned)b); }
 /* cpack: srai 15 + packs_epi32 (lte_dfts.c:123-131) */
@@ -235,8 +242,9 @@ static __device__ __forceinline__ void idft_level_lds(uint32_t *lds, int t, cons
 }
 
 /*
- * NA transforms by one unit.  `prod(n, x)` fills x[a] = input a at t + T n; `cons(a, f, y)`
- * stores output sample f of transform a.  Every thread of the workgroup must call this (it
+ * NA transforms by one unit.  `prod(n, x)` fills x[a] = input a at t + T n; `cons(a, t, off, y)`
+ * stores output sample f = t + off of transform a (off is a compile-time constant after
+ * unrolling, so stores can use immediate offsets from a per-thread base).  Every thread of the workgroup must call this (it
  * contains barriers), active or not.
  */
 template <int LOG2N, int NA, class Prod, class Cons>
@@ -278,7 +286,6 @@ static __device__ __forceinline__ void idft_unit(uint32_t *lds, int t, bool acti
     if (active) {
 #pragma unroll
       for (int j = 0; j < 4; j++) {
-        int q = t + T * j;
         const s16x2 *wt = tw.l64[j % idft_tw_t<6>::D64];
         const twp_t w[3] = {tw_of(wt[0]), tw_of(wt[1]), tw_of(wt[2])};
 #pragma unroll
@@ -287,7 +294,7 @@ static __device__ __forceinline__ void idft_unit(uint32_t *lds, int t, bool acti
           r4inv(v[a][j][0], cmulc16(v[a][j][1], w[0]), cmulc16(v[a][j][2], w[1]), cmulc16(v[a][j][3], w[2]), y[0],
                 y[1], y[2], y[3]);
 #pragma unroll
-          for (int m = 0; m < 4; m++) cons(a, q + 16 * m, scale ? shr3(y[m]) : y[m]);
+          for (int m = 0; m < 4; m++) cons(a, t, T * j + 16 * m, scale ? shr3(y[m]) : y[m]);
         }
       }
     }
@@ -308,8 +315,8 @@ static __device__ __forceinline__ void idft_unit(uint32_t *lds, int t, bool acti
             ibfly2(u2c(lds[a * LDSW + lphys((uint32_t)q)]), u2c(lds[a * LDSW + lphys((uint32_t)(SC + q))]),
                    tw_of(tw.r2[j % DR2]), y0, y1);
             if (scale) { y0 = mulhi2(y0); y1 = mulhi2(y1); }
-            cons(a, q, y0);
-            cons(a, q + SC, y1);
+            cons(a, t, T * j, y0);
+            cons(a, t, T * j + SC, y1);
           }
         }
       }
@@ -329,7 +336,7 @@ static __device__ __forceinline__ void idft_unit(uint32_t *lds, int t, bool acti
                    u2c(lds[a * LDSW + lphys((uint32_t)(2 * SC + q))]),
                    u2c(lds[a * LDSW + lphys((uint32_t)(3 * SC + q))]), w[0], w[1], w[2], y[0], y[1], y[2], y[3]);
 #pragma unroll
-            for (int m = 0; m < 4; m++) cons(a, q + SC * m, scale ? shr1(y[m]) : y[m]);
+            for (int m = 0; m < 4; m++) cons(a, t, T * j + SC * m, scale ? shr1(y[m]) : y[m]);
           }
         }
       }
@@ -364,7 +371,8 @@ __global__ void __launch_bounds__(128) k_ofdm(const int32_t *__restrict__ in, in
   const int cp = (int)d.cp;
   idft_unit<LOG2N, 1>(
       lds_all + unit * LDSW, t, active, twr, [&](int n, s16x2 *x) { x[0] = u2c(src[t + T * n]); },
-      [&](int, int f, s16x2 y) {
+      [&](int, int tt, int off, s16x2 y) {
+        const int f = tt + off;
         dst[f] = c2u(y);
         if (f >= N - cp) dst[f - N] = c2u(y);
       },
@@ -555,17 +563,21 @@ __global__ void __launch_bounds__(128) MODOFDM_ATTR k_modofdm(const cfg_dev_t *_
               if (pil_re) x[a] = (NA == 1 || (uint32_t)a == port) ? u2c(pv) : (s16x2){0, 0};
           }
         },
-        [&](int a, int f, s16x2 y) {
+        [&](int a, int tt, int off, s16x2 y) {
+          /* per-thread bases for each half of the symbol keep every store's offset within the
+           * 13-bit immediate; the CP test is compiled out where no t can reach N - CP_max */
+          constexpr int CPMAX = (N * 160) / 2048;
+          const bool hi = off >= N / 2;
+          const int ro = hi ? off - N / 2 : off;
+          auto store = [&](uint32_t *base) {
+            uint32_t *d = base + tt + (hi ? N / 2 : 0);
+            d[ro] = c2u(y);
+            if (off + T - 1 >= N - CPMAX && tt + off >= N - cp) d[ro - N] = c2u(y);
+          };
           if constexpr (NA == 2) {
-            uint32_t *d = dst0 + a * c->spt;
-            d[f] = c2u(y);
-            if (f >= N - cp) d[f - N] = c2u(y);
+            store(dst0 + a * c->spt);
           } else {
-            for (uint32_t aa = 0; aa < n_ant; aa++) {
-              uint32_t *d = dst0 + aa * c->spt;
-              d[f] = c2u(y);
-              if (f >= N - cp) d[f - N] = c2u(y);
-            }
+            for (uint32_t aa = 0; aa < n_ant; aa++) store(dst0 + aa * c->spt);
           }
         },
         1);
