@@ -394,17 +394,6 @@ static __device__ __forceinline__ uint32_t sx32(const uint32_t *a, int pos)
   return off ? (lo >> off) | (hi << (32 - off)) : lo;
 }
 
-/* 16 bits -> even bit positions of 32 */
-static __device__ __forceinline__ uint32_t spread16(uint32_t x)
-{
-  x &= 0xffffu;
-  x = (x | (x << 8)) & 0x00ff00ffu;
-  x = (x | (x << 4)) & 0x0f0f0f0fu;
-  x = (x | (x << 2)) & 0x33333333u;
-  x = (x | (x << 1)) & 0x55555555u;
-  return x;
-}
-
 /* 32x32 bit transpose across the 32 lanes of a half-wave: lane c ends with bit i = bit c of
  * lane i's input */
 static __device__ __forceinline__ uint32_t transpose32(uint32_t x, uint32_t lane32)
@@ -684,18 +673,19 @@ static __device__ void encode_codeword(const cfg_dev_t *__restrict__ c, uint32_t
   for (uint32_t i = tid; i < cw.wpk_off[C]; i += nth) wb[i] = 0u;
   __syncthreads();
 
-  /* ---- phase 4b: sub-block interleaving (lte_rate_matching.c:51-130).  Each half-wave takes a
-   * 32x32 tile of y^(s) (32 rows of 32 entries, NULL prefix of ND, y^(2) pre-shifted by one for
-   * the (pi(k)+1) mod Kpi rule), transposes it so lane c holds 32 rows of column c, and ORs that
-   * column run into packed w: column c sits at w column bitrev5(c), i.e. at bit bitrev5(c) R + row
-   * of v^(0), and interlaced (even bits v^(1), odd bits v^(2)) after Kpi. ---- */
+  /* ---- phase 4b: sub-block interleaving (lte_rate_matching.c:51-130).  Each half-wave takes
+   * a 32x32 bit tile and transposes it (5 shuffle stages) so that lane c holds a run of column
+   * c, then ORs the run into packed w.  v^(0) tiles are 32 rows of y^(0); a run of column c sits
+   * at w bit bitrev5(c) R + row.  Interlaced tiles are 16 rows of y^(1) and y^(2) alternating
+   * (lane 2i: y^(1) row, lane 2i+1: y^(2) row, pre-shifted by one for the (pi(k)+1) mod Kpi
+   * rule), so the transposed run is already w's v^(1)/v^(2) interlacing, at bit
+   * Kpi + 2 (bitrev5(c) R + row).  The host lists the tiles (cw.tasks). ---- */
   {
-    const uint32_t lane32 = tid & 31, ntask = cw.col_task[C], wcol = colperm(lane32);
-    for (uint32_t t = tid >> 5; t < ntask; t += nth >> 5) {
-      uint32_t r = 0;
-      while (r + 1 < C && t >= cw.col_task[r + 1]) r++;
-      const uint32_t R = cw.R[r], ND = cw.ND[r], RBW = (R + 31) >> 5;
-      const uint32_t tt = t - cw.col_task[r], s = tt / RBW, rb = tt - s * RBW, row = 32 * rb + lane32;
+    const uint32_t lane32 = tid & 31, wcol = colperm(lane32);
+    for (uint32_t t = tid >> 5; t < cw.ntask; t += nth >> 5) {
+      const uint32_t code = cw.tasks[t], r = code & 15u, il = (code >> 4) & 1u, rb = code >> 5;
+      const uint32_t R = cw.R[r], ND = cw.ND[r];
+      const uint32_t row = il ? 16 * rb + (lane32 >> 1) : 32 * rb + lane32, s = il ? 1 + (lane32 & 1) : 0;
       const uint32_t *st = strm + (r * 3 + s) * sw;
       uint32_t y = 0;
       if (row < R) {
@@ -706,14 +696,7 @@ static __device__ void encode_codeword(const cfg_dev_t *__restrict__ c, uint32_t
         }
       }
       y = transpose32(y, lane32);
-      uint32_t *w = wb + cw.wpk_off[r];
-      if (s == 0) {
-        or_bits(w, wcol * R + 32 * rb, y);
-      } else {
-        const uint32_t bit = cw.Kpi[r] + 2 * (wcol * R + 32 * rb) + (s - 1);
-        or_bits(w, bit, spread16(y));
-        or_bits(w, bit + 32, spread16(y >> 16));
-      }
+      or_bits(wb + cw.wpk_off[r], il ? cw.Kpi[r] + 2 * (wcol * R + 16 * rb) : wcol * R + 32 * rb, y);
     }
   }
   __syncthreads();

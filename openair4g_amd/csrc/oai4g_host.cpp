@@ -654,14 +654,13 @@ static int derive_cfg(oai4g_tx_config *cfg, const oai4g_tx_params_t *p, const ui
      * 32x32 transpose tiles of the sub-block interleaver (3 streams x ceil(R/32) per block) */
     uint32_t wwords = 0, ntask = 0;
     for (uint32_t r = 0; r < C; r++) {
-      uint32_t RBW = (c.R[r] + 31) / 32;
       c.wpk_off[r] = wwords;
-      c.col_task[r] = ntask;
       wwords += 3 * c.R[r] + 2;
-      ntask += 3 * RBW;
+      for (uint32_t rb = 0; rb < (c.R[r] + 31) / 32; rb++) c.tasks[ntask++] = (uint16_t)(r | (rb << 5));
+      for (uint32_t rb = 0; rb < (c.R[r] + 15) / 16; rb++) c.tasks[ntask++] = (uint16_t)(r | (1u << 4) | (rb << 5));
     }
     c.wpk_off[C] = wwords;
-    c.col_task[C] = ntask;
+    c.ntask = ntask;
     max_w = wwords > max_w ? wwords : max_w;
     uint32_t tbw = (c.A_bytes + 3 + 3) / 4 + 1;
     max_tb_words = tbw > max_tb_words ? tbw : max_tb_words;

@@ -16,6 +16,7 @@
 #define OAI4G_MAX_CB 16
 #define OAI4G_MAX_NULLS 104
 #define OAI4G_MAX_CHUNKS 192                /* 6144 / 32 */
+#define OAI4G_MAX_TASKS (OAI4G_MAX_CB * 20)  /* ceil(R/32) + ceil(R/16) tiles per block, R <= 193 */
 #define OAI4G_PIPE_MAX_CHUNKS 16
 #define OAI4G_CRS_CODE 0xE000u               /* remap codes >= this (and != 0xFFFF) are CRS REs */
 #define OAI4G_ENC_CRC_TABLE_WORDS (256 + 256 + 8 * 96 + 6 * 96) /* byte tables A/B + tree multipliers */
@@ -59,7 +60,8 @@ struct cw_dev_t {
   uint32_t k0c[OAI4G_MAX_CB];   /* non-NULL entries of w[0..k0): compacted start */
   uint32_t kidx[OAI4G_MAX_CB];  /* which null list (0: Kminus, 1: Kplus) */
   uint32_t wpk_off[OAI4G_MAX_CB + 1]; /* LDS word offset of block r's packed w (3R words + 2 pad) */
-  uint32_t col_task[OAI4G_MAX_CB + 1];/* prefix sum of transpose tasks (3 x RBW per block) */
+  uint32_t ntask;                     /* sub-block interleaver tiles of all blocks */
+  uint16_t tasks[OAI4G_MAX_TASKS];    /* block | kind << 4 (0: v0 rows, 1: v1/v2 rows) | tile << 5 */
   uint32_t ilv_off[OAI4G_MAX_CB + 1]; /* LDS word offset of block r's QPP-interleaved input words */
   /* QPP interleaver walk per 32-bit chunk j (kidx list): Pi(32j) | (Pi(32j+1)-Pi(32j) mod K) << 16,
    * and the second difference 2 f2 mod K (3gpplte.c:50-74 restated incrementally) */
