@@ -12,10 +12,10 @@
 #include <stdlib.h>
 #include <string.h>
 
-#include <mutex>
-#include <vector>
+#include <algorithm>
 #include <map>
 #include <mutex>
+#include <vector>
 
 #include "../../include/oai4g.h"
 #include "../../include/oai4g_qpp.h"
@@ -744,8 +744,18 @@ static int derive_cfg(oai4g_tx_config *cfg, const oai4g_tx_params_t *p, const ui
 static int upload_cfg(oai4g_tx_config *cfg)
 {
   if (!cfg->h_remap.empty()) {
-    HCK(hipMalloc(&cfg->d_remap, cfg->h_remap.size() * 2), -1);
-    HCK(hipMemcpy(cfg->d_remap, cfg->h_remap.data(), cfg->h_remap.size() * 2, hipMemcpyHostToDevice), -1);
+    /* natural layout followed by the thread-major copy the fused kernel reads */
+    const size_t n = cfg->h_remap.size(), N = cfg->h.N, T = N >> 4;
+    std::vector<uint16_t> both(2 * n);
+    std::copy(cfg->h_remap.begin(), cfg->h_remap.end(), both.begin());
+    for (size_t sl = 0; sl < n / N; sl++)
+      for (size_t t = 0; t < T; t++)
+        for (size_t k = 0; k < 16; k++) both[n + sl * N + t * 16 + k] = cfg->h_remap[sl * N + t + T * k];
+    HCK(hipMalloc(&cfg->d_remap, both.size() * 2), -1);
+    HCK(hipMemcpy(cfg->d_remap, both.data(), both.size() * 2, hipMemcpyHostToDevice), -1);
+    cfg->h.remap_tm = cfg->d_remap + n;
+  } else {
+    cfg->h.remap_tm = nullptr;
   }
   cfg->h.remap = cfg->d_remap;
   if (!cfg->h_crs.empty()) {

@@ -101,6 +101,8 @@ struct cfg_dev_t {
   uint32_t n_cu;                /* compute units of the device (persistent grids) */
   const uint16_t *remap;        /* [10][14][N] data-RE index | parity<<15; OAI4G_CRS_CODE | pilot
                                    symbol<<9 | port<<8 | m for a CRS RE; 0xFFFF = none */
+  const uint16_t *remap_tm;     /* the same codes thread-major: per (sf, l), [t][n] = remap[t + (N/16) n],
+                                   so each modofdm thread fetches its 16 codes with two 16-B loads */
   uint32_t with_crs;
   const uint32_t *crs_tab;      /* [10][4][200] packed CRS IQ of pilot symbol i (l = 0, 4, 7, 11), index m */
   const uint32_t *gold_x1;      /* [256]     x1 state after 50+16l word steps */

@@ -28,6 +28,8 @@
 typedef short s16x2 __attribute__((ext_vector_type(2)));
 typedef const __attribute__((address_space(1))) uint32_t gu32_t;
 typedef const __attribute__((address_space(1))) uint16_t gu16_t;
+typedef uint32_t u32x4_t __attribute__((ext_vector_type(4)));
+typedef const __attribute__((address_space(1))) u32x4_t gu128_t;
 
 static __device__ __forceinline__ s16x2 u2c(uint32_t v) { return __builtin_bit_cast(s16x2, v); }
 static __device__ __forceinline__ uint32_t c2u(s16x2 v) { return __builtin_bit_cast(uint32_t, v); }
@@ -254,13 +256,7 @@ static __device__ __forceinline__ void idft_unit(uint32_t *lds, int t, bool acti
   constexpr int N = 1 << LOG2N, T = N >> 4, LDSW = N + (N >> 5);
   if (active) {
     s16x2 x[NA][16];
-#pragma unroll
-    for (int n = 0; n < 16; n++) {
-      s16x2 xn[NA];
-      prod(n, xn);
-#pragma unroll
-      for (int a = 0; a < NA; a++) x[a][n] = xn[a];
-    }
+    prod(x);   /* fills x[a][n] = input point t + T n of antenna a: one call, so loads batch */
 #pragma unroll
     for (int a = 0; a < NA; a++) {
       idft16_reg(x[a], tw.l16);
@@ -370,7 +366,10 @@ __global__ void __launch_bounds__(128) k_ofdm(const int32_t *__restrict__ in, in
   uint32_t *dst = (uint32_t *)out + d.out_off;
   const int cp = (int)d.cp;
   idft_unit<LOG2N, 1>(
-      lds_all + unit * LDSW, t, active, twr, [&](int n, s16x2 *x) { x[0] = u2c(src[t + T * n]); },
+      lds_all + unit * LDSW, t, active, twr, [&](s16x2 (*x)[16]) {
+#pragma unroll
+        for (int n = 0; n < 16; n++) x[0][n] = u2c(src[t + T * n]);
+      },
       [&](int, int tt, int off, s16x2 y) {
         const int f = tt + off;
         dst[f] = c2u(y);
@@ -466,7 +465,7 @@ struct modofdm_geom {
 #else
 #define MODOFDM_ATTR
 #endif
-template <int LOG2N, int NA>
+template <int LOG2N, int NA, bool CW2, bool CRS>
 __global__ void __launch_bounds__(128) MODOFDM_ATTR k_modofdm(const cfg_dev_t *__restrict__ c, int n_items,
                                                  const uint32_t *__restrict__ ebits, int32_t *__restrict__ iq,
                                                  uint32_t sf0)
@@ -479,8 +478,7 @@ __global__ void __launch_bounds__(128) MODOFDM_ATTR k_modofdm(const cfg_dev_t *_
   const int unit = threadIdx.x / T, t = threadIdx.x % T;
   idft_tw_t<LOG2N> twr;
   twr.load(c->tw, t);
-  const uint32_t n_ant = c->n_ant, nsymb = c->nsymb, n_cw = c->n_cw;
-  const bool cdd = c->mimo_mode == OAI4G_LARGE_CDD;
+  const uint32_t n_ant = c->n_ant, nsymb = c->nsymb;
   for (uint32_t i = threadIdx.x; i < 256; i += blockDim.x) {
     const uint32_t cw = i >> 7, pil = (i >> 6) & 1, bits = i & 63;
     const cw_dev_t &w = c->cw[cw];
@@ -504,7 +502,7 @@ __global__ void __launch_bounds__(128) MODOFDM_ATTR k_modofdm(const cfg_dev_t *_
     const int cp = (int)(si == 0 ? c->cp0 : c->cp);
     uint32_t *dst0 = (uint32_t *)iq + (size_t)sf * n_ant * c->spt + body;
 
-    if (UNITS == 1 && nre == 0 && !(c->with_crs && pilots_any(l))) {
+    if (UNITS == 1 && nre == 0 && !(CRS && pilots_any(l))) {
       /* control-region symbol: the transform of an all-zero grid is zero */
       if (active)
         for (uint32_t a = 0; a < n_ant; a++) {
@@ -514,53 +512,88 @@ __global__ void __launch_bounds__(128) MODOFDM_ATTR k_modofdm(const cfg_dev_t *_
       continue;
     }
 
+    /* this thread's 16 RE codes (thread-major copy): two 16-B loads issued before any use */
+    const gu128_t *rsrc = (const gu128_t *)(c->remap_tm + ((size_t)sfi * 14 + l) * N + (size_t)t * 16);
+    const u32x4_t ra = rsrc[0], rb = rsrc[1];
+    const uint32_t rw[8] = {ra.x, ra.y, ra.z, ra.w, rb.x, rb.y, rb.z, rb.w};
+
     /* stage this symbol's e bits of each codeword (coalesced) */
-    const uint32_t *esf = ebits + (size_t)(sf * n_cw) * c->ebits_words;
+    const uint32_t *esf = ebits + (size_t)(sf * c->n_cw) * c->ebits_words;
     const uint32_t wlo0 = (re0 * Qm0) >> 5, wlo1 = (re0 * Qm1) >> 5;
     if (active && nre) {
       const uint32_t cnt0 = min((uint32_t)EW, (((re0 + nre) * Qm0 + 31) >> 5) - wlo0 + 1);
       for (uint32_t i = t; i < cnt0; i += T) lds_e[unit][0][i] = esf[wlo0 + i];
-      if (n_cw > 1) {
+      if constexpr (CW2) {
         const uint32_t cnt1 = min((uint32_t)EW, (((re0 + nre) * Qm1 + 31) >> 5) - wlo1 + 1);
         for (uint32_t i = t; i < cnt1; i += T) lds_e[unit][1][i] = esf[c->ebits_words + wlo1 + i];
       }
     }
     __syncthreads();
 
-    gu16_t *rm = (gu16_t *)(c->remap + ((size_t)sfi * 14 + l) * N);
     gu32_t *crs_tab = (gu32_t *)c->crs_tab;
-    const bool crs = c->with_crs != 0 && pilots_any(l);
+    const bool crs = CRS && pilots_any(l);
     const uint32_t *e0 = lds_e[unit][0], *e1 = lds_e[unit][1];
     const uint32_t *q0 = qtab[0][pil], *q1 = qtab[1][pil];
-    const uint32_t off0 = 32 * wlo0, off1 = 32 * wlo1;
+    /* bit position of data RE idx within the staged words: idx * Qm + (re0 * Qm - 32 wlo) */
+    const uint32_t b0 = re0 * Qm0 - 32 * wlo0, b1 = re0 * Qm1 - 32 * wlo1;
     idft_unit<LOG2N, NA>(
         lds_data + unit * NA * LDSW, t, active, twr,
-        [&](int n, s16x2 *x) {
-          /* branch-free so the 16 remap loads and LDS chains of a thread overlap; an RE outside
-           * the allocation reads data RE 0 (inside the staged words) and is zeroed by the select */
-          const uint32_t code = rm[t + T * n];
-          const bool valid = code < OAI4G_CRS_CODE;               /* a PDSCH data RE */
-          const uint32_t idx = valid ? (code & 0x7FFFu) : 0u;
-          const uint32_t p0 = (idx + re0) * Qm0 - off0;
-          uint32_t v0 = q0[__builtin_amdgcn_alignbit(e0[(p0 >> 5) + 1], e0[p0 >> 5], p0 & 31) & mask0], v1 = 0;
-          if (n_cw > 1) {
-            const uint32_t p1 = (idx + re0) * Qm1 - off1;
-            v1 = q1[__builtin_amdgcn_alignbit(e1[(p1 >> 5) + 1], e1[p1 >> 5], p1 & 31) & mask1];
-          }
-          const s16x2 x0 = u2c(valid ? v0 : 0u), x1 = u2c(valid ? v1 : 0u);
-          if constexpr (NA == 2) {
-            cdd_pair(x0, x1, code >> 15 & 1u, x[0], x[1]);
-          } else {
-            x[0] = cdd ? (s16x2){(short)(((int)x0.x + (int)x1.x) >> 1), (short)(((int)x0.y + (int)x1.y) >> 1)} : x0;
-          }
-          if (crs) {
-            /* cell-specific RS (pilots.c:43-168): overwrite the antenna carrying port p */
-            const bool pil_re = code >= OAI4G_CRS_CODE && code != 0xFFFFu;
-            const uint32_t ci = (code >> 9) & 3u, m = code & 0xFFu, port = (code >> 8) & 1u;
-            const uint32_t pv = pil_re ? crs_tab[(sfi * 4 + ci) * 200 + m] : 0u;
+        [&](s16x2 (*x)[16]) {
+          /* branch-free and staged in groups of GR REs so each LDS round trip is issued for the
+           * whole group before the first wait: codes -> bit offsets -> e words -> QAM words.  An RE
+           * outside the allocation reads data RE 0 (inside the staged words), zeroed by the select */
+#ifndef OAI4G_MOD_GROUP
+#define OAI4G_MOD_GROUP 4   /* REs whose LDS round trips are issued together (register budget) */
+#endif
+          constexpr int GR = OAI4G_MOD_GROUP;
 #pragma unroll
-            for (int a = 0; a < NA; a++)
-              if (pil_re) x[a] = (NA == 1 || (uint32_t)a == port) ? u2c(pv) : (s16x2){0, 0};
+          for (int g = 0; g < 16; g += GR) {
+            uint32_t code[GR], p[GR], lo[GR], hi[GR], v0[GR], v1[GR];
+#pragma unroll
+            for (int n = 0; n < GR; n++) {
+              code[n] = (rw[(g + n) >> 1] >> (16 * ((g + n) & 1))) & 0xFFFFu;
+              p[n] = __umul24(code[n] < OAI4G_CRS_CODE ? (code[n] & 0x7FFFu) : 0u, Qm0) + b0;
+            }
+#pragma unroll
+            for (int n = 0; n < GR; n++) { lo[n] = e0[p[n] >> 5]; hi[n] = e0[(p[n] >> 5) + 1]; }
+#pragma unroll
+            for (int n = 0; n < GR; n++) v0[n] = q0[__builtin_amdgcn_alignbit(hi[n], lo[n], p[n] & 31) & mask0];
+            if constexpr (CW2) {
+#pragma unroll
+              for (int n = 0; n < GR; n++) {
+                p[n] = __umul24(code[n] < OAI4G_CRS_CODE ? (code[n] & 0x7FFFu) : 0u, Qm1) + b1;
+                lo[n] = e1[p[n] >> 5];
+                hi[n] = e1[(p[n] >> 5) + 1];
+              }
+#pragma unroll
+              for (int n = 0; n < GR; n++) v1[n] = q1[__builtin_amdgcn_alignbit(hi[n], lo[n], p[n] & 31) & mask1];
+            }
+#pragma unroll
+            for (int n = 0; n < GR; n++) {
+              const bool valid = code[n] < OAI4G_CRS_CODE;         /* a PDSCH data RE */
+              const s16x2 x0 = u2c(valid ? v0[n] : 0u);
+              if constexpr (NA == 2) {
+                const s16x2 x1 = CW2 ? u2c(valid ? v1[n] : 0u) : (s16x2){0, 0};
+                cdd_pair(x0, x1, code[n] >> 15 & 1u, x[0][g + n], x[1][g + n]);
+              } else {
+                x[0][g + n] = x0;                                   /* TM1: SISO precoder */
+              }
+            }
+          }
+          if constexpr (CRS) {
+            if (crs) {
+              /* cell-specific RS (pilots.c:43-168): overwrite the antenna carrying port p */
+#pragma unroll
+              for (int n = 0; n < 16; n++) {
+                const uint32_t cd = (rw[n >> 1] >> (16 * (n & 1))) & 0xFFFFu;
+                const bool pil_re = cd >= OAI4G_CRS_CODE && cd != 0xFFFFu;
+                const uint32_t ci = (cd >> 9) & 3u, m = cd & 0xFFu, port = (cd >> 8) & 1u;
+                const uint32_t pv = pil_re ? crs_tab[(sfi * 4 + ci) * 200 + m] : 0u;
+#pragma unroll
+                for (int a = 0; a < NA; a++)
+                  if (pil_re) x[a][n] = (NA == 1 || (uint32_t)a == port) ? u2c(pv) : (s16x2){0, 0};
+              }
+            }
           }
         },
         [&](int a, int tt, int off, s16x2 y) {
@@ -585,21 +618,41 @@ __global__ void __launch_bounds__(128) MODOFDM_ATTR k_modofdm(const cfg_dev_t *_
   }
 }
 
-template <int LOG2N, int NA>
+template <int LOG2N, int NA, bool CW2, bool CRS>
 static hipError_t launch_modofdm_t(const cfg_dev_t *d_cfg, const cfg_dev_t *h_cfg, int sf0, int n_items,
                                    const uint32_t *d_ebits, int32_t *d_iq, hipStream_t s)
 {
   static int occ = 0;
   if (!occ) {
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, k_modofdm<LOG2N, NA>, 128, 0) != hipSuccess || occ < 1)
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, k_modofdm<LOG2N, NA, CW2, CRS>, 128, 0) != hipSuccess ||
+        occ < 1)
       occ = 1;
   }
   const int units = modofdm_geom<LOG2N>::UNITS;
   int want = (n_items + units - 1) / units, cap = occ * (int)h_cfg->n_cu;
   int grid = want < cap ? want : cap;
   if (grid < 1) grid = 1;
-  hipLaunchKernelGGL((k_modofdm<LOG2N, NA>), dim3(grid), dim3(128), 0, s, d_cfg, n_items, d_ebits, d_iq, (uint32_t)sf0);
+  hipLaunchKernelGGL((k_modofdm<LOG2N, NA, CW2, CRS>), dim3(grid), dim3(128), 0, s, d_cfg, n_items, d_ebits, d_iq,
+                     (uint32_t)sf0);
   return hipGetLastError();
+}
+
+/* antenna transforms per unit (NA), second codeword (LARGE_CDD only) and CRS are uniform per
+ * configuration and become template arguments: no per-RE uniform branches in the prologue */
+template <int LOG2N>
+static hipError_t launch_modofdm_n(const cfg_dev_t *d_cfg, const cfg_dev_t *h_cfg, int sf0, int n_items,
+                                   const uint32_t *d_ebits, int32_t *d_iq, hipStream_t s)
+{
+  const bool two = h_cfg->mimo_mode == OAI4G_LARGE_CDD, crs = h_cfg->with_crs != 0, cw2 = h_cfg->n_cw > 1;
+  if (two) {
+    if (cw2)
+      return crs ? launch_modofdm_t<LOG2N, 2, true, true>(d_cfg, h_cfg, sf0, n_items, d_ebits, d_iq, s)
+                 : launch_modofdm_t<LOG2N, 2, true, false>(d_cfg, h_cfg, sf0, n_items, d_ebits, d_iq, s);
+    return crs ? launch_modofdm_t<LOG2N, 2, false, true>(d_cfg, h_cfg, sf0, n_items, d_ebits, d_iq, s)
+               : launch_modofdm_t<LOG2N, 2, false, false>(d_cfg, h_cfg, sf0, n_items, d_ebits, d_iq, s);
+  }
+  return crs ? launch_modofdm_t<LOG2N, 1, false, true>(d_cfg, h_cfg, sf0, n_items, d_ebits, d_iq, s)
+             : launch_modofdm_t<LOG2N, 1, false, false>(d_cfg, h_cfg, sf0, n_items, d_ebits, d_iq, s);
 }
 
 /* subframes [sf0, sf0 + n_sf) of a batch whose e-bit words / IQ start at d_ebits / d_iq */
@@ -611,17 +664,12 @@ hipError_t oai4g_launch_modofdm(const cfg_dev_t *d_cfg, const cfg_dev_t *h_cfg, 
   d_ebits += (size_t)sf0 * h_cfg->n_cw * h_cfg->ebits_words;
   d_iq += (size_t)sf0 * h_cfg->n_ant * h_cfg->spt;
   /* two antenna transforms per unit only when they differ (LARGE_CDD); TM1 stores one n_ant times */
-  const bool two = h_cfg->mimo_mode == OAI4G_LARGE_CDD && h_cfg->n_ant == 2;
   if (h_cfg->mimo_mode == OAI4G_LARGE_CDD && h_cfg->n_ant != 2) return hipErrorInvalidValue;
   switch (h_cfg->log2N) {
-  case 7: return two ? launch_modofdm_t<7, 2>(d_cfg, h_cfg, sf0, n_items, d_ebits, d_iq, s)
-                     : launch_modofdm_t<7, 1>(d_cfg, h_cfg, sf0, n_items, d_ebits, d_iq, s);
-  case 8: return two ? launch_modofdm_t<8, 2>(d_cfg, h_cfg, sf0, n_items, d_ebits, d_iq, s)
-                     : launch_modofdm_t<8, 1>(d_cfg, h_cfg, sf0, n_items, d_ebits, d_iq, s);
-  case 10: return two ? launch_modofdm_t<10, 2>(d_cfg, h_cfg, sf0, n_items, d_ebits, d_iq, s)
-                      : launch_modofdm_t<10, 1>(d_cfg, h_cfg, sf0, n_items, d_ebits, d_iq, s);
-  case 11: return two ? launch_modofdm_t<11, 2>(d_cfg, h_cfg, sf0, n_items, d_ebits, d_iq, s)
-                      : launch_modofdm_t<11, 1>(d_cfg, h_cfg, sf0, n_items, d_ebits, d_iq, s);
+  case 7: return launch_modofdm_n<7>(d_cfg, h_cfg, sf0, n_items, d_ebits, d_iq, s);
+  case 8: return launch_modofdm_n<8>(d_cfg, h_cfg, sf0, n_items, d_ebits, d_iq, s);
+  case 10: return launch_modofdm_n<10>(d_cfg, h_cfg, sf0, n_items, d_ebits, d_iq, s);
+  case 11: return launch_modofdm_n<11>(d_cfg, h_cfg, sf0, n_items, d_ebits, d_iq, s);
   default: return hipErrorInvalidValue;
   }
 }
