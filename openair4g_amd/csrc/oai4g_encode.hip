@@ -142,8 +142,9 @@ static __device__ __forceinline__ void gold_step(uint32_t &x1, uint32_t &x2)
 
 typedef const __attribute__((address_space(1))) uint32_t gu32_t;
 
-/* Gold words 0..nwords-1 (word w = state after 50+w steps): lane l jumps to word 16l with the
- * host's M^(50+16l) tables and steps 16 words.  Needs blockDim.x == OAI4G_GOLD_LANES. */
+/* Gold words 0..nwords-1 (word w = state after 50+w steps): lane l jumps to word S l with the
+ * host's M^(50+S l) tables and steps S = OAI4G_GOLD_STRIDE words.  Needs blockDim.x ==
+ * OAI4G_GOLD_LANES. */
 static __device__ __forceinline__ void gold_generate(uint32_t *gold, uint32_t nwords, uint32_t c_init,
                                                      const uint32_t *gx1, const uint32_t *gx2j)
 {
@@ -600,18 +601,93 @@ static __device__ void encode_codeword(const cfg_dev_t *__restrict__ c, uint32_t
   __syncthreads();
   if (stop_phase <= 2) return;
 
-  /* ---- phase 3a: QPP-interleaved input words of every block (region A is free again) ---- */
+  /* ---- phase 3a: QPP-interleaved input words of every block, folded by quarters.  With
+   * Q = K/4, Pi(k + qQ) = Pi(k) + q c4 (mod K), so one walk over k < Q reads output bits k, k+Q,
+   * k+2Q, k+3Q from four rotations of c at the same position Pi(k): plane_r[x] = c[(x + rQ) mod K].
+   * Plane 0 is the systematic stream, planes 1 / 2 are staged in the (not yet written) parity
+   * stream slots of the block, plane 3 in region A behind the interleaved words. ---- */
   uint32_t *ilv = lds_base;
-  {
-    const uint32_t nw = cw.ilv_off[C];
-    for (uint32_t i = tid; i < nw; i += nth) {
-      uint32_t r = 0;
-      while (r + 1 < C && i >= cw.ilv_off[r + 1]) r++;
-      const uint32_t j = i - cw.ilv_off[r], ki = cw.kidx[r];
-      ilv[i] = qpp_gather_word(strm + r * 3 * sw, cw.K[r], cw.qpp0[ki][j], cw.qpp_d2[ki], j);
+  const uint32_t nw = cw.ilv_off[C], u0 = cw.u0, n0 = cw.n0;
+  uint32_t *pl3 = lds_base + nw;
+  /* word i of the interleaved space -> block r, word j, block size K (no per-lane table walks;
+   * the two block sizes are read once as wave-uniform values, selects stay in registers) */
+  const uint32_t kw0 = __builtin_amdgcn_readfirstlane(cw.kw[0]), kw1 = __builtin_amdgcn_readfirstlane(cw.kw[1]);
+  const uint32_t km0 = __builtin_amdgcn_readfirstlane(cw.kmag[0]), km1 = __builtin_amdgcn_readfirstlane(cw.kmag[1]);
+  const uint32_t kk0 = __builtin_amdgcn_readfirstlane(cw.kk[0]), kk1 = __builtin_amdgcn_readfirstlane(cw.kk[1]);
+  auto unit_of = [&](uint32_t i, uint32_t &r, uint32_t &j, uint32_t &K, uint32_t &ki) {
+    ki = i >= u0 ? 1u : 0u;
+    const uint32_t ii = ki ? i - u0 : i, kw = ki ? kw1 : kw0;
+    const uint32_t rr = __umul24(ii, ki ? km1 : km0) >> 20;
+    j = ii - __umul24(rr, kw);
+    r = ki ? n0 + rr : rr;
+    K = ki ? kk1 : kk0;
+  };
+  /* rotated planes 1..3 of every block: uniform loops over (block, plane), a word per lane */
+  for (uint32_t r = 0; r < C; r++) {
+    const uint32_t K = r < n0 ? kk0 : kk1, Kw = (K + 31) >> 5, Q = K >> 2, io = r < n0 ? r * kw0 : u0 + (r - n0) * kw1;
+    const uint32_t *sys = strm + r * 3 * sw;
+    for (uint32_t w = tid; w < Kw; w += nth) ilv[io + w] = 0u;
+#pragma unroll
+    for (uint32_t pr = 1; pr <= 3; pr++) {
+      uint32_t *dst = pr < 3 ? strm + (r * 3 + pr) * sw : pl3 + io;
+      for (uint32_t w = tid; w < Kw; w += nth) {
+        uint32_t src = 32 * w + pr * Q;
+        src = src >= K ? src - K : src;
+        const uint32_t wi = src >> 5;
+        const uint32_t lo = sys[wi], hi = wi + 1 < Kw ? sys[wi + 1] : 0u;   /* bits >= K are zero */
+        uint32_t v = __builtin_amdgcn_alignbit(hi, lo, src);
+        if (src + 32 > K) v |= sys[0] << (K - src);                          /* wrap to c_0.. */
+        dst[w] = v;
+      }
     }
   }
   __syncthreads();
+  {
+    /* 8-step units: unit j of block r walks k = 8j .. 8j+7 (< Q) and yields one byte of each
+     * quarter; there are ceil(K/32) units per block, indexed like the interleaved words */
+    const uint32_t d2a = __builtin_amdgcn_readfirstlane(cw.qpp_d2[0]), d2b = __builtin_amdgcn_readfirstlane(cw.qpp_d2[1]);
+    const bool s3a = __builtin_amdgcn_readfirstlane(cw.qpp_s3[0]) != 0, s3b = __builtin_amdgcn_readfirstlane(cw.qpp_s3[1]) != 0;
+    for (uint32_t i = tid; i < nw; i += nth) {
+      uint32_t r, j, K, ki;
+      unit_of(i, r, j, K, ki);
+      const uint32_t Q = K >> 2, start = cw.qpp0[ki][j], d2 = ki ? d2b : d2a;
+      const uint32_t *p0 = strm + r * 3 * sw, *p3 = pl3 + (i - j);
+      uint32_t pi = start & 0xffffu, dl = start >> 16, a0 = 0, a1 = 0, a2 = 0, a3 = 0;
+#pragma unroll
+      for (int b = 0; b < 8; b++) {
+        const uint32_t wi = pi >> 5;
+        a0 |= __builtin_amdgcn_ubfe(p0[wi], pi, 1u) << b;
+        a1 |= __builtin_amdgcn_ubfe(p0[wi + sw], pi, 1u) << b;
+        a2 |= __builtin_amdgcn_ubfe(p0[wi + 2 * sw], pi, 1u) << b;
+        a3 |= __builtin_amdgcn_ubfe(p3[wi], pi, 1u) << b;
+        pi += dl;
+        pi = min(pi, pi - K);
+        dl += d2;
+        dl = min(dl, dl - K);
+      }
+      const uint32_t n = Q - 8 * j;
+      if (n < 8) {
+        const uint32_t m = (1u << n) - 1u;
+        a0 &= m; a1 &= m; a2 &= m; a3 &= m;
+      }
+      /* output quarter q reads plane (q c4 / Q) mod 4 */
+      const bool s3 = ki ? s3b : s3a;
+      const uint32_t q1 = s3 ? a3 : a1, q3 = s3 ? a1 : a3;
+      uint32_t *o = ilv + (i - j);
+      if ((Q & 7u) == 0) {                                  /* byte-aligned quarters (32 | K) */
+        uint8_t *ob = (uint8_t *)o + j;
+        const uint32_t qb = Q >> 3;
+        ob[0] = (uint8_t)a0; ob[qb] = (uint8_t)q1; ob[2 * qb] = (uint8_t)a2; ob[3 * qb] = (uint8_t)q3;
+      } else {
+        or_bits(o, 8 * j, a0);
+        or_bits(o, Q + 8 * j, q1);
+        or_bits(o, 2 * Q + 8 * j, a2);
+        or_bits(o, 3 * Q + 8 * j, q3);
+      }
+    }
+  }
+  __syncthreads();
+  if (stop_phase == 23) return;   /* diagnostics: QPP interleaving only */
 
   /* ---- phase 3b: turbo encoding, one wave per (block, encoder) ---- */
   for (uint32_t seg = wave; seg < 2 * C; seg += nwaves) {
@@ -679,12 +755,24 @@ static __device__ void encode_codeword(const cfg_dev_t *__restrict__ c, uint32_t
    * at w bit bitrev5(c) R + row.  Interlaced tiles are 16 rows of y^(1) and y^(2) alternating
    * (lane 2i: y^(1) row, lane 2i+1: y^(2) row, pre-shifted by one for the (pi(k)+1) mod Kpi
    * rule), so the transposed run is already w's v^(1)/v^(2) interlacing, at bit
-   * Kpi + 2 (bitrev5(c) R + row).  The host lists the tiles (cw.tasks). ---- */
+   * Kpi + 2 (bitrev5(c) R + row).  Tile t maps to its block in closed form. ---- */
+  /* block geometry of the two block sizes as wave-uniform scalars (closed-form per-block offsets) */
+  const uint32_t R0 = __builtin_amdgcn_readfirstlane(cw.Rk[0]), R1 = __builtin_amdgcn_readfirstlane(cw.Rk[1]);
+  const uint32_t ws0 = 3 * R0 + 2, ws1 = 3 * R1 + 2;     /* packed w words per block (wpk_off stride) */
   {
+    const uint32_t ND0 = __builtin_amdgcn_readfirstlane(cw.NDk[0]), ND1 = __builtin_amdgcn_readfirstlane(cw.NDk[1]);
+    const uint32_t nt0 = __builtin_amdgcn_readfirstlane(cw.ntk[0]), nt1 = __builtin_amdgcn_readfirstlane(cw.ntk[1]);
+    const uint32_t tz0 = __builtin_amdgcn_readfirstlane(cw.t0k[0]), tz1 = __builtin_amdgcn_readfirstlane(cw.t0k[1]);
+    const uint32_t nm0 = __builtin_amdgcn_readfirstlane(cw.ntmag[0]), nm1 = __builtin_amdgcn_readfirstlane(cw.ntmag[1]);
+    const uint32_t tsplit = n0 * nt0, ntot = tsplit + (C - n0) * nt1;
     const uint32_t lane32 = tid & 31, wcol = colperm(lane32);
-    for (uint32_t t = tid >> 5; t < cw.ntask; t += nth >> 5) {
-      const uint32_t code = cw.tasks[t], r = code & 15u, il = (code >> 4) & 1u, rb = code >> 5;
-      const uint32_t R = cw.R[r], ND = cw.ND[r];
+    for (uint32_t t = tid >> 5; t < ntot; t += nth >> 5) {
+      /* tile t -> block r (tiles of block r: ceil(R/32) v0 tiles, then ceil(R/16) interlaced) */
+      const uint32_t ki = t >= tsplit ? 1u : 0u, tt = ki ? t - tsplit : t;
+      const uint32_t rr = __umul24(tt, ki ? nm1 : nm0) >> 20, rem = tt - __umul24(rr, ki ? nt1 : nt0);
+      const uint32_t r = ki ? n0 + rr : rr, R = ki ? R1 : R0, ND = ki ? ND1 : ND0, tz = ki ? tz1 : tz0;
+      const uint32_t il = rem >= tz ? 1u : 0u, rb = il ? rem - tz : rem;
+      const uint32_t wpk = ki ? n0 * ws0 + rr * ws1 : rr * ws0;
       const uint32_t row = il ? 16 * rb + (lane32 >> 1) : 32 * rb + lane32, s = il ? 1 + (lane32 & 1) : 0;
       const uint32_t *st = strm + (r * 3 + s) * sw;
       uint32_t y = 0;
@@ -696,7 +784,7 @@ static __device__ void encode_codeword(const cfg_dev_t *__restrict__ c, uint32_t
         }
       }
       y = transpose32(y, lane32);
-      or_bits(wb + cw.wpk_off[r], il ? cw.Kpi[r] + 2 * (wcol * R + 16 * rb) : wcol * R + 32 * rb, y);
+      or_bits(wb + wpk, il ? 32 * R + 2 * (wcol * R + 16 * rb) : wcol * R + 32 * rb, y);
     }
   }
   __syncthreads();
@@ -704,34 +792,48 @@ static __device__ void encode_codeword(const cfg_dev_t *__restrict__ c, uint32_t
 
   /* ---- phase 4c: rate matching (lte_rate_matching.c:548-566) of every block, XORed into the
    * Gold-prefilled staging words; each thread walks a run of consecutive output words ---- */
-  const uint32_t *roff = cw.roff[sfi];
-  uint32_t nwtot = 0;
-  for (uint32_t r = 0; r < C; r++) nwtot += (roff[r + 1] - roff[r] + 31) >> 5;
   {
+    /* blocks r < es carry E_lo bits (W_lo words), the rest E_hi (36.212 5.1.4.1.2) */
+    const uint32_t es = __builtin_amdgcn_readfirstlane(cw.esplit[sfi]);
+    const uint32_t Elo = __builtin_amdgcn_readfirstlane(cw.E[sfi][0]), Ehi = __builtin_amdgcn_readfirstlane(cw.E[sfi][C - 1]);
+    const uint32_t Wlo = __builtin_amdgcn_readfirstlane(cw.ew[sfi][0]), Whi = __builtin_amdgcn_readfirstlane(cw.ew[sfi][1]);
+    const uint32_t Mlo = __builtin_amdgcn_readfirstlane(cw.emag[sfi][0]), Mhi = __builtin_amdgcn_readfirstlane(cw.emag[sfi][1]);
+    const uint32_t Ncb0 = __builtin_amdgcn_readfirstlane(cw.Ncbk[0]), Ncb1 = __builtin_amdgcn_readfirstlane(cw.Ncbk[1]);
+    const uint32_t Nnn0 = __builtin_amdgcn_readfirstlane(cw.Nnnk[0]), Nnn1 = __builtin_amdgcn_readfirstlane(cw.Nnnk[1]);
+    const uint32_t k0c0 = __builtin_amdgcn_readfirstlane(cw.k0ck[0]), k0c1 = __builtin_amdgcn_readfirstlane(cw.k0ck[1]);
+    const uint32_t nn0 = __builtin_amdgcn_readfirstlane(cw.nnull[0]), nn1 = __builtin_amdgcn_readfirstlane(cw.nnull[1]);
+    const uint32_t wsplit = es * Wlo, nwtot = wsplit + (C - es) * Whi;
     const uint32_t per = (nwtot + nth - 1) / nth, i0 = tid * per, i1 = min(i0 + per, nwtot);
-    uint32_t r = 0, acc = 0;
+    /* each thread walks a run of consecutive output words [i0, i1) */
+    uint32_t r = 0, k = 0;
     if (i0 < i1) {
-      for (;;) {
-        uint32_t nwo = (roff[r + 1] - roff[r] + 31) >> 5;
-        if (r + 1 == C || i0 < acc + nwo) break;
-        acc += nwo;
-        r++;
-      }
+      const bool hi = i0 >= wsplit;
+      const uint32_t ii = hi ? i0 - wsplit : i0, W = hi ? Whi : Wlo;
+      uint32_t q = __umulhi(ii, hi ? Mhi : Mlo);
+      q = q * W > ii ? q - 1 : q;
+      r = hi ? es + q : q;
+      k = ii - q * W;
     }
-    uint32_t k = i0 - acc, p = 0, m = 0, nwo = 0, nn = 0;
+    uint32_t p = 0, m = 0, nwo = 0, nn = 0, Ncb = 0, E = 0, ro = 0, wpk = 0;
     const uint16_t *npl = np;
     bool fresh = true;
     for (uint32_t i = i0; i < i1; i++, k++) {
       if (fresh) {
-        nwo = (roff[r + 1] - roff[r] + 31) >> 5;
-        npl = np + cw.kidx[r] * OAI4G_MAX_NULLS;
-        nn = cw.nnull[cw.kidx[r]];
-        p = compact_to_pos2((cw.k0c[r] + 32 * k) % cw.Nnn[r], npl, nn, m);
+        const uint32_t ki = r < n0 ? 0u : 1u;
+        const bool eh = r >= es;
+        E = eh ? Ehi : Elo;
+        nwo = eh ? Whi : Wlo;
+        ro = eh ? es * Elo + (r - es) * Ehi : r * Elo;
+        npl = np + ki * OAI4G_MAX_NULLS;
+        nn = ki ? nn1 : nn0;
+        Ncb = ki ? Ncb1 : Ncb0;
+        wpk = ki ? n0 * ws0 + (r - n0) * ws1 : r * ws0;
+        p = compact_to_pos2(((ki ? k0c1 : k0c0) + 32 * k) % (ki ? Nnn1 : Nnn0), npl, nn, m);
         fresh = false;
       }
-      const uint32_t E = roff[r + 1] - roff[r], need = min(32u, E - 32 * k);
-      uint32_t out = rm_window(wb + cw.wpk_off[r], p, m, cw.Ncb[r], npl, nn, need);
-      uint32_t gpos = roff[r] + 32 * k, gw = gpos >> 5, off = gpos & 31;
+      const uint32_t need = min(32u, E - 32 * k);
+      uint32_t out = rm_window(wb + wpk, p, m, Ncb, npl, nn, need);
+      uint32_t gpos = ro + 32 * k, gw = gpos >> 5, off = gpos & 31;
       atomicXor(&ebuf[gw], out << off);
       if (off && (out >> (32 - off))) atomicXor(&ebuf[gw + 1], out >> (32 - off));
       if (k + 1 == nwo) {

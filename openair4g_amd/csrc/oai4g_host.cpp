@@ -139,7 +139,7 @@ static void do_init(void)
       tw[OAI4G_TW_TOTAL + off + m] = (uint16_t)(int16_t)(-im) | ((uint32_t)(uint16_t)re << 16);
     }
   }
-  /* Gold: x1 after 50+16l steps; x2 step-matrix powers M2^(50+16l) (columns) */
+  /* Gold: x1 after 50+S l word steps; x2 step-matrix powers M2^(50+S l) (columns), S = OAI4G_GOLD_STRIDE */
   uint32_t x1 = 1u + (1u << 31), cols[32];
   for (int b = 0; b < 32; b++) cols[b] = 1u << b;
   int steps_done = 0;
@@ -603,12 +603,13 @@ static int derive_cfg(oai4g_tx_config *cfg, const oai4g_tx_params_t *p, const ui
       if (K == 0 || (ki == 0 && !(C > 1 && Cm > 0))) continue;
       int qi = oai4g_qpp_index(K);
       uint64_t f1 = oai4g_qpp_table[qi].f1, f2 = oai4g_qpp_table[qi].f2;
-      for (uint32_t j = 0; j < (K + 31) / 32; j++) {
-        uint64_t k = 32 * j;
+      for (uint32_t j = 0; j < (K + 31) / 32; j++) {   /* k = 8j < K/4: walk starts of the quarter fold */
+        uint64_t k = 8 * j;
         uint32_t pi = (uint32_t)((f1 * k + f2 * k * k) % K), pi1 = (uint32_t)((f1 * (k + 1) + f2 * (k + 1) * (k + 1)) % K);
         c.qpp0[ki][j] = pi | (((pi1 + K - pi) % K) << 16);
       }
       c.qpp_d2[ki] = (uint32_t)((2 * f2) % K);
+      c.qpp_s3[ki] = (uint32_t)((f1 * (K / 4)) % K) == K / 4 ? 0u : 1u;
     }
     {
       uint32_t o = 0;
@@ -617,6 +618,14 @@ static int derive_cfg(oai4g_tx_config *cfg, const oai4g_tx_params_t *p, const ui
         o += (c.K[r] + 31) / 32;
       }
       c.ilv_off[C] = o;
+      c.n0 = (C > 1) ? Cm : 0;
+      c.kk[0] = c.n0 ? Km : Kp;
+      c.kk[1] = Kp;
+      for (int ki = 0; ki < 2; ki++) {
+        c.kw[ki] = (c.kk[ki] + 31) / 32;
+        c.kmag[ki] = ((1u << 20) + c.kw[ki] - 1) / c.kw[ki];
+      }
+      c.u0 = c.n0 * c.kw[0];
     }
     c.crc_per_tb = (c.A_bytes + 255) / 256;
     crc_mul_tables(c.crc_per_tb, 8, 0x864cfbu, c.crcmul_tb);
@@ -661,6 +670,25 @@ static int derive_cfg(oai4g_tx_config *cfg, const oai4g_tx_params_t *p, const ui
     }
     c.wpk_off[C] = wwords;
     c.ntask = ntask;
+    for (uint32_t r = 0; r < C; r++) {   /* every block of one size shares its geometry */
+      const uint32_t ki = r < c.n0 ? 0 : 1;
+      if (c.K[r] != c.kk[ki]) { set_err("block size order"); return -1; }
+      c.Rk[ki] = c.R[r]; c.NDk[ki] = c.ND[r]; c.Ncbk[ki] = c.Ncb[r]; c.Nnnk[ki] = c.Nnn[r]; c.k0ck[ki] = c.k0c[r];
+    }
+    for (uint32_t r = 0; r < C; r++) {
+      const uint32_t ki = r < c.n0 ? 0 : 1;
+      if (c.R[r] != c.Rk[ki] || c.ND[r] != c.NDk[ki] || c.Ncb[r] != c.Ncbk[ki] || c.Nnn[r] != c.Nnnk[ki] ||
+          c.k0c[r] != c.k0ck[ki] || c.kidx[r] != ki) {
+        set_err("per-size block geometry differs");
+        return -1;
+      }
+    }
+    if (c.n0 == 0) { c.Rk[0] = c.Rk[1]; c.NDk[0] = c.NDk[1]; c.Ncbk[0] = c.Ncbk[1]; c.Nnnk[0] = c.Nnnk[1]; c.k0ck[0] = c.k0ck[1]; }
+    for (int ki = 0; ki < 2; ki++) {
+      c.t0k[ki] = (c.Rk[ki] + 31) / 32;
+      c.ntk[ki] = c.t0k[ki] + (c.Rk[ki] + 15) / 16;
+      c.ntmag[ki] = ((1u << 20) + c.ntk[ki] - 1) / c.ntk[ki];
+    }
     max_w = wwords > max_w ? wwords : max_w;
     uint32_t tbw = (c.A_bytes + 3 + 3) / 4 + 1;
     max_tb_words = tbw > max_tb_words ? tbw : max_tb_words;
@@ -678,6 +706,12 @@ static int derive_cfg(oai4g_tx_config *cfg, const oai4g_tx_params_t *p, const ui
         off += E;
       }
       c.roff[sf][C] = off;
+      c.esplit[sf] = C - GpmodC;
+      for (int h = 0; h < 2; h++) {
+        const uint32_t E = c.E[sf][h ? C - 1 : 0], w = (E + 31) / 32;
+        c.ew[sf][h] = w;
+        c.emag[sf][h] = w ? (uint32_t)(((1ull << 32) + w - 1) / w) : 0u;
+      }
       uint32_t gw = (off + 31) / 32;
       max_gw = gw > max_gw ? gw : max_gw;
       max_bits = (uint32_t)G > max_bits ? (uint32_t)G : max_bits;
@@ -692,8 +726,8 @@ static int derive_cfg(oai4g_tx_config *cfg, const oai4g_tx_params_t *p, const ui
   (void)max_inw;
   /* encoder LDS regions with phase-disjoint lifetimes (see oai4g_encode.hip) */
   h.lds_a_words = max_tb_words + OAI4G_ENC_CRC_TABLE_WORDS;
-  for (int cw = 0; cw < p->n_cw; cw++)   /* region A also holds the interleaved words in phase 3 */
-    if (h.cw[cw].ilv_off[h.cw[cw].C] > h.lds_a_words) h.lds_a_words = h.cw[cw].ilv_off[h.cw[cw].C];
+  for (int cw = 0; cw < p->n_cw; cw++)   /* region A also holds the interleaved words and plane 3 in phase 3 */
+    if (2 * h.cw[cw].ilv_off[h.cw[cw].C] > h.lds_a_words) h.lds_a_words = 2 * h.cw[cw].ilv_off[h.cw[cw].C];
   if (max_w > h.lds_a_words) h.lds_a_words = max_w;
   h.lds_b_words = max_stream_words;
   /* RE maps */

@@ -21,7 +21,7 @@
 #define OAI4G_CRS_CODE 0xE000u               /* remap codes >= this (and != 0xFFFF) are CRS REs */
 #define OAI4G_ENC_CRC_TABLE_WORDS (256 + 256 + 8 * 96 + 6 * 96) /* byte tables A/B + tree multipliers */
 #define OAI4G_GOLD_LANES 256
-#define OAI4G_GOLD_STRIDE 16
+#define OAI4G_GOLD_STRIDE 17   /* odd: lanes 17l + k hit distinct LDS banks */
 #define OAI4G_MAX_GOLD_WORDS (OAI4G_GOLD_LANES * OAI4G_GOLD_STRIDE) /* >= (14*1200*6)/32 */
 #define OAI4G_TW_TOTAL (16 + 64 + 128 + 256 + 512 + 1024 + 2048)
 
@@ -63,10 +63,24 @@ struct cw_dev_t {
   uint32_t ntask;                     /* sub-block interleaver tiles of all blocks */
   uint16_t tasks[OAI4G_MAX_TASKS];    /* block | kind << 4 (0: v0 rows, 1: v1/v2 rows) | tile << 5 */
   uint32_t ilv_off[OAI4G_MAX_CB + 1]; /* LDS word offset of block r's QPP-interleaved input words */
-  /* QPP interleaver walk per 32-bit chunk j (kidx list): Pi(32j) | (Pi(32j+1)-Pi(32j) mod K) << 16,
-   * and the second difference 2 f2 mod K (3gpplte.c:50-74 restated incrementally) */
+  /* QPP interleaver walk per 8-step unit j of the quarter fold (kidx list): Pi(8j) | (Pi(8j+1) -
+   * Pi(8j) mod K) << 16, j < K/32, and the second difference 2 f2 mod K (3gpplte.c:50-74 restated
+   * incrementally) */
   uint32_t qpp0[2][OAI4G_MAX_CHUNKS];
   uint32_t qpp_d2[2];
+  /* quarter folding: Pi(k + K/4) = Pi(k) + c4 mod K with c4 = f1 K/4 mod K in {K/4, 3K/4}
+   * (f2 even, 8 | K); qpp_s3 = (c4 == 3K/4) */
+  uint32_t qpp_s3[2];
+  /* closed-form unit -> (block, word) map of the ilv word space: n0 blocks of size kk[0] first
+   * (u0 = n0 kw[0] words), then blocks of kk[1]; kmag[i] = ceil(2^20 / kw[i]) */
+  uint32_t n0, u0, kk[2], kw[2], kmag[2];
+  /* per block size (index as kk): sub-block interleaver / rate-matching geometry, so the encoder
+   * derives block metadata from wave-uniform scalars instead of per-lane table loads */
+  uint32_t Rk[2], NDk[2], Ncbk[2], Nnnk[2], k0ck[2];
+  uint32_t ntk[2], t0k[2], ntmag[2];   /* tiles per block, v0 tiles per block, ceil(2^20 / ntk) */
+  /* per subframe index: blocks r < esplit have E = E[sf][0], the rest E[sf][C-1]; ew = words of
+   * each, emag = ceil(2^32 / ew) */
+  uint32_t esplit[10], ew[10][2], emag[10][2];
   uint32_t nnull[2];
   uint16_t nullpos[2][OAI4G_MAX_NULLS]; /* sorted NULL positions of w for K = Kminus / Kplus */
   /* per subframe index */

@@ -11,7 +11,7 @@ p = oai.make_params(name)
 pipe = oai.TxPipeline(p, n_sf)
 pipe.fill_payload(1)
 prev = 0.0
-for ph, label in [(0, "load+gold"), (1, "crc"), (2, "segment"), (3, "turbo"), (4, "w-build"), (99, "rm+store")]:
+for ph, label in [(0, "load+gold"), (1, "crc"), (2, "segment"), (23, "qpp-ilv"), (3, "turbo"), (4, "w-build"), (99, "rm+store")]:
     ms = pipe.diag_encode_phase_ms(ph, 5)
     print(f"phase<= {ph:2d} {label:10s} cumulative {ms*1e3:9.1f} us   (+{(ms-prev)*1e3:8.1f})")
     prev = ms

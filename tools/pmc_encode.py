@@ -10,7 +10,7 @@ n_sf = int(sys.argv[2]) if len(sys.argv) > 2 else 2048
 p = oai.make_params(name)
 pipe = oai.TxPipeline(p, n_sf)
 pipe.fill_payload(1)
-for ph in (2, 3, 4, 99):
+for ph in (0, 1, 2, 23, 3, 4, 99):
     pipe.diag_encode_phase_ms(ph, 1)
 pipe.run()
 pipe.sync()
