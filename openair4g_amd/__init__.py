@@ -440,7 +440,7 @@ FULL_ALLOC_50 = (0xFFFFFFFF, 0x3FFFF, 0, 0)
 
 # TBS from 3GPP TS 36.213 Table 7.1.7.2.1-1 for the configurations exercised here
 TBS_TABLE = {(9, 6): 936, (4, 6): 408, (16, 100): 30576, (19, 100): 36696, (9, 100): 15840, (28, 100): 75376,
-             (5, 50): 4392, (15, 50): 14112, (26, 50): 30576}
+             (5, 50): 4392, (15, 50): 14112, (26, 50): 30576, (9, 15): 2344}
 
 CONFIGS = {
     # C1: dlsim 1.4 MHz SISO QPSK (MCS 9), 3 PDCCH symbols
@@ -452,6 +452,12 @@ CONFIGS = {
     # C3: dlsim 20 MHz 2x2 TM3 (LARGE_CDD) 64-QAM, MCS 19 on both codewords (highest the reference encodes)
     "C3": dict(N_RB_DL=100, nb_antennas_tx=2, mode1_flag=0, n_cw=2, mimo_mode=LARGE_CDD, num_pdcch_symbols=1,
                mcs=(19, 19), rb_alloc=FULL_ALLOC_100, nb_rb=100, Kmimo=2),
+    # TM2: dlsim 20 MHz 2 TX transmit diversity (ALAMOUTI, DCI format 1: one codeword, Nl = 1), 16-QAM
+    "TM2": dict(N_RB_DL=100, nb_antennas_tx=2, mode1_flag=0, n_cw=1, mimo_mode=ALAMOUTI, num_pdcch_symbols=1,
+                mcs=(16, 0), rb_alloc=FULL_ALLOC_100, nb_rb=100, Kmimo=1),
+    # TM2 at 1.4 MHz, QPSK (MCS 9), 3 PDCCH symbols
+    "TM2S": dict(N_RB_DL=6, nb_antennas_tx=2, mode1_flag=0, n_cw=1, mimo_mode=ALAMOUTI, num_pdcch_symbols=3,
+                 mcs=(9, 0), rb_alloc=FULL_ALLOC_6, nb_rb=6, Kmimo=1),
 }
 
 

@@ -390,24 +390,32 @@ static void crc_mul_tables(uint32_t per, int levels, uint32_t poly, uint32_t (*t
 }
 
 /* QAM tables (dlsch_modulation.c:79-103, 1223-1246) */
-static void qam_tables_scaled(int Qm, int16_t amp, int16_t srho_a, int16_t srho_b, int16_t *ta, int16_t *tb,
-                              int16_t *qa, int16_t *qb)
+static void qam_tables_scaled(int Qm, int16_t amp, int16_t srho_a, int16_t srho_b, bool alamouti, cw_dev_t &c)
 {
   int16_t q16[4], q64[8];
   for (int a = -1; a <= 1; a += 2)
     for (int b = -1; b <= 1; b += 2) {
       q16[(1 + a) + (1 + b) / 2] = (int16_t)(-a * (20724 + b * 10362));
-      for (int c = -1; c <= 1; c += 2)
-        q64[(1 + a) * 2 + (1 + b) + (1 + c) / 2] = (int16_t)(-a * (20225 + b * (10112 + c * 5056)));
+      for (int cc = -1; cc <= 1; cc += 2)
+        q64[(1 + a) * 2 + (1 + b) + (1 + cc) / 2] = (int16_t)(-a * (20225 + b * (10112 + cc * 5056)));
     }
   int16_t amp_a = (int16_t)(((int32_t)amp * srho_a) >> 13), amp_b = (int16_t)(((int32_t)amp * srho_b) >> 13);
+  c.qpsk_a = (int16_t)((amp_a * 23170) >> 15);
+  c.qpsk_b = (int16_t)((amp_b * 23170) >> 15);
+  /* ALAMOUTI normalises for two antennas: amp/sqrt2 times the raw table (:364, :398-399) */
+  const int16_t sa = alamouti ? (int16_t)(((int32_t)amp_a * 23170) >> 15) : amp_a;
+  const int16_t sb = alamouti ? (int16_t)(((int32_t)amp_b * 23170) >> 15) : amp_b;
   for (int i = 0; i < 8; i++) {
     int16_t v = Qm == 4 ? q16[i & 3] : q64[i];
-    ta[i] = (int16_t)(((int32_t)v * amp_a) >> 15);
-    tb[i] = (int16_t)(((int32_t)v * amp_b) >> 15);
+    c.qam_a[i] = (int16_t)(((int32_t)v * sa) >> 15);
+    c.qam_b[i] = (int16_t)(((int32_t)v * sb) >> 15);
   }
-  *qa = (int16_t)((amp_a * 23170) >> 15);
-  *qb = (int16_t)((amp_b * 23170) >> 15);
+  /* ALAMOUTI QPSK (:371-386): +-gain, then * ONE_OVER_SQRT2_Q15 >> 15 */
+  const int16_t g[2] = {c.qpsk_a, c.qpsk_b};
+  for (int pil = 0; pil < 2; pil++) {
+    c.alm_qpsk[pil][0] = (int16_t)(((int32_t)g[pil] * 23170) >> 15);
+    c.alm_qpsk[pil][1] = (int16_t)(((int32_t)(int16_t)-g[pil] * 23170) >> 15);
+  }
 }
 
 /* ------------------------------------------------------------------------------------------
@@ -424,8 +432,11 @@ static int not_pilot(int pilots, int re, int nushift, int use2nd)
 }
 
 static int build_remap(const oai4g_frame_parms_t *fp, const uint32_t *rb_alloc, int num_pdcch, int subframe,
-                       uint16_t *remap /* [14][N] */, uint32_t *symbase /* [14] */)
+                       int mimo_mode, uint16_t *remap /* [14][N] */, uint32_t *symbase /* [14] */,
+                       int *re_alloc /* the reference's re_allocated */)
 {
+  const bool alm = mimo_mode == OAI4G_ALAMOUTI;
+  int ralloc = 0;
   int N = fp->ofdm_symbol_size, nsymb = fp->Ncp == 0 ? 14 : 12, half = fp->N_RB_DL >> 1;
   int use2nd = fp->mode1_flag == 1;
   for (int i = 0; i < 14 * N; i++) remap[i] = 0xFFFF;
@@ -480,8 +491,27 @@ static int build_remap(const oai4g_frame_parms_t *fp, const uint32_t *rb_alloc, 
           if (!not_pilot(pilots, re, fp->nushift, use2nd)) continue;
           int k = re_off + re;
           if (k < 0 || k >= N) return -1;
+          if (alm) {
+            /* ALAMOUTI pair (:362-546, :868-876): symbols 2i, 2i+1 at RE n and its partner, the
+             * next carrier or the one after when that is a pilot (linear grid index); code =
+             * 2i | role.  A partner outside this symbol's row or on an RE that is written twice
+             * would need accumulation: not produced by any supported grid, rejected here. */
+            int k2 = k + (not_pilot(pilots, re + 1, fp->nushift, use2nd) ? 1 : 2);
+            if (k2 >= N || remap[l * N + k] != 0xFFFF || remap[l * N + k2] != 0xFFFF) return -1;
+            remap[l * N + k] = (uint16_t)idx;
+            remap[l * N + k2] = (uint16_t)(idx | 1u);
+            idx += 2;
+            ralloc += 2;
+            re++;
+            if (!not_pilot(pilots, re, fp->nushift, use2nd)) {
+              re++;
+              ralloc++;          /* the reference also counts the pilot it steps over */
+            }
+            continue;
+          }
           remap[l * N + k] = (uint16_t)(idx | (par << 15));
           idx++;
+          ralloc++;
           par ^= 1;
         }
       }
@@ -490,6 +520,7 @@ static int build_remap(const oai4g_frame_parms_t *fp, const uint32_t *rb_alloc, 
     }
     total += idx;
   }
+  if (re_alloc) *re_alloc = ralloc;
   return (int)total;
 }
 
@@ -506,6 +537,7 @@ struct oai4g_tx_config {
   uint32_t *d_crs = nullptr;
   std::vector<uint32_t> h_crs;          /* [10][4][200] packed CRS IQ */
   int re_count[10];
+  int re_alloc[10];                 /* dlsch_modulation's return value (ALAMOUTI counts skipped pilots) */
   /* optional pipelined batches (OAI4G_PIPE_CHUNK=n): the encoder runs on the caller's stream, the
    * modulator/IDFT on s_mod, chunk by chunk.  Off by default: measured slower on MI355X than the
    * serial pair (the persistent modulator grid already fills every CU). */
@@ -526,8 +558,12 @@ static int derive_cfg(oai4g_tx_config *cfg, const oai4g_tx_params_t *p, const ui
     return -1;
   cfg_dev_t &h = cfg->h;
   if (p->n_cw < 1 || p->n_cw > 2) { set_err("n_cw must be 1 or 2"); return -1; }
-  if (p->mimo_mode != OAI4G_SISO && p->mimo_mode != OAI4G_LARGE_CDD) {
-    set_err("mimo_mode %u not supported (SISO and LARGE_CDD only)", p->mimo_mode);
+  if (p->mimo_mode != OAI4G_SISO && p->mimo_mode != OAI4G_LARGE_CDD && p->mimo_mode != OAI4G_ALAMOUTI) {
+    set_err("mimo_mode %u not supported (SISO, ALAMOUTI and LARGE_CDD)", p->mimo_mode);
+    return -1;
+  }
+  if (p->mimo_mode == OAI4G_ALAMOUTI && (p->nb_antennas_tx != 2 || p->n_cw != 1)) {
+    set_err("ALAMOUTI requires 2 TX antennas and one codeword (dlsch_modulation.c:362)");
     return -1;
   }
   if (p->mimo_mode == OAI4G_LARGE_CDD && (p->nb_antennas_tx != 2 || p->n_cw != 2)) {
@@ -716,7 +752,7 @@ static int derive_cfg(oai4g_tx_config *cfg, const oai4g_tx_params_t *p, const ui
       max_gw = gw > max_gw ? gw : max_gw;
       max_bits = (uint32_t)G > max_bits ? (uint32_t)G : max_bits;
     }
-    qam_tables_scaled((int)c.Qm, p->amp, p->sqrt_rho_a, p->sqrt_rho_b, c.qam_a, c.qam_b, &c.qpsk_a, &c.qpsk_b);
+    qam_tables_scaled((int)c.Qm, p->amp, p->sqrt_rho_a, p->sqrt_rho_b, p->mimo_mode == OAI4G_ALAMOUTI, c);
   }
   if (max_gw > OAI4G_MAX_GOLD_WORDS) { set_err("G too large"); return -1; }
   h.lds_tb_words = max_tb_words;
@@ -736,8 +772,8 @@ static int derive_cfg(oai4g_tx_config *cfg, const oai4g_tx_params_t *p, const ui
     cfg->h_remap.assign((size_t)10 * 14 * N, 0xFFFF);
     for (int sf = 0; sf < 10; sf++) {
       if (only_sf >= 0 && sf != only_sf) continue;
-      int n = build_remap(&fp, p->rb_alloc, p->num_pdcch_symbols, sf, cfg->h_remap.data() + (size_t)sf * 14 * N,
-                          h.symbase[sf]);
+      int n = build_remap(&fp, p->rb_alloc, p->num_pdcch_symbols, sf, p->mimo_mode,
+                          cfg->h_remap.data() + (size_t)sf * 14 * N, h.symbase[sf], &cfg->re_alloc[sf]);
       if (n < 0) { set_err("RE map construction failed"); return -1; }
       cfg->re_count[sf] = n;
       if (p->with_crs) {
@@ -1285,7 +1321,8 @@ extern "C" int oai4g_dlsch_modulation(int32_t **txdataF, int16_t amp, uint32_t s
   if (h0->Nlayers > 1) return -1;
   p.amp = amp;
   if (p.mimo_mode == OAI4G_LARGE_CDD && !dlsch1) p.n_cw = 1;
-  if (p.mimo_mode != OAI4G_SISO && p.mimo_mode != OAI4G_LARGE_CDD) {
+  if (p.mimo_mode == OAI4G_ALAMOUTI) p.n_cw = 1;       /* both symbols of a pair come from dlsch0 */
+  if (p.mimo_mode != OAI4G_SISO && p.mimo_mode != OAI4G_LARGE_CDD && p.mimo_mode != OAI4G_ALAMOUTI) {
     set_err("dlsch_modulation: mimo_mode %u not supported", p.mimo_mode);
     return -1;
   }
@@ -1320,8 +1357,9 @@ extern "C" int oai4g_dlsch_modulation(int32_t **txdataF, int16_t amp, uint32_t s
     HCK(hipMemcpyAsync(txdataF[aa] + sym_off, buf + (size_t)aa * nsymb * N * 4, (size_t)nsymb * N * 4,
                        hipMemcpyDeviceToHost, g_scr.s), -1);
   HCK(hipStreamSynchronize(g_scr.s), -1);
+  const int ret = cfg.re_alloc[sf];
   release_cfg(&cfg);
-  return (int)n_re;
+  return ret;
 }
 
 /* ------------------------------------------------------------------------------------------

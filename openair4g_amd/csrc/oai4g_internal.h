@@ -89,6 +89,9 @@ struct cw_dev_t {
   uint32_t roff[10][OAI4G_MAX_CB + 1];
   int16_t qam_a[8], qam_b[8];   /* amp_rho-scaled QAM levels (dlsch_modulation.c:1223-1246) */
   int16_t qpsk_a, qpsk_b;
+  /* ALAMOUTI (dlsch_modulation.c:362-546): qam_a/qam_b hold the 1/sqrt2-scaled levels
+   * (amp/sqrt2 * table >> 15) and the QPSK symbol is scaled after its sign: [pilot][+g, -g] */
+  int16_t alm_qpsk[2][2];
   uint32_t stream_words;        /* LDS words per stream per block (padded) */
   /* CRC tree combine (x^(8*per*2^d) mod P as 6 nibble tables of 16 entries per level) */
   uint32_t crc_per_tb;          /* bytes per lane, 256 lanes, CRC-24A over the TB */

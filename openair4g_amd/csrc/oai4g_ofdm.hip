@@ -445,6 +445,33 @@ static __device__ __forceinline__ void cdd_pair(s16x2 x0, s16x2 x1, uint32_t par
   y1 = parity ? (s16x2){0, 0} - d : d;
 }
 
+/* ALAMOUTI levels (dlsch_modulation.c:362-546): TA = antenna 0 at RE n (x0/sqrt2), TB = antenna
+ * 1 at n (-conj(x1)/sqrt2); QPSK signs are applied before the 1/sqrt2 scaling, QAM negation after */
+static __device__ __forceinline__ s16x2 alm_ta(uint32_t bits, const cw_dev_t &w, uint32_t pil)
+{
+  if (w.Qm == 2) {
+    const short p = w.alm_qpsk[pil][0], n = w.alm_qpsk[pil][1];
+    return (s16x2){(bits & 1) ? n : p, (bits & 2) ? n : p};
+  }
+  return qam_map(bits, w.Qm, pil ? w.qam_b : w.qam_a, 0);
+}
+static __device__ __forceinline__ s16x2 alm_tb(uint32_t bits, const cw_dev_t &w, uint32_t pil)
+{
+  if (w.Qm == 2) {
+    const short p = w.alm_qpsk[pil][0], n = w.alm_qpsk[pil][1];
+    return (s16x2){(bits & 1) ? p : n, (bits & 2) ? n : p};
+  }
+  const s16x2 v = qam_map(bits, w.Qm, pil ? w.qam_b : w.qam_a, 0);
+  return (s16x2){(short)-v.x, v.y};
+}
+/* antenna values of an ALAMOUTI RE from its pair's TA / TB: role 0 = RE n, role 1 = the partner,
+ * (-TB.re, TB.im) and (TA.re, -TA.im) (:535-545) */
+static __device__ __forceinline__ void alm_pair(s16x2 ta, s16x2 tb, uint32_t role, s16x2 &y0, s16x2 &y1)
+{
+  y0 = role ? (s16x2){(short)-tb.x, tb.y} : ta;
+  y1 = role ? (s16x2){ta.x, (short)-ta.y} : tb;
+}
+
 /* ======================================================================================
  * Fused: packed scrambled e bits -> QAM -> RE map -> precoding -> IDFT -> CP -> IQ.
  * Persistent 128-thread workgroups; a unit of T threads owns one (subframe, symbol) at a time
@@ -465,13 +492,16 @@ struct modofdm_geom {
 #else
 #define MODOFDM_ATTR
 #endif
-template <int LOG2N, int NA, bool CW2, bool CRS>
+/* MODE: 0 = TM1 (one transform stored to every antenna), 1 = ALAMOUTI, 2 = LARGE_CDD */
+template <int LOG2N, int MODE, bool CRS>
 __global__ void __launch_bounds__(128) MODOFDM_ATTR k_modofdm(const cfg_dev_t *__restrict__ c, int n_items,
                                                  const uint32_t *__restrict__ ebits, int32_t *__restrict__ iq,
                                                  uint32_t sf0)
 {
   using G = modofdm_geom<LOG2N>;
   constexpr int N = G::N, T = G::T, UNITS = G::UNITS, LDSW = G::LDSW, EW = G::EW;
+  constexpr int NA = MODE == 0 ? 1 : 2;
+  constexpr bool CW2 = MODE == 2;
   __shared__ uint32_t lds_data[UNITS * NA * LDSW];
   __shared__ uint32_t lds_e[UNITS][2][EW];
   __shared__ uint32_t qtab[2][2][64];          /* [cw][pilot symbol][Qm bits] -> packed IQ */
@@ -481,8 +511,13 @@ __global__ void __launch_bounds__(128) MODOFDM_ATTR k_modofdm(const cfg_dev_t *_
   const uint32_t n_ant = c->n_ant, nsymb = c->nsymb;
   for (uint32_t i = threadIdx.x; i < 256; i += blockDim.x) {
     const uint32_t cw = i >> 7, pil = (i >> 6) & 1, bits = i & 63;
-    const cw_dev_t &w = c->cw[cw];
-    qtab[cw][pil][bits] = c2u(qam_map(bits, w.Qm, pil ? w.qam_b : w.qam_a, pil ? w.qpsk_b : w.qpsk_a));
+    if constexpr (MODE == 1) {          /* one codeword: [0] = TA, [1] = TB */
+      const cw_dev_t &w = c->cw[0];
+      qtab[cw][pil][bits] = c2u(cw ? alm_tb(bits, w, pil) : alm_ta(bits, w, pil));
+    } else {
+      const cw_dev_t &w = c->cw[cw];
+      qtab[cw][pil][bits] = c2u(qam_map(bits, w.Qm, pil ? w.qam_b : w.qam_a, pil ? w.qpsk_b : w.qpsk_a));
+    }
   }
   const uint32_t Qm0 = c->cw[0].Qm, Qm1 = c->cw[1].Qm;
   const uint32_t mask0 = (1u << Qm0) - 1u, mask1 = (1u << Qm1) - 1u;
@@ -549,15 +584,26 @@ __global__ void __launch_bounds__(128) MODOFDM_ATTR k_modofdm(const cfg_dev_t *_
 #pragma unroll
           for (int g = 0; g < 16; g += GR) {
             uint32_t code[GR], p[GR], lo[GR], hi[GR], v0[GR], v1[GR];
+            /* ALAMOUTI codes are 2i | role: both symbols of pair i start at bit 2i Qm */
+            constexpr uint32_t IDXM = MODE == 1 ? 0x7FFEu : 0x7FFFu;
 #pragma unroll
             for (int n = 0; n < GR; n++) {
               code[n] = (rw[(g + n) >> 1] >> (16 * ((g + n) & 1))) & 0xFFFFu;
-              p[n] = __umul24(code[n] < OAI4G_CRS_CODE ? (code[n] & 0x7FFFu) : 0u, Qm0) + b0;
+              p[n] = __umul24(code[n] < OAI4G_CRS_CODE ? (code[n] & IDXM) : 0u, Qm0) + b0;
             }
 #pragma unroll
             for (int n = 0; n < GR; n++) { lo[n] = e0[p[n] >> 5]; hi[n] = e0[(p[n] >> 5) + 1]; }
+            if constexpr (MODE == 1) {
 #pragma unroll
-            for (int n = 0; n < GR; n++) v0[n] = q0[__builtin_amdgcn_alignbit(hi[n], lo[n], p[n] & 31) & mask0];
+              for (int n = 0; n < GR; n++) {
+                const uint32_t wv = __builtin_amdgcn_alignbit(hi[n], lo[n], p[n] & 31);
+                v0[n] = q0[wv & mask0];
+                v1[n] = q1[(wv >> Qm0) & mask0];
+              }
+            } else {
+#pragma unroll
+              for (int n = 0; n < GR; n++) v0[n] = q0[__builtin_amdgcn_alignbit(hi[n], lo[n], p[n] & 31) & mask0];
+            }
             if constexpr (CW2) {
 #pragma unroll
               for (int n = 0; n < GR; n++) {
@@ -572,7 +618,9 @@ __global__ void __launch_bounds__(128) MODOFDM_ATTR k_modofdm(const cfg_dev_t *_
             for (int n = 0; n < GR; n++) {
               const bool valid = code[n] < OAI4G_CRS_CODE;         /* a PDSCH data RE */
               const s16x2 x0 = u2c(valid ? v0[n] : 0u);
-              if constexpr (NA == 2) {
+              if constexpr (MODE == 1) {
+                alm_pair(x0, u2c(valid ? v1[n] : 0u), code[n] & 1u, x[0][g + n], x[1][g + n]);
+              } else if constexpr (NA == 2) {
                 const s16x2 x1 = CW2 ? u2c(valid ? v1[n] : 0u) : (s16x2){0, 0};
                 cdd_pair(x0, x1, code[n] >> 15 & 1u, x[0][g + n], x[1][g + n]);
               } else {
@@ -618,13 +666,13 @@ __global__ void __launch_bounds__(128) MODOFDM_ATTR k_modofdm(const cfg_dev_t *_
   }
 }
 
-template <int LOG2N, int NA, bool CW2, bool CRS>
+template <int LOG2N, int MODE, bool CRS>
 static hipError_t launch_modofdm_t(const cfg_dev_t *d_cfg, const cfg_dev_t *h_cfg, int sf0, int n_items,
                                    const uint32_t *d_ebits, int32_t *d_iq, hipStream_t s)
 {
   static int occ = 0;
   if (!occ) {
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, k_modofdm<LOG2N, NA, CW2, CRS>, 128, 0) != hipSuccess ||
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, k_modofdm<LOG2N, MODE, CRS>, 128, 0) != hipSuccess ||
         occ < 1)
       occ = 1;
   }
@@ -632,27 +680,29 @@ static hipError_t launch_modofdm_t(const cfg_dev_t *d_cfg, const cfg_dev_t *h_cf
   int want = (n_items + units - 1) / units, cap = occ * (int)h_cfg->n_cu;
   int grid = want < cap ? want : cap;
   if (grid < 1) grid = 1;
-  hipLaunchKernelGGL((k_modofdm<LOG2N, NA, CW2, CRS>), dim3(grid), dim3(128), 0, s, d_cfg, n_items, d_ebits, d_iq,
+  hipLaunchKernelGGL((k_modofdm<LOG2N, MODE, CRS>), dim3(grid), dim3(128), 0, s, d_cfg, n_items, d_ebits, d_iq,
                      (uint32_t)sf0);
   return hipGetLastError();
 }
 
-/* antenna transforms per unit (NA), second codeword (LARGE_CDD only) and CRS are uniform per
- * configuration and become template arguments: no per-RE uniform branches in the prologue */
+/* precoding mode and CRS are uniform per configuration and become template arguments: no
+ * per-RE uniform branches in the prologue */
 template <int LOG2N>
 static hipError_t launch_modofdm_n(const cfg_dev_t *d_cfg, const cfg_dev_t *h_cfg, int sf0, int n_items,
                                    const uint32_t *d_ebits, int32_t *d_iq, hipStream_t s)
 {
-  const bool two = h_cfg->mimo_mode == OAI4G_LARGE_CDD, crs = h_cfg->with_crs != 0, cw2 = h_cfg->n_cw > 1;
-  if (two) {
-    if (cw2)
-      return crs ? launch_modofdm_t<LOG2N, 2, true, true>(d_cfg, h_cfg, sf0, n_items, d_ebits, d_iq, s)
-                 : launch_modofdm_t<LOG2N, 2, true, false>(d_cfg, h_cfg, sf0, n_items, d_ebits, d_iq, s);
-    return crs ? launch_modofdm_t<LOG2N, 2, false, true>(d_cfg, h_cfg, sf0, n_items, d_ebits, d_iq, s)
-               : launch_modofdm_t<LOG2N, 2, false, false>(d_cfg, h_cfg, sf0, n_items, d_ebits, d_iq, s);
+  const bool crs = h_cfg->with_crs != 0;
+  switch (h_cfg->mimo_mode) {
+  case OAI4G_LARGE_CDD:
+    return crs ? launch_modofdm_t<LOG2N, 2, true>(d_cfg, h_cfg, sf0, n_items, d_ebits, d_iq, s)
+               : launch_modofdm_t<LOG2N, 2, false>(d_cfg, h_cfg, sf0, n_items, d_ebits, d_iq, s);
+  case OAI4G_ALAMOUTI:
+    return crs ? launch_modofdm_t<LOG2N, 1, true>(d_cfg, h_cfg, sf0, n_items, d_ebits, d_iq, s)
+               : launch_modofdm_t<LOG2N, 1, false>(d_cfg, h_cfg, sf0, n_items, d_ebits, d_iq, s);
+  default:
+    return crs ? launch_modofdm_t<LOG2N, 0, true>(d_cfg, h_cfg, sf0, n_items, d_ebits, d_iq, s)
+               : launch_modofdm_t<LOG2N, 0, false>(d_cfg, h_cfg, sf0, n_items, d_ebits, d_iq, s);
   }
-  return crs ? launch_modofdm_t<LOG2N, 1, false, true>(d_cfg, h_cfg, sf0, n_items, d_ebits, d_iq, s)
-             : launch_modofdm_t<LOG2N, 1, false, false>(d_cfg, h_cfg, sf0, n_items, d_ebits, d_iq, s);
 }
 
 /* subframes [sf0, sf0 + n_sf) of a batch whose e-bit words / IQ start at d_ebits / d_iq */
@@ -663,8 +713,10 @@ hipError_t oai4g_launch_modofdm(const cfg_dev_t *d_cfg, const cfg_dev_t *h_cfg, 
   const int n_items = n_sf * (int)h_cfg->nsymb;
   d_ebits += (size_t)sf0 * h_cfg->n_cw * h_cfg->ebits_words;
   d_iq += (size_t)sf0 * h_cfg->n_ant * h_cfg->spt;
-  /* two antenna transforms per unit only when they differ (LARGE_CDD); TM1 stores one n_ant times */
-  if (h_cfg->mimo_mode == OAI4G_LARGE_CDD && h_cfg->n_ant != 2) return hipErrorInvalidValue;
+  /* two antenna transforms per unit only when they differ (LARGE_CDD, ALAMOUTI); TM1 stores one
+   * n_ant times */
+  if (h_cfg->mimo_mode != OAI4G_SISO && h_cfg->n_ant != 2) return hipErrorInvalidValue;
+  if (h_cfg->mimo_mode == OAI4G_LARGE_CDD && h_cfg->n_cw != 2) return hipErrorInvalidValue;
   switch (h_cfg->log2N) {
   case 7: return launch_modofdm_n<7>(d_cfg, h_cfg, sf0, n_items, d_ebits, d_iq, s);
   case 8: return launch_modofdm_n<8>(d_cfg, h_cfg, sf0, n_items, d_ebits, d_iq, s);
@@ -686,11 +738,33 @@ __global__ void __launch_bounds__(256) k_modulate_bytes(const cfg_dev_t *__restr
   uint32_t gid = blockIdx.x * blockDim.x + threadIdx.x;
   if (gid >= nsymb * N) return;
   uint32_t l = gid / N, k = gid % N;
-  uint32_t code = c->remap[((size_t)sfi * 14 + l) * N + k];
+  const uint16_t *row = c->remap + ((size_t)sfi * 14 + l) * N;
+  uint32_t code = row[k];
   if (code >= OAI4G_CRS_CODE) return;                 /* no data RE (CRS codes included) */
   const cw_dev_t &cw0 = c->cw[0];
   const cw_dev_t &cw1 = c->cw[1];
   bool pil = pilots_of(l) != 0;
+  if (c->mimo_mode == OAI4G_ALAMOUTI) {
+    /* the thread of RE n writes n and its partner: the partner adds the accumulated values
+     * of n (dlsch_modulation.c:535-545) */
+    if (code & 1u) return;
+    const uint32_t k2 = (k + 1 < N && row[k + 1] == (code | 1u)) ? k + 1 : k + 2;
+    const uint32_t base = ((code & 0x7FFEu) + c->symbase[sfi][l]) * cw0.Qm;
+    uint32_t ba = 0, bb = 0;
+    for (uint32_t i = 0; i < cw0.Qm; i++) {
+      ba |= (uint32_t)(e0[base + i] == 1) << i;
+      bb |= (uint32_t)(e0[base + cw0.Qm + i] == 1) << i;
+    }
+    uint32_t *g0 = (uint32_t *)grid + l * N, *g1 = g0 + (size_t)nsymb * N;
+    const s16x2 n0 = caddw(u2c(g0[k]), alm_ta(ba, cw0, pil)), n1 = caddw(u2c(g1[k]), alm_tb(bb, cw0, pil));
+    g0[k] = c2u(n0);
+    g1[k] = c2u(n1);
+    s16x2 y0, y1;
+    alm_pair(n0, n1, 1u, y0, y1);
+    g0[k2] = c2u(caddw(u2c(g0[k2]), y0));
+    g1[k2] = c2u(caddw(u2c(g1[k2]), y1));
+    return;
+  }
   uint32_t idx = (code & 0x7FFFu) + c->symbase[sfi][l];
   uint32_t b0 = 0, b1 = 0;
   /* the reference tests x[jj] == 1 per bit: any other byte value reads as 0 */

@@ -298,7 +298,7 @@ int orc_init_frame(orc_frame_t *fp, uint16_t N_RB_DL, uint16_t Nid_cell, uint8_t
 
 /* ======================================================================================
  * Modulation + RE mapping — dlsch_modulation.c:53-71 (is_not_pilot), :79-103 (QAM tables),
- * :139-982 (allocate_REs_in_RB: SISO and LARGE_CDD branches), :1181-1493 (dlsch_modulation).
+ * :139-982 (allocate_REs_in_RB: SISO, ALAMOUTI and LARGE_CDD branches), :1181-1493 (dlsch_modulation).
  * ==================================================================================== */
 static int16_t qam16_tab[4], qam64_tab[8];
 
@@ -445,6 +445,47 @@ static int modulation_impl(int32_t **txdataF, int16_t amp, uint32_t subframe, ui
             acc16(&txdataF[0][tti], 1, (i0 + i1) >> 1);
             acc16(&txdataF[1][tti], 1, s * ((i0 - i1) >> 1));
             s = -s;
+          } else if (cw0->mimo_mode == 1 && fp->nb_antennas_tx == 2) {         /* ALAMOUTI :362-546 */
+            /* antenna 0 at n: x0/sqrt2; antenna 1 at n: -conj(x1)/sqrt2 (both symbols from codeword 0) */
+            int16_t amp2 = (int16_t)(((int32_t)(pilots ? amp_b : amp_a) * 23170) >> 15);
+            int16_t v[4];
+            if (Qm0 == 2) {
+              const int16_t g = gain;
+              int16_t t1r = (cw0->e[jj] == 1) ? (int16_t)-g : g; jj++;
+              int16_t t1i = (cw0->e[jj] == 1) ? (int16_t)-g : g; jj++;
+              int16_t t2r = (cw0->e[jj] == 1) ? g : (int16_t)-g; jj++;
+              int16_t t2i = (cw0->e[jj] == 1) ? (int16_t)-g : g; jj++;
+              v[0] = (int16_t)((t1r * 23170) >> 15); v[1] = (int16_t)((t1i * 23170) >> 15);
+              v[2] = (int16_t)((t2r * 23170) >> 15); v[3] = (int16_t)((t2i * 23170) >> 15);
+            } else {
+              const int16_t *raw = Qm0 == 4 ? qam16_tab : qam64_tab;
+              int ir, ii;
+              qam_index(cw0->e, &jj, Qm0, &ir, &ii);
+              v[0] = (int16_t)(((int32_t)amp2 * raw[ir]) >> 15);
+              v[1] = (int16_t)(((int32_t)amp2 * raw[ii]) >> 15);
+              qam_index(cw0->e, &jj, Qm0, &ir, &ii);
+              v[2] = (int16_t)-(int16_t)(((int32_t)amp2 * raw[ir]) >> 15);
+              v[3] = (int16_t)(((int32_t)amp2 * raw[ii]) >> 15);
+            }
+            acc16(&txdataF[0][tti], 0, v[0]);
+            acc16(&txdataF[0][tti], 1, v[1]);
+            acc16(&txdataF[1][tti], 0, v[2]);
+            acc16(&txdataF[1][tti], 1, v[3]);
+            /* partner RE (:535-545): the next carrier, or the one after when that is a pilot;
+             * linear grid index (no DC re-offset), from the accumulated values at n */
+            uint32_t t2 = tti + (not_pilot(pilots, re + 1, fp->nushift, use2nd) ? 1u : 2u);
+            const int16_t *n0 = (const int16_t *)&txdataF[0][tti], *n1 = (const int16_t *)&txdataF[1][tti];
+            acc16(&txdataF[0][t2], 0, -n1[0]);
+            acc16(&txdataF[0][t2], 1, n1[1]);
+            acc16(&txdataF[1][t2], 0, n0[0]);
+            acc16(&txdataF[1][t2], 1, -n0[1]);
+            /* :868-876: skip the partner (and a pilot before it), counting both */
+            re++;
+            re_allocated++;
+            if (!not_pilot(pilots, re, fp->nushift, use2nd)) {
+              re++;
+              re_allocated++;
+            }
           } else {
             return -1;                                                          /* mode not restated */
           }
@@ -727,6 +768,9 @@ void orc_generate_pilots_subframe(int32_t **txdataF, int16_t amp, const orc_fram
   pilots_one(txdataF, amp, fp, table, (2u * subframe) % 20);
 }
 
+static int g_last_re_allocated = 0;
+int orc_last_re_allocated(void) { return g_last_re_allocated; }
+
 int orc_tx_subframe(const orc_tx_cfg_t *cfg, uint8_t *payload[2], int32_t **txdataF, int32_t **txdata,
                     uint8_t *e_out[2])
 {
@@ -772,6 +816,7 @@ int orc_tx_subframe(const orc_tx_cfg_t *cfg, uint8_t *payload[2], int32_t **txda
   if (cfg->with_crs) orc_generate_pilots_subframe(txdataF, cfg->amp, fp, cfg->subframe);   /* dlsim.c:2681-2684 */
   int ret = modulation_impl(txdataF, cfg->amp, cfg->subframe, 0, fp, cfg->num_pdcch_symbols, &c0,
                             cfg->n_cw > 1 ? &c1 : NULL, cfg->sqrt_rho_a, cfg->sqrt_rho_b);
+  g_last_re_allocated = ret;
   for (int aa = 0; aa < fp->nb_antennas_tx; aa++)
     for (int slot = 0; slot < 2; slot++)
       orc_normal_prefix_mod(txdataF[aa] + slot * N * 7, txdata[aa] + slot * (fp->samples_per_tti >> 1), 7, fp);

@@ -81,7 +81,7 @@ int orc_init_frame(orc_frame_t *fp, uint16_t N_RB_DL, uint16_t Nid_cell, uint8_t
                    uint8_t mode1_flag, uint8_t frame_type);
 
 /* ---- modulation + RE mapping (dlsch_modulation.c:139-1493) ----
- * mimo_mode: 0 = SISO, 1 = ALAMOUTI (not restated), 2 = LARGE_CDD */
+ * mimo_mode: 0 = SISO, 1 = ALAMOUTI, 2 = LARGE_CDD */
 typedef struct {
   const uint8_t *e;
   uint8_t mcs;
@@ -133,6 +133,7 @@ typedef struct {
 } orc_tx_cfg_t;
 int orc_tx_subframe(const orc_tx_cfg_t *cfg, uint8_t *payload[2], int32_t **txdataF, int32_t **txdata,
                     uint8_t *e_out[2] /* optional: scrambled e bytes per cw */);
+int orc_last_re_allocated(void);   /* dlsch_modulation's return value of the last orc_tx_subframe */
 
 /* ---- uplink turbo decoding (oai_oracle_td.c; 3gpplte_turbo_decoder_sse_16bit.c:945-1385,
  *      lte_rate_matching.c:193-243, 688-831) ---- */

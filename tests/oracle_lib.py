@@ -207,6 +207,12 @@ def tx_subframe(cfg, payloads, want_e=False):
     return np.stack(txd), np.stack(txF), es
 
 
+def modulation_count(cfg):
+    """dlsch_modulation's return value (re_allocated) for the subframe of cfg."""
+    tx_subframe(cfg, [np.zeros(cfg.TBS[cw] // 8 + 8, dtype=np.uint8) for cw in range(cfg.n_cw)])
+    return orc().orc_last_re_allocated()
+
+
 def generate_pilots(fp, amp, ntti=10):
     """Reference-layout frame grid(s) with CRS (pilots.c:43-168): [n_ant][ntti * 14 * N] int32."""
     N = fp.ofdm_symbol_size

@@ -13,9 +13,13 @@ own translation units cannot be built here ("Oracle and pinning")
   rate_match(...)         36.212 5.1.4.1.2 (Ncb, E per block, k0, circular selection)
   gold(c_init, n)         36.211 7.2 (length-31 Gold sequence, Nc = 1600)
   crs(...)                36.211 6.10.1 (cell-specific reference signals: sequence and mapping)
+  alamouti_grid(...)      36.211 6.3.4.3 / 6.3.5 (transmit diversity layer pairs on consecutive
+                          data REs), with the reference's fixed-point scaling rules
 
 Pure Python loops: use the small sizes of the CPU suite.
 """
+import numpy as np
+
 NULL = 2
 CRC24A = [24, 23, 18, 17, 14, 11, 10, 7, 6, 5, 4, 3, 1, 0]
 CRC24B = [24, 23, 6, 5, 1, 0]
@@ -156,3 +160,77 @@ def crs(N_RB, Nid, subframe, port, amp, N, first_carrier, Ncp=0):
                 fbin = first_carrier + k if k < 6 * N_RB else k - 6 * N_RB + 1
                 out[(slot * nsymb + lsym, fbin)] = (a * (1 - 2 * c[2 * mp]), a * (1 - 2 * c[2 * mp + 1]))
     return out
+
+
+# ------------------------------------------------------------------ transmit diversity (36.211 6.3.4.3)
+def _w16(v):
+    return ((int(v) + 32768) & 0xFFFF) - 32768
+
+
+# QAM levels in Q15 (16-QAM: 1/sqrt10 (2 +- 1); 64-QAM: 1/sqrt42 (4 +- (2 +- 1))).  The reference
+# keeps them in int16 tables, so the outermost 64-QAM level 7/sqrt42 = 35393 wraps to -30143
+# (dlsch_modulation.c:79-103 assigning into int16_t qam64_table); the model stores them the same way.
+QAM16_RAW = {}
+QAM64_RAW = {}
+for _a in (-1, 1):
+    for _b in (-1, 1):
+        QAM16_RAW[(1 + _a) + (1 + _b) // 2] = _w16(-_a * (20724 + _b * 10362))
+        for _c in (-1, 1):
+            QAM64_RAW[(1 + _a) * 2 + (1 + _b) + (1 + _c) // 2] = _w16(-_a * (20225 + _b * (10112 + _c * 5056)))
+
+
+def _sym_index(bits, Qm):
+    """(re, im) level indices of one QAM symbol: bit pairs alternate re / im, MSB weight first."""
+    ir = ii = 0
+    for j in range(0, Qm, 2):
+        w = 1 << ((Qm - 2 - j) >> 1)
+        ir += w * bits[j]
+        ii += w * bits[j + 1]
+    return ir, ii
+
+
+def alamouti_grid(e, N_RB, N, first_carrier, nushift, npdcch, Qm, amp=512, srho=8192):
+    """Transmit-diversity RE grid of one subframe (2 antennas, even N_RB, no PBCH/sync
+    exclusions): layer pairs x(2i), x(2i+1) go to consecutive data REs in frequency-first order
+    (36.211 6.3.4.3, 6.3.5): RE 2i: (x0, -x1*)/sqrt2, RE 2i+1: (x1, x0*)/sqrt2, in the
+    reference's fixed point (dlsch_modulation.c:362-546): amp_rho = amp*rho >> 13; QPSK +-g with
+    g = amp_rho/sqrt2 then a second 1/sqrt2 after the sign; QAM (amp_rho/sqrt2) * level >> 15
+    with the conjugate's negation applied after the scaling."""
+    ampr = (amp * srho) >> 13
+    g = (ampr * 23170) >> 15
+    a2 = (ampr * 23170) >> 15
+    raw = QAM16_RAW if Qm == 4 else QAM64_RAW
+    grid = np.zeros((2, 14 * N, 2), dtype=np.int64)
+    v = nushift % 3
+    pos = 0
+    for l in range(npdcch, 14):
+        pil = l in (4, 7, 11)
+        data = []
+        for rb in range(N_RB):
+            off = first_carrier + 12 * rb
+            if off >= N:
+                off = off - N + 1              # past DC (even N_RB)
+            for re in range(12):
+                if pil and re in (v, v + 3, v + 6, v + 9):
+                    continue
+                data.append(l * N + off + re)
+        assert len(data) % 2 == 0
+        for i in range(0, len(data), 2):
+            xa = [int(b) for b in e[pos:pos + Qm]]
+            xb = [int(b) for b in e[pos + Qm:pos + 2 * Qm]]
+            pos += 2 * Qm
+            if Qm == 2:
+                ta = (((-g if xa[0] else g) * 23170) >> 15, ((-g if xa[1] else g) * 23170) >> 15)
+                tb = (((g if xb[0] else -g) * 23170) >> 15, ((-g if xb[1] else g) * 23170) >> 15)
+            else:
+                ra, ia = _sym_index(xa, Qm)
+                rb_, ib = _sym_index(xb, Qm)
+                ta = ((a2 * raw[ra]) >> 15, (a2 * raw[ia]) >> 15)
+                tb = (-((a2 * raw[rb_]) >> 15), (a2 * raw[ib]) >> 15)
+            n, m = data[i], data[i + 1]
+            grid[0, n] = ta
+            grid[1, n] = tb
+            grid[0, m] = (_w16(-tb[0]), tb[1])
+            grid[1, m] = (ta[0], _w16(-ta[1]))
+    out = (grid[..., 0] & 0xFFFF) | ((grid[..., 1] & 0xFFFF) << 16)
+    return out.astype(np.uint32).view(np.int32), pos

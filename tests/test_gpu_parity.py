@@ -116,7 +116,8 @@ def test_rate_matching_rm_condition(gpu):
     assert len(e) == 0
 
 
-@pytest.mark.parametrize("name,subframe", [("C1", 7), ("C2", 7), ("C3", 7), ("C2", 0), ("C3", 5)])
+@pytest.mark.parametrize("name,subframe", [("C1", 7), ("C2", 7), ("C3", 7), ("C2", 0), ("C3", 5), ("TM2", 7),
+                                          ("TM2", 0), ("TM2S", 5)])
 def test_dlsch_encoding_scrambling_modulation(gpu, name, subframe):
     """The drop-in dlsch_encoding -> dlsch_scrambling -> dlsch_modulation chain vs the oracle."""
     p = gpu.make_params(name, subframe=subframe)
@@ -153,14 +154,21 @@ def test_dlsch_encoding_scrambling_modulation(gpu, name, subframe):
     N = p.N_RB_DL and fp.ofdm_symbol_size
     txF = [np.zeros(10 * 14 * N, dtype=np.int32) for _ in range(p.nb_antennas_tx)]
     n_re = gpu.dlsch_modulation(txF, 512, subframe, fp, p.num_pdcch_symbols, dls[0], dls[1] if p.n_cw > 1 else None)
-    assert n_re > 0
+    assert n_re == _re_allocated(p, subframe), name
     for aa in range(p.nb_antennas_tx):
         got = txF[aa][subframe * 14 * N:(subframe + 1) * 14 * N]
         assert np.array_equal(got, txF_o[aa]), (name, aa)
 
 
-def _pipeline_check(gpu, name, n_sf, first_sf, step, check_idx=None, seed=7):
-    p = gpu.make_params(name, subframe=first_sf, subframe_step=step)
+def _re_allocated(p, subframe):
+    """dlsch_modulation's return value from the oracle (ALAMOUTI also counts the pilot it steps
+    over inside a pair, dlsch_modulation.c:868-876)."""
+    cfg = O.tx_cfg_from_params(p, subframe)
+    return O.modulation_count(cfg)
+
+
+def _pipeline_check(gpu, name, n_sf, first_sf, step, check_idx=None, seed=7, **over):
+    p = gpu.make_params(name, subframe=first_sf, subframe_step=step, **over)
     pipe = gpu.TxPipeline(p, n_sf)
     rng = np.random.default_rng(seed)
     pay = rng.integers(0, 256, size=(n_sf, p.n_cw, p.payload_stride), dtype=np.uint8)
@@ -183,9 +191,17 @@ def _pipeline_check(gpu, name, n_sf, first_sf, step, check_idx=None, seed=7):
 
 
 @pytest.mark.parametrize("name,n_sf,first,step", [("C1", 10, 0, 1), ("C2", 3, 7, 0), ("C3", 10, 0, 1),
-                                                  ("C2", 10, 3, 1)])
+                                                  ("C2", 10, 3, 1), ("TM2", 10, 0, 1), ("TM2S", 10, 0, 1)])
 def test_pipeline_bit_exact(gpu, name, n_sf, first, step):
     _pipeline_check(gpu, name, n_sf, first, step)
+
+
+@pytest.mark.parametrize("nid", [0, 1, 2, 5])
+def test_pipeline_tm2_odd_bandwidth(gpu, nid):
+    """ALAMOUTI on 15 PRB (odd N_RB: the middle RB straddles DC; PBCH/sync half-RB exclusions in
+    subframes 0 and 5), every CRS shift class."""
+    _pipeline_check(gpu, "TM2S", 10, 0, 1, seed=nid, N_RB_DL=15, rb_alloc=gpu.FULL_ALLOC_15, nb_rb=15,
+                    num_pdcch_symbols=2, Nid_cell=nid)
 
 
 def test_pipeline_full_size_c3(gpu):
@@ -199,7 +215,8 @@ def test_pipeline_full_size_c3(gpu):
 
 
 # ---------------------------------------------------------------- CRS (A12)
-@pytest.mark.parametrize("name,n_sf,first,step,nid", [("C1", 10, 0, 1, 0), ("C2", 4, 4, 1, 77), ("C3", 10, 0, 1, 301)])
+@pytest.mark.parametrize("name,n_sf,first,step,nid", [("C1", 10, 0, 1, 0), ("C2", 4, 4, 1, 77), ("C3", 10, 0, 1, 301),
+                                                      ("TM2", 10, 0, 1, 41)])
 def test_pipeline_with_crs_bit_exact(gpu, name, n_sf, first, step, nid):
     p = gpu.make_params(name, subframe=first, subframe_step=step, Nid_cell=nid, with_crs=1)
     pipe = gpu.TxPipeline(p, n_sf)
