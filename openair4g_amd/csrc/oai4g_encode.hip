@@ -383,31 +383,45 @@ static __device__ __forceinline__ bool wwalk_null(const wwalk_t &w, uint32_t R, 
   return (cp + 1 < ND) || (w.col == 31 && R == 1 && ND > 0);
 }
 
-/* 32 bits of a packed LSB-first LDS bit array starting at bit `pos` (pos may be negative: zeros) */
+/* 32 bits of a packed LSB-first LDS bit array starting at bit `pos` (pos >= -32: zeros before 0) */
 static __device__ __forceinline__ uint32_t sx32(const uint32_t *a, int pos)
 {
-  int wi = pos >> 5;
-  uint32_t off = (uint32_t)pos & 31u;
-  uint32_t lo = a[(uint32_t)max(wi, 0)];
-  lo = wi >= 0 ? lo : 0u;
-  uint32_t hi = a[(uint32_t)max(wi + 1, 0)];
-  hi = wi + 1 >= 0 ? hi : 0u;
-  return off ? (lo >> off) | (hi << (32 - off)) : lo;
+  const int wi = pos >> 5;
+  const uint32_t lo = a[(uint32_t)max(wi, 0)] & (wi >= 0 ? 0xffffffffu : 0u);
+  const uint32_t hi = a[(uint32_t)(wi + 1)];
+  return __builtin_amdgcn_alignbit(hi, lo, (uint32_t)pos & 31u);
+}
+
+/* lane l ^ J of the 32-lane half: DPP quad permutes for 1 and 2, ds_swizzle (bit mode) above */
+template <uint32_t J>
+static __device__ __forceinline__ uint32_t xor_lane(uint32_t x)
+{
+  if constexpr (J == 1) return (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0xB1, 0xf, 0xf, false);   /* [1,0,3,2] */
+  else if constexpr (J == 2) return (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0x4E, 0xf, 0xf, false); /* [2,3,0,1] */
+  else return (uint32_t)__builtin_amdgcn_ds_swizzle((int)x, (int)((J << 10) | 0x1f));
 }
 
 /* 32x32 bit transpose across the 32 lanes of a half-wave: lane c ends with bit i = bit c of
- * lane i's input */
-static __device__ __forceinline__ uint32_t transpose32(uint32_t x, uint32_t lane32)
+ * lane i's input.  Branch-free butterfly: stage j exchanges the j-bit blocks that differ between
+ * partners l and l^j; the partner's word is rotated into place (right by j in the upper lane,
+ * left by j in the lower) and merged with a bit-field insert whose mask flips with the lane. */
+template <int K = 0>
+static __device__ __forceinline__ uint32_t transpose32_t(uint32_t x, uint32_t lane32)
 {
-  constexpr uint32_t m[5] = {0x0000ffffu, 0x00ff00ffu, 0x0f0f0f0fu, 0x33333333u, 0x55555555u};
-#pragma unroll
-  for (int k = 0; k < 5; k++) {
-    const uint32_t j = 16u >> k;
-    uint32_t p = __shfl_xor(x, j, 32);
-    x = (lane32 & j) ? ((x & ~m[k]) | ((p >> j) & m[k])) : ((x & m[k]) | ((p << j) & ~m[k]));
+  if constexpr (K == 5) {
+    return x;
+  } else {
+    constexpr uint32_t J = 16u >> K;
+    constexpr uint32_t M = K == 0 ? 0x0000ffffu : K == 1 ? 0x00ff00ffu : K == 2 ? 0x0f0f0f0fu : K == 3 ? 0x33333333u
+                                                                                                 : 0x55555555u;
+    const bool hi = (lane32 & J) != 0;
+    const uint32_t p = xor_lane<J>(x);
+    const uint32_t sh = __builtin_amdgcn_alignbit(p, p, hi ? J : 32u - J);
+    const uint32_t mm = hi ? ~M : M;
+    return transpose32_t<K + 1>((x & mm) | (sh & ~mm), lane32);
   }
-  return x;
 }
+static __device__ __forceinline__ uint32_t transpose32(uint32_t x, uint32_t lane32) { return transpose32_t<0>(x, lane32); }
 
 /* OR 32 bits into an LDS bit array at bit offset `bit` (LDS atomics: tiles of neighbouring
  * columns share boundary words) */
@@ -772,9 +786,9 @@ static __device__ void encode_codeword(const cfg_dev_t *__restrict__ c, uint32_t
       const uint32_t rr = __umul24(tt, ki ? nm1 : nm0) >> 20, rem = tt - __umul24(rr, ki ? nt1 : nt0);
       const uint32_t r = ki ? n0 + rr : rr, R = ki ? R1 : R0, ND = ki ? ND1 : ND0, tz = ki ? tz1 : tz0;
       const uint32_t il = rem >= tz ? 1u : 0u, rb = il ? rem - tz : rem;
-      const uint32_t wpk = ki ? n0 * ws0 + rr * ws1 : rr * ws0;
+      const uint32_t wpk = ki ? n0 * ws0 + __umul24(rr, ws1) : __umul24(rr, ws0);
       const uint32_t row = il ? 16 * rb + (lane32 >> 1) : 32 * rb + lane32, s = il ? 1 + (lane32 & 1) : 0;
-      const uint32_t *st = strm + (r * 3 + s) * sw;
+      const uint32_t *st = strm + __umul24(r * 3 + s, sw);
       uint32_t y = 0;
       if (row < R) {
         y = sx32(st, (int)(32 * row) - (int)ND + (s == 2 ? 1 : 0));
@@ -784,7 +798,7 @@ static __device__ void encode_codeword(const cfg_dev_t *__restrict__ c, uint32_t
         }
       }
       y = transpose32(y, lane32);
-      or_bits(wb + wpk, il ? 32 * R + 2 * (wcol * R + 16 * rb) : wcol * R + 32 * rb, y);
+      or_bits(wb + wpk, il ? 32 * R + 2 * (__umul24(wcol, R) + 16 * rb) : __umul24(wcol, R) + 32 * rb, y);
     }
   }
   __syncthreads();
