@@ -151,10 +151,10 @@ static __device__ __forceinline__ void gold_generate(uint32_t *gold, uint32_t nw
   const uint32_t l = threadIdx.x, w0 = OAI4G_GOLD_STRIDE * l;
   if (l >= OAI4G_GOLD_LANES || w0 >= nwords) return;
   const uint32_t x2i = c_init ^ ((c_init ^ (c_init >> 1) ^ (c_init >> 2) ^ (c_init >> 3)) << 31);
-  gu32_t *col = (gu32_t *)(gx2j + 32 * l);
+  gu32_t *col = (gu32_t *)(gx2j + l);            /* column b of lane l at [b][lane] */
   uint32_t cv[32];
 #pragma unroll
-  for (int b = 0; b < 32; b++) cv[b] = col[b];
+  for (int b = 0; b < 32; b++) cv[b] = col[OAI4G_GOLD_LANES * b];
   uint32_t x2 = 0;
 #pragma unroll
   for (int b = 0; b < 32; b++) x2 ^= cv[b] & (0u - ((x2i >> b) & 1u));
@@ -513,43 +513,53 @@ static __device__ void encode_codeword(const cfg_dev_t *__restrict__ c, uint32_t
   uint8_t *tbb = (uint8_t *)tbw;
   const uint32_t G = cw.G[sfi], Gw = (G + 31) >> 5;
 
-  /* ---- phase 0: TB bytes, zeroed streams, tables, Gold words ---- */
+  /* ---- phase 0: Gold words on lanes 0..OAI4G_GOLD_LANES-1, meanwhile the other lanes load the
+   * TB bytes, zero the stream words past each block's data and copy the tables ---- */
   const uint8_t *src = payload + (size_t)(DEBUG ? 0 : (sf * c->n_cw + cwi)) * c->payload_stride;
   const uint32_t Ab = cw.A_bytes;
-  for (uint32_t i = tid; i < c->lds_tb_words; i += nth) {
-    uint32_t v = 0;
-    if (4 * i < Ab) {
-      v = *(const uint32_t *)(src + 4 * i);
-      uint32_t valid = Ab - 4 * i;
-      if (valid < 4) v &= (1u << (8 * valid)) - 1u;
-    }
-    tbw[i] = v;
-  }
-  for (uint32_t i = tid; i < c->lds_stream_words; i += nth) strm[i] = 0;
-  for (uint32_t i = tid; i < 2 * OAI4G_MAX_NULLS; i += nth) np[i] = cw.nullpos[i / OAI4G_MAX_NULLS][i % OAI4G_MAX_NULLS];
-  for (uint32_t i = tid; i < 8 * 96; i += nth) mul_tb[i] = (&cw.crcmul_tb[0][0][0])[i];
-  for (uint32_t i = tid; i < 6 * 96; i += nth) mul_cb[i] = (&cw.crcmul_cb[0][0][0])[i];
-  for (uint32_t v = tid; v < 256; v += nth) {
-    uint32_t ra = v << 16, rb = v << 16;
-    for (int i = 0; i < 8; i++) {
-      ra = (ra & 0x800000u) ? ((ra << 1) ^ 0x864cfbu) & 0xffffffu : (ra << 1) & 0xffffffu;
-      rb = (rb & 0x800000u) ? ((rb << 1) ^ 0x800063u) & 0xffffffu : (rb << 1) & 0xffffffu;
-    }
-    crctab_a[v] = ra;
-    crctab_b[v] = rb;
-  }
-  if (tid < 128) {
-    (&tabs->next[0][0])[tid] = (&c_rsc.next[0][0])[tid];
-    (&tabs->par[0][0])[tid] = (&c_rsc.par[0][0])[tid];
-    if (tid < 64) (&tabs->apow[0][0])[tid] = (&c_rsc.apow[0][0])[tid];
-    if (tid < 8) tabs->zs[tid] = c_rsc.zs[tid];
-  }
   if (DEBUG) {
     for (uint32_t i = tid; i < Gw + 1; i += nth) ebuf[i] = 0;
-  } else {
+  } else if (tid < OAI4G_GOLD_LANES) {
     const uint32_t c_init = (c->rnti << 14) + (cw.q << 13) + (sfi << 9) + c->Nid_cell; /* Ns>>1 = subframe */
     gold_generate(ebuf, Gw, c_init, c->gold_x1, c->gold_x2j);
     if (tid == 0) ebuf[Gw] = 0;
+  }
+  if (DEBUG || tid >= OAI4G_GOLD_LANES) {
+    const uint32_t ct = DEBUG ? tid : tid - OAI4G_GOLD_LANES, cn = DEBUG ? nth : nth - OAI4G_GOLD_LANES;
+    for (uint32_t i = ct; i < c->lds_tb_words; i += cn) {
+      uint32_t v = 0;
+      if (4 * i < Ab) {
+        v = *(const uint32_t *)(src + 4 * i);
+        uint32_t valid = Ab - 4 * i;
+        if (valid < 4) v &= (1u << (8 * valid)) - 1u;
+      }
+      tbw[i] = v;
+    }
+    /* stream words past the data of each block (tail bits, read-ahead); the data words are
+     * fully written by segmentation (systematic) and the phase-3 planes / turbo (parity) */
+    for (uint32_t i = ct; i < C * 3 * 4; i += cn) {
+      const uint32_t slot = i >> 2, r = slot / 3;
+      const uint32_t w = ((cw.K[r] + 31) >> 5) + (i & 3u);
+      if (w < sw) strm[slot * sw + w] = 0u;
+    }
+    for (uint32_t i = ct; i < 2 * OAI4G_MAX_NULLS; i += cn) np[i] = cw.nullpos[i / OAI4G_MAX_NULLS][i % OAI4G_MAX_NULLS];
+    for (uint32_t i = ct; i < 8 * 96; i += cn) mul_tb[i] = (&cw.crcmul_tb[0][0][0])[i];
+    for (uint32_t i = ct; i < 6 * 96; i += cn) mul_cb[i] = (&cw.crcmul_cb[0][0][0])[i];
+    for (uint32_t v = ct; v < 256; v += cn) {
+      uint32_t ra = v << 16, rb = v << 16;
+      for (int i = 0; i < 8; i++) {
+        ra = (ra & 0x800000u) ? ((ra << 1) ^ 0x864cfbu) & 0xffffffu : (ra << 1) & 0xffffffu;
+        rb = (rb & 0x800000u) ? ((rb << 1) ^ 0x800063u) & 0xffffffu : (rb << 1) & 0xffffffu;
+      }
+      crctab_a[v] = ra;
+      crctab_b[v] = rb;
+    }
+    for (uint32_t i = ct; i < 128; i += cn) {
+      (&tabs->next[0][0])[i] = (&c_rsc.next[0][0])[i];
+      (&tabs->par[0][0])[i] = (&c_rsc.par[0][0])[i];
+      if (i < 64) (&tabs->apow[0][0])[i] = (&c_rsc.apow[0][0])[i];
+      if (i < 8) tabs->zs[i] = c_rsc.zs[i];
+    }
   }
   __syncthreads();
   if (stop_phase <= 0) return;

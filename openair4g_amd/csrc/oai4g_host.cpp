@@ -155,7 +155,7 @@ static void do_init(void)
       steps_done++;
     }
     h_gx1[l] = x1;
-    for (int b = 0; b < 32; b++) h_gx2j[32 * l + b] = cols[b];
+    for (int b = 0; b < 32; b++) h_gx2j[OAI4G_GOLD_LANES * b + l] = cols[b];   /* [b][lane]: coalesced */
   }
   if (hipMalloc(&g_tw, tw.size() * 4) != hipSuccess || hipMalloc(&g_gx1, sizeof(h_gx1)) != hipSuccess ||
       hipMalloc(&g_gx2j, sizeof(h_gx2j)) != hipSuccess ||
