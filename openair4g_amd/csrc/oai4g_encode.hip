@@ -448,11 +448,13 @@ static __device__ __forceinline__ uint32_t compact_to_pos2(uint32_t ci, const ui
 
 /*
  * Rate-matcher output word (lte_rate_matching.c:548-566): `need` non-NULL entries of the
- * circular buffer w[0..Ncb) starting at position p (m NULLs before p).  Inside the buffer a
- * 64-bit window of packed w with the (few) NULL bits squeezed out; across the wrap, bit by bit.
+ * circular buffer w[0..Ncb) starting at position p (m NULLs before p, nxt = position of NULL m
+ * or ~0).  Inside the buffer a 64-bit window of packed w with the (few) NULL bits squeezed out;
+ * the next NULL lives in a register, so a NULL-free word costs no table read.  Across the wrap,
+ * bit by bit.
  */
-static __device__ __forceinline__ uint32_t rm_window(const uint32_t *wpk, uint32_t &p, uint32_t &m, uint32_t Ncb,
-                                                     const uint16_t *np, uint32_t nn, uint32_t need)
+static __device__ __forceinline__ uint32_t rm_window(const uint32_t *wpk, uint32_t &p, uint32_t &m, uint32_t &nxt,
+                                                     uint32_t Ncb, const uint16_t *np, uint32_t nn, uint32_t need)
 {
   uint32_t out = 0;
   if (p + 64 <= Ncb && need == 32) {
@@ -461,21 +463,26 @@ static __device__ __forceinline__ uint32_t rm_window(const uint32_t *wpk, uint32
     x >>= off;
     if (off) x |= (uint64_t)wpk[wi + 2] << (64 - off);
     uint32_t del = 0;
-    while (m < nn) {
-      uint32_t k = (uint32_t)np[m] - p - del;
-      if (k >= 32) break;
-      uint64_t lo = (1ull << k) - 1ull;
+    while (nxt < p + 32 + del) {
+      const uint32_t k = nxt - p - del;
+      const uint64_t lo = (1ull << k) - 1ull;
       x = (x & lo) | ((x >> 1) & ~lo);
       del++;
       m++;
+      nxt = m < nn ? (uint32_t)np[m] : 0xffffffffu;
     }
     out = (uint32_t)x;
     p += 32 + del;
   } else {
     uint32_t got = 0;
     while (got < need) {
-      if (p >= Ncb) { p = 0; m = 0; }
-      if (m < nn && np[m] == p) { p++; m++; continue; }
+      if (p >= Ncb) { p = 0; m = 0; nxt = nn ? (uint32_t)np[0] : 0xffffffffu; }
+      if (p == nxt) {
+        p++;
+        m++;
+        nxt = m < nn ? (uint32_t)np[m] : 0xffffffffu;
+        continue;
+      }
       out |= ((wpk[p >> 5] >> (p & 31)) & 1u) << got;
       got++;
       p++;
@@ -838,7 +845,7 @@ static __device__ void encode_codeword(const cfg_dev_t *__restrict__ c, uint32_t
       r = hi ? es + q : q;
       k = ii - q * W;
     }
-    uint32_t p = 0, m = 0, nwo = 0, nn = 0, Ncb = 0, E = 0, ro = 0, wpk = 0;
+    uint32_t p = 0, m = 0, nxt = 0, nwo = 0, nn = 0, Ncb = 0, E = 0, ro = 0, wpk = 0;
     const uint16_t *npl = np;
     bool fresh = true;
     for (uint32_t i = i0; i < i1; i++, k++) {
@@ -853,10 +860,11 @@ static __device__ void encode_codeword(const cfg_dev_t *__restrict__ c, uint32_t
         Ncb = ki ? Ncb1 : Ncb0;
         wpk = ki ? n0 * ws0 + (r - n0) * ws1 : r * ws0;
         p = compact_to_pos2(((ki ? k0c1 : k0c0) + 32 * k) % (ki ? Nnn1 : Nnn0), npl, nn, m);
+        nxt = m < nn ? (uint32_t)npl[m] : 0xffffffffu;
         fresh = false;
       }
       const uint32_t need = min(32u, E - 32 * k);
-      uint32_t out = rm_window(wb + wpk, p, m, Ncb, npl, nn, need);
+      uint32_t out = rm_window(wb + wpk, p, m, nxt, Ncb, npl, nn, need);
       uint32_t gpos = ro + 32 * k, gw = gpos >> 5, off = gpos & 31;
       atomicXor(&ebuf[gw], out << off);
       if (off && (out >> (32 - off))) atomicXor(&ebuf[gw + 1], out >> (32 - off));
