@@ -185,15 +185,23 @@ static __device__ __forceinline__ uint32_t crc_mul_tab(uint32_t a, const uint32_
          t[64 + ((a >> 16) & 15u)] ^ t[80 + ((a >> 20) & 15u)];
 }
 
-/* lane chunk CRC of virtual bytes [lane*per, (lane+1)*per) of a message padded to nl*per */
+/* lane chunk CRC of virtual bytes [lane*per, (lane+1)*per) of a message padded to nl*per
+ * (per % 4 == 0): four byte reads are issued ahead of their four dependent table steps; the
+ * virtual zero bytes in front leave the zero register unchanged */
 static __device__ __forceinline__ uint32_t crc_chunk(const uint8_t *buf, uint32_t nbytes, uint32_t per, uint32_t lane,
                                                      uint32_t nl, const uint32_t *tab)
 {
-  int vstart = (int)(lane * per) - (int)(per * nl - nbytes);
+  const int vstart = (int)(lane * per) - (int)(per * nl - nbytes);
   uint32_t reg = 0;
-  for (uint32_t i = 0; i < per; i++) {
-    int idx = vstart + (int)i;
-    if (idx >= 0) reg = crc_step(reg, buf[idx], tab);
+  for (uint32_t i = 0; i < per; i += 4) {
+    uint32_t b[4];
+#pragma unroll
+    for (int q = 0; q < 4; q++) {
+      const int idx = vstart + (int)i + q;
+      b[q] = idx >= 0 ? (uint32_t)buf[idx] : 0u;
+    }
+#pragma unroll
+    for (int q = 0; q < 4; q++) reg = crc_step(reg, b[q], tab);
   }
   return reg;
 }
@@ -224,8 +232,8 @@ static __device__ __forceinline__ uint32_t crc_mulmod(uint32_t a, uint32_t b, ui
 static __device__ uint32_t crc24_wave(const uint8_t *buf, uint32_t nbytes, uint32_t poly, const uint32_t *tab)
 {
   const uint32_t lane = threadIdx.x & 63;
-  uint32_t per = (nbytes + 63) >> 6;
-  if (per == 0) return 0;
+  uint32_t per = (((nbytes + 63) >> 6) + 3) & ~3u;   /* crc_chunk wants a multiple of 4 */
+  if (nbytes == 0) return 0;
   uint32_t reg = crc_chunk(buf, nbytes, per, lane, 64, tab);
   uint32_t m = 1;
   for (uint32_t i = 0; i < per; i++) m = crc_step(m, 0, tab);   /* x^(8 per) mod P */

@@ -663,7 +663,7 @@ static int derive_cfg(oai4g_tx_config *cfg, const oai4g_tx_params_t *p, const ui
       }
       c.u0 = c.n0 * c.kw[0];
     }
-    c.crc_per_tb = (c.A_bytes + 255) / 256;
+    c.crc_per_tb = (((c.A_bytes + 255) / 256) + 3) & ~3u;   /* bytes per lane, a multiple of 4 */
     crc_mul_tables(c.crc_per_tb, 8, 0x864cfbu, c.crcmul_tb);
     uint32_t ncb_max = 0;
     for (uint32_t r = 0; r < C; r++) {
@@ -671,7 +671,7 @@ static int derive_cfg(oai4g_tx_config *cfg, const oai4g_tx_params_t *p, const ui
       if (c.src[r] + n > c.A_bytes) n = c.A_bytes > c.src[r] ? c.A_bytes - c.src[r] : 0;
       ncb_max = n > ncb_max ? n : ncb_max;
     }
-    c.crc_per_cb = (ncb_max + 63) / 64;
+    c.crc_per_cb = (((ncb_max + 63) / 64) + 3) & ~3u;
     crc_mul_tables(c.crc_per_cb ? c.crc_per_cb : 1, 6, 0x800063u, c.crcmul_cb);
     for (int ki = 0; ki < 2; ki++) {
       uint32_t K = ki == 0 ? (Km ? Km : Kp) : Kp;
