@@ -519,8 +519,8 @@ static __device__ void encode_codeword(const cfg_dev_t *__restrict__ c, uint32_t
   uint32_t *mul_tb = crctab_b + 256;                     /* [8][6][16] */
   uint32_t *mul_cb = mul_tb + 8 * 96;                    /* [6][6][16] */
   uint32_t *strm = lds_base + c->lds_a_words;
-  uint32_t *ebuf = strm + c->lds_b_words;
-  uint32_t *tails = ebuf + c->lds_gold_words;
+  uint32_t *ebuf = strm;                                 /* region B again from phase 4c: RM output words */
+  uint32_t *tails = strm + c->lds_b_words;
   uint32_t *crcs = tails + 2 * OAI4G_MAX_CB;             /* [0] = CRC24A, [1+r] = CRC24B of block r */
   uint32_t *red = crcs + OAI4G_MAX_CB + 2;               /* 4 per-wave partials */
   enc_tabs_t *tabs = (enc_tabs_t *)(red + 4);
@@ -528,19 +528,11 @@ static __device__ void encode_codeword(const cfg_dev_t *__restrict__ c, uint32_t
   uint8_t *tbb = (uint8_t *)tbw;
   const uint32_t G = cw.G[sfi], Gw = (G + 31) >> 5;
 
-  /* ---- phase 0: Gold words on lanes 0..OAI4G_GOLD_LANES-1, meanwhile the other lanes load the
-   * TB bytes, zero the stream words past each block's data and copy the tables ---- */
+  /* ---- phase 0: TB bytes, stream words past each block's data, tables ---- */
   const uint8_t *src = payload + (size_t)(DEBUG ? 0 : (sf * c->n_cw + cwi)) * c->payload_stride;
   const uint32_t Ab = cw.A_bytes;
-  if (DEBUG) {
-    for (uint32_t i = tid; i < Gw + 1; i += nth) ebuf[i] = 0;
-  } else if (tid < OAI4G_GOLD_LANES) {
-    const uint32_t c_init = (c->rnti << 14) + (cw.q << 13) + (sfi << 9) + c->Nid_cell; /* Ns>>1 = subframe */
-    gold_generate(ebuf, Gw, c_init, c->gold_x1, c->gold_x2j);
-    if (tid == 0) ebuf[Gw] = 0;
-  }
-  if (DEBUG || tid >= OAI4G_GOLD_LANES) {
-    const uint32_t ct = DEBUG ? tid : tid - OAI4G_GOLD_LANES, cn = DEBUG ? nth : nth - OAI4G_GOLD_LANES;
+  {
+    const uint32_t ct = tid, cn = nth;
     for (uint32_t i = ct; i < c->lds_tb_words; i += cn) {
       uint32_t v = 0;
       if (4 * i < Ab) {
@@ -828,6 +820,9 @@ static __device__ void encode_codeword(const cfg_dev_t *__restrict__ c, uint32_t
   }
   __syncthreads();
   if (stop_phase <= 4) return;
+  /* the streams are dead: region B becomes the zeroed RM output words */
+  for (uint32_t i = tid; i < Gw + 1; i += nth) ebuf[i] = 0u;
+  __syncthreads();
 
   /* ---- phase 4c: rate matching (lte_rate_matching.c:548-566) of every block, XORed into the
    * Gold-prefilled staging words; each thread walks a run of consecutive output words ---- */
@@ -889,9 +884,17 @@ static __device__ void encode_codeword(const cfg_dev_t *__restrict__ c, uint32_t
     for (uint32_t k = tid; k < G; k += nth) dbg.e[k] = (uint8_t)((ebuf[k >> 5] >> (k & 31)) & 1u);
     return;
   }
+  /* scrambling (dlsch_scrambling.c:51-97): Gold words into region A (packed w is dead), XORed
+   * into the RM output on the way out */
+  uint32_t *gold = lds_base;
+  if (tid < OAI4G_GOLD_LANES) {
+    const uint32_t c_init = (c->rnti << 14) + (cw.q << 13) + (sfi << 9) + c->Nid_cell; /* Ns>>1 = subframe */
+    gold_generate(gold, Gw, c_init, c->gold_x1, c->gold_x2j);
+  }
+  __syncthreads();
   uint32_t *eout = ebits + (size_t)(sf * c->n_cw + cwi) * c->ebits_words;
   for (uint32_t i = tid; i < Gw; i += nth) {
-    uint32_t v = ebuf[i];
+    uint32_t v = ebuf[i] ^ gold[i];
     uint32_t nb = min(32u, G - 32 * i);
     if (nb < 32) v &= (1u << nb) - 1u;
     eout[i] = v;
@@ -916,7 +919,7 @@ __global__ void __launch_bounds__(256) k_encode_debug(const cfg_dev_t *__restric
 
 static size_t enc_lds_bytes(const cfg_dev_t *h)
 {
-  size_t words = (size_t)h->lds_a_words + h->lds_b_words + h->lds_gold_words + 2 * OAI4G_MAX_CB + OAI4G_MAX_CB + 2 + 4;
+  size_t words = (size_t)h->lds_a_words + h->lds_b_words + 2 * OAI4G_MAX_CB + OAI4G_MAX_CB + 2 + 4;
   size_t bytes = words * 4 + sizeof(enc_tabs_t) + 2 * OAI4G_MAX_NULLS * 2;
   return (bytes + 15) & ~(size_t)15;
 }

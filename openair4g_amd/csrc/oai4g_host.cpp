@@ -766,6 +766,10 @@ static int derive_cfg(oai4g_tx_config *cfg, const oai4g_tx_params_t *p, const ui
     if (2 * h.cw[cw].ilv_off[h.cw[cw].C] > h.lds_a_words) h.lds_a_words = 2 * h.cw[cw].ilv_off[h.cw[cw].C];
   if (max_w > h.lds_a_words) h.lds_a_words = max_w;
   h.lds_b_words = max_stream_words;
+  /* region B holds the RM output words once the streams are dead; region A the Gold words once
+   * packed w is dead */
+  if (h.lds_gold_words > h.lds_b_words) h.lds_b_words = h.lds_gold_words;
+  if (h.lds_gold_words > h.lds_a_words) h.lds_a_words = h.lds_gold_words;
   /* RE maps */
   if (need_remap) {
     uint32_t N = h.N;

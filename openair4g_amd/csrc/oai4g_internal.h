@@ -20,8 +20,8 @@
 #define OAI4G_PIPE_MAX_CHUNKS 16
 #define OAI4G_CRS_CODE 0xE000u               /* remap codes >= this (and != 0xFFFF) are CRS REs */
 #define OAI4G_ENC_CRC_TABLE_WORDS (256 + 256 + 8 * 96 + 6 * 96) /* byte tables A/B + tree multipliers */
-#define OAI4G_GOLD_LANES 128
-#define OAI4G_GOLD_STRIDE 33   /* odd: lanes 33l + k hit distinct LDS banks */
+#define OAI4G_GOLD_LANES 256
+#define OAI4G_GOLD_STRIDE 17   /* odd: lanes 17l + k hit distinct LDS banks */
 #define OAI4G_MAX_GOLD_WORDS (OAI4G_GOLD_LANES * OAI4G_GOLD_STRIDE) /* >= (14*1200*6)/32 */
 #define OAI4G_TW_TOTAL (16 + 64 + 128 + 256 + 512 + 1024 + 2048)
 
