@@ -467,7 +467,7 @@ def make_params(name="C3", subframe=7, subframe_step=0, rnti=0x1234, Nid_cell=0,
     p = TxParams()
     p.N_RB_DL = c["N_RB_DL"]
     p.Nid_cell = Nid_cell
-    p.Ncp = 0
+    p.Ncp = c.get("Ncp", 0)
     p.nb_antennas_tx = c["nb_antennas_tx"]
     p.mode1_flag = c["mode1_flag"]
     p.frame_type = 0

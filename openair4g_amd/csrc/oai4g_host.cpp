@@ -782,10 +782,9 @@ static int derive_cfg(oai4g_tx_config *cfg, const oai4g_tx_params_t *p, const ui
       cfg->re_count[sf] = n;
       if (p->with_crs) {
         /* pilots.c:43-168: port 0 on antenna 0; antenna 1 port 0 (mode1) or port 1 */
-        if (fp.Ncp != 0) { set_err("CRS in the batched path supports normal CP only"); return -1; }
         uint32_t gt[20][2][14];
         lte_gold_table_h(&fp, gt);
-        const uint32_t psym[4] = {0, 4, 7, 11};
+        const uint32_t sps = fp.Ncp == 0 ? 7 : 6, psym[4] = {0, sps - 3, sps, 2 * sps - 3};   /* l' = 0, 4 (3) per slot */
         const int nports = (fp.nb_antennas_tx > 1 && !fp.mode1_flag) ? 2 : 1;
         cfg->h_crs.resize((size_t)10 * 4 * 200);
         for (uint32_t i = 0; i < 4; i++) {
@@ -866,7 +865,6 @@ static void release_cfg(oai4g_tx_config *cfg)
 extern "C" oai4g_tx_config_t *oai4g_tx_config_create(const oai4g_tx_params_t *p)
 {
   NEED_INIT(nullptr);
-  if (p->Ncp != 0) { set_err("batched path supports normal CP only"); return nullptr; }
   if (p->N_RB_DL != 6 && p->N_RB_DL != 15 && p->N_RB_DL != 50 && p->N_RB_DL != 100) {
     set_err("batched path supports N_RB_DL 6, 15, 50, 100 (IDFT 128/256/1024/2048)");
     return nullptr;

@@ -403,12 +403,17 @@ hipError_t oai4g_launch_ofdm(const int32_t *d_in, int32_t *d_out, int log2n, int
 /* ======================================================================================
  * Modulation helpers shared by the fused kernel and the drop-in grid kernel.
  * ==================================================================================== */
-static __device__ __forceinline__ int pilots_of(uint32_t l)
+/* PDSCH pilot class of symbol l (dlsch_modulation.c:1268-1282), normal or extended CP */
+static __device__ __forceinline__ int pilots_of(uint32_t l, bool ecp)
 {
-  return (l == 4 || l == 11) ? 2 : (l == 7 ? 1 : 0);  /* normal CP (dlsch_modulation.c:1268-1282) */
+  if (ecp) return (l == 3 || l == 9) ? 2 : (l == 6 ? 1 : 0);
+  return (l == 4 || l == 11) ? 2 : (l == 7 ? 1 : 0);
 }
-/* CRS-bearing symbols of a normal-CP subframe (pilots.c:43-168) */
-static __device__ __forceinline__ bool pilots_any(uint32_t l) { return l == 0 || l == 4 || l == 7 || l == 11; }
+/* CRS-bearing symbols of a subframe (pilots.c:43-168) */
+static __device__ __forceinline__ bool pilots_any(uint32_t l, bool ecp)
+{
+  return ecp ? (l == 0 || l == 3 || l == 6 || l == 9) : (l == 0 || l == 4 || l == 7 || l == 11);
+}
 
 /* QAM symbol from Qm bits b0..b(Qm-1) packed LSB-first in `bits` (dlsch_modulation.c:245-355). */
 static __device__ __forceinline__ s16x2 qam_map(uint32_t bits, uint32_t Qm, const int16_t *tab, int16_t gain)
@@ -508,7 +513,8 @@ __global__ void __launch_bounds__(128) MODOFDM_ATTR k_modofdm(const cfg_dev_t *_
   const int unit = threadIdx.x / T, t = threadIdx.x % T;
   idft_tw_t<LOG2N> twr;
   twr.load(c->tw, t);
-  const uint32_t n_ant = c->n_ant, nsymb = c->nsymb;
+  const uint32_t n_ant = c->n_ant, nsymb = c->nsymb, sps = nsymb >> 1;
+  const bool ecp = nsymb == 12;                    /* extended CP: 6 symbols per slot, one prefix length */
   for (uint32_t i = threadIdx.x; i < 256; i += blockDim.x) {
     const uint32_t cw = i >> 7, pil = (i >> 6) & 1, bits = i & 63;
     if constexpr (MODE == 1) {          /* one codeword: [0] = TA, [1] = TB */
@@ -530,14 +536,14 @@ __global__ void __launch_bounds__(128) MODOFDM_ATTR k_modofdm(const cfg_dev_t *_
     const uint32_t sf = it / nsymb, l = it - sf * nsymb;
     const uint32_t sfi = (c->first_sf + (sf0 + sf) * c->sf_step) % 10;
     const uint32_t nre = active ? c->symnre[sfi][l] : 0u, re0 = c->symbase[sfi][l];
-    const uint32_t pil = pilots_of(l) != 0;
-    /* output placement: slot = l / 7, symbol-in-slot i (normal CP) */
-    const uint32_t slot = l / 7, si = l % 7;
+    const uint32_t pil = pilots_of(l, ecp) != 0;
+    /* output placement: slot, symbol-in-slot i */
+    const uint32_t slot = l >= sps ? 1u : 0u, si = l - slot * sps;
     const uint32_t body = slot * (c->spt >> 1) + (si == 0 ? c->cp0 : (N + c->cp0) + (si - 1) * (N + c->cp) + c->cp);
     const int cp = (int)(si == 0 ? c->cp0 : c->cp);
     uint32_t *dst0 = (uint32_t *)iq + (size_t)sf * n_ant * c->spt + body;
 
-    if (UNITS == 1 && nre == 0 && !(CRS && pilots_any(l))) {
+    if (UNITS == 1 && nre == 0 && !(CRS && pilots_any(l, ecp))) {
       /* control-region symbol: the transform of an all-zero grid is zero */
       if (active)
         for (uint32_t a = 0; a < n_ant; a++) {
@@ -566,7 +572,7 @@ __global__ void __launch_bounds__(128) MODOFDM_ATTR k_modofdm(const cfg_dev_t *_
     __syncthreads();
 
     gu32_t *crs_tab = (gu32_t *)c->crs_tab;
-    const bool crs = CRS && pilots_any(l);
+    const bool crs = CRS && pilots_any(l, ecp);
     const uint32_t *e0 = lds_e[unit][0], *e1 = lds_e[unit][1];
     const uint32_t *q0 = qtab[0][pil], *q1 = qtab[1][pil];
     /* bit position of data RE idx within the staged words: idx * Qm + (re0 * Qm - 32 wlo) */
@@ -646,14 +652,15 @@ __global__ void __launch_bounds__(128) MODOFDM_ATTR k_modofdm(const cfg_dev_t *_
         },
         [&](int a, int tt, int off, s16x2 y) {
           /* per-thread bases for each half of the symbol keep every store's offset within the
-           * 13-bit immediate; the CP test is compiled out where no t can reach N - CP_max */
+           * 13-bit immediate; the CP test is compiled out where no t can reach N - CP_max of the
+           * normal prefix (the extended prefix, N/4, takes a uniform branch) */
           constexpr int CPMAX = (N * 160) / 2048;
           const bool hi = off >= N / 2;
           const int ro = hi ? off - N / 2 : off;
           auto store = [&](uint32_t *base) {
             uint32_t *d = base + tt + (hi ? N / 2 : 0);
             d[ro] = c2u(y);
-            if (off + T - 1 >= N - CPMAX && tt + off >= N - cp) d[ro - N] = c2u(y);
+            if ((off + T - 1 >= N - CPMAX || ecp) && tt + off >= N - cp) d[ro - N] = c2u(y);
           };
           if constexpr (NA == 2) {
             store(dst0 + a * c->spt);
@@ -743,7 +750,7 @@ __global__ void __launch_bounds__(256) k_modulate_bytes(const cfg_dev_t *__restr
   if (code >= OAI4G_CRS_CODE) return;                 /* no data RE (CRS codes included) */
   const cw_dev_t &cw0 = c->cw[0];
   const cw_dev_t &cw1 = c->cw[1];
-  bool pil = pilots_of(l) != 0;
+  bool pil = pilots_of(l, nsymb == 12) != 0;
   if (c->mimo_mode == OAI4G_ALAMOUTI) {
     /* the thread of RE n writes n and its partner: the partner adds the accumulated values
      * of n (dlsch_modulation.c:535-545) */

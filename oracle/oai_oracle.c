@@ -817,9 +817,17 @@ int orc_tx_subframe(const orc_tx_cfg_t *cfg, uint8_t *payload[2], int32_t **txda
   int ret = modulation_impl(txdataF, cfg->amp, cfg->subframe, 0, fp, cfg->num_pdcch_symbols, &c0,
                             cfg->n_cw > 1 ? &c1 : NULL, cfg->sqrt_rho_a, cfg->sqrt_rho_b);
   g_last_re_allocated = ret;
+  /* do_OFDM_mod (ofdm_mod.c:233-286): normal_prefix_mod per slot, or PHY_ofdm_mod of 6 symbols
+   * with the extended prefix */
+  const int sps = nsymb >> 1;
   for (int aa = 0; aa < fp->nb_antennas_tx; aa++)
-    for (int slot = 0; slot < 2; slot++)
-      orc_normal_prefix_mod(txdataF[aa] + slot * N * 7, txdata[aa] + slot * (fp->samples_per_tti >> 1), 7, fp);
+    for (int slot = 0; slot < 2; slot++) {
+      if (fp->Ncp == 1)
+        orc_ofdm_mod(txdataF[aa] + slot * N * sps, txdata[aa] + slot * (fp->samples_per_tti >> 1),
+                     (uint8_t)fp->log2_symbol_size, (uint8_t)sps, (uint16_t)fp->nb_prefix_samples);
+      else
+        orc_normal_prefix_mod(txdataF[aa] + slot * N * 7, txdata[aa] + slot * (fp->samples_per_tti >> 1), 7, fp);
+    }
   free(e_buf[0]);
   free(e_buf[1]);
   return ret < 0 ? -1 : 0;

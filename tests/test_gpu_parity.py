@@ -196,6 +196,28 @@ def test_pipeline_bit_exact(gpu, name, n_sf, first, step):
     _pipeline_check(gpu, name, n_sf, first, step)
 
 
+@pytest.mark.parametrize("name", ["C1", "C2", "C3", "TM2"])
+def test_pipeline_extended_cp(gpu, name):
+    """Extended cyclic prefix (12 symbols, one 512-sample-equivalent prefix): RE map with the
+    extended pilot symbols, 6-symbol slots through PHY_ofdm_mod (ofdm_mod.c:252-259)."""
+    _pipeline_check(gpu, name, 10, 0, 1, seed=3, Ncp=1)
+
+
+@pytest.mark.parametrize("name", ["C3", "TM2"])
+def test_pipeline_extended_cp_with_crs(gpu, name):
+    p = gpu.make_params(name, subframe=0, subframe_step=1, Nid_cell=13, with_crs=1, Ncp=1)
+    pipe = gpu.TxPipeline(p, 10)
+    pay = np.random.default_rng(5).integers(0, 256, size=(10, p.n_cw, p.payload_stride), dtype=np.uint8)
+    pipe.upload_payload(pay)
+    pipe.run()
+    pipe.sync()
+    iq = pipe.iq()
+    for i in range(10):
+        txd_o, _, _ = O.tx_subframe(O.tx_cfg_from_params(p, i), [pay[i, cw] for cw in range(p.n_cw)])
+        assert np.array_equal(iq[i], txd_o), (name, i)
+    pipe.close()
+
+
 @pytest.mark.parametrize("nid", [0, 1, 2, 5])
 def test_pipeline_tm2_odd_bandwidth(gpu, nid):
     """ALAMOUTI on 15 PRB (odd N_RB: the middle RB straddles DC; PBCH/sync half-RB exclusions in

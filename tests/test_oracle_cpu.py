@@ -200,3 +200,23 @@ def test_alamouti_matches_spec_model(name, mcs, tbs, nid, sf):
                                 p.num_pdcch_symbols, Qm)
     assert used == G
     assert np.array_equal(txF, ref)
+
+
+# ---------------------------------------------------------------- extended cyclic prefix (A13)
+@pytest.mark.parametrize("name", ["C1", "C2"])
+def test_oracle_extended_cp_layout(name):
+    """do_OFDM_mod with the extended prefix (ofdm_mod.c:252-259): per slot 6 symbols of N + N/4
+    samples, each prefix a copy of its symbol's last N/4 samples, bodies = IDFT of the grid."""
+    import openair4g_amd as oai
+    p = oai.make_params(name, subframe=3, Ncp=1)
+    cfg = O.tx_cfg_from_params(p, 3)
+    pay = np.random.default_rng(1).integers(0, 256, p.TBS[0] // 8 + 8, dtype=np.uint8)
+    txd, txF, _ = O.tx_subframe(cfg, [pay])
+    N, cp = cfg.fp.ofdm_symbol_size, cfg.fp.nb_prefix_samples
+    assert cp == N // 4 and cfg.fp.symbols_per_tti == 12
+    for l in range(12):
+        start = (l // 6) * (txd.shape[1] // 2) + (l % 6) * (N + cp)
+        sym = txd[0, start:start + N + cp]
+        assert np.array_equal(sym[:cp], sym[N:])
+        body = O.idft(txF[0, l * N:(l + 1) * N].view(np.int16), 1)
+        assert np.array_equal(sym[cp:].view(np.int16), body)
