@@ -498,7 +498,7 @@ struct modofdm_geom {
 #define MODOFDM_ATTR
 #endif
 /* MODE: 0 = TM1 (one transform stored to every antenna), 1 = ALAMOUTI, 2 = LARGE_CDD */
-template <int LOG2N, int MODE, bool CRS>
+template <int LOG2N, int MODE, bool CRS, bool ECP>
 __global__ void __launch_bounds__(128) MODOFDM_ATTR k_modofdm(const cfg_dev_t *__restrict__ c, int n_items,
                                                  const uint32_t *__restrict__ ebits, int32_t *__restrict__ iq,
                                                  uint32_t sf0)
@@ -513,8 +513,9 @@ __global__ void __launch_bounds__(128) MODOFDM_ATTR k_modofdm(const cfg_dev_t *_
   const int unit = threadIdx.x / T, t = threadIdx.x % T;
   idft_tw_t<LOG2N> twr;
   twr.load(c->tw, t);
-  const uint32_t n_ant = c->n_ant, nsymb = c->nsymb, sps = nsymb >> 1;
-  const bool ecp = nsymb == 12;                    /* extended CP: 6 symbols per slot, one prefix length */
+  const uint32_t n_ant = c->n_ant, nsymb = c->nsymb;
+  constexpr bool ecp = ECP;                        /* extended CP: 6 symbols per slot, one prefix length */
+  constexpr uint32_t sps = ECP ? 6 : 7;
   for (uint32_t i = threadIdx.x; i < 256; i += blockDim.x) {
     const uint32_t cw = i >> 7, pil = (i >> 6) & 1, bits = i & 63;
     if constexpr (MODE == 1) {          /* one codeword: [0] = TA, [1] = TB */
@@ -652,15 +653,14 @@ __global__ void __launch_bounds__(128) MODOFDM_ATTR k_modofdm(const cfg_dev_t *_
         },
         [&](int a, int tt, int off, s16x2 y) {
           /* per-thread bases for each half of the symbol keep every store's offset within the
-           * 13-bit immediate; the CP test is compiled out where no t can reach N - CP_max of the
-           * normal prefix (the extended prefix, N/4, takes a uniform branch) */
-          constexpr int CPMAX = (N * 160) / 2048;
+           * 13-bit immediate; the CP test is compiled out where no t can reach N - CP_max */
+          constexpr int CPMAX = ECP ? N / 4 : (N * 160) / 2048;
           const bool hi = off >= N / 2;
           const int ro = hi ? off - N / 2 : off;
           auto store = [&](uint32_t *base) {
             uint32_t *d = base + tt + (hi ? N / 2 : 0);
             d[ro] = c2u(y);
-            if ((off + T - 1 >= N - CPMAX || ecp) && tt + off >= N - cp) d[ro - N] = c2u(y);
+            if (off + T - 1 >= N - CPMAX && tt + off >= N - cp) d[ro - N] = c2u(y);
           };
           if constexpr (NA == 2) {
             store(dst0 + a * c->spt);
@@ -673,13 +673,13 @@ __global__ void __launch_bounds__(128) MODOFDM_ATTR k_modofdm(const cfg_dev_t *_
   }
 }
 
-template <int LOG2N, int MODE, bool CRS>
+template <int LOG2N, int MODE, bool CRS, bool ECP>
 static hipError_t launch_modofdm_t(const cfg_dev_t *d_cfg, const cfg_dev_t *h_cfg, int sf0, int n_items,
                                    const uint32_t *d_ebits, int32_t *d_iq, hipStream_t s)
 {
   static int occ = 0;
   if (!occ) {
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, k_modofdm<LOG2N, MODE, CRS>, 128, 0) != hipSuccess ||
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, k_modofdm<LOG2N, MODE, CRS, ECP>, 128, 0) != hipSuccess ||
         occ < 1)
       occ = 1;
   }
@@ -687,29 +687,38 @@ static hipError_t launch_modofdm_t(const cfg_dev_t *d_cfg, const cfg_dev_t *h_cf
   int want = (n_items + units - 1) / units, cap = occ * (int)h_cfg->n_cu;
   int grid = want < cap ? want : cap;
   if (grid < 1) grid = 1;
-  hipLaunchKernelGGL((k_modofdm<LOG2N, MODE, CRS>), dim3(grid), dim3(128), 0, s, d_cfg, n_items, d_ebits, d_iq,
+  hipLaunchKernelGGL((k_modofdm<LOG2N, MODE, CRS, ECP>), dim3(grid), dim3(128), 0, s, d_cfg, n_items, d_ebits, d_iq,
                      (uint32_t)sf0);
   return hipGetLastError();
 }
 
-/* precoding mode and CRS are uniform per configuration and become template arguments: no
- * per-RE uniform branches in the prologue */
+template <int LOG2N, int MODE, bool ECP>
+static hipError_t launch_modofdm_c(const cfg_dev_t *d_cfg, const cfg_dev_t *h_cfg, int sf0, int n_items,
+                                   const uint32_t *d_ebits, int32_t *d_iq, hipStream_t s)
+{
+  return h_cfg->with_crs ? launch_modofdm_t<LOG2N, MODE, true, ECP>(d_cfg, h_cfg, sf0, n_items, d_ebits, d_iq, s)
+                         : launch_modofdm_t<LOG2N, MODE, false, ECP>(d_cfg, h_cfg, sf0, n_items, d_ebits, d_iq, s);
+}
+
+template <int LOG2N, bool ECP>
+static hipError_t launch_modofdm_m(const cfg_dev_t *d_cfg, const cfg_dev_t *h_cfg, int sf0, int n_items,
+                                   const uint32_t *d_ebits, int32_t *d_iq, hipStream_t s)
+{
+  switch (h_cfg->mimo_mode) {
+  case OAI4G_LARGE_CDD: return launch_modofdm_c<LOG2N, 2, ECP>(d_cfg, h_cfg, sf0, n_items, d_ebits, d_iq, s);
+  case OAI4G_ALAMOUTI: return launch_modofdm_c<LOG2N, 1, ECP>(d_cfg, h_cfg, sf0, n_items, d_ebits, d_iq, s);
+  default: return launch_modofdm_c<LOG2N, 0, ECP>(d_cfg, h_cfg, sf0, n_items, d_ebits, d_iq, s);
+  }
+}
+
+/* precoding mode, CRS and the prefix type are uniform per configuration and become template
+ * arguments: no per-RE uniform branches in the prologue or the stores */
 template <int LOG2N>
 static hipError_t launch_modofdm_n(const cfg_dev_t *d_cfg, const cfg_dev_t *h_cfg, int sf0, int n_items,
                                    const uint32_t *d_ebits, int32_t *d_iq, hipStream_t s)
 {
-  const bool crs = h_cfg->with_crs != 0;
-  switch (h_cfg->mimo_mode) {
-  case OAI4G_LARGE_CDD:
-    return crs ? launch_modofdm_t<LOG2N, 2, true>(d_cfg, h_cfg, sf0, n_items, d_ebits, d_iq, s)
-               : launch_modofdm_t<LOG2N, 2, false>(d_cfg, h_cfg, sf0, n_items, d_ebits, d_iq, s);
-  case OAI4G_ALAMOUTI:
-    return crs ? launch_modofdm_t<LOG2N, 1, true>(d_cfg, h_cfg, sf0, n_items, d_ebits, d_iq, s)
-               : launch_modofdm_t<LOG2N, 1, false>(d_cfg, h_cfg, sf0, n_items, d_ebits, d_iq, s);
-  default:
-    return crs ? launch_modofdm_t<LOG2N, 0, true>(d_cfg, h_cfg, sf0, n_items, d_ebits, d_iq, s)
-               : launch_modofdm_t<LOG2N, 0, false>(d_cfg, h_cfg, sf0, n_items, d_ebits, d_iq, s);
-  }
+  return h_cfg->nsymb == 12 ? launch_modofdm_m<LOG2N, true>(d_cfg, h_cfg, sf0, n_items, d_ebits, d_iq, s)
+                            : launch_modofdm_m<LOG2N, false>(d_cfg, h_cfg, sf0, n_items, d_ebits, d_iq, s);
 }
 
 /* subframes [sf0, sf0 + n_sf) of a batch whose e-bit words / IQ start at d_ebits / d_iq */
