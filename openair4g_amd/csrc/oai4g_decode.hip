@@ -25,20 +25,20 @@ typedef const __attribute__((address_space(1))) int16_t gs16_t;
 
 static __device__ __forceinline__ short sadd(short a, short b) { return __builtin_elementwise_add_sat(a, b); }
 static __device__ __forceinline__ short ssub(short a, short b) { return __builtin_elementwise_sub_sat(a, b); }
-static __device__ __forceinline__ short smax(short a, short b) { return a > b ? a : b; }
 
 #define TD_MAXH 128    /* MAX / 2 */
+#define TD_SEG 4      /* alpha checkpoint interval (steps) */
 
 struct td_blk_t {      /* one block's scratch (int16 element offsets, see td_layout) */
   short *s0, *s1, *s2, *yp1, *yp2, *ext, *ext2;
-  uint4 *A;            /* alpha: [(K1 + 1)][8 lanes] x 8 states (16 B) */
+  uint4 *A;            /* alpha checkpoints: [ceil(K1/16) + 2][8 lanes] x 8 states (16 B) */
 };
 
 static __device__ __forceinline__ td_blk_t td_layout(uint8_t *base, uint32_t K)
 {
   td_blk_t b;
   short *p = (short *)base;
-  const uint32_t n16 = (K + 16 + 7) & ~7u, n128 = K + 128;
+  const uint32_t n16 = (K + 8 * TD_SEG + 16 + 7) & ~7u, n128 = K + 128;   /* segment read-ahead slack */
   b.s0 = p; p += n16;
   b.s1 = p; p += n16;
   b.s2 = p; p += n16;
@@ -52,57 +52,87 @@ static __device__ __forceinline__ td_blk_t td_layout(uint8_t *base, uint32_t K)
 
 size_t oai4g_td_block_bytes(uint32_t K)
 {
-  const size_t n16 = (K + 16 + 7) & ~7u, n128 = K + 128;
+  const size_t n16 = (K + 8 * TD_SEG + 16 + 7) & ~7u, n128 = K + 128;
   return (((5 * n16 + 2 * n128) * 2 + 15) & ~(size_t)15) + (size_t)(K / 8 + 1) * 8 * 16 + 256;
 }
 
-static __device__ __forceinline__ uint4 pack8(const short *v)
+/* Trellis metrics as four packed int16 pairs: S[0] = (s0, s1), S[1] = (s2, s3), S[2] = (s4, s5),
+ * S[3] = (s6, s7).  Saturating packed add/sub (v_pk_add/sub_i16 clamp) and packed max are the
+ * reference's adds/subs/max_epi16 lane for lane; x - (-g) == x + g under saturation because
+ * |g| <= 16384. */
+typedef short s2v __attribute__((ext_vector_type(2)));
+static __device__ __forceinline__ s2v adds2(s2v a, s2v b) { return __builtin_elementwise_add_sat(a, b); }
+static __device__ __forceinline__ s2v subs2(s2v a, s2v b) { return __builtin_elementwise_sub_sat(a, b); }
+static __device__ __forceinline__ s2v max2(s2v a, s2v b) { return __builtin_elementwise_max(a, b); }
+#define SHUF2(a, b, i, j) __builtin_shufflevector((a), (b), (i), (j))
+
+struct tm_t { s2v v[4]; };
+
+static __device__ __forceinline__ uint4 tm_pack(const tm_t &t)
 {
-  return make_uint4((uint16_t)v[0] | ((uint32_t)(uint16_t)v[1] << 16), (uint16_t)v[2] | ((uint32_t)(uint16_t)v[3] << 16),
-                    (uint16_t)v[4] | ((uint32_t)(uint16_t)v[5] << 16), (uint16_t)v[6] | ((uint32_t)(uint16_t)v[7] << 16));
+  return make_uint4(__builtin_bit_cast(uint32_t, t.v[0]), __builtin_bit_cast(uint32_t, t.v[1]),
+                    __builtin_bit_cast(uint32_t, t.v[2]), __builtin_bit_cast(uint32_t, t.v[3]));
 }
-static __device__ __forceinline__ void unpack8(uint4 u, short *v)
+static __device__ __forceinline__ tm_t tm_unpack(uint4 u)
 {
-  v[0] = (short)u.x; v[1] = (short)(u.x >> 16); v[2] = (short)u.y; v[3] = (short)(u.y >> 16);
-  v[4] = (short)u.z; v[5] = (short)(u.z >> 16); v[6] = (short)u.w; v[7] = (short)(u.w >> 16);
+  tm_t t;
+  t.v[0] = __builtin_bit_cast(s2v, u.x); t.v[1] = __builtin_bit_cast(s2v, u.y);
+  t.v[2] = __builtin_bit_cast(s2v, u.z); t.v[3] = __builtin_bit_cast(s2v, u.w);
+  return t;
+}
+static __device__ __forceinline__ tm_t tm_init(bool zero_first)
+{
+  tm_t t;
+  t.v[0] = (s2v){(short)(zero_first ? 0 : -TD_MAXH), (short)-TD_MAXH};
+  t.v[1] = t.v[2] = t.v[3] = (s2v){(short)-TD_MAXH, (short)-TD_MAXH};
+  return t;
 }
 
-/* forward step (compute_alpha16 :286-367) */
-static __device__ __forceinline__ void alpha_step(short *a, short g11, short g10)
+/* forward step (compute_alpha16 :286-367): r0 = max(a1+g11, a0-g11), r1 = max(a3-g10, a2+g10),
+ * r2 = max(a5+g10, a4-g10), r3 = max(a7-g11, a6+g11), r4..r7 the opposite signs; minus max */
+static __device__ __forceinline__ void alpha_step(tm_t &a, short g11, short g10)
 {
-  short r0 = smax(sadd(a[1], g11), ssub(a[0], g11)), r4 = smax(ssub(a[1], g11), sadd(a[0], g11));
-  short r1 = smax(ssub(a[3], g10), sadd(a[2], g10)), r5 = smax(sadd(a[3], g10), ssub(a[2], g10));
-  short r2 = smax(sadd(a[5], g10), ssub(a[4], g10)), r6 = smax(ssub(a[5], g10), sadd(a[4], g10));
-  short r3 = smax(ssub(a[7], g11), sadd(a[6], g11)), r7 = smax(sadd(a[7], g11), ssub(a[6], g11));
-  short mx = smax(smax(smax(r0, r1), smax(r2, r3)), smax(smax(r4, r5), smax(r6, r7)));
-  a[0] = ssub(r0, mx); a[1] = ssub(r1, mx); a[2] = ssub(r2, mx); a[3] = ssub(r3, mx);
-  a[4] = ssub(r4, mx); a[5] = ssub(r5, mx); a[6] = ssub(r6, mx); a[7] = ssub(r7, mx);
+  const s2v G = {g11, (short)-g10}, H = {g10, (short)-g11};
+  const s2v x13 = SHUF2(a.v[0], a.v[1], 1, 3), x02 = SHUF2(a.v[0], a.v[1], 0, 2);
+  const s2v x57 = SHUF2(a.v[2], a.v[3], 1, 3), x46 = SHUF2(a.v[2], a.v[3], 0, 2);
+  const s2v r01 = max2(adds2(x13, G), subs2(x02, G)), r45 = max2(subs2(x13, G), adds2(x02, G));
+  const s2v r23 = max2(adds2(x57, H), subs2(x46, H)), r67 = max2(subs2(x57, H), adds2(x46, H));
+  const s2v m = max2(max2(r01, r23), max2(r45, r67)), mm = max2(m, SHUF2(m, m, 1, 0));
+  a.v[0] = subs2(r01, mm); a.v[1] = subs2(r23, mm); a.v[2] = subs2(r45, mm); a.v[3] = subs2(r67, mm);
 }
 
-/* backward step (compute_beta16 :588-685) */
-static __device__ __forceinline__ void beta_step(short *b, short g11, short g10)
+/* backward step (compute_beta16 :588-685): r0 = max(b4+g11, b0-g11), r1 = max(b4-g11, b0+g11),
+ * r2 = max(b5-g10, b1+g10), r3 = max(b5+g10, b1-g10), r4 = max(b6+g10, b2-g10),
+ * r5 = max(b6-g10, b2+g10), r6 = max(b7-g11, b3+g11), r7 = max(b7+g11, b3-g11); minus max */
+static __device__ __forceinline__ void beta_step(tm_t &b, short g11, short g10)
 {
-  short r0 = smax(sadd(b[4], g11), ssub(b[0], g11)), r1 = smax(ssub(b[4], g11), sadd(b[0], g11));
-  short r2 = smax(ssub(b[5], g10), sadd(b[1], g10)), r3 = smax(sadd(b[5], g10), ssub(b[1], g10));
-  short r4 = smax(sadd(b[6], g10), ssub(b[2], g10)), r5 = smax(ssub(b[6], g10), sadd(b[2], g10));
-  short r6 = smax(ssub(b[7], g11), sadd(b[3], g11)), r7 = smax(sadd(b[7], g11), ssub(b[3], g11));
-  short mx = smax(smax(smax(r0, r1), smax(r2, r3)), smax(smax(r4, r5), smax(r6, r7)));
-  b[0] = ssub(r0, mx); b[1] = ssub(r1, mx); b[2] = ssub(r2, mx); b[3] = ssub(r3, mx);
-  b[4] = ssub(r4, mx); b[5] = ssub(r5, mx); b[6] = ssub(r6, mx); b[7] = ssub(r7, mx);
+  const s2v G = {g11, (short)-g10}, H = {g10, (short)-g11};
+  const s2v r02 = max2(adds2(b.v[2], G), subs2(b.v[0], G)), r13 = max2(subs2(b.v[2], G), adds2(b.v[0], G));
+  const s2v r46 = max2(adds2(b.v[3], H), subs2(b.v[1], H)), r57 = max2(subs2(b.v[3], H), adds2(b.v[1], H));
+  const s2v m = max2(max2(r02, r13), max2(r46, r57)), mm = max2(m, SHUF2(m, m, 1, 0));
+  const s2v n02 = subs2(r02, mm), n13 = subs2(r13, mm), n46 = subs2(r46, mm), n57 = subs2(r57, mm);
+  b.v[0] = SHUF2(n02, n13, 0, 2); b.v[1] = SHUF2(n02, n13, 1, 3);
+  b.v[2] = SHUF2(n46, n57, 0, 2); b.v[3] = SHUF2(n46, n57, 1, 3);
 }
 
-/* extrinsic of one step from alpha(k), beta(k+1), gamma(k) (compute_ext16 :733-875) */
-static __device__ __forceinline__ short ext_of(const short *a, const short *b, short g11, short g10)
+/* extrinsic of one step from alpha(k), beta(k+1), gamma(k) (compute_ext16 :733-875):
+ * m00 = max(a0+b0, a1+b4, a6+b7, a7+b3) - g11, m11 = max(a0+b4, a1+b0, a6+b3, a7+b7) + g11,
+ * m01 = max(a2+b5, a3+b1, a4+b2, a5+b6) - g10, m10 = max(a2+b1, a3+b5, a4+b6, a5+b2) + g10,
+ * ext = max(m10, m11) - max(m01, m00) */
+static __device__ __forceinline__ short ext_of(const tm_t &a, const tm_t &b, short g11, short g10)
 {
-  short m00 = smax(smax(sadd(a[0], b[0]), sadd(a[1], b[4])), smax(sadd(a[6], b[7]), sadd(a[7], b[3])));
-  short m11 = smax(smax(sadd(a[0], b[4]), sadd(a[1], b[0])), smax(sadd(a[6], b[3]), sadd(a[7], b[7])));
-  short m01 = smax(smax(sadd(a[2], b[5]), sadd(a[3], b[1])), smax(sadd(a[4], b[2]), sadd(a[5], b[6])));
-  short m10 = smax(smax(sadd(a[2], b[1]), sadd(a[3], b[5])), smax(sadd(a[4], b[6]), sadd(a[5], b[2])));
-  m01 = ssub(m01, g10);
-  m00 = ssub(m00, g11);
-  m10 = sadd(m10, g10);
-  m11 = sadd(m11, g11);
-  return ssub(smax(m10, m11), smax(m01, m00));
+  const s2v p04 = SHUF2(b.v[0], b.v[2], 0, 2), p40 = SHUF2(b.v[2], b.v[0], 0, 2);
+  const s2v q73 = SHUF2(b.v[3], b.v[1], 1, 3), q37 = SHUF2(b.v[1], b.v[3], 1, 3);
+  const s2v r51 = SHUF2(b.v[2], b.v[0], 1, 3), r15 = SHUF2(b.v[0], b.v[2], 1, 3);
+  const s2v s26 = SHUF2(b.v[1], b.v[3], 0, 2), s62 = SHUF2(b.v[3], b.v[1], 0, 2);
+  const s2v M00 = max2(adds2(a.v[0], p04), adds2(a.v[3], q73)), M11 = max2(adds2(a.v[0], p40), adds2(a.v[3], q37));
+  const s2v M01 = max2(adds2(a.v[1], r51), adds2(a.v[2], s26)), M10 = max2(adds2(a.v[1], r15), adds2(a.v[2], s62));
+  s2v T = max2(SHUF2(M00, M11, 0, 2), SHUF2(M00, M11, 1, 3));   /* (m00, m11) */
+  s2v U = max2(SHUF2(M01, M10, 0, 2), SHUF2(M01, M10, 1, 3));   /* (m01, m10) */
+  T = adds2(T, (s2v){(short)-g11, g11});
+  U = adds2(U, (s2v){(short)-g10, g10});
+  const s2v V = max2(T, U);                                      /* (max(m00, m01), max(m11, m10)) */
+  return __builtin_elementwise_sub_sat(V.y, V.x);
 }
 
 static __device__ __forceinline__ void gamma_of(const short *sys, const short *par, uint32_t e, short &g11, short &g10)
@@ -116,77 +146,107 @@ static __device__ __forceinline__ void gamma_of(const short *sys, const short *p
  * log_map16 for the calling lane (window q of its block): sys / par in the reference's vector
  * layout (element 8k + q), extrinsic out likewise.  Lanes of a block exchange re-run seeds with
  * width-8 shuffles; the 8 lanes of a block are always active together.
+ *
+ * Alpha is not stored per step: the forward pass keeps checkpoints alpha(S c) (those with
+ * S c <= 5, c = 0 included, from the re-run) plus the first run's alpha(5), and the backward
+ * pass recomputes each S-step segment into registers together with its gammas, reproducing the
+ * reference's mix exactly: alpha(0..5) from the re-run, alpha(6..) from the first run.  The
+ * alphas of the last 6 steps, needed again by the backward re-run, wait in LDS (asave).
  */
 static __device__ __forceinline__ void log_map(const short *sys, const short *par, short *ext, uint4 *A, uint32_t K,
-                                               uint32_t q, int tf)
+                                               uint32_t q, int tf, uint4 *asave /* [6][64] */)
 {
-  const uint32_t K1 = K >> 3;
-  short a[8], g11, g10;
+  const uint32_t K1 = K >> 3, nseg = (K1 + TD_SEG - 1) / TD_SEG, lane = threadIdx.x & 63;
+  uint4 *A5 = A + 8 * (nseg + 1);             /* first-run alpha(5) */
+  short g11, g10;
   /* forward, first run */
-#pragma unroll
-  for (int s = 0; s < 8; s++) a[s] = (s == 0 && q == 0) ? 0 : -TD_MAXH;
-  A[q] = pack8(a);
+  tm_t a = tm_init(q == 0);
   for (uint32_t k = 0; k < K1; k++) {
     gamma_of(sys, par, 8 * k + q, g11, g10);
     alpha_step(a, g11, g10);
-    A[8 * (k + 1) + q] = pack8(a);
+    if (k + 1 == 5) A5[q] = tm_pack(a);
+    if (((k + 1) & (TD_SEG - 1)) == 0) A[8 * ((k + 1) / TD_SEG) + q] = tm_pack(a);
   }
-  /* forward re-run over L/8 steps from the previous window's final alpha */
-  short fin[8];
+  /* forward re-run over L/8 steps from the previous window's final alpha; its alpha(0) is
+   * checkpoint 0, alpha(1..5) are recomputed from it */
+  const tm_t fin = a;
+  {
+    const tm_t z = tm_init(true);
 #pragma unroll
-  for (int s = 0; s < 8; s++) {
-    fin[s] = a[s];
-    short up = (short)__shfl_up((int)a[s], 1, 8);
-    a[s] = q == 0 ? (s == 0 ? 0 : -TD_MAXH) : up;
+    for (int v = 0; v < 4; v++) {
+      const uint32_t up = (uint32_t)__shfl_up((int)__builtin_bit_cast(uint32_t, a.v[v]), 1, 8);
+      a.v[v] = q == 0 ? z.v[v] : __builtin_bit_cast(s2v, up);
+    }
   }
-  A[q] = pack8(a);
+  A[q] = tm_pack(a);
   for (uint32_t k = 0; k < 5; k++) {
     gamma_of(sys, par, 8 * k + q, g11, g10);
     alpha_step(a, g11, g10);
-    A[8 * (k + 1) + q] = pack8(a);
+    /* checkpoints inside the re-run range hold re-run values (alpha(1..5) of the reference) */
+    if (((k + 1) & (TD_SEG - 1)) == 0 && k + 1 <= K1) A[8 * ((k + 1) / TD_SEG) + q] = tm_pack(a);
   }
   /* termination betas of the last window (compute_beta16 :467-521, int16 wrap arithmetic) */
-  short t[8];
+  tm_t t;
   {
-    short m[3], mm[3];
+    short m[3], mm[3], tv[8];
 #pragma unroll
     for (int j = 0; j < 3; j++) gamma_of(sys + 8 * tf, par, K + j, m[j], mm[j]);   /* m_11/m_10[n + j] */
     short beta0 = (short)-m[2], beta1 = m[2];
     short b0_2 = (short)(beta0 - m[1]), b1_2 = (short)(beta0 + m[1]), b2_2 = (short)(beta1 + mm[1]),
           b3_2 = (short)(beta1 - mm[1]);
-    t[0] = (short)(b0_2 - m[0]); t[1] = (short)(b0_2 + m[0]); t[2] = (short)(b1_2 + mm[0]); t[3] = (short)(b1_2 - mm[0]);
-    t[4] = (short)(b2_2 - mm[0]); t[5] = (short)(b2_2 + mm[0]); t[6] = (short)(b3_2 + m[0]); t[7] = (short)(b3_2 - m[0]);
-    short bm = t[0];
+    tv[0] = (short)(b0_2 - m[0]); tv[1] = (short)(b0_2 + m[0]); tv[2] = (short)(b1_2 + mm[0]); tv[3] = (short)(b1_2 - mm[0]);
+    tv[4] = (short)(b2_2 - mm[0]); tv[5] = (short)(b2_2 + mm[0]); tv[6] = (short)(b3_2 + m[0]); tv[7] = (short)(b3_2 - m[0]);
+    short bm = tv[0];
 #pragma unroll
-    for (int s = 1; s < 8; s++) bm = bm > t[s] ? bm : t[s];
+    for (int s = 1; s < 8; s++) bm = bm > tv[s] ? bm : tv[s];
 #pragma unroll
-    for (int s = 0; s < 8; s++) t[s] = (short)(t[s] - bm);
+    for (int v = 0; v < 4; v++) t.v[v] = (s2v){(short)(tv[2 * v] - bm), (short)(tv[2 * v + 1] - bm)};
   }
-  /* backward, first run: seeded with the lane's own final alpha as stored after the re-run
-   * (the re-run reaches step K1 when K1 == 5); extrinsic of steps whose beta the re-run does
-   * not touch */
-  unpack8(A[8 * K1 + q], fin);
-  short b[8], al[8];
+  /* backward, first run: seeded with the lane's own final alpha as the reference stores it
+   * after the re-run (the re-run reaches step K1 when K1 == 5); extrinsic of steps whose beta
+   * the re-run does not touch */
+  tm_t b = q == 7 ? t : (K1 == 5 ? a : fin);
+  const int kr = (int)K1 - 6;                 /* steps >= kr take their extrinsic from the re-run */
+  for (int seg = (int)nseg - 1; seg >= 0; seg--) {
+    const int k0 = seg * TD_SEG, n = min((int)TD_SEG, (int)K1 - k0);
+    /* a partial last segment reads padding past K1 (the arrays have TD_SEG steps of slack) and
+     * leaves beta untouched for those steps */
+    const short *sp = sys + 8 * k0 + q, *pp = par + 8 * k0 + q;
+    uint4 al[TD_SEG];
+    uint32_t gg[TD_SEG];                       /* g11 | g10 << 16 */
+    tm_t c = tm_unpack(A[8 * seg + q]);
 #pragma unroll
-  for (int s = 0; s < 8; s++) b[s] = q == 7 ? t[s] : fin[s];
-  for (int k = (int)K1 - 1; k >= 0; k--) {
-    gamma_of(sys, par, 8 * k + q, g11, g10);
-    if (k < (int)K1 - 6) {
-      unpack8(A[8 * k + q], al);
-      ext[8 * k + q] = ext_of(al, b, g11, g10);
+    for (int j = 0; j < TD_SEG; j++) {
+      short x11, x10;
+      gamma_of(sp, pp, 8 * j, x11, x10);
+      gg[j] = (uint16_t)x11 | ((uint32_t)(uint16_t)x10 << 16);
+      al[j] = tm_pack(c);
+      if (k0 + j == 5) c = tm_unpack(A5[q]);            /* alpha(6) continues the first run */
+      alpha_step(c, x11, x10);
     }
-    beta_step(b, g11, g10);
+#pragma unroll
+    for (int j = TD_SEG - 1; j >= 0; j--) {
+      const int k = k0 + j;
+      const short x11 = (short)gg[j], x10 = (short)(gg[j] >> 16);
+      if (j < n) {
+        if (k < kr) ext[8 * k + q] = ext_of(tm_unpack(al[j]), b, x11, x10);
+        else asave[(k - kr) * 64 + lane] = al[j];
+      }
+      tm_t nb = b;
+      beta_step(nb, x11, x10);
+#pragma unroll
+      for (int v = 0; v < 4; v++) b.v[v] = j < n ? nb.v[v] : b.v[v];
+    }
   }
   /* backward re-run over the last L/8 steps from the next window's beta[0] */
 #pragma unroll
-  for (int s = 0; s < 8; s++) {
-    short dn = (short)__shfl_down((int)b[s], 1, 8);
-    b[s] = q == 7 ? t[s] : dn;
+  for (int v = 0; v < 4; v++) {
+    const uint32_t dn = (uint32_t)__shfl_down((int)__builtin_bit_cast(uint32_t, b.v[v]), 1, 8);
+    b.v[v] = q == 7 ? t.v[v] : __builtin_bit_cast(s2v, dn);
   }
-  for (int k = (int)K1 - 1; k >= (int)K1 - 6 && k >= 0; k--) {
+  for (int k = (int)K1 - 1; k >= kr && k >= 0; k--) {
     gamma_of(sys, par, 8 * k + q, g11, g10);
-    unpack8(A[8 * k + q], al);
-    ext[8 * k + q] = ext_of(al, b, g11, g10);
+    ext[8 * k + q] = ext_of(tm_unpack(asave[(k - kr) * 64 + lane]), b, g11, g10);
     if (k >= (int)K1 - 5) beta_step(b, g11, g10);
   }
 }
@@ -215,6 +275,7 @@ __global__ void __launch_bounds__(64) k_td16(int n_cb, uint32_t K, const int16_t
   __shared__ uint32_t crctab[256];
   __shared__ uint8_t dec[8][6144 / 8 + 8];
   __shared__ uint32_t done_it[8];
+  __shared__ uint4 asave[6 * 64];
   const uint32_t lane = threadIdx.x, g = lane >> 3, q = lane & 7;
   const int cb = (int)(blockIdx.x * 8 + g);
   const bool valid = cb < n_cb;
@@ -244,14 +305,14 @@ __global__ void __launch_bounds__(64) k_td16(int n_cb, uint32_t K, const int16_t
   }
   __syncthreads();
   bool active = valid && max_it > 0;
-  if (valid) log_map(B.s0, B.yp1, B.ext, B.A, K, q, 0);
+  if (valid) log_map(B.s0, B.yp1, B.ext, B.A, K, q, 0, asave);
   __syncthreads();
   uint32_t it = 0;
   for (it = 1; it <= max_it; it++) {
     if (active)
       for (uint32_t v = 0; v < K1; v++) B.s2[8 * v + q] = B.ext[pi4[8 * v + q]];
     __syncthreads();
-    if (active) log_map(B.s2, B.yp2, B.ext2, B.A, K, q, 1);
+    if (active) log_map(B.s2, B.yp2, B.ext2, B.A, K, q, 1, asave);
     __syncthreads();
     if (active) {
       for (uint32_t v = 0; v < K1; v++) {
@@ -280,7 +341,7 @@ __global__ void __launch_bounds__(64) k_td16(int n_cb, uint32_t K, const int16_t
     }
     __syncthreads();
     if (active && done_it[g]) active = false;
-    if (active && it < max_it) log_map(B.s1, B.yp1, B.ext, B.A, K, q, 0);
+    if (active && it < max_it) log_map(B.s1, B.yp1, B.ext, B.A, K, q, 0, asave);
     __syncthreads();
     if (active && it < max_it)
       for (uint32_t v = 0; v < K1; v++) {
