@@ -27,7 +27,9 @@ static __device__ __forceinline__ short sadd(short a, short b) { return __builti
 static __device__ __forceinline__ short ssub(short a, short b) { return __builtin_elementwise_sub_sat(a, b); }
 
 #define TD_MAXH 128    /* MAX / 2 */
-#define TD_SEG 4      /* alpha checkpoint interval (steps) */
+#ifndef TD_SEG
+#define TD_SEG 8      /* alpha checkpoint interval (steps); measured best of 2/4/8/16 at C5 */
+#endif
 
 struct td_blk_t {      /* one block's scratch (int16 element offsets, see td_layout) */
   short *s0, *s1, *s2, *yp1, *yp2, *ext, *ext2;
