@@ -155,9 +155,17 @@ static __device__ __forceinline__ void gamma_of(const short *sys, const short *p
  * reference's mix exactly: alpha(0..5) from the re-run, alpha(6..) from the first run.  The
  * alphas of the last 6 steps, needed again by the backward re-run, wait in LDS (asave).
  */
-static __device__ __forceinline__ void log_map(const short *sys, const short *par, short *ext, uint4 *A, uint32_t K,
-                                               uint32_t q, int tf, uint4 *asave /* [6][64] */)
+/* Not inlined: one copy for the three call sites keeps the kernel at 2 waves per SIMD.
+ * POST: the stored extrinsic is already the next half-iteration's input, ext - sys + s0
+ * (the loop's update pass of phy_threegpplte_turbo_decoder16, fused into the store) */
+template <bool POST>
+static __device__ __attribute__((noinline)) void log_map(const short *sys, const short *par, short *ext, uint4 *A, uint32_t K,
+                                               uint32_t q, int tf, uint4 *asave /* [6][64] */, const short *s0)
 {
+  auto put = [&](uint32_t e, short v) {
+    if constexpr (POST) v = __builtin_elementwise_add_sat(__builtin_elementwise_sub_sat(v, sys[e]), s0[e]);
+    ext[e] = v;
+  };
   const uint32_t K1 = K >> 3, nseg = (K1 + TD_SEG - 1) / TD_SEG, lane = threadIdx.x & 63;
   uint4 *A5 = A + 8 * (nseg + 1);             /* first-run alpha(5) */
   short g11, g10;
@@ -231,7 +239,7 @@ static __device__ __forceinline__ void log_map(const short *sys, const short *pa
       const int k = k0 + j;
       const short x11 = (short)gg[j], x10 = (short)(gg[j] >> 16);
       if (j < n) {
-        if (k < kr) ext[8 * k + q] = ext_of(tm_unpack(al[j]), b, x11, x10);
+        if (k < kr) put(8 * k + q, ext_of(tm_unpack(al[j]), b, x11, x10));
         else asave[(k - kr) * 64 + lane] = al[j];
       }
       tm_t nb = b;
@@ -248,7 +256,7 @@ static __device__ __forceinline__ void log_map(const short *sys, const short *pa
   }
   for (int k = (int)K1 - 1; k >= kr && k >= 0; k--) {
     gamma_of(sys, par, 8 * k + q, g11, g10);
-    ext[8 * k + q] = ext_of(tm_unpack(asave[(k - kr) * 64 + lane]), b, g11, g10);
+    put(8 * k + q, ext_of(tm_unpack(asave[(k - kr) * 64 + lane]), b, g11, g10));
     if (k >= (int)K1 - 5) beta_step(b, g11, g10);
   }
 }
@@ -307,14 +315,14 @@ __global__ void __launch_bounds__(64) k_td16(int n_cb, uint32_t K, const int16_t
   }
   __syncthreads();
   bool active = valid && max_it > 0;
-  if (valid) log_map(B.s0, B.yp1, B.ext, B.A, K, q, 0, asave);
+  if (valid) log_map<false>(B.s0, B.yp1, B.ext, B.A, K, q, 0, asave, B.s0);
   __syncthreads();
   uint32_t it = 0;
   for (it = 1; it <= max_it; it++) {
     if (active)
       for (uint32_t v = 0; v < K1; v++) B.s2[8 * v + q] = B.ext[pi4[8 * v + q]];
     __syncthreads();
-    if (active) log_map(B.s2, B.yp2, B.ext2, B.A, K, q, 1, asave);
+    if (active) log_map<false>(B.s2, B.yp2, B.ext2, B.A, K, q, 1, asave, B.s0);
     __syncthreads();
     if (active) {
       for (uint32_t v = 0; v < K1; v++) {
@@ -343,13 +351,7 @@ __global__ void __launch_bounds__(64) k_td16(int n_cb, uint32_t K, const int16_t
     }
     __syncthreads();
     if (active && done_it[g]) active = false;
-    if (active && it < max_it) log_map(B.s1, B.yp1, B.ext, B.A, K, q, 0, asave);
-    __syncthreads();
-    if (active && it < max_it)
-      for (uint32_t v = 0; v < K1; v++) {
-        const uint32_t i = 8 * v + q;
-        B.ext[i] = sadd(ssub(B.ext[i], B.s1[i]), B.s0[i]);
-      }
+    if (active && it < max_it) log_map<true>(B.s1, B.yp1, B.ext, B.A, K, q, 0, asave, B.s0);
     __syncthreads();
     if (!__any(active)) break;
   }
