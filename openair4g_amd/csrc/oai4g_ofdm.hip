@@ -341,6 +341,181 @@ static __device__ __forceinline__ void idft_unit(uint32_t *lds, int t, bool acti
 }
 
 /* ======================================================================================
+ * idft2048 in three register passes and two LDS exchanges (T = 128 threads, NA transforms).
+ *
+ * Input index n = e + 2 r1 + 8 r2 + 32 r3 + 128 n4 (the reference's even/odd split, then three
+ * mod-4 splits, then the idft16 leaf), output index k = k4 + 16 m3 + 64 m2 + 256 m1 + 1024 m0.
+ *   pass A: thread t = (e, r1, r2, r3) runs leaf t (idft16 over n4) -> L_t[k4];
+ *   pass B: thread u = j + 8 k4 (j = e + 2 r1) holds L_(j, r2, r3)[k4] for all 16 (r2, r3) and
+ *           runs both the 64-level (ibfly4_16 over r3, >>3) and the 256-level (ibfly4 over r2,
+ *           >>1) in registers -> out256_j[k2], k2 = k4 + 16 m3 + 64 m2;
+ *   pass C: thread v holds out256_j[k2] for all 8 j and k2 in {v, v + 128}, runs the 1024-level
+ *           (ibfly4 over r1, >>1) and the 2048-level (ibfly2 over e, mulhi) and stores.
+ * Every butterfly, twiddle, shift and saturation is the reference's (lte_dfts.c:2779-2866 ->
+ * :2630-2687 -> :2284-2357 -> :1856-1946 -> :1597-1724); only the data movement differs from
+ * the level-by-level schedule of idft_unit (4 exchanges, 9 barriers per symbol there; 2
+ * exchanges, 3 barriers here).
+ * LDS images (one region of X1W words per transform, the second aliasing the first):
+ *   E1: L_t[k4] at k4*144 + 2 (t & 31) + ((t >> 5) & 1) + 64 (t >> 6)  — pass-A b32 stores 2-way
+ *       (free), pass-B ds_read_b64 of the (r3, r3 + 1) pair conflict-free;
+ *   E2: out256_j[k2] at 8 k2 + j + 2 (k2 >> 3) — pass-B b32 stores consecutive, pass-C
+ *       ds_read_b64 of (j, j + 1) conflict-free.
+ * ==================================================================================== */
+struct idft2048_tw_t {
+  static constexpr int X1W = 16 * 144;
+  twp_t l16[7];        /* W16^{0,1,2,3,4,6,9} (wave-uniform) */
+  s16x2 b64[3];        /* W64^{r k4}, r = 1..3, k4 = t >> 3 */
+  s16x2 b256[4][3];    /* W256^{r (k4 + 16 m3)} */
+  s16x2 c1024[2][3];   /* W1024^{r k2}, k2 = t + 128 h */
+  s16x2 c2048[8];      /* W2048^{k1}, k1 = t + 128 (h + 2 m1) */
+
+  __device__ __forceinline__ void load(const uint32_t *tw, int t)
+  {
+    gu32_t *g = (gu32_t *)tw;
+    constexpr int i16[7] = {0, 1, 2, 3, 4, 6, 9};
+#pragma unroll
+    for (int i = 0; i < 7; i++)
+      l16[i] = {u2c(g[oai4g_tw_offset(4) + i16[i]]), u2c(g[OAI4G_TW_TOTAL + oai4g_tw_offset(4) + i16[i]])};
+    const int k4 = t >> 3;
+#pragma unroll
+    for (int r = 0; r < 3; r++) b64[r] = u2c(g[oai4g_tw_offset(6) + (r + 1) * k4]);
+#pragma unroll
+    for (int m3 = 0; m3 < 4; m3++)
+#pragma unroll
+      for (int r = 0; r < 3; r++) b256[m3][r] = u2c(g[oai4g_tw_offset(8) + (r + 1) * (k4 + 16 * m3)]);
+#pragma unroll
+    for (int h = 0; h < 2; h++)
+#pragma unroll
+      for (int r = 0; r < 3; r++) c1024[h][r] = u2c(g[oai4g_tw_offset(10) + (r + 1) * (t + 128 * h)]);
+#pragma unroll
+    for (int i = 0; i < 8; i++) c2048[i] = u2c(g[oai4g_tw_offset(11) + t + 128 * i]);
+  }
+};
+
+typedef uint32_t u32x2_t __attribute__((ext_vector_type(2)));
+
+template <int NA, class Prod, class Cons>
+static __device__ __forceinline__ void idft2048_unit(uint32_t *lds, int t, bool active, const idft2048_tw_t &tw,
+                                                     Prod prod, Cons cons, int scale)
+{
+  constexpr int X1W = idft2048_tw_t::X1W;
+  s16x2 x[NA][16];
+  /* pass A: leaves */
+  if (active) {
+    prod(x);
+    const uint32_t wo = 2u * (t & 31) + ((t >> 5) & 1) + 64u * (t >> 6);
+#pragma unroll
+    for (int a = 0; a < NA; a++) {
+      idft16_reg(x[a], tw.l16);
+#pragma unroll
+      for (int k = 0; k < 16; k++) lds[a * X1W + k * 144 + wo] = c2u(x[a][k]);
+    }
+  }
+  __syncthreads();
+  /* pass B: 64- and 256-levels of the 256-point transform j = t & 7 at k4 = t >> 3 */
+  const int j = t & 7, k4 = t >> 3;
+  if (active) {
+    const uint32_t ro = (uint32_t)k4 * 144u + 2u * j;
+#pragma unroll
+    for (int a = 0; a < NA; a++)
+#pragma unroll
+      for (int r2 = 0; r2 < 4; r2++)
+#pragma unroll
+        for (int p = 0; p < 2; p++) {
+          const u32x2_t v = *(const u32x2_t *)&lds[a * X1W + ro + 16 * r2 + 64 * p];
+          x[a][4 * r2 + 2 * p] = u2c(v.x);
+          x[a][4 * r2 + 2 * p + 1] = u2c(v.y);
+        }
+  }
+  __syncthreads();   /* E2 aliases E1 */
+  if (active) {
+    const twp_t w64[3] = {tw_of(tw.b64[0]), tw_of(tw.b64[1]), tw_of(tw.b64[2])};
+#pragma unroll
+    for (int a = 0; a < NA; a++) {
+      s16x2 o[4][4];   /* [r2][m3] */
+#pragma unroll
+      for (int r2 = 0; r2 < 4; r2++) {
+        const s16x2 *v = &x[a][4 * r2];
+        r4inv(v[0], cmulc16(v[1], w64[0]), cmulc16(v[2], w64[1]), cmulc16(v[3], w64[2]), o[r2][0], o[r2][1],
+              o[r2][2], o[r2][3]);
+#pragma unroll
+        for (int m = 0; m < 4; m++) o[r2][m] = shr3(o[r2][m]);
+      }
+#pragma unroll
+      for (int m3 = 0; m3 < 4; m3++) {
+        const twp_t w[3] = {tw_of(tw.b256[m3][0]), tw_of(tw.b256[m3][1]), tw_of(tw.b256[m3][2])};
+        s16x2 y[4];
+        ibfly4(o[0][m3], o[1][m3], o[2][m3], o[3][m3], w[0], w[1], w[2], y[0], y[1], y[2], y[3]);
+#pragma unroll
+        for (int m2 = 0; m2 < 4; m2++) {
+          const uint32_t k2 = (uint32_t)k4 + 16u * m3 + 64u * m2;
+          lds[a * X1W + 8u * k2 + j + 2u * (k2 >> 3)] = c2u(shr1(y[m2]));
+        }
+      }
+    }
+  }
+  __syncthreads();
+  /* pass C: 1024- and 2048-levels for k2 = t + 128 h */
+  if (active) {
+#pragma unroll
+    for (int a = 0; a < NA; a++) {
+      s16x2 v[2][8];
+#pragma unroll
+      for (int h = 0; h < 2; h++) {
+        const uint32_t k2 = (uint32_t)t + 128u * h;
+        const uint32_t ro = 8u * k2 + 2u * (k2 >> 3);
+#pragma unroll
+        for (int i = 0; i < 4; i++) {
+          const u32x2_t q = *(const u32x2_t *)&lds[a * X1W + ro + 2 * i];
+          v[h][2 * i] = u2c(q.x);
+          v[h][2 * i + 1] = u2c(q.y);
+        }
+      }
+#pragma unroll
+      for (int h = 0; h < 2; h++) {
+        const twp_t w[3] = {tw_of(tw.c1024[h][0]), tw_of(tw.c1024[h][1]), tw_of(tw.c1024[h][2])};
+        s16x2 o[2][4];   /* [e][m1] */
+#pragma unroll
+        for (int e = 0; e < 2; e++) {
+          ibfly4(v[h][e], v[h][e + 2], v[h][e + 4], v[h][e + 6], w[0], w[1], w[2], o[e][0], o[e][1], o[e][2],
+                 o[e][3]);
+#pragma unroll
+          for (int m = 0; m < 4; m++) o[e][m] = shr1(o[e][m]);
+        }
+#pragma unroll
+        for (int m1 = 0; m1 < 4; m1++) {
+          s16x2 y0, y1;
+          ibfly2(o[0][m1], o[1][m1], tw_of(tw.c2048[h + 2 * m1]), y0, y1);
+          if (scale) { y0 = mulhi2(y0); y1 = mulhi2(y1); }
+          cons(a, t, 128 * h + 256 * m1, y0);
+          cons(a, t, 128 * h + 256 * m1 + 1024, y1);
+        }
+      }
+    }
+  }
+}
+
+/* twiddle registers and LDS words per transform of the schedule used for each size */
+template <int LOG2N>
+struct idft_sel {
+  using tw_t = idft_tw_t<LOG2N>;
+  static constexpr int XW = (1 << LOG2N) + ((1 << LOG2N) >> 5);
+};
+template <>
+struct idft_sel<11> {
+  using tw_t = idft2048_tw_t;
+  static constexpr int XW = idft2048_tw_t::X1W;
+};
+template <int LOG2N, int NA, class Prod, class Cons>
+static __device__ __forceinline__ void idft_any(uint32_t *lds, int t, bool active,
+                                                const typename idft_sel<LOG2N>::tw_t &tw, Prod prod, Cons cons,
+                                                int scale)
+{
+  if constexpr (LOG2N == 11) idft2048_unit<NA>(lds, t, active, tw, prod, cons, scale);
+  else idft_unit<LOG2N, NA>(lds, t, active, tw, prod, cons, scale);
+}
+
+/* ======================================================================================
  * Drop-in OFDM modulation: per-symbol IDFT + CP from a frequency grid in global memory.
  * 128-thread workgroups, 128/T units each.
  * ==================================================================================== */
@@ -354,18 +529,18 @@ template <int LOG2N>
 __global__ void __launch_bounds__(128) k_ofdm(const int32_t *__restrict__ in, int32_t *__restrict__ out,
                                               ofdm_args_t a, const uint32_t *__restrict__ tw)
 {
-  constexpr int N = 1 << LOG2N, T = N >> 4, UNITS = 128 / T, LDSW = N + (N >> 5);
+  constexpr int N = 1 << LOG2N, T = N >> 4, UNITS = 128 / T, LDSW = idft_sel<LOG2N>::XW;
   __shared__ uint32_t lds_all[UNITS * LDSW];
   const int unit = threadIdx.x / T, t = threadIdx.x % T;
   const int s = blockIdx.x * UNITS + unit;
   const bool active = s < a.nsym;
-  idft_tw_t<LOG2N> twr;
+  typename idft_sel<LOG2N>::tw_t twr;
   twr.load(tw, t);
   ofdm_sym_t d = active ? a.sym[s] : a.sym[0];
   const uint32_t *src = (const uint32_t *)in + d.in_off;
   uint32_t *dst = (uint32_t *)out + d.out_off;
   const int cp = (int)d.cp;
-  idft_unit<LOG2N, 1>(
+  idft_any<LOG2N, 1>(
       lds_all + unit * LDSW, t, active, twr, [&](s16x2 (*x)[16]) {
 #pragma unroll
         for (int n = 0; n < 16; n++) x[0][n] = u2c(src[t + T * n]);
@@ -485,10 +660,13 @@ static __device__ __forceinline__ void alm_pair(s16x2 ta, s16x2 tb, uint32_t rol
  * ==================================================================================== */
 template <int LOG2N>
 struct modofdm_geom {
-  static constexpr int N = 1 << LOG2N, T = N >> 4, UNITS = 128 / T, LDSW = N + (N >> 5);
+  static constexpr int N = 1 << LOG2N, T = N >> 4, UNITS = 128 / T, LDSW = idft_sel<LOG2N>::XW;
   static constexpr int EW = (6 * ((N * 5) / 8)) / 32 + 4;   /* staged e-bit words per codeword */
 };
 
+#ifndef OAI4G_DIAG_MODOFDM
+#define OAI4G_DIAG_MODOFDM 0   /* timing diagnostics only: 1 = no IQ stores, 2 = no e-bit staging */
+#endif
 #ifndef OAI4G_MODOFDM_WAVES
 #define OAI4G_MODOFDM_WAVES 3   /* measured: 3 waves/SIMD (<=168 VGPRs) beats 2 (no cap) and 4 (spills) */
 #endif
@@ -511,7 +689,7 @@ __global__ void __launch_bounds__(128) MODOFDM_ATTR k_modofdm(const cfg_dev_t *_
   __shared__ uint32_t lds_e[UNITS][2][EW];
   __shared__ uint32_t qtab[2][2][64];          /* [cw][pilot symbol][Qm bits] -> packed IQ */
   const int unit = threadIdx.x / T, t = threadIdx.x % T;
-  idft_tw_t<LOG2N> twr;
+  typename idft_sel<LOG2N>::tw_t twr;
   twr.load(c->tw, t);
   const uint32_t n_ant = c->n_ant, nsymb = c->nsymb;
   constexpr bool ecp = ECP;                        /* extended CP: 6 symbols per slot, one prefix length */
@@ -530,7 +708,41 @@ __global__ void __launch_bounds__(128) MODOFDM_ATTR k_modofdm(const cfg_dev_t *_
   const uint32_t mask0 = (1u << Qm0) - 1u, mask1 = (1u << Qm1) - 1u;
   __syncthreads();
 
-  for (int base = blockIdx.x * UNITS; base < n_items; base += gridDim.x * UNITS) {
+  /* software pipeline: the RE codes and e-bit words of a unit's next item are loaded while the
+   * current item is transformed, so no item starts with an exposed HBM round trip */
+  constexpr int EPT = (EW + T - 1) / T;          /* staged e words per thread and codeword */
+  const int stride = gridDim.x * UNITS;
+  struct pf_t {
+    u32x4_t ra, rb;
+    uint32_t e0[EPT], e1[EPT];
+  } pf;
+  auto fetch = [&](int bse) {
+    const int item = bse + unit;
+    const bool act = item < n_items;
+    const uint32_t it = act ? (uint32_t)item : 0u;
+    const uint32_t sf = it / nsymb, l = it - sf * nsymb;
+    const uint32_t sfi = (c->first_sf + (sf0 + sf) * c->sf_step) % 10;
+    const uint32_t nre = act ? c->symnre[sfi][l] : 0u, re0 = c->symbase[sfi][l];
+    const gu128_t *rsrc = (const gu128_t *)(c->remap_tm + ((size_t)sfi * 14 + l) * N + (size_t)t * 16);
+    pf.ra = rsrc[0];
+    pf.rb = rsrc[1];
+    if (act && nre && OAI4G_DIAG_MODOFDM != 2) {
+      gu32_t *esf = (gu32_t *)(ebits + (size_t)(sf * c->n_cw) * c->ebits_words);
+      const uint32_t wlo0 = (re0 * Qm0) >> 5, cnt0 = min((uint32_t)EW, (((re0 + nre) * Qm0 + 31) >> 5) - wlo0 + 1);
+#pragma unroll
+      for (int k = 0; k < EPT; k++)
+        if (t + k * T < (int)cnt0) pf.e0[k] = esf[wlo0 + t + k * T];
+      if constexpr (CW2) {
+        const uint32_t wlo1 = (re0 * Qm1) >> 5, cnt1 = min((uint32_t)EW, (((re0 + nre) * Qm1 + 31) >> 5) - wlo1 + 1);
+#pragma unroll
+        for (int k = 0; k < EPT; k++)
+          if (t + k * T < (int)cnt1) pf.e1[k] = esf[c->ebits_words + wlo1 + t + k * T];
+      }
+    }
+  };
+  fetch(blockIdx.x * UNITS);
+
+  for (int base = blockIdx.x * UNITS; base < n_items; base += stride) {
     const int item = base + unit;
     const bool active = item < n_items;
     const uint32_t it = active ? (uint32_t)item : 0u;
@@ -546,6 +758,7 @@ __global__ void __launch_bounds__(128) MODOFDM_ATTR k_modofdm(const cfg_dev_t *_
 
     if (UNITS == 1 && nre == 0 && !(CRS && pilots_any(l, ecp))) {
       /* control-region symbol: the transform of an all-zero grid is zero */
+      fetch(base + stride);
       if (active)
         for (uint32_t a = 0; a < n_ant; a++) {
           uint32_t *d = dst0 + (size_t)a * c->spt - cp;   /* CP start of antenna a */
@@ -554,23 +767,24 @@ __global__ void __launch_bounds__(128) MODOFDM_ATTR k_modofdm(const cfg_dev_t *_
       continue;
     }
 
-    /* this thread's 16 RE codes (thread-major copy): two 16-B loads issued before any use */
-    const gu128_t *rsrc = (const gu128_t *)(c->remap_tm + ((size_t)sfi * 14 + l) * N + (size_t)t * 16);
-    const u32x4_t ra = rsrc[0], rb = rsrc[1];
-    const uint32_t rw[8] = {ra.x, ra.y, ra.z, ra.w, rb.x, rb.y, rb.z, rb.w};
-
-    /* stage this symbol's e bits of each codeword (coalesced) */
-    const uint32_t *esf = ebits + (size_t)(sf * c->n_cw) * c->ebits_words;
+    /* this thread's 16 RE codes (thread-major copy, prefetched) */
+    const uint32_t rw[8] = {pf.ra.x, pf.ra.y, pf.ra.z, pf.ra.w, pf.rb.x, pf.rb.y, pf.rb.z, pf.rb.w};
+    /* stage this symbol's e bits of each codeword (prefetched words, coalesced) */
     const uint32_t wlo0 = (re0 * Qm0) >> 5, wlo1 = (re0 * Qm1) >> 5;
-    if (active && nre) {
+    if (active && nre && OAI4G_DIAG_MODOFDM != 2) {
       const uint32_t cnt0 = min((uint32_t)EW, (((re0 + nre) * Qm0 + 31) >> 5) - wlo0 + 1);
-      for (uint32_t i = t; i < cnt0; i += T) lds_e[unit][0][i] = esf[wlo0 + i];
+#pragma unroll
+      for (int k = 0; k < EPT; k++)
+        if (t + k * T < (int)cnt0) lds_e[unit][0][t + k * T] = pf.e0[k];
       if constexpr (CW2) {
         const uint32_t cnt1 = min((uint32_t)EW, (((re0 + nre) * Qm1 + 31) >> 5) - wlo1 + 1);
-        for (uint32_t i = t; i < cnt1; i += T) lds_e[unit][1][i] = esf[c->ebits_words + wlo1 + i];
+#pragma unroll
+        for (int k = 0; k < EPT; k++)
+          if (t + k * T < (int)cnt1) lds_e[unit][1][t + k * T] = pf.e1[k];
       }
     }
     __syncthreads();
+    fetch(base + stride);
 
     gu32_t *crs_tab = (gu32_t *)c->crs_tab;
     const bool crs = CRS && pilots_any(l, ecp);
@@ -578,7 +792,7 @@ __global__ void __launch_bounds__(128) MODOFDM_ATTR k_modofdm(const cfg_dev_t *_
     const uint32_t *q0 = qtab[0][pil], *q1 = qtab[1][pil];
     /* bit position of data RE idx within the staged words: idx * Qm + (re0 * Qm - 32 wlo) */
     const uint32_t b0 = re0 * Qm0 - 32 * wlo0, b1 = re0 * Qm1 - 32 * wlo1;
-    idft_unit<LOG2N, NA>(
+    idft_any<LOG2N, NA>(
         lds_data + unit * NA * LDSW, t, active, twr,
         [&](s16x2 (*x)[16]) {
           /* branch-free and staged in groups of GR REs so each LDS round trip is issued for the
@@ -659,6 +873,9 @@ __global__ void __launch_bounds__(128) MODOFDM_ATTR k_modofdm(const cfg_dev_t *_
           const int ro = hi ? off - N / 2 : off;
           auto store = [&](uint32_t *base) {
             uint32_t *d = base + tt + (hi ? N / 2 : 0);
+#if OAI4G_DIAG_MODOFDM == 1   /* timing diagnostic: the stores (almost) never happen */
+            if (c2u(y) != 0x12345678u) return;
+#endif
             d[ro] = c2u(y);
             if (off + T - 1 >= N - CPMAX && tt + off >= N - cp) d[ro - N] = c2u(y);
           };
