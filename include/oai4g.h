@@ -156,10 +156,11 @@ void oai4g_generate_pilots(int32_t **txdataF, int16_t amp, const oai4g_frame_par
  * Ns into one OFDM symbol `output` (ofdm_symbol_size REs).  Returns 0, or -1 for a bad port. */
 int oai4g_lte_dl_cell_spec(int32_t *output, int16_t amp, const oai4g_frame_parms_t *frame_parms, uint8_t Ns,
                            uint8_t l, uint8_t p);
-/* idft64..idft2048 (PHY/TOOLS/lte_dfts.c:1856-2866, decl TOOLS/defs.h:555): y = IDFT(x) */
+/* idft64..idft2048 (PHY/TOOLS/lte_dfts.c:1856-2866 incl. idft512 :2479, decl TOOLS/defs.h:555): y = IDFT(x) */
 int oai4g_idft(int log2n, const int16_t *x, int16_t *y, int scale);
 void oai4g_idft2048(const int16_t *x, int16_t *y, int scale);
 void oai4g_idft1024(const int16_t *x, int16_t *y, int scale);
+void oai4g_idft512(const int16_t *x, int16_t *y, int scale);   /* lte_dfts.c:2479 */
 void oai4g_idft256(const int16_t *x, int16_t *y, int scale);
 void oai4g_idft128(const int16_t *x, int16_t *y, int scale);
 void oai4g_idft64(const int16_t *x, int16_t *y, int scale);

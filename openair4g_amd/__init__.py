@@ -139,6 +139,7 @@ _SIGS = {
     "oai4g_idft": (ctypes.c_int, [ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int]),
     "oai4g_idft2048": (None, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int]),
     "oai4g_idft1024": (None, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int]),
+    "oai4g_idft512": (None, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int]),
     "oai4g_idft256": (None, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int]),
     "oai4g_idft128": (None, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int]),
     "oai4g_idft64": (None, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int]),
@@ -437,10 +438,12 @@ FULL_ALLOC_100 = (0xFFFFFFFF, 0xFFFFFFFF, 0xFFFFFFFF, 0xF)
 FULL_ALLOC_6 = (0x3F, 0, 0, 0)
 FULL_ALLOC_15 = (0x7FFF, 0, 0, 0)
 FULL_ALLOC_50 = (0xFFFFFFFF, 0x3FFFF, 0, 0)
+FULL_ALLOC_25 = (0x1FFFFFF, 0, 0, 0)
 
 # TBS from 3GPP TS 36.213 Table 7.1.7.2.1-1 for the configurations exercised here
 TBS_TABLE = {(9, 6): 936, (4, 6): 408, (16, 100): 30576, (19, 100): 36696, (9, 100): 15840, (28, 100): 75376,
-             (5, 50): 4392, (15, 50): 14112, (26, 50): 30576, (9, 15): 2344}
+             (5, 50): 4392, (15, 50): 14112, (26, 50): 30576, (9, 15): 2344,
+             (16, 25): 7736, (19, 25): 9144, (16, 50): 15264, (19, 50): 18336, (19, 15): 5352, (19, 6): 2152}
 
 CONFIGS = {
     # C1: dlsim 1.4 MHz SISO QPSK (MCS 9), 3 PDCCH symbols

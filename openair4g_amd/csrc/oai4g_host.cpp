@@ -865,8 +865,8 @@ static void release_cfg(oai4g_tx_config *cfg)
 extern "C" oai4g_tx_config_t *oai4g_tx_config_create(const oai4g_tx_params_t *p)
 {
   NEED_INIT(nullptr);
-  if (p->N_RB_DL != 6 && p->N_RB_DL != 15 && p->N_RB_DL != 50 && p->N_RB_DL != 100) {
-    set_err("batched path supports N_RB_DL 6, 15, 50, 100 (IDFT 128/256/1024/2048)");
+  if (p->N_RB_DL != 6 && p->N_RB_DL != 15 && p->N_RB_DL != 25 && p->N_RB_DL != 50 && p->N_RB_DL != 100) {
+    set_err("batched path supports N_RB_DL 6, 15, 25, 50, 100 (IDFT 128/256/512/1024/2048)");
     return nullptr;
   }
   oai4g_tx_config *cfg = new oai4g_tx_config();
@@ -1384,7 +1384,7 @@ static int run_ofdm(const int32_t *input, size_t in_n, int32_t *output, size_t o
   return 0;
 }
 
-static bool log2n_ok(int l) { return l == 6 || l == 7 || l == 8 || l == 10 || l == 11; }
+static bool log2n_ok(int l) { return l >= 6 && l <= 11; }
 
 extern "C" void oai4g_PHY_ofdm_mod(const int32_t *input, int32_t *output, uint8_t log2fftsize, uint8_t nb_symbols,
                                    uint16_t nb_prefix_samples, int etype)
@@ -1663,6 +1663,7 @@ extern "C" int oai4g_idft(int log2n, const int16_t *x, int16_t *y, int scale)
 
 extern "C" void oai4g_idft2048(const int16_t *x, int16_t *y, int scale) { oai4g_idft(11, x, y, scale); }
 extern "C" void oai4g_idft1024(const int16_t *x, int16_t *y, int scale) { oai4g_idft(10, x, y, scale); }
+extern "C" void oai4g_idft512(const int16_t *x, int16_t *y, int scale) { oai4g_idft(9, x, y, scale); }
 extern "C" void oai4g_idft256(const int16_t *x, int16_t *y, int scale) { oai4g_idft(8, x, y, scale); }
 extern "C" void oai4g_idft128(const int16_t *x, int16_t *y, int scale) { oai4g_idft(7, x, y, scale); }
 extern "C" void oai4g_idft64(const int16_t *x, int16_t *y, int scale) { oai4g_idft(6, x, y, scale); }

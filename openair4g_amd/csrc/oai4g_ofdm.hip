@@ -128,7 +128,8 @@ __host__ __device__ constexpr int tw_distinct(int T, int SC, int J) { return T >
 template <int LOG2N>
 struct idft_tw_t {
   static constexpr int N = 1 << LOG2N, T = N >> 4;
-  static constexpr bool HAS256 = LOG2N == 8 || LOG2N >= 10, HAS1024 = LOG2N >= 10, HASR2 = LOG2N == 7 || LOG2N == 11;
+  /* final level: radix-2 for odd sizes (idft128/512/2048), radix-4 for idft256/1024 */
+  static constexpr bool HAS256 = LOG2N >= 8, HAS1024 = LOG2N >= 10, HASR2 = (LOG2N & 1) != 0;
   static constexpr int D64 = tw_distinct(T, 16, 4), D256 = tw_distinct(T, 64, 4), D1024 = tw_distinct(T, 256, 4),
                        DR2 = tw_distinct(T, N / 2, 8);
   twp_t l16[7];                         /* W16^{0,1,2,3,4,6,9}: wave-uniform (scalar loads) */
@@ -296,10 +297,11 @@ static __device__ __forceinline__ void idft_unit(uint32_t *lds, int t, bool acti
     }
   } else {
     idft_level_lds<LOG2N, 6, 0, NA>(lds, t, tw.l64);
-    if constexpr (LOG2N >= 10) idft_level_lds<LOG2N, 8, 1, NA>(lds, t, tw.l256);
+    if constexpr (LOG2N >= 9) idft_level_lds<LOG2N, 8, 1, NA>(lds, t, tw.l256);
     if constexpr (LOG2N == 11) idft_level_lds<LOG2N, 10, 1, NA>(lds, t, tw.l1024);
-    if constexpr (LOG2N == 7 || LOG2N == 11) {
-      /* final radix-2 level (idft128 / idft2048): ibfly2 then mulhi scaling */
+    if constexpr ((LOG2N & 1) != 0) {
+      /* final radix-2 level (idft128 / idft512 / idft2048, lte_dfts.c:2058, 2479, 2779): ibfly2 then
+       * mulhi scaling */
       constexpr int SC = N >> 1, DR2 = idft_tw_t<LOG2N>::DR2;
       if (active) {
 #pragma unroll
@@ -568,6 +570,7 @@ hipError_t oai4g_launch_ofdm(const int32_t *d_in, int32_t *d_out, int log2n, int
   case 6: hipLaunchKernelGGL(k_ofdm<6>, grid, blk, 0, s, d_in, d_out, a, d_tw); break;
   case 7: hipLaunchKernelGGL(k_ofdm<7>, grid, blk, 0, s, d_in, d_out, a, d_tw); break;
   case 8: hipLaunchKernelGGL(k_ofdm<8>, grid, blk, 0, s, d_in, d_out, a, d_tw); break;
+  case 9: hipLaunchKernelGGL(k_ofdm<9>, grid, blk, 0, s, d_in, d_out, a, d_tw); break;
   case 10: hipLaunchKernelGGL(k_ofdm<10>, grid, blk, 0, s, d_in, d_out, a, d_tw); break;
   case 11: hipLaunchKernelGGL(k_ofdm<11>, grid, blk, 0, s, d_in, d_out, a, d_tw); break;
   default: return hipErrorInvalidValue;
@@ -661,7 +664,8 @@ static __device__ __forceinline__ void alm_pair(s16x2 ta, s16x2 tb, uint32_t rol
 template <int LOG2N>
 struct modofdm_geom {
   static constexpr int N = 1 << LOG2N, T = N >> 4, UNITS = 128 / T, LDSW = idft_sel<LOG2N>::XW;
-  static constexpr int EW = (6 * ((N * 5) / 8)) / 32 + 4;   /* staged e-bit words per codeword */
+  /* staged e-bit words per codeword: up to 12 N_RB <= 0.71 N data REs (15 PRB in 256) of 6 bits */
+  static constexpr int EW = (6 * ((N * 3) / 4)) / 32 + 4;
 };
 
 #ifndef OAI4G_DIAG_MODOFDM
@@ -953,6 +957,7 @@ hipError_t oai4g_launch_modofdm(const cfg_dev_t *d_cfg, const cfg_dev_t *h_cfg, 
   switch (h_cfg->log2N) {
   case 7: return launch_modofdm_n<7>(d_cfg, h_cfg, sf0, n_items, d_ebits, d_iq, s);
   case 8: return launch_modofdm_n<8>(d_cfg, h_cfg, sf0, n_items, d_ebits, d_iq, s);
+  case 9: return launch_modofdm_n<9>(d_cfg, h_cfg, sf0, n_items, d_ebits, d_iq, s);
   case 10: return launch_modofdm_n<10>(d_cfg, h_cfg, sf0, n_items, d_ebits, d_iq, s);
   case 11: return launch_modofdm_n<11>(d_cfg, h_cfg, sf0, n_items, d_ebits, d_iq, s);
   default: return hipErrorInvalidValue;

@@ -656,6 +656,7 @@ void orc_idft(int log2n, const int16_t *x, int16_t *y, int scale)
   case 6: idft64_c(xc, yc, scale); break;
   case 7: idft_r2(xc, yc, 64, idft64_c, scale); break;
   case 8: idft256_c(xc, yc, scale); break;
+  case 9: idft_r2(xc, yc, 256, idft256_c, scale); break;                      /* idft512 :2479-2564 */
   case 10: idft1024_c(xc, yc, scale); break;
   case 11: idft_r2(xc, yc, 1024, idft1024_c, scale); break;
   default: fprintf(stderr, "orc_idft: size 2^%d not restated\n", log2n); abort();

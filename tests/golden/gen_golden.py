@@ -2,7 +2,7 @@
 """Generate the committed golden fixtures under tests/golden/ (run in the dev container).
 
   idft_ref.npz      inputs and outputs of the REFERENCE's own fixed-point IDFTs
-                    (openair1/PHY/TOOLS/lte_dfts.c idft64/128/256/1024/2048, compiled unmodified
+                    (openair1/PHY/TOOLS/lte_dfts.c idft64/128/256/512/1024/2048, compiled unmodified
                     into oracle/_ref/libref_dfts.so by oracle/Makefile and run here): pins the
                     oracle and the GPU IDFT bit for bit.
   pipeline_C1.npz   oracle transmit vectors for config C1 (1.4 MHz, QPSK): payload bytes,
@@ -41,7 +41,7 @@ def gen_idft():
         raise SystemExit("oracle/_ref/libref_dfts.so missing: run make -C oracle (needs /root/reference)")
     rng = np.random.default_rng(20241015)
     out = {}
-    for log2n in (6, 7, 8, 10, 11):
+    for log2n in (6, 7, 8, 10, 11, 9):   # 9 appended later: earlier vectors unchanged
         n = 1 << log2n
         fn = getattr(ref, f"idft{n}")
         vecs = [rng.integers(-1024, 1024, 2 * n), rng.integers(-32768, 32768, 2 * n),

@@ -19,7 +19,7 @@ def test_gpu_idft_matches_reference_outputs(gpu):
             _, size, vi, scale = key.split("_")
             assert np.array_equal(gpu.idft(z[key], int(scale)), z[f"y_{size}_{vi}_{scale}"]), key
             n += 1
-    assert n == 20
+    assert n == 24
 
 
 def _run_one(gpu, p, pays):

@@ -19,7 +19,7 @@ def _rand_iq(n, amp, rng):
     return x
 
 
-@pytest.mark.parametrize("log2n", [6, 7, 8, 10, 11])
+@pytest.mark.parametrize("log2n", [6, 7, 8, 9, 10, 11])
 def test_idft_bit_exact(gpu, log2n):
     n = 1 << log2n
     rng = np.random.default_rng(log2n)
@@ -33,7 +33,7 @@ def test_idft_bit_exact(gpu, log2n):
             assert np.array_equal(y, O.idft(x, scale)), (log2n, trial, scale)
 
 
-@pytest.mark.parametrize("log2n,cp", [(7, 9), (11, 144), (10, 72), (8, 18)])
+@pytest.mark.parametrize("log2n,cp", [(7, 9), (11, 144), (10, 72), (8, 18), (9, 36)])
 def test_phy_ofdm_mod(gpu, log2n, cp):
     n = 1 << log2n
     nsym = 6
@@ -224,6 +224,18 @@ def test_pipeline_tm2_odd_bandwidth(gpu, nid):
     subframes 0 and 5), every CRS shift class."""
     _pipeline_check(gpu, "TM2S", 10, 0, 1, seed=nid, N_RB_DL=15, rb_alloc=gpu.FULL_ALLOC_15, nb_rb=15,
                     num_pdcch_symbols=2, Nid_cell=nid)
+
+
+@pytest.mark.parametrize("name,N_RB", [("C2", 25), ("C3", 25), ("TM2", 25), ("C2", 50), ("C3", 50), ("TM2", 50),
+                                       ("C3", 15), ("C3", 6)])
+def test_pipeline_bandwidths(gpu, name, N_RB):
+    """5 MHz (25 PRB, idft512, odd N_RB: DC-straddling middle RB), 10 MHz (50 PRB, idft1024) and
+    64-QAM TM3 on 3 / 1.4 MHz grids through the batched path, every subframe of a frame
+    (PBCH/sync exclusions in 0 and 5)."""
+    mcs = gpu.CONFIGS[name]["mcs"]
+    alloc = {6: gpu.FULL_ALLOC_6, 15: gpu.FULL_ALLOC_15, 25: gpu.FULL_ALLOC_25, 50: gpu.FULL_ALLOC_50}[N_RB]
+    _pipeline_check(gpu, name, 10, 0, 1, seed=N_RB, N_RB_DL=N_RB, rb_alloc=alloc, nb_rb=N_RB, num_pdcch_symbols=2,
+                    TBS=tuple(gpu.TBS_TABLE[(m, N_RB)] if m else 0 for m in mcs))
 
 
 def test_pipeline_full_size_c3(gpu):

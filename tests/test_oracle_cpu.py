@@ -37,11 +37,11 @@ def test_idft_matches_reference_fixture():
         y = O.idft(z[key], scale=int(scale))
         assert np.array_equal(y, z[f"y_{n}_{vi}_{scale}"]), key
         n_checked += 1
-    assert n_checked == 20
+    assert n_checked == 24
 
 
 @pytest.mark.skipif(O.ref_dfts() is None, reason="oracle/_ref not built (reference tree absent)")
-@pytest.mark.parametrize("log2n", [6, 7, 8, 10, 11])
+@pytest.mark.parametrize("log2n", [6, 7, 8, 9, 10, 11])
 def test_idft_matches_reference_live(log2n):
     ref = O.ref_dfts()
     n = 1 << log2n
