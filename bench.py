@@ -148,13 +148,16 @@ def main():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--config", default="C3")
-    ap.add_argument("--batch", type=int, default=2048, help="subframes per GPU per step")
+    ap.add_argument("--batch", type=int, default=None,
+                    help="subframes per GPU per step (default 2048; C4: 1024, SURVEY 8d: 8192 over 8 GPUs)")
     ap.add_argument("--subframe", type=int, default=7)
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--kernel-reps", type=int, default=5, help="serial runs timed per kernel for the roofline")
     ap.add_argument("--c5-mode", default="8it", choices=["8it", "snr"], help="C5 decoder inputs")
     args = ap.parse_args()
+    if args.batch is None:
+        args.batch = 1024 if args.config == "C4" else 2048
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -245,7 +248,8 @@ def main():
 
     if rank == 0:
         cfgname = {"C1": "dlsim 1.4 MHz SISO QPSK MCS9", "C2": "dlsim 20 MHz SISO 16-QAM MCS16",
-                   "C3": "dlsim 20 MHz 2x2 TM3 (LARGE_CDD) 64-QAM MCS19x2CW, 2x14 IDFT-2048"}[args.config]
+                   "C3": "dlsim 20 MHz 2x2 TM3 (LARGE_CDD) 64-QAM MCS19x2CW, 2x14 IDFT-2048",
+                   "C4": "20 MHz 4 TX TM3 (4-port large-delay CDD, build-defined) 64-QAM MCS19x2CW, 4x14 IDFT-2048"}[args.config]
         out = {
             "metric": "DL subframes/sec (20 MHz, 2x2, 64-QAM)" if args.config == "C3" else f"DL subframes/sec ({args.config})",
             "value": value,

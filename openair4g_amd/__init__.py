@@ -455,6 +455,10 @@ CONFIGS = {
     # C3: dlsim 20 MHz 2x2 TM3 (LARGE_CDD) 64-QAM, MCS 19 on both codewords (highest the reference encodes)
     "C3": dict(N_RB_DL=100, nb_antennas_tx=2, mode1_flag=0, n_cw=2, mimo_mode=LARGE_CDD, num_pdcch_symbols=1,
                mcs=(19, 19), rb_alloc=FULL_ALLOC_100, nb_rb=100, Kmimo=2),
+    # C4: C3 on 4 TX antennas (build-defined extension: 4-port CRS exclusions, 36.211 6.3.4.2.2
+    # large-delay CDD precoding over the rank-2 codebook entries 12-15)
+    "C4": dict(N_RB_DL=100, nb_antennas_tx=4, mode1_flag=0, n_cw=2, mimo_mode=LARGE_CDD, num_pdcch_symbols=1,
+               mcs=(19, 19), rb_alloc=FULL_ALLOC_100, nb_rb=100, Kmimo=2),
     # TM2: dlsim 20 MHz 2 TX transmit diversity (ALAMOUTI, DCI format 1: one codeword, Nl = 1), 16-QAM
     "TM2": dict(N_RB_DL=100, nb_antennas_tx=2, mode1_flag=0, n_cw=1, mimo_mode=ALAMOUTI, num_pdcch_symbols=1,
                 mcs=(16, 0), rb_alloc=FULL_ALLOC_100, nb_rb=100, Kmimo=1),

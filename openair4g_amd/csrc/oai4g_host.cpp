@@ -73,20 +73,25 @@ static void gold_step_h(uint32_t *x1, uint32_t *x2)
 }
 
 /* lte_gold (LTE_REFSIG/lte_gold.c:52-93): CRS Gold words [ns][pilot l][14] */
-static void lte_gold_table_h(const oai4g_frame_parms_t *fp, uint32_t t[20][2][14])
+/* 14 CRS Gold words of slot ns, symbol lsym of the slot: c_init = 2^10 (7(ns+1) + lsym + 1)
+ * (2 Nid + 1) + 2 Nid + N_CP (lte_gold.c:52-93; lsym = 1 for the port-2/3 extension) */
+static void gold_words_h(const oai4g_frame_parms_t *fp, uint32_t ns, uint32_t lsym, uint32_t w[14])
 {
   const uint32_t Ncp = 1 - fp->Ncp, Nid = fp->Nid_cell;
+  uint32_t x1 = 1u + (1u << 31);
+  uint32_t x2 = Ncp + (Nid << 1) + (((1 + (Nid << 1)) * (1 + lsym + 7 * (1 + ns))) << 10);
+  x2 ^= (x2 ^ (x2 >> 1) ^ (x2 >> 2) ^ (x2 >> 3)) << 31;
+  for (int n = 1; n < 50; n++) gold_step_h(&x1, &x2);
+  for (int n = 0; n < 14; n++) {
+    gold_step_h(&x1, &x2);
+    w[n] = x1 ^ x2;
+  }
+}
+
+static void lte_gold_table_h(const oai4g_frame_parms_t *fp, uint32_t t[20][2][14])
+{
   for (uint32_t ns = 0; ns < 20; ns++)
-    for (uint32_t l = 0; l < 2; l++) {
-      uint32_t x1 = 1u + (1u << 31);
-      uint32_t x2 = Ncp + (Nid << 1) + (((1 + (Nid << 1)) * (1 + (fp->Ncp == 0 ? 4 : 3) * l + 7 * (1 + ns))) << 10);
-      x2 ^= (x2 ^ (x2 >> 1) ^ (x2 >> 2) ^ (x2 >> 3)) << 31;
-      for (int n = 1; n < 50; n++) gold_step_h(&x1, &x2);
-      for (int n = 0; n < 14; n++) {
-        gold_step_h(&x1, &x2);
-        t[ns][l][n] = x1 ^ x2;
-      }
-    }
+    for (uint32_t l = 0; l < 2; l++) gold_words_h(fp, ns, (fp->Ncp == 0 ? 4 : 3) * l, t[ns][l]);
 }
 
 /* CRS pilot RE of port p, pilot l (0: symbol 0 of the slot, 1: symbol 4 / 3), index m
@@ -98,6 +103,14 @@ static uint32_t crs_bin(const oai4g_frame_parms_t *fp, uint32_t p, uint32_t l, u
   if (k > 5) k -= 6;
   k += fp->first_carrier_offset + 6 * m;
   if (k >= fp->ofdm_symbol_size) k = k + 1 - fp->ofdm_symbol_size;     /* DC skip */
+  return k;
+}
+/* CRS RE of port 2/3 (4-TX extension, 36.211 6.10.1.2): symbol 1 of slot ns, nu = 3 (ns mod 2)
+ * for p = 2, 3 + 3 (ns mod 2) for p = 3 */
+static uint32_t crs_bin_p23(const oai4g_frame_parms_t *fp, uint32_t p, uint32_t ns, uint32_t m)
+{
+  uint32_t k = ((p == 2 ? 0u : 3u) + 3u * (ns & 1u) + fp->nushift) % 6u + fp->first_carrier_offset + 6 * m;
+  if (k >= fp->ofdm_symbol_size) k = k + 1 - fp->ofdm_symbol_size;
   return k;
 }
 static uint32_t crs_qpsk(int16_t amp, uint32_t idx)
@@ -448,6 +461,7 @@ static int build_remap(const oai4g_frame_parms_t *fp, const uint32_t *rb_alloc, 
     int pilots;
     if (fp->Ncp == 0) pilots = (l == 4 || l == 11) ? 2 : (l == 7 ? 1 : 0);
     else pilots = (l == 3 || l == 9) ? 2 : (l == 6 ? 1 : 0);
+    if (fp->nb_antennas_tx == 4 && l % (nsymb >> 1) == 1) pilots = 3;   /* port-2/3 CRS (4-TX extension) */
     int re_offset = fp->first_carrier_offset;
     for (int rb = 0; rb < fp->N_RB_DL; rb++) {
       int alloc = rb_bit(rb_alloc, rb), skip_half = 0, skip_dc = 0;
@@ -566,8 +580,12 @@ static int derive_cfg(oai4g_tx_config *cfg, const oai4g_tx_params_t *p, const ui
     set_err("ALAMOUTI requires 2 TX antennas and one codeword (dlsch_modulation.c:362)");
     return -1;
   }
-  if (p->mimo_mode == OAI4G_LARGE_CDD && (p->nb_antennas_tx != 2 || p->n_cw != 2)) {
-    set_err("LARGE_CDD requires 2 TX antennas and 2 codewords (dlsch_modulation.c:551)");
+  if (p->mimo_mode == OAI4G_LARGE_CDD && ((p->nb_antennas_tx != 2 && p->nb_antennas_tx != 4) || p->n_cw != 2)) {
+    set_err("LARGE_CDD requires 2 (dlsch_modulation.c:551) or 4 (C4 extension) TX antennas and 2 codewords");
+    return -1;
+  }
+  if (p->nb_antennas_tx == 4 && p->mimo_mode != OAI4G_LARGE_CDD) {
+    set_err("4 TX antennas: LARGE_CDD only (C4 extension)");
     return -1;
   }
   if (p->payload_stride % 4) { set_err("payload_stride must be a multiple of 4"); return -1; }
@@ -731,7 +749,17 @@ static int derive_cfg(oai4g_tx_config *cfg, const oai4g_tx_params_t *p, const ui
     uint32_t strw = C * 3 * c.stream_words;
     max_stream_words = strw > max_stream_words ? strw : max_stream_words;
     for (int sf = 0; sf < 10; sf++) {
-      int G = oai4g_get_G(&fp, p->nb_rb, p->rb_alloc, (uint8_t)c.Qm, Nl[cw], p->num_pdcch_symbols, 0, (uint8_t)sf);
+      int G;
+      if (fp.nb_antennas_tx == 4) {
+        /* 4-TX extension: the reference's get_G formula knows no port-2/3 CRS; G = the RE map's
+         * PDSCH RE count x Qm (one layer per codeword) */
+        std::vector<uint16_t> tmp((size_t)14 * fp.ofdm_symbol_size);
+        uint32_t sb[14];
+        int n = build_remap(&fp, p->rb_alloc, p->num_pdcch_symbols, sf, p->mimo_mode, tmp.data(), sb, nullptr);
+        G = n < 0 ? -1 : n * (int)c.Qm;
+      } else {
+        G = oai4g_get_G(&fp, p->nb_rb, p->rb_alloc, (uint8_t)c.Qm, Nl[cw], p->num_pdcch_symbols, 0, (uint8_t)sf);
+      }
       if (G <= 0 || G > OAI4G_MAX_CHANNEL_BITS) { set_err("G=%d out of range", G); return -1; }
       c.G[sf] = (uint32_t)G;
       uint32_t Gp = (uint32_t)G / Nl[cw] / c.Qm, GpmodC = Gp % C, off = 0;
@@ -786,12 +814,12 @@ static int derive_cfg(oai4g_tx_config *cfg, const oai4g_tx_params_t *p, const ui
         lte_gold_table_h(&fp, gt);
         const uint32_t sps = fp.Ncp == 0 ? 7 : 6, psym[4] = {0, sps - 3, sps, 2 * sps - 3};   /* l' = 0, 4 (3) per slot */
         const int nports = (fp.nb_antennas_tx > 1 && !fp.mode1_flag) ? 2 : 1;
-        cfg->h_crs.resize((size_t)10 * 4 * 200);
+        cfg->h_crs.resize((size_t)10 * 6 * 200);
         for (uint32_t i = 0; i < 4; i++) {
           const uint32_t Ns = 2 * sf + (i >> 1), l = i & 1;
           for (uint32_t m = 0; m < 2u * fp.N_RB_DL; m++) {
             const uint32_t mp = 110 - fp.N_RB_DL + m;
-            cfg->h_crs[((size_t)sf * 4 + i) * 200 + m] = crs_qpsk(p->amp, (gt[Ns][l][mp >> 4] >> (2 * (mp & 15))) & 3);
+            cfg->h_crs[((size_t)sf * 6 + i) * 200 + m] = crs_qpsk(p->amp, (gt[Ns][l][mp >> 4] >> (2 * (mp & 15))) & 3);
             for (int port = 0; port < nports; port++) {
               uint16_t &code = cfg->h_remap[((size_t)sf * 14 + psym[i]) * N + crs_bin(&fp, port, l, m)];
               if (code != 0xFFFF) { set_err("CRS RE collides with a PDSCH RE"); return -1; }
@@ -799,6 +827,27 @@ static int derive_cfg(oai4g_tx_config *cfg, const oai4g_tx_params_t *p, const ui
             }
           }
         }
+        if (fp.nb_antennas_tx == 4)   /* ports 2/3: pilot entries 4, 5 = symbol 1 of each slot */
+          for (uint32_t s = 0; s < 2; s++) {
+            const uint32_t Ns = 2 * sf + s;
+            uint32_t gw[14];
+            gold_words_h(&fp, Ns, 1, gw);
+            for (uint32_t m = 0; m < 2u * fp.N_RB_DL; m++) {
+              const uint32_t mp = 110 - fp.N_RB_DL + m;
+              cfg->h_crs[((size_t)sf * 6 + 4 + s) * 200 + m] = crs_qpsk(p->amp, (gw[mp >> 4] >> (2 * (mp & 15))) & 3);
+              for (uint32_t port = 2; port < 4; port++) {
+                uint16_t &code = cfg->h_remap[((size_t)sf * 14 + s * sps + 1) * N + crs_bin_p23(&fp, port, Ns, m)];
+                if (code != 0xFFFF) { set_err("CRS RE collides with a PDSCH RE"); return -1; }
+                code = (uint16_t)(OAI4G_CRS_CODE | ((4 + s) << 9) | ((port & 1u) << 8) | m);
+              }
+            }
+          }
+      }
+      /* symbols whose QAM levels use rho_B (CRS-bearing: dlsch_modulation.c:1223-1246) */
+      h.pilmask = 0;
+      for (uint32_t l = 0, hs = h.nsymb >> 1; l < h.nsymb; l++) {
+        const uint32_t ls = l % hs;
+        if (ls == 0 || ls == hs - 3 || (fp.nb_antennas_tx == 4 && ls == 1)) h.pilmask |= 1u << l;
       }
       for (int l = 0; l < 14; l++) {
         uint32_t next = l + 1 < (int)h.nsymb ? h.symbase[sf][l + 1] : (uint32_t)n;

@@ -18,7 +18,8 @@
 #define OAI4G_MAX_CHUNKS 192                /* 6144 / 32 */
 #define OAI4G_MAX_TASKS (OAI4G_MAX_CB * 20)  /* ceil(R/32) + ceil(R/16) tiles per block, R <= 193 */
 #define OAI4G_PIPE_MAX_CHUNKS 16
-#define OAI4G_CRS_CODE 0xE000u               /* remap codes >= this (and != 0xFFFF) are CRS REs */
+#define OAI4G_CRS_CODE 0xE000u               /* remap codes >= this (and != 0xFFFF) are CRS REs:
+                                                CRS_CODE | pilot entry i << 9 | port & 1 << 8 | m */
 #define OAI4G_ENC_CRC_TABLE_WORDS (256 + 256 + 8 * 96 + 6 * 96) /* byte tables A/B + tree multipliers */
 #define OAI4G_GOLD_LANES 256
 #define OAI4G_GOLD_STRIDE 17   /* odd: lanes 17l + k hit distinct LDS banks */
@@ -121,7 +122,9 @@ struct cfg_dev_t {
   const uint16_t *remap_tm;     /* the same codes thread-major: per (sf, l), [t][n] = remap[t + (N/16) n],
                                    so each modofdm thread fetches its 16 codes with two 16-B loads */
   uint32_t with_crs;
-  const uint32_t *crs_tab;      /* [10][4][200] packed CRS IQ of pilot symbol i (l = 0, 4, 7, 11), index m */
+  uint32_t pilmask;             /* bit l: symbol l carries CRS (QAM levels scaled by rho_B) */
+  const uint32_t *crs_tab;      /* [10][6][200] packed CRS IQ of pilot symbol i (l = 0, 4, 7, 11; 1, 8 for
+                                   ports 2/3 with 4 TX antennas), index m */
   const uint32_t *gold_x1;      /* [256]     x1 state after 50+16l word steps */
   const uint32_t *gold_x2j;     /* [256][32] columns of M2^(50+16l) */
   const uint32_t *tw;           /* 2 x OAI4G_TW_TOTAL packed twiddles t, then (-t.im, t.re) */

@@ -587,11 +587,6 @@ static __device__ __forceinline__ int pilots_of(uint32_t l, bool ecp)
   if (ecp) return (l == 3 || l == 9) ? 2 : (l == 6 ? 1 : 0);
   return (l == 4 || l == 11) ? 2 : (l == 7 ? 1 : 0);
 }
-/* CRS-bearing symbols of a subframe (pilots.c:43-168) */
-static __device__ __forceinline__ bool pilots_any(uint32_t l, bool ecp)
-{
-  return ecp ? (l == 0 || l == 3 || l == 6 || l == 9) : (l == 0 || l == 4 || l == 7 || l == 11);
-}
 
 /* QAM symbol from Qm bits b0..b(Qm-1) packed LSB-first in `bits` (dlsch_modulation.c:245-355). */
 static __device__ __forceinline__ s16x2 qam_map(uint32_t bits, uint32_t Qm, const int16_t *tab, int16_t gain)
@@ -655,6 +650,36 @@ static __device__ __forceinline__ void alm_pair(s16x2 ta, s16x2 tb, uint32_t rol
   y1 = role ? (s16x2){ta.x, (short)-ta.y} : tb;
 }
 
+/* 4-port large-delay CDD, rank 2 (configuration C4, a build-defined extension: 36.211 6.3.4.2.2,
+ * y = W(i) D(i) U x(i), W(i) = C_k/sqrt2 over the codebook entries 12..15, k = floor(i/2) mod 4,
+ * D(i) = diag(1, (-1)^i)).  Every entry of 4 W D U is +-1, so each antenna carries +-x0/2 or
+ * +-x1/2 exactly: y_p = floor(c x_q / 2).  Bit (i mod 8) * 4 + p of CDD4_QSEL selects q = 1 and
+ * of CDD4_NEG the sign c = -1 (tests/spec_model.py: cdd4_precode pins the tables to the
+ * Householder codebook). */
+__host__ __device__ constexpr uint32_t cdd4_mask(bool neg)
+{
+  constexpr int8_t M4[4][4][2] = {{{1, 1}, {1, 1}, {1, -1}, {-1, 1}},       /* W_12^{12} x 2 sqrt2 */
+                                  {{1, -1}, {1, 1}, {-1, 1}, {1, 1}},       /* W_13^{13} */
+                                  {{1, 1}, {-1, 1}, {1, 1}, {1, -1}},       /* W_14^{13} */
+                                  {{1, -1}, {-1, 1}, {-1, -1}, {-1, -1}}};  /* W_15^{12} */
+  uint32_t m = 0;
+  for (int i8 = 0; i8 < 8; i8++)
+    for (int p = 0; p < 4; p++) {
+      const int a = M4[i8 >> 1][p][0], b = M4[i8 >> 1][p][1] * ((i8 & 1) ? -1 : 1);
+      if (neg ? a < 0 : a != b) m |= 1u << (i8 * 4 + p);
+    }
+  return m;
+}
+static constexpr uint32_t CDD4_QSEL = cdd4_mask(false), CDD4_NEG = cdd4_mask(true);
+
+/* floor(x/2) or floor(-x/2) per int16 lane: -x/2 rounded down = ~(x >> 1) + (~x & 1) */
+static __device__ __forceinline__ s16x2 half_signed(s16x2 x, bool neg)
+{
+  const s16x2 h = x >> (s16x2){1, 1};
+  const s16x2 nh = u2c(~c2u(h)) + u2c(~c2u(x) & 0x00010001u);
+  return neg ? nh : h;
+}
+
 /* ======================================================================================
  * Fused: packed scrambled e bits -> QAM -> RE map -> precoding -> IDFT -> CP -> IQ.
  * Persistent 128-thread workgroups; a unit of T threads owns one (subframe, symbol) at a time
@@ -679,7 +704,8 @@ struct modofdm_geom {
 #else
 #define MODOFDM_ATTR
 #endif
-/* MODE: 0 = TM1 (one transform stored to every antenna), 1 = ALAMOUTI, 2 = LARGE_CDD */
+/* MODE: 0 = TM1 (one transform stored to every antenna), 1 = ALAMOUTI, 2 = LARGE_CDD, 3 = 4-port
+ * LARGE_CDD (C4: two items per symbol, each transforming one antenna pair) */
 template <int LOG2N, int MODE, bool CRS, bool ECP>
 __global__ void __launch_bounds__(128) MODOFDM_ATTR k_modofdm(const cfg_dev_t *__restrict__ c, int n_items,
                                                  const uint32_t *__restrict__ ebits, int32_t *__restrict__ iq,
@@ -688,7 +714,8 @@ __global__ void __launch_bounds__(128) MODOFDM_ATTR k_modofdm(const cfg_dev_t *_
   using G = modofdm_geom<LOG2N>;
   constexpr int N = G::N, T = G::T, UNITS = G::UNITS, LDSW = G::LDSW, EW = G::EW;
   constexpr int NA = MODE == 0 ? 1 : 2;
-  constexpr bool CW2 = MODE == 2;
+  constexpr bool CW2 = MODE == 2 || MODE == 3;
+  constexpr uint32_t IPS = MODE == 3 ? 2u : 1u;   /* items per (subframe, symbol) */
   __shared__ uint32_t lds_data[UNITS * NA * LDSW];
   __shared__ uint32_t lds_e[UNITS][2][EW];
   __shared__ uint32_t qtab[2][2][64];          /* [cw][pilot symbol][Qm bits] -> packed IQ */
@@ -696,7 +723,6 @@ __global__ void __launch_bounds__(128) MODOFDM_ATTR k_modofdm(const cfg_dev_t *_
   typename idft_sel<LOG2N>::tw_t twr;
   twr.load(c->tw, t);
   const uint32_t n_ant = c->n_ant, nsymb = c->nsymb;
-  constexpr bool ecp = ECP;                        /* extended CP: 6 symbols per slot, one prefix length */
   constexpr uint32_t sps = ECP ? 6 : 7;
   for (uint32_t i = threadIdx.x; i < 256; i += blockDim.x) {
     const uint32_t cw = i >> 7, pil = (i >> 6) & 1, bits = i & 63;
@@ -723,7 +749,7 @@ __global__ void __launch_bounds__(128) MODOFDM_ATTR k_modofdm(const cfg_dev_t *_
   auto fetch = [&](int bse) {
     const int item = bse + unit;
     const bool act = item < n_items;
-    const uint32_t it = act ? (uint32_t)item : 0u;
+    const uint32_t it = (act ? (uint32_t)item : 0u) / IPS;
     const uint32_t sf = it / nsymb, l = it - sf * nsymb;
     const uint32_t sfi = (c->first_sf + (sf0 + sf) * c->sf_step) % 10;
     const uint32_t nre = act ? c->symnre[sfi][l] : 0u, re0 = c->symbase[sfi][l];
@@ -749,22 +775,23 @@ __global__ void __launch_bounds__(128) MODOFDM_ATTR k_modofdm(const cfg_dev_t *_
   for (int base = blockIdx.x * UNITS; base < n_items; base += stride) {
     const int item = base + unit;
     const bool active = item < n_items;
-    const uint32_t it = active ? (uint32_t)item : 0u;
+    const uint32_t it = (active ? (uint32_t)item : 0u) / IPS, pair = (uint32_t)item % IPS;
     const uint32_t sf = it / nsymb, l = it - sf * nsymb;
     const uint32_t sfi = (c->first_sf + (sf0 + sf) * c->sf_step) % 10;
     const uint32_t nre = active ? c->symnre[sfi][l] : 0u, re0 = c->symbase[sfi][l];
-    const uint32_t pil = pilots_of(l, ecp) != 0;
+    const bool crs_sym = (c->pilmask >> l) & 1u;    /* CRS-bearing symbol: rho_B QAM levels */
+    const uint32_t pil = crs_sym ? 1u : 0u;
     /* output placement: slot, symbol-in-slot i */
     const uint32_t slot = l >= sps ? 1u : 0u, si = l - slot * sps;
     const uint32_t body = slot * (c->spt >> 1) + (si == 0 ? c->cp0 : (N + c->cp0) + (si - 1) * (N + c->cp) + c->cp);
     const int cp = (int)(si == 0 ? c->cp0 : c->cp);
     uint32_t *dst0 = (uint32_t *)iq + (size_t)sf * n_ant * c->spt + body;
 
-    if (UNITS == 1 && nre == 0 && !(CRS && pilots_any(l, ecp))) {
+    if (UNITS == 1 && nre == 0 && !(CRS && crs_sym)) {
       /* control-region symbol: the transform of an all-zero grid is zero */
       fetch(base + stride);
       if (active)
-        for (uint32_t a = 0; a < n_ant; a++) {
+        for (uint32_t a = MODE == 3 ? 2 * pair : 0; a < (MODE == 3 ? 2 * pair + 2 : n_ant); a++) {
           uint32_t *d = dst0 + (size_t)a * c->spt - cp;   /* CP start of antenna a */
           for (int f = t; f < N + cp; f += T) d[f] = 0u;
         }
@@ -791,7 +818,7 @@ __global__ void __launch_bounds__(128) MODOFDM_ATTR k_modofdm(const cfg_dev_t *_
     fetch(base + stride);
 
     gu32_t *crs_tab = (gu32_t *)c->crs_tab;
-    const bool crs = CRS && pilots_any(l, ecp);
+    const bool crs = CRS && crs_sym;
     const uint32_t *e0 = lds_e[unit][0], *e1 = lds_e[unit][1];
     const uint32_t *q0 = qtab[0][pil], *q1 = qtab[1][pil];
     /* bit position of data RE idx within the staged words: idx * Qm + (re0 * Qm - 32 wlo) */
@@ -845,6 +872,12 @@ __global__ void __launch_bounds__(128) MODOFDM_ATTR k_modofdm(const cfg_dev_t *_
               const s16x2 x0 = u2c(valid ? v0[n] : 0u);
               if constexpr (MODE == 1) {
                 alm_pair(x0, u2c(valid ? v1[n] : 0u), code[n] & 1u, x[0][g + n], x[1][g + n]);
+              } else if constexpr (MODE == 3) {
+                const s16x2 x1 = u2c(valid ? v1[n] : 0u);
+                const uint32_t sel = ((re0 + (code[n] & 0x7FFFu)) & 7u) * 4u + 2u * pair;   /* (i mod 8, p) */
+#pragma unroll
+                for (int a = 0; a < 2; a++)
+                  x[a][g + n] = half_signed(((CDD4_QSEL >> (sel + a)) & 1u) ? x1 : x0, (CDD4_NEG >> (sel + a)) & 1u);
               } else if constexpr (NA == 2) {
                 const s16x2 x1 = CW2 ? u2c(valid ? v1[n] : 0u) : (s16x2){0, 0};
                 cdd_pair(x0, x1, code[n] >> 15 & 1u, x[0][g + n], x[1][g + n]);
@@ -860,11 +893,11 @@ __global__ void __launch_bounds__(128) MODOFDM_ATTR k_modofdm(const cfg_dev_t *_
               for (int n = 0; n < 16; n++) {
                 const uint32_t cd = (rw[n >> 1] >> (16 * (n & 1))) & 0xFFFFu;
                 const bool pil_re = cd >= OAI4G_CRS_CODE && cd != 0xFFFFu;
-                const uint32_t ci = (cd >> 9) & 3u, m = cd & 0xFFu, port = (cd >> 8) & 1u;
-                const uint32_t pv = pil_re ? crs_tab[(sfi * 4 + ci) * 200 + m] : 0u;
+                const uint32_t ci = (cd >> 9) & 7u, m = cd & 0xFFu, port = ((cd >> 8) & 1u) | (ci >= 4 ? 2u : 0u);
+                const uint32_t pv = pil_re ? crs_tab[(sfi * 6 + ci) * 200 + m] : 0u;
 #pragma unroll
                 for (int a = 0; a < NA; a++)
-                  if (pil_re) x[a][n] = (NA == 1 || (uint32_t)a == port) ? u2c(pv) : (s16x2){0, 0};
+                  if (pil_re) x[a][n] = (NA == 1 || (uint32_t)a + 2 * pair == port) ? u2c(pv) : (s16x2){0, 0};
               }
             }
           }
@@ -884,7 +917,7 @@ __global__ void __launch_bounds__(128) MODOFDM_ATTR k_modofdm(const cfg_dev_t *_
             if (off + T - 1 >= N - CPMAX && tt + off >= N - cp) d[ro - N] = c2u(y);
           };
           if constexpr (NA == 2) {
-            store(dst0 + a * c->spt);
+            store(dst0 + (a + 2 * pair) * c->spt);
           } else {
             for (uint32_t aa = 0; aa < n_ant; aa++) store(dst0 + aa * c->spt);
           }
@@ -926,7 +959,9 @@ static hipError_t launch_modofdm_m(const cfg_dev_t *d_cfg, const cfg_dev_t *h_cf
                                    const uint32_t *d_ebits, int32_t *d_iq, hipStream_t s)
 {
   switch (h_cfg->mimo_mode) {
-  case OAI4G_LARGE_CDD: return launch_modofdm_c<LOG2N, 2, ECP>(d_cfg, h_cfg, sf0, n_items, d_ebits, d_iq, s);
+  case OAI4G_LARGE_CDD:
+    return h_cfg->n_ant == 4 ? launch_modofdm_c<LOG2N, 3, ECP>(d_cfg, h_cfg, sf0, 2 * n_items, d_ebits, d_iq, s)
+                             : launch_modofdm_c<LOG2N, 2, ECP>(d_cfg, h_cfg, sf0, n_items, d_ebits, d_iq, s);
   case OAI4G_ALAMOUTI: return launch_modofdm_c<LOG2N, 1, ECP>(d_cfg, h_cfg, sf0, n_items, d_ebits, d_iq, s);
   default: return launch_modofdm_c<LOG2N, 0, ECP>(d_cfg, h_cfg, sf0, n_items, d_ebits, d_iq, s);
   }
@@ -952,7 +987,8 @@ hipError_t oai4g_launch_modofdm(const cfg_dev_t *d_cfg, const cfg_dev_t *h_cfg, 
   d_iq += (size_t)sf0 * h_cfg->n_ant * h_cfg->spt;
   /* two antenna transforms per unit only when they differ (LARGE_CDD, ALAMOUTI); TM1 stores one
    * n_ant times */
-  if (h_cfg->mimo_mode != OAI4G_SISO && h_cfg->n_ant != 2) return hipErrorInvalidValue;
+  if (h_cfg->mimo_mode != OAI4G_SISO && h_cfg->n_ant != 2 && !(h_cfg->mimo_mode == OAI4G_LARGE_CDD && h_cfg->n_ant == 4))
+    return hipErrorInvalidValue;
   if (h_cfg->mimo_mode == OAI4G_LARGE_CDD && h_cfg->n_cw != 2) return hipErrorInvalidValue;
   switch (h_cfg->log2N) {
   case 7: return launch_modofdm_n<7>(d_cfg, h_cfg, sf0, n_items, d_ebits, d_iq, s);

@@ -377,10 +377,15 @@ static int modulation_impl(int32_t **txdataF, int16_t amp, uint32_t subframe, ui
   int re_allocated = 0;
   int use2nd = fp->mode1_flag == 1;
   int N = fp->ofdm_symbol_size, half = fp->N_RB_DL >> 1;
+  /* 4 TX antennas (configuration C4, a build-defined extension: the reference modulates 1 or 2
+   * ports only): the CRS of ports 2/3 also occupy symbol 1 of each slot (36.211 6.10.1.2), with
+   * the same four REs per RB as ports 0/1 (nu_shift mod 3 + {0, 3, 6, 9}) */
+  const int ports4 = fp->nb_antennas_tx == 4, sps = nsymb >> 1;
   for (int l = num_pdcch_symbols; l < nsymb; l++) {
     int pilots;
     if (fp->Ncp == 0) pilots = (l == 4 || l == 11) ? 2 : (l == 7 ? 1 : 0);
     else pilots = (l == 3 || l == 9) ? 2 : (l == 6 ? 1 : 0);
+    if (ports4 && l % sps == 1) pilots = 3;
     int re_offset = fp->first_carrier_offset;
     uint32_t symbol_offset = (uint32_t)N * (l + grid_sf * nsymb);
     for (int rb = 0; rb < fp->N_RB_DL; rb++) {
@@ -428,6 +433,7 @@ static int modulation_impl(int32_t **txdataF, int16_t amp, uint32_t subframe, ui
           uint32_t tti = symbol_offset + re_off + re;
           if (!not_pilot(pilots, re, fp->nushift, use2nd)) continue;
           re_allocated++;
+          if (!txdataF) continue;                                                /* count only (4-port G) */
           if (cw0->mimo_mode == 0) {                                            /* SISO :245-360 */
             int16_t vr, vi;
             qam_symbol(cw0->e, &jj, Qm0, gain, tab0, &vr, &vi);
@@ -445,6 +451,28 @@ static int modulation_impl(int32_t **txdataF, int16_t amp, uint32_t subframe, ui
             acc16(&txdataF[0][tti], 1, (i0 + i1) >> 1);
             acc16(&txdataF[1][tti], 1, s * ((i0 - i1) >> 1));
             s = -s;
+          } else if (cw0->mimo_mode == 2 && ports4) {
+            /* 4-port large-delay CDD, rank 2 (36.211 6.3.4.2.2): y = W(i) D(i) U x(i) with
+             * U = [[1, 1], [1, -1]]/sqrt2, D(i) = diag(1, (-1)^i), W(i) = C_k/sqrt2 for
+             * k = floor(i/2) mod 4 over the codebook entries 12, 13, 14, 15 (Table 6.3.4.2.3-2,
+             * rank-2 columns {1,2}, {1,3}, {1,3}, {1,2} of W_n = I - 2 u_n u_n^H / u_n^H u_n).
+             * Every entry of 4 W D U is +-1, so y_p = (a_p (x0 + x1) + b_p s (x0 - x1)) / 4 with
+             * i the layer-symbol (allocated RE) index of the subframe; rounded down (arithmetic
+             * shift), accumulated into the int16 grid like the 2-port branch. */
+            static const int8_t M4[4][4][2] = {{{1, 1}, {1, 1}, {1, -1}, {-1, 1}},    /* W_12^{12} */
+                                               {{1, -1}, {1, 1}, {-1, 1}, {1, 1}},    /* W_13^{13} */
+                                               {{1, 1}, {-1, 1}, {1, 1}, {1, -1}},    /* W_14^{13} */
+                                               {{1, -1}, {-1, 1}, {-1, -1}, {-1, -1}}}; /* W_15^{12} */
+            const int i = re_allocated - 1, k = (i >> 1) & 3, sg = (i & 1) ? -1 : 1;
+            int16_t r0, i0, r1, i1;
+            qam_symbol(cw0->e, &jj, Qm0, gain, tab0, &r0, &i0);
+            if (cw1) qam_symbol(cw1->e, &jj2, Qm1, gain, tab1, &r1, &i1);
+            else { r1 = 0; i1 = 0; }
+            for (int p = 0; p < 4; p++) {
+              const int a = M4[k][p][0], b = M4[k][p][1] * sg;
+              acc16(&txdataF[p][tti], 0, (a * (r0 + r1) + b * (r0 - r1)) >> 2);
+              acc16(&txdataF[p][tti], 1, (a * (i0 + i1) + b * (i0 - i1)) >> 2);
+            }
           } else if (cw0->mimo_mode == 1 && fp->nb_antennas_tx == 2) {         /* ALAMOUTI :362-546 */
             /* antenna 0 at n: x0/sqrt2; antenna 1 at n: -conj(x1)/sqrt2 (both symbols from codeword 0) */
             int16_t amp2 = (int16_t)(((int32_t)(pilots ? amp_b : amp_a) * 23170) >> 15);
@@ -496,6 +524,15 @@ static int modulation_impl(int32_t **txdataF, int16_t amp, uint32_t subframe, ui
     }
   }
   return re_allocated;
+}
+
+/* PDSCH REs of a subframe (the allocation loop of dlsch_modulation without writing): G of the
+ * 4-port extension, whose CRS exclusions the reference's get_G formula does not know */
+int orc_count_pdsch_res(const orc_frame_t *fp, const uint32_t rb_alloc[4], uint8_t num_pdcch_symbols, uint32_t subframe)
+{
+  orc_cw_t c = {NULL, 0, 2, 1, {0}};
+  memcpy(c.rb_alloc, rb_alloc, sizeof(c.rb_alloc));
+  return modulation_impl(NULL, 512, subframe, subframe, fp, num_pdcch_symbols, &c, NULL, 8192, 8192);
 }
 
 int orc_modulation(int32_t **txdataF, int16_t amp, uint32_t subframe, const orc_frame_t *fp,
@@ -736,8 +773,34 @@ int orc_lte_dl_cell_spec(int32_t *output, int16_t amp, const orc_frame_t *fp, co
   return 0;
 }
 
+/* CRS of antenna ports 2/3 (4-TX extension; the reference generates ports 0/1 only): 36.211
+ * 6.10.1 with l = 1 in each slot, nu = 3 (ns mod 2) for p = 2 and 3 + 3 (ns mod 2) for p = 3,
+ * c_init = 2^10 (7(ns+1) + l + 1)(2 Nid + 1) + 2 Nid + N_CP as in lte_gold.c:52-93 */
+void orc_cell_spec_p23(int32_t *output, int16_t amp, const orc_frame_t *fp, uint8_t Ns, uint8_t p)
+{
+  uint32_t Ncp = 1 - fp->Ncp, Nid = fp->Nid_cell, x1, words[14];
+  uint32_t x2 = Ncp + (Nid << 1) + (((1 + (Nid << 1)) * (1 + 1 + 7 * (1 + (uint32_t)Ns))) << 10);
+  words[0] = orc_gold_generic(&x1, &x2, 1);
+  for (int n = 1; n < 14; n++) words[n] = orc_gold_generic(&x1, &x2, 0);
+  int16_t a = (int16_t)((amp * 23170) >> 15);
+  uint32_t nu = (p == 2 ? 0u : 3u) + 3u * (Ns & 1u), k = (nu + fp->nushift) % 6 + fp->first_carrier_offset;
+  uint32_t mprime = 110 - fp->N_RB_DL;
+  for (uint32_t m = 0; m < 2u * fp->N_RB_DL; m++, mprime++) {
+    uint32_t c = (words[mprime >> 4] >> (2 * (mprime & 15))) & 3;
+    int16_t *o = (int16_t *)&output[k];
+    o[0] = (c & 1) ? (int16_t)-a : a;
+    o[1] = (c & 2) ? (int16_t)-a : a;
+    k += 6;
+    if (k >= fp->ofdm_symbol_size) {
+      k++;
+      k -= fp->ofdm_symbol_size;
+    }
+  }
+}
+
 /* pilots.c:43-168 for the symbols of one subframe grid: port 0 on antenna 0; antenna 1 gets
- * port 0 too in mode1 (single-port CRS), port 1 otherwise */
+ * port 0 too in mode1 (single-port CRS), port 1 otherwise; with 4 TX antennas ports 2/3 on
+ * antennas 2/3 in symbol 1 of each slot */
 static void pilots_one(int32_t **grid, int16_t amp, const orc_frame_t *fp, const uint32_t table[20][2][14],
                        uint32_t slot_offset)
 {
@@ -748,6 +811,10 @@ static void pilots_one(int32_t **grid, int16_t amp, const orc_frame_t *fp, const
     orc_lte_dl_cell_spec(grid[0] + sym[i] * N, amp, fp, table, Ns, l, 0);
     if (fp->nb_antennas_tx > 1) orc_lte_dl_cell_spec(grid[1] + sym[i] * N, amp, fp, table, Ns, l, fp->mode1_flag ? 0 : 1);
   }
+  if (fp->nb_antennas_tx == 4)
+    for (uint32_t s = 0; s < 2; s++)
+      for (uint8_t p = 2; p < 4; p++)
+        orc_cell_spec_p23(grid[p] + (s * (Nsymb >> 1) + 1) * N, amp, fp, (uint8_t)(slot_offset + s), p);
 }
 
 void orc_generate_pilots(int32_t **txdataF, int16_t amp, const orc_frame_t *fp, uint16_t Ntti)
@@ -756,8 +823,8 @@ void orc_generate_pilots(int32_t **txdataF, int16_t amp, const orc_frame_t *fp, 
   orc_lte_gold_table(fp, table);
   uint32_t Nsymb = fp->Ncp == 0 ? 14 : 12;
   for (uint32_t tti = 0; tti < Ntti; tti++) {
-    int32_t *g[2] = {txdataF[0] + tti * fp->ofdm_symbol_size * Nsymb,
-                     fp->nb_antennas_tx > 1 ? txdataF[1] + tti * fp->ofdm_symbol_size * Nsymb : NULL};
+    int32_t *g[4] = {NULL, NULL, NULL, NULL};
+    for (int aa = 0; aa < fp->nb_antennas_tx && aa < 4; aa++) g[aa] = txdataF[aa] + tti * fp->ofdm_symbol_size * Nsymb;
     pilots_one(g, amp, fp, table, (tti * 2) % 20);
   }
 }
@@ -781,8 +848,10 @@ int orc_tx_subframe(const orc_tx_cfg_t *cfg, uint8_t *payload[2], int32_t **txda
   for (int cw = 0; cw < cfg->n_cw; cw++) {
     uint32_t A = cfg->TBS[cw];
     uint8_t Qm = orc_get_Qm(cfg->mcs[cw]);
-    int G = orc_get_G(fp->N_RB_DL, fp->Ncp, fp->mode1_flag, fp->frame_type, cfg->nb_rb, cfg->rb_alloc, Qm, 1,
-                      cfg->num_pdcch_symbols, cfg->subframe);
+    int G = fp->nb_antennas_tx == 4
+                ? orc_count_pdsch_res(fp, cfg->rb_alloc, cfg->num_pdcch_symbols, cfg->subframe) * Qm
+                : orc_get_G(fp->N_RB_DL, fp->Ncp, fp->mode1_flag, fp->frame_type, cfg->nb_rb, cfg->rb_alloc, Qm, 1,
+                            cfg->num_pdcch_symbols, cfg->subframe);
     e_buf[cw] = calloc((size_t)G + 64, 1);
     uint8_t *a = payload[cw];
     uint32_t crc = orc_crc24a(a, (int)A) >> 8;                              /* dlsch_coding.c:296-300 */

@@ -89,6 +89,9 @@ typedef struct {
   uint8_t Nlayers;
   uint32_t rb_alloc[4];
 } orc_cw_t;
+/* 4-TX extension (configuration C4): PDSCH RE count with the port-2/3 CRS exclusions (G = count x Qm) */
+int orc_count_pdsch_res(const orc_frame_t *fp, const uint32_t rb_alloc[4], uint8_t num_pdcch_symbols, uint32_t subframe);
+void orc_cell_spec_p23(int32_t *output, int16_t amp, const orc_frame_t *fp, uint8_t Ns, uint8_t p);
 int orc_modulation(int32_t **txdataF, int16_t amp, uint32_t subframe, const orc_frame_t *fp,
                    uint8_t num_pdcch_symbols, const orc_cw_t *cw0, const orc_cw_t *cw1,
                    int16_t sqrt_rho_a, int16_t sqrt_rho_b);

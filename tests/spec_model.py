@@ -234,3 +234,91 @@ def alamouti_grid(e, N_RB, N, first_carrier, nushift, npdcch, Qm, amp=512, srho=
             grid[1, m] = (ta[0], _w16(-ta[1]))
     out = (grid[..., 0] & 0xFFFF) | ((grid[..., 1] & 0xFFFF) << 16)
     return out.astype(np.uint32).view(np.int32), pos
+
+
+# ------------------------------------------------------------------ 4-port large-delay CDD (36.211 6.3.4.2.2)
+# Codebook for 4 antenna ports, Table 6.3.4.2.3-2: W_n = I - 2 u_n u_n^H / (u_n^H u_n); the rank-2
+# entry of n = 12, 13, 14, 15 takes the columns {1,2}, {1,3}, {1,3}, {1,2} (scaled by 1/sqrt2).
+U_N = {12: (1, -1, -1, 1), 13: (1, -1, 1, -1), 14: (1, 1, -1, -1), 15: (1, 1, 1, 1)}
+RANK2_COLS = {12: (0, 1), 13: (0, 2), 14: (0, 2), 15: (0, 1)}
+
+
+def householder(n):
+    from fractions import Fraction
+    u = U_N[n]
+    nn = sum(x * x for x in u)
+    return [[Fraction(int(i == j)) - Fraction(2 * u[i] * u[j], nn) for j in range(4)] for i in range(4)]
+
+
+def cdd4_precode(i, x0, x1):
+    """y_p (p = 0..3) of layer-symbol i for complex layers x0, x1 (integer pairs): y = W(i) D(i) U x(i)
+    with U = [[1,1],[1,-1]]/sqrt2, D(i) = diag(1, e^{-j pi i}), W(i) = C_k/sqrt2, C_k the rank-2
+    codebook matrix of index 12 + (floor(i/2) mod 4); the two 1/sqrt2 combine to 1/2.  Exact
+    rational arithmetic, rounded down per component."""
+    import math
+    n = 12 + (i // 2) % 4
+    Wn = householder(n)
+    c0, c1 = RANK2_COLS[n]
+    s = -1 if i % 2 else 1
+    v = [(x0[0] + x1[0], x0[1] + x1[1]), (s * (x0[0] - x1[0]), s * (x0[1] - x1[1]))]   # D U x, times sqrt2
+    out = []
+    for p in range(4):
+        re = (Wn[p][c0] * v[0][0] + Wn[p][c1] * v[1][0]) / 2
+        im = (Wn[p][c0] * v[0][1] + Wn[p][c1] * v[1][1]) / 2
+        out.append((_w16(math.floor(re)), _w16(math.floor(im))))
+    return out
+
+
+def cdd4_grid(e0, e1, N_RB, N, first_carrier, nushift, npdcch, Qm, amp=512, srho=8192):
+    """4-antenna large-delay CDD RE grid of one subframe (2 codewords of one layer each, even
+    N_RB, no PBCH/sync exclusions).  Data REs in frequency-first order skip the CRS of ports 0/1
+    (symbols 0, 4, 7, 11) and 2/3 (symbols 1, 8): nu_shift mod 3 + {0, 3, 6, 9} in each RB.
+    QAM levels as the reference's LARGE_CDD branch: (raw level * amp_rho) >> 15."""
+    ampr = (amp * srho) >> 13
+    raw = QAM16_RAW if Qm == 4 else QAM64_RAW
+    grid = np.zeros((4, 14 * N, 2), dtype=np.int64)
+    v = nushift % 3
+    pos = i = 0
+    for l in range(npdcch, 14):
+        pil = l in (1, 4, 7, 8, 11)
+        for rb in range(N_RB):
+            off = first_carrier + 12 * rb
+            if off >= N:
+                off = off - N + 1
+            for re in range(12):
+                if pil and re in (v, v + 3, v + 6, v + 9):
+                    continue
+                xs = []
+                for e in (e0, e1):
+                    b = [int(x) for x in e[pos:pos + Qm]]
+                    if Qm == 2:
+                        g = (ampr * 23170) >> 15
+                        xs.append((-g if b[0] else g, -g if b[1] else g))
+                    else:
+                        ir, ii = _sym_index(b, Qm)
+                        xs.append(((raw[ir] * ampr) >> 15, (raw[ii] * ampr) >> 15))
+                pos += Qm
+                for p, y in enumerate(cdd4_precode(i, xs[0], xs[1])):
+                    grid[p, l * N + off + re] = y
+                i += 1
+    out = (grid[..., 0] & 0xFFFF) | ((grid[..., 1] & 0xFFFF) << 16)
+    return out.astype(np.uint32).view(np.int32), i
+
+
+def crs_p23(N_RB, Nid, subframe, port, amp, N, first_carrier, Ncp=0):
+    """CRS of antenna port 2 or 3 (36.211 6.10.1.2): symbol l = 1 of each slot, nu = 3 (ns mod 2)
+    (port 2) or 3 + 3 (ns mod 2) (port 3); same sequence rule as crs() with l = 1."""
+    a = (amp * 23170) >> 15
+    out = {}
+    nsymb = 7 if Ncp == 0 else 6
+    for slot in (0, 1):
+        ns = 2 * subframe + slot
+        c_init = (1 << 10) * (7 * (ns + 1) + 1 + 1) * (2 * Nid + 1) + 2 * Nid + (1 - Ncp)
+        c = gold(c_init, 4 * 110)
+        nu = (0 if port == 2 else 3) + 3 * (ns % 2)
+        for m in range(2 * N_RB):
+            mp = m + 110 - N_RB
+            k = 6 * m + (nu + Nid % 6) % 6
+            fbin = first_carrier + k if k < 6 * N_RB else k - 6 * N_RB + 1
+            out[(slot * nsymb + 1, fbin)] = (a * (1 - 2 * c[2 * mp]), a * (1 - 2 * c[2 * mp + 1]))
+    return out

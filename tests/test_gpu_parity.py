@@ -191,7 +191,8 @@ def _pipeline_check(gpu, name, n_sf, first_sf, step, check_idx=None, seed=7, **o
 
 
 @pytest.mark.parametrize("name,n_sf,first,step", [("C1", 10, 0, 1), ("C2", 3, 7, 0), ("C3", 10, 0, 1),
-                                                  ("C2", 10, 3, 1), ("TM2", 10, 0, 1), ("TM2S", 10, 0, 1)])
+                                                  ("C2", 10, 3, 1), ("TM2", 10, 0, 1), ("TM2S", 10, 0, 1),
+                                                  ("C4", 10, 0, 1)])
 def test_pipeline_bit_exact(gpu, name, n_sf, first, step):
     _pipeline_check(gpu, name, n_sf, first, step)
 
@@ -236,6 +237,18 @@ def test_pipeline_bandwidths(gpu, name, N_RB):
     alloc = {6: gpu.FULL_ALLOC_6, 15: gpu.FULL_ALLOC_15, 25: gpu.FULL_ALLOC_25, 50: gpu.FULL_ALLOC_50}[N_RB]
     _pipeline_check(gpu, name, 10, 0, 1, seed=N_RB, N_RB_DL=N_RB, rb_alloc=alloc, nb_rb=N_RB, num_pdcch_symbols=2,
                     TBS=tuple(gpu.TBS_TABLE[(m, N_RB)] if m else 0 for m in mcs))
+
+
+@pytest.mark.parametrize("nid,ncp,crs", [(0, 0, 0), (13, 0, 1), (301, 0, 1), (5, 1, 0), (8, 1, 1)])
+def test_pipeline_c4(gpu, nid, ncp, crs):
+    """C4 (4 TX, 4-port large-delay CDD, build-defined): every subframe of a frame, every CRS
+    shift class, normal / extended CP, with and without the 4-port CRS."""
+    _pipeline_check(gpu, "C4", 10, 0, 1, seed=nid + 1, Nid_cell=nid, Ncp=ncp, with_crs=crs)
+
+
+def test_pipeline_full_size_c4(gpu):
+    """Bench-size C4 batch (1024 subframes per GPU): sampled bit-exact checks."""
+    _pipeline_check(gpu, "C4", 1024, 7, 0, check_idx=[0, 511, 1023], seed=21)
 
 
 def test_pipeline_full_size_c3(gpu):

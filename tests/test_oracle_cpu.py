@@ -9,6 +9,7 @@
     36.212 / 36.211 textbook model in tests/spec_model.py.
   - Whole-subframe regression: the oracle reproduces tests/golden/pipeline_C1.npz.
 """
+import ctypes
 import os
 
 import numpy as np
@@ -200,6 +201,60 @@ def test_alamouti_matches_spec_model(name, mcs, tbs, nid, sf):
                                 p.num_pdcch_symbols, Qm)
     assert used == G
     assert np.array_equal(txF, ref)
+
+
+# ---------------------------------------------------------------- 4 TX antennas (C4, build-defined)
+@pytest.mark.parametrize("mcs,tbs,nid,sf", [(19, 36696, 0, 7), (16, 30576, 4, 3), (9, 15840, 2, 9), (19, 36696, 5, 1)])
+def test_cdd4_matches_spec_model(mcs, tbs, nid, sf):
+    """The oracle's 4-port large-delay CDD (C4) equals 36.211 6.3.4.2.2 computed in exact rational
+    arithmetic from the Householder codebook (W(i) D(i) U, rounded down), with the port-2/3 CRS
+    exclusions in symbols 1 and 8; G = RE count x Qm."""
+    import openair4g_amd as oai
+    p = oai.make_params("C4", subframe=sf, Nid_cell=nid, mcs=(mcs, mcs), TBS=(tbs, tbs))
+    cfg = O.tx_cfg_from_params(p, sf)
+    rng = np.random.default_rng(tbs + nid)
+    pays = [rng.integers(0, 256, tbs // 8 + 8, dtype=np.uint8) for _ in range(2)]
+    _, txF, e = O.tx_subframe(cfg, pays, want_e=True)
+    Qm = 2 if mcs < 10 else (4 if mcs < 17 else 6)
+    fp = cfg.fp
+    n = O.orc().orc_count_pdsch_res(ctypes.byref(fp), (ctypes.c_uint32 * 4)(*p.rb_alloc), 1, sf)
+    assert n == 13 * 1200 - 5 * 400                  # 8 of 12 REs per RB in symbols 1, 4, 7, 8, 11
+    ref, used = S.cdd4_grid(e[0], e[1], p.N_RB_DL, fp.ofdm_symbol_size, fp.first_carrier_offset, nid % 6, 1, Qm)
+    assert used == n
+    assert np.array_equal(txF, ref)
+
+
+@pytest.mark.parametrize("nid,sf", [(0, 7), (7, 0), (301, 4)])
+def test_crs_ports23_matches_spec_model(nid, sf):
+    """CRS of ports 2/3 on antennas 2/3 (4-TX extension) at the 36.211 6.10.1 positions and values."""
+    import openair4g_amd as oai
+    p = oai.make_params("C4", subframe=sf, Nid_cell=nid, with_crs=1)
+    cfg = O.tx_cfg_from_params(p, sf)
+    cfg.num_pdcch_symbols = 3
+    cfg.rb_alloc[0] = cfg.rb_alloc[1] = cfg.rb_alloc[2] = cfg.rb_alloc[3] = 0   # pilots only
+    pays = [np.zeros(p.TBS[0] // 8 + 8, dtype=np.uint8)] * 2
+    N = cfg.fp.ofdm_symbol_size
+    for port in (2, 3):
+        ref = S.crs_p23(p.N_RB_DL, nid, sf, port, 512, N, cfg.fp.first_carrier_offset)
+        for l in (1, 8):
+            row = np.zeros((N, 2), dtype=np.int64)
+            for (ll, k), v in ref.items():
+                if ll == l:
+                    row[k] = v
+            assert len([1 for (ll, _) in ref if ll == l]) == 2 * p.N_RB_DL
+            ref_row = ((row[:, 0] & 0xFFFF) | ((row[:, 1] & 0xFFFF) << 16)).astype(np.uint32).view(np.int32)
+            txF = _tx_grid_pilots(cfg, pays)[port]
+            assert np.array_equal(txF[l * N:(l + 1) * N], ref_row), (port, l)
+
+
+def _tx_grid_pilots(cfg, pays):
+    # rb_alloc 0 makes G = 0: run only the pilot generator through orc_generate_pilots_subframe
+    n_ant = cfg.fp.nb_antennas_tx
+    N = cfg.fp.ofdm_symbol_size
+    txF = [np.zeros(14 * N, dtype=np.int32) for _ in range(n_ant)]
+    ptrs = (ctypes.c_void_p * n_ant)(*[a.ctypes.data for a in txF])
+    O.orc().orc_generate_pilots_subframe(ptrs, ctypes.c_int16(512), ctypes.byref(cfg.fp), cfg.subframe)
+    return txF
 
 
 # ---------------------------------------------------------------- extended cyclic prefix (A13)
