@@ -142,6 +142,82 @@ def bench_c5(args, world, rank, dist, torch):
             "cpu_baseline": cpu}), flush=True)
 
 
+def bench_fep(args, world, rank, dist, torch):
+    """UE receive front end (SURVEY 8f item 3, config "FEP"): slot_fep of every symbol of
+    20 MHz subframes on 2 receive antennas (CP removal + 14 x dft2048 per antenna), batched."""
+    import numpy as np
+    import openair4g_amd as oai
+    oai.init()
+    n_sf, n_ant = args.batch, 2
+    fp = oai.frame_parms(100, nb_antennas_tx=2, mode1_flag=0)
+    N, nsym, spt = fp.ofdm_symbol_size, fp.symbols_per_tti, fp.samples_per_tti
+    rng = np.random.default_rng(0xFE9 + rank)
+    rx = rng.integers(-3000, 3000, (n_sf, n_ant, 2 * spt), dtype=np.int16).view(np.int32)
+    fb = oai.FepBatch(fp, n_sf, n_ant)
+    fb.upload(rx)
+    for _ in range(args.warmup):
+        fb.run()
+    oai.lib().oai4g_sync()
+    if dist is not None:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        fb.run()
+    oai.lib().oai4g_sync()
+    torch.cuda.synchronize()
+    if dist is not None:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if dist is not None:
+        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    fb.close()
+    value = n_sf * args.steps * world / elapsed
+    per_launch_ms = elapsed * 1000.0 / args.steps       # one k_fep launch per step
+    alg = n_sf * n_ant * nsym * N * 4 * 2                # DFT windows read + frequency symbols written
+    ach = alg / (per_launch_ms * 1e-3) / 1e9
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        sys.path.insert(0, os.path.join(ROOT, "tests"))
+        import ctypes
+        import oracle_lib as O
+        from test_fep_cpu import window_start
+        ref = O.ref_dfts()                               # the reference's own lte_dfts.c (oracle/_ref)
+        fpo = O.frame(100, nb_antennas_tx=2, mode1_flag=0)
+        buf = np.zeros(spt + N + 64, np.int32)
+        frame = buf[(-buf.ctypes.data % 64) // 4:][:spt + N]
+        frame[:spt] = rx[0, 0]
+        obuf = np.zeros(nsym * N + 64, np.int32)
+        rxF = obuf[(-obuf.ctypes.data % 64) // 4:][:nsym * N]
+        nsl = nsym // 2
+        wins = [window_start(fpo, l, Ns, 0, 0) for Ns in (0, 1) for l in range(nsl)]   # 16-B aligned at 20 MHz
+        fn = ref.dft2048 if ref is not None else (lambda x, y, s: O.orc().orc_dft(11, x, y, s))
+        n, t1 = 0, time.perf_counter()
+        while time.perf_counter() - t1 < args.cpu_seconds:
+            for a in range(n_ant):
+                for i, st in enumerate(wins):            # slot_fep: dft straight from the rx buffer
+                    fn(ctypes.c_void_p(frame.ctypes.data + 4 * st), ctypes.c_void_p(rxF.ctypes.data + 4 * N * i), 1)
+            n += 1
+        dt = time.perf_counter() - t1
+        cpu = {"value": n / dt, "unit": "subframes/s", "cores": 1, "kind": "reference" if ref is not None else "port",
+               "sample": f"{n} subframes x {n_ant} antennas x {nsym} dft2048 ("
+                         f"{'the reference lte_dfts.c dft2048 built into oracle/_ref' if ref is not None else 'C oracle'}"
+                         f"), single thread, {dt:.1f} s"}
+    if rank == 0:
+        print(json.dumps({
+            "metric": "UE RX front-end subframes/sec (slot_fep, 20 MHz, 2 RX)", "value": value, "unit": "subframes/s",
+            "n_gpus": world, "steps": args.steps, "warmup": args.warmup, "ms_per_step": per_launch_ms,
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "int16",
+            "data": "synthetic int16 IQ, resident in HBM",
+            "config": {"workload": "slot_fep 20 MHz normal CP, 2 RX antennas, 14 x dft2048 per antenna",
+                       "config_id": "FEP", "subframes_per_gpu_per_step": n_sf, "parallelism": f"subframe-sharded x{world}"},
+            "roofline": {"bound": "hbm", "kernel": "k_fep<11>", "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": ach / HBM_PEAK_GBS, "traffic": None},
+            "cpu_baseline": cpu}), flush=True)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -172,8 +248,8 @@ def main():
     else:
         torch.cuda.set_device(0)
 
-    if args.config == "C5":
-        bench_c5(args, world, rank, dist, torch)
+    if args.config in ("C5", "FEP"):
+        (bench_c5 if args.config == "C5" else bench_fep)(args, world, rank, dist, torch)
         if dist is not None:
             dist.destroy_process_group()
         return

@@ -165,6 +165,32 @@ void oai4g_idft256(const int16_t *x, int16_t *y, int scale);
 void oai4g_idft128(const int16_t *x, int16_t *y, int scale);
 void oai4g_idft64(const int16_t *x, int16_t *y, int scale);
 
+/* ---------------- UE receive front end ---------------- */
+/* dft64..dft2048 (PHY/TOOLS/lte_dfts.c:1766, 1957, 2172, 2359, 2574, 2689; decl TOOLS/defs.h):
+ * y = DFT(x), bit-exact fixed point.  oai4g_dft returns 0 or -1. */
+int oai4g_dft(int log2n, const int16_t *x, int16_t *y, int scale);
+void oai4g_dft2048(const int16_t *x, int16_t *y, int scale);
+void oai4g_dft1024(const int16_t *x, int16_t *y, int scale);
+void oai4g_dft512(const int16_t *x, int16_t *y, int scale);
+void oai4g_dft256(const int16_t *x, int16_t *y, int scale);
+void oai4g_dft128(const int16_t *x, int16_t *y, int scale);
+void oai4g_dft64(const int16_t *x, int16_t *y, int scale);
+/* slot_fep's DFT window start (slot_fep.c:55-150) before the % frame_length; -1 for bad l / Ns */
+int64_t oai4g_slot_fep_offset(const oai4g_frame_parms_t *frame_parms, uint8_t l, uint8_t Ns, int sample_offset,
+                              int no_prefix);
+/* slot_fep (PHY/MODULATION/slot_fep.c:40, decl MODULATION/defs.h): the reference passes
+ * PHY_VARS_UE; here its rxdata / rxdataF / frame parameters / antenna count are explicit.
+ * rxdata[aa]: 10 * samples_per_tti + ofdm_symbol_size words (wrap extension, written as the
+ * reference does); rxdataF[aa]: symbols_per_tti * ofdm_symbol_size words.  Returns 0 or -1.
+ * Channel estimation (perfect_ce == 0 branch, :179-222) is not included. */
+int oai4g_slot_fep(int32_t *const *rxdata, int32_t *const *rxdataF, const oai4g_frame_parms_t *frame_parms,
+                   uint8_t nb_antennas_rx, uint8_t l, uint8_t Ns, int sample_offset, int no_prefix);
+/* Batched FEP, device pointers: d_rx [n_sf][n_ant][samples_per_tti] -> d_rxF
+ * [n_sf][n_ant][symbols_per_tti][ofdm_symbol_size] (every symbol of both slots, sample_offset 0).
+ * Asynchronous on `stream` (a hipStream_t, NULL = default). */
+int oai4g_fep_batch(const oai4g_frame_parms_t *frame_parms, int n_sf, int n_ant, const int32_t *d_rx,
+                    int32_t *d_rxF, void *stream);
+
 /* ---------------- uplink turbo decoding ---------------- */
 enum { OAI4G_CRC24_A = 0, OAI4G_CRC24_B = 1 };
 /* phy_threegpplte_turbo_decoder16 (PHY/CODING/3gpplte_turbo_decoder_sse_16bit.c:945, decl

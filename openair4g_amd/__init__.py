@@ -143,6 +143,20 @@ _SIGS = {
     "oai4g_idft256": (None, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int]),
     "oai4g_idft128": (None, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int]),
     "oai4g_idft64": (None, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int]),
+    "oai4g_dft": (ctypes.c_int, [ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int]),
+    "oai4g_dft2048": (None, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int]),
+    "oai4g_dft1024": (None, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int]),
+    "oai4g_dft512": (None, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int]),
+    "oai4g_dft256": (None, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int]),
+    "oai4g_dft128": (None, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int]),
+    "oai4g_dft64": (None, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int]),
+    "oai4g_slot_fep_offset": (ctypes.c_int64, [ctypes.POINTER(FrameParms), ctypes.c_uint8, ctypes.c_uint8,
+                                               ctypes.c_int, ctypes.c_int]),
+    "oai4g_slot_fep": (ctypes.c_int, [ctypes.POINTER(ctypes.c_void_p), ctypes.POINTER(ctypes.c_void_p),
+                                      ctypes.POINTER(FrameParms), ctypes.c_uint8, ctypes.c_uint8, ctypes.c_uint8,
+                                      ctypes.c_int, ctypes.c_int]),
+    "oai4g_fep_batch": (ctypes.c_int, [ctypes.POINTER(FrameParms), ctypes.c_int, ctypes.c_int, ctypes.c_void_p,
+                                       ctypes.c_void_p, ctypes.c_void_p]),
     "oai4g_tx_config_create": (ctypes.c_void_p, [ctypes.POINTER(TxParams)]),
     "oai4g_tx_config_destroy": (None, [ctypes.c_void_p]),
     "oai4g_tx_G": (ctypes.c_uint32, [ctypes.c_void_p, ctypes.c_int, ctypes.c_int]),
@@ -287,6 +301,59 @@ def idft(x, scale=1):
     y = np.zeros_like(x)
     _check(lib().oai4g_idft(int(n).bit_length() - 1, _ptr(x), _ptr(y), scale) == 0)
     return y
+
+
+def dft(x, scale=1):
+    """Forward DFT (lte_dfts.c dft64..dft2048): complex int16 pairs, int16 array of length 2N."""
+    init()
+    x = np.ascontiguousarray(x, dtype=np.int16)
+    n = len(x) // 2
+    y = np.zeros_like(x)
+    _check(lib().oai4g_dft(int(n).bit_length() - 1, _ptr(x), _ptr(y), scale) == 0)
+    return y
+
+
+def slot_fep(rxdata, rxdataF, fp, l, Ns, sample_offset=0, no_prefix=0):
+    """slot_fep drop-in: rxdata / rxdataF are lists (one per RX antenna) of int32 arrays, modified
+    in place (rxdata: 10 subframes + N words of wrap extension).  Returns the entry point's code."""
+    init()
+    n = len(rxdata)
+    rp = (ctypes.c_void_p * n)(*[a.ctypes.data for a in rxdata])
+    fpp = (ctypes.c_void_p * n)(*[a.ctypes.data for a in rxdataF])
+    return lib().oai4g_slot_fep(rp, fpp, ctypes.byref(fp), n, l, Ns, sample_offset, no_prefix)
+
+
+class FepBatch:
+    """Device-resident batched FEP (oai4g_fep_batch): n_sf subframes x n_ant antennas."""
+
+    def __init__(self, fp, n_sf, n_ant):
+        init()
+        self.L = lib()
+        self.fp, self.n_sf, self.n_ant = fp, n_sf, n_ant
+        self.n_in = n_sf * n_ant * fp.samples_per_tti
+        self.n_out = n_sf * n_ant * fp.symbols_per_tti * fp.ofdm_symbol_size
+        self.d_rx = self.L.oai4g_dev_alloc(self.n_in * 4)
+        self.d_rxF = self.L.oai4g_dev_alloc(self.n_out * 4)
+        _check(bool(self.d_rx) and bool(self.d_rxF))
+
+    def upload(self, rx):
+        rx = np.ascontiguousarray(rx, dtype=np.int32)
+        assert rx.size == self.n_in
+        _check(self.L.oai4g_memcpy_h2d(self.d_rx, _ptr(rx), rx.nbytes) == 0)
+
+    def run(self, stream=None):
+        _check(self.L.oai4g_fep_batch(ctypes.byref(self.fp), self.n_sf, self.n_ant, self.d_rx, self.d_rxF,
+                                      stream) == 0)
+
+    def result(self):
+        _check(self.L.oai4g_sync() == 0)
+        out = np.empty((self.n_sf, self.n_ant, self.fp.symbols_per_tti, self.fp.ofdm_symbol_size), dtype=np.int32)
+        _check(self.L.oai4g_memcpy_d2h(_ptr(out), self.d_rxF, out.nbytes) == 0)
+        return out
+
+    def close(self):
+        self.L.oai4g_dev_free(self.d_rx)
+        self.L.oai4g_dev_free(self.d_rxF)
 
 
 def ofdm_mod(grid, log2n, nb_symbols, cp):

@@ -12,7 +12,7 @@ ROOT = os.path.dirname(HERE)
 CSRC = os.path.join(HERE, "csrc")
 LIBDIR = os.path.join(HERE, "lib")
 LIB = os.path.join(LIBDIR, "libopenair4g_amd.so")
-SOURCES = ["oai4g_host.cpp", "oai4g_encode.hip", "oai4g_ofdm.hip", "oai4g_decode.hip"]
+SOURCES = ["oai4g_host.cpp", "oai4g_encode.hip", "oai4g_ofdm.hip", "oai4g_decode.hip", "oai4g_fep.hip"]
 EXTRA = [os.path.join(ROOT, "include", "oai4g_qpp.c")]
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = os.environ.get("OAI4G_ARCH", "gfx950")
@@ -31,7 +31,7 @@ def build_lib(force=False, verbose=False, out=None, defines=()):
     libdir = os.path.dirname(lib)
     os.makedirs(libdir, exist_ok=True)
     srcs = [os.path.join(CSRC, s) for s in SOURCES]
-    deps = srcs + EXTRA + [os.path.join(CSRC, "oai4g_internal.h"), os.path.join(ROOT, "include", "oai4g.h")]
+    deps = srcs + EXTRA + [os.path.join(CSRC, "oai4g_internal.h"), os.path.join(CSRC, "oai4g_dft_prims.h"), os.path.join(ROOT, "include", "oai4g.h")]
     if not force and not _newer(lib, deps):
         return lib
     objs = []

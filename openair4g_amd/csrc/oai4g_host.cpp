@@ -52,7 +52,7 @@ extern "C" const char *oai4g_last_error(void) { return g_err; }
 static pthread_once_t g_once = PTHREAD_ONCE_INIT;
 static int g_init_status = -1;
 static char g_init_err[512] = "";
-static uint32_t *g_tw = nullptr, *g_gx1 = nullptr, *g_gx2j = nullptr;
+static uint32_t *g_tw = nullptr, *g_twf = nullptr, *g_gx1 = nullptr, *g_gx2j = nullptr;
 static int g_n_cu = 256;
 static uint32_t h_gx1[OAI4G_GOLD_LANES], h_gx2j[OAI4G_GOLD_LANES * 32];
 
@@ -62,6 +62,19 @@ static void twiddle_host(int N, int m, int16_t *re, int16_t *im)
   double a = 2.0 * M_PI * (double)m / (double)N;
   *re = (int16_t)floor(32767.0 * cos(a));
   *im = (int16_t)floor(-32767.0 * sin(a));
+}
+
+/* forward DFT operand pair (a, b) with x * W = (dot2(x, a), dot2(x, b)): a = (Wr, -Wi), b = (Wi, Wr)
+ * for cmult (tw1024, tw2048) and the packed_cmult2 tables tw16a/b … tw512a/b; tw256a alone holds
+ * floor(32767 sin) as its second entry (lte_dfts.c:2162 vs :2167) */
+static void dft_twiddle_ab_host(int N, int m, int16_t a[2], int16_t b[2])
+{
+  int16_t wr, wi;
+  twiddle_host(N, m, &wr, &wi);
+  a[0] = wr;
+  a[1] = (N == 256) ? (int16_t)floor(32767.0 * sin(2.0 * M_PI * (double)m / (double)N)) : (int16_t)-wi;
+  b[0] = wi;
+  b[1] = wr;
 }
 
 static void gold_step_h(uint32_t *x1, uint32_t *x2)
@@ -152,6 +165,17 @@ static void do_init(void)
       tw[OAI4G_TW_TOTAL + off + m] = (uint16_t)(int16_t)(-im) | ((uint32_t)(uint16_t)re << 16);
     }
   }
+  std::vector<uint32_t> twf(2 * OAI4G_TW_TOTAL);  /* forward: a, then b */
+  for (int log2s : sizes) {
+    int N = 1 << log2s;
+    uint32_t off = oai4g_tw_offset(log2s);
+    for (int m = 0; m < N; m++) {
+      int16_t a[2], b[2];
+      dft_twiddle_ab_host(N, m, a, b);
+      twf[off + m] = (uint16_t)a[0] | ((uint32_t)(uint16_t)a[1] << 16);
+      twf[OAI4G_TW_TOTAL + off + m] = (uint16_t)b[0] | ((uint32_t)(uint16_t)b[1] << 16);
+    }
+  }
   /* Gold: x1 after 50+S l word steps; x2 step-matrix powers M2^(50+S l) (columns), S = OAI4G_GOLD_STRIDE */
   uint32_t x1 = 1u + (1u << 31), cols[32];
   for (int b = 0; b < 32; b++) cols[b] = 1u << b;
@@ -170,7 +194,9 @@ static void do_init(void)
     h_gx1[l] = x1;
     for (int b = 0; b < 32; b++) h_gx2j[OAI4G_GOLD_LANES * b + l] = cols[b];   /* [b][lane]: coalesced */
   }
-  if (hipMalloc(&g_tw, tw.size() * 4) != hipSuccess || hipMalloc(&g_gx1, sizeof(h_gx1)) != hipSuccess ||
+  if (hipMalloc(&g_tw, tw.size() * 4) != hipSuccess || hipMalloc(&g_twf, twf.size() * 4) != hipSuccess ||
+      hipMemcpy(g_twf, twf.data(), twf.size() * 4, hipMemcpyHostToDevice) != hipSuccess ||
+      hipMalloc(&g_gx1, sizeof(h_gx1)) != hipSuccess ||
       hipMalloc(&g_gx2j, sizeof(h_gx2j)) != hipSuccess ||
       hipMemcpy(g_tw, tw.data(), tw.size() * 4, hipMemcpyHostToDevice) != hipSuccess ||
       hipMemcpy(g_gx1, h_gx1, sizeof(h_gx1), hipMemcpyHostToDevice) != hipSuccess ||
@@ -1716,3 +1742,122 @@ extern "C" void oai4g_idft512(const int16_t *x, int16_t *y, int scale) { oai4g_i
 extern "C" void oai4g_idft256(const int16_t *x, int16_t *y, int scale) { oai4g_idft(8, x, y, scale); }
 extern "C" void oai4g_idft128(const int16_t *x, int16_t *y, int scale) { oai4g_idft(7, x, y, scale); }
 extern "C" void oai4g_idft64(const int16_t *x, int16_t *y, int scale) { oai4g_idft(6, x, y, scale); }
+
+/* ------------------------------------------------------------------------------------------
+ * UE receive front end: forward DFT drop-ins, slot_fep, batched FEP
+ * ---------------------------------------------------------------------------------------- */
+static int run_fep_window(const int32_t *h_in, int32_t *h_out, int log2n, int scale)
+{
+  NEED_INIT(-1);
+  const size_t N = (size_t)1 << log2n;
+  uint8_t *buf = scratch(2 * N * 4 + 256);
+  if (!buf) return -1;
+  int32_t *d_in = (int32_t *)buf, *d_out = (int32_t *)(buf + ((N * 4 + 255) & ~(size_t)255));
+  fep_args_t a;
+  memset(&a, 0, sizeof(a));
+  a.n_units = 1;
+  a.nsym = 1;
+  a.in_stride = a.in_len = (uint32_t)N;
+  a.out_stride = (uint32_t)N;
+  a.scale = scale;
+  HCK(hipMemcpyAsync(d_in, h_in, N * 4, hipMemcpyHostToDevice, g_scr.s), -1);
+  HCK(oai4g_launch_fep(d_in, d_out, log2n, a, g_twf, g_n_cu, g_scr.s), -1);
+  HCK(hipMemcpyAsync(h_out, d_out, N * 4, hipMemcpyDeviceToHost, g_scr.s), -1);
+  HCK(hipStreamSynchronize(g_scr.s), -1);
+  return 0;
+}
+
+extern "C" int oai4g_dft(int log2n, const int16_t *x, int16_t *y, int scale)
+{
+  if (!log2n_ok(log2n)) { set_err("dft: size 2^%d not supported", log2n); return -1; }
+  return run_fep_window((const int32_t *)x, (int32_t *)y, log2n, scale);
+}
+extern "C" void oai4g_dft2048(const int16_t *x, int16_t *y, int scale) { oai4g_dft(11, x, y, scale); }
+extern "C" void oai4g_dft1024(const int16_t *x, int16_t *y, int scale) { oai4g_dft(10, x, y, scale); }
+extern "C" void oai4g_dft512(const int16_t *x, int16_t *y, int scale) { oai4g_dft(9, x, y, scale); }
+extern "C" void oai4g_dft256(const int16_t *x, int16_t *y, int scale) { oai4g_dft(8, x, y, scale); }
+extern "C" void oai4g_dft128(const int16_t *x, int16_t *y, int scale) { oai4g_dft(7, x, y, scale); }
+extern "C" void oai4g_dft64(const int16_t *x, int16_t *y, int scale) { oai4g_dft(6, x, y, scale); }
+
+/* slot_fep's DFT window (slot_fep.c:55-150), unsigned arithmetic as in the reference: returns
+ * rx_offset (before the % frame_length of the read), -1 for a bad l / Ns */
+extern "C" int64_t oai4g_slot_fep_offset(const oai4g_frame_parms_t *fp, uint8_t l, uint8_t Ns, int sample_offset,
+                                         int no_prefix)
+{
+  if (l >= 7 - fp->Ncp) {
+    fprintf(stderr, "slot_fep: l must be between 0 and %d\n", 7 - fp->Ncp);
+    set_err("slot_fep: l must be between 0 and %d", 7 - fp->Ncp);
+    return -1;
+  }
+  if (Ns >= 20) {
+    fprintf(stderr, "slot_fep: Ns must be between 0 and 19\n");
+    set_err("slot_fep: Ns must be between 0 and 19");
+    return -1;
+  }
+  const uint32_t N = fp->ofdm_symbol_size;
+  const uint32_t cp = no_prefix ? 0u : fp->nb_prefix_samples, cp0 = no_prefix ? 0u : fp->nb_prefix_samples0;
+  uint32_t subframe_offset, slot_offset;
+  if (no_prefix) {
+    subframe_offset = N * fp->symbols_per_tti * (Ns >> 1);
+    slot_offset = N * (fp->symbols_per_tti >> 1) * (Ns % 2);
+  } else {
+    subframe_offset = fp->samples_per_tti * (Ns >> 1);
+    slot_offset = (fp->samples_per_tti >> 1) * (Ns % 2);
+  }
+  uint32_t rx_offset = (uint32_t)sample_offset + slot_offset + cp0 + subframe_offset;
+  rx_offset = rx_offset - rx_offset % 4;                     /* "Align with 128 bit" (:118) */
+  if (l > 0) rx_offset += (N + cp) + (N + cp) * (uint32_t)(l - 1);
+  return (int64_t)rx_offset;
+}
+
+/* slot_fep (PHY/MODULATION/slot_fep.c:40, decl MODULATION/defs.h): CP removal + DFT of symbol l of
+ * slot Ns for every receive antenna.  rxdata[aa] holds the frame (10 samples_per_tti) plus
+ * ofdm_symbol_size words of wrap extension, rxdataF[aa] the frequency-domain subframe.  The
+ * channel / frequency-offset estimation that follows in the reference (perfect_ce == 0) is not
+ * part of this entry point. */
+extern "C" int oai4g_slot_fep(int32_t *const *rxdata, int32_t *const *rxdataF, const oai4g_frame_parms_t *fp,
+                              uint8_t nb_antennas_rx, uint8_t l, uint8_t Ns, int sample_offset, int no_prefix)
+{
+  NEED_INIT(-1);
+  const int64_t off = oai4g_slot_fep_offset(fp, l, Ns, sample_offset, no_prefix);
+  if (off < 0) return -1;
+  const uint32_t N = fp->ofdm_symbol_size, fl = fp->samples_per_tti * 10, rx_offset = (uint32_t)off;
+  const uint32_t symbol = l + (7 - fp->Ncp) * (Ns & 1);
+  std::vector<int32_t> win(N);
+  for (int aa = 0; aa < nb_antennas_rx; aa++) {
+    if (rx_offset > fl - N) memcpy(&rxdata[aa][fl], &rxdata[aa][0], N * sizeof(int32_t));   /* :123-126, :153-156 */
+    const uint32_t st = rx_offset % fl;
+    memcpy(win.data(), &rxdata[aa][st], N * sizeof(int32_t));   /* the window the reference's dft reads */
+    if (run_fep_window(win.data(), &rxdataF[aa][N * symbol], fp->log2_symbol_size, 1) != 0) return -1;
+  }
+  return 0;
+}
+
+/* Batched FEP: every symbol of n_sf subframes x n_ant antennas, device pointers
+ *   d_rx  [n_sf][n_ant][samples_per_tti] int32, d_rxF [n_sf][n_ant][symbols_per_tti][N] int32;
+ * each subframe is slot_fep'd (slots 0 and 1, sample_offset 0, with prefix) on its own samples. */
+extern "C" int oai4g_fep_batch(const oai4g_frame_parms_t *fp, int n_sf, int n_ant, const int32_t *d_rx, int32_t *d_rxF,
+                               void *stream)
+{
+  NEED_INIT(-1);
+  if (n_sf < 0 || n_ant <= 0 || !log2n_ok(fp->log2_symbol_size) || fp->symbols_per_tti > OAI4G_FEP_MAX_SYM) {
+    set_err("fep_batch: bad arguments");
+    return -1;
+  }
+  const uint32_t N = fp->ofdm_symbol_size, spt = fp->samples_per_tti, nslot = fp->symbols_per_tti / 2;
+  fep_args_t a;
+  memset(&a, 0, sizeof(a));
+  a.nsym = fp->symbols_per_tti;
+  a.n_units = n_sf * n_ant * a.nsym;
+  a.in_stride = a.in_len = spt;
+  a.out_stride = N * a.nsym;
+  a.scale = 1;
+  for (int sym = 0; sym < a.nsym; sym++) {
+    const int64_t off = oai4g_slot_fep_offset(fp, (uint8_t)(sym % nslot), (uint8_t)(sym / nslot), 0, 0);
+    if (off < 0 || (uint64_t)off + N > spt) { set_err("fep_batch: symbol %d window outside its subframe", sym); return -1; }
+    a.in_off[sym] = (uint32_t)off;
+    a.out_off[sym] = N * (uint32_t)sym;
+  }
+  HCK(oai4g_launch_fep(d_rx, d_rxF, fp->log2_symbol_size, a, g_twf, g_n_cu, (hipStream_t)stream), -1);
+  return 0;
+}

@@ -183,5 +183,17 @@ struct ofdm_sym_t {
 };
 hipError_t oai4g_launch_ofdm(const int32_t *d_in, int32_t *d_out, int log2n, int nsym, const ofdm_sym_t *syms,
                              int scale, const uint32_t *d_tw, hipStream_t s);
+/* UE receive front end (oai4g_fep.hip): per-symbol CP removal + forward DFT */
+#define OAI4G_FEP_MAX_SYM 14
+struct fep_args_t {
+  int n_units;        /* items x nsym */
+  int nsym;           /* symbols per item */
+  uint32_t in_stride, in_len, out_stride;   /* int32 samples */
+  uint32_t in_off[OAI4G_FEP_MAX_SYM];       /* DFT window start of each symbol (< in_len) */
+  uint32_t out_off[OAI4G_FEP_MAX_SYM];      /* output offset of each symbol */
+  int scale;
+};
+hipError_t oai4g_launch_fep(const int32_t *d_in, int32_t *d_out, int log2n, const fep_args_t &a,
+                            const uint32_t *d_twf, int n_cu, hipStream_t s);
 hipError_t oai4g_launch_modulate_bytes(const cfg_dev_t *d_cfg, const cfg_dev_t *h_cfg, int sf,
                                        const uint8_t *d_e0, const uint8_t *d_e1, int32_t *d_grid, hipStream_t s);

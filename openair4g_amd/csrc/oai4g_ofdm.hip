@@ -25,99 +25,7 @@
  */
 #include "oai4g_internal.h"
 
-typedef short s16x2 __attribute__((ext_vector_type(2)));
-typedef const __attribute__((address_space(1))) uint32_t gu32_t;
-typedef const __attribute__((address_space(1))) uint16_t gu16_t;
-typedef uint32_t u32x4_t __attribute__((ext_vector_type(4)));
-typedef const __attribute__((address_space(1))) u32x4_t gu128_t;
-
-static __device__ __forceinline__ s16x2 u2c(uint32_t v) { return __builtin_bit_cast(s16x2, v); }
-static __device__ __forceinline__ uint32_t c2u(s16x2 v) { return __builtin_bit_cast(uint32_t, v); }
-static __device__ __forceinline__ s16x2 cadds(s16x2 a, s16x2 b) { return __builtin_elementwise_add_sat(a, b); }
-static __device__ __forceinline__ s16x2 csubs(s16x2 a, s16x2 b) { return __builtin_elementwise_sub_sat(a, b); }
-static __device__ __forceinline__ s16x2 caddw(s16x2 a, s16x2 b) { return a + b; }
-/* sign_epi16(x,{-1,1}) + pair swap: -j*x with a wrapping negate (lte_dfts.c:1463-1466) */
-static __device__ __forceinline__ s16x2 cflip(s16x2 a) { return (s16x2){a.y, (short)(-(int)a.x)}; }
-/* v_dot2_i32_i16 with an inline-zero accumulator (the compiler otherwise picks the tied
- * v_dot2c form and zeroes its accumulator with an extra v_mov per product) */
-static __device__ __forceinline__ int dot2(s16x2 a, s16x2 b)
-{
-  int r;
-  asm("v_dot2_i32_i16 %0, %1, %2, 0" : "=v"(r) : "v"(a), "v"(b));
-  return r;
-}
-static __device__ __forceinline__ int wadd(int a, int b) { return (int)((unsigned)a + (unsigned)b); }
-static __device__ __forceinline__ int wsub(int a, int b) { return (int)((unsigned)a - (unsigned)b); }
-/* cpack: srai 15 + packs_epi32 (lte_dfts.c:123-131) */
-static __device__ __forceinline__ s16x2 cpack32(int re, int im)
-{
-  return __builtin_bit_cast(s16x2, __builtin_amdgcn_cvt_pk_i16(re >> 15, im >> 15));
-}
-
-/* a twiddle t and its rotated companion (-t.im, t.re) for the imaginary half of x*conj(t) */
-struct twp_t {
-  s16x2 t, tn;
-};
-
-/* x * conj(t), 32-bit (cmultc, lte_dfts.c:132-141) */
-static __device__ __forceinline__ void cmulc32(s16x2 x, const twp_t &w, int &re, int &im)
-{
-  re = dot2(x, w.t);
-  im = dot2(x, w.tn);
-}
-static __device__ __forceinline__ s16x2 cmulc16(s16x2 x, const twp_t &w)
-{
-  int re, im;
-  cmulc32(x, w, re, im);
-  return cpack32(re, im);
-}
-
-/* saturating inverse radix-4 (idft16 stages; ibfly4_16 lte_dfts.c:1049-1090) */
-static __device__ __forceinline__ void r4inv(s16x2 p0, s16x2 p1, s16x2 p2, s16x2 p3, s16x2 &o0, s16x2 &o1,
-                                             s16x2 &o2, s16x2 &o3)
-{
-  s16x2 s02 = cadds(p0, p2), s13 = cadds(p1, p3);
-  o0 = cadds(s02, s13);
-  o2 = csubs(s02, s13);
-  s16x2 d02 = csubs(p0, p2), d13 = csubs(cflip(p1), cflip(p3));
-  o3 = cadds(d02, d13);
-  o1 = csubs(d02, d13);
-}
-
-/* ibfly4 (lte_dfts.c:795-819): 32-bit products, one cpack per output, wrapping add of x0 */
-static __device__ __forceinline__ void ibfly4(s16x2 x0, s16x2 x1, s16x2 x2, s16x2 x3, const twp_t &t1,
-                                              const twp_t &t2, const twp_t &t3, s16x2 &y0, s16x2 &y1, s16x2 &y2,
-                                              s16x2 &y3)
-{
-  int a1r, a1i, a2r, a2i, a3r, a3i;
-  cmulc32(x1, t1, a1r, a1i);
-  cmulc32(x2, t2, a2r, a2i);
-  cmulc32(x3, t3, a3r, a3i);
-  y0 = caddw(x0, cpack32(wadd(a1r, wadd(a2r, a3r)), wadd(a1i, wadd(a2i, a3i))));
-  y3 = caddw(x0, cpack32(wsub(a1i, wadd(a2r, a3i)), wsub(wsub(a3r, a2i), a1r)));
-  y2 = caddw(x0, cpack32(wsub(wsub(a2r, a3r), a1r), wsub(wsub(a2i, a3i), a1i)));
-  y1 = caddw(x0, cpack32(wsub(wsub(a3i, a2r), a1i), wsub(a1r, wadd(a2i, a3r))));
-}
-
-/* ibfly2 (lte_dfts.c:502-527): x0 * 32767 via the same madd as the twiddled operand */
-static __device__ __forceinline__ void ibfly2(s16x2 x0, s16x2 x1, const twp_t &t, s16x2 &y0, s16x2 &y1)
-{
-  int a0r = dot2(x0, (s16x2){32767, 0}), a0i = dot2(x0, (s16x2){0, 32767}), a1r, a1i;
-  cmulc32(x1, t, a1r, a1i);
-  y0 = cpack32(wadd(a0r, a1r), wadd(a0i, a1i));
-  y1 = cpack32(wsub(a0r, a1r), wsub(a0i, a1i));
-}
-
-static __device__ __forceinline__ s16x2 shr3(s16x2 a) { return (s16x2){(short)(a.x >> 3), (short)(a.y >> 3)}; }
-static __device__ __forceinline__ s16x2 shr1(s16x2 a) { return (s16x2){(short)(a.x >> 1), (short)(a.y >> 1)}; }
-/* mulhi_int16(a, 23170) = slli(mulhi_epi16(a, 23170), 1) (lte_dfts.c:1755); |result| <= 23170 */
-static __device__ __forceinline__ s16x2 mulhi2(s16x2 a)
-{
-  int pr = dot2(a, (s16x2){23170, 0}), pi = dot2(a, (s16x2){0, 23170});
-  return (s16x2){(short)((pr >> 16) << 1), (short)((pi >> 16) << 1)};
-}
-
-static __device__ __forceinline__ uint32_t lphys(uint32_t pos) { return pos + (pos >> 5); }
+#include "oai4g_dft_prims.h"
 
 /* ---------------------------------------------------------------------------------------
  * Per-thread twiddle registers.  At a level with quarter size SC a thread's butterfly j

@@ -700,6 +700,202 @@ void orc_idft(int log2n, const int16_t *x, int16_t *y, int scale)
   }
 }
 
+/* ======================================================================================
+ * Forward fixed-point DFT — lte_dfts.c dft16 … dft2048 (the UE receive front end,
+ * slot_fep.c:40-148).  Same DIT decomposition as the inverse, forward butterflies.
+ * ==================================================================================== */
+/* Forward twiddle tables.  "a"/"b" are the packed_cmult2 operand pairs (lte_dfts.c:178-188):
+ * x * W = cpack(madd(x, a), madd(x, b)) with a = (Wr, -Wi), b = (Wi, Wr) where W = orc_twiddle;
+ * tw256a alone rounds its second entry as floor(32767 sin) instead (lte_dfts.c:2162). */
+void orc_dft_twiddle_ab(int N, int m, int16_t a[2], int16_t b[2])
+{
+  int16_t wr, wi;
+  orc_twiddle(N, m, &wr, &wi);
+  a[0] = wr;
+  a[1] = (N == 256) ? (int16_t)floor(32767.0 * sin(2.0 * M_PI * (double)m / (double)N)) : (int16_t)-wi;
+  b[0] = wi;
+  b[1] = wr;
+}
+
+/* packed_cmult2 (:178-188) */
+static inline c16 cmul2_16(c16 x, int N, int m)
+{
+  int16_t a[2], b[2];
+  orc_dft_twiddle_ab(N, m, a, b);
+  return cpack32((int32_t)x.r * a[0] + (int32_t)x.i * a[1], (int32_t)x.r * b[0] + (int32_t)x.i * b[1]);
+}
+
+/* cmult (:106-118): x * t in 32 bits, t from the plain table (tw1024 / tw2048 / W0) */
+static inline void cmul32(c16 x, c16 t, int32_t *re, int32_t *im)
+{
+  *re = (int32_t)x.r * t.r + (int32_t)x.i * (int32_t)wrap16(-(int32_t)t.i);
+  *im = (int32_t)x.r * t.i + (int32_t)x.i * t.r;
+}
+
+/* forward radix-4 on saturating int16 (bfly4_tw1 :860-889, dft16 stages :1453-1500, bfly4_16 :965-1006):
+ * flip = sign(x, {-1,1}) then pair swap = -j x; y1 = x0 - x2 + (f1 - f3), y3 = x0 - x2 - (f1 - f3) */
+static inline void r4fwd(c16 p0, c16 p1, c16 p2, c16 p3, c16 *o0, c16 *o1, c16 *o2, c16 *o3)
+{
+  c16 s02 = cadds(p0, p2), s13 = cadds(p1, p3);
+  *o0 = cadds(s02, s13);
+  *o2 = csubs(s02, s13);
+  c16 f1 = {p1.i, wrap16(-(int32_t)p1.r)}, f3 = {p3.i, wrap16(-(int32_t)p3.r)};
+  c16 d02 = csubs(p0, p2), d13 = csubs(f1, f3);
+  *o1 = cadds(d02, d13);
+  *o3 = csubs(d02, d13);
+}
+
+static void dft16_c(const c16 *x, c16 *y)                                      /* :1431-1500 */
+{
+  c16 S[4][4];
+  for (int j = 0; j < 4; j++) r4fwd(x[j], x[4 + j], x[8 + j], x[12 + j], &S[0][j], &S[1][j], &S[2][j], &S[3][j]);
+  /* unpack transposes: butterfly k of the second stage takes S[k][0..3], input j twiddled by W16^(j k) (tw16a/b) */
+  for (int k = 0; k < 4; k++) {
+    c16 in[4];
+    for (int j = 0; j < 4; j++) in[j] = (j == 0) ? S[k][j] : cmul2_16(S[k][j], 16, j * k);
+    r4fwd(in[0], in[1], in[2], in[3], &y[k], &y[4 + k], &y[8 + k], &y[12 + k]);
+  }
+}
+
+static void dft64_c(const c16 *x, c16 *y, int scale)                           /* :1766-1854 */
+{
+  c16 blk[4][16], Y[4][16];
+  for (int r = 0; r < 4; r++) {
+    for (int n = 0; n < 16; n++) blk[r][n] = x[4 * n + r];
+    dft16_c(blk[r], Y[r]);
+  }
+  for (int k = 0; k < 16; k++)                                                  /* bfly4_16, tw64a/b */
+    r4fwd(Y[0][k], cmul2_16(Y[1][k], 64, k), cmul2_16(Y[2][k], 64, 2 * k), cmul2_16(Y[3][k], 64, 3 * k),
+          &y[k], &y[16 + k], &y[32 + k], &y[48 + k]);
+  if (scale > 0)
+    for (int k = 0; k < 64; k++) { y[k].r >>= 3; y[k].i >>= 3; }
+}
+
+static void dft256_c(const c16 *x, c16 *y, int scale)                          /* :2172-2282 */
+{
+  c16 blk[4][64], Y[4][64];
+  for (int r = 0; r < 4; r++) {
+    for (int n = 0; n < 64; n++) blk[r][n] = x[4 * n + r];
+    dft64_c(blk[r], Y[r], 1);
+  }
+  for (int k = 0; k < 64; k++)                                                  /* bfly4_16, tw256a/b */
+    r4fwd(Y[0][k], cmul2_16(Y[1][k], 256, k), cmul2_16(Y[2][k], 256, 2 * k), cmul2_16(Y[3][k], 256, 3 * k),
+          &y[k], &y[64 + k], &y[128 + k], &y[192 + k]);
+  if (scale > 0)
+    for (int k = 0; k < 256; k++) { y[k].r >>= 1; y[k].i >>= 1; }
+}
+
+/* bfly4 (:709-745): 32-bit products, one cpack per output, wrapping add of x0 */
+static inline void bfly4_c(c16 x0, c16 x1, c16 x2, c16 x3, c16 t1, c16 t2, c16 t3,
+                           c16 *y0, c16 *y1, c16 *y2, c16 *y3)
+{
+  int32_t a1r, a1i, a2r, a2i, a3r, a3i;
+  cmul32(x1, t1, &a1r, &a1i);
+  cmul32(x2, t2, &a2r, &a2i);
+  cmul32(x3, t3, &a3r, &a3i);
+  *y0 = caddw(x0, cpack32(wadd32(a1r, wadd32(a2r, a3r)), wadd32(a1i, wadd32(a2i, a3i))));
+  *y1 = caddw(x0, cpack32(wsub32(a1i, wadd32(a2r, a3i)), wsub32(wsub32(a3r, a2i), a1r)));
+  *y2 = caddw(x0, cpack32(wsub32(wsub32(a2r, a3r), a1r), wsub32(wsub32(a2i, a3i), a1i)));
+  *y3 = caddw(x0, cpack32(wsub32(wsub32(a3i, a2r), a1i), wsub32(a1r, wadd32(a2i, a3r))));
+}
+
+static void dft1024_c(const c16 *x, c16 *y, int scale)                         /* :2574-2628 */
+{
+  c16 *blk = malloc(sizeof(c16) * 1024), *Y = malloc(sizeof(c16) * 1024);
+  for (int r = 0; r < 4; r++) {
+    for (int n = 0; n < 256; n++) blk[r * 256 + n] = x[4 * n + r];
+    dft256_c(blk + r * 256, Y + r * 256, 1);
+  }
+  for (int k = 0; k < 256; k++)
+    bfly4_c(Y[k], Y[256 + k], Y[512 + k], Y[768 + k], tw(1024, k), tw(1024, 2 * k), tw(1024, 3 * k),
+            &y[k], &y[256 + k], &y[512 + k], &y[768 + k]);
+  if (scale > 0)
+    for (int k = 0; k < 1024; k++) { y[k].r >>= 1; y[k].i >>= 1; }
+  free(blk);
+  free(Y);
+}
+
+/* radix-2 levels: bfly2_16 (:471-483, dft128 / dft512) or bfly2 (:396-419, dft2048), then the
+ * mulhi(23170) << 1 scaling (:1755) */
+static void dft_r2(const c16 *x, c16 *y, int M, void (*sub)(const c16 *, c16 *, int), int scale)
+{
+  int N = 2 * M;
+  c16 *blk = malloc(sizeof(c16) * N), *Y = malloc(sizeof(c16) * N);
+  for (int r = 0; r < 2; r++) {
+    for (int n = 0; n < M; n++) blk[r * M + n] = x[2 * n + r];
+    sub(blk + r * M, Y + r * M, 1);
+  }
+  for (int k = 0; k < M; k++) {
+    if (N == 2048) {
+      int32_t a0r, a0i, a1r, a1i;
+      c16 w0 = {32767, 0};
+      cmul32(Y[k], w0, &a0r, &a0i);
+      cmul32(Y[M + k], tw(N, k), &a1r, &a1i);
+      y[k] = cpack32(wadd32(a0r, a1r), wadd32(a0i, a1i));
+      y[M + k] = cpack32(wsub32(a0r, a1r), wsub32(a0i, a1i));
+    } else {
+      c16 t = cmul2_16(Y[M + k], N, k);
+      y[k] = cadds(Y[k], t);
+      y[M + k] = csubs(Y[k], t);
+    }
+  }
+  if (scale > 0)
+    for (int k = 0; k < N; k++) { y[k].r = mulhi_scale(y[k].r); y[k].i = mulhi_scale(y[k].i); }
+  free(blk);
+  free(Y);
+}
+
+void orc_dft(int log2n, const int16_t *x, int16_t *y, int scale)
+{
+  const c16 *xc = (const c16 *)x;
+  c16 *yc = (c16 *)y;
+  switch (log2n) {
+  case 6: dft64_c(xc, yc, scale); break;
+  case 7: dft_r2(xc, yc, 64, dft64_c, scale); break;                           /* dft128 :1957-2056 */
+  case 8: dft256_c(xc, yc, scale); break;
+  case 9: dft_r2(xc, yc, 256, dft256_c, scale); break;                         /* dft512 :2359-2477 */
+  case 10: dft1024_c(xc, yc, scale); break;
+  case 11: dft_r2(xc, yc, 1024, dft1024_c, scale); break;                      /* dft2048 :2689-2777 */
+  default: fprintf(stderr, "orc_dft: size 2^%d not restated\n", log2n); abort();
+  }
+}
+
+/* slot_fep (PHY/MODULATION/slot_fep.c:40-177), DFT part (channel / frequency-offset estimation of
+ * the perfect_ce == 0 branch :179-222 excluded).  rxdata[aa] = frame + N words of wrap extension. */
+int orc_slot_fep(int32_t **rxdata, int32_t **rxdataF, const orc_frame_t *fp, int nb_antennas_rx, uint8_t l,
+                 uint8_t Ns, int sample_offset, int no_prefix)
+{
+  unsigned int N = fp->ofdm_symbol_size;
+  unsigned char symbol = l + ((7 - fp->Ncp) * (Ns & 1));                                  /* :51 */
+  unsigned int nb_prefix_samples = no_prefix ? 0 : fp->nb_prefix_samples;
+  unsigned int nb_prefix_samples0 = no_prefix ? 0 : fp->nb_prefix_samples0;
+  unsigned int subframe_offset, slot_offset, frame_length_samples = fp->samples_per_tti * 10, rx_offset;
+  if (no_prefix) {                                                                         /* :87-93 */
+    subframe_offset = N * fp->symbols_per_tti * (Ns >> 1);
+    slot_offset = N * (fp->symbols_per_tti >> 1) * (Ns % 2);
+  } else {
+    subframe_offset = fp->samples_per_tti * (Ns >> 1);
+    slot_offset = (fp->samples_per_tti >> 1) * (Ns % 2);
+  }
+  if (l >= 7 - fp->Ncp) { printf("slot_fep: l must be between 0 and %d\n", 7 - fp->Ncp); return -1; }
+  if (Ns >= 20) { printf("slot_fep: Ns must be between 0 and 19\n"); return -1; }
+  int32_t tmp[2048];
+  for (int aa = 0; aa < nb_antennas_rx; aa++) {
+    memset(&rxdataF[aa][N * symbol], 0, N * sizeof(int32_t));
+    rx_offset = sample_offset + slot_offset + nb_prefix_samples0 + subframe_offset;       /* :111 */
+    rx_offset = rx_offset - rx_offset % 4;
+    if (l > 0) rx_offset += (N + nb_prefix_samples) + (N + nb_prefix_samples) * (l - 1);   /* :146 */
+    if (rx_offset > (frame_length_samples - N))                                            /* :123, :153 */
+      memcpy(&rxdata[aa][frame_length_samples], &rxdata[aa][0], N * sizeof(int32_t));
+    if (l == 0 && (rx_offset & 3) != 0)        /* :129-133: unreachable after the alignment, restated */
+      memcpy(tmp, &rxdata[aa][(rx_offset - nb_prefix_samples0) % frame_length_samples], N * sizeof(int32_t));
+    else                                       /* :135-139, :163-170 (the misaligned copy reads the same words) */
+      memcpy(tmp, &rxdata[aa][rx_offset % frame_length_samples], N * sizeof(int32_t));
+    orc_dft(fp->log2_symbol_size, (const int16_t *)tmp, (int16_t *)&rxdataF[aa][N * symbol], 1);
+  }
+  return 0;
+}
+
 /* PHY_ofdm_mod, CYCLIC_PREFIX branch (ofdm_mod.c:85-171) */
 void orc_ofdm_mod(const int32_t *input, int32_t *output, uint8_t log2fftsize, uint8_t nb_symbols,
                   uint16_t nb_prefix_samples)

@@ -99,6 +99,11 @@ int orc_modulation(int32_t **txdataF, int16_t amp, uint32_t subframe, const orc_
 /* ---- fixed-point IDFT (lte_dfts.c:1597-2866) and OFDM modulation (ofdm_mod.c:47-229) ---- */
 void orc_idft(int log2n, const int16_t *x, int16_t *y, int scale);
 void orc_twiddle(int N, int m, int16_t *re, int16_t *im);
+void orc_dft(int log2n, const int16_t *x, int16_t *y, int scale);           /* forward dft64 … dft2048 */
+void orc_dft_twiddle_ab(int N, int m, int16_t a[2], int16_t b[2]);
+/* slot_fep DFT part (slot_fep.c:40-177); rxdata[aa] = 10 subframes + N words of wrap extension */
+int orc_slot_fep(int32_t **rxdata, int32_t **rxdataF, const orc_frame_t *fp, int nb_antennas_rx, uint8_t l,
+                 uint8_t Ns, int sample_offset, int no_prefix);
 void orc_ofdm_mod(const int32_t *input, int32_t *output, uint8_t log2fftsize, uint8_t nb_symbols,
                   uint16_t nb_prefix_samples);
 void orc_normal_prefix_mod(const int32_t *txdataF, int32_t *txdata, uint8_t nsymb, const orc_frame_t *fp);

@@ -1,6 +1,10 @@
 #!/usr/bin/env python3
 """Generate the committed golden fixtures under tests/golden/ (run in the dev container).
 
+  dft_ref.npz       inputs and outputs of the REFERENCE's own fixed-point forward DFTs
+                    (lte_dfts.c dft64/128/256/512/1024/2048, same library), and the reference's
+                    forward twiddle tables tw16a/b … tw512a/b, tw1024, tw2048 (data it holds):
+                    pins the oracle's forward DFT and the GPU slot_fep path.
   idft_ref.npz      inputs and outputs of the REFERENCE's own fixed-point IDFTs
                     (openair1/PHY/TOOLS/lte_dfts.c idft64/128/256/512/1024/2048, compiled unmodified
                     into oracle/_ref/libref_dfts.so by oracle/Makefile and run here): pins the
@@ -33,6 +37,35 @@ def aligned_i16(n):
     buf = np.zeros(n + 32, dtype=np.int16)
     off = (-buf.ctypes.data % 64) // 2
     return buf[off:off + n]
+
+
+def gen_dft():
+    ref = O.ref_dfts()
+    if ref is None:
+        raise SystemExit("oracle/_ref/libref_dfts.so missing: run make -C oracle (needs /root/reference)")
+    import ctypes
+    rng = np.random.default_rng(20261016)
+    out = {}
+    for log2n in (6, 7, 8, 9, 10, 11):
+        n = 1 << log2n
+        fn = getattr(ref, f"dft{n}")
+        vecs = [rng.integers(-1024, 1024, 2 * n), rng.integers(-32768, 32768, 2 * n),
+                rng.choice(np.array([-32768, 32767, -20000, 20000]), 2 * n),
+                np.r_[np.full(2, 8000), np.zeros(2 * n - 2, dtype=np.int64)]]
+        for vi, v in enumerate(vecs):
+            for scale in ((0, 1) if vi == 0 else (1,)):
+                x = aligned_i16(2 * n)
+                x[:] = v.astype(np.int16)
+                y = aligned_i16(2 * n)
+                fn(O.P(x), O.P(y), scale)
+                out[f"x_{n}_{vi}_{scale}"] = x.copy()
+                out[f"y_{n}_{vi}_{scale}"] = y.copy()
+    for name, cnt in (("tw16a", 24), ("tw16b", 24), ("tw64a", 96), ("tw64b", 96), ("tw128a", 128), ("tw128b", 128),
+                      ("tw256a", 384), ("tw256b", 384), ("tw512a", 512), ("tw512b", 512), ("tw1024", 1536),
+                      ("tw2048", 2048)):
+        out["table_" + name] = np.ctypeslib.as_array((ctypes.c_int16 * cnt).in_dll(ref, name)).copy()
+    np.savez_compressed(os.path.join(HERE, "dft_ref.npz"), **out)
+    print("dft_ref.npz:", len(out), "arrays")
 
 
 def gen_idft():
@@ -99,5 +132,10 @@ def gen_pipeline():
 
 
 if __name__ == "__main__":
-    gen_idft()
-    gen_pipeline()
+    which = sys.argv[1:] or ["idft", "dft", "pipeline"]
+    if "idft" in which:
+        gen_idft()
+    if "dft" in which:
+        gen_dft()
+    if "pipeline" in which:
+        gen_pipeline()

@@ -69,6 +69,11 @@ def orc():
                                        ctypes.c_uint16]
         L.orc_scramble.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_uint32]
         L.orc_idft.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int]
+        L.orc_dft.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int]
+        L.orc_dft_twiddle_ab.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p]
+        L.orc_slot_fep.argtypes = [ctypes.POINTER(ctypes.c_void_p), ctypes.POINTER(ctypes.c_void_p),
+                                   ctypes.POINTER(OrcFrame), ctypes.c_int, ctypes.c_uint8, ctypes.c_uint8,
+                                   ctypes.c_int, ctypes.c_int]
         L.orc_ofdm_mod.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint8, ctypes.c_uint8, ctypes.c_uint16]
         L.orc_normal_prefix_mod.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint8, ctypes.POINTER(OrcFrame)]
         L.orc_generate_pilots.argtypes = [ctypes.c_void_p, ctypes.c_int16, ctypes.POINTER(OrcFrame), ctypes.c_uint16]
@@ -151,6 +156,28 @@ def idft(x, scale=1):
     y = np.zeros_like(x)
     orc().orc_idft(int(len(x) // 2).bit_length() - 1, P(x), P(y), scale)
     return y
+
+
+def dft(x, scale=1):
+    x = np.ascontiguousarray(x, dtype=np.int16)
+    y = np.zeros_like(x)
+    orc().orc_dft(int(len(x) // 2).bit_length() - 1, P(x), P(y), scale)
+    return y
+
+
+def dft_twiddle_ab(N, m):
+    a = np.zeros(2, np.int16)
+    b = np.zeros(2, np.int16)
+    orc().orc_dft_twiddle_ab(N, m, P(a), P(b))
+    return a, b
+
+
+def slot_fep(rxdata, rxdataF, fp, l, Ns, sample_offset=0, no_prefix=0):
+    """orc_slot_fep on lists of int32 arrays (modified in place); returns its code."""
+    n = len(rxdata)
+    rp = (ctypes.c_void_p * n)(*[a.ctypes.data for a in rxdata])
+    fpp = (ctypes.c_void_p * n)(*[a.ctypes.data for a in rxdataF])
+    return orc().orc_slot_fep(rp, fpp, ctypes.byref(fp), n, l, Ns, sample_offset, no_prefix)
 
 
 def get_G(N_RB_DL, Ncp, mode1_flag, frame_type, nb_rb, rb_alloc, Qm, Nl, num_pdcch, subframe):

@@ -16,3 +16,4 @@ step smoke 300 python -c "import __graft_entry__ as g; g.smoke()"
 step bench_C3 600 python bench.py --steps 20 --warmup 3
 step bench_C4 600 python bench.py --steps 10 --warmup 2 --config C4 --cpu-seconds 5
 step bench_C5 600 python bench.py --steps 5 --warmup 1 --config C5 --cpu-seconds 5
+step bench_FEP 600 python bench.py --steps 20 --warmup 3 --config FEP --cpu-seconds 5
