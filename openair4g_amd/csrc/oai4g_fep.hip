@@ -231,6 +231,145 @@ static __device__ __forceinline__ void dft_unit(uint32_t *la, int t, bool active
 }
 
 /* ======================================================================================
+ * dft2048 in three register passes and two LDS exchanges (T = 128): the data movement of
+ * idft2048_unit (oai4g_ofdm.hip) with the forward butterflies of lte_dfts.c:2689-2777.
+ * Input index n = e + 2 r1 + 8 r2 + 32 r3 + 128 n4, output k = k4 + 16 m3 + 64 m2 + 256 m1 + 1024 m0.
+ *   pass A: thread t = (e, r1, r2, r3) runs leaf t (dft16 over n4) -> L_t[k4];
+ *   pass B: thread u = j + 8 k4 (j = e + 2 r1) runs the 64-level (bfly4_16 over r3, >>3) and the
+ *           256-level (bfly4_16 over r2, >>1) in registers -> out256_j[k2], k2 = k4 + 16 m3 + 64 m2;
+ *   pass C: thread v, k2 in {v, v + 128}: the 1024-level (bfly4 over r1, >>1) and the 2048-level
+ *           (bfly2 over e, mulhi) and the stores.
+ * LDS images as in idft2048_unit (E1: L_t[k4] at k4*144 + 2 (t & 31) + ((t >> 5) & 1) + 64 (t >> 6);
+ * E2: out256_j[k2] at 8 k2 + j + 2 (k2 >> 3), aliasing E1).
+ * ==================================================================================== */
+/* (a, b) from a for every table but tw256a/b: b = (Wi, Wr) = (-a.y, a.x) */
+static __device__ __forceinline__ twp_t fwd_ab(s16x2 a) { return {a, (s16x2){(short)(-(int)a.y), a.x}}; }
+
+struct dft2048_tw_t {
+  static constexpr int X1W = 16 * 144;
+  twp_t l16[7];        /* W16^{0,1,2,3,4,6,9} */
+  s16x2 b64[3];        /* a of W64^{r k4}, k4 = t >> 3 */
+  twp_t b256[4][3];    /* (a, b) of W256^{r (k4 + 16 m3)}: tw256a rounds on its own */
+  s16x2 c1024[2][3];   /* a of W1024^{r k2}, k2 = t + 128 h */
+  s16x2 c2048[8];      /* a of W2048^{k1}, k1 = t + 128 (h + 2 m1) */
+
+  __device__ __forceinline__ void load(const uint32_t *twf, int t)
+  {
+    gu32_t *g = (gu32_t *)twf;
+    constexpr int i16[7] = {0, 1, 2, 3, 4, 6, 9};
+#pragma unroll
+    for (int i = 0; i < 7; i++) l16[i] = dft_tw_t<11>::ab(twf, oai4g_tw_offset(4) + i16[i]);
+    const int k4 = t >> 3;
+#pragma unroll
+    for (int r = 0; r < 3; r++) b64[r] = u2c(g[oai4g_tw_offset(6) + (r + 1) * k4]);
+#pragma unroll
+    for (int m3 = 0; m3 < 4; m3++)
+#pragma unroll
+      for (int r = 0; r < 3; r++) b256[m3][r] = dft_tw_t<11>::ab(twf, oai4g_tw_offset(8) + (r + 1) * (k4 + 16 * m3));
+#pragma unroll
+    for (int h = 0; h < 2; h++)
+#pragma unroll
+      for (int r = 0; r < 3; r++) c1024[h][r] = u2c(g[oai4g_tw_offset(10) + (r + 1) * (t + 128 * h)]);
+#pragma unroll
+    for (int i = 0; i < 8; i++) c2048[i] = u2c(g[oai4g_tw_offset(11) + t + 128 * i]);
+  }
+};
+
+typedef uint32_t u32x2_t __attribute__((ext_vector_type(2)));
+
+template <class Prod, class Cons>
+static __device__ __forceinline__ void dft2048_unit(uint32_t *lds, int t, bool active, const dft2048_tw_t &tw,
+                                                    Prod prod, Cons cons, int scale)
+{
+  s16x2 x[16];
+  /* pass A: leaves */
+  if (active) {
+    prod(x);
+    dft16_reg(x, tw.l16);
+    const uint32_t wo = 2u * (t & 31) + ((t >> 5) & 1) + 64u * (t >> 6);
+#pragma unroll
+    for (int k = 0; k < 16; k++) lds[k * 144 + wo] = c2u(x[k]);
+  }
+  __syncthreads();
+  /* pass B: 64- and 256-levels of the 256-point transform j = t & 7 at k4 = t >> 3 */
+  const int j = t & 7, k4 = t >> 3;
+  if (active) {
+    const uint32_t ro = (uint32_t)k4 * 144u + 2u * j;
+#pragma unroll
+    for (int r2 = 0; r2 < 4; r2++)
+#pragma unroll
+      for (int p = 0; p < 2; p++) {
+        const u32x2_t v = *(const u32x2_t *)&lds[ro + 16 * r2 + 64 * p];
+        x[4 * r2 + 2 * p] = u2c(v.x);
+        x[4 * r2 + 2 * p + 1] = u2c(v.y);
+      }
+  }
+  __syncthreads();   /* E2 aliases E1 */
+  if (active) {
+    const twp_t w64[3] = {fwd_ab(tw.b64[0]), fwd_ab(tw.b64[1]), fwd_ab(tw.b64[2])};
+    s16x2 o[4][4];   /* [r2][m3] */
+#pragma unroll
+    for (int r2 = 0; r2 < 4; r2++) fwd_r4<0, 3>(&x[4 * r2], w64, o[r2], true);
+#pragma unroll
+    for (int m3 = 0; m3 < 4; m3++) {
+      const s16x2 v[4] = {o[0][m3], o[1][m3], o[2][m3], o[3][m3]};
+      s16x2 y[4];
+      fwd_r4<0, 1>(v, tw.b256[m3], y, true);
+#pragma unroll
+      for (int m2 = 0; m2 < 4; m2++) {
+        const uint32_t k2 = (uint32_t)k4 + 16u * m3 + 64u * m2;
+        lds[8u * k2 + j + 2u * (k2 >> 3)] = c2u(y[m2]);
+      }
+    }
+  }
+  __syncthreads();
+  /* pass C: 1024- and 2048-levels for k2 = t + 128 h */
+  if (active) {
+    s16x2 v[2][8];
+#pragma unroll
+    for (int h = 0; h < 2; h++) {
+      const uint32_t k2 = (uint32_t)t + 128u * h;
+      const uint32_t ro = 8u * k2 + 2u * (k2 >> 3);
+#pragma unroll
+      for (int i = 0; i < 4; i++) {
+        const u32x2_t q = *(const u32x2_t *)&lds[ro + 2 * i];
+        v[h][2 * i] = u2c(q.x);
+        v[h][2 * i + 1] = u2c(q.y);
+      }
+    }
+#pragma unroll
+    for (int h = 0; h < 2; h++) {
+      const twp_t w[3] = {fwd_ab(tw.c1024[h][0]), fwd_ab(tw.c1024[h][1]), fwd_ab(tw.c1024[h][2])};
+      s16x2 o[2][4];   /* [e][m1] */
+#pragma unroll
+      for (int e = 0; e < 2; e++) {
+        const s16x2 in[4] = {v[h][e], v[h][e + 2], v[h][e + 4], v[h][e + 6]};
+        fwd_r4<1, 1>(in, w, o[e], true);
+      }
+#pragma unroll
+      for (int m1 = 0; m1 < 4; m1++) {
+        s16x2 y0, y1;
+        bfly2(o[0][m1], o[1][m1], fwd_ab(tw.c2048[h + 2 * m1]), y0, y1);
+        if (scale) { y0 = mulhi2(y0); y1 = mulhi2(y1); }
+        cons(t + 128 * h + 256 * m1, y0);
+        cons(t + 128 * h + 256 * m1 + 1024, y1);
+      }
+    }
+  }
+}
+
+template <int LOG2N>
+struct dft_sel {
+  using tw_t = dft_tw_t<LOG2N>;
+  static constexpr int XW = (1 << LOG2N) + ((1 << LOG2N) >> 5);
+};
+template <>
+struct dft_sel<11> {
+  using tw_t = dft2048_tw_t;
+  static constexpr int XW = dft2048_tw_t::X1W;
+};
+
+/* ======================================================================================
  * k_fep: per-symbol CP removal + forward DFT.  Unit s = item * nsym + sym; item = (subframe,
  * antenna) with input base item * in_stride and output base item * out_stride; the DFT window of
  * symbol sym starts at in_off[sym] and wraps at in_len (the reference's circular frame buffer).
@@ -240,10 +379,10 @@ template <int LOG2N>
 __global__ void __launch_bounds__(128) k_fep(const int32_t *__restrict__ in, int32_t *__restrict__ out,
                                              fep_args_t a, const uint32_t *__restrict__ twf)
 {
-  constexpr int N = 1 << LOG2N, T = N >> 4, UNITS = 128 / T, LDSW = N + (N >> 5);
+  constexpr int N = 1 << LOG2N, T = N >> 4, UNITS = 128 / T, LDSW = dft_sel<LOG2N>::XW;
   __shared__ uint32_t lds_all[UNITS * LDSW];
   const int unit = threadIdx.x / T, t = threadIdx.x % T;
-  dft_tw_t<LOG2N> twr;
+  typename dft_sel<LOG2N>::tw_t twr;
   twr.load(twf, t);
   uint32_t *la = lds_all + unit * LDSW;
   for (int s0 = blockIdx.x * UNITS; s0 < a.n_units; s0 += gridDim.x * UNITS) {
@@ -253,17 +392,17 @@ __global__ void __launch_bounds__(128) k_fep(const int32_t *__restrict__ in, int
     gu32_t *src = (gu32_t *)in + (size_t)item * a.in_stride;
     uint32_t *dst = (uint32_t *)out + (size_t)item * a.out_stride + a.out_off[sym];
     const uint32_t off = a.in_off[sym], len = a.in_len;
-    dft_unit<LOG2N>(
-        la, t, active, twr,
-        [&](s16x2 *x) {
+    auto prod = [&](s16x2 *x) {
 #pragma unroll
-          for (int n = 0; n < 16; n++) {
-            uint32_t i = off + (uint32_t)(t + T * n);
-            i = (i >= len) ? i - len : i;
-            x[n] = u2c(src[i]);
-          }
-        },
-        [&](int f, s16x2 y) { dst[f] = c2u(y); }, a.scale);
+      for (int n = 0; n < 16; n++) {
+        uint32_t i = off + (uint32_t)(t + T * n);
+        i = (i >= len) ? i - len : i;
+        x[n] = u2c(src[i]);
+      }
+    };
+    auto cons = [&](int f, s16x2 y) { dst[f] = c2u(y); };
+    if constexpr (LOG2N == 11) dft2048_unit(la, t, active, twr, prod, cons, a.scale);
+    else dft_unit<LOG2N>(la, t, active, twr, prod, cons, a.scale);
     __syncthreads();   /* the next round's leaf stores reuse la */
   }
 }
