@@ -40,7 +40,7 @@ static __device__ __forceinline__ td_blk_t td_layout(uint8_t *base, uint32_t K)
 {
   td_blk_t b;
   short *p = (short *)base;
-  const uint32_t n16 = (K + 8 * TD_SEG + 16 + 7) & ~7u, n128 = K + 128;   /* segment read-ahead slack */
+  const uint32_t n16 = (K + 16 * TD_SEG + 16 + 7) & ~7u, n128 = K + 128;   /* chunk read-ahead slack (2 TD_SEG steps) */
   b.s0 = p; p += n16;
   b.s1 = p; p += n16;
   b.s2 = p; p += n16;
@@ -54,7 +54,7 @@ static __device__ __forceinline__ td_blk_t td_layout(uint8_t *base, uint32_t K)
 
 size_t oai4g_td_block_bytes(uint32_t K)
 {
-  const size_t n16 = (K + 8 * TD_SEG + 16 + 7) & ~7u, n128 = K + 128;
+  const size_t n16 = (K + 16 * TD_SEG + 16 + 7) & ~7u, n128 = K + 128;
   return (((5 * n16 + 2 * n128) * 2 + 15) & ~(size_t)15) + (size_t)(K / 8 + 1) * 8 * 16 + 256;
 }
 
@@ -162,20 +162,39 @@ template <bool POST>
 static __device__ __attribute__((noinline)) void log_map(const short *sys, const short *par, short *ext, uint4 *A, uint32_t K,
                                                uint32_t q, int tf, uint4 *asave /* [6][64] */, const short *s0)
 {
-  auto put = [&](uint32_t e, short v) {
-    if constexpr (POST) v = __builtin_elementwise_add_sat(__builtin_elementwise_sub_sat(v, sys[e]), s0[e]);
-    ext[e] = v;
-  };
+  /* Every global operand of a step is loaded one chunk ahead into registers: the loads are
+   * independent of the recursions, but the compiler cannot hoist them across the (possibly
+   * aliasing) ext / checkpoint stores, so without this each step waits a full memory latency. */
   const uint32_t K1 = K >> 3, nseg = (K1 + TD_SEG - 1) / TD_SEG, lane = threadIdx.x & 63;
   uint4 *A5 = A + 8 * (nseg + 1);             /* first-run alpha(5) */
   short g11, g10;
-  /* forward, first run */
+  /* forward, first run, in chunks of FS steps (operands of the next chunk in flight) */
+  constexpr int FS = 2 * TD_SEG;
+  const uint32_t nfc = (K1 + FS - 1) / FS;
   tm_t a = tm_init(q == 0);
-  for (uint32_t k = 0; k < K1; k++) {
-    gamma_of(sys, par, 8 * k + q, g11, g10);
-    alpha_step(a, g11, g10);
-    if (k + 1 == 5) A5[q] = tm_pack(a);
-    if (((k + 1) & (TD_SEG - 1)) == 0) A[8 * ((k + 1) / TD_SEG) + q] = tm_pack(a);
+  {
+    s2v nsp[FS];                                /* (sys, par) of the next chunk */
+#pragma unroll
+    for (int j = 0; j < FS; j++) nsp[j] = (s2v){sys[8 * j + q], par[8 * j + q]};
+    for (uint32_t c = 0; c < nfc; c++) {
+      s2v csp[FS];
+#pragma unroll
+      for (int j = 0; j < FS; j++) csp[j] = nsp[j];
+      if (c + 1 < nfc) {
+        const uint32_t b = 8 * FS * (c + 1) + q;
+#pragma unroll
+        for (int j = 0; j < FS; j++) nsp[j] = (s2v){sys[b + 8 * j], par[b + 8 * j]};
+      }
+#pragma unroll
+      for (int j = 0; j < FS; j++) {
+        const uint32_t k = c * FS + j;
+        if (k < K1) {
+          alpha_step(a, (short)(sadd(csp[j].x, csp[j].y) >> 1), (short)(ssub(csp[j].x, csp[j].y) >> 1));
+          if (k + 1 == 5) A5[q] = tm_pack(a);
+          if (((k + 1) & (TD_SEG - 1)) == 0) A[8 * ((k + 1) / TD_SEG) + q] = tm_pack(a);
+        }
+      }
+    }
   }
   /* forward re-run over L/8 steps from the previous window's final alpha; its alpha(0) is
    * checkpoint 0, alpha(1..5) are recomputed from it */
@@ -214,24 +233,47 @@ static __device__ __attribute__((noinline)) void log_map(const short *sys, const
   }
   /* backward, first run: seeded with the lane's own final alpha as the reference stores it
    * after the re-run (the re-run reaches step K1 when K1 == 5); extrinsic of steps whose beta
-   * the re-run does not touch */
+   * the re-run does not touch.  Segment operands (sys, par, s0, checkpoint) one segment ahead. */
   tm_t b = q == 7 ? t : (K1 == 5 ? a : fin);
   const int kr = (int)K1 - 6;                 /* steps >= kr take their extrinsic from the re-run */
+  const uint4 a5v = A5[q];
+  s2v nsp[TD_SEG], nzz[TD_SEG / 2];            /* (sys, par) and (POST) s0 pairs of the next segment */
+  uint4 nA;
+  auto fetch = [&](int seg) {
+    const uint32_t b0 = 8u * (uint32_t)(seg * TD_SEG) + q;
+#pragma unroll
+    for (int j = 0; j < TD_SEG; j++) nsp[j] = (s2v){sys[b0 + 8 * j], par[b0 + 8 * j]};
+    if constexpr (POST) {
+#pragma unroll
+      for (int i = 0; i < TD_SEG / 2; i++) nzz[i] = (s2v){s0[b0 + 16 * i], s0[b0 + 16 * i + 8]};
+    }
+    nA = A[8 * seg + q];
+  };
+  fetch((int)nseg - 1);
   for (int seg = (int)nseg - 1; seg >= 0; seg--) {
     const int k0 = seg * TD_SEG, n = min((int)TD_SEG, (int)K1 - k0);
     /* a partial last segment reads padding past K1 (the arrays have TD_SEG steps of slack) and
      * leaves beta untouched for those steps */
-    const short *sp = sys + 8 * k0 + q, *pp = par + 8 * k0 + q;
+    s2v css[TD_SEG / 2], czz[TD_SEG / 2];      /* sys and s0 of the segment's steps, pairwise */
     uint4 al[TD_SEG];
     uint32_t gg[TD_SEG];                       /* g11 | g10 << 16 */
-    tm_t c = tm_unpack(A[8 * seg + q]);
+    tm_t c = tm_unpack(nA);
 #pragma unroll
     for (int j = 0; j < TD_SEG; j++) {
-      short x11, x10;
-      gamma_of(sp, pp, 8 * j, x11, x10);
+      const short x11 = (short)(sadd(nsp[j].x, nsp[j].y) >> 1), x10 = (short)(ssub(nsp[j].x, nsp[j].y) >> 1);
       gg[j] = (uint16_t)x11 | ((uint32_t)(uint16_t)x10 << 16);
+    }
+#pragma unroll
+    for (int i = 0; i < TD_SEG / 2; i++) {
+      css[i] = (s2v){nsp[2 * i].x, nsp[2 * i + 1].x};
+      czz[i] = nzz[i];
+    }
+    if (seg > 0) fetch(seg - 1);
+#pragma unroll
+    for (int j = 0; j < TD_SEG; j++) {
+      const short x11 = (short)gg[j], x10 = (short)(gg[j] >> 16);
       al[j] = tm_pack(c);
-      if (k0 + j == 5) c = tm_unpack(A5[q]);            /* alpha(6) continues the first run */
+      if (k0 + j == 5) c = tm_unpack(a5v);               /* alpha(6) continues the first run */
       alpha_step(c, x11, x10);
     }
 #pragma unroll
@@ -239,8 +281,16 @@ static __device__ __attribute__((noinline)) void log_map(const short *sys, const
       const int k = k0 + j;
       const short x11 = (short)gg[j], x10 = (short)(gg[j] >> 16);
       if (j < n) {
-        if (k < kr) put(8 * k + q, ext_of(tm_unpack(al[j]), b, x11, x10));
-        else asave[(k - kr) * 64 + lane] = al[j];
+        if (k < kr) {
+          short v = ext_of(tm_unpack(al[j]), b, x11, x10);
+          if constexpr (POST) {
+            const short sv = (j & 1) ? css[j >> 1].y : css[j >> 1].x, zv = (j & 1) ? czz[j >> 1].y : czz[j >> 1].x;
+            v = __builtin_elementwise_add_sat(__builtin_elementwise_sub_sat(v, sv), zv);
+          }
+          ext[8 * k + q] = v;
+        } else {
+          asave[(k - kr) * 64 + lane] = al[j];
+        }
       }
       tm_t nb = b;
       beta_step(nb, x11, x10);
@@ -255,8 +305,11 @@ static __device__ __attribute__((noinline)) void log_map(const short *sys, const
     b.v[v] = q == 7 ? t.v[v] : __builtin_bit_cast(s2v, dn);
   }
   for (int k = (int)K1 - 1; k >= kr && k >= 0; k--) {
-    gamma_of(sys, par, 8 * k + q, g11, g10);
-    put(8 * k + q, ext_of(tm_unpack(asave[(k - kr) * 64 + lane]), b, g11, g10));
+    const uint32_t e = 8 * k + q;
+    gamma_of(sys, par, e, g11, g10);
+    short v = ext_of(tm_unpack(asave[(k - kr) * 64 + lane]), b, g11, g10);
+    if constexpr (POST) v = __builtin_elementwise_add_sat(__builtin_elementwise_sub_sat(v, sys[e]), s0[e]);
+    ext[e] = v;
     if (k >= (int)K1 - 5) beta_step(b, g11, g10);
   }
 }
