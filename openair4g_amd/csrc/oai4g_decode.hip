@@ -372,23 +372,60 @@ __global__ void __launch_bounds__(64) k_td16(int n_cb, uint32_t K, const int16_t
   __syncthreads();
   uint32_t it = 0;
   for (it = 1; it <= max_it; it++) {
-    if (active)
-      for (uint32_t v = 0; v < K1; v++) B.s2[8 * v + q] = B.ext[pi4[8 * v + q]];
+    if (active)   /* interleave (pi4): 8 steps per round, all index loads then all gathers in flight */
+      for (uint32_t v0 = 0; v0 < K1; v0 += 8) {
+        uint32_t ix[8];
+        short val[8];
+#pragma unroll
+        for (int u = 0; u < 8; u++) ix[u] = v0 + u < K1 ? pi4[8 * (v0 + u) + q] : 0u;
+#pragma unroll
+        for (int u = 0; u < 8; u++) val[u] = B.ext[ix[u]];
+#pragma unroll
+        for (int u = 0; u < 8; u++)
+          if (v0 + u < K1) B.s2[8 * (v0 + u) + q] = val[u];
+      }
     __syncthreads();
     if (active) log_map<false>(B.s2, B.yp2, B.ext2, B.A, K, q, 1, asave, B.s0);
     __syncthreads();
     if (active) {
-      for (uint32_t v = 0; v < K1; v++) {
-        const uint32_t i = 8 * v + q;
-        B.s1[i] = sadd(ssub(B.ext2[pi5[i]], B.ext[i]), B.s0[i]);
+      for (uint32_t v0 = 0; v0 < K1; v0 += 8) {   /* deinterleave (pi5) + update, batched likewise */
+        uint32_t ix[8];
+        short e2[8], e1[8], z[8];
+#pragma unroll
+        for (int u = 0; u < 8; u++) {
+          const uint32_t i = v0 + u < K1 ? 8 * (v0 + u) + q : q;
+          ix[u] = pi5[i];
+          e1[u] = B.ext[i];
+          z[u] = B.s0[i];
+        }
+#pragma unroll
+        for (int u = 0; u < 8; u++) e2[u] = B.ext2[ix[u]];
+#pragma unroll
+        for (int u = 0; u < 8; u++)
+          if (v0 + u < K1) B.s1[8 * (v0 + u) + q] = sadd(ssub(e2[u], e1[u]), z[u]);
       }
       if (it > 1)
-        for (uint32_t i = q; i < Kb; i += 8) {   /* hard decisions (:1267-1283), MSB first */
-          uint32_t byte = 0;
+        for (uint32_t i0 = q; i0 < Kb; i0 += 16) {   /* hard decisions (:1267-1283), MSB first, 2 bytes per round */
+          uint32_t ix[16];
+          short x[16];
 #pragma unroll
-          for (int bb = 0; bb < 8; bb++) byte |= (uint32_t)(B.ext2[pi6[8 * i + bb]] > 0) << (7 - bb);
-          dec[g][i] = (uint8_t)byte;
-          out[(size_t)cb * out_stride + i] = (uint8_t)byte;
+          for (int u = 0; u < 16; u++) {
+            const uint32_t i = i0 + 8 * (u >> 3);
+            ix[u] = i < Kb ? pi6[8 * i + (u & 7)] : 0u;
+          }
+#pragma unroll
+          for (int u = 0; u < 16; u++) x[u] = B.ext2[ix[u]];
+#pragma unroll
+          for (int h = 0; h < 2; h++) {
+            const uint32_t i = i0 + 8 * h;
+            uint32_t byte = 0;
+#pragma unroll
+            for (int bb = 0; bb < 8; bb++) byte |= (uint32_t)(x[8 * h + bb] > 0) << (7 - bb);
+            if (i < Kb) {
+              dec[g][i] = (uint8_t)byte;
+              out[(size_t)cb * out_stride + i] = (uint8_t)byte;
+            }
+          }
         }
     }
     __syncthreads();
