@@ -349,11 +349,23 @@ __global__ void __launch_bounds__(64) k_td16(int n_cb, uint32_t K, const int16_t
   if (valid) {
     /* demux (:1038-1158): bit i = window q, step v -> element 8v + q */
     gs16_t *y = (gs16_t *)(llr + (size_t)cb * llr_stride);
-    for (uint32_t v = 0; v < K1; v++) {
-      const uint32_t i = q * K1 + v, j = 8 * v + q;
-      B.s0[j] = y[3 * i];
-      B.yp1[j] = y[3 * i + 1];
-      B.yp2[j] = y[3 * i + 2];
+    for (uint32_t v0 = 0; v0 < K1; v0 += 8) {   /* 8 steps per round: all loads, then all stores */
+      short t0[8], t1[8], t2[8];
+#pragma unroll
+      for (int u = 0; u < 8; u++) {
+        const uint32_t i = q * K1 + (v0 + u < K1 ? v0 + u : K1 - 1);
+        t0[u] = y[3 * i];
+        t1[u] = y[3 * i + 1];
+        t2[u] = y[3 * i + 2];
+      }
+#pragma unroll
+      for (int u = 0; u < 8; u++)
+        if (v0 + u < K1) {
+          const uint32_t j = 8 * (v0 + u) + q;
+          B.s0[j] = t0[u];
+          B.yp1[j] = t1[u];
+          B.yp2[j] = t2[u];
+        }
     }
     if (q == 0) {
       for (uint32_t i = 0; i < 3; i++) {   /* tails (:1164-1186) */
