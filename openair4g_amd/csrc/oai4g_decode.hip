@@ -27,6 +27,9 @@ static __device__ __forceinline__ short sadd(short a, short b) { return __builti
 static __device__ __forceinline__ short ssub(short a, short b) { return __builtin_elementwise_sub_sat(a, b); }
 
 #define TD_MAXH 128    /* MAX / 2 */
+#ifndef TD_XR
+#define TD_XR 32      /* steps per round of the exchange gathers (index loads, then gathers, in flight) */
+#endif
 #ifndef TD_SEG
 #define TD_SEG 8      /* alpha checkpoint interval (steps); measured best of 2/4/8/16 at C5 */
 #endif
@@ -384,51 +387,51 @@ __global__ void __launch_bounds__(64) k_td16(int n_cb, uint32_t K, const int16_t
   __syncthreads();
   uint32_t it = 0;
   for (it = 1; it <= max_it; it++) {
-    if (active)   /* interleave (pi4): 8 steps per round, all index loads then all gathers in flight */
-      for (uint32_t v0 = 0; v0 < K1; v0 += 8) {
-        uint32_t ix[8];
-        short val[8];
+    if (active)   /* interleave (pi4): TD_XR steps per round, all index loads then all gathers in flight */
+      for (uint32_t v0 = 0; v0 < K1; v0 += TD_XR) {
+        uint32_t ix[TD_XR];
+        short val[TD_XR];
 #pragma unroll
-        for (int u = 0; u < 8; u++) ix[u] = v0 + u < K1 ? pi4[8 * (v0 + u) + q] : 0u;
+        for (int u = 0; u < TD_XR; u++) ix[u] = v0 + u < K1 ? pi4[8 * (v0 + u) + q] : 0u;
 #pragma unroll
-        for (int u = 0; u < 8; u++) val[u] = B.ext[ix[u]];
+        for (int u = 0; u < TD_XR; u++) val[u] = B.ext[ix[u]];
 #pragma unroll
-        for (int u = 0; u < 8; u++)
+        for (int u = 0; u < TD_XR; u++)
           if (v0 + u < K1) B.s2[8 * (v0 + u) + q] = val[u];
       }
     __syncthreads();
     if (active) log_map<false>(B.s2, B.yp2, B.ext2, B.A, K, q, 1, asave, B.s0);
     __syncthreads();
     if (active) {
-      for (uint32_t v0 = 0; v0 < K1; v0 += 8) {   /* deinterleave (pi5) + update, batched likewise */
-        uint32_t ix[8];
-        short e2[8], e1[8], z[8];
+      for (uint32_t v0 = 0; v0 < K1; v0 += TD_XR) {   /* deinterleave (pi5) + update, batched likewise */
+        uint32_t ix[TD_XR];
+        short e2[TD_XR], e1[TD_XR], z[TD_XR];
 #pragma unroll
-        for (int u = 0; u < 8; u++) {
+        for (int u = 0; u < TD_XR; u++) {
           const uint32_t i = v0 + u < K1 ? 8 * (v0 + u) + q : q;
           ix[u] = pi5[i];
           e1[u] = B.ext[i];
           z[u] = B.s0[i];
         }
 #pragma unroll
-        for (int u = 0; u < 8; u++) e2[u] = B.ext2[ix[u]];
+        for (int u = 0; u < TD_XR; u++) e2[u] = B.ext2[ix[u]];
 #pragma unroll
-        for (int u = 0; u < 8; u++)
+        for (int u = 0; u < TD_XR; u++)
           if (v0 + u < K1) B.s1[8 * (v0 + u) + q] = sadd(ssub(e2[u], e1[u]), z[u]);
       }
       if (it > 1)
-        for (uint32_t i0 = q; i0 < Kb; i0 += 16) {   /* hard decisions (:1267-1283), MSB first, 2 bytes per round */
-          uint32_t ix[16];
-          short x[16];
+        for (uint32_t i0 = q; i0 < Kb; i0 += 8 * (TD_XR / 8)) {   /* hard decisions (:1267-1283), MSB first */
+          uint32_t ix[TD_XR];
+          short x[TD_XR];
 #pragma unroll
-          for (int u = 0; u < 16; u++) {
+          for (int u = 0; u < TD_XR; u++) {
             const uint32_t i = i0 + 8 * (u >> 3);
             ix[u] = i < Kb ? pi6[8 * i + (u & 7)] : 0u;
           }
 #pragma unroll
-          for (int u = 0; u < 16; u++) x[u] = B.ext2[ix[u]];
+          for (int u = 0; u < TD_XR; u++) x[u] = B.ext2[ix[u]];
 #pragma unroll
-          for (int h = 0; h < 2; h++) {
+          for (int h = 0; h < TD_XR / 8; h++) {
             const uint32_t i = i0 + 8 * h;
             uint32_t byte = 0;
 #pragma unroll
