@@ -34,23 +34,27 @@ static __device__ __forceinline__ short ssub(short a, short b) { return __builti
 #define TD_SEG 8      /* alpha checkpoint interval (steps); measured best of 2/4/8/16 at C5 */
 #endif
 
-struct td_blk_t {      /* one block's scratch (int16 element offsets, see td_layout) */
+struct td_blk_t {      /* one wave's scratch: the 8 blocks interleaved, element i of block g at
+                          64 (i >> 3) + 8 g + (i & 7), so a step's loads / stores of the whole
+                          wave touch one 128-byte line instead of 8 */
   short *s0, *s1, *s2, *yp1, *yp2, *ext, *ext2;
-  uint4 *A;            /* alpha checkpoints: [ceil(K1/16) + 2][8 lanes] x 8 states (16 B) */
+  uint4 *A;            /* alpha checkpoints: [ceil(K1/TD_SEG) + 2][8 blocks][8 lanes] x 8 states (16 B) */
 };
+
+static __device__ __forceinline__ uint32_t td_ix(uint32_t i) { return ((i >> 3) << 6) | (i & 7); }
 
 static __device__ __forceinline__ td_blk_t td_layout(uint8_t *base, uint32_t K)
 {
   td_blk_t b;
   short *p = (short *)base;
   const uint32_t n16 = (K + 16 * TD_SEG + 16 + 7) & ~7u, n128 = K + 128;   /* chunk read-ahead slack (2 TD_SEG steps) */
-  b.s0 = p; p += n16;
-  b.s1 = p; p += n16;
-  b.s2 = p; p += n16;
-  b.yp1 = p; p += n16;
-  b.yp2 = p; p += n16;
-  b.ext = p; p += n128;
-  b.ext2 = p; p += n128;
+  b.s0 = p; p += 8 * n16;
+  b.s1 = p; p += 8 * n16;
+  b.s2 = p; p += 8 * n16;
+  b.yp1 = p; p += 8 * n16;
+  b.yp2 = p; p += 8 * n16;
+  b.ext = p; p += 8 * n128;
+  b.ext2 = p; p += 8 * n128;
   b.A = (uint4 *)(((uintptr_t)p + 15) & ~(uintptr_t)15);
   return b;
 }
@@ -169,7 +173,7 @@ static __device__ __attribute__((noinline)) void log_map(const short *sys, const
    * independent of the recursions, but the compiler cannot hoist them across the (possibly
    * aliasing) ext / checkpoint stores, so without this each step waits a full memory latency. */
   const uint32_t K1 = K >> 3, nseg = (K1 + TD_SEG - 1) / TD_SEG, lane = threadIdx.x & 63;
-  uint4 *A5 = A + 8 * (nseg + 1);             /* first-run alpha(5) */
+  uint4 *A5 = A + 64 * (nseg + 1);             /* first-run alpha(5) */
   short g11, g10;
   /* forward, first run, in chunks of FS steps (operands of the next chunk in flight) */
   constexpr int FS = 2 * TD_SEG;
@@ -178,15 +182,15 @@ static __device__ __attribute__((noinline)) void log_map(const short *sys, const
   {
     s2v nsp[FS];                                /* (sys, par) of the next chunk */
 #pragma unroll
-    for (int j = 0; j < FS; j++) nsp[j] = (s2v){sys[8 * j + q], par[8 * j + q]};
+    for (int j = 0; j < FS; j++) nsp[j] = (s2v){sys[64 * j + q], par[64 * j + q]};
     for (uint32_t c = 0; c < nfc; c++) {
       s2v csp[FS];
 #pragma unroll
       for (int j = 0; j < FS; j++) csp[j] = nsp[j];
       if (c + 1 < nfc) {
-        const uint32_t b = 8 * FS * (c + 1) + q;
+        const uint32_t b = 64 * FS * (c + 1) + q;
 #pragma unroll
-        for (int j = 0; j < FS; j++) nsp[j] = (s2v){sys[b + 8 * j], par[b + 8 * j]};
+        for (int j = 0; j < FS; j++) nsp[j] = (s2v){sys[b + 64 * j], par[b + 64 * j]};
       }
 #pragma unroll
       for (int j = 0; j < FS; j++) {
@@ -194,7 +198,7 @@ static __device__ __attribute__((noinline)) void log_map(const short *sys, const
         if (k < K1) {
           alpha_step(a, (short)(sadd(csp[j].x, csp[j].y) >> 1), (short)(ssub(csp[j].x, csp[j].y) >> 1));
           if (k + 1 == 5) A5[q] = tm_pack(a);
-          if (((k + 1) & (TD_SEG - 1)) == 0) A[8 * ((k + 1) / TD_SEG) + q] = tm_pack(a);
+          if (((k + 1) & (TD_SEG - 1)) == 0) A[64 * ((k + 1) / TD_SEG) + q] = tm_pack(a);
         }
       }
     }
@@ -212,17 +216,17 @@ static __device__ __attribute__((noinline)) void log_map(const short *sys, const
   }
   A[q] = tm_pack(a);
   for (uint32_t k = 0; k < 5; k++) {
-    gamma_of(sys, par, 8 * k + q, g11, g10);
+    gamma_of(sys, par, 64 * k + q, g11, g10);
     alpha_step(a, g11, g10);
     /* checkpoints inside the re-run range hold re-run values (alpha(1..5) of the reference) */
-    if (((k + 1) & (TD_SEG - 1)) == 0 && k + 1 <= K1) A[8 * ((k + 1) / TD_SEG) + q] = tm_pack(a);
+    if (((k + 1) & (TD_SEG - 1)) == 0 && k + 1 <= K1) A[64 * ((k + 1) / TD_SEG) + q] = tm_pack(a);
   }
   /* termination betas of the last window (compute_beta16 :467-521, int16 wrap arithmetic) */
   tm_t t;
   {
     short m[3], mm[3], tv[8];
 #pragma unroll
-    for (int j = 0; j < 3; j++) gamma_of(sys + 8 * tf, par, K + j, m[j], mm[j]);   /* m_11/m_10[n + j] */
+    for (int j = 0; j < 3; j++) gamma_of(sys + 64 * tf, par, 64 * K1 + j, m[j], mm[j]);   /* m_11/m_10[n + j] */
     short beta0 = (short)-m[2], beta1 = m[2];
     short b0_2 = (short)(beta0 - m[1]), b1_2 = (short)(beta0 + m[1]), b2_2 = (short)(beta1 + mm[1]),
           b3_2 = (short)(beta1 - mm[1]);
@@ -243,14 +247,14 @@ static __device__ __attribute__((noinline)) void log_map(const short *sys, const
   s2v nsp[TD_SEG], nzz[TD_SEG / 2];            /* (sys, par) and (POST) s0 pairs of the next segment */
   uint4 nA;
   auto fetch = [&](int seg) {
-    const uint32_t b0 = 8u * (uint32_t)(seg * TD_SEG) + q;
+    const uint32_t b0 = 64u * (uint32_t)(seg * TD_SEG) + q;
 #pragma unroll
-    for (int j = 0; j < TD_SEG; j++) nsp[j] = (s2v){sys[b0 + 8 * j], par[b0 + 8 * j]};
+    for (int j = 0; j < TD_SEG; j++) nsp[j] = (s2v){sys[b0 + 64 * j], par[b0 + 64 * j]};
     if constexpr (POST) {
 #pragma unroll
-      for (int i = 0; i < TD_SEG / 2; i++) nzz[i] = (s2v){s0[b0 + 16 * i], s0[b0 + 16 * i + 8]};
+      for (int i = 0; i < TD_SEG / 2; i++) nzz[i] = (s2v){s0[b0 + 128 * i], s0[b0 + 128 * i + 64]};
     }
-    nA = A[8 * seg + q];
+    nA = A[64 * seg + q];
   };
   fetch((int)nseg - 1);
   for (int seg = (int)nseg - 1; seg >= 0; seg--) {
@@ -290,7 +294,7 @@ static __device__ __attribute__((noinline)) void log_map(const short *sys, const
             const short sv = (j & 1) ? css[j >> 1].y : css[j >> 1].x, zv = (j & 1) ? czz[j >> 1].y : czz[j >> 1].x;
             v = __builtin_elementwise_add_sat(__builtin_elementwise_sub_sat(v, sv), zv);
           }
-          ext[8 * k + q] = v;
+          ext[64 * k + q] = v;
         } else {
           asave[(k - kr) * 64 + lane] = al[j];
         }
@@ -308,7 +312,7 @@ static __device__ __attribute__((noinline)) void log_map(const short *sys, const
     b.v[v] = q == 7 ? t.v[v] : __builtin_bit_cast(s2v, dn);
   }
   for (int k = (int)K1 - 1; k >= kr && k >= 0; k--) {
-    const uint32_t e = 8 * k + q;
+    const uint32_t e = 64 * k + q;
     gamma_of(sys, par, e, g11, g10);
     short v = ext_of(tm_unpack(asave[(k - kr) * 64 + lane]), b, g11, g10);
     if constexpr (POST) v = __builtin_elementwise_add_sat(__builtin_elementwise_sub_sat(v, sys[e]), s0[e]);
@@ -348,7 +352,10 @@ __global__ void __launch_bounds__(64) k_td16(int n_cb, uint32_t K, const int16_t
   const uint32_t K1 = K >> 3, Kb = K >> 3;
   td_crc_tab(crctab, crc_type == 0 ? 0x864cfbu : 0x800063u);
   if (lane < 8) done_it[lane] = 0;
-  td_blk_t B = td_layout(scratch + (size_t)(valid ? cb : 0) * blk_bytes, K);
+  const td_blk_t W = td_layout(scratch + (size_t)blockIdx.x * 8 * blk_bytes, K);
+  td_blk_t B;   /* this lane's block: element i at td_ix(i) */
+  B.s0 = W.s0 + 8 * g; B.s1 = W.s1 + 8 * g; B.s2 = W.s2 + 8 * g; B.yp1 = W.yp1 + 8 * g; B.yp2 = W.yp2 + 8 * g;
+  B.ext = W.ext + 8 * g; B.ext2 = W.ext2 + 8 * g; B.A = W.A + 8 * g;
   if (valid) {
     /* demux (:1038-1158): bit i = window q, step v -> element 8v + q */
     gs16_t *y = (gs16_t *)(llr + (size_t)cb * llr_stride);
@@ -364,7 +371,7 @@ __global__ void __launch_bounds__(64) k_td16(int n_cb, uint32_t K, const int16_t
 #pragma unroll
       for (int u = 0; u < 8; u++)
         if (v0 + u < K1) {
-          const uint32_t j = 8 * (v0 + u) + q;
+          const uint32_t j = 64 * (v0 + u) + q;
           B.s0[j] = t0[u];
           B.yp1[j] = t1[u];
           B.yp2[j] = t2[u];
@@ -374,10 +381,11 @@ __global__ void __launch_bounds__(64) k_td16(int n_cb, uint32_t K, const int16_t
       for (uint32_t i = 0; i < 3; i++) {   /* tails (:1164-1186) */
         const short s_a = y[3 * K + 2 * i], p_a = y[3 * K + 2 * i + 1];
         const short s_b = y[3 * K + 6 + 2 * i], p_b = y[3 * K + 6 + 2 * i + 1];
-        B.s0[K + i] = B.s1[K + i] = B.s2[K + i] = s_a;
-        B.yp1[K + i] = p_a;
-        B.s0[K + 8 + i] = B.s1[K + 8 + i] = B.s2[K + 8 + i] = s_b;
-        B.yp2[K + i] = p_b;
+        const uint32_t ia = 64 * K1 + i, ib = 64 * (K1 + 1) + i;
+        B.s0[ia] = B.s1[ia] = B.s2[ia] = s_a;
+        B.yp1[ia] = p_a;
+        B.s0[ib] = B.s1[ib] = B.s2[ib] = s_b;
+        B.yp2[ia] = p_b;
       }
     }
   }
@@ -394,10 +402,10 @@ __global__ void __launch_bounds__(64) k_td16(int n_cb, uint32_t K, const int16_t
 #pragma unroll
         for (int u = 0; u < TD_XR; u++) ix[u] = v0 + u < K1 ? pi4[8 * (v0 + u) + q] : 0u;
 #pragma unroll
-        for (int u = 0; u < TD_XR; u++) val[u] = B.ext[ix[u]];
+        for (int u = 0; u < TD_XR; u++) val[u] = B.ext[td_ix(ix[u])];
 #pragma unroll
         for (int u = 0; u < TD_XR; u++)
-          if (v0 + u < K1) B.s2[8 * (v0 + u) + q] = val[u];
+          if (v0 + u < K1) B.s2[64 * (v0 + u) + q] = val[u];
       }
     __syncthreads();
     if (active) log_map<false>(B.s2, B.yp2, B.ext2, B.A, K, q, 1, asave, B.s0);
@@ -410,14 +418,14 @@ __global__ void __launch_bounds__(64) k_td16(int n_cb, uint32_t K, const int16_t
         for (int u = 0; u < TD_XR; u++) {
           const uint32_t i = v0 + u < K1 ? 8 * (v0 + u) + q : q;
           ix[u] = pi5[i];
-          e1[u] = B.ext[i];
-          z[u] = B.s0[i];
+          e1[u] = B.ext[td_ix(i)];
+          z[u] = B.s0[td_ix(i)];
         }
 #pragma unroll
-        for (int u = 0; u < TD_XR; u++) e2[u] = B.ext2[ix[u]];
+        for (int u = 0; u < TD_XR; u++) e2[u] = B.ext2[td_ix(ix[u])];
 #pragma unroll
         for (int u = 0; u < TD_XR; u++)
-          if (v0 + u < K1) B.s1[8 * (v0 + u) + q] = sadd(ssub(e2[u], e1[u]), z[u]);
+          if (v0 + u < K1) B.s1[64 * (v0 + u) + q] = sadd(ssub(e2[u], e1[u]), z[u]);
       }
       if (it > 1)
         for (uint32_t i0 = q; i0 < Kb; i0 += 8 * (TD_XR / 8)) {   /* hard decisions (:1267-1283), MSB first */
@@ -429,7 +437,7 @@ __global__ void __launch_bounds__(64) k_td16(int n_cb, uint32_t K, const int16_t
             ix[u] = i < Kb ? pi6[8 * i + (u & 7)] : 0u;
           }
 #pragma unroll
-          for (int u = 0; u < TD_XR; u++) x[u] = B.ext2[ix[u]];
+          for (int u = 0; u < TD_XR; u++) x[u] = B.ext2[td_ix(ix[u])];
 #pragma unroll
           for (int h = 0; h < TD_XR / 8; h++) {
             const uint32_t i = i0 + 8 * h;

@@ -1631,7 +1631,8 @@ static const uint16_t *td_tables(uint32_t K)
   return d;
 }
 
-extern "C" size_t oai4g_td_scratch_bytes(uint16_t K, int n_cb) { return (size_t)n_cb * oai4g_td_block_bytes(K); }
+/* per wave of 8 blocks (the decoder interleaves a wave's blocks in its scratch) */
+extern "C" size_t oai4g_td_scratch_bytes(uint16_t K, int n_cb) { return (size_t)((n_cb + 7) & ~7) * oai4g_td_block_bytes(K); }
 
 extern "C" int oai4g_td_batch(int n_cb, uint16_t K, const int16_t *d_llr, size_t llr_stride, uint8_t *d_out,
                               size_t out_stride, uint8_t *d_iters, uint8_t max_iterations, uint8_t crc_type, uint8_t F,
@@ -1656,7 +1657,7 @@ extern "C" uint8_t oai4g_phy_threegpplte_turbo_decoder16(const int16_t *y, uint8
   if (crc_type > 3) { set_err("Illegal crc length!"); return 255; }
   if (oai4g_qpp_index(n) < 0) { set_err("Illegal frame length!"); return 255; }
   if (crc_type > OAI4G_CRC24_B) { set_err("turbo decoder: CRC16 / CRC8 are not on the path"); return 255; }
-  const size_t ybytes = (3 * (size_t)n + 12) * 2, sbytes = oai4g_td_block_bytes(n);
+  const size_t ybytes = (3 * (size_t)n + 12) * 2, sbytes = oai4g_td_scratch_bytes(n, 1);
   uint8_t *buf = scratch(ybytes + 256 + (size_t)n / 8 + 256 + sbytes + 512);
   if (!buf) return 255;
   int16_t *d_y = (int16_t *)buf;
