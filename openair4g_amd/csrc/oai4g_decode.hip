@@ -27,11 +27,14 @@ static __device__ __forceinline__ short sadd(short a, short b) { return __builti
 static __device__ __forceinline__ short ssub(short a, short b) { return __builtin_elementwise_sub_sat(a, b); }
 
 #define TD_MAXH 128    /* MAX / 2 */
+#ifndef TD_FS
+#define TD_FS 16             /* forward chunk (steps whose operands are loaded one chunk ahead) */
+#endif
 #ifndef TD_XR
 #define TD_XR 32      /* steps per round of the exchange gathers (index loads, then gathers, in flight) */
 #endif
 #ifndef TD_SEG
-#define TD_SEG 8      /* alpha checkpoint interval (steps); measured best of 2/4/8/16 at C5 */
+#define TD_SEG 4      /* alpha checkpoint interval (steps); measured best of 2/4/8/16 at C5 (with TD_FS = 16) */
 #endif
 
 struct td_blk_t {      /* one wave's scratch: the 8 blocks interleaved, element i of block g at
@@ -47,7 +50,7 @@ static __device__ __forceinline__ td_blk_t td_layout(uint8_t *base, uint32_t K)
 {
   td_blk_t b;
   short *p = (short *)base;
-  const uint32_t n16 = (K + 16 * TD_SEG + 16 + 7) & ~7u, n128 = K + 128;   /* chunk read-ahead slack (2 TD_SEG steps) */
+  const uint32_t n16 = (K + 8 * (TD_FS + TD_SEG) + 16 + 7) & ~7u, n128 = K + 128;   /* read-ahead slack */
   b.s0 = p; p += 8 * n16;
   b.s1 = p; p += 8 * n16;
   b.s2 = p; p += 8 * n16;
@@ -61,7 +64,7 @@ static __device__ __forceinline__ td_blk_t td_layout(uint8_t *base, uint32_t K)
 
 size_t oai4g_td_block_bytes(uint32_t K)
 {
-  const size_t n16 = (K + 16 * TD_SEG + 16 + 7) & ~7u, n128 = K + 128;
+  const size_t n16 = (K + 8 * (TD_FS + TD_SEG) + 16 + 7) & ~7u, n128 = K + 128;
   return (((5 * n16 + 2 * n128) * 2 + 15) & ~(size_t)15) + (size_t)(K / 8 + 1) * 8 * 16 + 256;
 }
 
@@ -176,7 +179,7 @@ static __device__ __attribute__((noinline)) void log_map(const short *sys, const
   uint4 *A5 = A + 64 * (nseg + 1);             /* first-run alpha(5) */
   short g11, g10;
   /* forward, first run, in chunks of FS steps (operands of the next chunk in flight) */
-  constexpr int FS = 2 * TD_SEG;
+  constexpr int FS = TD_FS;
   const uint32_t nfc = (K1 + FS - 1) / FS;
   tm_t a = tm_init(q == 0);
   {
