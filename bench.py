@@ -31,6 +31,15 @@ def algorithmic_bytes(p, spt):
     return payload, iq
 
 
+def _traffic(config, kernel):
+    """calibrated HBM bytes per launch from the committed rocprofv3 PMC summary (tools/summarize_prof.py)"""
+    tpath = os.path.join(ROOT, "profiles", f"traffic_{config}.json")
+    try:
+        return json.load(open(tpath)).get(kernel)
+    except Exception:
+        return None
+
+
 def cpu_baseline(name, seconds, subframe):
     """Oracle ("port") timed on one host core over a bounded sample of the same workload."""
     import numpy as np
@@ -224,7 +233,7 @@ def bench_fep(args, world, rank, dist, torch):
             "config": {"workload": "slot_fep 20 MHz normal CP, 2 RX antennas, 14 x dft2048 per antenna",
                        "config_id": "FEP", "subframes_per_gpu_per_step": n_sf, "parallelism": f"subframe-sharded x{world}"},
             "roofline": {"bound": "hbm", "kernel": "k_fep<11>", "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": ach / HBM_PEAK_GBS, "traffic": None, "kernel_ms": kern_ms,
+                         "frac": ach / HBM_PEAK_GBS, "traffic": _traffic("FEP", "k_fep<11>"), "kernel_ms": kern_ms,
                          "algorithmic_bytes_per_launch": alg},
             "cpu_baseline": cpu}), flush=True)
 

@@ -13,7 +13,7 @@ import json
 import os
 import sys
 
-KMAP = {"k_encode": "encode_rm_scramble", "k_modofdm": "modulate_idft_cp"}
+KMAP = {"k_encode": "encode_rm_scramble", "k_modofdm": "modulate_idft_cp", "k_fep": "k_fep<11>", "k_td16": "k_td16"}
 
 
 def short(name):
