@@ -242,7 +242,11 @@ typedef struct {
   uint8_t q[2];               /* scrambling codeword index q (dlsim passes 0) */
   uint32_t TBS[2];
   uint32_t payload_stride;    /* bytes between consecutive transport blocks in the payload buffer */
-  uint32_t reserved[8];
+  uint32_t rm_limited_buffer; /* opt-in extension: 36.212 5.1.4.1.2 limited-buffer
+                                 rate matching when Ncb < Kw, where the reference prints "RM condition"
+                                 and emits E = 0 (lte_rate_matching.c:518-521); unlocks TM3 MCS >= 20.
+                                 0 (default) keeps the reference's behaviour (config_create fails). */
+  uint32_t reserved[7];
 } oai4g_tx_params_t;
 
 typedef struct oai4g_tx_config oai4g_tx_config_t;

@@ -71,7 +71,8 @@ class TxParams(ctypes.Structure):
                 ("amp", ctypes.c_int16), ("sqrt_rho_a", ctypes.c_int16), ("sqrt_rho_b", ctypes.c_int16),
                 ("rb_alloc", ctypes.c_uint32 * 4), ("nb_rb", ctypes.c_uint16), ("mcs", ctypes.c_uint8 * 2),
                 ("rvidx", ctypes.c_uint8 * 2), ("q", ctypes.c_uint8 * 2), ("TBS", ctypes.c_uint32 * 2),
-                ("payload_stride", ctypes.c_uint32), ("reserved", ctypes.c_uint32 * 8)]
+                ("payload_stride", ctypes.c_uint32), ("rm_limited_buffer", ctypes.c_uint32),
+                ("reserved", ctypes.c_uint32 * 7)]
 
     def to_bytes(self):
         return bytes(ctypes.string_at(ctypes.addressof(self), ctypes.sizeof(self)))

@@ -20,6 +20,10 @@
  */
 #include "oai4g_dft_prims.h"
 
+#ifndef OAI4G_FEP_WG_PER_CU
+#define OAI4G_FEP_WG_PER_CU 16   /* persistent workgroups per CU (64 VGPRs, 9 KB LDS: 8 waves per SIMD) */
+#endif
+
 /* forward radix-4 on saturating int16 (bfly4_tw1 lte_dfts.c:860-889, the dft16 stages
  * :1453-1500, bfly4_16 :965-1006): flip = -j x; y1 = (x0 - x2) + (f1 - f3), y3 = (x0 - x2) - (f1 - f3) */
 static __device__ __forceinline__ void r4fwd(s16x2 p0, s16x2 p1, s16x2 p2, s16x2 p3, s16x2 &o0, s16x2 &o1,
@@ -413,7 +417,7 @@ hipError_t oai4g_launch_fep(const int32_t *d_in, int32_t *d_out, int log2n, cons
   if (a.n_units <= 0) return hipSuccess;
   if (a.nsym <= 0 || a.nsym > OAI4G_FEP_MAX_SYM) return hipErrorInvalidValue;
   const int units = 128 / ((1 << log2n) >> 4);
-  const int need = (a.n_units + units - 1) / units, cap = n_cu * 8;
+  const int need = (a.n_units + units - 1) / units, cap = n_cu * OAI4G_FEP_WG_PER_CU;
   const dim3 grid(need < cap ? need : cap), blk(128);
   switch (log2n) {
   case 6: hipLaunchKernelGGL(k_fep<6>, grid, blk, 0, s, d_in, d_out, a, d_twf); break;

@@ -667,12 +667,12 @@ static int derive_cfg(oai4g_tx_config *cfg, const oai4g_tx_params_t *p, const ui
       uint32_t Kw = 3 * Kpi;
       uint32_t Nir = OAI4G_NSOFT / p->Kmimo / (p->Mdlharq < 8 ? p->Mdlharq : 8);
       uint32_t Ncb = (Nir / C < Kw) ? Nir / C : Kw;
-      if (Ncb < Kw) {
+      if (Ncb < Kw && !p->rm_limited_buffer) {
         printf("Exiting, RM condition (Nir %u, Nsoft %u, Kw %u\n", Nir, OAI4G_NSOFT, Kw);
         set_err("RM condition: Ncb %u < Kw %u (the reference emits E=0, lte_rate_matching.c:518-521)", Ncb, Kw);
         rm_fail = true;
         Ncb = Kw;
-      }
+      }   /* else (opt-in): the circular buffer is w[0..Ncb), 36.212 5.1.4.1.2 */
       c.Ncb[r] = Ncb;
       c.kidx[r] = (C > 1 && r < Cm) ? 0 : 1;
     }
@@ -728,11 +728,13 @@ static int derive_cfg(oai4g_tx_config *cfg, const oai4g_tx_params_t *p, const ui
       const uint16_t *np = c.nullpos[c.kidx[r]];
       uint32_t ncol8 = R << 3;
       uint32_t k0 = R * (2 + p->rvidx[cw] * ((Ncb % ncol8 ? 1 : 0) + Ncb / ncol8) * 2);
-      uint32_t before = 0;
-      for (uint32_t i = 0; i < nn; i++)
+      uint32_t before = 0, inbuf = 0;
+      for (uint32_t i = 0; i < nn; i++) {
         if (np[i] < k0) before++;
+        if (np[i] < Ncb) inbuf++;             /* NULLs inside the (possibly limited) circular buffer */
+      }
       c.k0c[r] = k0 - before;
-      c.Nnn[r] = Ncb - nn;
+      c.Nnn[r] = Ncb - inbuf;
     }
     uint32_t nw = (maxK + 31) >> 5;
     c.stream_words = nw + 3;   /* + tail word + read-ahead words */

@@ -165,6 +165,11 @@ uint32_t orc_subblock_interleave(uint32_t D, uint8_t *d, uint8_t *w)
 /* ======================================================================================
  * Rate matching — lte_rate_matching.c:464-634 (36.212 §5.1.4.1.2).
  * ==================================================================================== */
+/* opt-in limited-buffer rate matching (the build's extension): when set, Ncb < Kw
+ * selects circularly from w[0..Ncb) (36.212 5.1.4.1.2) instead of the reference's E = 0 exit */
+static int g_rm_limited = 0;
+void orc_set_rm_limited(int on) { g_rm_limited = on; }
+
 uint32_t orc_rate_match(uint32_t RTC, uint32_t G, const uint8_t *w, uint8_t *e, uint8_t C,
                         uint32_t Nsoft, uint8_t Mdlharq, uint8_t Kmimo, uint8_t rvidx, uint8_t Qm,
                         uint8_t Nl, uint8_t r)
@@ -172,7 +177,7 @@ uint32_t orc_rate_match(uint32_t RTC, uint32_t G, const uint8_t *w, uint8_t *e, 
   uint32_t Kw = 3 * (RTC << 5);
   uint32_t Nir = Nsoft / Kmimo / (Mdlharq < 8 ? Mdlharq : 8);
   uint32_t Ncb = (Nir / C < Kw) ? Nir / C : Kw;
-  if (Ncb < Kw) {                                                               /* :518-521 */
+  if (Ncb < Kw && !g_rm_limited) {                                              /* :518-521 */
     printf("Exiting, RM condition (Nir %u, Nsoft %u, Kw %u\n", Nir, Nsoft, Kw);
     return 0;
   }

@@ -46,6 +46,7 @@ void orc_turbo_encode(const uint8_t *c, uint16_t nbytes, uint8_t *d /* 3K+12 */,
 uint32_t orc_subblock_interleave(uint32_t D, uint8_t *d, uint8_t *w);
 
 /* ---- rate matching (lte_rate_matching.c:464-634) ---- */
+void orc_set_rm_limited(int on);   /* opt-in limited-buffer RM (extension, not the reference) */
 uint32_t orc_rate_match(uint32_t RTC, uint32_t G, const uint8_t *w, uint8_t *e, uint8_t C,
                         uint32_t Nsoft, uint8_t Mdlharq, uint8_t Kmimo, uint8_t rvidx, uint8_t Qm,
                         uint8_t Nl, uint8_t r);

@@ -144,6 +144,10 @@ def rate_match(RTC, G, w, C, r, Qm, rvidx=0, Nl=1, Kmimo=1, Mdlharq=8, Nsoft=182
     return e[:E]
 
 
+def set_rm_limited(on):
+    orc().orc_set_rm_limited(1 if on else 0)
+
+
 def scramble(e, G, c_init):
     buf = np.zeros((1 + (G >> 5)) * 32 + 32, dtype=np.uint8)
     buf[:len(e)] = e

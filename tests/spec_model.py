@@ -107,12 +107,13 @@ def subblock(streams):
     return R, w
 
 
-def rate_match(w, R, G, C, r, Qm, Nl=1, rv=0, Nsoft=1827072, Kmimo=1, Mdlharq=8):
-    """e_0..e_{E-1} of code block r; None when Ncb < Kw (the reference's limited-buffer exit)."""
+def rate_match(w, R, G, C, r, Qm, Nl=1, rv=0, Nsoft=1827072, Kmimo=1, Mdlharq=8, limited=False):
+    """e_0..e_{E-1} of code block r; None when Ncb < Kw (the reference's limited-buffer exit) unless
+    `limited` (36.212's own limited-buffer rule, the build's opt-in extension)."""
     Kw = 3 * 32 * R
     Nir = Nsoft // (Kmimo * min(Mdlharq, 8))
     Ncb = min(Nir // C, Kw)
-    if Ncb < Kw:
+    if Ncb < Kw and not limited:
         return None
     Gp = G // (Nl * Qm)
     gamma = Gp % C

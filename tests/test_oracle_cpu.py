@@ -275,3 +275,21 @@ def test_oracle_extended_cp_layout(name):
         assert np.array_equal(sym[:cp], sym[N:])
         body = O.idft(txF[0, l * N:(l + 1) * N].view(np.int16), 1)
         assert np.array_equal(sym[cp:].view(np.int16), body)
+
+
+@pytest.mark.parametrize("C,r,rv", [(7, 0, 0), (7, 6, 2), (13, 12, 3), (13, 4, 1)])
+def test_limited_buffer_rate_matching_matches_spec_model(C, r, rv):
+    """Opt-in extension: with Ncb < Kw the oracle's rate matcher follows
+    36.212 5.1.4.1.2's limited circular buffer w[0..Ncb) instead of the reference's E = 0 exit."""
+    rng = np.random.default_rng(C * 10 + r)
+    d = rng.integers(0, 2, 3 * 6144 + 12).astype(np.uint8)
+    rtc, w, _ = O.subblock(d, 6148)
+    R, w_spec = S.subblock(S.streams_from_d(d.tolist(), 6144))
+    O.set_rm_limited(True)
+    try:
+        e = O.rate_match(rtc, 86400, w, C, r, 6, rvidx=rv, Kmimo=2)
+    finally:
+        O.set_rm_limited(False)
+    e_spec = S.rate_match(w_spec, R, 86400, C, r, 6, rv=rv, Kmimo=2, limited=True)
+    assert e_spec is not None and e.tolist() == e_spec
+    assert len(O.rate_match(rtc, 86400, w, C, r, 6, rvidx=rv, Kmimo=2)) == 0   # flag off: the reference exit
