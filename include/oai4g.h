@@ -165,6 +165,17 @@ void oai4g_idft256(const int16_t *x, int16_t *y, int scale);
 void oai4g_idft128(const int16_t *x, int16_t *y, int scale);
 void oai4g_idft64(const int16_t *x, int16_t *y, int scale);
 
+/* ---------------- control region of the transmit grid ---------------- */
+/* generate_pcfich_reg_mapping (PHY/LTE_TRANSPORT/pcfich.c:48): REG indices (units of 6 REs) and
+ * the index of the lowest; prints them as the reference does. */
+void oai4g_generate_pcfich_reg_mapping(const oai4g_frame_parms_t *frame_parms, uint16_t pcfich_reg[4],
+                                       uint8_t *pcfich_first_reg_idx);
+/* generate_pcfich (pcfich.c:144, decl LTE_TRANSPORT/proto.h:1432): CFI codeword, scrambling, QPSK
+ * (SISO / ALAMOUTI) and REG mapping into symbol 0 of `subframe` of the frame grids txdataF[ant]
+ * (overwrites 16 REs per antenna).  Returns 0, or -1 (num_pdcch_symbols outside 1..3). */
+int oai4g_generate_pcfich(uint8_t num_pdcch_symbols, int16_t amp, const oai4g_frame_parms_t *frame_parms,
+                          int32_t **txdataF, uint8_t subframe);
+
 /* ---------------- UE receive front end ---------------- */
 /* dft64..dft2048 (PHY/TOOLS/lte_dfts.c:1766, 1957, 2172, 2359, 2574, 2689; decl TOOLS/defs.h):
  * y = DFT(x), bit-exact fixed point.  oai4g_dft returns 0 or -1. */

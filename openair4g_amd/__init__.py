@@ -144,6 +144,10 @@ _SIGS = {
     "oai4g_idft256": (None, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int]),
     "oai4g_idft128": (None, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int]),
     "oai4g_idft64": (None, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int]),
+    "oai4g_generate_pcfich_reg_mapping": (None, [ctypes.POINTER(FrameParms), ctypes.POINTER(ctypes.c_uint16),
+                                                  ctypes.POINTER(ctypes.c_uint8)]),
+    "oai4g_generate_pcfich": (ctypes.c_int, [ctypes.c_uint8, ctypes.c_int16, ctypes.POINTER(FrameParms),
+                                             ctypes.POINTER(ctypes.c_void_p), ctypes.c_uint8]),
     "oai4g_dft": (ctypes.c_int, [ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int]),
     "oai4g_dft2048": (None, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int]),
     "oai4g_dft1024": (None, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int]),
@@ -302,6 +306,14 @@ def idft(x, scale=1):
     y = np.zeros_like(x)
     _check(lib().oai4g_idft(int(n).bit_length() - 1, _ptr(x), _ptr(y), scale) == 0)
     return y
+
+
+def generate_pcfich(cfi, amp, fp, grids, subframe):
+    """generate_pcfich drop-in on a list of frame grids (int32 arrays, modified in place)."""
+    init()
+    n = len(grids)
+    gp = (ctypes.c_void_p * n)(*[g.ctypes.data for g in grids])
+    return lib().oai4g_generate_pcfich(cfi, amp, ctypes.byref(fp), gp, subframe)
 
 
 def dft(x, scale=1):

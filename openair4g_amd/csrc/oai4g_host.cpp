@@ -1864,3 +1864,70 @@ extern "C" int oai4g_fep_batch(const oai4g_frame_parms_t *fp, int n_sf, int n_an
   HCK(oai4g_launch_fep(d_rx, d_rxF, fp->log2_symbol_size, a, g_twf, g_n_cu, (hipStream_t)stream), -1);
   return 0;
 }
+
+/* ------------------------------------------------------------------------------------------
+ * Control region: PCFICH (pcfich.c:48-228)
+ * ---------------------------------------------------------------------------------------- */
+/* generate_pcfich_reg_mapping (pcfich.c:48-84): the four REGs (units of 6 REs from the first
+ * carrier) and the index of the lowest; prints them as the reference does */
+extern "C" void oai4g_generate_pcfich_reg_mapping(const oai4g_frame_parms_t *fp, uint16_t pcfich_reg[4],
+                                                  uint8_t *pcfich_first_reg_idx)
+{
+  const uint32_t NRB = fp->N_RB_DL, kbar = 6 * (fp->Nid_cell % (2 * NRB));
+  uint16_t first;
+  pcfich_reg[0] = (uint16_t)(kbar / 6);
+  first = pcfich_reg[0];
+  *pcfich_first_reg_idx = 0;
+  const uint32_t steps[3] = {(NRB >> 1) * 6, NRB * 6, ((3 * NRB) >> 1) * 6};
+  for (int i = 1; i < 4; i++) {
+    pcfich_reg[i] = (uint16_t)(((kbar + steps[i - 1]) % (NRB * 12)) / 6);
+    if (pcfich_reg[i] < first) {
+      *pcfich_first_reg_idx = (uint8_t)i;
+      first = pcfich_reg[i];
+    }
+  }
+  printf("pcfich_reg : %d,%d,%d,%d\n", pcfich_reg[0], pcfich_reg[1], pcfich_reg[2], pcfich_reg[3]);
+}
+
+/* generate_pcfich (pcfich.c:144, decl proto.h:1432): overwrites the 16 PCFICH REs of symbol 0 of
+ * `subframe` in the frame grids txdataF[0] (and txdataF[1] with two antennas).  The reference
+ * reads frame_parms->pcfich_reg (set at init by generate_pcfich_reg_mapping); here they are
+ * derived from fp.  num_pdcch_symbols outside 1..3 is rejected (-1): the reference would map an
+ * uninitialised codeword (pcfich.c:164-165). */
+extern "C" int oai4g_generate_pcfich(uint8_t num_pdcch_symbols, int16_t amp, const oai4g_frame_parms_t *fp,
+                                     int32_t **txdataF, uint8_t subframe)
+{
+  NEED_INIT(-1);
+  if (num_pdcch_symbols < 1 || num_pdcch_symbols > 3 || subframe > 9) {
+    set_err("generate_pcfich: num_pdcch_symbols %u / subframe %u out of range", num_pdcch_symbols, subframe);
+    return -1;
+  }
+  uint16_t reg[4];
+  uint8_t first_idx;
+  oai4g_generate_pcfich_reg_mapping(fp, reg, &first_idx);
+  const uint32_t N = fp->ofdm_symbol_size, nsymb = fp->Ncp == 0 ? 14 : 12;
+  const size_t symbol_offset = (size_t)N * subframe * nsymb;
+  pcfich_args_t a;
+  memset(&a, 0, sizeof(a));
+  a.c_init = ((((2u * fp->Nid_cell) + 1u) * (1u + subframe)) << 9) + fp->Nid_cell;
+  a.cfi = num_pdcch_symbols;
+  a.gain = fp->mode1_flag == 1 ? (int16_t)((amp * 23170) >> 15) : (int16_t)(amp / 2);
+  a.mode1 = fp->mode1_flag ? 1 : 0;
+  a.nushift3 = (uint8_t)(fp->nushift % 3);
+  for (int q = 0; q < 4; q++) {
+    uint32_t ro = fp->first_carrier_offset + (uint32_t)reg[q] * 6;
+    if (ro >= N) ro = 1 + ro - N;
+    a.reg_off[q] = ro;
+  }
+  a.n_ant = fp->nb_antennas_tx > 1 ? 2 : 1;
+  uint8_t *buf = scratch(2 * (size_t)N * 4 + 256);
+  if (!buf) return -1;
+  int32_t *d0 = (int32_t *)buf, *d1 = (int32_t *)(buf + (((size_t)N * 4 + 255) & ~(size_t)255));
+  for (uint32_t aa = 0; aa < a.n_ant; aa++)
+    HCK(hipMemcpyAsync(aa ? d1 : d0, txdataF[aa] + symbol_offset, (size_t)N * 4, hipMemcpyHostToDevice, g_scr.s), -1);
+  HCK(oai4g_launch_pcfich(d0, d1, a, g_scr.s), -1);
+  for (uint32_t aa = 0; aa < a.n_ant; aa++)
+    HCK(hipMemcpyAsync(txdataF[aa] + symbol_offset, aa ? d1 : d0, (size_t)N * 4, hipMemcpyDeviceToHost, g_scr.s), -1);
+  HCK(hipStreamSynchronize(g_scr.s), -1);
+  return 0;
+}

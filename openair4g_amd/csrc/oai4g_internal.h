@@ -183,6 +183,18 @@ struct ofdm_sym_t {
 };
 hipError_t oai4g_launch_ofdm(const int32_t *d_in, int32_t *d_out, int log2n, int nsym, const ofdm_sym_t *syms,
                              int scale, const uint32_t *d_tw, hipStream_t s);
+/* control region (oai4g_ctrl.hip): PCFICH */
+struct pcfich_args_t {
+  uint32_t c_init;      /* pcfich_scrambling x2 (pcfich.c:97) */
+  uint32_t cfi;         /* num_pdcch_symbols, 1..3 */
+  int16_t gain;         /* QPSK amplitude (pcfich.c:168-171) */
+  uint8_t mode1;        /* 1 = SISO mapping, 0 = ALAMOUTI */
+  uint8_t nushift3;     /* nushift % 3 */
+  uint32_t reg_off[4];  /* first RE of each REG in the symbol, DC-skip applied (pcfich.c:210-213) */
+  uint32_t n_ant;
+};
+hipError_t oai4g_launch_pcfich(int32_t *d_g0, int32_t *d_g1, const pcfich_args_t &a, hipStream_t s);
+
 /* UE receive front end (oai4g_fep.hip): per-symbol CP removal + forward DFT */
 #define OAI4G_FEP_MAX_SYM 14
 struct fep_args_t {

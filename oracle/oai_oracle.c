@@ -1103,3 +1103,78 @@ int orc_tx_subframe(const orc_tx_cfg_t *cfg, uint8_t *payload[2], int32_t **txda
   free(e_buf[1]);
   return ret < 0 ? -1 : 0;
 }
+
+/* ======================================================================================
+ * PCFICH — pcfich.c:48-228 (generate_pcfich_reg_mapping, pcfich_scrambling, generate_pcfich)
+ * ==================================================================================== */
+static const uint8_t orc_pcfich_b[4][32] = {                                    /* :138-142 */
+  {0,1,1,0,1,1,0,1,1,0,1,1,0,1,1,0,1,1,0,1,1,0,1,1,0,1,1,0,1,1,0,1},
+  {1,0,1,1,0,1,1,0,1,1,0,1,1,0,1,1,0,1,1,0,1,1,0,1,1,0,1,1,0,1,1,0},
+  {1,1,0,1,1,0,1,1,0,1,1,0,1,1,0,1,1,0,1,1,0,1,1,0,1,1,0,1,1,0,1,1},
+  {0}};
+
+void orc_pcfich_reg_mapping(const orc_frame_t *fp, uint16_t reg[4], uint8_t *first_idx)  /* :48-84 */
+{
+  uint16_t kbar = 6 * (fp->Nid_cell % (2 * fp->N_RB_DL)), first;
+  reg[0] = kbar / 6;
+  first = reg[0];
+  *first_idx = 0;
+  reg[1] = ((kbar + (fp->N_RB_DL >> 1) * 6) % (fp->N_RB_DL * 12)) / 6;
+  if (reg[1] < reg[0]) { *first_idx = 1; first = reg[1]; }
+  reg[2] = ((kbar + (fp->N_RB_DL) * 6) % (fp->N_RB_DL * 12)) / 6;
+  if (reg[2] < first) { *first_idx = 2; first = reg[2]; }
+  reg[3] = ((kbar + ((3 * fp->N_RB_DL) >> 1) * 6) % (fp->N_RB_DL * 12)) / 6;
+  if (reg[3] < first) { *first_idx = 3; first = reg[3]; }
+}
+
+int orc_generate_pcfich(uint8_t num_pdcch_symbols, int16_t amp, const orc_frame_t *fp, int32_t **txdataF,
+                        uint8_t subframe)
+{
+  uint8_t bt[32], first_idx;
+  int16_t d[2][16][2];
+  uint16_t reg[4];
+  if (num_pdcch_symbols < 1 || num_pdcch_symbols > 3) return -1;   /* :164 (else bt is uninitialised) */
+  orc_pcfich_reg_mapping(fp, reg, &first_idx);
+  uint32_t x1, x2 = ((((2 * fp->Nid_cell) + 1) * (1 + subframe)) << 9) + fp->Nid_cell, s = 0;  /* :97 */
+  for (int i = 0; i < 32; i++) {                                                                /* :99-108 */
+    if ((i & 0x1f) == 0) s = orc_gold_generic(&x1, &x2, 1);
+    bt[i] = (orc_pcfich_b[num_pdcch_symbols - 1][i] & 1) ^ ((s >> (i & 0x1f)) & 1);
+  }
+  int16_t g = fp->mode1_flag == 1 ? (int16_t)((amp * 23170) >> 15) : (int16_t)(amp / 2);       /* :168-171 */
+  if (fp->mode1_flag) {
+    for (int i = 0; i < 16; i++) {
+      d[0][i][0] = d[1][i][0] = bt[2 * i] == 1 ? -g : g;
+      d[0][i][1] = d[1][i][1] = bt[2 * i + 1] == 1 ? -g : g;
+    }
+  } else {                                                                                      /* :182-196 */
+    for (int i = 0; i < 16; i += 2) {
+      d[0][i][0] = bt[2 * i] == 1 ? -g : g;
+      d[0][i][1] = bt[2 * i + 1] == 1 ? -g : g;
+      d[1][i][0] = bt[2 * i + 2] == 1 ? g : -g;
+      d[1][i][1] = bt[2 * i + 3] == 1 ? -g : g;
+      d[0][i + 1][0] = -d[1][i][0];
+      d[0][i + 1][1] = d[1][i][1];
+      d[1][i + 1][0] = d[0][i][0];
+      d[1][i + 1][1] = -d[0][i][1];
+    }
+  }
+  uint32_t nsymb = fp->Ncp == 0 ? 14 : 12, N = fp->ofdm_symbol_size;
+  uint32_t symbol_offset = N * (subframe * nsymb), m = 0, nushiftmod3 = fp->nushift % 3;
+  for (int q = 0; q < 4; q++) {                                                                 /* :209-226 */
+    uint32_t reg_offset = fp->first_carrier_offset + (uint16_t)reg[q] * 6;
+    if (reg_offset >= N) reg_offset = 1 + reg_offset - N;
+    for (uint32_t i = 0; i < 6; i++)
+      if (i != nushiftmod3 && i != nushiftmod3 + 3) {
+        int16_t *t0 = (int16_t *)&txdataF[0][symbol_offset + reg_offset + i];
+        t0[0] = d[0][m][0];
+        t0[1] = d[0][m][1];
+        if (fp->nb_antennas_tx > 1) {
+          int16_t *t1 = (int16_t *)&txdataF[1][symbol_offset + reg_offset + i];
+          t1[0] = d[1][m][0];
+          t1[1] = d[1][m][1];
+        }
+        m++;
+      }
+  }
+  return 0;
+}

@@ -102,6 +102,10 @@ void orc_idft(int log2n, const int16_t *x, int16_t *y, int scale);
 void orc_twiddle(int N, int m, int16_t *re, int16_t *im);
 void orc_dft(int log2n, const int16_t *x, int16_t *y, int scale);           /* forward dft64 … dft2048 */
 void orc_dft_twiddle_ab(int N, int m, int16_t a[2], int16_t b[2]);
+/* PCFICH (pcfich.c:48-228) into symbol 0 of `subframe` of frame grids txdataF[ant] */
+void orc_pcfich_reg_mapping(const orc_frame_t *fp, uint16_t reg[4], uint8_t *first_idx);
+int orc_generate_pcfich(uint8_t num_pdcch_symbols, int16_t amp, const orc_frame_t *fp, int32_t **txdataF,
+                        uint8_t subframe);
 /* slot_fep DFT part (slot_fep.c:40-177); rxdata[aa] = 10 subframes + N words of wrap extension */
 int orc_slot_fep(int32_t **rxdata, int32_t **rxdataF, const orc_frame_t *fp, int nb_antennas_rx, uint8_t l,
                  uint8_t Ns, int sample_offset, int no_prefix);

@@ -144,6 +144,20 @@ def rate_match(RTC, G, w, C, r, Qm, rvidx=0, Nl=1, Kmimo=1, Mdlharq=8, Nsoft=182
     return e[:E]
 
 
+def generate_pcfich(cfi, amp, fp, grids, subframe):
+    """orc_generate_pcfich on a list of frame grids (int32 arrays, modified in place)"""
+    n = len(grids)
+    gp = (ctypes.c_void_p * n)(*[g.ctypes.data for g in grids])
+    return orc().orc_generate_pcfich(cfi, amp, ctypes.byref(fp), gp, subframe)
+
+
+def pcfich_reg_mapping(fp):
+    reg = (ctypes.c_uint16 * 4)()
+    first = ctypes.c_uint8()
+    orc().orc_pcfich_reg_mapping(ctypes.byref(fp), reg, ctypes.byref(first))
+    return list(reg), first.value
+
+
 def set_rm_limited(on):
     orc().orc_set_rm_limited(1 if on else 0)
 

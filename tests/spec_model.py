@@ -323,3 +323,39 @@ def crs_p23(N_RB, Nid, subframe, port, amp, N, first_carrier, Ncp=0):
             fbin = first_carrier + k if k < 6 * N_RB else k - 6 * N_RB + 1
             out[(slot * nsymb + 1, fbin)] = (a * (1 - 2 * c[2 * mp]), a * (1 - 2 * c[2 * mp + 1]))
     return out
+
+
+def pcfich(N_RB, Nid, subframe, cfi, amp, N, first_carrier, mode1, n_ant):
+    """PCFICH REs of symbol 0 per antenna: {grid index: (re, im)} (36.212 5.3.4 CFI codeword,
+    36.211 6.7.1 scrambling, 7.1.2 QPSK, 6.3.3.3 / 6.3.4.3 transmit diversity, 6.7.4 mapping to
+    four REGs, 6.2.4 REGs of symbol 0 skipping the port-0/1 RS positions)."""
+    cw = {1: (0, 1, 1), 2: (1, 0, 1), 3: (1, 1, 0)}[cfi]
+    c = gold(((subframe + 1) * (2 * Nid + 1) << 9) + Nid, 32)
+    bt = [cw[i % 3] ^ c[i] for i in range(32)]
+    g = (amp * 23170) >> 15 if mode1 else int(amp / 2)
+    x = [(-g if bt[2 * i] else g, -g if bt[2 * i + 1] else g) for i in range(16)]
+    if mode1:
+        y = [x, x]
+    else:
+        y0, y1 = [None] * 16, [None] * 16
+        for k in range(0, 16, 2):
+            a, b = x[k], x[k + 1]
+            y0[k], y1[k] = a, (-b[0], b[1])            # x0, -x1*
+            y0[k + 1], y1[k + 1] = b, (a[0], -a[1])    # x1,  x0*
+        y = [y0, y1]
+    kbar = 6 * (Nid % (2 * N_RB))
+    vs = (Nid % 6) % 3
+    out = [dict() for _ in range(n_ant)]
+    m = 0
+    for i in range(4):
+        k0 = (kbar + (i * N_RB // 2) * 6) % (12 * N_RB)
+        for j in range(6):
+            if j in (vs, vs + 3):
+                continue
+            idx = first_carrier + k0 + j
+            if idx >= N:
+                idx = idx - N + 1                      # DC skip
+            for a in range(n_ant):
+                out[a][idx] = y[a][m]
+            m += 1
+    return out
