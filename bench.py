@@ -147,7 +147,8 @@ def bench_c5(args, world, rank, dist, torch):
                        "config_id": "C5", "subframes_per_gpu_per_step": n_sf, "code_blocks_per_step": n_cb,
                        "mean_iterations": float(np.mean(its)), "parallelism": f"block-sharded x{world}"},
             "roofline": {"bound": "hbm", "kernel": "k_td16", "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": ach / HBM_PEAK_GBS, "traffic": None},
+                         "frac": ach / HBM_PEAK_GBS, "traffic": _traffic("C5", "k_td16"),
+                         "note": "latency-bound: traffic (scratch streaming per half-iteration) >> algorithmic bytes"},
             "cpu_baseline": cpu}), flush=True)
 
 
