@@ -398,18 +398,26 @@ __global__ void __launch_bounds__(64) k_td16(int n_cb, uint32_t K, const int16_t
   __syncthreads();
   uint32_t it = 0;
   for (it = 1; it <= max_it; it++) {
-    if (active)   /* interleave (pi4): TD_XR steps per round, all index loads then all gathers in flight */
+    if (active) {  /* interleave (pi4): TD_XR steps per round; the next round's indices load during the gathers */
+      uint32_t ixn[TD_XR];
+#pragma unroll
+      for (int u = 0; u < TD_XR; u++) ixn[u] = (uint32_t)u < K1 ? pi4[8 * u + q] : 0u;
       for (uint32_t v0 = 0; v0 < K1; v0 += TD_XR) {
         uint32_t ix[TD_XR];
         short val[TD_XR];
 #pragma unroll
-        for (int u = 0; u < TD_XR; u++) ix[u] = v0 + u < K1 ? pi4[8 * (v0 + u) + q] : 0u;
+        for (int u = 0; u < TD_XR; u++) ix[u] = ixn[u];
+        if (v0 + TD_XR < K1) {
+#pragma unroll
+          for (int u = 0; u < TD_XR; u++) ixn[u] = v0 + TD_XR + u < K1 ? pi4[8 * (v0 + TD_XR + u) + q] : 0u;
+        }
 #pragma unroll
         for (int u = 0; u < TD_XR; u++) val[u] = B.ext[td_ix(ix[u])];
 #pragma unroll
         for (int u = 0; u < TD_XR; u++)
           if (v0 + u < K1) B.s2[64 * (v0 + u) + q] = val[u];
       }
+    }
     __syncthreads();
     if (active) log_map<false>(B.s2, B.yp2, B.ext2, B.A, K, q, 1, asave, B.s0);
     __syncthreads();
