@@ -104,6 +104,18 @@ int oai4g_init_frame_parms(oai4g_frame_parms_t *fp, uint16_t N_RB_DL, uint16_t N
 uint8_t oai4g_get_Qm(uint8_t mcs);
 int oai4g_get_G(const oai4g_frame_parms_t *fp, uint16_t nb_rb, const uint32_t *rb_alloc, uint8_t mod_order,
                 uint8_t Nl, uint8_t num_pdcch_symbols, int frame, uint8_t subframe);
+/* get_Qm_ul (lte_mcs.c:57), get_I_TBS (:69), get_I_TBS_UL (:84) */
+uint8_t oai4g_get_Qm_ul(uint8_t mcs);
+uint8_t oai4g_get_I_TBS(uint8_t mcs);
+uint8_t oai4g_get_I_TBS_UL(uint8_t mcs);
+/* TBStable[I_TBS][nb_rb-1] (LTE_TRANSPORT/dlsch_tbs_full.h:34, 36.213 Table 7.1.7.2.1-1) in bits,
+ * 0 outside 0..26 x 1..110.  The reference's entry for I_TBS 6, 1 PRB is 328 (the spec's is 88);
+ * the table keeps the reference's value. */
+uint32_t oai4g_tbs_bits(uint8_t I_TBS, uint16_t nb_rb);
+/* get_TBS_DL (lte_mcs.c:118) / get_TBS_UL (:137): TBS in BYTES, as the reference returns it;
+ * 0 when nb_rb == 0 or mcs >= 29 */
+uint32_t oai4g_get_TBS_DL(uint8_t mcs, uint16_t nb_rb);
+uint32_t oai4g_get_TBS_UL(uint8_t mcs, uint16_t nb_rb);
 /* new_eNB_dlsch / free_eNB_dlsch (dlsch_coding.c:120 / :85) */
 oai4g_dlsch_t *oai4g_new_dlsch(uint8_t Kmimo, uint8_t Mdlharq, uint8_t N_RB_DL);
 void oai4g_free_dlsch(oai4g_dlsch_t *dlsch);

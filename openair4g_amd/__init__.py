@@ -93,6 +93,12 @@ _SIGS = {
     "oai4g_init_frame_parms": (ctypes.c_int, [ctypes.POINTER(FrameParms), ctypes.c_uint16, ctypes.c_uint16,
                                               ctypes.c_uint8, ctypes.c_uint8, ctypes.c_uint8, ctypes.c_uint8]),
     "oai4g_get_Qm": (ctypes.c_uint8, [ctypes.c_uint8]),
+    "oai4g_get_Qm_ul": (ctypes.c_uint8, [ctypes.c_uint8]),
+    "oai4g_get_I_TBS": (ctypes.c_uint8, [ctypes.c_uint8]),
+    "oai4g_get_I_TBS_UL": (ctypes.c_uint8, [ctypes.c_uint8]),
+    "oai4g_tbs_bits": (ctypes.c_uint32, [ctypes.c_uint8, ctypes.c_uint16]),
+    "oai4g_get_TBS_DL": (ctypes.c_uint32, [ctypes.c_uint8, ctypes.c_uint16]),
+    "oai4g_get_TBS_UL": (ctypes.c_uint32, [ctypes.c_uint8, ctypes.c_uint16]),
     "oai4g_get_G": (ctypes.c_int, [ctypes.POINTER(FrameParms), ctypes.c_uint16, ctypes.POINTER(ctypes.c_uint32),
                                    ctypes.c_uint8, ctypes.c_uint8, ctypes.c_uint8, ctypes.c_int, ctypes.c_uint8]),
     "oai4g_new_dlsch": (ctypes.POINTER(Dlsch), [ctypes.c_uint8, ctypes.c_uint8, ctypes.c_uint8]),
@@ -520,10 +526,14 @@ FULL_ALLOC_15 = (0x7FFF, 0, 0, 0)
 FULL_ALLOC_50 = (0xFFFFFFFF, 0x3FFFF, 0, 0)
 FULL_ALLOC_25 = (0x1FFFFFF, 0, 0, 0)
 
-# TBS from 3GPP TS 36.213 Table 7.1.7.2.1-1 for the configurations exercised here
-TBS_TABLE = {(9, 6): 936, (4, 6): 408, (16, 100): 30576, (19, 100): 36696, (9, 100): 15840, (28, 100): 75376,
-             (5, 50): 4392, (15, 50): 14112, (26, 50): 30576, (9, 15): 2344,
-             (16, 25): 7736, (19, 25): 9144, (16, 50): 15264, (19, 50): 18336, (19, 15): 5352, (19, 6): 2152}
+def get_TBS_DL(mcs, nb_rb):
+    """get_TBS_DL (lte_mcs.c:118): transport block size in BYTES, from the library's TBStable."""
+    return lib().oai4g_get_TBS_DL(mcs, nb_rb)
+
+
+def tbs_bits(mcs, nb_rb):
+    """TBS in bits for (mcs, nb_rb) as dlsim uses it (get_TBS_DL << 3; dci_tools.c)."""
+    return get_TBS_DL(mcs, nb_rb) << 3
 
 CONFIGS = {
     # C1: dlsim 1.4 MHz SISO QPSK (MCS 9), 3 PDCCH symbols
@@ -578,7 +588,7 @@ def make_params(name="C3", subframe=7, subframe_step=0, rnti=0x1234, Nid_cell=0,
         p.mcs[cw] = c["mcs"][cw]
         p.rvidx[cw] = 0
         p.q[cw] = 0
-        p.TBS[cw] = tbs[cw] if tbs else TBS_TABLE[(c["mcs"][cw], c["nb_rb"])]
+        p.TBS[cw] = tbs[cw] if tbs else tbs_bits(c["mcs"][cw], c["nb_rb"])
     maxA = max(p.TBS[cw] // 8 for cw in range(p.n_cw))
     p.payload_stride = (maxA + 3 + 15) & ~15
     return p

@@ -19,6 +19,7 @@
 
 #include "../../include/oai4g.h"
 #include "../../include/oai4g_qpp.h"
+#include "../../include/oai4g_tbs.h"
 #include "oai4g_internal.h"
 
 /* ------------------------------------------------------------------------------------------
@@ -293,6 +294,49 @@ extern "C" int oai4g_init_frame_parms(oai4g_frame_parms_t *fp, uint16_t N_RB_DL,
 }
 
 extern "C" uint8_t oai4g_get_Qm(uint8_t mcs) { return mcs < 10 ? 2 : (mcs < 17 ? 4 : 6); }
+
+/* get_Qm_ul (lte_mcs.c:57) */
+extern "C" uint8_t oai4g_get_Qm_ul(uint8_t mcs) { return mcs < 11 ? 2 : (mcs < 21 ? 4 : 6); }
+
+/* get_I_TBS (lte_mcs.c:69-82): 36.213 Table 7.1.7.1-1 */
+extern "C" uint8_t oai4g_get_I_TBS(uint8_t mcs)
+{
+  if (mcs < 10) return mcs;
+  if (mcs == 10) return 9;
+  if (mcs < 17) return (uint8_t)(mcs - 1);
+  if (mcs == 17) return 15;
+  return (uint8_t)(mcs - 2);
+}
+
+/* get_I_TBS_UL (lte_mcs.c:84-95): its `I_MCS == 10` branch is unreachable after `<= 10`, kept as is */
+extern "C" uint8_t oai4g_get_I_TBS_UL(uint8_t mcs)
+{
+  if (mcs <= 10) return mcs;
+  if (mcs < 21) return (uint8_t)(mcs - 1);
+  return (uint8_t)(mcs - 2);
+}
+
+/* TBStable[I_TBS][N_PRB-1] (dlsch_tbs_full.h:34) in bits; 0 outside the table */
+extern "C" uint32_t oai4g_tbs_bits(uint8_t I_TBS, uint16_t nb_rb)
+{
+  if (I_TBS > 26 || nb_rb < 1 || nb_rb > 110) return 0;
+  return oai4g_tbs_by_prb[nb_rb - 1][I_TBS];
+}
+
+/* get_TBS_DL (lte_mcs.c:118-137): transport block size in BYTES (TBStable >> 3), 0 for nb_rb = 0
+ * or mcs >= 29 — the reference's unit, which its callers multiply back by 8 */
+extern "C" uint32_t oai4g_get_TBS_DL(uint8_t mcs, uint16_t nb_rb)
+{
+  if (nb_rb == 0 || mcs >= 29) return 0;
+  return oai4g_tbs_bits(oai4g_get_I_TBS(mcs), nb_rb) >> 3;
+}
+
+/* get_TBS_UL (lte_mcs.c:137-155), same unit */
+extern "C" uint32_t oai4g_get_TBS_UL(uint8_t mcs, uint16_t nb_rb)
+{
+  if (nb_rb == 0 || mcs >= 29) return 0;
+  return oai4g_tbs_bits(oai4g_get_I_TBS_UL(mcs), nb_rb) >> 3;
+}
 
 static int rb_bit(const uint32_t *rb_alloc, int rb)
 {

@@ -359,3 +359,166 @@ def pcfich(N_RB, Nid, subframe, cfi, amp, N, first_carrier, mode1, n_ant):
                 out[a][idx] = y[a][m]
             m += 1
     return out
+
+
+# ------------------------------------------------------------------ whole DLSCH chain (36.212 5.3.2)
+def _qpp_params():
+    import os
+    import re
+    src = open(os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "include",
+                            "oai4g_qpp.c")).read()
+    return {int(a): (int(b), int(c)) for a, b, c in re.findall(r"\{\s*(\d+)\s*,\s*(\d+)\s*,\s*(\d+)\s*\}", src)}
+
+
+def segment(b):
+    """36.212 5.1.2 code block segmentation of the bit list b (TB + CRC24A): returns the code
+    blocks (lists of K_r bits, CRC24B appended when C > 1) and F.  Filler bits are zeros: the
+    reference encodes them as 0 rather than <NULL> (A6q, 3gpplte_sse.c:380-476; the oracle and
+    the reference TU agree, tests/test_ref_pin_cpu.py)."""
+    Ks = sorted(_qpp_params())
+    Z = 6144
+    B = len(b)
+    if B <= Z:
+        C, Bp = 1, B
+    else:
+        C = -(-B // (Z - 24))
+        Bp = B + 24 * C
+    Kp = min(K for K in Ks if C * K >= Bp)
+    if C == 1:
+        Cp, Km, Cm = 1, 0, 0
+    else:
+        Km = max(K for K in Ks if K < Kp)
+        Cm = (C * Kp - Bp) // (Kp - Km)
+        Cp = C - Cm
+    F = Cp * Kp + Cm * Km - Bp
+    blocks, s = [], 0
+    for r in range(C):
+        K = Km if r < Cm else Kp
+        blk = [0] * (F if r == 0 else 0)
+        n = K - len(blk) - (24 if C > 1 else 0)
+        blk += list(b[s:s + n])
+        s += n
+        if C > 1:
+            blk += crc24(blk, CRC24B)
+        blocks.append(blk)
+    return blocks, F
+
+
+def dlsch_e(payload, TBS, G, Qm, Nl=1, rv=0, Kmimo=1, Mdlharq=8, c_init=None, Nsoft=1827072):
+    """Scrambled bits e_0..e_{G-1} of one transport block: CRC24A, segmentation, turbo coding,
+    sub-block interleaving, rate matching (E per block, concatenated) and the 36.211 6.3.1
+    scrambling with the Gold sequence of c_init (None: unscrambled)."""
+    f = _qpp_params()
+    a = bytes_to_bits(payload, TBS)
+    blocks, _ = segment(a + crc24(a, CRC24A))
+    e = []
+    for r, c in enumerate(blocks):
+        K = len(c)
+        R, w = subblock(streams_from_d(turbo_encode(c, *f[K]), K))
+        er = rate_match(w, R, G, len(blocks), r, Qm, Nl=Nl, rv=rv, Kmimo=Kmimo, Mdlharq=Mdlharq, Nsoft=Nsoft)
+        assert er is not None, "limited-buffer rate matching (Ncb < Kw): no reference output"
+        e += er
+    assert len(e) == G
+    if c_init is not None:
+        g = gold(c_init, G)
+        e = [x ^ y for x, y in zip(e, g)]
+    return e
+
+
+# ------------------------------------------------------------------ PDSCH resource mapping (36.211 6.3.5)
+def pdsch_res(N_RB, N, first_carrier, nushift, npdcch, subframe, crs_ports, Ncp=0, rb_alloc=None):
+    """Data REs of one FDD subframe in the order 36.211 6.3.5 maps them: for each OFDM symbol
+    l >= npdcch, increasing subcarrier k over the allocated PRBs.  Excluded: the CRS of the ports
+    in use (6.10.1.2: k = 6m + (v + v_shift) mod 6 with v = 0 / 3 in symbols 0 / N_symb-3 of each
+    slot, ports 0 and 1 swapped; 1 port when crs_ports == 1), PBCH (6.6.4: subframe 0, slot 1
+    symbols 0-3, the 72 centre subcarriers) and the FDD synchronisation signals (6.11: subframes
+    0 and 5, the last two symbols of slot 0, the 72 centre subcarriers).  Subcarrier k sits in FFT
+    bin first_carrier + k below DC and k - 6 N_RB + 1 above it (the DC bin is unused).
+    Returns a list of (l, bin, rb)."""
+    nsymb = 14 if Ncp == 0 else 12
+    nsl = nsymb // 2
+    out = []
+    for l in range(npdcch, nsymb):
+        ls = l % nsl
+        crs_sym = ls == 0 or ls == nsl - 3
+        pbch = subframe == 0 and nsl <= l < nsl + 4
+        sync = subframe in (0, 5) and l in (nsl - 2, nsl - 1)
+        for rb in range(N_RB):
+            if rb_alloc is not None and not (rb_alloc[rb >> 5] >> (rb & 31)) & 1:
+                continue
+            for kk in range(12):
+                k = 12 * rb + kk
+                if crs_sym:
+                    if crs_ports == 1:
+                        if k % 6 == ((0 if ls == 0 else 3) + nushift) % 6:
+                            continue
+                    elif k % 3 == nushift % 3:          # ports 0 and 1: v and v + 3
+                        continue
+                if (pbch or sync) and 6 * N_RB - 36 <= k < 6 * N_RB + 36:
+                    continue
+                b = first_carrier + k
+                out.append((l, b if b < N else b - N + 1, rb))
+    return out
+
+
+def crs_symbol(l, Ncp=0):
+    nsl = 7 if Ncp == 0 else 6
+    return l % nsl in (0, nsl - 3)
+
+
+def qam(bits, Qm, ampr, raw16=None, raw64=None):
+    """One modulation symbol (36.211 7.1) in the reference's fixed point: QPSK +-(ampr/sqrt2)
+    ((ampr * 23170) >> 15, bit 1 -> negative); 16/64-QAM (level * ampr) >> 15 with the levels
+    kept as the reference's int16 Q15 tables (the 64-QAM 7/sqrt42 entry wraps, see QAM64_RAW)."""
+    if Qm == 2:
+        g = (ampr * 23170) >> 15
+        return (-g if bits[0] else g, -g if bits[1] else g)
+    raw = QAM16_RAW if Qm == 4 else QAM64_RAW
+    ir, ii = _sym_index(bits, Qm)
+    return ((raw[ir] * ampr) >> 15, (raw[ii] * ampr) >> 15)
+
+
+def _pack(grid):
+    out = (grid[..., 0] & 0xFFFF) | ((grid[..., 1] & 0xFFFF) << 16)
+    return out.astype(np.uint32).view(np.int32)
+
+
+def siso_grid(e, res, Qm, n_ant, N, amp=512, srho_a=8192, srho_b=8192, Ncp=0):
+    """Single-layer PDSCH grid of one subframe (36.211 6.3.4.1: one antenna port, no precoding):
+    consecutive Qm bits -> one symbol -> the next RE of res.  PDSCH EPRE: rho_A in symbols without
+    CRS, rho_B in symbols with CRS (36.213 5.2), amp_rho = (amp * sqrt_rho) >> 13 in Q13.  The
+    reference writes the port-0 symbol to every TX antenna (dlsch_modulation.c:266-273)."""
+    nsymb = 14 if Ncp == 0 else 12
+    grid = np.zeros((n_ant, nsymb * N, 2), dtype=np.int64)
+    ra, rb_ = (amp * srho_a) >> 13, (amp * srho_b) >> 13
+    for i, (l, b, _) in enumerate(res):
+        x = qam([int(v) for v in e[Qm * i:Qm * i + Qm]], Qm, rb_ if crs_symbol(l, Ncp) else ra)
+        for a in range(n_ant):
+            grid[a, l * N + b] = (_w16(x[0]), _w16(x[1]))
+    return _pack(grid), Qm * len(res)
+
+
+def cdd2_grid(e0, e1, res, Qm0, Qm1, N, amp=512, srho_a=8192, srho_b=8192, Ncp=0, sign_reset_per_rb=False):
+    """Two-layer large-delay CDD on 2 antenna ports (36.211 6.3.4.2.2, codebook index 0):
+    y(i) = W D(i) U x(i) with W = I/sqrt2, U = [[1, 1], [1, -1]]/sqrt2, D(i) = diag(1, (-1)^i),
+    i.e. y0 = (x0 + x1)/2, y1 = (-1)^i (x0 - x1)/2; layer i of codeword q carries its codeword's
+    i-th symbol (6.3.3.2, two codewords, one layer each).  Fixed-point rule of the reference
+    (dlsch_modulation.c:720-727): floor halving of the int16 sums, sign applied after the
+    floor, accumulated into int16.  The reference counts i per resource block (its sign s is
+    reset to +1 at every allocate_REs_in_RB call, :198, :748): sign_reset_per_rb=True models that;
+    the two agree whenever every RB contributes an even number of REs."""
+    nsymb = 14 if Ncp == 0 else 12
+    grid = np.zeros((2, nsymb * N, 2), dtype=np.int64)
+    ra, rb_ = (amp * srho_a) >> 13, (amp * srho_b) >> 13
+    prev, i_rb = None, 0
+    for i, (l, b, rb) in enumerate(res):
+        if (l, rb) != prev:
+            prev, i_rb = (l, rb), 0
+        ampr = rb_ if crs_symbol(l, Ncp) else ra
+        x0 = qam([int(v) for v in e0[Qm0 * i:Qm0 * i + Qm0]], Qm0, ampr)
+        x1 = qam([int(v) for v in e1[Qm1 * i:Qm1 * i + Qm1]], Qm1, ampr)
+        s = -1 if (i_rb if sign_reset_per_rb else i) % 2 else 1
+        grid[0, l * N + b] = (_w16((x0[0] + x1[0]) >> 1), _w16((x0[1] + x1[1]) >> 1))
+        grid[1, l * N + b] = (_w16(s * ((x0[0] - x1[0]) >> 1)), _w16(s * ((x0[1] - x1[1]) >> 1)))
+        i_rb += 1
+    return _pack(grid), len(res)

@@ -236,7 +236,7 @@ def test_pipeline_bandwidths(gpu, name, N_RB):
     mcs = gpu.CONFIGS[name]["mcs"]
     alloc = {6: gpu.FULL_ALLOC_6, 15: gpu.FULL_ALLOC_15, 25: gpu.FULL_ALLOC_25, 50: gpu.FULL_ALLOC_50}[N_RB]
     _pipeline_check(gpu, name, 10, 0, 1, seed=N_RB, N_RB_DL=N_RB, rb_alloc=alloc, nb_rb=N_RB, num_pdcch_symbols=2,
-                    TBS=tuple(gpu.TBS_TABLE[(m, N_RB)] if m else 0 for m in mcs))
+                    TBS=tuple(gpu.tbs_bits(m, N_RB) if m else 0 for m in mcs))
 
 
 @pytest.mark.parametrize("nid,ncp,crs", [(0, 0, 0), (13, 0, 1), (301, 0, 1), (5, 1, 0), (8, 1, 1)])
