@@ -31,35 +31,90 @@ def algorithmic_bytes(p, spt):
     return payload, iq
 
 
-def _traffic(config, kernel):
-    """calibrated HBM bytes per launch from the committed rocprofv3 PMC summary (tools/summarize_prof.py)"""
+def _traffic(config, kernel, batch):
+    """Calibrated HBM bytes per launch from the committed rocprofv3 PMC summary
+    (tools/summarize_prof.py), only when it was measured at this batch size (else null)."""
     tpath = os.path.join(ROOT, "profiles", f"traffic_{config}.json")
     try:
-        return json.load(open(tpath)).get(kernel)
+        t = json.load(open(tpath))
     except Exception:
         return None
+    return t.get(kernel) if t.get("batch") == batch else None
+
+
+def cpu_model():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def host_cores():
+    """Cores this process may use (the GPU box's CPU share is 16 however many the machine shows)."""
+    try:
+        n = len(os.sched_getaffinity(0))
+    except AttributeError:
+        n = os.cpu_count() or 1
+    return max(1, min(n, int(os.environ.get("OMP_NUM_THREADS", "16") or 16), 16))
+
+
+_PORT_WORKER = r"""
+import sys, time, numpy as np
+sys.path.insert(0, sys.argv[1]); sys.path.insert(0, sys.argv[1] + '/tests')
+import oracle_lib as O, openair4g_amd as oai
+p = oai.make_params(sys.argv[2], subframe=int(sys.argv[3]))
+cfg = O.tx_cfg_from_params(p, int(sys.argv[3]))
+rng = np.random.default_rng(int(sys.argv[5]))
+pays = [rng.integers(0, 256, size=p.TBS[cw] // 8 + 8, dtype=np.uint8) for cw in range(p.n_cw)]
+O.tx_subframe(cfg, pays)
+n, t0 = 0, time.perf_counter()
+while time.perf_counter() - t0 < float(sys.argv[4]):
+    O.tx_subframe(cfg, pays); n += 1
+print(n, time.perf_counter() - t0)
+"""
+
+
+def _port_rate(name, subframe, seconds, procs):
+    """The oracle port in `procs` independent processes for `seconds`: aggregate subframes/s."""
+    import subprocess
+    ps = [subprocess.Popen([sys.executable, "-c", _PORT_WORKER, ROOT, name, str(subframe), str(seconds), str(i)],
+                           stdout=subprocess.PIPE, text=True) for i in range(procs)]
+    tot, n_all = 0.0, 0
+    for p in ps:
+        out, _ = p.communicate()
+        n, dt = out.split()
+        tot += int(n) / float(dt)
+        n_all += int(n)
+    return tot, n_all
 
 
 def cpu_baseline(name, seconds, subframe):
-    """Oracle ("port") timed on one host core over a bounded sample of the same workload."""
-    import numpy as np
-    sys.path.insert(0, os.path.join(ROOT, "tests"))
-    import oracle_lib as O
-    import openair4g_amd as oai
-    p = oai.make_params(name, subframe=subframe)
-    cfg = O.tx_cfg_from_params(p, subframe)
-    rng = np.random.default_rng(1)
-    pays = [rng.integers(0, 256, size=p.TBS[cw] // 8 + 8, dtype=np.uint8) for cw in range(p.n_cw)]
-    n = 0
-    t0 = time.perf_counter()
-    while True:
-        O.tx_subframe(cfg, pays)
-        n += 1
-        if time.perf_counter() - t0 >= seconds:
-            break
-    dt = time.perf_counter() - t0
-    return {"value": n / dt, "unit": "subframes/s", "cores": 1, "kind": "port",
-            "sample": f"{n} subframes of {name} (sf {subframe}) through the C oracle, single thread, {dt:.1f} s"}
+    """The oracle ("port") on the host cores over a bounded sample of the same workload: one core,
+    then every core of this process's share (independent processes, as N dlsim instances would
+    run), plus the reference-equivalent rate through BASELINE.md section 3's calibration
+    (profiles/cpu_calibration.json: the reference TUs' 870 subframes/s/core measured by the survey
+    in the build container vs the port's rate measured in the same container)."""
+    one, n1 = _port_rate(name, subframe, seconds, 1)
+    cores = host_cores()
+    allc, nall = _port_rate(name, subframe, max(2.0, seconds / 2), cores) if cores > 1 else (one, n1)
+    cal = None
+    try:
+        cal = json.load(open(os.path.join(ROOT, "profiles", "cpu_calibration.json"))).get(name)
+    except Exception:
+        pass
+    out = {"value": one, "unit": "subframes/s", "cores": 1, "kind": "port", "cpu_model": cpu_model(),
+           "value_all_cores": allc, "cores_all": cores,
+           "sample": f"{n1} subframes of {name} (sf {subframe}) through the C oracle on 1 core in {seconds:.0f} s; "
+                     f"{nall} on {cores} cores (independent processes)"}
+    if cal:
+        r = cal["ref_per_core"] / cal["port_per_core"]
+        out["ref_equiv_per_core"] = one * r
+        out["ref_equiv_all_cores"] = allc * r
+        out["calibration"] = cal
+    return out
 
 
 C5_K, C5_CB = 5504, 8          # UL 100 PRB MCS 20: TBS 43816 -> C = 8 blocks of K = 5504 (SURVEY 8d)
@@ -147,7 +202,7 @@ def bench_c5(args, world, rank, dist, torch):
                        "config_id": "C5", "subframes_per_gpu_per_step": n_sf, "code_blocks_per_step": n_cb,
                        "mean_iterations": float(np.mean(its)), "parallelism": f"block-sharded x{world}"},
             "roofline": {"bound": "hbm", "kernel": "k_td16", "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": ach / HBM_PEAK_GBS, "traffic": _traffic("C5", "k_td16"),
+                         "frac": ach / HBM_PEAK_GBS, "traffic": _traffic("C5", "k_td16", n_sf),
                          "note": "latency-bound: traffic (scratch streaming per half-iteration) >> algorithmic bytes"},
             "cpu_baseline": cpu}), flush=True)
 
@@ -234,9 +289,128 @@ def bench_fep(args, world, rank, dist, torch):
             "config": {"workload": "slot_fep 20 MHz normal CP, 2 RX antennas, 14 x dft2048 per antenna",
                        "config_id": "FEP", "subframes_per_gpu_per_step": n_sf, "parallelism": f"subframe-sharded x{world}"},
             "roofline": {"bound": "hbm", "kernel": "k_fep<11>", "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": ach / HBM_PEAK_GBS, "traffic": _traffic("FEP", "k_fep<11>"), "kernel_ms": kern_ms,
+                         "frac": ach / HBM_PEAK_GBS, "traffic": _traffic("FEP", "k_fep<11>", n_sf), "kernel_ms": kern_ms,
                          "algorithmic_bytes_per_launch": alg},
             "cpu_baseline": cpu}), flush=True)
+
+
+def launch_ranks(n, argv):
+    """`bench.py --gpus N` without a launcher: start N fresh child processes of this script, one
+    per GPU (RANK / LOCAL_RANK / WORLD_SIZE / MASTER_ADDR / MASTER_PORT as torch.distributed.run
+    sets them), before this process imports torch or touches a GPU.  Rank 0's JSON line reaches
+    stdout directly; a failing rank stops the others and the exit code is non-zero."""
+    import signal
+    import socket
+    import subprocess
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + argv, env=env))
+    rc = 0
+    live = set(range(n))
+    while live:
+        for r in sorted(live):
+            c = procs[r].poll()
+            if c is None:
+                continue
+            live.discard(r)
+            if c != 0 and rc == 0:
+                rc = c if c > 0 else 128 - c
+                print(f"bench: rank {r} exited with {c}; stopping the other ranks", file=sys.stderr)
+                for q in live:
+                    procs[q].send_signal(signal.SIGTERM)
+        time.sleep(0.05)
+    return rc
+
+
+class Host:
+    """Device-side plumbing of the timing harness: RCCL + HIP on the GPU, or (--cpu-stub) gloo on
+    the CPU so the rank / broadcast / barrier / max-reduce code runs in the CPU test suite."""
+
+    def __init__(self, args, world, rank, local_rank):
+        import torch
+        self.torch, self.world, self.rank, self.dist = torch, world, rank, None
+        self.stub = args.cpu_stub
+        self.device = "cpu" if self.stub else "cuda"
+        if not self.stub:
+            torch.cuda.set_device(local_rank)
+        if world > 1:
+            import torch.distributed as dist
+            self.dist = dist
+            if self.stub or args.backend == "gloo":
+                dist.init_process_group(args.backend)
+            else:
+                dist.init_process_group(args.backend, device_id=torch.device("cuda", local_rank))
+
+    def sync(self):
+        if not self.stub:
+            self.torch.cuda.synchronize()
+
+    def barrier(self):
+        if self.dist is not None:
+            self.dist.barrier()
+
+    def max_over_ranks(self, v):
+        if self.dist is None:
+            return v
+        t = self.torch.tensor([v], dtype=self.torch.float64, device=self.device)
+        self.dist.all_reduce(t, op=self.dist.ReduceOp.MAX)
+        return float(t.item())
+
+    def sum_over_ranks(self, v):
+        if self.dist is None:
+            return v
+        t = self.torch.tensor([v], dtype=self.torch.float64, device=self.device)
+        self.dist.all_reduce(t, op=self.dist.ReduceOp.SUM)
+        return float(t.item())
+
+    def close(self):
+        if self.dist is not None:
+            self.dist.destroy_process_group()
+
+
+class StubPipeline:
+    """CPU stand-in for TxPipeline under --cpu-stub (harness test only: no GPU, no oracle): the
+    same methods, a payload-sized XOR fold per subframe as the 'work'."""
+
+    def __init__(self, params, n_sf):
+        import numpy as np
+        import openair4g_amd as oai
+        self.np, self.params, self.n_sf = np, params, n_sf
+        self.spt = 30720 if params.N_RB_DL == 100 else 1920
+        self.fp = oai.frame_parms(params.N_RB_DL, params.Nid_cell, params.Ncp, params.nb_antennas_tx,
+                                  params.mode1_flag, 0)
+        self.checksum = 0
+
+    def fill_payload(self, seed):
+        rng = self.np.random.default_rng(seed)
+        self.pay = rng.integers(0, 2 ** 63, size=(self.n_sf, self.params.payload_stride // 8), dtype=self.np.uint64)
+
+    def run(self, stream=None):
+        self.checksum ^= int(self.np.bitwise_xor.reduce(self.pay, axis=None))
+
+    def run_timed(self, stream=None):
+        t0 = time.perf_counter()
+        self.run()
+        t1 = time.perf_counter()
+        self.run()
+        return (t1 - t0) * 1e3, (time.perf_counter() - t1) * 1e3
+
+    def G(self, cw, subframe):
+        import openair4g_amd as oai
+        p = self.params
+        Qm = oai.lib().oai4g_get_Qm(p.mcs[cw])
+        return oai.get_G(self.fp, p.nb_rb, list(p.rb_alloc), Qm, 1, p.num_pdcch_symbols, subframe)
+
+    def sync(self):
+        pass
+
+    def close(self):
+        pass
 
 
 def main():
@@ -246,63 +420,72 @@ def main():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--config", default="C3")
     ap.add_argument("--batch", type=int, default=None,
-                    help="subframes per GPU per step (default: C3 8192, C4 4096, FEP 8192, C5 2048); measured on "
-                         "C3: 2048 -> 4.20M, 5120 -> 4.56M, 10240 -> 4.67M subframes/s (launch tails amortised)")
+                    help="subframes per GPU per step (default: C3 8192, C4 1024 = BASELINE config 4's 8192 over "
+                         "8 GPUs, FEP 8192, C5 2048); measured on C3: 2048 -> 4.20M, 5120 -> 4.56M, 10240 -> 4.67M "
+                         "subframes/s (launch tails amortised)")
     ap.add_argument("--subframe", type=int, default=7)
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--kernel-reps", type=int, default=5, help="serial runs timed per kernel for the roofline")
     ap.add_argument("--c5-mode", default="8it", choices=["8it", "snr"], help="C5 decoder inputs")
+    ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"], help="nccl = RCCL on ROCm")
+    ap.add_argument("--cpu-stub", action="store_true",
+                    help="harness test on CPU: gloo, StubPipeline, no GPU (exercises ranks/broadcast/timing)")
     args = ap.parse_args()
     if args.batch is None:
-        args.batch = {"C3": 8192, "C4": 4096, "FEP": 8192}.get(args.config, 2048)
+        args.batch = {"C3": 8192, "C4": 1024, "FEP": 8192}.get(args.config, 2048)
+    if args.cpu_stub:
+        args.backend = "gloo"
 
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(launch_ranks(args.gpus, sys.argv[1:]))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        print(f"bench: --gpus {args.gpus} but WORLD_SIZE={world}", file=sys.stderr)
+        sys.exit(2)
 
-    import torch
-    dist = None
-    if world > 1:
-        import torch.distributed as dist
-        torch.cuda.set_device(local_rank)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
-    else:
-        torch.cuda.set_device(0)
-
+    host = Host(args, world, rank, local_rank)
+    torch, dist = host.torch, host.dist
     if args.config in ("C5", "FEP"):
+        if host.stub:
+            sys.exit("bench: --cpu-stub covers the transmit configurations only")
         (bench_c5 if args.config == "C5" else bench_fep)(args, world, rank, dist, torch)
-        if dist is not None:
-            dist.destroy_process_group()
+        host.close()
         return
+    bench_tx(args, world, rank, host)
+    host.close()
 
+
+def bench_tx(args, world, rank, host):
+    """Transmit path (C1-C4): a step = one pass of encode + modulate/IDFT/CP over the batch."""
     import openair4g_amd as oai
-    oai.init()
-
     from openair4g_amd import dist as odist
+    dist = host.dist
+    if not host.stub:
+        oai.init()
     # ---- parameter block: built on rank 0, broadcast over RCCL (the only collective) ----
     p0 = oai.make_params(args.config, subframe=args.subframe) if rank == 0 else None
-    params = odist.broadcast_params(p0, dist, device="cuda") if dist is not None else p0
+    params = odist.broadcast_params(p0, dist, device=host.device) if dist is not None else p0
 
-    pipe = oai.TxPipeline(params, args.batch)
+    pipe = (StubPipeline if host.stub else oai.TxPipeline)(params, args.batch)
     pipe.fill_payload(seed=odist.payload_seed(0x5EED0000, rank))   # this rank's shard of synthetic TBs
     pipe.sync()
 
     for _ in range(args.warmup):
         pipe.run()
     pipe.sync()
-    torch.cuda.synchronize()
+    host.sync()
 
-    if dist is not None:
-        dist.barrier()
-    torch.cuda.synchronize()
+    host.barrier()
+    host.sync()
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        pipe.run()                # encoder and modulator/IDFT overlapped chunk-wise on two streams
+        pipe.run()
     pipe.sync()
-    torch.cuda.synchronize()
-    if dist is not None:
-        dist.barrier()
+    host.sync()
+    host.barrier()
     elapsed = time.perf_counter() - t0
 
     # per-kernel launch durations for the roofline: the same batch run serially, HIP events on the
@@ -312,13 +495,10 @@ def main():
         a, b = pipe.run_timed()
         kern[0] += a
         kern[1] += b
-    if dist is not None:
-        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+    elapsed = host.max_over_ranks(elapsed)
+    units = host.sum_over_ranks(args.batch * args.steps)      # subframes all ranks processed
 
-    total_sf = args.batch * args.steps * world
-    value = total_sf / elapsed
+    value = units / elapsed
     ms_per_step = elapsed * 1000.0 / args.steps
 
     payload_b, iq_b = algorithmic_bytes(params, pipe.spt)
@@ -332,13 +512,7 @@ def main():
     }
     dom = max(per_kernel, key=lambda k: per_kernel[k]["ms"])
     ach = per_kernel[dom]["bytes"] / (per_kernel[dom]["ms"] * 1e-3) / 1e9
-    traffic = None
-    tpath = os.path.join(ROOT, "profiles", f"traffic_{args.config}.json")
-    if os.path.exists(tpath):
-        try:
-            traffic = json.load(open(tpath)).get(dom)
-        except Exception:
-            traffic = None
+    traffic = _traffic(args.config, dom, args.batch)
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
@@ -360,7 +534,8 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "int16",
-            "data": "synthetic (device-generated splitmix64 transport blocks, resident in HBM)",
+            "data": "synthetic (device-generated splitmix64 transport blocks, resident in HBM)" if not host.stub
+                    else "cpu-stub harness run (no GPU): not a measurement",
             "config": {"workload": cfgname, "config_id": args.config, "subframes_per_gpu_per_step": args.batch,
                        "global_batch": args.batch * world, "subframe_index": args.subframe,
                        "TBS": [params.TBS[cw] for cw in range(params.n_cw)], "G": G,
@@ -375,8 +550,6 @@ def main():
         print(json.dumps(out), flush=True)
 
     pipe.close()
-    if dist is not None:
-        dist.destroy_process_group()
 
 
 if __name__ == "__main__":

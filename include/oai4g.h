@@ -231,7 +231,9 @@ int oai4g_lte_rate_matching_turbo_rx(uint32_t RTC, uint32_t G, int16_t *w, const
 void oai4g_sub_block_deinterleaving_turbo(uint32_t D, int16_t *d, const int16_t *w);
 /* Batched decoder, device pointers: n_cb blocks of size K, llr [n_cb][llr_stride] int16
  * (3K+12 each), out [n_cb][out_stride] bytes (K/8 each), iters [n_cb]; scratch of
- * oai4g_td_scratch_bytes(K, n_cb) bytes.  Asynchronous on `stream`. */
+ * oai4g_td_scratch_bytes(K, n_cb) bytes.  Asynchronous on `stream`.  As the reference's
+ * decoded_bytes, a block's out row is written only by hard decisions (iteration >= 2): with
+ * max_iterations = 1 it keeps the caller's previous contents. */
 size_t oai4g_td_scratch_bytes(uint16_t K, int n_cb);
 int oai4g_td_batch(int n_cb, uint16_t K, const int16_t *d_llr, size_t llr_stride, uint8_t *d_out, size_t out_stride,
                    uint8_t *d_iters, uint8_t max_iterations, uint8_t crc_type, uint8_t F, void *d_scratch,

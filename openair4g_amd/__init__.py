@@ -443,6 +443,10 @@ class TurboDecoderBatch:
         self.d_it = self.L.oai4g_dev_alloc(max(256, n_cb))
         self.d_scr = self.L.oai4g_dev_alloc(self.L.oai4g_td_scratch_bytes(K, n_cb))
         _check(all([self.d_llr, self.d_out, self.d_it, self.d_scr]))
+        # the decoder writes d_out only once a hard decision is made (iteration >= 2), as the
+        # reference leaves decoded_bytes untouched at max_iterations = 1: start from a zeroed buffer
+        z = np.zeros(n_cb * (K // 8), dtype=np.uint8)
+        _check(self.L.oai4g_memcpy_h2d(self.d_out, _ptr(z), z.nbytes) == 0)
 
     def upload(self, llr):
         buf = np.zeros((self.n_cb, self.llr_stride), dtype=np.int16)

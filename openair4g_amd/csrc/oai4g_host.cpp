@@ -1913,9 +1913,9 @@ extern "C" int oai4g_fep_batch(const oai4g_frame_parms_t *fp, int n_sf, int n_an
  * Control region: PCFICH (pcfich.c:48-228)
  * ---------------------------------------------------------------------------------------- */
 /* generate_pcfich_reg_mapping (pcfich.c:48-84): the four REGs (units of 6 REs from the first
- * carrier) and the index of the lowest; prints them as the reference does */
-extern "C" void oai4g_generate_pcfich_reg_mapping(const oai4g_frame_parms_t *fp, uint16_t pcfich_reg[4],
-                                                  uint8_t *pcfich_first_reg_idx)
+ * carrier) and the index of the lowest.  The silent helper serves generate_pcfich; the exported
+ * drop-in prints them as the reference does (once, at init, in the reference's callers). */
+static void pcfich_regs(const oai4g_frame_parms_t *fp, uint16_t pcfich_reg[4], uint8_t *pcfich_first_reg_idx)
 {
   const uint32_t NRB = fp->N_RB_DL, kbar = 6 * (fp->Nid_cell % (2 * NRB));
   uint16_t first;
@@ -1930,6 +1930,12 @@ extern "C" void oai4g_generate_pcfich_reg_mapping(const oai4g_frame_parms_t *fp,
       first = pcfich_reg[i];
     }
   }
+}
+
+extern "C" void oai4g_generate_pcfich_reg_mapping(const oai4g_frame_parms_t *fp, uint16_t pcfich_reg[4],
+                                                  uint8_t *pcfich_first_reg_idx)
+{
+  pcfich_regs(fp, pcfich_reg, pcfich_first_reg_idx);
   printf("pcfich_reg : %d,%d,%d,%d\n", pcfich_reg[0], pcfich_reg[1], pcfich_reg[2], pcfich_reg[3]);
 }
 
@@ -1948,7 +1954,7 @@ extern "C" int oai4g_generate_pcfich(uint8_t num_pdcch_symbols, int16_t amp, con
   }
   uint16_t reg[4];
   uint8_t first_idx;
-  oai4g_generate_pcfich_reg_mapping(fp, reg, &first_idx);
+  pcfich_regs(fp, reg, &first_idx);
   const uint32_t N = fp->ofdm_symbol_size, nsymb = fp->Ncp == 0 ? 14 : 12;
   const size_t symbol_offset = (size_t)N * subframe * nsymb;
   pcfich_args_t a;

@@ -104,30 +104,21 @@ _refc = None
 
 
 def ref_coding():
-    """The reference's own coding TUs (oracle/_ref/libref_coding.so: crc_byte.c, 3gpplte_sse.c,
-    3gpplte_turbo_decoder_sse_16bit.c / _8bit.c, ccoding_byte_lte.c), initialised as the
-    reference's phy_init_lte_top does (lte_init.c:880-910: crcTableInit, init_td16/8,
-    ccodelte_init), or None when it was not built here (the GPU box never has it)."""
+    """The reference's own CRC and tail-biting convolutional coder (oracle/_ref/libref_coding.so:
+    PHY/CODING/crc_byte.c, ccoding_byte_lte.c, compiled unmodified), initialised as the reference's
+    phy_init_lte_top does (lte_init.c: crcTableInit, ccodelte_init), or None when it was not built
+    here (the GPU box never has it)."""
     global _refc
     if _refc is None:
         if not os.path.exists(REF_CODING_SO):
             return None
         L = ctypes.CDLL(REF_CODING_SO)
-        L.ref_qpp_init()
         L.crcTableInit()
-        L.init_td16()
-        L.init_td8()
         L.ccodelte_init()
         L.crc24a.restype = ctypes.c_uint32
         L.crc24b.restype = ctypes.c_uint32
         L.crc16.restype = ctypes.c_uint32
         L.crc8.restype = ctypes.c_uint32
-        L.threegpplte_turbo_encoder.argtypes = [ctypes.c_void_p, ctypes.c_uint16, ctypes.c_void_p, ctypes.c_uint8,
-                                                ctypes.c_uint16, ctypes.c_uint16]
-        for fn in (L.phy_threegpplte_turbo_decoder16, L.phy_threegpplte_turbo_decoder8):
-            fn.restype = ctypes.c_uint8
-            fn.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint16, ctypes.c_uint16, ctypes.c_uint16,
-                           ctypes.c_uint8, ctypes.c_uint8, ctypes.c_uint8] + [ctypes.c_void_p] * 7
         L.ccodelte_encode.argtypes = [ctypes.c_int32, ctypes.c_uint8, ctypes.c_void_p, ctypes.c_void_p,
                                       ctypes.c_uint16]
         _refc = L
@@ -139,30 +130,6 @@ def _aligned(n, dtype, align=64):
     raw = np.zeros(n + align // itemsize, dtype=dtype)
     off = (-raw.ctypes.data % align) // itemsize
     return raw[off:off + n]
-
-
-def ref_turbo_encode(c, F=0):
-    """threegpplte_turbo_encoder (3gpplte_sse.c:380-476) of the reference on K/8 bytes c:
-    3K+12 output bytes (x, z, z') per bit then the 12 tail bits."""
-    L = ref_coding()
-    c = np.ascontiguousarray(c, dtype=np.uint8)
-    K = 8 * len(c)
-    src = _aligned(len(c) + 16, np.uint8)
-    src[:len(c)] = c
-    d = _aligned(3 * K + 12 + 32, np.uint8)
-    L.threegpplte_turbo_encoder(P(src), len(c), P(d), F, 0, 0)
-    return d[:3 * K + 12].copy()
-
-
-def ref_turbo_decode(y, K, max_it=8, crc_type=0, F=0, bits=16):
-    """phy_threegpplte_turbo_decoder16 / 8 of the reference: (return value, K/8 decoded bytes)."""
-    L = ref_coding()
-    src = _aligned(3 * K + 12 + 64, np.int16)
-    src[:3 * K + 12] = np.asarray(y, dtype=np.int16)[:3 * K + 12]
-    out = _aligned(K // 8 + 16, np.uint8)
-    fn = L.phy_threegpplte_turbo_decoder16 if bits == 16 else L.phy_threegpplte_turbo_decoder8
-    it = fn(P(src), P(out), K, 0, 0, max_it, crc_type, F, None, None, None, None, None, None, None)
-    return it, out[:K // 8].copy()
 
 
 def ref_crc(data, bitlen, kind="24a"):

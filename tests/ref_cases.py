@@ -1,8 +1,7 @@
-"""Seeded input cases shared by the reference pin (tests/test_ref_pin_cpu.py, live against
-oracle/_ref) and the golden fixture tests/golden/ref_coding.npz (tests/golden/gen_ref_coding.py),
-which carries the reference's outputs for the same cases to the GPU box
-(tests/test_gpu_ref_golden.py).  TEST INFRASTRUCTURE: the inputs are built with the oracle's
-encoder / CRC, which are themselves pinned to the reference by test_ref_pin_cpu.py."""
+"""Seeded decoder / encoder input cases shared by the CPU pins (tests/test_td_spec_cpu.py) and the
+GPU parity tests (tests/test_gpu_decoder_cases.py).  TEST INFRASTRUCTURE: the inputs are built
+with the oracle's encoder / CRC, which are pinned to tests/spec_model.py and to the reference's
+own crc_byte.c (tests/test_ref_pin_cpu.py)."""
 import hashlib
 import os
 import re

@@ -20,9 +20,9 @@ FULL = {6: (0x3F, 0, 0, 0), 15: (0x7FFF, 0, 0, 0), 25: (0x1FFFFFF, 0, 0, 0),
         50: (0xFFFFFFFF, 0x3FFFF, 0, 0), 100: (0xFFFFFFFF, 0xFFFFFFFF, 0xFFFFFFFF, 0xF)}
 
 
-def run_case(name, N_RB, mcs, sf, nid, npdcch):
+def run_case(name, N_RB, mcs, sf, nid, npdcch, tbs=None):
     import openair4g_amd as oai
-    tbs = tuple(oai.tbs_bits(m, N_RB) if m else 0 for m in mcs)
+    tbs = tbs or tuple(oai.tbs_bits(m, N_RB) if m else 0 for m in mcs)
     kw = dict(N_RB_DL=N_RB, rb_alloc=FULL[N_RB], nb_rb=N_RB, num_pdcch_symbols=npdcch, mcs=mcs, TBS=tbs)
     p = oai.make_params(name, subframe=sf, Nid_cell=nid, **kw)
     cfg = O.tx_cfg_from_params(p, sf)
@@ -65,3 +65,14 @@ def test_config_grid_matches_spec(case, sf):
 def test_bandwidth_sweep_matches_spec(name, mcs, N_RB, nid, sf):
     """odd N_RB (DC-straddling RB, half-RB PBCH/sync edges) and every CRS shift class"""
     run_case(name, N_RB, mcs, sf, nid, 2)
+
+
+@pytest.mark.parametrize("case", [("C1", 6, (9, 0), (1008, 0)), ("C2", 100, (16, 0), (10008, 0)),
+                                  ("C3", 100, (19, 19), (30008, 20000))], ids=lambda c: c[0])
+def test_filler_bits_match_spec(case):
+    """Non-table TBS whose segmentation leaves F > 0 filler bits (A6q: encoded as 0,
+    3gpplte_sse.c:380-476 / lte_segmentation.c:137-139), end to end through the grid."""
+    name, N_RB, mcs, tbs = case
+    B = tbs[0] + 24
+    assert S.segment([0] * B)[1] > 0
+    run_case(name, N_RB, mcs, 7, 1, 2, tbs=tbs)
