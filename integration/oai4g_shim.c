@@ -1,0 +1,190 @@
+/* oai4g_shim.c — reference-side binding of the MI355X DLSCH transmit path.
+ * Replaces: dlsch_coding.c:254 dlsch_encoding, dlsch_scrambling.c:51, dlsch_modulation.c:1181,
+ * ofdm_mod.c:47/85/233, lte_dfts.c idft64..idft2048, crc_byte.c:117/135, lte_segmentation.c:39,
+ * 3gpplte_sse.c:380, lte_rate_matching.c:51/464. */
+#include "PHY/defs.h"
+#include "PHY/extern.h"
+#include "oai4g.h"
+
+static void fp_to(const LTE_DL_FRAME_PARMS *f, oai4g_frame_parms_t *o)
+{
+  memset(o, 0, sizeof(*o));
+  o->N_RB_DL = f->N_RB_DL;            o->Nid_cell = f->Nid_cell;
+  o->Ncp = f->Ncp;                    o->nushift = f->nushift;
+  o->mode1_flag = f->mode1_flag;      o->nb_antennas_tx = f->nb_antennas_tx;
+  o->frame_type = f->frame_type;      o->symbols_per_tti = f->symbols_per_tti;
+  o->log2_symbol_size = f->log2_symbol_size;
+  o->ofdm_symbol_size = f->ofdm_symbol_size;
+  o->first_carrier_offset = f->first_carrier_offset;
+  o->nb_prefix_samples = f->nb_prefix_samples;
+  o->nb_prefix_samples0 = f->nb_prefix_samples0;
+  o->samples_per_tti = f->samples_per_tti;
+}
+
+/* The mirror points INTO the reference's own HARQ buffers, so every write lands in place. */
+typedef struct { oai4g_dlsch_t d; oai4g_dl_harq_t h[8]; } shim_dlsch_t;
+
+static void harq_to(LTE_DL_eNB_HARQ_t *r, oai4g_dl_harq_t *o)
+{
+  int i;
+  o->TBS = r->TBS;  o->B = r->B;  o->b = r->b;
+  for (i = 0; i < MAX_NUM_DLSCH_SEGMENTS; i++) {
+    o->c[i] = r->c[i];  o->d[i] = r->d[i];  o->w[i] = r->w[i];  o->RTC[i] = r->RTC[i];
+  }
+  o->round = r->round;  o->mcs = r->mcs;  o->rvidx = r->rvidx;  o->mimo_mode = r->mimo_mode;
+  memcpy(o->rb_alloc, r->rb_alloc, sizeof(o->rb_alloc));
+  o->nb_rb = r->nb_rb;  o->e = r->e;
+  o->C = r->C;  o->Cminus = r->Cminus;  o->Cplus = r->Cplus;
+  o->Kminus = r->Kminus;  o->Kplus = r->Kplus;  o->F = r->F;
+  o->Nl = r->Nl;  o->Nlayers = r->Nlayers;  o->first_layer = r->first_layer;
+}
+
+static void harq_from(const oai4g_dl_harq_t *o, LTE_DL_eNB_HARQ_t *r)
+{
+  int i;   /* scalar outputs of segmentation / sub-block interleaving */
+  r->B = o->B;  r->C = o->C;  r->Cminus = o->Cminus;  r->Cplus = o->Cplus;
+  r->Kminus = o->Kminus;  r->Kplus = o->Kplus;  r->F = o->F;
+  for (i = 0; i < MAX_NUM_DLSCH_SEGMENTS; i++) r->RTC[i] = o->RTC[i];
+}
+
+static oai4g_dlsch_t *dlsch_to(LTE_eNB_DLSCH_t *r, shim_dlsch_t *s)
+{
+  int i;
+  if (!r) return NULL;
+  s->d.rnti = r->rnti;  s->d.current_harq_pid = r->current_harq_pid;
+  s->d.Mdlharq = r->Mdlharq;  s->d.Kmimo = r->Kmimo;
+  s->d.sqrt_rho_a = r->sqrt_rho_a;  s->d.sqrt_rho_b = r->sqrt_rho_b;
+  for (i = 0; i < 8; i++) {
+    s->d.harq_processes[i] = r->harq_processes[i] ? &s->h[i] : NULL;
+    if (r->harq_processes[i]) harq_to(r->harq_processes[i], &s->h[i]);
+  }
+  return &s->d;
+}
+
+int32_t dlsch_encoding(uint8_t *a, LTE_DL_FRAME_PARMS *frame_parms, uint8_t num_pdcch_symbols,
+                       LTE_eNB_DLSCH_t *dlsch, int frame, uint8_t subframe,
+                       time_stats_t *rm_stats, time_stats_t *te_stats, time_stats_t *i_stats)
+{
+  oai4g_frame_parms_t fp;  shim_dlsch_t s;  int ret;
+  fp_to(frame_parms, &fp);
+  ret = oai4g_dlsch_encoding(a, &fp, num_pdcch_symbols, dlsch_to(dlsch, &s), frame, subframe);
+  harq_from(&s.h[dlsch->current_harq_pid], dlsch->harq_processes[dlsch->current_harq_pid]);
+  return ret;                          /* 0, or -1 like the reference (dlsch_coding.c:316,336) */
+}
+
+void dlsch_scrambling(LTE_DL_FRAME_PARMS *frame_parms, int mbsfn_flag, LTE_eNB_DLSCH_t *dlsch,
+                      int G, uint8_t q, uint8_t Ns)
+{
+  oai4g_frame_parms_t fp;  shim_dlsch_t s;
+  fp_to(frame_parms, &fp);
+  oai4g_dlsch_scrambling(&fp, mbsfn_flag, dlsch_to(dlsch, &s), G, q, Ns);
+}
+
+int32_t dlsch_modulation(mod_sym_t **txdataF, int16_t amp, uint32_t sub_frame_offset,
+                         LTE_DL_FRAME_PARMS *frame_parms, uint8_t num_pdcch_symbols,
+                         LTE_eNB_DLSCH_t *dlsch0, LTE_eNB_DLSCH_t *dlsch1)
+{
+  oai4g_frame_parms_t fp;  shim_dlsch_t s0, s1;
+  fp_to(frame_parms, &fp);
+  return oai4g_dlsch_modulation((int32_t **)txdataF, amp, sub_frame_offset, &fp, num_pdcch_symbols,
+                                dlsch_to(dlsch0, &s0), dlsch_to(dlsch1, &s1));
+}
+
+void PHY_ofdm_mod(int *input, int *output, unsigned char log2fftsize, unsigned char nb_symbols,
+                  unsigned short nb_prefix_samples, Extension_t etype)
+{
+  oai4g_PHY_ofdm_mod(input, output, log2fftsize, nb_symbols, nb_prefix_samples, (int)etype);
+}
+
+void normal_prefix_mod(int32_t *txdataF, int32_t *txdata, uint8_t nsymb, LTE_DL_FRAME_PARMS *frame_parms)
+{
+  oai4g_frame_parms_t fp;
+  fp_to(frame_parms, &fp);
+  oai4g_normal_prefix_mod(txdataF, txdata, nsymb, &fp);
+}
+
+void do_OFDM_mod(mod_sym_t **txdataF, int32_t **txdata, uint32_t frame, uint16_t next_slot,
+                 LTE_DL_FRAME_PARMS *frame_parms)
+{
+  oai4g_frame_parms_t fp;
+  fp_to(frame_parms, &fp);
+  oai4g_do_OFDM_mod((int32_t **)txdataF, txdata, frame, next_slot, &fp);
+}
+
+void idft2048(int16_t *x, int16_t *y, int scale) { oai4g_idft2048(x, y, scale); }
+void idft1024(int16_t *x, int16_t *y, int scale) { oai4g_idft1024(x, y, scale); }
+void idft256(int16_t *x, int16_t *y, int scale)  { oai4g_idft256(x, y, scale); }
+void idft128(int16_t *x, int16_t *y, int scale)  { oai4g_idft128(x, y, scale); }
+void idft64(int16_t *x, int16_t *y, int scale)   { oai4g_idft64(x, y, scale); }
+
+/* UE receive front end: lte_dfts.c dft64..dft2048 (TOOLS/defs.h) and slot_fep.c:40 */
+void dft2048(int16_t *x, int16_t *y, int scale) { oai4g_dft2048(x, y, scale); }
+void dft1024(int16_t *x, int16_t *y, int scale) { oai4g_dft1024(x, y, scale); }
+void dft512(int16_t *x, int16_t *y, int scale)  { oai4g_dft512(x, y, scale); }
+void dft256(int16_t *x, int16_t *y, int scale)  { oai4g_dft256(x, y, scale); }
+void dft128(int16_t *x, int16_t *y, int scale)  { oai4g_dft128(x, y, scale); }
+void dft64(int16_t *x, int16_t *y, int scale)   { oai4g_dft64(x, y, scale); }
+
+int slot_fep(PHY_VARS_UE *ue, unsigned char l, unsigned char Ns, int sample_offset, int no_prefix,
+             int reset_freq_est)
+{
+  oai4g_frame_parms_t fp;
+  fp_to(&ue->lte_frame_parms, &fp);
+  /* CP removal + DFT on the GPU (rxdata keeps its frame + ofdm_symbol_size wrap extension, as
+   * allocated by lte_init.c) */
+  int ret = oai4g_slot_fep((int32_t **)ue->lte_ue_common_vars.rxdata, (int32_t **)ue->lte_ue_common_vars.rxdataF,
+                           &fp, ue->lte_frame_parms.nb_antennas_rx, l, Ns, sample_offset, no_prefix);
+  if (ret != 0) return ret;
+  /* channel and frequency-offset estimation stay on the reference's CPU code (slot_fep.c:179-222) */
+  if (ue->perfect_ce == 0 && (l == 0 || l == 4 - ue->lte_frame_parms.Ncp)) {
+    const unsigned char symbol = l + (7 - ue->lte_frame_parms.Ncp) * (Ns & 1);
+    for (int aa = 0; aa < ue->lte_frame_parms.nb_antennas_tx_eNB; aa++) {
+      lte_dl_channel_estimation(ue, 0, 0, Ns, aa, l, symbol);
+      for (int i = 0; i < ue->PHY_measurements.n_adj_cells; i++)
+        lte_dl_channel_estimation(ue, 0, i + 1, Ns, aa, l, symbol);
+    }
+    if (l == 4 - ue->lte_frame_parms.Ncp)
+      lte_est_freq_offset(ue->lte_ue_common_vars.dl_ch_estimates[0], &ue->lte_frame_parms, l,
+                          &ue->lte_ue_common_vars.freq_offset, reset_freq_est);
+  }
+  return 0;
+}
+
+/* control region: pcfich.c:48 / :144 (frame_parms->pcfich_reg is derived inside the library) */
+void generate_pcfich_reg_mapping(LTE_DL_FRAME_PARMS *frame_parms)
+{
+  oai4g_frame_parms_t fp;
+  fp_to(frame_parms, &fp);
+  oai4g_generate_pcfich_reg_mapping(&fp, frame_parms->pcfich_reg, &frame_parms->pcfich_first_reg_idx);
+}
+void generate_pcfich(uint8_t num_pdcch_symbols, int16_t amp, LTE_DL_FRAME_PARMS *frame_parms,
+                     mod_sym_t **txdataF, uint8_t subframe)
+{
+  oai4g_frame_parms_t fp;
+  fp_to(frame_parms, &fp);
+  oai4g_generate_pcfich(num_pdcch_symbols, amp, &fp, (int32_t **)txdataF, subframe);
+}
+
+/* callees that dlsim / ltetest also call directly */
+uint32_t crc24a(uint8_t *inPtr, int32_t bitlen) { return oai4g_crc24a(inPtr, bitlen); }   /* CODING/defs.h:375 */
+uint32_t crc24b(uint8_t *inPtr, int32_t bitlen) { return oai4g_crc24b(inPtr, bitlen); }
+int32_t lte_segmentation(uint8_t *input_buffer, uint8_t **output_buffers, uint32_t B, uint32_t *C,
+                         uint32_t *Cplus, uint32_t *Cminus, uint32_t *Kplus, uint32_t *Kminus, uint32_t *F)
+{                                                                                         /* CODING/defs.h:79 */
+  return oai4g_lte_segmentation(input_buffer, output_buffers, B, C, Cplus, Cminus, Kplus, Kminus, F);
+}
+void threegpplte_turbo_encoder(uint8_t *input, uint16_t input_length_bytes, uint8_t *output, uint8_t F,
+                               uint16_t interleaver_f1, uint16_t interleaver_f2)          /* CODING/defs.h:315 */
+{
+  oai4g_threegpplte_turbo_encoder(input, input_length_bytes, output, F, interleaver_f1, interleaver_f2);
+}
+uint32_t sub_block_interleaving_turbo(uint32_t D, uint8_t *d, uint8_t *w)
+{
+  return oai4g_sub_block_interleaving_turbo(D, d, w);
+}
+uint32_t lte_rate_matching_turbo(uint32_t RTC, uint32_t G, uint8_t *w, uint8_t *e, uint8_t C, uint32_t Nsoft,
+                                 uint8_t Mdlharq, uint8_t Kmimo, uint8_t rvidx, uint8_t Qm, uint8_t Nl, uint8_t r,
+                                 uint8_t nb_rb, uint8_t m)
+{
+  return oai4g_lte_rate_matching_turbo(RTC, G, w, e, C, Nsoft, Mdlharq, Kmimo, rvidx, Qm, Nl, r, nb_rb, m);
+}

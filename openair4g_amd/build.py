@@ -52,6 +52,21 @@ def build_lib(force=False, verbose=False, out=None, defines=()):
     return lib
 
 
+def build_host_tools(verbose=False):
+    """gcc-built C host programs over the C ABI (tools/dlsim_tx.c -> tools/bin/dlsim_tx)."""
+    out = os.path.join(ROOT, "tools", "bin", "dlsim_tx")
+    src = os.path.join(ROOT, "tools", "dlsim_tx.c")
+    if not _newer(out, [src, LIB, os.path.join(ROOT, "include", "oai4g.h")]):
+        return out
+    os.makedirs(os.path.dirname(out), exist_ok=True)
+    cmd = ["gcc", "-O2", "-std=gnu11", "-Wall", "-I", os.path.join(ROOT, "include"), src, "-L", LIBDIR,
+           "-lopenair4g_amd", "-Wl,-rpath,$ORIGIN/../../openair4g_amd/lib", "-o", out]
+    if verbose:
+        print(" ".join(cmd))
+    subprocess.run(cmd, check=True)
+    return out
+
+
 def build_oracle(verbose=False):
     subprocess.run(["make", "-s", "-C", os.path.join(ROOT, "oracle")], check=True,
                    stdout=None if verbose else subprocess.DEVNULL)
@@ -65,5 +80,6 @@ if __name__ == "__main__":
                                  defines=defs))
         sys.exit(0)
     build_lib(force="--force" in sys.argv, verbose=True)
+    build_host_tools(verbose=True)
     build_oracle(verbose=True)
     print("built", LIB)
