@@ -56,7 +56,23 @@ typedef struct {
   uint16_t nb_prefix_samples;
   uint16_t nb_prefix_samples0;
   uint32_t samples_per_tti;
+  /* control region (phich_config_common, tdd_config, nb_antennas_tx_eNB of LTE_DL_FRAME_PARMS) */
+  uint8_t phich_resource;   /* PHICH_RESOURCE_t (impl_defs_lte.h:80-85): 1, 3, 6, 12 = Ng 1/6, 1/2, 1, 2 */
+  uint8_t phich_duration;   /* 0 normal (extended is not supported by the PDCCH path) */
+  uint8_t tdd_config;
+  uint8_t nb_antennas_tx_eNB;
 } oai4g_frame_parms_t;
+
+/* DCI_ALLOC_t (PHY/LTE_TRANSPORT/defs.h:734-749) */
+typedef struct {
+  uint8_t dci_length;       /* bits */
+  uint8_t L;                /* log2 aggregation level 0..3 */
+  int32_t nCCE;             /* first CCE; < 0: not transmitted */
+  uint8_t ra_flag;
+  uint16_t rnti;
+  uint32_t format;          /* DCI_format_t (not used by the encoder) */
+  uint8_t dci_pdu[8];
+} oai4g_dci_alloc_t;
 
 /* LTE_DL_eNB_HARQ_t (PHY/LTE_TRANSPORT/defs.h:104-169), path fields only. */
 typedef struct {
@@ -188,6 +204,31 @@ void oai4g_generate_pcfich_reg_mapping(const oai4g_frame_parms_t *frame_parms, u
 int oai4g_generate_pcfich(uint8_t num_pdcch_symbols, int16_t amp, const oai4g_frame_parms_t *frame_parms,
                           int32_t **txdataF, uint8_t subframe);
 
+/* PDCCH geometry (host-side scalar helpers): get_mi (phich.c:59), get_nquad / get_nCCE
+ * (dci.c:2494-2538), get_num_pdcch_symbols (dci.c:1964), generate_phich_reg_mapping
+ * (phich.c:280; normal duration: returns the number of groups written into phich_reg[56][3]),
+ * get_nCCE_offset (SCHED/phy_procedures_lte_eNb.c:308, over the library's CCE table, cleared by
+ * oai4g_init_nCCE_table as init_nCCE_table :302 does; not thread-safe, like the reference) */
+uint8_t oai4g_get_mi(const oai4g_frame_parms_t *frame_parms, uint8_t subframe);
+uint16_t oai4g_get_nquad(uint8_t num_pdcch_symbols, const oai4g_frame_parms_t *frame_parms, uint8_t mi);
+uint16_t oai4g_get_nCCE(uint8_t num_pdcch_symbols, const oai4g_frame_parms_t *frame_parms, uint8_t mi);
+uint8_t oai4g_get_num_pdcch_symbols(uint8_t num_dci, const oai4g_dci_alloc_t *dci_alloc,
+                                    const oai4g_frame_parms_t *frame_parms, uint8_t subframe);
+int oai4g_generate_phich_reg_mapping(const oai4g_frame_parms_t *frame_parms, uint16_t phich_reg[56][3]);
+void oai4g_init_nCCE_table(void);
+int oai4g_get_nCCE_offset(uint8_t L, int nCCE, int common_dci, uint16_t rnti, uint8_t subframe);
+/* generate_dci_top (PHY/LTE_TRANSPORT/dci.c:2024, decl LTE_TRANSPORT/proto.h): PCFICH + every
+ * DCI (CRC16 with the RNTI mask, tail-biting convolutional code, rate matching to 72 * 2^L bits
+ * at CCE nCCE), <NIL> filling, scrambling, QPSK (SISO / ALAMOUTI), quadruplet interleaving with
+ * the cell-id cyclic shift and the REG mapping around the PCFICH / PHICH REGs, into the control
+ * symbols of `subframe` of the frame grids txdataF[0..1] (overwrites).  Returns
+ * num_pdcch_symbols; when that is outside 1..3 (too many CCEs, or an N_RB_DL without a PDCCH
+ * geometry in get_nquad: 15 / 75) nothing is written (the reference maps an undefined CFI
+ * codeword there) and oai4g_last_error() says why. */
+uint8_t oai4g_generate_dci_top(uint8_t num_ue_spec_dci, uint8_t num_common_dci, const oai4g_dci_alloc_t *dci_alloc,
+                               uint32_t n_rnti, int16_t amp, const oai4g_frame_parms_t *frame_parms,
+                               int32_t **txdataF, uint32_t subframe);
+
 /* ---------------- UE receive front end ---------------- */
 /* dft64..dft2048 (PHY/TOOLS/lte_dfts.c:1766, 1957, 2172, 2359, 2574, 2689; decl TOOLS/defs.h):
  * y = DFT(x), bit-exact fixed point.  oai4g_dft returns 0 or -1. */
@@ -297,6 +338,12 @@ int oai4g_tx_batch(const oai4g_tx_config_t *cfg, int n_sf, const uint8_t *d_payl
  * two kernel durations in ms (kernel_ms[0] = encode/RM/scramble, [1] = modulate/IDFT/CP). */
 int oai4g_tx_batch_timed(const oai4g_tx_config_t *cfg, int n_sf, const uint8_t *d_payload, void *d_work,
                          int32_t *d_iq, void *stream, float *kernel_ms);
+/* Control region in the batched grid: every batch element of subframe index
+ * sf also carries generate_dci_top's PCFICH + PDCCH for this DCI set (the same DCIs in every
+ * subframe, as dlsim transmits them), merged by the modulator; n_dci = 0 switches it off.
+ * The control values are computed on the GPU once here, per subframe index.  Returns 0 / -1. */
+int oai4g_tx_config_set_control(oai4g_tx_config_t *cfg, uint8_t num_ue_spec_dci, uint8_t num_common_dci,
+                                const oai4g_dci_alloc_t *dci_alloc);
 /* Stage entry for parity tests: run only the encoder kernel (payload -> packed e bits). */
 int oai4g_tx_encode(const oai4g_tx_config_t *cfg, int n_sf, const uint8_t *d_payload, void *d_work, void *stream);
 

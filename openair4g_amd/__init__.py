@@ -40,7 +40,16 @@ class FrameParms(ctypes.Structure):
                 ("log2_symbol_size", ctypes.c_uint8), ("pad0", ctypes.c_uint8),
                 ("ofdm_symbol_size", ctypes.c_uint16), ("first_carrier_offset", ctypes.c_uint16),
                 ("nb_prefix_samples", ctypes.c_uint16), ("nb_prefix_samples0", ctypes.c_uint16),
-                ("samples_per_tti", ctypes.c_uint32)]
+                ("samples_per_tti", ctypes.c_uint32), ("phich_resource", ctypes.c_uint8),
+                ("phich_duration", ctypes.c_uint8), ("tdd_config", ctypes.c_uint8),
+                ("nb_antennas_tx_eNB", ctypes.c_uint8)]
+
+
+class DciAlloc(ctypes.Structure):
+    """oai4g_dci_alloc_t — DCI_ALLOC_t (PHY/LTE_TRANSPORT/defs.h:734-749)."""
+    _fields_ = [("dci_length", ctypes.c_uint8), ("L", ctypes.c_uint8), ("nCCE", ctypes.c_int32),
+                ("ra_flag", ctypes.c_uint8), ("rnti", ctypes.c_uint16), ("format", ctypes.c_uint32),
+                ("dci_pdu", ctypes.c_uint8 * 8)]
 
 
 class DlHarq(ctypes.Structure):
@@ -152,6 +161,20 @@ _SIGS = {
     "oai4g_idft64": (None, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int]),
     "oai4g_generate_pcfich_reg_mapping": (None, [ctypes.POINTER(FrameParms), ctypes.POINTER(ctypes.c_uint16),
                                                   ctypes.POINTER(ctypes.c_uint8)]),
+    "oai4g_get_mi": (ctypes.c_uint8, [ctypes.POINTER(FrameParms), ctypes.c_uint8]),
+    "oai4g_get_nquad": (ctypes.c_uint16, [ctypes.c_uint8, ctypes.POINTER(FrameParms), ctypes.c_uint8]),
+    "oai4g_get_nCCE": (ctypes.c_uint16, [ctypes.c_uint8, ctypes.POINTER(FrameParms), ctypes.c_uint8]),
+    "oai4g_get_num_pdcch_symbols": (ctypes.c_uint8, [ctypes.c_uint8, ctypes.POINTER(DciAlloc),
+                                                     ctypes.POINTER(FrameParms), ctypes.c_uint8]),
+    "oai4g_generate_phich_reg_mapping": (ctypes.c_int, [ctypes.POINTER(FrameParms), ctypes.POINTER(ctypes.c_uint16)]),
+    "oai4g_init_nCCE_table": (None, []),
+    "oai4g_get_nCCE_offset": (ctypes.c_int, [ctypes.c_uint8, ctypes.c_int, ctypes.c_int, ctypes.c_uint16,
+                                             ctypes.c_uint8]),
+    "oai4g_generate_dci_top": (ctypes.c_uint8, [ctypes.c_uint8, ctypes.c_uint8, ctypes.POINTER(DciAlloc),
+                                                ctypes.c_uint32, ctypes.c_int16, ctypes.POINTER(FrameParms),
+                                                ctypes.c_void_p, ctypes.c_uint32]),
+    "oai4g_tx_config_set_control": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_uint8, ctypes.c_uint8,
+                                                    ctypes.POINTER(DciAlloc)]),
     "oai4g_generate_pcfich": (ctypes.c_int, [ctypes.c_uint8, ctypes.c_int16, ctypes.POINTER(FrameParms),
                                              ctypes.POINTER(ctypes.c_void_p), ctypes.c_uint8]),
     "oai4g_dft": (ctypes.c_int, [ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int]),
@@ -470,6 +493,24 @@ class TurboDecoderBatch:
             self.L.oai4g_dev_free(p)
 
 
+def dci_allocs(items):
+    """items: (dci_length, L, nCCE, rnti, pdu bytes) -> ctypes array of DciAlloc"""
+    arr = (DciAlloc * max(1, len(items)))()
+    for a, (ln, L, ncce, rnti, pdu) in zip(arr, items):
+        a.dci_length, a.L, a.nCCE, a.rnti = ln, L, ncce, rnti
+        for i, b in enumerate(list(pdu)[:8]):
+            a.dci_pdu[i] = int(b)
+    return arr
+
+
+def generate_dci_top(items, n_common, amp, fp, txdataF, subframe):
+    """generate_dci_top on frame grids (int32 arrays, modified in place): num_pdcch_symbols"""
+    init()
+    arr = dci_allocs(items)
+    gp = (ctypes.c_void_p * len(txdataF))(*[g.ctypes.data for g in txdataF])
+    return lib().oai4g_generate_dci_top(len(items) - n_common, n_common, arr, 0, amp, ctypes.byref(fp), gp, subframe)
+
+
 def normal_prefix_mod(txdataF, fp, nsymb=7, out=None):
     init()
     txdataF = np.ascontiguousarray(txdataF, dtype=np.int32)
@@ -629,6 +670,12 @@ class TxPipeline:
 
     def G(self, cw, subframe):
         return self.L.oai4g_tx_G(self.cfg, cw, subframe)
+
+    def set_control(self, items, n_common=0):
+        """oai4g_tx_config_set_control: generate_dci_top's PCFICH + PDCCH for these DCIs in every
+        batch element (items as for generate_dci_top; [] switches it off)."""
+        arr = dci_allocs(items)
+        _check(self.L.oai4g_tx_config_set_control(self.cfg, len(items) - n_common, n_common, arr) == 0)
 
     def fill_payload(self, seed):
         _check(self.L.oai4g_fill_payload(self.d_payload, self.payload_bytes, seed, None) == 0)

@@ -13,6 +13,7 @@
 #include <string.h>
 
 #include <algorithm>
+#include <vector>
 #include <map>
 #include <mutex>
 #include <vector>
@@ -290,6 +291,10 @@ extern "C" int oai4g_init_frame_parms(oai4g_frame_parms_t *fp, uint16_t N_RB_DL,
   fp->first_carrier_offset = (uint16_t)(fp->ofdm_symbol_size - 6 * N_RB_DL);
   fp->nb_prefix_samples = (uint16_t)(cp >> sh);
   fp->nb_prefix_samples0 = (uint16_t)(cp0 >> sh);
+  fp->phich_resource = 6;                 /* Ng = one (dlsim.c:138) */
+  fp->phich_duration = 0;
+  fp->tdd_config = 3;
+  fp->nb_antennas_tx_eNB = nb_antennas_tx; /* dlsim.c:137 */
   return 0;
 }
 
@@ -620,6 +625,7 @@ struct oai4g_tx_config {
   std::vector<uint16_t> h_remap;
   uint32_t *d_crs = nullptr;
   std::vector<uint32_t> h_crs;          /* [10][4][200] packed CRS IQ */
+  uint32_t *d_ctl = nullptr;            /* control region values (oai4g_tx_config_set_control) */
   int re_count[10];
   int re_alloc[10];                 /* dlsch_modulation's return value (ALAMOUTI counts skipped pilots) */
   /* optional pipelined batches (OAI4G_PIPE_CHUNK=n): the encoder runs on the caller's stream, the
@@ -935,8 +941,10 @@ static int derive_cfg(oai4g_tx_config *cfg, const oai4g_tx_params_t *p, const ui
   return rm_fail ? -2 : 0;
 }
 
-static int upload_cfg(oai4g_tx_config *cfg)
+static int upload_remap(oai4g_tx_config *cfg)
 {
+  if (cfg->d_remap) hipFree(cfg->d_remap);
+  cfg->d_remap = nullptr;
   if (!cfg->h_remap.empty()) {
     /* natural layout followed by the thread-major copy the fused kernel reads */
     const size_t n = cfg->h_remap.size(), N = cfg->h.N, T = N >> 4;
@@ -952,6 +960,12 @@ static int upload_cfg(oai4g_tx_config *cfg)
     cfg->h.remap_tm = nullptr;
   }
   cfg->h.remap = cfg->d_remap;
+  return 0;
+}
+
+static int upload_cfg(oai4g_tx_config *cfg)
+{
+  if (upload_remap(cfg) != 0) return -1;
   if (!cfg->h_crs.empty()) {
     HCK(hipMalloc(&cfg->d_crs, cfg->h_crs.size() * 4), -1);
     HCK(hipMemcpy(cfg->d_crs, cfg->h_crs.data(), cfg->h_crs.size() * 4, hipMemcpyHostToDevice), -1);
@@ -978,7 +992,9 @@ static void release_cfg(oai4g_tx_config *cfg)
   if (cfg->d) hipFree(cfg->d);
   if (cfg->d_remap) hipFree(cfg->d_remap);
   if (cfg->d_crs) hipFree(cfg->d_crs);
+  if (cfg->d_ctl) hipFree(cfg->d_ctl);
   cfg->d_crs = nullptr;
+  cfg->d_ctl = nullptr;
   cfg->d = nullptr;
   cfg->d_remap = nullptr;
 }
@@ -1979,5 +1995,397 @@ extern "C" int oai4g_generate_pcfich(uint8_t num_pdcch_symbols, int16_t amp, con
   for (uint32_t aa = 0; aa < a.n_ant; aa++)
     HCK(hipMemcpyAsync(txdataF[aa] + symbol_offset, aa ? d1 : d0, (size_t)N * 4, hipMemcpyDeviceToHost, g_scr.s), -1);
   HCK(hipStreamSynchronize(g_scr.s), -1);
+  return 0;
+}
+
+/* ----------------------------------------------------------------------------------------
+ * Control region: PDCCH / DCI (generate_dci_top, dci.c:2024-2346) — host-side geometry
+ * (the reference's init-time / scalar helpers) + the k_dci kernel for the per-subframe data.
+ * ---------------------------------------------------------------------------------------- */
+extern "C" uint8_t oai4g_get_mi(const oai4g_frame_parms_t *fp, uint8_t sf)
+{
+  if (fp->frame_type == 0) return 1;                                  /* phich.c:59-118 */
+  switch (fp->tdd_config) {
+  case 0: return (sf == 0 || sf == 5) ? 2 : 1;
+  case 1: return (sf == 0 || sf == 5) ? 0 : 1;
+  case 2: return (sf == 3 || sf == 8) ? 1 : 0;
+  case 3: return (sf == 0 || sf == 8 || sf == 9) ? 1 : 0;
+  case 4: return (sf == 8 || sf == 9) ? 1 : 0;
+  case 5: return sf == 8 ? 1 : 0;
+  case 6: return 1;
+  default: return 0;
+  }
+}
+
+static uint32_t phich_ngroup(const oai4g_frame_parms_t *fp)   /* Ngroup_PHICH (phich.c:292-303) */
+{
+  uint32_t ng = (fp->phich_resource * fp->N_RB_DL) / 48;
+  if ((fp->phich_resource * fp->N_RB_DL) % 48) ng++;
+  if (fp->Ncp == 1) ng <<= 1;
+  return ng;
+}
+
+extern "C" uint16_t oai4g_get_nquad(uint8_t npdcch, const oai4g_frame_parms_t *fp, uint8_t mi)
+{
+  uint32_t Nreg = 0;                                                  /* dci.c:2499-2538 */
+  uint8_t ng = (uint8_t)((fp->phich_resource * fp->N_RB_DL) / 48);    /* uint8_t, as :2502 */
+  if ((fp->phich_resource * fp->N_RB_DL) % 48) ng++;
+  if (fp->Ncp == 1) ng = (uint8_t)(ng << 1);
+  ng = (uint8_t)(ng * mi);
+  if (npdcch > 0 && npdcch < 4) {
+    switch (fp->N_RB_DL) {
+    case 6: Nreg = 12 + (npdcch - 1) * 18; break;
+    case 25: Nreg = 50 + (npdcch - 1) * 75; break;
+    case 50: Nreg = 100 + (npdcch - 1) * 150; break;
+    case 100: Nreg = 200 + (npdcch - 1) * 300; break;
+    default: return 0;
+    }
+  }
+  return (uint16_t)(Nreg - 4 - 3 * ng);
+}
+
+extern "C" uint16_t oai4g_get_nCCE(uint8_t npdcch, const oai4g_frame_parms_t *fp, uint8_t mi)
+{
+  return (uint16_t)(oai4g_get_nquad(npdcch, fp, mi) / 9);
+}
+
+extern "C" uint8_t oai4g_get_num_pdcch_symbols(uint8_t num_dci, const oai4g_dci_alloc_t *dci,
+                                               const oai4g_frame_parms_t *fp, uint8_t sf)
+{
+  uint16_t numCCE = 0;                                                /* dci.c:1964-2022 */
+  uint8_t nmin = 0;
+  if (fp->Ncp == 1)
+    nmin = (fp->frame_type == 1 && (fp->tdd_config < 3 || fp->tdd_config == 6) && (sf == 1 || sf == 6)) ? 2 : 3;
+  for (int i = 0; i < num_dci; i++) numCCE = (uint16_t)(numCCE + (1 << dci[i].L));
+  const uint8_t mi = oai4g_get_mi(fp, sf);
+  for (uint8_t n = 1; n <= 3; n++)
+    if (numCCE <= oai4g_get_nCCE(n, fp, mi)) return nmin > n ? nmin : n;
+  if (fp->N_RB_DL <= 10 && 9u * numCCE <= fp->N_RB_DL * (fp->nb_antennas_tx_eNB == 4 ? (fp->Ncp ? 9u : 10u)
+                                                                                  : (fp->Ncp ? 10u : 11u)))
+    return 4;
+  return 0;
+}
+
+extern "C" int oai4g_generate_phich_reg_mapping(const oai4g_frame_parms_t *fp, uint16_t phich_reg[56][3])
+{
+  uint16_t pcf[4];                                                    /* phich.c:280-386 */
+  uint8_t fi;
+  pcfich_regs(fp, pcf, &fi);
+  const uint32_t n0 = fp->N_RB_DL * 2u - 4u, ng = phich_ngroup(fp), nloop = fp->Ncp == 0 ? ng : ng >> 1;
+  for (uint32_t m = 0; m < nloop && m < 56; m++) {
+    const uint32_t base[3] = {(fp->Nid_cell + m) % n0, (fp->Nid_cell + m + n0 / 3) % n0,
+                              (fp->Nid_cell + m + 2 * n0 / 3) % n0};
+    for (int j = 0; j < 3; j++) {
+      uint32_t r = base[j];
+      for (int q = 0; q < 4; q++)
+        if (r >= pcf[(fi + q) & 3]) r++;
+      phich_reg[m][j] = (uint16_t)r;
+    }
+  }
+  return (int)nloop;
+}
+
+static int g_cce_table[800];
+extern "C" void oai4g_init_nCCE_table(void) { memset(g_cce_table, 0, sizeof(g_cce_table)); }
+
+extern "C" int oai4g_get_nCCE_offset(uint8_t L, int nCCE, int common_dci, uint16_t rnti, uint8_t subframe)
+{
+  int *T = g_cce_table;                                               /* phy_procedures_lte_eNb.c:308-391 */
+  if (L == 0 || nCCE / L <= 0) return -1;
+  if (common_dci == 1) {
+    int nb = L == 4 ? 4 : 2;
+    if (nCCE / L < nb) nb = nCCE / L;
+    for (int m = nb - 1; m >= 0; m--) {
+      int fr = 1;
+      for (int l = 0; l < L; l++) fr &= T[m * L + l] != 1;
+      if (fr) {
+        for (int l = 0; l < L; l++) T[m * L + l] = 1;
+        return m * L;
+      }
+    }
+    return -1;
+  }
+  uint32_t Yk = rnti;
+  for (int i = 0; i <= subframe; i++) Yk = (Yk * 39827u) % 65537u;
+  Yk %= (uint32_t)(nCCE / L);
+  const int nb = (L == 1 || L == 2) ? 6 : 2;
+  for (int m = 0; m < nb; m++) {
+    const int s0 = (int)(((Yk + m) % (uint32_t)(nCCE / L)) * L);
+    int fr = 1;
+    for (int l = 0; l < L; l++) fr &= T[s0 + l] != 1;
+    if (fr) {
+      for (int l = 0; l < L; l++) T[s0 + l] = 1;
+      return s0;
+    }
+  }
+  return -1;
+}
+
+/* The static part of generate_dci_top for (fp, npdcch, subframe): the QPSK symbol interleaving
+ * (pdcch_interleaving, dci.c:277-341: 32-column sub-block interleaver on quadruplets with the
+ * <NULL>s dropped, then the cyclic shift by Nid_cell) composed with the REG allocation
+ * (:2234-2340: k' outer, l' inner, PCFICH / PHICH REGs skipped (check_phich_reg :62-121), six-RE
+ * REGs around the RS in symbol 0, four-RE REGs with the DC split elsewhere), cut at Msymb2
+ * mapped REs.  map[r] = l * N + subcarrier, src[r] = QPSK symbol index.  Returns the RE count. */
+static uint32_t pdcch_map(const oai4g_frame_parms_t *fp, uint8_t npdcch, uint8_t mi, std::vector<uint32_t> &map,
+                          std::vector<uint16_t> &src)
+{
+  static const uint8_t bitrev_cc[32] = {1, 17, 9, 25, 5, 21, 13, 29, 3, 19, 11, 27, 7, 23, 15, 31,
+                                        0, 16, 8, 24, 4, 20, 12, 28, 2, 18, 10, 26, 6, 22, 14, 30};
+  const uint32_t N = fp->ofdm_symbol_size, Mquad = oai4g_get_nquad(npdcch, fp, mi);
+  const int Msymb = ((2 * 33 + 22) * 72) / 2;
+  int Msymb2;
+  switch (fp->N_RB_DL) {
+  case 100: Msymb2 = Msymb; break;
+  case 75: Msymb2 = 3 * Msymb / 4; break;
+  case 50: Msymb2 = Msymb >> 1; break;
+  case 25: Msymb2 = Msymb >> 2; break;
+  case 15: Msymb2 = Msymb * 15 / 100; break;
+  case 6: Msymb2 = Msymb * 6 / 100; break;
+  default: Msymb2 = Msymb >> 2; break;
+  }
+  /* quadruplet k of wtemp <- quadruplet perm[k] of y; wbar[i] = wtemp[(i + Nid) mod Mquad] */
+  std::vector<uint32_t> perm;
+  const uint32_t RCC = (Mquad + 31) >> 5, ND = (RCC << 5) - Mquad;
+  for (uint32_t col = 0; col < 32; col++)
+    for (uint32_t row = 0, idx = bitrev_cc[col]; row < RCC; row++, idx += 32)
+      if (idx >= ND) perm.push_back(idx - ND);
+  uint16_t pcf[4], phr[56][3];
+  uint8_t fi;
+  memset(phr, 0, sizeof(phr));            /* groups the mapping never writes read as REG 0 (calloc'd frame_parms) */
+  pcfich_regs(fp, pcf, &fi);
+  oai4g_generate_phich_reg_mapping(fp, phr);
+  const uint32_t ng = phich_ngroup(fp), ns3 = fp->nushift % 3;
+  const bool tx4 = fp->nb_antennas_tx_eNB == 4;
+  auto phich_or_pcfich = [&](uint32_t kp, uint32_t lp) {
+    if (lp > 0 && fp->Ncp == 0) return false;
+    const uint32_t m = (lp == 0 || (lp == 1 && tx4)) ? kp / 6 : kp >> 2;
+    if (lp == 0 && (m == pcf[0] || m == pcf[1] || m == pcf[2] || m == pcf[3])) return true;
+    if (mi > 0)
+      for (uint32_t i = 0; i < ng && i < 56; i++)
+        if (m == phr[i][0] || m == phr[i][1] || m == phr[i][2]) return true;
+    return false;
+  };
+  map.clear();
+  src.clear();
+  uint32_t mprime = 0;
+  int re_offset = fp->first_carrier_offset;
+  auto put = [&](uint32_t off) {
+    const uint32_t q = mprime >> 2;       /* wbar quadruplet -> y symbol */
+    map.push_back(off);
+    src.push_back((uint16_t)(4 * perm[(q + fp->Nid_cell) % Mquad] + (mprime & 3)));
+    mprime++;
+  };
+  for (uint32_t kp = 0; kp < (uint32_t)fp->N_RB_DL * 12; kp++) {
+    for (uint32_t lp = 0; lp < npdcch; lp++) {
+      const uint32_t tti = N * lp + (uint32_t)re_offset;
+      if (!phich_or_pcfich(kp, lp)) {
+        const uint32_t km = kp % 12;
+        if (lp == 0 || (lp == 1 && tx4)) {
+          if (km == 0 || km == 6)
+            for (uint32_t i = 0; i < 6; i++)
+              if (i != ns3 && i != ns3 + 3) put(tti + i);
+        } else if (km == 0 || km == 4 || km == 8) {
+          if (re_offset != (int)N - 2) {
+            for (uint32_t i = 0; i < 4; i++) put(tti + i);
+          } else {                        /* the REG straddles DC */
+            put(tti);
+            put(tti + 1);
+            put(tti - N + 3);
+            put(tti - N + 4);
+          }
+        }
+        if (mprime >= (uint32_t)Msymb2) return (uint32_t)map.size();
+      }
+    }
+    re_offset++;
+    if (re_offset == (int)N) re_offset = 1;
+  }
+  return (uint32_t)map.size();
+}
+
+/* Fills the kernel arguments and the map of one subframe; returns npdcch (0 on error). */
+static uint8_t dci_prepare(uint8_t n_ue, uint8_t n_common, const oai4g_dci_alloc_t *dci, int16_t amp,
+                           const oai4g_frame_parms_t *fp, uint32_t subframe, dci_args_t &a, std::vector<uint32_t> &map,
+                           std::vector<uint16_t> &src)
+{
+  const uint32_t n = (uint32_t)n_ue + n_common;
+  if (n > OAI4G_MAX_DCI) { set_err("generate_dci_top: %u DCIs (at most %d)", n, OAI4G_MAX_DCI); return 0; }
+  if (fp->phich_duration != 0 || fp->Ncp != 0) {
+    set_err("generate_dci_top: only the normal cyclic prefix with normal PHICH duration is supported");
+    return 0;
+  }
+  const uint8_t npd = oai4g_get_num_pdcch_symbols((uint8_t)n, dci, fp, (uint8_t)subframe);
+  if (npd < 1 || npd > 3) {
+    set_err("generate_dci_top: num_pdcch_symbols %u (too many CCEs, or no PDCCH geometry for N_RB_DL %u)", npd,
+            fp->N_RB_DL);
+    return npd;
+  }
+  const uint8_t mi = oai4g_get_mi(fp, (uint8_t)subframe);
+  memset(&a, 0, sizeof(a));
+  /* generate_dci_top's order: aggregation level 3 .. 0, common DCIs first within a level; the
+   * encoded blocks land at their own CCEs, so only later writers over overlapping CCEs matter */
+  uint32_t k = 0;
+  for (int L = 3; L >= 0; L--)
+    for (uint32_t i = 0; i < n; i++)
+      if (dci[i].L == L && dci[i].nCCE >= 0) {
+        dci_dev_t &d = a.dci[k++];
+        const uint8_t *p = dci[i].dci_pdu;
+        for (int b = 0; b < 8; b++) d.flip[b] = 0;
+        if (dci[i].dci_length <= 32) for (int b = 0; b < 4; b++) d.flip[b] = p[3 - b];
+        else for (int b = 0; b < 8; b++) d.flip[b] = p[7 - b];
+        d.A = dci[i].dci_length;
+        d.L = dci[i].L;
+        d.nCCE = dci[i].nCCE;
+        d.rnti = dci[i].rnti;
+        if (d.A > 64 || d.A < 8 || d.L > 3 || 72u * (uint32_t)(d.nCCE + (1 << d.L)) > (2 * 33 + 22 + 8) * 72u) {
+          set_err("generate_dci_top: DCI %u: length %u / L %u / nCCE %d out of range", i, d.A, d.L, d.nCCE);
+          return 0;
+        }
+      }
+  a.n_dci = k;
+  a.nbits = 8u * oai4g_get_nquad(npd, fp, mi);
+  a.c_init = (subframe << 9) + fp->Nid_cell;
+  a.gain = fp->mode1_flag == 1 ? (int16_t)((amp * 23170) >> 15) : (int16_t)(amp / 2);
+  a.mode1 = fp->mode1_flag ? 1 : 0;
+  a.n_ant = fp->nb_antennas_tx_eNB > 1 ? 2 : 1;
+  a.n_re = pdcch_map(fp, npd, mi, map, src);
+  return npd;
+}
+
+extern "C" uint8_t oai4g_generate_dci_top(uint8_t num_ue_spec_dci, uint8_t num_common_dci,
+                                          const oai4g_dci_alloc_t *dci_alloc, uint32_t n_rnti, int16_t amp,
+                                          const oai4g_frame_parms_t *fp, int32_t **txdataF, uint32_t subframe)
+{
+  (void)n_rnti;
+  NEED_INIT(0);
+  if (subframe > 9) { set_err("generate_dci_top: subframe %u", subframe); return 0; }
+  dci_args_t a;
+  std::vector<uint32_t> map;
+  std::vector<uint16_t> src;
+  const uint8_t npd = dci_prepare(num_ue_spec_dci, num_common_dci, dci_alloc, amp, fp, subframe, a, map, src);
+  if (npd < 1 || npd > 3) return npd;
+  const uint32_t N = fp->ofdm_symbol_size, nsymb = 14;
+  const size_t sym_off = (size_t)N * subframe * nsymb, gbytes = (size_t)npd * N * 4;
+  const size_t gpad = (gbytes + 255) & ~(size_t)255, mbytes = ((size_t)a.n_re * 4 + 255) & ~(size_t)255;
+  uint8_t *buf = scratch(2 * gpad + mbytes + (size_t)a.n_re * 2 + 256);
+  if (!buf) return 0;
+  int32_t *d0 = (int32_t *)buf, *d1 = (int32_t *)(buf + gpad);
+  uint32_t *dmap = (uint32_t *)(buf + 2 * gpad);
+  uint16_t *dsrc = (uint16_t *)(buf + 2 * gpad + mbytes);
+  const uint32_t n_ant = a.n_ant;
+  for (uint32_t aa = 0; aa < n_ant; aa++)
+    HCK(hipMemcpyAsync(aa ? d1 : d0, txdataF[aa] + sym_off, gbytes, hipMemcpyHostToDevice, g_scr.s), 0);
+  HCK(hipMemcpyAsync(dmap, map.data(), (size_t)a.n_re * 4, hipMemcpyHostToDevice, g_scr.s), 0);
+  HCK(hipMemcpyAsync(dsrc, src.data(), (size_t)a.n_re * 2, hipMemcpyHostToDevice, g_scr.s), 0);
+  /* PCFICH first (generate_dci_top :2084-2088), then the PDCCH REs */
+  pcfich_args_t pa;
+  memset(&pa, 0, sizeof(pa));
+  {
+    uint16_t reg[4];
+    uint8_t fi;
+    pcfich_regs(fp, reg, &fi);
+    pa.c_init = ((((2u * fp->Nid_cell) + 1u) * (1u + subframe)) << 9) + fp->Nid_cell;
+    pa.cfi = npd;
+    pa.gain = a.gain;
+    pa.mode1 = a.mode1;
+    pa.nushift3 = (uint8_t)(fp->nushift % 3);
+    for (int q = 0; q < 4; q++) {
+      uint32_t ro = fp->first_carrier_offset + (uint32_t)reg[q] * 6;
+      if (ro >= N) ro = 1 + ro - N;
+      pa.reg_off[q] = ro;
+    }
+    pa.n_ant = n_ant;
+  }
+  HCK(oai4g_launch_pcfich(d0, d1, pa, g_scr.s), 0);
+  HCK(oai4g_launch_dci(a, dmap, dsrc, d0, d1, 0, g_scr.s), 0);
+  for (uint32_t aa = 0; aa < n_ant; aa++)
+    HCK(hipMemcpyAsync(txdataF[aa] + sym_off, aa ? d1 : d0, gbytes, hipMemcpyDeviceToHost, g_scr.s), 0);
+  HCK(hipStreamSynchronize(g_scr.s), 0);
+  return npd;
+}
+
+/* Batched control region: generate_dci_top's PCFICH + PDCCH for every subframe index, computed
+ * on the GPU by the drop-in kernels into a [10][3][2][N] table, marked in the RE map with
+ * OAI4G_CTL_CODE and merged by the modulator. */
+extern "C" int oai4g_tx_config_set_control(oai4g_tx_config_t *cfg, uint8_t n_ue, uint8_t n_common,
+                                           const oai4g_dci_alloc_t *dci)
+{
+  NEED_INIT(-1);
+  const uint32_t N = cfg->h.N;
+  for (auto &c : cfg->h_remap)
+    if ((c & 0xE000u) == OAI4G_CTL_CODE) c = 0xFFFF;
+  memset(cfg->h.ctlmask, 0, sizeof(cfg->h.ctlmask));
+  cfg->h.ctl_on = 0;
+  if (cfg->d_ctl) hipFree(cfg->d_ctl);
+  cfg->d_ctl = nullptr;
+  cfg->h.ctl_tab = nullptr;
+  if ((uint32_t)n_ue + n_common > 0) {
+    if (cfg->h_remap.empty()) { set_err("set_control: configuration has no RE map"); return -1; }
+    std::vector<uint32_t> tab((size_t)10 * 3 * 2 * N, 0);
+    const size_t gbytes = (size_t)3 * N * 4, gpad = (gbytes + 255) & ~(size_t)255;
+    const size_t mcap = (size_t)4 * 1024;    /* >= 4 nquad REs for every geometry */
+    uint8_t *buf = scratch(2 * gpad + mcap * 4 + mcap * 2 + 256);
+    if (!buf) return -1;
+    int32_t *d0 = (int32_t *)buf, *d1 = (int32_t *)(buf + gpad);
+    uint32_t *dmap = (uint32_t *)(buf + 2 * gpad);
+    uint16_t *dsrc = (uint16_t *)(buf + 2 * gpad + mcap * 4);
+    std::vector<uint32_t> g(3 * (size_t)N);
+    for (uint32_t sf = 0; sf < 10; sf++) {
+      dci_args_t a;
+      std::vector<uint32_t> map;
+      std::vector<uint16_t> src;
+      const uint8_t npd = dci_prepare(n_ue, n_common, dci, cfg->p.amp, &cfg->fp, sf, a, map, src);
+      if (npd < 1 || npd > 3) return -1;
+      if (npd > cfg->p.num_pdcch_symbols) {
+        set_err("set_control: the DCIs need %u control symbols but the PDSCH starts at symbol %u (dlsim.c:2562-2565)",
+                npd, cfg->p.num_pdcch_symbols);
+        return -1;
+      }
+      if (map.size() > mcap) { set_err("set_control: PDCCH map too large"); return -1; }
+      HCK(hipMemsetAsync(buf, 0, 2 * gpad, g_scr.s), -1);
+      HCK(hipMemcpyAsync(dmap, map.data(), map.size() * 4, hipMemcpyHostToDevice, g_scr.s), -1);
+      HCK(hipMemcpyAsync(dsrc, src.data(), src.size() * 2, hipMemcpyHostToDevice, g_scr.s), -1);
+      pcfich_args_t pa;
+      memset(&pa, 0, sizeof(pa));
+      uint16_t reg[4];
+      uint8_t fi;
+      pcfich_regs(&cfg->fp, reg, &fi);
+      pa.c_init = ((((2u * cfg->fp.Nid_cell) + 1u) * (1u + sf)) << 9) + cfg->fp.Nid_cell;
+      pa.cfi = npd;
+      pa.gain = a.gain;
+      pa.mode1 = a.mode1;
+      pa.nushift3 = (uint8_t)(cfg->fp.nushift % 3);
+      for (int q = 0; q < 4; q++) {
+        uint32_t ro = cfg->fp.first_carrier_offset + (uint32_t)reg[q] * 6;
+        if (ro >= N) ro = 1 + ro - N;
+        pa.reg_off[q] = ro;
+      }
+      pa.n_ant = a.n_ant;
+      HCK(oai4g_launch_pcfich(d0, d1, pa, g_scr.s), -1);
+      HCK(oai4g_launch_dci(a, dmap, dsrc, d0, d1, 0, g_scr.s), -1);
+      for (uint32_t ant = 0; ant < 2; ant++) {
+        HCK(hipMemcpyAsync(g.data(), ant ? (void *)d1 : (void *)d0, gbytes, hipMemcpyDeviceToHost, g_scr.s), -1);
+        HCK(hipStreamSynchronize(g_scr.s), -1);
+        if (ant >= a.n_ant) continue;
+        for (uint32_t l = 0; l < npd; l++)
+          for (uint32_t k = 0; k < N; k++) {
+            const uint32_t v = g[(size_t)l * N + k];
+            if (!v) continue;
+            tab[(((size_t)sf * 3 + l) * 2 + ant) * N + k] = v;
+            uint16_t &code = cfg->h_remap[((size_t)sf * 14 + l) * N + k];
+            if (code != 0xFFFF && code != OAI4G_CTL_CODE) { set_err("set_control: control RE collides"); return -1; }
+            code = (uint16_t)OAI4G_CTL_CODE;
+            cfg->h.ctlmask[sf] |= 1u << l;
+          }
+      }
+    }
+    HCK(hipMalloc(&cfg->d_ctl, tab.size() * 4), -1);
+    HCK(hipMemcpy(cfg->d_ctl, tab.data(), tab.size() * 4, hipMemcpyHostToDevice), -1);
+    cfg->h.ctl_tab = cfg->d_ctl;
+    cfg->h.ctl_on = 1;
+  }
+  if (upload_remap(cfg) != 0) return -1;
+  HCK(hipMemcpy(cfg->d, &cfg->h, sizeof(cfg_dev_t), hipMemcpyHostToDevice), -1);
   return 0;
 }

@@ -20,6 +20,7 @@
 #define OAI4G_PIPE_MAX_CHUNKS 16
 #define OAI4G_CRS_CODE 0xE000u               /* remap codes >= this (and != 0xFFFF) are CRS REs:
                                                 CRS_CODE | pilot entry i << 9 | port & 1 << 8 | m */
+#define OAI4G_CTL_CODE 0xC000u               /* remap code of a control-region RE (generate_dci_top) */
 #define OAI4G_ENC_CRC_TABLE_WORDS (256 + 256 + 8 * 96 + 6 * 96) /* byte tables A/B + tree multipliers */
 #define OAI4G_GOLD_LANES 256
 #define OAI4G_GOLD_STRIDE 17   /* odd: lanes 17l + k hit distinct LDS banks */
@@ -125,6 +126,10 @@ struct cfg_dev_t {
   uint32_t pilmask;             /* bit l: symbol l carries CRS (QAM levels scaled by rho_B) */
   const uint32_t *crs_tab;      /* [10][6][200] packed CRS IQ of pilot symbol i (l = 0, 4, 7, 11; 1, 8 for
                                    ports 2/3 with 4 TX antennas), index m */
+  const uint32_t *ctl_tab;      /* [10][3][2][N] packed IQ of the control region (PCFICH + PDCCH, antennas
+                                   0 / 1) per subframe index; REs with code OAI4G_CTL_CODE take it */
+  uint32_t ctlmask[10];         /* bit l: symbol l of subframe index sf carries control REs */
+  uint32_t ctl_on;
   const uint32_t *gold_x1;      /* [256]     x1 state after 50+16l word steps */
   const uint32_t *gold_x2j;     /* [256][32] columns of M2^(50+16l) */
   const uint32_t *tw;           /* 2 x OAI4G_TW_TOTAL packed twiddles t, then (-t.im, t.re) */
@@ -194,6 +199,30 @@ struct pcfich_args_t {
   uint32_t n_ant;
 };
 hipError_t oai4g_launch_pcfich(int32_t *d_g0, int32_t *d_g1, const pcfich_args_t &a, hipStream_t s);
+
+/* PDCCH (generate_dci_top, dci.c:2024-2346) */
+#define OAI4G_MAX_DCI 32
+struct dci_dev_t {
+  uint8_t flip[8];      /* the pdu bytes in generate_dci0's order (dci.c:233-251) */
+  uint32_t A;           /* DCI bits */
+  uint32_t L;           /* log2 aggregation level */
+  int32_t nCCE;
+  uint32_t rnti;
+};
+struct dci_args_t {
+  uint32_t n_dci;
+  dci_dev_t dci[OAI4G_MAX_DCI];
+  uint32_t nbits;       /* scrambled PDCCH bits, 8 * nquad (pdcch_scrambling length) */
+  uint32_t c_init;      /* (subframe << 9) + Nid_cell */
+  uint32_t n_re;        /* REs mapped */
+  int16_t gain;         /* QPSK amplitude (dci.c:2170-2174) */
+  uint8_t mode1;        /* 1: SISO (<NIL> -> 0), 0: ALAMOUTI (<NIL> -> +gain) */
+  uint8_t n_ant;        /* antennas written (nb_antennas_tx_eNB > 1 ? 2 : 1) */
+};
+/* map[r] = grid offset of mapped RE r (symbol * N + subcarrier), src[r] = its QPSK symbol index
+ * after quadruplet interleaving and the cyclic shift.  One workgroup. */
+hipError_t oai4g_launch_dci(const dci_args_t &a, const uint32_t *d_map, const uint16_t *d_src, int32_t *d_g0,
+                            int32_t *d_g1, uint32_t g1_stride, hipStream_t s);
 
 /* UE receive front end (oai4g_fep.hip): per-symbol CP removal + forward DFT */
 #define OAI4G_FEP_MAX_SYM 14

@@ -688,6 +688,8 @@ __global__ void __launch_bounds__(128) MODOFDM_ATTR k_modofdm(const cfg_dev_t *_
     const uint32_t sfi = (c->first_sf + (sf0 + sf) * c->sf_step) % 10;
     const uint32_t nre = active ? c->symnre[sfi][l] : 0u, re0 = c->symbase[sfi][l];
     const bool crs_sym = (c->pilmask >> l) & 1u;    /* CRS-bearing symbol: rho_B QAM levels */
+    /* symbol with static REs: CRS (with_crs) or the control region (set_control) */
+    const bool stat_sym = (c->with_crs && crs_sym) || ((c->ctlmask[sfi] >> l) & 1u);
     const uint32_t pil = crs_sym ? 1u : 0u;
     /* output placement: slot, symbol-in-slot i */
     const uint32_t slot = l >= sps ? 1u : 0u, si = l - slot * sps;
@@ -695,7 +697,7 @@ __global__ void __launch_bounds__(128) MODOFDM_ATTR k_modofdm(const cfg_dev_t *_
     const int cp = (int)(si == 0 ? c->cp0 : c->cp);
     uint32_t *dst0 = (uint32_t *)iq + (size_t)sf * n_ant * c->spt + body;
 
-    if (UNITS == 1 && nre == 0 && !(CRS && crs_sym)) {
+    if (UNITS == 1 && nre == 0 && !(CRS && stat_sym)) {
       /* control-region symbol: the transform of an all-zero grid is zero */
       fetch(base + stride);
       if (active)
@@ -726,7 +728,8 @@ __global__ void __launch_bounds__(128) MODOFDM_ATTR k_modofdm(const cfg_dev_t *_
     fetch(base + stride);
 
     gu32_t *crs_tab = (gu32_t *)c->crs_tab;
-    const bool crs = CRS && crs_sym;
+    const bool crs = CRS && stat_sym;
+    gu32_t *ctl_tab = (gu32_t *)c->ctl_tab;
     const uint32_t *e0 = lds_e[unit][0], *e1 = lds_e[unit][1];
     const uint32_t *q0 = qtab[0][pil], *q1 = qtab[1][pil];
     /* bit position of data RE idx within the staged words: idx * Qm + (re0 * Qm - 32 wlo) */
@@ -749,7 +752,7 @@ __global__ void __launch_bounds__(128) MODOFDM_ATTR k_modofdm(const cfg_dev_t *_
 #pragma unroll
             for (int n = 0; n < GR; n++) {
               code[n] = (rw[(g + n) >> 1] >> (16 * ((g + n) & 1))) & 0xFFFFu;
-              p[n] = __umul24(code[n] < OAI4G_CRS_CODE ? (code[n] & IDXM) : 0u, Qm0) + b0;
+              p[n] = __umul24(code[n] < OAI4G_CTL_CODE ? (code[n] & IDXM) : 0u, Qm0) + b0;
             }
 #pragma unroll
             for (int n = 0; n < GR; n++) { lo[n] = e0[p[n] >> 5]; hi[n] = e0[(p[n] >> 5) + 1]; }
@@ -767,7 +770,7 @@ __global__ void __launch_bounds__(128) MODOFDM_ATTR k_modofdm(const cfg_dev_t *_
             if constexpr (CW2) {
 #pragma unroll
               for (int n = 0; n < GR; n++) {
-                p[n] = __umul24(code[n] < OAI4G_CRS_CODE ? (code[n] & 0x7FFFu) : 0u, Qm1) + b1;
+                p[n] = __umul24(code[n] < OAI4G_CTL_CODE ? (code[n] & 0x7FFFu) : 0u, Qm1) + b1;
                 lo[n] = e1[p[n] >> 5];
                 hi[n] = e1[(p[n] >> 5) + 1];
               }
@@ -776,7 +779,7 @@ __global__ void __launch_bounds__(128) MODOFDM_ATTR k_modofdm(const cfg_dev_t *_
             }
 #pragma unroll
             for (int n = 0; n < GR; n++) {
-              const bool valid = code[n] < OAI4G_CRS_CODE;         /* a PDSCH data RE */
+              const bool valid = code[n] < OAI4G_CTL_CODE;         /* a PDSCH data RE */
               const s16x2 x0 = u2c(valid ? v0[n] : 0u);
               if constexpr (MODE == 1) {
                 alm_pair(x0, u2c(valid ? v1[n] : 0u), code[n] & 1u, x[0][g + n], x[1][g + n]);
@@ -806,6 +809,16 @@ __global__ void __launch_bounds__(128) MODOFDM_ATTR k_modofdm(const cfg_dev_t *_
 #pragma unroll
                 for (int a = 0; a < NA; a++)
                   if (pil_re) x[a][n] = (NA == 1 || (uint32_t)a + 2 * pair == port) ? u2c(pv) : (s16x2){0, 0};
+                /* control region (generate_dci_top writes antennas 0 and 1 only, dci.c:2260-2336) */
+                const bool ctl_re = (cd & 0xE000u) == OAI4G_CTL_CODE;
+                if (ctl_re) {
+                  const size_t cb = ((size_t)(sfi * 3 + l) * 2) * N + (uint32_t)t + (uint32_t)(N / 16) * (uint32_t)n;
+#pragma unroll
+                  for (int a = 0; a < NA; a++) {
+                    const uint32_t ant = NA == 1 ? 0u : (uint32_t)a + 2 * pair;
+                    x[a][n] = ant < 2 ? u2c(ctl_tab[cb + ant * N]) : (s16x2){0, 0};
+                  }
+                }
               }
             }
           }
@@ -858,7 +871,7 @@ template <int LOG2N, int MODE, bool ECP>
 static hipError_t launch_modofdm_c(const cfg_dev_t *d_cfg, const cfg_dev_t *h_cfg, int sf0, int n_items,
                                    const uint32_t *d_ebits, int32_t *d_iq, hipStream_t s)
 {
-  return h_cfg->with_crs ? launch_modofdm_t<LOG2N, MODE, true, ECP>(d_cfg, h_cfg, sf0, n_items, d_ebits, d_iq, s)
+  return (h_cfg->with_crs || h_cfg->ctl_on) ? launch_modofdm_t<LOG2N, MODE, true, ECP>(d_cfg, h_cfg, sf0, n_items, d_ebits, d_iq, s)
                          : launch_modofdm_t<LOG2N, MODE, false, ECP>(d_cfg, h_cfg, sf0, n_items, d_ebits, d_iq, s);
 }
 
@@ -922,7 +935,7 @@ __global__ void __launch_bounds__(256) k_modulate_bytes(const cfg_dev_t *__restr
   uint32_t l = gid / N, k = gid % N;
   const uint16_t *row = c->remap + ((size_t)sfi * 14 + l) * N;
   uint32_t code = row[k];
-  if (code >= OAI4G_CRS_CODE) return;                 /* no data RE (CRS codes included) */
+  if (code >= OAI4G_CTL_CODE) return;                 /* no data RE (CRS / control codes included) */
   const cw_dev_t &cw0 = c->cw[0];
   const cw_dev_t &cw1 = c->cw[1];
   bool pil = pilots_of(l, nsymb == 12) != 0;

@@ -298,6 +298,10 @@ int orc_init_frame(orc_frame_t *fp, uint16_t N_RB_DL, uint16_t Nid_cell, uint8_t
   fp->first_carrier_offset = fp->ofdm_symbol_size - 6 * N_RB_DL;
   fp->nb_prefix_samples = cp >> sh;
   fp->nb_prefix_samples0 = cp0 >> sh;
+  fp->phich_resource = 6;              /* Ng = one, as dlsim.c:138 */
+  fp->phich_duration = 0;
+  fp->tdd_config = 3;
+  fp->nb_antennas_tx_eNB = nb_antennas_tx;   /* dlsim.c:137 */
   return 0;
 }
 
@@ -1040,8 +1044,24 @@ void orc_generate_pilots_subframe(int32_t **txdataF, int16_t amp, const orc_fram
 static int g_last_re_allocated = 0;
 int orc_last_re_allocated(void) { return g_last_re_allocated; }
 
+static int tx_subframe_impl(const orc_tx_cfg_t *cfg, uint8_t *payload[2], int32_t **txdataF, int32_t **txdata,
+                            uint8_t *e_out[2], uint8_t n_ue_dci, uint8_t n_common_dci, const orc_dci_alloc_t *dci);
+
 int orc_tx_subframe(const orc_tx_cfg_t *cfg, uint8_t *payload[2], int32_t **txdataF, int32_t **txdata,
                     uint8_t *e_out[2])
+{
+  return tx_subframe_impl(cfg, payload, txdataF, txdata, e_out, 0, 0, NULL);
+}
+
+/* dlsim's phy_proc_tx grid: generate_dci_top (dlsim.c:2553) + PDSCH + pilots, then OFDM */
+int orc_tx_subframe_dci(const orc_tx_cfg_t *cfg, uint8_t *payload[2], int32_t **txdataF, int32_t **txdata,
+                        uint8_t *e_out[2], uint8_t n_ue_dci, uint8_t n_common_dci, const orc_dci_alloc_t *dci)
+{
+  return tx_subframe_impl(cfg, payload, txdataF, txdata, e_out, n_ue_dci, n_common_dci, dci);
+}
+
+static int tx_subframe_impl(const orc_tx_cfg_t *cfg, uint8_t *payload[2], int32_t **txdataF, int32_t **txdata,
+                            uint8_t *e_out[2], uint8_t n_ue_dci, uint8_t n_common_dci, const orc_dci_alloc_t *dci)
 {
   const orc_frame_t *fp = &cfg->fp;
   uint8_t *e_buf[2] = {NULL, NULL};
@@ -1088,6 +1108,18 @@ int orc_tx_subframe(const orc_tx_cfg_t *cfg, uint8_t *payload[2], int32_t **txda
   int ret = modulation_impl(txdataF, cfg->amp, cfg->subframe, 0, fp, cfg->num_pdcch_symbols, &c0,
                             cfg->n_cw > 1 ? &c1 : NULL, cfg->sqrt_rho_a, cfg->sqrt_rho_b);
   g_last_re_allocated = ret;
+  if (n_ue_dci + n_common_dci > 0) {            /* control region on a frame grid, copied back */
+    int32_t *fg[4] = {0};
+    for (int aa = 0; aa < fp->nb_antennas_tx; aa++) {
+      fg[aa] = (int32_t *)calloc((size_t)10 * nsymb * N, sizeof(int32_t));
+      memcpy(fg[aa] + (size_t)cfg->subframe * nsymb * N, txdataF[aa], sizeof(int32_t) * N * nsymb);
+    }
+    orc_generate_dci_top(n_ue_dci, n_common_dci, dci, 0, cfg->amp, fp, fg, cfg->subframe);
+    for (int aa = 0; aa < fp->nb_antennas_tx; aa++) {
+      memcpy(txdataF[aa], fg[aa] + (size_t)cfg->subframe * nsymb * N, sizeof(int32_t) * N * nsymb);
+      free(fg[aa]);
+    }
+  }
   /* do_OFDM_mod (ofdm_mod.c:233-286): normal_prefix_mod per slot, or PHY_ofdm_mod of 6 symbols
    * with the extended prefix */
   const int sps = nsymb >> 1;

@@ -77,6 +77,11 @@ typedef struct {
   uint16_t nb_prefix_samples;
   uint16_t nb_prefix_samples0;
   uint32_t samples_per_tti;
+  /* control region (LTE_DL_FRAME_PARMS phich_config_common, tdd_config, nb_antennas_tx_eNB) */
+  uint8_t phich_resource;   /* PHICH_RESOURCE_t (impl_defs_lte.h:80-85): 1, 3, 6, 12 = Ng 1/6, 1/2, 1, 2 */
+  uint8_t phich_duration;   /* 0 normal, 1 extended */
+  uint8_t tdd_config;
+  uint8_t nb_antennas_tx_eNB;
 } orc_frame_t;
 int orc_init_frame(orc_frame_t *fp, uint16_t N_RB_DL, uint16_t Nid_cell, uint8_t Ncp, uint8_t nb_antennas_tx,
                    uint8_t mode1_flag, uint8_t frame_type);
@@ -158,6 +163,41 @@ int orc_rate_matching_turbo_rx(uint32_t RTC, uint32_t G, int16_t *w, const uint8
                                uint8_t C, uint32_t Nsoft, uint8_t Mdlharq, uint8_t Kmimo, uint8_t rvidx, uint8_t clear,
                                uint8_t Qm, uint8_t Nl, uint8_t r, uint32_t *E_out);
 void orc_sub_block_deinterleaving_turbo(uint32_t D, int16_t *d, const int16_t *w);
+
+/* ---- control region: PDCCH / DCI (oai_oracle_ctrl.c; dci.c:62-341, 1905-2346, 2494-2538,
+ *      phich.c:59-118, 280-386, ccoding_byte_lte.c:55-230, lte_rate_matching.c:133-190, 637-680,
+ *      crc_byte.c:155-171, phy_procedures_lte_eNb.c:308-391) ---- */
+typedef struct {           /* DCI_ALLOC_t (LTE_TRANSPORT/defs.h:734-749) */
+  uint8_t dci_length;      /* bits */
+  uint8_t L;               /* log2 aggregation level */
+  int32_t nCCE;            /* first CCE, < 0: not transmitted */
+  uint8_t ra_flag;
+  uint16_t rnti;
+  uint32_t format;
+  uint8_t dci_pdu[8];
+} orc_dci_alloc_t;
+uint32_t orc_crc16(const uint8_t *in, int bitlen);
+void orc_ccodelte_encode(int32_t numbits, uint8_t add_crc, const uint8_t *in, uint8_t *out, uint16_t rnti);
+uint32_t orc_sub_block_interleaving_cc(uint32_t D, const uint8_t *d, uint8_t *w);
+uint32_t orc_lte_rate_matching_cc(uint32_t RCC, uint16_t E, const uint8_t *w, uint8_t *e);
+uint8_t orc_get_mi(const orc_frame_t *fp, uint8_t subframe);
+uint16_t orc_get_nquad(uint8_t num_pdcch_symbols, const orc_frame_t *fp, uint8_t mi);
+uint16_t orc_get_nCCE(uint8_t num_pdcch_symbols, const orc_frame_t *fp, uint8_t mi);
+uint8_t orc_get_num_pdcch_symbols(uint8_t num_dci, const orc_dci_alloc_t *dci_alloc, const orc_frame_t *fp,
+                                  uint8_t subframe);
+/* phich_reg[56][3] (normal PHICH duration); returns the number of groups written */
+int orc_phich_reg_mapping(const orc_frame_t *fp, uint16_t phich_reg[56][3]);
+/* get_nCCE_offset over a caller-owned CCE_table[800] */
+int orc_get_nCCE_offset(int *CCE_table, uint8_t L, int nCCE, int common_dci, uint16_t rnti, uint8_t subframe);
+/* generate_dci_top into the frame grids txdataF[ant]; returns num_pdcch_symbols */
+uint8_t orc_generate_dci_top(uint8_t num_ue_spec_dci, uint8_t num_common_dci, const orc_dci_alloc_t *dci_alloc,
+                             uint32_t n_rnti, int16_t amp, const orc_frame_t *fp, int32_t **txdataF,
+                             uint32_t subframe);
+/* the scrambled PDCCH bits e[] of the last orc_generate_dci_top (values 0/1/2 = NIL), for tests */
+const uint8_t *orc_last_dci_e(uint32_t *len);
+/* orc_tx_subframe plus generate_dci_top's PCFICH + PDCCH before the OFDM step (dlsim.c:2553) */
+int orc_tx_subframe_dci(const orc_tx_cfg_t *cfg, uint8_t *payload[2], int32_t **txdataF, int32_t **txdata,
+                        uint8_t *e_out[2], uint8_t n_ue_dci, uint8_t n_common_dci, const orc_dci_alloc_t *dci);
 
 #ifdef __cplusplus
 }

@@ -24,7 +24,9 @@ class OrcFrame(ctypes.Structure):
                 ("frame_type", ctypes.c_uint8), ("symbols_per_tti", ctypes.c_uint8),
                 ("log2_symbol_size", ctypes.c_uint8), ("ofdm_symbol_size", ctypes.c_uint16),
                 ("first_carrier_offset", ctypes.c_uint16), ("nb_prefix_samples", ctypes.c_uint16),
-                ("nb_prefix_samples0", ctypes.c_uint16), ("samples_per_tti", ctypes.c_uint32)]
+                ("nb_prefix_samples0", ctypes.c_uint16), ("samples_per_tti", ctypes.c_uint32),
+                ("phich_resource", ctypes.c_uint8), ("phich_duration", ctypes.c_uint8), ("tdd_config", ctypes.c_uint8),
+                ("nb_antennas_tx_eNB", ctypes.c_uint8)]
 
 
 class OrcCw(ctypes.Structure):
@@ -269,8 +271,9 @@ def tx_cfg_from_params(p, subframe):
     return c
 
 
-def tx_subframe(cfg, payloads, want_e=False):
-    """Run the oracle on one subframe.  payloads: list of byte arrays (TBS/8 each).
+def tx_subframe(cfg, payloads, want_e=False, dci=None, n_common=0):
+    """Run the oracle on one subframe.  payloads: list of byte arrays (TBS/8 each); dci: optional
+    generate_dci_top items (dci_length, L, nCCE, rnti, pdu) for the control region.
     Returns (txdata [n_ant][spt] int32, txdataF [n_ant][14*N], e list)."""
     fp = cfg.fp
     n_ant = fp.nb_antennas_tx
@@ -287,7 +290,11 @@ def tx_subframe(cfg, payloads, want_e=False):
     dptrs = (ctypes.c_void_p * n_ant)(*[a.ctypes.data for a in txd])
     es = [np.zeros(14 * 1200 * 6 + 64, dtype=np.uint8) for _ in range(cfg.n_cw)]
     eptrs = (ctypes.c_void_p * 2)(*[e.ctypes.data for e in es] + [None] * (2 - len(es)))
-    rc = orc().orc_tx_subframe(ctypes.byref(cfg), pay, fptrs, dptrs, eptrs if want_e else None)
+    if dci:
+        rc = orc().orc_tx_subframe_dci(ctypes.byref(cfg), pay, fptrs, dptrs, eptrs if want_e else None,
+                                       len(dci) - n_common, n_common, dci_allocs(dci))
+    else:
+        rc = orc().orc_tx_subframe(ctypes.byref(cfg), pay, fptrs, dptrs, eptrs if want_e else None)
     assert rc == 0
     return np.stack(txd), np.stack(txF), es
 
@@ -346,3 +353,84 @@ def subblock_deinterleave(w, K):
                                              P(np.ascontiguousarray(w, dtype=np.int16)))
     return buf[96:96 + 3 * K + 12].copy()
 
+
+
+# ------------------------------------------------------------------ control region (oai_oracle_ctrl.c)
+class OrcDciAlloc(ctypes.Structure):
+    """orc_dci_alloc_t = DCI_ALLOC_t (LTE_TRANSPORT/defs.h:734-749)"""
+    _fields_ = [("dci_length", ctypes.c_uint8), ("L", ctypes.c_uint8), ("nCCE", ctypes.c_int32),
+                ("ra_flag", ctypes.c_uint8), ("rnti", ctypes.c_uint16), ("format", ctypes.c_uint32),
+                ("dci_pdu", ctypes.c_uint8 * 8)]
+
+
+def dci_allocs(items, cls=OrcDciAlloc):
+    """items: list of (dci_length, L, nCCE, rnti, pdu bytes) -> ctypes array"""
+    arr = (cls * max(1, len(items)))()
+    for a, (ln, L, ncce, rnti, pdu) in zip(arr, items):
+        a.dci_length, a.L, a.nCCE, a.rnti = ln, L, ncce, rnti
+        for i, b in enumerate(pdu[:8]):
+            a.dci_pdu[i] = int(b)
+    return arr
+
+
+def crc16(data, bitlen):
+    a = np.zeros(len(data) + 8, np.uint8)
+    a[:len(data)] = data
+    orc().orc_crc16.restype = ctypes.c_uint32
+    return orc().orc_crc16(P(a), bitlen)
+
+
+def ccode_encode(data, numbits, add_crc, rnti):
+    a = np.zeros(len(data) + 8, np.uint8)
+    a[:len(data)] = data
+    out = np.zeros(3 * (numbits + 16) + 16, np.uint8)
+    orc().orc_ccodelte_encode(numbits, add_crc, P(a), P(out), ctypes.c_uint16(rnti))
+    return out[:3 * (numbits + (16 if add_crc == 2 else 0))]
+
+
+def ref_ccode_encode(data, numbits, add_crc, rnti):
+    L = ref_coding()
+    a = np.zeros(len(data) + 8, np.uint8)
+    a[:len(data)] = data
+    out = np.zeros(3 * (numbits + 16) + 16, np.uint8)
+    L.ccodelte_encode(numbits, add_crc, P(a), P(out), rnti)
+    return out[:3 * (numbits + (16 if add_crc == 2 else 0))]
+
+
+def generate_dci_top(items, n_common, amp, fp, grids, subframe):
+    """orc_generate_dci_top on frame grids (int32 arrays, modified in place); returns num_pdcch_symbols"""
+    L = orc()
+    L.orc_generate_dci_top.restype = ctypes.c_uint8
+    arr = dci_allocs(items)
+    gp = (ctypes.c_void_p * len(grids))(*[g.ctypes.data for g in grids])
+    return L.orc_generate_dci_top(len(items) - n_common, n_common, arr, 0, ctypes.c_int16(amp), ctypes.byref(fp),
+                                  gp, subframe)
+
+
+def last_dci_e():
+    L = orc()
+    L.orc_last_dci_e.restype = ctypes.POINTER(ctypes.c_uint8)
+    n = ctypes.c_uint32()
+    p = L.orc_last_dci_e(ctypes.byref(n))
+    return np.ctypeslib.as_array(p, shape=(n.value,)).copy() if n.value else np.zeros(0, np.uint8)
+
+
+def get_nCCE(npdcch, fp, mi=1):
+    orc().orc_get_nCCE.restype = ctypes.c_uint16
+    return orc().orc_get_nCCE(npdcch, ctypes.byref(fp), mi)
+
+
+def get_nquad(npdcch, fp, mi=1):
+    orc().orc_get_nquad.restype = ctypes.c_uint16
+    return orc().orc_get_nquad(npdcch, ctypes.byref(fp), mi)
+
+
+def phich_reg_mapping(fp):
+    reg = (ctypes.c_uint16 * (56 * 3))()
+    n = orc().orc_phich_reg_mapping(ctypes.byref(fp), reg)
+    return [tuple(reg[3 * i:3 * i + 3]) for i in range(n)]
+
+
+def get_nCCE_offset(table, L, nCCE, common, rnti, subframe):
+    return orc().orc_get_nCCE_offset(table.ctypes.data_as(ctypes.POINTER(ctypes.c_int)), L, nCCE, common, rnti,
+                                     subframe)

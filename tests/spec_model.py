@@ -522,3 +522,187 @@ def cdd2_grid(e0, e1, res, Qm0, Qm1, N, amp=512, srho_a=8192, srho_b=8192, Ncp=0
         grid[1, l * N + b] = (_w16(s * ((x0[0] - x1[0]) >> 1)), _w16(s * ((x0[1] - x1[1]) >> 1)))
         i_rb += 1
     return _pack(grid), len(res)
+
+
+# ------------------------------------------------------------------ PDCCH (36.212 5.3.3, 36.211 6.8)
+CC_COLPERM = [1, 17, 9, 25, 5, 21, 13, 29, 3, 19, 11, 27, 7, 23, 15, 31,
+              0, 16, 8, 24, 4, 20, 12, 28, 2, 18, 10, 26, 6, 22, 14, 30]   # 36.212 Table 5.1.4-2
+
+
+def crc16_ref(bits):
+    """CRC16 parity bits p_0..p_15 of 36.212 5.1.1 (g = D^16 + D^12 + D^5 + 1) for whole bytes.
+    Departure (cited parameter): for a partial last byte the reference's crc16 (crc_byte.c:167-168)
+    shifts the register by `resbit` and looks up a table entry indexed by the resbit-bit
+    remainder, which is not the spec's polynomial division; the model reproduces that step."""
+    g = [16, 12, 5, 0]
+    n = len(bits)
+    full = n - n % 8
+    reg = 0                                          # 16-bit register, MSB = oldest
+    for b in bits[:full]:
+        fb = ((reg >> 15) & 1) ^ b
+        reg = (reg << 1) & 0xFFFF
+        if fb:
+            reg ^= 0x1021
+    r = n % 8
+    if r:
+        tab = _crc16_byte_table()
+        v = 0
+        for b in bits[full:]:
+            v = (v << 1) | b
+        crc32 = reg << 16
+        crc32 = ((crc32 << r) & 0xFFFFFFFF) ^ (tab[(v ^ (crc32 >> (32 - r))) & 0xFF] << 16)
+        reg = (crc32 >> 16) & 0xFFFF
+    return [(reg >> (15 - i)) & 1 for i in range(16)]
+
+
+_C16 = []
+
+
+def _crc16_byte_table():
+    if not _C16:
+        for v in range(256):
+            reg = 0
+            for i in range(8):
+                fb = ((reg >> 15) & 1) ^ ((v >> (7 - i)) & 1)
+                reg = (reg << 1) & 0xFFFF
+                if fb:
+                    reg ^= 0x1021
+            _C16.append(reg)
+    return _C16
+
+
+def tbcc_encode(c):
+    """36.212 5.1.3.1 tail-biting convolutional code, g0 = 133, g1 = 171, g2 = 165 (octal): the
+    register starts with the last six input bits; returns d in the reference layout
+    (d^(0)_k, d^(1)_k, d^(2)_k per k)."""
+    G = [[(g >> (6 - j)) & 1 for j in range(7)] for g in (0o133, 0o171, 0o165)]
+    K = len(c)
+    d = []
+    for k in range(K):
+        taps = [c[(k - j) % K] for j in range(7)]     # c_k, c_{k-1}, ... (tail-biting wrap)
+        for i in range(3):
+            d.append(sum(G[i][j] & taps[j] for j in range(7)) & 1)
+    return d
+
+
+def cc_rate_match(d, E):
+    """36.212 5.1.4.2: sub-block interleaving of each stream (Table 5.1.4-2 permutation, <NULL>
+    padding in front), w = v0 || v1 || v2, circular selection skipping <NULL>."""
+    D = len(d) // 3
+    R = -(-D // 32)
+    ND = 32 * R - D
+    w = []
+    for s in range(3):
+        y = [NULL] * ND + d[s::3]
+        w += [y[32 * row + CC_COLPERM[col]] for col in range(32) for row in range(R)]
+    e, k = [], 0
+    while len(e) < E:
+        if w[k % len(w)] != NULL:
+            e.append(w[k % len(w)])
+        k += 1
+    return e
+
+
+def dci_bits(pdu, length):
+    """The DCI payload a_0..a_{A-1}: generate_dci0 reads the DCI_ALLOC_t pdu bytes in reverse
+    order (dci.c:233-251, the little-endian bit-field struct) and takes the first A bits MSB-first."""
+    flip = list(reversed(list(pdu[:4]))) if length <= 32 else list(reversed(list(pdu[:8])))
+    return bytes_to_bits(flip, length)
+
+
+def dci_e(pdu, length, L, rnti):
+    """36.212 5.3.3: CRC16 attachment with the RNTI mask, TBCC, rate matching to 72 * 2^L bits."""
+    a = dci_bits(pdu, length)
+    p = crc16_ref(a)
+    x = [(rnti >> (15 - i)) & 1 for i in range(16)]
+    c = a + [p[i] ^ x[i] for i in range(16)]
+    return cc_rate_match(tbcc_encode(c), 72 << L)
+
+
+def n_reg_pdcch(N_RB, npdcch, n_ant=2):
+    """REGs of the control region (36.211 6.2.4): 2 per RB in symbol 0 (and symbol 1 with 4 ports),
+    3 per RB elsewhere (normal CP)."""
+    return sum((2 if (l == 0 or (l == 1 and n_ant == 4)) else 3) * N_RB for l in range(npdcch))
+
+
+def phich_regs(N_RB, Nid, Ng6, pcfich_regs):
+    """36.211 6.9.3, normal duration, normal CP: PHICH group m' uses REG n_bar_i of symbol 0,
+    n_bar_i = (Nid + m' + floor(i n_0 / 3)) mod n_0 counted over the REGs of symbol 0 NOT used by
+    PCFICH; returned as absolute REG indices of symbol 0 (units of 6 subcarriers)."""
+    ngroup = -(-Ng6 * N_RB // 48)
+    free = [r for r in range(2 * N_RB) if r not in pcfich_regs]
+    n0 = len(free)
+    return [[free[(Nid + m + (i * n0) // 3) % n0] for i in range(3)] for m in range(ngroup)]
+
+
+def pdcch_grid(N_RB, Nid, subframe, dcis, npdcch, amp, N, first_carrier, mode1, n_ant, Ng6=6):
+    """PDCCH REs of the control region per antenna {grid index within the subframe: (re, im)}
+    (36.211 6.8.2 multiplexing with <NIL>, 6.8.2 scrambling c_init = ns/2 2^9 + Nid, 7.1.2 QPSK,
+    6.3.3.3 / 6.3.4.3 transmit diversity, 6.8.5 quadruplet interleaving (36.212 5.1.4.2.1 with the
+    <NULL>s removed) and cyclic shift by Nid, REG mapping frequency-first over k' then l' skipping
+    the PCFICH and PHICH REGs; normal CP, normal PHICH duration).  dcis: (pdu, length, L, nCCE,
+    rnti).  Departures (cited parameters): <NIL> quadruplets carry 0 with one port and +g on both
+    bits with two (dci.c:2182-2224), gains as PCFICH (amp 23170 >> 15, amp / 2)."""
+    nreg = n_reg_pdcch(N_RB, npdcch, n_ant)
+    kbar = 6 * (Nid % (2 * N_RB))
+    pcf = [((kbar + (i * N_RB // 2) * 6) % (12 * N_RB)) // 6 for i in range(4)]
+    ph = phich_regs(N_RB, Nid, Ng6, pcf)
+    ph_set = {r for g in ph for r in g}
+    nquad = nreg - 4 - 3 * len(ph)
+    Mbits = 8 * nquad
+    b = [NIL] * Mbits
+    for pdu, length, L, ncce, rnti in dcis:
+        if ncce < 0:                                 # no free candidate in the search space: not sent
+            continue
+        e = dci_e(pdu, length, L, rnti)
+        b[72 * ncce:72 * ncce + len(e)] = e
+    b = b[:Mbits]
+    c = gold((subframe << 9) + Nid, Mbits)
+    b = [x if x == NIL else x ^ c[i] for i, x in enumerate(b)]
+    g = (amp * 23170) >> 15 if mode1 else int(amp / 2)
+    nsym = Mbits // 2
+    if mode1:
+        d = [(0 if b[2 * i] == NIL else (-g if b[2 * i] else g), 0 if b[2 * i + 1] == NIL else (-g if b[2 * i + 1] else g))
+             for i in range(nsym)]
+        y = [d, d]
+    else:
+        s = [(-g if x == 1 else g) for x in b]     # <NIL> -> +g
+        y0, y1 = [None] * nsym, [None] * nsym
+        for i in range(0, nsym, 2):
+            x0, x1 = (s[2 * i], s[2 * i + 1]), (s[2 * i + 2], s[2 * i + 3])
+            y0[i], y1[i] = x0, (-x1[0], x1[1])
+            y0[i + 1], y1[i + 1] = x1, (x0[0], -x0[1])
+        y = [y0, y1]
+    # quadruplet interleaving (36.212 5.1.4.2.1 on quadruplets, <NULL> removed) + cyclic shift
+    R = -(-nquad // 32)
+    ND = 32 * R - nquad
+    seq = [None] * ND + list(range(nquad))
+    perm = [seq[32 * row + CC_COLPERM[col]] for col in range(32) for row in range(R)]
+    perm = [p for p in perm if p is not None]
+    wbar = [perm[(i + Nid) % nquad] for i in range(nquad)]
+    out = [dict() for _ in range(n_ant)]
+    vs = (Nid % 6) % 3
+    m = 0
+    for kp in range(12 * N_RB):
+        for lp in range(npdcch):
+            if lp == 0:                                  # REGs of 6 REs around the port-0/1 RS
+                if kp % 6 or kp // 6 in pcf or kp // 6 in ph_set:
+                    continue
+                res = [kp + j for j in range(6) if j not in (vs, vs + 3)]
+            else:
+                if kp % 4:
+                    continue
+                res = [kp + j for j in range(4)]
+            q = wbar[m]
+            for j, k in enumerate(res):
+                idx = first_carrier + k
+                if idx >= N:
+                    idx = idx - N + 1
+                for a in range(n_ant):
+                    out[a][lp * N + idx] = y[min(a, 1)][4 * q + j]
+            m += 1
+    assert m == nquad
+    return out
+
+
+NIL = 3
