@@ -13,6 +13,6 @@ step() {  # name, seconds, command...
   return 0
 }
 if [ -n "$PYTEST_K" ]; then KARG=(-k "$PYTEST_K"); else KARG=(); fi
-step pytest_gpu 900 python -m pytest tests -m gpu -q -rf --timeout 300 "${KARG[@]}"
+step pytest_gpu 900 python -u -m pytest tests -m gpu -q -rf --timeout 300 --timeout-method thread "${KARG[@]}"
 step smoke 300 python -c "import __graft_entry__ as g; g.smoke()"
 step bench 600 python bench.py --steps ${BENCH_STEPS:-10} --warmup 2 --cpu-seconds ${CPU_SECONDS:-8}
