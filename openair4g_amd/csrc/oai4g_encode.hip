@@ -441,64 +441,6 @@ static __device__ __forceinline__ void or_bits(uint32_t *w, uint32_t bit, uint32
   if (sh && (v >> (32 - sh))) atomicOr(&w[wi + 1], v >> (32 - sh));
 }
 
-/* position p of the ci-th non-NULL entry of w and m = NULLs before p */
-static __device__ __forceinline__ uint32_t compact_to_pos2(uint32_t ci, const uint16_t *np, uint32_t nn, uint32_t &m)
-{
-  uint32_t lo = 0, hi = nn;
-  while (lo < hi) {
-    uint32_t mid = (lo + hi) >> 1;
-    if ((uint32_t)np[mid] - mid <= ci) lo = mid + 1;
-    else hi = mid;
-  }
-  m = lo;
-  return ci + lo;
-}
-
-/*
- * Rate-matcher output word (lte_rate_matching.c:548-566): `need` non-NULL entries of the
- * circular buffer w[0..Ncb) starting at position p (m NULLs before p, nxt = position of NULL m
- * or ~0).  Inside the buffer a 64-bit window of packed w with the (few) NULL bits squeezed out;
- * the next NULL lives in a register, so a NULL-free word costs no table read.  Across the wrap,
- * bit by bit.
- */
-static __device__ __forceinline__ uint32_t rm_window(const uint32_t *wpk, uint32_t &p, uint32_t &m, uint32_t &nxt,
-                                                     uint32_t Ncb, const uint16_t *np, uint32_t nn, uint32_t need)
-{
-  uint32_t out = 0;
-  if (p + 64 <= Ncb && need == 32) {
-    uint32_t wi = p >> 5, off = p & 31;
-    uint64_t x = ((uint64_t)wpk[wi + 1] << 32) | wpk[wi];
-    x >>= off;
-    if (off) x |= (uint64_t)wpk[wi + 2] << (64 - off);
-    uint32_t del = 0;
-    while (nxt < p + 32 + del) {
-      const uint32_t k = nxt - p - del;
-      const uint64_t lo = (1ull << k) - 1ull;
-      x = (x & lo) | ((x >> 1) & ~lo);
-      del++;
-      m++;
-      nxt = m < nn ? (uint32_t)np[m] : 0xffffffffu;
-    }
-    out = (uint32_t)x;
-    p += 32 + del;
-  } else {
-    uint32_t got = 0;
-    while (got < need) {
-      if (p >= Ncb) { p = 0; m = 0; nxt = nn ? (uint32_t)np[0] : 0xffffffffu; }
-      if (p == nxt) {
-        p++;
-        m++;
-        nxt = m < nn ? (uint32_t)np[m] : 0xffffffffu;
-        continue;
-      }
-      out |= ((wpk[p >> 5] >> (p & 31)) & 1u) << got;
-      got++;
-      p++;
-    }
-  }
-  return need < 32 ? out & ((1u << need) - 1u) : out;
-}
-
 /* ---------------------------------------------------------------------------------------
  * The fused encoder.
  * ------------------------------------------------------------------------------------- */
@@ -519,12 +461,10 @@ static __device__ void encode_codeword(const cfg_dev_t *__restrict__ c, uint32_t
   uint32_t *mul_tb = crctab_b + 256;                     /* [8][6][16] */
   uint32_t *mul_cb = mul_tb + 8 * 96;                    /* [6][6][16] */
   uint32_t *strm = lds_base + c->lds_a_words;
-  uint32_t *ebuf = strm;                                 /* region B again from phase 4c: RM output words */
   uint32_t *tails = strm + c->lds_b_words;
   uint32_t *crcs = tails + 2 * OAI4G_MAX_CB;             /* [0] = CRC24A, [1+r] = CRC24B of block r */
   uint32_t *red = crcs + OAI4G_MAX_CB + 2;               /* 4 per-wave partials */
   enc_tabs_t *tabs = (enc_tabs_t *)(red + 4);
-  uint16_t *np = (uint16_t *)(tabs + 1);
   uint8_t *tbb = (uint8_t *)tbw;
   const uint32_t G = cw.G[sfi], Gw = (G + 31) >> 5;
 
@@ -549,7 +489,6 @@ static __device__ void encode_codeword(const cfg_dev_t *__restrict__ c, uint32_t
       const uint32_t w = ((cw.K[r] + 31) >> 5) + (i & 3u);
       if (w < sw) strm[slot * sw + w] = 0u;
     }
-    for (uint32_t i = ct; i < 2 * OAI4G_MAX_NULLS; i += cn) np[i] = cw.nullpos[i / OAI4G_MAX_NULLS][i % OAI4G_MAX_NULLS];
     for (uint32_t i = ct; i < 8 * 96; i += cn) mul_tb[i] = (&cw.crcmul_tb[0][0][0])[i];
     for (uint32_t i = ct; i < 6 * 96; i += cn) mul_cb[i] = (&cw.crcmul_cb[0][0][0])[i];
     for (uint32_t v = ct; v < 256; v += cn) {
@@ -775,35 +714,41 @@ static __device__ void encode_codeword(const cfg_dev_t *__restrict__ c, uint32_t
   }
   __syncthreads();
 
-  /* ---- phase 4a: zero packed w (region A; the interleaved words are dead) ---- */
-  uint32_t *wb = lds_base;
-  for (uint32_t i = tid; i < cw.wpk_off[C]; i += nth) wb[i] = 0u;
+  /* ---- phase 4: sub-block interleaving (lte_rate_matching.c:51-130) and rate matching
+   * (:464-566) fused.  Each half-wave takes a 32x32 bit tile of one block's streams and transposes
+   * it (5 shuffle stages) so that lane c holds a run of 32 consecutive w bits of column
+   * bitrev5(c): v^(0) tiles are 32 rows of y^(0); interlaced tiles are 16 rows of y^(1) and y^(2)
+   * alternating (lane 2i: y^(1) row, lane 2i+1: y^(2) row, pre-shifted by one for the
+   * (pi(k)+1) mod Kpi rule), so the transposed run is already w's v^(1)/v^(2) interlacing.  w is
+   * never materialised: NULLs sit only at row 0 of a column (and at w[3Kpi-1]), so the run's
+   * position among the non-NULL entries of w is closed-form, and the run goes straight to its
+   * place(s) in the circular-buffer output: e index (ci - k0c) mod Nnn (+ j Nnn while < E),
+   * positions >= Ncb excluded.  Region A (the interleaved words are dead) holds the output. ---- */
+  uint32_t *ebuf = lds_base;
+  for (uint32_t i = tid; i < Gw + 1; i += nth) ebuf[i] = 0u;
   __syncthreads();
-
-  /* ---- phase 4b: sub-block interleaving (lte_rate_matching.c:51-130).  Each half-wave takes
-   * a 32x32 bit tile and transposes it (5 shuffle stages) so that lane c holds a run of column
-   * c, then ORs the run into packed w.  v^(0) tiles are 32 rows of y^(0); a run of column c sits
-   * at w bit bitrev5(c) R + row.  Interlaced tiles are 16 rows of y^(1) and y^(2) alternating
-   * (lane 2i: y^(1) row, lane 2i+1: y^(2) row, pre-shifted by one for the (pi(k)+1) mod Kpi
-   * rule), so the transposed run is already w's v^(1)/v^(2) interlacing, at bit
-   * Kpi + 2 (bitrev5(c) R + row).  Tile t maps to its block in closed form. ---- */
-  /* block geometry of the two block sizes as wave-uniform scalars (closed-form per-block offsets) */
-  const uint32_t R0 = __builtin_amdgcn_readfirstlane(cw.Rk[0]), R1 = __builtin_amdgcn_readfirstlane(cw.Rk[1]);
-  const uint32_t ws0 = 3 * R0 + 2, ws1 = 3 * R1 + 2;     /* packed w words per block (wpk_off stride) */
   {
+    const uint32_t R0 = __builtin_amdgcn_readfirstlane(cw.Rk[0]), R1 = __builtin_amdgcn_readfirstlane(cw.Rk[1]);
     const uint32_t ND0 = __builtin_amdgcn_readfirstlane(cw.NDk[0]), ND1 = __builtin_amdgcn_readfirstlane(cw.NDk[1]);
     const uint32_t nt0 = __builtin_amdgcn_readfirstlane(cw.ntk[0]), nt1 = __builtin_amdgcn_readfirstlane(cw.ntk[1]);
     const uint32_t tz0 = __builtin_amdgcn_readfirstlane(cw.t0k[0]), tz1 = __builtin_amdgcn_readfirstlane(cw.t0k[1]);
     const uint32_t nm0 = __builtin_amdgcn_readfirstlane(cw.ntmag[0]), nm1 = __builtin_amdgcn_readfirstlane(cw.ntmag[1]);
+    const uint32_t Ncb0 = __builtin_amdgcn_readfirstlane(cw.Ncbk[0]), Ncb1 = __builtin_amdgcn_readfirstlane(cw.Ncbk[1]);
+    const uint32_t Nnn0 = __builtin_amdgcn_readfirstlane(cw.Nnnk[0]), Nnn1 = __builtin_amdgcn_readfirstlane(cw.Nnnk[1]);
+    const uint32_t k0c0 = __builtin_amdgcn_readfirstlane(cw.k0ck[0]), k0c1 = __builtin_amdgcn_readfirstlane(cw.k0ck[1]);
+    const uint32_t nc00 = __builtin_amdgcn_readfirstlane(cw.nullcol[0][0]), nc01 = __builtin_amdgcn_readfirstlane(cw.nullcol[0][1]);
+    const uint32_t nc10 = __builtin_amdgcn_readfirstlane(cw.nullcol[1][0]), nc11 = __builtin_amdgcn_readfirstlane(cw.nullcol[1][1]);
+    /* blocks r < es carry E_lo bits, the rest E_hi (36.212 5.1.4.1.2) */
+    const uint32_t es = __builtin_amdgcn_readfirstlane(cw.esplit[sfi]);
+    const uint32_t Elo = __builtin_amdgcn_readfirstlane(cw.E[sfi][0]), Ehi = __builtin_amdgcn_readfirstlane(cw.E[sfi][C - 1]);
     const uint32_t tsplit = n0 * nt0, ntot = tsplit + (C - n0) * nt1;
-    const uint32_t lane32 = tid & 31, wcol = colperm(lane32);
+    const uint32_t lane32 = tid & 31, wcol = colperm(lane32), below = (1u << wcol) - 1u;
     for (uint32_t t = tid >> 5; t < ntot; t += nth >> 5) {
       /* tile t -> block r (tiles of block r: ceil(R/32) v0 tiles, then ceil(R/16) interlaced) */
       const uint32_t ki = t >= tsplit ? 1u : 0u, tt = ki ? t - tsplit : t;
       const uint32_t rr = __umul24(tt, ki ? nm1 : nm0) >> 20, rem = tt - __umul24(rr, ki ? nt1 : nt0);
       const uint32_t r = ki ? n0 + rr : rr, R = ki ? R1 : R0, ND = ki ? ND1 : ND0, tz = ki ? tz1 : tz0;
       const uint32_t il = rem >= tz ? 1u : 0u, rb = il ? rem - tz : rem;
-      const uint32_t wpk = ki ? n0 * ws0 + __umul24(rr, ws1) : __umul24(rr, ws0);
       const uint32_t row = il ? 16 * rb + (lane32 >> 1) : 32 * rb + lane32, s = il ? 1 + (lane32 & 1) : 0;
       const uint32_t *st = strm + __umul24(r * 3 + s, sw);
       uint32_t y = 0;
@@ -815,78 +760,50 @@ static __device__ void encode_codeword(const cfg_dev_t *__restrict__ c, uint32_t
         }
       }
       y = transpose32(y, lane32);
-      or_bits(wb + wpk, il ? 32 * R + 2 * (__umul24(wcol, R) + 16 * rb) : __umul24(wcol, R) + 32 * rb, y);
+      /* lane c = lane32 now holds w bits [p0, p0 + n) of column wcol, rows from 32 rb (v0) or
+       * 16 rb (interlaced); the column's row-0 entries are NULL for c < ND (and y^(2): c + 1 < ND) */
+      const uint32_t Kpi = 32 * R;
+      uint32_t n = il ? min(32u, 2 * (R - 16 * rb)) : min(32u, R - 32 * rb);
+      if (il && lane32 == 31 && ND > 0 && R - 16 * rb <= 16) n--;            /* w[3Kpi-1] is NULL */
+      const uint32_t m0 = ki ? nc10 : nc00, m1 = ki ? nc11 : nc01;
+      const uint32_t zc = (lane32 < ND ? 1u : 0u) + (il && lane32 + 1 < ND ? 1u : 0u);
+      const uint32_t cs = il ? (Kpi - ND) + 2 * __umul24(wcol, R) - __builtin_popcount(m0 & below) -
+                                   __builtin_popcount(m1 & below)
+                             : __umul24(wcol, R) - __builtin_popcount(m0 & below);
+      const uint32_t p0 = il ? Kpi + 2 * (__umul24(wcol, R) + 16 * rb) : __umul24(wcol, R) + 32 * rb;
+      const uint32_t z = rb ? 0u : zc, ci0 = rb ? cs + 32 * rb - zc : cs;
+      const uint32_t Ncb = ki ? Ncb1 : Ncb0, Nnn = ki ? Nnn1 : Nnn0, k0c = ki ? k0c1 : k0c0;
+      int m = (int)n - (int)z;
+      if (p0 + n > Ncb) m = (int)Ncb - (int)(p0 + z);                          /* limited buffer */
+      if (m > 0) {
+        y >>= z;
+        if (m < 32) y &= (1u << m) - 1u;
+        const bool eh = r >= es;
+        const uint32_t E = eh ? Ehi : Elo, ro = eh ? es * Elo + (r - es) * Ehi : r * Elo;
+        /* circular read from compact index k0c: the run may straddle the wrap back to k0c */
+        const uint32_t o = ci0 >= k0c ? ci0 - k0c : ci0 + Nnn - k0c;
+        const uint32_t ma = min((uint32_t)m, Nnn - o);
+        for (uint32_t part = 0; part < 2; part++) {
+          const uint32_t len = part ? (uint32_t)m - ma : ma, os = part ? 0u : o;
+          const uint32_t v = part ? (ma < 32 ? y >> ma : 0u) : (ma < 32 ? y & ((1u << ma) - 1u) : y);
+          for (uint32_t x = os; len && x < E; x += Nnn) {                       /* repetition rounds */
+            const uint32_t l = min(len, E - x);
+            or_bits(ebuf, ro + x, l < 32 ? v & ((1u << l) - 1u) : v);
+          }
+        }
+      }
     }
   }
   __syncthreads();
   if (stop_phase <= 4) return;
-  /* the streams are dead: region B becomes the zeroed RM output words */
-  for (uint32_t i = tid; i < Gw + 1; i += nth) ebuf[i] = 0u;
-  __syncthreads();
-
-  /* ---- phase 4c: rate matching (lte_rate_matching.c:548-566) of every block, XORed into the
-   * Gold-prefilled staging words; each thread walks a run of consecutive output words ---- */
-  {
-    /* blocks r < es carry E_lo bits (W_lo words), the rest E_hi (36.212 5.1.4.1.2) */
-    const uint32_t es = __builtin_amdgcn_readfirstlane(cw.esplit[sfi]);
-    const uint32_t Elo = __builtin_amdgcn_readfirstlane(cw.E[sfi][0]), Ehi = __builtin_amdgcn_readfirstlane(cw.E[sfi][C - 1]);
-    const uint32_t Wlo = __builtin_amdgcn_readfirstlane(cw.ew[sfi][0]), Whi = __builtin_amdgcn_readfirstlane(cw.ew[sfi][1]);
-    const uint32_t Mlo = __builtin_amdgcn_readfirstlane(cw.emag[sfi][0]), Mhi = __builtin_amdgcn_readfirstlane(cw.emag[sfi][1]);
-    const uint32_t Ncb0 = __builtin_amdgcn_readfirstlane(cw.Ncbk[0]), Ncb1 = __builtin_amdgcn_readfirstlane(cw.Ncbk[1]);
-    const uint32_t Nnn0 = __builtin_amdgcn_readfirstlane(cw.Nnnk[0]), Nnn1 = __builtin_amdgcn_readfirstlane(cw.Nnnk[1]);
-    const uint32_t k0c0 = __builtin_amdgcn_readfirstlane(cw.k0ck[0]), k0c1 = __builtin_amdgcn_readfirstlane(cw.k0ck[1]);
-    const uint32_t nn0 = __builtin_amdgcn_readfirstlane(cw.nnull[0]), nn1 = __builtin_amdgcn_readfirstlane(cw.nnull[1]);
-    const uint32_t wsplit = es * Wlo, nwtot = wsplit + (C - es) * Whi;
-    const uint32_t per = (nwtot + nth - 1) / nth, i0 = tid * per, i1 = min(i0 + per, nwtot);
-    /* each thread walks a run of consecutive output words [i0, i1) */
-    uint32_t r = 0, k = 0;
-    if (i0 < i1) {
-      const bool hi = i0 >= wsplit;
-      const uint32_t ii = hi ? i0 - wsplit : i0, W = hi ? Whi : Wlo;
-      uint32_t q = __umulhi(ii, hi ? Mhi : Mlo);
-      q = q * W > ii ? q - 1 : q;
-      r = hi ? es + q : q;
-      k = ii - q * W;
-    }
-    uint32_t p = 0, m = 0, nxt = 0, nwo = 0, nn = 0, Ncb = 0, E = 0, ro = 0, wpk = 0;
-    const uint16_t *npl = np;
-    bool fresh = true;
-    for (uint32_t i = i0; i < i1; i++, k++) {
-      if (fresh) {
-        const uint32_t ki = r < n0 ? 0u : 1u;
-        const bool eh = r >= es;
-        E = eh ? Ehi : Elo;
-        nwo = eh ? Whi : Wlo;
-        ro = eh ? es * Elo + (r - es) * Ehi : r * Elo;
-        npl = np + ki * OAI4G_MAX_NULLS;
-        nn = ki ? nn1 : nn0;
-        Ncb = ki ? Ncb1 : Ncb0;
-        wpk = ki ? n0 * ws0 + (r - n0) * ws1 : r * ws0;
-        p = compact_to_pos2(((ki ? k0c1 : k0c0) + 32 * k) % (ki ? Nnn1 : Nnn0), npl, nn, m);
-        nxt = m < nn ? (uint32_t)npl[m] : 0xffffffffu;
-        fresh = false;
-      }
-      const uint32_t need = min(32u, E - 32 * k);
-      uint32_t out = rm_window(wb + wpk, p, m, nxt, Ncb, npl, nn, need);
-      uint32_t gpos = ro + 32 * k, gw = gpos >> 5, off = gpos & 31;
-      atomicXor(&ebuf[gw], out << off);
-      if (off && (out >> (32 - off))) atomicXor(&ebuf[gw + 1], out >> (32 - off));
-      if (k + 1 == nwo) {
-        r++;
-        k = (uint32_t)-1;
-        fresh = true;
-      }
-    }
-  }
-  __syncthreads();
 
   if (DEBUG) {
     for (uint32_t k = tid; k < G; k += nth) dbg.e[k] = (uint8_t)((ebuf[k >> 5] >> (k & 31)) & 1u);
     return;
   }
-  /* scrambling (dlsch_scrambling.c:51-97): Gold words into region A (packed w is dead), XORed
+  /* scrambling (dlsch_scrambling.c:51-97): Gold words into region B (the streams are dead), XORed
    * into the RM output on the way out */
-  uint32_t *gold = lds_base;
+  uint32_t *gold = strm;
   if (tid < OAI4G_GOLD_LANES) {
     const uint32_t c_init = (c->rnti << 14) + (cw.q << 13) + (sfi << 9) + c->Nid_cell; /* Ns>>1 = subframe */
     gold_generate(gold, Gw, c_init, c->gold_x1, c->gold_x2j);
@@ -920,7 +837,7 @@ __global__ void __launch_bounds__(256) k_encode_debug(const cfg_dev_t *__restric
 static size_t enc_lds_bytes(const cfg_dev_t *h)
 {
   size_t words = (size_t)h->lds_a_words + h->lds_b_words + 2 * OAI4G_MAX_CB + OAI4G_MAX_CB + 2 + 4;
-  size_t bytes = words * 4 + sizeof(enc_tabs_t) + 2 * OAI4G_MAX_NULLS * 2;
+  size_t bytes = words * 4 + sizeof(enc_tabs_t);
   return (bytes + 15) & ~(size_t)15;
 }
 

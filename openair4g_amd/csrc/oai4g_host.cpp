@@ -817,6 +817,13 @@ static int derive_cfg(oai4g_tx_config *cfg, const oai4g_tx_params_t *p, const ui
     }
     if (c.n0 == 0) { c.Rk[0] = c.Rk[1]; c.NDk[0] = c.NDk[1]; c.Ncbk[0] = c.Ncbk[1]; c.Nnnk[0] = c.Nnnk[1]; c.k0ck[0] = c.k0ck[1]; }
     for (int ki = 0; ki < 2; ki++) {
+      c.nullcol[ki][0] = c.nullcol[ki][1] = 0;
+      for (uint32_t wc = 0; wc < 32; wc++) {
+        uint32_t pc = 0;
+        for (int b = 0; b < 5; b++) pc |= ((wc >> b) & 1u) << (4 - b);   /* bitrev5 column permutation */
+        if (pc < c.NDk[ki]) c.nullcol[ki][0] |= 1u << wc;
+        if (pc + 1 < c.NDk[ki]) c.nullcol[ki][1] |= 1u << wc;
+      }
       c.t0k[ki] = (c.Rk[ki] + 31) / 32;
       c.ntk[ki] = c.t0k[ki] + (c.Rk[ki] + 15) / 16;
       c.ntmag[ki] = ((1u << 20) + c.ntk[ki] - 1) / c.ntk[ki];
@@ -870,10 +877,9 @@ static int derive_cfg(oai4g_tx_config *cfg, const oai4g_tx_params_t *p, const ui
   h.lds_a_words = max_tb_words + OAI4G_ENC_CRC_TABLE_WORDS;
   for (int cw = 0; cw < p->n_cw; cw++)   /* region A also holds the interleaved words and plane 3 in phase 3 */
     if (2 * h.cw[cw].ilv_off[h.cw[cw].C] > h.lds_a_words) h.lds_a_words = 2 * h.cw[cw].ilv_off[h.cw[cw].C];
-  if (max_w > h.lds_a_words) h.lds_a_words = max_w;
   h.lds_b_words = max_stream_words;
-  /* region B holds the RM output words once the streams are dead; region A the Gold words once
-   * packed w is dead */
+  /* region A holds the rate-matcher output words once the interleaved words are dead; region B
+   * the Gold words once the streams are dead */
   if (h.lds_gold_words > h.lds_b_words) h.lds_b_words = h.lds_gold_words;
   if (h.lds_gold_words > h.lds_a_words) h.lds_a_words = h.lds_gold_words;
   /* RE maps */

@@ -304,6 +304,15 @@ struct idft2048_tw_t {
 
 typedef uint32_t u32x2_t __attribute__((ext_vector_type(2)));
 
+#ifndef OAI4G_DIAG_NOSYNC
+#define OAI4G_DIAG_NOSYNC 0   /* timing diagnostic only: 1 = the idft2048 exchanges skip their barriers (wrong output) */
+#endif
+#if OAI4G_DIAG_NOSYNC
+#define IDFT_SYNC() do { } while (0)
+#else
+#define IDFT_SYNC() __syncthreads()
+#endif
+
 template <int NA, class Prod, class Cons>
 static __device__ __forceinline__ void idft2048_unit(uint32_t *lds, int t, bool active, const idft2048_tw_t &tw,
                                                      Prod prod, Cons cons, int scale)
@@ -321,7 +330,7 @@ static __device__ __forceinline__ void idft2048_unit(uint32_t *lds, int t, bool 
       for (int k = 0; k < 16; k++) lds[a * X1W + k * 144 + wo] = c2u(x[a][k]);
     }
   }
-  __syncthreads();
+  IDFT_SYNC();
   /* pass B: 64- and 256-levels of the 256-point transform j = t & 7 at k4 = t >> 3 */
   const int j = t & 7, k4 = t >> 3;
   if (active) {
@@ -337,7 +346,7 @@ static __device__ __forceinline__ void idft2048_unit(uint32_t *lds, int t, bool 
           x[a][4 * r2 + 2 * p + 1] = u2c(v.y);
         }
   }
-  __syncthreads();   /* E2 aliases E1 */
+  IDFT_SYNC();   /* E2 aliases E1 */
   if (active) {
     const twp_t w64[3] = {tw_of(tw.b64[0]), tw_of(tw.b64[1]), tw_of(tw.b64[2])};
 #pragma unroll
@@ -364,7 +373,7 @@ static __device__ __forceinline__ void idft2048_unit(uint32_t *lds, int t, bool 
       }
     }
   }
-  __syncthreads();
+  IDFT_SYNC();
   /* pass C: 1024- and 2048-levels for k2 = t + 128 h */
   if (active) {
 #pragma unroll
@@ -602,7 +611,7 @@ struct modofdm_geom {
 };
 
 #ifndef OAI4G_DIAG_MODOFDM
-#define OAI4G_DIAG_MODOFDM 0   /* timing diagnostics only: 1 = no IQ stores, 2 = no e-bit staging */
+#define OAI4G_DIAG_MODOFDM 0   /* timing diagnostics only: 1 = no IQ stores, 2 = no e-bit staging, 3 = no QAM lookups */
 #endif
 #ifndef OAI4G_MODOFDM_WAVES
 #define OAI4G_MODOFDM_WAVES 3   /* measured: 3 waves/SIMD (<=168 VGPRs) beats 2 (no cap) and 4 (spills) */
@@ -744,6 +753,13 @@ __global__ void __launch_bounds__(128) MODOFDM_ATTR k_modofdm(const cfg_dev_t *_
 #define OAI4G_MOD_GROUP 4   /* REs whose LDS round trips are issued together (register budget) */
 #endif
           constexpr int GR = OAI4G_MOD_GROUP;
+#if OAI4G_DIAG_MODOFDM == 3
+#pragma unroll
+          for (int n = 0; n < 16; n++)
+#pragma unroll
+            for (int a = 0; a < NA; a++) x[a][n] = u2c(rw[n >> 1] + (uint32_t)(a + n));
+          if (0)
+#endif
 #pragma unroll
           for (int g = 0; g < 16; g += GR) {
             uint32_t code[GR], p[GR], lo[GR], hi[GR], v0[GR], v1[GR];
