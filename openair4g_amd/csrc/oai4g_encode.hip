@@ -743,12 +743,36 @@ static __device__ void encode_codeword(const cfg_dev_t *__restrict__ c, uint32_t
     const uint32_t Elo = __builtin_amdgcn_readfirstlane(cw.E[sfi][0]), Ehi = __builtin_amdgcn_readfirstlane(cw.E[sfi][C - 1]);
     const uint32_t tsplit = n0 * nt0, ntot = tsplit + (C - n0) * nt1;
     const uint32_t lane32 = tid & 31, wcol = colperm(lane32), below = (1u << wcol) - 1u;
-    for (uint32_t t = tid >> 5; t < ntot; t += nth >> 5) {
-      /* tile t -> block r (tiles of block r: ceil(R/32) v0 tiles, then ceil(R/16) interlaced) */
-      const uint32_t ki = t >= tsplit ? 1u : 0u, tt = ki ? t - tsplit : t;
-      const uint32_t rr = __umul24(tt, ki ? nm1 : nm0) >> 20, rem = tt - __umul24(rr, ki ? nt1 : nt0);
+    /* per-lane column constants for (block size ki, region il): compact index of the column's
+     * first non-NULL entry, its row-0 NULL count, w position of the column start */
+    uint32_t csv[2][2], zcv[2][2], pcv[2][2];
+#pragma unroll
+    for (int ki = 0; ki < 2; ki++) {
+      const uint32_t R = ki ? R1 : R0, ND = ki ? ND1 : ND0;
+      const uint32_t b0 = __builtin_popcount((ki ? nc10 : nc00) & below), b1 = __builtin_popcount((ki ? nc11 : nc01) & below);
+      const uint32_t wr = __umul24(wcol, R);
+      csv[ki][0] = wr - b0;
+      csv[ki][1] = 32 * R - ND + 2 * wr - b0 - b1;
+      zcv[ki][0] = lane32 < ND ? 1u : 0u;
+      zcv[ki][1] = zcv[ki][0] + (lane32 + 1 < ND ? 1u : 0u);
+      pcv[ki][0] = wr;
+      pcv[ki][1] = 32 * R + 2 * wr;
+    }
+    /* a wave takes tiles rb = 2 rbp and 2 rbp + 1 of one (block, region): every block quantity is
+     * wave-uniform (scalar); pairs of block r: ceil(t0/2) v0 pairs, then ceil((nt - t0)/2) */
+    const uint32_t pv0 = (tz0 + 1) >> 1, pv1 = (tz1 + 1) >> 1;
+    const uint32_t pp0 = pv0 + ((nt0 - tz0 + 1) >> 1), pp1 = pv1 + ((nt1 - tz1 + 1) >> 1);
+    const uint32_t psplit = n0 * pp0, ptot = psplit + (C - n0) * pp1, half = lane >> 5;
+    const uint32_t pm0 = ((1u << 20) + pp0 - 1) / pp0, pm1 = ((1u << 20) + pp1 - 1) / pp1;   /* once, scalar */
+    (void)ntot; (void)nm0; (void)nm1;
+    for (uint32_t pw = wave; pw < ptot; pw += nwaves) {
+      const uint32_t P = __builtin_amdgcn_readfirstlane(pw);
+      const uint32_t ki = P >= psplit ? 1u : 0u, PP = ki ? P - psplit : P, pp = ki ? pp1 : pp0;
+      const uint32_t rr = (PP * (ki ? pm1 : pm0)) >> 20, rem = PP - rr * pp;
       const uint32_t r = ki ? n0 + rr : rr, R = ki ? R1 : R0, ND = ki ? ND1 : ND0, tz = ki ? tz1 : tz0;
-      const uint32_t il = rem >= tz ? 1u : 0u, rb = il ? rem - tz : rem;
+      const uint32_t pvz = ki ? pv1 : pv0, il = rem >= pvz ? 1u : 0u;
+      const uint32_t rb = 2 * (il ? rem - pvz : rem) + half;
+      const bool tile_ok = rb < (il ? (ki ? nt1 : nt0) - tz : tz);
       const uint32_t row = il ? 16 * rb + (lane32 >> 1) : 32 * rb + lane32, s = il ? 1 + (lane32 & 1) : 0;
       const uint32_t *st = strm + __umul24(r * 3 + s, sw);
       uint32_t y = 0;
@@ -762,33 +786,35 @@ static __device__ void encode_codeword(const cfg_dev_t *__restrict__ c, uint32_t
       y = transpose32(y, lane32);
       /* lane c = lane32 now holds w bits [p0, p0 + n) of column wcol, rows from 32 rb (v0) or
        * 16 rb (interlaced); the column's row-0 entries are NULL for c < ND (and y^(2): c + 1 < ND) */
-      const uint32_t Kpi = 32 * R;
-      uint32_t n = il ? min(32u, 2 * (R - 16 * rb)) : min(32u, R - 32 * rb);
-      if (il && lane32 == 31 && ND > 0 && R - 16 * rb <= 16) n--;            /* w[3Kpi-1] is NULL */
-      const uint32_t m0 = ki ? nc10 : nc00, m1 = ki ? nc11 : nc01;
-      const uint32_t zc = (lane32 < ND ? 1u : 0u) + (il && lane32 + 1 < ND ? 1u : 0u);
-      const uint32_t cs = il ? (Kpi - ND) + 2 * __umul24(wcol, R) - __builtin_popcount(m0 & below) -
-                                   __builtin_popcount(m1 & below)
-                             : __umul24(wcol, R) - __builtin_popcount(m0 & below);
-      const uint32_t p0 = il ? Kpi + 2 * (__umul24(wcol, R) + 16 * rb) : __umul24(wcol, R) + 32 * rb;
+      const int left = il ? 2 * ((int)R - 16 * (int)rb) : (int)R - 32 * (int)rb; /* w bits left in the column */
+      uint32_t n = tile_ok ? (uint32_t)min(32, left) : 0u;
+      if (il && lane32 == 31 && ND > 0 && left <= 32 && n) n--;               /* w[3Kpi-1] is NULL */
+      const uint32_t zc = ki ? (il ? zcv[1][1] : zcv[1][0]) : (il ? zcv[0][1] : zcv[0][0]);
+      const uint32_t cs = ki ? (il ? csv[1][1] : csv[1][0]) : (il ? csv[0][1] : csv[0][0]);
+      const uint32_t p0 = (ki ? (il ? pcv[1][1] : pcv[1][0]) : (il ? pcv[0][1] : pcv[0][0])) + 32 * rb;
       const uint32_t z = rb ? 0u : zc, ci0 = rb ? cs + 32 * rb - zc : cs;
       const uint32_t Ncb = ki ? Ncb1 : Ncb0, Nnn = ki ? Nnn1 : Nnn0, k0c = ki ? k0c1 : k0c0;
-      int m = (int)n - (int)z;
-      if (p0 + n > Ncb) m = (int)Ncb - (int)(p0 + z);                          /* limited buffer */
+      const int m = p0 + n > Ncb ? (int)Ncb - (int)(p0 + z) : (int)n - (int)z;  /* limited buffer */
       if (m > 0) {
-        y >>= z;
-        if (m < 32) y &= (1u << m) - 1u;
+        y = (y >> z) & (0xffffffffu >> (32 - m));
         const bool eh = r >= es;
         const uint32_t E = eh ? Ehi : Elo, ro = eh ? es * Elo + (r - es) * Ehi : r * Elo;
-        /* circular read from compact index k0c: the run may straddle the wrap back to k0c */
-        const uint32_t o = ci0 >= k0c ? ci0 - k0c : ci0 + Nnn - k0c;
-        const uint32_t ma = min((uint32_t)m, Nnn - o);
-        for (uint32_t part = 0; part < 2; part++) {
-          const uint32_t len = part ? (uint32_t)m - ma : ma, os = part ? 0u : o;
-          const uint32_t v = part ? (ma < 32 ? y >> ma : 0u) : (ma < 32 ? y & ((1u << ma) - 1u) : y);
-          for (uint32_t x = os; len && x < E; x += Nnn) {                       /* repetition rounds */
-            const uint32_t l = min(len, E - x);
-            or_bits(ebuf, ro + x, l < 32 ? v & ((1u << l) - 1u) : v);
+        /* circular read from compact index k0c */
+        uint32_t o = ci0 + Nnn - k0c;
+        o = o >= Nnn ? o - Nnn : o;
+        if (E <= Nnn && o + (uint32_t)m <= Nnn) {
+          /* one placement at most (no repetition, no wrap inside the run) */
+          if (o < E) or_bits(ebuf, ro + o, y & (0xffffffffu >> (32 - min((uint32_t)m, E - o))));
+        } else {
+          /* the run may straddle the wrap back to k0c; E > Nnn repeats the buffer */
+          const uint32_t ma = min((uint32_t)m, Nnn - o);
+          for (uint32_t part = 0; part < 2; part++) {
+            const uint32_t len = part ? (uint32_t)m - ma : ma, os = part ? 0u : o;
+            const uint32_t v = part ? (ma < 32 ? y >> ma : 0u) : (ma < 32 ? y & ((1u << ma) - 1u) : y);
+            for (uint32_t x = os; len && x < E; x += Nnn) {                     /* repetition rounds */
+              const uint32_t l = min(len, E - x);
+              or_bits(ebuf, ro + x, v & (0xffffffffu >> (32 - l)));
+            }
           }
         }
       }
