@@ -229,6 +229,41 @@ uint8_t oai4g_generate_dci_top(uint8_t num_ue_spec_dci, uint8_t num_common_dci, 
                                uint32_t n_rnti, int16_t amp, const oai4g_frame_parms_t *frame_parms,
                                int32_t **txdataF, uint32_t subframe);
 
+/* ---------------- synchronisation, broadcast and HARQ-indicator channels ---------------- */
+/* generate_pss (PHY/LTE_TRANSPORT/pss.c:50, decl LTE_TRANSPORT/proto.h): the Zadoff-Chu sequence
+ * of root 25 / 29 / 34 (Nid_cell % 3, the Q15 table of PHY/LTE_REFSIG/primary_synch.h, here
+ * generated as floor(32767 x)) scaled (a v) >> 15, a = amp or (amp 23170) >> 15 with two antennas,
+ * on the 62 subcarriers around DC of symbol `symbol` of slot `slot_offset` of every frame grid
+ * txdataF[ant] (overwrites).  Returns 0. */
+int oai4g_generate_pss(int32_t **txdataF, int16_t amp, const oai4g_frame_parms_t *frame_parms, uint16_t symbol,
+                       uint16_t slot_offset);
+/* generate_sss (sss.c:47): d0_sss / d5_sss (PHY/LTE_TRANSPORT/sss.h, 36.211 6.11.2.1 m-sequences,
+ * slot_offset < 3 selects d0) as (a d, 0) on the same 62 subcarriers.  Returns 0. */
+int oai4g_generate_sss(int32_t **txdataF, int16_t amp, const oai4g_frame_parms_t *frame_parms, uint16_t symbol,
+                       uint16_t slot_offset);
+/* LTE_eNB_PBCH (LTE_TRANSPORT/defs.h): the scrambled coded bits, one byte per bit, computed when
+ * frame_mod4 == 0 and mapped a quarter per frame */
+typedef struct {
+  uint8_t pbch_e[1920];
+} oai4g_pbch_t;
+/* generate_pbch (pbch.c:161): MIB (pbch_pdu[0..2]), CRC16 with the antenna mask, tail-biting
+ * convolutional code, rate matching to 1920 (1728) bits and scrambling (frame_mod4 == 0), then
+ * quarter frame_mod4 in QPSK (SISO / ALAMOUTI) on slot 1 symbols 0..3 of the subframe-0 grids
+ * txdataF[ant] ('+='), around the RS positions.  Returns 0. */
+int oai4g_generate_pbch(oai4g_pbch_t *eNB_pbch, int32_t **txdataF, int amp, const oai4g_frame_parms_t *frame_parms,
+                        const uint8_t *pbch_pdu, uint8_t frame_mod4);
+/* generate_phich (phich.c:401, normal cyclic prefix): HI -> BPSK x3, orthogonal sequence nseq,
+ * scrambling, SISO / ALAMOUTI, onto the three REGs of group ngroup in symbol 0 of `subframe` of the
+ * frame grids y[ant] ('+=').  The reference returns void; here 0, or -1 for what it does not
+ * define (extended CP, extended PHICH duration, nushift >= 3 where phich.c:563-569 reads past its
+ * 8-entry arrays, ngroup / nseq out of range). */
+int oai4g_generate_phich(const oai4g_frame_parms_t *frame_parms, int16_t amp, uint8_t nseq_PHICH, uint8_t ngroup_PHICH,
+                         uint8_t HI, uint8_t subframe, int32_t **y);
+/* generate_phich_top's group / sequence of an uplink allocation (phich.c:1449-1465, FDD):
+ * ngroup = (first_rb + n_DMRS) mod Ngroup, nseq = (first_rb / Ngroup + n_DMRS) mod 2 NSF. */
+int oai4g_phich_group_seq(const oai4g_frame_parms_t *frame_parms, uint16_t first_rb, uint8_t n_DMRS, uint8_t *ngroup_PHICH,
+                          uint8_t *nseq_PHICH);
+
 /* ---------------- UE receive front end ---------------- */
 /* dft64..dft2048 (PHY/TOOLS/lte_dfts.c:1766, 1957, 2172, 2359, 2574, 2689; decl TOOLS/defs.h):
  * y = DFT(x), bit-exact fixed point.  oai4g_dft returns 0 or -1. */
@@ -344,6 +379,24 @@ int oai4g_tx_batch_timed(const oai4g_tx_config_t *cfg, int n_sf, const uint8_t *
  * The control values are computed on the GPU once here, per subframe index.  Returns 0 / -1. */
 int oai4g_tx_config_set_control(oai4g_tx_config_t *cfg, uint8_t num_ue_spec_dci, uint8_t num_common_dci,
                                 const oai4g_dci_alloc_t *dci_alloc);
+/* Common signals in the batched grid (the eNB's common signal procedures,
+ * phy_procedures_lte_eNb.c:1529-1760, and generate_phich_top :2585): PSS + SSS in subframe
+ * indices 0 and 5, the PBCH quarter frame_mod4 of pbch_pdu in subframe index 0, and the listed
+ * PHICHs; merged with the PCFICH / PDCCH of oai4g_tx_config_set_control, so with with_crs = 1 the
+ * GPU grid is the eNB's complete txdataF.  NULL switches them off.  Returns 0 / -1. */
+#define OAI4G_MAX_PHICH_ITEMS 64
+typedef struct {
+  uint8_t subframe, ngroup, nseq, hi;
+} oai4g_phich_item_t;
+typedef struct {
+  uint8_t pss_sss;
+  uint8_t pbch;
+  uint8_t pbch_pdu[3];
+  uint8_t frame_mod4;
+  uint8_t n_phich;
+  oai4g_phich_item_t phich[OAI4G_MAX_PHICH_ITEMS];
+} oai4g_common_sig_t;
+int oai4g_tx_config_set_common(oai4g_tx_config_t *cfg, const oai4g_common_sig_t *common);
 /* Stage entry for parity tests: run only the encoder kernel (payload -> packed e bits). */
 int oai4g_tx_encode(const oai4g_tx_config_t *cfg, int n_sf, const uint8_t *d_payload, void *d_work, void *stream);
 

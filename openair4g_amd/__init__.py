@@ -177,6 +177,16 @@ _SIGS = {
                                                     ctypes.POINTER(DciAlloc)]),
     "oai4g_generate_pcfich": (ctypes.c_int, [ctypes.c_uint8, ctypes.c_int16, ctypes.POINTER(FrameParms),
                                              ctypes.POINTER(ctypes.c_void_p), ctypes.c_uint8]),
+    "oai4g_generate_pss": (ctypes.c_int, [ctypes.POINTER(ctypes.c_void_p), ctypes.c_int16, ctypes.POINTER(FrameParms),
+                                          ctypes.c_uint16, ctypes.c_uint16]),
+    "oai4g_generate_sss": (ctypes.c_int, [ctypes.POINTER(ctypes.c_void_p), ctypes.c_int16, ctypes.POINTER(FrameParms),
+                                          ctypes.c_uint16, ctypes.c_uint16]),
+    "oai4g_generate_pbch": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(ctypes.c_void_p), ctypes.c_int,
+                                           ctypes.POINTER(FrameParms), ctypes.c_void_p, ctypes.c_uint8]),
+    "oai4g_generate_phich": (ctypes.c_int, [ctypes.POINTER(FrameParms), ctypes.c_int16, ctypes.c_uint8, ctypes.c_uint8,
+                                            ctypes.c_uint8, ctypes.c_uint8, ctypes.POINTER(ctypes.c_void_p)]),
+    "oai4g_phich_group_seq": (ctypes.c_int, [ctypes.POINTER(FrameParms), ctypes.c_uint16, ctypes.c_uint8,
+                                             ctypes.POINTER(ctypes.c_uint8), ctypes.POINTER(ctypes.c_uint8)]),
     "oai4g_dft": (ctypes.c_int, [ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int]),
     "oai4g_dft2048": (None, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int]),
     "oai4g_dft1024": (None, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int]),
@@ -343,6 +353,46 @@ def generate_pcfich(cfi, amp, fp, grids, subframe):
     n = len(grids)
     gp = (ctypes.c_void_p * n)(*[g.ctypes.data for g in grids])
     return lib().oai4g_generate_pcfich(cfi, amp, ctypes.byref(fp), gp, subframe)
+
+
+def _grid_ptrs(grids):
+    return (ctypes.c_void_p * len(grids))(*[g.ctypes.data for g in grids])
+
+
+def generate_pss(grids, amp, fp, symbol, slot_offset):
+    """generate_pss drop-in (pss.c:50) on frame grids (int32 arrays, modified in place)."""
+    init()
+    return lib().oai4g_generate_pss(_grid_ptrs(grids), amp, ctypes.byref(fp), symbol, slot_offset)
+
+
+def generate_sss(grids, amp, fp, symbol, slot_offset):
+    """generate_sss drop-in (sss.c:47)."""
+    init()
+    return lib().oai4g_generate_sss(_grid_ptrs(grids), amp, ctypes.byref(fp), symbol, slot_offset)
+
+
+class Pbch(ctypes.Structure):
+    """oai4g_pbch_t (LTE_eNB_PBCH): the scrambled coded bits kept across frame_mod4."""
+    _fields_ = [("pbch_e", ctypes.c_uint8 * 1920)]
+
+
+def generate_pbch(state, grids, amp, fp, pdu, frame_mod4):
+    """generate_pbch drop-in (pbch.c:161) on the subframe-0 grids."""
+    init()
+    pdu = np.ascontiguousarray(pdu, dtype=np.uint8)
+    return lib().oai4g_generate_pbch(ctypes.byref(state), _grid_ptrs(grids), amp, ctypes.byref(fp), _ptr(pdu), frame_mod4)
+
+
+def generate_phich(fp, amp, nseq, ngroup, hi, subframe, grids):
+    """generate_phich drop-in (phich.c:401) on frame grids."""
+    init()
+    return lib().oai4g_generate_phich(ctypes.byref(fp), amp, nseq, ngroup, hi, subframe, _grid_ptrs(grids))
+
+
+def phich_group_seq(fp, first_rb, n_dmrs):
+    g, q = ctypes.c_uint8(), ctypes.c_uint8()
+    _check(lib().oai4g_phich_group_seq(ctypes.byref(fp), first_rb, n_dmrs, ctypes.byref(g), ctypes.byref(q)) == 0)
+    return g.value, q.value
 
 
 def dft(x, scale=1):

@@ -189,3 +189,260 @@ hipError_t oai4g_launch_dci(const dci_args_t &a, const uint32_t *d_map, const ui
   hipLaunchKernelGGL(k_dci, dim3(1), dim3(256), 0, s, a, d_map, d_src, d_g0, d_g1);
   return hipGetLastError();
 }
+
+/* ======================================================================================
+ * PSS / SSS (pss.c:50-103, sss.c:47-92): one thread per sequence element m = 0..61 of the
+ * inner 62 subcarriers, k = N - 31 + m with the DC skip; every antenna gets the same value,
+ * written with '=' as the reference does.
+ * ==================================================================================== */
+struct sync_ptrs_t {
+  int32_t *g[4];
+};
+
+__global__ void __launch_bounds__(64) k_sync(sync_ptrs_t p, sync_args_t a)
+{
+  const uint32_t m = threadIdx.x;
+  if (m >= 62) return;
+  uint32_t k = a.N - 31 + m;
+  if (k >= a.N) k = k + 1 - a.N;                       /* k++ (skip DC), k -= N */
+  int16_t re, im;
+  if (a.pss) {
+    re = (int16_t)(((int32_t)a.a * a.val[m][0]) >> 15);
+    im = (int16_t)(((int32_t)a.a * a.val[m][1]) >> 15);
+  } else {
+    re = (int16_t)((int32_t)a.a * a.val[m][0]);
+    im = 0;
+  }
+  const int32_t v = (int32_t)((uint16_t)re | ((uint32_t)(uint16_t)im << 16));
+  for (uint32_t aa = 0; aa < a.n_ant; aa++) p.g[aa][k] = v;
+}
+
+hipError_t oai4g_launch_sync(int32_t *const *d_sym, const sync_args_t &a, hipStream_t s)
+{
+  sync_ptrs_t p = {};
+  for (uint32_t aa = 0; aa < a.n_ant && aa < 4; aa++) p.g[aa] = d_sym[aa];
+  hipLaunchKernelGGL(k_sync, dim3(1), dim3(64), 0, s, p, a);
+  return hipGetLastError();
+}
+
+/* ======================================================================================
+ * PBCH (pbch.c:161-420).  One 256-thread workgroup:
+ *   1. (frame_mod4 == 0) lane 0: CRC16 of the 24 MIB bits XOR the antenna mask
+ *      (ccodelte_encode add_crc = 2, ccoding_byte_lte.c:84-92); every thread then produces
+ *      rate-matched bits e_k directly: k -> (stream, compacted index) of the circular buffer
+ *      (lte_rate_matching.c:637-680) -> (column, row) of the 32-column interleaver
+ *      (:133-190) -> TBCC output d^(s)_i as a circular convolution of c; scrambled with the
+ *      Gold words of c_init = Nid_cell (pbch_scrambling :760-783) and stored as bytes (the
+ *      reference's eNB_pbch->pbch_e, kept for frame_mod4 = 1..3);
+ *   2. the quarter frame_mod4 of e mapped to the 240 (216) REs of slot 1 symbols 0..3: RE slot
+ *      j = the j-th non-pilot subcarrier of the 72 around DC, k first then l; QPSK with
+ *      gain (amp 23170) >> 15, SISO on every antenna or the ALAMOUTI pair (j, j + 1) with the
+ *      reference's 1/sqrt2 floor scaling and the partner written from the accumulated values
+ *      of RE j (allocate_pbch_REs_in_RB :62-158); '+=' into the grid.
+ * ==================================================================================== */
+struct pbch_ptrs_t {
+  int32_t *g[4];
+};
+
+static __device__ __forceinline__ int32_t pk16(int16_t re, int16_t im)
+{
+  return (int32_t)((uint16_t)re | ((uint32_t)(uint16_t)im << 16));
+}
+static __device__ __forceinline__ int16_t lo16(int32_t v) { return (int16_t)(v & 0xFFFF); }
+static __device__ __forceinline__ int16_t hi16(int32_t v) { return (int16_t)((uint32_t)v >> 16); }
+
+__global__ void __launch_bounds__(256) k_pbch(pbch_ptrs_t p, uint8_t *__restrict__ ebytes, pbch_args_t a)
+{
+  __shared__ uint8_t c[40];
+  __shared__ uint32_t gold[64];
+  __shared__ uint8_t e[1920];
+  const uint32_t tid = threadIdx.x;
+  if (a.encode) {
+    if (tid == 0) {
+      uint32_t crc = 0;                                  /* crc16 over 3 whole bytes (crc_byte.c:155-171) */
+      for (int b = 0; b < 3; b++) crc = (crc << 8) ^ (crc16_byte(a.a[b] ^ ((crc >> 24) & 0xFFu)) << 16);
+      crc ^= (uint32_t)a.amask << 16;
+      for (int i = 0; i < 24; i++) c[i] = (uint8_t)((a.a[i >> 3] >> (7 - (i & 7))) & 1u);
+      for (int i = 0; i < 16; i++) c[24 + i] = (uint8_t)((crc >> (31 - i)) & 1u);
+    }
+    if (tid == 64) {                                     /* lte_gold_generic, c_init = Nid */
+      uint32_t x1 = 1u + (1u << 31), x2 = a.Nid;
+      x2 = x2 ^ ((x2 ^ (x2 >> 1) ^ (x2 >> 2) ^ (x2 >> 3)) << 31);
+      for (int n = 1; n < 50; n++) pcfich_gold_step(x1, x2);
+      for (uint32_t w = 0; w < (a.E + 31u) / 32u; w++) {
+        pcfich_gold_step(x1, x2);
+        gold[w] = x1 ^ x2;
+      }
+    }
+    __syncthreads();
+    const uint32_t D = 40, R = 2, ND = 32 * R - D;
+    for (uint32_t k = tid; k < a.E; k += blockDim.x) {
+      const uint32_t jj = k % (3 * D), s = jj / D;
+      uint32_t j = jj - s * D, col = 0;
+      for (; col < 32; col++) {
+        const uint32_t n = R - (c_bitrev_cc[col] < ND ? 1u : 0u);
+        if (j < n) break;
+        j -= n;
+      }
+      const uint32_t row = j + (c_bitrev_cc[col] < ND ? 1u : 0u);
+      const uint32_t i = 32 * row + c_bitrev_cc[col] - ND;
+      const uint32_t g = s == 0 ? 0133u : (s == 1 ? 0171u : 0165u);
+      uint32_t par = 0;
+#pragma unroll
+      for (uint32_t t = 0; t < 7; t++) par ^= ((g >> (6 - t)) & 1u) & c[(i + D - t) % D];
+      e[k] = (uint8_t)(par ^ ((gold[k >> 5] >> (k & 31)) & 1u));
+    }
+    __syncthreads();
+    for (uint32_t k = tid; k < a.E; k += blockDim.x) ebytes[k] = e[k];
+  } else {
+    for (uint32_t k = tid; k < a.E; k += blockDim.x) e[k] = ebytes[k];
+  }
+  __syncthreads();
+  /* RE slots of the quarter: 4 symbols, 72 subcarriers each minus the pilot positions */
+  const uint8_t *x = e + a.quarter * (a.E >> 2);
+  const uint32_t nre = (a.E >> 2) >> 1;
+  const int16_t g = a.gain;
+  auto bin = [&](uint32_t sc) {                            /* subcarrier 0..71 around DC -> grid bin */
+    const uint32_t b = a.N - 36 + sc;
+    return b >= a.N ? b - a.N + 1 : b;
+  };
+  auto pos = [&](uint32_t j) {                             /* RE slot -> offset in the 4-symbol window */
+    uint32_t l = 0;
+    for (; l < 4; l++) {
+      const uint32_t n = ((a.pil_mask >> l) & 1u) ? 48u : 72u;
+      if (j < n) break;
+      j -= n;
+    }
+    uint32_t sc = j;
+    if ((a.pil_mask >> l) & 1u) {                         /* the j-th of the 8 non-pilot REs per RB */
+      const uint32_t rb = j >> 3, q = j & 7u;
+      uint32_t cnt = 0, re = 0;
+      for (uint32_t r = 0; r < 12; r++)
+        if (r % 3 != a.nushift3) {
+          if (cnt == q) re = r;
+          cnt++;
+        }
+      sc = 12 * rb + re;
+    }
+    return l * a.N + bin(sc);
+  };
+  if (a.mode1) {
+    for (uint32_t j = tid; j < nre; j += blockDim.x) {
+      const uint32_t o = pos(j);
+      const int16_t re = x[2 * j] == 1 ? (int16_t)-g : g, im = x[2 * j + 1] == 1 ? (int16_t)-g : g;
+      for (uint32_t aa = 0; aa < a.n_ant; aa++) {
+        const int32_t v = p.g[aa][o];
+        p.g[aa][o] = pk16((int16_t)(lo16(v) + re), (int16_t)(hi16(v) + im));
+      }
+    }
+  } else {
+    for (uint32_t j = 2 * tid; j < nre; j += 2 * blockDim.x) {
+      const uint32_t o = pos(j), o2 = pos(j + 1);
+      const int16_t t1r = x[2 * j] == 1 ? (int16_t)-g : g, t1i = x[2 * j + 1] == 1 ? (int16_t)-g : g;
+      const int16_t t2r = x[2 * j + 2] == 1 ? g : (int16_t)-g, t2i = x[2 * j + 3] == 1 ? (int16_t)-g : g;
+      const int32_t v0 = p.g[0][o], v1 = p.g[1][o];
+      const int16_t y0r = (int16_t)(lo16(v0) + (int16_t)((t1r * 23170) >> 15));
+      const int16_t y0i = (int16_t)(hi16(v0) + (int16_t)((t1i * 23170) >> 15));
+      const int16_t y1r = (int16_t)(lo16(v1) + (int16_t)((t2r * 23170) >> 15));
+      const int16_t y1i = (int16_t)(hi16(v1) + (int16_t)((t2i * 23170) >> 15));
+      p.g[0][o] = pk16(y0r, y0i);
+      p.g[1][o] = pk16(y1r, y1i);
+      const int32_t w0 = p.g[0][o2], w1 = p.g[1][o2];
+      p.g[0][o2] = pk16((int16_t)(lo16(w0) - y1r), (int16_t)(hi16(w0) + y1i));
+      p.g[1][o2] = pk16((int16_t)(lo16(w1) + y0r), (int16_t)(hi16(w1) - y0i));
+    }
+  }
+}
+
+hipError_t oai4g_launch_pbch(int32_t *const *d_g, uint8_t *d_e, const pbch_args_t &a, hipStream_t s)
+{
+  pbch_ptrs_t p = {};
+  for (uint32_t aa = 0; aa < a.n_ant && aa < 4; aa++) p.g[aa] = d_g[aa];
+  hipLaunchKernelGGL(k_pbch, dim3(1), dim3(256), 0, s, p, d_e, a);
+  return hipGetLastError();
+}
+
+/* ======================================================================================
+ * PHICH (generate_phich, phich.c:401-780, normal CP).  One thread per (PHICH, symbol i of 12):
+ * the scrambling word of the PHICH's c_init (one Gold word), the orthogonal-sequence sign,
+ * BPSK with the gain, SISO or the ALAMOUTI pair (i even: (x0, -x1*), i odd: (x1, x0*)), RE =
+ * the (i mod 4)-th non-RS position of REG i / 4.  Several PHICHs may share REs, and the
+ * reference accumulates int16 with wrap-around, so contributions go through int32 atomics and
+ * are folded into the grid afterwards (wrap-add commutes).
+ * ==================================================================================== */
+struct phich_ptrs_t {
+  int32_t *g[2];
+};
+
+__global__ void __launch_bounds__(256) k_phich(phich_ptrs_t p, int32_t *__restrict__ acc, phich_args_t a)
+{
+  const uint32_t tid = threadIdx.x;
+  for (uint32_t i = tid; i < 4 * a.win; i += blockDim.x) acc[i] = 0;
+  __syncthreads();
+  for (uint32_t t = tid; t < 12 * a.n; t += blockDim.x) {
+    const phich_item_t &it = a.it[t / 12];
+    const uint32_t i = t % 12;
+    uint32_t x1 = 1u + (1u << 31), x2 = it.c_init;
+    x2 = x2 ^ ((x2 ^ (x2 >> 1) ^ (x2 >> 2) ^ (x2 >> 3)) << 31);
+    for (int n = 1; n < 50; n++) pcfich_gold_step(x1, x2);
+    pcfich_gold_step(x1, x2);
+    const uint32_t sw = x1 ^ x2;
+    const int hi = it.hi ? 1 : 0;
+    auto dsym = [&](uint32_t q, int &re, int &im) {   /* d[2q], d[2q + 1] of phich.c:455-536 */
+      const int cs = ((sw >> q) & 1u) == 0 ? 1 - 2 * hi : 2 * hi - 1;
+      const uint32_t w = it.nseq & 3u;                /* +-1 pattern of Table 6.9.1-2 */
+      const int sg = ((w == 1 && (q & 1)) || (w == 2 && (q & 2)) || (w == 3 && ((q ^ (q >> 1)) & 1))) ? -1 : 1;
+      const int v = sg * cs;
+      if (it.nseq < 4) { re = v; im = v; }
+      else { re = -v; im = v; }
+    };
+    int re0, im0;
+    dsym(i, re0, im0);
+    int y0r, y0i, y1r = 0, y1i = 0;
+    const int g = a.gain;
+    if (a.mode1) {
+      y0r = (int16_t)(re0 * g);
+      y0i = (int16_t)(im0 * g);
+    } else {
+      const uint32_t i0 = i & ~1u;
+      int ar, ai, br, bi;
+      dsym(i0, ar, ai);
+      dsym(i0 + 1, br, bi);
+      const int16_t a0r = (int16_t)(ar * g), a0i = (int16_t)(ai * g);
+      const int16_t b1r = (int16_t)(-br * g), b1i = (int16_t)(bi * g);   /* -x1* */
+      if ((i & 1u) == 0) { y0r = a0r; y0i = a0i; y1r = b1r; y1i = b1i; }
+      else { y0r = (int16_t)-b1r; y0i = b1i; y1r = a0r; y1i = (int16_t)-a0i; }
+    }
+    const uint32_t q = i >> 2, m = i & 3u;
+    uint32_t pos = 0, cnt = 0;
+    for (uint32_t r = 0; r < 6; r++)
+      if (r != a.nushift && r != a.nushift + 3) {
+        if (cnt == m) pos = r;
+        cnt++;
+      }
+    const uint32_t o = it.reg_off[q] + pos;
+    atomicAdd(&acc[o], y0r);
+    atomicAdd(&acc[a.win + o], y0i);
+    if (a.n_ant > 1) {
+      atomicAdd(&acc[2 * a.win + o], y1r);
+      atomicAdd(&acc[3 * a.win + o], y1i);
+    }
+  }
+  __syncthreads();
+  for (uint32_t o = tid; o < a.win; o += blockDim.x)
+    for (uint32_t aa = 0; aa < a.n_ant; aa++) {
+      const int32_t ar = acc[2 * aa * a.win + o], ai = acc[(2 * aa + 1) * a.win + o];
+      if (ar == 0 && ai == 0) continue;
+      const int32_t v = p.g[aa][o];
+      p.g[aa][o] = pk16((int16_t)(lo16(v) + (int16_t)ar), (int16_t)(hi16(v) + (int16_t)ai));
+    }
+}
+
+hipError_t oai4g_launch_phich(int32_t *const *d_g, int32_t *d_acc, const phich_args_t &a, hipStream_t s)
+{
+  if (a.n == 0) return hipSuccess;
+  phich_ptrs_t p = {};
+  for (uint32_t aa = 0; aa < a.n_ant && aa < 2; aa++) p.g[aa] = d_g[aa];
+  hipLaunchKernelGGL(k_phich, dim3(1), dim3(256), 0, s, p, d_acc, a);
+  return hipGetLastError();
+}

@@ -625,7 +625,11 @@ struct oai4g_tx_config {
   std::vector<uint16_t> h_remap;
   uint32_t *d_crs = nullptr;
   std::vector<uint32_t> h_crs;          /* [10][4][200] packed CRS IQ */
-  uint32_t *d_ctl = nullptr;            /* control region values (oai4g_tx_config_set_control) */
+  uint32_t *d_ctl = nullptr;            /* static RE values [10][14][2][N] (set_control / set_common) */
+  std::vector<oai4g_dci_alloc_t> dci;   /* oai4g_tx_config_set_control's DCI set */
+  uint8_t n_ue_dci = 0, n_common_dci = 0;
+  bool common_on = false;
+  oai4g_common_sig_t common;            /* oai4g_tx_config_set_common's signals */
   int re_count[10];
   int re_alloc[10];                 /* dlsch_modulation's return value (ALAMOUTI counts skipped pilots) */
   /* optional pipelined batches (OAI4G_PIPE_CHUNK=n): the encoder runs on the caller's stream, the
@@ -2311,14 +2315,20 @@ extern "C" uint8_t oai4g_generate_dci_top(uint8_t num_ue_spec_dci, uint8_t num_c
   return npd;
 }
 
-/* Batched control region: generate_dci_top's PCFICH + PDCCH for every subframe index, computed
- * on the GPU by the drop-in kernels into a [10][3][2][N] table, marked in the RE map with
- * OAI4G_CTL_CODE and merged by the modulator. */
-extern "C" int oai4g_tx_config_set_control(oai4g_tx_config_t *cfg, uint8_t n_ue, uint8_t n_common,
-                                           const oai4g_dci_alloc_t *dci)
+/* Batched static REs: generate_dci_top's PCFICH + PDCCH (set_control) and the PSS / SSS, PBCH and
+ * PHICH of the common signal procedures (set_common, phy_procedures_lte_eNb.c:1529-1760, 2585)
+ * for every subframe index, computed on the GPU by the drop-in kernels into one subframe grid per
+ * subframe index, gathered into a [10][14][2][N] table, marked in the RE map with OAI4G_CTL_CODE
+ * and merged by the modulator. */
+static void sync_args(const oai4g_frame_parms_t *fp, int16_t amp, bool pss, uint16_t slot_offset, sync_args_t &a);
+static void pbch_args(const oai4g_frame_parms_t *fp, int amp, const uint8_t *pdu, uint8_t frame_mod4, pbch_args_t &a);
+static int phich_item(const oai4g_frame_parms_t *fp, uint8_t nseq, uint8_t ngroup, uint8_t HI, uint8_t subframe,
+                      phich_item_t &it);
+static void phich_common(const oai4g_frame_parms_t *fp, int16_t amp, phich_args_t &a);
+
+static int rebuild_static(oai4g_tx_config_t *cfg)
 {
-  NEED_INIT(-1);
-  const uint32_t N = cfg->h.N;
+  const uint32_t N = cfg->h.N, nsymb = cfg->h.nsymb, n_ant = cfg->p.nb_antennas_tx;
   for (auto &c : cfg->h_remap)
     if ((c & 0xE000u) == OAI4G_CTL_CODE) c = 0xFFFF;
   memset(cfg->h.ctlmask, 0, sizeof(cfg->h.ctlmask));
@@ -2326,61 +2336,112 @@ extern "C" int oai4g_tx_config_set_control(oai4g_tx_config_t *cfg, uint8_t n_ue,
   if (cfg->d_ctl) hipFree(cfg->d_ctl);
   cfg->d_ctl = nullptr;
   cfg->h.ctl_tab = nullptr;
-  if ((uint32_t)n_ue + n_common > 0) {
-    if (cfg->h_remap.empty()) { set_err("set_control: configuration has no RE map"); return -1; }
-    std::vector<uint32_t> tab((size_t)10 * 3 * 2 * N, 0);
-    const size_t gbytes = (size_t)3 * N * 4, gpad = (gbytes + 255) & ~(size_t)255;
+  const bool dci_on = (uint32_t)cfg->n_ue_dci + cfg->n_common_dci > 0;
+  if (dci_on || cfg->common_on) {
+    if (cfg->h_remap.empty()) { set_err("static REs: configuration has no RE map"); return -1; }
+    const oai4g_frame_parms_t &fp = cfg->fp;
+    std::vector<uint32_t> tab((size_t)10 * 14 * 2 * N, 0);
+    const size_t gbytes = (size_t)14 * N * 4, gpad = (gbytes + 255) & ~(size_t)255;
     const size_t mcap = (size_t)4 * 1024;    /* >= 4 nquad REs for every geometry */
-    uint8_t *buf = scratch(2 * gpad + mcap * 4 + mcap * 2 + 256);
+    const size_t accb = (size_t)4 * 2 * N * 4;
+    uint8_t *buf = scratch(4 * gpad + mcap * 4 + mcap * 2 + accb + 2048 + 256);
     if (!buf) return -1;
-    int32_t *d0 = (int32_t *)buf, *d1 = (int32_t *)(buf + gpad);
-    uint32_t *dmap = (uint32_t *)(buf + 2 * gpad);
-    uint16_t *dsrc = (uint16_t *)(buf + 2 * gpad + mcap * 4);
-    std::vector<uint32_t> g(3 * (size_t)N);
+    int32_t *dg[4] = {(int32_t *)buf, (int32_t *)(buf + gpad), (int32_t *)(buf + 2 * gpad), (int32_t *)(buf + 3 * gpad)};
+    uint32_t *dmap = (uint32_t *)(buf + 4 * gpad);
+    uint16_t *dsrc = (uint16_t *)(buf + 4 * gpad + mcap * 4);
+    int32_t *dacc = (int32_t *)(buf + 4 * gpad + mcap * 6);
+    uint8_t *dpe = buf + 4 * gpad + mcap * 6 + accb;
+    std::vector<uint32_t> g((size_t)14 * N);
     for (uint32_t sf = 0; sf < 10; sf++) {
-      dci_args_t a;
-      std::vector<uint32_t> map;
-      std::vector<uint16_t> src;
-      const uint8_t npd = dci_prepare(n_ue, n_common, dci, cfg->p.amp, &cfg->fp, sf, a, map, src);
-      if (npd < 1 || npd > 3) return -1;
-      if (npd > cfg->p.num_pdcch_symbols) {
-        set_err("set_control: the DCIs need %u control symbols but the PDSCH starts at symbol %u (dlsim.c:2562-2565)",
-                npd, cfg->p.num_pdcch_symbols);
-        return -1;
+      HCK(hipMemsetAsync(buf, 0, 4 * gpad, g_scr.s), -1);
+      uint32_t n_out = n_ant > 2 ? 2 : n_ant;          /* antennas whose values the table keeps */
+      if (dci_on) {
+        dci_args_t a;
+        std::vector<uint32_t> map;
+        std::vector<uint16_t> src;
+        const uint8_t npd = dci_prepare(cfg->n_ue_dci, cfg->n_common_dci, cfg->dci.data(), cfg->p.amp, &cfg->fp, sf, a,
+                                        map, src);
+        if (npd < 1 || npd > 3) return -1;
+        if (npd > cfg->p.num_pdcch_symbols) {
+          set_err("set_control: the DCIs need %u control symbols but the PDSCH starts at symbol %u (dlsim.c:2562-2565)",
+                  npd, cfg->p.num_pdcch_symbols);
+          return -1;
+        }
+        if (map.size() > mcap) { set_err("set_control: PDCCH map too large"); return -1; }
+        HCK(hipMemcpyAsync(dmap, map.data(), map.size() * 4, hipMemcpyHostToDevice, g_scr.s), -1);
+        HCK(hipMemcpyAsync(dsrc, src.data(), src.size() * 2, hipMemcpyHostToDevice, g_scr.s), -1);
+        pcfich_args_t pa;
+        memset(&pa, 0, sizeof(pa));
+        uint16_t reg[4];
+        uint8_t fi;
+        pcfich_regs(&fp, reg, &fi);
+        pa.c_init = ((((2u * fp.Nid_cell) + 1u) * (1u + sf)) << 9) + fp.Nid_cell;
+        pa.cfi = npd;
+        pa.gain = a.gain;
+        pa.mode1 = a.mode1;
+        pa.nushift3 = (uint8_t)(fp.nushift % 3);
+        for (int q = 0; q < 4; q++) {
+          uint32_t ro = fp.first_carrier_offset + (uint32_t)reg[q] * 6;
+          if (ro >= N) ro = 1 + ro - N;
+          pa.reg_off[q] = ro;
+        }
+        pa.n_ant = a.n_ant;
+        HCK(oai4g_launch_pcfich(dg[0], dg[1], pa, g_scr.s), -1);
+        HCK(oai4g_launch_dci(a, dmap, dsrc, dg[0], dg[1], 0, g_scr.s), -1);
       }
-      if (map.size() > mcap) { set_err("set_control: PDCCH map too large"); return -1; }
-      HCK(hipMemsetAsync(buf, 0, 2 * gpad, g_scr.s), -1);
-      HCK(hipMemcpyAsync(dmap, map.data(), map.size() * 4, hipMemcpyHostToDevice, g_scr.s), -1);
-      HCK(hipMemcpyAsync(dsrc, src.data(), src.size() * 2, hipMemcpyHostToDevice, g_scr.s), -1);
-      pcfich_args_t pa;
-      memset(&pa, 0, sizeof(pa));
-      uint16_t reg[4];
-      uint8_t fi;
-      pcfich_regs(&cfg->fp, reg, &fi);
-      pa.c_init = ((((2u * cfg->fp.Nid_cell) + 1u) * (1u + sf)) << 9) + cfg->fp.Nid_cell;
-      pa.cfi = npd;
-      pa.gain = a.gain;
-      pa.mode1 = a.mode1;
-      pa.nushift3 = (uint8_t)(cfg->fp.nushift % 3);
-      for (int q = 0; q < 4; q++) {
-        uint32_t ro = cfg->fp.first_carrier_offset + (uint32_t)reg[q] * 6;
-        if (ro >= N) ro = 1 + ro - N;
-        pa.reg_off[q] = ro;
+      if (cfg->common_on) {
+        const oai4g_common_sig_t &cm = cfg->common;
+        const uint32_t nsl = nsymb / 2;
+        if (cm.pss_sss && (sf == 0 || sf == 5)) {
+          sync_args_t sa;
+          int32_t *sp[4];
+          sync_args(&fp, cfg->p.amp, true, (uint16_t)(2 * sf), sa);
+          for (uint32_t aa = 0; aa < 4; aa++) sp[aa] = dg[aa] + (size_t)(nsl - 1) * N;
+          HCK(oai4g_launch_sync(sp, sa, g_scr.s), -1);
+          sync_args(&fp, cfg->p.amp, false, (uint16_t)(2 * sf), sa);
+          for (uint32_t aa = 0; aa < 4; aa++) sp[aa] = dg[aa] + (size_t)(nsl - 2) * N;
+          HCK(oai4g_launch_sync(sp, sa, g_scr.s), -1);
+        }
+        if (cm.pbch && sf == 0) {
+          pbch_args_t pa;
+          pbch_args(&fp, cfg->p.amp, cm.pbch_pdu, 0, pa);
+          int32_t *pp[4];
+          for (uint32_t aa = 0; aa < 4; aa++) pp[aa] = dg[aa] + (size_t)nsl * N;
+          if (cm.frame_mod4) {                          /* encode (quarter 0) into a scratch grid, then map */
+            HCK(oai4g_launch_pbch(pp, dpe, pa, g_scr.s), -1);
+            HCK(hipMemsetAsync(buf, 0, 4 * gpad, g_scr.s), -1);
+            pbch_args(&fp, cfg->p.amp, cm.pbch_pdu, cm.frame_mod4, pa);
+          }
+          HCK(oai4g_launch_pbch(pp, dpe, pa, g_scr.s), -1);
+        }
+        static thread_local phich_args_t ph;
+        memset(&ph, 0, sizeof(ph));
+        phich_common(&fp, cfg->p.amp, ph);
+        for (uint32_t i = 0; i < cm.n_phich; i++) {
+          const oai4g_phich_item_t &it = cm.phich[i];
+          if (it.subframe != sf) continue;
+          if (phich_item(&fp, it.nseq, it.ngroup, it.hi, (uint8_t)sf, ph.it[ph.n]) != 0) return -1;
+          ph.n++;
+        }
+        if (ph.n) {
+          if (ph.n_ant > 1 && n_ant < 2) { set_err("set_common: ALAMOUTI PHICH needs two antennas"); return -1; }
+          HCK(oai4g_launch_phich(dg, dacc, ph, g_scr.s), -1);
+        }
+        if (cm.pbch || cm.pss_sss) n_out = n_ant;
       }
-      pa.n_ant = a.n_ant;
-      HCK(oai4g_launch_pcfich(d0, d1, pa, g_scr.s), -1);
-      HCK(oai4g_launch_dci(a, dmap, dsrc, d0, d1, 0, g_scr.s), -1);
-      for (uint32_t ant = 0; ant < 2; ant++) {
-        HCK(hipMemcpyAsync(g.data(), ant ? (void *)d1 : (void *)d0, gbytes, hipMemcpyDeviceToHost, g_scr.s), -1);
+      for (uint32_t ant = 0; ant < n_out && ant < 2; ant++) {
+        HCK(hipMemcpyAsync(g.data(), dg[ant], gbytes, hipMemcpyDeviceToHost, g_scr.s), -1);
         HCK(hipStreamSynchronize(g_scr.s), -1);
-        if (ant >= a.n_ant) continue;
-        for (uint32_t l = 0; l < npd; l++)
+        for (uint32_t l = 0; l < nsymb; l++)
           for (uint32_t k = 0; k < N; k++) {
             const uint32_t v = g[(size_t)l * N + k];
             if (!v) continue;
-            tab[(((size_t)sf * 3 + l) * 2 + ant) * N + k] = v;
+            tab[(((size_t)sf * 14 + l) * 2 + ant) * N + k] = v;
             uint16_t &code = cfg->h_remap[((size_t)sf * 14 + l) * N + k];
-            if (code != 0xFFFF && code != OAI4G_CTL_CODE) { set_err("set_control: control RE collides"); return -1; }
+            if (code != 0xFFFF && code != OAI4G_CTL_CODE) {
+              set_err("static REs: subframe %u symbol %u RE %u collides with a PDSCH / CRS RE", sf, l, k);
+              return -1;
+            }
             code = (uint16_t)OAI4G_CTL_CODE;
             cfg->h.ctlmask[sf] |= 1u << l;
           }
@@ -2393,5 +2454,249 @@ extern "C" int oai4g_tx_config_set_control(oai4g_tx_config_t *cfg, uint8_t n_ue,
   }
   if (upload_remap(cfg) != 0) return -1;
   HCK(hipMemcpy(cfg->d, &cfg->h, sizeof(cfg_dev_t), hipMemcpyHostToDevice), -1);
+  return 0;
+}
+
+extern "C" int oai4g_tx_config_set_control(oai4g_tx_config_t *cfg, uint8_t n_ue, uint8_t n_common,
+                                           const oai4g_dci_alloc_t *dci)
+{
+  NEED_INIT(-1);
+  cfg->dci.assign(dci, dci + ((uint32_t)n_ue + n_common));
+  cfg->n_ue_dci = n_ue;
+  cfg->n_common_dci = n_common;
+  return rebuild_static(cfg);
+}
+
+extern "C" int oai4g_tx_config_set_common(oai4g_tx_config_t *cfg, const oai4g_common_sig_t *c)
+{
+  NEED_INIT(-1);
+  if (c && c->n_phich > OAI4G_MAX_PHICH_ITEMS) { set_err("set_common: %u PHICHs", c->n_phich); return -1; }
+  if (c && c->n_phich && cfg->p.mode1_flag == 1 && cfg->p.nb_antennas_tx > 1) {
+    set_err("set_common: a SISO PHICH on antenna 0 only is not representable in the one-transform TM1 grid");
+    return -1;
+  }
+  cfg->common_on = c != nullptr && (c->pss_sss || c->pbch || c->n_phich);
+  if (c) cfg->common = *c;
+  return rebuild_static(cfg);
+}
+
+/* ----------------------------------------------------------------------------------------
+ * Synchronisation, broadcast and HARQ-indicator channels: host geometry and
+ * tables of pss.c / sss.c / pbch.c / phich.c, the per-call data on the GPU (oai4g_ctrl.hip).
+ * -------------------------------------------------------------------------------------- */
+/* primary_synch0/1/2 (PHY/LTE_REFSIG/primary_synch.h): entries 10..133 of the reference table are
+ * floor(32767 x) of the Zadoff-Chu sequence d_u(n), u = 25 / 29 / 34 (checked entry by entry
+ * against the header in tests/test_sync_cpu.py) */
+static void pss_table(uint32_t Nid2, int16_t v[62][2])
+{
+  static const int u[3] = {25, 29, 34};
+  for (int n = 0; n < 62; n++) {
+    const int m = n < 31 ? n : n + 1;
+    const double ang = -M_PI * u[Nid2 % 3] * m * (m + 1) / 63.0;
+    v[n][0] = (int16_t)floor(32767.0 * cos(ang));
+    v[n][1] = (int16_t)floor(32767.0 * sin(ang));
+  }
+}
+
+/* d0_sss / d5_sss (PHY/LTE_TRANSPORT/sss.h) restated from 36.211 6.11.2.1 */
+static void sss_table(uint32_t Nid_cell, bool sf5, int16_t d[62])
+{
+  auto mseq = [](const int *taps, int nt, int8_t *out) {
+    int x[31] = {0, 0, 0, 0, 1};
+    for (int i = 0; i < 26; i++) {
+      int v = 0;
+      for (int t = 0; t < nt; t++) v += x[i + taps[t]];
+      x[i + 5] = v & 1;
+    }
+    for (int i = 0; i < 31; i++) out[i] = (int8_t)(1 - 2 * x[i]);
+  };
+  static const int ts[2] = {2, 0}, tc[2] = {3, 0}, tz[4] = {4, 2, 1, 0};
+  int8_t st[31], ct[31], zt[31];
+  mseq(ts, 2, st);
+  mseq(tc, 2, ct);
+  mseq(tz, 4, zt);
+  const int n1 = (int)Nid_cell / 3, n2 = (int)Nid_cell % 3;
+  const int qp = n1 / 30, q = (n1 + qp * (qp + 1) / 2) / 30, mp = n1 + q * (q + 1) / 2;
+  const int m0 = mp % 31, m1 = (m0 + mp / 31 + 1) % 31;
+  for (int n = 0; n < 31; n++) {
+    const int s0 = st[(n + m0) % 31], s1 = st[(n + m1) % 31], c0 = ct[(n + n2) % 31], c1 = ct[(n + n2 + 3) % 31];
+    const int z0 = zt[(n + m0 % 8) % 31], z1 = zt[(n + m1 % 8) % 31];
+    d[2 * n] = (int16_t)(sf5 ? s1 * c0 : s0 * c0);
+    d[2 * n + 1] = (int16_t)(sf5 ? s0 * c1 * z1 : s1 * c1 * z0);
+  }
+}
+
+static void sync_args(const oai4g_frame_parms_t *fp, int16_t amp, bool pss, uint16_t slot_offset, sync_args_t &a)
+{
+  memset(&a, 0, sizeof(a));
+  if (pss) {
+    pss_table(fp->Nid_cell % 3, a.val);
+  } else {
+    int16_t d[62];
+    sss_table(fp->Nid_cell, slot_offset >= 3, d);
+    for (int i = 0; i < 62; i++) a.val[i][0] = d[i];
+  }
+  a.a = fp->nb_antennas_tx == 1 ? amp : (int16_t)((amp * 23170) >> 15);
+  a.pss = pss ? 1 : 0;
+  a.n_ant = fp->nb_antennas_tx;
+  a.N = fp->ofdm_symbol_size;
+}
+
+/* one symbol of every antenna: upload, kernel, download */
+static int sync_dropin(int32_t **txdataF, int16_t amp, const oai4g_frame_parms_t *fp, uint16_t symbol,
+                       uint16_t slot_offset, bool pss)
+{
+  NEED_INIT(-1);
+  const uint32_t N = fp->ofdm_symbol_size, Nsymb = fp->Ncp == 0 ? 14 : 12, n_ant = fp->nb_antennas_tx;
+  if (n_ant < 1 || n_ant > 4) { set_err("generate_%s: nb_antennas_tx %u", pss ? "pss" : "sss", n_ant); return -1; }
+  const size_t off = (size_t)slot_offset * Nsymb / 2 * N + (size_t)symbol * N, sb = ((size_t)N * 4 + 255) & ~(size_t)255;
+  sync_args_t a;
+  sync_args(fp, amp, pss, slot_offset, a);
+  uint8_t *buf = scratch(4 * sb);
+  if (!buf) return -1;
+  int32_t *d[4];
+  for (uint32_t aa = 0; aa < n_ant; aa++) {
+    d[aa] = (int32_t *)(buf + aa * sb);
+    HCK(hipMemcpyAsync(d[aa], txdataF[aa] + off, (size_t)N * 4, hipMemcpyHostToDevice, g_scr.s), -1);
+  }
+  HCK(oai4g_launch_sync(d, a, g_scr.s), -1);
+  for (uint32_t aa = 0; aa < n_ant; aa++)
+    HCK(hipMemcpyAsync(txdataF[aa] + off, d[aa], (size_t)N * 4, hipMemcpyDeviceToHost, g_scr.s), -1);
+  HCK(hipStreamSynchronize(g_scr.s), -1);
+  return 0;
+}
+
+extern "C" int oai4g_generate_pss(int32_t **txdataF, int16_t amp, const oai4g_frame_parms_t *fp, uint16_t symbol,
+                                  uint16_t slot_offset)
+{
+  return sync_dropin(txdataF, amp, fp, symbol, slot_offset, true);
+}
+
+extern "C" int oai4g_generate_sss(int32_t **txdataF, int16_t amp, const oai4g_frame_parms_t *fp, uint16_t symbol,
+                                  uint16_t slot_offset)
+{
+  return sync_dropin(txdataF, amp, fp, symbol, slot_offset, false);
+}
+
+static void pbch_args(const oai4g_frame_parms_t *fp, int amp, const uint8_t *pdu, uint8_t frame_mod4, pbch_args_t &a)
+{
+  memset(&a, 0, sizeof(a));
+  for (int i = 0; i < 3; i++) a.a[3 - i - 1] = pdu[i];       /* pbch.c:214-215 */
+  a.encode = frame_mod4 == 0 ? 1 : 0;
+  a.amask = fp->mode1_flag == 1 ? 0 : (fp->nb_antennas_tx_eNB == 2 ? 0xffff : (fp->nb_antennas_tx_eNB == 4 ? 0x5555 : 0));
+  a.E = fp->Ncp == 0 ? 1920 : 1728;
+  a.Nid = fp->Nid_cell;
+  a.quarter = frame_mod4 & 3u;
+  a.N = fp->ofdm_symbol_size;
+  const uint32_t nsymb = fp->Ncp == 0 ? 14 : 12, second = fp->Ncp == 0 ? 4 : 3;
+  for (uint32_t i = 0; i < 4; i++) {                          /* pbch.c:345-362 */
+    const uint32_t l = (nsymb >> 1) + i;
+    if (l == 0 || l == (nsymb >> 1) || l == 1 || l == (nsymb >> 1) + 1 || l == second || l == second + (nsymb >> 1))
+      a.pil_mask |= 1u << i;
+  }
+  a.nushift3 = fp->nushift % 3;
+  a.gain = (int16_t)((amp * 23170) >> 15);
+  a.mode1 = fp->mode1_flag == 1 ? 1 : 0;
+  a.n_ant = fp->nb_antennas_tx;
+}
+
+extern "C" int oai4g_generate_pbch(oai4g_pbch_t *st, int32_t **txdataF, int amp, const oai4g_frame_parms_t *fp,
+                                   const uint8_t *pbch_pdu, uint8_t frame_mod4)
+{
+  NEED_INIT(-1);
+  const uint32_t N = fp->ofdm_symbol_size, nsymb = fp->Ncp == 0 ? 14 : 12, n_ant = fp->nb_antennas_tx;
+  if (n_ant < 1 || n_ant > 4 || (fp->mode1_flag != 1 && n_ant != 2) || frame_mod4 > 3) {
+    set_err("generate_pbch: %u antennas (mode1 %u), frame_mod4 %u", n_ant, fp->mode1_flag, frame_mod4);
+    return -1;
+  }
+  pbch_args_t a;
+  pbch_args(fp, amp, pbch_pdu, frame_mod4, a);
+  const size_t gb = (size_t)4 * N * 4, gs = (gb + 255) & ~(size_t)255, off = (size_t)(nsymb >> 1) * N;
+  uint8_t *buf = scratch(4 * gs + 2048);
+  if (!buf) return -1;
+  int32_t *d[4];
+  uint8_t *de = buf + 4 * gs;
+  for (uint32_t aa = 0; aa < n_ant; aa++) {
+    d[aa] = (int32_t *)(buf + aa * gs);
+    HCK(hipMemcpyAsync(d[aa], txdataF[aa] + off, gb, hipMemcpyHostToDevice, g_scr.s), -1);
+  }
+  if (!a.encode) HCK(hipMemcpyAsync(de, st->pbch_e, a.E, hipMemcpyHostToDevice, g_scr.s), -1);
+  HCK(oai4g_launch_pbch(d, de, a, g_scr.s), -1);
+  if (a.encode) HCK(hipMemcpyAsync(st->pbch_e, de, a.E, hipMemcpyDeviceToHost, g_scr.s), -1);
+  for (uint32_t aa = 0; aa < n_ant; aa++)
+    HCK(hipMemcpyAsync(txdataF[aa] + off, d[aa], gb, hipMemcpyDeviceToHost, g_scr.s), -1);
+  HCK(hipStreamSynchronize(g_scr.s), -1);
+  return 0;
+}
+
+static uint32_t ngroup_phich_h(const oai4g_frame_parms_t *fp)
+{
+  uint32_t n = ((uint32_t)fp->phich_resource * fp->N_RB_DL) / 48;
+  if (((uint32_t)fp->phich_resource * fp->N_RB_DL) % 48) n++;
+  return n;
+}
+
+/* phich_item_t of one generate_phich call; offsets relative to symbol 0 of the subframe */
+static int phich_item(const oai4g_frame_parms_t *fp, uint8_t nseq, uint8_t ngroup, uint8_t HI, uint8_t subframe,
+                      phich_item_t &it)
+{
+  if (fp->Ncp != 0 || fp->phich_duration != 0 || fp->nushift >= 3) {
+    set_err("generate_phich: only normal CP, normal duration and nushift < 3 are defined (phich.c:540-580)");
+    return -1;
+  }
+  uint16_t reg[56][3];
+  const int ng = oai4g_generate_phich_reg_mapping(fp, reg);
+  if (ngroup >= ng || nseq > 7 || subframe > 9) { set_err("generate_phich: group %u / seq %u", ngroup, nseq); return -1; }
+  it.c_init = ((((uint32_t)subframe + 1u) * (fp->Nid_cell + 1u)) << 9) + fp->Nid_cell;
+  const uint32_t N = fp->ofdm_symbol_size;
+  for (int q = 0; q < 3; q++) {
+    uint32_t ro = fp->first_carrier_offset + (uint32_t)reg[ngroup][q] * 6;
+    if (ro > N) ro -= N - 1;                                   /* '>' as phich.c:560 */
+    it.reg_off[q] = ro;
+  }
+  it.nseq = nseq;
+  it.hi = HI ? 1 : 0;
+  return 0;
+}
+
+static void phich_common(const oai4g_frame_parms_t *fp, int16_t amp, phich_args_t &a)
+{
+  a.gain = fp->mode1_flag == 1 ? (int16_t)(((int32_t)amp * 23170) >> 15) : (int16_t)(amp / 2);
+  a.mode1 = fp->mode1_flag == 1 ? 1 : 0;
+  a.n_ant = fp->mode1_flag == 1 ? 1 : 2;                      /* SISO writes y[0] only (phich.c:696-760) */
+  a.nushift = fp->nushift;
+  a.win = 2u * fp->ofdm_symbol_size;
+}
+
+extern "C" int oai4g_generate_phich(const oai4g_frame_parms_t *fp, int16_t amp, uint8_t nseq_PHICH, uint8_t ngroup_PHICH,
+                                    uint8_t HI, uint8_t subframe, int32_t **y)
+{
+  NEED_INIT(-1);
+  static thread_local phich_args_t a;
+  memset(&a, 0, sizeof(a));
+  if (phich_item(fp, nseq_PHICH, ngroup_PHICH, HI, subframe, a.it[0]) != 0) return -1;
+  a.n = 1;
+  phich_common(fp, amp, a);
+  if (a.n_ant > 1 && fp->nb_antennas_tx < 2) { set_err("generate_phich: ALAMOUTI needs two grids"); return -1; }
+  const uint32_t N = fp->ofdm_symbol_size;
+  const size_t wb = (size_t)a.win * 4, ws = (wb + 255) & ~(size_t)255, off = (size_t)14 * N * subframe;
+  uint8_t *buf = scratch(2 * ws + 4 * ws);
+  if (!buf) return -1;
+  int32_t *d[2] = {(int32_t *)buf, (int32_t *)(buf + ws)};
+  int32_t *acc = (int32_t *)(buf + 2 * ws);
+  for (uint32_t aa = 0; aa < a.n_ant; aa++) HCK(hipMemcpyAsync(d[aa], y[aa] + off, wb, hipMemcpyHostToDevice, g_scr.s), -1);
+  HCK(oai4g_launch_phich(d, acc, a, g_scr.s), -1);
+  for (uint32_t aa = 0; aa < a.n_ant; aa++) HCK(hipMemcpyAsync(y[aa] + off, d[aa], wb, hipMemcpyDeviceToHost, g_scr.s), -1);
+  HCK(hipStreamSynchronize(g_scr.s), -1);
+  return 0;
+}
+
+extern "C" int oai4g_phich_group_seq(const oai4g_frame_parms_t *fp, uint16_t first_rb, uint8_t n_DMRS, uint8_t *ngroup,
+                                     uint8_t *nseq)
+{
+  const uint32_t Ng = ngroup_phich_h(fp), NSF = fp->Ncp == 1 ? 2 : 4;
+  if (!Ng) { set_err("phich_group_seq: no PHICH groups"); return -1; }
+  *ngroup = (uint8_t)((first_rb + n_DMRS) % Ng);
+  *nseq = (uint8_t)((first_rb / Ng + n_DMRS) % (2 * NSF));
   return 0;
 }

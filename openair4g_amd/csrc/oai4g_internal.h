@@ -129,7 +129,7 @@ struct cfg_dev_t {
   uint32_t pilmask;             /* bit l: symbol l carries CRS (QAM levels scaled by rho_B) */
   const uint32_t *crs_tab;      /* [10][6][200] packed CRS IQ of pilot symbol i (l = 0, 4, 7, 11; 1, 8 for
                                    ports 2/3 with 4 TX antennas), index m */
-  const uint32_t *ctl_tab;      /* [10][3][2][N] packed IQ of the control region (PCFICH + PDCCH, antennas
+  const uint32_t *ctl_tab;      /* [10][14][2][N] packed IQ of the static REs (PCFICH, PDCCH, PHICH, PSS, SSS, PBCH; antennas
                                    0 / 1) per subframe index; REs with code OAI4G_CTL_CODE take it */
   uint32_t ctlmask[10];         /* bit l: symbol l of subframe index sf carries control REs */
   uint32_t ctl_on;
@@ -226,6 +226,50 @@ struct dci_args_t {
  * after quadruplet interleaving and the cyclic shift.  One workgroup. */
 hipError_t oai4g_launch_dci(const dci_args_t &a, const uint32_t *d_map, const uint16_t *d_src, int32_t *d_g0,
                             int32_t *d_g1, uint32_t g1_stride, hipStream_t s);
+
+/* synchronisation / broadcast / HARQ-indicator channels (oai4g_ctrl.hip) */
+struct sync_args_t {    /* generate_pss (pss.c:50-103) / generate_sss (sss.c:47-92) */
+  int16_t val[62][2];   /* PSS: the Zadoff-Chu table entries (primary_synch.h); SSS: (d(n), 0), d = +-1 */
+  int16_t a;            /* amp or (amp ONE_OVER_SQRT2_Q15) >> 15 */
+  uint8_t pss;          /* 1: (a v) >> 15 per component; 0: (int16)(a v), imaginary 0 */
+  uint8_t n_ant;
+  uint32_t N;           /* ofdm_symbol_size: k starts at N - 31 and skips DC */
+};
+hipError_t oai4g_launch_sync(int32_t *const *d_sym /* per antenna: the symbol's N REs */, const sync_args_t &a,
+                             hipStream_t s);
+struct pbch_args_t {    /* generate_pbch (pbch.c:161-420) */
+  uint8_t a[3];         /* pbch_a: the pdu bytes reversed (pbch.c:214-215) */
+  uint8_t encode;       /* frame_mod4 == 0: encode and scramble into e; else map the stored e */
+  uint16_t amask;       /* CRC16 antenna mask (pbch.c:223-238) */
+  uint16_t E;           /* 1920 (normal CP) / 1728 */
+  uint32_t Nid;         /* scrambling c_init (pbch.c:770) */
+  uint32_t quarter;     /* frame_mod4 */
+  uint32_t N;           /* ofdm_symbol_size */
+  uint32_t pil_mask;    /* bit l (0..3): symbol nsymb/2 + l is a pilot symbol for the PBCH (pbch.c:345-362) */
+  uint32_t nushift3;
+  int16_t gain;         /* (amp ONE_OVER_SQRT2_Q15) >> 15 */
+  uint8_t mode1;
+  uint8_t n_ant;
+};
+/* d_g[a]: 4 consecutive symbols (nsymb/2 .. +3) of antenna a; d_e: the 1920-bit state (bytes) */
+hipError_t oai4g_launch_pbch(int32_t *const *d_g, uint8_t *d_e, const pbch_args_t &a, hipStream_t s);
+#define OAI4G_MAX_PHICH 64
+struct phich_item_t {
+  uint32_t c_init;      /* ((subframe + 1)(Nid + 1)) << 9 + Nid (phich.c:440) */
+  uint32_t reg_off[3];  /* first RE of each REG relative to the subframe's symbol 0 (phich.c:556-561) */
+  uint8_t nseq, hi;
+};
+struct phich_args_t {   /* generate_phich (phich.c:401-780), normal CP */
+  uint32_t n;
+  phich_item_t it[OAI4G_MAX_PHICH];
+  int16_t gain;         /* SISO (amp 23170) >> 15, ALAMOUTI amp / 2 */
+  uint8_t mode1;
+  uint8_t n_ant;
+  uint32_t nushift;     /* < 3 */
+  uint32_t win;         /* REs of the window the offsets index (2 symbols) */
+};
+/* d_g[a]: window of symbols 0..1 of the subframe, antenna a; d_acc: 4 * win int32 scratch */
+hipError_t oai4g_launch_phich(int32_t *const *d_g, int32_t *d_acc, const phich_args_t &a, hipStream_t s);
 
 /* UE receive front end (oai4g_fep.hip): per-symbol CP removal + forward DFT */
 #define OAI4G_FEP_MAX_SYM 14

@@ -828,7 +828,7 @@ __global__ void __launch_bounds__(128) MODOFDM_ATTR k_modofdm(const cfg_dev_t *_
                 /* control region (generate_dci_top writes antennas 0 and 1 only, dci.c:2260-2336) */
                 const bool ctl_re = (cd & 0xE000u) == OAI4G_CTL_CODE;
                 if (ctl_re) {
-                  const size_t cb = ((size_t)(sfi * 3 + l) * 2) * N + (uint32_t)t + (uint32_t)(N / 16) * (uint32_t)n;
+                  const size_t cb = ((size_t)(sfi * 14 + l) * 2) * N + (uint32_t)t + (uint32_t)(N / 16) * (uint32_t)n;
 #pragma unroll
                   for (int a = 0; a < NA; a++) {
                     const uint32_t ant = NA == 1 ? 0u : (uint32_t)a + 2 * pair;

@@ -195,6 +195,22 @@ uint8_t orc_generate_dci_top(uint8_t num_ue_spec_dci, uint8_t num_common_dci, co
                              uint32_t subframe);
 /* the scrambled PDCCH bits e[] of the last orc_generate_dci_top (values 0/1/2 = NIL), for tests */
 const uint8_t *orc_last_dci_e(uint32_t *len);
+/* ---- synchronisation / broadcast / HARQ-indicator channels (oai_oracle_sync.c; pss.c:50-103,
+ *      sss.c:47-92, pbch.c:62-420, 760-783, phich.c:401-780, primary_synch.h, sss.h) ---- */
+typedef struct {           /* LTE_eNB_PBCH (LTE_TRANSPORT/defs.h): state kept across frame_mod4 */
+  uint8_t pbch_d[96 + 3 * (16 + 24)];
+  uint8_t pbch_w[3 * 3 * (16 + 24)];
+  uint8_t pbch_e[1920];
+} orc_pbch_t;
+void orc_primary_synch(uint8_t Nid2, int16_t out[144]);
+void orc_sss_seq(uint16_t Nid_cell, int sf5, int16_t d[62]);
+int orc_generate_pss(int32_t **txdataF, int16_t amp, const orc_frame_t *fp, uint16_t symbol, uint16_t slot_offset);
+int orc_generate_sss(int32_t **txdataF, int16_t amp, const orc_frame_t *fp, uint16_t symbol, uint16_t slot_offset);
+void orc_pbch_scrambling(const orc_frame_t *fp, uint8_t *e, uint32_t length);
+int orc_generate_pbch(orc_pbch_t *st, int32_t **txdataF, int amp, const orc_frame_t *fp, const uint8_t *pbch_pdu,
+                      uint8_t frame_mod4);
+int orc_generate_phich(const orc_frame_t *fp, int16_t amp, uint8_t nseq_PHICH, uint8_t ngroup_PHICH, uint8_t HI,
+                       uint8_t subframe, int32_t **y);
 /* orc_tx_subframe plus generate_dci_top's PCFICH + PDCCH before the OFDM step (dlsim.c:2553) */
 int orc_tx_subframe_dci(const orc_tx_cfg_t *cfg, uint8_t *payload[2], int32_t **txdataF, int32_t **txdata,
                         uint8_t *e_out[2], uint8_t n_ue_dci, uint8_t n_common_dci, const orc_dci_alloc_t *dci);

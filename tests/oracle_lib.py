@@ -434,3 +434,44 @@ def phich_reg_mapping(fp):
 def get_nCCE_offset(table, L, nCCE, common, rnti, subframe):
     return orc().orc_get_nCCE_offset(table.ctypes.data_as(ctypes.POINTER(ctypes.c_int)), L, nCCE, common, rnti,
                                      subframe)
+
+
+# ---- synchronisation / broadcast / HARQ-indicator channels (oracle/oai_oracle_sync.c) ----
+class OrcPbch(ctypes.Structure):
+    _fields_ = [("pbch_d", ctypes.c_uint8 * (96 + 120)), ("pbch_w", ctypes.c_uint8 * 360),
+                ("pbch_e", ctypes.c_uint8 * 1920)]
+
+
+def _grid_ptrs(grids):
+    return (ctypes.c_void_p * len(grids))(*[g.ctypes.data for g in grids])
+
+
+def primary_synch(nid2):
+    out = np.zeros(144, dtype=np.int16)
+    orc().orc_primary_synch(nid2, P(out))
+    return out
+
+
+def sss_seq(nid_cell, sf5):
+    d = np.zeros(62, dtype=np.int16)
+    orc().orc_sss_seq(nid_cell, int(sf5), P(d))
+    return d
+
+
+def generate_pss(grids, amp, fp, symbol, slot_offset):
+    return orc().orc_generate_pss(_grid_ptrs(grids), ctypes.c_int16(amp), ctypes.byref(fp), symbol, slot_offset)
+
+
+def generate_sss(grids, amp, fp, symbol, slot_offset):
+    return orc().orc_generate_sss(_grid_ptrs(grids), ctypes.c_int16(amp), ctypes.byref(fp), symbol, slot_offset)
+
+
+def generate_pbch(state, grids, amp, fp, pdu, frame_mod4):
+    """orc_generate_pbch on the subframe-0 grids (state: OrcPbch kept across frame_mod4, as eNB_pbch)"""
+    pdu = np.ascontiguousarray(pdu, dtype=np.uint8)
+    return orc().orc_generate_pbch(ctypes.byref(state), _grid_ptrs(grids), amp, ctypes.byref(fp), P(pdu), frame_mod4)
+
+
+def generate_phich(fp, amp, nseq, ngroup, hi, subframe, grids):
+    return orc().orc_generate_phich(ctypes.byref(fp), ctypes.c_int16(amp), nseq, ngroup, hi, subframe,
+                                    _grid_ptrs(grids))

@@ -706,3 +706,173 @@ def pdcch_grid(N_RB, Nid, subframe, dcis, npdcch, amp, N, first_carrier, mode1, 
 
 
 NIL = 3
+
+
+# ------------------------------------------------------------------ synchronisation signals (36.211 6.11)
+def _bin(k, N_RB, N, first_carrier):
+    """FFT bin of subcarrier k (0 .. 12 N_RB - 1): below DC from first_carrier, above it from 1."""
+    return first_carrier + k if k < 6 * N_RB else k - 6 * N_RB + 1
+
+
+def pss_seq(Nid2):
+    """36.211 6.11.1.1 Zadoff-Chu d_u(n), u = 25 / 29 / 34, as (re, im) in Q15 with the reference
+    table's rounding floor(32767 x) (cited parameter: PHY/LTE_REFSIG/primary_synch.h)."""
+    import math
+    u = (25, 29, 34)[Nid2]
+    out = []
+    for n in range(62):
+        m = n if n < 31 else n + 1
+        ang = -math.pi * u * m * (m + 1) / 63
+        out.append((math.floor(32767 * math.cos(ang)), math.floor(32767 * math.sin(ang))))
+    return out
+
+
+def sss_seq(Nid, subframe5):
+    """36.211 6.11.2.1: d(2n) / d(2n+1) from the m-sequences s, c, z (values +-1)."""
+    def mseq(taps):
+        x = [0, 0, 0, 0, 1]
+        for i in range(26):
+            x.append(sum(x[i + t] for t in taps) % 2)
+        return [1 - 2 * v for v in x]
+    st, ct, zt = mseq((2, 0)), mseq((3, 0)), mseq((4, 2, 1, 0))
+    n1, n2 = Nid // 3, Nid % 3
+    qp = n1 // 30
+    q = (n1 + qp * (qp + 1) // 2) // 30
+    mp = n1 + q * (q + 1) // 2
+    m0 = mp % 31
+    m1 = (m0 + mp // 31 + 1) % 31
+    d = [0] * 62
+    for n in range(31):
+        s0, s1 = st[(n + m0) % 31], st[(n + m1) % 31]
+        c0, c1 = ct[(n + n2) % 31], ct[(n + n2 + 3) % 31]
+        z0, z1 = zt[(n + m0 % 8) % 31], zt[(n + m1 % 8) % 31]
+        if not subframe5:
+            d[2 * n], d[2 * n + 1] = s0 * c0, s1 * c1 * z0
+        else:
+            d[2 * n], d[2 * n + 1] = s1 * c0, s0 * c1 * z1
+    return d
+
+
+def sync_grid(N_RB, Nid, amp, N, first_carrier, n_ant, Ncp=0):
+    """PSS and SSS of subframes 0 and 5 (FDD, 36.211 6.11.1.2 / 6.11.2.2): {(subframe, l, bin):
+    (re, im)}, the same on every antenna; a = amp (one antenna) or (amp 23170) >> 15, PSS values
+    (a d) >> 15 in Q15, SSS values a d (+-a, imaginary 0)."""
+    a = amp if n_ant == 1 else (amp * 23170) >> 15
+    nsl = 7 if Ncp == 0 else 6
+    ps = pss_seq(Nid % 3)
+    out = {}
+    for sf in (0, 5):
+        ss = sss_seq(Nid, sf == 5)
+        for n in range(62):
+            b = _bin(n - 31 + 6 * N_RB, N_RB, N, first_carrier)
+            out[(sf, nsl - 1, b)] = ((a * ps[n][0]) >> 15, (a * ps[n][1]) >> 15)
+            out[(sf, nsl - 2, b)] = (_w16(a * ss[n]), 0)
+    return out
+
+
+# ------------------------------------------------------------------ PBCH (36.212 5.3.1, 36.211 6.6)
+def pbch_e(pdu, Nid, n_ant_enb, mode1, Ncp=0):
+    """The scrambled PBCH bits of one 40 ms period: a = the 24 MIB bits (the reference's pdu bytes
+    in reverse order, pbch.c:214-215), CRC16 XOR the antenna mask (36.212 Table 5.3.1.1-1: 0,
+    all-ones, 0101...; the reference applies none in transmission mode 1), TBCC, rate matching to
+    1920 (1728) bits, scrambling with c_init = Nid (36.211 6.6.1)."""
+    a = bytes_to_bits(list(reversed(list(pdu[:3]))), 24)
+    mask = 0 if mode1 else {1: 0, 2: 0xFFFF, 4: 0x5555}[n_ant_enb]
+    p = crc16_ref(a)
+    c = a + [p[i] ^ ((mask >> (15 - i)) & 1) for i in range(16)]
+    E = 1920 if Ncp == 0 else 1728
+    e = cc_rate_match(tbcc_encode(c), E)
+    cs = gold(Nid, E)
+    return [e[i] ^ cs[i] for i in range(E)]
+
+
+def pbch_grid(pdu, frame_mod4, N_RB, Nid, amp, N, first_carrier, mode1, n_ant, n_ant_enb=2, Ncp=0):
+    """PBCH REs of subframe 0 per antenna, {(l, bin): (re, im)}: quarter frame_mod4 of pbch_e,
+    QPSK (7.1.2) with gain g = (amp 23170) >> 15, the 72 subcarriers around DC of symbols 0..3 of
+    slot 1 minus the positions reserved for the RS of ports 0..3 (k = v_shift mod 3 + 3j in the
+    symbols that carry them), k first then l (6.6.4).  Two antennas: SFBC (6.3.4.3) with the
+    reference's fixed point (cited departures, pbch.c:116-145): each component (+-g 23170) >> 15
+    (floor, so -g maps to one LSB more than +g), and the partner RE written as the negated /
+    conjugated values of RE n."""
+    E = 1920 if Ncp == 0 else 1728
+    e = pbch_e(pdu, Nid, n_ant_enb, mode1, Ncp)[frame_mod4 * (E // 4):(frame_mod4 + 1) * (E // 4)]
+    g = (amp * 23170) >> 15
+    nsl = 7 if Ncp == 0 else 6
+    pil_l = {0, 1} | ({3} if Ncp else set())        # slot-1 symbols carrying RS of ports 0..3
+    vs3 = (Nid % 6) % 3
+    res = []
+    for lp in range(4):
+        for kp in range(72):
+            if lp in pil_l and kp % 3 == vs3:
+                continue
+            res.append((nsl + lp, _bin(6 * N_RB - 36 + kp, N_RB, N, first_carrier)))
+    qp = [(-g if e[2 * i] else g, -g if e[2 * i + 1] else g) for i in range(len(res))]
+    out = [dict() for _ in range(n_ant)]
+    if mode1:
+        for i, r in enumerate(res):
+            for aa in range(n_ant):
+                out[aa][r] = qp[i]
+        return out
+    s = lambda v: (v * 23170) >> 15
+    for i in range(0, len(res), 2):
+        x0, x1 = qp[i], qp[i + 1]
+        y0 = (s(x0[0]), s(x0[1]))
+        y1 = (s(-x1[0]), s(x1[1]))                   # -x1*
+        out[0][res[i]], out[1][res[i]] = y0, y1
+        out[0][res[i + 1]] = (_w16(-y1[0]), y1[1])    # x1
+        out[1][res[i + 1]] = (y0[0], _w16(-y0[1]))    # x0*
+    return out
+
+
+# ------------------------------------------------------------------ PHICH (36.212 5.3.5, 36.211 6.9)
+PHICH_W = [(1, 1, 1, 1), (1, -1, 1, -1), (1, 1, -1, -1), (1, -1, -1, 1),
+           ('j', 'j', 'j', 'j'), ('j', '-j', 'j', '-j'), ('j', 'j', '-j', '-j'), ('j', '-j', '-j', 'j')]
+
+
+def phich_grid(N_RB, Nid, subframe, ngroup, nseq, hi, amp, N, first_carrier, mode1, n_ant, pcfich_regs, Ng6=1,
+               ref_c_init=True):
+    """One PHICH of symbol 0 (normal CP, normal duration) per antenna, {bin: (re, im)} accumulated:
+    HI repeated 3 times (5.3.5), BPSK z = (1 + j)(1 - 2b) in units of the gain, orthogonal
+    sequence w (Table 6.9.1-2) and scrambling (1 - 2c(i)) per symbol (6.9.1), SISO gain
+    (amp 23170) >> 15 or SFBC with amp / 2 (6.3.4.3), quadruplet i on REG n_bar_i (6.9.3).
+    ref_c_init: the reference's c_init = ((subframe + 1)(Nid + 1)) 2^9 + Nid (phich.c:440) instead
+    of the spec's (subframe + 1)(2 Nid + 1) 2^9 + Nid (cited departure)."""
+    ci = (((subframe + 1) * (Nid + 1)) << 9) + Nid if ref_c_init else (((subframe + 1) * (2 * Nid + 1)) << 9) + Nid
+    c = gold(ci, 12)
+    b = 1 if hi else 0
+    d = []
+    for i in range(12):
+        v = (1 - 2 * c[i]) * (1 - 2 * b)
+        w = PHICH_W[nseq][i % 4]
+        if w in (1, -1):
+            d.append((w * v, w * v))
+        else:
+            sgn = 1 if w == 'j' else -1
+            d.append((-sgn * v, sgn * v))                  # j (1 + j) = -1 + j
+    g = (amp * 23170) >> 15 if mode1 else amp // 2
+    if mode1:
+        y = [[(_w16(x[0] * g), _w16(x[1] * g)) for x in d]] * n_ant
+    else:
+        y0, y1 = [None] * 12, [None] * 12
+        for k in range(0, 12, 2):
+            a0 = (_w16(d[k][0] * g), _w16(d[k][1] * g))
+            b1 = (_w16(-d[k + 1][0] * g), _w16(d[k + 1][1] * g))
+            y0[k], y1[k] = a0, b1
+            y0[k + 1], y1[k + 1] = (_w16(-b1[0]), b1[1]), (a0[0], _w16(-a0[1]))
+        y = [y0, y1]
+    regs = phich_regs(N_RB, Nid, Ng6, pcfich_regs)[ngroup]
+    vs = (Nid % 6) % 3
+    out = [dict() for _ in range(n_ant)]
+    for q in range(3):
+        ro = first_carrier + 6 * regs[q]
+        if ro > N:
+            ro -= N - 1                                     # '>' (phich.c:560), not '>='
+        m = 0
+        for j in range(6):
+            if j in (vs, vs + 3):
+                continue
+            for a in range(n_ant):
+                r0, i0 = out[a].get(ro + j, (0, 0))
+                out[a][ro + j] = (_w16(r0 + y[a][4 * q + m][0]), _w16(i0 + y[a][4 * q + m][1]))
+            m += 1
+    return out
