@@ -187,6 +187,7 @@ _SIGS = {
                                             ctypes.c_uint8, ctypes.c_uint8, ctypes.POINTER(ctypes.c_void_p)]),
     "oai4g_phich_group_seq": (ctypes.c_int, [ctypes.POINTER(FrameParms), ctypes.c_uint16, ctypes.c_uint8,
                                              ctypes.POINTER(ctypes.c_uint8), ctypes.POINTER(ctypes.c_uint8)]),
+    "oai4g_tx_config_set_common": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p]),
     "oai4g_dft": (ctypes.c_int, [ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int]),
     "oai4g_dft2048": (None, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int]),
     "oai4g_dft1024": (None, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int]),
@@ -369,6 +370,16 @@ def generate_sss(grids, amp, fp, symbol, slot_offset):
     """generate_sss drop-in (sss.c:47)."""
     init()
     return lib().oai4g_generate_sss(_grid_ptrs(grids), amp, ctypes.byref(fp), symbol, slot_offset)
+
+
+class PhichItem(ctypes.Structure):
+    _fields_ = [("subframe", ctypes.c_uint8), ("ngroup", ctypes.c_uint8), ("nseq", ctypes.c_uint8), ("hi", ctypes.c_uint8)]
+
+
+class CommonSig(ctypes.Structure):
+    """oai4g_common_sig_t"""
+    _fields_ = [("pss_sss", ctypes.c_uint8), ("pbch", ctypes.c_uint8), ("pbch_pdu", ctypes.c_uint8 * 3),
+                ("frame_mod4", ctypes.c_uint8), ("n_phich", ctypes.c_uint8), ("phich", PhichItem * 64)]
 
 
 class Pbch(ctypes.Structure):
@@ -726,6 +737,23 @@ class TxPipeline:
         batch element (items as for generate_dci_top; [] switches it off)."""
         arr = dci_allocs(items)
         _check(self.L.oai4g_tx_config_set_control(self.cfg, len(items) - n_common, n_common, arr) == 0)
+
+    def set_common(self, pss_sss=False, pbch_pdu=None, frame_mod4=0, phich=()):
+        """oai4g_tx_config_set_common: PSS + SSS (subframe indices 0 / 5), the PBCH quarter
+        frame_mod4 of pbch_pdu (subframe index 0) and PHICHs (subframe, ngroup, nseq, hi);
+        with no argument it switches them off."""
+        c = CommonSig()
+        c.pss_sss = 1 if pss_sss else 0
+        if pbch_pdu is not None:
+            c.pbch = 1
+            for i in range(3):
+                c.pbch_pdu[i] = int(pbch_pdu[i])
+        c.frame_mod4 = frame_mod4
+        c.n_phich = len(phich)
+        for i, (sf, g, q, h) in enumerate(phich):
+            c.phich[i].subframe, c.phich[i].ngroup, c.phich[i].nseq, c.phich[i].hi = sf, g, q, h
+        on = c.pss_sss or c.pbch or c.n_phich
+        _check(self.L.oai4g_tx_config_set_common(self.cfg, ctypes.byref(c) if on else None) == 0)
 
     def fill_payload(self, seed):
         _check(self.L.oai4g_fill_payload(self.d_payload, self.payload_bytes, seed, None) == 0)

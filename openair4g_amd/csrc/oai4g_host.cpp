@@ -2343,7 +2343,7 @@ static int rebuild_static(oai4g_tx_config_t *cfg)
     std::vector<uint32_t> tab((size_t)10 * 14 * 2 * N, 0);
     const size_t gbytes = (size_t)14 * N * 4, gpad = (gbytes + 255) & ~(size_t)255;
     const size_t mcap = (size_t)4 * 1024;    /* >= 4 nquad REs for every geometry */
-    const size_t accb = (size_t)4 * 2 * N * 4;
+    const size_t accb = (size_t)4 * 4 * N * 4;   /* PHICH accumulators / PBCH encode grid (4 antennas x 4 symbols) */
     uint8_t *buf = scratch(4 * gpad + mcap * 4 + mcap * 2 + accb + 2048 + 256);
     if (!buf) return -1;
     int32_t *dg[4] = {(int32_t *)buf, (int32_t *)(buf + gpad), (int32_t *)(buf + 2 * gpad), (int32_t *)(buf + 3 * gpad)};
@@ -2408,8 +2408,9 @@ static int rebuild_static(oai4g_tx_config_t *cfg)
           int32_t *pp[4];
           for (uint32_t aa = 0; aa < 4; aa++) pp[aa] = dg[aa] + (size_t)nsl * N;
           if (cm.frame_mod4) {                          /* encode (quarter 0) into a scratch grid, then map */
-            HCK(oai4g_launch_pbch(pp, dpe, pa, g_scr.s), -1);
-            HCK(hipMemsetAsync(buf, 0, 4 * gpad, g_scr.s), -1);
+            int32_t *sp[4];
+            for (uint32_t aa = 0; aa < 4; aa++) sp[aa] = dacc + (size_t)aa * 4 * N;
+            HCK(oai4g_launch_pbch(sp, dpe, pa, g_scr.s), -1);
             pbch_args(&fp, cfg->p.amp, cm.pbch_pdu, cm.frame_mod4, pa);
           }
           HCK(oai4g_launch_pbch(pp, dpe, pa, g_scr.s), -1);
