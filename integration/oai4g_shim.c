@@ -1,7 +1,8 @@
 /* oai4g_shim.c — reference-side binding of the MI355X DLSCH transmit path.
  * Replaces: dlsch_coding.c:254 dlsch_encoding, dlsch_scrambling.c:51, dlsch_modulation.c:1181,
  * ofdm_mod.c:47/85/233, lte_dfts.c idft64..idft2048, crc_byte.c:117/135, lte_segmentation.c:39,
- * 3gpplte_sse.c:380, lte_rate_matching.c:51/464. */
+ * 3gpplte_sse.c:380, lte_rate_matching.c:51/464, pcfich.c:48/144, dci.c:2024, pss.c:50, sss.c:47,
+ * pbch.c:161, phich.c:401. */
 #include "PHY/defs.h"
 #include "PHY/extern.h"
 #include "oai4g.h"
@@ -19,6 +20,9 @@ static void fp_to(const LTE_DL_FRAME_PARMS *f, oai4g_frame_parms_t *o)
   o->nb_prefix_samples = f->nb_prefix_samples;
   o->nb_prefix_samples0 = f->nb_prefix_samples0;
   o->samples_per_tti = f->samples_per_tti;
+  o->phich_resource = f->phich_config_common.phich_resource;
+  o->phich_duration = f->phich_config_common.phich_duration;
+  o->tdd_config = f->tdd_config;      o->nb_antennas_tx_eNB = f->nb_antennas_tx_eNB;
 }
 
 /* The mirror points INTO the reference's own HARQ buffers, so every write lands in place. */
@@ -163,6 +167,38 @@ void generate_pcfich(uint8_t num_pdcch_symbols, int16_t amp, LTE_DL_FRAME_PARMS 
   oai4g_frame_parms_t fp;
   fp_to(frame_parms, &fp);
   oai4g_generate_pcfich(num_pdcch_symbols, amp, &fp, (int32_t **)txdataF, subframe);
+}
+
+/* synchronisation, broadcast and HARQ-indicator channels: pss.c:50, sss.c:47, pbch.c:161
+ * (LTE_eNB_PBCH's pbch_e is the library's oai4g_pbch_t state, impl_defs_lte.h:959-963),
+ * phich.c:401 (void in the reference; the library's -1 for its undefined cases is dropped) */
+int generate_pss(mod_sym_t **txdataF, short amp, LTE_DL_FRAME_PARMS *frame_parms, unsigned short symbol,
+                 unsigned short slot_offset)
+{
+  oai4g_frame_parms_t fp;
+  fp_to(frame_parms, &fp);
+  return oai4g_generate_pss((int32_t **)txdataF, amp, &fp, symbol, slot_offset);
+}
+int generate_sss(mod_sym_t **txdataF, int16_t amp, LTE_DL_FRAME_PARMS *frame_parms, uint16_t symbol,
+                 uint16_t slot_offset)
+{
+  oai4g_frame_parms_t fp;
+  fp_to(frame_parms, &fp);
+  return oai4g_generate_sss((int32_t **)txdataF, amp, &fp, symbol, slot_offset);
+}
+int generate_pbch(LTE_eNB_PBCH *eNB_pbch, mod_sym_t **txdataF, int amp, LTE_DL_FRAME_PARMS *frame_parms,
+                  uint8_t *pbch_pdu, uint8_t frame_mod4)
+{
+  oai4g_frame_parms_t fp;
+  fp_to(frame_parms, &fp);
+  return oai4g_generate_pbch((oai4g_pbch_t *)eNB_pbch->pbch_e, (int32_t **)txdataF, amp, &fp, pbch_pdu, frame_mod4);
+}
+void generate_phich(LTE_DL_FRAME_PARMS *frame_parms, int16_t amp, uint8_t nseq_PHICH, uint8_t ngroup_PHICH,
+                    uint8_t HI, uint8_t subframe, mod_sym_t **y)
+{
+  oai4g_frame_parms_t fp;
+  fp_to(frame_parms, &fp);
+  (void)oai4g_generate_phich(&fp, amp, nseq_PHICH, ngroup_PHICH, HI, subframe, (int32_t **)y);
 }
 
 /* callees that dlsim / ltetest also call directly */
