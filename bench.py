@@ -42,6 +42,26 @@ def _traffic(config, kernel, batch):
     return t.get(kernel) if t.get("batch") == batch else None
 
 
+def _valu_busy(config, batch):
+    """VALU-busy fraction per kernel (SQ_ACTIVE_INST_VALU / CUs / GRBM_GUI_ACTIVE) from the committed
+    rocprofv3 --pmc pass (tools/gpu_pmc_valu.sh -> profiles/valu_<config>.json), only when it was
+    measured at this batch size (else null)."""
+    try:
+        t = json.load(open(os.path.join(ROOT, "profiles", f"valu_{config}.json")))
+    except Exception:
+        return None
+    if t.get("batch") != batch:
+        return None
+    out = {}
+    for k, v in t.items():
+        if not isinstance(v, dict):
+            continue
+        name = "encode_rm_scramble" if k.startswith("k_encode") else "modulate_idft_cp" if "k_modofdm" in k else None
+        if name:
+            out[name] = round(v["valu_busy"], 4)
+    return out or None
+
+
 def cpu_model():
     try:
         for line in open("/proc/cpuinfo"):
@@ -542,6 +562,7 @@ def bench_tx(args, world, rank, host):
                        "parallelism": f"subframe-sharded x{world}"},
             "roofline": {"bound": "hbm", "kernel": dom, "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": ach / HBM_PEAK_GBS, "traffic": traffic,
+                         "valu_issue_frac": _valu_busy(args.config, args.batch),
                          "kernel_ms": {k: v["ms"] for k, v in per_kernel.items()},
                          "algorithmic_bytes_per_launch": {k: v["bytes"] for k, v in per_kernel.items()}},
             "end_to_end_algorithmic_GBps": value * (payload_b + iq_b) / 1e9,

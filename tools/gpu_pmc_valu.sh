@@ -10,5 +10,5 @@ timeout -s KILL 300 rocprofv3 --pmc $CTRS --output-format csv -d gpurun_out/pmc/
   python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline --kernel-reps 1 --config $CONFIG > gpurun_out/pmc/valu_${CONFIG}.log 2>&1
 rc=$?; echo "pmc rc=$rc"; tail -2 gpurun_out/pmc/valu_${CONFIG}.log
 [ $rc -eq 0 ] || exit $rc
-python3 tools/valu_table.py gpurun_out/pmc/valu_${CONFIG} $CONFIG > gpurun_out/pmc/valu_${CONFIG}.md
+python3 tools/valu_table.py gpurun_out/pmc/valu_${CONFIG} $CONFIG ${BATCH:-8192} > gpurun_out/pmc/valu_${CONFIG}.md
 cat gpurun_out/pmc/valu_${CONFIG}.md

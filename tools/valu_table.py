@@ -9,6 +9,7 @@ import sys
 from collections import defaultdict
 
 d, config = sys.argv[1], sys.argv[2]
+batch = int(sys.argv[3]) if len(sys.argv) > 3 else None
 f = glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True)[0]
 acc = defaultdict(lambda: defaultdict(list))   # kernel -> counter -> [per-dispatch values]
 disp = defaultdict(lambda: defaultdict(float))
@@ -39,4 +40,5 @@ for k, c in sorted(acc.items()):
               "wait_inst_frac": wait, "dispatches": len(c["SQ_INSTS_VALU"])}
     print(f"| `{k}` | {len(c['SQ_INSTS_VALU'])} | {m.get('SQ_INSTS_VALU', 0):.4g} | {busy:.3f} | {clk:.2f} | "
           f"{m.get('SQ_INSTS_LDS', 0):.4g} | {m.get('SQ_LDS_BANK_CONFLICT', 0):.4g} | {wait:.3f} |")
+out["batch"] = batch
 json.dump(out, open(os.path.join(d, f"valu_{config}.json"), "w"), indent=1)
