@@ -229,6 +229,38 @@ uint8_t oai4g_generate_dci_top(uint8_t num_ue_spec_dci, uint8_t num_common_dci, 
                                uint32_t n_rnti, int16_t amp, const oai4g_frame_parms_t *frame_parms,
                                int32_t **txdataF, uint32_t subframe);
 
+/* ---------------- UE PDSCH demodulation (second half) ---------------- */
+/* rx_pdsch (PHY/LTE_TRANSPORT/dlsch_demodulation.c:82) over the PDSCH symbols of one subframe as
+ * dlsim runs it (dlsim.c:3188-3260): dlsch_extract_rbs_single (:3167), dlsch_channel_level (:2777)
+ * -> log2_maxh, dlsch_channel_compensation (:801) and dlsch_qpsk / 16qam / 64qam_llr
+ * (dlsch_llr_computation.c:636, 688, 810).  Transmission mode 1 (one TX port), one receive
+ * antenna, even N_RB_DL (6 / 50 / 100; the reference's odd-N_RB extraction is not restated), the
+ * first PDSCH symbol without pilots.  rxdataF and dl_ch_estimates are one subframe, [nsymb][N]
+ * each (estimate of subcarrier 12 rb + i at entry 5 + 12 rb + i of its symbol, the layout of the
+ * reference's estimator and of dlsim's perfect-CE mode, dlsim.c:2935-2966).  Writes the LLR
+ * stream (not unscrambled) and log2_maxh; returns its length or -1. */
+int oai4g_rx_pdsch_siso(const oai4g_frame_parms_t *frame_parms, const int32_t *rxdataF, const int32_t *dl_ch_estimates,
+                        const uint32_t rb_alloc[4], uint8_t Qm, uint8_t num_pdcch_symbols, uint8_t subframe,
+                        int16_t *llr, uint8_t *log2_maxh);
+/* dlsch_unscrambling (dlsch_scrambling.c:99, decl LTE_TRANSPORT/proto.h): llr[k] *= 2 c(k) - 1
+ * for k < 32 (1 + G / 32) with c_init = rnti 2^14 + q 2^13 + (Ns / 2) 2^9 + Nid_cell (the
+ * reference reads rnti from its LTE_UE_DLSCH_t; mbsfn_flag 1 is not supported). */
+void oai4g_dlsch_unscrambling(const oai4g_frame_parms_t *frame_parms, int mbsfn_flag, uint16_t rnti, int G,
+                              int16_t *llr, uint8_t q, uint8_t Ns);
+/* Batched demodulation: n_sf subframes (subframe index first_subframe + i * subframe_step mod 10)
+ * of rxdataF and per-symbol channel estimates ([n_sf][nsymb][N] int32 each, device) -> LLR
+ * streams [n_sf][oai4g_rx_llr_stride] int16 (device), unscrambled (q = 0, Ns = 2 subframe) when
+ * unscramble != 0.  The demodulator is elementwise per RE after the per-subframe channel level. */
+typedef struct oai4g_rx_config oai4g_rx_config_t;
+oai4g_rx_config_t *oai4g_rx_config_create(const oai4g_frame_parms_t *frame_parms, const uint32_t rb_alloc[4], uint8_t Qm,
+                                          uint8_t num_pdcch_symbols, uint16_t rnti, uint8_t first_subframe,
+                                          uint8_t subframe_step);
+void oai4g_rx_config_destroy(oai4g_rx_config_t *cfg);
+int oai4g_rx_llr_count(const oai4g_rx_config_t *cfg, int subframe_index);
+size_t oai4g_rx_llr_stride(const oai4g_rx_config_t *cfg);
+int oai4g_rx_batch(oai4g_rx_config_t *cfg, int n_sf, const int32_t *d_rxdataF, const int32_t *d_dl_ch_estimates,
+                   int16_t *d_llr, int unscramble, void *stream);
+
 /* ---------------- synchronisation, broadcast and HARQ-indicator channels ---------------- */
 /* generate_pss (PHY/LTE_TRANSPORT/pss.c:50, decl LTE_TRANSPORT/proto.h): the Zadoff-Chu sequence
  * of root 25 / 29 / 34 (Nid_cell % 3, the Q15 table of PHY/LTE_REFSIG/primary_synch.h, here

@@ -188,6 +188,19 @@ _SIGS = {
     "oai4g_phich_group_seq": (ctypes.c_int, [ctypes.POINTER(FrameParms), ctypes.c_uint16, ctypes.c_uint8,
                                              ctypes.POINTER(ctypes.c_uint8), ctypes.POINTER(ctypes.c_uint8)]),
     "oai4g_tx_config_set_common": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p]),
+    "oai4g_rx_pdsch_siso": (ctypes.c_int, [ctypes.POINTER(FrameParms), ctypes.c_void_p, ctypes.c_void_p,
+                                           ctypes.POINTER(ctypes.c_uint32), ctypes.c_uint8, ctypes.c_uint8,
+                                           ctypes.c_uint8, ctypes.c_void_p, ctypes.POINTER(ctypes.c_uint8)]),
+    "oai4g_dlsch_unscrambling": (None, [ctypes.POINTER(FrameParms), ctypes.c_int, ctypes.c_uint16, ctypes.c_int,
+                                        ctypes.c_void_p, ctypes.c_uint8, ctypes.c_uint8]),
+    "oai4g_rx_config_create": (ctypes.c_void_p, [ctypes.POINTER(FrameParms), ctypes.POINTER(ctypes.c_uint32),
+                                                 ctypes.c_uint8, ctypes.c_uint8, ctypes.c_uint16, ctypes.c_uint8,
+                                                 ctypes.c_uint8]),
+    "oai4g_rx_config_destroy": (None, [ctypes.c_void_p]),
+    "oai4g_rx_llr_count": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
+    "oai4g_rx_llr_stride": (ctypes.c_size_t, [ctypes.c_void_p]),
+    "oai4g_rx_batch": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                      ctypes.c_int, ctypes.c_void_p]),
     "oai4g_dft": (ctypes.c_int, [ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int]),
     "oai4g_dft2048": (None, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int]),
     "oai4g_dft1024": (None, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int]),
@@ -424,6 +437,68 @@ def slot_fep(rxdata, rxdataF, fp, l, Ns, sample_offset=0, no_prefix=0):
     rp = (ctypes.c_void_p * n)(*[a.ctypes.data for a in rxdata])
     fpp = (ctypes.c_void_p * n)(*[a.ctypes.data for a in rxdataF])
     return lib().oai4g_slot_fep(rp, fpp, ctypes.byref(fp), n, l, Ns, sample_offset, no_prefix)
+
+
+def rx_pdsch_siso(fp, rxdataF, dl_ch, rb_alloc, Qm, num_pdcch, subframe):
+    """rx_pdsch over one subframe's PDSCH symbols (TM1, one RX antenna): rxdataF / dl_ch are
+    int32 [nsymb*N].  Returns (LLR stream int16, log2_maxh)."""
+    init()
+    rxdataF = np.ascontiguousarray(rxdataF, dtype=np.int32)
+    dl_ch = np.ascontiguousarray(dl_ch, dtype=np.int32)
+    out = np.zeros(14 * 1200 * 6 + 64, dtype=np.int16)
+    sh = ctypes.c_uint8()
+    ra = (ctypes.c_uint32 * 4)(*rb_alloc)
+    n = lib().oai4g_rx_pdsch_siso(ctypes.byref(fp), _ptr(rxdataF), _ptr(dl_ch), ra, Qm, num_pdcch, subframe,
+                                  _ptr(out), ctypes.byref(sh))
+    _check(n >= 0)
+    return out[:n], sh.value
+
+
+def dlsch_unscrambling(fp, rnti, G, llr, q, Ns):
+    """dlsch_unscrambling drop-in (in place on an int16 array of >= 32 (1 + G/32) entries)."""
+    init()
+    lib().oai4g_dlsch_unscrambling(ctypes.byref(fp), 0, rnti, G, _ptr(llr), q, Ns)
+    return llr
+
+
+class RxBatch:
+    """Device-resident batched PDSCH demodulation (oai4g_rx_batch)."""
+
+    def __init__(self, fp, rb_alloc, Qm, num_pdcch, rnti, n_sf, first_subframe=0, subframe_step=1):
+        init()
+        self.L = lib()
+        ra = (ctypes.c_uint32 * 4)(*rb_alloc)
+        self.cfg = self.L.oai4g_rx_config_create(ctypes.byref(fp), ra, Qm, num_pdcch, rnti, first_subframe,
+                                                 subframe_step)
+        _check(bool(self.cfg))
+        self.fp, self.n_sf = fp, n_sf
+        self.stride = self.L.oai4g_rx_llr_stride(self.cfg)
+        n_in = n_sf * fp.symbols_per_tti * fp.ofdm_symbol_size
+        self.d_y = self.L.oai4g_dev_alloc(n_in * 4)
+        self.d_h = self.L.oai4g_dev_alloc(n_in * 4)
+        self.d_llr = self.L.oai4g_dev_alloc(n_sf * self.stride * 2)
+        _check(bool(self.d_y) and bool(self.d_h) and bool(self.d_llr))
+
+    def llr_count(self, sfi):
+        return self.L.oai4g_rx_llr_count(self.cfg, sfi)
+
+    def run(self, rxdataF, dl_ch, unscramble=1, d_rxdataF=None):
+        if d_rxdataF is None:
+            y = np.ascontiguousarray(rxdataF, dtype=np.int32)
+            _check(self.L.oai4g_memcpy_h2d(self.d_y, _ptr(y), y.nbytes) == 0)
+        h = np.ascontiguousarray(dl_ch, dtype=np.int32)
+        _check(self.L.oai4g_memcpy_h2d(self.d_h, _ptr(h), h.nbytes) == 0)
+        _check(self.L.oai4g_rx_batch(self.cfg, self.n_sf, d_rxdataF or self.d_y, self.d_h, self.d_llr, unscramble,
+                                     None) == 0)
+        _check(self.L.oai4g_sync() == 0)
+        out = np.empty((self.n_sf, self.stride), dtype=np.int16)
+        _check(self.L.oai4g_memcpy_d2h(_ptr(out), self.d_llr, out.nbytes) == 0)
+        return out
+
+    def close(self):
+        for p in (self.d_y, self.d_h, self.d_llr):
+            self.L.oai4g_dev_free(p)
+        self.L.oai4g_rx_config_destroy(self.cfg)
 
 
 class FepBatch:

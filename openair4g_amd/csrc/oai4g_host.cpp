@@ -477,15 +477,16 @@ static void crc_mul_tables(uint32_t per, int levels, uint32_t poly, uint32_t (*t
   }
 }
 
-/* QAM tables (dlsch_modulation.c:79-103, 1223-1246) */
+/* QAM tables (dlsch_modulation.c:79-103, 1223-1246).  The raw tables are int (LTE_TRANSPORT/
+ * vars.h:72): the outer 64-QAM level 35393 exceeds int16 and is only narrowed after the scaling. */
 static void qam_tables_scaled(int Qm, int16_t amp, int16_t srho_a, int16_t srho_b, bool alamouti, cw_dev_t &c)
 {
-  int16_t q16[4], q64[8];
+  int32_t q16[4], q64[8];
   for (int a = -1; a <= 1; a += 2)
     for (int b = -1; b <= 1; b += 2) {
-      q16[(1 + a) + (1 + b) / 2] = (int16_t)(-a * (20724 + b * 10362));
+      q16[(1 + a) + (1 + b) / 2] = -a * (20724 + b * 10362);
       for (int cc = -1; cc <= 1; cc += 2)
-        q64[(1 + a) * 2 + (1 + b) + (1 + cc) / 2] = (int16_t)(-a * (20225 + b * (10112 + cc * 5056)));
+        q64[(1 + a) * 2 + (1 + b) + (1 + cc) / 2] = -a * (20225 + b * (10112 + cc * 5056));
     }
   int16_t amp_a = (int16_t)(((int32_t)amp * srho_a) >> 13), amp_b = (int16_t)(((int32_t)amp * srho_b) >> 13);
   c.qpsk_a = (int16_t)((amp_a * 23170) >> 15);
@@ -494,9 +495,9 @@ static void qam_tables_scaled(int Qm, int16_t amp, int16_t srho_a, int16_t srho_
   const int16_t sa = alamouti ? (int16_t)(((int32_t)amp_a * 23170) >> 15) : amp_a;
   const int16_t sb = alamouti ? (int16_t)(((int32_t)amp_b * 23170) >> 15) : amp_b;
   for (int i = 0; i < 8; i++) {
-    int16_t v = Qm == 4 ? q16[i & 3] : q64[i];
-    c.qam_a[i] = (int16_t)(((int32_t)v * sa) >> 15);
-    c.qam_b[i] = (int16_t)(((int32_t)v * sb) >> 15);
+    const int32_t v = Qm == 4 ? q16[i & 3] : q64[i];
+    c.qam_a[i] = (int16_t)((v * sa) >> 15);
+    c.qam_b[i] = (int16_t)((v * sb) >> 15);
   }
   /* ALAMOUTI QPSK (:371-386): +-gain, then * ONE_OVER_SQRT2_Q15 >> 15 */
   const int16_t g[2] = {c.qpsk_a, c.qpsk_b};
@@ -2700,4 +2701,245 @@ extern "C" int oai4g_phich_group_seq(const oai4g_frame_parms_t *fp, uint16_t fir
   *ngroup = (uint8_t)((first_rb + n_DMRS) % Ng);
   *nseq = (uint8_t)((first_rb / Ng + n_DMRS) % (2 * NSF));
   return 0;
+}
+
+/* ----------------------------------------------------------------------------------------
+ * UE PDSCH demodulation (second half): host geometry of rx_pdsch's
+ * extraction / LLR lengths (dlsch_demodulation.c:3167-3300, dlsch_llr_computation.c:636-930,
+ * adjust_G2 lte_mcs.c:157-245) and the scrambling words; the per-RE work on the GPU
+ * (oai4g_rx.hip).  TM1, one receive antenna, even N_RB_DL.
+ * -------------------------------------------------------------------------------------- */
+struct oai4g_rx_config {
+  oai4g_frame_parms_t fp;
+  rx_dev_t h;
+  rx_dev_t *d = nullptr;
+  uint32_t *d_map = nullptr, *d_gold = nullptr;
+  uint8_t *d_shift = nullptr;
+  int shift_cap = 0;
+  uint32_t llr_count[10];
+};
+
+static int rx_alloc_bit(const uint32_t rb_alloc[4], int rb)
+{
+  if (rb < 32) return (rb_alloc[0] >> rb) & 1;
+  if (rb < 64) return (rb_alloc[1] >> (rb - 32)) & 1;
+  if (rb < 96) return (rb_alloc[2] >> (rb - 64)) & 1;
+  if (rb < 100) return (rb_alloc[3] >> (rb - 96)) & 1;
+  return 0;
+}
+
+/* adjust_G2 (lte_mcs.c:157-245) */
+static int rx_adjust_G2(const oai4g_frame_parms_t *fp, const uint32_t rb_alloc[4], uint32_t subframe, uint32_t symbol)
+{
+  const uint32_t nsymb = fp->Ncp == 0 ? 14 : 12;
+  int re = 0;
+  if (subframe != 0 && subframe != 5 && subframe != 6) return 0;
+  if (symbol < (nsymb >> 1) && fp->frame_type == 1 && subframe != 6) return 0;
+  if (fp->frame_type == 1) {
+    if (symbol > (nsymb >> 1) + 3 && symbol != nsymb - 1) return 0;
+    if (subframe == 5 && symbol != nsymb - 1) return 0;
+    if (subframe == 6 && symbol != 2) return 0;
+  } else {
+    if (symbol > (nsymb >> 1) + 3 || symbol < (nsymb >> 1) - 2) return 0;
+    if (subframe == 5 && symbol != (nsymb >> 1) - 1 && symbol != (nsymb >> 1) - 2) return 0;
+    if (subframe == 6) return 0;
+  }
+  const int half = fp->N_RB_DL >> 1;
+  if (fp->N_RB_DL & 1) {
+    for (int rb = half - 3; rb <= half + 3; rb++)
+      if (rx_alloc_bit(rb_alloc, rb)) re += (rb == half - 3 || rb == half + 3) ? 6 : 12;
+  } else {
+    for (int rb = half - 3; rb < half + 3; rb++)
+      if (rx_alloc_bit(rb_alloc, rb)) re += 12;
+  }
+  return re;
+}
+
+extern "C" oai4g_rx_config_t *oai4g_rx_config_create(const oai4g_frame_parms_t *fp, const uint32_t rb_alloc[4], uint8_t Qm,
+                                                     uint8_t num_pdcch_symbols, uint16_t rnti, uint8_t first_subframe,
+                                                     uint8_t subframe_step)
+{
+  NEED_INIT(nullptr);
+  if ((fp->N_RB_DL & 1) || fp->nb_antennas_tx != 1 || fp->mode1_flag != 1 || (Qm != 2 && Qm != 4 && Qm != 6) ||
+      num_pdcch_symbols < 1 || num_pdcch_symbols > 3) {
+    set_err("rx_config: TM1 (one TX port), even N_RB_DL, Qm 2/4/6, 1..3 PDCCH symbols only");
+    return nullptr;
+  }
+  const uint32_t nsymb = fp->Ncp == 0 ? 14 : 12, N = fp->ofdm_symbol_size;
+  const uint32_t first_mod = num_pdcch_symbols >= 7u - fp->Ncp ? num_pdcch_symbols - (7u - fp->Ncp) : num_pdcch_symbols;
+  if (first_mod == 0 || first_mod == 4u - fp->Ncp) {
+    set_err("rx_config: the first PDSCH symbol carries pilots (dlsch_channel_level would read past the extracted REs)");
+    return nullptr;
+  }
+  auto *cfg = new oai4g_rx_config();
+  cfg->fp = *fp;
+  rx_dev_t &h = cfg->h;
+  memset(&h, 0, sizeof(h));
+  h.N = N;
+  h.nsymb = nsymb;
+  h.Qm = Qm;
+  h.npdcch = num_pdcch_symbols;
+  h.n_sym = nsymb - num_pdcch_symbols;
+  h.first_sf = first_subframe % 10;
+  h.sf_step = subframe_step;
+  h.a1 = Qm == 4 ? 20724 : (Qm == 6 ? 20225 : 0);          /* QAM16_n1 / QAM64_n1 (impl_defs_top.h:215-224) */
+  h.a2 = Qm == 6 ? 10112 : 0;                               /* QAM64_n2 */
+  std::vector<uint32_t> map;
+  uint32_t max_llr = 0;
+  for (uint32_t sf = 0; sf < 10; sf++) {
+    uint32_t off = 0;
+    for (uint32_t k = 0; k < h.n_sym; k++) {
+      const uint32_t l = num_pdcch_symbols + k;
+      const uint32_t smod = l >= 7u - fp->Ncp ? l - (7u - fp->Ncp) : l;
+      const bool pil = smod == 0 || smod == 4u - fp->Ncp;
+      const uint32_t poff = smod == 4u - fp->Ncp ? 3 : 0;
+      h.map_off[sf][k] = (uint32_t)map.size();
+      uint32_t n = 0, nb_rb = 0, bin = fp->first_carrier_offset;
+      for (uint32_t rb = 0; rb < fp->N_RB_DL; rb++) {        /* dlsch_extract_rbs_single, even N_RB_DL */
+        if (rb == (fp->N_RB_DL >> 1u)) bin = 1;
+        if (rx_alloc_bit(rb_alloc, (int)rb)) {
+          for (uint32_t i = 0; i < 12; i++)
+            if (!pil || (i != fp->nushift + poff && i != (fp->nushift + poff + 6) % 12)) {
+              map.push_back((bin + i) | ((5 + 12 * rb + i) << 16));
+              n++;
+            }
+          nb_rb++;
+        }
+        bin += 12;
+      }
+      h.n_ext[sf][k] = n;
+      const int adj = Qm == 2 ? 0 : rx_adjust_G2(fp, rb_alloc, sf, l);
+      const int len = pil ? (int)nb_rb * 10 - 5 * adj / 6 : (int)nb_rb * 12 - adj;
+      h.len[sf][k] = (uint32_t)(len > 0 ? len : 0);
+      h.llr_off[sf][k] = off;
+      off += h.len[sf][k] * Qm;
+      if (k == 0) {
+        h.lvl_n[sf] = 12 * nb_rb;
+        h.lvl_div[sf] = (pil ? 10 : 12) * nb_rb;
+      }
+      if (nb_rb == 0) { set_err("rx_config: empty allocation"); delete cfg; return nullptr; }
+    }
+    cfg->llr_count[sf] = off;
+    max_llr = off > max_llr ? off : max_llr;
+  }
+  h.llr_stride = (max_llr + 63) & ~63u;
+  /* scrambling words per subframe index: c_init = rnti 2^14 + q 2^13 + (Ns/2) 2^9 + Nid, q = 0,
+   * Ns = 2 subframe (dlsch_scrambling.c:116), word w = lte_gold_generic output 50 + w */
+  h.gold_words = (max_llr + 31) / 32 + 1;
+  std::vector<uint32_t> gold((size_t)10 * h.gold_words);
+  for (uint32_t sf = 0; sf < 10; sf++) {
+    uint32_t x1 = 1u + (1u << 31), x2 = ((uint32_t)rnti << 14) + (sf << 9) + fp->Nid_cell;
+    x2 = x2 ^ ((x2 ^ (x2 >> 1) ^ (x2 >> 2) ^ (x2 >> 3)) << 31);
+    auto step = [&]() {
+      x1 = (x1 >> 1) ^ (x1 >> 4);
+      x1 = x1 ^ (x1 << 31) ^ (x1 << 28);
+      x2 = (x2 >> 1) ^ (x2 >> 2) ^ (x2 >> 3) ^ (x2 >> 4);
+      x2 = x2 ^ (x2 << 31) ^ (x2 << 30) ^ (x2 << 29) ^ (x2 << 28);
+    };
+    for (int n = 1; n < 50; n++) step();
+    for (uint32_t w = 0; w < h.gold_words; w++) {
+      step();
+      gold[(size_t)sf * h.gold_words + w] = x1 ^ x2;
+    }
+  }
+  if (hipMalloc(&cfg->d_map, map.size() * 4) != hipSuccess || hipMalloc(&cfg->d_gold, gold.size() * 4) != hipSuccess ||
+      hipMalloc(&cfg->d, sizeof(rx_dev_t)) != hipSuccess) {
+    set_err("rx_config: device allocation failed");
+    oai4g_rx_config_destroy(cfg);
+    return nullptr;
+  }
+  h.map = cfg->d_map;
+  h.gold = cfg->d_gold;
+  if (hipMemcpy(cfg->d_map, map.data(), map.size() * 4, hipMemcpyHostToDevice) != hipSuccess ||
+      hipMemcpy(cfg->d_gold, gold.data(), gold.size() * 4, hipMemcpyHostToDevice) != hipSuccess ||
+      hipMemcpy(cfg->d, &h, sizeof(rx_dev_t), hipMemcpyHostToDevice) != hipSuccess) {
+    set_err("rx_config: upload failed");
+    oai4g_rx_config_destroy(cfg);
+    return nullptr;
+  }
+  return cfg;
+}
+
+extern "C" void oai4g_rx_config_destroy(oai4g_rx_config_t *cfg)
+{
+  if (!cfg) return;
+  if (cfg->d) hipFree(cfg->d);
+  if (cfg->d_map) hipFree(cfg->d_map);
+  if (cfg->d_gold) hipFree(cfg->d_gold);
+  if (cfg->d_shift) hipFree(cfg->d_shift);
+  delete cfg;
+}
+
+extern "C" int oai4g_rx_llr_count(const oai4g_rx_config_t *cfg, int subframe_index)
+{
+  return (subframe_index < 0 || subframe_index > 9) ? -1 : (int)cfg->llr_count[subframe_index];
+}
+
+extern "C" size_t oai4g_rx_llr_stride(const oai4g_rx_config_t *cfg) { return cfg->h.llr_stride; }
+
+extern "C" int oai4g_rx_batch(oai4g_rx_config_t *cfg, int n_sf, const int32_t *d_rxdataF, const int32_t *d_ch,
+                              int16_t *d_llr, int unscramble, void *stream)
+{
+  NEED_INIT(-1);
+  if (n_sf <= 0) return 0;
+  if (n_sf > cfg->shift_cap) {
+    if (cfg->d_shift) hipFree(cfg->d_shift);
+    HCK(hipMalloc(&cfg->d_shift, (size_t)n_sf), -1);
+    cfg->shift_cap = n_sf;
+  }
+  HCK(oai4g_launch_rx(cfg->d, &cfg->h, n_sf, d_rxdataF, d_ch, d_llr, cfg->d_shift, unscramble, (hipStream_t)stream), -1);
+  return 0;
+}
+
+/* rx_pdsch over the PDSCH symbols of one subframe (dlsim.c:3188-3260) on host buffers:
+ * rxdataF / dl_ch_estimates = [nsymb][N] of the subframe; writes the LLR stream (not unscrambled)
+ * and log2_maxh; returns the stream length or -1. */
+extern "C" int oai4g_rx_pdsch_siso(const oai4g_frame_parms_t *fp, const int32_t *rxdataF, const int32_t *dl_ch_estimates,
+                                   const uint32_t rb_alloc[4], uint8_t Qm, uint8_t num_pdcch_symbols, uint8_t subframe,
+                                   int16_t *llr, uint8_t *log2_maxh)
+{
+  NEED_INIT(-1);
+  oai4g_rx_config_t *cfg = oai4g_rx_config_create(fp, rb_alloc, Qm, num_pdcch_symbols, 0, subframe, 1);
+  if (!cfg) return -1;
+  const size_t gb = (size_t)cfg->h.nsymb * cfg->h.N * 4, gs = (gb + 255) & ~(size_t)255;
+  const int n = (int)cfg->llr_count[subframe % 10];
+  uint8_t *buf = scratch(2 * gs + (size_t)cfg->h.llr_stride * 2 + 256);
+  if (!buf) { oai4g_rx_config_destroy(cfg); return -1; }
+  int32_t *dy = (int32_t *)buf, *dh = (int32_t *)(buf + gs);
+  int16_t *dl = (int16_t *)(buf + 2 * gs);
+  int rc = -1;
+  if (hipMemcpyAsync(dy, rxdataF, gb, hipMemcpyHostToDevice, g_scr.s) == hipSuccess &&
+      hipMemcpyAsync(dh, dl_ch_estimates, gb, hipMemcpyHostToDevice, g_scr.s) == hipSuccess &&
+      oai4g_rx_batch(cfg, 1, dy, dh, dl, 0, g_scr.s) == 0 &&
+      hipMemcpyAsync(llr, dl, (size_t)n * 2, hipMemcpyDeviceToHost, g_scr.s) == hipSuccess &&
+      (!log2_maxh || hipMemcpyAsync(log2_maxh, cfg->d_shift, 1, hipMemcpyDeviceToHost, g_scr.s) == hipSuccess) &&
+      hipStreamSynchronize(g_scr.s) == hipSuccess)
+    rc = n;
+  else
+    set_err("rx_pdsch_siso: HIP error");
+  oai4g_rx_config_destroy(cfg);
+  return rc;
+}
+
+/* dlsch_unscrambling (dlsch_scrambling.c:99-137): llr[k] *= 2 c(k) - 1 for k < 32 (1 + G / 32),
+ * c_init = rnti 2^14 + q 2^13 + (Ns / 2) 2^9 + Nid_cell (mbsfn_flag = 0); host buffer */
+extern "C" void oai4g_dlsch_unscrambling(const oai4g_frame_parms_t *fp, int mbsfn_flag, uint16_t rnti, int G,
+                                         int16_t *llr, uint8_t q, uint8_t Ns)
+{
+  (void)mbsfn_flag;
+  uint32_t x1 = 1u + (1u << 31), x2 = ((uint32_t)rnti << 14) + ((uint32_t)q << 13) + ((uint32_t)(Ns >> 1) << 9) + fp->Nid_cell;
+  x2 = x2 ^ ((x2 ^ (x2 >> 1) ^ (x2 >> 2) ^ (x2 >> 3)) << 31);
+  auto step = [&]() {
+    x1 = (x1 >> 1) ^ (x1 >> 4);
+    x1 = x1 ^ (x1 << 31) ^ (x1 << 28);
+    x2 = (x2 >> 1) ^ (x2 >> 2) ^ (x2 >> 3) ^ (x2 >> 4);
+    x2 = x2 ^ (x2 << 31) ^ (x2 << 30) ^ (x2 << 29) ^ (x2 << 28);
+  };
+  for (int n = 1; n < 50; n++) step();
+  int k = 0;
+  for (int i = 0; i < 1 + (G >> 5); i++) {
+    step();
+    const uint32_t s = x1 ^ x2;
+    for (int j = 0; j < 32; j++, k++) llr[k] = (int16_t)(((2 * ((s >> j) & 1)) - 1) * llr[k]);
+  }
 }

@@ -285,3 +285,21 @@ hipError_t oai4g_launch_fep(const int32_t *d_in, int32_t *d_out, int log2n, cons
                             const uint32_t *d_twf, int n_cu, hipStream_t s);
 hipError_t oai4g_launch_modulate_bytes(const cfg_dev_t *d_cfg, const cfg_dev_t *h_cfg, int sf,
                                        const uint8_t *d_e0, const uint8_t *d_e1, int32_t *d_grid, hipStream_t s);
+
+/* UE PDSCH demodulation (oai4g_rx.hip): TM1, one receive antenna, even N_RB_DL */
+struct rx_dev_t {
+  uint32_t N, nsymb, Qm, npdcch;
+  uint32_t llr_stride;            /* LLRs per batch element */
+  uint32_t n_sym;                 /* PDSCH symbols per subframe (nsymb - npdcch) */
+  /* per subframe index and PDSCH symbol: extraction map offset, extracted REs, demodulated REs,
+   * LLR offset; level REs and divisor for the first symbol */
+  uint32_t map_off[10][14], n_ext[10][14], len[10][14], llr_off[10][14];
+  uint32_t lvl_n[10], lvl_div[10];
+  uint32_t gold_words;            /* scrambling words per subframe index */
+  uint32_t first_sf, sf_step;
+  int16_t a1, a2;                 /* QAM_n1 / QAM_n2 of the channel magnitude (0 for QPSK) */
+  const uint32_t *map;            /* extracted RE j: FFT bin | (estimate index within the symbol) << 16 */
+  const uint32_t *gold;           /* [10][gold_words] */
+};
+hipError_t oai4g_launch_rx(const rx_dev_t *d_cfg, const rx_dev_t *h_cfg, int n_sf, const int32_t *d_rxF,
+                           const int32_t *d_ch, int16_t *d_llr, uint8_t *d_shift, int unscramble, hipStream_t s);

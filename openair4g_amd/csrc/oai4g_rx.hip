@@ -1,0 +1,97 @@
+/*
+ * gfx950 kernels for the UE's PDSCH demodulation after the FEP (second
+ * half): TM1 (one transmit port), one receive antenna, even N_RB_DL.
+ *   dlsch_extract_rbs_single    PHY/LTE_TRANSPORT/dlsch_demodulation.c:3167-3300
+ *   dlsch_channel_level         dlsch_demodulation.c:2777-2835, log2_maxh :286-300
+ *   dlsch_channel_compensation  dlsch_demodulation.c:801-960
+ *   dlsch_qpsk/16qam/64qam_llr  PHY/LTE_TRANSPORT/dlsch_llr_computation.c:636-930
+ *   dlsch_unscrambling          PHY/LTE_TRANSPORT/dlsch_scrambling.c:99-137
+ * Every step after the channel level is elementwise per extracted RE, so the demodulator is one
+ * thread per RE of a (subframe, symbol): the host's extraction map gives the FFT bin and the
+ * channel-estimate index, the RE's Qm LLRs go to their place in the subframe's LLR stream with the
+ * scrambling sign applied.  Integer arithmetic is the reference's SSE arithmetic lane for lane:
+ * madd_epi16 (int32 wrap) with the conjugate by sign_epi16 (int16 wrap), srai + packs_epi32
+ * (saturation), mulhi_epi16 << 1, abs_epi16 (-32768 stays), subs_epi16.
+ */
+#include "oai4g_internal.h"
+
+static __device__ __forceinline__ int16_t rx_sat16(int32_t v) { return (int16_t)max(-32768, min(32767, v)); }
+static __device__ __forceinline__ int16_t rx_abs16(int16_t v) { return v < 0 ? (int16_t)(-(int32_t)v) : v; }
+static __device__ __forceinline__ int32_t rx_madd(int16_t a0, int16_t b0, int16_t a1, int16_t b1)
+{
+  return (int32_t)((uint32_t)((int32_t)a0 * b0) + (uint32_t)((int32_t)a1 * b1));
+}
+
+/* dlsch_channel_level over the first PDSCH symbol -> log2_maxh = log2_approx(avg) / 2, per subframe */
+__global__ void __launch_bounds__(256) k_rx_level(const rx_dev_t *__restrict__ c, const int32_t *__restrict__ ch,
+                                                  uint8_t *__restrict__ shift)
+{
+  __shared__ uint32_t acc;
+  const uint32_t sf = blockIdx.x, sfi = (c->first_sf + sf * c->sf_step) % 10, l = c->npdcch;
+  if (threadIdx.x == 0) acc = 0;
+  __syncthreads();
+  const uint32_t *map = c->map + c->map_off[sfi][0];
+  const int32_t *chs = ch + ((size_t)sf * c->nsymb + l) * c->N;
+  uint32_t part = 0;
+  for (uint32_t j = threadIdx.x; j < c->lvl_n[sfi]; j += blockDim.x) {
+    const uint32_t h = (uint32_t)chs[map[j] >> 16];
+    part += (uint32_t)rx_madd((int16_t)h, (int16_t)h, (int16_t)(h >> 16), (int16_t)(h >> 16));
+  }
+  atomicAdd(&acc, part);                       /* int32 wrap-add commutes (the reference's epi32 lanes) */
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const int32_t avg = (int32_t)acc / (int32_t)c->lvl_div[sfi];
+    const uint32_t x = avg > 0 ? (uint32_t)avg : 0u;
+    const uint32_t l2 = x ? 32u - __clz(x & 0x7FFFFFFFu) : 0u;   /* log2_approx: bits 0..30 */
+    shift[sf] = (uint8_t)(l2 / 2);
+  }
+}
+
+__global__ void __launch_bounds__(256) k_rx_llr(const rx_dev_t *__restrict__ c, const int32_t *__restrict__ rxF,
+                                                const int32_t *__restrict__ ch, int16_t *__restrict__ llr,
+                                                const uint8_t *__restrict__ shift, int unscramble)
+{
+  const uint32_t sf = blockIdx.y, k = blockIdx.x, sfi = (c->first_sf + sf * c->sf_step) % 10;
+  const uint32_t l = c->npdcch + k, len = c->len[sfi][k], Qm = c->Qm;
+  const uint32_t *map = c->map + c->map_off[sfi][k];
+  const size_t so = ((size_t)sf * c->nsymb + l) * c->N;
+  const int32_t *y = rxF + so, *h = ch + so;
+  int16_t *out = llr + (size_t)sf * c->llr_stride + c->llr_off[sfi][k];
+  const uint32_t sh = shift[sf], base = c->llr_off[sfi][k];
+  const uint32_t *gold = c->gold + (size_t)sfi * c->gold_words;
+  for (uint32_t j = blockIdx.z * blockDim.x + threadIdx.x; j < len; j += gridDim.z * blockDim.x) {
+    const uint32_t m = map[j];
+    const uint32_t hv = (uint32_t)h[m >> 16], yv = (uint32_t)y[m & 0xFFFFu];
+    const int16_t hr = (int16_t)hv, hi = (int16_t)(hv >> 16), yr = (int16_t)yv, yi = (int16_t)(yv >> 16);
+    const int16_t nhi = (int16_t)(-(int32_t)hi);
+    int16_t v[6];
+    v[0] = rx_sat16(rx_madd(hr, yr, hi, yi) >> sh);
+    v[1] = rx_sat16(rx_madd(nhi, yr, hr, yi) >> sh);
+    if (Qm > 2) {
+      const int16_t mg = rx_sat16(rx_madd(hr, hr, hi, hi) >> sh);
+      const int16_t mag = (int16_t)((((int32_t)mg * c->a1) >> 16) << 1), magb = (int16_t)((((int32_t)mg * c->a2) >> 16) << 1);
+      v[2] = rx_sat16((int32_t)mag - rx_abs16(v[0]));
+      v[3] = rx_sat16((int32_t)mag - rx_abs16(v[1]));
+      v[4] = rx_sat16((int32_t)magb - rx_abs16(v[2]));
+      v[5] = rx_sat16((int32_t)magb - rx_abs16(v[3]));
+    }
+    for (uint32_t q = 0; q < Qm; q++) {
+      int16_t o = v[q];
+      if (unscramble) {
+        const uint32_t b = base + j * Qm + q;
+        o = (int16_t)(((gold[b >> 5] >> (b & 31)) & 1u) ? o : -(int32_t)o);   /* llr * (2 c - 1), int16 */
+      }
+      out[j * Qm + q] = o;
+    }
+  }
+}
+
+hipError_t oai4g_launch_rx(const rx_dev_t *d_cfg, const rx_dev_t *h_cfg, int n_sf, const int32_t *d_rxF,
+                           const int32_t *d_ch, int16_t *d_llr, uint8_t *d_shift, int unscramble, hipStream_t s)
+{
+  if (n_sf <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_rx_level, dim3(n_sf), dim3(256), 0, s, d_cfg, d_ch, d_shift);
+  hipLaunchKernelGGL(k_rx_llr, dim3(h_cfg->n_sym, n_sf, 2), dim3(256), 0, s, d_cfg, d_rxF, d_ch, d_llr, d_shift,
+                     unscramble);
+  return hipGetLastError();
+}

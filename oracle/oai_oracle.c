@@ -309,15 +309,17 @@ int orc_init_frame(orc_frame_t *fp, uint16_t N_RB_DL, uint16_t Nid_cell, uint8_t
  * Modulation + RE mapping — dlsch_modulation.c:53-71 (is_not_pilot), :79-103 (QAM tables),
  * :139-982 (allocate_REs_in_RB: SISO, ALAMOUTI and LARGE_CDD branches), :1181-1493 (dlsch_modulation).
  * ==================================================================================== */
-static int16_t qam16_tab[4], qam64_tab[8];
+/* int tables, as the reference's (LTE_TRANSPORT/vars.h:72 `int qam64_table[8],qam16_table[4]`):
+ * the outer 64-QAM level 20225 + 10112 + 5056 = 35393 does not fit int16 and must not wrap */
+static int32_t qam16_tab[4], qam64_tab[8];
 
 static void qam_tables(void)
 {
   for (int a = -1; a <= 1; a += 2)
     for (int b = -1; b <= 1; b += 2) {
-      qam16_tab[(1 + a) + (1 + b) / 2] = (int16_t)(-a * (20724 + b * 10362));
+      qam16_tab[(1 + a) + (1 + b) / 2] = -a * (20724 + b * 10362);
       for (int c = -1; c <= 1; c += 2)
-        qam64_tab[(1 + a) * 2 + (1 + b) + (1 + c) / 2] = (int16_t)(-a * (20225 + b * (10112 + c * 5056)));
+        qam64_tab[(1 + a) * 2 + (1 + b) + (1 + c) / 2] = -a * (20225 + b * (10112 + c * 5056));
     }
 }
 
@@ -374,7 +376,7 @@ static int modulation_impl(int32_t **txdataF, int16_t amp, uint32_t subframe, ui
   int16_t amp_a = (int16_t)(((int32_t)amp * sqrt_rho_a) >> 13);
   int16_t amp_b = (int16_t)(((int32_t)amp * sqrt_rho_b) >> 13);
   int16_t t0a[8], t0b[8], t1a[8], t1b[8];
-  const int16_t *src0 = Qm0 == 4 ? qam16_tab : qam64_tab, *src1 = Qm1 == 4 ? qam16_tab : qam64_tab;
+  const int32_t *src0 = Qm0 == 4 ? qam16_tab : qam64_tab, *src1 = Qm1 == 4 ? qam16_tab : qam64_tab;
   for (int i = 0; i < 8; i++) {
     t0a[i] = (int16_t)(((int32_t)src0[i & (Qm0 == 4 ? 3 : 7)] * amp_a) >> 15);
     t0b[i] = (int16_t)(((int32_t)src0[i & (Qm0 == 4 ? 3 : 7)] * amp_b) >> 15);
@@ -495,7 +497,7 @@ static int modulation_impl(int32_t **txdataF, int16_t amp, uint32_t subframe, ui
               v[0] = (int16_t)((t1r * 23170) >> 15); v[1] = (int16_t)((t1i * 23170) >> 15);
               v[2] = (int16_t)((t2r * 23170) >> 15); v[3] = (int16_t)((t2i * 23170) >> 15);
             } else {
-              const int16_t *raw = Qm0 == 4 ? qam16_tab : qam64_tab;
+              const int32_t *raw = Qm0 == 4 ? qam16_tab : qam64_tab;
               int ir, ii;
               qam_index(cw0->e, &jj, Qm0, &ir, &ii);
               v[0] = (int16_t)(((int32_t)amp2 * raw[ir]) >> 15);

@@ -211,6 +211,18 @@ int orc_generate_pbch(orc_pbch_t *st, int32_t **txdataF, int amp, const orc_fram
                       uint8_t frame_mod4);
 int orc_generate_phich(const orc_frame_t *fp, int16_t amp, uint8_t nseq_PHICH, uint8_t ngroup_PHICH, uint8_t HI,
                        uint8_t subframe, int32_t **y);
+/* ---- UE PDSCH demodulation after the FEP, TM1 / one RX antenna / even N_RB_DL (oai_oracle_rx.c;
+ *      dlsch_demodulation.c:82-700, 801-960, 2777-2835, 3167-3300, dlsch_llr_computation.c:636-930,
+ *      lte_mcs.c:157-245, dlsch_scrambling.c:99-137, log2_approx.c:29-45) ----
+ * rxdataF: one subframe [nsymb][N]; dl_ch_estimates: [nsymb][N] per-symbol estimates (entry
+ * 5 + 12 rb + i = subcarrier 12 rb + i).  Writes the LLR stream of every PDSCH symbol; returns
+ * its length or -1. */
+uint8_t orc_log2_approx(uint32_t x);
+int orc_adjust_G2(const orc_frame_t *fp, const uint32_t rb_alloc[4], uint8_t subframe, uint8_t symbol);
+int orc_rx_pdsch_siso(const orc_frame_t *fp, const int32_t *rxdataF, const int32_t *dl_ch_estimates,
+                      const uint32_t rb_alloc[4], uint8_t Qm, uint8_t num_pdcch_symbols, uint8_t subframe,
+                      int16_t *llr, uint8_t *log2_maxh_out);
+void orc_dlsch_unscrambling(int16_t *llr, int G, uint32_t c_init);
 /* orc_tx_subframe plus generate_dci_top's PCFICH + PDCCH before the OFDM step (dlsim.c:2553) */
 int orc_tx_subframe_dci(const orc_tx_cfg_t *cfg, uint8_t *payload[2], int32_t **txdataF, int32_t **txdata,
                         uint8_t *e_out[2], uint8_t n_ue_dci, uint8_t n_common_dci, const orc_dci_alloc_t *dci);

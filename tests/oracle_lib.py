@@ -475,3 +475,27 @@ def generate_pbch(state, grids, amp, fp, pdu, frame_mod4):
 def generate_phich(fp, amp, nseq, ngroup, hi, subframe, grids):
     return orc().orc_generate_phich(ctypes.byref(fp), ctypes.c_int16(amp), nseq, ngroup, hi, subframe,
                                     _grid_ptrs(grids))
+
+
+# ---- UE PDSCH demodulation (oracle/oai_oracle_rx.c) ----
+def rx_pdsch_siso(fp, rxdataF, dl_ch, rb_alloc, Qm, num_pdcch, subframe):
+    L = orc()
+    rxdataF = np.ascontiguousarray(rxdataF, dtype=np.int32)
+    dl_ch = np.ascontiguousarray(dl_ch, dtype=np.int32)
+    out = np.zeros(14 * 1200 * 6 + 64, dtype=np.int16)
+    sh = ctypes.c_uint8()
+    ra = (ctypes.c_uint32 * 4)(*rb_alloc)
+    n = L.orc_rx_pdsch_siso(ctypes.byref(fp), P(rxdataF), P(dl_ch), ra, Qm, num_pdcch, subframe, P(out),
+                            ctypes.byref(sh))
+    assert n >= 0
+    return out[:n], sh.value
+
+
+def dlsch_unscrambling(llr, G, c_init):
+    orc().orc_dlsch_unscrambling(P(llr), G, ctypes.c_uint32(c_init))
+    return llr
+
+
+def adjust_G2(fp, rb_alloc, subframe, symbol):
+    ra = (ctypes.c_uint32 * 4)(*rb_alloc)
+    return orc().orc_adjust_G2(ctypes.byref(fp), ra, subframe, symbol)

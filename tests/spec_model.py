@@ -169,15 +169,15 @@ def _w16(v):
 
 
 # QAM levels in Q15 (16-QAM: 1/sqrt10 (2 +- 1); 64-QAM: 1/sqrt42 (4 +- (2 +- 1))).  The reference
-# keeps them in int16 tables, so the outermost 64-QAM level 7/sqrt42 = 35393 wraps to -30143
-# (dlsch_modulation.c:79-103 assigning into int16_t qam64_table); the model stores them the same way.
+# keeps them in int tables (LTE_TRANSPORT/vars.h:72, filled by dlsch_modulation.c:79-103), so the
+# outermost 64-QAM level 7/sqrt42 = 35393 stays > 32767 until it is scaled by amp >> 15.
 QAM16_RAW = {}
 QAM64_RAW = {}
 for _a in (-1, 1):
     for _b in (-1, 1):
-        QAM16_RAW[(1 + _a) + (1 + _b) // 2] = _w16(-_a * (20724 + _b * 10362))
+        QAM16_RAW[(1 + _a) + (1 + _b) // 2] = -_a * (20724 + _b * 10362)
         for _c in (-1, 1):
-            QAM64_RAW[(1 + _a) * 2 + (1 + _b) + (1 + _c) // 2] = _w16(-_a * (20225 + _b * (10112 + _c * 5056)))
+            QAM64_RAW[(1 + _a) * 2 + (1 + _b) + (1 + _c) // 2] = -_a * (20225 + _b * (10112 + _c * 5056))
 
 
 def _sym_index(bits, Qm):
@@ -469,7 +469,7 @@ def crs_symbol(l, Ncp=0):
 def qam(bits, Qm, ampr, raw16=None, raw64=None):
     """One modulation symbol (36.211 7.1) in the reference's fixed point: QPSK +-(ampr/sqrt2)
     ((ampr * 23170) >> 15, bit 1 -> negative); 16/64-QAM (level * ampr) >> 15 with the levels
-    kept as the reference's int16 Q15 tables (the 64-QAM 7/sqrt42 entry wraps, see QAM64_RAW)."""
+    kept as the reference's int Q15 tables (the 64-QAM 7/sqrt42 entry 35393 > 32767, see QAM64_RAW)."""
     if Qm == 2:
         g = (ampr * 23170) >> 15
         return (-g if bits[0] else g, -g if bits[1] else g)

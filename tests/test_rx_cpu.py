@@ -1,0 +1,148 @@
+"""UE PDSCH demodulation oracle (oracle/oai_oracle_rx.c: dlsch_extract_rbs_single,
+dlsch_channel_level, dlsch_channel_compensation, dlsch_qpsk / 16qam / 64qam_llr, adjust_G2,
+dlsch_unscrambling).  The reference translation units (dlsch_demodulation.c,
+dlsch_llr_computation.c) include PHY/defs.h and are unbuildable here, so the restatement is pinned
+by the loop property: the oracle's own noiseless transmit grid (TM1, subframes without PBCH / sync)
+demodulated with dlsim's perfect channel estimate (AMP, 0) (dlsim.c:2955-2966) gives an LLR stream
+of exactly G entries whose signs reproduce every scrambled e bit, for QPSK, 16- and 64-QAM and
+6 / 50 / 100 PRB; plus the arithmetic corner cases restated from the SSE code."""
+import numpy as np
+import pytest
+
+import oracle_lib as O
+import openair4g_amd as oai
+
+
+def perfect_ce(fp, amp=512):
+    return np.full(fp.symbols_per_tti * fp.ofdm_symbol_size, amp, dtype=np.int32)
+
+
+def alloc(N_RB):
+    return [((1 << min(32, max(0, N_RB - 32 * i))) - 1) & 0xFFFFFFFF for i in range(4)]
+
+
+def params(name, N_RB, mcs, npdcch, sf, **kw):
+    return oai.make_params(name, subframe=sf, N_RB_DL=N_RB, nb_rb=N_RB, rb_alloc=alloc(N_RB), mcs=[mcs], TBS=None,
+                           num_pdcch_symbols=npdcch, with_crs=1, **kw)
+
+
+CASES = [("C2", 100, 16, 1, 7), ("C2", 100, 9, 3, 3), ("C2", 50, 27, 2, 8), ("C1", 6, 9, 3, 2), ("C2", 100, 20, 1, 9),
+         ("C2", 6, 2, 2, 4)]
+
+
+@pytest.mark.parametrize("name,N_RB,mcs,npdcch,sf", CASES)
+def test_noiseless_loop_hard_decisions(name, N_RB, mcs, npdcch, sf):
+    p = params(name, N_RB, mcs, npdcch, sf)
+    cfg = O.tx_cfg_from_params(p, sf)
+    rng = np.random.default_rng(N_RB + mcs)
+    pay = rng.integers(0, 256, p.payload_stride, dtype=np.uint8)
+    _, txF, es = O.tx_subframe(cfg, [pay], want_e=True)
+    fp = cfg.fp
+    Qm = 2 if mcs < 10 else 4 if mcs < 17 else 6
+    G = O.get_G(N_RB, 0, 1, 0, p.nb_rb, list(p.rb_alloc), Qm, 1, npdcch, sf)
+    llr, sh = O.rx_pdsch_siso(fp, txF[0], perfect_ce(fp), list(p.rb_alloc), Qm, npdcch, sf)
+    assert len(llr) == G and sh == 9                     # log2_approx(512^2) / 2
+    e = es[0][:G].astype(np.int32)
+    L = llr.reshape(-1, Qm).astype(np.int32)
+    B = e.reshape(-1, Qm)
+    # per component (re: bits 0, 2, 4; im: 1, 3, 5) the noiseless LLRs are a one-to-one function of
+    # the component's bits
+    for comp in (0, 1):
+        cols = list(range(comp, Qm, 2))
+        pat = {}
+        for bits, l in zip(map(tuple, B[:, cols]), map(tuple, L[:, cols])):
+            assert pat.setdefault(bits, l) == l, (comp, bits)
+        assert len(pat) == 2 ** len(cols) and len(set(pat.values())) == len(pat)
+    for q in range(Qm):                                  # bit 1 <-> negative LLR
+        assert np.array_equal(L[:, q] < 0, B[:, q] == 1), q
+    # unscrambling (dlsch_scrambling.c:116-131): c_init = rnti 2^14 + (Ns / 2) 2^9 + Nid, Ns = 2 sf
+    u = np.zeros(32 * (1 + G // 32), np.int16)
+    u[:G] = llr
+    O.dlsch_unscrambling(u, G, (p.rnti << 14) + (sf << 9) + fp.Nid_cell)
+    c = np.array(O_gold((p.rnti << 14) + (sf << 9) + fp.Nid_cell, G))
+    assert np.array_equal(u[:G], np.where(c == 1, llr, -llr.astype(np.int32)).astype(np.int16))
+
+
+def decode_tb(llr, G, TBS, Qm, C_ops=None, max_it=4):
+    """dlsch_decoding's per-block chain (dlsch_decoding.c:250-430) on unscrambled LLRs (positive =
+    bit 1): segmentation (36.212 5.1.2, spec_model.segment), lte_rate_matching_turbo_rx,
+    sub_block_deinterleaving_turbo, the 16-bit turbo decoder with CRC24B (C > 1) / CRC24A.
+    C_ops = (rate_match_rx(soft, K, G, C, r, Qm) -> (w, E), deinterleave(w, K) -> d,
+    decode(d, K, crc_type, F) -> (iterations, bytes)); the oracle's by default.
+    Returns the list of per-block (iterations, decoded bytes, expected K) and the TB bytes."""
+    import spec_model as S
+    rm, dei, dec = C_ops or (O.rate_match_rx, O.subblock_deinterleave,
+                             lambda d, K, ct, F: O.turbo_decode(d, K, max_it=max_it, crc_type=ct, F=F))
+    C_n = len(S.segment([0] * (TBS + 24))[0])
+    blocks, F = S.segment([0] * (TBS + 24))
+    soft = np.ascontiguousarray(llr[:G], dtype=np.int16)
+    off, res, bits = 0, [], []
+    for r, blk in enumerate(blocks):
+        K = len(blk)
+        w, E = rm(soft[off:], K, G, C_n, r, Qm)
+        off += E
+        it, out = dec(dei(w, K), K, 1 if C_n > 1 else 0, F if r == 0 else 0)
+        res.append((it, out))
+        b = np.unpackbits(out)[:K]
+        bits.append(b[(F if r == 0 else 0):K - (24 if C_n > 1 else 0)])
+    assert off == G
+    tb = np.packbits(np.concatenate(bits)[:TBS])
+    return res, tb
+
+
+def loop_llr(p, sf, pay):
+    """The oracle's transmit subframe -> IQ -> slot_fep (14 symbols) -> rx_pdsch_siso with dlsim's
+    perfect channel estimate -> dlsch_unscrambling.  Returns (unscrambled LLRs, G, Qm)."""
+    cfg = O.tx_cfg_from_params(p, sf)
+    fp = cfg.fp
+    txd, _, _ = O.tx_subframe(cfg, [pay])
+    spt, N = fp.samples_per_tti, fp.ofdm_symbol_size
+    frame = np.zeros(10 * spt + N, np.int32)
+    frame[sf * spt:(sf + 1) * spt] = txd[0]
+    rxF = np.zeros(20 * 7 * N + N, np.int32)
+    for Ns in (2 * sf, 2 * sf + 1):
+        for l in range(7):
+            assert O.slot_fep([frame], [rxF], fp, l, Ns) == 0
+    Qm = 2 if p.mcs[0] < 10 else 4 if p.mcs[0] < 17 else 6
+    llr, _ = O.rx_pdsch_siso(fp, rxF[:14 * N], perfect_ce(fp), list(p.rb_alloc), Qm, p.num_pdcch_symbols, sf)
+    G = len(llr)
+    u = np.zeros(32 * (1 + G // 32), np.int16)
+    u[:G] = llr
+    O.dlsch_unscrambling(u, G, (p.rnti << 14) + (sf << 9) + fp.Nid_cell)
+    return u[:G], G, Qm
+
+
+LOOP = [(100, 16, 1, 7), (100, 27, 2, 3), (50, 4, 3, 8), (50, 24, 1, 9), (100, 9, 2, 4), (100, 22, 3, 1)]
+
+
+@pytest.mark.parametrize("N_RB,mcs,npdcch,sf", LOOP)
+def test_loop_decodes_transport_block(N_RB, mcs, npdcch, sf):
+    """Closed loop on the oracle: every code block's CRC passes and the TB comes back.  Not in the
+    set, as the reference itself does not close the loop there: subframes 0 / 5 (even N_RB_DL: the
+    UE extracts the PBCH / sync REs as PDSCH, dlsch_demodulation.c:3218-3281, and only shortens
+    the LLR stream by adjust_G2) and 6 PRB with dlsim's perfect estimate (slot_fep aligns the
+    window start down to a multiple of 4, slot_fep.c:113-115, a 2-sample shift at a 10-sample
+    prefix that a real channel estimate absorbs but the constant (AMP, 0) does not)."""
+    p = params("C2", N_RB, mcs, npdcch, sf)
+    pay = np.random.default_rng(mcs + N_RB).integers(0, 256, p.payload_stride, dtype=np.uint8)
+    llr, G, Qm = loop_llr(p, sf, pay)
+    res, tb = decode_tb(llr, G, p.TBS[0], Qm)
+    assert all(it <= 4 for it, _ in res), [it for it, _ in res]
+    assert np.array_equal(tb, pay[:p.TBS[0] // 8])
+
+
+def O_gold(c_init, n):
+    import spec_model as S
+    return S.gold(c_init, n)
+
+
+def test_adjust_G2_matches_get_G():
+    """adjust_G2 per symbol sums to the PBCH / sync exclusions of get_G in subframes 0 and 5."""
+    for N_RB in (6, 50, 100):
+        fp = O.frame(N_RB)
+        ra = [0xFFFFFFFF] * 3 + [0xF]
+        for sf in (0, 5):
+            adj = sum(O.adjust_G2(fp, ra, sf, l) for l in range(14))
+            nre = O.get_G(N_RB, 0, 1, 0, N_RB, ra, 2, 1, 1, 7) // 2 - O.get_G(N_RB, 0, 1, 0, N_RB, ra, 2, 1, 1, sf) // 2
+            assert adj >= nre                        # get_G also drops the PBCH's RS-shared REs
+        assert all(O.adjust_G2(fp, ra, 7, l) == 0 for l in range(14))

@@ -6,8 +6,9 @@ bench and the GPU parity suite use (C1, C2, C3) and a bandwidth sweep 6 ... 100 
 subframes 0 (PBCH + sync exclusions), 5 (sync) and 7 (none).
 
 The model shares nothing with the oracle's code; its departures from the spec are the
-reference's, written as cited parameters: A6q filler bits encoded as 0, the int16 Q15 QAM tables
-with the wrapping 64-QAM outer level, floor halving with the sign after the floor in CDD, and
+reference's, written as cited parameters: A6q filler bits encoded as 0, the int Q15 QAM tables
+(the 64-QAM outer level 35393 exceeds int16 until the amp scaling; LTE_TRANSPORT/vars.h:72),
+floor halving with the sign after the floor in CDD, and
 the CDD sign reset per resource block (checked to coincide with the spec's global (-1)^i here:
 every RB contributes an even number of REs)."""
 import numpy as np
