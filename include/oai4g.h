@@ -261,6 +261,31 @@ size_t oai4g_rx_llr_stride(const oai4g_rx_config_t *cfg);
 int oai4g_rx_batch(oai4g_rx_config_t *cfg, int n_sf, const int32_t *d_rxdataF, const int32_t *d_dl_ch_estimates,
                    int16_t *d_llr, int unscramble, void *stream);
 
+/* lte_dl_channel_estimation (PHY/LTE_ESTIMATION/lte_dl_channel_estimation.c:37, decl
+ * LTE_ESTIMATION/defs.h; called by slot_fep.c:188 for the pilot symbols of every slot) with the
+ * reference's defaults high_speed_flag = 1 (dlsim.c:2057), eNB_offset 0, one RX antenna: the
+ * frequency interpolation of the conjugate-pilot products of port p (filt96_32.h filters) into row
+ * `symbol` of dl_ch_estimates (subcarrier i of RB rb at 5 + 12 rb + i), then the temporal
+ * interpolation of the rows between this pilot symbol and the previous one (symbol 0 closes rows
+ * 12 / 13 of the previous subframe's pilot 11).  rxdataF / dl_ch_estimates = [nsymb][N] host
+ * buffers of the subframe; N_RB_DL 6 / 50 / 100 (other even sizes: the reference's "not
+ * implemented" row of zeros; 15 / 25 PRB return -1).  The idft of the estimate into
+ * dl_ch_estimates_time (:704-738, the UE's timing tracker) is not produced.  Returns 0 / -1. */
+int oai4g_lte_dl_channel_estimation(const oai4g_frame_parms_t *frame_parms, const int32_t *rxdataF,
+                                    int32_t *dl_ch_estimates, uint8_t Ns, uint8_t p, uint8_t l, uint8_t symbol);
+/* The six interpolation filters of pilot offset k = (nu + nushift) % 6 as the estimator uses them
+ * (lte_dl_channel_estimation.c:105-180): fl, f2l2, f, f2, fr, f2r2 (filt96_32.h by formula). */
+void oai4g_chest_filters(uint8_t k, int16_t out[6][24]);
+/* Batched estimation of every symbol of n_sf consecutive subframes (subframe index first_subframe
+ * + i * subframe_step mod 10) in dlsim's order (dlsim.c:2907-2931): d_rxdataF = [n_sf][nsymb][N]
+ * followed by the symbol 0 of the subframe after the batch (N more words), d_est = [n_sf][nsymb][N]
+ * -- the rows rx_pdsch reads for each subframe (row 0 that subframe's own estimate). */
+typedef struct oai4g_chest_config oai4g_chest_config_t;
+oai4g_chest_config_t *oai4g_chest_config_create(const oai4g_frame_parms_t *frame_parms, uint8_t p,
+                                                uint8_t first_subframe, uint8_t subframe_step);
+void oai4g_chest_config_destroy(oai4g_chest_config_t *cfg);
+int oai4g_chest_batch(oai4g_chest_config_t *cfg, int n_sf, const int32_t *d_rxdataF, int32_t *d_est, void *stream);
+
 /* ---------------- synchronisation, broadcast and HARQ-indicator channels ---------------- */
 /* generate_pss (PHY/LTE_TRANSPORT/pss.c:50, decl LTE_TRANSPORT/proto.h): the Zadoff-Chu sequence
  * of root 25 / 29 / 34 (Nid_cell % 3, the Q15 table of PHY/LTE_REFSIG/primary_synch.h, here

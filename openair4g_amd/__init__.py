@@ -201,6 +201,14 @@ _SIGS = {
     "oai4g_rx_llr_stride": (ctypes.c_size_t, [ctypes.c_void_p]),
     "oai4g_rx_batch": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
                                       ctypes.c_int, ctypes.c_void_p]),
+    "oai4g_lte_dl_channel_estimation": (ctypes.c_int, [ctypes.POINTER(FrameParms), ctypes.c_void_p, ctypes.c_void_p,
+                                                       ctypes.c_uint8, ctypes.c_uint8, ctypes.c_uint8, ctypes.c_uint8]),
+    "oai4g_chest_filters": (None, [ctypes.c_uint8, ctypes.c_void_p]),
+    "oai4g_chest_config_create": (ctypes.c_void_p, [ctypes.POINTER(FrameParms), ctypes.c_uint8, ctypes.c_uint8,
+                                                    ctypes.c_uint8]),
+    "oai4g_chest_config_destroy": (None, [ctypes.c_void_p]),
+    "oai4g_chest_batch": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p,
+                                         ctypes.c_void_p]),
     "oai4g_dft": (ctypes.c_int, [ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int]),
     "oai4g_dft2048": (None, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int]),
     "oai4g_dft1024": (None, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int]),
@@ -459,6 +467,55 @@ def dlsch_unscrambling(fp, rnti, G, llr, q, Ns):
     init()
     lib().oai4g_dlsch_unscrambling(ctypes.byref(fp), 0, rnti, G, _ptr(llr), q, Ns)
     return llr
+
+
+def lte_dl_channel_estimation(fp, rxdataF, est, Ns, p, l, symbol):
+    """lte_dl_channel_estimation drop-in (high_speed_flag 1): rxdataF / est int32 [nsymb*N]; est in place."""
+    init()
+    rxdataF = np.ascontiguousarray(rxdataF, dtype=np.int32)
+    assert est.dtype == np.int32 and est.flags.c_contiguous
+    _check(lib().oai4g_lte_dl_channel_estimation(ctypes.byref(fp), _ptr(rxdataF), _ptr(est), Ns, p, l, symbol) == 0)
+    return est
+
+
+def chest_filters(k):
+    """The six filt96_32.h filters (fl, f2l2, f, f2, fr, f2r2) of pilot offset k, as the library builds them."""
+    out = np.zeros((6, 24), dtype=np.int16)
+    lib().oai4g_chest_filters(k, _ptr(out))
+    return out
+
+
+class ChestBatch:
+    """Device-resident batched channel estimation (oai4g_chest_batch) of n_sf consecutive subframes."""
+
+    def __init__(self, fp, n_sf, p=0, first_subframe=0, subframe_step=1):
+        init()
+        self.L = lib()
+        self.cfg = self.L.oai4g_chest_config_create(ctypes.byref(fp), p, first_subframe, subframe_step)
+        _check(bool(self.cfg))
+        self.fp, self.n_sf = fp, n_sf
+        self.n_grid = n_sf * fp.symbols_per_tti * fp.ofdm_symbol_size
+        self.d_rx = self.L.oai4g_dev_alloc((self.n_grid + fp.ofdm_symbol_size) * 4)
+        self.d_est = self.L.oai4g_dev_alloc(self.n_grid * 4)
+        _check(bool(self.d_rx) and bool(self.d_est))
+
+    def run(self, rxdataF, next_symbol0, d_rxdataF=None):
+        """rxdataF [n_sf][nsymb*N] and the N words of the following subframe's symbol 0."""
+        if d_rxdataF is None:
+            y = np.concatenate([np.ascontiguousarray(rxdataF, dtype=np.int32).ravel(),
+                                np.ascontiguousarray(next_symbol0, dtype=np.int32).ravel()])
+            assert y.size == self.n_grid + self.fp.ofdm_symbol_size
+            _check(self.L.oai4g_memcpy_h2d(self.d_rx, _ptr(y), y.nbytes) == 0)
+        _check(self.L.oai4g_chest_batch(self.cfg, self.n_sf, d_rxdataF or self.d_rx, self.d_est, None) == 0)
+        _check(self.L.oai4g_sync() == 0)
+        out = np.empty((self.n_sf, self.n_grid // self.n_sf), dtype=np.int32)
+        _check(self.L.oai4g_memcpy_d2h(_ptr(out), self.d_est, out.nbytes) == 0)
+        return out
+
+    def close(self):
+        self.L.oai4g_dev_free(self.d_rx)
+        self.L.oai4g_dev_free(self.d_est)
+        self.L.oai4g_chest_config_destroy(self.cfg)
 
 
 class RxBatch:

@@ -1,0 +1,196 @@
+/*
+ * gfx950 kernels for the UE's downlink channel estimation from the cell-specific reference
+ * signals:
+ *   lte_dl_channel_estimation   PHY/LTE_ESTIMATION/lte_dl_channel_estimation.c:37-336 (6 / 50 / 100
+ *                               PRB interpolator), 629-701 (temporal interpolation with
+ *                               high_speed_flag = 1, dlsim.c:2057)
+ *   lte_dl_cell_spec_rx         PHY/LTE_REFSIG/lte_dl_cell_spec.c:205-260
+ *   multadd_real_vector_complex_scalar / multadd_complex_vector_real_scalar  PHY/TOOLS/cmult_sv.c:55-122
+ *
+ * The reference walks the pilots of a symbol left to right and saturating-adds each pilot's
+ * 24-tap filter response into the estimate row (adds_epi16), so an estimate entry is the ordered
+ * saturating sum of the <= 4 pilots whose windows cover it.  Here one thread owns one subcarrier
+ * column of a subframe: a workgroup first computes the conjugate-pilot products of every pilot
+ * its 256 columns see (5 pilot symbols: 0, 4, 7, 11 and the next subframe's symbol 0) into LDS,
+ * then each thread sums its column's covering pilots in ascending pilot order (the reference's
+ * order, so the saturation points agree), applies the temporal interpolation of every row and
+ * writes the subframe's 14 estimate rows once — coalesced, no read-modify-write of the estimate
+ * buffer.  HBM traffic per subframe = 14 N words written + the pilot REs read.
+ */
+#include "oai4g_internal.h"
+
+namespace {
+
+constexpr uint32_t CE_WG = 256;
+constexpr uint32_t CE_MAXP = 64;   /* pilots a 256-column window can see: 2 (ceil(283 / 12) + 1) = 50 */
+
+__device__ __forceinline__ int16_t ce_sat16(int32_t v) { return (int16_t)max(-32768, min(32767, v)); }
+
+/* mulhi_epi16 then slli_epi16 by s (the shift wraps in 16 bits) */
+__device__ __forceinline__ int16_t ce_mulhi_shl(int16_t a, int16_t b, uint32_t s)
+{
+  return (int16_t)(uint16_t)((uint32_t)(((int32_t)a * b) >> 16) << s);
+}
+
+/* conj(pilot m) * rx >> 15 of one pilot symbol (lte_dl_channel_estimation.c:214-215) */
+__device__ uint32_t ce_pilot_ch(const chest_dev_t *__restrict__ c, const int32_t *__restrict__ row, uint32_t Ns,
+                                uint32_t l01, uint32_t m)
+{
+  const uint32_t k = c->k[l01], N_RB = c->N_RB, mp = 110 - N_RB + m;
+  const uint32_t idx = (c->gold[Ns][l01][mp >> 4] >> (2 * (mp & 15))) & 3u;
+  /* lte_dl_cell_spec_rx's conjugated QPSK: (a,-a), (-a,-a), (a,a), (-a,a), a = ONE_OVER_SQRT2_Q15 */
+  const int32_t pr = (idx & 1u) ? -23170 : 23170, pi = idx < 2 ? -23170 : 23170;
+  const uint32_t bin = m < N_RB ? c->fco + k + 6 * m : 1 + k + 6 * (m - N_RB);
+  const uint32_t w = (uint32_t)row[bin];
+  const int32_t rr = (int16_t)w, ri = (int16_t)(w >> 16);
+  const int16_t chr = (int16_t)((pr * rr - pi * ri) >> 15), chi = (int16_t)((pr * ri + pi * rr) >> 15);
+  return (uint32_t)(uint16_t)chr | ((uint32_t)(uint16_t)chi << 16);
+}
+
+/* first pair index whose windows [12 q, 12 q + 28) can cover column j */
+__device__ __forceinline__ uint32_t ce_qlo(uint32_t j) { return j >= 27 ? (j - 16) / 12 : 0; }
+
+/* estimate entry j of one pilot symbol: ordered saturating sum over the covering pilots */
+__device__ uint32_t ce_column(uint32_t N_RB, const int16_t (*__restrict__ f)[24], const uint32_t *__restrict__ chl,
+                              uint32_t m_base, uint32_t j)
+{
+  int32_t ar = 0, ai = 0;
+  const uint32_t q_hi = min(N_RB - 1, j / 12);
+  for (uint32_t q = ce_qlo(j); q <= q_hi; q++)
+    for (uint32_t h = 0; h < 2; h++) {
+      const uint32_t m = 2 * q + h, s = 12 * q + 4 * h;
+      if (j < s || j - s >= 24) continue;
+      const uint32_t kind = m == 0 ? 0 : m == 1 ? 1 : m == 2 * N_RB - 2 ? 4 : m == 2 * N_RB - 1 ? 5 : 2 + h;
+      const int16_t tap = f[kind][j - s];
+      if (!tap) continue;                                   /* adds of 0: exact to skip */
+      const uint32_t v = chl[m - m_base];
+      ar = ce_sat16(ar + ce_mulhi_shl((int16_t)v, tap, 2));
+      ai = ce_sat16(ai + ce_mulhi_shl((int16_t)(v >> 16), tap, 2));
+    }
+  return (uint32_t)(uint16_t)ar | ((uint32_t)(uint16_t)ai << 16);
+}
+
+/* one interpolated entry: mulhi(a, wa) << 1, then adds mulhi(b, wb) << 1 (cmult_sv.c:55-80) */
+__device__ __forceinline__ int32_t ce_ip(uint32_t a, int16_t wa, uint32_t b, int16_t wb)
+{
+  const int16_t r = ce_sat16((int32_t)ce_mulhi_shl((int16_t)a, wa, 1) + ce_mulhi_shl((int16_t)b, wb, 1));
+  const int16_t i = ce_sat16((int32_t)ce_mulhi_shl((int16_t)(a >> 16), wa, 1) + ce_mulhi_shl((int16_t)(b >> 16), wb, 1));
+  return (int32_t)((uint32_t)(uint16_t)r | ((uint32_t)(uint16_t)i << 16));
+}
+
+/* the temporal interpolation that follows the estimate `cur` of pilot symbol `symbol`, with `prev`
+ * the estimate of the preceding pilot symbol (lte_dl_channel_estimation.c:639-698) */
+__device__ __forceinline__ void ce_interp(int32_t *__restrict__ E, uint32_t N, uint32_t Ncp, uint32_t symbol,
+                                          uint32_t prev, uint32_t cur)
+{
+  const uint32_t p1 = Ncp ? 3 : 4, p2 = Ncp ? 6 : 7, p3 = Ncp ? 9 : 11;
+  if (symbol == 0) {
+    E[(p3 + 1) * N] = ce_ip(prev, 21845, cur, 10923);
+    E[(p3 + 2) * N] = ce_ip(prev, 10923, cur, 21845);
+  } else if (symbol == p2) {
+    E[(p1 + 1) * N] = ce_ip(prev, 21845, cur, 10923);
+    E[(p1 + 2) * N] = ce_ip(prev, 10923, cur, 21845);
+  } else {                                                   /* pilot1 (from row 0) or pilot3 (from pilot2) */
+    const uint32_t r0 = symbol == p1 ? 1 : p2 + 1;
+    if (Ncp == 0) {
+      E[r0 * N] = ce_ip(prev, 24576, cur, 8192);
+      E[(r0 + 1) * N] = ce_ip(prev, 16384, cur, 16384);
+      E[(r0 + 2) * N] = ce_ip(prev, 8192, cur, 24576);
+    } else {                                                 /* the reference's 1/3, 2/3 weights, as written */
+      E[r0 * N] = ce_ip(prev, 10923, cur, 21845);
+      E[(r0 + 1) * N] = ce_ip(prev, 21845, cur, 10923);
+    }
+  }
+}
+
+/* pilot index range a workgroup's columns [j0, j0 + 256) need */
+__device__ __forceinline__ void ce_window(uint32_t N_RB, uint32_t j0, uint32_t j1, uint32_t &m_base, uint32_t &n_p)
+{
+  const uint32_t q_lo = ce_qlo(j0), q_hi = min(N_RB - 1, (j1 - 1) / 12);
+  m_base = 2 * q_lo;
+  n_p = q_hi >= q_lo ? 2 * (q_hi - q_lo + 1) : 0;
+}
+
+}  // namespace
+
+/* batch: grid (ceil(N / 256), n_sf); rxF = n_sf subframes of nsymb x N words followed by the
+ * symbol 0 of the subframe after the batch; est = n_sf x nsymb x N */
+__global__ void __launch_bounds__(CE_WG) k_chest(const chest_dev_t *__restrict__ c, const int32_t *__restrict__ rxF,
+                                                 int32_t *__restrict__ est)
+{
+  __shared__ uint32_t chl[5][CE_MAXP];
+  __shared__ int16_t flt[2][6][24];
+  const uint32_t sf = blockIdx.y, N = c->N, nsymb = c->nsymb, Ncp = c->Ncp, N_RB = c->N_RB;
+  const uint32_t sfi = (c->first_sf + sf * c->sf_step) % 10;
+  const uint32_t p1 = Ncp ? 3 : 4, p2 = Ncp ? 6 : 7, p3 = Ncp ? 9 : 11;
+  const uint32_t j0 = blockIdx.x * CE_WG, j1 = min(N, j0 + CE_WG);
+  uint32_t m_base, n_p;
+  ce_window(N_RB, j0, j1, m_base, n_p);
+  for (uint32_t i = threadIdx.x; i < 2 * 6 * 24; i += CE_WG) (&flt[0][0][0])[i] = (&c->filt[0][0][0])[i];
+  const int32_t *base = rxF + (size_t)sf * nsymb * N;
+  if (c->branch)
+    for (uint32_t i = threadIdx.x; i < 5 * n_p; i += CE_WG) {
+      const uint32_t in = i / n_p, m = m_base + i % n_p;
+      const uint32_t sym = in == 0 ? 0 : in == 1 ? p1 : in == 2 ? p2 : in == 3 ? p3 : nsymb;  /* nsymb: next sf */
+      const uint32_t Ns = in < 2 ? 2 * sfi : in < 4 ? 2 * sfi + 1 : (2 * sfi + 2) % 20;
+      chl[in][i % n_p] = ce_pilot_ch(c, base + (size_t)sym * N, Ns, in & 1u, m);
+    }
+  __syncthreads();
+  const uint32_t j = j0 + threadIdx.x;
+  if (j >= N) return;
+  uint32_t P[5] = {0, 0, 0, 0, 0};
+  if (c->branch)
+    for (uint32_t in = 0; in < 5; in++) P[in] = ce_column(N_RB, flt[in & 1u], chl[in], m_base, j);
+  int32_t *E = est + (size_t)sf * nsymb * N + j;
+  E[0] = (int32_t)P[0];
+  E[p1 * N] = (int32_t)P[1];
+  E[p2 * N] = (int32_t)P[2];
+  E[p3 * N] = (int32_t)P[3];
+  ce_interp(E, N, Ncp, p1, P[0], P[1]);
+  ce_interp(E, N, Ncp, p2, P[1], P[2]);
+  ce_interp(E, N, Ncp, p3, P[2], P[3]);
+  ce_interp(E, N, Ncp, 0, P[3], P[4]);
+}
+
+/* one call of lte_dl_channel_estimation (drop-in): row `symbol` from the pilot symbol rxF_sym,
+ * then the interpolation of the rows it closes, reading the previous pilot row from est */
+__global__ void __launch_bounds__(CE_WG) k_chest_symbol(const chest_dev_t *__restrict__ c,
+                                                        const int32_t *__restrict__ rxF_sym, int32_t *__restrict__ est,
+                                                        uint32_t Ns, uint32_t l01, uint32_t symbol)
+{
+  __shared__ uint32_t chl[CE_MAXP];
+  __shared__ int16_t flt[6][24];
+  const uint32_t N = c->N, Ncp = c->Ncp, N_RB = c->N_RB;
+  const uint32_t p1 = Ncp ? 3 : 4, p2 = Ncp ? 6 : 7, p3 = Ncp ? 9 : 11;
+  const uint32_t j0 = blockIdx.x * CE_WG, j1 = min(N, j0 + CE_WG);
+  uint32_t m_base, n_p;
+  ce_window(N_RB, j0, j1, m_base, n_p);
+  for (uint32_t i = threadIdx.x; i < 6 * 24; i += CE_WG) (&flt[0][0])[i] = (&c->filt[l01][0][0])[i];
+  if (c->branch)
+    for (uint32_t i = threadIdx.x; i < n_p; i += CE_WG) chl[i] = ce_pilot_ch(c, rxF_sym, Ns, l01, m_base + i);
+  __syncthreads();
+  const uint32_t j = j0 + threadIdx.x;
+  if (j >= N) return;
+  const uint32_t cur = c->branch ? ce_column(N_RB, flt, chl, m_base, j) : 0u;
+  int32_t *E = est + j;
+  const uint32_t prev_row = symbol == 0 ? p3 : symbol == p1 ? 0 : symbol == p2 ? p1 : p2;
+  const uint32_t prev = (uint32_t)E[prev_row * N];
+  E[symbol * N] = (int32_t)cur;
+  ce_interp(E, N, Ncp, symbol, prev, cur);
+}
+
+hipError_t oai4g_launch_chest(const chest_dev_t *d_cfg, const chest_dev_t *h_cfg, int n_sf, const int32_t *d_rxF,
+                              int32_t *d_est, hipStream_t s)
+{
+  if (n_sf <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_chest, dim3((h_cfg->N + CE_WG - 1) / CE_WG, n_sf), dim3(CE_WG), 0, s, d_cfg, d_rxF, d_est);
+  return hipGetLastError();
+}
+
+hipError_t oai4g_launch_chest_symbol(const chest_dev_t *d_cfg, const chest_dev_t *h_cfg, const int32_t *d_rxF_sym,
+                                     int32_t *d_est, int Ns, int l, int symbol, hipStream_t s)
+{
+  hipLaunchKernelGGL(k_chest_symbol, dim3((h_cfg->N + CE_WG - 1) / CE_WG), dim3(CE_WG), 0, s, d_cfg, d_rxF_sym, d_est,
+                     (uint32_t)Ns, (uint32_t)(l == 0 ? 0 : 1), (uint32_t)symbol);
+  return hipGetLastError();
+}

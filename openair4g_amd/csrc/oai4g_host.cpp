@@ -2922,11 +2922,14 @@ extern "C" int oai4g_rx_pdsch_siso(const oai4g_frame_parms_t *fp, const int32_t 
 }
 
 /* dlsch_unscrambling (dlsch_scrambling.c:99-137): llr[k] *= 2 c(k) - 1 for k < 32 (1 + G / 32),
- * c_init = rnti 2^14 + q 2^13 + (Ns / 2) 2^9 + Nid_cell (mbsfn_flag = 0); host buffer */
+ * c_init = rnti 2^14 + q 2^13 + (Ns / 2) 2^9 + Nid_cell (mbsfn_flag = 0), on a host buffer: the
+ * sequence words are set up here, the sign flips run on the GPU (k_rx_unscramble) */
 extern "C" void oai4g_dlsch_unscrambling(const oai4g_frame_parms_t *fp, int mbsfn_flag, uint16_t rnti, int G,
                                          int16_t *llr, uint8_t q, uint8_t Ns)
 {
   (void)mbsfn_flag;
+  NEED_INIT();
+  if (G < 0) return;
   uint32_t x1 = 1u + (1u << 31), x2 = ((uint32_t)rnti << 14) + ((uint32_t)q << 13) + ((uint32_t)(Ns >> 1) << 9) + fp->Nid_cell;
   x2 = x2 ^ ((x2 ^ (x2 >> 1) ^ (x2 >> 2) ^ (x2 >> 3)) << 31);
   auto step = [&]() {
@@ -2936,10 +2939,144 @@ extern "C" void oai4g_dlsch_unscrambling(const oai4g_frame_parms_t *fp, int mbsf
     x2 = x2 ^ (x2 << 31) ^ (x2 << 30) ^ (x2 << 29) ^ (x2 << 28);
   };
   for (int n = 1; n < 50; n++) step();
-  int k = 0;
-  for (int i = 0; i < 1 + (G >> 5); i++) {
+  const int words = 1 + (G >> 5);
+  std::vector<uint32_t> c(words);
+  for (int i = 0; i < words; i++) {
     step();
-    const uint32_t s = x1 ^ x2;
-    for (int j = 0; j < 32; j++, k++) llr[k] = (int16_t)(((2 * ((s >> j) & 1)) - 1) * llr[k]);
+    c[i] = x1 ^ x2;
   }
+  const size_t lb = (size_t)words * 64, lbs = (lb + 255) & ~(size_t)255;
+  uint8_t *buf = scratch(lbs + (size_t)words * 4);
+  if (!buf) return;
+  int16_t *dl = (int16_t *)buf;
+  uint32_t *dc = (uint32_t *)(buf + lbs);
+  if (hipMemcpyAsync(dl, llr, lb, hipMemcpyHostToDevice, g_scr.s) != hipSuccess ||
+      hipMemcpyAsync(dc, c.data(), (size_t)words * 4, hipMemcpyHostToDevice, g_scr.s) != hipSuccess ||
+      oai4g_launch_unscramble(dl, dc, words * 32, g_scr.s) != hipSuccess ||
+      hipMemcpyAsync(llr, dl, lb, hipMemcpyDeviceToHost, g_scr.s) != hipSuccess ||
+      hipStreamSynchronize(g_scr.s) != hipSuccess)
+    set_err("dlsch_unscrambling: HIP error");
+}
+
+/* ------------------------------------------------------------------------------------------
+ * Downlink channel estimation (lte_dl_channel_estimation.c:37-701 with high_speed_flag = 1;
+ * one RX antenna; the 6 / 50 / 100 PRB interpolator).
+ * ---------------------------------------------------------------------------------------- */
+/* filt96_32.h by formula: ramp levels floor(16384 v / 6); the six filters of pilot offset k
+ * (lte_dl_channel_estimation.c:105-180) as fl, f2l2, f, f2, fr, f2r2 */
+extern "C" void oai4g_chest_filters(uint8_t k, int16_t out[6][24])
+{
+  auto lv = [](int v) { return (int16_t)((16384 * v) / 6); };
+  const int s1 = k, s2 = k + 2;
+  for (int t = 0; t < 24; t++) {
+    const int u1 = t - s1, u2 = t - s2;
+    const int16_t tri1 = (u1 >= 0 && u1 <= 10) ? lv(6 - std::abs(u1 - 5)) : 0;
+    const int16_t tri2 = (u2 >= 0 && u2 <= 10) ? lv(6 - std::abs(u2 - 5)) : 0;
+    out[2][t] = tri1;                                                           /* filt24_k */
+    out[3][t] = tri2;                                                           /* filt24_(k+2) */
+    out[4][t] = (u1 >= 11 && u1 <= 16) ? (int16_t)-lv(u1 - 11) : tri1;          /* filt24_kr2 */
+    out[5][t] = (u2 >= 0 && u2 <= 10) ? lv(u2 + 1) : 0;                         /* filt24_(k+2)r */
+    if (k == 0) {                                                               /* filt24_0, filt24_2 */
+      out[0][t] = tri1;
+      out[1][t] = tri2;
+    } else {
+      out[0][t] = (u1 >= 0 && u1 <= 10 && !(k == 3 && (t == 3 || t == 4))) ? lv(11 - u1) : 0;   /* filt24_kl */
+      out[1][t] = (u2 >= -6 && u2 <= -1) ? (int16_t)(k == 3 && t == 0 ? 0 : -lv(-u2 - 1)) : tri2; /* _(k+2)l2 */
+    }
+  }
+}
+
+struct oai4g_chest_config {
+  chest_dev_t h;
+  chest_dev_t *d = nullptr;
+};
+
+static int chest_fill(const oai4g_frame_parms_t *fp, uint8_t p, chest_dev_t &h)
+{
+  const uint32_t N_RB = fp->N_RB_DL;
+  if (p > 1) { set_err("lte_dl_channel_estimation: p %d (ports 0 / 1 only)", p); return -1; }
+  if (N_RB == 15 || N_RB == 25) {
+    set_err("lte_dl_channel_estimation: the odd-N_RB_DL interpolators (15 / 25 PRB) are not built");
+    return -1;
+  }
+  memset(&h, 0, sizeof(h));
+  h.N = fp->ofdm_symbol_size;
+  h.N_RB = N_RB;
+  h.nsymb = fp->Ncp == 0 ? 14 : 12;
+  h.Ncp = fp->Ncp;
+  h.fco = fp->first_carrier_offset;
+  h.p = p;
+  h.branch = (N_RB == 6 || N_RB == 50 || N_RB == 100) ? 1 : 0;   /* others: "not implemented", rows of 0 */
+  for (int l01 = 0; l01 < 2; l01++) {
+    const uint32_t nu = p == 0 ? (l01 ? 3 : 0) : (l01 ? 0 : 3);
+    h.k[l01] = (nu + fp->nushift) % 6;
+    oai4g_chest_filters((uint8_t)h.k[l01], h.filt[l01]);
+  }
+  lte_gold_table_h(fp, h.gold);
+  return 0;
+}
+
+extern "C" oai4g_chest_config_t *oai4g_chest_config_create(const oai4g_frame_parms_t *fp, uint8_t p,
+                                                           uint8_t first_subframe, uint8_t subframe_step)
+{
+  NEED_INIT(nullptr);
+  auto *cfg = new oai4g_chest_config();
+  if (chest_fill(fp, p, cfg->h) != 0) { delete cfg; return nullptr; }
+  cfg->h.first_sf = first_subframe % 10;
+  cfg->h.sf_step = subframe_step;
+  if (hipMalloc(&cfg->d, sizeof(chest_dev_t)) != hipSuccess ||
+      hipMemcpy(cfg->d, &cfg->h, sizeof(chest_dev_t), hipMemcpyHostToDevice) != hipSuccess) {
+    set_err("chest_config: device allocation / upload failed");
+    oai4g_chest_config_destroy(cfg);
+    return nullptr;
+  }
+  return cfg;
+}
+
+extern "C" void oai4g_chest_config_destroy(oai4g_chest_config_t *cfg)
+{
+  if (!cfg) return;
+  if (cfg->d) hipFree(cfg->d);
+  delete cfg;
+}
+
+extern "C" int oai4g_chest_batch(oai4g_chest_config_t *cfg, int n_sf, const int32_t *d_rxdataF, int32_t *d_est,
+                                 void *stream)
+{
+  NEED_INIT(-1);
+  if (!cfg || n_sf < 0) { set_err("chest_batch: bad arguments"); return -1; }
+  HCK(oai4g_launch_chest(cfg->d, &cfg->h, n_sf, d_rxdataF, d_est, (hipStream_t)stream), -1);
+  return 0;
+}
+
+/* lte_dl_channel_estimation drop-in on host buffers: rxdataF / dl_ch_estimates = [nsymb][N] of the
+ * subframe (the UE's rxdataF and dl_ch_estimates[eNB_offset 0][(p << 1) + 0]); Ns, p, l, symbol as
+ * slot_fep passes them (slot_fep.c:188-192) */
+extern "C" int oai4g_lte_dl_channel_estimation(const oai4g_frame_parms_t *fp, const int32_t *rxdataF,
+                                               int32_t *dl_ch_estimates, uint8_t Ns, uint8_t p, uint8_t l,
+                                               uint8_t symbol)
+{
+  NEED_INIT(-1);
+  const uint32_t nsymb = fp->Ncp == 0 ? 14 : 12, p1 = fp->Ncp ? 3 : 4, p2 = fp->Ncp ? 6 : 7, p3 = fp->Ncp ? 9 : 11;
+  if (Ns >= 20 || (symbol != 0 && symbol != p1 && symbol != p2 && symbol != p3)) {
+    set_err("lte_dl_channel_estimation: Ns %d / symbol %d is not a pilot symbol", Ns, symbol);
+    return -1;
+  }
+  chest_dev_t h;
+  if (chest_fill(fp, p, h) != 0) return -1;
+  const size_t N = fp->ofdm_symbol_size, eb = (size_t)nsymb * N * 4, cs = (sizeof(chest_dev_t) + 255) & ~(size_t)255;
+  uint8_t *buf = scratch(cs + eb + N * 4);
+  if (!buf) return -1;
+  chest_dev_t *dc = (chest_dev_t *)buf;
+  int32_t *de = (int32_t *)(buf + cs), *dr = (int32_t *)(buf + cs + eb);
+  if (hipMemcpyAsync(dc, &h, sizeof(h), hipMemcpyHostToDevice, g_scr.s) != hipSuccess ||
+      hipMemcpyAsync(de, dl_ch_estimates, eb, hipMemcpyHostToDevice, g_scr.s) != hipSuccess ||
+      hipMemcpyAsync(dr, rxdataF + (size_t)symbol * N, N * 4, hipMemcpyHostToDevice, g_scr.s) != hipSuccess ||
+      oai4g_launch_chest_symbol(dc, &h, dr, de, Ns, l, symbol, g_scr.s) != hipSuccess ||
+      hipMemcpyAsync(dl_ch_estimates, de, eb, hipMemcpyDeviceToHost, g_scr.s) != hipSuccess ||
+      hipStreamSynchronize(g_scr.s) != hipSuccess) {
+    set_err("lte_dl_channel_estimation: HIP error");
+    return -1;
+  }
+  return 0;
 }

@@ -287,6 +287,21 @@ hipError_t oai4g_launch_modulate_bytes(const cfg_dev_t *d_cfg, const cfg_dev_t *
                                        const uint8_t *d_e0, const uint8_t *d_e1, int32_t *d_grid, hipStream_t s);
 
 /* UE PDSCH demodulation (oai4g_rx.hip): TM1, one receive antenna, even N_RB_DL */
+/* downlink channel estimation (lte_dl_channel_estimation, high_speed_flag = 1, one RX antenna) */
+struct chest_dev_t {
+  uint32_t N, N_RB, nsymb, Ncp, fco, p;
+  uint32_t first_sf, sf_step;
+  uint32_t branch;                /* 1: the 6 / 50 / 100 PRB interpolator; 0: "not implemented" (rows of 0) */
+  uint32_t k[2];                  /* pilot offset (nu + nushift) % 6 for pilot symbols l = 0 / l > 0 */
+  int16_t filt[2][6][24];         /* fl, f2l2, f, f2, fr, f2r2 (filt96_32.h) for k[0] / k[1] */
+  uint32_t gold[20][2][14];       /* lte_gold_table */
+};
+hipError_t oai4g_launch_unscramble(int16_t *d_llr, const uint32_t *d_c, int n, hipStream_t s);
+hipError_t oai4g_launch_chest(const chest_dev_t *d_cfg, const chest_dev_t *h_cfg, int n_sf, const int32_t *d_rxF,
+                              int32_t *d_est, hipStream_t s);
+hipError_t oai4g_launch_chest_symbol(const chest_dev_t *d_cfg, const chest_dev_t *h_cfg, const int32_t *d_rxF_sym,
+                                     int32_t *d_est, int Ns, int l, int symbol, hipStream_t s);
+
 struct rx_dev_t {
   uint32_t N, nsymb, Qm, npdcch;
   uint32_t llr_stride;            /* LLRs per batch element */

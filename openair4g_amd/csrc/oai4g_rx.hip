@@ -86,6 +86,21 @@ __global__ void __launch_bounds__(256) k_rx_llr(const rx_dev_t *__restrict__ c, 
   }
 }
 
+/* dlsch_unscrambling drop-in: llr[k] *= 2 c(k) - 1 (int16), c = the words of the Gold sequence */
+__global__ void __launch_bounds__(256) k_rx_unscramble(int16_t *__restrict__ llr, const uint32_t *__restrict__ c,
+                                                       uint32_t n)
+{
+  for (uint32_t k = blockIdx.x * blockDim.x + threadIdx.x; k < n; k += gridDim.x * blockDim.x)
+    if (!((c[k >> 5] >> (k & 31)) & 1u)) llr[k] = (int16_t)(-(int32_t)llr[k]);
+}
+
+hipError_t oai4g_launch_unscramble(int16_t *d_llr, const uint32_t *d_c, int n, hipStream_t s)
+{
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_rx_unscramble, dim3(min((n + 255) / 256, 1024)), dim3(256), 0, s, d_llr, d_c, (uint32_t)n);
+  return hipGetLastError();
+}
+
 hipError_t oai4g_launch_rx(const rx_dev_t *d_cfg, const rx_dev_t *h_cfg, int n_sf, const int32_t *d_rxF,
                            const int32_t *d_ch, int16_t *d_llr, uint8_t *d_shift, int unscramble, hipStream_t s)
 {

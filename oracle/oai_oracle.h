@@ -230,4 +230,9 @@ int orc_tx_subframe_dci(const orc_tx_cfg_t *cfg, uint8_t *payload[2], int32_t **
 #ifdef __cplusplus
 }
 #endif
+/* ---- downlink channel estimation (LTE_ESTIMATION/lte_dl_channel_estimation.c:37-701, high_speed_flag 1) ---- */
+void orc_chest_filters(uint8_t k, int16_t out[6][24]);
+int  orc_lte_dl_channel_estimation(const orc_frame_t *fp, const uint32_t gold[20][2][14], const int32_t *rxdataF,
+                                   int32_t *dl_ch_estimates, uint8_t Ns, uint8_t p, uint8_t l, uint8_t symbol);
+
 #endif

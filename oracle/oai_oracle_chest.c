@@ -1,0 +1,174 @@
+/*
+ * TEST INFRASTRUCTURE ONLY — CPU oracle of the UE's downlink channel estimation from the
+ * cell-specific reference signals, a plain-C restatement of the reference's
+ * algorithm loop for loop; never linked into the product library.
+ *
+ *   lte_dl_channel_estimation  PHY/LTE_ESTIMATION/lte_dl_channel_estimation.c:37-336, 629-701
+ *                              (N_RB_DL 6 / 50 / 100 branch; high_speed_flag = 1, dlsim.c:2057 and
+ *                              lte_init.c:1212; perfect_ce = 0; eNB_offset 0; one RX antenna).
+ *                              The final idft of the estimate into dl_ch_estimates_time (:704-738,
+ *                              consumed only by the UE's timing tracker) is not restated.
+ *   lte_dl_cell_spec_rx        PHY/LTE_REFSIG/lte_dl_cell_spec.c:205-260 (conjugated QPSK pilots,
+ *                              amplitude ONE_OVER_SQRT2_Q15)
+ *   multadd_real_vector_complex_scalar  PHY/TOOLS/cmult_sv.c:81-122 (mulhi << 2, adds)
+ *   multadd_complex_vector_real_scalar  cmult_sv.c:55-80 (mulhi << 1, optional adds)
+ *   filt24_* interpolation filters      PHY/LTE_ESTIMATION/filt96_32.h, restated by formula in
+ *                              orc_chest_filters (tests/test_chest_cpu.py checks them entry by
+ *                              entry against the header when the reference tree is present).
+ *
+ * dl_ch_estimates holds one row of ofdm_symbol_size words per OFDM symbol of the subframe
+ * (high_speed_flag = 1: ch_offset = symbol * ofdm_symbol_size), subcarrier i of RB rb at
+ * 5 + 12 rb + i, the layout dlsch_extract_rbs_single reads.
+ */
+#include <stdlib.h>
+#include <string.h>
+
+#include "oai_oracle.h"
+
+static int16_t sat16(int32_t v) { return (int16_t)(v > 32767 ? 32767 : (v < -32768 ? -32768 : v)); }
+
+/* floor(16384 v / 6): the ramp levels of every filt24 table */
+static int16_t lvl(int v) { return (int16_t)((16384 * v) / 6); }
+
+/* the six filters one pilot symbol uses, for pilot offset k = (nu + nushift) % 6
+ * (lte_dl_channel_estimation.c:105-180): [0] fl (first pilot), [1] f2l2 (second pilot),
+ * [2] f (even pilots), [3] f2 (odd pilots), [4] fr (last-but-one pilot), [5] f2r2 (last pilot).
+ * Shapes (s = filter shift, u = tap - s):
+ *   filt24_s   : triangle lvl(6 - |u - 5|) on u in [0, 10]
+ *   filt24_sl  : left-edge ramp lvl(11 - u) on [0, 10]      (filt24_3l: taps 3, 4 zeroed)
+ *   filt24_sl2 : triangle plus -lvl(-u - 1) on u in [-6, -1] (filt24_5l2: tap 0 zeroed)
+ *   filt24_sr  : right-edge ramp lvl(u + 1) on [0, 10]
+ *   filt24_sr2 : triangle plus -lvl(u - 11) on u in [11, 16] */
+void orc_chest_filters(uint8_t k, int16_t out[6][24])
+{
+  memset(out, 0, sizeof(int16_t) * 6 * 24);
+  const int s1 = k, s2 = k + 2;
+  for (int t = 0; t < 24; t++) {
+    const int u1 = t - s1, u2 = t - s2;
+    const int16_t tri1 = (u1 >= 0 && u1 <= 10) ? lvl(6 - abs(u1 - 5)) : 0;
+    const int16_t tri2 = (u2 >= 0 && u2 <= 10) ? lvl(6 - abs(u2 - 5)) : 0;
+    out[2][t] = tri1;
+    out[3][t] = tri2;
+    if (k == 0) {                                          /* :106-119 */
+      out[0][t] = tri1;
+      out[1][t] = tri2;
+      out[4][t] = (u1 >= 11 && u1 <= 16) ? (int16_t)-lvl(u1 - 11) : tri1;     /* filt24_0r2 */
+      out[5][t] = (u2 >= 0 && u2 <= 10) ? lvl(u2 + 1) : 0;                     /* filt24_2r */
+    } else {
+      out[0][t] = (u1 >= 0 && u1 <= 10) ? lvl(11 - u1) : 0;                    /* filt24_kl */
+      if (k == 3 && (t == 3 || t == 4)) out[0][t] = 0;
+      out[1][t] = (u2 >= -6 && u2 <= -1) ? (int16_t)-lvl(-u2 - 1) : tri2;      /* filt24_(k+2)l2 */
+      if (k == 3 && t == 0) out[1][t] = 0;
+      out[4][t] = (u1 >= 11 && u1 <= 16) ? (int16_t)-lvl(u1 - 11) : tri1;     /* filt24_kr2 */
+      out[5][t] = (u2 >= 0 && u2 <= 10) ? lvl(u2 + 1) : 0;                     /* filt24_(k+2)r */
+    }
+  }
+}
+
+/* multadd_complex_vector_real_scalar over one row of N complex entries */
+static void multadd_row(const int32_t *x, int16_t alpha, int32_t *y, int zero_flag, int N)
+{
+  for (int n = 0; n < N; n++) {
+    int16_t v[2], o[2];
+    memcpy(v, &x[n], 4);
+    memcpy(o, &y[n], 4);
+    for (int c = 0; c < 2; c++) {
+      const int16_t m = (int16_t)(uint16_t)((uint32_t)(((int32_t)v[c] * alpha) >> 16) << 1);
+      o[c] = zero_flag ? m : sat16((int32_t)o[c] + m);
+    }
+    memcpy(&y[n], o, 4);
+  }
+}
+
+int orc_lte_dl_channel_estimation(const orc_frame_t *fp, const uint32_t gold[20][2][14], const int32_t *rxdataF,
+                                  int32_t *dl_ch_estimates, uint8_t Ns, uint8_t p, uint8_t l, uint8_t symbol)
+{
+  const int N = fp->ofdm_symbol_size, N_RB = fp->N_RB_DL;
+  const int pilot1 = fp->Ncp == 0 ? 4 : 3, pilot2 = fp->Ncp == 0 ? 7 : 6, pilot3 = fp->Ncp == 0 ? 11 : 9;
+  int nu;
+  if (p == 0) nu = l == 0 ? 0 : 3;                          /* :76-87 */
+  else if (p == 1) nu = l == 0 ? 3 : 0;
+  else return -1;
+  const int k = (nu + fp->nushift) % 6;
+  int16_t f[6][24];
+  orc_chest_filters((uint8_t)k, f);
+  /* lte_dl_cell_spec_rx: conjugated QPSK pilots, m' = 110 - N_RB_DL + m */
+  const int16_t pamp = 23170;
+  const int16_t qpsk[4][2] = {{pamp, (int16_t)-pamp}, {(int16_t)-pamp, (int16_t)-pamp}, {pamp, pamp}, {(int16_t)-pamp, pamp}};
+  const int32_t *rx = rxdataF + symbol * N;
+  int32_t *dl_ch = dl_ch_estimates + N * symbol;            /* ch_offset, high_speed_flag = 1 */
+  memset(dl_ch, 0, sizeof(int32_t) * N);
+  if (N_RB == 6 || N_RB == 50 || N_RB == 100) {
+    const int l01 = l == 0 ? 0 : 1;
+    for (int m = 0; m < 2 * N_RB; m++) {
+      const int mp = 110 - N_RB + m;
+      const int16_t *pil = qpsk[(gold[Ns][l01][mp >> 4] >> (2 * (mp & 15))) & 3];
+      /* first half from first_carrier_offset + k, second half from 1 + k (DC skipped) */
+      const int32_t word = m < N_RB ? rx[fp->first_carrier_offset + k + 6 * m] : rx[1 + k + 6 * (m - N_RB)];
+      int16_t r[2];
+      memcpy(r, &word, 4);
+      int16_t ch[2];
+      ch[0] = (int16_t)(((int32_t)pil[0] * r[0] - (int32_t)pil[1] * r[1]) >> 15);
+      ch[1] = (int16_t)(((int32_t)pil[0] * r[1] + (int32_t)pil[1] * r[0]) >> 15);
+      const int16_t *flt = m == 0 ? f[0] : m == 1 ? f[1] : m == 2 * N_RB - 2 ? f[4] : m == 2 * N_RB - 1 ? f[5]
+                         : (m & 1) ? f[3] : f[2];
+      /* dl_ch advances 4 entries after the first pilot of a pair and 8 after the second */
+      int32_t *y = dl_ch + 12 * (m >> 1) + 4 * (m & 1);
+      for (int i = 0; i < 24; i++) {                         /* multadd_real_vector_complex_scalar */
+        int16_t o[2];
+        memcpy(o, &y[i], 4);
+        for (int c = 0; c < 2; c++) {
+          const int16_t v = (int16_t)(uint16_t)((uint32_t)(((int32_t)ch[c] * flt[i]) >> 16) << 2);
+          o[c] = sat16((int32_t)o[c] + v);
+        }
+        memcpy(&y[i], o, 4);
+      }
+    }
+  } else if (N_RB == 15 || N_RB == 25) {
+    return -1;                                               /* odd-N_RB branches: not restated */
+  }                                                          /* other N_RB: "not implemented", row stays 0 */
+  /* temporal interpolation (high_speed_flag = 1, :639-698) */
+  int32_t *E = dl_ch_estimates;
+#define ROW(r) (E + (r) * N)
+  if (symbol == 0) {
+    multadd_row(ROW(pilot3), 21845, ROW(pilot3 + 1), 1, N);
+    multadd_row(dl_ch, 10923, ROW(pilot3 + 1), 0, N);
+    multadd_row(ROW(pilot3), 10923, ROW(pilot3 + 2), 1, N);
+    multadd_row(dl_ch, 21845, ROW(pilot3 + 2), 0, N);
+  } else if (symbol == pilot1) {
+    if (fp->Ncp == 0) {
+      multadd_row(ROW(0), 24576, ROW(1), 1, N);
+      multadd_row(dl_ch, 8192, ROW(1), 0, N);
+      multadd_row(ROW(0), 16384, ROW(2), 1, N);
+      multadd_row(dl_ch, 16384, ROW(2), 0, N);
+      multadd_row(ROW(0), 8192, ROW(3), 1, N);
+      multadd_row(dl_ch, 24576, ROW(3), 0, N);
+    } else {                                                 /* 1/3, 2/3 as the reference weights them */
+      multadd_row(ROW(0), 10923, ROW(1), 1, N);
+      multadd_row(dl_ch, 21845, ROW(1), 0, N);
+      multadd_row(ROW(0), 21845, ROW(2), 1, N);
+      multadd_row(dl_ch, 10923, ROW(2), 0, N);
+    }
+  } else if (symbol == pilot2) {
+    multadd_row(ROW(pilot1), 21845, ROW(pilot1 + 1), 1, N);
+    multadd_row(dl_ch, 10923, ROW(pilot1 + 1), 0, N);
+    multadd_row(ROW(pilot1), 10923, ROW(pilot1 + 2), 1, N);
+    multadd_row(dl_ch, 21845, ROW(pilot1 + 2), 0, N);
+  } else {                                                   /* symbol == pilot3 */
+    if (fp->Ncp == 0) {
+      multadd_row(ROW(pilot2), 24576, ROW(pilot2 + 1), 1, N);
+      multadd_row(dl_ch, 8192, ROW(pilot2 + 1), 0, N);
+      multadd_row(ROW(pilot2), 16384, ROW(pilot2 + 2), 1, N);
+      multadd_row(dl_ch, 16384, ROW(pilot2 + 2), 0, N);
+      multadd_row(ROW(pilot2), 8192, ROW(pilot2 + 3), 1, N);
+      multadd_row(dl_ch, 24576, ROW(pilot2 + 3), 0, N);
+    } else {
+      multadd_row(ROW(pilot2), 10923, ROW(pilot2 + 1), 1, N);
+      multadd_row(dl_ch, 21845, ROW(pilot2 + 1), 0, N);
+      multadd_row(ROW(pilot2), 21845, ROW(pilot2 + 2), 1, N);
+      multadd_row(dl_ch, 10923, ROW(pilot2 + 2), 0, N);
+    }
+  }
+#undef ROW
+  return 0;
+}

@@ -499,3 +499,43 @@ def dlsch_unscrambling(llr, G, c_init):
 def adjust_G2(fp, rb_alloc, subframe, symbol):
     ra = (ctypes.c_uint32 * 4)(*rb_alloc)
     return orc().orc_adjust_G2(ctypes.byref(fp), ra, subframe, symbol)
+
+
+def chest_filters(k):
+    out = np.zeros((6, 24), np.int16)
+    orc().orc_chest_filters(k, P(out))
+    return out
+
+
+def gold_table(fp):
+    t = np.zeros((20, 2, 14), np.uint32)
+    orc().orc_lte_gold_table(ctypes.byref(fp), P(t))
+    return t
+
+
+def dl_channel_estimation(fp, gold, rxdataF, est, Ns, p, l, symbol):
+    """lte_dl_channel_estimation on one subframe grid rxdataF [nsymb*N] into est [nsymb*N] (in place)."""
+    rc = orc().orc_lte_dl_channel_estimation(ctypes.byref(fp), P(gold), P(np.ascontiguousarray(rxdataF, np.int32)),
+                                             P(est), Ns, p, l, symbol)
+    assert rc == 0
+    return est
+
+
+def chest_subframe(fp, rxF, rxF_next0, sf, p=0):
+    """The estimates rx_pdsch reads for every symbol of subframe sf, in dlsim's call order
+    (dlsim.c:2907-2931 -> slot_fep.c:180-199): pilot symbols 0, 4, 7, 11 of slots 2 sf, 2 sf + 1
+    and then symbol 0 of slot 2 sf + 2, which interpolates rows 12 / 13 (and overwrites row 0 with
+    the next subframe's estimate, so the current row 0 is kept).  Extended prefix: 0, 3, 6, 9."""
+    N = fp.ofdm_symbol_size
+    nsymb = 14 if fp.Ncp == 0 else 12
+    lp = 4 if fp.Ncp == 0 else 3
+    est = np.zeros(nsymb * N, np.int32)
+    g = gold_table(fp)
+    for Ns, l, sym in ((2 * sf, 0, 0), (2 * sf, lp, lp), (2 * sf + 1, 0, nsymb // 2), (2 * sf + 1, lp, nsymb // 2 + lp)):
+        dl_channel_estimation(fp, g, rxF, est, Ns, p, l, sym)
+    row0 = est[:N].copy()
+    nxt = np.zeros(nsymb * N, np.int32)
+    nxt[:N] = rxF_next0
+    dl_channel_estimation(fp, g, nxt, est, (2 * sf + 2) % 20, p, 0, 0)
+    est[:N] = row0
+    return est

@@ -1,0 +1,101 @@
+"""Downlink channel estimation oracle (oracle/oai_oracle_chest.c: lte_dl_channel_estimation with
+high_speed_flag = 1, the 6 / 50 / 100 PRB branch).  Pinned
+  - to the reference's own interpolation filters entry by entry (PHY/LTE_ESTIMATION/filt96_32.h,
+    read as data when the reference tree is present): the oracle (and the library, test_gpu_chest)
+    derive them from one formula with three cited exceptions, and
+  - by dlsim's closed loop with perfect_ce = 0: the oracle's transmit subframe with CRS -> IQ ->
+    slot_fep -> this estimator -> rx_pdsch -> unscrambling -> RX rate matching -> the 16-bit
+    turbo decoder recovers the transport block, also at 6 PRB where slot_fep's 4-sample alignment
+    shifts the window (the estimate absorbs the phase ramp that a constant estimate cannot).
+No GPU needed."""
+import os
+import re
+
+import numpy as np
+import pytest
+
+import oracle_lib as O
+from test_rx_cpu import decode_tb, params
+
+REF = "/root/reference/openair1/PHY/LTE_ESTIMATION/filt96_32.h"
+
+
+def _ref_filters():
+    src = re.sub(r"/\*.*?\*/", "", re.sub(r"//[^\n]*", "", open(REF).read()), flags=re.S)
+    return {m.group(1): [int(v) for v in re.findall(r"-?\d+", m.group(2))]
+            for m in re.finditer(r"short\s+(filt24_\w+)\[24\][^=]*=\s*\{([^}]*)\}", src)}
+
+
+@pytest.mark.skipif(not os.path.exists(REF), reason="reference tree absent")
+def test_filters_equal_reference_header():
+    ref = _ref_filters()
+    for k in range(6):
+        # lte_dl_channel_estimation.c:105-180
+        names = (["filt24_0", "filt24_2", "filt24_0", "filt24_2", "filt24_0r2", "filt24_2r"] if k == 0 else
+                 [f"filt24_{k}l", f"filt24_{k + 2}l2", f"filt24_{k}", f"filt24_{k + 2}", f"filt24_{k}r2",
+                  f"filt24_{k + 2}r"])
+        got = O.chest_filters(k)
+        for i, nm in enumerate(names):
+            want = (ref[nm] + [0] * 24)[:24]          # filt24_0_dcr has 23 initialisers (the 24th is 0)
+            assert got[i].tolist() == want, (k, nm)
+
+
+def _frame_loop(p, sf, pays, fp):
+    """Two consecutive subframes sf, sf + 1 through the oracle's TX (CRS on) into one frame, then
+    slot_fep of slots 2 sf, 2 sf + 1 and symbol 0 of slot 2 sf + 2."""
+    spt, N = fp.samples_per_tti, fp.ofdm_symbol_size
+    frame = np.zeros(10 * spt + N, np.int32)
+    for d, pay in enumerate(pays):
+        s = (sf + d) % 10
+        txd, _, _ = O.tx_subframe(O.tx_cfg_from_params(params("C2", fp.N_RB_DL, p.mcs[0], p.num_pdcch_symbols, s), s),
+                                  [pay])
+        frame[s * spt:(s + 1) * spt] = txd[0]
+    rxF = np.zeros(15 * N, np.int32)                      # slot_fep writes row l + 7 (Ns & 1)
+    for Ns in (2 * sf, 2 * sf + 1):
+        for l in range(7):
+            assert O.slot_fep([frame], [rxF], fp, l, Ns) == 0
+    nxt = np.zeros(15 * N, np.int32)
+    assert O.slot_fep([frame], [nxt], fp, 0, (2 * sf + 2) % 20) == 0
+    return rxF[:14 * N].copy(), nxt[:N].copy()
+
+
+LOOP = [(6, 9, 2, 2), (6, 16, 3, 7), (50, 16, 1, 3), (100, 27, 2, 7), (100, 4, 1, 8), (50, 24, 3, 1)]
+
+
+@pytest.mark.parametrize("N_RB,mcs,npdcch,sf", LOOP)
+def test_estimated_channel_loop_decodes(N_RB, mcs, npdcch, sf):
+    p = params("C2", N_RB, mcs, npdcch, sf)
+    fp = O.tx_cfg_from_params(p, sf).fp
+    rng = np.random.default_rng(N_RB + mcs)
+    pays = [rng.integers(0, 256, p.payload_stride, dtype=np.uint8) for _ in range(2)]
+    # the frame grid is indexed by subframe inside the frame: rxF rows start at slot 2 sf
+    rxF_sf, next0 = _frame_loop(p, sf, pays, fp)
+    est = O.chest_subframe(fp, rxF_sf, next0, sf)
+    N = fp.ofdm_symbol_size
+    # every row carries an estimate over the allocated band
+    band = np.r_[5:5 + 12 * N_RB]
+    assert all(np.count_nonzero(est[r * N:(r + 1) * N][band]) > 0.9 * len(band) for r in range(14))
+    Qm = 2 if mcs < 10 else 4 if mcs < 17 else 6
+    llr, _ = O.rx_pdsch_siso(fp, rxF_sf, est, list(p.rb_alloc), Qm, npdcch, sf)
+    G = len(llr)
+    u = np.zeros(32 * (1 + G // 32), np.int16)
+    u[:G] = llr
+    O.dlsch_unscrambling(u, G, (p.rnti << 14) + (sf << 9) + fp.Nid_cell)
+    res, tb = decode_tb(u[:G], G, p.TBS[0], Qm)
+    assert all(it <= 4 for it, _ in res), [it for it, _ in res]
+    assert np.array_equal(tb, pays[0][:p.TBS[0] // 8])
+
+
+def test_constant_channel_interior_is_flat():
+    """A flat channel (received grid = the CRS of amplitude AMP = 1024 themselves) gives an interior
+    estimate of (AMP, 0) within the filters' floor rounding: conj(pilot) * rx sums two products of
+    ONE_OVER_SQRT2 amplitudes (>> 15), and neighbouring triangle taps sum to 16383 / 16384."""
+    fp = O.frame(50, Nid_cell=5)
+    N = fp.ofdm_symbol_size
+    g = O.gold_table(fp)
+    grid = np.zeros(14 * N, np.int32)
+    O.orc().orc_generate_pilots_subframe((O.ctypes.c_void_p * 1)(grid.ctypes.data), 1024, O.ctypes.byref(fp), 3)
+    est = np.zeros(14 * N, np.int32)
+    O.dl_channel_estimation(fp, g, grid, est, 6, 0, 0, 0)
+    row = est[:N].view(np.int16).reshape(-1, 2)[5 + 24:5 + 12 * 50 - 24]
+    assert np.all(np.abs(row[:, 0].astype(int) - 1024) <= 8) and np.all(np.abs(row[:, 1]) <= 8), row[:4]
