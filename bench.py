@@ -42,6 +42,12 @@ def _traffic(config, kernel, batch):
     return t.get(kernel) if t.get("batch") == batch else None
 
 
+def _stage_traffic(config, stage, batch):
+    """_traffic of a stage made of several kernels ("k_a+k_b"): the sum, or null if any is missing."""
+    parts = [_traffic(config, k, batch) for k in stage.split("+")]
+    return None if any(t is None for t in parts) else sum(parts)
+
+
 def _valu_busy(config, batch):
     """VALU-busy fraction per kernel (SQ_ACTIVE_INST_VALU / CUs / GRBM_GUI_ACTIVE) from the committed
     rocprofv3 --pmc pass (tools/gpu_pmc_valu.sh -> profiles/valu_<config>.json), only when it was
@@ -314,6 +320,118 @@ def bench_fep(args, world, rank, dist, torch):
             "cpu_baseline": cpu}), flush=True)
 
 
+def bench_ue(args, world, rank, dist, torch):
+    """UE PDSCH receive chain (SURVEY 8f item 3, config "UE"): dlsim's C2 receiver with
+    perfect_ce = 0 -- slot_fep of every symbol, lte_dl_channel_estimation of the pilot symbols
+    with the temporal interpolation of every row, rx_pdsch (extraction, channel level,
+    compensation, 16-QAM LLRs) and dlsch_unscrambling -- over a batch of consecutive 20 MHz TM1
+    subframes (1 TX, 1 RX antenna) produced once by the GPU transmit pipeline."""
+    import numpy as np
+    import openair4g_amd as oai
+    oai.init()
+    n_sf = args.batch
+    p = oai.make_params("C2", subframe=0, subframe_step=1, with_crs=1, rnti=0x1234)
+    fp = oai.frame_parms(100)
+    N, nsym, spt = fp.ofdm_symbol_size, fp.symbols_per_tti, fp.samples_per_tti
+    Qm = oai.lib().oai4g_get_Qm(p.mcs[0])
+    # input: n_sf + 1 consecutive transmitted subframes (the last one's symbol 0 closes rows 12 / 13)
+    tx = oai.TxPipeline(p, n_sf + 1)
+    tx.fill_payload(0x5EED + rank)
+    tx.run()
+    tx.sync()
+    fb = oai.FepBatch(fp, n_sf + 1, 1)
+    fb.upload(tx.iq())
+    tx.close()
+    cb = oai.ChestBatch(fp, n_sf, first_subframe=0)
+    rb = oai.RxBatch(fp, list(p.rb_alloc), Qm, p.num_pdcch_symbols, p.rnti, n_sf, first_subframe=0, subframe_step=1)
+    sid = torch.cuda.current_stream().cuda_stream
+
+    def step(stream):
+        fb.run(stream=stream)
+        cb.launch(fb.d_rxF, stream=stream)
+        rb.launch(fb.d_rxF, cb.d_est, 1, stream=stream)
+    for _ in range(args.warmup):
+        step(None)
+    oai.lib().oai4g_sync()
+    if dist is not None:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step(sid)
+    oai.lib().oai4g_sync()
+    torch.cuda.synchronize()
+    if dist is not None:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if dist is not None:
+        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    # per-stage launch durations (HIP events on the launch stream)
+    stages = {"k_fep": lambda: fb.run(stream=sid), "k_chest": lambda: cb.launch(fb.d_rxF, stream=sid),
+              "k_rx_level+k_rx_llr": lambda: rb.launch(fb.d_rxF, cb.d_est, 1, stream=sid)}
+    kern_ms = {}
+    for name, fn in stages.items():
+        evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+               for _ in range(args.kernel_reps)]
+        for e0, e1 in evs:
+            e0.record()
+            fn()
+            e1.record()
+        torch.cuda.synchronize()
+        kern_ms[name] = sum(e0.elapsed_time(e1) for e0, e1 in evs) / len(evs)
+    n_llr = sum(rb.llr_count(i % 10) for i in range(n_sf))
+    n_re = n_llr // Qm
+    alg = {"k_fep": (n_sf + 1) * (spt * 4 + nsym * N * 4),                 # IQ read + frequency grid written
+           "k_chest": n_sf * (nsym * N * 4 + 5 * N * 4),                     # 14 rows written + 5 pilot rows read
+           "k_rx_level+k_rx_llr": n_re * 8 + n_llr * 2 + n_sf * 1200 * 4}    # y + h per RE, LLRs, level row
+    fb.close()
+    cb.close()
+    rb.close()
+    value = n_sf * args.steps * world / elapsed
+    dom = max(kern_ms, key=kern_ms.get)
+    ach = alg[dom] / (kern_ms[dom] * 1e-3) / 1e9
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        sys.path.insert(0, os.path.join(ROOT, "tests"))
+        import oracle_lib as O
+        fpo = O.frame(100)
+        rng = np.random.default_rng(1)
+        frame = np.zeros(10 * spt + N, np.int32)
+        frame[:2 * spt] = rng.integers(-2000, 2000, (2 * spt, 2), dtype=np.int16).view(np.int32).ravel()
+        rxF, nxt = np.zeros(15 * N, np.int32), np.zeros(15 * N, np.int32)
+        n, t1 = 0, time.perf_counter()
+        while time.perf_counter() - t1 < args.cpu_seconds:
+            for Ns in (0, 1):
+                for l in range(7):
+                    O.slot_fep([frame], [rxF], fpo, l, Ns)
+            O.slot_fep([frame], [nxt], fpo, 0, 2)
+            est = O.chest_subframe(fpo, rxF[:14 * N], nxt[:N], 0)
+            llr, _ = O.rx_pdsch_siso(fpo, rxF[:14 * N], est, list(p.rb_alloc), Qm, p.num_pdcch_symbols, 0)
+            u = np.zeros(32 * (1 + len(llr) // 32), np.int16)
+            u[:len(llr)] = llr
+            O.dlsch_unscrambling(u, len(llr), (p.rnti << 14) + fpo.Nid_cell)
+            n += 1
+        dt = time.perf_counter() - t1
+        cpu = {"value": n / dt, "unit": "subframes/s", "cores": 1, "kind": "port",
+               "sample": f"{n} subframes through the C oracle (slot_fep + 5 lte_dl_channel_estimation calls + "
+                         f"rx_pdsch + dlsch_unscrambling), single thread, {dt:.1f} s"}
+    if rank == 0:
+        print(json.dumps({
+            "metric": "UE PDSCH RX subframes/sec (20 MHz TM1 16-QAM, 1 RX, estimated channel)", "value": value,
+            "unit": "subframes/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+            "ms_per_step": elapsed * 1000.0 / args.steps, "higher_is_better": True, "scaling": "weak",
+            "vs_baseline": None, "dtype": "int16", "data": "GPU-transmitted C2 subframes (synthetic payload), resident in HBM",
+            "config": {"workload": "slot_fep + lte_dl_channel_estimation + rx_pdsch + dlsch_unscrambling, C2 20 MHz",
+                       "config_id": "UE", "subframes_per_gpu_per_step": n_sf, "parallelism": f"subframe-sharded x{world}"},
+            "roofline": {"bound": "hbm", "kernel": dom, "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": ach / HBM_PEAK_GBS, "traffic": _stage_traffic("UE", dom, n_sf), "kernel_ms": kern_ms,
+                         "algorithmic_bytes_per_launch": alg},
+            "end_to_end_algorithmic_GBps": sum(alg.values()) / (elapsed / args.steps) / 1e9,
+            "cpu_baseline": cpu}), flush=True)
+
+
 def launch_ranks(n, argv):
     """`bench.py --gpus N` without a launcher: start N fresh child processes of this script, one
     per GPU (RANK / LOCAL_RANK / WORLD_SIZE / MASTER_ADDR / MASTER_PORT as torch.distributed.run
@@ -453,7 +571,7 @@ def main():
                     help="harness test on CPU: gloo, StubPipeline, no GPU (exercises ranks/broadcast/timing)")
     args = ap.parse_args()
     if args.batch is None:
-        args.batch = {"C3": 8192, "C4": 1024, "FEP": 8192}.get(args.config, 2048)
+        args.batch = {"C3": 8192, "C4": 1024, "FEP": 8192, "UE": 4096}.get(args.config, 2048)
     if args.cpu_stub:
         args.backend = "gloo"
 
@@ -468,10 +586,10 @@ def main():
 
     host = Host(args, world, rank, local_rank)
     torch, dist = host.torch, host.dist
-    if args.config in ("C5", "FEP"):
+    if args.config in ("C5", "FEP", "UE"):
         if host.stub:
             sys.exit("bench: --cpu-stub covers the transmit configurations only")
-        (bench_c5 if args.config == "C5" else bench_fep)(args, world, rank, dist, torch)
+        {"C5": bench_c5, "FEP": bench_fep, "UE": bench_ue}[args.config](args, world, rank, dist, torch)
         host.close()
         return
     bench_tx(args, world, rank, host)

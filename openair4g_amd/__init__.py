@@ -506,11 +506,15 @@ class ChestBatch:
                                 np.ascontiguousarray(next_symbol0, dtype=np.int32).ravel()])
             assert y.size == self.n_grid + self.fp.ofdm_symbol_size
             _check(self.L.oai4g_memcpy_h2d(self.d_rx, _ptr(y), y.nbytes) == 0)
-        _check(self.L.oai4g_chest_batch(self.cfg, self.n_sf, d_rxdataF or self.d_rx, self.d_est, None) == 0)
+        self.launch(d_rxdataF or self.d_rx)
         _check(self.L.oai4g_sync() == 0)
         out = np.empty((self.n_sf, self.n_grid // self.n_sf), dtype=np.int32)
         _check(self.L.oai4g_memcpy_d2h(_ptr(out), self.d_est, out.nbytes) == 0)
         return out
+
+    def launch(self, d_rxdataF, stream=None):
+        """Device-only: estimates of d_rxdataF (n_sf grids + the next symbol 0) into self.d_est."""
+        _check(self.L.oai4g_chest_batch(self.cfg, self.n_sf, d_rxdataF, self.d_est, stream) == 0)
 
     def close(self):
         self.L.oai4g_dev_free(self.d_rx)
@@ -545,12 +549,15 @@ class RxBatch:
             _check(self.L.oai4g_memcpy_h2d(self.d_y, _ptr(y), y.nbytes) == 0)
         h = np.ascontiguousarray(dl_ch, dtype=np.int32)
         _check(self.L.oai4g_memcpy_h2d(self.d_h, _ptr(h), h.nbytes) == 0)
-        _check(self.L.oai4g_rx_batch(self.cfg, self.n_sf, d_rxdataF or self.d_y, self.d_h, self.d_llr, unscramble,
-                                     None) == 0)
+        self.launch(d_rxdataF or self.d_y, self.d_h, unscramble)
         _check(self.L.oai4g_sync() == 0)
         out = np.empty((self.n_sf, self.stride), dtype=np.int16)
         _check(self.L.oai4g_memcpy_d2h(_ptr(out), self.d_llr, out.nbytes) == 0)
         return out
+
+    def launch(self, d_rxdataF, d_est, unscramble=1, stream=None):
+        """Device-only: LLRs of d_rxdataF / d_est into self.d_llr."""
+        _check(self.L.oai4g_rx_batch(self.cfg, self.n_sf, d_rxdataF, d_est, self.d_llr, unscramble, stream) == 0)
 
     def close(self):
         for p in (self.d_y, self.d_h, self.d_llr):

@@ -2811,6 +2811,7 @@ extern "C" oai4g_rx_config_t *oai4g_rx_config_create(const oai4g_frame_parms_t *
       const int adj = Qm == 2 ? 0 : rx_adjust_G2(fp, rb_alloc, sf, l);
       const int len = pil ? (int)nb_rb * 10 - 5 * adj / 6 : (int)nb_rb * 12 - adj;
       h.len[sf][k] = (uint32_t)(len > 0 ? len : 0);
+      if (h.len[sf][k] > 1280) { set_err("rx_config: > 1280 REs in a symbol (k_rx_llr covers 256 x 5)"); delete cfg; return nullptr; }
       h.llr_off[sf][k] = off;
       off += h.len[sf][k] * Qm;
       if (k == 0) {

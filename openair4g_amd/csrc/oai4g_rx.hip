@@ -47,41 +47,78 @@ __global__ void __launch_bounds__(256) k_rx_level(const rx_dev_t *__restrict__ c
   }
 }
 
+/* A 256-thread workgroup per (subframe, PDSCH symbol); thread t takes REs t + 256 r, r < 5 (>= the
+ * 1200 REs of 100 PRB).  All map words, then all estimate / received words are loaded before any
+ * arithmetic, so each thread waits for two memory round trips rather than two per RE.  An RE's Qm
+ * LLRs leave as one 4 / 8 / 12-byte store (a symbol's stream offset is a multiple of Qm entries);
+ * the scrambling signs of all Qm come from one 64-bit window of the Gold words (gold_words carries
+ * one word of slack). */
+constexpr int RX_R = 5;
+
+template <int QM>
 __global__ void __launch_bounds__(256) k_rx_llr(const rx_dev_t *__restrict__ c, const int32_t *__restrict__ rxF,
                                                 const int32_t *__restrict__ ch, int16_t *__restrict__ llr,
                                                 const uint8_t *__restrict__ shift, int unscramble)
 {
   const uint32_t sf = blockIdx.y, k = blockIdx.x, sfi = (c->first_sf + sf * c->sf_step) % 10;
-  const uint32_t l = c->npdcch + k, len = c->len[sfi][k], Qm = c->Qm;
+  const uint32_t l = c->npdcch + k, len = c->len[sfi][k];
   const uint32_t *map = c->map + c->map_off[sfi][k];
   const size_t so = ((size_t)sf * c->nsymb + l) * c->N;
   const int32_t *y = rxF + so, *h = ch + so;
   int16_t *out = llr + (size_t)sf * c->llr_stride + c->llr_off[sfi][k];
   const uint32_t sh = shift[sf], base = c->llr_off[sfi][k];
   const uint32_t *gold = c->gold + (size_t)sfi * c->gold_words;
-  for (uint32_t j = blockIdx.z * blockDim.x + threadIdx.x; j < len; j += gridDim.z * blockDim.x) {
-    const uint32_t m = map[j];
-    const uint32_t hv = (uint32_t)h[m >> 16], yv = (uint32_t)y[m & 0xFFFFu];
-    const int16_t hr = (int16_t)hv, hi = (int16_t)(hv >> 16), yr = (int16_t)yv, yi = (int16_t)(yv >> 16);
+  const int16_t a1 = c->a1, a2 = c->a2;
+  uint32_t mw[RX_R], hv[RX_R], yv[RX_R];
+#pragma unroll
+  for (int r = 0; r < RX_R; r++) {
+    const uint32_t j = threadIdx.x + 256 * r;
+    mw[r] = j < len ? map[j] : 0u;
+  }
+#pragma unroll
+  for (int r = 0; r < RX_R; r++) {
+    hv[r] = (uint32_t)h[mw[r] >> 16];
+    yv[r] = (uint32_t)y[mw[r] & 0xFFFFu];
+  }
+#pragma unroll
+  for (int r = 0; r < RX_R; r++) {
+    const uint32_t j = threadIdx.x + 256 * r;
+    if (j >= len) break;
+    const int16_t hr = (int16_t)hv[r], hi = (int16_t)(hv[r] >> 16), yr = (int16_t)yv[r], yi = (int16_t)(yv[r] >> 16);
     const int16_t nhi = (int16_t)(-(int32_t)hi);
     int16_t v[6];
     v[0] = rx_sat16(rx_madd(hr, yr, hi, yi) >> sh);
     v[1] = rx_sat16(rx_madd(nhi, yr, hr, yi) >> sh);
-    if (Qm > 2) {
+    if (QM > 2) {
       const int16_t mg = rx_sat16(rx_madd(hr, hr, hi, hi) >> sh);
-      const int16_t mag = (int16_t)((((int32_t)mg * c->a1) >> 16) << 1), magb = (int16_t)((((int32_t)mg * c->a2) >> 16) << 1);
+      const int16_t mag = (int16_t)((((int32_t)mg * a1) >> 16) << 1);
       v[2] = rx_sat16((int32_t)mag - rx_abs16(v[0]));
       v[3] = rx_sat16((int32_t)mag - rx_abs16(v[1]));
-      v[4] = rx_sat16((int32_t)magb - rx_abs16(v[2]));
-      v[5] = rx_sat16((int32_t)magb - rx_abs16(v[3]));
-    }
-    for (uint32_t q = 0; q < Qm; q++) {
-      int16_t o = v[q];
-      if (unscramble) {
-        const uint32_t b = base + j * Qm + q;
-        o = (int16_t)(((gold[b >> 5] >> (b & 31)) & 1u) ? o : -(int32_t)o);   /* llr * (2 c - 1), int16 */
+      if (QM > 4) {
+        const int16_t magb = (int16_t)((((int32_t)mg * a2) >> 16) << 1);
+        v[4] = rx_sat16((int32_t)magb - rx_abs16(v[2]));
+        v[5] = rx_sat16((int32_t)magb - rx_abs16(v[3]));
       }
-      out[j * Qm + q] = o;
+    }
+    if (unscramble) {                            /* llr * (2 c - 1), int16 */
+      const uint32_t b = base + j * QM, w = b >> 5;
+      const uint64_t win = ((uint64_t)gold[w] | ((uint64_t)gold[w + 1] << 32)) >> (b & 31);
+#pragma unroll
+      for (int q = 0; q < QM; q++)
+        if (!((win >> q) & 1u)) v[q] = (int16_t)(-(int32_t)v[q]);
+    }
+    uint32_t pk[3];
+#pragma unroll
+    for (int q = 0; q < QM / 2; q++) pk[q] = (uint32_t)(uint16_t)v[2 * q] | ((uint32_t)(uint16_t)v[2 * q + 1] << 16);
+    if (QM == 2) {
+      *(uint32_t *)(out + 2 * j) = pk[0];
+    } else if (QM == 4) {
+      *(uint2 *)(out + 4 * j) = make_uint2(pk[0], pk[1]);
+    } else {
+      uint32_t *o = (uint32_t *)(out + 6 * j);
+      o[0] = pk[0];
+      o[1] = pk[1];
+      o[2] = pk[2];
     }
   }
 }
@@ -106,7 +143,12 @@ hipError_t oai4g_launch_rx(const rx_dev_t *d_cfg, const rx_dev_t *h_cfg, int n_s
 {
   if (n_sf <= 0) return hipSuccess;
   hipLaunchKernelGGL(k_rx_level, dim3(n_sf), dim3(256), 0, s, d_cfg, d_ch, d_shift);
-  hipLaunchKernelGGL(k_rx_llr, dim3(h_cfg->n_sym, n_sf, 2), dim3(256), 0, s, d_cfg, d_rxF, d_ch, d_llr, d_shift,
-                     unscramble);
+  const dim3 g(h_cfg->n_sym, n_sf), b(256);                  /* 256 x RX_R >= 1200 REs per symbol */
+  if (h_cfg->Qm == 2)
+    hipLaunchKernelGGL(k_rx_llr<2>, g, b, 0, s, d_cfg, d_rxF, d_ch, d_llr, d_shift, unscramble);
+  else if (h_cfg->Qm == 4)
+    hipLaunchKernelGGL(k_rx_llr<4>, g, b, 0, s, d_cfg, d_rxF, d_ch, d_llr, d_shift, unscramble);
+  else
+    hipLaunchKernelGGL(k_rx_llr<6>, g, b, 0, s, d_cfg, d_rxF, d_ch, d_llr, d_shift, unscramble);
   return hipGetLastError();
 }

@@ -13,7 +13,8 @@ import json
 import os
 import sys
 
-KMAP = {"k_encode": "encode_rm_scramble", "k_modofdm": "modulate_idft_cp", "k_fep": "k_fep<11>", "k_td16": "k_td16"}
+KMAP = {"k_encode": "encode_rm_scramble", "k_modofdm": "modulate_idft_cp", "k_fep": "k_fep<11>", "k_td16": "k_td16",
+        "k_chest": "k_chest", "k_rx_llr": "k_rx_llr", "k_rx_level": "k_rx_level"}
 
 
 def short(name):
