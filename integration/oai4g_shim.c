@@ -2,7 +2,8 @@
  * Replaces: dlsch_coding.c:254 dlsch_encoding, dlsch_scrambling.c:51, dlsch_modulation.c:1181,
  * ofdm_mod.c:47/85/233, lte_dfts.c idft64..idft2048, crc_byte.c:117/135, lte_segmentation.c:39,
  * 3gpplte_sse.c:380, lte_rate_matching.c:51/464, pcfich.c:48/144, dci.c:2024, pss.c:50, sss.c:47,
- * pbch.c:161, phich.c:401. */
+ * pbch.c:161, phich.c:401, lte_dl_channel_estimation.c:37, dlsch_demodulation.c:82 (rx_pdsch, TM1),
+ * dlsch_scrambling.c:99 (dlsch_unscrambling). */
 #include "PHY/defs.h"
 #include "PHY/extern.h"
 #include "oai4g.h"
@@ -139,7 +140,8 @@ int slot_fep(PHY_VARS_UE *ue, unsigned char l, unsigned char Ns, int sample_offs
   int ret = oai4g_slot_fep((int32_t **)ue->lte_ue_common_vars.rxdata, (int32_t **)ue->lte_ue_common_vars.rxdataF,
                            &fp, ue->lte_frame_parms.nb_antennas_rx, l, Ns, sample_offset, no_prefix);
   if (ret != 0) return ret;
-  /* channel and frequency-offset estimation stay on the reference's CPU code (slot_fep.c:179-222) */
+  /* channel estimation: lte_dl_channel_estimation below (GPU); the frequency-offset estimator
+   * stays on the reference's CPU code (slot_fep.c:179-222) */
   if (ue->perfect_ce == 0 && (l == 0 || l == 4 - ue->lte_frame_parms.Ncp)) {
     const unsigned char symbol = l + (7 - ue->lte_frame_parms.Ncp) * (Ns & 1);
     for (int aa = 0; aa < ue->lte_frame_parms.nb_antennas_tx_eNB; aa++) {
@@ -223,4 +225,56 @@ uint32_t lte_rate_matching_turbo(uint32_t RTC, uint32_t G, uint8_t *w, uint8_t *
                                  uint8_t nb_rb, uint8_t m)
 {
   return oai4g_lte_rate_matching_turbo(RTC, G, w, e, C, Nsoft, Mdlharq, Kmimo, rvidx, Qm, Nl, r, nb_rb, m);
+}
+
+/* UE receive chain after the FFT.
+ * lte_dl_channel_estimation (lte_dl_channel_estimation.c:37): the library covers eNB_offset 0,
+ * high_speed_flag 1 (dlsim's and lte_init's default) and one RX antenna; anything else reports -1
+ * as the reference does for its unsupported (p, l) cases. */
+int lte_dl_channel_estimation(PHY_VARS_UE *ue, uint8_t eNB_id, uint8_t eNB_offset, unsigned char Ns, unsigned char p,
+                              unsigned char l, unsigned char symbol)
+{
+  (void)eNB_id;
+  if (eNB_offset != 0 || ue->high_speed_flag != 1 || ue->lte_frame_parms.nb_antennas_rx != 1) return -1;
+  oai4g_frame_parms_t fp;
+  fp_to(&ue->lte_frame_parms, &fp);
+  return oai4g_lte_dl_channel_estimation(&fp, (const int32_t *)ue->lte_ue_common_vars.rxdataF[0],
+                                         (int32_t *)ue->lte_ue_common_vars.dl_ch_estimates[0][p << 1], Ns, p, l,
+                                         symbol);
+}
+
+/* rx_pdsch (dlsch_demodulation.c:82) for TM1 / one RX antenna / localized allocations
+ * (rb_alloc_even == rb_alloc_odd): the library demodulates a whole subframe, so the shim runs it
+ * when dlsim's last per-symbol call arrives (dlsim.c:3236-3260) -- the LLR stream and log2_maxh in
+ * lte_ue_pdsch_vars[eNB_id] are then the reference's. */
+int rx_pdsch(PHY_VARS_UE *ue, PDSCH_t type, unsigned char eNB_id, unsigned char eNB_id_i, uint8_t subframe,
+             unsigned char symbol, unsigned char first_symbol_flag, unsigned char dual_stream_flag,
+             unsigned char i_mod, unsigned char harq_pid)
+{
+  (void)eNB_id_i;
+  (void)first_symbol_flag;
+  (void)i_mod;
+  LTE_DL_UE_HARQ_t *h = ue->dlsch_ue[eNB_id][0]->harq_processes[harq_pid];
+  if (type != PDSCH || dual_stream_flag || ue->lte_frame_parms.nb_antennas_rx != 1 ||
+      ue->lte_frame_parms.nb_antennas_tx_eNB != 1 || memcmp(h->rb_alloc_even, h->rb_alloc_odd, 16) != 0)
+    return -1;
+  if (symbol != ue->lte_frame_parms.symbols_per_tti - 1) return 0;
+  oai4g_frame_parms_t fp;
+  fp_to(&ue->lte_frame_parms, &fp);
+  uint8_t log2_maxh = 0;
+  const int n = oai4g_rx_pdsch_siso(&fp, (const int32_t *)ue->lte_ue_common_vars.rxdataF[0],
+                                    (const int32_t *)ue->lte_ue_common_vars.dl_ch_estimates[eNB_id][0],
+                                    h->rb_alloc_even, get_Qm(h->mcs), ue->lte_ue_pdcch_vars[eNB_id]->num_pdcch_symbols,
+                                    subframe, ue->lte_ue_pdsch_vars[eNB_id]->llr[0], &log2_maxh);
+  if (n < 0) return -1;
+  ue->lte_ue_pdsch_vars[eNB_id]->log2_maxh = log2_maxh;
+  return 0;
+}
+
+void dlsch_unscrambling(LTE_DL_FRAME_PARMS *frame_parms, int mbsfn_flag, LTE_UE_DLSCH_t *dlsch, int G,
+                        int16_t *llr, uint8_t q, uint8_t Ns)                          /* dlsch_scrambling.c:99 */
+{
+  oai4g_frame_parms_t fp;
+  fp_to(frame_parms, &fp);
+  oai4g_dlsch_unscrambling(&fp, mbsfn_flag, dlsch->rnti, G, llr, q, Ns);
 }
