@@ -88,3 +88,57 @@ def test_c5_bench_batch_16384_blocks(gpu, mode):
         assert np.all(its == 9)                 # unstructured LLRs: every CRC check fails
     else:
         assert np.all(its <= 8)
+
+
+def test_ue_bench_batch_4096(gpu):
+    """bench.py --config UE at its default 4096 subframes: the GPU-transmitted C2 batch through
+    FEP -> channel estimation -> demodulation -> unscrambling, sampled subframes checked against the
+    oracle's chain on the same IQ (slot_fep, lte_dl_channel_estimation x 5, rx_pdsch,
+    dlsch_unscrambling), and their transport blocks decoded back to the device payload."""
+    from test_rx_cpu import decode_tb
+    n_sf = 4096
+    p = gpu.make_params("C2", subframe=0, subframe_step=1, with_crs=1, rnti=0x1234)
+    fg, fo = gpu.frame_parms(100), O.frame(100)
+    N, spt = fo.ofdm_symbol_size, fo.samples_per_tti
+    Qm = gpu.lib().oai4g_get_Qm(p.mcs[0])
+    tx = gpu.TxPipeline(p, n_sf + 1)
+    tx.fill_payload(0x5EED)                      # bench_ue, rank 0
+    tx.run()
+    tx.sync()
+    iq = tx.iq()
+    pay = tx.download_payload()
+    tx.close()
+    fb = gpu.FepBatch(fg, n_sf + 1, 1)
+    fb.upload(iq)
+    fb.run()
+    cb = gpu.ChestBatch(fg, n_sf, first_subframe=0)
+    rb = gpu.RxBatch(fg, list(p.rb_alloc), Qm, p.num_pdcch_symbols, p.rnti, n_sf, first_subframe=0, subframe_step=1)
+    cb.launch(fb.d_rxF)
+    rb.launch(fb.d_rxF, cb.d_est, 1)
+    gpu.lib().oai4g_sync()
+    out = np.empty((n_sf, rb.stride), dtype=np.int16)
+    gpu.lib().oai4g_memcpy_d2h(gpu._ptr(out), rb.d_llr, out.nbytes)
+    for i in _samples(n_sf, 3, 11):
+        sf = i % 10
+        frame = np.zeros(10 * spt + N, np.int32)
+        frame[sf * spt:(sf + 1) * spt] = iq[i, 0]
+        nsf = (sf + 1) % 10
+        frame[nsf * spt:(nsf + 1) * spt] = iq[i + 1, 0]
+        rxF, nxt = np.zeros(15 * N, np.int32), np.zeros(15 * N, np.int32)
+        for Ns in (2 * sf, 2 * sf + 1):
+            for l in range(7):
+                assert O.slot_fep([frame], [rxF], fo, l, Ns) == 0
+        assert O.slot_fep([frame], [nxt], fo, 0, (2 * sf + 2) % 20) == 0
+        est = O.chest_subframe(fo, rxF[:14 * N], nxt[:N], sf)
+        lo, _ = O.rx_pdsch_siso(fo, rxF[:14 * N], est, list(p.rb_alloc), Qm, p.num_pdcch_symbols, sf)
+        G = len(lo)
+        u = np.zeros(32 * (1 + G // 32), np.int16)
+        u[:G] = lo
+        O.dlsch_unscrambling(u, G, (p.rnti << 14) + (sf << 9) + fo.Nid_cell)
+        assert rb.llr_count(sf) == G and np.array_equal(out[i, :G], u[:G]), i
+        if sf not in (0, 5):                    # the reference's even-N_RB extraction of PBCH / sync REs
+            res, tb = decode_tb(out[i], G, p.TBS[0], Qm)
+            assert np.array_equal(tb, pay[i, 0, :p.TBS[0] // 8]), i
+    fb.close()
+    cb.close()
+    rb.close()
