@@ -67,7 +67,7 @@ def main(prof_dir, tag, config, out_dir):
         lines.append(f"| {k} | {f:.0f} | {w:.0f} | {b/1e6:.1f} MB | {res.get(k)} |")
     os.makedirs(out_dir, exist_ok=True)
     open(os.path.join(out_dir, f"rocprof_{tag}_{config}.md"), "w").write("\n".join(lines) + "\n")
-    traffic["batch"] = int(os.environ.get("BATCH", {"C3": 8192, "C4": 1024, "C5": 2048, "FEP": 8192}.get(config, 0)))
+    traffic["batch"] = int(os.environ.get("BATCH", {"C3": 8192, "C4": 1024, "C5": 2048, "FEP": 8192, "UE": 4096}.get(config, 0)))
     json.dump(traffic, open(os.path.join(out_dir, f"traffic_{config}.json"), "w"), indent=1)
     for s in ("trace", "fetch", "write", "calfetch", "calwrite"):
         d = os.path.join(prof_dir, f"{s}_{tag}")
