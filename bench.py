@@ -170,6 +170,72 @@ def c5_llrs(n_cb, mode, seed):
     return np.stack([base[i % 64] for i in range(n_cb)])
 
 
+C5_TBS, C5_G, C5_QM = 43816, 57600, 4   # UL 100 PRB MCS 20: 12 data symbols x 1200 REs x 16-QAM
+
+
+def bench_c5_chain(args, world, rank, dist, torch):
+    """C5 from the e soft bits (ulsch_decoding.c:1208-1350): per TB of 8 x 5504 blocks, RX rate
+    matching + sub-block deinterleaving (k_ul_rm_deint) and the 16-bit decoder (k_td16);
+    unstructured soft bits, so every block runs the full 8 iterations."""
+    import numpy as np
+    import openair4g_amd as oai
+    n_sf = args.batch
+    rng = np.random.default_rng(0xC5E + rank)
+    e = rng.integers(-40, 41, size=(n_sf, C5_G)).astype(np.int16)
+    ub = oai.UlDecodeBatch(C5_TBS + 24, C5_G, C5_QM, n_sf, max_iterations=8)
+    ub.upload(e)
+    sid = torch.cuda.current_stream().cuda_stream
+    for _ in range(args.warmup):
+        ub.launch()
+    ub.results()
+    if dist is not None:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        ub.launch(stream=sid)
+    oai.lib().oai4g_sync()
+    torch.cuda.synchronize()
+    if dist is not None:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if dist is not None:
+        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    its, _ = ub.results()
+    ub.close()
+    value = n_sf * args.steps * world / elapsed
+    per_launch_ms = elapsed * 1000.0 / args.steps
+    alg = n_sf * (2 * C5_G + C5_CB * (C5_K // 8))           # soft bits read + decoded bytes written
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        sys.path.insert(0, os.path.join(ROOT, "tests"))
+        import oracle_lib as O
+        n, t1 = 0, time.perf_counter()
+        while time.perf_counter() - t1 < args.cpu_seconds:
+            O.ulsch_decode(e[n % n_sf], C5_TBS + 24, C5_G, C5_QM, max_it=8)
+            n += 1
+        dt = time.perf_counter() - t1
+        cpu = {"value": n / dt, "unit": "subframes/s", "cores": 1, "kind": "port",
+               "sample": f"{n} transport blocks (8 x K={C5_K}) through the C oracle chain (RM-rx, deinterleave, "
+                         f"decoder16), single thread, {dt:.1f} s"}
+    if rank == 0:
+        print(json.dumps({
+            "metric": "UL subframes/sec (C5 RM-rx + deinterleave + turbo decode)", "value": value,
+            "unit": "subframes/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+            "ms_per_step": per_launch_ms, "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+            "dtype": "int16", "data": "synthetic soft bits (unstructured: 8 iterations per block)",
+            "config": {"workload": "ulsch_decoding 20 MHz MCS20: G 57600 -> 8 x K=5504, max 8 iterations",
+                       "config_id": "C5", "subframes_per_gpu_per_step": n_sf, "mean_iterations": float(np.mean(its)),
+                       "parallelism": f"TB-sharded x{world}"},
+            "roofline": {"bound": "hbm", "kernel": "k_ul_rm_deint+k_td16", "achieved": alg / (per_launch_ms * 1e-3) / 1e9,
+                         "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": alg / (per_launch_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, "traffic": None,
+                         "algorithmic_bytes_per_launch": alg},
+            "cpu_baseline": cpu}), flush=True)
+
+
 def bench_c5(args, world, rank, dist, torch):
     """UL turbo decoding throughput (config C5): subframes of 8 code blocks, K = 5504."""
     import numpy as np
@@ -179,6 +245,8 @@ def bench_c5(args, world, rank, dist, torch):
     n_sf = args.batch
     n_cb = n_sf * C5_CB
     crc_type = 1                           # C > 1: per-block CRC24_B (ulsch_decoding.c)
+    if args.c5_mode == "chain":
+        return bench_c5_chain(args, world, rank, dist, torch)
     llr = c5_llrs(n_cb, args.c5_mode, 0xC5 + rank)
     dec = oai.TurboDecoderBatch(C5_K, n_cb)
     dec.upload(llr)
@@ -565,7 +633,8 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--kernel-reps", type=int, default=5, help="serial runs timed per kernel for the roofline")
-    ap.add_argument("--c5-mode", default="8it", choices=["8it", "snr"], help="C5 decoder inputs")
+    ap.add_argument("--c5-mode", default="8it", choices=["8it", "snr", "chain"],
+                    help="C5 decoder inputs; chain = from the e soft bits through RM-rx + deinterleaving")
     ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"], help="nccl = RCCL on ROCm")
     ap.add_argument("--cpu-stub", action="store_true",
                     help="harness test on CPU: gloo, StubPipeline, no GPU (exercises ranks/broadcast/timing)")

@@ -372,6 +372,28 @@ int oai4g_td_batch(int n_cb, uint16_t K, const int16_t *d_llr, size_t llr_stride
                    uint8_t *d_iters, uint8_t max_iterations, uint8_t crc_type, uint8_t F, void *d_scratch,
                    void *stream);
 
+/* generate_dummy_w (PHY/CODING/lte_rate_matching.c:293, decl CODING/defs.h): marks LTE_NULL in w at
+ * the NULL / filler positions of the 3 Kpi circular buffer of a block of D = K + 4 bits with F
+ * filler bits (other entries untouched, as the reference); returns R = ceil(D / 32). */
+uint32_t oai4g_generate_dummy_w(uint32_t D, uint8_t *w, uint8_t F);
+
+/* Batched UL receive chain of ulsch_decoding (PHY/LTE_TRANSPORT/ulsch_decoding.c:1208-1350) for
+ * n_tb transport blocks of one configuration (B = TBS + 24 bits, G soft bits, Qm, rvidx, first
+ * round: clear = 1, Nl = 1, Kmimo = 1): per code block r, lte_rate_matching_turbo_rx of the
+ * E_r soft bits at offset r_offset(r) of the TB's e stream, sub_block_deinterleaving_turbo and
+ * phy_threegpplte_turbo_decoder16 (CRC24_B when C > 1, else CRC24_A with the filler F).  Device
+ * pointers: d_e [n_tb][e_stride] int16, d_c [n_tb][C][c_stride] bytes (the reference's c[r],
+ * K_r / 8 each), d_iters [n_tb][C] (iterations, or max_iterations + 1 on a CRC failure). */
+typedef struct oai4g_ul_config oai4g_ul_config_t;
+oai4g_ul_config_t *oai4g_ul_config_create(uint32_t B, uint32_t G, uint8_t Qm, uint8_t rvidx, uint8_t Mdlharq,
+                                          uint32_t Nsoft, uint8_t max_iterations);
+void oai4g_ul_config_destroy(oai4g_ul_config_t *cfg);
+int oai4g_ul_config_C(const oai4g_ul_config_t *cfg);
+uint32_t oai4g_ul_config_E(const oai4g_ul_config_t *cfg, int r);
+uint32_t oai4g_ul_config_G_offset(const oai4g_ul_config_t *cfg, int r);
+int oai4g_ul_decode_batch(oai4g_ul_config_t *cfg, int n_tb, const int16_t *d_e, size_t e_stride, uint8_t *d_c,
+                          size_t c_stride, uint8_t *d_iters, void *stream);
+
 /* ---------------- batched device-resident transmit path ---------------- */
 /* Plain-old-data parameter block: what rank 0 broadcasts (RCCL) to the other ranks. */
 typedef struct {

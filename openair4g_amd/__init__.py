@@ -209,6 +209,15 @@ _SIGS = {
     "oai4g_chest_config_destroy": (None, [ctypes.c_void_p]),
     "oai4g_chest_batch": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p,
                                          ctypes.c_void_p]),
+    "oai4g_generate_dummy_w": (ctypes.c_uint32, [ctypes.c_uint32, ctypes.c_void_p, ctypes.c_uint8]),
+    "oai4g_ul_config_create": (ctypes.c_void_p, [ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint8, ctypes.c_uint8,
+                                                 ctypes.c_uint8, ctypes.c_uint32, ctypes.c_uint8]),
+    "oai4g_ul_config_destroy": (None, [ctypes.c_void_p]),
+    "oai4g_ul_config_C": (ctypes.c_int, [ctypes.c_void_p]),
+    "oai4g_ul_config_E": (ctypes.c_uint32, [ctypes.c_void_p, ctypes.c_int]),
+    "oai4g_ul_config_G_offset": (ctypes.c_uint32, [ctypes.c_void_p, ctypes.c_int]),
+    "oai4g_ul_decode_batch": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_size_t,
+                                             ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p, ctypes.c_void_p]),
     "oai4g_dft": (ctypes.c_int, [ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int]),
     "oai4g_dft2048": (None, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int]),
     "oai4g_dft1024": (None, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int]),
@@ -651,6 +660,61 @@ def sub_block_deinterleaving_turbo(D, w):
     lib().oai4g_sub_block_deinterleaving_turbo(D, ctypes.c_void_p(buf.ctypes.data + 2 * 96),
                                                _ptr(np.ascontiguousarray(w, dtype=np.int16)))
     return buf
+
+
+def generate_dummy_w(D, F=0):
+    """generate_dummy_w: the uint8 NULL-mark buffer (3 Kpi) of a block of D = K + 4 with F fillers."""
+    R = (D + 31) >> 5
+    w = np.zeros(3 * 32 * R + 64, dtype=np.uint8)
+    lib().oai4g_generate_dummy_w(D, _ptr(w), F)
+    return w
+
+
+class UlDecodeBatch:
+    """Batched ulsch_decoding chain (oai4g_ul_decode_batch): n_tb transport blocks of B = TBS + 24
+    bits, G soft bits each -> RM-rx + deinterleaving + 16-bit turbo decoding per code block."""
+
+    def __init__(self, B, G, Qm, n_tb, rvidx=0, max_iterations=8, Mdlharq=8, Nsoft=1827072):
+        init()
+        self.L = lib()
+        self.cfg = self.L.oai4g_ul_config_create(B, G, Qm, rvidx, Mdlharq, Nsoft, max_iterations)
+        _check(bool(self.cfg))
+        self.C = self.L.oai4g_ul_config_C(self.cfg)
+        self.n_tb, self.G = n_tb, G
+        self.e_stride = (G + 63) & ~63
+        self.c_stride = 6144 // 8 + 8
+        self.d_e = self.L.oai4g_dev_alloc(n_tb * self.e_stride * 2)
+        self.d_c = self.L.oai4g_dev_alloc(n_tb * self.C * self.c_stride)
+        self.d_it = self.L.oai4g_dev_alloc(n_tb * self.C)
+        _check(bool(self.d_e) and bool(self.d_c) and bool(self.d_it))
+
+    def E(self, r):
+        return self.L.oai4g_ul_config_E(self.cfg, r)
+
+    def offset(self, r):
+        return self.L.oai4g_ul_config_G_offset(self.cfg, r)
+
+    def upload(self, e):
+        buf = np.zeros((self.n_tb, self.e_stride), dtype=np.int16)
+        buf[:, :self.G] = np.asarray(e, dtype=np.int16).reshape(self.n_tb, -1)[:, :self.G]
+        _check(self.L.oai4g_memcpy_h2d(self.d_e, _ptr(buf), buf.nbytes) == 0)
+
+    def launch(self, stream=None):
+        _check(self.L.oai4g_ul_decode_batch(self.cfg, self.n_tb, self.d_e, self.e_stride, self.d_c, self.c_stride,
+                                            self.d_it, stream) == 0)
+
+    def results(self):
+        _check(self.L.oai4g_sync() == 0)
+        c = np.empty((self.n_tb, self.C, self.c_stride), dtype=np.uint8)
+        it = np.empty((self.n_tb, self.C), dtype=np.uint8)
+        _check(self.L.oai4g_memcpy_d2h(_ptr(c), self.d_c, c.nbytes) == 0)
+        _check(self.L.oai4g_memcpy_d2h(_ptr(it), self.d_it, it.nbytes) == 0)
+        return it, c
+
+    def close(self):
+        for p in (self.d_e, self.d_c, self.d_it):
+            self.L.oai4g_dev_free(p)
+        self.L.oai4g_ul_config_destroy(self.cfg)
 
 
 class TurboDecoderBatch:

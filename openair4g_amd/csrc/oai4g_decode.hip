@@ -336,22 +336,26 @@ __device__ static const uint32_t *td_crc_tab(uint32_t *lds, uint32_t poly)
 
 /*
  * Batch decoder: blockIdx.x decodes blocks 8 blockIdx.x .. +7 (one 64-lane wave).
- * llr: [n_cb][llr_stride] int16 (3K + 12 each), out: [n_cb][out_stride] bytes, iters: [n_cb].
+ * llr: [..][llr_stride] int16 (3K + 12 each), out: [..][out_stride] bytes, iters: [..].  Block cb
+ * of the launch lives at slot (cb / cg) c_per + r0 + cb % cg of those arrays: the identity for
+ * cg = c_per = 1, r0 = 0; the code blocks r0 .. r0 + cg - 1 of every transport block of a
+ * [tb][C] batch otherwise (one launch per block size).
  */
 __global__ void __launch_bounds__(64) k_td16(int n_cb, uint32_t K, const int16_t *__restrict__ llr, size_t llr_stride,
                                              uint8_t *__restrict__ out, size_t out_stride, uint8_t *__restrict__ iters,
                                              uint32_t max_it, uint32_t crc_type, uint32_t F,
                                              const uint16_t *__restrict__ pi4, const uint16_t *__restrict__ pi5,
                                              const uint16_t *__restrict__ pi6, uint8_t *__restrict__ scratch,
-                                             size_t blk_bytes)
+                                             size_t blk_bytes, uint32_t cg, uint32_t c_per, uint32_t r0)
 {
   __shared__ uint32_t crctab[256];
   __shared__ uint8_t dec[8][6144 / 8 + 8];
   __shared__ uint32_t done_it[8];
   __shared__ uint4 asave[6 * 64];
   const uint32_t lane = threadIdx.x, g = lane >> 3, q = lane & 7;
-  const int cb = (int)(blockIdx.x * 8 + g);
-  const bool valid = cb < n_cb;
+  const int cbl = (int)(blockIdx.x * 8 + g);
+  const bool valid = cbl < n_cb;
+  const size_t cb = (size_t)(cbl / (int)cg) * c_per + r0 + (uint32_t)cbl % cg;   /* slot in llr / out / iters */
   const uint32_t K1 = K >> 3, Kb = K >> 3;
   td_crc_tab(crctab, crc_type == 0 ? 0x864cfbu : 0x800063u);
   if (lane < 8) done_it[lane] = 0;
@@ -361,7 +365,7 @@ __global__ void __launch_bounds__(64) k_td16(int n_cb, uint32_t K, const int16_t
   B.ext = W.ext + 8 * g; B.ext2 = W.ext2 + 8 * g; B.A = W.A + 8 * g;
   if (valid) {
     /* demux (:1038-1158): bit i = window q, step v -> element 8v + q */
-    gs16_t *y = (gs16_t *)(llr + (size_t)cb * llr_stride);
+    gs16_t *y = (gs16_t *)(llr + cb * llr_stride);
     for (uint32_t v0 = 0; v0 < K1; v0 += 8) {   /* 8 steps per round: all loads, then all stores */
       short t0[8], t1[8], t2[8];
 #pragma unroll
@@ -457,7 +461,7 @@ __global__ void __launch_bounds__(64) k_td16(int n_cb, uint32_t K, const int16_t
             for (int bb = 0; bb < 8; bb++) byte |= (uint32_t)(x[8 * h + bb] > 0) << (7 - bb);
             if (i < Kb) {
               dec[g][i] = (uint8_t)byte;
-              out[(size_t)cb * out_stride + i] = (uint8_t)byte;
+              out[cb * out_stride + i] = (uint8_t)byte;
             }
           }
         }
@@ -484,11 +488,13 @@ __global__ void __launch_bounds__(64) k_td16(int n_cb, uint32_t K, const int16_t
 
 hipError_t oai4g_launch_td16(int n_cb, uint32_t K, const int16_t *d_llr, size_t llr_stride, uint8_t *d_out,
                              size_t out_stride, uint8_t *d_iters, uint32_t max_it, uint32_t crc_type, uint32_t F,
-                             const uint16_t *d_pi, uint8_t *d_scratch, hipStream_t s)
+                             const uint16_t *d_pi, uint8_t *d_scratch, hipStream_t s, uint32_t cg, uint32_t c_per,
+                             uint32_t r0)
 {
   if (n_cb <= 0) return hipSuccess;
   hipLaunchKernelGGL(k_td16, dim3((n_cb + 7) / 8), dim3(64), 0, s, n_cb, K, d_llr, llr_stride, d_out, out_stride,
-                     d_iters, max_it, crc_type, F, d_pi, d_pi + K, d_pi + 2 * K, d_scratch, oai4g_td_block_bytes(K));
+                     d_iters, max_it, crc_type, F, d_pi, d_pi + K, d_pi + 2 * K, d_scratch, oai4g_td_block_bytes(K), cg,
+                     c_per, r0);
   return hipGetLastError();
 }
 
@@ -526,6 +532,43 @@ __global__ void __launch_bounds__(256) k_subblock_deint(uint32_t D, int16_t *__r
   d1[index3] = w[k];
   d1[index3 + 1] = w[Kpi + 2 * k];
   d1[index3 + 5] = w[Kpi + 2 * k + 1];
+}
+
+/* ulsch_decoding's per-block RX chain fused (ulsch_decoding.c:1208-1287), one thread per entry i of
+ * code block j's deinterleaved d buffer (blockIdx.y = j: tb = j / C, r = j % C), so the stores are
+ * contiguous.  sub_block_deinterleaving_turbo puts w[k] at d1[index3], w[Kpi + 2k] at
+ * d1[index3 + 1] and w[Kpi + 2k + 1] at d1[index3 + 5] (index3 = 3 bitrev5(col) + 96 row,
+ * k = col R + row, d1 = dfull + 96 - 3 ND); inverting that gives the w position p of entry i, whose
+ * value is lte_rate_matching_turbo_rx's (clear = 1): the int16 wrap sum of the soft inputs the
+ * circular selection maps to p, 0 for NULL positions.  d1[2] is never written (the reference's
+ * prefix slot), d1[3 Kpi + 2] is the d[3D + 2] entry the +5 of the last column produces. */
+__global__ void __launch_bounds__(256) k_ul_rm_deint(const ul_dev_t *__restrict__ c, const int16_t *__restrict__ e,
+                                                     size_t e_stride, int16_t *__restrict__ dfull, size_t d_stride)
+{
+  const uint32_t j = blockIdx.y, tb = j / c->C, r = j - tb * c->C;
+  const ul_pat_t &P = c->pat[c->pat_of[r]];
+  const uint32_t R = P.R, Kpi = R << 5, i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= 3 * Kpi + 3 || i == 2) return;
+  const uint32_t sft = i % 3, base = sft == 2 ? i - 5 : i, row = base / 96, cp = (base % 96) / 3;
+  if (row >= R) return;
+  const uint32_t k = (__builtin_bitreverse32(cp) >> 27) * R + row;
+  const uint32_t p = sft == 0 ? k : Kpi + 2 * k + (sft == 2 ? 1 : 0);
+  int16_t acc = 0;
+  if (p < P.Ncb && P.dummy[p] != OAI4G_LTE_NULL) {
+    const int16_t *soft = e + tb * e_stride + c->off[r];
+    const uint32_t ci = P.cidx[p], E = c->E[r];
+    for (uint32_t q = ci >= P.k0c ? ci - P.k0c : ci + P.Nnn - P.k0c; q < E; q += P.Nnn) acc = (int16_t)(acc + soft[q]);
+  }
+  dfull[(size_t)j * d_stride + 96 - 3 * (Kpi - P.D) + i] = acc;
+}
+
+hipError_t oai4g_launch_ul_rm_deint(const ul_dev_t *d_cfg, const ul_dev_t *h_cfg, int n_tb, const int16_t *d_e,
+                                    size_t e_stride, int16_t *d_dfull, size_t d_stride, hipStream_t s)
+{
+  if (n_tb <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_ul_rm_deint, dim3((3 * (h_cfg->Rmax << 5) + 3 + 255) / 256, n_tb * h_cfg->C), dim3(256), 0, s, d_cfg,
+                     d_e, e_stride, d_dfull, d_stride);
+  return hipGetLastError();
 }
 
 hipError_t oai4g_launch_rm_rx(const int16_t *d_soft, uint32_t E, int16_t *d_w, const uint8_t *d_dummy,

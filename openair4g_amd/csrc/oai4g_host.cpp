@@ -1721,6 +1721,174 @@ extern "C" int oai4g_td_batch(int n_cb, uint16_t K, const int16_t *d_llr, size_t
   return 0;
 }
 
+/* generate_dummy_w (lte_rate_matching.c:293-382): LTE_NULL marks of the 3 Kpi circular buffer of a
+ * block of D = K + 4 bits with F filler bits; returns R (RTC) */
+static uint32_t dummy_w_h(uint32_t D, uint32_t F, std::vector<uint8_t> &w)
+{
+  const uint32_t R = (D >> 5) + ((D & 31) ? 1 : 0), Kpi = R << 5, ND = Kpi - D;
+  w.assign(3 * (size_t)Kpi, 0);
+  for (uint32_t col = 0, k = 0; col < 32; col++, k += R) {
+    const uint32_t index = __builtin_bitreverse32(col) >> 27;
+    if (index < ND + F) { w[k] = OAI4G_LTE_NULL; w[Kpi + 2 * k] = OAI4G_LTE_NULL; }
+    if (index + 32 < ND + F) { w[k + 1] = OAI4G_LTE_NULL; w[Kpi + 2 + 2 * k] = OAI4G_LTE_NULL; }
+    if (index + 64 < ND + F) { w[k + 2] = OAI4G_LTE_NULL; w[Kpi + 4 + 2 * k] = OAI4G_LTE_NULL; }
+    if (index + 1 < ND) w[Kpi + 1 + 2 * k] = OAI4G_LTE_NULL;
+  }
+  if (ND > 0) w[3 * Kpi - 1] = OAI4G_LTE_NULL;
+  return R;
+}
+
+extern "C" uint32_t oai4g_generate_dummy_w(uint32_t D, uint8_t *w, uint8_t F)
+{
+  std::vector<uint8_t> v;
+  const uint32_t R = dummy_w_h(D, F, v);
+  for (size_t i = 0; i < v.size(); i++)
+    if (v[i] == OAI4G_LTE_NULL) w[i] = OAI4G_LTE_NULL;   /* the reference only writes the NULL marks */
+  return R;
+}
+
+/* ------------------------------------------------------------------------------------------
+ * Batched UL receive chain (ulsch_decoding.c:1208-1350): n_tb transport blocks of one
+ * configuration, e soft bits -> RM-rx + sub-block deinterleaving (k_ul_rm_deint) -> 16-bit turbo
+ * decoding (k_td16, one launch per block size) with CRC24B / CRC24A early stop.
+ * ---------------------------------------------------------------------------------------- */
+struct oai4g_ul_config {
+  ul_dev_t h;
+  ul_dev_t *d = nullptr;
+  uint32_t B, G, C, Cminus, Kminus, Kplus, F, max_it;
+  std::vector<void *> dev;
+  size_t d_stride = 0;
+  int cap = 0;
+  int16_t *d_dfull = nullptr;
+  uint8_t *d_td = nullptr;
+};
+
+extern "C" void oai4g_ul_config_destroy(oai4g_ul_config_t *cfg)
+{
+  if (!cfg) return;
+  for (void *p : cfg->dev) hipFree(p);
+  if (cfg->d_dfull) hipFree(cfg->d_dfull);
+  if (cfg->d_td) hipFree(cfg->d_td);
+  if (cfg->d) hipFree(cfg->d);
+  delete cfg;
+}
+
+extern "C" oai4g_ul_config_t *oai4g_ul_config_create(uint32_t B, uint32_t G, uint8_t Qm, uint8_t rvidx, uint8_t Mdlharq,
+                                                     uint32_t Nsoft, uint8_t max_iterations)
+{
+  NEED_INIT(nullptr);
+  auto *cfg = new oai4g_ul_config();
+  uint32_t Cplus, L;
+  if (Qm == 0 || Mdlharq == 0 || rvidx > 3 ||
+      seg_params(B, &cfg->C, &Cplus, &cfg->Cminus, &cfg->Kplus, &cfg->Kminus, &cfg->F, &L) < 0 ||
+      cfg->C > OAI4G_UL_MAX_C || (cfg->F & 7) || cfg->F + 24 > cfg->Kplus) {
+    set_err("ul_config: unsupported (B %u, Qm %u, rv %u, Mdlharq %u)", B, Qm, rvidx, Mdlharq);
+    delete cfg;
+    return nullptr;
+  }
+  cfg->B = B;
+  cfg->G = G;
+  cfg->max_it = max_iterations;
+  ul_dev_t &h = cfg->h;
+  memset(&h, 0, sizeof(h));
+  h.C = cfg->C;
+  const uint32_t C = cfg->C, Nir = Nsoft / (Mdlharq < 8 ? Mdlharq : 8), Gp = G / Qm, GpmodC = Gp % C;
+  uint32_t off = 0, npat = 0, keyK[3] = {0, 0, 0}, keyF[3] = {0, 0, 0};
+  for (uint32_t r = 0; r < C; r++) {
+    h.E[r] = r < C - GpmodC ? Qm * (Gp / C) : Qm * ((GpmodC == 0 ? 0 : 1) + Gp / C);   /* Nl = 1 */
+    h.off[r] = off;
+    off += h.E[r];
+    const uint32_t K = r < cfg->Cminus ? cfg->Kminus : cfg->Kplus, Fr = r == 0 ? cfg->F : 0;
+    uint32_t pi = 0;
+    while (pi < npat && !(keyK[pi] == K && keyF[pi] == Fr)) pi++;
+    if (pi == npat) {
+      keyK[npat] = K;
+      keyF[npat] = Fr;
+      ul_pat_t &P = h.pat[npat++];
+      std::vector<uint8_t> dw;
+      P.D = K + 4;
+      P.R = dummy_w_h(P.D, Fr, dw);
+      const uint32_t Kw = 3 * (P.R << 5);
+      P.Ncb = Nir / C < Kw ? Nir / C : Kw;
+      const uint32_t Ncbmod = P.Ncb % (P.R << 3);
+      const uint32_t k0 = P.R * (2 + (rvidx * (((Ncbmod == 0) ? 0 : 1) + (P.Ncb / (P.R << 3))) * 2));
+      std::vector<uint32_t> cidx(P.Ncb);
+      uint32_t nn = 0, k0c = 0;
+      for (uint32_t q = 0; q < P.Ncb; q++) {
+        if (q == k0) k0c = nn;
+        cidx[q] = nn;
+        if (dw[q] != OAI4G_LTE_NULL) nn++;
+      }
+      if (k0 >= P.Ncb) k0c = 0;
+      P.Nnn = nn;
+      P.k0c = k0c;
+      if (P.R > h.Rmax) h.Rmax = P.R;
+      uint8_t *dd = nullptr;
+      uint32_t *dc = nullptr;
+      if (hipMalloc(&dd, dw.size()) != hipSuccess || hipMalloc(&dc, cidx.size() * 4) != hipSuccess ||
+          hipMemcpy(dd, dw.data(), dw.size(), hipMemcpyHostToDevice) != hipSuccess ||
+          hipMemcpy(dc, cidx.data(), cidx.size() * 4, hipMemcpyHostToDevice) != hipSuccess) {
+        if (dd) cfg->dev.push_back(dd);
+        if (dc) cfg->dev.push_back(dc);
+        set_err("ul_config: device allocation failed");
+        oai4g_ul_config_destroy(cfg);
+        return nullptr;
+      }
+      cfg->dev.push_back(dd);
+      cfg->dev.push_back(dc);
+      P.dummy = dd;
+      P.cidx = dc;
+    }
+    h.pat_of[r] = pi;
+  }
+  if (!td_tables(cfg->Kplus) || (cfg->Cminus && !td_tables(cfg->Kminus))) { oai4g_ul_config_destroy(cfg); return nullptr; }
+  cfg->d_stride = (96 + 3 * (size_t)cfg->Kplus + 12 + 15) & ~(size_t)15;
+  if (hipMalloc(&cfg->d, sizeof(ul_dev_t)) != hipSuccess ||
+      hipMemcpy(cfg->d, &h, sizeof(ul_dev_t), hipMemcpyHostToDevice) != hipSuccess) {
+    set_err("ul_config: upload failed");
+    oai4g_ul_config_destroy(cfg);
+    return nullptr;
+  }
+  return cfg;
+}
+
+extern "C" int oai4g_ul_config_C(const oai4g_ul_config_t *cfg) { return (int)cfg->C; }
+extern "C" uint32_t oai4g_ul_config_G_offset(const oai4g_ul_config_t *cfg, int r) { return cfg->h.off[r]; }
+extern "C" uint32_t oai4g_ul_config_E(const oai4g_ul_config_t *cfg, int r) { return cfg->h.E[r]; }
+
+extern "C" int oai4g_ul_decode_batch(oai4g_ul_config_t *cfg, int n_tb, const int16_t *d_e, size_t e_stride,
+                                     uint8_t *d_c, size_t c_stride, uint8_t *d_iters, void *stream)
+{
+  NEED_INIT(-1);
+  if (n_tb <= 0) return 0;
+  if (c_stride < cfg->Kplus / 8 || e_stride < cfg->G) { set_err("ul_decode_batch: strides too small"); return -1; }
+  if (n_tb > cfg->cap) {
+    if (cfg->d_dfull) hipFree(cfg->d_dfull);
+    if (cfg->d_td) hipFree(cfg->d_td);
+    cfg->d_dfull = nullptr;
+    cfg->d_td = nullptr;
+    const size_t nb = (size_t)n_tb * cfg->C;
+    const size_t td = oai4g_td_scratch_bytes((uint16_t)cfg->Kplus, (int)nb);
+    if (hipMalloc(&cfg->d_dfull, nb * cfg->d_stride * 2) != hipSuccess || hipMalloc(&cfg->d_td, td) != hipSuccess) {
+      set_err("ul_decode_batch: device allocation failed");
+      cfg->cap = 0;
+      return -1;
+    }
+    cfg->cap = n_tb;
+  }
+  hipStream_t s = (hipStream_t)stream;
+  HCK(oai4g_launch_ul_rm_deint(cfg->d, &cfg->h, n_tb, d_e, e_stride, cfg->d_dfull, cfg->d_stride, s), -1);
+  const uint32_t crc = cfg->C == 1 ? OAI4G_CRC24_A : OAI4G_CRC24_B, F = cfg->C == 1 ? cfg->F : 0;
+  const int16_t *y = cfg->d_dfull + 96;
+  if (cfg->Cminus)
+    HCK(oai4g_launch_td16(n_tb * (int)cfg->Cminus, cfg->Kminus, y, cfg->d_stride, d_c, c_stride, d_iters, cfg->max_it,
+                          crc, F, td_tables(cfg->Kminus), cfg->d_td, s, cfg->Cminus, cfg->C, 0), -1);
+  HCK(oai4g_launch_td16(n_tb * (int)(cfg->C - cfg->Cminus), cfg->Kplus, y, cfg->d_stride, d_c, c_stride, d_iters,
+                        cfg->max_it, crc, F, td_tables(cfg->Kplus), cfg->d_td, s, cfg->C - cfg->Cminus, cfg->C,
+                        cfg->Cminus), -1);
+  return 0;
+}
+
 extern "C" uint8_t oai4g_phy_threegpplte_turbo_decoder16(const int16_t *y, uint8_t *decoded_bytes, uint16_t n,
                                                          uint16_t f1, uint16_t f2, uint8_t max_iterations,
                                                          uint8_t crc_type, uint8_t F)

@@ -176,7 +176,23 @@ hipError_t oai4g_launch_diag_stream(const void *src, void *dst, size_t bytes, in
 size_t oai4g_td_block_bytes(uint32_t K);
 hipError_t oai4g_launch_td16(int n_cb, uint32_t K, const int16_t *d_llr, size_t llr_stride, uint8_t *d_out,
                              size_t out_stride, uint8_t *d_iters, uint32_t max_it, uint32_t crc_type, uint32_t F,
-                             const uint16_t *d_pi /* pi4 | pi5 | pi6, K each */, uint8_t *d_scratch, hipStream_t s);
+                             const uint16_t *d_pi /* pi4 | pi5 | pi6, K each */, uint8_t *d_scratch, hipStream_t s,
+                             uint32_t cg = 1, uint32_t c_per = 1, uint32_t r0 = 0);
+/* batched UL receive chain (ulsch_decoding.c:1208-1350): per code-block pattern (block size,
+ * filler) the NULL map and compact indices of the rate-matching circular buffer */
+#define OAI4G_UL_MAX_C 16
+struct ul_pat_t {
+  uint32_t D, R, Ncb, Nnn, k0c;
+  const uint8_t *dummy;            /* [3 R 32] LTE_NULL marks */
+  const uint32_t *cidx;            /* [Ncb] compact index */
+};
+struct ul_dev_t {
+  uint32_t C, Rmax;
+  uint32_t E[OAI4G_UL_MAX_C], off[OAI4G_UL_MAX_C], pat_of[OAI4G_UL_MAX_C];
+  ul_pat_t pat[3];
+};
+hipError_t oai4g_launch_ul_rm_deint(const ul_dev_t *d_cfg, const ul_dev_t *h_cfg, int n_tb, const int16_t *d_e,
+                                    size_t e_stride, int16_t *d_dfull, size_t d_stride, hipStream_t s);
 hipError_t oai4g_launch_rm_rx(const int16_t *d_soft, uint32_t E, int16_t *d_w, const uint8_t *d_dummy,
                               const uint32_t *d_cidx, uint32_t Ncb, uint32_t Nnn, uint32_t k0c, int clear, hipStream_t s);
 hipError_t oai4g_launch_subblock_deint(uint32_t D, int16_t *d_dfull, const int16_t *d_w, hipStream_t s);

@@ -159,6 +159,7 @@ enum { ORC_CRC24_A = 0, ORC_CRC24_B = 1, ORC_CRC16 = 2, ORC_CRC8 = 3 };
 uint8_t orc_turbo_decoder16(const int16_t *y, uint8_t *decoded_bytes, uint16_t n, uint8_t max_iterations,
                             uint8_t crc_type, uint8_t F);
 uint32_t orc_generate_dummy_w(uint32_t D, uint8_t *w);
+uint32_t orc_generate_dummy_w_F(uint32_t D, uint8_t *w, uint8_t F);
 int orc_rate_matching_turbo_rx(uint32_t RTC, uint32_t G, int16_t *w, const uint8_t *dummy_w, const int16_t *soft_input,
                                uint8_t C, uint32_t Nsoft, uint8_t Mdlharq, uint8_t Kmimo, uint8_t rvidx, uint8_t clear,
                                uint8_t Qm, uint8_t Nl, uint8_t r, uint32_t *E_out);

@@ -284,6 +284,31 @@ uint32_t orc_generate_dummy_w(uint32_t D, uint8_t *w)
   return orc_subblock_interleave(D, dbuf + 96, w);
 }
 
+/* generate_dummy_w with filler bits (lte_rate_matching.c:293-382): only the NULL marks are written;
+ * rows 0..2 of a column carry the ND + F NULL / filler positions of the systematic and first
+ * parity streams, the second parity's ND NULLs sit one position later (index + 1 < ND) */
+uint32_t orc_generate_dummy_w_F(uint32_t D, uint8_t *w, uint8_t F)
+{
+  static const uint8_t bitrev[32] = {0, 16, 8, 24, 4, 20, 12, 28, 2, 18, 10, 26, 6, 22, 14, 30,
+                                     1, 17, 9, 25, 5, 21, 13, 29, 3, 19, 11, 27, 7, 23, 15, 31};
+  uint32_t RTC = D >> 5;
+  if (D & 0x1f) RTC++;
+  const uint32_t Kpi = RTC << 5, ND = Kpi - D;
+  uint8_t *wKpi = &w[Kpi], *wKpi1 = &w[Kpi + 1], *wKpi2 = &w[Kpi + 2], *wKpi4 = &w[Kpi + 4];
+  uint32_t k = 0, k2 = 0;
+  for (uint32_t col = 0; col < 32; col++) {
+    const uint32_t index = bitrev[col];
+    if (index < ND + F) { w[k] = ORC_LTE_NULL; wKpi[k2] = ORC_LTE_NULL; }
+    if (index + 32 < ND + F) { w[k + 1] = ORC_LTE_NULL; wKpi2[k2] = ORC_LTE_NULL; }
+    if (index + 64 < ND + F) { w[k + 2] = ORC_LTE_NULL; wKpi4[k2] = ORC_LTE_NULL; }
+    if (index + 1 < ND) wKpi1[k2] = ORC_LTE_NULL;
+    k += RTC;
+    k2 = k << 1;
+  }
+  if (ND > 0) w[3 * Kpi - 1] = ORC_LTE_NULL;
+  return RTC;
+}
+
 /* lte_rate_matching_turbo_rx (lte_rate_matching.c:688-831): w[ind] += soft (int16 wrap) */
 int orc_rate_matching_turbo_rx(uint32_t RTC, uint32_t G, int16_t *w, const uint8_t *dummy_w, const int16_t *soft_input,
                                uint8_t C, uint32_t Nsoft, uint8_t Mdlharq, uint8_t Kmimo, uint8_t rvidx, uint8_t clear,

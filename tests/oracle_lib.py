@@ -330,11 +330,19 @@ def dummy_w(D):
     return w
 
 
-def rate_match_rx(soft, K, G, C, r, Qm, rvidx=0, Nl=1, Kmimo=1, Mdlharq=8, w=None, clear=1, Nsoft=1827072):
+def dummy_w_F(D, F):
+    """generate_dummy_w(D, w, F) of lte_rate_matching.c:293 (filler-aware NULL marks)."""
+    R = (D + 31) >> 5
+    w = np.zeros(3 * 32 * R + 64, dtype=np.uint8)
+    orc().orc_generate_dummy_w_F(D, P(w), F)
+    return w
+
+
+def rate_match_rx(soft, K, G, C, r, Qm, rvidx=0, Nl=1, Kmimo=1, Mdlharq=8, w=None, clear=1, Nsoft=1827072, dw=None):
     """lte_rate_matching_turbo_rx: returns (w int16, E)."""
     D = K + 4
     R = (D + 31) >> 5
-    dw = dummy_w(D)
+    dw = dummy_w(D) if dw is None else dw
     if w is None:
         w = np.zeros(3 * 32 * R + 64, dtype=np.int16)
     soft = np.ascontiguousarray(soft, dtype=np.int16)
@@ -539,3 +547,23 @@ def chest_subframe(fp, rxF, rxF_next0, sf, p=0):
     dl_channel_estimation(fp, g, nxt, est, (2 * sf + 2) % 20, p, 0, 0)
     est[:N] = row0
     return est
+
+
+def ulsch_decode(e, B, G, Qm, rvidx=0, max_it=8, Mdlharq=8):
+    """ulsch_decoding.c:1208-1350 on one TB's soft bits e (first round): per code block r,
+    generate_dummy_w(4 + K_r, F if r == 0), lte_rate_matching_turbo_rx (clear), sub-block
+    deinterleaving, phy_threegpplte_turbo_decoder16 (CRC24_B if C > 1 else CRC24_A with F).
+    Returns [(iterations, bytes K_r / 8)] per block."""
+    import spec_model as S
+    blocks, F = S.segment([0] * B)
+    C = len(blocks)
+    e = np.ascontiguousarray(e, dtype=np.int16)
+    off, out = 0, []
+    for r, blk in enumerate(blocks):
+        K = len(blk)
+        dw = dummy_w_F(K + 4, F if r == 0 else 0)
+        w, E = rate_match_rx(e[off:], K, G, C, r, Qm, rvidx=rvidx, Mdlharq=Mdlharq, dw=dw)
+        off += E
+        d = subblock_deinterleave(w, K)
+        out.append(turbo_decode(d, K, max_it=max_it, crc_type=1 if C > 1 else 0, F=(F if C == 1 else 0)))
+    return out
