@@ -416,8 +416,11 @@ def bench_ue(args, world, rank, dist, torch):
 
     def step(stream):
         fb.run(stream=stream)
-        cb.launch(fb.d_rxF, stream=stream)
-        rb.launch(fb.d_rxF, cb.d_est, 1, stream=stream)
+        if args.ue_unfused:
+            cb.launch(fb.d_rxF, stream=stream)
+            rb.launch(fb.d_rxF, cb.d_est, 1, stream=stream)
+        else:
+            rb.launch_estimated(cb, fb.d_rxF, 1, stream=stream)
     for _ in range(args.warmup):
         step(None)
     oai.lib().oai4g_sync()
@@ -437,8 +440,12 @@ def bench_ue(args, world, rank, dist, torch):
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     # per-stage launch durations (HIP events on the launch stream)
-    stages = {"k_fep": lambda: fb.run(stream=sid), "k_chest": lambda: cb.launch(fb.d_rxF, stream=sid),
-              "k_rx_level+k_rx_llr": lambda: rb.launch(fb.d_rxF, cb.d_est, 1, stream=sid)}
+    if args.ue_unfused:
+        stages = {"k_fep": lambda: fb.run(stream=sid), "k_chest": lambda: cb.launch(fb.d_rxF, stream=sid),
+                  "k_rx_level+k_rx_llr": lambda: rb.launch(fb.d_rxF, cb.d_est, 1, stream=sid)}
+    else:
+        stages = {"k_fep": lambda: fb.run(stream=sid),
+                  "k_rx_chest": lambda: rb.launch_estimated(cb, fb.d_rxF, 1, stream=sid)}
     kern_ms = {}
     for name, fn in stages.items():
         evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
@@ -453,7 +460,9 @@ def bench_ue(args, world, rank, dist, torch):
     n_re = n_llr // Qm
     alg = {"k_fep": (n_sf + 1) * (spt * 4 + nsym * N * 4),                 # IQ read + frequency grid written
            "k_chest": n_sf * (nsym * N * 4 + 5 * N * 4),                     # 14 rows written + 5 pilot rows read
-           "k_rx_level+k_rx_llr": n_re * 8 + n_llr * 2 + n_sf * 1200 * 4}    # y + h per RE, LLRs, level row
+           "k_rx_level+k_rx_llr": n_re * 8 + n_llr * 2 + n_sf * 1200 * 4,    # y + h per RE, LLRs, level row
+           "k_rx_chest": n_re * 4 + n_llr * 2 + n_sf * 5 * 1200 * 4}         # y per RE, LLRs, 5 pilot rows
+    alg = {k: v for k, v in alg.items() if k in stages}
     fb.close()
     cb.close()
     rb.close()
@@ -491,7 +500,9 @@ def bench_ue(args, world, rank, dist, torch):
             "unit": "subframes/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
             "ms_per_step": elapsed * 1000.0 / args.steps, "higher_is_better": True, "scaling": "weak",
             "vs_baseline": None, "dtype": "int16", "data": "GPU-transmitted C2 subframes (synthetic payload), resident in HBM",
-            "config": {"workload": "slot_fep + lte_dl_channel_estimation + rx_pdsch + dlsch_unscrambling, C2 20 MHz",
+            "config": {"workload": "slot_fep + lte_dl_channel_estimation + rx_pdsch + dlsch_unscrambling, C2 20 MHz"
+                                   + (" (estimation and demodulation as separate kernels)" if args.ue_unfused else
+                                      " (estimation fused into the demodulator)"),
                        "config_id": "UE", "subframes_per_gpu_per_step": n_sf, "parallelism": f"subframe-sharded x{world}"},
             "roofline": {"bound": "hbm", "kernel": dom, "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": ach / HBM_PEAK_GBS, "traffic": _stage_traffic("UE", dom, n_sf), "kernel_ms": kern_ms,
@@ -635,6 +646,7 @@ def main():
     ap.add_argument("--kernel-reps", type=int, default=5, help="serial runs timed per kernel for the roofline")
     ap.add_argument("--c5-mode", default="8it", choices=["8it", "snr", "chain"],
                     help="C5 decoder inputs; chain = from the e soft bits through RM-rx + deinterleaving")
+    ap.add_argument("--ue-unfused", action="store_true", help="UE: estimate buffer + separate demodulation kernels")
     ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"], help="nccl = RCCL on ROCm")
     ap.add_argument("--cpu-stub", action="store_true",
                     help="harness test on CPU: gloo, StubPipeline, no GPU (exercises ranks/broadcast/timing)")

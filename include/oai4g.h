@@ -285,6 +285,12 @@ oai4g_chest_config_t *oai4g_chest_config_create(const oai4g_frame_parms_t *frame
                                                 uint8_t first_subframe, uint8_t subframe_step);
 void oai4g_chest_config_destroy(oai4g_chest_config_t *cfg);
 int oai4g_chest_batch(oai4g_chest_config_t *cfg, int n_sf, const int32_t *d_rxdataF, int32_t *d_est, void *stream);
+/* The batch chain without the estimate buffer: oai4g_chest_batch followed by oai4g_rx_batch, fused
+ * (the estimate of each PDSCH RE is formed in LDS from the pilot rows), same LLRs; d_rxdataF as
+ * for oai4g_chest_batch (n_sf subframes + the next symbol 0).  rx and ce describe the same frame
+ * and subframe sequence (port 0). */
+int oai4g_rx_batch_estimated(oai4g_rx_config_t *rx, oai4g_chest_config_t *ce, int n_sf, const int32_t *d_rxdataF,
+                             int16_t *d_llr, int unscramble, void *stream);
 
 /* ---------------- synchronisation, broadcast and HARQ-indicator channels ---------------- */
 /* generate_pss (PHY/LTE_TRANSPORT/pss.c:50, decl LTE_TRANSPORT/proto.h): the Zadoff-Chu sequence

@@ -207,6 +207,8 @@ _SIGS = {
     "oai4g_chest_config_create": (ctypes.c_void_p, [ctypes.POINTER(FrameParms), ctypes.c_uint8, ctypes.c_uint8,
                                                     ctypes.c_uint8]),
     "oai4g_chest_config_destroy": (None, [ctypes.c_void_p]),
+    "oai4g_rx_batch_estimated": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p,
+                                                ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p]),
     "oai4g_chest_batch": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p,
                                          ctypes.c_void_p]),
     "oai4g_generate_dummy_w": (ctypes.c_uint32, [ctypes.c_uint32, ctypes.c_void_p, ctypes.c_uint8]),
@@ -559,6 +561,18 @@ class RxBatch:
         h = np.ascontiguousarray(dl_ch, dtype=np.int32)
         _check(self.L.oai4g_memcpy_h2d(self.d_h, _ptr(h), h.nbytes) == 0)
         self.launch(d_rxdataF or self.d_y, self.d_h, unscramble)
+        _check(self.L.oai4g_sync() == 0)
+        out = np.empty((self.n_sf, self.stride), dtype=np.int16)
+        _check(self.L.oai4g_memcpy_d2h(_ptr(out), self.d_llr, out.nbytes) == 0)
+        return out
+
+    def launch_estimated(self, chest, d_rxdataF, unscramble=1, stream=None):
+        """Device-only, fused with the channel estimation of `chest` (a ChestBatch of the same
+        subframes): LLRs of d_rxdataF into self.d_llr, no estimate buffer."""
+        _check(self.L.oai4g_rx_batch_estimated(self.cfg, chest.cfg, self.n_sf, d_rxdataF, self.d_llr, unscramble,
+                                               stream) == 0)
+
+    def llrs(self):
         _check(self.L.oai4g_sync() == 0)
         out = np.empty((self.n_sf, self.stride), dtype=np.int16)
         _check(self.L.oai4g_memcpy_d2h(_ptr(out), self.d_llr, out.nbytes) == 0)

@@ -17,7 +17,7 @@
  * writes the subframe's 14 estimate rows once — coalesced, no read-modify-write of the estimate
  * buffer.  HBM traffic per subframe = 14 N words written + the pilot REs read.
  */
-#include "oai4g_internal.h"
+#include "oai4g_rx_prims.h"
 
 namespace {
 
@@ -177,6 +177,152 @@ __global__ void __launch_bounds__(CE_WG) k_chest_symbol(const chest_dev_t *__res
   const uint32_t prev = (uint32_t)E[prev_row * N];
   E[symbol * N] = (int32_t)cur;
   ce_interp(E, N, Ncp, symbol, prev, cur);
+}
+
+/* ======================================================================================
+ * Fused estimation + demodulation (batch path): the estimate rows rx_pdsch would read are never
+ * written to HBM.  One 256-thread workgroup per subframe: the conjugate-pilot products of the 5
+ * pilot symbols (LDS), their frequency-interpolated rows over the 12 N_RB estimate columns
+ * (LDS, the k_chest sums), then the channel level of the first PDSCH symbol and the LLRs of
+ * every PDSCH RE, each RE's estimate formed from the two pilot rows of its symbol with the
+ * temporal interpolation's weights.  Bit-identical to k_chest followed by k_rx_level / k_rx_llr.
+ * ==================================================================================== */
+/* estimate row l as (instance a, weight wa, instance b, weight wb); wb = 0: pilot row a itself.
+ * Instances: 0 = symbol 0, 1 = pilot1, 2 = pilot2, 3 = pilot3, 4 = next subframe's symbol 0
+ * (lte_dl_channel_estimation.c:639-698 with high_speed_flag = 1) */
+__device__ __forceinline__ void ce_row_src(uint32_t Ncp, uint32_t l, uint32_t &a, int16_t &wa, uint32_t &b, int16_t &wb)
+{
+  if (Ncp == 0) {
+    switch (l) {
+      case 0: a = 0; b = 0; wa = 0; wb = 0; return;
+      case 1: a = 0; b = 1; wa = 24576; wb = 8192; return;
+      case 2: a = 0; b = 1; wa = 16384; wb = 16384; return;
+      case 3: a = 0; b = 1; wa = 8192; wb = 24576; return;
+      case 4: a = 1; b = 1; wa = 0; wb = 0; return;
+      case 5: a = 1; b = 2; wa = 21845; wb = 10923; return;
+      case 6: a = 1; b = 2; wa = 10923; wb = 21845; return;
+      case 7: a = 2; b = 2; wa = 0; wb = 0; return;
+      case 8: a = 2; b = 3; wa = 24576; wb = 8192; return;
+      case 9: a = 2; b = 3; wa = 16384; wb = 16384; return;
+      case 10: a = 2; b = 3; wa = 8192; wb = 24576; return;
+      case 11: a = 3; b = 3; wa = 0; wb = 0; return;
+      case 12: a = 3; b = 4; wa = 21845; wb = 10923; return;
+      default: a = 3; b = 4; wa = 10923; wb = 21845; return;
+    }
+  }
+  switch (l) {
+    case 0: a = 0; b = 0; wa = 0; wb = 0; return;
+    case 1: a = 0; b = 1; wa = 10923; wb = 21845; return;
+    case 2: a = 0; b = 1; wa = 21845; wb = 10923; return;
+    case 3: a = 1; b = 1; wa = 0; wb = 0; return;
+    case 4: a = 1; b = 2; wa = 21845; wb = 10923; return;
+    case 5: a = 1; b = 2; wa = 10923; wb = 21845; return;
+    case 6: a = 2; b = 2; wa = 0; wb = 0; return;
+    case 7: a = 2; b = 3; wa = 10923; wb = 21845; return;
+    case 8: a = 2; b = 3; wa = 21845; wb = 10923; return;
+    case 9: a = 3; b = 3; wa = 0; wb = 0; return;
+    case 10: a = 3; b = 4; wa = 21845; wb = 10923; return;
+    default: a = 3; b = 4; wa = 10923; wb = 21845; return;
+  }
+}
+
+constexpr uint32_t RXC_COLS = 1200;          /* 12 N_RB estimate columns, N_RB <= 100 */
+constexpr uint32_t RXC_WG = 512;
+constexpr uint32_t RXC_R = 3;                /* REs per thread and symbol: 512 x 3 >= 1200 */
+constexpr uint32_t RXC_S = 2;                /* symbols whose loads are in flight together */
+
+template <int QM>
+__global__ void __launch_bounds__(RXC_WG) k_rx_chest(const chest_dev_t *__restrict__ ce, const rx_dev_t *__restrict__ c,
+                                                     const int32_t *__restrict__ rxF, int16_t *__restrict__ llr,
+                                                     uint8_t *__restrict__ shift, int unscramble)
+{
+  __shared__ uint32_t chl[5][2 * 100];
+  __shared__ int16_t flt[2][6][24];
+  __shared__ uint32_t P[5][RXC_COLS];
+  __shared__ uint32_t acc;
+  const uint32_t sf = blockIdx.x, N = ce->N, nsymb = ce->nsymb, Ncp = ce->Ncp, N_RB = ce->N_RB;
+  const uint32_t sfi = (ce->first_sf + sf * ce->sf_step) % 10;
+  const uint32_t p1 = Ncp ? 3 : 4, p2 = Ncp ? 6 : 7, p3 = Ncp ? 9 : 11, np = 2 * N_RB, ncol = 12 * N_RB;
+  const int32_t *base = rxF + (size_t)sf * nsymb * N;
+  for (uint32_t i = threadIdx.x; i < 2 * 6 * 24; i += RXC_WG) (&flt[0][0][0])[i] = (&ce->filt[0][0][0])[i];
+  if (threadIdx.x == 0) acc = 0;
+  if (ce->branch)
+    for (uint32_t i = threadIdx.x; i < 5 * np; i += RXC_WG) {
+      const uint32_t in = i / np, m = i - in * np;
+      const uint32_t sym = in == 0 ? 0 : in == 1 ? p1 : in == 2 ? p2 : in == 3 ? p3 : nsymb;
+      const uint32_t Ns = in < 2 ? 2 * sfi : in < 4 ? 2 * sfi + 1 : (2 * sfi + 2) % 20;
+      chl[in][m] = ce_pilot_ch(ce, base + (size_t)sym * N, Ns, in & 1u, m);
+    }
+  __syncthreads();
+  for (uint32_t i = threadIdx.x; i < 5 * ncol; i += RXC_WG) {
+    const uint32_t in = i / ncol, col = i - in * ncol;
+    P[in][col] = ce->branch ? ce_column(N_RB, flt[in & 1u], chl[in], 0, 5 + col) : 0u;
+  }
+  __syncthreads();
+  auto est = [&](uint32_t l, uint32_t col) -> uint32_t {
+    uint32_t a, b;
+    int16_t wa, wb;
+    ce_row_src(Ncp, l, a, wa, b, wb);
+    return wb == 0 ? P[a][col] : (uint32_t)ce_ip(P[a][col], wa, P[b][col], wb);
+  };
+  /* dlsch_channel_level over the first PDSCH symbol */
+  {
+    const uint32_t l = c->npdcch, *map = c->map + c->map_off[sfi][0];
+    uint32_t part = 0;
+    for (uint32_t j = threadIdx.x; j < c->lvl_n[sfi]; j += RXC_WG) part += rx_h2(est(l, (map[j] >> 16) - 5));
+    atomicAdd(&acc, part);
+  }
+  __syncthreads();
+  const uint32_t sh = rx_shift_of((int32_t)acc, c->lvl_div[sfi]);
+  if (threadIdx.x == 0) shift[sf] = (uint8_t)sh;
+  const uint32_t *gold = unscramble ? c->gold + (size_t)sfi * c->gold_words : nullptr;
+  const int16_t a1 = c->a1, a2 = c->a2;
+  for (uint32_t k0 = 0; k0 < c->n_sym; k0 += RXC_S) {
+    /* all map words, then all received words of RXC_S symbols, then the arithmetic */
+    uint32_t mw[RXC_S][RXC_R], yv[RXC_S][RXC_R];
+#pragma unroll
+    for (uint32_t u = 0; u < RXC_S; u++) {
+      const uint32_t k = k0 + u, len = k < c->n_sym ? c->len[sfi][k] : 0u;
+      const uint32_t *map = c->map + c->map_off[sfi][k < c->n_sym ? k : 0];
+#pragma unroll
+      for (uint32_t r = 0; r < RXC_R; r++) {
+        const uint32_t j = threadIdx.x + RXC_WG * r;
+        mw[u][r] = j < len ? map[j] : 5u << 16;
+      }
+    }
+#pragma unroll
+    for (uint32_t u = 0; u < RXC_S; u++) {
+      const int32_t *y = base + (size_t)(c->npdcch + k0 + u < nsymb ? c->npdcch + k0 + u : 0) * N;
+#pragma unroll
+      for (uint32_t r = 0; r < RXC_R; r++) yv[u][r] = (uint32_t)y[mw[u][r] & 0xFFFFu];
+    }
+#pragma unroll
+    for (uint32_t u = 0; u < RXC_S; u++) {
+      const uint32_t k = k0 + u;
+      if (k >= c->n_sym) break;
+      const uint32_t l = c->npdcch + k, len = c->len[sfi][k], lb = c->llr_off[sfi][k];
+      int16_t *out = llr + (size_t)sf * c->llr_stride + lb;
+#pragma unroll
+      for (uint32_t r = 0; r < RXC_R; r++) {
+        const uint32_t j = threadIdx.x + RXC_WG * r;
+        if (j >= len) break;
+        rx_re_llr<QM>(est(l, (mw[u][r] >> 16) - 5), yv[u][r], sh, a1, a2, gold, lb + j * QM, out + QM * j);
+      }
+    }
+  }
+}
+
+hipError_t oai4g_launch_rx_chest(const chest_dev_t *d_ce, const rx_dev_t *d_rx, const rx_dev_t *h_rx, int n_sf,
+                                 const int32_t *d_rxF, int16_t *d_llr, uint8_t *d_shift, int unscramble, hipStream_t s)
+{
+  if (n_sf <= 0) return hipSuccess;
+  if (h_rx->Qm == 2)
+    hipLaunchKernelGGL(k_rx_chest<2>, dim3(n_sf), dim3(RXC_WG), 0, s, d_ce, d_rx, d_rxF, d_llr, d_shift, unscramble);
+  else if (h_rx->Qm == 4)
+    hipLaunchKernelGGL(k_rx_chest<4>, dim3(n_sf), dim3(RXC_WG), 0, s, d_ce, d_rx, d_rxF, d_llr, d_shift, unscramble);
+  else
+    hipLaunchKernelGGL(k_rx_chest<6>, dim3(n_sf), dim3(RXC_WG), 0, s, d_ce, d_rx, d_rxF, d_llr, d_shift, unscramble);
+  return hipGetLastError();
 }
 
 hipError_t oai4g_launch_chest(const chest_dev_t *d_cfg, const chest_dev_t *h_cfg, int n_sf, const int32_t *d_rxF,

@@ -3218,6 +3218,28 @@ extern "C" int oai4g_chest_batch(oai4g_chest_config_t *cfg, int n_sf, const int3
   return 0;
 }
 
+/* Fused batch: estimation + demodulation without the estimate buffer (k_rx_chest); the two
+ * configurations must describe the same frame and subframe sequence. */
+extern "C" int oai4g_rx_batch_estimated(oai4g_rx_config_t *rx, oai4g_chest_config_t *ce, int n_sf,
+                                        const int32_t *d_rxdataF, int16_t *d_llr, int unscramble, void *stream)
+{
+  NEED_INIT(-1);
+  if (!rx || !ce || n_sf < 0) { set_err("rx_batch_estimated: bad arguments"); return -1; }
+  if (rx->h.N != ce->h.N || rx->h.nsymb != ce->h.nsymb || rx->h.first_sf != ce->h.first_sf ||
+      rx->h.sf_step != ce->h.sf_step || ce->h.p != 0 || ce->h.N_RB > 100) {
+    set_err("rx_batch_estimated: the demodulation and estimation configurations differ (frame, subframes, port 0)");
+    return -1;
+  }
+  if (n_sf > rx->shift_cap) {
+    if (rx->d_shift) hipFree(rx->d_shift);
+    HCK(hipMalloc(&rx->d_shift, (size_t)n_sf), -1);
+    rx->shift_cap = n_sf;
+  }
+  HCK(oai4g_launch_rx_chest(ce->d, rx->d, &rx->h, n_sf, d_rxdataF, d_llr, rx->d_shift, unscramble,
+                            (hipStream_t)stream), -1);
+  return 0;
+}
+
 /* lte_dl_channel_estimation drop-in on host buffers: rxdataF / dl_ch_estimates = [nsymb][N] of the
  * subframe (the UE's rxdataF and dl_ch_estimates[eNB_offset 0][(p << 1) + 0]); Ns, p, l, symbol as
  * slot_fep passes them (slot_fep.c:188-192) */

@@ -332,5 +332,7 @@ struct rx_dev_t {
   const uint32_t *map;            /* extracted RE j: FFT bin | (estimate index within the symbol) << 16 */
   const uint32_t *gold;           /* [10][gold_words] */
 };
+hipError_t oai4g_launch_rx_chest(const chest_dev_t *d_ce, const rx_dev_t *d_rx, const rx_dev_t *h_rx, int n_sf,
+                                 const int32_t *d_rxF, int16_t *d_llr, uint8_t *d_shift, int unscramble, hipStream_t s);
 hipError_t oai4g_launch_rx(const rx_dev_t *d_cfg, const rx_dev_t *h_cfg, int n_sf, const int32_t *d_rxF,
                            const int32_t *d_ch, int16_t *d_llr, uint8_t *d_shift, int unscramble, hipStream_t s);

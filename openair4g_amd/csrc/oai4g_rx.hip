@@ -13,14 +13,7 @@
  * madd_epi16 (int32 wrap) with the conjugate by sign_epi16 (int16 wrap), srai + packs_epi32
  * (saturation), mulhi_epi16 << 1, abs_epi16 (-32768 stays), subs_epi16.
  */
-#include "oai4g_internal.h"
-
-static __device__ __forceinline__ int16_t rx_sat16(int32_t v) { return (int16_t)max(-32768, min(32767, v)); }
-static __device__ __forceinline__ int16_t rx_abs16(int16_t v) { return v < 0 ? (int16_t)(-(int32_t)v) : v; }
-static __device__ __forceinline__ int32_t rx_madd(int16_t a0, int16_t b0, int16_t a1, int16_t b1)
-{
-  return (int32_t)((uint32_t)((int32_t)a0 * b0) + (uint32_t)((int32_t)a1 * b1));
-}
+#include "oai4g_rx_prims.h"
 
 /* dlsch_channel_level over the first PDSCH symbol -> log2_maxh = log2_approx(avg) / 2, per subframe */
 __global__ void __launch_bounds__(256) k_rx_level(const rx_dev_t *__restrict__ c, const int32_t *__restrict__ ch,
@@ -33,18 +26,10 @@ __global__ void __launch_bounds__(256) k_rx_level(const rx_dev_t *__restrict__ c
   const uint32_t *map = c->map + c->map_off[sfi][0];
   const int32_t *chs = ch + ((size_t)sf * c->nsymb + l) * c->N;
   uint32_t part = 0;
-  for (uint32_t j = threadIdx.x; j < c->lvl_n[sfi]; j += blockDim.x) {
-    const uint32_t h = (uint32_t)chs[map[j] >> 16];
-    part += (uint32_t)rx_madd((int16_t)h, (int16_t)h, (int16_t)(h >> 16), (int16_t)(h >> 16));
-  }
+  for (uint32_t j = threadIdx.x; j < c->lvl_n[sfi]; j += blockDim.x) part += rx_h2((uint32_t)chs[map[j] >> 16]);
   atomicAdd(&acc, part);                       /* int32 wrap-add commutes (the reference's epi32 lanes) */
   __syncthreads();
-  if (threadIdx.x == 0) {
-    const int32_t avg = (int32_t)acc / (int32_t)c->lvl_div[sfi];
-    const uint32_t x = avg > 0 ? (uint32_t)avg : 0u;
-    const uint32_t l2 = x ? 32u - __clz(x & 0x7FFFFFFFu) : 0u;   /* log2_approx: bits 0..30 */
-    shift[sf] = (uint8_t)(l2 / 2);
-  }
+  if (threadIdx.x == 0) shift[sf] = rx_shift_of((int32_t)acc, c->lvl_div[sfi]);
 }
 
 /* A 256-thread workgroup per (subframe, PDSCH symbol); thread t takes REs t + 256 r, r < 5 (>= the
@@ -84,42 +69,7 @@ __global__ void __launch_bounds__(256) k_rx_llr(const rx_dev_t *__restrict__ c, 
   for (int r = 0; r < RX_R; r++) {
     const uint32_t j = threadIdx.x + 256 * r;
     if (j >= len) break;
-    const int16_t hr = (int16_t)hv[r], hi = (int16_t)(hv[r] >> 16), yr = (int16_t)yv[r], yi = (int16_t)(yv[r] >> 16);
-    const int16_t nhi = (int16_t)(-(int32_t)hi);
-    int16_t v[6];
-    v[0] = rx_sat16(rx_madd(hr, yr, hi, yi) >> sh);
-    v[1] = rx_sat16(rx_madd(nhi, yr, hr, yi) >> sh);
-    if (QM > 2) {
-      const int16_t mg = rx_sat16(rx_madd(hr, hr, hi, hi) >> sh);
-      const int16_t mag = (int16_t)((((int32_t)mg * a1) >> 16) << 1);
-      v[2] = rx_sat16((int32_t)mag - rx_abs16(v[0]));
-      v[3] = rx_sat16((int32_t)mag - rx_abs16(v[1]));
-      if (QM > 4) {
-        const int16_t magb = (int16_t)((((int32_t)mg * a2) >> 16) << 1);
-        v[4] = rx_sat16((int32_t)magb - rx_abs16(v[2]));
-        v[5] = rx_sat16((int32_t)magb - rx_abs16(v[3]));
-      }
-    }
-    if (unscramble) {                            /* llr * (2 c - 1), int16 */
-      const uint32_t b = base + j * QM, w = b >> 5;
-      const uint64_t win = ((uint64_t)gold[w] | ((uint64_t)gold[w + 1] << 32)) >> (b & 31);
-#pragma unroll
-      for (int q = 0; q < QM; q++)
-        if (!((win >> q) & 1u)) v[q] = (int16_t)(-(int32_t)v[q]);
-    }
-    uint32_t pk[3];
-#pragma unroll
-    for (int q = 0; q < QM / 2; q++) pk[q] = (uint32_t)(uint16_t)v[2 * q] | ((uint32_t)(uint16_t)v[2 * q + 1] << 16);
-    if (QM == 2) {
-      *(uint32_t *)(out + 2 * j) = pk[0];
-    } else if (QM == 4) {
-      *(uint2 *)(out + 4 * j) = make_uint2(pk[0], pk[1]);
-    } else {
-      uint32_t *o = (uint32_t *)(out + 6 * j);
-      o[0] = pk[0];
-      o[1] = pk[1];
-      o[2] = pk[2];
-    }
+    rx_re_llr<QM>(hv[r], yv[r], sh, a1, a2, unscramble ? gold : nullptr, base + j * QM, out + QM * j);
   }
 }
 

@@ -1,0 +1,76 @@
+/*
+ * Per-RE demodulation arithmetic shared by k_rx_llr (oai4g_rx.hip) and the fused estimator +
+ * demodulator k_rx_chest (oai4g_chest.hip): the reference's SSE lane arithmetic of
+ * dlsch_channel_compensation (dlsch_demodulation.c:801-960) and dlsch_qpsk/16qam/64qam_llr
+ * (dlsch_llr_computation.c:636-930) plus dlsch_unscrambling's sign (dlsch_scrambling.c:99-137).
+ */
+#ifndef OAI4G_RX_PRIMS_H
+#define OAI4G_RX_PRIMS_H
+#include "oai4g_internal.h"
+
+static __device__ __forceinline__ int16_t rx_sat16(int32_t v) { return (int16_t)max(-32768, min(32767, v)); }
+static __device__ __forceinline__ int16_t rx_abs16(int16_t v) { return v < 0 ? (int16_t)(-(int32_t)v) : v; }
+static __device__ __forceinline__ int32_t rx_madd(int16_t a0, int16_t b0, int16_t a1, int16_t b1)
+{
+  return (int32_t)((uint32_t)((int32_t)a0 * b0) + (uint32_t)((int32_t)a1 * b1));
+}
+
+/* |h|^2 of one estimate word (dlsch_channel_level's madd, int32 wrap) */
+static __device__ __forceinline__ uint32_t rx_h2(uint32_t h)
+{
+  return (uint32_t)rx_madd((int16_t)h, (int16_t)h, (int16_t)(h >> 16), (int16_t)(h >> 16));
+}
+
+/* the Qm LLRs of one RE (estimate hv, received yv), unscrambled with the Gold bits starting at
+ * stream position b when gold != nullptr, stored at out (one 4 / 8 / 12-byte store) */
+template <int QM>
+static __device__ __forceinline__ void rx_re_llr(uint32_t hv, uint32_t yv, uint32_t sh, int16_t a1, int16_t a2,
+                                                 const uint32_t *__restrict__ gold, uint32_t b, int16_t *out)
+{
+  const int16_t hr = (int16_t)hv, hi = (int16_t)(hv >> 16), yr = (int16_t)yv, yi = (int16_t)(yv >> 16);
+  const int16_t nhi = (int16_t)(-(int32_t)hi);
+  int16_t v[6];
+  v[0] = rx_sat16(rx_madd(hr, yr, hi, yi) >> sh);
+  v[1] = rx_sat16(rx_madd(nhi, yr, hr, yi) >> sh);
+  if (QM > 2) {
+    const int16_t mg = rx_sat16(rx_madd(hr, hr, hi, hi) >> sh);
+    const int16_t mag = (int16_t)((((int32_t)mg * a1) >> 16) << 1);
+    v[2] = rx_sat16((int32_t)mag - rx_abs16(v[0]));
+    v[3] = rx_sat16((int32_t)mag - rx_abs16(v[1]));
+    if (QM > 4) {
+      const int16_t magb = (int16_t)((((int32_t)mg * a2) >> 16) << 1);
+      v[4] = rx_sat16((int32_t)magb - rx_abs16(v[2]));
+      v[5] = rx_sat16((int32_t)magb - rx_abs16(v[3]));
+    }
+  }
+  if (gold) {                                    /* llr * (2 c - 1), int16 */
+    const uint32_t w = b >> 5;
+    const uint64_t win = ((uint64_t)gold[w] | ((uint64_t)gold[w + 1] << 32)) >> (b & 31);
+#pragma unroll
+    for (int q = 0; q < QM; q++)
+      if (!((win >> q) & 1u)) v[q] = (int16_t)(-(int32_t)v[q]);
+  }
+  uint32_t pk[3];
+#pragma unroll
+  for (int q = 0; q < QM / 2; q++) pk[q] = (uint32_t)(uint16_t)v[2 * q] | ((uint32_t)(uint16_t)v[2 * q + 1] << 16);
+  if (QM == 2) {
+    *(uint32_t *)out = pk[0];
+  } else if (QM == 4) {
+    *(uint2 *)out = make_uint2(pk[0], pk[1]);
+  } else {
+    uint32_t *o = (uint32_t *)out;
+    o[0] = pk[0];
+    o[1] = pk[1];
+    o[2] = pk[2];
+  }
+}
+
+/* log2_approx(avg) / 2 of dlsch_channel_level (log2_approx: bits 0..30) */
+static __device__ __forceinline__ uint8_t rx_shift_of(int32_t acc, uint32_t div)
+{
+  const int32_t avg = acc / (int32_t)div;
+  const uint32_t x = avg > 0 ? (uint32_t)avg : 0u;
+  const uint32_t l2 = x ? 32u - __clz(x & 0x7FFFFFFFu) : 0u;
+  return (uint8_t)(l2 / 2);
+}
+#endif

@@ -111,3 +111,38 @@ def test_gpu_estimated_channel_loop(gpu, N_RB, mcs, npd, sf):
         assert all(it <= 4 for it, _ in res), (s, [it for it, _ in res])
         assert np.array_equal(tb, pay[i, 0, :p.TBS[0] // 8]), s
     rx.close()
+
+
+@pytest.mark.parametrize("N_RB,Qm,npd,first,Ncp", [(100, 4, 1, 3, 0), (50, 6, 2, 8, 0), (6, 2, 3, 0, 0),
+                                                    (100, 6, 1, 9, 0), (50, 4, 2, 1, 1)])
+def test_gpu_fused_estimation_demodulation(gpu, N_RB, Qm, npd, first, Ncp):
+    """oai4g_rx_batch_estimated (k_rx_chest) = oai4g_chest_batch then oai4g_rx_batch, and = the
+    oracle's chain, on full-range random grids (saturating estimates and LLRs)."""
+    fo = O.frame(N_RB, Nid_cell=N_RB + first, Ncp=Ncp)
+    fg = gpu.frame_parms(N_RB, Nid_cell=N_RB + first, Ncp=Ncp)
+    N, nsymb = fo.ofdm_symbol_size, fo.symbols_per_tti
+    n_sf = 10
+    rng = np.random.default_rng(N_RB * Qm + first)
+    y = (rng.integers(-2**15, 2**15, ((n_sf + 1) * nsymb * N, 2)).astype(np.int16)).view(np.int32).ravel()
+    cb = gpu.ChestBatch(fg, n_sf, first_subframe=first)
+    rb = gpu.RxBatch(fg, alloc(N_RB), Qm, npd, 0x2345, n_sf, first_subframe=first, subframe_step=1)
+    yin = np.ascontiguousarray(y[:n_sf * nsymb * N + N])          # the batch + the next symbol 0
+    assert gpu.lib().oai4g_memcpy_h2d(cb.d_rx, gpu._ptr(yin), yin.nbytes) == 0
+    cb.launch(cb.d_rx)
+    rb.launch(cb.d_rx, cb.d_est, 1)
+    two = rb.llrs()
+    rb.launch_estimated(cb, cb.d_rx, 1)
+    fused = rb.llrs()
+    for i in range(n_sf):
+        sf = (first + i) % 10
+        G = rb.llr_count(sf)
+        assert np.array_equal(fused[i, :G], two[i, :G]), i
+        if i in (0, n_sf - 1) and Ncp == 0:
+            est = O.chest_subframe(fo, y[i * nsymb * N:(i + 1) * nsymb * N], y[(i + 1) * nsymb * N:][:N], sf)
+            lo, _ = O.rx_pdsch_siso(fo, y[i * nsymb * N:(i + 1) * nsymb * N], est, alloc(N_RB), Qm, npd, sf)
+            u = np.zeros(32 * (1 + len(lo) // 32), np.int16)
+            u[:len(lo)] = lo
+            O.dlsch_unscrambling(u, len(lo), (0x2345 << 14) + (sf << 9) + fo.Nid_cell)
+            assert np.array_equal(fused[i, :G], u[:G]), i
+    cb.close()
+    rb.close()
