@@ -236,4 +236,10 @@ void orc_chest_filters(uint8_t k, int16_t out[6][24]);
 int  orc_lte_dl_channel_estimation(const orc_frame_t *fp, const uint32_t gold[20][2][14], const int32_t *rxdataF,
                                    int32_t *dl_ch_estimates, uint8_t Ns, uint8_t p, uint8_t l, uint8_t symbol);
 
+/* ---- 8-bit turbo decoder (CODING/3gpplte_turbo_decoder_sse_8bit.c:846-1658), n % 16 == 0, n >= 512 ---- */
+void    orc_td8_tables(int n, int *pi2, int *pi4, int *pi5, int *pi6);
+int     orc_td8_input(const int16_t *y, int n, int8_t *y8);
+uint8_t orc_turbo_decoder8(const int16_t *y, uint8_t *decoded_bytes, uint16_t n, uint8_t max_iterations,
+                           uint8_t crc_type, uint8_t F);
+
 #endif

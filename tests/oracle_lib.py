@@ -567,3 +567,15 @@ def ulsch_decode(e, B, G, Qm, rvidx=0, max_it=8, Mdlharq=8):
         d = subblock_deinterleave(w, K)
         out.append(turbo_decode(d, K, max_it=max_it, crc_type=1 if C > 1 else 0, F=(F if C == 1 else 0)))
     return out
+
+
+def turbo_decode8(y, K, max_it=8, crc_type=0, F=0):
+    """phy_threegpplte_turbo_decoder8 (oracle/oai_oracle_td8.c): y = 3K+12 int16 LLRs (4 more
+    entries are read, zero here).  Returns (iterations, decoded bytes)."""
+    buf = np.zeros(3 * K + 64, dtype=np.int16)
+    y = np.asarray(y, dtype=np.int16)
+    buf[:len(y)] = y
+    out = np.zeros(K // 8 + 8, dtype=np.uint8)
+    orc().orc_turbo_decoder8.restype = ctypes.c_uint8
+    it = orc().orc_turbo_decoder8(P(buf), P(out), K, max_it, crc_type, F)
+    return it, out[:K // 8]
