@@ -248,7 +248,7 @@ def bench_c5(args, world, rank, dist, torch):
     if args.c5_mode == "chain":
         return bench_c5_chain(args, world, rank, dist, torch)
     llr = c5_llrs(n_cb, args.c5_mode, 0xC5 + rank)
-    dec = oai.TurboDecoderBatch(C5_K, n_cb)
+    dec = (oai.TurboDecoder8Batch if args.c5_bits == 8 else oai.TurboDecoderBatch)(C5_K, n_cb)
     dec.upload(llr)
     for _ in range(args.warmup):
         dec.run(max_iterations=8, crc_type=crc_type)
@@ -279,8 +279,9 @@ def bench_c5(args, world, rank, dist, torch):
         sys.path.insert(0, os.path.join(ROOT, "tests"))
         import oracle_lib as O
         n, t1 = 0, time.perf_counter()
+        dec_fn = O.turbo_decode8 if args.c5_bits == 8 else O.turbo_decode
         while time.perf_counter() - t1 < args.cpu_seconds:
-            O.turbo_decode(llr[n % len(llr)], C5_K, max_it=8, crc_type=crc_type)
+            dec_fn(llr[n % len(llr)], C5_K, max_it=8, crc_type=crc_type)
             n += 1
         dt = time.perf_counter() - t1
         cpu = {"value": n / C5_CB / dt, "unit": "subframes/s", "cores": 1, "kind": "port",
@@ -288,15 +289,17 @@ def bench_c5(args, world, rank, dist, torch):
                          f"single thread, {dt:.1f} s"}
     if rank == 0:
         print(json.dumps({
-            "metric": "UL subframes/sec (C5 turbo decode)", "value": value, "unit": "subframes/s", "n_gpus": world,
+            "metric": "UL subframes/sec (C5 turbo decode)" + (", 8-bit decoder" if args.c5_bits == 8 else ""),
+            "value": value, "unit": "subframes/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": per_launch_ms, "higher_is_better": True,
-            "scaling": "weak", "vs_baseline": None, "dtype": "int16",
+            "scaling": "weak", "vs_baseline": None, "dtype": "int8" if args.c5_bits == 8 else "int16",
             "data": f"synthetic LLRs ({args.c5_mode})",
-            "config": {"workload": "ulsim 20 MHz MCS20 decode: 8 x K=5504, 16-bit max-log-MAP, max 8 iterations",
+            "config": {"workload": "ulsim 20 MHz MCS20 decode: 8 x K=5504, "
+                                   + ("8-bit (16-window)" if args.c5_bits == 8 else "16-bit") + " max-log-MAP, max 8 iterations",
                        "config_id": "C5", "subframes_per_gpu_per_step": n_sf, "code_blocks_per_step": n_cb,
                        "mean_iterations": float(np.mean(its)), "parallelism": f"block-sharded x{world}"},
-            "roofline": {"bound": "hbm", "kernel": "k_td16", "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": ach / HBM_PEAK_GBS, "traffic": _traffic("C5", "k_td16", n_sf),
+            "roofline": {"bound": "hbm", "kernel": "k_td8" if args.c5_bits == 8 else "k_td16", "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": ach / HBM_PEAK_GBS, "traffic": None if args.c5_bits == 8 else _traffic("C5", "k_td16", n_sf),
                          "note": "latency-bound: traffic (scratch streaming per half-iteration) >> algorithmic bytes"},
             "cpu_baseline": cpu}), flush=True)
 
@@ -646,6 +649,7 @@ def main():
     ap.add_argument("--kernel-reps", type=int, default=5, help="serial runs timed per kernel for the roofline")
     ap.add_argument("--c5-mode", default="8it", choices=["8it", "snr", "chain"],
                     help="C5 decoder inputs; chain = from the e soft bits through RM-rx + deinterleaving")
+    ap.add_argument("--c5-bits", type=int, default=16, choices=[16, 8], help="C5 decoder: 16-bit or 8-bit")
     ap.add_argument("--ue-unfused", action="store_true", help="UE: estimate buffer + separate demodulation kernels")
     ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"], help="nccl = RCCL on ROCm")
     ap.add_argument("--cpu-stub", action="store_true",

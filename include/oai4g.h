@@ -378,6 +378,19 @@ int oai4g_td_batch(int n_cb, uint16_t K, const int16_t *d_llr, size_t llr_stride
                    uint8_t *d_iters, uint8_t max_iterations, uint8_t crc_type, uint8_t F, void *d_scratch,
                    void *stream);
 
+/* phy_threegpplte_turbo_decoder8 (PHY/CODING/3gpplte_turbo_decoder_sse_8bit.c:894, decl CODING/defs.h):
+ * the 8-bit decoder (16 windows of int8 lanes, inputs scaled by their |LLR| mean).  Restated for
+ * n % 16 == 0 and n >= 512 (other sizes: the reference reads past its interleaver tables) and
+ * CRC24_A / CRC24_B; returns 255 outside that scope.  f1 / f2 are implied by n. */
+uint8_t oai4g_phy_threegpplte_turbo_decoder8(const int16_t *y, uint8_t *decoded_bytes, uint16_t n, uint16_t f1,
+                                             uint16_t f2, uint8_t max_iterations, uint8_t crc_type, uint8_t F);
+/* Batched 8-bit decoder, device pointers as oai4g_td_batch; llr rows of >= 3K + 16 int16 (the
+ * last 4 are read by the input scaling only); scratch of oai4g_td8_scratch_bytes(K, n_cb). */
+size_t oai4g_td8_scratch_bytes(uint16_t K, int n_cb);
+int oai4g_td8_batch(int n_cb, uint16_t K, const int16_t *d_llr, size_t llr_stride, uint8_t *d_out, size_t out_stride,
+                    uint8_t *d_iters, uint8_t max_iterations, uint8_t crc_type, uint8_t F, void *d_scratch,
+                    void *stream);
+
 /* generate_dummy_w (PHY/CODING/lte_rate_matching.c:293, decl CODING/defs.h): marks LTE_NULL in w at
  * the NULL / filler positions of the 3 Kpi circular buffer of a block of D = K + 4 bits with F
  * filler bits (other entries untouched, as the reference); returns R = ceil(D / 32). */

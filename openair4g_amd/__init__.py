@@ -211,6 +211,13 @@ _SIGS = {
                                                 ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p]),
     "oai4g_chest_batch": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p,
                                          ctypes.c_void_p]),
+    "oai4g_phy_threegpplte_turbo_decoder8": (ctypes.c_uint8, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint16,
+                                                              ctypes.c_uint16, ctypes.c_uint16, ctypes.c_uint8,
+                                                              ctypes.c_uint8, ctypes.c_uint8]),
+    "oai4g_td8_scratch_bytes": (ctypes.c_size_t, [ctypes.c_uint16, ctypes.c_int]),
+    "oai4g_td8_batch": (ctypes.c_int, [ctypes.c_int, ctypes.c_uint16, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p,
+                                       ctypes.c_size_t, ctypes.c_void_p, ctypes.c_uint8, ctypes.c_uint8, ctypes.c_uint8,
+                                       ctypes.c_void_p, ctypes.c_void_p]),
     "oai4g_generate_dummy_w": (ctypes.c_uint32, [ctypes.c_uint32, ctypes.c_void_p, ctypes.c_uint8]),
     "oai4g_ul_config_create": (ctypes.c_void_p, [ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint8, ctypes.c_uint8,
                                                  ctypes.c_uint8, ctypes.c_uint32, ctypes.c_uint8]),
@@ -674,6 +681,53 @@ def sub_block_deinterleaving_turbo(D, w):
     lib().oai4g_sub_block_deinterleaving_turbo(D, ctypes.c_void_p(buf.ctypes.data + 2 * 96),
                                                _ptr(np.ascontiguousarray(w, dtype=np.int16)))
     return buf
+
+
+def turbo_decoder8(y, n, max_iterations=8, crc_type=0, F=0):
+    """phy_threegpplte_turbo_decoder8 drop-in: y = 3n+12 int16 LLRs.  Returns (iterations, bytes)."""
+    init()
+    y = np.ascontiguousarray(y, dtype=np.int16)
+    out = np.zeros(n // 8, dtype=np.uint8)
+    it = lib().oai4g_phy_threegpplte_turbo_decoder8(_ptr(y), _ptr(out), n, 0, 0, max_iterations, crc_type, F)
+    _check(it != 255)
+    return it, out
+
+
+class TurboDecoder8Batch:
+    """Device-resident batch of n_cb blocks of size K through the 8-bit decoder (oai4g_td8_batch)."""
+
+    def __init__(self, K, n_cb):
+        init()
+        self.L = lib()
+        self.K, self.n_cb = K, n_cb
+        self.llr_stride = 3 * K + 16
+        self.d_llr = self.L.oai4g_dev_alloc(n_cb * self.llr_stride * 2)
+        self.d_out = self.L.oai4g_dev_alloc(n_cb * (K // 8))
+        self.d_it = self.L.oai4g_dev_alloc(n_cb)
+        self.d_scr = self.L.oai4g_dev_alloc(self.L.oai4g_td8_scratch_bytes(K, n_cb))
+        _check(all(bool(p) for p in (self.d_llr, self.d_out, self.d_it, self.d_scr)))
+
+    def upload(self, llr):
+        buf = np.zeros((self.n_cb, self.llr_stride), dtype=np.int16)
+        llr = np.asarray(llr, dtype=np.int16)
+        buf[:, :llr.shape[1]] = llr
+        _check(self.L.oai4g_memcpy_h2d(self.d_llr, _ptr(buf), buf.nbytes) == 0)
+
+    def run(self, max_iterations=8, crc_type=0, F=0, stream=None):
+        _check(self.L.oai4g_td8_batch(self.n_cb, self.K, self.d_llr, self.llr_stride, self.d_out, self.K // 8,
+                                      self.d_it, max_iterations, crc_type, F, self.d_scr, stream) == 0)
+
+    def results(self):
+        _check(self.L.oai4g_sync() == 0)
+        out = np.empty((self.n_cb, self.K // 8), dtype=np.uint8)
+        it = np.empty(self.n_cb, dtype=np.uint8)
+        _check(self.L.oai4g_memcpy_d2h(_ptr(out), self.d_out, out.nbytes) == 0)
+        _check(self.L.oai4g_memcpy_d2h(_ptr(it), self.d_it, it.nbytes) == 0)
+        return it, out
+
+    def close(self):
+        for p in (self.d_llr, self.d_out, self.d_it, self.d_scr):
+            self.L.oai4g_dev_free(p)
 
 
 def generate_dummy_w(D, F=0):

@@ -1,0 +1,428 @@
+/*
+ * gfx950 8-bit turbo decoder: phy_threegpplte_turbo_decoder8 (PHY/CODING/3gpplte_turbo_decoder_sse_8bit.c
+ * :894-1658, x86 branch), for n % 16 == 0 and n >= 512 (the reference's other sizes read past its
+ * tables, see oracle/oai_oracle_td8.c).
+ *
+ * The reference keeps 16 int8 SSE lanes = 16 windows of n/16 trellis steps.  Here one 64-lane wave
+ * decodes 4 code blocks: lane (g, q) owns window q of block g, one column of the reference's
+ * registers.  The int8 saturating adds / subs are exact int16 sums clamped to [-128, 127] (the
+ * operands are int8, so no int16 overflow precedes the clamp) on packed state pairs, max is
+ * max; everything else follows the 16-bit kernel (oai4g_decode.hip): alpha checkpoints every
+ * TD8_SEG steps recomputed during the backward pass, operands loaded one chunk ahead, exchanges
+ * in rounds of index loads then gathers.  The 8-bit decoder's own schedule:
+ *   - the int16 inputs are scaled by the block's |LLR| mean (the reference's quirky sum) and
+ *     packed to int8 (:1001-1031);
+ *   - the alpha re-run spans L = 16 steps from the previous window's final alpha (:242-318), so
+ *     alpha(1..16) are re-run values and alpha(17..) continue the first run;
+ *   - beta starts from the lane's final alpha with window 15 at 0 (the reference's zeroed
+ *     termination, :519-543); its re-run covers the last 16 steps from the next window's beta(0),
+ *     so the extrinsic of the last 17 steps comes from the re-run;
+ *   - hard decisions: n mod 128 = 0 from ext2 deinterleaved (pi5), else from ext2 + systematic2
+ *     through pi6 (:1392-1581).
+ */
+#include "oai4g_internal.h"
+
+typedef short s2v8 __attribute__((ext_vector_type(2)));
+
+#define TD8_FS 16
+#define TD8_SEG 4
+#define TD8_XR 32
+#define TD8_L 16
+
+namespace {
+
+__device__ __forceinline__ s2v8 cl8(s2v8 x)
+{
+  return __builtin_elementwise_min(__builtin_elementwise_max(x, (s2v8){-128, -128}), (s2v8){127, 127});
+}
+__device__ __forceinline__ s2v8 a8(s2v8 a, s2v8 b) { return cl8(a + b); }
+__device__ __forceinline__ s2v8 d8(s2v8 a, s2v8 b) { return cl8(a - b); }
+__device__ __forceinline__ s2v8 m8(s2v8 a, s2v8 b) { return __builtin_elementwise_max(a, b); }
+__device__ __forceinline__ short sa8(int v) { return (short)max(-128, min(127, v)); }
+#define SH8(a, b, i, j) __builtin_shufflevector((a), (b), (i), (j))
+
+struct tm8_t { s2v8 v[4]; };
+
+__device__ __forceinline__ uint4 pk8(const tm8_t &t)
+{
+  return make_uint4(__builtin_bit_cast(uint32_t, t.v[0]), __builtin_bit_cast(uint32_t, t.v[1]),
+                    __builtin_bit_cast(uint32_t, t.v[2]), __builtin_bit_cast(uint32_t, t.v[3]));
+}
+__device__ __forceinline__ tm8_t up8(uint4 u)
+{
+  tm8_t t;
+  t.v[0] = __builtin_bit_cast(s2v8, u.x); t.v[1] = __builtin_bit_cast(s2v8, u.y);
+  t.v[2] = __builtin_bit_cast(s2v8, u.z); t.v[3] = __builtin_bit_cast(s2v8, u.w);
+  return t;
+}
+__device__ __forceinline__ tm8_t init8(bool zero_first)
+{
+  tm8_t t;
+  t.v[0] = (s2v8){(short)(zero_first ? 0 : -63), (short)-63};
+  t.v[1] = t.v[2] = t.v[3] = (s2v8){(short)-63, (short)-63};
+  return t;
+}
+__device__ __forceinline__ tm8_t zero8()
+{
+  tm8_t t;
+  t.v[0] = t.v[1] = t.v[2] = t.v[3] = (s2v8){0, 0};
+  return t;
+}
+
+/* compute_alpha8 step (:249-297): r0 = max(a1+g11, a0-g11), r1 = max(a3-g10, a2+g10), ...
+ * (x - (-g) equals x + g: both are the exact sum clamped) */
+__device__ __forceinline__ void alpha8_step(tm8_t &a, short g11, short g10)
+{
+  const s2v8 G = {g11, (short)-g10}, H = {g10, (short)-g11};
+  const s2v8 x13 = SH8(a.v[0], a.v[1], 1, 3), x02 = SH8(a.v[0], a.v[1], 0, 2);
+  const s2v8 x57 = SH8(a.v[2], a.v[3], 1, 3), x46 = SH8(a.v[2], a.v[3], 0, 2);
+  const s2v8 r01 = m8(a8(x13, G), d8(x02, G)), r45 = m8(d8(x13, G), a8(x02, G));
+  const s2v8 r23 = m8(a8(x57, H), d8(x46, H)), r67 = m8(d8(x57, H), a8(x46, H));
+  const s2v8 m = m8(m8(r01, r23), m8(r45, r67)), mm = m8(m, SH8(m, m, 1, 0));
+  a.v[0] = d8(r01, mm); a.v[1] = d8(r23, mm); a.v[2] = d8(r45, mm); a.v[3] = d8(r67, mm);
+}
+
+/* compute_beta8 step (:554-600) */
+__device__ __forceinline__ void beta8_step(tm8_t &b, short g11, short g10)
+{
+  const s2v8 G = {g11, (short)-g10}, H = {g10, (short)-g11};
+  const s2v8 r02 = m8(a8(b.v[2], G), d8(b.v[0], G)), r13 = m8(d8(b.v[2], G), a8(b.v[0], G));
+  const s2v8 r46 = m8(a8(b.v[3], H), d8(b.v[1], H)), r57 = m8(d8(b.v[3], H), a8(b.v[1], H));
+  const s2v8 m = m8(m8(r02, r13), m8(r46, r57)), mm = m8(m, SH8(m, m, 1, 0));
+  const s2v8 n02 = d8(r02, mm), n13 = d8(r13, mm), n46 = d8(r46, mm), n57 = d8(r57, mm);
+  b.v[0] = SH8(n02, n13, 0, 2); b.v[1] = SH8(n02, n13, 1, 3);
+  b.v[2] = SH8(n46, n57, 0, 2); b.v[3] = SH8(n46, n57, 1, 3);
+}
+
+/* compute_ext8 (:726-767) from alpha(k), beta(k+1), gamma(k) */
+__device__ __forceinline__ short ext8_of(const tm8_t &a, const tm8_t &b, short g11, short g10)
+{
+  const s2v8 p04 = SH8(b.v[0], b.v[2], 0, 2), p40 = SH8(b.v[2], b.v[0], 0, 2);
+  const s2v8 q73 = SH8(b.v[3], b.v[1], 1, 3), q37 = SH8(b.v[1], b.v[3], 1, 3);
+  const s2v8 r51 = SH8(b.v[2], b.v[0], 1, 3), r15 = SH8(b.v[0], b.v[2], 1, 3);
+  const s2v8 s26 = SH8(b.v[1], b.v[3], 0, 2), s62 = SH8(b.v[3], b.v[1], 0, 2);
+  const s2v8 M00 = m8(a8(a.v[0], p04), a8(a.v[3], q73)), M11 = m8(a8(a.v[0], p40), a8(a.v[3], q37));
+  const s2v8 M01 = m8(a8(a.v[1], r51), a8(a.v[2], s26)), M10 = m8(a8(a.v[1], r15), a8(a.v[2], s62));
+  s2v8 T = m8(SH8(M00, M11, 0, 2), SH8(M00, M11, 1, 3));   /* (m00, m11) */
+  s2v8 U = m8(SH8(M01, M10, 0, 2), SH8(M01, M10, 1, 3));   /* (m01, m10) */
+  T = a8(T, (s2v8){(short)-g11, g11});
+  U = a8(U, (s2v8){(short)-g10, g10});
+  const s2v8 V = m8(T, U);
+  return sa8((int)V.y - V.x);
+}
+
+struct td8_blk_t {   /* one wave's scratch: 4 blocks interleaved, element e of block g at
+                        64 (e >> 4) + 16 g + (e & 15) (a step of the whole wave = one 128-byte line) */
+  short *s0, *s1, *s2, *yp1, *yp2, *ext, *ext2;
+  uint4 *A;
+};
+
+__device__ __forceinline__ uint32_t t8_ix(uint32_t e) { return ((e >> 4) << 6) | (e & 15); }
+
+__host__ __device__ __forceinline__ size_t t8_n16(uint32_t K) { return (K + 16 * (TD8_FS + TD8_SEG) + 64 + 15) & ~(size_t)15; }
+
+__device__ __forceinline__ td8_blk_t t8_layout(uint8_t *base, uint32_t K)
+{
+  td8_blk_t b;
+  short *p = (short *)base;
+  const size_t n = t8_n16(K);
+  b.s0 = p; p += 4 * n;
+  b.s1 = p; p += 4 * n;
+  b.s2 = p; p += 4 * n;
+  b.yp1 = p; p += 4 * n;
+  b.yp2 = p; p += 4 * n;
+  b.ext = p; p += 4 * n;
+  b.ext2 = p; p += 4 * n;
+  b.A = (uint4 *)(((uintptr_t)p + 15) & ~(uintptr_t)15);
+  return b;
+}
+
+/* log_map8 for the calling lane (window q of its block) */
+template <bool POST>
+__device__ __attribute__((noinline)) void log_map8_lane(const short *sys, const short *par, short *ext, uint4 *A, uint32_t K,
+                                                        uint32_t q, uint4 *asave /* [17][64] */, const short *s0)
+{
+  const uint32_t K1 = K >> 4, nseg = (K1 + TD8_SEG - 1) / TD8_SEG, lane = threadIdx.x & 63;
+  uint4 *A16 = A + 64 * (nseg + 1);              /* first-run alpha(16) */
+  constexpr int FS = TD8_FS;
+  const uint32_t nfc = (K1 + FS - 1) / FS;
+  tm8_t a = init8(q == 0);
+  {
+    s2v8 nsp[FS];
+#pragma unroll
+    for (int j = 0; j < FS; j++) nsp[j] = (s2v8){sys[64 * j + q], par[64 * j + q]};
+    for (uint32_t c = 0; c < nfc; c++) {
+      s2v8 csp[FS];
+#pragma unroll
+      for (int j = 0; j < FS; j++) csp[j] = nsp[j];
+      if (c + 1 < nfc) {
+        const uint32_t b = 64 * FS * (c + 1) + q;
+#pragma unroll
+        for (int j = 0; j < FS; j++) nsp[j] = (s2v8){sys[b + 64 * j], par[b + 64 * j]};
+      }
+#pragma unroll
+      for (int j = 0; j < FS; j++) {
+        const uint32_t k = c * FS + j;
+        if (k < K1) {
+          alpha8_step(a, (short)(((int)csp[j].x + csp[j].y) >> 1), (short)(((int)csp[j].x - csp[j].y) >> 1));
+          if (k + 1 == TD8_L) A16[q] = pk8(a);
+          if (((k + 1) & (TD8_SEG - 1)) == 0) A[64 * ((k + 1) / TD8_SEG) + q] = pk8(a);
+        }
+      }
+    }
+  }
+  const tm8_t fin = a;
+  {   /* re-run seed: slli by one lane; window 0 restarts from the known state */
+    const tm8_t z = init8(true);
+#pragma unroll
+    for (int v = 0; v < 4; v++) {
+      const uint32_t up = (uint32_t)__shfl_up((int)__builtin_bit_cast(uint32_t, a.v[v]), 1, 16);
+      a.v[v] = q == 0 ? z.v[v] : __builtin_bit_cast(s2v8, up);
+    }
+  }
+  A[q] = pk8(a);
+  for (uint32_t k = 0; k < TD8_L; k++) {
+    const short s = sys[64 * k + q], p = par[64 * k + q];
+    alpha8_step(a, (short)(((int)s + p) >> 1), (short)(((int)s - p) >> 1));
+    if (((k + 1) & (TD8_SEG - 1)) == 0) A[64 * ((k + 1) / TD8_SEG) + q] = pk8(a);
+  }
+  /* backward first run from the final alpha, window 15 from the zeroed termination */
+  tm8_t b = q == 15 ? zero8() : fin;
+  const int kr = (int)K1 - (TD8_L + 1);          /* steps >= kr take their extrinsic from the re-run */
+  const uint4 a16v = A16[q];
+  s2v8 nsp[TD8_SEG], nzz[TD8_SEG / 2];
+  uint4 nA;
+  auto fetch = [&](int seg) {
+    const uint32_t b0 = 64u * (uint32_t)(seg * TD8_SEG) + q;
+#pragma unroll
+    for (int j = 0; j < TD8_SEG; j++) nsp[j] = (s2v8){sys[b0 + 64 * j], par[b0 + 64 * j]};
+    if constexpr (POST) {
+#pragma unroll
+      for (int i = 0; i < TD8_SEG / 2; i++) nzz[i] = (s2v8){s0[b0 + 128 * i], s0[b0 + 128 * i + 64]};
+    }
+    nA = A[64 * seg + q];
+  };
+  fetch((int)nseg - 1);
+  for (int seg = (int)nseg - 1; seg >= 0; seg--) {
+    const int k0 = seg * TD8_SEG, n = min((int)TD8_SEG, (int)K1 - k0);
+    s2v8 css[TD8_SEG / 2], czz[TD8_SEG / 2];
+    uint4 al[TD8_SEG];
+    uint32_t gg[TD8_SEG];
+    tm8_t c = up8(nA);
+#pragma unroll
+    for (int j = 0; j < TD8_SEG; j++) {
+      const short x11 = (short)(((int)nsp[j].x + nsp[j].y) >> 1), x10 = (short)(((int)nsp[j].x - nsp[j].y) >> 1);
+      gg[j] = (uint16_t)x11 | ((uint32_t)(uint16_t)x10 << 16);
+    }
+#pragma unroll
+    for (int i = 0; i < TD8_SEG / 2; i++) {
+      css[i] = (s2v8){nsp[2 * i].x, nsp[2 * i + 1].x};
+      czz[i] = nzz[i];
+    }
+    if (seg > 0) fetch(seg - 1);
+#pragma unroll
+    for (int j = 0; j < TD8_SEG; j++) {
+      al[j] = pk8(c);
+      if (k0 + j == TD8_L) c = up8(a16v);        /* alpha(17) continues the first run */
+      alpha8_step(c, (short)gg[j], (short)(gg[j] >> 16));
+    }
+#pragma unroll
+    for (int j = TD8_SEG - 1; j >= 0; j--) {
+      const int k = k0 + j;
+      const short x11 = (short)gg[j], x10 = (short)(gg[j] >> 16);
+      if (j < n) {
+        if (k < kr) {
+          short v = ext8_of(up8(al[j]), b, x11, x10);
+          if constexpr (POST) {
+            const short sv = (j & 1) ? css[j >> 1].y : css[j >> 1].x, zv = (j & 1) ? czz[j >> 1].y : czz[j >> 1].x;
+            v = sa8((int)sa8((int)v - sv) + zv);
+          }
+          ext[64 * k + q] = v;
+        } else {
+          asave[(k - kr) * 64 + lane] = al[j];
+        }
+      }
+      tm8_t nb = b;
+      beta8_step(nb, x11, x10);
+#pragma unroll
+      for (int v = 0; v < 4; v++) b.v[v] = j < n ? nb.v[v] : b.v[v];
+    }
+  }
+  /* backward re-run over the last 16 steps from the next window's beta(0) (srli; window 15: 0) */
+#pragma unroll
+  for (int v = 0; v < 4; v++) {
+    const uint32_t dn = (uint32_t)__shfl_down((int)__builtin_bit_cast(uint32_t, b.v[v]), 1, 16);
+    b.v[v] = q == 15 ? (s2v8){0, 0} : __builtin_bit_cast(s2v8, dn);
+  }
+  for (int k = (int)K1 - 1; k >= kr; k--) {
+    const uint32_t e = 64 * k + q;
+    const short s = sys[e], p = par[e], g11 = (short)(((int)s + p) >> 1), g10 = (short)(((int)s - p) >> 1);
+    short v = ext8_of(up8(asave[(k - kr) * 64 + lane]), b, g11, g10);
+    if constexpr (POST) v = sa8((int)sa8((int)v - s) + s0[e]);
+    ext[e] = v;
+    if (k >= (int)K1 - TD8_L) beta8_step(b, g11, g10);
+  }
+}
+
+}  // namespace
+
+size_t oai4g_td8_wave_bytes(uint32_t K)
+{
+  const size_t K1 = K >> 4, nseg = (K1 + TD8_SEG - 1) / TD8_SEG;
+  return ((7 * 4 * t8_n16(K) * 2 + 15) & ~(size_t)15) + (nseg + 2) * 64 * 16 + 256;
+}
+
+/* blockIdx.x decodes blocks 4 blockIdx.x .. +3 (one 64-lane wave).  llr: [n_cb][llr_stride] int16
+ * (3K + 12, 4 more readable), out: [n_cb][out_stride] bytes, iters: [n_cb]. */
+__global__ void __launch_bounds__(64) k_td8(int n_cb, uint32_t K, const int16_t *__restrict__ llr, size_t llr_stride,
+                                            uint8_t *__restrict__ out, size_t out_stride, uint8_t *__restrict__ iters,
+                                            uint32_t max_it, uint32_t crc_type, uint32_t F,
+                                            const uint16_t *__restrict__ pi4, const uint16_t *__restrict__ pi5,
+                                            const uint16_t *__restrict__ pi6, uint8_t *__restrict__ scratch,
+                                            size_t wave_bytes)
+{
+  __shared__ uint32_t crctab[256];
+  __shared__ uint8_t dec[4][6144 / 8 + 8];
+  __shared__ uint32_t done_it[4];
+  __shared__ uint4 asave[(TD8_L + 1) * 64];
+  const uint32_t lane = threadIdx.x, g = lane >> 4, q = lane & 15;
+  const int cb = (int)(blockIdx.x * 4 + g);
+  const bool valid = cb < n_cb;
+  const uint32_t K1 = K >> 4, Kb = K >> 3;
+  for (uint32_t v = lane; v < 256; v += 64) {
+    const uint32_t poly = crc_type == 0 ? 0x864cfbu : 0x800063u;
+    uint32_t r = v << 16;
+    for (int i = 0; i < 8; i++) r = (r & 0x800000u) ? ((r << 1) ^ poly) & 0xffffffu : (r << 1) & 0xffffffu;
+    crctab[v] = r;
+  }
+  if (lane < 4) done_it[lane] = 0;
+  const td8_blk_t Wv = t8_layout(scratch + (size_t)blockIdx.x * wave_bytes, K);
+  td8_blk_t B;
+  B.s0 = Wv.s0 + 16 * g; B.s1 = Wv.s1 + 16 * g; B.s2 = Wv.s2 + 16 * g; B.yp1 = Wv.yp1 + 16 * g;
+  B.yp2 = Wv.yp2 + 16 * g; B.ext = Wv.ext + 16 * g; B.ext2 = Wv.ext2 + 16 * g; B.A = Wv.A + 16 * g;
+  const int16_t *y = llr + (size_t)(valid ? cb : 0) * llr_stride;
+  /* input scaling (:1001-1031): mean of |w0|+|w1|+|w2|+|w3|+2|w4|+2|w5| over 3 (K/16) + 1
+   * vectors of 8 (abs_epi16 keeps -32768), reduced over the block's 16 lanes */
+  int32_t part = 0;
+  if (valid)
+    for (uint32_t i = q; i < 3 * K1 + 1; i += 16) {
+      const int16_t *v = y + 8 * i;
+      int32_t a[6];
+#pragma unroll
+      for (int t = 0; t < 6; t++) a[t] = (int16_t)(v[t] < 0 ? (int16_t)(-(int32_t)v[t]) : v[t]);
+      part += a[0] + a[1] + a[2] + a[3] + 2 * a[4] + 2 * a[5];
+    }
+#pragma unroll
+  for (int o = 8; o >= 1; o >>= 1) part += __shfl_xor(part, o, 16);
+  const int32_t ravg = part / (int32_t)(3 * K);
+  const uint32_t sl = ravg < 16 ? 0 : ravg < 32 ? 1 : ravg < 64 ? 2 : 3, sh = ravg < 128 ? sl : 4;
+  if (valid) {
+    /* demux (:1071-1077): window q, step v <- y8[3 (q K1 + v) + c] */
+    for (uint32_t v0 = 0; v0 < K1; v0 += 8) {
+      short t0[8], t1[8], t2[8];
+#pragma unroll
+      for (int u = 0; u < 8; u++) {
+        const uint32_t t = 3 * (q * K1 + (v0 + u < K1 ? v0 + u : K1 - 1));
+        t0[u] = sa8(y[t] >> (((t) & 15) < 8 ? sl : sh));
+        t1[u] = sa8(y[t + 1] >> (((t + 1) & 15) < 8 ? sl : sh));
+        t2[u] = sa8(y[t + 2] >> (((t + 2) & 15) < 8 ? sl : sh));
+      }
+#pragma unroll
+      for (int u = 0; u < 8; u++)
+        if (v0 + u < K1) {
+          const uint32_t j = 64 * (v0 + u) + q;
+          B.s0[j] = t0[u];
+          B.yp1[j] = t1[u];
+          B.yp2[j] = t2[u];
+        }
+    }
+  }
+  __syncthreads();
+  bool active = valid && max_it > 0;
+  if (valid) log_map8_lane<false>(B.s0, B.yp1, B.ext, B.A, K, q, asave, B.s0);
+  __syncthreads();
+  uint32_t it = 0;
+  for (it = 1; it <= max_it; it++) {
+    if (active) {   /* interleave (pi4) */
+      for (uint32_t v0 = 0; v0 < K1; v0 += TD8_XR) {
+        uint32_t ix[TD8_XR];
+        short val[TD8_XR];
+#pragma unroll
+        for (int u = 0; u < TD8_XR; u++) ix[u] = v0 + u < K1 ? pi4[16 * (v0 + u) + q] : 0u;
+#pragma unroll
+        for (int u = 0; u < TD8_XR; u++) val[u] = B.ext[t8_ix(ix[u])];
+#pragma unroll
+        for (int u = 0; u < TD8_XR; u++)
+          if (v0 + u < K1) B.s2[64 * (v0 + u) + q] = val[u];
+      }
+    }
+    __syncthreads();
+    if (active) log_map8_lane<false>(B.s2, B.yp2, B.ext2, B.A, K, q, asave, B.s0);
+    __syncthreads();
+    if (active) {
+      for (uint32_t v0 = 0; v0 < K1; v0 += TD8_XR) {   /* deinterleave (pi5) + update */
+        uint32_t ix[TD8_XR];
+        short e2[TD8_XR], e1[TD8_XR], z[TD8_XR];
+#pragma unroll
+        for (int u = 0; u < TD8_XR; u++) {
+          const uint32_t i = v0 + u < K1 ? 16 * (v0 + u) + q : q;
+          ix[u] = pi5[i];
+          e1[u] = B.ext[t8_ix(i)];
+          z[u] = B.s0[t8_ix(i)];
+        }
+#pragma unroll
+        for (int u = 0; u < TD8_XR; u++) e2[u] = B.ext2[t8_ix(ix[u])];
+#pragma unroll
+        for (int u = 0; u < TD8_XR; u++)
+          if (v0 + u < K1) B.s1[64 * (v0 + u) + q] = sa8((int)sa8((int)e2[u] - e1[u]) + z[u]);
+      }
+      if (it > 1) {   /* hard decisions, natural MSB-first order (window w = bits [w K1, (w + 1) K1)) */
+        const bool r128 = (K & 0x7f) == 0;
+        for (uint32_t i = q; i < Kb; i += 16) {
+          uint32_t byte = 0;
+#pragma unroll
+          for (int bb = 0; bb < 8; bb++) {
+            const uint32_t bit = 8 * i + bb;
+            short x;
+            if (r128) {
+              const uint32_t w = bit / K1, k = bit - w * K1;
+              x = B.ext2[t8_ix(pi5[16 * k + w])];
+            } else {
+              const uint32_t p = t8_ix(pi6[bit]);
+              x = sa8((int)B.ext2[p] + B.s2[p]);
+            }
+            byte |= (uint32_t)(x > 0) << (7 - bb);
+          }
+          dec[g][i] = (uint8_t)byte;
+          out[(size_t)cb * out_stride + i] = (uint8_t)byte;
+        }
+      }
+    }
+    __syncthreads();
+    if (active && it > 1 && q == 0) {            /* CRC early stop (:1583-1628) */
+      const uint32_t s0b = crc_type == 0 ? (F >> 3) : 0;
+      const uint32_t nbytes = crc_type == 0 ? (K - 24 - F) >> 3 : (K - 24) >> 3;
+      uint32_t reg = 0;
+      for (uint32_t i = 0; i < nbytes; i++) reg = ((reg << 8) & 0xffffffu) ^ crctab[((reg >> 16) ^ dec[g][s0b + i]) & 0xffu];
+      const uint32_t oldcrc = (uint32_t)dec[g][Kb - 3] | ((uint32_t)dec[g][Kb - 2] << 8) | ((uint32_t)dec[g][Kb - 1] << 16);
+      const uint32_t crc = ((reg & 0xffu) << 16) | (reg & 0xff00u) | ((reg >> 16) & 0xffu);
+      if (crc == oldcrc && crc != 0) done_it[g] = it;
+    }
+    __syncthreads();
+    if (active && done_it[g]) active = false;
+    if (active && it < max_it) log_map8_lane<true>(B.s1, B.yp1, B.ext, B.A, K, q, asave, B.s0);
+    __syncthreads();
+    if (!__any(active)) break;
+  }
+  if (valid && q == 0) iters[cb] = (uint8_t)(done_it[g] ? done_it[g] : max_it + 1);
+}
+
+hipError_t oai4g_launch_td8(int n_cb, uint32_t K, const int16_t *d_llr, size_t llr_stride, uint8_t *d_out,
+                            size_t out_stride, uint8_t *d_iters, uint32_t max_it, uint32_t crc_type, uint32_t F,
+                            const uint16_t *d_pi, uint8_t *d_scratch, hipStream_t s)
+{
+  if (n_cb <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_td8, dim3((n_cb + 3) / 4), dim3(64), 0, s, n_cb, K, d_llr, llr_stride, d_out, out_stride,
+                     d_iters, max_it, crc_type, F, d_pi, d_pi + K, d_pi + 2 * K, d_scratch, oai4g_td8_wave_bytes(K));
+  return hipGetLastError();
+}

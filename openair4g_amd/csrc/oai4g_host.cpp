@@ -1704,6 +1704,93 @@ static const uint16_t *td_tables(uint32_t K)
   return d;
 }
 
+/* init_td8 (3gpplte_turbo_decoder_sse_8bit.c:846-892) for K % 16 == 0: 16 windows */
+static const uint16_t *td8_tables(uint32_t K)
+{
+  static std::mutex mu;
+  static std::map<uint32_t, uint16_t *> cache;
+  std::lock_guard<std::mutex> lk(mu);
+  auto it = cache.find(K);
+  if (it != cache.end()) return it->second;
+  const int qi = oai4g_qpp_index(K);
+  if (qi < 0 || (K & 15)) return nullptr;
+  const uint64_t f1 = oai4g_qpp_table[qi].f1, f2 = oai4g_qpp_table[qi].f2;
+  std::vector<uint32_t> pi2(K);
+  for (uint32_t i = 0, j = 0; i < K; i++, j += 16) {
+    if (j >= K) j -= (K - 1);
+    pi2[i] = j;
+  }
+  std::vector<uint16_t> t(3 * (size_t)K);
+  for (uint32_t i = 0; i < K; i++) {
+    const uint32_t pi = (uint32_t)((f1 * i + f2 * (uint64_t)i * i) % K), pi3 = pi2[pi];
+    t[pi2[i]] = (uint16_t)pi3;          /* pi4 */
+    t[K + pi3] = (uint16_t)pi2[i];      /* pi5 */
+    t[2 * K + pi] = (uint16_t)pi2[i];   /* pi6 */
+  }
+  uint16_t *d = nullptr;
+  if (hipMalloc(&d, t.size() * 2) != hipSuccess || hipMemcpy(d, t.data(), t.size() * 2, hipMemcpyHostToDevice) != hipSuccess) {
+    set_err("decoder8 table upload failed");
+    return nullptr;
+  }
+  cache[K] = d;
+  return d;
+}
+
+extern "C" size_t oai4g_td8_scratch_bytes(uint16_t K, int n_cb) { return (size_t)((n_cb + 3) / 4) * oai4g_td8_wave_bytes(K); }
+
+extern "C" int oai4g_td8_batch(int n_cb, uint16_t K, const int16_t *d_llr, size_t llr_stride, uint8_t *d_out,
+                               size_t out_stride, uint8_t *d_iters, uint8_t max_iterations, uint8_t crc_type, uint8_t F,
+                               void *d_scratch, void *stream)
+{
+  NEED_INIT(-1);
+  if (crc_type > OAI4G_CRC24_B) { set_err("turbo decoder8: only CRC24_A / CRC24_B are on the path"); return -1; }
+  if ((K & 15) || K < 512 || oai4g_qpp_index(K) < 0) {
+    set_err("turbo decoder8: K %u outside n %% 16 == 0, n >= 512 (the reference reads past its tables there)", K);
+    return -1;
+  }
+  if ((F & 7) || F + 24 > K) { set_err("turbo decoder8: filler F=%u unsupported", F); return -1; }
+  if (llr_stride < 3 * (size_t)K + 16) { set_err("turbo decoder8: llr_stride < 3K + 16"); return -1; }
+  const uint16_t *pi = td8_tables(K);
+  if (!pi) return -1;
+  HCK(oai4g_launch_td8(n_cb, K, d_llr, llr_stride, d_out, out_stride, d_iters, max_iterations, crc_type, F, pi,
+                       (uint8_t *)d_scratch, (hipStream_t)stream), -1);
+  return 0;
+}
+
+/* phy_threegpplte_turbo_decoder8 drop-in: y = 3n + 12 int16 (the reference's conversion reads 4 more
+ * entries; they only reach its unused tail and are taken as 0 here); decoded_bytes n/8 bytes. */
+extern "C" uint8_t oai4g_phy_threegpplte_turbo_decoder8(const int16_t *y, uint8_t *decoded_bytes, uint16_t n,
+                                                       uint16_t f1, uint16_t f2, uint8_t max_iterations,
+                                                       uint8_t crc_type, uint8_t F)
+{
+  (void)f1;
+  (void)f2;
+  if (oai4g_init() != 0) return 255;
+  if ((n & 15) || n < 512 || oai4g_qpp_index(n) < 0 || crc_type > OAI4G_CRC24_B) {
+    set_err("turbo decoder8: n %u / crc %u outside the restated scope", n, crc_type);
+    return 255;
+  }
+  const size_t ly = 3 * (size_t)n + 16, b_y = (ly * 2 + 255) & ~(size_t)255, b_o = ((size_t)n / 8 + 256) & ~(size_t)255;
+  const size_t b_s = oai4g_td8_scratch_bytes(n, 1);
+  uint8_t *buf = scratch(b_y + b_o + 256 + b_s);
+  if (!buf) return 255;
+  int16_t *dy = (int16_t *)buf;
+  uint8_t *dout = buf + b_y, *dit = dout + b_o, *dscr = dit + 256;
+  std::vector<int16_t> h(ly, 0);
+  memcpy(h.data(), y, (3 * (size_t)n + 12) * 2);
+  uint8_t itc = 255;
+  if (hipMemcpyAsync(dy, h.data(), ly * 2, hipMemcpyHostToDevice, g_scr.s) != hipSuccess ||
+      hipMemcpyAsync(dout, decoded_bytes, n / 8, hipMemcpyHostToDevice, g_scr.s) != hipSuccess ||
+      oai4g_td8_batch(1, n, dy, ly, dout, n / 8, dit, max_iterations, crc_type, F, dscr, g_scr.s) != 0 ||
+      hipMemcpyAsync(decoded_bytes, dout, n / 8, hipMemcpyDeviceToHost, g_scr.s) != hipSuccess ||
+      hipMemcpyAsync(&itc, dit, 1, hipMemcpyDeviceToHost, g_scr.s) != hipSuccess ||
+      hipStreamSynchronize(g_scr.s) != hipSuccess) {
+    set_err("turbo decoder8: HIP error");
+    return 255;
+  }
+  return itc;
+}
+
 /* per wave of 8 blocks (the decoder interleaves a wave's blocks in its scratch) */
 extern "C" size_t oai4g_td_scratch_bytes(uint16_t K, int n_cb) { return (size_t)((n_cb + 7) & ~7) * oai4g_td_block_bytes(K); }
 

@@ -178,6 +178,11 @@ hipError_t oai4g_launch_td16(int n_cb, uint32_t K, const int16_t *d_llr, size_t 
                              size_t out_stride, uint8_t *d_iters, uint32_t max_it, uint32_t crc_type, uint32_t F,
                              const uint16_t *d_pi /* pi4 | pi5 | pi6, K each */, uint8_t *d_scratch, hipStream_t s,
                              uint32_t cg = 1, uint32_t c_per = 1, uint32_t r0 = 0);
+/* 8-bit turbo decoder (oai4g_decode8.hip) */
+size_t oai4g_td8_wave_bytes(uint32_t K);
+hipError_t oai4g_launch_td8(int n_cb, uint32_t K, const int16_t *d_llr, size_t llr_stride, uint8_t *d_out,
+                            size_t out_stride, uint8_t *d_iters, uint32_t max_it, uint32_t crc_type, uint32_t F,
+                            const uint16_t *d_pi, uint8_t *d_scratch, hipStream_t s);
 /* batched UL receive chain (ulsch_decoding.c:1208-1350): per code-block pattern (block size,
  * filler) the NULL map and compact indices of the rate-matching circular buffer */
 #define OAI4G_UL_MAX_C 16
