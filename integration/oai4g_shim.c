@@ -3,7 +3,8 @@
  * ofdm_mod.c:47/85/233, lte_dfts.c idft64..idft2048, crc_byte.c:117/135, lte_segmentation.c:39,
  * 3gpplte_sse.c:380, lte_rate_matching.c:51/464, pcfich.c:48/144, dci.c:2024, pss.c:50, sss.c:47,
  * pbch.c:161, phich.c:401, lte_dl_channel_estimation.c:37, dlsch_demodulation.c:82 (rx_pdsch, TM1),
- * dlsch_scrambling.c:99 (dlsch_unscrambling). */
+ * dlsch_scrambling.c:99 (dlsch_unscrambling), 3gpplte_turbo_decoder_sse_16bit.c:945 / _8bit.c:894,
+ * lte_rate_matching.c:193 / :293 / :688 (the UL decoding chain). */
 #include "PHY/defs.h"
 #include "PHY/extern.h"
 #include "oai4g.h"
@@ -278,3 +279,38 @@ void dlsch_unscrambling(LTE_DL_FRAME_PARMS *frame_parms, int mbsfn_flag, LTE_UE_
   fp_to(frame_parms, &fp);
   oai4g_dlsch_unscrambling(&fp, mbsfn_flag, dlsch->rnti, G, llr, q, Ns);
 }
+
+/* UL turbo decoding chain (CODING/defs.h:470-513, lte_rate_matching.c): the decoders, RX rate
+ * matching, deinterleaving and generate_dummy_w.  The 8-bit decoder covers n % 16 == 0, n >= 512
+ * (255 otherwise, as the reference returns on illegal arguments). */
+uint8_t phy_threegpplte_turbo_decoder16(int16_t *y, uint8_t *decoded_bytes, uint16_t n, uint16_t interleaver_f1,
+                                        uint16_t interleaver_f2, uint8_t max_iterations, uint8_t crc_type, uint8_t F,
+                                        time_stats_t *init_stats, time_stats_t *alpha_stats, time_stats_t *beta_stats,
+                                        time_stats_t *gamma_stats, time_stats_t *ext_stats, time_stats_t *intl1_stats,
+                                        time_stats_t *intl2_stats)
+{
+  (void)init_stats; (void)alpha_stats; (void)beta_stats; (void)gamma_stats; (void)ext_stats; (void)intl1_stats;
+  (void)intl2_stats;
+  return oai4g_phy_threegpplte_turbo_decoder16(y, decoded_bytes, n, interleaver_f1, interleaver_f2, max_iterations,
+                                               crc_type, F);
+}
+uint8_t phy_threegpplte_turbo_decoder8(int16_t *y, uint8_t *decoded_bytes, uint16_t n, uint16_t interleaver_f1,
+                                       uint16_t interleaver_f2, uint8_t max_iterations, uint8_t crc_type, uint8_t F,
+                                       time_stats_t *init_stats, time_stats_t *alpha_stats, time_stats_t *beta_stats,
+                                       time_stats_t *gamma_stats, time_stats_t *ext_stats, time_stats_t *intl1_stats,
+                                       time_stats_t *intl2_stats)
+{
+  (void)init_stats; (void)alpha_stats; (void)beta_stats; (void)gamma_stats; (void)ext_stats; (void)intl1_stats;
+  (void)intl2_stats;
+  return oai4g_phy_threegpplte_turbo_decoder8(y, decoded_bytes, n, interleaver_f1, interleaver_f2, max_iterations,
+                                              crc_type, F);
+}
+int lte_rate_matching_turbo_rx(uint32_t RTC, uint32_t G, int16_t *w, uint8_t *dummy_w, int16_t *soft_input, uint8_t C,
+                               uint32_t Nsoft, uint8_t Mdlharq, uint8_t Kmimo, uint8_t rvidx, uint8_t clear, uint8_t Qm,
+                               uint8_t Nl, uint8_t r, uint32_t *E)
+{
+  return oai4g_lte_rate_matching_turbo_rx(RTC, G, w, dummy_w, soft_input, C, Nsoft, Mdlharq, Kmimo, rvidx, clear, Qm,
+                                          Nl, r, E);
+}
+void sub_block_deinterleaving_turbo(uint32_t D, int16_t *d, int16_t *w) { oai4g_sub_block_deinterleaving_turbo(D, d, w); }
+uint32_t generate_dummy_w(uint32_t D, uint8_t *w, uint8_t F) { return oai4g_generate_dummy_w(D, w, F); }
