@@ -16,8 +16,9 @@
  *     termination betas), produces the extrinsic of each step on the way (compute_ext16), and
  *     its re-run over the last 5 steps starts from the next window's beta[0]; the 6 extrinsic
  *     values that depend on re-run betas are produced by the re-run.
- * Between half-iterations the permuted exchanges (pi4 / pi5 / pi6 of init_td16) go through the
- * block's scratch in global memory; the CRC early stop runs per block.
+ * The permuted exchanges (pi4 / pi5 of init_td16) are fused into the forward pass of the next
+ * half-iteration, which gathers its systematic input and writes it back for its backward pass;
+ * the hard decisions (pi6) and the CRC early stop run per block between the half-iterations.
  */
 #include "oai4g_internal.h"
 
@@ -29,6 +30,10 @@ static __device__ __forceinline__ short ssub(short a, short b) { return __builti
 #define TD_MAXH 128    /* MAX / 2 */
 #ifndef TD_FS
 #define TD_FS 16             /* forward chunk (steps whose operands are loaded one chunk ahead) */
+#endif
+#ifndef TD_FSG
+#define TD_FSG 4             /* forward chunk of the gathered forms (two loads deep: pi, then the gather;
+                                measured best of 2 / 4 / 6 / 8 / 12 / 16 at C5) */
 #endif
 #ifndef TD_XR
 #define TD_XR 32      /* steps per round of the exchange gathers (index loads, then gathers, in flight) */
@@ -168,9 +173,17 @@ static __device__ __forceinline__ void gamma_of(const short *sys, const short *p
 /* Not inlined: one copy for the three call sites keeps the kernel at 2 waves per SIMD.
  * POST: the stored extrinsic is already the next half-iteration's input, ext - sys + s0
  * (the loop's update pass of phy_threegpplte_turbo_decoder16, fused into the store) */
-template <bool POST>
-static __device__ __attribute__((noinline)) void log_map(const short *sys, const short *par, short *ext, uint4 *A, uint32_t K,
-                                               uint32_t q, int tf, uint4 *asave /* [6][64] */, const short *s0)
+/* SRC: where the forward pass takes the systematic input of step k (element 8k + q) from.
+ *   TD_SRC_SYS:  sys[] as stored;
+ *   TD_SRC_INTL: decoder 2's input, ext[pi4] gathered (the interleave exchange of the loop);
+ *   TD_SRC_DINT: decoder 1's input, ext2[pi5] - ext + s0 (the deinterleave + update pass).
+ * The gathered forms are written to sys[] as they are consumed, for the backward pass: the
+ * exchange passes and their re-reads of the exchanged stream disappear. */
+enum { TD_SRC_SYS = 0, TD_SRC_INTL = 1, TD_SRC_DINT = 2 };
+template <bool POST, int SRC>
+static __device__ __attribute__((noinline)) void log_map(short *sys, const short *par, short *ext, uint4 *A, uint32_t K,
+                                               uint32_t q, int tf, uint4 *asave /* [6][64] */, const short *s0,
+                                               const short *gsrc, const uint16_t *pi)
 {
   /* Every global operand of a step is loaded one chunk ahead into registers: the loads are
    * independent of the recursions, but the compiler cannot hoist them across the (possibly
@@ -179,26 +192,64 @@ static __device__ __attribute__((noinline)) void log_map(const short *sys, const
   uint4 *A5 = A + 64 * (nseg + 1);             /* first-run alpha(5) */
   short g11, g10;
   /* forward, first run, in chunks of FS steps (operands of the next chunk in flight) */
-  constexpr int FS = TD_FS;
+  constexpr int FS = SRC == TD_SRC_SYS ? TD_FS : TD_FSG;
   const uint32_t nfc = (K1 + FS - 1) / FS;
   tm_t a = tm_init(q == 0);
   {
     s2v nsp[FS];                                /* (sys, par) of the next chunk */
+    uint32_t nix[FS];                           /* gathered forms: pi of the chunk after next */
+    s2v nez[FS];                                /* TD_SRC_DINT: (ext, s0) of the next chunk */
+    auto pix = [&](uint32_t k) { return (uint32_t)pi[8 * (k < K1 ? k : K1 - 1) + q]; };
+    if constexpr (SRC == TD_SRC_SYS) {
 #pragma unroll
-    for (int j = 0; j < FS; j++) nsp[j] = (s2v){sys[64 * j + q], par[64 * j + q]};
+      for (int j = 0; j < FS; j++) nsp[j] = (s2v){sys[64 * j + q], par[64 * j + q]};
+    } else {
+      uint32_t ix0[FS];
+#pragma unroll
+      for (int j = 0; j < FS; j++) ix0[j] = pix(j);
+#pragma unroll
+      for (int j = 0; j < FS; j++) nix[j] = pix(FS + j);
+#pragma unroll
+      for (int j = 0; j < FS; j++) nsp[j] = (s2v){gsrc[td_ix(ix0[j])], par[64 * j + q]};
+      if constexpr (SRC == TD_SRC_DINT) {
+#pragma unroll
+        for (int j = 0; j < FS; j++) nez[j] = (s2v){ext[64 * j + q], s0[64 * j + q]};
+      }
+    }
     for (uint32_t c = 0; c < nfc; c++) {
       s2v csp[FS];
+      s2v cez[FS];
 #pragma unroll
       for (int j = 0; j < FS; j++) csp[j] = nsp[j];
+      if constexpr (SRC == TD_SRC_DINT) {
+#pragma unroll
+        for (int j = 0; j < FS; j++) cez[j] = nez[j];
+      }
       if (c + 1 < nfc) {
         const uint32_t b = 64 * FS * (c + 1) + q;
+        if constexpr (SRC == TD_SRC_SYS) {
 #pragma unroll
-        for (int j = 0; j < FS; j++) nsp[j] = (s2v){sys[b + 64 * j], par[b + 64 * j]};
+          for (int j = 0; j < FS; j++) nsp[j] = (s2v){sys[b + 64 * j], par[b + 64 * j]};
+        } else {
+          uint32_t ix[FS];
+#pragma unroll
+          for (int j = 0; j < FS; j++) ix[j] = nix[j];
+#pragma unroll
+          for (int j = 0; j < FS; j++) nix[j] = pix(FS * (c + 2) + j);
+#pragma unroll
+          for (int j = 0; j < FS; j++) nsp[j] = (s2v){gsrc[td_ix(ix[j])], par[b + 64 * j]};
+          if constexpr (SRC == TD_SRC_DINT) {
+#pragma unroll
+            for (int j = 0; j < FS; j++) nez[j] = (s2v){ext[b + 64 * j], s0[b + 64 * j]};
+          }
+        }
       }
 #pragma unroll
       for (int j = 0; j < FS; j++) {
         const uint32_t k = c * FS + j;
         if (k < K1) {
+          if constexpr (SRC == TD_SRC_DINT) csp[j].x = sadd(ssub(csp[j].x, cez[j].x), cez[j].y);
+          if constexpr (SRC != TD_SRC_SYS) sys[64 * k + q] = csp[j].x;
           alpha_step(a, (short)(sadd(csp[j].x, csp[j].y) >> 1), (short)(ssub(csp[j].x, csp[j].y) >> 1));
           if (k + 1 == 5) A5[q] = tm_pack(a);
           if (((k + 1) & (TD_SEG - 1)) == 0) A[64 * ((k + 1) / TD_SEG) + q] = tm_pack(a);
@@ -398,73 +449,36 @@ __global__ void __launch_bounds__(64) k_td16(int n_cb, uint32_t K, const int16_t
   }
   __syncthreads();
   bool active = valid && max_it > 0;
-  if (valid) log_map<false>(B.s0, B.yp1, B.ext, B.A, K, q, 0, asave, B.s0);
+  if (valid) log_map<false, TD_SRC_SYS>(B.s0, B.yp1, B.ext, B.A, K, q, 0, asave, B.s0, nullptr, nullptr);
   __syncthreads();
   uint32_t it = 0;
   for (it = 1; it <= max_it; it++) {
-    if (active) {  /* interleave (pi4): TD_XR steps per round; the next round's indices load during the gathers */
-      uint32_t ixn[TD_XR];
-#pragma unroll
-      for (int u = 0; u < TD_XR; u++) ixn[u] = (uint32_t)u < K1 ? pi4[8 * u + q] : 0u;
-      for (uint32_t v0 = 0; v0 < K1; v0 += TD_XR) {
-        uint32_t ix[TD_XR];
-        short val[TD_XR];
-#pragma unroll
-        for (int u = 0; u < TD_XR; u++) ix[u] = ixn[u];
-        if (v0 + TD_XR < K1) {
-#pragma unroll
-          for (int u = 0; u < TD_XR; u++) ixn[u] = v0 + TD_XR + u < K1 ? pi4[8 * (v0 + TD_XR + u) + q] : 0u;
-        }
-#pragma unroll
-        for (int u = 0; u < TD_XR; u++) val[u] = B.ext[td_ix(ix[u])];
-#pragma unroll
-        for (int u = 0; u < TD_XR; u++)
-          if (v0 + u < K1) B.s2[64 * (v0 + u) + q] = val[u];
-      }
-    }
+    /* decoder 2 takes ext[pi4] straight from decoder 1's output (interleave exchange fused) */
+    if (active) log_map<false, TD_SRC_INTL>(B.s2, B.yp2, B.ext2, B.A, K, q, 1, asave, B.s0, B.ext, pi4);
     __syncthreads();
-    if (active) log_map<false>(B.s2, B.yp2, B.ext2, B.A, K, q, 1, asave, B.s0);
-    __syncthreads();
-    if (active) {
-      for (uint32_t v0 = 0; v0 < K1; v0 += TD_XR) {   /* deinterleave (pi5) + update, batched likewise */
+    if (active && it > 1) {
+      for (uint32_t i0 = q; i0 < Kb; i0 += 8 * (TD_XR / 8)) {   /* hard decisions (:1267-1283), MSB first */
         uint32_t ix[TD_XR];
-        short e2[TD_XR], e1[TD_XR], z[TD_XR];
+        short x[TD_XR];
 #pragma unroll
         for (int u = 0; u < TD_XR; u++) {
-          const uint32_t i = v0 + u < K1 ? 8 * (v0 + u) + q : q;
-          ix[u] = pi5[i];
-          e1[u] = B.ext[td_ix(i)];
-          z[u] = B.s0[td_ix(i)];
+          const uint32_t i = i0 + 8 * (u >> 3);
+          ix[u] = i < Kb ? pi6[8 * i + (u & 7)] : 0u;
         }
 #pragma unroll
-        for (int u = 0; u < TD_XR; u++) e2[u] = B.ext2[td_ix(ix[u])];
+        for (int u = 0; u < TD_XR; u++) x[u] = B.ext2[td_ix(ix[u])];
 #pragma unroll
-        for (int u = 0; u < TD_XR; u++)
-          if (v0 + u < K1) B.s1[64 * (v0 + u) + q] = sadd(ssub(e2[u], e1[u]), z[u]);
+        for (int h = 0; h < TD_XR / 8; h++) {
+          const uint32_t i = i0 + 8 * h;
+          uint32_t byte = 0;
+#pragma unroll
+          for (int bb = 0; bb < 8; bb++) byte |= (uint32_t)(x[8 * h + bb] > 0) << (7 - bb);
+          if (i < Kb) {
+            dec[g][i] = (uint8_t)byte;
+            out[cb * out_stride + i] = (uint8_t)byte;
+          }
+        }
       }
-      if (it > 1)
-        for (uint32_t i0 = q; i0 < Kb; i0 += 8 * (TD_XR / 8)) {   /* hard decisions (:1267-1283), MSB first */
-          uint32_t ix[TD_XR];
-          short x[TD_XR];
-#pragma unroll
-          for (int u = 0; u < TD_XR; u++) {
-            const uint32_t i = i0 + 8 * (u >> 3);
-            ix[u] = i < Kb ? pi6[8 * i + (u & 7)] : 0u;
-          }
-#pragma unroll
-          for (int u = 0; u < TD_XR; u++) x[u] = B.ext2[td_ix(ix[u])];
-#pragma unroll
-          for (int h = 0; h < TD_XR / 8; h++) {
-            const uint32_t i = i0 + 8 * h;
-            uint32_t byte = 0;
-#pragma unroll
-            for (int bb = 0; bb < 8; bb++) byte |= (uint32_t)(x[8 * h + bb] > 0) << (7 - bb);
-            if (i < Kb) {
-              dec[g][i] = (uint8_t)byte;
-              out[cb * out_stride + i] = (uint8_t)byte;
-            }
-          }
-        }
     }
     __syncthreads();
     if (active && it > 1 && q == 0) {            /* CRC early stop (:1304-1351) */
@@ -479,7 +493,8 @@ __global__ void __launch_bounds__(64) k_td16(int n_cb, uint32_t K, const int16_t
     }
     __syncthreads();
     if (active && done_it[g]) active = false;
-    if (active && it < max_it) log_map<true>(B.s1, B.yp1, B.ext, B.A, K, q, 0, asave, B.s0);
+    /* decoder 1 takes ext2[pi5] - ext + s0 (deinterleave + update fused) */
+    if (active && it < max_it) log_map<true, TD_SRC_DINT>(B.s1, B.yp1, B.ext, B.A, K, q, 0, asave, B.s0, B.ext2, pi5);
     __syncthreads();
     if (!__any(active)) break;
   }
