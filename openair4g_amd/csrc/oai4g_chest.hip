@@ -267,7 +267,8 @@ __global__ void __launch_bounds__(RXC_WG) k_rx_chest(const chest_dev_t *__restri
   };
   /* dlsch_channel_level over the first PDSCH symbol */
   {
-    const uint32_t l = c->npdcch, *map = c->map + c->map_off[sfi][0];
+    const uint32_t l = c->npdcch;
+    rg32_t *map = (rg32_t *)(c->map + c->map_off[sfi][0]);
     uint32_t part = 0;
     for (uint32_t j = threadIdx.x; j < c->lvl_n[sfi]; j += RXC_WG) part += rx_h2(est(l, (map[j] >> 16) - 5));
     atomicAdd(&acc, part);
@@ -275,7 +276,7 @@ __global__ void __launch_bounds__(RXC_WG) k_rx_chest(const chest_dev_t *__restri
   __syncthreads();
   const uint32_t sh = rx_shift_of((int32_t)acc, c->lvl_div[sfi]);
   if (threadIdx.x == 0) shift[sf] = (uint8_t)sh;
-  const uint32_t *gold = unscramble ? c->gold + (size_t)sfi * c->gold_words : nullptr;
+  rg32_t *gold = unscramble ? (rg32_t *)(c->gold + (size_t)sfi * c->gold_words) : nullptr;
   const int16_t a1 = c->a1, a2 = c->a2;
   for (uint32_t k0 = 0; k0 < c->n_sym; k0 += RXC_S) {
     /* all map words, then all received words of RXC_S symbols, then the arithmetic */
@@ -283,7 +284,7 @@ __global__ void __launch_bounds__(RXC_WG) k_rx_chest(const chest_dev_t *__restri
 #pragma unroll
     for (uint32_t u = 0; u < RXC_S; u++) {
       const uint32_t k = k0 + u, len = k < c->n_sym ? c->len[sfi][k] : 0u;
-      const uint32_t *map = c->map + c->map_off[sfi][k < c->n_sym ? k : 0];
+      rg32_t *map = (rg32_t *)(c->map + c->map_off[sfi][k < c->n_sym ? k : 0]);
 #pragma unroll
       for (uint32_t r = 0; r < RXC_R; r++) {
         const uint32_t j = threadIdx.x + RXC_WG * r;

@@ -23,7 +23,7 @@ __global__ void __launch_bounds__(256) k_rx_level(const rx_dev_t *__restrict__ c
   const uint32_t sf = blockIdx.x, sfi = (c->first_sf + sf * c->sf_step) % 10, l = c->npdcch;
   if (threadIdx.x == 0) acc = 0;
   __syncthreads();
-  const uint32_t *map = c->map + c->map_off[sfi][0];
+  rg32_t *map = (rg32_t *)(c->map + c->map_off[sfi][0]);
   const int32_t *chs = ch + ((size_t)sf * c->nsymb + l) * c->N;
   uint32_t part = 0;
   for (uint32_t j = threadIdx.x; j < c->lvl_n[sfi]; j += blockDim.x) part += rx_h2((uint32_t)chs[map[j] >> 16]);
@@ -47,12 +47,12 @@ __global__ void __launch_bounds__(256) k_rx_llr(const rx_dev_t *__restrict__ c, 
 {
   const uint32_t sf = blockIdx.y, k = blockIdx.x, sfi = (c->first_sf + sf * c->sf_step) % 10;
   const uint32_t l = c->npdcch + k, len = c->len[sfi][k];
-  const uint32_t *map = c->map + c->map_off[sfi][k];
+  rg32_t *map = (rg32_t *)(c->map + c->map_off[sfi][k]);
   const size_t so = ((size_t)sf * c->nsymb + l) * c->N;
   const int32_t *y = rxF + so, *h = ch + so;
   int16_t *out = llr + (size_t)sf * c->llr_stride + c->llr_off[sfi][k];
   const uint32_t sh = shift[sf], base = c->llr_off[sfi][k];
-  const uint32_t *gold = c->gold + (size_t)sfi * c->gold_words;
+  rg32_t *gold = (rg32_t *)(c->gold + (size_t)sfi * c->gold_words);
   const int16_t a1 = c->a1, a2 = c->a2;
   uint32_t mw[RX_R], hv[RX_R], yv[RX_R];
 #pragma unroll

@@ -8,6 +8,10 @@
 #define OAI4G_RX_PRIMS_H
 #include "oai4g_internal.h"
 
+/* global-qualified view of pointers read from the device configuration (generic pointers would
+ * make their loads flat ops, waited for together with every LDS access) */
+typedef const __attribute__((address_space(1))) uint32_t rg32_t;
+
 static __device__ __forceinline__ int16_t rx_sat16(int32_t v) { return (int16_t)max(-32768, min(32767, v)); }
 static __device__ __forceinline__ int16_t rx_abs16(int16_t v) { return v < 0 ? (int16_t)(-(int32_t)v) : v; }
 static __device__ __forceinline__ int32_t rx_madd(int16_t a0, int16_t b0, int16_t a1, int16_t b1)
@@ -25,7 +29,7 @@ static __device__ __forceinline__ uint32_t rx_h2(uint32_t h)
  * stream position b when gold != nullptr, stored at out (one 4 / 8 / 12-byte store) */
 template <int QM>
 static __device__ __forceinline__ void rx_re_llr(uint32_t hv, uint32_t yv, uint32_t sh, int16_t a1, int16_t a2,
-                                                 const uint32_t *__restrict__ gold, uint32_t b, int16_t *out)
+                                                 rg32_t *__restrict__ gold, uint32_t b, int16_t *out)
 {
   const int16_t hr = (int16_t)hv, hi = (int16_t)(hv >> 16), yr = (int16_t)yv, yi = (int16_t)(yv >> 16);
   const int16_t nhi = (int16_t)(-(int32_t)hi);
