@@ -873,6 +873,12 @@ static hipError_t launch_modofdm_t(const cfg_dev_t *d_cfg, const cfg_dev_t *h_cf
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, k_modofdm<LOG2N, MODE, CRS, ECP>, 128, 0) != hipSuccess ||
         occ < 1)
       occ = 1;
+    /* OAI4G_MODOFDM_OCC=n caps the persistent grid at n workgroups per CU (diagnostic: leaves
+     * room for encoder workgroups of the pipelined mode) */
+    if (const char *e = getenv("OAI4G_MODOFDM_OCC")) {
+      const int cap = atoi(e);
+      if (cap >= 1 && cap < occ) occ = cap;
+    }
   }
   const int units = modofdm_geom<LOG2N>::UNITS;
   int want = (n_items + units - 1) / units, cap = occ * (int)h_cfg->n_cu;
