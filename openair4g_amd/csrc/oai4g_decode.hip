@@ -507,10 +507,7 @@ hipError_t oai4g_launch_td16(int n_cb, uint32_t K, const int16_t *d_llr, size_t 
                              uint32_t r0)
 {
   if (n_cb <= 0) return hipSuccess;
-  /* OAI4G_TD_LDS_PAD=bytes (diagnostic): unused dynamic LDS per workgroup, which caps the
-   * workgroups resident per CU */
-  static const int pad = [] { const char *e = getenv("OAI4G_TD_LDS_PAD"); return e ? atoi(e) : 0; }();
-  hipLaunchKernelGGL(k_td16, dim3((n_cb + 7) / 8), dim3(64), (size_t)pad, s, n_cb, K, d_llr, llr_stride, d_out, out_stride,
+  hipLaunchKernelGGL(k_td16, dim3((n_cb + 7) / 8), dim3(64), 0, s, n_cb, K, d_llr, llr_stride, d_out, out_stride,
                      d_iters, max_it, crc_type, F, d_pi, d_pi + K, d_pi + 2 * K, d_scratch, oai4g_td_block_bytes(K), cg,
                      c_per, r0);
   return hipGetLastError();
