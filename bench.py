@@ -236,6 +236,42 @@ def bench_c5_chain(args, world, rank, dist, torch):
             "cpu_baseline": cpu}), flush=True)
 
 
+_C5_WORKER = r"""
+import sys, time
+sys.path.insert(0, sys.argv[1]); sys.path.insert(0, sys.argv[1] + '/tests')
+import bench, oracle_lib as O
+llr = bench.c5_llrs(64, sys.argv[3], 0xC5 + int(sys.argv[5]))
+fn = O.turbo_decode8 if sys.argv[2] == "8" else O.turbo_decode
+n, t0 = 0, time.perf_counter()
+while time.perf_counter() - t0 < float(sys.argv[4]):
+    fn(llr[n % len(llr)], bench.C5_K, max_it=8, crc_type=1); n += 1
+print(n, time.perf_counter() - t0)
+"""
+
+
+def _c5_port_rate(bits, mode, seconds, procs):
+    """The oracle decoder in `procs` independent processes: aggregate code blocks/s."""
+    import subprocess
+    ps = [subprocess.Popen([sys.executable, "-c", _C5_WORKER, ROOT, str(bits), mode, str(seconds), str(i)],
+                           stdout=subprocess.PIPE, text=True) for i in range(procs)]
+    tot, n_all = 0.0, 0
+    for p in ps:
+        out, _ = p.communicate()
+        n, dt = out.split()
+        tot += int(n) / float(dt)
+        n_all += int(n)
+    return tot, n_all
+
+
+def _c5_valu(batch):
+    """k_td16's VALU-busy fraction from the committed pass (profiles/valu_C5.json) at this batch."""
+    try:
+        t = json.load(open(os.path.join(ROOT, "profiles", "valu_C5.json")))
+    except Exception:
+        return None
+    return round(t["k_td16"]["valu_busy"], 4) if t.get("batch") == batch and "k_td16" in t else None
+
+
 def bench_c5(args, world, rank, dist, torch):
     """UL turbo decoding throughput (config C5): subframes of 8 code blocks, K = 5504."""
     import numpy as np
@@ -284,9 +320,13 @@ def bench_c5(args, world, rank, dist, torch):
             dec_fn(llr[n % len(llr)], C5_K, max_it=8, crc_type=crc_type)
             n += 1
         dt = time.perf_counter() - t1
+        cores = host_cores()
+        allc, nall = _c5_port_rate(args.c5_bits, args.c5_mode, max(2.0, args.cpu_seconds / 2), cores) \
+            if cores > 1 else (n / dt, n)
         cpu = {"value": n / C5_CB / dt, "unit": "subframes/s", "cores": 1, "kind": "port",
+               "cpu_model": cpu_model(), "value_all_cores": allc / C5_CB, "cores_all": cores,
                "sample": f"{n} code blocks (K={C5_K}, mode {args.c5_mode}) through the C oracle decoder, "
-                         f"single thread, {dt:.1f} s"}
+                         f"single thread, {dt:.1f} s; {nall} on {cores} cores (independent processes)"}
     if rank == 0:
         print(json.dumps({
             "metric": "UL subframes/sec (C5 turbo decode)" + (", 8-bit decoder" if args.c5_bits == 8 else ""),
@@ -300,6 +340,7 @@ def bench_c5(args, world, rank, dist, torch):
                        "mean_iterations": float(np.mean(its)), "parallelism": f"block-sharded x{world}"},
             "roofline": {"bound": "hbm", "kernel": "k_td8" if args.c5_bits == 8 else "k_td16", "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": ach / HBM_PEAK_GBS, "traffic": None if args.c5_bits == 8 else _traffic("C5", "k_td16", n_sf),
+                         "valu_issue_frac": None if args.c5_bits == 8 or args.c5_mode != "8it" else _c5_valu(n_sf),
                          "note": "latency-bound: traffic (scratch streaming per half-iteration) >> algorithmic bytes"},
             "cpu_baseline": cpu}), flush=True)
 
