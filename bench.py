@@ -345,6 +345,47 @@ def bench_c5(args, world, rank, dist, torch):
             "cpu_baseline": cpu}), flush=True)
 
 
+_FEP_WORKER = r"""
+import sys, time, ctypes, numpy as np
+sys.path.insert(0, sys.argv[1]); sys.path.insert(0, sys.argv[1] + '/tests')
+import oracle_lib as O
+from test_fep_cpu import window_start
+N, n_ant = 2048, int(sys.argv[3])
+fpo = O.frame(100, nb_antennas_tx=2, mode1_flag=0)
+spt, nsym = fpo.samples_per_tti, fpo.symbols_per_tti
+rng = np.random.default_rng(int(sys.argv[4]))
+buf = np.zeros(spt + N + 64, np.int32)
+frame = buf[(-buf.ctypes.data % 64) // 4:][:spt + N]
+frame[:spt] = rng.integers(-2**31, 2**31, size=spt, dtype=np.int64).astype(np.int32)
+obuf = np.zeros(nsym * N + 64, np.int32)
+rxF = obuf[(-obuf.ctypes.data % 64) // 4:][:nsym * N]
+wins = [window_start(fpo, l, Ns, 0, 0) for Ns in (0, 1) for l in range(nsym // 2)]
+ref = O.ref_dfts()
+fn = ref.dft2048 if ref is not None else (lambda x, y, s: O.orc().orc_dft(11, x, y, s))
+n, t0 = 0, time.perf_counter()
+while time.perf_counter() - t0 < float(sys.argv[2]):
+    for a in range(n_ant):
+        for i, st in enumerate(wins):
+            fn(ctypes.c_void_p(frame.ctypes.data + 4 * st), ctypes.c_void_p(rxF.ctypes.data + 4 * N * i), 1)
+    n += 1
+print(n, time.perf_counter() - t0)
+"""
+
+
+def _fep_port_rate(seconds, procs, n_ant):
+    """slot_fep's dft2048 loop (reference build if present, else the oracle) in `procs` processes."""
+    import subprocess
+    ps = [subprocess.Popen([sys.executable, "-c", _FEP_WORKER, ROOT, str(seconds), str(n_ant), str(i)],
+                           stdout=subprocess.PIPE, text=True) for i in range(procs)]
+    tot, n_all = 0.0, 0
+    for p in ps:
+        out, _ = p.communicate()
+        n, dt = out.split()
+        tot += int(n) / float(dt)
+        n_all += int(n)
+    return tot, n_all
+
+
 def bench_fep(args, world, rank, dist, torch):
     """UE receive front end (SURVEY 8f item 3, config "FEP"): slot_fep of every symbol of
     20 MHz subframes on 2 receive antennas (CP removal + 14 x dft2048 per antenna), batched."""
@@ -414,10 +455,13 @@ def bench_fep(args, world, rank, dist, torch):
                     fn(ctypes.c_void_p(frame.ctypes.data + 4 * st), ctypes.c_void_p(rxF.ctypes.data + 4 * N * i), 1)
             n += 1
         dt = time.perf_counter() - t1
+        cores = host_cores()
+        allc, nall = _fep_port_rate(max(2.0, args.cpu_seconds / 2), cores, n_ant) if cores > 1 else (n / dt, n)
         cpu = {"value": n / dt, "unit": "subframes/s", "cores": 1, "kind": "reference" if ref is not None else "port",
+               "cpu_model": cpu_model(), "value_all_cores": allc, "cores_all": cores,
                "sample": f"{n} subframes x {n_ant} antennas x {nsym} dft2048 ("
                          f"{'the reference lte_dfts.c dft2048 built into oracle/_ref' if ref is not None else 'C oracle'}"
-                         f"), single thread, {dt:.1f} s"}
+                         f"), single thread, {dt:.1f} s; {nall} on {cores} cores (independent processes)"}
     if rank == 0:
         print(json.dumps({
             "metric": "UE RX front-end subframes/sec (slot_fep, 20 MHz, 2 RX)", "value": value, "unit": "subframes/s",
