@@ -50,7 +50,7 @@ typedef struct {
   uint8_t frame_type;       /* 0 = FDD, 1 = TDD */
   uint8_t symbols_per_tti;
   uint8_t log2_symbol_size;
-  uint8_t pad0;
+  uint8_t Nid_cell_mbsfn;   /* MBSFN area id (impl_defs_lte.h:482; 36.211 N_ID^MBSFN is 0..255) */
   uint16_t ofdm_symbol_size;
   uint16_t first_carrier_offset;
   uint16_t nb_prefix_samples;
@@ -243,8 +243,9 @@ int oai4g_rx_pdsch_siso(const oai4g_frame_parms_t *frame_parms, const int32_t *r
                         const uint32_t rb_alloc[4], uint8_t Qm, uint8_t num_pdcch_symbols, uint8_t subframe,
                         int16_t *llr, uint8_t *log2_maxh);
 /* dlsch_unscrambling (dlsch_scrambling.c:99, decl LTE_TRANSPORT/proto.h): llr[k] *= 2 c(k) - 1
- * for k < 32 (1 + G / 32) with c_init = rnti 2^14 + q 2^13 + (Ns / 2) 2^9 + Nid_cell (the
- * reference reads rnti from its LTE_UE_DLSCH_t; mbsfn_flag 1 is not supported). */
+ * for k < 32 (1 + G / 32) with c_init = rnti 2^14 + q 2^13 + (Ns / 2) 2^9 + Nid_cell, or with
+ * mbsfn_flag != 0 (PMCH) c_init = (Ns / 2) 2^9 + Nid_cell_mbsfn (:115-118).  The reference reads
+ * rnti from its LTE_UE_DLSCH_t. */
 void oai4g_dlsch_unscrambling(const oai4g_frame_parms_t *frame_parms, int mbsfn_flag, uint16_t rnti, int G,
                               int16_t *llr, uint8_t q, uint8_t Ns);
 /* Batched demodulation: n_sf subframes (subframe index first_subframe + i * subframe_step mod 10)
@@ -268,14 +269,17 @@ int oai4g_rx_batch(oai4g_rx_config_t *cfg, int n_sf, const int32_t *d_rxdataF, c
  * `symbol` of dl_ch_estimates (subcarrier i of RB rb at 5 + 12 rb + i), then the temporal
  * interpolation of the rows between this pilot symbol and the previous one (symbol 0 closes rows
  * 12 / 13 of the previous subframe's pilot 11).  rxdataF / dl_ch_estimates = [nsymb][N] host
- * buffers of the subframe; N_RB_DL 6 / 50 / 100 (other even sizes: the reference's "not
- * implemented" row of zeros; 15 / 25 PRB return -1).  The idft of the estimate into
+ * buffers of the subframe; N_RB_DL 6 / 15 / 25 / 50 / 100 (other sizes: the reference's "not
+ * implemented" row of zeros; 15 PRB with its second-half start 1 + nushift + 3 p, :582).  The idft of the estimate into
  * dl_ch_estimates_time (:704-738, the UE's timing tracker) is not produced.  Returns 0 / -1. */
 int oai4g_lte_dl_channel_estimation(const oai4g_frame_parms_t *frame_parms, const int32_t *rxdataF,
                                     int32_t *dl_ch_estimates, uint8_t Ns, uint8_t p, uint8_t l, uint8_t symbol);
 /* The six interpolation filters of pilot offset k = (nu + nushift) % 6 as the estimator uses them
  * (lte_dl_channel_estimation.c:105-180): fl, f2l2, f, f2, fr, f2r2 (filt96_32.h by formula). */
 void oai4g_chest_filters(uint8_t k, int16_t out[6][24]);
+/* The 25-PRB branch's DC pair (lte_dl_channel_estimation.c:116-173): filt24_k_dcr, filt24_(k+2)_dcl
+ * (filt96_32.h table data). */
+void oai4g_chest_dc_filters(uint8_t k, int16_t out[2][24]);
 /* Batched estimation of every symbol of n_sf consecutive subframes (subframe index first_subframe
  * + i * subframe_step mod 10) in dlsim's order (dlsim.c:2907-2931): d_rxdataF = [n_sf][nsymb][N]
  * followed by the symbol 0 of the subframe after the batch (N more words), d_est = [n_sf][nsymb][N]
@@ -284,6 +288,9 @@ typedef struct oai4g_chest_config oai4g_chest_config_t;
 oai4g_chest_config_t *oai4g_chest_config_create(const oai4g_frame_parms_t *frame_parms, uint8_t p,
                                                 uint8_t first_subframe, uint8_t subframe_step);
 void oai4g_chest_config_destroy(oai4g_chest_config_t *cfg);
+/* Batch elements `subframes_per_element` subframes apart in d_rxdataF (default 1): dlsim's BLER
+ * loop keeps each trial's subframe followed by the next one, whose symbol 0 closes rows 12 / 13. */
+int oai4g_chest_config_set_stride(oai4g_chest_config_t *cfg, uint32_t subframes_per_element);
 int oai4g_chest_batch(oai4g_chest_config_t *cfg, int n_sf, const int32_t *d_rxdataF, int32_t *d_est, void *stream);
 /* The batch chain without the estimate buffer: oai4g_chest_batch followed by oai4g_rx_batch, fused
  * (the estimate of each PDSCH RE is formed in LDS from the pilot rows), same LLRs; d_rxdataF as
@@ -353,6 +360,24 @@ int oai4g_slot_fep(int32_t *const *rxdata, int32_t *const *rxdataF, const oai4g_
 int oai4g_fep_batch(const oai4g_frame_parms_t *frame_parms, int n_sf, int n_ant, const int32_t *d_rx,
                     int32_t *d_rxF, void *stream);
 
+/* ---------------- dlsim's channel stage (SIMULATION/LTE_PHY/dlsim.c:2714-2866) ---------------- */
+/* signal_energy (PHY/TOOLS/signal_energy.c:66, decl TOOLS/defs.h): mean of (re^2 + im^2) >> 4 over
+ * `length` complex int16 samples minus the squared DC, with the SSE code's integer wraps; >= 1. */
+int32_t oai4g_signal_energy(const int32_t *input, uint32_t length);
+/* Batched, device pointers: d_energy[i] = signal_energy(d_x + i * stride, length) — dlsim's tx_lev
+ * of one transmit antenna (:2714-2719).  Asynchronous on `stream`. */
+int oai4g_signal_energy_batch(const int32_t *d_x, int n, size_t stride, uint32_t length, int32_t *d_energy,
+                              void *stream);
+/* dlsim's AWGN (:2852-2866), device pointers, n <= 65535 vectors: vector i is the tx_len samples at
+ * d_tx + i * tx_stride followed by the tail_len samples of the common d_tail (dlsim adds the noise
+ * over two subframes, the second carrying only the next subframe's CRS); d_rx + i * rx_stride gets
+ * (short)(s + sqrt(sigma2_i / 2) g) per I / Q component with sigma2_i in dB = 10 log10(d_tx_lev[i])
+ * + offset_db (offset_db = 10 log10(N / (12 NB_RB)) - SNR - pa_dB) and g ~ N(0, 1) from a counter-
+ * based stream keyed by (seed, first_vector + i, sample).  Asynchronous on `stream`. */
+int oai4g_awgn_batch(const int32_t *d_tx, size_t tx_stride, uint32_t tx_len, const int32_t *d_tail, uint32_t tail_len,
+                     int32_t *d_rx, size_t rx_stride, int n, const int32_t *d_tx_lev, double offset_db, uint64_t seed,
+                     uint32_t first_vector, void *stream);
+
 /* ---------------- uplink turbo decoding ---------------- */
 enum { OAI4G_CRC24_A = 0, OAI4G_CRC24_B = 1 };
 /* phy_threegpplte_turbo_decoder16 (PHY/CODING/3gpplte_turbo_decoder_sse_16bit.c:945, decl
@@ -408,6 +433,9 @@ oai4g_ul_config_t *oai4g_ul_config_create(uint32_t B, uint32_t G, uint8_t Qm, ui
                                           uint32_t Nsoft, uint8_t max_iterations);
 void oai4g_ul_config_destroy(oai4g_ul_config_t *cfg);
 int oai4g_ul_config_C(const oai4g_ul_config_t *cfg);
+/* Decoder of the chain: 16 (default, phy_threegpplte_turbo_decoder16) or 8 (the 8-bit decoder, as
+ * dlsch_decoding with llr8_flag = 1, dlsim -L; one block size K % 16 == 0, K >= 512).  0 / -1. */
+int oai4g_ul_config_set_decoder(oai4g_ul_config_t *cfg, int bits);
 uint32_t oai4g_ul_config_E(const oai4g_ul_config_t *cfg, int r);
 uint32_t oai4g_ul_config_G_offset(const oai4g_ul_config_t *cfg, int r);
 int oai4g_ul_decode_batch(oai4g_ul_config_t *cfg, int n_tb, const int16_t *d_e, size_t e_stride, uint8_t *d_c,

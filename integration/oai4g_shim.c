@@ -25,6 +25,7 @@ static void fp_to(const LTE_DL_FRAME_PARMS *f, oai4g_frame_parms_t *o)
   o->phich_resource = f->phich_config_common.phich_resource;
   o->phich_duration = f->phich_config_common.phich_duration;
   o->tdd_config = f->tdd_config;      o->nb_antennas_tx_eNB = f->nb_antennas_tx_eNB;
+  o->Nid_cell_mbsfn = (uint8_t)f->Nid_cell_mbsfn;   /* 0..255 (36.211 N_ID^MBSFN) */
 }
 
 /* The mirror points INTO the reference's own HARQ buffers, so every write lands in place. */

@@ -37,7 +37,7 @@ class FrameParms(ctypes.Structure):
     _fields_ = [("N_RB_DL", ctypes.c_uint16), ("Nid_cell", ctypes.c_uint16), ("Ncp", ctypes.c_uint8),
                 ("nushift", ctypes.c_uint8), ("mode1_flag", ctypes.c_uint8), ("nb_antennas_tx", ctypes.c_uint8),
                 ("frame_type", ctypes.c_uint8), ("symbols_per_tti", ctypes.c_uint8),
-                ("log2_symbol_size", ctypes.c_uint8), ("pad0", ctypes.c_uint8),
+                ("log2_symbol_size", ctypes.c_uint8), ("Nid_cell_mbsfn", ctypes.c_uint8),
                 ("ofdm_symbol_size", ctypes.c_uint16), ("first_carrier_offset", ctypes.c_uint16),
                 ("nb_prefix_samples", ctypes.c_uint16), ("nb_prefix_samples0", ctypes.c_uint16),
                 ("samples_per_tti", ctypes.c_uint32), ("phich_resource", ctypes.c_uint8),
@@ -204,6 +204,16 @@ _SIGS = {
     "oai4g_lte_dl_channel_estimation": (ctypes.c_int, [ctypes.POINTER(FrameParms), ctypes.c_void_p, ctypes.c_void_p,
                                                        ctypes.c_uint8, ctypes.c_uint8, ctypes.c_uint8, ctypes.c_uint8]),
     "oai4g_chest_filters": (None, [ctypes.c_uint8, ctypes.c_void_p]),
+    "oai4g_chest_dc_filters": (None, [ctypes.c_uint8, ctypes.c_void_p]),
+    "oai4g_ul_config_set_decoder": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
+    "oai4g_chest_config_set_stride": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_uint32]),
+    "oai4g_signal_energy": (ctypes.c_int32, [ctypes.c_void_p, ctypes.c_uint32]),
+    "oai4g_signal_energy_batch": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_size_t, ctypes.c_uint32,
+                                                 ctypes.c_void_p, ctypes.c_void_p]),
+    "oai4g_awgn_batch": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_uint32, ctypes.c_void_p,
+                                        ctypes.c_uint32, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int,
+                                        ctypes.c_void_p, ctypes.c_double, ctypes.c_uint64, ctypes.c_uint32,
+                                        ctypes.c_void_p]),
     "oai4g_chest_config_create": (ctypes.c_void_p, [ctypes.POINTER(FrameParms), ctypes.c_uint8, ctypes.c_uint8,
                                                     ctypes.c_uint8]),
     "oai4g_chest_config_destroy": (None, [ctypes.c_void_p]),
@@ -480,10 +490,10 @@ def rx_pdsch_siso(fp, rxdataF, dl_ch, rb_alloc, Qm, num_pdcch, subframe):
     return out[:n], sh.value
 
 
-def dlsch_unscrambling(fp, rnti, G, llr, q, Ns):
+def dlsch_unscrambling(fp, rnti, G, llr, q, Ns, mbsfn_flag=0):
     """dlsch_unscrambling drop-in (in place on an int16 array of >= 32 (1 + G/32) entries)."""
     init()
-    lib().oai4g_dlsch_unscrambling(ctypes.byref(fp), 0, rnti, G, _ptr(llr), q, Ns)
+    lib().oai4g_dlsch_unscrambling(ctypes.byref(fp), mbsfn_flag, rnti, G, _ptr(llr), q, Ns)
     return llr
 
 
@@ -494,6 +504,13 @@ def lte_dl_channel_estimation(fp, rxdataF, est, Ns, p, l, symbol):
     assert est.dtype == np.int32 and est.flags.c_contiguous
     _check(lib().oai4g_lte_dl_channel_estimation(ctypes.byref(fp), _ptr(rxdataF), _ptr(est), Ns, p, l, symbol) == 0)
     return est
+
+
+def chest_dc_filters(k):
+    """The 25-PRB DC-pair filters (filt24_k_dcr, filt24_(k+2)_dcl) of pilot offset k."""
+    out = np.zeros((2, 24), dtype=np.int16)
+    lib().oai4g_chest_dc_filters(k, _ptr(out))
+    return out
 
 
 def chest_filters(k):
@@ -883,8 +900,8 @@ def dlsch_encoding(a, fp, num_pdcch, dl, subframe):
     return lib().oai4g_dlsch_encoding(_ptr(a), ctypes.byref(fp), num_pdcch, dl.ptr, 0, subframe)
 
 
-def dlsch_scrambling(fp, dl, G, q, Ns):
-    lib().oai4g_dlsch_scrambling(ctypes.byref(fp), 0, dl.ptr, G, q, Ns)
+def dlsch_scrambling(fp, dl, G, q, Ns, mbsfn_flag=0):
+    lib().oai4g_dlsch_scrambling(ctypes.byref(fp), mbsfn_flag, dl.ptr, G, q, Ns)
 
 
 def dlsch_modulation(txdataF, amp, subframe, fp, num_pdcch, dl0, dl1=None):

@@ -12,7 +12,7 @@ ROOT = os.path.dirname(HERE)
 CSRC = os.path.join(HERE, "csrc")
 LIBDIR = os.path.join(HERE, "lib")
 LIB = os.path.join(LIBDIR, "libopenair4g_amd.so")
-SOURCES = ["oai4g_host.cpp", "oai4g_encode.hip", "oai4g_ofdm.hip", "oai4g_decode.hip", "oai4g_decode8.hip", "oai4g_fep.hip", "oai4g_ctrl.hip", "oai4g_rx.hip", "oai4g_chest.hip"]
+SOURCES = ["oai4g_host.cpp", "oai4g_encode.hip", "oai4g_ofdm.hip", "oai4g_decode.hip", "oai4g_decode8.hip", "oai4g_fep.hip", "oai4g_ctrl.hip", "oai4g_rx.hip", "oai4g_chest.hip", "oai4g_channel.hip"]
 EXTRA = [os.path.join(ROOT, "include", "oai4g_qpp.c"), os.path.join(ROOT, "include", "oai4g_tbs.c")]
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = os.environ.get("OAI4G_ARCH", "gfx950")

@@ -2,7 +2,8 @@
  * gfx950 kernels for the UE's downlink channel estimation from the cell-specific reference
  * signals:
  *   lte_dl_channel_estimation   PHY/LTE_ESTIMATION/lte_dl_channel_estimation.c:37-336 (6 / 50 / 100
- *                               PRB interpolator), 629-701 (temporal interpolation with
+ *                               PRB interpolator), 338-533 (25 PRB: the DC-pair filters),
+ *                               535-623 (15 PRB: f / f2 only, its second-half start), 629-701 (temporal interpolation with
  *                               high_speed_flag = 1, dlsim.c:2057)
  *   lte_dl_cell_spec_rx         PHY/LTE_REFSIG/lte_dl_cell_spec.c:205-260
  *   multadd_real_vector_complex_scalar / multadd_complex_vector_real_scalar  PHY/TOOLS/cmult_sv.c:55-122
@@ -40,11 +41,23 @@ __device__ uint32_t ce_pilot_ch(const chest_dev_t *__restrict__ c, const int32_t
   const uint32_t idx = (c->gold[Ns][l01][mp >> 4] >> (2 * (mp & 15))) & 3u;
   /* lte_dl_cell_spec_rx's conjugated QPSK: (a,-a), (-a,-a), (a,a), (-a,a), a = ONE_OVER_SQRT2_Q15 */
   const int32_t pr = (idx & 1u) ? -23170 : 23170, pi = idx < 2 ? -23170 : 23170;
-  const uint32_t bin = m < N_RB ? c->fco + k + 6 * m : 1 + k + 6 * (m - N_RB);
+  const uint32_t bin = m < N_RB ? c->fco + k + 6 * m : c->off2[l01] + 6 * (m - N_RB);
   const uint32_t w = (uint32_t)row[bin];
   const int32_t rr = (int16_t)w, ri = (int16_t)(w >> 16);
   const int16_t chr = (int16_t)((pr * rr - pi * ri) >> 15), chi = (int16_t)((pr * ri + pi * rr) >> 15);
   return (uint32_t)(uint16_t)chr | ((uint32_t)(uint16_t)chi << 16);
+}
+
+/* filter of pilot m (of 2 N_RB): the edge filters except at 15 PRB, the DC pair (24, 25) at 25 PRB
+ * (lte_dl_channel_estimation.c:212-623) */
+__device__ __forceinline__ uint32_t ce_kind(uint32_t N_RB, uint32_t m)
+{
+  if (N_RB != 15) {
+    if (m < 2) return m;
+    if (m + 2 >= 2 * N_RB) return 4 + (m + 2 - 2 * N_RB);
+    if (N_RB == 25 && (m >> 1) == 12) return 6 + (m & 1u);
+  }
+  return 2 + (m & 1u);
 }
 
 /* first pair index whose windows [12 q, 12 q + 28) can cover column j */
@@ -60,8 +73,7 @@ __device__ uint32_t ce_column(uint32_t N_RB, const int16_t (*__restrict__ f)[24]
     for (uint32_t h = 0; h < 2; h++) {
       const uint32_t m = 2 * q + h, s = 12 * q + 4 * h;
       if (j < s || j - s >= 24) continue;
-      const uint32_t kind = m == 0 ? 0 : m == 1 ? 1 : m == 2 * N_RB - 2 ? 4 : m == 2 * N_RB - 1 ? 5 : 2 + h;
-      const int16_t tap = f[kind][j - s];
+      const int16_t tap = f[ce_kind(N_RB, m)][j - s];
       if (!tap) continue;                                   /* adds of 0: exact to skip */
       const uint32_t v = chl[m - m_base];
       ar = ce_sat16(ar + ce_mulhi_shl((int16_t)v, tap, 2));
@@ -119,15 +131,15 @@ __global__ void __launch_bounds__(CE_WG) k_chest(const chest_dev_t *__restrict__
                                                  int32_t *__restrict__ est)
 {
   __shared__ uint32_t chl[5][CE_MAXP];
-  __shared__ int16_t flt[2][6][24];
+  __shared__ int16_t flt[2][8][24];
   const uint32_t sf = blockIdx.y, N = c->N, nsymb = c->nsymb, Ncp = c->Ncp, N_RB = c->N_RB;
   const uint32_t sfi = (c->first_sf + sf * c->sf_step) % 10;
   const uint32_t p1 = Ncp ? 3 : 4, p2 = Ncp ? 6 : 7, p3 = Ncp ? 9 : 11;
   const uint32_t j0 = blockIdx.x * CE_WG, j1 = min(N, j0 + CE_WG);
   uint32_t m_base, n_p;
   ce_window(N_RB, j0, j1, m_base, n_p);
-  for (uint32_t i = threadIdx.x; i < 2 * 6 * 24; i += CE_WG) (&flt[0][0][0])[i] = (&c->filt[0][0][0])[i];
-  const int32_t *base = rxF + (size_t)sf * nsymb * N;
+  for (uint32_t i = threadIdx.x; i < 2 * 8 * 24; i += CE_WG) (&flt[0][0][0])[i] = (&c->filt[0][0][0])[i];
+  const int32_t *base = rxF + (size_t)sf * c->elem_syms * N;
   if (c->branch)
     for (uint32_t i = threadIdx.x; i < 5 * n_p; i += CE_WG) {
       const uint32_t in = i / n_p, m = m_base + i % n_p;
@@ -159,13 +171,13 @@ __global__ void __launch_bounds__(CE_WG) k_chest_symbol(const chest_dev_t *__res
                                                         uint32_t Ns, uint32_t l01, uint32_t symbol)
 {
   __shared__ uint32_t chl[CE_MAXP];
-  __shared__ int16_t flt[6][24];
+  __shared__ int16_t flt[8][24];
   const uint32_t N = c->N, Ncp = c->Ncp, N_RB = c->N_RB;
   const uint32_t p1 = Ncp ? 3 : 4, p2 = Ncp ? 6 : 7, p3 = Ncp ? 9 : 11;
   const uint32_t j0 = blockIdx.x * CE_WG, j1 = min(N, j0 + CE_WG);
   uint32_t m_base, n_p;
   ce_window(N_RB, j0, j1, m_base, n_p);
-  for (uint32_t i = threadIdx.x; i < 6 * 24; i += CE_WG) (&flt[0][0])[i] = (&c->filt[l01][0][0])[i];
+  for (uint32_t i = threadIdx.x; i < 8 * 24; i += CE_WG) (&flt[0][0])[i] = (&c->filt[l01][0][0])[i];
   if (c->branch)
     for (uint32_t i = threadIdx.x; i < n_p; i += CE_WG) chl[i] = ce_pilot_ch(c, rxF_sym, Ns, l01, m_base + i);
   __syncthreads();
@@ -237,14 +249,14 @@ __global__ void __launch_bounds__(RXC_WG) k_rx_chest(const chest_dev_t *__restri
                                                      uint8_t *__restrict__ shift, int unscramble)
 {
   __shared__ uint32_t chl[5][2 * 100];
-  __shared__ int16_t flt[2][6][24];
+  __shared__ int16_t flt[2][8][24];
   __shared__ uint32_t P[5][RXC_COLS];
   __shared__ uint32_t acc;
   const uint32_t sf = blockIdx.x, N = ce->N, nsymb = ce->nsymb, Ncp = ce->Ncp, N_RB = ce->N_RB;
   const uint32_t sfi = (ce->first_sf + sf * ce->sf_step) % 10;
   const uint32_t p1 = Ncp ? 3 : 4, p2 = Ncp ? 6 : 7, p3 = Ncp ? 9 : 11, np = 2 * N_RB, ncol = 12 * N_RB;
-  const int32_t *base = rxF + (size_t)sf * nsymb * N;
-  for (uint32_t i = threadIdx.x; i < 2 * 6 * 24; i += RXC_WG) (&flt[0][0][0])[i] = (&ce->filt[0][0][0])[i];
+  const int32_t *base = rxF + (size_t)sf * ce->elem_syms * N;
+  for (uint32_t i = threadIdx.x; i < 2 * 8 * 24; i += RXC_WG) (&flt[0][0][0])[i] = (&ce->filt[0][0][0])[i];
   if (threadIdx.x == 0) acc = 0;
   if (ce->branch)
     for (uint32_t i = threadIdx.x; i < 5 * np; i += RXC_WG) {

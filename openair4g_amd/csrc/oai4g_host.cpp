@@ -1183,6 +1183,50 @@ extern "C" int oai4g_sync(void)
   HCK(hipDeviceSynchronize(), -1);
   return 0;
 }
+/* ------------------------------------------------------------------------------------------
+ * dlsim's channel stage (dlsim.c:2714-2866): tx_lev and AWGN, device batches and the host drop-in
+ * ---------------------------------------------------------------------------------------- */
+extern "C" int oai4g_signal_energy_batch(const int32_t *d_x, int n, size_t stride, uint32_t length, int32_t *d_energy,
+                                         void *stream)
+{
+  NEED_INIT(-1);
+  if (n < 0 || length < 2 || (n > 0 && (!d_x || !d_energy))) { set_err("signal_energy_batch: bad arguments"); return -1; }
+  HCK(oai4g_launch_signal_energy(d_x, n, stride, length, d_energy, (hipStream_t)stream), -1);
+  return 0;
+}
+
+extern "C" int32_t oai4g_signal_energy(const int32_t *input, uint32_t length)
+{
+  NEED_INIT(-1);
+  if (!input || length < 2) { set_err("signal_energy: bad arguments"); return -1; }
+  int32_t e = -1;
+  uint8_t *buf = scratch((size_t)length * 4 + 256);
+  if (!buf) { set_err("signal_energy: scratch allocation failed"); return -1; }
+  int32_t *d_x = (int32_t *)buf, *d_e = (int32_t *)(buf + (((size_t)length * 4 + 127) & ~(size_t)127));
+  if (hipMemcpyAsync(d_x, input, (size_t)length * 4, hipMemcpyHostToDevice, g_scr.s) != hipSuccess ||
+      oai4g_launch_signal_energy(d_x, 1, 0, length, d_e, g_scr.s) != hipSuccess ||
+      hipMemcpyAsync(&e, d_e, 4, hipMemcpyDeviceToHost, g_scr.s) != hipSuccess || hipStreamSynchronize(g_scr.s) != hipSuccess) {
+    set_err("signal_energy: device call failed");
+    return -1;
+  }
+  return e;
+}
+
+extern "C" int oai4g_awgn_batch(const int32_t *d_tx, size_t tx_stride, uint32_t tx_len, const int32_t *d_tail,
+                                uint32_t tail_len, int32_t *d_rx, size_t rx_stride, int n, const int32_t *d_tx_lev,
+                                double offset_db, uint64_t seed, uint32_t first_vector, void *stream)
+{
+  NEED_INIT(-1);
+  if (n < 0 || (n > 0 && (!d_tx || !d_rx || !d_tx_lev || (tail_len && !d_tail))) || n > 65535 ||
+      tx_len + tail_len == 0) {
+    set_err("awgn_batch: bad arguments");
+    return -1;
+  }
+  HCK(oai4g_launch_awgn(d_tx, tx_stride, tx_len, d_tail, tail_len, d_rx, rx_stride, n, d_tx_lev, offset_db, seed,
+                        first_vector, (hipStream_t)stream), -1);
+  return 0;
+}
+
 extern "C" int oai4g_fill_payload(uint8_t *d_payload, size_t bytes, uint64_t seed, void *stream)
 {
   NEED_INIT(-1);
@@ -1449,7 +1493,7 @@ extern "C" void oai4g_dlsch_scrambling(const oai4g_frame_parms_t *frame_parms, i
   uint8_t *e = dlsch->harq_processes[dlsch->current_harq_pid]->e;
   uint32_t x2 = mbsfn_flag == 0 ? ((uint32_t)dlsch->rnti << 14) + ((uint32_t)q << 13) + ((uint32_t)(Ns >> 1) << 9) +
                                       frame_parms->Nid_cell
-                                : ((uint32_t)(Ns >> 1) << 9) + frame_parms->Nid_cell;
+                                : ((uint32_t)(Ns >> 1) << 9) + frame_parms->Nid_cell_mbsfn;   /* :70-72 */
   int n = (1 + (G >> 5)) * 32; /* the reference writes past G (dlsch_scrambling.c:83-92) */
   uint8_t *buf = scratch((size_t)n + 64);
   if (!buf) return;
@@ -1848,6 +1892,7 @@ struct oai4g_ul_config {
   int cap = 0;
   int16_t *d_dfull = nullptr;
   uint8_t *d_td = nullptr;
+  int bits = 16;                  /* 16: phy_threegpplte_turbo_decoder16; 8: the 8-bit decoder (llr8_flag) */
 };
 
 extern "C" void oai4g_ul_config_destroy(oai4g_ul_config_t *cfg)
@@ -1939,6 +1984,25 @@ extern "C" oai4g_ul_config_t *oai4g_ul_config_create(uint32_t B, uint32_t G, uin
   return cfg;
 }
 
+extern "C" int oai4g_ul_config_set_decoder(oai4g_ul_config_t *cfg, int bits)
+{
+  if (!cfg || (bits != 8 && bits != 16)) { set_err("ul_config_set_decoder: bits must be 8 or 16"); return -1; }
+  if (bits == 8 && (cfg->Cminus || (cfg->Kplus & 15) || cfg->Kplus < 512 || (cfg->C == 1 && (cfg->F & 7)))) {
+    set_err("ul_config_set_decoder: the 8-bit decoder needs one block size K %% 16 == 0, K >= 512 (K %u, C- %u)",
+            cfg->Kplus, cfg->Cminus);
+    return -1;
+  }
+  if (bits != cfg->bits) {          /* the scratch size differs: reallocate on the next batch */
+    if (cfg->d_dfull) hipFree(cfg->d_dfull);
+    if (cfg->d_td) hipFree(cfg->d_td);
+    cfg->d_dfull = nullptr;
+    cfg->d_td = nullptr;
+    cfg->cap = 0;
+  }
+  cfg->bits = bits;
+  return 0;
+}
+
 extern "C" int oai4g_ul_config_C(const oai4g_ul_config_t *cfg) { return (int)cfg->C; }
 extern "C" uint32_t oai4g_ul_config_G_offset(const oai4g_ul_config_t *cfg, int r) { return cfg->h.off[r]; }
 extern "C" uint32_t oai4g_ul_config_E(const oai4g_ul_config_t *cfg, int r) { return cfg->h.E[r]; }
@@ -1955,7 +2019,8 @@ extern "C" int oai4g_ul_decode_batch(oai4g_ul_config_t *cfg, int n_tb, const int
     cfg->d_dfull = nullptr;
     cfg->d_td = nullptr;
     const size_t nb = (size_t)n_tb * cfg->C;
-    const size_t td = oai4g_td_scratch_bytes((uint16_t)cfg->Kplus, (int)nb);
+    const size_t td = cfg->bits == 8 ? oai4g_td8_scratch_bytes((uint16_t)cfg->Kplus, (int)nb)
+                                     : oai4g_td_scratch_bytes((uint16_t)cfg->Kplus, (int)nb);
     if (hipMalloc(&cfg->d_dfull, nb * cfg->d_stride * 2) != hipSuccess || hipMalloc(&cfg->d_td, td) != hipSuccess) {
       set_err("ul_decode_batch: device allocation failed");
       cfg->cap = 0;
@@ -1967,6 +2032,14 @@ extern "C" int oai4g_ul_decode_batch(oai4g_ul_config_t *cfg, int n_tb, const int
   HCK(oai4g_launch_ul_rm_deint(cfg->d, &cfg->h, n_tb, d_e, e_stride, cfg->d_dfull, cfg->d_stride, s), -1);
   const uint32_t crc = cfg->C == 1 ? OAI4G_CRC24_A : OAI4G_CRC24_B, F = cfg->C == 1 ? cfg->F : 0;
   const int16_t *y = cfg->d_dfull + 96;
+  if (cfg->bits == 8) {
+    /* every block of one size (set_decoder checked), rows (tb, r) in the d_c / d_iters order */
+    const uint16_t *pi = td8_tables(cfg->Kplus);
+    if (!pi) return -1;
+    HCK(oai4g_launch_td8(n_tb * (int)cfg->C, cfg->Kplus, y, cfg->d_stride, d_c, c_stride, d_iters, cfg->max_it, crc, F,
+                         pi, cfg->d_td, s), -1);
+    return 0;
+  }
   if (cfg->Cminus)
     HCK(oai4g_launch_td16(n_tb * (int)cfg->Cminus, cfg->Kminus, y, cfg->d_stride, d_c, c_stride, d_iters, cfg->max_it,
                           crc, F, td_tables(cfg->Kminus), cfg->d_td, s, cfg->Cminus, cfg->C, 0), -1);
@@ -2972,6 +3045,7 @@ struct oai4g_rx_config {
   uint8_t *d_shift = nullptr;
   int shift_cap = 0;
   uint32_t llr_count[10];
+  bool bad[10];                   /* subframe index whose LLR stream would read unwritten ext slots */
 };
 
 static int rx_alloc_bit(const uint32_t rb_alloc[4], int rb)
@@ -3010,14 +3084,95 @@ static int rx_adjust_G2(const oai4g_frame_parms_t *fp, const uint32_t rb_alloc[4
   return re;
 }
 
+/* dlsch_extract_rbs_single (dlsch_demodulation.c:3167-3681) of one symbol as an extraction map:
+ * the ext slots the call leaves written, each FFT bin | (estimate column 5 + 12 rb + i) << 16, with
+ * the reference's pointer steps (the odd-N_RB RB around DC can write one slot past the step it then
+ * takes; the next RB overwrites it).  n = slots written; nb_rb as the reference counts it. */
+static void rx_extract_map(const oai4g_frame_parms_t *fp, const uint32_t rb_alloc[4], uint32_t subframe, uint32_t l,
+                           std::vector<uint32_t> &map, uint32_t &nb_rb, uint32_t &n)
+{
+  const uint32_t smod = l >= 7u - fp->Ncp ? l - (7u - fp->Ncp) : l;
+  const bool pil = smod == 0 || smod == 4u - fp->Ncp;
+  const uint32_t poff = smod == 4u - fp->Ncp ? 3 : 0, ns = fp->nushift;
+  const int nsymb = fp->Ncp == 0 ? 14 : 12, half = fp->N_RB_DL >> 1;
+  uint32_t slot[12 * 110 + 12];
+  uint32_t ptr = 0, hw = 0;
+  nb_rb = 0;
+  auto put = [&](uint32_t pos, uint32_t bin, uint32_t col) {
+    slot[pos] = bin | (col << 16);
+    hw = pos + 1 > hw ? pos + 1 : hw;
+  };
+  if ((fp->N_RB_DL & 1) == 0) {
+    uint32_t bin = fp->first_carrier_offset;
+    for (int rb = 0; rb < fp->N_RB_DL; rb++) {
+      if (rb == half) bin = 1;
+      if (rx_alloc_bit(rb_alloc, rb)) {
+        for (uint32_t i = 0; i < 12; i++)
+          if (!pil || (i != ns + poff && i != (ns + poff + 6) % 12)) put(ptr++, bin + i, 5 + 12 * rb + i);
+        nb_rb++;
+      }
+      bin += 12;
+    }
+  } else {
+    const int sss_symb = fp->frame_type == 1 ? nsymb - 1 : (nsymb >> 1) - 2;
+    const int pss_symb = fp->frame_type == 1 ? 2 : (nsymb >> 1) - 1;
+    const int li = (int)l;
+    const bool pbch = subframe == 0 && li >= (nsymb >> 1) && li < (nsymb >> 1) + 4;
+    const bool sss = (subframe == 0 || subframe == 5) && li == sss_symb;
+    const bool pss = (fp->frame_type == 0 && (subframe == 0 || subframe == 5) && li == pss_symb) ||
+                     (fp->frame_type == 1 && subframe == 6 && li == pss_symb);
+    const bool excl = pbch || sss || pss;
+    uint32_t bin = fp->first_carrier_offset;
+    for (int rb = 0; rb < fp->N_RB_DL; rb++) {
+      int ind = rx_alloc_bit(rb_alloc, rb);
+      const uint32_t col = 5 + 12 * rb;
+      if (rb == half) {                                       /* :3434-3525, split at bin 0 */
+        if (excl) ind = 0;
+        if (ind) {
+          uint32_t j = 0;
+          for (uint32_t i = 0; i < 12; i++) {
+            const uint32_t b = i < 6 ? bin + i : 1 + i - 6;
+            if (!pil) put(ptr + i, b, col + i);
+            else if (i < 6 ? i != (ns + poff) % 6 : i != (ns + 6 + poff) % 12) put(ptr + j++, b, col + i);
+          }
+          ptr += pil ? 10 : 12;
+          nb_rb++;
+        }
+        bin = 7;
+        continue;
+      }
+      int skip_half = 0;
+      if (excl && rb > half - 3 && rb < half + 3) ind = 0;
+      if (excl) skip_half = rb == half - 3 ? 1 : (rb == half + 3 ? 2 : 0);
+      if (ind) {
+        uint32_t j = 0;
+        if (skip_half) {
+          const uint32_t o = skip_half == 2 ? 6 : 0;
+          for (uint32_t i = 0; i < 6; i++)
+            if (!pil || i != (ns + poff) % 6) put(ptr + j++, bin + i + o, col + i + o);
+          ptr += pil ? 5 : 6;
+        } else {
+          for (uint32_t i = 0; i < 12; i++)
+            if (!pil || (i != ns + poff && i != (ns + poff + 6) % 12)) put(ptr + j++, bin + i, col + i);
+          ptr += pil ? 10 : 12;
+        }
+        nb_rb++;
+      }
+      bin += 12;
+    }
+  }
+  n = hw;
+  map.insert(map.end(), slot, slot + hw);
+}
+
 extern "C" oai4g_rx_config_t *oai4g_rx_config_create(const oai4g_frame_parms_t *fp, const uint32_t rb_alloc[4], uint8_t Qm,
                                                      uint8_t num_pdcch_symbols, uint16_t rnti, uint8_t first_subframe,
                                                      uint8_t subframe_step)
 {
   NEED_INIT(nullptr);
-  if ((fp->N_RB_DL & 1) || fp->nb_antennas_tx != 1 || fp->mode1_flag != 1 || (Qm != 2 && Qm != 4 && Qm != 6) ||
+  if (fp->nb_antennas_tx != 1 || fp->mode1_flag != 1 || (Qm != 2 && Qm != 4 && Qm != 6) ||
       num_pdcch_symbols < 1 || num_pdcch_symbols > 3) {
-    set_err("rx_config: TM1 (one TX port), even N_RB_DL, Qm 2/4/6, 1..3 PDCCH symbols only");
+    set_err("rx_config: TM1 (one TX port), Qm 2/4/6, 1..3 PDCCH symbols only");
     return nullptr;
   }
   const uint32_t nsymb = fp->Ncp == 0 ? 14 : 12, N = fp->ofdm_symbol_size;
@@ -3047,25 +3202,20 @@ extern "C" oai4g_rx_config_t *oai4g_rx_config_create(const oai4g_frame_parms_t *
       const uint32_t l = num_pdcch_symbols + k;
       const uint32_t smod = l >= 7u - fp->Ncp ? l - (7u - fp->Ncp) : l;
       const bool pil = smod == 0 || smod == 4u - fp->Ncp;
-      const uint32_t poff = smod == 4u - fp->Ncp ? 3 : 0;
       h.map_off[sf][k] = (uint32_t)map.size();
-      uint32_t n = 0, nb_rb = 0, bin = fp->first_carrier_offset;
-      for (uint32_t rb = 0; rb < fp->N_RB_DL; rb++) {        /* dlsch_extract_rbs_single, even N_RB_DL */
-        if (rb == (fp->N_RB_DL >> 1u)) bin = 1;
-        if (rx_alloc_bit(rb_alloc, (int)rb)) {
-          for (uint32_t i = 0; i < 12; i++)
-            if (!pil || (i != fp->nushift + poff && i != (fp->nushift + poff + 6) % 12)) {
-              map.push_back((bin + i) | ((5 + 12 * rb + i) << 16));
-              n++;
-            }
-          nb_rb++;
-        }
-        bin += 12;
-      }
+      uint32_t nb_rb = 0, n = 0;
+      rx_extract_map(fp, rb_alloc, sf, l, map, nb_rb, n);
       h.n_ext[sf][k] = n;
       const int adj = Qm == 2 ? 0 : rx_adjust_G2(fp, rb_alloc, sf, l);
       const int len = pil ? (int)nb_rb * 10 - 5 * adj / 6 : (int)nb_rb * 12 - adj;
       h.len[sf][k] = (uint32_t)(len > 0 ? len : 0);
+      if (h.len[sf][k] > n || (k == 0 && 12 * nb_rb > n)) {
+        /* the reference would read ext slots this symbol did not write (odd N_RB_DL with a
+         * PBCH / sync half RB and the unadjusted QPSK length, :3354-3427): a batch that runs
+         * this subframe index is refused */
+        cfg->bad[sf] = true;
+        h.len[sf][k] = h.len[sf][k] < n ? h.len[sf][k] : n;
+      }
       if (h.len[sf][k] > 1280) { set_err("rx_config: > 1280 REs in a symbol (k_rx_llr covers 256 x 5)"); delete cfg; return nullptr; }
       h.llr_off[sf][k] = off;
       off += h.len[sf][k] * Qm;
@@ -3073,7 +3223,7 @@ extern "C" oai4g_rx_config_t *oai4g_rx_config_create(const oai4g_frame_parms_t *
         h.lvl_n[sf] = 12 * nb_rb;
         h.lvl_div[sf] = (pil ? 10 : 12) * nb_rb;
       }
-      if (nb_rb == 0) { set_err("rx_config: empty allocation"); delete cfg; return nullptr; }
+      if (nb_rb == 0) cfg->bad[sf] = true;                   /* empty allocation in this symbol */
     }
     cfg->llr_count[sf] = off;
     max_llr = off > max_llr ? off : max_llr;
@@ -3133,11 +3283,27 @@ extern "C" int oai4g_rx_llr_count(const oai4g_rx_config_t *cfg, int subframe_ind
 
 extern "C" size_t oai4g_rx_llr_stride(const oai4g_rx_config_t *cfg) { return cfg->h.llr_stride; }
 
+/* a batch of n_sf elements must not run a subframe index whose stream the reference would build
+ * from ext slots it did not write (rx_config's bad[]) */
+static int rx_check_batch(const oai4g_rx_config_t *cfg, int n_sf)
+{
+  for (int i = 0; i < n_sf && i < 10; i++) {
+    const uint32_t sfi = (cfg->h.first_sf + (uint32_t)i * cfg->h.sf_step) % 10;
+    if (cfg->bad[sfi]) {
+      set_err("rx_batch: subframe index %u reads extracted REs the reference does not write (odd N_RB_DL with "
+              "PBCH / sync half RBs, or an empty symbol)", sfi);
+      return -1;
+    }
+  }
+  return 0;
+}
+
 extern "C" int oai4g_rx_batch(oai4g_rx_config_t *cfg, int n_sf, const int32_t *d_rxdataF, const int32_t *d_ch,
                               int16_t *d_llr, int unscramble, void *stream)
 {
   NEED_INIT(-1);
   if (n_sf <= 0) return 0;
+  if (rx_check_batch(cfg, n_sf) != 0) return -1;
   if (n_sf > cfg->shift_cap) {
     if (cfg->d_shift) hipFree(cfg->d_shift);
     HCK(hipMalloc(&cfg->d_shift, (size_t)n_sf), -1);
@@ -3157,6 +3323,7 @@ extern "C" int oai4g_rx_pdsch_siso(const oai4g_frame_parms_t *fp, const int32_t 
   NEED_INIT(-1);
   oai4g_rx_config_t *cfg = oai4g_rx_config_create(fp, rb_alloc, Qm, num_pdcch_symbols, 0, subframe, 1);
   if (!cfg) return -1;
+  if (rx_check_batch(cfg, 1) != 0) { oai4g_rx_config_destroy(cfg); return -1; }
   const size_t gb = (size_t)cfg->h.nsymb * cfg->h.N * 4, gs = (gb + 255) & ~(size_t)255;
   const int n = (int)cfg->llr_count[subframe % 10];
   uint8_t *buf = scratch(2 * gs + (size_t)cfg->h.llr_stride * 2 + 256);
@@ -3183,10 +3350,12 @@ extern "C" int oai4g_rx_pdsch_siso(const oai4g_frame_parms_t *fp, const int32_t 
 extern "C" void oai4g_dlsch_unscrambling(const oai4g_frame_parms_t *fp, int mbsfn_flag, uint16_t rnti, int G,
                                          int16_t *llr, uint8_t q, uint8_t Ns)
 {
-  (void)mbsfn_flag;
   NEED_INIT();
   if (G < 0) return;
-  uint32_t x1 = 1u + (1u << 31), x2 = ((uint32_t)rnti << 14) + ((uint32_t)q << 13) + ((uint32_t)(Ns >> 1) << 9) + fp->Nid_cell;
+  /* dlsch_scrambling.c:115-118: the PMCH (mbsfn_flag) sequence depends on the MBSFN area only */
+  uint32_t x1 = 1u + (1u << 31),
+           x2 = mbsfn_flag ? ((uint32_t)(Ns >> 1) << 9) + fp->Nid_cell_mbsfn
+                           : ((uint32_t)rnti << 14) + ((uint32_t)q << 13) + ((uint32_t)(Ns >> 1) << 9) + fp->Nid_cell;
   x2 = x2 ^ ((x2 ^ (x2 >> 1) ^ (x2 >> 2) ^ (x2 >> 3)) << 31);
   auto step = [&]() {
     x1 = (x1 >> 1) ^ (x1 >> 4);
@@ -3216,7 +3385,7 @@ extern "C" void oai4g_dlsch_unscrambling(const oai4g_frame_parms_t *fp, int mbsf
 
 /* ------------------------------------------------------------------------------------------
  * Downlink channel estimation (lte_dl_channel_estimation.c:37-701 with high_speed_flag = 1;
- * one RX antenna; the 6 / 50 / 100 PRB interpolator).
+ * one RX antenna; the 6 / 50 / 100, 25 and 15 PRB interpolators).
  * ---------------------------------------------------------------------------------------- */
 /* filt96_32.h by formula: ramp levels floor(16384 v / 6); the six filters of pilot offset k
  * (lte_dl_channel_estimation.c:105-180) as fl, f2l2, f, f2, fr, f2r2 */
@@ -3242,6 +3411,30 @@ extern "C" void oai4g_chest_filters(uint8_t k, int16_t out[6][24])
   }
 }
 
+/* The DC-pair filters of the 25-PRB interpolator, filt24_k_dcr (last pilot below DC) and
+ * filt24_(k+2)_dcl (first pilot above it), k = 0..5 (filt96_32.h:35-113; used at
+ * lte_dl_channel_estimation.c:431-454).  Their slopes round irregularly, so they are table data. */
+static const int16_t chest_dcr[6][24] = {
+    {2730, 5461, 8192, 10922, 13653, 16384, 14043, 11703, 9362, 7022, 4681},
+    {0, 2730, 5461, 8192, 10922, 13653, 16384, 14043, 11703, 9362, 7022, 4681},
+    {0, 0, 2730, 5461, 8192, 10922, 13653, 16384, 14043, 11703, 9362, 4681, 2341},
+    {0, 0, 0, 2730, 5461, 8192, 10922, 13653, 16384, 14043, 11703, 7022, 4681, 2341},
+    {0, 0, 0, 0, 2730, 5461, 8192, 10922, 13653, 16384, 14043, 11703, 7022, 4681, 2341},
+    {0, 0, 0, 0, 0, 2730, 5461, 8192, 10922, 13653, 16384, 11703, 9362, 7022, 4681, 2730}};
+static const int16_t chest_dcl[6][24] = {
+    {0, 0, 2341, 4681, 7022, 9362, 11703, 16384, 13653, 10922, 8192, 5461, 2730},
+    {0, 0, 0, 2341, 4681, 7022, 9362, 14043, 16384, 13653, 10922, 8192, 5461, 2730},
+    {0, 0, 0, 0, 2341, 7022, 9362, 11703, 14043, 16384, 13653, 10922, 8192, 5461, 2730},
+    {0, 0, 0, 0, 0, 2341, 4681, 9362, 11703, 14043, 16384, 13653, 10922, 8192, 5461, 2730},
+    {0, 0, 0, 0, 0, 0, 4681, 7022, 9362, 11703, 14043, 16384, 13653, 10922, 8192, 5461, 2730},
+    {0, 0, 0, 0, 0, 0, 0, 4681, 7022, 9362, 11703, 14043, 16384, 13653, 10922, 8192, 5461, 2730}};
+
+extern "C" void oai4g_chest_dc_filters(uint8_t k, int16_t out[2][24])
+{
+  memcpy(out[0], chest_dcr[k % 6], sizeof(out[0]));
+  memcpy(out[1], chest_dcl[k % 6], sizeof(out[1]));
+}
+
 struct oai4g_chest_config {
   chest_dev_t h;
   chest_dev_t *d = nullptr;
@@ -3251,22 +3444,24 @@ static int chest_fill(const oai4g_frame_parms_t *fp, uint8_t p, chest_dev_t &h)
 {
   const uint32_t N_RB = fp->N_RB_DL;
   if (p > 1) { set_err("lte_dl_channel_estimation: p %d (ports 0 / 1 only)", p); return -1; }
-  if (N_RB == 15 || N_RB == 25) {
-    set_err("lte_dl_channel_estimation: the odd-N_RB_DL interpolators (15 / 25 PRB) are not built");
-    return -1;
-  }
   memset(&h, 0, sizeof(h));
   h.N = fp->ofdm_symbol_size;
   h.N_RB = N_RB;
   h.nsymb = fp->Ncp == 0 ? 14 : 12;
+  h.elem_syms = h.nsymb;
   h.Ncp = fp->Ncp;
   h.fco = fp->first_carrier_offset;
   h.p = p;
-  h.branch = (N_RB == 6 || N_RB == 50 || N_RB == 100) ? 1 : 0;   /* others: "not implemented", rows of 0 */
+  h.branch = (N_RB == 6 || N_RB == 15 || N_RB == 25 || N_RB == 50 || N_RB == 100) ? 1 : 0;   /* others: "not implemented" */
   for (int l01 = 0; l01 < 2; l01++) {
     const uint32_t nu = p == 0 ? (l01 ? 3 : 0) : (l01 ? 0 : 3);
     h.k[l01] = (nu + fp->nushift) % 6;
+    /* the pilots above DC start at bin 1 + k; the 15-PRB branch uses 1 + nushift + 3 p whatever
+     * nu is (lte_dl_channel_estimation.c:582) */
+    h.off2[l01] = N_RB == 15 ? 1 + fp->nushift + 3 * p : 1 + h.k[l01];
     oai4g_chest_filters((uint8_t)h.k[l01], h.filt[l01]);
+    memcpy(h.filt[l01][6], chest_dcr[h.k[l01]], sizeof(h.filt[l01][6]));
+    memcpy(h.filt[l01][7], chest_dcl[h.k[l01]], sizeof(h.filt[l01][7]));
   }
   lte_gold_table_h(fp, h.gold);
   return 0;
@@ -3287,6 +3482,18 @@ extern "C" oai4g_chest_config_t *oai4g_chest_config_create(const oai4g_frame_par
     return nullptr;
   }
   return cfg;
+}
+
+extern "C" int oai4g_chest_config_set_stride(oai4g_chest_config_t *cfg, uint32_t subframes_per_element)
+{
+  NEED_INIT(-1);
+  if (!cfg || subframes_per_element < 1) { set_err("chest_config_set_stride: bad arguments"); return -1; }
+  cfg->h.elem_syms = cfg->h.nsymb * subframes_per_element;
+  if (hipMemcpy(cfg->d, &cfg->h, sizeof(chest_dev_t), hipMemcpyHostToDevice) != hipSuccess) {
+    set_err("chest_config_set_stride: upload failed");
+    return -1;
+  }
+  return 0;
 }
 
 extern "C" void oai4g_chest_config_destroy(oai4g_chest_config_t *cfg)
@@ -3312,6 +3519,7 @@ extern "C" int oai4g_rx_batch_estimated(oai4g_rx_config_t *rx, oai4g_chest_confi
 {
   NEED_INIT(-1);
   if (!rx || !ce || n_sf < 0) { set_err("rx_batch_estimated: bad arguments"); return -1; }
+  if (rx_check_batch(rx, n_sf) != 0) return -1;
   if (rx->h.N != ce->h.N || rx->h.nsymb != ce->h.nsymb || rx->h.first_sf != ce->h.first_sf ||
       rx->h.sf_step != ce->h.sf_step || ce->h.p != 0 || ce->h.N_RB > 100) {
     set_err("rx_batch_estimated: the demodulation and estimation configurations differ (frame, subframes, port 0)");

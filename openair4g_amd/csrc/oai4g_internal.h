@@ -312,11 +312,19 @@ hipError_t oai4g_launch_modulate_bytes(const cfg_dev_t *d_cfg, const cfg_dev_t *
 struct chest_dev_t {
   uint32_t N, N_RB, nsymb, Ncp, fco, p;
   uint32_t first_sf, sf_step;
-  uint32_t branch;                /* 1: the 6 / 50 / 100 PRB interpolator; 0: "not implemented" (rows of 0) */
+  uint32_t branch;                /* 1: the 6 / 15 / 25 / 50 / 100 PRB interpolators; 0: "not implemented" (rows of 0) */
   uint32_t k[2];                  /* pilot offset (nu + nushift) % 6 for pilot symbols l = 0 / l > 0 */
-  int16_t filt[2][6][24];         /* fl, f2l2, f, f2, fr, f2r2 (filt96_32.h) for k[0] / k[1] */
+  uint32_t off2[2];               /* first bin of the pilots above DC: 1 + k, or 1 + nushift + 3 p at 15 PRB */
+  uint32_t elem_syms;             /* symbols between batch elements in rxdataF (nsymb; 2 nsymb in dlsim's BLER
+                                     loop, where each trial's subframe is followed by the next one) */
+  int16_t filt[2][8][24];         /* fl, f2l2, f, f2, fr, f2r2, f_dc, f2_dc (filt96_32.h) for k[0] / k[1] */
   uint32_t gold[20][2][14];       /* lte_gold_table */
 };
+hipError_t oai4g_launch_signal_energy(const int32_t *d_x, int n, size_t stride, uint32_t length, int32_t *d_out,
+                                      hipStream_t s);
+hipError_t oai4g_launch_awgn(const int32_t *d_tx, size_t tx_stride, uint32_t tx_len, const int32_t *d_tail,
+                             uint32_t tail_len, int32_t *d_rx, size_t rx_stride, int n, const int32_t *d_tx_lev,
+                             double offset_db, uint64_t seed, uint32_t vec0, hipStream_t s);
 hipError_t oai4g_launch_unscramble(int16_t *d_llr, const uint32_t *d_c, int n, hipStream_t s);
 hipError_t oai4g_launch_chest(const chest_dev_t *d_cfg, const chest_dev_t *h_cfg, int n_sf, const int32_t *d_rxF,
                               int32_t *d_est, hipStream_t s);

@@ -1,6 +1,7 @@
 /*
  * gfx950 kernels for the UE's PDSCH demodulation after the FEP (second
- * half): TM1 (one transmit port), one receive antenna, even N_RB_DL.
+ * half): TM1 (one transmit port), one receive antenna; any N_RB_DL (the extraction map carries the
+ * odd-N_RB split around DC).
  *   dlsch_extract_rbs_single    PHY/LTE_TRANSPORT/dlsch_demodulation.c:3167-3300
  *   dlsch_channel_level         dlsch_demodulation.c:2777-2835, log2_maxh :286-300
  *   dlsch_channel_compensation  dlsch_demodulation.c:801-960

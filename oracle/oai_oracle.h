@@ -233,8 +233,19 @@ int orc_tx_subframe_dci(const orc_tx_cfg_t *cfg, uint8_t *payload[2], int32_t **
 #endif
 /* ---- downlink channel estimation (LTE_ESTIMATION/lte_dl_channel_estimation.c:37-701, high_speed_flag 1) ---- */
 void orc_chest_filters(uint8_t k, int16_t out[6][24]);
+void orc_chest_dc_filters(uint8_t k, int16_t out[2][24]);      /* filt24_k_dcr, filt24_(k+2)_dcl */
+const int16_t *orc_chest_pilot_filter(const int16_t f[6][24], const int16_t fdc[2][24], int N_RB, int m);
 int  orc_lte_dl_channel_estimation(const orc_frame_t *fp, const uint32_t gold[20][2][14], const int32_t *rxdataF,
                                    int32_t *dl_ch_estimates, uint8_t Ns, uint8_t p, uint8_t l, uint8_t symbol);
+
+/* ---- dlsim's channel stage (PHY/TOOLS/signal_energy.c:66-110, SIMULATION/TOOLS/rangen_double.c:47-118,
+ *      SIMULATION/LTE_PHY/dlsim.c:2852-2866) ---- */
+int32_t orc_signal_energy(const int32_t *input, uint32_t length);
+void    orc_randominit(uint32_t seed_init);
+double  orc_uniformrandom(void);
+double  orc_gaussdouble(double mean, double variance);
+double  orc_awgn_sigma2(int32_t tx_lev, double offset_db);
+void    orc_awgn(const int32_t *tx, int32_t *rx, uint32_t n, double sigma2);
 
 /* ---- 8-bit turbo decoder (CODING/3gpplte_turbo_decoder_sse_8bit.c:846-1658), n % 16 == 0, n >= 512 ---- */
 void    orc_td8_tables(int n, int *pi2, int *pi4, int *pi5, int *pi6);

@@ -3,8 +3,8 @@
  * cell-specific reference signals, a plain-C restatement of the reference's
  * algorithm loop for loop; never linked into the product library.
  *
- *   lte_dl_channel_estimation  PHY/LTE_ESTIMATION/lte_dl_channel_estimation.c:37-336, 629-701
- *                              (N_RB_DL 6 / 50 / 100 branch; high_speed_flag = 1, dlsim.c:2057 and
+ *   lte_dl_channel_estimation  PHY/LTE_ESTIMATION/lte_dl_channel_estimation.c:37-623, 629-701
+ *                              (N_RB_DL 6 / 50 / 100, 25 and 15 branches; high_speed_flag = 1, dlsim.c:2057 and
  *                              lte_init.c:1212; perfect_ce = 0; eNB_offset 0; one RX antenna).
  *                              The final idft of the estimate into dl_ch_estimates_time (:704-738,
  *                              consumed only by the UE's timing tracker) is not restated.
@@ -65,6 +65,47 @@ void orc_chest_filters(uint8_t k, int16_t out[6][24])
   }
 }
 
+/* The DC-pair filters of the 25-PRB interpolator (filt96_32.h:35-113), reference data (their
+ * right / left slopes round irregularly, so they are kept as the table entries):
+ * filt24_k_dcr for the last pilot below DC, filt24_(k+2)_dcl for the first one above it
+ * (lte_dl_channel_estimation.c:116-173). */
+static const int16_t dcr_tab[6][24] = {
+  {2730, 5461, 8192, 10922, 13653, 16384, 14043, 11703, 9362, 7022, 4681, 0},
+  {0, 2730, 5461, 8192, 10922, 13653, 16384, 14043, 11703, 9362, 7022, 4681},
+  {0, 0, 2730, 5461, 8192, 10922, 13653, 16384, 14043, 11703, 9362, 4681, 2341},
+  {0, 0, 0, 2730, 5461, 8192, 10922, 13653, 16384, 14043, 11703, 7022, 4681, 2341},
+  {0, 0, 0, 0, 2730, 5461, 8192, 10922, 13653, 16384, 14043, 11703, 7022, 4681, 2341},
+  {0, 0, 0, 0, 0, 2730, 5461, 8192, 10922, 13653, 16384, 11703, 9362, 7022, 4681, 2730}};
+static const int16_t dcl_tab[6][24] = {   /* filt24_2_dcl ... filt24_7_dcl */
+  {0, 0, 2341, 4681, 7022, 9362, 11703, 16384, 13653, 10922, 8192, 5461, 2730},
+  {0, 0, 0, 2341, 4681, 7022, 9362, 14043, 16384, 13653, 10922, 8192, 5461, 2730},
+  {0, 0, 0, 0, 2341, 7022, 9362, 11703, 14043, 16384, 13653, 10922, 8192, 5461, 2730},
+  {0, 0, 0, 0, 0, 2341, 4681, 9362, 11703, 14043, 16384, 13653, 10922, 8192, 5461, 2730},
+  {0, 0, 0, 0, 0, 0, 4681, 7022, 9362, 11703, 14043, 16384, 13653, 10922, 8192, 5461, 2730},
+  {0, 0, 0, 0, 0, 0, 0, 4681, 7022, 9362, 11703, 14043, 16384, 13653, 10922, 8192, 5461, 2730}};
+
+void orc_chest_dc_filters(uint8_t k, int16_t out[2][24])
+{
+  memcpy(out[0], dcr_tab[k % 6], sizeof(out[0]));
+  memcpy(out[1], dcl_tab[k % 6], sizeof(out[1]));
+}
+
+/* the filter of pilot m (of 2 N_RB): 6 / 50 / 100 PRB fl, f2l2 at the left edge and fr, f2r2 at
+ * the right edge (:212-333); 25 PRB the same plus f_dc, f2_dc on pilots 24 / 25 (:338-533);
+ * 15 PRB f / f2 throughout (:535-623) */
+const int16_t *orc_chest_pilot_filter(const int16_t f[6][24], const int16_t fdc[2][24], int N_RB, int m)
+{
+  if (N_RB != 15) {
+    if (m == 0) return f[0];
+    if (m == 1) return f[1];
+    if (m == 2 * N_RB - 2) return f[4];
+    if (m == 2 * N_RB - 1) return f[5];
+    if (N_RB == 25 && m == 24) return fdc[0];
+    if (N_RB == 25 && m == 25) return fdc[1];
+  }
+  return (m & 1) ? f[3] : f[2];
+}
+
 /* multadd_complex_vector_real_scalar over one row of N complex entries */
 static void multadd_row(const int32_t *x, int16_t alpha, int32_t *y, int zero_flag, int N)
 {
@@ -90,29 +131,34 @@ int orc_lte_dl_channel_estimation(const orc_frame_t *fp, const uint32_t gold[20]
   else if (p == 1) nu = l == 0 ? 3 : 0;
   else return -1;
   const int k = (nu + fp->nushift) % 6;
-  int16_t f[6][24];
+  int16_t f[6][24], fdc[2][24];
   orc_chest_filters((uint8_t)k, f);
+  orc_chest_dc_filters((uint8_t)k, fdc);
   /* lte_dl_cell_spec_rx: conjugated QPSK pilots, m' = 110 - N_RB_DL + m */
   const int16_t pamp = 23170;
   const int16_t qpsk[4][2] = {{pamp, (int16_t)-pamp}, {(int16_t)-pamp, (int16_t)-pamp}, {pamp, pamp}, {(int16_t)-pamp, pamp}};
   const int32_t *rx = rxdataF + symbol * N;
   int32_t *dl_ch = dl_ch_estimates + N * symbol;            /* ch_offset, high_speed_flag = 1 */
   memset(dl_ch, 0, sizeof(int32_t) * N);
-  if (N_RB == 6 || N_RB == 50 || N_RB == 100) {
+  const int even = N_RB == 6 || N_RB == 50 || N_RB == 100;
+  if (even || N_RB == 15 || N_RB == 25) {
+    /* pilot m of 2 N_RB, left to right; the first N_RB sit above first_carrier_offset, the rest
+     * from bin 1 (DC skipped).  15 PRB restarts the second half at 1 + nushift + 3 p instead of
+     * 1 + k (:582), whatever nu is: reproduced. */
+    const int off2 = N_RB == 15 ? 1 + fp->nushift + 3 * p : 1 + k;
     const int l01 = l == 0 ? 0 : 1;
     for (int m = 0; m < 2 * N_RB; m++) {
       const int mp = 110 - N_RB + m;
       const int16_t *pil = qpsk[(gold[Ns][l01][mp >> 4] >> (2 * (mp & 15))) & 3];
-      /* first half from first_carrier_offset + k, second half from 1 + k (DC skipped) */
-      const int32_t word = m < N_RB ? rx[fp->first_carrier_offset + k + 6 * m] : rx[1 + k + 6 * (m - N_RB)];
+      const int32_t word = m < N_RB ? rx[fp->first_carrier_offset + k + 6 * m] : rx[off2 + 6 * (m - N_RB)];
       int16_t r[2];
       memcpy(r, &word, 4);
       int16_t ch[2];
       ch[0] = (int16_t)(((int32_t)pil[0] * r[0] - (int32_t)pil[1] * r[1]) >> 15);
       ch[1] = (int16_t)(((int32_t)pil[0] * r[1] + (int32_t)pil[1] * r[0]) >> 15);
-      const int16_t *flt = m == 0 ? f[0] : m == 1 ? f[1] : m == 2 * N_RB - 2 ? f[4] : m == 2 * N_RB - 1 ? f[5]
-                         : (m & 1) ? f[3] : f[2];
-      /* dl_ch advances 4 entries after the first pilot of a pair and 8 after the second */
+      const int16_t *flt = orc_chest_pilot_filter(f, fdc, N_RB, m);
+      /* dl_ch advances 4 entries after an even pilot and 8 after an odd one (also across the DC
+       * pair of 15 / 25 PRB, :431-457, :573-592) */
       int32_t *y = dl_ch + 12 * (m >> 1) + 4 * (m & 1);
       for (int i = 0; i < 24; i++) {                         /* multadd_real_vector_complex_scalar */
         int16_t o[2];
@@ -124,8 +170,6 @@ int orc_lte_dl_channel_estimation(const orc_frame_t *fp, const uint32_t gold[20]
         memcpy(&y[i], o, 4);
       }
     }
-  } else if (N_RB == 15 || N_RB == 25) {
-    return -1;                                               /* odd-N_RB branches: not restated */
   }                                                          /* other N_RB: "not implemented", row stays 0 */
   /* temporal interpolation (high_speed_flag = 1, :639-698) */
   int32_t *E = dl_ch_estimates;

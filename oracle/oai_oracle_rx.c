@@ -1,12 +1,15 @@
 /*
  * TEST INFRASTRUCTURE ONLY — CPU oracle of the UE's PDSCH demodulation after the FEP (SURVEY.md
- * §8f item 3, second half), single transmit port (TM1), one receive antenna, even N_RB_DL.
+ * §8f item 3, second half), single transmit port (TM1), one receive antenna.
  * A plain-C restatement of the reference's algorithm, loop for loop; never linked into the
  * product library.
  *
- *   dlsch_extract_rbs_single    PHY/LTE_TRANSPORT/dlsch_demodulation.c:3167-3300 (even N_RB_DL:
- *                               every allocated RB, pilots skipped in symbols 0 / 4-Ncp of a slot;
- *                               NB the reference applies no PBCH / PSS / SSS exclusion here)
+ *   dlsch_extract_rbs_single    PHY/LTE_TRANSPORT/dlsch_demodulation.c:3167-3681 (even N_RB_DL:
+ *                               every allocated RB, pilots skipped in symbols 0 / 4-Ncp of a slot,
+ *                               no PBCH / PSS / SSS exclusion; odd N_RB_DL: the RB around DC split
+ *                               at bin 0, PBCH / PSS / SSS RBs dropped and the two edge RBs
+ *                               halved, with the reference's pointer steps — a stream that would
+ *                               read ext slots the call did not write returns -1)
  *   dlsch_channel_level         dlsch_demodulation.c:2777-2835 (first PDSCH symbol, int32 sums)
  *   log2_maxh                   dlsch_demodulation.c:286-300, log2_approx TOOLS/log2_approx.c:29-45
  *   dlsch_channel_compensation  dlsch_demodulation.c:801-960 (conj(h) y >> shift, packs; |h|^2 >>
@@ -73,25 +76,87 @@ int orc_adjust_G2(const orc_frame_t *fp, const uint32_t rb_alloc[4], uint8_t sub
   return re;
 }
 
-/* extraction of one symbol: returns the number of extracted REs */
+/* one RE of dlsch_extract_rbs_single: writes slot *pos of the ext arrays (tracking the highest
+ * slot written: the odd-N_RB branch can write one past the pointer it then advances) */
+static void put(int32_t *rx_ext, int32_t *ch_ext, int pos, int32_t rx, int32_t ch, int *hw)
+{
+  rx_ext[pos] = rx;
+  ch_ext[pos] = ch;
+  if (pos + 1 > *hw) *hw = pos + 1;
+}
+
+/* extraction of one symbol (dlsch_extract_rbs_single, dlsch_demodulation.c:3167-3681): returns the
+ * final ext pointer; *hw = the number of ext slots written (>= the pointer) */
 static int extract(const orc_frame_t *fp, const int32_t *rxF_sym, const int32_t *ch_sym, const uint32_t rb_alloc[4],
-                   uint8_t symbol, int32_t *rx_ext, int32_t *ch_ext, int *nb_rb)
+                   uint8_t symbol, uint8_t subframe, int32_t *rx_ext, int32_t *ch_ext, int *nb_rb, int *hw)
 {
   const int symbol_mod = symbol >= 7 - fp->Ncp ? symbol - (7 - fp->Ncp) : symbol;
   const int pilots = symbol_mod == 0 || symbol_mod == 4 - fp->Ncp;
   const int poffset = symbol_mod == 4 - fp->Ncp ? 3 : 0;
+  const int nsymb = fp->Ncp == 0 ? 14 : 12, l = symbol, half = fp->N_RB_DL >> 1;
+  const int sss_symb = fp->frame_type == 1 ? nsymb - 1 : (nsymb >> 1) - 2;
+  const int pss_symb = fp->frame_type == 1 ? 2 : (nsymb >> 1) - 1;
   const int32_t *rxF = rxF_sym + fp->first_carrier_offset, *dl_ch0 = ch_sym + 5;
   int n = 0;
   *nb_rb = 0;
+  *hw = 0;
+  if ((fp->N_RB_DL & 1) == 0) {                               /* :3218-3281, no PBCH / PSS / SSS exclusion */
+    for (int rb = 0; rb < fp->N_RB_DL; rb++) {
+      if (rb == half) rxF = rxF_sym + 1;
+      if (alloc_bit(rb_alloc, rb)) {
+        for (int i = 0; i < 12; i++)
+          if (!pilots || (i != fp->nushift + poffset && i != (fp->nushift + poffset + 6) % 12)) {
+            put(rx_ext, ch_ext, n, rxF[i], dl_ch0[i], hw);
+            n++;
+          }
+        (*nb_rb)++;
+      }
+      dl_ch0 += 12;
+      rxF += 12;
+    }
+    return n;
+  }
+  /* odd N_RB_DL (:3282-3676) */
+  const int pbch_l = subframe == 0 && l >= (nsymb >> 1) && l < (nsymb >> 1) + 4;
+  const int sss_l = (subframe == 0 || subframe == 5) && l == sss_symb;
+  const int pss_l = (fp->frame_type == 0 && (subframe == 0 || subframe == 5) && l == pss_symb) ||
+                    (fp->frame_type == 1 && subframe == 6 && l == pss_symb);
   for (int rb = 0; rb < fp->N_RB_DL; rb++) {
-    if (rb == (fp->N_RB_DL >> 1)) rxF = rxF_sym + 1;
-    if (alloc_bit(rb_alloc, rb)) {
-      for (int i = 0; i < 12; i++)
-        if (!pilots || (i != fp->nushift + poffset && i != (fp->nushift + poffset + 6) % 12)) {
-          rx_ext[n] = rxF[i];
-          ch_ext[n] = dl_ch0[i];
-          n++;
+    int ind = alloc_bit(rb_alloc, rb);
+    if (rb == half) {                                         /* the RB around DC (:3434-3525) */
+      if (pbch_l || sss_l || pss_l) ind = 0;
+      if (ind) {
+        int j = 0;
+        for (int i = 0; i < 12; i++) {
+          const int32_t rxv = i < 6 ? rxF[i] : rxF_sym[1 + i - 6];
+          if (!pilots) put(rx_ext, ch_ext, n + i, rxv, dl_ch0[i], hw);
+          else if (i < 6 ? i != (fp->nushift + poffset) % 6 : i != (fp->nushift + 6 + poffset) % 12)
+            put(rx_ext, ch_ext, n + j++, rxv, dl_ch0[i], hw);
         }
+        n += pilots ? 10 : 12;
+        (*nb_rb)++;
+      }
+      rxF = rxF_sym + 7;
+      dl_ch0 += 12;
+      continue;
+    }
+    int skip_half = 0;
+    if ((pbch_l || sss_l || pss_l) && rb > half - 3 && rb < half + 3) ind = 0;
+    if (pbch_l || sss_l || pss_l) skip_half = rb == half - 3 ? 1 : (rb == half + 3 ? 2 : 0);
+    if (ind) {
+      if (skip_half) {
+        const int o = skip_half == 2 ? 6 : 0;
+        int j = 0;
+        for (int i = 0; i < 6; i++)
+          if (!pilots || i != (fp->nushift + poffset) % 6) put(rx_ext, ch_ext, n + j++, rxF[i + o], dl_ch0[i + o], hw);
+        n += pilots ? 5 : 6;
+      } else {
+        int j = 0;
+        for (int i = 0; i < 12; i++)
+          if (!pilots || (i != fp->nushift + poffset && i != (fp->nushift + poffset + 6) % 12))
+            put(rx_ext, ch_ext, n + j++, rxF[i], dl_ch0[i], hw);
+        n += pilots ? 10 : 12;
+      }
       (*nb_rb)++;
     }
     dl_ch0 += 12;
@@ -104,21 +169,20 @@ int orc_rx_pdsch_siso(const orc_frame_t *fp, const int32_t *rxdataF, const int32
                       const uint32_t rb_alloc[4], uint8_t Qm, uint8_t num_pdcch_symbols, uint8_t subframe,
                       int16_t *llr, uint8_t *log2_maxh_out)
 {
-  if (fp->N_RB_DL & 1) return -1;
   const int N = fp->ofdm_symbol_size, nsymb = fp->Ncp == 0 ? 14 : 12;
   int32_t *rx_ext = (int32_t *)malloc(sizeof(int32_t) * 12 * 110), *ch_ext = (int32_t *)malloc(sizeof(int32_t) * 12 * 110);
   int16_t *out = llr;
   uint8_t log2_maxh = 0;
   for (int symbol = num_pdcch_symbols; symbol < nsymb; symbol++) {
-    int nb_rb;
-    const int n = extract(fp, rxdataF + symbol * N, dl_ch_estimates + symbol * N, rb_alloc, (uint8_t)symbol, rx_ext,
-                          ch_ext, &nb_rb);
-    (void)n;
+    int nb_rb, hw;
+    extract(fp, rxdataF + symbol * N, dl_ch_estimates + symbol * N, rb_alloc, (uint8_t)symbol, subframe, rx_ext, ch_ext,
+            &nb_rb, &hw);
     const int symbol_mod = symbol >= 7 - fp->Ncp ? symbol - (7 - fp->Ncp) : symbol;
     const int pil = symbol_mod == 0 || symbol_mod == 4 - fp->Ncp;
     if (symbol == num_pdcch_symbols) {                       /* dlsch_channel_level, first symbol */
       int32_t acc = 0;
       const int nre = pil ? 10 : 12;                           /* mode1_flag = 1 */
+      if (nb_rb * 12 > hw) { out = NULL; break; }              /* would read stale ext slots */
       for (int j = 0; j < nb_rb * 12; j++) {                   /* 3 groups of 4 REs per RB */
         const int16_t hr = (int16_t)(ch_ext[j] & 0xFFFF), hi = (int16_t)(ch_ext[j] >> 16);
         acc = (int32_t)((uint32_t)acc + (uint32_t)((int32_t)hr * hr) + (uint32_t)((int32_t)hi * hi));
@@ -130,6 +194,7 @@ int orc_rx_pdsch_siso(const orc_frame_t *fp, const int32_t *rxdataF, const int32
     if (Qm == 2) len = pil ? nb_rb * 10 : nb_rb * 12;
     else len = (pil ? nb_rb * 10 - 5 * orc_adjust_G2(fp, rb_alloc, subframe, (uint8_t)symbol) / 6
                     : nb_rb * 12 - orc_adjust_G2(fp, rb_alloc, subframe, (uint8_t)symbol));
+    if (len > hw) { out = NULL; break; }                       /* would read stale ext slots */
     const int16_t a1 = Qm == 4 ? QAM16_n1 : QAM64_n1, a2 = Qm == 4 ? 0 : QAM64_n2;
     for (int j = 0; j < len; j++) {
       const int16_t hr = (int16_t)(ch_ext[j] & 0xFFFF), hi = (int16_t)(ch_ext[j] >> 16);
@@ -158,6 +223,7 @@ int orc_rx_pdsch_siso(const orc_frame_t *fp, const int32_t *rxdataF, const int32
   }
   free(rx_ext);
   free(ch_ext);
+  if (!out) return -1;
   if (log2_maxh_out) *log2_maxh_out = log2_maxh;
   return (int)(out - llr);
 }

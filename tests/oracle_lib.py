@@ -515,6 +515,12 @@ def chest_filters(k):
     return out
 
 
+def chest_dc_filters(k):
+    out = np.zeros((2, 24), np.int16)
+    orc().orc_chest_dc_filters(k, P(out))
+    return out
+
+
 def gold_table(fp):
     t = np.zeros((20, 2, 14), np.uint32)
     orc().orc_lte_gold_table(ctypes.byref(fp), P(t))

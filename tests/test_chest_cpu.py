@@ -1,5 +1,5 @@
 """Downlink channel estimation oracle (oracle/oai_oracle_chest.c: lte_dl_channel_estimation with
-high_speed_flag = 1, the 6 / 50 / 100 PRB branch).  Pinned
+high_speed_flag = 1, the 6 / 50 / 100, 25 and 15 PRB branches).  Pinned
   - to the reference's own interpolation filters entry by entry (PHY/LTE_ESTIMATION/filt96_32.h,
     read as data when the reference tree is present): the oracle (and the library, test_gpu_chest)
     derive them from one formula with three cited exceptions, and
@@ -38,6 +38,10 @@ def test_filters_equal_reference_header():
         for i, nm in enumerate(names):
             want = (ref[nm] + [0] * 24)[:24]          # filt24_0_dcr has 23 initialisers (the 24th is 0)
             assert got[i].tolist() == want, (k, nm)
+        # the DC pair of the 25-PRB branch (:116-173): filt24_k_dcr, filt24_(k+2)_dcl
+        got = O.chest_dc_filters(k)
+        for i, nm in enumerate((f"filt24_{k}_dcr", f"filt24_{k + 2}_dcl")):
+            assert got[i].tolist() == (ref[nm] + [0] * 24)[:24], (k, nm)
 
 
 def _frame_loop(p, sf, pays, fp):
@@ -47,7 +51,8 @@ def _frame_loop(p, sf, pays, fp):
     frame = np.zeros(10 * spt + N, np.int32)
     for d, pay in enumerate(pays):
         s = (sf + d) % 10
-        txd, _, _ = O.tx_subframe(O.tx_cfg_from_params(params("C2", fp.N_RB_DL, p.mcs[0], p.num_pdcch_symbols, s), s),
+        txd, _, _ = O.tx_subframe(O.tx_cfg_from_params(params("C2", fp.N_RB_DL, p.mcs[0], p.num_pdcch_symbols, s,
+                                                             Nid_cell=fp.Nid_cell), s),
                                   [pay])
         frame[s * spt:(s + 1) * spt] = txd[0]
     rxF = np.zeros(15 * N, np.int32)                      # slot_fep writes row l + 7 (Ns & 1)
@@ -59,7 +64,9 @@ def _frame_loop(p, sf, pays, fp):
     return rxF[:14 * N].copy(), nxt[:N].copy()
 
 
-LOOP = [(6, 9, 2, 2), (6, 16, 3, 7), (50, 16, 1, 3), (100, 27, 2, 7), (100, 4, 1, 8), (50, 24, 3, 1)]
+LOOP = [(6, 9, 2, 2), (6, 16, 3, 7), (50, 16, 1, 3), (100, 27, 2, 7), (100, 4, 1, 8), (50, 24, 3, 1),
+        # odd N_RB_DL: the 25-PRB branch with its DC-pair filters (15 PRB: below)
+        (25, 16, 1, 7), (25, 0, 1, 7), (25, 27, 2, 3), (25, 9, 3, 8)]
 
 
 @pytest.mark.parametrize("N_RB,mcs,npdcch,sf", LOOP)
@@ -84,6 +91,27 @@ def test_estimated_channel_loop_decodes(N_RB, mcs, npdcch, sf):
     res, tb = decode_tb(u[:G], G, p.TBS[0], Qm)
     assert all(it <= 4 for it, _ in res), [it for it, _ in res]
     assert np.array_equal(tb, pays[0][:p.TBS[0] // 8])
+
+
+@pytest.mark.parametrize("Nid_cell", [0, 4])
+def test_15prb_second_half_quirk(Nid_cell):
+    """The 15-PRB branch (:535-623) starts the second half of every pilot symbol at 1 + nushift + 3 p
+    (:582) instead of 1 + k, k = (nu + nushift) mod 6.  For port 0 that is right at l = 0 (nu = 0)
+    and 3 bins off at l > 0 (nu = 3): the upper half of the estimate rows 4 / 11 is built from data
+    REs.  Reproduced as written, so on a flat noiseless channel row 0 is flat across the band while
+    row 4 is flat only below DC (the reference's 15-PRB receiver cannot close dlsim's loop)."""
+    p = params("C2", 15, 9, 2, 3, Nid_cell=Nid_cell)
+    fp = O.tx_cfg_from_params(p, 3).fp
+    rng = np.random.default_rng(Nid_cell)
+    pays = [rng.integers(0, 256, p.payload_stride, dtype=np.uint8) for _ in range(2)]
+    rxF_sf, next0 = _frame_loop(p, 3, pays, fp)
+    est = O.chest_subframe(fp, rxF_sf, next0, 3)
+    N = fp.ofdm_symbol_size
+    iq = est.view(np.int16).reshape(14, N, 2).astype(float)
+    lo, hi = slice(5 + 12, 5 + 84), slice(5 + 96, 5 + 168)    # away from the band edges and from DC
+    spread = lambda r, sl: np.ptp(iq[r, sl, 0]) + np.ptp(iq[r, sl, 1])
+    assert spread(0, lo) < 40 and spread(0, hi) < 40 and spread(4, lo) < 40
+    assert spread(4, hi) > 200
 
 
 def test_constant_channel_interior_is_flat():

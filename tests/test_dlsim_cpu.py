@@ -1,0 +1,83 @@
+"""dlsim's channel stage and BLER loop on the CPU oracle (tests/dlsim_oracle.py):
+  - orc_signal_energy equals the reference's own signal_energy (PHY/TOOLS/signal_energy.c compiled
+    unmodified into oracle/_ref/libref_tools.so when the reference tree is present), wraps included;
+  - the restated rangen_double generator gives N(0, 1) deviates;
+  - the oracle's whole dlsim trial (TX with control + CRS, tx_lev, AWGN, FEP, channel estimation,
+    rx_pdsch, unscrambling, dlsch_decoding) reproduces the reference-held BLER curve
+    AWGN_results/bler_tx1_chan18_nrx1_mcs9.csv (8-bit decoder, dlsim -L) within the
+    binomial error of a small CPU sample.  The GPU reproduces the same rows with 32 768 trials each
+    (tests/test_gpu_dlsim.py)."""
+import ctypes
+import os
+
+import numpy as np
+import pytest
+
+import dlsim_oracle as D
+import oracle_lib as O
+
+REF_TOOLS = os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "oracle", "_ref", "libref_tools.so")
+
+
+@pytest.mark.skipif(not os.path.exists(REF_TOOLS), reason="reference build absent")
+@pytest.mark.parametrize("length,scale", [(7680, 600), (30720, 300), (1920, 32767), (7680, 32767), (15360, 9000),
+                                          (1535, 500)])
+def test_signal_energy_equals_reference(length, scale):
+    R = ctypes.CDLL(os.path.abspath(REF_TOOLS))
+    R.signal_energy.restype = ctypes.c_int32
+    O.orc().orc_signal_energy.restype = ctypes.c_int32
+    rng = np.random.default_rng(length * 3 + scale)
+    for trial in range(4):
+        x = (rng.integers(-scale, scale + 1, (length + 2, 2)).astype(np.int16)).view(np.int32).ravel()
+        if trial == 1:
+            x[:] = x[0]                                  # pure DC: the DC term is removed
+        if trial == 2:
+            x[:] = 0
+        got = O.orc().orc_signal_energy(O.P(x), length)
+        want = R.signal_energy(O.P(x), length)
+        assert got == want, (trial, got, want)
+
+
+def test_tx_lev_of_dlsim_subframe():
+    """tx_lev of the 25-PRB TM1 subframe with PCFICH + PDCCH + CRS (dlsim.c:2714-2719): QPSK symbols
+    of (amp 23170 >> 15) per component, the IDFT's 1/sqrt(512) scaling and 4038 loaded REs of 7680
+    samples put it near 2 * 362^2 * 4038 / 512 / 7680 * 512 ~ 138 k (exactly: the reference's integer
+    arithmetic on the oracle IQ; the per-sample >> 4 and the IDFT rounding move it by < 3 %)."""
+    t = D.OracleTrial(0)
+    rng = np.random.default_rng(2)
+    levs = [t.tx_lev(t.transmit(rng.integers(0, 256, t.p.payload_stride, dtype=np.uint8))) for _ in range(3)]
+    assert max(levs) - min(levs) < 0.03 * max(levs)      # QPSK: constant-modulus REs, IDFT rounding only
+    assert 120000 < levs[0] < 160000, levs
+
+
+def test_gaussdouble_moments():
+    D.randominit(1234567)
+    L = O.orc()
+    L.orc_gaussdouble.restype = ctypes.c_double
+    g = np.array([L.orc_gaussdouble(ctypes.c_double(0.0), ctypes.c_double(1.0)) for _ in range(200000)])
+    assert abs(g.mean()) < 0.01 and abs(g.var() - 1) < 0.01
+    assert abs(np.mean(g ** 4) - 3) < 0.05
+    assert abs(np.mean(np.abs(g) > 3) - 0.0027) < 0.0006
+
+
+def test_oracle_trial_noiseless_decodes():
+    for mcs in (0, 9, 16, 27):
+        t = D.OracleTrial(mcs)
+        pay = np.random.default_rng(mcs).integers(0, 256, t.p.payload_stride, dtype=np.uint8)
+        err, res, tb = t.trial(pay, 40.0)
+        assert not err and np.array_equal(tb, pay[:t.TBS // 8]), (mcs, [r[0] for r in res])
+
+
+@pytest.mark.parametrize("snr,n", [(3.7, 500), (3.8, 700)])
+def test_oracle_bler_matches_reference_curve_mcs9(snr, n):
+    """The oracle chain's BLER at MCS 9 (8-bit decoder) against bler_tx1_chan18_nrx1_mcs9.csv: the
+    two binomial estimates differ by less than 3 combined standard errors."""
+    ref = [r for r in D.load_curves()[9] if abs(r[0] - snr) < 1e-6][0]
+    D.randominit(1000 + int(snr * 10))
+    t = D.OracleTrial(9, llr8=True)
+    rng = np.random.default_rng(int(snr * 100))
+    k = sum(t.trial(rng.integers(0, 256, t.p.payload_stride, dtype=np.uint8), snr)[0] for _ in range(n))
+    p, q = k / n, ref[1] / ref[2]
+    z = (p - q) / np.sqrt(p * (1 - p) / n + q * (1 - q) / ref[2] + 1e-12)
+    print(f"SNR {snr}: oracle {k}/{n} = {p:.4f}, reference {ref[1]}/{ref[2]} = {q:.4f}, z = {z:+.2f}")
+    assert abs(z) < 3, (k, n, ref)

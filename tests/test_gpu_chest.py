@@ -16,9 +16,12 @@ pytestmark = pytest.mark.gpu
 def test_gpu_filters_equal_oracle(gpu):
     for k in range(6):
         assert np.array_equal(gpu.chest_filters(k), O.chest_filters(k)), k
+        assert np.array_equal(gpu.chest_dc_filters(k), O.chest_dc_filters(k)), k
 
 
-CASES = [(100, 0, 0, 0), (100, 301, 1, 0), (50, 7, 0, 1), (6, 2, 1, 0), (6, 11, 0, 1), (50, 4, 1, 1), (100, 88, 1, 1)]
+CASES = [(100, 0, 0, 0), (100, 301, 1, 0), (50, 7, 0, 1), (6, 2, 1, 0), (6, 11, 0, 1), (50, 4, 1, 1), (100, 88, 1, 1),
+         # odd N_RB_DL: the 25-PRB DC pair, the 15-PRB second-half start 1 + nushift + 3 p
+         (25, 0, 0, 0), (25, 13, 1, 0), (25, 30, 0, 1), (15, 4, 0, 0), (15, 9, 1, 1), (15, 2, 1, 0)]
 
 
 @pytest.mark.parametrize("N_RB,nid,p,Ncp", CASES)
@@ -42,11 +45,6 @@ def test_gpu_drop_in_call_sequence(gpu, N_RB, nid, p, Ncp):
 
 
 def test_gpu_drop_in_rejects(gpu):
-    fg = gpu.frame_parms(25)
-    est = np.zeros(14 * fg.ofdm_symbol_size, np.int32)
-    y = np.zeros_like(est)
-    with pytest.raises(gpu.OAI4GError):
-        gpu.lte_dl_channel_estimation(fg, y, est, 0, 0, 0, 0)        # 25 PRB interpolator not built
     fg = gpu.frame_parms(50)
     est = np.zeros(14 * fg.ofdm_symbol_size, np.int32)
     y = np.zeros_like(est)
@@ -56,7 +54,8 @@ def test_gpu_drop_in_rejects(gpu):
         gpu.lte_dl_channel_estimation(fg, y, est, 0, 0, 0, 3)        # not a pilot symbol
 
 
-@pytest.mark.parametrize("N_RB,nid,Ncp,first", [(100, 17, 0, 3), (6, 1, 0, 8), (50, 40, 1, 0), (100, 5, 1, 9)])
+@pytest.mark.parametrize("N_RB,nid,Ncp,first", [(100, 17, 0, 3), (6, 1, 0, 8), (50, 40, 1, 0), (100, 5, 1, 9),
+                                                 (25, 3, 0, 7), (25, 11, 1, 0), (15, 2, 0, 2)])
 def test_gpu_batch_matches_oracle(gpu, N_RB, nid, Ncp, first):
     fo = O.frame(N_RB, Nid_cell=nid, Ncp=Ncp)
     fg = gpu.frame_parms(N_RB, Nid_cell=nid, Ncp=Ncp)
@@ -73,7 +72,8 @@ def test_gpu_batch_matches_oracle(gpu, N_RB, nid, Ncp, first):
         assert np.array_equal(got[i], want), i
 
 
-@pytest.mark.parametrize("N_RB,mcs,npd,sf", [(100, 16, 1, 7), (100, 27, 2, 3), (6, 9, 2, 2), (50, 24, 3, 1)])
+@pytest.mark.parametrize("N_RB,mcs,npd,sf", [(100, 16, 1, 7), (100, 27, 2, 3), (6, 9, 2, 2), (50, 24, 3, 1),
+                                              (25, 16, 1, 7), (25, 27, 2, 3), (25, 0, 1, 7)])
 def test_gpu_estimated_channel_loop(gpu, N_RB, mcs, npd, sf):
     """dlsim's receive path with perfect_ce = 0, all on the GPU: TxPipeline (TM1, CRS) over three
     consecutive subframes -> FepBatch -> ChestBatch (the FEP output buffer, its third subframe's
@@ -114,7 +114,8 @@ def test_gpu_estimated_channel_loop(gpu, N_RB, mcs, npd, sf):
 
 
 @pytest.mark.parametrize("N_RB,Qm,npd,first,Ncp", [(100, 4, 1, 3, 0), (50, 6, 2, 8, 0), (6, 2, 3, 0, 0),
-                                                    (100, 6, 1, 9, 0), (50, 4, 2, 1, 1)])
+                                                    (100, 6, 1, 9, 0), (50, 4, 2, 1, 1),
+                                                    (25, 4, 1, 3, 0), (25, 6, 2, 7, 0), (15, 4, 1, 1, 0), (25, 6, 1, 2, 1)])
 def test_gpu_fused_estimation_demodulation(gpu, N_RB, Qm, npd, first, Ncp):
     """oai4g_rx_batch_estimated (k_rx_chest) = oai4g_chest_batch then oai4g_rx_batch, and = the
     oracle's chain, on full-range random grids (saturating estimates and LLRs)."""

@@ -1,0 +1,155 @@
+"""dlsim's BLER loop on the GPU (openair4g_amd/dlsim.py): the channel-stage kernels against the
+oracle / the reference, the whole GPU trial bit-exact against the oracle's trial on the same noisy
+samples, and the BLER against the reference-held AWGN curves
+(BLER_SIMULATIONS/AWGN/AWGN_results/bler_tx1_chan18_nrx1_mcs*.csv, tests/golden/bler_awgn_tx1_nrx1.json)."""
+import ctypes
+import os
+
+import numpy as np
+import pytest
+
+import dlsim_oracle as D
+import oracle_lib as O
+
+pytestmark = pytest.mark.gpu
+
+
+def _ref_energy():
+    p = os.path.join(os.path.dirname(O.__file__), "..", "oracle", "_ref", "libref_tools.so")
+    if not os.path.exists(p):
+        return None
+    L = ctypes.CDLL(os.path.abspath(p))
+    L.signal_energy.restype = ctypes.c_int32
+    return L
+
+
+@pytest.mark.parametrize("length,scale", [(7680, 600), (30720, 300), (1920, 32767), (7680, 32767), (15360, 9000)])
+def test_gpu_signal_energy(gpu, length, scale):
+    """k_signal_energy (batch and drop-in) = orc_signal_energy = the reference's signal_energy
+    (compiled here when the reference tree was present) on random vectors, including full-scale
+    samples whose pmaddwd / sums wrap."""
+    rng = np.random.default_rng(length + scale)
+    n = 6
+    x = (rng.integers(-scale, scale + 1, (n, length, 2)).astype(np.int16)).view(np.int32).reshape(n, length)
+    x[1, :] = x[1, 0]                                    # a strong DC component
+    want = [O.orc().orc_signal_energy(O.P(np.ascontiguousarray(x[i])), length) for i in range(n)]
+    R = _ref_energy()
+    if R is not None:
+        assert want == [R.signal_energy(O.P(np.ascontiguousarray(x[i])), length) for i in range(n)]
+    L = gpu.lib()
+    d_x, d_e = L.oai4g_dev_alloc(x.nbytes), L.oai4g_dev_alloc(4 * n)
+    assert L.oai4g_memcpy_h2d(d_x, gpu._ptr(x), x.nbytes) == 0
+    assert L.oai4g_signal_energy_batch(d_x, n, length, length, d_e, None) == 0
+    got = np.empty(n, np.int32)
+    assert L.oai4g_sync() == 0 and L.oai4g_memcpy_d2h(gpu._ptr(got), d_e, got.nbytes) == 0
+    L.oai4g_dev_free(d_x)
+    L.oai4g_dev_free(d_e)
+    assert got.tolist() == [int(np.int32(w)) for w in want]
+    assert L.oai4g_signal_energy(gpu._ptr(np.ascontiguousarray(x[2])), length) == np.int32(want[2])
+
+
+def test_gpu_awgn_statistics(gpu):
+    """k_awgn: noise of variance sigma2 / 2 per component with sigma2 from tx_lev and the offset
+    (dlsim.c:2852-2866), zero mean, Gaussian (4th moment 3 sigma^4), truncation toward zero,
+    reproducible per (seed, vector, sample), the tail appended."""
+    L = gpu.lib()
+    n, ln, tl = 4, 7680, 7680
+    rng = np.random.default_rng(3)
+    x = (rng.integers(-500, 500, (n, ln, 2)).astype(np.int16)).view(np.int32).reshape(n, ln)
+    tail = (rng.integers(-500, 500, (tl, 2)).astype(np.int16)).view(np.int32).ravel()
+    lev = np.array([1000, 40000, 250000, 7], np.int32)
+    off = -3.0
+    d = {k: L.oai4g_dev_alloc(sz) for k, sz in (("x", x.nbytes), ("t", tail.nbytes), ("r", n * (ln + tl) * 4),
+                                                 ("r2", n * (ln + tl) * 4), ("l", lev.nbytes))}
+    for k, a in (("x", x), ("t", tail), ("l", lev)):
+        assert L.oai4g_memcpy_h2d(d[k], gpu._ptr(a), a.nbytes) == 0
+    for key, seed in (("r", 99), ("r2", 99)):
+        assert L.oai4g_awgn_batch(d["x"], ln, ln, d["t"], tl, d[key], ln + tl, n, d["l"], off, seed, 5, None) == 0
+    r = np.empty((n, ln + tl), np.int32)
+    r2 = np.empty_like(r)
+    assert L.oai4g_sync() == 0
+    assert L.oai4g_memcpy_d2h(gpu._ptr(r), d["r"], r.nbytes) == 0
+    assert L.oai4g_memcpy_d2h(gpu._ptr(r2), d["r2"], r2.nbytes) == 0
+    for p in d.values():
+        L.oai4g_dev_free(p)
+    assert np.array_equal(r, r2)
+    src = np.concatenate([x, np.broadcast_to(tail, (n, tl))], axis=1)
+    s16 = src.view(np.int16).reshape(n, -1, 2).astype(np.float64)
+    r16 = r.view(np.int16).reshape(n, -1, 2).astype(np.float64)
+    for i in range(n):
+        var = 10 ** ((10 * np.log10(lev[i]) + off) / 10) / 2
+        d_ = (r16[i] - s16[i]).ravel()
+        # truncation toward zero loses up to one LSB toward the origin: compare against the exact
+        # noise variance within the sampling error of 30720 draws plus the rounding bias
+        assert abs(d_.mean()) < 0.05 * np.sqrt(var) + 0.6, i
+        if var > 50:
+            assert abs(d_.var() / var - 1) < 0.05, (i, d_.var(), var)
+            k4 = np.mean((d_ - d_.mean()) ** 4) / d_.var() ** 2
+            assert abs(k4 - 3) < 0.25, (i, k4)
+
+
+@pytest.mark.parametrize("mcs,snr,llr8", [(9, 3.4, False), (16, 8.6, False), (0, -3.4, False), (27, 16.9, False),
+                                          (9, 3.6, True), (16, 8.7, True), (0, -1.0, True)])
+def test_gpu_trial_equals_oracle_trial(gpu, mcs, snr, llr8):
+    """Every stage of a GPU BLER batch equals the oracle's dlsim trial: the transmit IQ with CRS +
+    PCFICH + PDCCH, tx_lev, and — fed the GPU's own noisy samples — the oracle UE's LLRs and
+    decoder outcome per trial (the k_rx_chest elements two subframes apart, the next subframe's
+    symbol 0 closing rows 12 / 13); with llr8 the chain's 8-bit decoder (dlsim -L)."""
+    from openair4g_amd.dlsim import DlsimBler
+    B = 6
+    sim = DlsimBler(mcs, batch=B, llr8=llr8)
+    err, c, pay = sim.run_batch(snr, seed=7, want_bits=True)
+    L = gpu.lib()
+    iq = sim.tx.iq()[:, 0]
+    lev = sim.tx_lev()
+    rx = np.empty((2 * B, sim.spt), np.int32)
+    assert L.oai4g_memcpy_d2h(gpu._ptr(rx), sim.fep.d_rx, rx.nbytes) == 0
+    llr = np.empty((B, sim.rx.stride), np.int16)
+    assert L.oai4g_memcpy_d2h(gpu._ptr(llr), sim.rx.d_llr, llr.nbytes) == 0
+    it, _ = sim.dec.results()
+    t = D.OracleTrial(mcs, llr8=llr8)
+    assert np.array_equal(t.tail, sim.tail)
+    for i in range(B):
+        txd = t.transmit(pay[i, 0])
+        assert np.array_equal(iq[i], txd), i
+        assert lev[i] == t.tx_lev(txd), i
+        u = t.receive(rx.reshape(B, 2 * sim.spt)[i])
+        assert len(u) == sim.G and np.array_equal(llr[i, :sim.G], u), i
+        res, _ = t.decode(u)
+        assert [r[0] for r in res] == it[i].tolist(), i
+        assert err[i] == any(r[0] > 4 for r in res)
+    sim.close()
+
+
+# Statistical pin to the reference-held curves.  Their dlsim options are not recorded with them;
+# measured here (tools/bler_sweep.py, 16 384 trials per row): MCS 9 follows the curve
+# with the 8-bit decoder (dlsim -L) over the whole waterfall and its tail, MCS 27 with the 16-bit
+# decoder to within 0.1 dB (and inside the CI along the tail); MCS 0 / 16 come out 0.35 / 0.27 dB
+# better than the CSVs with either decoder.  The assertion: at least 3 CSV rows whose 95 % Wilson
+# interval contains the GPU estimate, and the fitted SNR shift within the stated bound.
+PINS = [(9, True, [3.6, 3.7, 3.8, 3.9, 4.0, 4.1], 3, 0.05),
+        (27, False, [17.4, 17.5, 17.6, 17.7, 17.8, 17.9], 3, 0.1)]
+
+
+@pytest.mark.parametrize("mcs,llr8,snrs,need,shift", PINS)
+def test_gpu_bler_matches_reference_curves(gpu, mcs, llr8, snrs, need, shift):
+    from openair4g_amd.dlsim import DlsimBler, wilson
+    curves = D.load_curves()[mcs]
+    sim = DlsimBler(mcs, batch=4096, llr8=llr8)
+    inside, rows = 0, []
+    for snr in snrs:
+        ref = [r for r in curves if abs(r[0] - snr) < 1e-6][0]
+        k, n = sim.run_point(snr, 32768, seed=int(round(100 * snr)) + mcs)
+        lo, hi = wilson(ref[1], ref[2])
+        inside += lo <= k / n <= hi
+        rows.append((snr, k / n, ref[1] / ref[2]))
+        print(f"MCS {mcs} {'8' if llr8 else '16'}-bit SNR {snr}: GPU {k}/{n} = {k / n:.4f}  reference "
+              f"{ref[1]}/{ref[2]} = {ref[1] / ref[2]:.4f} [{lo:.4f}, {hi:.4f}]")
+    sim.close()
+    assert inside >= need, rows
+    # fitted shift: ref(s) ~ gpu(s + d) on log-BLER
+    s = np.array([r[0] for r in rows])
+    g, q = np.log(np.array([r[1] for r in rows])), np.log(np.array([r[2] for r in rows]))
+    ds = np.arange(-0.3, 0.3001, 0.005)
+    errs = [np.nanmean((np.interp(s + d, s, g, left=np.nan, right=np.nan) - q) ** 2) for d in ds]
+    assert abs(ds[int(np.nanargmin(errs))]) <= shift, ds[int(np.nanargmin(errs))]

@@ -12,7 +12,10 @@ from test_rx_cpu import alloc, decode_tb, loop_llr, params, perfect_ce
 pytestmark = pytest.mark.gpu
 
 RAND = [(100, 2, 1, 7, None), (100, 4, 2, 0, None), (100, 6, 3, 5, None), (50, 6, 1, 0, None), (6, 4, 3, 9, None),
-        (50, 2, 2, 5, [0x0F0F0F0F, 0x3, 0, 0]), (100, 6, 1, 1, [0xFFFF0000, 0xFFFFFFFF, 0x0000FFFF, 0x3])]
+        (50, 2, 2, 5, [0x0F0F0F0F, 0x3, 0, 0]), (100, 6, 1, 1, [0xFFFF0000, 0xFFFFFFFF, 0x0000FFFF, 0x3]),
+        # odd N_RB_DL: the DC split, PBCH / PSS / SSS RBs dropped and halved in subframes 0 / 5
+        (25, 2, 1, 7, None), (25, 4, 2, 0, None), (25, 6, 1, 5, None), (15, 6, 3, 0, None), (25, 2, 2, 3, [0x1F0F0F0, 0, 0, 0]),
+        (15, 4, 1, 5, [0x7F80, 0, 0, 0]), (25, 6, 3, 0, [0x00FFF000, 0, 0, 0])]
 
 
 @pytest.mark.parametrize("N_RB,Qm,npdcch,sf,ra", RAND)
@@ -52,10 +55,21 @@ def test_gpu_rx_batch_and_unscrambling(gpu):
         v[:len(lo)] = lo
         gpu.dlsch_unscrambling(fg, rnti, len(lo), v, 0, 2 * sf)
         assert np.array_equal(v[:len(lo)], u[:len(lo)])
+        # PMCH (mbsfn_flag = 1): c_init = (Ns / 2) 2^9 + Nid_cell_mbsfn (dlsch_scrambling.c:115-118)
+        fg.Nid_cell_mbsfn = 37 + sf
+        m = np.zeros_like(u)
+        m[:len(lo)] = lo
+        O.dlsch_unscrambling(m, len(lo), (sf << 9) + 37 + sf)
+        v[:] = 0
+        v[:len(lo)] = lo
+        gpu.dlsch_unscrambling(fg, rnti, len(lo), v, 0, 2 * sf, mbsfn_flag=1)
+        assert np.array_equal(v[:len(lo)], m[:len(lo)])
+        fg.Nid_cell_mbsfn = 0
     rx.close()
 
 
-@pytest.mark.parametrize("N_RB,mcs,npd,sf", [(100, 16, 1, 7), (100, 27, 2, 3), (50, 9, 3, 8), (100, 22, 1, 1)])
+@pytest.mark.parametrize("N_RB,mcs,npd,sf", [(100, 16, 1, 7), (100, 27, 2, 3), (50, 9, 3, 8), (100, 22, 1, 1),
+                                              (25, 16, 1, 7), (25, 9, 2, 3)])
 def test_gpu_tx_fep_rx_decode_loop(gpu, N_RB, mcs, npd, sf):
     """TM1 with CRS, two consecutive subframes: the GPU transmit batch -> IQ -> batched FEP ->
     batched demodulation with dlsim's perfect channel estimate (AMP, 0) and unscrambling, LLRs
@@ -104,3 +118,21 @@ def _gpu_rm(soft, K, G, C, r, Qm):
 def gpu_mod():
     import openair4g_amd
     return openair4g_amd
+
+
+def test_gpu_pmch_scrambling(gpu):
+    """dlsch_scrambling with mbsfn_flag = 1 (PMCH, dlsch_scrambling.c:70-72): c_init =
+    (Ns / 2) 2^9 + Nid_cell_mbsfn, independent of the RNTI and the cell id."""
+    fg = gpu.frame_parms(50, Nid_cell=11)
+    fg.Nid_cell_mbsfn = 201
+    dl = gpu.DlschHandle(Kmimo=1, Mdlharq=8, N_RB_DL=50)
+    dl.d.rnti = 0x4321
+    G = 5000
+    rng = np.random.default_rng(8)
+    e0 = rng.integers(0, 2, 32 * (1 + G // 32), dtype=np.uint8)
+    e = dl.view("e", len(e0))
+    e[:] = e0
+    gpu.dlsch_scrambling(fg, dl, G, 0, 14, mbsfn_flag=1)
+    want = O.scramble(e0.copy(), G, (7 << 9) + 201)
+    assert np.array_equal(dl.view("e", G), np.asarray(want)[:G])
+    dl.close()

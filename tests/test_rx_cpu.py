@@ -27,7 +27,9 @@ def params(name, N_RB, mcs, npdcch, sf, **kw):
 
 
 CASES = [("C2", 100, 16, 1, 7), ("C2", 100, 9, 3, 3), ("C2", 50, 27, 2, 8), ("C1", 6, 9, 3, 2), ("C2", 100, 20, 1, 9),
-         ("C2", 6, 2, 2, 4)]
+         ("C2", 6, 2, 2, 4),
+         # odd N_RB_DL: the RB around DC is split at bin 0 (dlsch_demodulation.c:3434-3525)
+         ("C2", 25, 16, 1, 7), ("C2", 25, 0, 2, 3), ("C2", 25, 27, 3, 8), ("C2", 15, 9, 1, 2), ("C2", 15, 22, 2, 9)]
 
 
 @pytest.mark.parametrize("name,N_RB,mcs,npdcch,sf", CASES)
@@ -112,7 +114,8 @@ def loop_llr(p, sf, pay):
     return u[:G], G, Qm
 
 
-LOOP = [(100, 16, 1, 7), (100, 27, 2, 3), (50, 4, 3, 8), (50, 24, 1, 9), (100, 9, 2, 4), (100, 22, 3, 1)]
+LOOP = [(100, 16, 1, 7), (100, 27, 2, 3), (50, 4, 3, 8), (50, 24, 1, 9), (100, 9, 2, 4), (100, 22, 3, 1),
+        (25, 16, 1, 7), (25, 27, 2, 4), (25, 0, 3, 8)]
 
 
 @pytest.mark.parametrize("N_RB,mcs,npdcch,sf", LOOP)
