@@ -639,6 +639,7 @@ class Host:
     def __init__(self, args, world, rank, local_rank):
         import torch
         self.torch, self.world, self.rank, self.dist = torch, world, rank, None
+        self.local_rank = local_rank
         self.stub = args.cpu_stub
         self.device = "cpu" if self.stub else "cuda"
         if not self.stub:
@@ -674,6 +675,9 @@ class Host:
         return float(t.item())
 
     def close(self):
+        if not self.stub and self.world > 1:
+            import openair4g_amd as oai
+            oai.lib().oai4g_dist_finalize()
         if self.dist is not None:
             self.dist.destroy_process_group()
 
@@ -772,13 +776,23 @@ def bench_tx(args, world, rank, host):
     from openair4g_amd import dist as odist
     dist = host.dist
     if not host.stub:
+        oai.lib().oai4g_set_device(host.local_rank)
         oai.init()
-    # ---- parameter block: built on rank 0, broadcast over RCCL (the only collective) ----
+    # ---- parameter block: built on rank 0, broadcast over RCCL (the only collective): the C ABI's
+    # oai4g_dist_broadcast_params on the GPU, torch.distributed (gloo) under --cpu-stub ----
     p0 = oai.make_params(args.config, subframe=args.subframe) if rank == 0 else None
-    params = odist.broadcast_params(p0, dist, device=host.device) if dist is not None else p0
+    if dist is None:
+        params = p0
+    elif host.stub:
+        params = odist.broadcast_params(p0, dist, device=host.device)
+    else:
+        odist.c_dist_init(rank, world, dist)
+        params = odist.c_broadcast_params(p0)
 
     pipe = (StubPipeline if host.stub else oai.TxPipeline)(params, args.batch)
-    pipe.fill_payload(seed=odist.payload_seed(0x5EED0000, rank))   # this rank's shard of synthetic TBs
+    # this rank's shard of the global stream of synthetic TBs: global subframes [rank B, (rank + 1) B)
+    first, _ = odist.shard_range(world * args.batch, rank, world)
+    pipe.fill_payload(seed=odist.global_payload_seed(0x5EED0000, first, params))
     pipe.sync()
 
     for _ in range(args.warmup):

@@ -533,6 +533,33 @@ int oai4g_diag_encode_phase_ms(const oai4g_tx_config_t *cfg, int n_sf, const uin
 /* PMC calibration: stream `bytes` through HBM at 4 B per lane (mode 0 read, 1 write) */
 int oai4g_diag_stream(const void *d_src, void *d_dst, size_t bytes, int mode, void *stream);
 
+/* ---------------- multi-GPU: one process per GPU, RCCL over xGMI ---------------- */
+/* The device this process drives (its local rank); call before any other oai4g_ call.  0 / -1. */
+int oai4g_set_device(int device);
+#define OAI4G_DIST_ID_BYTES 128
+/* rank 0: a fresh RCCL unique id (ncclGetUniqueId) for every rank, passed out of band.  0 / -1. */
+int oai4g_dist_unique_id(uint8_t id[OAI4G_DIST_ID_BYTES]);
+/* join the RCCL communicator as `rank` of `world` (ncclCommInitRank, on the oai4g_set_device
+ * device).  0 / -1. */
+int oai4g_dist_init(int rank, int world, const uint8_t id[OAI4G_DIST_ID_BYTES]);
+/* the parameter block of rank `root` into *p on every rank (ncclBroadcast of its bytes): the one
+ * collective the transmit path needs.  0 / -1. */
+int oai4g_dist_broadcast_params(oai4g_tx_params_t *p, int root);
+/* in-place sum of n counters / checksums, max of n doubles (timings) over the ranks.  0 / -1. */
+int oai4g_dist_allreduce_sum_u64(uint64_t *v, int n);
+int oai4g_dist_allreduce_max_f64(double *v, int n);
+int oai4g_dist_barrier(void);
+int oai4g_dist_rank(void);             /* -1 before oai4g_dist_init */
+int oai4g_dist_world(void);            /* 0 before oai4g_dist_init */
+int oai4g_dist_finalize(void);
+/* the contiguous shard [*first, *first + *count) of n_total units owned by rank of world (sizes
+ * differ by at most one) */
+void oai4g_shard_range(int n_total, int rank, int world, int *first, int *count);
+/* the oai4g_fill_payload seed that makes a rank's buffer of global subframes [first_subframe, ...)
+ * equal to that slice of the global payload stream of `seed` (payloads derive from (seed, global
+ * subframe index), whatever the world size) */
+uint64_t oai4g_payload_seed(uint64_t seed, uint64_t first_subframe, uint32_t n_cw, uint32_t payload_stride);
+
 /* ---------------- device memory helpers (for hosts without another allocator) ---------------- */
 void *oai4g_dev_alloc(size_t bytes);
 void oai4g_dev_free(void *p);

@@ -206,6 +206,19 @@ _SIGS = {
     "oai4g_chest_filters": (None, [ctypes.c_uint8, ctypes.c_void_p]),
     "oai4g_chest_dc_filters": (None, [ctypes.c_uint8, ctypes.c_void_p]),
     "oai4g_ul_config_set_decoder": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
+    "oai4g_set_device": (ctypes.c_int, [ctypes.c_int]),
+    "oai4g_dist_unique_id": (ctypes.c_int, [ctypes.c_void_p]),
+    "oai4g_dist_init": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.c_void_p]),
+    "oai4g_dist_broadcast_params": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
+    "oai4g_dist_allreduce_sum_u64": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
+    "oai4g_dist_allreduce_max_f64": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
+    "oai4g_dist_barrier": (ctypes.c_int, []),
+    "oai4g_dist_rank": (ctypes.c_int, []),
+    "oai4g_dist_world": (ctypes.c_int, []),
+    "oai4g_dist_finalize": (ctypes.c_int, []),
+    "oai4g_shard_range": (None, [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.POINTER(ctypes.c_int),
+                                 ctypes.POINTER(ctypes.c_int)]),
+    "oai4g_payload_seed": (ctypes.c_uint64, [ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint32]),
     "oai4g_chest_config_set_stride": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_uint32]),
     "oai4g_signal_energy": (ctypes.c_int32, [ctypes.c_void_p, ctypes.c_uint32]),
     "oai4g_signal_energy_batch": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_size_t, ctypes.c_uint32,

@@ -12,7 +12,7 @@ ROOT = os.path.dirname(HERE)
 CSRC = os.path.join(HERE, "csrc")
 LIBDIR = os.path.join(HERE, "lib")
 LIB = os.path.join(LIBDIR, "libopenair4g_amd.so")
-SOURCES = ["oai4g_host.cpp", "oai4g_encode.hip", "oai4g_ofdm.hip", "oai4g_decode.hip", "oai4g_decode8.hip", "oai4g_fep.hip", "oai4g_ctrl.hip", "oai4g_rx.hip", "oai4g_chest.hip", "oai4g_channel.hip"]
+SOURCES = ["oai4g_host.cpp", "oai4g_encode.hip", "oai4g_ofdm.hip", "oai4g_decode.hip", "oai4g_decode8.hip", "oai4g_fep.hip", "oai4g_ctrl.hip", "oai4g_rx.hip", "oai4g_chest.hip", "oai4g_channel.hip", "oai4g_dist.cpp"]
 EXTRA = [os.path.join(ROOT, "include", "oai4g_qpp.c"), os.path.join(ROOT, "include", "oai4g_tbs.c")]
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = os.environ.get("OAI4G_ARCH", "gfx950")
@@ -45,7 +45,8 @@ def build_lib(force=False, verbose=False, out=None, defines=()):
             print(" ".join(cmd))
         subprocess.run(cmd, check=True)
         objs.append(obj)
-    cmd = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", lib] + objs + ["-lpthread"]
+    cmd = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", lib] + objs + ["-L/opt/rocm/lib", "-lrccl", "-lpthread",
+                                                                                "-Wl,-rpath,/opt/rocm/lib"]
     if verbose:
         print(" ".join(cmd))
     subprocess.run(cmd, check=True)

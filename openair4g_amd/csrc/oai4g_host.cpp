@@ -38,6 +38,15 @@ static void set_err(const char *fmt, ...)
 
 extern "C" const char *oai4g_last_error(void) { return g_err; }
 
+/* the error slot for the library's other translation units (oai4g_dist.cpp) */
+void oai4g_set_error(const char *fmt, ...)
+{
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(g_err, sizeof(g_err), fmt, ap);
+  va_end(ap);
+}
+
 #define HCK(call, ret)                                                                          \
   do {                                                                                          \
     hipError_t e_ = (call);                                                                     \
@@ -135,8 +144,10 @@ static uint32_t crs_qpsk(int16_t amp, uint32_t idx)
   return (uint16_t)re | ((uint32_t)(uint16_t)im << 16);
 }
 
+static bool g_init_done = false;
 static void do_init(void)
 {
+  g_init_done = true;
   int n = 0;
   hipError_t e = hipGetDeviceCount(&n);
   if (e != hipSuccess || n == 0) {
@@ -208,6 +219,23 @@ static void do_init(void)
     return;
   }
   g_init_status = 0;
+}
+
+extern "C" int oai4g_set_device(int device)
+{
+  /* before the first oai4g_init: the process's rank drives `device` (one process per GPU) */
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess || device < 0 || device >= n) {
+    set_err("set_device: device %d of %d", device, n);
+    return -1;
+  }
+  int cur = -1;
+  if (g_init_done && (hipGetDevice(&cur) != hipSuccess || cur != device)) {
+    set_err("set_device: the library is already initialised on device %d", cur);
+    return -1;
+  }
+  HCK(hipSetDevice(device), -1);
+  return 0;
 }
 
 extern "C" int oai4g_init(void)

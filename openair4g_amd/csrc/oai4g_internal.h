@@ -320,6 +320,7 @@ struct chest_dev_t {
   int16_t filt[2][8][24];         /* fl, f2l2, f, f2, fr, f2r2, f_dc, f2_dc (filt96_32.h) for k[0] / k[1] */
   uint32_t gold[20][2][14];       /* lte_gold_table */
 };
+void oai4g_set_error(const char *fmt, ...);
 hipError_t oai4g_launch_signal_energy(const int32_t *d_x, int n, size_t stride, uint32_t length, int32_t *d_out,
                                       hipStream_t s);
 hipError_t oai4g_launch_awgn(const int32_t *d_tx, size_t tx_stride, uint32_t tx_len, const int32_t *d_tail,

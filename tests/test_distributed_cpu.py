@@ -86,3 +86,25 @@ def test_two_rank_gloo_matches_single_process(tmp_path):
 
 if __name__ == "__main__":
     pytest.main([__file__, "-q"])
+
+
+def test_c_shard_range_and_payload_seed():
+    """The C ABI's oai4g_shard_range (the one bench.py and tools/dlsim_tx.c -g use) covers
+    [0, n) in rank order with sizes differing by at most one; oai4g_payload_seed advances the
+    generator by whole subframes (n_cw payload_stride / 8 splitmix64 words each)."""
+    import ctypes
+    import openair4g_amd as oai
+    L = oai.load_library()
+    for n in (0, 1, 7, 8192, 8193, 65535):
+        for world in (1, 2, 3, 8):
+            nxt = 0
+            sizes = []
+            for r in range(world):
+                f, c = ctypes.c_int(), ctypes.c_int()
+                L.oai4g_shard_range(n, r, world, ctypes.byref(f), ctypes.byref(c))
+                assert f.value == nxt
+                nxt += c.value
+                sizes.append(c.value)
+            assert nxt == n and max(sizes) - min(sizes) <= 1
+    assert L.oai4g_payload_seed(100, 0, 2, 4608) == 100
+    assert L.oai4g_payload_seed(100, 3, 2, 4608) == 100 + 3 * 2 * 576

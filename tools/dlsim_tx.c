@@ -21,12 +21,21 @@
  *   -o iq_dropin.bin     IQ of the drop-in subframe [n_ant][samples_per_tti] int32
  *   -O iq_batch.bin      IQ of batch element 0
  *   -P                   print the timing lines
+ *   -g N                 multi-GPU: fork N ranks before any HIP call, one per GPU; rank 0
+ *                        builds the parameter block and oai4g_dist_broadcast_params (RCCL over xGMI)
+ *                        hands it to the others; each rank runs the batch path over its shard
+ *                        (oai4g_shard_range) of N x B global subframes with payloads derived from
+ *                        (seed, global subframe index) (oai4g_payload_seed); the per-rank IQ checksums
+ *                        are summed and the step times max-reduced over the ranks (RCCL); rank 0
+ *                        prints "world N checksum 0x..." and the aggregate rate.  The checksum does
+ *                        not depend on N.  No drop-in path in this mode.
  * Exit code 0 when both paths ran and (with -B) their IQ agree, 1 otherwise.
  */
 #include <stdint.h>
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <sys/wait.h>
 #include <time.h>
 #include <unistd.h>
 
@@ -75,11 +84,90 @@ static uint64_t splitmix64(uint64_t *s)
     }                                                                                    \
   } while (0)
 
+/* the batch path of one rank of -g N: parameters broadcast from rank 0, this rank's shard of the
+ * N x batch global subframes, checksum and timing reduced over the ranks */
+static int dist_batch(const cfg_t *c, int subframe, int batch, int rank, int world, int print_timing)
+{
+  oai4g_tx_params_t p;
+  memset(&p, 0, sizeof(p));
+  if (rank == 0) {
+    uint32_t ra[4];
+    full_alloc(c->N_RB_DL, ra);
+    p.N_RB_DL = c->N_RB_DL;
+    p.nb_antennas_tx = c->n_ant;
+    p.mode1_flag = c->mode1;
+    p.n_cw = c->n_cw;
+    p.mimo_mode = c->mimo_mode;
+    p.num_pdcch_symbols = c->npdcch;
+    p.Kmimo = c->Kmimo;
+    p.Mdlharq = 8;
+    p.first_subframe = (uint8_t)subframe;
+    p.rnti = 0x1234;
+    p.amp = 512;
+    p.sqrt_rho_a = p.sqrt_rho_b = 8192;
+    memcpy(p.rb_alloc, ra, sizeof(ra));
+    p.nb_rb = c->N_RB_DL;
+    const uint8_t mcs[2] = {c->mcs0, c->mcs1};
+    uint32_t maxA = 0;
+    for (int cw = 0; cw < c->n_cw; cw++) {
+      p.mcs[cw] = mcs[cw];
+      p.TBS[cw] = oai4g_get_TBS_DL(mcs[cw], c->N_RB_DL) << 3;
+      if (p.TBS[cw] / 8 > maxA) maxA = p.TBS[cw] / 8;
+    }
+    p.payload_stride = (maxA + 3 + 15) & ~15u;
+  }
+  CHECK(oai4g_dist_broadcast_params(&p, 0) == 0, "dist_broadcast_params");
+  int first = 0, count = 0;
+  oai4g_shard_range(world * batch, rank, world, &first, &count);
+  oai4g_tx_config_t *cfg = oai4g_tx_config_create(&p);
+  CHECK(cfg, "tx_config_create (broadcast parameters)");
+  const size_t spt = oai4g_tx_iq_samples(cfg);
+  const size_t pbytes = (size_t)count * p.n_cw * p.payload_stride, iqn = (size_t)count * p.nb_antennas_tx * spt;
+  uint8_t *d_pay = (uint8_t *)oai4g_dev_alloc(pbytes);
+  void *d_work = oai4g_dev_alloc(oai4g_tx_workspace_bytes(cfg, count));
+  int32_t *d_iq = (int32_t *)oai4g_dev_alloc(iqn * 4);
+  CHECK(d_pay && d_work && d_iq, "device allocation");
+  CHECK(oai4g_fill_payload(d_pay, pbytes, oai4g_payload_seed(0x5EED, (uint64_t)first, p.n_cw, p.payload_stride),
+                           NULL) == 0, "fill_payload");
+  CHECK(oai4g_tx_batch(cfg, count, d_pay, d_work, d_iq, NULL) == 0 && oai4g_sync() == 0, "tx_batch (warm-up)");
+  CHECK(oai4g_dist_barrier() == 0, "barrier");
+  const int reps = 10;
+  const double b0 = now_us();
+  for (int r = 0; r < reps; r++) CHECK(oai4g_tx_batch(cfg, count, d_pay, d_work, d_iq, NULL) == 0, "tx_batch");
+  CHECK(oai4g_sync() == 0, "sync");
+  double dt = (now_us() - b0) / reps;
+  CHECK(oai4g_dist_allreduce_max_f64(&dt, 1) == 0, "allreduce max");
+  /* position-weighted IQ checksum of this shard: additive over ranks, independent of N */
+  uint32_t *iq = (uint32_t *)malloc(iqn * 4);
+  CHECK(iq && oai4g_memcpy_d2h(iq, d_iq, iqn * 4) == 0, "IQ download");
+  uint64_t sums[2] = {0, (uint64_t)count};
+  const size_t per_sf = (size_t)p.nb_antennas_tx * spt;
+  for (size_t i = 0; i < iqn; i++) {
+    const uint64_t g = (uint64_t)first * per_sf + i;
+    sums[0] += (uint64_t)iq[i] * (g * 0x9E3779B97F4A7C15ull + 1);
+  }
+  free(iq);
+  CHECK(oai4g_dist_allreduce_sum_u64(sums, 2) == 0, "allreduce sum");
+  if (rank == 0) {
+    printf("dlsim_tx %s world %d checksum 0x%016llx subframes %llu\n", c->name, world, (unsigned long long)sums[0],
+           (unsigned long long)sums[1]);
+    if (print_timing)
+      printf("[batch x%d] %.0f subframes/s aggregate (%d subframes per GPU per launch, max over ranks %.1f us)\n",
+             world, 1e6 * (double)sums[1] / dt, batch, dt);
+  }
+  oai4g_dev_free(d_pay);
+  oai4g_dev_free(d_work);
+  oai4g_dev_free(d_iq);
+  oai4g_tx_config_destroy(cfg);
+  CHECK(oai4g_dist_finalize() == 0, "dist_finalize");
+  return 0;
+}
+
 int main(int argc, char **argv)
 {
   const char *cname = "C3", *pay_file = NULL, *out_drop = NULL, *out_batch = NULL;
-  int subframe = 7, trials = 10, batch = 1024, print_timing = 0, opt;
-  while ((opt = getopt(argc, argv, "c:s:n:B:i:o:O:P")) != -1) {
+  int subframe = 7, trials = 10, batch = 1024, print_timing = 0, opt, world = 0, rank = 0;
+  while ((opt = getopt(argc, argv, "c:s:n:B:i:o:O:Pg:")) != -1) {
     switch (opt) {
     case 'c': cname = optarg; break;
     case 's': subframe = atoi(optarg); break;
@@ -89,6 +177,7 @@ int main(int argc, char **argv)
     case 'o': out_drop = optarg; break;
     case 'O': out_batch = optarg; break;
     case 'P': print_timing = 1; break;
+    case 'g': world = atoi(optarg); break;
     default:
       fprintf(stderr, "usage: %s [-c C1|C2|C3|C4|TM2] [-s sf] [-n trials] [-B batch] [-i pay] [-o iq] [-O iq] [-P]\n",
               argv[0]);
@@ -101,6 +190,44 @@ int main(int argc, char **argv)
   if (!c || subframe < 0 || subframe > 9 || trials < 1) {
     fprintf(stderr, "dlsim_tx: bad configuration / subframe / trials\n");
     return 2;
+  }
+  if (world > 0) {
+    /* one process per GPU: fork the ranks before anything touches HIP; rank 0's RCCL unique id
+     * reaches the others through pipes */
+    if (batch < 1 || world > 64) {
+      fprintf(stderr, "dlsim_tx: -g needs -B >= 1 and at most 64 ranks\n");
+      return 2;
+    }
+    int fds[64][2];
+    for (int r = 1; r < world; r++) CHECK(pipe(fds[r]) == 0, "pipe");
+    pid_t pids[64];
+    for (int r = 0; r < world; r++) {
+      pids[r] = fork();
+      CHECK(pids[r] >= 0, "fork");
+      if (pids[r] == 0) {
+        rank = r;
+        goto rank_main;
+      }
+    }
+    int rc_all = 0;
+    for (int r = 0; r < world; r++) {
+      int st = 0;
+      waitpid(pids[r], &st, 0);
+      if (!WIFEXITED(st) || WEXITSTATUS(st) != 0) rc_all = 1;
+    }
+    return rc_all;
+  rank_main:
+    CHECK(oai4g_set_device(rank) == 0, "set_device");
+    CHECK(oai4g_init() == 0, "no usable gfx950 device");
+    uint8_t id[OAI4G_DIST_ID_BYTES];
+    if (rank == 0) {
+      CHECK(oai4g_dist_unique_id(id) == 0, "dist_unique_id");
+      for (int r = 1; r < world; r++) CHECK(write(fds[r][1], id, sizeof(id)) == (ssize_t)sizeof(id), "id pipe write");
+    } else {
+      CHECK(read(fds[rank][0], id, sizeof(id)) == (ssize_t)sizeof(id), "id pipe read");
+    }
+    CHECK(oai4g_dist_init(rank, world, id) == 0, "dist_init");
+    return dist_batch(c, subframe, batch, rank, world, print_timing);
   }
   CHECK(oai4g_init() == 0, "no usable gfx950 device");
 
