@@ -262,6 +262,25 @@ size_t oai4g_rx_llr_stride(const oai4g_rx_config_t *cfg);
 int oai4g_rx_batch(oai4g_rx_config_t *cfg, int n_sf, const int32_t *d_rxdataF, const int32_t *d_dl_ch_estimates,
                    int16_t *d_llr, int unscramble, void *stream);
 
+/* TM3 (LARGE_CDD, two TX ports) with dlsim's UE (rx_pdsch with dual_stream_flag = 0,
+ * dlsch_demodulation.c:82-800): dlsch_extract_rbs_dual, dlsch_channel_level_TM3 + log2_maxh,
+ * dlsch_channel_compensation_TM3 (prec2A_TM3), dlsch_detection_mrc over nb_rx (1-2) receive
+ * antennas, then the single-stream 16 / 64-QAM LLRs of codeword 0 (Qm0 4 / 6; the reference
+ * computes no codeword-1 LLRs there).  Drop-in on host buffers: rxdataF[a] = [nsymb][N] per receive
+ * antenna, dl_ch_estimates[p * 2 + a] = [nsymb][N] (the reference's dl_ch_estimates[(p << 1) + a]).
+ * Returns the LLR count (not unscrambled) or -1. */
+int oai4g_rx_pdsch_tm3(const oai4g_frame_parms_t *frame_parms, int nb_rx, const int32_t *const *rxdataF,
+                       const int32_t *const *dl_ch_estimates, const uint32_t rb_alloc[4], uint8_t Qm0, uint8_t Qm1,
+                       uint8_t mcs0, uint8_t num_pdcch_symbols, uint8_t subframe, int16_t *llr, uint8_t *log2_maxh);
+/* Batched TM3 demodulation: d_rxdataF = [n_sf][nb_rx][nsymb][N] (the FEP batch output),
+ * d_est = four planes [p * 2 + a][n_sf][nsymb][N] (channel estimation batches of ports 0 / 1 per
+ * receive antenna) -> codeword 0's LLR streams [n_sf][oai4g_rx_llr_stride] (unscrambled when asked). */
+oai4g_rx_config_t *oai4g_rx_config_create_tm3(const oai4g_frame_parms_t *frame_parms, const uint32_t rb_alloc[4],
+                                              uint8_t Qm0, uint8_t Qm1, uint8_t mcs0, uint8_t num_pdcch_symbols,
+                                              uint16_t rnti, uint8_t first_subframe, uint8_t subframe_step, uint8_t nb_rx);
+int oai4g_rx_batch_tm3(oai4g_rx_config_t *cfg, int n_sf, const int32_t *d_rxdataF, const int32_t *d_est, int16_t *d_llr,
+                       int unscramble, void *stream);
+
 /* lte_dl_channel_estimation (PHY/LTE_ESTIMATION/lte_dl_channel_estimation.c:37, decl
  * LTE_ESTIMATION/defs.h; called by slot_fep.c:188 for the pilot symbols of every slot) with the
  * reference's defaults high_speed_flag = 1 (dlsim.c:2057), eNB_offset 0, one RX antenna: the
@@ -288,9 +307,11 @@ typedef struct oai4g_chest_config oai4g_chest_config_t;
 oai4g_chest_config_t *oai4g_chest_config_create(const oai4g_frame_parms_t *frame_parms, uint8_t p,
                                                 uint8_t first_subframe, uint8_t subframe_step);
 void oai4g_chest_config_destroy(oai4g_chest_config_t *cfg);
-/* Batch elements `subframes_per_element` subframes apart in d_rxdataF (default 1): dlsim's BLER
- * loop keeps each trial's subframe followed by the next one, whose symbol 0 closes rows 12 / 13. */
-int oai4g_chest_config_set_stride(oai4g_chest_config_t *cfg, uint32_t subframes_per_element);
+/* Batch elements `subframes_per_element` subframes apart in d_rxdataF, the symbol 0 that closes rows
+ * 12 / 13 `next_subframes` subframes after each element's start (default 1 / 1).  dlsim's BLER loop:
+ * 2 / 1 (each trial's subframe followed by the next one); a receive antenna of an n-antenna FEP
+ * batch: n / n (pass d_rxdataF + a nsymb N). */
+int oai4g_chest_config_set_stride(oai4g_chest_config_t *cfg, uint32_t subframes_per_element, uint32_t next_subframes);
 int oai4g_chest_batch(oai4g_chest_config_t *cfg, int n_sf, const int32_t *d_rxdataF, int32_t *d_est, void *stream);
 /* The batch chain without the estimate buffer: oai4g_chest_batch followed by oai4g_rx_batch, fused
  * (the estimate of each PDSCH RE is formed in LDS from the pilot rows), same LLRs; d_rxdataF as

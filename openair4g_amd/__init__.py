@@ -219,7 +219,15 @@ _SIGS = {
     "oai4g_shard_range": (None, [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.POINTER(ctypes.c_int),
                                  ctypes.POINTER(ctypes.c_int)]),
     "oai4g_payload_seed": (ctypes.c_uint64, [ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint32]),
-    "oai4g_chest_config_set_stride": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_uint32]),
+    "oai4g_chest_config_set_stride": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint32]),
+    "oai4g_rx_pdsch_tm3": (ctypes.c_int, [ctypes.POINTER(FrameParms), ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p,
+                                          ctypes.c_void_p, ctypes.c_uint8, ctypes.c_uint8, ctypes.c_uint8,
+                                          ctypes.c_uint8, ctypes.c_uint8, ctypes.c_void_p, ctypes.c_void_p]),
+    "oai4g_rx_config_create_tm3": (ctypes.c_void_p, [ctypes.POINTER(FrameParms), ctypes.c_void_p, ctypes.c_uint8,
+                                                     ctypes.c_uint8, ctypes.c_uint8, ctypes.c_uint8, ctypes.c_uint16,
+                                                     ctypes.c_uint8, ctypes.c_uint8, ctypes.c_uint8]),
+    "oai4g_rx_batch_tm3": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p,
+                                          ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p]),
     "oai4g_signal_energy": (ctypes.c_int32, [ctypes.c_void_p, ctypes.c_uint32]),
     "oai4g_signal_energy_batch": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_size_t, ctypes.c_uint32,
                                                  ctypes.c_void_p, ctypes.c_void_p]),
@@ -501,6 +509,90 @@ def rx_pdsch_siso(fp, rxdataF, dl_ch, rb_alloc, Qm, num_pdcch, subframe):
                                   _ptr(out), ctypes.byref(sh))
     _check(n >= 0)
     return out[:n], sh.value
+
+
+def rx_pdsch_tm3(fp, rxF, est, rb_alloc, Qm0, Qm1, mcs0, num_pdcch, subframe):
+    """rx_pdsch for TM3 (dual_stream_flag = 0): rxF = [nb_rx][nsymb*N], est[(p, a)] = [nsymb*N].
+    Returns (codeword-0 LLRs, log2_maxh)."""
+    init()
+    nb_rx = len(rxF)
+    rx = [np.ascontiguousarray(r, dtype=np.int32) for r in rxF]
+    keep = {k: np.ascontiguousarray(v, dtype=np.int32) for k, v in est.items()}
+    ep = (ctypes.c_void_p * 4)()
+    for (p_, a), arr in keep.items():
+        if a < nb_rx:
+            ep[2 * p_ + a] = arr.ctypes.data
+    rp = (ctypes.c_void_p * 2)(*[r.ctypes.data for r in rx] + [None] * (2 - nb_rx))
+    out = np.zeros(14 * 1200 * 6 + 64, dtype=np.int16)
+    sh = ctypes.c_uint8()
+    ra = (ctypes.c_uint32 * 4)(*rb_alloc)
+    n = lib().oai4g_rx_pdsch_tm3(ctypes.byref(fp), nb_rx, rp, ep, ra, Qm0, Qm1, mcs0, num_pdcch, subframe, _ptr(out),
+                                 ctypes.byref(sh))
+    _check(n >= 0)
+    return out[:n], sh.value
+
+
+class RxBatchTM3:
+    """Device-resident batched TM3 demodulation (oai4g_rx_batch_tm3): codeword 0's LLRs from the FEP
+    output of nb_rx antennas and the four estimate planes (ports 0 / 1 per antenna)."""
+
+    def __init__(self, fp, rb_alloc, Qm0, Qm1, mcs0, num_pdcch, rnti, n_sf, nb_rx=2, first_subframe=0,
+                 subframe_step=1):
+        init()
+        self.L = lib()
+        ra = (ctypes.c_uint32 * 4)(*rb_alloc)
+        self.cfg = self.L.oai4g_rx_config_create_tm3(ctypes.byref(fp), ra, Qm0, Qm1, mcs0, num_pdcch, rnti,
+                                                     first_subframe, subframe_step, nb_rx)
+        _check(bool(self.cfg))
+        self.fp, self.n_sf, self.nb_rx = fp, n_sf, nb_rx
+        self.stride = self.L.oai4g_rx_llr_stride(self.cfg)
+        self.plane = n_sf * fp.symbols_per_tti * fp.ofdm_symbol_size
+        self.d_est = self.L.oai4g_dev_alloc(4 * self.plane * 4)
+        self.d_llr = self.L.oai4g_dev_alloc(n_sf * self.stride * 2)
+        _check(bool(self.d_est) and bool(self.d_llr))
+
+    def llr_count(self, sfi):
+        return self.L.oai4g_rx_llr_count(self.cfg, sfi)
+
+    def est_plane(self, p, a):
+        """device pointer of the estimate plane of port p at receive antenna a"""
+        return ctypes.c_void_p(self.d_est + (2 * p + a) * self.plane * 4)
+
+    def estimate(self, d_rxF, first_subframe=0, subframe_step=1, stream=None):
+        """The four channel-estimation batches over the FEP output [n_sf + 1][nb_rx][nsymb][N]
+        (the extra element's symbol 0 closes the last subframe's rows 12 / 13)."""
+        N, nsymb = self.fp.ofdm_symbol_size, self.fp.symbols_per_tti
+        for p in (0, 1):
+            cfg = self.L.oai4g_chest_config_create(ctypes.byref(self.fp), p, first_subframe, subframe_step)
+            _check(bool(cfg))
+            try:
+                _check(self.L.oai4g_chest_config_set_stride(cfg, self.nb_rx, self.nb_rx) == 0)
+                for a in range(self.nb_rx):
+                    _check(self.L.oai4g_chest_batch(cfg, self.n_sf, ctypes.c_void_p(d_rxF + a * nsymb * N * 4),
+                                                    self.est_plane(p, a), stream) == 0)
+            finally:
+                _check(self.L.oai4g_sync() == 0)
+                self.L.oai4g_chest_config_destroy(cfg)
+
+    def launch(self, d_rxF, unscramble=1, stream=None):
+        _check(self.L.oai4g_rx_batch_tm3(self.cfg, self.n_sf, d_rxF, self.d_est, self.d_llr, unscramble, stream) == 0)
+
+    def llrs(self):
+        _check(self.L.oai4g_sync() == 0)
+        out = np.empty((self.n_sf, self.stride), dtype=np.int16)
+        _check(self.L.oai4g_memcpy_d2h(_ptr(out), self.d_llr, out.nbytes) == 0)
+        return out
+
+    def estimates(self):
+        _check(self.L.oai4g_sync() == 0)
+        out = np.empty((4, self.n_sf, self.plane // self.n_sf), dtype=np.int32)
+        _check(self.L.oai4g_memcpy_d2h(_ptr(out), self.d_est, out.nbytes) == 0)
+        return out
+
+    def close(self):
+        self.L.oai4g_dev_free(self.d_est)
+        self.L.oai4g_dev_free(self.d_llr)
+        self.L.oai4g_rx_config_destroy(self.cfg)
 
 
 def dlsch_unscrambling(fp, rnti, G, llr, q, Ns, mbsfn_flag=0):

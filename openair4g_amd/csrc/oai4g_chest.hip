@@ -143,7 +143,7 @@ __global__ void __launch_bounds__(CE_WG) k_chest(const chest_dev_t *__restrict__
   if (c->branch)
     for (uint32_t i = threadIdx.x; i < 5 * n_p; i += CE_WG) {
       const uint32_t in = i / n_p, m = m_base + i % n_p;
-      const uint32_t sym = in == 0 ? 0 : in == 1 ? p1 : in == 2 ? p2 : in == 3 ? p3 : nsymb;  /* nsymb: next sf */
+      const uint32_t sym = in == 0 ? 0 : in == 1 ? p1 : in == 2 ? p2 : in == 3 ? p3 : c->next_syms;  /* next sf */
       const uint32_t Ns = in < 2 ? 2 * sfi : in < 4 ? 2 * sfi + 1 : (2 * sfi + 2) % 20;
       chl[in][i % n_p] = ce_pilot_ch(c, base + (size_t)sym * N, Ns, in & 1u, m);
     }
@@ -261,7 +261,7 @@ __global__ void __launch_bounds__(RXC_WG) k_rx_chest(const chest_dev_t *__restri
   if (ce->branch)
     for (uint32_t i = threadIdx.x; i < 5 * np; i += RXC_WG) {
       const uint32_t in = i / np, m = i - in * np;
-      const uint32_t sym = in == 0 ? 0 : in == 1 ? p1 : in == 2 ? p2 : in == 3 ? p3 : nsymb;
+      const uint32_t sym = in == 0 ? 0 : in == 1 ? p1 : in == 2 ? p2 : in == 3 ? p3 : ce->next_syms;
       const uint32_t Ns = in < 2 ? 2 * sfi : in < 4 ? 2 * sfi + 1 : (2 * sfi + 2) % 20;
       chl[in][m] = ce_pilot_ch(ce, base + (size_t)sym * N, Ns, in & 1u, m);
     }

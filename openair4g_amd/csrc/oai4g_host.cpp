@@ -3193,14 +3193,118 @@ static void rx_extract_map(const oai4g_frame_parms_t *fp, const uint32_t rb_allo
   map.insert(map.end(), slot, slot + hw);
 }
 
-extern "C" oai4g_rx_config_t *oai4g_rx_config_create(const oai4g_frame_parms_t *fp, const uint32_t rb_alloc[4], uint8_t Qm,
-                                                     uint8_t num_pdcch_symbols, uint16_t rnti, uint8_t first_subframe,
-                                                     uint8_t subframe_step)
+/* dlsch_extract_rbs_dual (dlsch_demodulation.c:3683-4056) of one symbol as an extraction map of
+ * the slots one receive antenna's call leaves written (every antenna and both ports share it): the
+ * PBCH / PSS / SSS RBs are dropped; 8 REs per RB in pilot symbols; odd N_RB_DL as written there —
+ * the RB around DC reads bins 0..5 for its upper half in non-pilot symbols, and the skip_half = 2
+ * pilot branch advances the pointers inside its RE loop. */
+static void rx_extract_map_dual(const oai4g_frame_parms_t *fp, const uint32_t rb_alloc[4], uint32_t subframe, uint32_t l,
+                                std::vector<uint32_t> &map, uint32_t &nb_rb, uint32_t &n)
+{
+  const uint32_t smod = l >= 7u - fp->Ncp ? l - (7u - fp->Ncp) : l;
+  const bool pil = smod == 0 || smod == 4u - fp->Ncp;
+  const int nsymb = fp->Ncp == 0 ? 14 : 12, half = fp->N_RB_DL >> 1, li = (int)l;
+  const uint32_t ns = fp->nushift;
+  const int sss_symb = fp->frame_type == 1 ? nsymb - 1 : (nsymb >> 1) - 2;
+  const int pss_symb = fp->frame_type == 1 ? 2 : (nsymb >> 1) - 1;
+  std::vector<uint32_t> slot(12 * 110 + 256, 0);
+  uint32_t p = 0, hw = 0;
+  nb_rb = 0;
+  auto put = [&](uint32_t pos, uint32_t bin, uint32_t col) {
+    slot[pos] = bin | ((5 + col) << 16);
+    hw = pos + 1 > hw ? pos + 1 : hw;
+  };
+  auto data_re = [&](uint32_t i) { return i != ns && i != ns + 3 && i != ns + 6 && i != (ns + 9) % 12; };
+  for (int prb = 0; prb < fp->N_RB_DL; prb++) {
+    int ind = rx_alloc_bit(rb_alloc, prb), skip_half = 0;
+    if (subframe == 0 && prb > half - 3 && prb < half + 3 && li >= (nsymb >> 1) && li < (nsymb >> 1) + 4) ind = 0;
+    if ((subframe == 0 || subframe == 5) && prb > half - 3 && prb < half + 3 && li == sss_symb) ind = 0;
+    if (fp->frame_type == 0 && (subframe == 0 || subframe == 5) && prb > half - 3 && prb < half + 3 && li == pss_symb) ind = 0;
+    if (fp->frame_type == 1 && subframe == 6 && prb >= half - 3 && prb <= half + 3 && li == pss_symb) ind = 0;
+    if (!ind) continue;
+    const uint32_t col0 = 12 * prb;
+    if ((fp->N_RB_DL & 1) == 0) {
+      const uint32_t b0 = prb < half ? fp->first_carrier_offset + 12 * prb : 1 + 12 * (prb - half);
+      uint32_t j = 0;
+      for (uint32_t i = 0; i < 12; i++)
+        if (!pil || data_re(i)) put(p + j++, b0 + i, col0 + i);
+      p += pil ? 8 : 12;
+      nb_rb++;
+      continue;
+    }
+    if (subframe == 0 && prb == half - 3 && li >= (nsymb >> 1) && li < (nsymb >> 1) + 4) skip_half = 1;
+    else if (subframe == 0 && prb == half + 3 && li >= (nsymb >> 1) && li < (nsymb >> 1) + 4) skip_half = 2;
+    if ((subframe == 0 || subframe == 5) && prb == half - 3 && li == sss_symb) skip_half = 1;
+    else if ((subframe == 0 || subframe == 5) && prb == half + 3 && li == sss_symb) skip_half = 2;
+    if ((fp->frame_type == 0 && (subframe == 0 || subframe == 5)) || (fp->frame_type == 1 && (subframe == 2 || subframe == 6))) {
+      if (prb == half - 3 && li == pss_symb) skip_half = 1;
+      else if ((subframe == 0 || subframe == 5) && prb == half + 3 && li == pss_symb) skip_half = 2;
+    }
+    const uint32_t b0 = prb <= half ? fp->first_carrier_offset + 12 * prb : 7 + 12 * (prb - half - 1);
+    if (prb != half) {
+      if (!pil) {
+        const uint32_t o = skip_half == 2 ? 6 : 0, cnt = skip_half ? 6 : 12;
+        for (uint32_t i = 0; i < cnt; i++) put(p + i, b0 + o + i, col0 + o + i);
+        p += cnt;
+      } else if (skip_half == 1) {
+        uint32_t j = 0;
+        for (uint32_t i = 0; i < 6; i++)
+          if (i != ns && i != (ns + 3) % 6) put(p + j++, b0 + i, col0 + i);
+        p += 4;
+      } else if (skip_half == 2) {
+        uint32_t j = 0;
+        for (uint32_t i = 0; i < 6; i++) {
+          if (i != ns && i != (ns + 3) % 6) put(p + j++, b0 + i + 6, col0 + i + 6);
+          p += 4;                                            /* inside the loop, as written */
+        }
+      } else {
+        uint32_t j = 0;
+        for (uint32_t i = 0; i < 12; i++)
+          if (data_re(i)) put(p + j++, b0 + i, col0 + i);
+        p += 8;
+      }
+    } else {                                                 /* the RB around DC */
+      if (!pil) {
+        for (uint32_t i = 0; i < 6; i++) put(p + i, b0 + i, col0 + i);
+        for (uint32_t i = 0; i < 6; i++) put(p + 6 + i, i, col0 + 6 + i);
+        p += 12;
+      } else {
+        uint32_t j = 0, i = 0;
+        for (; i < 6; i++)
+          if (i != ns && i != (ns + 3) % 6) put(p + j++, b0 + i, col0 + i);
+        for (; i < 12; i++)
+          if (i != (ns + 6) % 12 && i != (ns + 9) % 12) put(p + j++, 1 + i - 6, col0 + i);
+        p += 8;
+      }
+    }
+    nb_rb++;
+  }
+  n = hw;
+  map.insert(map.end(), slot.begin(), slot.begin() + hw);
+}
+
+/* offset_mumimo_llr_drange (dlsch_demodulation.c:76, the active table) [MCS][Qm1 / 2 - 1] */
+static const uint8_t k_mumimo_off[29][3] = {{0, 6, 5}, {0, 4, 5}, {0, 4, 5}, {0, 5, 4}, {0, 5, 6}, {0, 5, 3}, {0, 4, 4},
+                                            {0, 4, 4}, {0, 3, 3}, {0, 1, 2}, {1, 1, 0}, {1, 3, 2}, {3, 4, 1}, {2, 0, 0},
+                                            {2, 2, 2}, {1, 1, 1}, {2, 1, 0}, {2, 1, 1}, {1, 0, 1}, {1, 0, 1}, {0, 0, 0},
+                                            {1, 0, 0}, {0, 0, 0}, {0, 1, 0}, {1, 0, 0}, {0, 0, 0}, {0, 0, 0}, {0, 0, 0},
+                                            {0, 0, 0}};
+
+static oai4g_rx_config_t *rx_config_build(const oai4g_frame_parms_t *fp, const uint32_t rb_alloc[4], uint8_t Qm,
+                                          uint8_t num_pdcch_symbols, uint16_t rnti, uint8_t first_subframe,
+                                          uint8_t subframe_step, int tm3, uint8_t Qm1, uint8_t mcs0, uint8_t nb_rx)
 {
   NEED_INIT(nullptr);
-  if (fp->nb_antennas_tx != 1 || fp->mode1_flag != 1 || (Qm != 2 && Qm != 4 && Qm != 6) ||
-      num_pdcch_symbols < 1 || num_pdcch_symbols > 3) {
+  if (!tm3 && (fp->nb_antennas_tx != 1 || fp->mode1_flag != 1 || (Qm != 2 && Qm != 4 && Qm != 6) ||
+               num_pdcch_symbols < 1 || num_pdcch_symbols > 3)) {
     set_err("rx_config: TM1 (one TX port), Qm 2/4/6, 1..3 PDCCH symbols only");
+    return nullptr;
+  }
+  if (tm3 && (fp->nb_antennas_tx != 2 || fp->mode1_flag != 0 || (Qm != 4 && Qm != 6) ||
+              (Qm1 != 2 && Qm1 != 4 && Qm1 != 6) || mcs0 > 28 || nb_rx < 1 || nb_rx > 2 || num_pdcch_symbols < 1 ||
+              num_pdcch_symbols > 3)) {
+    set_err("rx_config_tm3: two TX ports, Qm0 4/6 (Qm0 = 2 needs the interference-aware LLRs), Qm1 2/4/6, "
+            "1-2 RX antennas, 1..3 PDCCH symbols");
     return nullptr;
   }
   const uint32_t nsymb = fp->Ncp == 0 ? 14 : 12, N = fp->ofdm_symbol_size;
@@ -3222,6 +3326,9 @@ extern "C" oai4g_rx_config_t *oai4g_rx_config_create(const oai4g_frame_parms_t *
   h.sf_step = subframe_step;
   h.a1 = Qm == 4 ? 20724 : (Qm == 6 ? 20225 : 0);          /* QAM16_n1 / QAM64_n1 (impl_defs_top.h:215-224) */
   h.a2 = Qm == 6 ? 10112 : 0;                               /* QAM64_n2 */
+  h.tm3 = tm3 ? 1u : 0u;
+  h.nb_rx = tm3 ? nb_rx : 1u;
+  h.mu_off = tm3 ? k_mumimo_off[mcs0][(Qm1 >> 1) - 1] : 0;
   std::vector<uint32_t> map;
   uint32_t max_llr = 0;
   for (uint32_t sf = 0; sf < 10; sf++) {
@@ -3232,12 +3339,19 @@ extern "C" oai4g_rx_config_t *oai4g_rx_config_create(const oai4g_frame_parms_t *
       const bool pil = smod == 0 || smod == 4u - fp->Ncp;
       h.map_off[sf][k] = (uint32_t)map.size();
       uint32_t nb_rb = 0, n = 0;
-      rx_extract_map(fp, rb_alloc, sf, l, map, nb_rb, n);
+      if (tm3)
+        rx_extract_map_dual(fp, rb_alloc, sf, l, map, nb_rb, n);
+      else
+        rx_extract_map(fp, rb_alloc, sf, l, map, nb_rb, n);
       h.n_ext[sf][k] = n;
       const int adj = Qm == 2 ? 0 : rx_adjust_G2(fp, rb_alloc, sf, l);
-      const int len = pil ? (int)nb_rb * 10 - 5 * adj / 6 : (int)nb_rb * 12 - adj;
+      /* dlsch_*_llr: pilot symbols carry 10 (one port) or 8 (two ports, mode1_flag 0) REs per RB */
+      const int len = pil ? (tm3 ? (int)nb_rb * 8 - 2 * adj / 3 : (int)nb_rb * 10 - 5 * adj / 6) : (int)nb_rb * 12 - adj;
       h.len[sf][k] = (uint32_t)(len > 0 ? len : 0);
-      if (h.len[sf][k] > n || (k == 0 && 12 * nb_rb > n)) {
+      /* channel_level_TM3 takes 8 REs per RB only where symbol_mod == 0 (its 4-Ncp test reads
+       * Ncp-1, :2917-2922); the SISO level reads 12 per RB */
+      const uint32_t lvl_nre = tm3 && smod == 0 ? 8u : 12u;
+      if (h.len[sf][k] > n || (k == 0 && lvl_nre * nb_rb > n)) {
         /* the reference would read ext slots this symbol did not write (odd N_RB_DL with a
          * PBCH / sync half RB and the unadjusted QPSK length, :3354-3427): a batch that runs
          * this subframe index is refused */
@@ -3248,8 +3362,8 @@ extern "C" oai4g_rx_config_t *oai4g_rx_config_create(const oai4g_frame_parms_t *
       h.llr_off[sf][k] = off;
       off += h.len[sf][k] * Qm;
       if (k == 0) {
-        h.lvl_n[sf] = 12 * nb_rb;
-        h.lvl_div[sf] = (pil ? 10 : 12) * nb_rb;
+        h.lvl_n[sf] = lvl_nre * nb_rb;
+        h.lvl_div[sf] = tm3 ? lvl_nre * nb_rb : (pil ? 10 : 12) * nb_rb;
       }
       if (nb_rb == 0) cfg->bad[sf] = true;                   /* empty allocation in this symbol */
     }
@@ -3292,6 +3406,21 @@ extern "C" oai4g_rx_config_t *oai4g_rx_config_create(const oai4g_frame_parms_t *
     return nullptr;
   }
   return cfg;
+}
+
+extern "C" oai4g_rx_config_t *oai4g_rx_config_create(const oai4g_frame_parms_t *fp, const uint32_t rb_alloc[4], uint8_t Qm,
+                                                     uint8_t num_pdcch_symbols, uint16_t rnti, uint8_t first_subframe,
+                                                     uint8_t subframe_step)
+{
+  return rx_config_build(fp, rb_alloc, Qm, num_pdcch_symbols, rnti, first_subframe, subframe_step, 0, 0, 0, 1);
+}
+
+extern "C" oai4g_rx_config_t *oai4g_rx_config_create_tm3(const oai4g_frame_parms_t *fp, const uint32_t rb_alloc[4],
+                                                         uint8_t Qm0, uint8_t Qm1, uint8_t mcs0,
+                                                         uint8_t num_pdcch_symbols, uint16_t rnti,
+                                                         uint8_t first_subframe, uint8_t subframe_step, uint8_t nb_rx)
+{
+  return rx_config_build(fp, rb_alloc, Qm0, num_pdcch_symbols, rnti, first_subframe, subframe_step, 1, Qm1, mcs0, nb_rx);
 }
 
 extern "C" void oai4g_rx_config_destroy(oai4g_rx_config_t *cfg)
@@ -3344,6 +3473,57 @@ extern "C" int oai4g_rx_batch(oai4g_rx_config_t *cfg, int n_sf, const int32_t *d
 /* rx_pdsch over the PDSCH symbols of one subframe (dlsim.c:3188-3260) on host buffers:
  * rxdataF / dl_ch_estimates = [nsymb][N] of the subframe; writes the LLR stream (not unscrambled)
  * and log2_maxh; returns the stream length or -1. */
+extern "C" int oai4g_rx_batch_tm3(oai4g_rx_config_t *cfg, int n_sf, const int32_t *d_rxdataF, const int32_t *d_est,
+                                  int16_t *d_llr, int unscramble, void *stream)
+{
+  NEED_INIT(-1);
+  if (!cfg || !cfg->h.tm3) { set_err("rx_batch_tm3: not a TM3 configuration (oai4g_rx_config_create_tm3)"); return -1; }
+  if (n_sf <= 0) return 0;
+  if (rx_check_batch(cfg, n_sf) != 0) return -1;
+  if (n_sf > cfg->shift_cap) {
+    if (cfg->d_shift) hipFree(cfg->d_shift);
+    HCK(hipMalloc(&cfg->d_shift, (size_t)n_sf), -1);
+    cfg->shift_cap = n_sf;
+  }
+  const size_t plane = (size_t)n_sf * cfg->h.nsymb * cfg->h.N;
+  HCK(oai4g_launch_rx_tm3(cfg->d, &cfg->h, n_sf, d_rxdataF, d_est, plane, d_llr, cfg->d_shift, unscramble,
+                          (hipStream_t)stream), -1);
+  return 0;
+}
+
+extern "C" int oai4g_rx_pdsch_tm3(const oai4g_frame_parms_t *fp, int nb_rx, const int32_t *const *rxdataF,
+                                  const int32_t *const *dl_ch_estimates, const uint32_t rb_alloc[4], uint8_t Qm0,
+                                  uint8_t Qm1, uint8_t mcs0, uint8_t num_pdcch_symbols, uint8_t subframe, int16_t *llr,
+                                  uint8_t *log2_maxh)
+{
+  NEED_INIT(-1);
+  oai4g_rx_config_t *cfg = oai4g_rx_config_create_tm3(fp, rb_alloc, Qm0, Qm1, mcs0, num_pdcch_symbols, 0, subframe, 1,
+                                                      (uint8_t)nb_rx);
+  if (!cfg) return -1;
+  if (rx_check_batch(cfg, 1) != 0) { oai4g_rx_config_destroy(cfg); return -1; }
+  const size_t gb = (size_t)cfg->h.nsymb * cfg->h.N * 4, gs = (gb + 255) & ~(size_t)255;
+  const int n = (int)cfg->llr_count[subframe % 10];
+  uint8_t *buf = scratch(6 * gs + (size_t)cfg->h.llr_stride * 2 + 256);
+  if (!buf) { oai4g_rx_config_destroy(cfg); return -1; }
+  int32_t *dy = (int32_t *)buf, *de = (int32_t *)(buf + 2 * gs);   /* [nb_rx][grid], planes [p * 2 + a] */
+  int16_t *dl = (int16_t *)(buf + 6 * gs);
+  bool ok = true;
+  for (int a = 0; a < nb_rx && ok; a++) ok = hipMemcpyAsync((uint8_t *)dy + a * gb, rxdataF[a], gb, hipMemcpyHostToDevice, g_scr.s) == hipSuccess;
+  for (int pa = 0; pa < 4 && ok; pa++)
+    if ((pa & 1) < nb_rx)
+      ok = hipMemcpyAsync((uint8_t *)de + pa * gb, dl_ch_estimates[pa], gb, hipMemcpyHostToDevice, g_scr.s) == hipSuccess;
+  int rc = -1;
+  if (ok && oai4g_rx_batch_tm3(cfg, 1, dy, de, dl, 0, g_scr.s) == 0 &&
+      hipMemcpyAsync(llr, dl, (size_t)n * 2, hipMemcpyDeviceToHost, g_scr.s) == hipSuccess &&
+      (!log2_maxh || hipMemcpyAsync(log2_maxh, cfg->d_shift, 1, hipMemcpyDeviceToHost, g_scr.s) == hipSuccess) &&
+      hipStreamSynchronize(g_scr.s) == hipSuccess)
+    rc = n;
+  else
+    set_err("rx_pdsch_tm3: HIP error");
+  oai4g_rx_config_destroy(cfg);
+  return rc;
+}
+
 extern "C" int oai4g_rx_pdsch_siso(const oai4g_frame_parms_t *fp, const int32_t *rxdataF, const int32_t *dl_ch_estimates,
                                    const uint32_t rb_alloc[4], uint8_t Qm, uint8_t num_pdcch_symbols, uint8_t subframe,
                                    int16_t *llr, uint8_t *log2_maxh)
@@ -3477,6 +3657,7 @@ static int chest_fill(const oai4g_frame_parms_t *fp, uint8_t p, chest_dev_t &h)
   h.N_RB = N_RB;
   h.nsymb = fp->Ncp == 0 ? 14 : 12;
   h.elem_syms = h.nsymb;
+  h.next_syms = h.nsymb;
   h.Ncp = fp->Ncp;
   h.fco = fp->first_carrier_offset;
   h.p = p;
@@ -3512,11 +3693,13 @@ extern "C" oai4g_chest_config_t *oai4g_chest_config_create(const oai4g_frame_par
   return cfg;
 }
 
-extern "C" int oai4g_chest_config_set_stride(oai4g_chest_config_t *cfg, uint32_t subframes_per_element)
+extern "C" int oai4g_chest_config_set_stride(oai4g_chest_config_t *cfg, uint32_t subframes_per_element,
+                                             uint32_t next_subframes)
 {
   NEED_INIT(-1);
-  if (!cfg || subframes_per_element < 1) { set_err("chest_config_set_stride: bad arguments"); return -1; }
+  if (!cfg || subframes_per_element < 1 || next_subframes < 1) { set_err("chest_config_set_stride: bad arguments"); return -1; }
   cfg->h.elem_syms = cfg->h.nsymb * subframes_per_element;
+  cfg->h.next_syms = cfg->h.nsymb * next_subframes;
   if (hipMemcpy(cfg->d, &cfg->h, sizeof(chest_dev_t), hipMemcpyHostToDevice) != hipSuccess) {
     set_err("chest_config_set_stride: upload failed");
     return -1;

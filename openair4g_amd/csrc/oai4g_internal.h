@@ -317,6 +317,7 @@ struct chest_dev_t {
   uint32_t off2[2];               /* first bin of the pilots above DC: 1 + k, or 1 + nushift + 3 p at 15 PRB */
   uint32_t elem_syms;             /* symbols between batch elements in rxdataF (nsymb; 2 nsymb in dlsim's BLER
                                      loop, where each trial's subframe is followed by the next one) */
+  uint32_t next_syms;             /* symbols from an element's start to the symbol 0 closing its rows 12 / 13 */
   int16_t filt[2][8][24];         /* fl, f2l2, f, f2, fr, f2r2, f_dc, f2_dc (filt96_32.h) for k[0] / k[1] */
   uint32_t gold[20][2][14];       /* lte_gold_table */
 };
@@ -345,8 +346,15 @@ struct rx_dev_t {
   int16_t a1, a2;                 /* QAM_n1 / QAM_n2 of the channel magnitude (0 for QPSK) */
   const uint32_t *map;            /* extracted RE j: FFT bin | (estimate index within the symbol) << 16 */
   const uint32_t *gold;           /* [10][gold_words] */
+  /* TM3 (LARGE_CDD, dual extraction; rx_pdsch with dual_stream_flag = 0): receive antennas, the
+   * channel_level_TM3 RE count per RB of the first PDSCH symbol, offset_mumimo_llr_drange */
+  uint32_t tm3, nb_rx, lvl_nre;
+  int32_t mu_off;
 };
 hipError_t oai4g_launch_rx_chest(const chest_dev_t *d_ce, const rx_dev_t *d_rx, const rx_dev_t *h_rx, int n_sf,
                                  const int32_t *d_rxF, int16_t *d_llr, uint8_t *d_shift, int unscramble, hipStream_t s);
+hipError_t oai4g_launch_rx_tm3(const rx_dev_t *d_cfg, const rx_dev_t *h_cfg, int n_sf, const int32_t *d_rxF,
+                               const int32_t *d_est, size_t plane, int16_t *d_llr, uint8_t *d_shift, int unscramble,
+                               hipStream_t s);
 hipError_t oai4g_launch_rx(const rx_dev_t *d_cfg, const rx_dev_t *h_cfg, int n_sf, const int32_t *d_rxF,
                            const int32_t *d_ch, int16_t *d_llr, uint8_t *d_shift, int unscramble, hipStream_t s);

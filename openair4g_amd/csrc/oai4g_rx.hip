@@ -74,6 +74,134 @@ __global__ void __launch_bounds__(256) k_rx_llr(const rx_dev_t *__restrict__ c, 
   }
 }
 
+/* ======================================================================================
+ * TM3 (LARGE_CDD, two ports), nb_rx receive antennas, rx_pdsch with dual_stream_flag = 0:
+ *   dlsch_extract_rbs_dual      dlsch_demodulation.c:3683-4056 (the host's map; ports 0 / 1 and
+ *                               every receive antenna share the slots)
+ *   dlsch_channel_level_TM3     :2902-2981 (stream-0 |h|^2 per register lane e mod 4, int32 wrap,
+ *                               accumulated over the antennas without reset, per-lane division)
+ *   log2_maxh                   :390-394 (log2_approx(avg) - 13 + offset_mumimo_llr_drange, >= 0)
+ *   dlsch_channel_compensation_TM3 :1846-2120 with prec2A_TM3_128 (s alternates per slot)
+ *   dlsch_detection_mrc         :2583-2718 (stream 0: (a >> 1) +sat (b >> 1))
+ *   dlsch_16qam / 64qam_llr     of stream 0, unscrambled
+ * d_est holds the estimate planes [p * 2 + a][n_sf][nsymb][N] (plane = n_sf nsymb N words), d_rxF
+ * the FEP output [n_sf][nb_rx][nsymb][N].
+ * ==================================================================================== */
+__global__ void __launch_bounds__(256) k_rx_level_tm3(const rx_dev_t *__restrict__ c, const int32_t *__restrict__ est,
+                                                      size_t plane, uint8_t *__restrict__ shift)
+{
+  __shared__ uint32_t lane[2][4];
+  const uint32_t sf = blockIdx.x, sfi = (c->first_sf + sf * c->sf_step) % 10, l = c->npdcch;
+  if (threadIdx.x < 8) lane[threadIdx.x >> 2][threadIdx.x & 3] = 0;
+  __syncthreads();
+  rg32_t *map = (rg32_t *)(c->map + c->map_off[sfi][0]);
+  const size_t so = ((size_t)sf * c->nsymb + l) * c->N;
+  uint32_t part[2][4] = {{0, 0, 0, 0}, {0, 0, 0, 0}};
+  for (uint32_t j = threadIdx.x; j < c->lvl_n[sfi]; j += blockDim.x) {
+    const uint32_t col = map[j] >> 16;
+    for (uint32_t a = 0; a < c->nb_rx; a++) {
+      const uint32_t h0 = (uint32_t)est[a * plane + so + col], h1 = (uint32_t)est[(2 + a) * plane + so + col];
+      const uint32_t v = rx_h2(rx_prec_tm3(h0, h1, (j & 1u) != 0));
+#pragma unroll
+      for (int q = 0; q < 4; q++)
+        if ((j & 3u) == (uint32_t)q) part[a][q] += v;
+    }
+  }
+#pragma unroll
+  for (int a = 0; a < 2; a++)
+#pragma unroll
+    for (int q = 0; q < 4; q++)
+      if (part[a][q]) atomicAdd(&lane[a][q], part[a][q]);
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const int32_t div = (int32_t)c->lvl_div[sfi];
+    int32_t avg[2] = {0, 0};
+    uint32_t cum[4] = {0, 0, 0, 0};
+    for (uint32_t a = 0; a < c->nb_rx; a++) {
+      for (int q = 0; q < 4; q++) cum[q] += lane[a][q];      /* avg128D is not reset per antenna */
+      avg[a] = (int32_t)cum[0] / div + (int32_t)cum[1] / div + (int32_t)cum[2] / div + (int32_t)cum[3] / div;
+    }
+    const int32_t m = avg[0] > avg[1] ? avg[0] : avg[1];     /* cmax(avg[0], avg[1]); avg[1] = 0 with one antenna */
+    const uint32_t x = (uint32_t)m;
+    const int32_t l2 = x ? 32 - (int32_t)__clz(x & 0x7FFFFFFFu) : 0;   /* log2_approx (bits 0..30) */
+    const int32_t v = l2 - 13 + c->mu_off;
+    shift[sf] = (uint8_t)(v > 0 ? v : 0);
+  }
+}
+
+template <int QM>
+__global__ void __launch_bounds__(256) k_rx_llr_tm3(const rx_dev_t *__restrict__ c, const int32_t *__restrict__ rxF,
+                                                    const int32_t *__restrict__ est, size_t plane,
+                                                    int16_t *__restrict__ llr, const uint8_t *__restrict__ shift,
+                                                    int unscramble)
+{
+  const uint32_t sf = blockIdx.y, k = blockIdx.x, sfi = (c->first_sf + sf * c->sf_step) % 10;
+  const uint32_t l = c->npdcch + k, len = c->len[sfi][k], nb_rx = c->nb_rx, NS = c->nsymb * c->N;
+  rg32_t *map = (rg32_t *)(c->map + c->map_off[sfi][k]);
+  const size_t eo = ((size_t)sf * c->nsymb + l) * c->N;
+  int16_t *out = llr + (size_t)sf * c->llr_stride + c->llr_off[sfi][k];
+  const uint32_t sh = shift[sf], base = c->llr_off[sfi][k];
+  rg32_t *gold = (rg32_t *)(c->gold + (size_t)sfi * c->gold_words);
+  const int16_t a1 = c->a1, a2 = c->a2;
+  uint32_t mw[RX_R];
+#pragma unroll
+  for (int r = 0; r < RX_R; r++) {
+    const uint32_t j = threadIdx.x + 256 * r;
+    mw[r] = j < len ? map[j] : 0u;
+  }
+  uint32_t yv[2][RX_R], h0[2][RX_R], h1[2][RX_R];
+#pragma unroll
+  for (uint32_t a = 0; a < 2; a++)
+#pragma unroll
+    for (int r = 0; r < RX_R; r++) {
+      const uint32_t aa = a < nb_rx ? a : 0u;
+      const size_t yo = ((size_t)sf * nb_rx + aa) * NS + (size_t)l * c->N;
+      yv[a][r] = (uint32_t)rxF[yo + (mw[r] & 0xFFFFu)];
+      h0[a][r] = (uint32_t)est[aa * plane + eo + (mw[r] >> 16)];
+      h1[a][r] = (uint32_t)est[(2 + aa) * plane + eo + (mw[r] >> 16)];
+    }
+#pragma unroll
+  for (int r = 0; r < RX_R; r++) {
+    const uint32_t j = threadIdx.x + 256 * r;
+    if (j >= len) break;
+    int16_t cr[2], ci[2], mg[2], mgb[2];
+#pragma unroll
+    for (uint32_t a = 0; a < 2; a++) {
+      const uint32_t p = rx_prec_tm3(h0[a][r], h1[a][r], (j & 1u) != 0);
+      const int16_t hr = (int16_t)p, hi = (int16_t)(p >> 16), yr = (int16_t)yv[a][r], yi = (int16_t)(yv[a][r] >> 16);
+      const int16_t nhi = (int16_t)(-(int32_t)hi);
+      cr[a] = rx_sat16(rx_madd(hr, yr, hi, yi) >> sh);
+      ci[a] = rx_sat16(rx_madd(nhi, yr, hr, yi) >> sh);
+      const int16_t m = rx_sat16(rx_madd(hr, hr, hi, hi) >> sh);
+      mg[a] = (int16_t)((((int32_t)m * a1) >> 16) << 1);
+      mgb[a] = (int16_t)((((int32_t)m * a2) >> 16) << 1);
+    }
+    if (nb_rx > 1) {                                          /* dlsch_detection_mrc */
+      cr[0] = rx_sat16((cr[0] >> 1) + (cr[1] >> 1));
+      ci[0] = rx_sat16((ci[0] >> 1) + (ci[1] >> 1));
+      mg[0] = rx_sat16((mg[0] >> 1) + (mg[1] >> 1));
+      mgb[0] = rx_sat16((mgb[0] >> 1) + (mgb[1] >> 1));
+    }
+    int16_t v[6];
+    rx_llr_values<QM>(cr[0], ci[0], mg[0], mgb[0], v);
+    rx_llr_store<QM>(v, unscramble ? gold : nullptr, base + j * QM, out + QM * j);
+  }
+}
+
+hipError_t oai4g_launch_rx_tm3(const rx_dev_t *d_cfg, const rx_dev_t *h_cfg, int n_sf, const int32_t *d_rxF,
+                               const int32_t *d_est, size_t plane, int16_t *d_llr, uint8_t *d_shift, int unscramble,
+                               hipStream_t s)
+{
+  if (n_sf <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_rx_level_tm3, dim3(n_sf), dim3(256), 0, s, d_cfg, d_est, plane, d_shift);
+  const dim3 g(h_cfg->n_sym, n_sf), b(256);
+  if (h_cfg->Qm == 4)
+    hipLaunchKernelGGL(k_rx_llr_tm3<4>, g, b, 0, s, d_cfg, d_rxF, d_est, plane, d_llr, d_shift, unscramble);
+  else
+    hipLaunchKernelGGL(k_rx_llr_tm3<6>, g, b, 0, s, d_cfg, d_rxF, d_est, plane, d_llr, d_shift, unscramble);
+  return hipGetLastError();
+}
+
 /* dlsch_unscrambling drop-in: llr[k] *= 2 c(k) - 1 (int16), c = the words of the Gold sequence */
 __global__ void __launch_bounds__(256) k_rx_unscramble(int16_t *__restrict__ llr, const uint32_t *__restrict__ c,
                                                        uint32_t n)

@@ -25,28 +25,11 @@ static __device__ __forceinline__ uint32_t rx_h2(uint32_t h)
   return (uint32_t)rx_madd((int16_t)h, (int16_t)h, (int16_t)(h >> 16), (int16_t)(h >> 16));
 }
 
-/* the Qm LLRs of one RE (estimate hv, received yv), unscrambled with the Gold bits starting at
- * stream position b when gold != nullptr, stored at out (one 4 / 8 / 12-byte store) */
+/* unscramble (when gold != nullptr, Gold bits from stream position b) and store one RE's Qm LLRs
+ * at out (one 4 / 8 / 12-byte store) */
 template <int QM>
-static __device__ __forceinline__ void rx_re_llr(uint32_t hv, uint32_t yv, uint32_t sh, int16_t a1, int16_t a2,
-                                                 rg32_t *__restrict__ gold, uint32_t b, int16_t *out)
+static __device__ __forceinline__ void rx_llr_store(int16_t *v, rg32_t *__restrict__ gold, uint32_t b, int16_t *out)
 {
-  const int16_t hr = (int16_t)hv, hi = (int16_t)(hv >> 16), yr = (int16_t)yv, yi = (int16_t)(yv >> 16);
-  const int16_t nhi = (int16_t)(-(int32_t)hi);
-  int16_t v[6];
-  v[0] = rx_sat16(rx_madd(hr, yr, hi, yi) >> sh);
-  v[1] = rx_sat16(rx_madd(nhi, yr, hr, yi) >> sh);
-  if (QM > 2) {
-    const int16_t mg = rx_sat16(rx_madd(hr, hr, hi, hi) >> sh);
-    const int16_t mag = (int16_t)((((int32_t)mg * a1) >> 16) << 1);
-    v[2] = rx_sat16((int32_t)mag - rx_abs16(v[0]));
-    v[3] = rx_sat16((int32_t)mag - rx_abs16(v[1]));
-    if (QM > 4) {
-      const int16_t magb = (int16_t)((((int32_t)mg * a2) >> 16) << 1);
-      v[4] = rx_sat16((int32_t)magb - rx_abs16(v[2]));
-      v[5] = rx_sat16((int32_t)magb - rx_abs16(v[3]));
-    }
-  }
   if (gold) {                                    /* llr * (2 c - 1), int16 */
     const uint32_t w = b >> 5;
     const uint64_t win = ((uint64_t)gold[w] | ((uint64_t)gold[w + 1] << 32)) >> (b & 31);
@@ -67,6 +50,53 @@ static __device__ __forceinline__ void rx_re_llr(uint32_t hv, uint32_t yv, uint3
     o[1] = pk[1];
     o[2] = pk[2];
   }
+}
+
+/* dlsch_qpsk/16qam/64qam_llr of one compensated RE (cr, ci) with magnitudes mag / magb */
+template <int QM>
+static __device__ __forceinline__ void rx_llr_values(int16_t cr, int16_t ci, int16_t mag, int16_t magb, int16_t *v)
+{
+  v[0] = cr;
+  v[1] = ci;
+  if (QM > 2) {
+    v[2] = rx_sat16((int32_t)mag - rx_abs16(v[0]));
+    v[3] = rx_sat16((int32_t)mag - rx_abs16(v[1]));
+    if (QM > 4) {
+      v[4] = rx_sat16((int32_t)magb - rx_abs16(v[2]));
+      v[5] = rx_sat16((int32_t)magb - rx_abs16(v[3]));
+    }
+  }
+}
+
+/* the Qm LLRs of one RE (estimate hv, received yv), unscrambled with the Gold bits starting at
+ * stream position b when gold != nullptr, stored at out (one 4 / 8 / 12-byte store) */
+template <int QM>
+static __device__ __forceinline__ void rx_re_llr(uint32_t hv, uint32_t yv, uint32_t sh, int16_t a1, int16_t a2,
+                                                 rg32_t *__restrict__ gold, uint32_t b, int16_t *out)
+{
+  const int16_t hr = (int16_t)hv, hi = (int16_t)(hv >> 16), yr = (int16_t)yv, yi = (int16_t)(yv >> 16);
+  const int16_t nhi = (int16_t)(-(int32_t)hi);
+  int16_t v[6];
+  const int16_t cr = rx_sat16(rx_madd(hr, yr, hi, yi) >> sh), ci = rx_sat16(rx_madd(nhi, yr, hr, yi) >> sh);
+  int16_t mag = 0, magb = 0;
+  if (QM > 2) {
+    const int16_t mg = rx_sat16(rx_madd(hr, hr, hi, hi) >> sh);
+    mag = (int16_t)((((int32_t)mg * a1) >> 16) << 1);
+    magb = (int16_t)((((int32_t)mg * a2) >> 16) << 1);
+  }
+  rx_llr_values<QM>(cr, ci, mag, magb, v);
+  rx_llr_store<QM>(v, gold, b, out);
+}
+
+/* prec2A_TM3_128 (dlsch_demodulation.c:1364-1396) on one RE: the stream-0 channel
+ * (h0 + s h1) >> 1 per component, adds_epi16 then srai; s h1 by sign_epi16 (int16 wrap) */
+static __device__ __forceinline__ uint32_t rx_prec_tm3(uint32_t h0, uint32_t h1, bool neg)
+{
+  const int16_t b0 = neg ? (int16_t)(-(int32_t)(int16_t)h1) : (int16_t)h1;
+  const int16_t b1 = neg ? (int16_t)(-(int32_t)(int16_t)(h1 >> 16)) : (int16_t)(h1 >> 16);
+  const int16_t r = (int16_t)(rx_sat16((int32_t)(int16_t)h0 + b0) >> 1);
+  const int16_t i = (int16_t)(rx_sat16((int32_t)(int16_t)(h0 >> 16) + b1) >> 1);
+  return (uint32_t)(uint16_t)r | ((uint32_t)(uint16_t)i << 16);
 }
 
 /* log2_approx(avg) / 2 of dlsch_channel_level (log2_approx: bits 0..30) */

@@ -72,7 +72,7 @@ class DlsimBler:
         _check(bool(self.d_tail) and bool(self.d_lev))
         _check(L.oai4g_memcpy_h2d(self.d_tail, _ptr(tail), tail.nbytes) == 0)
         self.ce = ChestBatch(self.fp, batch, first_subframe=subframe, subframe_step=0)
-        _check(L.oai4g_chest_config_set_stride(self.ce.cfg, 2) == 0)
+        _check(L.oai4g_chest_config_set_stride(self.ce.cfg, 2, 1) == 0)
         self.rx = RxBatch(self.fp, list(FULL_ALLOC[N_RB_DL]), self.Qm, num_pdcch_symbols, rnti, batch,
                           first_subframe=subframe, subframe_step=0)
         self.G = self.rx.llr_count(subframe)

@@ -238,3 +238,228 @@ void orc_dlsch_unscrambling(int16_t *llr, int G, uint32_t c_init)
     s = orc_gold_generic(&x1, &x2, 0);
   }
 }
+
+/* ======================================================================================
+ * TM3 (LARGE_CDD, 2 TX ports), nb_rx receive antennas: rx_pdsch with dual_stream_flag = 0
+ * (dlsim's TM3 UE), dlsch_demodulation.c:82-800:
+ *   dlsch_extract_rbs_dual      :3683-4056 (PBCH / PSS / SSS RBs dropped, 8 REs per RB in pilot
+ *                               symbols; odd N_RB_DL: the RB around DC, whose non-pilot second half
+ *                               is read from bins 0..5, and the skip_half = 2 pilot branch whose
+ *                               pointers advance inside the RE loop — all as written)
+ *   dlsch_channel_level_TM3     :2902-2981 (precoded stream-0 |h|^2 per register lane, int32 wrap,
+ *                               accumulated over the receive antennas without reset, per-lane
+ *                               division, max of the per-antenna values)
+ *   log2_maxh                   :390-394 (log2_approx(avg) - 13 + offset_mumimo_llr_drange[mcs0]
+ *                               [Qm1 / 2 - 1], >= 0; the active table :76)
+ *   prec2A_TM3_128              :1364-1396 (h0' = sat(h0 + s h1) >> 1, h1' = sat(h0 - s h1) >> 1,
+ *                               s = +1, -1 alternating per extracted RE, sign_epi16 wrap)
+ *   dlsch_channel_compensation_TM3 :1846-2120 (magnitudes and matched filters per antenna)
+ *   dlsch_detection_mrc         :2583-2718 (stream 0 and its magnitudes: (a >> 1) +sat (b >> 1))
+ *   dlsch_qpsk / 16qam / 64qam_llr of stream 0 (:583-800; qpsk with Qm1 = 2 is the interference-
+ *                               aware qpsk_qpsk and is not restated: refused)
+ * Codeword 1 is not demodulated in this mode (the reference computes llr[1] only for Qm0 = Qm1
+ * = 2).  Even N_RB_DL and odd.
+ * ==================================================================================== */
+static const uint8_t mumimo_off[29][3] = {{0, 6, 5}, {0, 4, 5}, {0, 4, 5}, {0, 5, 4}, {0, 5, 6}, {0, 5, 3}, {0, 4, 4},
+                                          {0, 4, 4}, {0, 3, 3}, {0, 1, 2}, {1, 1, 0}, {1, 3, 2}, {3, 4, 1}, {2, 0, 0},
+                                          {2, 2, 2}, {1, 1, 1}, {2, 1, 0}, {2, 1, 1}, {1, 0, 1}, {1, 0, 1}, {0, 0, 0},
+                                          {1, 0, 0}, {0, 0, 0}, {0, 1, 0}, {1, 0, 0}, {0, 0, 0}, {0, 0, 0}, {0, 0, 0},
+                                          {0, 0, 0}};
+
+/* one antenna's dual extraction of one symbol into ext slots (literal pointer arithmetic); returns
+ * the final pointer, *hw the slots written, *nb_rb the allocated RBs counted once */
+static int extract_dual(const orc_frame_t *fp, const int32_t *rxF_sym, const int32_t *ch0_sym, const int32_t *ch1_sym,
+                        const uint32_t rb_alloc[4], uint8_t symbol, uint8_t subframe, int32_t *rx_ext, int32_t *c0_ext,
+                        int32_t *c1_ext, int *nb_rb, int *hw)
+{
+  const int symbol_mod = symbol >= 7 - fp->Ncp ? symbol - (7 - fp->Ncp) : symbol;
+  const int pilots = symbol_mod == 0 || symbol_mod == 4 - fp->Ncp;
+  const int nsymb = fp->Ncp == 0 ? 14 : 12, l = symbol, half = fp->N_RB_DL >> 1, ns = fp->nushift;
+  const int sss_symb = fp->frame_type == 1 ? nsymb - 1 : (nsymb >> 1) - 2;
+  const int pss_symb = fp->frame_type == 1 ? 2 : (nsymb >> 1) - 1;
+  int p = 0;                                                   /* the ext pointer (slot index) */
+  *nb_rb = 0;
+  *hw = 0;
+#define PUT(pos, bin, col)                                                              \
+  do {                                                                                  \
+    rx_ext[pos] = rxF_sym[bin];                                                         \
+    c0_ext[pos] = ch0_sym[5 + (col)];                                                   \
+    c1_ext[pos] = ch1_sym[5 + (col)];                                                   \
+    if ((pos) + 1 > *hw) *hw = (pos) + 1;                                               \
+  } while (0)
+  for (int prb = 0; prb < fp->N_RB_DL; prb++) {
+    int ind = alloc_bit(rb_alloc, prb), skip_half = 0;
+    if (subframe == 0 && prb > half - 3 && prb < half + 3 && l >= (nsymb >> 1) && l < (nsymb >> 1) + 4) ind = 0;
+    if ((subframe == 0 || subframe == 5) && prb > half - 3 && prb < half + 3 && l == sss_symb) ind = 0;
+    if (fp->frame_type == 0 && (subframe == 0 || subframe == 5) && prb > half - 3 && prb < half + 3 && l == pss_symb) ind = 0;
+    if (fp->frame_type == 1 && subframe == 6 && prb >= half - 3 && prb <= half + 3 && l == pss_symb) ind = 0;
+    if (!ind) continue;
+    const int col0 = 12 * prb;
+    if ((fp->N_RB_DL & 1) == 0) {
+      const int b0 = prb < half ? fp->first_carrier_offset + 12 * prb : 1 + 12 * (prb - half);
+      if (!pilots) {
+        for (int i = 0; i < 12; i++) PUT(p + i, b0 + i, col0 + i);
+        p += 12;
+      } else {
+        int j = 0;
+        for (int i = 0; i < 12; i++)
+          if (i != ns && i != ns + 3 && i != ns + 6 && i != (ns + 9) % 12) { PUT(p + j, b0 + i, col0 + i); j++; }
+        p += 8;
+      }
+      (*nb_rb)++;
+      continue;
+    }
+    /* odd N_RB_DL */
+    if (subframe == 0 && prb == half - 3 && l >= (nsymb >> 1) && l < (nsymb >> 1) + 4) skip_half = 1;
+    else if (subframe == 0 && prb == half + 3 && l >= (nsymb >> 1) && l < (nsymb >> 1) + 4) skip_half = 2;
+    if ((subframe == 0 || subframe == 5) && prb == half - 3 && l == sss_symb) skip_half = 1;
+    else if ((subframe == 0 || subframe == 5) && prb == half + 3 && l == sss_symb) skip_half = 2;
+    if ((fp->frame_type == 0 && (subframe == 0 || subframe == 5)) || (fp->frame_type == 1 && (subframe == 2 || subframe == 6))) {
+      if (prb == half - 3 && l == pss_symb) skip_half = 1;
+      else if ((subframe == 0 || subframe == 5) && prb == half + 3 && l == pss_symb) skip_half = 2;
+    }
+    const int b0 = prb <= half ? fp->first_carrier_offset + 12 * prb : 7 + 12 * (prb - half - 1);
+    if (prb != half) {
+      if (!pilots) {
+        const int o = skip_half == 2 ? 6 : 0, n = skip_half ? 6 : 12;
+        for (int i = 0; i < n; i++) PUT(p + i, b0 + o + i, col0 + o + i);
+        p += n;
+      } else if (skip_half == 1) {
+        int j = 0;
+        for (int i = 0; i < 6; i++)
+          if (i != ns && i != (ns + 3) % 6) { PUT(p + j, b0 + i, col0 + i); j++; }
+        p += 4;
+      } else if (skip_half == 2) {
+        int j = 0;
+        for (int i = 0; i < 6; i++) {
+          if (i != ns && i != (ns + 3) % 6) { PUT(p + j, b0 + i + 6, col0 + i + 6); j++; }
+          p += 4;                                            /* inside the loop, as written (:3961-3963) */
+        }
+      } else {
+        int j = 0;
+        for (int i = 0; i < 12; i++)
+          if (i != ns && i != ns + 3 && i != ns + 6 && i != (ns + 9) % 12) { PUT(p + j, b0 + i, col0 + i); j++; }
+        p += 8;
+      }
+    } else {                                                   /* the RB around DC */
+      if (!pilots) {
+        for (int i = 0; i < 6; i++) PUT(p + i, b0 + i, col0 + i);
+        for (int i = 0; i < 6; i++) PUT(p + 6 + i, i, col0 + 6 + i);   /* bins 0..5 (:4003-4007) */
+        p += 12;
+      } else {
+        int j = 0, i = 0;
+        for (; i < 6; i++)
+          if (i != ns && i != (ns + 3) % 6) { PUT(p + j, b0 + i, col0 + i); j++; }
+        for (; i < 12; i++)
+          if (i != (ns + 6) % 12 && i != (ns + 9) % 12) { PUT(p + j, 1 + i - 6, col0 + i); j++; }
+        p += 8;
+      }
+    }
+    (*nb_rb)++;
+  }
+#undef PUT
+  return p;
+}
+
+static int16_t sgn16(int16_t x, int s) { return s < 0 ? (int16_t)(uint16_t)(0u - (uint16_t)x) : x; }   /* sign_epi16 */
+
+int orc_rx_pdsch_tm3(const orc_frame_t *fp, int nb_rx, const int32_t *const *rxdataF, const int32_t *const *est,
+                     const uint32_t rb_alloc[4], uint8_t Qm0, uint8_t Qm1, uint8_t mcs0, uint8_t num_pdcch_symbols,
+                     uint8_t subframe, int16_t *llr, uint8_t *log2_maxh_out)
+{
+  /* rxdataF[a] = [nsymb][N] of receive antenna a; est[p * 2 + a] = dl_ch_estimates[(p << 1) + a] */
+  if (nb_rx < 1 || nb_rx > 2 || (Qm0 != 4 && Qm0 != 6) || (Qm1 != 2 && Qm1 != 4 && Qm1 != 6) || mcs0 > 28) return -1;
+  const int N = fp->ofdm_symbol_size, nsymb = fp->Ncp == 0 ? 14 : 12;
+  const size_t X = 12 * 110 + 64;
+  int32_t *rx_ext = (int32_t *)calloc(2 * X, 4), *c0 = (int32_t *)calloc(2 * X, 4), *c1 = (int32_t *)calloc(2 * X, 4);
+  int16_t *comp = (int16_t *)calloc(2 * X * 2, 2), *mag = (int16_t *)calloc(2 * X, 2), *magb = (int16_t *)calloc(2 * X, 2);
+  int16_t *out = llr;
+  uint8_t log2_maxh = 0;
+  const int16_t a1 = Qm0 == 4 ? QAM16_n1 : QAM64_n1, a2 = Qm0 == 4 ? 0 : QAM64_n2;
+  for (int symbol = num_pdcch_symbols; symbol < nsymb && out; symbol++) {
+    int nb_rb = 0, hw[2] = {0, 0}, ptr[2] = {0, 0};
+    for (int a = 0; a < nb_rx; a++)
+      ptr[a] = extract_dual(fp, rxdataF[a] + symbol * N, est[a] + symbol * N, est[2 + a] + symbol * N, rb_alloc,
+                            (uint8_t)symbol, subframe, rx_ext + a * X, c0 + a * X, c1 + a * X, &nb_rb, &hw[a]);
+    (void)ptr;
+    const int symbol_mod = symbol >= 7 - fp->Ncp ? symbol - (7 - fp->Ncp) : symbol;
+    const int pil = symbol_mod == 0 || symbol_mod == 4 - fp->Ncp;
+    const int nre_rb = pil ? 8 : 12;
+    if (nb_rb == 0) { out = NULL; break; }
+    if (symbol == num_pdcch_symbols) {
+      /* dlsch_channel_level_TM3: symbol_mod == 0 only (the 4-Ncp test is written Ncp-1) takes 8 */
+      const int nre = symbol_mod == 0 ? 8 : 12;
+      if (hw[0] < nb_rb * nre) { out = NULL; break; }      /* would read unwritten ext slots */
+      uint32_t lane[4] = {0, 0, 0, 0};
+      int32_t avg[2] = {0, 0};
+      for (int a = 0; a < nb_rx; a++) {
+        for (int rb = 0; rb < nb_rb; rb++)
+          for (int r = 0; r < (nre == 8 ? 2 : 3); r++)
+            for (int k = 0; k < 4; k++) {
+              const int e = rb * nre + 4 * r + k;            /* ext slot of this register lane */
+              int16_t h0[2], h1[2];
+              memcpy(h0, &c0[a * X + e], 4);
+              memcpy(h1, &c1[a * X + e], 4);
+              const int s = (k & 1) ? -1 : 1;
+              int16_t p0[2];
+              for (int c = 0; c < 2; c++) p0[c] = (int16_t)(sat16((int32_t)h0[c] + sgn16(h1[c], s)) >> 1);
+              lane[k] += (uint32_t)((int32_t)p0[0] * p0[0]) + (uint32_t)((int32_t)p0[1] * p0[1]);
+            }
+        const int div = nb_rb * nre;
+        avg[a] = (int32_t)lane[0] / div + (int32_t)lane[1] / div + (int32_t)lane[2] / div + (int32_t)lane[3] / div;
+      }
+      const int32_t avg0 = nb_rx > 1 ? (avg[0] > avg[1] ? avg[0] : avg[1]) : (avg[0] > 0 ? avg[0] : 0);  /* cmax(avg[0], avg[1]), avg[1] = 0 with 1 RX */
+      const int v = (int)orc_log2_approx((uint32_t)avg0) - 13 + mumimo_off[mcs0][(Qm1 >> 1) - 1];
+      log2_maxh = (uint8_t)(v > 0 ? v : 0);
+    }
+    /* precoding, magnitudes, matched filter per antenna (ext slots [0, nb_rb * nre_rb)) */
+    const int n = nb_rb * nre_rb;
+    for (int a = 0; a < nb_rx; a++)
+      for (int e = 0; e < n; e++) {
+        int16_t h0[2], h1[2], y[2];
+        memcpy(h0, &c0[a * X + e], 4);
+        memcpy(h1, &c1[a * X + e], 4);
+        memcpy(y, &rx_ext[a * X + e], 4);
+        const int s = (e & 1) ? -1 : 1;
+        int16_t p0[2];
+        for (int c = 0; c < 2; c++) p0[c] = (int16_t)(sat16((int32_t)h0[c] + sgn16(h1[c], s)) >> 1);
+        const int16_t m = sat16((int32_t)((uint32_t)((int32_t)p0[0] * p0[0]) + (uint32_t)((int32_t)p0[1] * p0[1])) >> log2_maxh);
+        mag[a * X + e] = mulhi2(m, a1);
+        magb[a * X + e] = mulhi2(m, a2);
+        const int16_t nhi = (int16_t)-p0[1];                 /* sign_epi16 by the conjugate mask */
+        comp[(a * X + e) * 2] = sat16((int32_t)((uint32_t)((int32_t)p0[0] * y[0]) + (uint32_t)((int32_t)p0[1] * y[1])) >> log2_maxh);
+        comp[(a * X + e) * 2 + 1] = sat16((int32_t)((uint32_t)((int32_t)nhi * y[0]) + (uint32_t)((int32_t)p0[0] * y[1])) >> log2_maxh);
+      }
+    if (nb_rx > 1)                                           /* dlsch_detection_mrc, stream 0 */
+      for (int e = 0; e < n; e++) {
+        for (int c = 0; c < 2; c++)
+          comp[e * 2 + c] = sat16((comp[e * 2 + c] >> 1) + (comp[(X + e) * 2 + c] >> 1));
+        mag[e] = sat16((mag[e] >> 1) + (mag[X + e] >> 1));
+        magb[e] = sat16((magb[e] >> 1) + (magb[X + e] >> 1));
+      }
+    const int len = pil ? nb_rb * 8 - 2 * orc_adjust_G2(fp, rb_alloc, subframe, (uint8_t)symbol) / 3
+                        : nb_rb * 12 - orc_adjust_G2(fp, rb_alloc, subframe, (uint8_t)symbol);
+    if (len > hw[0]) { out = NULL; break; }
+    for (int j = 0; j < len; j++) {
+      const int16_t cr = comp[j * 2], ci = comp[j * 2 + 1];
+      const int16_t x1r = sat16((int32_t)mag[j] - abs16(cr)), x1i = sat16((int32_t)mag[j] - abs16(ci));
+      *out++ = cr;
+      *out++ = ci;
+      *out++ = x1r;
+      *out++ = x1i;
+      if (Qm0 == 6) {
+        *out++ = sat16((int32_t)magb[j] - abs16(x1r));
+        *out++ = sat16((int32_t)magb[j] - abs16(x1i));
+      }
+    }
+  }
+  free(rx_ext);
+  free(c0);
+  free(c1);
+  free(comp);
+  free(mag);
+  free(magb);
+  if (!out) return -1;
+  if (log2_maxh_out) *log2_maxh_out = log2_maxh;
+  return (int)(out - llr);
+}

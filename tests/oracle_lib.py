@@ -585,3 +585,23 @@ def turbo_decode8(y, K, max_it=8, crc_type=0, F=0):
     orc().orc_turbo_decoder8.restype = ctypes.c_uint8
     it = orc().orc_turbo_decoder8(P(buf), P(out), K, max_it, crc_type, F)
     return it, out[:K // 8]
+
+
+def rx_pdsch_tm3(fp, rxF, est, rb_alloc, Qm0, Qm1, mcs0, num_pdcch, subframe):
+    """orc_rx_pdsch_tm3: rxF = [nb_rx][nsymb*N], est[(p, a)] = [nsymb*N] estimates of port p at RX a.
+    Returns (codeword-0 LLRs, log2_maxh)."""
+    nb_rx = len(rxF)
+    rx = [np.ascontiguousarray(r, dtype=np.int32) for r in rxF]
+    keep = {k: np.ascontiguousarray(v, dtype=np.int32) for k, v in est.items()}
+    ep = (ctypes.c_void_p * 4)()
+    for (p_, a), arr in keep.items():
+        if a < nb_rx:
+            ep[2 * p_ + a] = arr.ctypes.data
+    rp = (ctypes.c_void_p * 2)(*[r.ctypes.data for r in rx] + [None] * (2 - nb_rx))
+    out = np.zeros(14 * 1200 * 6 + 64, dtype=np.int16)
+    sh = ctypes.c_uint8()
+    ra = (ctypes.c_uint32 * 4)(*rb_alloc)
+    n = orc().orc_rx_pdsch_tm3(ctypes.byref(fp), nb_rx, rp, ep, ra, Qm0, Qm1, mcs0, num_pdcch, subframe, P(out),
+                               ctypes.byref(sh))
+    assert n >= 0
+    return out[:n], sh.value

@@ -1,0 +1,78 @@
+"""GPU parity of the TM3 (LARGE_CDD, 2 TX ports) receive chain — dlsch_extract_rbs_dual,
+dlsch_channel_level_TM3, prec2A_TM3 + dlsch_channel_compensation_TM3, dlsch_detection_mrc, the
+codeword-0 LLRs (k_rx_level_tm3 / k_rx_llr_tm3) — against the oracle restatement
+(tests/test_rx_tm3_cpu.py pins it by the decoding loop): the drop-in on full-range random grids and
+estimates (saturation / wrap paths, 1 and 2 receive antennas, odd N_RB_DL with the PBCH / sync
+subframes), and the headline configuration's receive loop on the GPU: C3 TxPipeline (both ports'
+CRS) -> channel H = I -> FepBatch over 2 antennas -> 4 channel-estimation batches -> RxBatchTM3 ->
+RM-rx / deinterleaving / turbo decoding: codeword 0 comes back, LLRs bit-exact vs the oracle."""
+import numpy as np
+import pytest
+
+import oracle_lib as O
+from test_rx_cpu import alloc, decode_tb
+from test_rx_tm3_cpu import c3_params
+
+pytestmark = pytest.mark.gpu
+
+RAND = [(100, 6, 6, 19, 1, 7, 2, None), (50, 4, 2, 12, 2, 3, 2, None), (100, 6, 4, 22, 3, 0, 2, None),
+        (25, 6, 6, 19, 1, 0, 2, None), (25, 4, 4, 14, 2, 5, 1, None), (15, 6, 6, 20, 1, 0, 2, None),
+        (100, 4, 6, 10, 2, 8, 1, [0xF0F0F0F0, 0x0000FFFF, 0, 0x3])]
+
+
+@pytest.mark.parametrize("N_RB,Qm0,Qm1,mcs,npd,sf,nb_rx,ra", RAND)
+def test_gpu_tm3_random_inputs(gpu, N_RB, Qm0, Qm1, mcs, npd, sf, nb_rx, ra):
+    ra = ra or alloc(N_RB)
+    fo = O.frame(N_RB, Nid_cell=N_RB + sf, nb_antennas_tx=2, mode1_flag=0)
+    fg = gpu.frame_parms(N_RB, Nid_cell=N_RB + sf, nb_antennas_tx=2, mode1_flag=0)
+    n = fo.symbols_per_tti * fo.ofdm_symbol_size
+    rng = np.random.default_rng(N_RB * 7 + Qm0 + sf)
+    for scale in (2 ** 31 - 1, 3000):
+        rx = [rng.integers(-scale, scale, n, dtype=np.int64).astype(np.int32) for _ in range(nb_rx)]
+        est = {(p, a): rng.integers(-scale, scale, n, dtype=np.int64).astype(np.int32) for p in (0, 1)
+               for a in range(nb_rx)}
+        lo, so = O.rx_pdsch_tm3(fo, rx, est, ra, Qm0, Qm1, mcs, npd, sf)
+        lg, sg = gpu.rx_pdsch_tm3(fg, rx, est, ra, Qm0, Qm1, mcs, npd, sf)
+        assert sg == so and np.array_equal(lg, lo), (scale, so, sg)
+
+
+@pytest.mark.parametrize("N_RB,mcs,npd,sf", [(100, 19, 1, 7), (100, 16, 2, 3), (50, 19, 1, 8)])
+def test_gpu_tm3_receive_loop(gpu, N_RB, mcs, npd, sf):
+    n_tx, n_sf = 3, 2
+    p = c3_params(N_RB, mcs, npd, sf)
+    p.subframe_step = 1
+    pipe = gpu.TxPipeline(p, n_tx)
+    rng = np.random.default_rng(mcs + N_RB)
+    pay = rng.integers(0, 256, size=(n_tx, 2, p.payload_stride), dtype=np.uint8)
+    pipe.upload_payload(pay)
+    pipe.run()
+    pipe.sync()
+    iq = pipe.iq()                                      # [n_tx][2 antennas][spt]: H = I, RX a <- TX a
+    fg = gpu.frame_parms(N_RB, nb_antennas_tx=2, mode1_flag=0)
+    fep = gpu.FepBatch(fg, n_tx, 2)
+    fep.upload(iq)
+    fep.run()
+    Qm = 4 if mcs < 17 else 6
+    rx = gpu.RxBatchTM3(fg, alloc(N_RB), Qm, Qm, mcs, npd, p.rnti, n_sf, nb_rx=2, first_subframe=sf)
+    rx.estimate(fep.d_rxF, first_subframe=sf)
+    rx.launch(fep.d_rxF, unscramble=1)
+    llr = rx.llrs()
+    rxF = fep.result()                                   # [n_tx][2][nsymb][N]
+    N = fg.ofdm_symbol_size
+    fo = O.frame(N_RB, nb_antennas_tx=2, mode1_flag=0)
+    for i in range(n_sf):
+        s = (sf + i) % 10
+        est = {(pp, a): O.chest_subframe(fo, rxF[i, a].ravel(), rxF[i + 1, a, 0], s, p=pp) for pp in (0, 1)
+               for a in (0, 1)}
+        lo, _ = O.rx_pdsch_tm3(fo, [rxF[i, 0].ravel(), rxF[i, 1].ravel()], est, alloc(N_RB), Qm, Qm, mcs, npd, s)
+        G = rx.llr_count(s)
+        u = np.zeros(32 * (1 + G // 32), np.int16)
+        u[:G] = lo
+        O.dlsch_unscrambling(u, G, (p.rnti << 14) + (s << 9) + fo.Nid_cell)
+        assert len(lo) == G and np.array_equal(llr[i, :G], u[:G]), s
+        res, tb = decode_tb(llr[i, :G], G, p.TBS[0], Qm)
+        assert all(it <= 4 for it, _ in res), (s, [it for it, _ in res])
+        assert np.array_equal(tb, pay[i, 0, :p.TBS[0] // 8]), s
+    rx.close()
+    fep.close()
+    pipe.close()

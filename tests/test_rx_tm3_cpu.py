@@ -1,0 +1,94 @@
+"""TM3 (LARGE_CDD, 2 TX ports) receive chain on the oracle (oracle/oai_oracle_rx.c:
+orc_rx_pdsch_tm3 — dlsch_extract_rbs_dual, dlsch_channel_level_TM3, prec2A_TM3_128,
+dlsch_channel_compensation_TM3, dlsch_detection_mrc, the single-stream LLRs of codeword 0, as
+dlsim's TM3 UE runs rx_pdsch with dual_stream_flag = 0).  The reference translation units are
+unbuildable here (PHY/defs.h), so the restatement is pinned by the closed loop: the oracle's C3
+transmit subframe (2 antennas, both ports' CRS) -> per receive antenna slot_fep -> the estimates of
+ports 0 / 1 -> TM3 demodulation -> codeword 0's transport block comes back, over the channel
+H = I (each receive antenna sees one transmit antenna: the large-delay CDD precoding and the
+receiver's prec2A_TM3 + MRC then separate the two streams exactly), with 2 and with 1 receive
+antenna and the two-antenna MRC.  The LLR stream has exactly G entries."""
+import numpy as np
+import pytest
+
+import oracle_lib as O
+from test_rx_cpu import alloc, decode_tb
+
+
+def c3_params(N_RB, mcs, npdcch, sf, Nid=0):
+    import openair4g_amd as oai
+    return oai.make_params("C3", subframe=sf, N_RB_DL=N_RB, nb_rb=N_RB, rb_alloc=alloc(N_RB), mcs=[mcs, mcs], TBS=None,
+                           num_pdcch_symbols=npdcch, with_crs=1, Nid_cell=Nid)
+
+
+def tm3_loop(p, sf, pays, H, nb_rx=2):
+    """TX of subframes sf, sf + 1 (C3 with CRS) -> flat channel H[rx][tx] (int) -> per RX antenna the
+    FEP of subframe sf and symbol 0 of the next -> estimates of ports 0 / 1 -> orc_rx_pdsch_tm3."""
+    cfg = O.tx_cfg_from_params(p, sf)
+    fp = cfg.fp
+    spt, N = fp.samples_per_tti, fp.ofdm_symbol_size
+    frames = [np.zeros(10 * spt + N, np.int32) for _ in range(nb_rx)]
+    for d, pay in enumerate(pays):
+        s = (sf + d) % 10
+        txd, _, _ = O.tx_subframe(O.tx_cfg_from_params(p, s), [pay[0], pay[1]])
+        t16 = txd.view(np.int16).reshape(2, spt, 2).astype(np.int64)
+        for a in range(nb_rx):
+            r = H[a][0] * t16[0] + H[a][1] * t16[1]
+            frames[a][s * spt:(s + 1) * spt] = np.clip(r, -32768, 32767).astype(np.int16).reshape(-1).view(np.int32)
+    rxF, est = [], {}
+    for a in range(nb_rx):
+        g = np.zeros(15 * N, np.int32)
+        for Ns in (2 * sf, 2 * sf + 1):
+            for l in range(7):
+                assert O.slot_fep([frames[a]], [g], fp, l, Ns) == 0
+        nxt = np.zeros(15 * N, np.int32)
+        assert O.slot_fep([frames[a]], [nxt], fp, 0, (2 * sf + 2) % 20) == 0
+        rxF.append(g[:14 * N].copy())
+        for port in (0, 1):
+            est[(port, a)] = O.chest_subframe(fp, g[:14 * N].copy(), nxt[:N].copy(), sf, p=port)
+    return fp, rxF, est
+
+
+# (N_RB, mcs, PDCCH symbols, subframe, RX antennas).  One RX antenna: the channel [1, 1] (dlsim's AWGN
+# sum of the transmit antennas) carries stream 0 alone on every other RE (s = +1) and erases it on
+# the rest (h0' = 0): a low-rate 16-QAM codeword still decodes.
+CASES = [(100, 19, 1, 7, 2), (50, 16, 2, 3, 2), (100, 11, 3, 8, 1), (25, 19, 1, 7, 2), (100, 12, 1, 1, 2)]
+
+
+@pytest.mark.parametrize("N_RB,mcs,npdcch,sf,nb_rx", CASES)
+def test_tm3_loop_decodes_codeword0(N_RB, mcs, npdcch, sf, nb_rx):
+    p = c3_params(N_RB, mcs, npdcch, sf)
+    rng = np.random.default_rng(N_RB * mcs + sf)
+    pays = [[rng.integers(0, 256, p.payload_stride, dtype=np.uint8) for _ in range(2)] for _ in range(2)]
+    H = [[1, 0], [0, 1]] if nb_rx == 2 else [[1, 1]]
+    fp, rxF, est = tm3_loop(p, sf, pays, H, nb_rx)
+    Qm = 4 if mcs < 17 else 6
+    llr, sh = O.rx_pdsch_tm3(fp, rxF[:nb_rx], est, alloc(N_RB), Qm, Qm, mcs, npdcch, sf)
+    G = O.get_G(N_RB, 0, 0, 0, N_RB, alloc(N_RB), Qm, 1, npdcch, sf)
+    assert len(llr) == G
+    u = np.zeros(32 * (1 + G // 32), np.int16)
+    u[:G] = llr
+    O.dlsch_unscrambling(u, G, (p.rnti << 14) + (sf << 9) + fp.Nid_cell)
+    res, tb = decode_tb(u[:G], G, p.TBS[0], Qm)
+    assert all(it <= 4 for it, _ in res), [it for it, _ in res]
+    assert np.array_equal(tb, pays[0][0][:p.TBS[0] // 8])
+
+
+def test_tm3_rejects_qpsk_and_reports_garbage_free_lengths():
+    fp = O.frame(50, nb_antennas_tx=2, mode1_flag=0)
+    N = fp.ofdm_symbol_size
+    rng = np.random.default_rng(1)
+    rx = [rng.integers(-3000, 3000, 14 * N).astype(np.int32) for _ in range(2)]
+    est = {(pp, a): rng.integers(-3000, 3000, 14 * N).astype(np.int32) for pp in (0, 1) for a in (0, 1)}
+    import ctypes
+    out = np.zeros(14 * 1200 * 6, np.int16)
+    rp = (ctypes.c_void_p * 2)(*[r.ctypes.data for r in rx])
+    ep = (ctypes.c_void_p * 4)(*[est[(pp, a)].ctypes.data for pp in (0, 1) for a in (0, 1)])
+    ra = (ctypes.c_uint32 * 4)(*alloc(50))
+    # Qm0 = 2 needs the interference-aware qpsk_qpsk / qpsk_qam LLRs: not restated
+    assert O.orc().orc_rx_pdsch_tm3(ctypes.byref(fp), 2, rp, ep, ra, 2, 2, 5, 1, 7, O.P(out), None) == -1
+    # subframes 0 / 5 drop the PBCH / sync RBs (unlike the single-antenna extraction) and shorten by
+    # adjust_G2 (16-QAM: pilot symbols by 2/3 of it)
+    for sf in (0, 5, 7):
+        llr, _ = O.rx_pdsch_tm3(fp, rx, est, alloc(50), 4, 4, 14, 2, sf)
+        assert len(llr) % 4 == 0 and len(llr) > 0
