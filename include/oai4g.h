@@ -588,7 +588,8 @@ int oai4g_memcpy_h2d(void *dst, const void *src, size_t bytes);
 int oai4g_memcpy_d2h(void *dst, const void *src, size_t bytes);
 int oai4g_memset_d(void *dst, int value, size_t bytes);
 int oai4g_sync(void);
-/* Deterministic device-side payload generator (splitmix64 of (seed, byte index)). */
+/* Deterministic device-side payload generator: 8-byte word w = splitmix64 output for the counter
+ * seed + 0x9e3779b97f4a7c15 (w + 1) (little-endian bytes). */
 int oai4g_fill_payload(uint8_t *d_payload, size_t bytes, uint64_t seed, void *stream);
 
 #ifdef __cplusplus

@@ -165,8 +165,8 @@ extern "C" void oai4g_shard_range(int n_total, int rank, int world, int *first, 
 
 extern "C" uint64_t oai4g_payload_seed(uint64_t seed, uint64_t first_subframe, uint32_t n_cw, uint32_t payload_stride)
 {
-  /* k_fill: byte i of a buffer = byte (i mod 8) of splitmix64(seed + i / 8), so the buffer of
-   * global subframes [first, ...) equals the global payload when seeded seed + first n_cw
-   * stride / 8 (payload_stride is a multiple of 16) */
-  return seed + first_subframe * n_cw * (payload_stride / 8);
+  /* k_fill: word w of a buffer = splitmix64 output of seed + gamma (w + 1), gamma = 0x9e37...7c15,
+   * so the buffer of global subframes [first, ...) equals the global payload when seeded
+   * seed + gamma first n_cw stride / 8 (payload_stride is a multiple of 16) */
+  return seed + 0x9e3779b97f4a7c15ull * (first_subframe * n_cw * (payload_stride / 8));
 }

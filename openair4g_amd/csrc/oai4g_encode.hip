@@ -1083,7 +1083,7 @@ hipError_t oai4g_launch_scramble_bytes(uint8_t *d_e, int n_entries, uint32_t c_i
   return hipGetLastError();
 }
 
-/* deterministic payload: byte i = low byte of splitmix64(seed + i/8) >> (8*(i%8)) */
+/* deterministic payload: 8-byte word w = splitmix64 output for the counter seed + gamma (w + 1) */
 __global__ void k_fill(uint8_t *__restrict__ d, size_t bytes, uint64_t seed)
 {
   size_t nw = bytes / 8;

@@ -3208,10 +3208,12 @@ static void rx_extract_map_dual(const oai4g_frame_parms_t *fp, const uint32_t rb
   const int sss_symb = fp->frame_type == 1 ? nsymb - 1 : (nsymb >> 1) - 2;
   const int pss_symb = fp->frame_type == 1 ? 2 : (nsymb >> 1) - 1;
   std::vector<uint32_t> slot(12 * 110 + 256, 0);
+  std::vector<uint8_t> wr(12 * 110 + 256, 0);
   uint32_t p = 0, hw = 0;
   nb_rb = 0;
   auto put = [&](uint32_t pos, uint32_t bin, uint32_t col) {
     slot[pos] = bin | ((5 + col) << 16);
+    wr[pos] = 1;
     hw = pos + 1 > hw ? pos + 1 : hw;
   };
   auto data_re = [&](uint32_t i) { return i != ns && i != ns + 3 && i != ns + 6 && i != (ns + 9) % 12; };
@@ -3279,7 +3281,10 @@ static void rx_extract_map_dual(const oai4g_frame_parms_t *fp, const uint32_t rb
     }
     nb_rb++;
   }
-  n = hw;
+  /* n = the written prefix: the skip_half = 2 pilot branch leaves holes, which the reference would
+   * fill from earlier symbols' ext data (a stream reaching one is refused) */
+  n = 0;
+  while (n < hw && wr[n]) n++;
   map.insert(map.end(), slot.begin(), slot.begin() + hw);
 }
 

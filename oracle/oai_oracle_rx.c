@@ -278,6 +278,8 @@ static int extract_dual(const orc_frame_t *fp, const int32_t *rxF_sym, const int
   const int sss_symb = fp->frame_type == 1 ? nsymb - 1 : (nsymb >> 1) - 2;
   const int pss_symb = fp->frame_type == 1 ? 2 : (nsymb >> 1) - 1;
   int p = 0;                                                   /* the ext pointer (slot index) */
+  uint8_t wr[12 * 110 + 256];
+  memset(wr, 0, sizeof(wr));
   *nb_rb = 0;
   *hw = 0;
 #define PUT(pos, bin, col)                                                              \
@@ -285,6 +287,7 @@ static int extract_dual(const orc_frame_t *fp, const int32_t *rxF_sym, const int
     rx_ext[pos] = rxF_sym[bin];                                                         \
     c0_ext[pos] = ch0_sym[5 + (col)];                                                   \
     c1_ext[pos] = ch1_sym[5 + (col)];                                                   \
+    wr[pos] = 1;                                                                        \
     if ((pos) + 1 > *hw) *hw = (pos) + 1;                                               \
   } while (0)
   for (int prb = 0; prb < fp->N_RB_DL; prb++) {
@@ -358,6 +361,11 @@ static int extract_dual(const orc_frame_t *fp, const int32_t *rxF_sym, const int
     (*nb_rb)++;
   }
 #undef PUT
+  /* *hw = the written prefix (the skip_half = 2 pilot branch leaves holes that the reference fills
+   * from earlier symbols' ext data: a stream reaching one is refused) */
+  int n = 0;
+  while (n < *hw && wr[n]) n++;
+  *hw = n;
   return p;
 }
 

@@ -91,7 +91,8 @@ if __name__ == "__main__":
 def test_c_shard_range_and_payload_seed():
     """The C ABI's oai4g_shard_range (the one bench.py and tools/dlsim_tx.c -g use) covers
     [0, n) in rank order with sizes differing by at most one; oai4g_payload_seed advances the
-    generator by whole subframes (n_cw payload_stride / 8 splitmix64 words each)."""
+    splitmix64 counter (seed + gamma (w + 1) per 8-byte word) by whole subframes (n_cw
+    payload_stride / 8 words each)."""
     import ctypes
     import openair4g_amd as oai
     L = oai.load_library()
@@ -107,4 +108,4 @@ def test_c_shard_range_and_payload_seed():
                 sizes.append(c.value)
             assert nxt == n and max(sizes) - min(sizes) <= 1
     assert L.oai4g_payload_seed(100, 0, 2, 4608) == 100
-    assert L.oai4g_payload_seed(100, 3, 2, 4608) == 100 + 3 * 2 * 576
+    assert L.oai4g_payload_seed(100, 3, 2, 4608) == (100 + 0x9E3779B97F4A7C15 * 3 * 2 * 576) % 2 ** 64

@@ -16,7 +16,7 @@ from test_rx_tm3_cpu import c3_params
 pytestmark = pytest.mark.gpu
 
 RAND = [(100, 6, 6, 19, 1, 7, 2, None), (50, 4, 2, 12, 2, 3, 2, None), (100, 6, 4, 22, 3, 0, 2, None),
-        (25, 6, 6, 19, 1, 0, 2, None), (25, 4, 4, 14, 2, 5, 1, None), (15, 6, 6, 20, 1, 0, 2, None),
+        (25, 6, 6, 19, 1, 5, 2, None), (25, 4, 4, 14, 2, 5, 1, None), (15, 6, 6, 20, 1, 5, 2, None),
         (100, 4, 6, 10, 2, 8, 1, [0xF0F0F0F0, 0x0000FFFF, 0, 0x3])]
 
 
@@ -34,6 +34,16 @@ def test_gpu_tm3_random_inputs(gpu, N_RB, Qm0, Qm1, mcs, npd, sf, nb_rx, ra):
         lo, so = O.rx_pdsch_tm3(fo, rx, est, ra, Qm0, Qm1, mcs, npd, sf)
         lg, sg = gpu.rx_pdsch_tm3(fg, rx, est, ra, Qm0, Qm1, mcs, npd, sf)
         assert sg == so and np.array_equal(lg, lo), (scale, so, sg)
+
+
+def test_gpu_tm3_refuses_holes(gpu):
+    """Odd N_RB_DL, subframe 0: the dual extraction's skip_half = 2 pilot branch (symbol 7 of the
+    PBCH rows) leaves ext slots unwritten that the stream reaches — refused on both sides."""
+    fg = gpu.frame_parms(25, nb_antennas_tx=2, mode1_flag=0)
+    n = fg.symbols_per_tti * fg.ofdm_symbol_size
+    z = np.zeros(n, np.int32)
+    with pytest.raises(gpu.OAI4GError):
+        gpu.rx_pdsch_tm3(fg, [z, z], {(p, a): z for p in (0, 1) for a in (0, 1)}, alloc(25), 6, 6, 19, 1, 0)
 
 
 @pytest.mark.parametrize("N_RB,mcs,npd,sf", [(100, 19, 1, 7), (100, 16, 2, 3), (50, 19, 1, 8)])
