@@ -91,22 +91,30 @@ _PORT_WORKER = r"""
 import sys, time, numpy as np
 sys.path.insert(0, sys.argv[1]); sys.path.insert(0, sys.argv[1] + '/tests')
 import oracle_lib as O, openair4g_amd as oai
-p = oai.make_params(sys.argv[2], subframe=int(sys.argv[3]))
-cfg = O.tx_cfg_from_params(p, int(sys.argv[3]))
+full = sys.argv[6] == "1"
 rng = np.random.default_rng(int(sys.argv[5]))
+if full:      # --full-grid: subframes 0..9 with CRS + PCFICH/PDCCH (bench.full_grid_items' DCI)
+    import bench
+    p = oai.make_params(sys.argv[2], subframe=0, subframe_step=1, with_crs=1)
+    dci = bench.full_grid_items(p, sys.argv[2])[0]
+    cfgs = [O.tx_cfg_from_params(p, sf) for sf in range(10)]
+else:
+    p = oai.make_params(sys.argv[2], subframe=int(sys.argv[3]))
+    dci, cfgs = None, [O.tx_cfg_from_params(p, int(sys.argv[3]))]
 pays = [rng.integers(0, 256, size=p.TBS[cw] // 8 + 8, dtype=np.uint8) for cw in range(p.n_cw)]
-O.tx_subframe(cfg, pays)
+O.tx_subframe(cfgs[0], pays, dci=dci)
 n, t0 = 0, time.perf_counter()
 while time.perf_counter() - t0 < float(sys.argv[4]):
-    O.tx_subframe(cfg, pays); n += 1
+    O.tx_subframe(cfgs[n % len(cfgs)], pays, dci=dci); n += 1
 print(n, time.perf_counter() - t0)
 """
 
 
-def _port_rate(name, subframe, seconds, procs):
+def _port_rate(name, subframe, seconds, procs, full=False):
     """The oracle port in `procs` independent processes for `seconds`: aggregate subframes/s."""
     import subprocess
-    ps = [subprocess.Popen([sys.executable, "-c", _PORT_WORKER, ROOT, name, str(subframe), str(seconds), str(i)],
+    ps = [subprocess.Popen([sys.executable, "-c", _PORT_WORKER, ROOT, name, str(subframe), str(seconds), str(i),
+                            "1" if full else "0"],
                            stdout=subprocess.PIPE, text=True) for i in range(procs)]
     tot, n_all = 0.0, 0
     for p in ps:
@@ -117,15 +125,15 @@ def _port_rate(name, subframe, seconds, procs):
     return tot, n_all
 
 
-def cpu_baseline(name, seconds, subframe):
+def cpu_baseline(name, seconds, subframe, full=False):
     """The oracle ("port") on the host cores over a bounded sample of the same workload: one core,
     then every core of this process's share (independent processes, as N dlsim instances would
     run), plus the reference-equivalent rate through BASELINE.md section 3's calibration
     (profiles/cpu_calibration.json: the reference TUs' 870 subframes/s/core measured by the survey
     in the build container vs the port's rate measured in the same container)."""
-    one, n1 = _port_rate(name, subframe, seconds, 1)
+    one, n1 = _port_rate(name, subframe, seconds, 1, full)
     cores = host_cores()
-    allc, nall = _port_rate(name, subframe, max(2.0, seconds / 2), cores) if cores > 1 else (one, n1)
+    allc, nall = _port_rate(name, subframe, max(2.0, seconds / 2), cores, full) if cores > 1 else (one, n1)
     cal = None
     try:
         cal = json.load(open(os.path.join(ROOT, "profiles", "cpu_calibration.json"))).get(name)
@@ -133,9 +141,12 @@ def cpu_baseline(name, seconds, subframe):
         pass
     out = {"value": one, "unit": "subframes/s", "cores": 1, "kind": "port", "cpu_model": cpu_model(),
            "value_all_cores": allc, "cores_all": cores,
-           "sample": f"{n1} subframes of {name} (sf {subframe}) through the C oracle on 1 core in {seconds:.0f} s; "
+           "sample": f"{n1} subframes of {name} "
+                     + ("(subframes 0..9 with CRS + PCFICH/PDCCH; the common signals, < 1 % of the REs, not in the "
+                        "CPU sample)" if full else f"(sf {subframe})")
+                     + f" through the C oracle on 1 core in {seconds:.0f} s; "
                      f"{nall} on {cores} cores (independent processes)"}
-    if cal:
+    if cal and not full:
         r = cal["ref_per_core"] / cal["port_per_core"]
         out["ref_equiv_per_core"] = one * r
         out["ref_equiv_all_cores"] = allc * r
@@ -477,38 +488,67 @@ def bench_fep(args, world, rank, dist, torch):
 
 
 def bench_ue(args, world, rank, dist, torch):
-    """UE PDSCH receive chain (SURVEY 8f item 3, config "UE"): dlsim's C2 receiver with
+    """UE PDSCH receive chain.  Config "UE": dlsim's C2 receiver with
     perfect_ce = 0 -- slot_fep of every symbol, lte_dl_channel_estimation of the pilot symbols
     with the temporal interpolation of every row, rx_pdsch (extraction, channel level,
     compensation, 16-QAM LLRs) and dlsch_unscrambling -- over a batch of consecutive 20 MHz TM1
-    subframes (1 TX, 1 RX antenna) produced once by the GPU transmit pipeline."""
+    subframes (1 TX, 1 RX antenna) produced once by the GPU transmit pipeline.  Config "UE3": the
+    C3 receiver (TM3 large-delay CDD, 2 TX x 2 RX, H = I): slot_fep of both antennas, the four
+    (port, antenna) estimations, rx_pdsch's TM3 branch (extract_rbs_dual, channel_level_TM3,
+    prec2A_TM3 + compensation_TM3, MRC, codeword 0's 64-QAM LLRs) and dlsch_unscrambling."""
     import numpy as np
     import openair4g_amd as oai
     oai.init()
+    tm3 = args.config == "UE3"
     n_sf = args.batch
-    p = oai.make_params("C2", subframe=0, subframe_step=1, with_crs=1, rnti=0x1234)
-    fp = oai.frame_parms(100)
+    nrx = 2 if tm3 else 1
+    if tm3:
+        p = oai.make_params("C3", subframe=0, subframe_step=1, with_crs=1, rnti=0x1234)
+        fp = oai.frame_parms(100, nb_antennas_tx=2, mode1_flag=0)
+    else:
+        p = oai.make_params("C2", subframe=0, subframe_step=1, with_crs=1, rnti=0x1234)
+        fp = oai.frame_parms(100)
     N, nsym, spt = fp.ofdm_symbol_size, fp.symbols_per_tti, fp.samples_per_tti
     Qm = oai.lib().oai4g_get_Qm(p.mcs[0])
-    # input: n_sf + 1 consecutive transmitted subframes (the last one's symbol 0 closes rows 12 / 13)
+    # input: n_sf + 1 consecutive transmitted subframes (the last one's symbol 0 closes rows 12 / 13);
+    # TM3: receive antenna a = transmit antenna a (H = I)
     tx = oai.TxPipeline(p, n_sf + 1)
     tx.fill_payload(0x5EED + rank)
     tx.run()
     tx.sync()
-    fb = oai.FepBatch(fp, n_sf + 1, 1)
+    fb = oai.FepBatch(fp, n_sf + 1, nrx)
     fb.upload(tx.iq())
     tx.close()
-    cb = oai.ChestBatch(fp, n_sf, first_subframe=0)
-    rb = oai.RxBatch(fp, list(p.rb_alloc), Qm, p.num_pdcch_symbols, p.rnti, n_sf, first_subframe=0, subframe_step=1)
     sid = torch.cuda.current_stream().cuda_stream
+    if tm3:
+        rb = oai.RxBatchTM3(fp, list(p.rb_alloc), Qm, oai.lib().oai4g_get_Qm(p.mcs[1]), p.mcs[0],
+                            p.num_pdcch_symbols, p.rnti, n_sf, nb_rx=2, first_subframe=0)
+        cb = None
 
-    def step(stream):
-        fb.run(stream=stream)
+        def step(stream):
+            fb.run(stream=stream)
+            rb.estimate(fb.d_rxF, stream=stream)
+            rb.launch(fb.d_rxF, 1, stream=stream)
+        stages = {"k_fep": lambda: fb.run(stream=sid), "k_chest x4": lambda: rb.estimate(fb.d_rxF, stream=sid),
+                  "k_rx_level_tm3+k_rx_llr_tm3": lambda: rb.launch(fb.d_rxF, 1, stream=sid)}
+    else:
+        cb = oai.ChestBatch(fp, n_sf, first_subframe=0)
+        rb = oai.RxBatch(fp, list(p.rb_alloc), Qm, p.num_pdcch_symbols, p.rnti, n_sf, first_subframe=0,
+                         subframe_step=1)
+
+        def step(stream):
+            fb.run(stream=stream)
+            if args.ue_unfused:
+                cb.launch(fb.d_rxF, stream=stream)
+                rb.launch(fb.d_rxF, cb.d_est, 1, stream=stream)
+            else:
+                rb.launch_estimated(cb, fb.d_rxF, 1, stream=stream)
         if args.ue_unfused:
-            cb.launch(fb.d_rxF, stream=stream)
-            rb.launch(fb.d_rxF, cb.d_est, 1, stream=stream)
+            stages = {"k_fep": lambda: fb.run(stream=sid), "k_chest": lambda: cb.launch(fb.d_rxF, stream=sid),
+                      "k_rx_level+k_rx_llr": lambda: rb.launch(fb.d_rxF, cb.d_est, 1, stream=sid)}
         else:
-            rb.launch_estimated(cb, fb.d_rxF, 1, stream=stream)
+            stages = {"k_fep": lambda: fb.run(stream=sid),
+                      "k_rx_chest": lambda: rb.launch_estimated(cb, fb.d_rxF, 1, stream=sid)}
     for _ in range(args.warmup):
         step(None)
     oai.lib().oai4g_sync()
@@ -528,12 +568,6 @@ def bench_ue(args, world, rank, dist, torch):
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     # per-stage launch durations (HIP events on the launch stream)
-    if args.ue_unfused:
-        stages = {"k_fep": lambda: fb.run(stream=sid), "k_chest": lambda: cb.launch(fb.d_rxF, stream=sid),
-                  "k_rx_level+k_rx_llr": lambda: rb.launch(fb.d_rxF, cb.d_est, 1, stream=sid)}
-    else:
-        stages = {"k_fep": lambda: fb.run(stream=sid),
-                  "k_rx_chest": lambda: rb.launch_estimated(cb, fb.d_rxF, 1, stream=sid)}
     kern_ms = {}
     for name, fn in stages.items():
         evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
@@ -546,57 +580,88 @@ def bench_ue(args, world, rank, dist, torch):
         kern_ms[name] = sum(e0.elapsed_time(e1) for e0, e1 in evs) / len(evs)
     n_llr = sum(rb.llr_count(i % 10) for i in range(n_sf))
     n_re = n_llr // Qm
-    alg = {"k_fep": (n_sf + 1) * (spt * 4 + nsym * N * 4),                 # IQ read + frequency grid written
-           "k_chest": n_sf * (nsym * N * 4 + 5 * N * 4),                     # 14 rows written + 5 pilot rows read
-           "k_rx_level+k_rx_llr": n_re * 8 + n_llr * 2 + n_sf * 1200 * 4,    # y + h per RE, LLRs, level row
-           "k_rx_chest": n_re * 4 + n_llr * 2 + n_sf * 5 * 1200 * 4}         # y per RE, LLRs, 5 pilot rows
+    alg = {"k_fep": (n_sf + 1) * nrx * (spt * 4 + nsym * N * 4),        # IQ read + frequency grid written
+           "k_chest": n_sf * (nsym * N * 4 + 5 * N * 4),                   # 14 rows written + 5 pilot rows read
+           "k_chest x4": 4 * n_sf * (nsym * N * 4 + 5 * N * 4),
+           "k_rx_level+k_rx_llr": n_re * 8 + n_llr * 2 + n_sf * 1200 * 4,  # y + h per RE, LLRs, level row
+           "k_rx_chest": n_re * 4 + n_llr * 2 + n_sf * 5 * 1200 * 4,       # y per RE, LLRs, 5 pilot rows
+           # 2 y + 4 h per RE, LLRs, the level symbol's 4 estimate rows
+           "k_rx_level_tm3+k_rx_llr_tm3": n_re * 24 + n_llr * 2 + n_sf * 4 * 1200 * 4}
     alg = {k: v for k, v in alg.items() if k in stages}
     fb.close()
-    cb.close()
+    if cb is not None:
+        cb.close()
     rb.close()
     value = n_sf * args.steps * world / elapsed
     dom = max(kern_ms, key=kern_ms.get)
     ach = alg[dom] / (kern_ms[dom] * 1e-3) / 1e9
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        sys.path.insert(0, os.path.join(ROOT, "tests"))
-        import oracle_lib as O
-        fpo = O.frame(100)
-        rng = np.random.default_rng(1)
-        frame = np.zeros(10 * spt + N, np.int32)
-        frame[:2 * spt] = rng.integers(-2000, 2000, (2 * spt, 2), dtype=np.int16).view(np.int32).ravel()
-        rxF, nxt = np.zeros(15 * N, np.int32), np.zeros(15 * N, np.int32)
-        n, t1 = 0, time.perf_counter()
-        while time.perf_counter() - t1 < args.cpu_seconds:
-            for Ns in (0, 1):
-                for l in range(7):
-                    O.slot_fep([frame], [rxF], fpo, l, Ns)
-            O.slot_fep([frame], [nxt], fpo, 0, 2)
-            est = O.chest_subframe(fpo, rxF[:14 * N], nxt[:N], 0)
-            llr, _ = O.rx_pdsch_siso(fpo, rxF[:14 * N], est, list(p.rb_alloc), Qm, p.num_pdcch_symbols, 0)
-            u = np.zeros(32 * (1 + len(llr) // 32), np.int16)
-            u[:len(llr)] = llr
-            O.dlsch_unscrambling(u, len(llr), (p.rnti << 14) + fpo.Nid_cell)
-            n += 1
-        dt = time.perf_counter() - t1
-        cpu = {"value": n / dt, "unit": "subframes/s", "cores": 1, "kind": "port",
-               "sample": f"{n} subframes through the C oracle (slot_fep + 5 lte_dl_channel_estimation calls + "
-                         f"rx_pdsch + dlsch_unscrambling), single thread, {dt:.1f} s"}
+        cpu = _ue_cpu_baseline(args, p, Qm, tm3)
+    if tm3:
+        metric = "UE PDSCH RX subframes/sec (20 MHz TM3 2x2 64-QAM, estimated channel)"
+        wl = ("slot_fep x2 + lte_dl_channel_estimation (2 ports x 2 RX) + rx_pdsch TM3 (dual extraction, "
+              "level_TM3, prec2A/compensation_TM3, MRC, codeword-0 LLRs) + dlsch_unscrambling, C3 20 MHz")
+    else:
+        metric = "UE PDSCH RX subframes/sec (20 MHz TM1 16-QAM, 1 RX, estimated channel)"
+        wl = ("slot_fep + lte_dl_channel_estimation + rx_pdsch + dlsch_unscrambling, C2 20 MHz"
+              + (" (estimation and demodulation as separate kernels)" if args.ue_unfused else
+                 " (estimation fused into the demodulator)"))
     if rank == 0:
         print(json.dumps({
-            "metric": "UE PDSCH RX subframes/sec (20 MHz TM1 16-QAM, 1 RX, estimated channel)", "value": value,
+            "metric": metric, "value": value,
             "unit": "subframes/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
             "ms_per_step": elapsed * 1000.0 / args.steps, "higher_is_better": True, "scaling": "weak",
-            "vs_baseline": None, "dtype": "int16", "data": "GPU-transmitted C2 subframes (synthetic payload), resident in HBM",
-            "config": {"workload": "slot_fep + lte_dl_channel_estimation + rx_pdsch + dlsch_unscrambling, C2 20 MHz"
-                                   + (" (estimation and demodulation as separate kernels)" if args.ue_unfused else
-                                      " (estimation fused into the demodulator)"),
-                       "config_id": "UE", "subframes_per_gpu_per_step": n_sf, "parallelism": f"subframe-sharded x{world}"},
+            "vs_baseline": None, "dtype": "int16",
+            "data": f"GPU-transmitted {'C3' if tm3 else 'C2'} subframes (synthetic payload), resident in HBM",
+            "config": {"workload": wl, "config_id": args.config, "subframes_per_gpu_per_step": n_sf,
+                       "parallelism": f"subframe-sharded x{world}"},
             "roofline": {"bound": "hbm", "kernel": dom, "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": ach / HBM_PEAK_GBS, "traffic": _stage_traffic("UE", dom, n_sf), "kernel_ms": kern_ms,
-                         "algorithmic_bytes_per_launch": alg},
+                         "frac": ach / HBM_PEAK_GBS, "traffic": _stage_traffic(args.config, dom, n_sf),
+                         "kernel_ms": kern_ms, "algorithmic_bytes_per_launch": alg},
             "end_to_end_algorithmic_GBps": sum(alg.values()) / (elapsed / args.steps) / 1e9,
             "cpu_baseline": cpu}), flush=True)
+
+
+def _ue_cpu_baseline(args, p, Qm, tm3):
+    """The C oracle's UE chain, one thread, on random samples of one subframe (+ the next slot)."""
+    import numpy as np
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import oracle_lib as O
+    fpo = O.frame(100, nb_antennas_tx=2, mode1_flag=0) if tm3 else O.frame(100)
+    N, spt = fpo.ofdm_symbol_size, fpo.samples_per_tti
+    nrx = 2 if tm3 else 1
+    rng = np.random.default_rng(1)
+    frames = []
+    for _ in range(nrx):
+        f = np.zeros(10 * spt + N, np.int32)
+        f[:2 * spt] = rng.integers(-2000, 2000, (2 * spt, 2), dtype=np.int16).view(np.int32).ravel()
+        frames.append(f)
+    rxF = [np.zeros(15 * N, np.int32) for _ in range(nrx)]
+    nxt = [np.zeros(15 * N, np.int32) for _ in range(nrx)]
+    n, t1 = 0, time.perf_counter()
+    while time.perf_counter() - t1 < args.cpu_seconds:
+        for Ns in (0, 1):
+            for l in range(7):
+                O.slot_fep(frames, rxF, fpo, l, Ns)
+        O.slot_fep(frames, nxt, fpo, 0, 2)
+        if tm3:
+            est = {(pp, a): O.chest_subframe(fpo, rxF[a][:14 * N], nxt[a][:N], 0, p=pp) for pp in (0, 1)
+                   for a in (0, 1)}
+            llr, _ = O.rx_pdsch_tm3(fpo, [rxF[0][:14 * N], rxF[1][:14 * N]], est, list(p.rb_alloc), Qm, Qm,
+                                    p.mcs[0], p.num_pdcch_symbols, 0)
+        else:
+            est = O.chest_subframe(fpo, rxF[0][:14 * N], nxt[0][:N], 0)
+            llr, _ = O.rx_pdsch_siso(fpo, rxF[0][:14 * N], est, list(p.rb_alloc), Qm, p.num_pdcch_symbols, 0)
+        u = np.zeros(32 * (1 + len(llr) // 32), np.int16)
+        u[:len(llr)] = llr
+        O.dlsch_unscrambling(u, len(llr), (p.rnti << 14) + fpo.Nid_cell)
+        n += 1
+    dt = time.perf_counter() - t1
+    what = ("slot_fep x2 antennas + 4 x 5 lte_dl_channel_estimation calls + rx_pdsch TM3" if tm3 else
+            "slot_fep + 5 lte_dl_channel_estimation calls + rx_pdsch")
+    return {"value": n / dt, "unit": "subframes/s", "cores": 1, "kind": "port",
+            "sample": f"{n} subframes through the C oracle ({what} + dlsch_unscrambling), single thread, {dt:.1f} s"}
 
 
 def launch_ranks(n, argv):
@@ -733,6 +798,9 @@ def main():
                          "8 GPUs, FEP 8192, C5 2048); measured on C3: 2048 -> 4.20M, 5120 -> 4.56M, 10240 -> 4.67M "
                          "subframes/s (launch tails amortised)")
     ap.add_argument("--subframe", type=int, default=7)
+    ap.add_argument("--full-grid", action="store_true",
+                    help="transmit configurations: the eNB's whole grid (PDSCH + CRS + PCFICH/PDCCH + PSS/SSS/PBCH + "
+                         "PHICH) over subframe indices 0..9 instead of the PDSCH of --subframe")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--kernel-reps", type=int, default=5, help="serial runs timed per kernel for the roofline")
@@ -745,7 +813,7 @@ def main():
                     help="harness test on CPU: gloo, StubPipeline, no GPU (exercises ranks/broadcast/timing)")
     args = ap.parse_args()
     if args.batch is None:
-        args.batch = {"C3": 8192, "C4": 1024, "FEP": 8192, "UE": 4096}.get(args.config, 2048)
+        args.batch = {"C3": 8192, "C4": 1024, "FEP": 8192, "UE": 4096, "UE3": 2048}.get(args.config, 2048)
     if args.cpu_stub:
         args.backend = "gloo"
 
@@ -760,14 +828,44 @@ def main():
 
     host = Host(args, world, rank, local_rank)
     torch, dist = host.torch, host.dist
-    if args.config in ("C5", "FEP", "UE"):
+    if args.config in ("C5", "FEP", "UE", "UE3"):
         if host.stub:
             sys.exit("bench: --cpu-stub covers the transmit configurations only")
-        {"C5": bench_c5, "FEP": bench_fep, "UE": bench_ue}[args.config](args, world, rank, dist, torch)
+        {"C5": bench_c5, "FEP": bench_fep, "UE": bench_ue, "UE3": bench_ue}[args.config](args, world, rank, dist, torch)
         host.close()
         return
     bench_tx(args, world, rank, host)
     host.close()
+
+
+FULL_GRID_DCI_LEN = {"C1": 23, "C2": 39, "C3": 48, "C4": 48}    # format 1 / 2A (dlsim's DCIs), L = 1
+FULL_GRID_PBCH_PDU = (0xA5, 0x3C, 0x0F)
+
+
+def full_grid_items(params, name):
+    """The control and common signals of --full-grid: one UE-specific DCI (dlsim.c's format 1 / 2A,
+    aggregation 1, CCE from get_nCCE_offset) for PCFICH + PDCCH, PSS + SSS (subframe indices 0 / 5),
+    the PBCH (index 0, frame_mod4 0) and one PHICH per subframe (group 0) — phy_procedures_lte_eNb.c's
+    txdataF with with_crs = 1."""
+    import ctypes
+    import openair4g_amd as oai
+    L = oai.lib()
+    fp = oai.frame_parms(params.N_RB_DL, Nid_cell=params.Nid_cell, Ncp=params.Ncp,
+                         nb_antennas_tx=params.nb_antennas_tx, mode1_flag=params.mode1_flag)
+    L.oai4g_init_nCCE_table()
+    nCCE = L.oai4g_get_nCCE(params.num_pdcch_symbols, ctypes.byref(fp), 1)
+    ncce = L.oai4g_get_nCCE_offset(2, nCCE, 0, params.rnti, 7)
+    pdu = bytes(range(0x31, 0x39))
+    items = [(FULL_GRID_DCI_LEN[name], 1, ncce, params.rnti, pdu)]
+    phich = [] if params.mode1_flag == 1 and params.nb_antennas_tx > 1 else \
+        [(sf, 0, sf % 8, sf & 1) for sf in range(10)]
+    return items, phich
+
+
+def full_grid_setup(pipe, params, name):
+    items, phich = full_grid_items(params, name)
+    pipe.set_control(items)
+    pipe.set_common(pss_sss=True, pbch_pdu=FULL_GRID_PBCH_PDU, frame_mod4=0, phich=phich)
 
 
 def bench_tx(args, world, rank, host):
@@ -780,7 +878,10 @@ def bench_tx(args, world, rank, host):
         oai.init()
     # ---- parameter block: built on rank 0, broadcast over RCCL (the only collective): the C ABI's
     # oai4g_dist_broadcast_params on the GPU, torch.distributed (gloo) under --cpu-stub ----
-    p0 = oai.make_params(args.config, subframe=args.subframe) if rank == 0 else None
+    if args.full_grid:           # the eNB's whole grid over all 10 subframe indices (subframe_step 1)
+        p0 = oai.make_params(args.config, subframe=0, subframe_step=1, with_crs=1) if rank == 0 else None
+    else:
+        p0 = oai.make_params(args.config, subframe=args.subframe) if rank == 0 else None
     if dist is None:
         params = p0
     elif host.stub:
@@ -790,6 +891,8 @@ def bench_tx(args, world, rank, host):
         params = odist.c_broadcast_params(p0)
 
     pipe = (StubPipeline if host.stub else oai.TxPipeline)(params, args.batch)
+    if args.full_grid and not host.stub:
+        full_grid_setup(pipe, params, args.config)
     # this rank's shard of the global stream of synthetic TBs: global subframes [rank B, (rank + 1) B)
     first, _ = odist.shard_range(world * args.batch, rank, world)
     pipe.fill_payload(seed=odist.global_payload_seed(0x5EED0000, first, params))
@@ -824,8 +927,9 @@ def bench_tx(args, world, rank, host):
     ms_per_step = elapsed * 1000.0 / args.steps
 
     payload_b, iq_b = algorithmic_bytes(params, pipe.spt)
-    G = [pipe.G(cw, args.subframe) for cw in range(params.n_cw)]
-    ebits_b = sum((g + 7) // 8 for g in G)
+    sfs = range(10) if args.full_grid else [args.subframe]
+    G = [sum(pipe.G(cw, sf) for sf in sfs) / len(sfs) for cw in range(params.n_cw)]      # mean over the batch
+    ebits_b = sum((g + 7) / 8 for g in G)
     enc_ms = kern[0] / args.kernel_reps
     mod_ms = kern[1] / args.kernel_reps
     per_kernel = {
@@ -834,18 +938,23 @@ def bench_tx(args, world, rank, host):
     }
     dom = max(per_kernel, key=lambda k: per_kernel[k]["ms"])
     ach = per_kernel[dom]["bytes"] / (per_kernel[dom]["ms"] * 1e-3) / 1e9
-    traffic = _traffic(args.config, dom, args.batch)
+    ptag = args.config + ("_full" if args.full_grid else "")     # profiles/traffic_<tag>.json
+    traffic = _traffic(ptag, dom, args.batch)
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        cpu = cpu_baseline(args.config, args.cpu_seconds, args.subframe)
+        cpu = cpu_baseline(args.config, args.cpu_seconds, args.subframe, args.full_grid)
 
     if rank == 0:
         cfgname = {"C1": "dlsim 1.4 MHz SISO QPSK MCS9", "C2": "dlsim 20 MHz SISO 16-QAM MCS16",
                    "C3": "dlsim 20 MHz 2x2 TM3 (LARGE_CDD) 64-QAM MCS19x2CW, 2x14 IDFT-2048",
-                   "C4": "20 MHz 4 TX TM3 (4-port large-delay CDD, build-defined) 64-QAM MCS19x2CW, 4x14 IDFT-2048"}[args.config]
+                   "C4": "20 MHz 4 TX TM3 rank 2 on 4 ports (large-delay CDD, build-defined) 64-QAM MCS19x2CW, "
+                         "4x14 IDFT-2048"}[args.config]
+        if args.full_grid:
+            cfgname += " + full eNB grid (CRS, PCFICH/PDCCH, PSS/SSS/PBCH, PHICH) over subframes 0..9"
         out = {
-            "metric": "DL subframes/sec (20 MHz, 2x2, 64-QAM)" if args.config == "C3" else f"DL subframes/sec ({args.config})",
+            "metric": ("DL subframes/sec (20 MHz, 2x2, 64-QAM)" if args.config == "C3" else
+                       f"DL subframes/sec ({args.config})") + (" full grid" if args.full_grid else ""),
             "value": value,
             "unit": "subframes/s",
             "n_gpus": world,
@@ -859,12 +968,14 @@ def bench_tx(args, world, rank, host):
             "data": "synthetic (device-generated splitmix64 transport blocks, resident in HBM)" if not host.stub
                     else "cpu-stub harness run (no GPU): not a measurement",
             "config": {"workload": cfgname, "config_id": args.config, "subframes_per_gpu_per_step": args.batch,
-                       "global_batch": args.batch * world, "subframe_index": args.subframe,
+                       "global_batch": args.batch * world,
+                       "subframe_index": "0..9 (subframe_step 1)" if args.full_grid else args.subframe,
+                       "full_grid": bool(args.full_grid),
                        "TBS": [params.TBS[cw] for cw in range(params.n_cw)], "G": G,
                        "parallelism": f"subframe-sharded x{world}"},
             "roofline": {"bound": "hbm", "kernel": dom, "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": ach / HBM_PEAK_GBS, "traffic": traffic,
-                         "valu_issue_frac": _valu_busy(args.config, args.batch),
+                         "valu_issue_frac": _valu_busy(ptag, args.batch),
                          "kernel_ms": {k: v["ms"] for k, v in per_kernel.items()},
                          "algorithmic_bytes_per_launch": {k: v["bytes"] for k, v in per_kernel.items()}},
             "end_to_end_algorithmic_GBps": value * (payload_b + iq_b) / 1e9,

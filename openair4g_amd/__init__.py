@@ -550,6 +550,7 @@ class RxBatchTM3:
         self.d_est = self.L.oai4g_dev_alloc(4 * self.plane * 4)
         self.d_llr = self.L.oai4g_dev_alloc(n_sf * self.stride * 2)
         _check(bool(self.d_est) and bool(self.d_llr))
+        self._chest = {}
 
     def llr_count(self, sfi):
         return self.L.oai4g_rx_llr_count(self.cfg, sfi)
@@ -558,21 +559,27 @@ class RxBatchTM3:
         """device pointer of the estimate plane of port p at receive antenna a"""
         return ctypes.c_void_p(self.d_est + (2 * p + a) * self.plane * 4)
 
+    def _chest_cfgs(self, first_subframe, subframe_step):
+        """the ports' 0 / 1 estimation configurations (element stride nb_rx subframes), cached"""
+        key = (first_subframe, subframe_step)
+        if key not in self._chest:
+            cfgs = []
+            for p in (0, 1):
+                cfg = self.L.oai4g_chest_config_create(ctypes.byref(self.fp), p, first_subframe, subframe_step)
+                _check(bool(cfg))
+                cfgs.append(cfg)
+                _check(self.L.oai4g_chest_config_set_stride(cfg, self.nb_rx, self.nb_rx) == 0)
+            self._chest[key] = cfgs
+        return self._chest[key]
+
     def estimate(self, d_rxF, first_subframe=0, subframe_step=1, stream=None):
         """The four channel-estimation batches over the FEP output [n_sf + 1][nb_rx][nsymb][N]
         (the extra element's symbol 0 closes the last subframe's rows 12 / 13)."""
         N, nsymb = self.fp.ofdm_symbol_size, self.fp.symbols_per_tti
-        for p in (0, 1):
-            cfg = self.L.oai4g_chest_config_create(ctypes.byref(self.fp), p, first_subframe, subframe_step)
-            _check(bool(cfg))
-            try:
-                _check(self.L.oai4g_chest_config_set_stride(cfg, self.nb_rx, self.nb_rx) == 0)
-                for a in range(self.nb_rx):
-                    _check(self.L.oai4g_chest_batch(cfg, self.n_sf, ctypes.c_void_p(d_rxF + a * nsymb * N * 4),
-                                                    self.est_plane(p, a), stream) == 0)
-            finally:
-                _check(self.L.oai4g_sync() == 0)
-                self.L.oai4g_chest_config_destroy(cfg)
+        for p, cfg in enumerate(self._chest_cfgs(first_subframe, subframe_step)):
+            for a in range(self.nb_rx):
+                _check(self.L.oai4g_chest_batch(cfg, self.n_sf, ctypes.c_void_p(d_rxF + a * nsymb * N * 4),
+                                                self.est_plane(p, a), stream) == 0)
 
     def launch(self, d_rxF, unscramble=1, stream=None):
         _check(self.L.oai4g_rx_batch_tm3(self.cfg, self.n_sf, d_rxF, self.d_est, self.d_llr, unscramble, stream) == 0)
@@ -590,6 +597,11 @@ class RxBatchTM3:
         return out
 
     def close(self):
+        self.L.oai4g_sync()
+        for cfgs in self._chest.values():
+            for cfg in cfgs:
+                self.L.oai4g_chest_config_destroy(cfg)
+        self._chest = {}
         self.L.oai4g_dev_free(self.d_est)
         self.L.oai4g_dev_free(self.d_llr)
         self.L.oai4g_rx_config_destroy(self.cfg)
