@@ -234,7 +234,8 @@ uint8_t oai4g_generate_dci_top(uint8_t num_ue_spec_dci, uint8_t num_common_dci, 
  * dlsim runs it (dlsim.c:3188-3260): dlsch_extract_rbs_single (:3167), dlsch_channel_level (:2777)
  * -> log2_maxh, dlsch_channel_compensation (:801) and dlsch_qpsk / 16qam / 64qam_llr
  * (dlsch_llr_computation.c:636, 688, 810).  Transmission mode 1 (one TX port), one receive
- * antenna, even N_RB_DL (6 / 50 / 100; the reference's odd-N_RB extraction is not restated), the
+ * antenna, every N_RB_DL (the odd 15 / 25 PRB extraction around the DC carrier included; a
+ * subframe whose extraction would read slots the reference leaves unwritten returns -1), the
  * first PDSCH symbol without pilots.  rxdataF and dl_ch_estimates are one subframe, [nsymb][N]
  * each (estimate of subcarrier 12 rb + i at entry 5 + 12 rb + i of its symbol, the layout of the
  * reference's estimator and of dlsim's perfect-CE mode, dlsim.c:2935-2966).  Writes the LLR

@@ -2,7 +2,7 @@
  * Replaces: dlsch_coding.c:254 dlsch_encoding, dlsch_scrambling.c:51, dlsch_modulation.c:1181,
  * ofdm_mod.c:47/85/233, lte_dfts.c idft64..idft2048, crc_byte.c:117/135, lte_segmentation.c:39,
  * 3gpplte_sse.c:380, lte_rate_matching.c:51/464, pcfich.c:48/144, dci.c:2024, pss.c:50, sss.c:47,
- * pbch.c:161, phich.c:401, lte_dl_channel_estimation.c:37, dlsch_demodulation.c:82 (rx_pdsch, TM1),
+ * pbch.c:161, phich.c:401, lte_dl_channel_estimation.c:37, dlsch_demodulation.c:82 (rx_pdsch, TM1/TM3),
  * dlsch_scrambling.c:99 (dlsch_unscrambling), 3gpplte_turbo_decoder_sse_16bit.c:945 / _8bit.c:894,
  * lte_rate_matching.c:193 / :293 / :688 (the UL decoding chain). */
 #include "PHY/defs.h"
@@ -230,44 +230,77 @@ uint32_t lte_rate_matching_turbo(uint32_t RTC, uint32_t G, uint8_t *w, uint8_t *
 }
 
 /* UE receive chain after the FFT.
- * lte_dl_channel_estimation (lte_dl_channel_estimation.c:37): the library covers eNB_offset 0,
- * high_speed_flag 1 (dlsim's and lte_init's default) and one RX antenna; anything else reports -1
- * as the reference does for its unsupported (p, l) cases. */
+ * lte_dl_channel_estimation (lte_dl_channel_estimation.c:37): the library covers eNB_offset 0 and
+ * high_speed_flag 1 (dlsim's and lte_init's default); like the reference it estimates every
+ * receive antenna (1 or 2) into dl_ch_estimates[eNB_offset][(p << 1) + aarx].  Anything else
+ * reports -1 as the reference does for its unsupported (p, l) cases. */
 int lte_dl_channel_estimation(PHY_VARS_UE *ue, uint8_t eNB_id, uint8_t eNB_offset, unsigned char Ns, unsigned char p,
                               unsigned char l, unsigned char symbol)
 {
   (void)eNB_id;
-  if (eNB_offset != 0 || ue->high_speed_flag != 1 || ue->lte_frame_parms.nb_antennas_rx != 1) return -1;
+  const int nrx = ue->lte_frame_parms.nb_antennas_rx;
+  if (eNB_offset != 0 || ue->high_speed_flag != 1 || nrx < 1 || nrx > 2) return -1;
   oai4g_frame_parms_t fp;
   fp_to(&ue->lte_frame_parms, &fp);
-  return oai4g_lte_dl_channel_estimation(&fp, (const int32_t *)ue->lte_ue_common_vars.rxdataF[0],
-                                         (int32_t *)ue->lte_ue_common_vars.dl_ch_estimates[0][p << 1], Ns, p, l,
-                                         symbol);
+  for (int a = 0; a < nrx; a++)
+    if (oai4g_lte_dl_channel_estimation(&fp, (const int32_t *)ue->lte_ue_common_vars.rxdataF[a],
+                                        (int32_t *)ue->lte_ue_common_vars.dl_ch_estimates[0][(p << 1) + a], Ns, p, l,
+                                        symbol) != 0)
+      return -1;
+  return 0;
 }
 
-/* rx_pdsch (dlsch_demodulation.c:82) for TM1 / one RX antenna / localized allocations
- * (rb_alloc_even == rb_alloc_odd): the library demodulates a whole subframe, so the shim runs it
- * when dlsim's last per-symbol call arrives (dlsim.c:3236-3260) -- the LLR stream and log2_maxh in
- * lte_ue_pdsch_vars[eNB_id] are then the reference's. */
+/* rx_pdsch (dlsch_demodulation.c:82) for TM1 (one TX port, one RX antenna) and TM3 (LARGE_CDD,
+ * two TX ports, 1-2 RX antennas, dual_stream_flag 0), localized allocations (rb_alloc_even ==
+ * rb_alloc_odd).  CONTRACT: the library demodulates a whole subframe, so the shim accepts dlsim's
+ * call sequence only (dlsim.c:3236-3260): first_symbol_flag on symbol num_pdcch_symbols, then
+ * every following symbol in order; the work runs at the last symbol, when the LLR stream and
+ * log2_maxh in lte_ue_pdsch_vars[eNB_id] become the reference's.  The per-symbol intermediates
+ * (rxdataF_comp, dl_ch_mag / magb) are NOT filled.  A call out of that sequence returns -1
+ * (state per thread, so concurrent UE threads each keep their own sequence). */
+static __thread int rx_next_symbol = -1;
+
 int rx_pdsch(PHY_VARS_UE *ue, PDSCH_t type, unsigned char eNB_id, unsigned char eNB_id_i, uint8_t subframe,
              unsigned char symbol, unsigned char first_symbol_flag, unsigned char dual_stream_flag,
              unsigned char i_mod, unsigned char harq_pid)
 {
   (void)eNB_id_i;
-  (void)first_symbol_flag;
   (void)i_mod;
+  const LTE_DL_FRAME_PARMS *f = &ue->lte_frame_parms;
   LTE_DL_UE_HARQ_t *h = ue->dlsch_ue[eNB_id][0]->harq_processes[harq_pid];
-  if (type != PDSCH || dual_stream_flag || ue->lte_frame_parms.nb_antennas_rx != 1 ||
-      ue->lte_frame_parms.nb_antennas_tx_eNB != 1 || memcmp(h->rb_alloc_even, h->rb_alloc_odd, 16) != 0)
+  const int tm3 = f->nb_antennas_tx_eNB == 2 && h->mimo_mode == LARGE_CDD;
+  if (type != PDSCH || dual_stream_flag || memcmp(h->rb_alloc_even, h->rb_alloc_odd, 16) != 0 ||
+      (!tm3 && (f->nb_antennas_rx != 1 || f->nb_antennas_tx_eNB != 1)) || (tm3 && f->nb_antennas_rx > 2))
     return -1;
-  if (symbol != ue->lte_frame_parms.symbols_per_tti - 1) return 0;
+  const int npdcch = ue->lte_ue_pdcch_vars[eNB_id]->num_pdcch_symbols;
+  if (first_symbol_flag) {
+    if (symbol != npdcch) { rx_next_symbol = -1; return -1; }
+  } else if (symbol != rx_next_symbol) {
+    rx_next_symbol = -1;
+    return -1;
+  }
+  rx_next_symbol = symbol + 1;
+  if (symbol != f->symbols_per_tti - 1) return 0;
+  rx_next_symbol = -1;
   oai4g_frame_parms_t fp;
-  fp_to(&ue->lte_frame_parms, &fp);
+  fp_to(f, &fp);
   uint8_t log2_maxh = 0;
-  const int n = oai4g_rx_pdsch_siso(&fp, (const int32_t *)ue->lte_ue_common_vars.rxdataF[0],
-                                    (const int32_t *)ue->lte_ue_common_vars.dl_ch_estimates[eNB_id][0],
-                                    h->rb_alloc_even, get_Qm(h->mcs), ue->lte_ue_pdcch_vars[eNB_id]->num_pdcch_symbols,
-                                    subframe, ue->lte_ue_pdsch_vars[eNB_id]->llr[0], &log2_maxh);
+  int n;
+  if (tm3) {
+    const int32_t *rxF[2], *est[4];
+    for (int a = 0; a < f->nb_antennas_rx; a++) {
+      rxF[a] = (const int32_t *)ue->lte_ue_common_vars.rxdataF[a];
+      est[a] = (const int32_t *)ue->lte_ue_common_vars.dl_ch_estimates[eNB_id][a];
+      est[2 + a] = (const int32_t *)ue->lte_ue_common_vars.dl_ch_estimates[eNB_id][2 + a];
+    }
+    LTE_DL_UE_HARQ_t *h1 = ue->dlsch_ue[eNB_id][1]->harq_processes[harq_pid];
+    n = oai4g_rx_pdsch_tm3(&fp, f->nb_antennas_rx, rxF, est, h->rb_alloc_even, get_Qm(h->mcs), get_Qm(h1->mcs),
+                           h->mcs, npdcch, subframe, ue->lte_ue_pdsch_vars[eNB_id]->llr[0], &log2_maxh);
+  } else {
+    n = oai4g_rx_pdsch_siso(&fp, (const int32_t *)ue->lte_ue_common_vars.rxdataF[0],
+                            (const int32_t *)ue->lte_ue_common_vars.dl_ch_estimates[eNB_id][0], h->rb_alloc_even,
+                            get_Qm(h->mcs), npdcch, subframe, ue->lte_ue_pdsch_vars[eNB_id]->llr[0], &log2_maxh);
+  }
   if (n < 0) return -1;
   ue->lte_ue_pdsch_vars[eNB_id]->log2_maxh = log2_maxh;
   return 0;

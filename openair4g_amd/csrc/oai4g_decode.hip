@@ -558,9 +558,10 @@ __global__ void __launch_bounds__(256) k_subblock_deint(uint32_t D, int16_t *__r
  * circular selection maps to p, 0 for NULL positions.  d1[2] is never written (the reference's
  * prefix slot), d1[3 Kpi + 2] is the d[3D + 2] entry the +5 of the last column produces. */
 __global__ void __launch_bounds__(256) k_ul_rm_deint(const ul_dev_t *__restrict__ c, const int16_t *__restrict__ e,
-                                                     size_t e_stride, int16_t *__restrict__ dfull, size_t d_stride)
+                                                     size_t e_stride, int16_t *__restrict__ dfull, size_t d_stride,
+                                                     uint32_t j0)
 {
-  const uint32_t j = blockIdx.y, tb = j / c->C, r = j - tb * c->C;
+  const uint32_t j = j0 + blockIdx.y, tb = j / c->C, r = j - tb * c->C;
   const ul_pat_t &P = c->pat[c->pat_of[r]];
   const uint32_t R = P.R, Kpi = R << 5, i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= 3 * Kpi + 3 || i == 2) return;
@@ -581,9 +582,15 @@ hipError_t oai4g_launch_ul_rm_deint(const ul_dev_t *d_cfg, const ul_dev_t *h_cfg
                                     size_t e_stride, int16_t *d_dfull, size_t d_stride, hipStream_t s)
 {
   if (n_tb <= 0) return hipSuccess;
-  hipLaunchKernelGGL(k_ul_rm_deint, dim3((3 * (h_cfg->Rmax << 5) + 3 + 255) / 256, n_tb * h_cfg->C), dim3(256), 0, s, d_cfg,
-                     d_e, e_stride, d_dfull, d_stride);
-  return hipGetLastError();
+  /* (tb, r) rows in chunks within the 65535 limit of gridDim.y */
+  const uint32_t rows = (uint32_t)n_tb * h_cfg->C, gx = (3 * (h_cfg->Rmax << 5) + 3 + 255) / 256;
+  for (uint32_t j0 = 0; j0 < rows; j0 += 65535u) {
+    const uint32_t n = rows - j0 < 65535u ? rows - j0 : 65535u;
+    hipLaunchKernelGGL(k_ul_rm_deint, dim3(gx, n), dim3(256), 0, s, d_cfg, d_e, e_stride, d_dfull, d_stride, j0);
+    const hipError_t err = hipGetLastError();
+    if (err != hipSuccess) return err;
+  }
+  return hipSuccess;
 }
 
 hipError_t oai4g_launch_rm_rx(const int16_t *d_soft, uint32_t E, int16_t *d_w, const uint8_t *d_dummy,

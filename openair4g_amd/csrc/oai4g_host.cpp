@@ -3496,20 +3496,66 @@ extern "C" int oai4g_rx_batch_tm3(oai4g_rx_config_t *cfg, int n_sf, const int32_
   return 0;
 }
 
+/* The rx_pdsch drop-ins' configurations, cached per calling thread (the UE calls rx_pdsch once per
+ * subframe with a handful of distinct (frame, allocation, modulation, subframe) keys; building one
+ * costs Gold generation, allocations and copies).  Round-robin over 32 entries; an evicted entry
+ * is destroyed.  Entries of an exiting thread are not reclaimed (the UE's threads live as long as
+ * the process, and tearing down device memory in thread-exit handlers can run after the HIP
+ * runtime is gone). */
+namespace {
+struct rx_key_t {
+  oai4g_frame_parms_t fp;
+  uint32_t rb_alloc[4];
+  uint8_t Qm, Qm1, mcs0, npdcch, subframe, tm3, nb_rx, pad;
+};
+struct rx_cache_t {
+  rx_key_t key[32];
+  oai4g_rx_config_t *cfg[32] = {};
+  int next = 0;
+};
+thread_local rx_cache_t t_rx_cache;
+
+oai4g_rx_config_t *rx_cached(const oai4g_frame_parms_t *fp, const uint32_t rb_alloc[4], uint8_t Qm, uint8_t Qm1,
+                             uint8_t mcs0, uint8_t npdcch, uint8_t subframe, int tm3, int nb_rx)
+{
+  rx_key_t k;
+  memset(&k, 0, sizeof(k));
+  k.fp = *fp;
+  memcpy(k.rb_alloc, rb_alloc, sizeof(k.rb_alloc));
+  k.Qm = Qm; k.Qm1 = Qm1; k.mcs0 = mcs0; k.npdcch = npdcch; k.subframe = subframe;
+  k.tm3 = (uint8_t)tm3; k.nb_rx = (uint8_t)nb_rx;
+  rx_cache_t &c = t_rx_cache;
+  for (int i = 0; i < 32; i++)
+    if (c.cfg[i] && memcmp(&c.key[i], &k, sizeof(k)) == 0) return c.cfg[i];
+  oai4g_rx_config_t *cfg = tm3 ? oai4g_rx_config_create_tm3(fp, rb_alloc, Qm, Qm1, mcs0, npdcch, 0, subframe, 1,
+                                                              (uint8_t)nb_rx)
+                               : oai4g_rx_config_create(fp, rb_alloc, Qm, npdcch, 0, subframe, 1);
+  if (!cfg) return nullptr;
+  const int slot = c.next;
+  c.next = (c.next + 1) % 32;
+  if (c.cfg[slot]) {
+    hipStreamSynchronize(g_scr.s);
+    oai4g_rx_config_destroy(c.cfg[slot]);
+  }
+  c.cfg[slot] = cfg;
+  c.key[slot] = k;
+  return cfg;
+}
+}  // namespace
+
 extern "C" int oai4g_rx_pdsch_tm3(const oai4g_frame_parms_t *fp, int nb_rx, const int32_t *const *rxdataF,
                                   const int32_t *const *dl_ch_estimates, const uint32_t rb_alloc[4], uint8_t Qm0,
                                   uint8_t Qm1, uint8_t mcs0, uint8_t num_pdcch_symbols, uint8_t subframe, int16_t *llr,
                                   uint8_t *log2_maxh)
 {
   NEED_INIT(-1);
-  oai4g_rx_config_t *cfg = oai4g_rx_config_create_tm3(fp, rb_alloc, Qm0, Qm1, mcs0, num_pdcch_symbols, 0, subframe, 1,
-                                                      (uint8_t)nb_rx);
+  oai4g_rx_config_t *cfg = rx_cached(fp, rb_alloc, Qm0, Qm1, mcs0, num_pdcch_symbols, subframe, 1, nb_rx);
   if (!cfg) return -1;
-  if (rx_check_batch(cfg, 1) != 0) { oai4g_rx_config_destroy(cfg); return -1; }
+  if (rx_check_batch(cfg, 1) != 0) return -1;
   const size_t gb = (size_t)cfg->h.nsymb * cfg->h.N * 4, gs = (gb + 255) & ~(size_t)255;
   const int n = (int)cfg->llr_count[subframe % 10];
   uint8_t *buf = scratch(6 * gs + (size_t)cfg->h.llr_stride * 2 + 256);
-  if (!buf) { oai4g_rx_config_destroy(cfg); return -1; }
+  if (!buf) return -1;
   int32_t *dy = (int32_t *)buf, *de = (int32_t *)(buf + 2 * gs);   /* [nb_rx][grid], planes [p * 2 + a] */
   int16_t *dl = (int16_t *)(buf + 6 * gs);
   bool ok = true;
@@ -3525,7 +3571,6 @@ extern "C" int oai4g_rx_pdsch_tm3(const oai4g_frame_parms_t *fp, int nb_rx, cons
     rc = n;
   else
     set_err("rx_pdsch_tm3: HIP error");
-  oai4g_rx_config_destroy(cfg);
   return rc;
 }
 
@@ -3534,13 +3579,13 @@ extern "C" int oai4g_rx_pdsch_siso(const oai4g_frame_parms_t *fp, const int32_t 
                                    int16_t *llr, uint8_t *log2_maxh)
 {
   NEED_INIT(-1);
-  oai4g_rx_config_t *cfg = oai4g_rx_config_create(fp, rb_alloc, Qm, num_pdcch_symbols, 0, subframe, 1);
+  oai4g_rx_config_t *cfg = rx_cached(fp, rb_alloc, Qm, 0, 0, num_pdcch_symbols, subframe, 0, 1);
   if (!cfg) return -1;
-  if (rx_check_batch(cfg, 1) != 0) { oai4g_rx_config_destroy(cfg); return -1; }
+  if (rx_check_batch(cfg, 1) != 0) return -1;
   const size_t gb = (size_t)cfg->h.nsymb * cfg->h.N * 4, gs = (gb + 255) & ~(size_t)255;
   const int n = (int)cfg->llr_count[subframe % 10];
   uint8_t *buf = scratch(2 * gs + (size_t)cfg->h.llr_stride * 2 + 256);
-  if (!buf) { oai4g_rx_config_destroy(cfg); return -1; }
+  if (!buf) return -1;
   int32_t *dy = (int32_t *)buf, *dh = (int32_t *)(buf + gs);
   int16_t *dl = (int16_t *)(buf + 2 * gs);
   int rc = -1;
@@ -3553,7 +3598,6 @@ extern "C" int oai4g_rx_pdsch_siso(const oai4g_frame_parms_t *fp, const int32_t 
     rc = n;
   else
     set_err("rx_pdsch_siso: HIP error");
-  oai4g_rx_config_destroy(cfg);
   return rc;
 }
 
@@ -3771,11 +3815,20 @@ extern "C" int oai4g_lte_dl_channel_estimation(const oai4g_frame_parms_t *fp, co
   if (!buf) return -1;
   chest_dev_t *dc = (chest_dev_t *)buf;
   int32_t *de = (int32_t *)(buf + cs), *dr = (int32_t *)(buf + cs + eb);
+  /* the call reads the previous pilot row and writes its own row plus the rows between the two
+   * (k_chest_symbol / ce_interp): only those rows cross PCIe */
+  const uint32_t prev_row = symbol == 0 ? p3 : symbol == p1 ? 0 : symbol == p2 ? p1 : p2;
+  const size_t rb = N * 4;
+  auto rows_d2h = [&](uint32_t r0, uint32_t n) {
+    return hipMemcpyAsync(dl_ch_estimates + (size_t)r0 * N, de + (size_t)r0 * N, n * rb, hipMemcpyDeviceToHost,
+                          g_scr.s) == hipSuccess;
+  };
   if (hipMemcpyAsync(dc, &h, sizeof(h), hipMemcpyHostToDevice, g_scr.s) != hipSuccess ||
-      hipMemcpyAsync(de, dl_ch_estimates, eb, hipMemcpyHostToDevice, g_scr.s) != hipSuccess ||
+      hipMemcpyAsync(de + (size_t)prev_row * N, dl_ch_estimates + (size_t)prev_row * N, rb, hipMemcpyHostToDevice,
+                     g_scr.s) != hipSuccess ||
       hipMemcpyAsync(dr, rxdataF + (size_t)symbol * N, N * 4, hipMemcpyHostToDevice, g_scr.s) != hipSuccess ||
       oai4g_launch_chest_symbol(dc, &h, dr, de, Ns, l, symbol, g_scr.s) != hipSuccess ||
-      hipMemcpyAsync(dl_ch_estimates, de, eb, hipMemcpyDeviceToHost, g_scr.s) != hipSuccess ||
+      !(symbol == 0 ? rows_d2h(p3 + 1, nsymb - 1 - p3) && rows_d2h(0, 1) : rows_d2h(prev_row + 1, symbol - prev_row)) ||
       hipStreamSynchronize(g_scr.s) != hipSuccess) {
     set_err("lte_dl_channel_estimation: HIP error");
     return -1;

@@ -58,3 +58,20 @@ def test_gpu_ul_chain_c5_batch(gpu):
             assert its[t, r] == it and np.array_equal(c[t, r, :len(d)], d), (t, r)
     assert np.all(its <= 8)                     # this SNR decodes every block
     ub.close()
+
+
+def test_gpu_ul_chain_rows_beyond_grid_y_limit(gpu):
+    """n_tb x C above gridDim.y's 65 535: k_ul_rm_deint runs in row chunks; the TBs on both sides
+    of every chunk boundary decode as the oracle does."""
+    tbs, G, Qm, n_tb = 16, 288, 2, 70000
+    e = _batch(tbs, G, Qm, n_tb, 9, 50, 20, n_unique=4)
+    ub = gpu.UlDecodeBatch(tbs + 24, G, Qm, n_tb, max_iterations=4)
+    assert ub.C == 1
+    ub.upload(e)
+    ub.launch()
+    its, c = ub.results()
+    for t in (0, 1, 65534, 65535, 65536, n_tb - 1):
+        ref = O.ulsch_decode(e[t], tbs + 24, G, Qm, max_it=4)
+        for r, (it, d) in enumerate(ref):
+            assert its[t, r] == it and np.array_equal(c[t, r, :len(d)], d), (t, r)
+    ub.close()
