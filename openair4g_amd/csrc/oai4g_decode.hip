@@ -410,7 +410,13 @@ __global__ void __launch_bounds__(64) k_td16(int n_cb, uint32_t K, const int16_t
   const uint32_t K1 = K >> 3, Kb = K >> 3;
   td_crc_tab(crctab, crc_type == 0 ? 0x864cfbu : 0x800063u);
   if (lane < 8) done_it[lane] = 0;
+#ifdef TD_DIAG_L2
+  /* DIAGNOSTIC ONLY (wrong results): the waves of a launch share TD_DIAG_L2 scratch regions, so the
+   * whole scratch working set stays in the L2s and the launch time is the kernel's no-HBM floor */
+  const td_blk_t W = td_layout(scratch + (size_t)(blockIdx.x % TD_DIAG_L2) * 8 * blk_bytes, K);
+#else
   const td_blk_t W = td_layout(scratch + (size_t)blockIdx.x * 8 * blk_bytes, K);
+#endif
   td_blk_t B;   /* this lane's block: element i at td_ix(i) */
   B.s0 = W.s0 + 8 * g; B.s1 = W.s1 + 8 * g; B.s2 = W.s2 + 8 * g; B.yp1 = W.yp1 + 8 * g; B.yp2 = W.yp2 + 8 * g;
   B.ext = W.ext + 8 * g; B.ext2 = W.ext2 + 8 * g; B.A = W.A + 8 * g;

@@ -296,7 +296,12 @@ __global__ void __launch_bounds__(64) k_td8(int n_cb, uint32_t K, const int16_t 
     crctab[v] = r;
   }
   if (lane < 4) done_it[lane] = 0;
+#ifdef TD_DIAG_L2
+  /* DIAGNOSTIC ONLY (wrong results): shared scratch regions, the working set stays in the L2s */
+  const td8_blk_t Wv = t8_layout(scratch + (size_t)(blockIdx.x % TD_DIAG_L2) * wave_bytes, K);
+#else
   const td8_blk_t Wv = t8_layout(scratch + (size_t)blockIdx.x * wave_bytes, K);
+#endif
   td8_blk_t B;
   B.s0 = Wv.s0 + 16 * g; B.s1 = Wv.s1 + 16 * g; B.s2 = Wv.s2 + 16 * g; B.yp1 = Wv.yp1 + 16 * g;
   B.yp2 = Wv.yp2 + 16 * g; B.ext = Wv.ext + 16 * g; B.ext2 = Wv.ext2 + 16 * g; B.A = Wv.A + 16 * g;
