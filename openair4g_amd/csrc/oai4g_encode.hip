@@ -727,6 +727,61 @@ static __device__ void encode_codeword(const cfg_dev_t *__restrict__ c, uint32_t
   uint32_t *ebuf = lds_base;
   for (uint32_t i = tid; i < Gw + 1; i += nth) ebuf[i] = 0u;
   __syncthreads();
+#ifndef OAI4G_ENC_RM_GENERIC
+  /* the host-built plan (cw.rm_src / rm_dst, oai4g_host.cpp rm_plan): per (block size, tile, lane)
+   * the stream bits to load and, after the transpose, where the column run goes */
+  {
+    const uint32_t lane32 = tid & 31, half = lane >> 5;
+    const uint32_t nt0 = __builtin_amdgcn_readfirstlane(cw.ntk[0]), nt1 = __builtin_amdgcn_readfirstlane(cw.ntk[1]);
+    const uint32_t ND0 = __builtin_amdgcn_readfirstlane(cw.NDk[0]), ND1 = __builtin_amdgcn_readfirstlane(cw.NDk[1]);
+    const uint32_t Nnn0 = __builtin_amdgcn_readfirstlane(cw.Nnnk[0]), Nnn1 = __builtin_amdgcn_readfirstlane(cw.Nnnk[1]);
+    const uint32_t es = __builtin_amdgcn_readfirstlane(cw.esplit[sfi]);
+    const uint32_t Elo = __builtin_amdgcn_readfirstlane(cw.E[sfi][0]), Ehi = __builtin_amdgcn_readfirstlane(cw.E[sfi][C - 1]);
+    /* no repetition (E <= Nnn for every block): a run lands once at most */
+    const bool once = Ehi <= min(Nnn0, Nnn1) && Elo <= min(Nnn0, Nnn1);
+    const uint32_t pp0 = (nt0 + 1) >> 1, pp1 = (nt1 + 1) >> 1;            /* tile pairs per block */
+    const uint32_t psplit = n0 * pp0, ptot = psplit + (C - n0) * pp1;
+    const uint32_t pm0 = ((1u << 20) + pp0 - 1) / pp0, pm1 = ((1u << 20) + pp1 - 1) / pp1;
+    for (uint32_t pw = wave; pw < ptot; pw += nwaves) {
+      const uint32_t P = __builtin_amdgcn_readfirstlane(pw);
+      const uint32_t ki = P >= psplit ? 1u : 0u, PP = ki ? P - psplit : P, pp = ki ? pp1 : pp0;
+      const uint32_t rr = (PP * (ki ? pm1 : pm0)) >> 20, rem = PP - rr * pp;
+      const uint32_t r = ki ? n0 + rr : rr, nt = ki ? nt1 : nt0, ND = ki ? ND1 : ND0;
+      const uint32_t t = 2 * rem + half, tc = t < nt ? t : nt - 1;
+      const uint32_t src = cw.rm_src[ki][tc][lane32];
+      const uint32_t dst = t < nt ? cw.rm_dst[ki][tc][lane32] : 0u;
+      const uint32_t *st = strm + __umul24(r * 3 + ((src >> 16) & 3u), sw);
+      const int pos = (int)(src & 0xffffu) - 64, wi = pos >> 5;             /* bits before 0 are NULLs */
+      uint32_t y = __builtin_amdgcn_alignbit(st[wi + 1], st[wi], (uint32_t)pos & 31u);
+      if (src & OAI4G_RM_SRC_LAST) {
+        y &= 0x7fffffffu;                       /* j = Kpi-1 reads y^(2)_0: NULL if ND > 0 */
+        if (ND == 0) y |= (st[0] & 1u) << 31;
+      }
+      y = transpose32(y, lane32);
+      const uint32_t m = (dst >> 21) & 63u;
+      if (m) {
+        const uint32_t z = (dst >> 16) & 31u, o = dst & 0xffffu;
+        y = (y >> z) & (0xffffffffu >> (32 - m));
+        const bool eh = r >= es;
+        const uint32_t E = eh ? Ehi : Elo, ro = eh ? es * Elo + (r - es) * Ehi : r * Elo;
+        if (once && !(dst & OAI4G_RM_DST_WRAP)) {
+          if (o < E) or_bits(ebuf, ro + o, y & (0xffffffffu >> (32 - min(m, E - o))));
+        } else {
+          /* the run may straddle the wrap back to k0c; E > Nnn repeats the buffer */
+          const uint32_t Nnn = ki ? Nnn1 : Nnn0, ma = min(m, Nnn - o);
+          for (uint32_t part = 0; part < 2; part++) {
+            const uint32_t len = part ? m - ma : ma, os = part ? 0u : o;
+            const uint32_t v = part ? (ma < 32 ? y >> ma : 0u) : (ma < 32 ? y & ((1u << ma) - 1u) : y);
+            for (uint32_t x = os; len && x < E; x += Nnn) {                     /* repetition rounds */
+              const uint32_t l = min(len, E - x);
+              or_bits(ebuf, ro + x, v & (0xffffffffu >> (32 - l)));
+            }
+          }
+        }
+      }
+    }
+  }
+#else
   {
     const uint32_t R0 = __builtin_amdgcn_readfirstlane(cw.Rk[0]), R1 = __builtin_amdgcn_readfirstlane(cw.Rk[1]);
     const uint32_t ND0 = __builtin_amdgcn_readfirstlane(cw.NDk[0]), ND1 = __builtin_amdgcn_readfirstlane(cw.NDk[1]);
@@ -820,6 +875,7 @@ static __device__ void encode_codeword(const cfg_dev_t *__restrict__ c, uint32_t
       }
     }
   }
+#endif
   __syncthreads();
   if (stop_phase <= 4) return;
 

@@ -670,6 +670,57 @@ struct oai4g_tx_config {
   int pipe_chunk = 0;
 };
 
+/* The sub-block interleaver + rate matcher plan of block size ki (k_encode phase 4;
+ * lte_rate_matching.c:51-130, 464-566).  Tile t: v0 tiles cover 32 rows of y0, interlaced tiles 16
+ * rows of y1 / y2 alternating per lane (lane 2i: y1 row, 2i + 1: y2 row, shifted by one for the
+ * (pi(k) + 1) mod Kpi rule).  After the half-wave's 32x32 transpose lane c holds matrix column c =
+ * w column bitrev5(c), rows of the tile: its NULLs (row 0 of the column) lead the run, and the
+ * run's place in the NULL-free circular buffer is closed-form. */
+static void rm_plan(cw_dev_t &c, int ki)
+{
+  const uint32_t R = c.Rk[ki], ND = c.NDk[ki], Ncb = c.Ncbk[ki], Nnn = c.Nnnk[ki], k0c = c.k0ck[ki];
+  const uint32_t tz = c.t0k[ki], nt = c.ntk[ki];
+  memset(c.rm_src[ki], 0, sizeof(c.rm_src[ki]));
+  memset(c.rm_dst[ki], 0, sizeof(c.rm_dst[ki]));
+  for (uint32_t t = 0; t < nt; t++) {
+    const bool il = t >= tz;
+    const uint32_t rb = il ? t - tz : t;
+    for (uint32_t L = 0; L < 32; L++) {
+      /* source: row of the tile this lane loads */
+      const uint32_t row = il ? 16 * rb + (L >> 1) : 32 * rb + L, s = il ? 1 + (L & 1) : 0;
+      if (row < R) {
+        const int pos = (int)(32 * row) - (int)ND + (s == 2 ? 1 : 0);
+        c.rm_src[ki][t][L] = (uint32_t)(pos + 64) | (s << 16) | (s == 2 && row == R - 1 ? OAI4G_RM_SRC_LAST : 0u);
+      } else {
+        c.rm_src[ki][t][L] = 64u;     /* past the last row: any bits, beyond the run */
+      }
+      /* destination: the run of matrix column L = w column wc */
+      uint32_t wc = 0;
+      for (int b = 0; b < 5; b++) wc |= ((L >> b) & 1u) << (4 - b);
+      uint32_t b0 = 0, b1 = 0;           /* NULL-headed w columns before wc in v0 / v1, v2 */
+      for (uint32_t w2 = 0; w2 < wc; w2++) {
+        uint32_t p2 = 0;
+        for (int b = 0; b < 5; b++) p2 |= ((w2 >> b) & 1u) << (4 - b);
+        b0 += p2 < ND ? 1u : 0u;
+        b1 += p2 + 1 < ND ? 1u : 0u;
+      }
+      const uint32_t z0 = L < ND ? 1u : 0u, z1 = z0 + (L + 1 < ND ? 1u : 0u);
+      const uint32_t zc = il ? z1 : z0;
+      const uint32_t cs = il ? 32 * R - ND + 2 * wc * R - b0 - b1 : wc * R - b0;   /* compact index of the column's first entry */
+      const uint32_t pc = il ? 32 * R + 2 * wc * R : wc * R;                       /* w position of the column start */
+      const int left = il ? 2 * ((int)R - 16 * (int)rb) : (int)R - 32 * (int)rb;
+      int n = left < 32 ? left : 32;
+      if (il && L == 31 && ND > 0 && left <= 32 && n) n--;                         /* w[3Kpi-1] is NULL */
+      const uint32_t z = rb ? 0u : zc, ci0 = rb ? cs + 32 * rb - zc : cs, p0 = pc + 32 * rb;
+      const int m = p0 + (uint32_t)n > Ncb ? (int)Ncb - (int)(p0 + z) : n - (int)z;   /* limited buffer */
+      if (m <= 0) continue;
+      uint32_t o = ci0 + Nnn - k0c;
+      o = o >= Nnn ? o - Nnn : o;
+      c.rm_dst[ki][t][L] = o | (z << 16) | ((uint32_t)m << 21) | (o + (uint32_t)m > Nnn ? OAI4G_RM_DST_WRAP : 0u);
+    }
+  }
+}
+
 static int derive_cfg(oai4g_tx_config *cfg, const oai4g_tx_params_t *p, const uint8_t Nl[2], bool need_remap,
                       int only_sf)
 {
@@ -860,6 +911,8 @@ static int derive_cfg(oai4g_tx_config *cfg, const oai4g_tx_params_t *p, const ui
       c.t0k[ki] = (c.Rk[ki] + 31) / 32;
       c.ntk[ki] = c.t0k[ki] + (c.Rk[ki] + 15) / 16;
       c.ntmag[ki] = ((1u << 20) + c.ntk[ki] - 1) / c.ntk[ki];
+      if (c.ntk[ki] > OAI4G_RM_TILES) { set_err("rate-matching plan: %u tiles", c.ntk[ki]); return -1; }
+      rm_plan(c, ki);
     }
     max_w = wwords > max_w ? wwords : max_w;
     uint32_t tbw = (c.A_bytes + 3 + 3) / 4 + 1;

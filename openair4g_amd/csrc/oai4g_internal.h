@@ -17,6 +17,9 @@
 #define OAI4G_MAX_NULLS 104
 #define OAI4G_MAX_CHUNKS 192                /* 6144 / 32 */
 #define OAI4G_MAX_TASKS (OAI4G_MAX_CB * 20)  /* ceil(R/32) + ceil(R/16) tiles per block, R <= 193 */
+#define OAI4G_RM_TILES 20                     /* ceil(R/32) + ceil(R/16) for R <= 193 */
+#define OAI4G_RM_SRC_LAST (1u << 20)
+#define OAI4G_RM_DST_WRAP (1u << 27)
 #define OAI4G_PIPE_MAX_CHUNKS 16
 #define OAI4G_CRS_CODE 0xE000u               /* remap codes >= this (and != 0xFFFF) are CRS REs:
                                                 CRS_CODE | pilot entry i << 9 | port & 1 << 8 | m */
@@ -103,6 +106,15 @@ struct cw_dev_t {
   uint32_t crc_per_cb;          /* bytes per lane, 64 lanes, CRC-24B per block */
   uint32_t crcmul_tb[8][6][16];
   uint32_t crcmul_cb[6][6][16];
+  /* sub-block interleaver + rate matcher plan per block size (k_encode phase 4), tile t of a
+   * block (v0 tiles of 32 rows, then interlaced tiles of 16 y1 / y2 row pairs), half-wave lane L:
+   *   rm_src: before the 32x32 transpose, the stream bits lane L loads: bit position (pos + 64),
+   *           stream s << 16, RM_SRC_LAST (stream-2 row R-1: bit 31 is y2_0, not a stream bit);
+   *   rm_dst: after it, the run of column lane L: circular offset o = (compact index - k0c) mod
+   *           Nnn, leading NULLs z << 16, run length m << 21 (0: nothing), RM_DST_WRAP when
+   *           o + m > Nnn. */
+  uint32_t rm_src[2][OAI4G_RM_TILES][32];
+  uint32_t rm_dst[2][OAI4G_RM_TILES][32];
 };
 
 struct cfg_dev_t {
