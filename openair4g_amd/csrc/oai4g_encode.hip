@@ -95,14 +95,18 @@ static constexpr rsc_tables_t make_rsc_tables()
 
 static constexpr rsc_tables_t k_rsc = make_rsc_tables();
 
-/* truncated carry-less product u * hz (compile-time constant taps) */
+/* truncated carry-less product u * hz.  hz = g / f over GF(2)[D] mod D^32 with the feedback
+ * f = 1 + D^2 + D^3 and the parity taps g = 1 + D + D^3; f divides 1 + D^7, so
+ * 1 / f = (1 + D^2 + D^3 + D^4)(1 + D^7 + D^14 + D^21 + D^28) mod D^32 and the product takes
+ * 13 shift / xor steps instead of one per tap of hz (20) */
 static __device__ __forceinline__ uint32_t rsc_parity_word(uint32_t u)
 {
-  uint32_t acc = 0;
-#pragma unroll
-  for (int i = 0; i < 32; i++)
-    if ((k_rsc.hz >> i) & 1u) acc ^= u << i;
-  return acc;
+  static_assert(k_rsc.hz == 0xe9d3a74fu, "RSC impulse response");
+  const uint32_t x = u ^ (u << 2) ^ (u << 3) ^ (u << 4);
+  uint32_t y = x ^ (x << 7);
+  y ^= y << 14;
+  y ^= x << 28;
+  return y ^ (y << 1) ^ (y << 3);
 }
 
 static __device__ __forceinline__ uint32_t rsc_exit_input(uint32_t u)
@@ -392,7 +396,7 @@ static __device__ __forceinline__ bool wwalk_null(const wwalk_t &w, uint32_t R, 
 }
 
 /* 32 bits of a packed LSB-first LDS bit array starting at bit `pos` (pos >= -32: zeros before 0) */
-static __device__ __forceinline__ uint32_t sx32(const uint32_t *a, int pos)
+[[maybe_unused]] static __device__ __forceinline__ uint32_t sx32(const uint32_t *a, int pos)
 {
   const int wi = pos >> 5;
   const uint32_t lo = a[(uint32_t)max(wi, 0)] & (wi >= 0 ? 0xffffffffu : 0u);
@@ -578,7 +582,7 @@ static __device__ void encode_codeword(const cfg_dev_t *__restrict__ c, uint32_t
    * stream slots of the block, plane 3 in region A behind the interleaved words. ---- */
   uint32_t *ilv = lds_base;
   const uint32_t nw = cw.ilv_off[C], u0 = cw.u0, n0 = cw.n0;
-  uint32_t *pl3 = lds_base + nw;
+  [[maybe_unused]] uint32_t *pl3 = lds_base + nw;
   /* word i of the interleaved space -> block r, word j, block size K (no per-lane table walks;
    * the two block sizes are read once as wave-uniform values, selects stay in registers) */
   const uint32_t kw0 = __builtin_amdgcn_readfirstlane(cw.kw[0]), kw1 = __builtin_amdgcn_readfirstlane(cw.kw[1]);
@@ -592,6 +596,78 @@ static __device__ void encode_codeword(const cfg_dev_t *__restrict__ c, uint32_t
     r = ki ? n0 + rr : rr;
     K = ki ? kk1 : kk0;
   };
+#ifndef OAI4G_ENC_QPP_WALK
+  /* byte-interleaved planes of every block, over x' < Q only: word w holds positions x' = 8w..8w+7,
+   * byte q = plane q (c[x' + qQ]); plane p at x = x' + uQ is byte (p + u) mod 4 there, so one
+   * rotate by 8u + (x' & 7) aligns all four bits of position x.  Built from four 32-bit plane words
+   * per 32 positions with byte permutes. */
+  uint32_t *bi = lds_base + nw;
+  for (uint32_t r = 0; r < C; r++) {
+    const uint32_t K = r < n0 ? kk0 : kk1, Kw = (K + 31) >> 5, Q = K >> 2, io = r < n0 ? r * kw0 : u0 + (r - n0) * kw1;
+    const uint32_t *sys = strm + r * 3 * sw;
+    for (uint32_t w = tid; w < Kw; w += nth) ilv[io + w] = 0u;
+    const uint32_t ng = (Q + 31) >> 5, nbw = (Q + 7) >> 3;
+    for (uint32_t g = tid; g < ng; g += nth) {
+      uint32_t P[4];
+#pragma unroll
+      for (uint32_t q = 0; q < 4; q++) {
+        const uint32_t src = 32 * g + q * Q, wi = src >> 5;                  /* src < K */
+        const uint32_t lo = sys[wi], hi = wi + 1 < Kw ? sys[wi + 1] : 0u;    /* bits >= K are zero */
+        uint32_t v = __builtin_amdgcn_alignbit(hi, lo, src);
+        if (src + 32 > K) v |= sys[0] << (K - src);                          /* wrap to c_0.. */
+        P[q] = v;
+      }
+#pragma unroll
+      for (uint32_t jb = 0; jb < 4; jb++) {
+        const uint32_t t01 = __builtin_amdgcn_perm(P[1], P[0], 0x0c0c0000u | jb | ((4 + jb) << 8));
+        const uint32_t t23 = __builtin_amdgcn_perm(P[3], P[2], 0x00000c0cu | (jb << 16) | ((4 + jb) << 24));
+        if (4 * g + jb < nbw) bi[io + 4 * g + jb] = t01 | t23;
+      }
+    }
+  }
+  __syncthreads();
+  {
+    /* 8-step units: unit j of block r walks k = 8j .. 8j+7 (< Q) through the host table and
+     * yields one byte of each quarter; ceil(K/32) units per block, indexed like the interleaved words */
+    const bool s3a = __builtin_amdgcn_readfirstlane(cw.qpp_s3[0]) != 0, s3b = __builtin_amdgcn_readfirstlane(cw.qpp_s3[1]) != 0;
+    for (uint32_t i = tid; i < nw; i += nth) {
+      uint32_t r, j, K, ki;
+      unit_of(i, r, j, K, ki);
+      (void)r;
+      const uint32_t Q = K >> 2;
+      const uint4 e4 = *(const uint4 *)&cw.qpp_tab[ki][4 * j];
+      const uint32_t ew[4] = {e4.x, e4.y, e4.z, e4.w};
+      const uint32_t *b8 = bi + (i - j);
+      uint32_t acc = 0;
+#pragma unroll
+      for (int b = 0; b < 8; b++) {
+        const uint32_t e = (ew[b >> 1] >> (16 * (b & 1))) & 0xffffu;
+        const uint32_t D = b8[e & 0x7ffu];
+        acc |= (__builtin_amdgcn_alignbit(D, D, e >> 11) & 0x01010101u) << b;
+      }
+      uint32_t a0 = acc & 0xffu, a1 = (acc >> 8) & 0xffu, a2 = (acc >> 16) & 0xffu, a3 = acc >> 24;
+      const uint32_t n = Q - 8 * j;
+      if (n < 8) {
+        const uint32_t m = (1u << n) - 1u;
+        a0 &= m; a1 &= m; a2 &= m; a3 &= m;
+      }
+      /* output quarter q reads plane (q c4 / Q) mod 4 */
+      const bool s3 = ki ? s3b : s3a;
+      const uint32_t q1 = s3 ? a3 : a1, q3 = s3 ? a1 : a3;
+      uint32_t *o = ilv + (i - j);
+      if ((Q & 7u) == 0) {                                  /* byte-aligned quarters (32 | K) */
+        uint8_t *ob = (uint8_t *)o + j;
+        const uint32_t qb = Q >> 3;
+        ob[0] = (uint8_t)a0; ob[qb] = (uint8_t)q1; ob[2 * qb] = (uint8_t)a2; ob[3 * qb] = (uint8_t)q3;
+      } else {
+        or_bits(o, 8 * j, a0);
+        or_bits(o, Q + 8 * j, q1);
+        or_bits(o, 2 * Q + 8 * j, a2);
+        or_bits(o, 3 * Q + 8 * j, q3);
+      }
+    }
+  }
+#else
   /* rotated planes 1..3 of every block: uniform loops over (block, plane), a word per lane */
   for (uint32_t r = 0; r < C; r++) {
     const uint32_t K = r < n0 ? kk0 : kk1, Kw = (K + 31) >> 5, Q = K >> 2, io = r < n0 ? r * kw0 : u0 + (r - n0) * kw1;
@@ -656,6 +732,7 @@ static __device__ void encode_codeword(const cfg_dev_t *__restrict__ c, uint32_t
       }
     }
   }
+#endif
   __syncthreads();
   if (stop_phase == 23) return;   /* diagnostics: QPP interleaving only */
 

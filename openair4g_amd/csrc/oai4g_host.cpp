@@ -823,6 +823,11 @@ static int derive_cfg(oai4g_tx_config *cfg, const oai4g_tx_params_t *p, const ui
         c.qpp0[ki][j] = pi | (((pi1 + K - pi) % K) << 16);
       }
       c.qpp_d2[ki] = (uint32_t)((2 * f2) % K);
+      memset(c.qpp_tab[ki], 0, sizeof(c.qpp_tab[ki]));
+      for (uint64_t k = 0; k < K / 4; k++) {
+        const uint32_t x = (uint32_t)((f1 * k + f2 * k * k) % K), Q = K / 4, xp = x % Q, u = x / Q;
+        c.qpp_tab[ki][k >> 1] |= ((xp >> 3) | ((8 * u + (xp & 7)) << 11)) << (16 * (k & 1));
+      }
       c.qpp_s3[ki] = (uint32_t)((f1 * (K / 4)) % K) == K / 4 ? 0u : 1u;
     }
     {

@@ -72,6 +72,10 @@ struct cw_dev_t {
    * Pi(8j) mod K) << 16, j < K/32, and the second difference 2 f2 mod K (3gpplte.c:50-74 restated
    * incrementally) */
   uint32_t qpp0[2][OAI4G_MAX_CHUNKS];
+  /* the quarter fold's walk as a table: entry k < K/4 (two uint16 per word) = word index of
+   * x' = Pi(k) mod K/4 in the byte-interleaved planes (x' >> 3) | shift (8 (Pi(k) div K/4) +
+   * (x' & 7)) << 11 */
+  alignas(16) uint32_t qpp_tab[2][OAI4G_MAX_CHUNKS * 4];
   uint32_t qpp_d2[2];
   /* quarter folding: Pi(k + K/4) = Pi(k) + c4 mod K with c4 = f1 K/4 mod K in {K/4, 3K/4}
    * (f2 even, 8 | K); qpp_s3 = (c4 == 3K/4) */
