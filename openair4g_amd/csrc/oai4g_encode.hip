@@ -211,13 +211,30 @@ static __device__ __forceinline__ uint32_t crc_chunk(const uint8_t *buf, uint32_
 }
 
 /* 6-level in-wave tree; mul = [6][6][16] tables; result valid in lane 0 */
-static __device__ __forceinline__ uint32_t crc_wave_tree(uint32_t reg, const uint32_t *mul)
+[[maybe_unused]] static __device__ __forceinline__ uint32_t crc_wave_tree(uint32_t reg, const uint32_t *mul)
 {
   const uint32_t lane = threadIdx.x & 63;
   for (int d = 0; d < 6; d++) {
     uint32_t other = __shfl_down(reg, 1u << d, 64);
     if ((lane & ((2u << d) - 1u)) == 0) reg = crc_mul_tab(reg, mul + d * 96) ^ other;
   }
+  return reg;
+}
+
+/* two-level in-wave combine (cw_dev_t crc2_*): every lane multiplies once by its position in its
+ * group of 8, the groups XOR-reduce, the group sums multiply by the group's position, the wave
+ * XOR-reduces; the result is in every lane.  Multiplier tables read from global memory (L1 / L2). */
+static __device__ __forceinline__ uint32_t crc_wave_tree2(uint32_t reg, const uint32_t (*mul)[8][96])
+{
+  const uint32_t lane = threadIdx.x & 63;
+  reg = crc_mul_tab(reg, mul[0][7 - (lane & 7)]);
+  reg ^= __shfl_xor(reg, 1, 64);
+  reg ^= __shfl_xor(reg, 2, 64);
+  reg ^= __shfl_xor(reg, 4, 64);
+  reg = crc_mul_tab(reg, mul[1][7 - (lane >> 3)]);
+  reg ^= __shfl_xor(reg, 8, 64);
+  reg ^= __shfl_xor(reg, 16, 64);
+  reg ^= __shfl_xor(reg, 32, 64);
   return reg;
 }
 
@@ -462,8 +479,6 @@ static __device__ void encode_codeword(const cfg_dev_t *__restrict__ c, uint32_t
   uint32_t *tbw = lds_base;
   uint32_t *crctab_a = tbw + c->lds_tb_words;
   uint32_t *crctab_b = crctab_a + 256;
-  uint32_t *mul_tb = crctab_b + 256;                     /* [8][6][16] */
-  uint32_t *mul_cb = mul_tb + 8 * 96;                    /* [6][6][16] */
   uint32_t *strm = lds_base + c->lds_a_words;
   uint32_t *tails = strm + c->lds_b_words;
   uint32_t *crcs = tails + 2 * OAI4G_MAX_CB;             /* [0] = CRC24A, [1+r] = CRC24B of block r */
@@ -493,16 +508,9 @@ static __device__ void encode_codeword(const cfg_dev_t *__restrict__ c, uint32_t
       const uint32_t w = ((cw.K[r] + 31) >> 5) + (i & 3u);
       if (w < sw) strm[slot * sw + w] = 0u;
     }
-    for (uint32_t i = ct; i < 8 * 96; i += cn) mul_tb[i] = (&cw.crcmul_tb[0][0][0])[i];
-    for (uint32_t i = ct; i < 6 * 96; i += cn) mul_cb[i] = (&cw.crcmul_cb[0][0][0])[i];
     for (uint32_t v = ct; v < 256; v += cn) {
-      uint32_t ra = v << 16, rb = v << 16;
-      for (int i = 0; i < 8; i++) {
-        ra = (ra & 0x800000u) ? ((ra << 1) ^ 0x864cfbu) & 0xffffffu : (ra << 1) & 0xffffffu;
-        rb = (rb & 0x800000u) ? ((rb << 1) ^ 0x800063u) & 0xffffffu : (rb << 1) & 0xffffffu;
-      }
-      crctab_a[v] = ra;
-      crctab_b[v] = rb;
+      crctab_a[v] = c->crctab[0][v];
+      crctab_b[v] = c->crctab[1][v];
     }
     for (uint32_t i = ct; i < 128; i += cn) {
       (&tabs->next[0][0])[i] = (&c_rsc.next[0][0])[i];
@@ -517,13 +525,13 @@ static __device__ void encode_codeword(const cfg_dev_t *__restrict__ c, uint32_t
   /* ---- phase 1: CRC-24A over the TB (dlsch_coding.c:296-300), 256 lanes ---- */
   {
     uint32_t reg = crc_chunk(tbb, Ab, cw.crc_per_tb, tid, nth, crctab_a);
-    reg = crc_wave_tree(reg, mul_tb);
+    reg = crc_wave_tree2(reg, cw.crc2_tb);
     if (lane == 0) red[wave] = reg;
     __syncthreads();
     if (tid == 0) {
-      uint32_t v01 = crc_mul_tab(red[0], mul_tb + 6 * 96) ^ red[1];
-      uint32_t v23 = crc_mul_tab(red[2], mul_tb + 6 * 96) ^ red[3];
-      uint32_t crc = crc_mul_tab(v01, mul_tb + 7 * 96) ^ v23;
+      uint32_t v01 = crc_mul_tab(red[0], cw.crcmul_tb[6][0]) ^ red[1];
+      uint32_t v23 = crc_mul_tab(red[2], cw.crcmul_tb[6][0]) ^ red[3];
+      uint32_t crc = crc_mul_tab(v01, cw.crcmul_tb[7][0]) ^ v23;
       tbb[Ab] = (uint8_t)(crc >> 16);
       tbb[Ab + 1] = (uint8_t)(crc >> 8);
       tbb[Ab + 2] = (uint8_t)crc;
@@ -536,7 +544,7 @@ static __device__ void encode_codeword(const cfg_dev_t *__restrict__ c, uint32_t
       uint32_t s0 = cw.src[r], n = cw.ncopy[r];
       if (s0 + n > Ab) n = Ab > s0 ? Ab - s0 : 0;
       uint32_t reg = crc_chunk(tbb + s0, n, cw.crc_per_cb, lane, 64, crctab_b);
-      reg = crc_wave_tree(reg, mul_cb);
+      reg = crc_wave_tree2(reg, cw.crc2_cb);
       if (lane == 0) crcs[1 + r] = reg;
     }
   }

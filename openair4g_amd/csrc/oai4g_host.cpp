@@ -496,6 +496,17 @@ static uint32_t crc_xpow8_h(uint64_t n, uint32_t poly)   /* x^(8n) mod P */
 }
 
 /* tab[d][k][v] = (v * x^(4k)) * x^(8*per*2^d) mod P, so a*m_d = xor_k tab[d][k][nibble_k(a)] */
+/* nibble tables of the two-level combine: [0][j] = x^(8 per j), [1][j] = x^(64 per j) mod P */
+static void crc_mul_tables2(uint32_t per, uint32_t poly, uint32_t (*tab)[8][96])
+{
+  for (int lv = 0; lv < 2; lv++)
+    for (uint32_t j = 0; j < 8; j++) {
+      const uint32_t m = crc_xpow8_h((uint64_t)per * j * (lv ? 8u : 1u), poly);
+      for (int k = 0; k < 6; k++)
+        for (uint32_t v = 0; v < 16; v++) tab[lv][j][16 * k + v] = crc_mulmod_h((v << (4 * k)) & 0xffffffu, m, poly);
+    }
+}
+
 static void crc_mul_tables(uint32_t per, int levels, uint32_t poly, uint32_t (*tab)[6][16])
 {
   for (int d = 0; d < levels; d++) {
@@ -766,6 +777,15 @@ static int derive_cfg(oai4g_tx_config *cfg, const oai4g_tx_params_t *p, const ui
   h.first_sf = p->first_subframe % 10;
   h.sf_step = p->subframe_step;
   h.payload_stride = p->payload_stride;
+  for (uint32_t v = 0; v < 256; v++) {            /* crc_byte.c:98-105 */
+    uint32_t ra = v << 16, rb = v << 16;
+    for (int i = 0; i < 8; i++) {
+      ra = (ra & 0x800000u) ? ((ra << 1) ^ 0x864cfbu) & 0xffffffu : (ra << 1) & 0xffffffu;
+      rb = (rb & 0x800000u) ? ((rb << 1) ^ 0x800063u) & 0xffffffu : (rb << 1) & 0xffffffu;
+    }
+    h.crctab[0][v] = ra;
+    h.crctab[1][v] = rb;
+  }
   uint32_t max_tb_words = 0, max_stream_words = 0, max_gw = 0, max_bits = 0, max_w = 0, max_inw = 0;
   bool rm_fail = false;
   for (int cw = 0; cw < p->n_cw; cw++) {
@@ -848,6 +868,7 @@ static int derive_cfg(oai4g_tx_config *cfg, const oai4g_tx_params_t *p, const ui
     }
     c.crc_per_tb = (((c.A_bytes + 255) / 256) + 3) & ~3u;   /* bytes per lane, a multiple of 4 */
     crc_mul_tables(c.crc_per_tb, 8, 0x864cfbu, c.crcmul_tb);
+    crc_mul_tables2(c.crc_per_tb, 0x864cfbu, c.crc2_tb);
     uint32_t ncb_max = 0;
     for (uint32_t r = 0; r < C; r++) {
       uint32_t n = c.ncopy[r];
@@ -856,6 +877,7 @@ static int derive_cfg(oai4g_tx_config *cfg, const oai4g_tx_params_t *p, const ui
     }
     c.crc_per_cb = (((ncb_max + 63) / 64) + 3) & ~3u;
     crc_mul_tables(c.crc_per_cb ? c.crc_per_cb : 1, 6, 0x800063u, c.crcmul_cb);
+    crc_mul_tables2(c.crc_per_cb ? c.crc_per_cb : 1, 0x800063u, c.crc2_cb);
     for (int ki = 0; ki < 2; ki++) {
       uint32_t K = ki == 0 ? (Km ? Km : Kp) : Kp;
       int n = null_positions(K, c.nullpos[ki], OAI4G_MAX_NULLS);

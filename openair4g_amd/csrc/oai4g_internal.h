@@ -24,7 +24,8 @@
 #define OAI4G_CRS_CODE 0xE000u               /* remap codes >= this (and != 0xFFFF) are CRS REs:
                                                 CRS_CODE | pilot entry i << 9 | port & 1 << 8 | m */
 #define OAI4G_CTL_CODE 0xC000u               /* remap code of a control-region RE (generate_dci_top) */
-#define OAI4G_ENC_CRC_TABLE_WORDS (256 + 256 + 8 * 96 + 6 * 96) /* byte tables A/B + tree multipliers */
+#define OAI4G_ENC_CRC_TABLE_WORDS (256 + 256) /* byte tables A/B (the combine multipliers stay in global memory;
+                                                  slice-by-4 tables, 2048 words, cost one workgroup per CU: slower) */
 #define OAI4G_GOLD_LANES 256
 #define OAI4G_GOLD_STRIDE 17   /* odd: lanes 17l + k hit distinct LDS banks */
 #define OAI4G_MAX_GOLD_WORDS (OAI4G_GOLD_LANES * OAI4G_GOLD_STRIDE) /* >= (14*1200*6)/32 */
@@ -110,6 +111,10 @@ struct cw_dev_t {
   uint32_t crc_per_cb;          /* bytes per lane, 64 lanes, CRC-24B per block */
   uint32_t crcmul_tb[8][6][16];
   uint32_t crcmul_cb[6][6][16];
+  /* two-level in-wave combine: lane l's chunk CRC times x^(8 per (7 - l mod 8)) ([0][j] = power
+   * j), XOR over the 8 lanes of its group, times x^(64 per (7 - l / 8)) ([1][j]), XOR over the wave */
+  uint32_t crc2_tb[2][8][96];
+  uint32_t crc2_cb[2][8][96];
   /* sub-block interleaver + rate matcher plan per block size (k_encode phase 4), tile t of a
    * block (v0 tiles of 32 rows, then interlaced tiles of 16 y1 / y2 row pairs), half-wave lane L:
    *   rm_src: before the 32x32 transpose, the stream bits lane L loads: bit position (pos + 64),
@@ -133,6 +138,7 @@ struct cfg_dev_t {
   uint32_t lds_a_words;         /* region A: TB + CRC tables (0-2) | interleaved words (3) | packed w (4) */
   uint32_t lds_b_words;         /* region B: constituent streams */
   uint32_t pad[2];
+  uint32_t crctab[2][256];      /* CRC byte tables (crc_byte.c:98-105): [0] CRC-24A, [1] CRC-24B */
   cw_dev_t cw[2];
   uint32_t symbase[10][14];     /* data REs before symbol l */
   uint16_t symnre[10][14];      /* data REs in symbol l */
