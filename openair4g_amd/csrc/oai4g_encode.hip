@@ -421,7 +421,14 @@ static __device__ __forceinline__ bool wwalk_null(const wwalk_t &w, uint32_t R, 
   return __builtin_amdgcn_alignbit(hi, lo, (uint32_t)pos & 31u);
 }
 
-/* lane l ^ J of the 32-lane half: DPP quad permutes for 1 and 2, ds_swizzle (bit mode) above */
+/* lane l ^ J of the 32-lane half without the LDS pipe: DPP quad permutes for 1 and 2, the half-row
+ * mirror (l ^ 7) then quad_perm [3,2,1,0] (l ^ 3) for 4, a row rotate by 8 for 8, and
+ * v_permlane16_swap for 16 (it swaps odd rows of its first operand with even rows of its second:
+ * with both = x, the second result holds row 1 in row 0 and the first holds row 0 in row 1) */
+#ifndef OAI4G_ENC_XOR_DPP
+/* lane l ^ J of the 32-lane half: DPP quad permutes for 1 and 2, ds_swizzle (bit mode) above.
+ * (OAI4G_ENC_XOR_DPP: the same without the LDS pipe, below; measured slower: the kernel is bound
+ * by VALU issue and the DPP forms of 4 / 16 take two VALU ops where ds_swizzle takes none) */
 template <uint32_t J>
 static __device__ __forceinline__ uint32_t xor_lane(uint32_t x)
 {
@@ -429,6 +436,24 @@ static __device__ __forceinline__ uint32_t xor_lane(uint32_t x)
   else if constexpr (J == 2) return (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0x4E, 0xf, 0xf, false); /* [2,3,0,1] */
   else return (uint32_t)__builtin_amdgcn_ds_swizzle((int)x, (int)((J << 10) | 0x1f));
 }
+#else
+template <uint32_t J>
+static __device__ __forceinline__ uint32_t xor_lane(uint32_t x)
+{
+  if constexpr (J == 1) return (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0xB1, 0xf, 0xf, false);   /* [1,0,3,2] */
+  else if constexpr (J == 2) return (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0x4E, 0xf, 0xf, false); /* [2,3,0,1] */
+  else if constexpr (J == 4) {
+    const int m = __builtin_amdgcn_mov_dpp((int)x, 0x141, 0xf, 0xf, false);                          /* half mirror */
+    return (uint32_t)__builtin_amdgcn_mov_dpp(m, 0x1B, 0xf, 0xf, false);                               /* [3,2,1,0] */
+  } else if constexpr (J == 8) {
+    return (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0x128, 0xf, 0xf, false);                         /* row_ror:8 */
+  } else {
+    static_assert(J == 16, "xor_lane");
+    const auto r = __builtin_amdgcn_permlane16_swap(x, x, false, false);
+    return (threadIdx.x & 16u) ? (uint32_t)r[0] : (uint32_t)r[1];
+  }
+}
+#endif
 
 /* 32x32 bit transpose across the 32 lanes of a half-wave: lane c ends with bit i = bit c of
  * lane i's input.  Branch-free butterfly: stage j exchanges the j-bit blocks that differ between
@@ -561,36 +586,9 @@ static __device__ void encode_codeword(const cfg_dev_t *__restrict__ c, uint32_t
     for (uint32_t i = tid; i < Ab + 3; i += nth) dbg.b[i] = tbb[i];
   if (stop_phase <= 1) return;
 
-  /* ---- phase 2: segmentation -> systematic streams (LSB-first words) ---- */
-  for (uint32_t r = 0; r < C; r++) {
-    uint32_t K = cw.K[r], nw = (K + 31) >> 5, fill = cw.fill[r], ncopy = cw.ncopy[r], s0 = cw.src[r];
-    uint32_t crcb = C > 1 ? crcs[1 + r] : 0;
-    uint32_t *sys = strm + r * 3 * sw;
-    for (uint32_t j = tid; j < nw; j += nth) {
-      uint32_t le = 0;
-      for (uint32_t q = 0; q < 4; q++) {
-        uint32_t i = 4 * j + q, byte = 0;
-        if (i < fill) byte = 0;
-        else if (i < fill + ncopy) byte = tbb[s0 + i - fill];
-        else if (C > 1 && i < fill + ncopy + 3) byte = (crcb >> (8 * (2 - (i - fill - ncopy)))) & 0xffu;
-        le |= byte << (8 * q);
-      }
-      uint32_t wv = bytes_to_seq(le);
-      if (32 * (j + 1) > K) wv &= (1u << (K - 32 * j)) - 1u;
-      sys[j] = wv;
-    }
-  }
-  __syncthreads();
-  if (stop_phase <= 2) return;
-
-  /* ---- phase 3a: QPP-interleaved input words of every block, folded by quarters.  With
-   * Q = K/4, Pi(k + qQ) = Pi(k) + q c4 (mod K), so one walk over k < Q reads output bits k, k+Q,
-   * k+2Q, k+3Q from four rotations of c at the same position Pi(k): plane_r[x] = c[(x + rQ) mod K].
-   * Plane 0 is the systematic stream, planes 1 / 2 are staged in the (not yet written) parity
-   * stream slots of the block, plane 3 in region A behind the interleaved words. ---- */
-  uint32_t *ilv = lds_base;
+  /* ---- phase 2: segmentation -> systematic streams (LSB-first words), one word per thread over
+   * the words of all blocks; a word inside the copied bytes is one unaligned 4-byte read ---- */
   const uint32_t nw = cw.ilv_off[C], u0 = cw.u0, n0 = cw.n0;
-  [[maybe_unused]] uint32_t *pl3 = lds_base + nw;
   /* word i of the interleaved space -> block r, word j, block size K (no per-lane table walks;
    * the two block sizes are read once as wave-uniform values, selects stay in registers) */
   const uint32_t kw0 = __builtin_amdgcn_readfirstlane(cw.kw[0]), kw1 = __builtin_amdgcn_readfirstlane(cw.kw[1]);
@@ -604,6 +602,41 @@ static __device__ void encode_codeword(const cfg_dev_t *__restrict__ c, uint32_t
     r = ki ? n0 + rr : rr;
     K = ki ? kk1 : kk0;
   };
+  for (uint32_t i = tid; i < nw; i += nth) {
+    uint32_t r, j, K, ki;
+    unit_of(i, r, j, K, ki);
+    (void)ki;
+    const uint32_t fill = cw.fill[r], ncopy = cw.ncopy[r], s0 = cw.src[r], i0 = 4 * j;
+    uint32_t le;
+    if (i0 >= fill && i0 + 4 <= fill + ncopy) {
+      const uint32_t a = s0 + i0 - fill, wi = a >> 2;
+      le = __builtin_amdgcn_alignbit(tbw[wi + 1], tbw[wi], (a & 3u) * 8u);
+    } else {
+      const uint32_t crcb = C > 1 ? crcs[1 + r] : 0;
+      le = 0;
+      for (uint32_t q = 0; q < 4; q++) {
+        const uint32_t ib = i0 + q;
+        uint32_t byte = 0;
+        if (ib < fill) byte = 0;
+        else if (ib < fill + ncopy) byte = tbb[s0 + ib - fill];
+        else if (C > 1 && ib < fill + ncopy + 3) byte = (crcb >> (8 * (2 - (ib - fill - ncopy)))) & 0xffu;
+        le |= byte << (8 * q);
+      }
+    }
+    uint32_t wv = bytes_to_seq(le);
+    if (32 * (j + 1) > K) wv &= (1u << (K - 32 * j)) - 1u;
+    strm[r * 3 * sw + j] = wv;
+  }
+  __syncthreads();
+  if (stop_phase <= 2) return;
+
+  /* ---- phase 3a: QPP-interleaved input words of every block, folded by quarters.  With
+   * Q = K/4, Pi(k + qQ) = Pi(k) + q c4 (mod K), so one walk over k < Q reads output bits k, k+Q,
+   * k+2Q, k+3Q from four rotations of c at the same position Pi(k): plane_r[x] = c[(x + rQ) mod K].
+   * Plane 0 is the systematic stream, planes 1 / 2 are staged in the (not yet written) parity
+   * stream slots of the block, plane 3 in region A behind the interleaved words. ---- */
+  uint32_t *ilv = lds_base;
+  [[maybe_unused]] uint32_t *pl3 = lds_base + nw;
 #ifndef OAI4G_ENC_QPP_WALK
   /* byte-interleaved planes of every block, over x' < Q only: word w holds positions x' = 8w..8w+7,
    * byte q = plane q (c[x' + qQ]); plane p at x = x' + uQ is byte (p + u) mod 4 there, so one
@@ -827,14 +860,36 @@ static __device__ void encode_codeword(const cfg_dev_t *__restrict__ c, uint32_t
     const uint32_t pp0 = (nt0 + 1) >> 1, pp1 = (nt1 + 1) >> 1;            /* tile pairs per block */
     const uint32_t psplit = n0 * pp0, ptot = psplit + (C - n0) * pp1;
     const uint32_t pm0 = ((1u << 20) + pp0 - 1) / pp0, pm1 = ((1u << 20) + pp1 - 1) / pp1;
+    /* tile pair P -> (block size, block, tile); its plan words are loaded one pair ahead */
+    auto decode = [&](uint32_t P, uint32_t &ki, uint32_t &r, uint32_t &t, uint32_t &tc) {
+      ki = P >= psplit ? 1u : 0u;
+      const uint32_t PP = ki ? P - psplit : P, pp = ki ? pp1 : pp0;
+      const uint32_t rr = (PP * (ki ? pm1 : pm0)) >> 20, rem = PP - rr * pp, nt = ki ? nt1 : nt0;
+      r = ki ? n0 + rr : rr;
+      t = 2 * rem + half;
+      tc = t < nt ? t : nt - 1;
+    };
+    uint32_t nsrc = 0, ndst = 0;
+    if (wave < ptot) {
+      uint32_t ki, r, t, tc;
+      decode(__builtin_amdgcn_readfirstlane(wave), ki, r, t, tc);
+      nsrc = cw.rm_src[ki][tc][lane32];
+      ndst = t < (ki ? nt1 : nt0) ? cw.rm_dst[ki][tc][lane32] : 0u;
+    }
     for (uint32_t pw = wave; pw < ptot; pw += nwaves) {
       const uint32_t P = __builtin_amdgcn_readfirstlane(pw);
-      const uint32_t ki = P >= psplit ? 1u : 0u, PP = ki ? P - psplit : P, pp = ki ? pp1 : pp0;
-      const uint32_t rr = (PP * (ki ? pm1 : pm0)) >> 20, rem = PP - rr * pp;
-      const uint32_t r = ki ? n0 + rr : rr, nt = ki ? nt1 : nt0, ND = ki ? ND1 : ND0;
-      const uint32_t t = 2 * rem + half, tc = t < nt ? t : nt - 1;
-      const uint32_t src = cw.rm_src[ki][tc][lane32];
-      const uint32_t dst = t < nt ? cw.rm_dst[ki][tc][lane32] : 0u;
+      uint32_t ki, r, t, tc;
+      decode(P, ki, r, t, tc);
+      (void)t; (void)tc;
+      const uint32_t ND = ki ? ND1 : ND0;
+      const uint32_t src = nsrc, dst = ndst;
+      if (P + nwaves < ptot) {
+        uint32_t k2, r2, t2, tc2;
+        decode(P + nwaves, k2, r2, t2, tc2);
+        (void)r2;
+        nsrc = cw.rm_src[k2][tc2][lane32];
+        ndst = t2 < (k2 ? nt1 : nt0) ? cw.rm_dst[k2][tc2][lane32] : 0u;
+      }
       const uint32_t *st = strm + __umul24(r * 3 + ((src >> 16) & 3u), sw);
       const int pos = (int)(src & 0xffffu) - 64, wi = pos >> 5;             /* bits before 0 are NULLs */
       uint32_t y = __builtin_amdgcn_alignbit(st[wi + 1], st[wi], (uint32_t)pos & 31u);
