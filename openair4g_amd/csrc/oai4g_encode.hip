@@ -849,7 +849,7 @@ static __device__ void encode_codeword(const cfg_dev_t *__restrict__ c, uint32_t
   /* the host-built plan (cw.rm_src / rm_dst, oai4g_host.cpp rm_plan): per (block size, tile, lane)
    * the stream bits to load and, after the transpose, where the column run goes */
   {
-    const uint32_t lane32 = tid & 31, half = lane >> 5;
+    const uint32_t lane32 = tid & 31;
     const uint32_t nt0 = __builtin_amdgcn_readfirstlane(cw.ntk[0]), nt1 = __builtin_amdgcn_readfirstlane(cw.ntk[1]);
     const uint32_t ND0 = __builtin_amdgcn_readfirstlane(cw.NDk[0]), ND1 = __builtin_amdgcn_readfirstlane(cw.NDk[1]);
     const uint32_t Nnn0 = __builtin_amdgcn_readfirstlane(cw.Nnnk[0]), Nnn1 = __builtin_amdgcn_readfirstlane(cw.Nnnk[1]);
@@ -860,42 +860,41 @@ static __device__ void encode_codeword(const cfg_dev_t *__restrict__ c, uint32_t
     const uint32_t pp0 = (nt0 + 1) >> 1, pp1 = (nt1 + 1) >> 1;            /* tile pairs per block */
     const uint32_t psplit = n0 * pp0, ptot = psplit + (C - n0) * pp1;
     const uint32_t pm0 = ((1u << 20) + pp0 - 1) / pp0, pm1 = ((1u << 20) + pp1 - 1) / pp1;
-    /* tile pair P -> (block size, block, tile); its plan words are loaded one pair ahead */
-    auto decode = [&](uint32_t P, uint32_t &ki, uint32_t &r, uint32_t &t, uint32_t &tc) {
+    /* tile pair P -> (block size, block, first tile); the pair's plan rows are contiguous, so a
+     * lane's plan words sit at a wave-uniform base + 4 lane.  Loaded one pair ahead. */
+    auto decode = [&](uint32_t P, uint32_t &ki, uint32_t &r, uint32_t &t0) {
       ki = P >= psplit ? 1u : 0u;
       const uint32_t PP = ki ? P - psplit : P, pp = ki ? pp1 : pp0;
-      const uint32_t rr = (PP * (ki ? pm1 : pm0)) >> 20, rem = PP - rr * pp, nt = ki ? nt1 : nt0;
+      const uint32_t rr = (PP * (ki ? pm1 : pm0)) >> 20, rem = PP - rr * pp;
       r = ki ? n0 + rr : rr;
-      t = 2 * rem + half;
-      tc = t < nt ? t : nt - 1;
+      t0 = 2 * rem;
     };
-    uint32_t nsrc = 0, ndst = 0;
+    uint32_t nsrc = 1u << 5, ndst = 0;
     if (wave < ptot) {
-      uint32_t ki, r, t, tc;
-      decode(__builtin_amdgcn_readfirstlane(wave), ki, r, t, tc);
-      nsrc = cw.rm_src[ki][tc][lane32];
-      ndst = t < (ki ? nt1 : nt0) ? cw.rm_dst[ki][tc][lane32] : 0u;
+      uint32_t ki, r, t0;
+      decode(__builtin_amdgcn_readfirstlane(wave), ki, r, t0);
+      nsrc = (&cw.rm_src[ki][t0][0])[lane];
+      ndst = (&cw.rm_dst[ki][t0][0])[lane];
     }
     for (uint32_t pw = wave; pw < ptot; pw += nwaves) {
       const uint32_t P = __builtin_amdgcn_readfirstlane(pw);
-      uint32_t ki, r, t, tc;
-      decode(P, ki, r, t, tc);
-      (void)t; (void)tc;
+      uint32_t ki, r, t0;
+      decode(P, ki, r, t0);
       const uint32_t ND = ki ? ND1 : ND0;
       const uint32_t src = nsrc, dst = ndst;
       if (P + nwaves < ptot) {
-        uint32_t k2, r2, t2, tc2;
-        decode(P + nwaves, k2, r2, t2, tc2);
+        uint32_t k2, r2, t2;
+        decode(P + nwaves, k2, r2, t2);
         (void)r2;
-        nsrc = cw.rm_src[k2][tc2][lane32];
-        ndst = t2 < (k2 ? nt1 : nt0) ? cw.rm_dst[k2][tc2][lane32] : 0u;
+        nsrc = (&cw.rm_src[k2][t2][0])[lane];
+        ndst = (&cw.rm_dst[k2][t2][0])[lane];
       }
-      const uint32_t *st = strm + __umul24(r * 3 + ((src >> 16) & 3u), sw);
-      const int pos = (int)(src & 0xffffu) - 64, wi = pos >> 5;             /* bits before 0 are NULLs */
-      uint32_t y = __builtin_amdgcn_alignbit(st[wi + 1], st[wi], (uint32_t)pos & 31u);
+      const uint32_t *bb = strm + r * 3 * sw - 1;                           /* block streams - 1 word */
+      const uint32_t *wp = bb + ((src >> 5) & 0x7fffu);
+      uint32_t y = __builtin_amdgcn_alignbit(wp[1], wp[0], src);            /* bits before 0 are NULLs */
       if (src & OAI4G_RM_SRC_LAST) {
         y &= 0x7fffffffu;                       /* j = Kpi-1 reads y^(2)_0: NULL if ND > 0 */
-        if (ND == 0) y |= (st[0] & 1u) << 31;
+        if (ND == 0) y |= (bb[1 + 2 * sw] & 1u) << 31;
       }
       y = transpose32(y, lane32);
       const uint32_t m = (dst >> 21) & 63u;

@@ -690,9 +690,10 @@ struct oai4g_tx_config {
 static void rm_plan(cw_dev_t &c, int ki)
 {
   const uint32_t R = c.Rk[ki], ND = c.NDk[ki], Ncb = c.Ncbk[ki], Nnn = c.Nnnk[ki], k0c = c.k0ck[ki];
-  const uint32_t tz = c.t0k[ki], nt = c.ntk[ki];
-  memset(c.rm_src[ki], 0, sizeof(c.rm_src[ki]));
+  const uint32_t tz = c.t0k[ki], nt = c.ntk[ki], sw = c.stream_words;
   memset(c.rm_dst[ki], 0, sizeof(c.rm_dst[ki]));
+  for (uint32_t t = 0; t <= OAI4G_RM_TILES; t++)
+    for (uint32_t L = 0; L < 32; L++) c.rm_src[ki][t][L] = 1u << 5;   /* idle: word 0 of stream 0 */
   for (uint32_t t = 0; t < nt; t++) {
     const bool il = t >= tz;
     const uint32_t rb = il ? t - tz : t;
@@ -700,11 +701,10 @@ static void rm_plan(cw_dev_t &c, int ki)
       /* source: row of the tile this lane loads */
       const uint32_t row = il ? 16 * rb + (L >> 1) : 32 * rb + L, s = il ? 1 + (L & 1) : 0;
       if (row < R) {
-        const int pos = (int)(32 * row) - (int)ND + (s == 2 ? 1 : 0);
-        c.rm_src[ki][t][L] = (uint32_t)(pos + 64) | (s << 16) | (s == 2 && row == R - 1 ? OAI4G_RM_SRC_LAST : 0u);
-      } else {
-        c.rm_src[ki][t][L] = 64u;     /* past the last row: any bits, beyond the run */
-      }
+        const int pos = (int)(32 * row) - (int)ND + (s == 2 ? 1 : 0);     /* >= -32 */
+        const uint32_t wrel = (uint32_t)((int)(s * sw) + (pos >> 5) + 1);
+        c.rm_src[ki][t][L] = ((uint32_t)pos & 31u) | (wrel << 5) | (s == 2 && row == R - 1 ? OAI4G_RM_SRC_LAST : 0u);
+      }   /* past the last row: the idle word (any bits, beyond the run) */
       /* destination: the run of matrix column L = w column wc */
       uint32_t wc = 0;
       for (int b = 0; b < 5; b++) wc |= ((L >> b) & 1u) << (4 - b);

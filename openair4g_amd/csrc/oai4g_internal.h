@@ -117,13 +117,14 @@ struct cw_dev_t {
   uint32_t crc2_cb[2][8][96];
   /* sub-block interleaver + rate matcher plan per block size (k_encode phase 4), tile t of a
    * block (v0 tiles of 32 rows, then interlaced tiles of 16 y1 / y2 row pairs), half-wave lane L:
-   *   rm_src: before the 32x32 transpose, the stream bits lane L loads: bit position (pos + 64),
-   *           stream s << 16, RM_SRC_LAST (stream-2 row R-1: bit 31 is y2_0, not a stream bit);
+   *   rm_src: before the 32x32 transpose, the stream bits lane L loads: bit shift (0..4) and LDS
+   *           word (5..19) relative to the block's streams minus one word (s sw + (pos >> 5) + 1),
+   *           RM_SRC_LAST (stream-2 row R-1: bit 31 is y2_0, not a stream bit);
    *   rm_dst: after it, the run of column lane L: circular offset o = (compact index - k0c) mod
    *           Nnn, leading NULLs z << 16, run length m << 21 (0: nothing), RM_DST_WRAP when
    *           o + m > Nnn. */
-  uint32_t rm_src[2][OAI4G_RM_TILES][32];
-  uint32_t rm_dst[2][OAI4G_RM_TILES][32];
+  uint32_t rm_src[2][OAI4G_RM_TILES + 1][32];   /* + one idle tile: a pair's second tile may be past nt */
+  uint32_t rm_dst[2][OAI4G_RM_TILES + 1][32];
 };
 
 struct cfg_dev_t {
