@@ -99,17 +99,24 @@ static constexpr rsc_tables_t k_rsc = make_rsc_tables();
  * f = 1 + D^2 + D^3 and the parity taps g = 1 + D + D^3; f divides 1 + D^7, so
  * 1 / f = (1 + D^2 + D^3 + D^4)(1 + D^7 + D^14 + D^21 + D^28) mod D^32 and the product takes
  * 13 shift / xor steps instead of one per tap of hz (20) */
-static __device__ __forceinline__ uint32_t rsc_parity_word(uint32_t u)
+/* v = u / f mod D^32: the feedback register's input sequence from the zero state, so bit k of v is
+ * the newest state bit after step k and the zero-start exit state (s2 s1 s0) = (v31 v30 v29) = v >> 29 */
+static __device__ __forceinline__ uint32_t rsc_feedback_word(uint32_t u)
 {
-  static_assert(k_rsc.hz == 0xe9d3a74fu, "RSC impulse response");
   const uint32_t x = u ^ (u << 2) ^ (u << 3) ^ (u << 4);
   uint32_t y = x ^ (x << 7);
   y ^= y << 14;
-  y ^= x << 28;
-  return y ^ (y << 1) ^ (y << 3);
+  return y ^ (x << 28);
+}
+/* zero-start parity word = v g */
+static __device__ __forceinline__ uint32_t rsc_parity_of_feedback(uint32_t v) { return v ^ (v << 1) ^ (v << 3); }
+[[maybe_unused]] static __device__ __forceinline__ uint32_t rsc_parity_word(uint32_t u)
+{
+  static_assert(k_rsc.hz == 0xe9d3a74fu, "RSC impulse response");
+  return rsc_parity_of_feedback(rsc_feedback_word(u));
 }
 
-static __device__ __forceinline__ uint32_t rsc_exit_input(uint32_t u)
+[[maybe_unused]] static __device__ __forceinline__ uint32_t rsc_exit_input(uint32_t u)
 {
   return (__builtin_popcount(u & k_rsc.fm[0]) & 1u) | ((__builtin_popcount(u & k_rsc.fm[1]) & 1u) << 1) |
          ((__builtin_popcount(u & k_rsc.fm[2]) & 1u) << 2);
@@ -149,7 +156,7 @@ typedef const __attribute__((address_space(1))) uint32_t gu32_t;
 /* Gold words 0..nwords-1 (word w = state after 50+w steps): lane l jumps to word S l with the
  * host's M^(50+S l) tables and steps S = OAI4G_GOLD_STRIDE words.  Needs blockDim.x ==
  * OAI4G_GOLD_LANES. */
-static __device__ __forceinline__ void gold_generate(uint32_t *gold, uint32_t nwords, uint32_t c_init,
+[[maybe_unused]] static __device__ __forceinline__ void gold_generate(uint32_t *gold, uint32_t nwords, uint32_t c_init,
                                                      const uint32_t *gx1, const uint32_t *gx2j)
 {
   const uint32_t l = threadIdx.x, w0 = OAI4G_GOLD_STRIDE * l;
@@ -313,16 +320,17 @@ static __device__ __forceinline__ void turbo_segment(const uint32_t *in, uint32_
   const uint32_t lane = threadIdx.x & 63;
   const uint32_t nch = (K + 31) >> 5;
   const uint32_t lq = nch <= 64 ? 0 : (nch <= 128 ? 1 : 2), qp = 1u << lq;
-  uint32_t u[4];
+  uint32_t u[4], v[4];
   uint32_t S = 0;
 #pragma unroll
   for (int t = 0; t < 4; t++) {
     u[t] = 0;
     uint32_t j = lane * qp + t;
     if (t < (int)qp && j < nch) u[t] = in[j];
-    /* zero-start exit state of a full chunk: A^32 contribution of the inputs (partial chunks
+    /* zero-start exit state of a full chunk: the feedback word's last three bits (partial chunks
      * only feed later lanes, whose values are not used) */
-    if (t < (int)qp) S = tb->apow[0][S] ^ rsc_exit_input(u[t]);
+    v[t] = rsc_feedback_word(u[t]);
+    if (t < (int)qp) S = tb->apow[0][S] ^ (v[t] >> 29);
   }
   /* inclusive scan over lanes: S_l ^= A^(32 qp 2^d) S_(l - 2^d) */
 #pragma unroll
@@ -337,12 +345,12 @@ static __device__ __forceinline__ void turbo_segment(const uint32_t *in, uint32_
     uint32_t j = lane * qp + t;
     if (t < (int)qp && j < nch) {
       uint32_t n = min(32u, K - 32 * j);
-      uint32_t par = rsc_parity_word(u[t]) ^ tb->zs[s];
+      uint32_t par = rsc_parity_of_feedback(v[t]) ^ tb->zs[s];
       if (n < 32) {
         par &= (1u << n) - 1u;
         for (uint32_t q = 0; q < (n >> 2); q++) s = tb->next[s][(u[t] >> (4 * q)) & 15u];
       } else {
-        s = tb->apow[0][s] ^ rsc_exit_input(u[t]);
+        s = tb->apow[0][s] ^ (v[t] >> 29);
       }
       par_out[j] = par;
       if (j == nch - 1) {
@@ -1022,14 +1030,10 @@ static __device__ void encode_codeword(const cfg_dev_t *__restrict__ c, uint32_t
     for (uint32_t k = tid; k < G; k += nth) dbg.e[k] = (uint8_t)((ebuf[k >> 5] >> (k & 31)) & 1u);
     return;
   }
-  /* scrambling (dlsch_scrambling.c:51-97): Gold words into region B (the streams are dead), XORed
-   * into the RM output on the way out */
-  uint32_t *gold = strm;
-  if (tid < OAI4G_GOLD_LANES) {
-    const uint32_t c_init = (c->rnti << 14) + (cw.q << 13) + (sfi << 9) + c->Nid_cell; /* Ns>>1 = subframe */
-    gold_generate(gold, Gw, c_init, c->gold_x1, c->gold_x2j);
-  }
-  __syncthreads();
+  /* scrambling (dlsch_scrambling.c:51-97): c_init = rnti 2^14 + q 2^13 + subframe 2^9 + Nid_cell
+   * depends only on (subframe index, codeword), so the Gold words come from the configuration's
+   * table (L2-resident) and are XORed into the RM output on the way out */
+  gu32_t *gold = (gu32_t *)(c->gold_tab + (size_t)(sfi * c->n_cw + cwi) * c->ebits_words);
   uint32_t *eout = ebits + (size_t)(sf * c->n_cw + cwi) * c->ebits_words;
   for (uint32_t i = tid; i < Gw; i += nth) {
     uint32_t v = ebuf[i] ^ gold[i];

@@ -664,6 +664,7 @@ struct oai4g_tx_config {
   uint16_t *d_remap = nullptr;
   std::vector<uint16_t> h_remap;
   uint32_t *d_crs = nullptr;
+  uint32_t *d_gold = nullptr;           /* [10][n_cw][ebits_words] scrambling words */
   std::vector<uint32_t> h_crs;          /* [10][4][200] packed CRS IQ */
   uint32_t *d_ctl = nullptr;            /* static RE values [10][14][2][N] (set_control / set_common) */
   std::vector<oai4g_dci_alloc_t> dci;   /* oai4g_tx_config_set_control's DCI set */
@@ -1082,9 +1083,43 @@ static int upload_remap(oai4g_tx_config *cfg)
   return 0;
 }
 
+/* the scrambling words of every (subframe index, codeword): lte_gold_generic (lte_gold.c:151-177)
+ * with c_init = rnti 2^14 + q 2^13 + subframe 2^9 + Nid_cell (dlsch_scrambling.c:74-76) */
+static int upload_gold(oai4g_tx_config *cfg)
+{
+  const cfg_dev_t &h = cfg->h;
+  const size_t stride = h.ebits_words;
+  std::vector<uint32_t> g((size_t)10 * h.n_cw * stride, 0u);
+  for (uint32_t sf = 0; sf < 10; sf++)
+    for (uint32_t cw = 0; cw < h.n_cw; cw++) {
+      const uint32_t c_init = (h.rnti << 14) + (h.cw[cw].q << 13) + (sf << 9) + h.Nid_cell;
+      uint32_t x1 = 1u + (1u << 31), x2 = c_init ^ ((c_init ^ (c_init >> 1) ^ (c_init >> 2) ^ (c_init >> 3)) << 31);
+      auto step = [&]() {
+        x1 = (x1 >> 1) ^ (x1 >> 4);
+        x1 = x1 ^ (x1 << 31) ^ (x1 << 28);
+        x2 = (x2 >> 1) ^ (x2 >> 2) ^ (x2 >> 3) ^ (x2 >> 4);
+        x2 = x2 ^ (x2 << 31) ^ (x2 << 30) ^ (x2 << 29) ^ (x2 << 28);
+      };
+      for (int n = 1; n < 50; n++) step();
+      const size_t nw = std::min(stride, (size_t)(h.cw[cw].G[sf] + 31) / 32);
+      uint32_t *o = g.data() + ((size_t)sf * h.n_cw + cw) * stride;
+      for (size_t w = 0; w < nw; w++) {
+        step();
+        o[w] = x1 ^ x2;
+      }
+    }
+  if (cfg->d_gold) hipFree(cfg->d_gold);
+  cfg->d_gold = nullptr;
+  HCK(hipMalloc(&cfg->d_gold, g.size() * 4), -1);
+  HCK(hipMemcpy(cfg->d_gold, g.data(), g.size() * 4, hipMemcpyHostToDevice), -1);
+  cfg->h.gold_tab = cfg->d_gold;
+  return 0;
+}
+
 static int upload_cfg(oai4g_tx_config *cfg)
 {
   if (upload_remap(cfg) != 0) return -1;
+  if (upload_gold(cfg) != 0) return -1;
   if (!cfg->h_crs.empty()) {
     HCK(hipMalloc(&cfg->d_crs, cfg->h_crs.size() * 4), -1);
     HCK(hipMemcpy(cfg->d_crs, cfg->h_crs.data(), cfg->h_crs.size() * 4, hipMemcpyHostToDevice), -1);
@@ -1112,6 +1147,8 @@ static void release_cfg(oai4g_tx_config *cfg)
   if (cfg->d_remap) hipFree(cfg->d_remap);
   if (cfg->d_crs) hipFree(cfg->d_crs);
   if (cfg->d_ctl) hipFree(cfg->d_ctl);
+  if (cfg->d_gold) hipFree(cfg->d_gold);
+  cfg->d_gold = nullptr;
   cfg->d_crs = nullptr;
   cfg->d_ctl = nullptr;
   cfg->d = nullptr;

@@ -156,6 +156,8 @@ struct cfg_dev_t {
                                    0 / 1) per subframe index; REs with code OAI4G_CTL_CODE take it */
   uint32_t ctlmask[10];         /* bit l: symbol l of subframe index sf carries control REs */
   uint32_t ctl_on;
+  const uint32_t *gold_tab;     /* [10][n_cw][ebits_words] scrambling words (dlsch_scrambling.c:51-97) per
+                                   subframe index and codeword: c_init depends on nothing else */
   const uint32_t *gold_x1;      /* [256]     x1 state after 50+16l word steps */
   const uint32_t *gold_x2j;     /* [256][32] columns of M2^(50+16l) */
   const uint32_t *tw;           /* 2 x OAI4G_TW_TOTAL packed twiddles t, then (-t.im, t.re) */
