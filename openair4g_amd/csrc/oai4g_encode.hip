@@ -217,6 +217,29 @@ static __device__ __forceinline__ uint32_t crc_chunk(const uint8_t *buf, uint32_
   return reg;
 }
 
+/* lane chunk CRC over 4-byte words: bytes [lane per, (lane + 1) per) of the message base8 + start
+ * of nbytes bytes, virtually front-padded to nl per bytes (per % 4 == 0; the zero bytes in front
+ * leave the zero register unchanged), one unaligned word read per 4 bytes.  The register is kept
+ * in the top 24 bits (tab8[v] = crc_byte.c's table entry << 8), so a byte step is
+ * reg = (reg << 8) ^ tab8[(reg >> 24) ^ byte]. */
+static __device__ __forceinline__ uint32_t crc_chunk_w(const uint32_t *base32, uint32_t start, uint32_t nbytes,
+                                                       uint32_t per, uint32_t lane, uint32_t nl, const uint32_t *tab8)
+{
+  const int vstart = (int)(lane * per) - (int)(per * nl - nbytes);
+  uint32_t reg = 0;
+  for (uint32_t i = 0; i < per; i += 4) {
+    const int o = vstart + (int)i;
+    const uint32_t a = start + (uint32_t)(o > 0 ? o : 0), wi = a >> 2;
+    uint32_t w = __builtin_amdgcn_alignbit(base32[wi + 1], base32[wi], (a & 3u) * 8u);
+    if (o < 0) w = o <= -4 ? 0u : w << (8 * (uint32_t)(-o));   /* bytes before the message are zero */
+    reg = (reg << 8) ^ tab8[(reg >> 24) ^ (w & 0xffu)];
+    reg = (reg << 8) ^ tab8[(reg >> 24) ^ ((w >> 8) & 0xffu)];
+    reg = (reg << 8) ^ tab8[(reg >> 24) ^ ((w >> 16) & 0xffu)];
+    reg = (reg << 8) ^ tab8[(reg >> 24) ^ (w >> 24)];
+  }
+  return reg >> 8;
+}
+
 /* 6-level in-wave tree; mul = [6][6][16] tables; result valid in lane 0 */
 [[maybe_unused]] static __device__ __forceinline__ uint32_t crc_wave_tree(uint32_t reg, const uint32_t *mul)
 {
@@ -541,9 +564,9 @@ static __device__ void encode_codeword(const cfg_dev_t *__restrict__ c, uint32_t
       const uint32_t w = ((cw.K[r] + 31) >> 5) + (i & 3u);
       if (w < sw) strm[slot * sw + w] = 0u;
     }
-    for (uint32_t v = ct; v < 256; v += cn) {
-      crctab_a[v] = c->crctab[0][v];
-      crctab_b[v] = c->crctab[1][v];
+    for (uint32_t v = ct; v < 256; v += cn) {     /* the register-in-the-top-24-bits form */
+      crctab_a[v] = c->crctab[0][v] << 8;
+      crctab_b[v] = c->crctab[1][v] << 8;
     }
     for (uint32_t i = ct; i < 128; i += cn) {
       (&tabs->next[0][0])[i] = (&c_rsc.next[0][0])[i];
@@ -557,7 +580,7 @@ static __device__ void encode_codeword(const cfg_dev_t *__restrict__ c, uint32_t
 
   /* ---- phase 1: CRC-24A over the TB (dlsch_coding.c:296-300), 256 lanes ---- */
   {
-    uint32_t reg = crc_chunk(tbb, Ab, cw.crc_per_tb, tid, nth, crctab_a);
+    uint32_t reg = crc_chunk_w(tbw, 0, Ab, cw.crc_per_tb, tid, nth, crctab_a);
     reg = crc_wave_tree2(reg, cw.crc2_tb);
     if (lane == 0) red[wave] = reg;
     __syncthreads();
@@ -576,7 +599,7 @@ static __device__ void encode_codeword(const cfg_dev_t *__restrict__ c, uint32_t
     for (uint32_t r = wave; r < C; r += nwaves) {
       uint32_t s0 = cw.src[r], n = cw.ncopy[r];
       if (s0 + n > Ab) n = Ab > s0 ? Ab - s0 : 0;
-      uint32_t reg = crc_chunk(tbb + s0, n, cw.crc_per_cb, lane, 64, crctab_b);
+      uint32_t reg = crc_chunk_w(tbw, s0, n, cw.crc_per_cb, lane, 64, crctab_b);
       reg = crc_wave_tree2(reg, cw.crc2_cb);
       if (lane == 0) crcs[1 + r] = reg;
     }
@@ -585,7 +608,7 @@ static __device__ void encode_codeword(const cfg_dev_t *__restrict__ c, uint32_t
   if (C > 1 && tid == 0) {
     for (uint32_t r = 0; r < C; r++) {
       uint32_t s0 = cw.src[r], e0 = s0 + cw.ncopy[r], reg = crcs[1 + r];
-      for (uint32_t i = (s0 > Ab ? s0 : Ab); i < e0; i++) reg = crc_step(reg, tbb[i], crctab_b);
+      for (uint32_t i = (s0 > Ab ? s0 : Ab); i < e0; i++) reg = ((reg << 8) & 0xffffffu) ^ (crctab_b[((reg >> 16) ^ tbb[i]) & 0xffu] >> 8);
       crcs[1 + r] = reg;
     }
   }
