@@ -635,16 +635,7 @@ __global__ void __launch_bounds__(128) MODOFDM_ATTR k_modofdm(const cfg_dev_t *_
   constexpr uint32_t IPS = MODE == 3 ? 2u : 1u;   /* items per (subframe, symbol) */
   __shared__ uint32_t lds_data[UNITS * NA * LDSW];
   __shared__ uint32_t lds_e[UNITS][2][EW];
-#ifndef OAI4G_MOD_QPAIR
   __shared__ uint32_t qtab[2][2][64];          /* [cw][pilot symbol][Qm bits] -> packed IQ */
-#else
-  /* the same table as 32 eight-byte slots (entries k, k + 32): a ds_read_b64 lookup's bank pair is
-   * the slot's own, so the 32 lanes of a half never conflict (a 64-entry b32 table puts entries k
-   * and k + 32 on one bank) */
-  __shared__ uint64_t qtab2[2][2][32];
-  uint32_t *qtab_w = (uint32_t *)qtab2;
-#define qtab(cw, pil, bits) qtab_w[(((cw) * 2 + (pil)) * 32 + ((bits) & 31u)) * 2 + ((bits) >> 5)]
-#endif
   const int unit = threadIdx.x / T, t = threadIdx.x % T;
   typename idft_sel<LOG2N>::tw_t twr;
   twr.load(c->tw, t);
@@ -654,18 +645,10 @@ __global__ void __launch_bounds__(128) MODOFDM_ATTR k_modofdm(const cfg_dev_t *_
     const uint32_t cw = i >> 7, pil = (i >> 6) & 1, bits = i & 63;
     if constexpr (MODE == 1) {          /* one codeword: [0] = TA, [1] = TB */
       const cw_dev_t &w = c->cw[0];
-#ifndef OAI4G_MOD_QPAIR
       qtab[cw][pil][bits] = c2u(cw ? alm_tb(bits, w, pil) : alm_ta(bits, w, pil));
-#else
-      qtab(cw, pil, bits) = c2u(cw ? alm_tb(bits, w, pil) : alm_ta(bits, w, pil));
-#endif
     } else {
       const cw_dev_t &w = c->cw[cw];
-#ifndef OAI4G_MOD_QPAIR
       qtab[cw][pil][bits] = c2u(qam_map(bits, w.Qm, pil ? w.qam_b : w.qam_a, pil ? w.qpsk_b : w.qpsk_a));
-#else
-      qtab(cw, pil, bits) = c2u(qam_map(bits, w.Qm, pil ? w.qam_b : w.qam_a, pil ? w.qpsk_b : w.qpsk_a));
-#endif
     }
   }
   const uint32_t Qm0 = c->cw[0].Qm, Qm1 = c->cw[1].Qm;
@@ -757,13 +740,7 @@ __global__ void __launch_bounds__(128) MODOFDM_ATTR k_modofdm(const cfg_dev_t *_
     const bool crs = CRS && stat_sym;
     gu32_t *ctl_tab = (gu32_t *)c->ctl_tab;
     const uint32_t *e0 = lds_e[unit][0], *e1 = lds_e[unit][1];
-#ifndef OAI4G_MOD_QPAIR
     const uint32_t *q0 = qtab[0][pil], *q1 = qtab[1][pil];
-#define QLOOK(q, b) (q)[b]
-#else
-    const uint64_t *q0 = qtab2[0][pil], *q1 = qtab2[1][pil];
-#define QLOOK(q, b) ((uint32_t)((q)[(b) & 31u] >> ((b) & 32u)))
-#endif
     /* bit position of data RE idx within the staged words: idx * Qm + (re0 * Qm - 32 wlo) */
     const uint32_t b0 = re0 * Qm0 - 32 * wlo0, b1 = re0 * Qm1 - 32 * wlo1;
     idft_any<LOG2N, NA>(
@@ -799,12 +776,12 @@ __global__ void __launch_bounds__(128) MODOFDM_ATTR k_modofdm(const cfg_dev_t *_
 #pragma unroll
               for (int n = 0; n < GR; n++) {
                 const uint32_t wv = __builtin_amdgcn_alignbit(hi[n], lo[n], p[n] & 31);
-                v0[n] = QLOOK(q0, wv & mask0);
-                v1[n] = QLOOK(q1, (wv >> Qm0) & mask0);
+                v0[n] = q0[wv & mask0];
+                v1[n] = q1[(wv >> Qm0) & mask0];
               }
             } else {
 #pragma unroll
-              for (int n = 0; n < GR; n++) v0[n] = QLOOK(q0, __builtin_amdgcn_alignbit(hi[n], lo[n], p[n] & 31) & mask0);
+              for (int n = 0; n < GR; n++) v0[n] = q0[__builtin_amdgcn_alignbit(hi[n], lo[n], p[n] & 31) & mask0];
             }
             if constexpr (CW2) {
 #pragma unroll
@@ -814,7 +791,7 @@ __global__ void __launch_bounds__(128) MODOFDM_ATTR k_modofdm(const cfg_dev_t *_
                 hi[n] = e1[(p[n] >> 5) + 1];
               }
 #pragma unroll
-              for (int n = 0; n < GR; n++) v1[n] = QLOOK(q1, __builtin_amdgcn_alignbit(hi[n], lo[n], p[n] & 31) & mask1);
+              for (int n = 0; n < GR; n++) v1[n] = q1[__builtin_amdgcn_alignbit(hi[n], lo[n], p[n] & 31) & mask1];
             }
 #pragma unroll
             for (int n = 0; n < GR; n++) {
