@@ -282,6 +282,20 @@ oai4g_rx_config_t *oai4g_rx_config_create_tm3(const oai4g_frame_parms_t *frame_p
 int oai4g_rx_batch_tm3(oai4g_rx_config_t *cfg, int n_sf, const int32_t *d_rxdataF, const int32_t *d_est, int16_t *d_llr,
                        int unscramble, void *stream);
 
+/* TM2 (ALAMOUTI, two TX ports, mode1_flag 0) with dlsim's UE (rx_pdsch, dlsch_demodulation.c:82-800):
+ * dlsch_extract_rbs_dual, dlsch_channel_level over both ports (log2_maxh = log2_approx(max avg) / 2),
+ * dlsch_channel_compensation per (port, RX antenna), dlsch_detection_mrc over nb_rx (1-2),
+ * dlsch_alamouti over pairs of extracted REs, dlsch_qpsk / 16qam / 64qam_llr.  Same buffers as the
+ * TM3 entry points (estimate planes [p * 2 + a]).  Returns the LLR count (not unscrambled) or -1. */
+int oai4g_rx_pdsch_tm2(const oai4g_frame_parms_t *frame_parms, int nb_rx, const int32_t *const *rxdataF,
+                       const int32_t *const *dl_ch_estimates, const uint32_t rb_alloc[4], uint8_t Qm,
+                       uint8_t num_pdcch_symbols, uint8_t subframe, int16_t *llr, uint8_t *log2_maxh);
+oai4g_rx_config_t *oai4g_rx_config_create_tm2(const oai4g_frame_parms_t *frame_parms, const uint32_t rb_alloc[4],
+                                              uint8_t Qm, uint8_t num_pdcch_symbols, uint16_t rnti,
+                                              uint8_t first_subframe, uint8_t subframe_step, uint8_t nb_rx);
+int oai4g_rx_batch_tm2(oai4g_rx_config_t *cfg, int n_sf, const int32_t *d_rxdataF, const int32_t *d_est, int16_t *d_llr,
+                       int unscramble, void *stream);
+
 /* lte_dl_channel_estimation (PHY/LTE_ESTIMATION/lte_dl_channel_estimation.c:37, decl
  * LTE_ESTIMATION/defs.h; called by slot_fep.c:188 for the pilot symbols of every slot) with the
  * reference's defaults high_speed_flag = 1 (dlsim.c:2057), eNB_offset 0, one RX antenna: the

@@ -2,7 +2,7 @@
  * Replaces: dlsch_coding.c:254 dlsch_encoding, dlsch_scrambling.c:51, dlsch_modulation.c:1181,
  * ofdm_mod.c:47/85/233, lte_dfts.c idft64..idft2048, crc_byte.c:117/135, lte_segmentation.c:39,
  * 3gpplte_sse.c:380, lte_rate_matching.c:51/464, pcfich.c:48/144, dci.c:2024, pss.c:50, sss.c:47,
- * pbch.c:161, phich.c:401, lte_dl_channel_estimation.c:37, dlsch_demodulation.c:82 (rx_pdsch, TM1/TM3),
+ * pbch.c:161, phich.c:401, lte_dl_channel_estimation.c:37, dlsch_demodulation.c:82 (rx_pdsch, TM1/TM2/TM3),
  * dlsch_scrambling.c:99 (dlsch_unscrambling), 3gpplte_turbo_decoder_sse_16bit.c:945 / _8bit.c:894,
  * lte_rate_matching.c:193 / :293 / :688 (the UL decoding chain). */
 #include "PHY/defs.h"
@@ -250,8 +250,8 @@ int lte_dl_channel_estimation(PHY_VARS_UE *ue, uint8_t eNB_id, uint8_t eNB_offse
   return 0;
 }
 
-/* rx_pdsch (dlsch_demodulation.c:82) for TM1 (one TX port, one RX antenna) and TM3 (LARGE_CDD,
- * two TX ports, 1-2 RX antennas, dual_stream_flag 0), localized allocations (rb_alloc_even ==
+/* rx_pdsch (dlsch_demodulation.c:82) for TM1 (one TX port, one RX antenna), TM2 (ALAMOUTI) and TM3
+ * (LARGE_CDD; both two TX ports, 1-2 RX antennas, dual_stream_flag 0), localized allocations (rb_alloc_even ==
  * rb_alloc_odd).  CONTRACT: the library demodulates a whole subframe, so the shim accepts dlsim's
  * call sequence only (dlsim.c:3236-3260): first_symbol_flag on symbol num_pdcch_symbols, then
  * every following symbol in order; the work runs at the last symbol, when the LLR stream and
@@ -269,8 +269,10 @@ int rx_pdsch(PHY_VARS_UE *ue, PDSCH_t type, unsigned char eNB_id, unsigned char 
   const LTE_DL_FRAME_PARMS *f = &ue->lte_frame_parms;
   LTE_DL_UE_HARQ_t *h = ue->dlsch_ue[eNB_id][0]->harq_processes[harq_pid];
   const int tm3 = f->nb_antennas_tx_eNB == 2 && h->mimo_mode == LARGE_CDD;
+  const int tm2 = f->nb_antennas_tx_eNB == 2 && h->mimo_mode == ALAMOUTI;
   if (type != PDSCH || dual_stream_flag || memcmp(h->rb_alloc_even, h->rb_alloc_odd, 16) != 0 ||
-      (!tm3 && (f->nb_antennas_rx != 1 || f->nb_antennas_tx_eNB != 1)) || (tm3 && f->nb_antennas_rx > 2))
+      (!tm3 && !tm2 && (f->nb_antennas_rx != 1 || f->nb_antennas_tx_eNB != 1)) ||
+      ((tm3 || tm2) && f->nb_antennas_rx > 2))
     return -1;
   const int npdcch = ue->lte_ue_pdcch_vars[eNB_id]->num_pdcch_symbols;
   if (first_symbol_flag) {
@@ -286,16 +288,21 @@ int rx_pdsch(PHY_VARS_UE *ue, PDSCH_t type, unsigned char eNB_id, unsigned char 
   fp_to(f, &fp);
   uint8_t log2_maxh = 0;
   int n;
-  if (tm3) {
+  if (tm3 || tm2) {
     const int32_t *rxF[2], *est[4];
     for (int a = 0; a < f->nb_antennas_rx; a++) {
       rxF[a] = (const int32_t *)ue->lte_ue_common_vars.rxdataF[a];
       est[a] = (const int32_t *)ue->lte_ue_common_vars.dl_ch_estimates[eNB_id][a];
       est[2 + a] = (const int32_t *)ue->lte_ue_common_vars.dl_ch_estimates[eNB_id][2 + a];
     }
-    LTE_DL_UE_HARQ_t *h1 = ue->dlsch_ue[eNB_id][1]->harq_processes[harq_pid];
-    n = oai4g_rx_pdsch_tm3(&fp, f->nb_antennas_rx, rxF, est, h->rb_alloc_even, get_Qm(h->mcs), get_Qm(h1->mcs),
-                           h->mcs, npdcch, subframe, ue->lte_ue_pdsch_vars[eNB_id]->llr[0], &log2_maxh);
+    if (tm2) {
+      n = oai4g_rx_pdsch_tm2(&fp, f->nb_antennas_rx, rxF, est, h->rb_alloc_even, get_Qm(h->mcs), npdcch, subframe,
+                             ue->lte_ue_pdsch_vars[eNB_id]->llr[0], &log2_maxh);
+    } else {
+      LTE_DL_UE_HARQ_t *h1 = ue->dlsch_ue[eNB_id][1]->harq_processes[harq_pid];
+      n = oai4g_rx_pdsch_tm3(&fp, f->nb_antennas_rx, rxF, est, h->rb_alloc_even, get_Qm(h->mcs), get_Qm(h1->mcs),
+                             h->mcs, npdcch, subframe, ue->lte_ue_pdsch_vars[eNB_id]->llr[0], &log2_maxh);
+    }
   } else {
     n = oai4g_rx_pdsch_siso(&fp, (const int32_t *)ue->lte_ue_common_vars.rxdataF[0],
                             (const int32_t *)ue->lte_ue_common_vars.dl_ch_estimates[eNB_id][0], h->rb_alloc_even,

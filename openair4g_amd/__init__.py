@@ -228,6 +228,14 @@ _SIGS = {
                                                      ctypes.c_uint8, ctypes.c_uint8, ctypes.c_uint8]),
     "oai4g_rx_batch_tm3": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p,
                                           ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p]),
+    "oai4g_rx_pdsch_tm2": (ctypes.c_int, [ctypes.POINTER(FrameParms), ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p,
+                                          ctypes.c_void_p, ctypes.c_uint8, ctypes.c_uint8, ctypes.c_uint8,
+                                          ctypes.c_void_p, ctypes.c_void_p]),
+    "oai4g_rx_config_create_tm2": (ctypes.c_void_p, [ctypes.POINTER(FrameParms), ctypes.c_void_p, ctypes.c_uint8,
+                                                     ctypes.c_uint8, ctypes.c_uint16, ctypes.c_uint8, ctypes.c_uint8,
+                                                     ctypes.c_uint8]),
+    "oai4g_rx_batch_tm2": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p,
+                                          ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p]),
     "oai4g_signal_energy": (ctypes.c_int32, [ctypes.c_void_p, ctypes.c_uint32]),
     "oai4g_signal_energy_batch": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_size_t, ctypes.c_uint32,
                                                  ctypes.c_void_p, ctypes.c_void_p]),
@@ -532,6 +540,27 @@ def rx_pdsch_tm3(fp, rxF, est, rb_alloc, Qm0, Qm1, mcs0, num_pdcch, subframe):
     return out[:n], sh.value
 
 
+def rx_pdsch_tm2(fp, rxF, est, rb_alloc, Qm, num_pdcch, subframe):
+    """rx_pdsch for TM2 (ALAMOUTI): rxF = [nb_rx][nsymb*N], est[(p, a)] = [nsymb*N].
+    Returns (LLRs, log2_maxh)."""
+    init()
+    nb_rx = len(rxF)
+    rx = [np.ascontiguousarray(r, dtype=np.int32) for r in rxF]
+    keep = {k: np.ascontiguousarray(v, dtype=np.int32) for k, v in est.items()}
+    ep = (ctypes.c_void_p * 4)()
+    for (p_, a), arr in keep.items():
+        if a < nb_rx:
+            ep[2 * p_ + a] = arr.ctypes.data
+    rp = (ctypes.c_void_p * 2)(*[r.ctypes.data for r in rx] + [None] * (2 - nb_rx))
+    out = np.zeros(14 * 1200 * 6 + 64, dtype=np.int16)
+    sh = ctypes.c_uint8()
+    ra = (ctypes.c_uint32 * 4)(*rb_alloc)
+    n = lib().oai4g_rx_pdsch_tm2(ctypes.byref(fp), nb_rx, rp, ep, ra, Qm, num_pdcch, subframe, _ptr(out),
+                                 ctypes.byref(sh))
+    _check(n >= 0)
+    return out[:n], sh.value
+
+
 class RxBatchTM3:
     """Device-resident batched TM3 demodulation (oai4g_rx_batch_tm3): codeword 0's LLRs from the FEP
     output of nb_rx antennas and the four estimate planes (ports 0 / 1 per antenna)."""
@@ -544,6 +573,9 @@ class RxBatchTM3:
         self.cfg = self.L.oai4g_rx_config_create_tm3(ctypes.byref(fp), ra, Qm0, Qm1, mcs0, num_pdcch, rnti,
                                                      first_subframe, subframe_step, nb_rx)
         _check(bool(self.cfg))
+        self._setup(fp, n_sf, nb_rx)
+
+    def _setup(self, fp, n_sf, nb_rx):
         self.fp, self.n_sf, self.nb_rx = fp, n_sf, nb_rx
         self.stride = self.L.oai4g_rx_llr_stride(self.cfg)
         self.plane = n_sf * fp.symbols_per_tti * fp.ofdm_symbol_size
@@ -605,6 +637,22 @@ class RxBatchTM3:
         self.L.oai4g_dev_free(self.d_est)
         self.L.oai4g_dev_free(self.d_llr)
         self.L.oai4g_rx_config_destroy(self.cfg)
+
+class RxBatchTM2(RxBatchTM3):
+    """Device-resident batched TM2 demodulation (oai4g_rx_batch_tm2): the ALAMOUTI-combined stream's
+    LLRs from the FEP output of nb_rx antennas and the four estimate planes (ports 0 / 1 per antenna)."""
+
+    def __init__(self, fp, rb_alloc, Qm, num_pdcch, rnti, n_sf, nb_rx=2, first_subframe=0, subframe_step=1):
+        init()
+        self.L = lib()
+        ra = (ctypes.c_uint32 * 4)(*rb_alloc)
+        self.cfg = self.L.oai4g_rx_config_create_tm2(ctypes.byref(fp), ra, Qm, num_pdcch, rnti, first_subframe,
+                                                     subframe_step, nb_rx)
+        _check(bool(self.cfg))
+        self._setup(fp, n_sf, nb_rx)
+
+    def launch(self, d_rxF, unscramble=1, stream=None):
+        _check(self.L.oai4g_rx_batch_tm2(self.cfg, self.n_sf, d_rxF, self.d_est, self.d_llr, unscramble, stream) == 0)
 
 
 def dlsch_unscrambling(fp, rnti, G, llr, q, Ns, mbsfn_flag=0):

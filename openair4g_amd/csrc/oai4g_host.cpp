@@ -3414,10 +3414,17 @@ static const uint8_t k_mumimo_off[29][3] = {{0, 6, 5}, {0, 4, 5}, {0, 4, 5}, {0,
 
 static oai4g_rx_config_t *rx_config_build(const oai4g_frame_parms_t *fp, const uint32_t rb_alloc[4], uint8_t Qm,
                                           uint8_t num_pdcch_symbols, uint16_t rnti, uint8_t first_subframe,
-                                          uint8_t subframe_step, int tm3, uint8_t Qm1, uint8_t mcs0, uint8_t nb_rx)
+                                          uint8_t subframe_step, int tm3, uint8_t Qm1, uint8_t mcs0, uint8_t nb_rx,
+                                          int tm2 = 0)
 {
   NEED_INIT(nullptr);
-  if (!tm3 && (fp->nb_antennas_tx != 1 || fp->mode1_flag != 1 || (Qm != 2 && Qm != 4 && Qm != 6) ||
+  const bool dual = tm3 || tm2;
+  if (tm2 && (fp->nb_antennas_tx != 2 || fp->mode1_flag != 0 || (Qm != 2 && Qm != 4 && Qm != 6) || nb_rx < 1 ||
+              nb_rx > 2 || num_pdcch_symbols < 1 || num_pdcch_symbols > 3)) {
+    set_err("rx_config_tm2: two TX ports (mode1_flag 0), Qm 2/4/6, 1-2 RX antennas, 1..3 PDCCH symbols");
+    return nullptr;
+  }
+  if (!dual && (fp->nb_antennas_tx != 1 || fp->mode1_flag != 1 || (Qm != 2 && Qm != 4 && Qm != 6) ||
                num_pdcch_symbols < 1 || num_pdcch_symbols > 3)) {
     set_err("rx_config: TM1 (one TX port), Qm 2/4/6, 1..3 PDCCH symbols only");
     return nullptr;
@@ -3449,7 +3456,8 @@ static oai4g_rx_config_t *rx_config_build(const oai4g_frame_parms_t *fp, const u
   h.a1 = Qm == 4 ? 20724 : (Qm == 6 ? 20225 : 0);          /* QAM16_n1 / QAM64_n1 (impl_defs_top.h:215-224) */
   h.a2 = Qm == 6 ? 10112 : 0;                               /* QAM64_n2 */
   h.tm3 = tm3 ? 1u : 0u;
-  h.nb_rx = tm3 ? nb_rx : 1u;
+  h.tm2 = tm2 ? 1u : 0u;
+  h.nb_rx = dual ? nb_rx : 1u;
   h.mu_off = tm3 ? k_mumimo_off[mcs0][(Qm1 >> 1) - 1] : 0;
   std::vector<uint32_t> map;
   uint32_t max_llr = 0;
@@ -3461,19 +3469,21 @@ static oai4g_rx_config_t *rx_config_build(const oai4g_frame_parms_t *fp, const u
       const bool pil = smod == 0 || smod == 4u - fp->Ncp;
       h.map_off[sf][k] = (uint32_t)map.size();
       uint32_t nb_rb = 0, n = 0;
-      if (tm3)
+      if (dual)
         rx_extract_map_dual(fp, rb_alloc, sf, l, map, nb_rb, n);
       else
         rx_extract_map(fp, rb_alloc, sf, l, map, nb_rb, n);
       h.n_ext[sf][k] = n;
       const int adj = Qm == 2 ? 0 : rx_adjust_G2(fp, rb_alloc, sf, l);
       /* dlsch_*_llr: pilot symbols carry 10 (one port) or 8 (two ports, mode1_flag 0) REs per RB */
-      const int len = pil ? (tm3 ? (int)nb_rb * 8 - 2 * adj / 3 : (int)nb_rb * 10 - 5 * adj / 6) : (int)nb_rb * 12 - adj;
+      const int len = pil ? (dual ? (int)nb_rb * 8 - 2 * adj / 3 : (int)nb_rb * 10 - 5 * adj / 6) : (int)nb_rb * 12 - adj;
       h.len[sf][k] = (uint32_t)(len > 0 ? len : 0);
       /* channel_level_TM3 takes 8 REs per RB only where symbol_mod == 0 (its 4-Ncp test reads
        * Ncp-1, :2917-2922); the SISO level reads 12 per RB */
-      const uint32_t lvl_nre = tm3 && smod == 0 ? 8u : 12u;
-      if (h.len[sf][k] > n || (k == 0 && lvl_nre * nb_rb > n)) {
+      const uint32_t lvl_nre = dual && smod == 0 ? 8u : 12u;
+      /* TM2 combines RE pairs: the partner of an odd last RE must have been extracted too */
+      const uint32_t need = tm2 ? (h.len[sf][k] + 1) & ~1u : h.len[sf][k];
+      if (need > n || (k == 0 && lvl_nre * nb_rb > n)) {
         /* the reference would read ext slots this symbol did not write (odd N_RB_DL with a
          * PBCH / sync half RB and the unadjusted QPSK length, :3354-3427): a batch that runs
          * this subframe index is refused */
@@ -3485,7 +3495,7 @@ static oai4g_rx_config_t *rx_config_build(const oai4g_frame_parms_t *fp, const u
       off += h.len[sf][k] * Qm;
       if (k == 0) {
         h.lvl_n[sf] = lvl_nre * nb_rb;
-        h.lvl_div[sf] = tm3 ? lvl_nre * nb_rb : (pil ? 10 : 12) * nb_rb;
+        h.lvl_div[sf] = dual ? lvl_nre * nb_rb : (pil ? 10 : 12) * nb_rb;
       }
       if (nb_rb == 0) cfg->bad[sf] = true;                   /* empty allocation in this symbol */
     }
@@ -3543,6 +3553,13 @@ extern "C" oai4g_rx_config_t *oai4g_rx_config_create_tm3(const oai4g_frame_parms
                                                          uint8_t first_subframe, uint8_t subframe_step, uint8_t nb_rx)
 {
   return rx_config_build(fp, rb_alloc, Qm0, num_pdcch_symbols, rnti, first_subframe, subframe_step, 1, Qm1, mcs0, nb_rx);
+}
+
+extern "C" oai4g_rx_config_t *oai4g_rx_config_create_tm2(const oai4g_frame_parms_t *fp, const uint32_t rb_alloc[4],
+                                                         uint8_t Qm, uint8_t num_pdcch_symbols, uint16_t rnti,
+                                                         uint8_t first_subframe, uint8_t subframe_step, uint8_t nb_rx)
+{
+  return rx_config_build(fp, rb_alloc, Qm, num_pdcch_symbols, rnti, first_subframe, subframe_step, 0, 0, 0, nb_rx, 1);
 }
 
 extern "C" void oai4g_rx_config_destroy(oai4g_rx_config_t *cfg)
@@ -3613,6 +3630,24 @@ extern "C" int oai4g_rx_batch_tm3(oai4g_rx_config_t *cfg, int n_sf, const int32_
   return 0;
 }
 
+extern "C" int oai4g_rx_batch_tm2(oai4g_rx_config_t *cfg, int n_sf, const int32_t *d_rxdataF, const int32_t *d_est,
+                                  int16_t *d_llr, int unscramble, void *stream)
+{
+  NEED_INIT(-1);
+  if (!cfg || !cfg->h.tm2) { set_err("rx_batch_tm2: not a TM2 configuration (oai4g_rx_config_create_tm2)"); return -1; }
+  if (n_sf <= 0) return 0;
+  if (rx_check_batch(cfg, n_sf) != 0) return -1;
+  if (n_sf > cfg->shift_cap) {
+    if (cfg->d_shift) hipFree(cfg->d_shift);
+    HCK(hipMalloc(&cfg->d_shift, (size_t)n_sf), -1);
+    cfg->shift_cap = n_sf;
+  }
+  const size_t plane = (size_t)n_sf * cfg->h.nsymb * cfg->h.N;
+  HCK(oai4g_launch_rx_tm2(cfg->d, &cfg->h, n_sf, d_rxdataF, d_est, plane, d_llr, cfg->d_shift, unscramble,
+                          (hipStream_t)stream), -1);
+  return 0;
+}
+
 /* The rx_pdsch drop-ins' configurations, cached per calling thread (the UE calls rx_pdsch once per
  * subframe with a handful of distinct (frame, allocation, modulation, subframe) keys; building one
  * costs Gold generation, allocations and copies).  Round-robin over 32 entries; an evicted entry
@@ -3644,9 +3679,10 @@ oai4g_rx_config_t *rx_cached(const oai4g_frame_parms_t *fp, const uint32_t rb_al
   rx_cache_t &c = t_rx_cache;
   for (int i = 0; i < 32; i++)
     if (c.cfg[i] && memcmp(&c.key[i], &k, sizeof(k)) == 0) return c.cfg[i];
-  oai4g_rx_config_t *cfg = tm3 ? oai4g_rx_config_create_tm3(fp, rb_alloc, Qm, Qm1, mcs0, npdcch, 0, subframe, 1,
-                                                              (uint8_t)nb_rx)
-                               : oai4g_rx_config_create(fp, rb_alloc, Qm, npdcch, 0, subframe, 1);
+  oai4g_rx_config_t *cfg = tm3 == 2 ? oai4g_rx_config_create_tm2(fp, rb_alloc, Qm, npdcch, 0, subframe, 1, (uint8_t)nb_rx)
+                          : tm3 ? oai4g_rx_config_create_tm3(fp, rb_alloc, Qm, Qm1, mcs0, npdcch, 0, subframe, 1,
+                                                             (uint8_t)nb_rx)
+                                : oai4g_rx_config_create(fp, rb_alloc, Qm, npdcch, 0, subframe, 1);
   if (!cfg) return nullptr;
   const int slot = c.next;
   c.next = (c.next + 1) % 32;
@@ -3688,6 +3724,36 @@ extern "C" int oai4g_rx_pdsch_tm3(const oai4g_frame_parms_t *fp, int nb_rx, cons
     rc = n;
   else
     set_err("rx_pdsch_tm3: HIP error");
+  return rc;
+}
+
+extern "C" int oai4g_rx_pdsch_tm2(const oai4g_frame_parms_t *fp, int nb_rx, const int32_t *const *rxdataF,
+                                  const int32_t *const *dl_ch_estimates, const uint32_t rb_alloc[4], uint8_t Qm,
+                                  uint8_t num_pdcch_symbols, uint8_t subframe, int16_t *llr, uint8_t *log2_maxh)
+{
+  NEED_INIT(-1);
+  oai4g_rx_config_t *cfg = rx_cached(fp, rb_alloc, Qm, 0, 0, num_pdcch_symbols, subframe, 2, nb_rx);
+  if (!cfg) return -1;
+  if (rx_check_batch(cfg, 1) != 0) return -1;
+  const size_t gb = (size_t)cfg->h.nsymb * cfg->h.N * 4, gs = (gb + 255) & ~(size_t)255;
+  const int n = (int)cfg->llr_count[subframe % 10];
+  uint8_t *buf = scratch(6 * gs + (size_t)cfg->h.llr_stride * 2 + 256);
+  if (!buf) return -1;
+  int32_t *dy = (int32_t *)buf, *de = (int32_t *)(buf + 2 * gs);   /* [nb_rx][grid], planes [p * 2 + a] */
+  int16_t *dl = (int16_t *)(buf + 6 * gs);
+  bool ok = true;
+  for (int a = 0; a < nb_rx && ok; a++) ok = hipMemcpyAsync((uint8_t *)dy + a * gb, rxdataF[a], gb, hipMemcpyHostToDevice, g_scr.s) == hipSuccess;
+  for (int pa = 0; pa < 4 && ok; pa++)
+    if ((pa & 1) < nb_rx)
+      ok = hipMemcpyAsync((uint8_t *)de + pa * gb, dl_ch_estimates[pa], gb, hipMemcpyHostToDevice, g_scr.s) == hipSuccess;
+  int rc = -1;
+  if (ok && oai4g_rx_batch_tm2(cfg, 1, dy, de, dl, 0, g_scr.s) == 0 &&
+      hipMemcpyAsync(llr, dl, (size_t)n * 2, hipMemcpyDeviceToHost, g_scr.s) == hipSuccess &&
+      (!log2_maxh || hipMemcpyAsync(log2_maxh, cfg->d_shift, 1, hipMemcpyDeviceToHost, g_scr.s) == hipSuccess) &&
+      hipStreamSynchronize(g_scr.s) == hipSuccess)
+    rc = n;
+  else
+    set_err("rx_pdsch_tm2: HIP error");
   return rc;
 }
 

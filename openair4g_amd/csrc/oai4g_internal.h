@@ -375,10 +375,15 @@ struct rx_dev_t {
    * channel_level_TM3 RE count per RB of the first PDSCH symbol, offset_mumimo_llr_drange */
   uint32_t tm3, nb_rx, lvl_nre;
   int32_t mu_off;
+  /* TM2 (ALAMOUTI, dual extraction): dlsch_channel_level over both ports, dlsch_alamouti */
+  uint32_t tm2;
 };
 hipError_t oai4g_launch_rx_chest(const chest_dev_t *d_ce, const rx_dev_t *d_rx, const rx_dev_t *h_rx, int n_sf,
                                  const int32_t *d_rxF, int16_t *d_llr, uint8_t *d_shift, int unscramble, hipStream_t s);
 hipError_t oai4g_launch_rx_tm3(const rx_dev_t *d_cfg, const rx_dev_t *h_cfg, int n_sf, const int32_t *d_rxF,
+                               const int32_t *d_est, size_t plane, int16_t *d_llr, uint8_t *d_shift, int unscramble,
+                               hipStream_t s);
+hipError_t oai4g_launch_rx_tm2(const rx_dev_t *d_cfg, const rx_dev_t *h_cfg, int n_sf, const int32_t *d_rxF,
                                const int32_t *d_est, size_t plane, int16_t *d_llr, uint8_t *d_shift, int unscramble,
                                hipStream_t s);
 hipError_t oai4g_launch_rx(const rx_dev_t *d_cfg, const rx_dev_t *h_cfg, int n_sf, const int32_t *d_rxF,

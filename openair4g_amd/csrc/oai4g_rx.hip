@@ -202,6 +202,137 @@ hipError_t oai4g_launch_rx_tm3(const rx_dev_t *d_cfg, const rx_dev_t *h_cfg, int
   return hipGetLastError();
 }
 
+/* ======================================================================================
+ * TM2 (ALAMOUTI, two TX ports) with dlsim's UE (rx_pdsch, dual_stream_flag = 0):
+ *   dlsch_extract_rbs_dual      (the TM3 map)
+ *   dlsch_channel_level         :2777-2838 per (port, RX antenna): int32 |h|^2 sum / (nb_rb nre),
+ *                               log2_maxh = log2_approx(max(0, max avg)) / 2 (:276-285)
+ *   dlsch_channel_compensation  :801-980 per (port, RX antenna)
+ *   dlsch_detection_mrc         :2583-2621 per port
+ *   dlsch_alamouti              :3067-3160 pairs (2k, 2k + 1) of extracted REs, int16 wrap sums,
+ *                               magnitudes (m0 +sat m1) >> 1, mulhi(., 23170) << 1
+ *   dlsch_qpsk / 16qam / 64qam_llr, unscrambled
+ * One thread per RE pair; planes and layouts as for TM3.
+ * ==================================================================================== */
+__global__ void __launch_bounds__(256) k_rx_level_tm2(const rx_dev_t *__restrict__ c, const int32_t *__restrict__ est,
+                                                      size_t plane, uint8_t *__restrict__ shift)
+{
+  __shared__ uint32_t tot[4];
+  const uint32_t sf = blockIdx.x, sfi = (c->first_sf + sf * c->sf_step) % 10, l = c->npdcch;
+  if (threadIdx.x < 4) tot[threadIdx.x] = 0;
+  __syncthreads();
+  rg32_t *map = (rg32_t *)(c->map + c->map_off[sfi][0]);
+  const size_t so = ((size_t)sf * c->nsymb + l) * c->N;
+  uint32_t part[4] = {0, 0, 0, 0};
+  for (uint32_t j = threadIdx.x; j < c->lvl_n[sfi]; j += blockDim.x) {
+    const uint32_t col = map[j] >> 16;
+#pragma unroll
+    for (uint32_t pa = 0; pa < 4; pa++)
+      if ((pa & 1u) < c->nb_rx) part[pa] += rx_h2((uint32_t)est[pa * plane + so + col]);
+  }
+#pragma unroll
+  for (int pa = 0; pa < 4; pa++)
+    if (part[pa]) atomicAdd(&tot[pa], part[pa]);
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    uint8_t m = 0;
+    for (uint32_t pa = 0; pa < 4; pa++)
+      if ((pa & 1u) < c->nb_rx) {
+        const uint8_t v = rx_shift_of((int32_t)tot[pa], c->lvl_div[sfi]);   /* log2 monotone: max of shifts */
+        m = v > m ? v : m;
+      }
+    shift[sf] = m;
+  }
+}
+
+template <int QM>
+__global__ void __launch_bounds__(256) k_rx_llr_tm2(const rx_dev_t *__restrict__ c, const int32_t *__restrict__ rxF,
+                                                    const int32_t *__restrict__ est, size_t plane,
+                                                    int16_t *__restrict__ llr, const uint8_t *__restrict__ shift,
+                                                    int unscramble)
+{
+  const uint32_t sf = blockIdx.y, k = blockIdx.x, sfi = (c->first_sf + sf * c->sf_step) % 10;
+  const uint32_t l = c->npdcch + k, len = c->len[sfi][k], nb_rx = c->nb_rx, NS = c->nsymb * c->N;
+  rg32_t *map = (rg32_t *)(c->map + c->map_off[sfi][k]);
+  const size_t eo = ((size_t)sf * c->nsymb + l) * c->N;
+  int16_t *out = llr + (size_t)sf * c->llr_stride + c->llr_off[sfi][k];
+  const uint32_t sh = shift[sf], base = c->llr_off[sfi][k];
+  rg32_t *gold = (rg32_t *)(c->gold + (size_t)sfi * c->gold_words);
+  const int16_t a1 = c->a1, a2 = c->a2;
+  for (uint32_t q = threadIdx.x; 2 * q < len; q += blockDim.x) {
+    /* the pair's two REs (the config guarantees map entries up to len rounded up to even) */
+    const uint32_t m0 = map[2 * q], m1 = map[2 * q + 1];
+    int16_t cr[2][2], ci[2][2], mg[2][2], mgb[2][2];            /* [port][RE of the pair] */
+#pragma unroll
+    for (int e = 0; e < 2; e++) {
+      const uint32_t mw = e ? m1 : m0;
+      int16_t r_[2][2], i_[2][2], g_[2][2], gb_[2][2];        /* [port][antenna] */
+#pragma unroll
+      for (uint32_t a = 0; a < 2; a++) {
+        const uint32_t aa = a < nb_rx ? a : 0u;
+        const uint32_t yv = (uint32_t)rxF[((size_t)sf * nb_rx + aa) * NS + (size_t)l * c->N + (mw & 0xFFFFu)];
+        const int16_t yr = (int16_t)yv, yi = (int16_t)(yv >> 16);
+#pragma unroll
+        for (uint32_t p = 0; p < 2; p++) {
+          const uint32_t hv = (uint32_t)est[(2 * p + aa) * plane + eo + (mw >> 16)];
+          const int16_t hr = (int16_t)hv, hi = (int16_t)(hv >> 16), nhi = (int16_t)(-(int32_t)hi);
+          r_[p][a] = rx_sat16(rx_madd(hr, yr, hi, yi) >> sh);
+          i_[p][a] = rx_sat16(rx_madd(nhi, yr, hr, yi) >> sh);
+          if (QM > 2) {
+            const int16_t m = rx_sat16(rx_madd(hr, hr, hi, hi) >> sh);
+            g_[p][a] = (int16_t)((((int32_t)m * a1) >> 16) << 1);
+            gb_[p][a] = (int16_t)((((int32_t)m * a2) >> 16) << 1);
+          } else {
+            g_[p][a] = gb_[p][a] = 0;
+          }
+        }
+      }
+#pragma unroll
+      for (int p = 0; p < 2; p++) {
+        if (nb_rx > 1) {                                        /* dlsch_detection_mrc */
+          cr[p][e] = rx_sat16((r_[p][0] >> 1) + (r_[p][1] >> 1));
+          ci[p][e] = rx_sat16((i_[p][0] >> 1) + (i_[p][1] >> 1));
+          mg[p][e] = rx_sat16((g_[p][0] >> 1) + (g_[p][1] >> 1));
+          mgb[p][e] = rx_sat16((gb_[p][0] >> 1) + (gb_[p][1] >> 1));
+        } else {
+          cr[p][e] = r_[p][0]; ci[p][e] = i_[p][0]; mg[p][e] = g_[p][0]; mgb[p][e] = gb_[p][0];
+        }
+      }
+    }
+    /* dlsch_alamouti (C short arithmetic: wraps) */
+    const int16_t y0r = (int16_t)(cr[0][0] + cr[1][1]), y0i = (int16_t)(ci[0][0] - ci[1][1]);
+    const int16_t y1r = (int16_t)(cr[0][1] - cr[1][0]), y1i = (int16_t)(ci[0][1] + ci[1][0]);
+    const int16_t yr2[2] = {y0r, y1r}, yi2[2] = {y0i, y1i};
+#pragma unroll
+    for (int e = 0; e < 2; e++) {
+      const uint32_t j = 2 * q + e;
+      if (j >= len) break;
+      const int16_t m = (int16_t)(rx_sat16((int32_t)mg[0][e] + mg[1][e]) >> 1);
+      const int16_t mb = (int16_t)(rx_sat16((int32_t)mgb[0][e] + mgb[1][e]) >> 1);
+      const int16_t xr = (int16_t)((((int32_t)yr2[e] * 23170) >> 16) << 1), xi = (int16_t)((((int32_t)yi2[e] * 23170) >> 16) << 1);
+      int16_t v[6];
+      rx_llr_values<QM>(xr, xi, m, mb, v);
+      rx_llr_store<QM>(v, unscramble ? gold : nullptr, base + j * QM, out + QM * j);
+    }
+  }
+}
+
+hipError_t oai4g_launch_rx_tm2(const rx_dev_t *d_cfg, const rx_dev_t *h_cfg, int n_sf, const int32_t *d_rxF,
+                               const int32_t *d_est, size_t plane, int16_t *d_llr, uint8_t *d_shift, int unscramble,
+                               hipStream_t s)
+{
+  if (n_sf <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_rx_level_tm2, dim3(n_sf), dim3(256), 0, s, d_cfg, d_est, plane, d_shift);
+  const dim3 g(h_cfg->n_sym, n_sf), b(256);
+  if (h_cfg->Qm == 2)
+    hipLaunchKernelGGL(k_rx_llr_tm2<2>, g, b, 0, s, d_cfg, d_rxF, d_est, plane, d_llr, d_shift, unscramble);
+  else if (h_cfg->Qm == 4)
+    hipLaunchKernelGGL(k_rx_llr_tm2<4>, g, b, 0, s, d_cfg, d_rxF, d_est, plane, d_llr, d_shift, unscramble);
+  else
+    hipLaunchKernelGGL(k_rx_llr_tm2<6>, g, b, 0, s, d_cfg, d_rxF, d_est, plane, d_llr, d_shift, unscramble);
+  return hipGetLastError();
+}
+
 /* dlsch_unscrambling drop-in: llr[k] *= 2 c(k) - 1 (int16), c = the words of the Gold sequence */
 __global__ void __launch_bounds__(256) k_rx_unscramble(int16_t *__restrict__ llr, const uint32_t *__restrict__ c,
                                                        uint32_t n)

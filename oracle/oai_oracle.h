@@ -229,6 +229,9 @@ void orc_dlsch_unscrambling(int16_t *llr, int G, uint32_t c_init);
 int orc_rx_pdsch_tm3(const orc_frame_t *fp, int nb_rx, const int32_t *const *rxdataF, const int32_t *const *est,
                      const uint32_t rb_alloc[4], uint8_t Qm0, uint8_t Qm1, uint8_t mcs0, uint8_t num_pdcch_symbols,
                      uint8_t subframe, int16_t *llr, uint8_t *log2_maxh_out);
+int orc_rx_pdsch_tm2(const orc_frame_t *fp, int nb_rx, const int32_t *const *rxdataF, const int32_t *const *est,
+                     const uint32_t rb_alloc[4], uint8_t Qm, uint8_t num_pdcch_symbols, uint8_t subframe,
+                     int16_t *llr, uint8_t *log2_maxh_out);
 /* orc_tx_subframe plus generate_dci_top's PCFICH + PDCCH before the OFDM step (dlsim.c:2553) */
 int orc_tx_subframe_dci(const orc_tx_cfg_t *cfg, uint8_t *payload[2], int32_t **txdataF, int32_t **txdata,
                         uint8_t *e_out[2], uint8_t n_ue_dci, uint8_t n_common_dci, const orc_dci_alloc_t *dci);

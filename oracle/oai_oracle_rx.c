@@ -471,3 +471,125 @@ int orc_rx_pdsch_tm3(const orc_frame_t *fp, int nb_rx, const int32_t *const *rxd
   if (log2_maxh_out) *log2_maxh_out = log2_maxh;
   return (int)(out - llr);
 }
+
+/* rx_pdsch for TM2 (ALAMOUTI, two TX ports) with dlsim's UE (dual_stream_flag 0,
+ * dlsch_demodulation.c:82-800):
+ *   dlsch_extract_rbs_dual      as for TM3 (extract_dual above)
+ *   dlsch_channel_level         :2777-2838: per (port, RX antenna) the int32 sum of |h|^2 over the
+ *                               first PDSCH symbol's nb_rb RBs (8 REs per RB where symbol_mod == 0,
+ *                               its 4-Ncp test is written Ncp-1, else 12), divided by nb_rb nre;
+ *                               log2_maxh = log2_approx(max(0, max avg)) / 2 (:276-285)
+ *   dlsch_channel_compensation  :801-980 per (port, RX antenna): conj(h) y >> log2_maxh (madd, packs),
+ *                               |h|^2 >> log2_maxh (packs) times QAM16_n1 / QAM64_n1 / QAM64_n2
+ *                               (mulhi << 1); rho (:982-) only feeds the dual-stream LLRs
+ *   dlsch_detection_mrc         :2583-2621 per port: (a >> 1) +sat (b >> 1), also the magnitudes
+ *   dlsch_alamouti              :3067-3160 pairs of consecutive extracted REs (2k, 2k + 1):
+ *                               y0 += conj-pair of port 1 (int16 wrap: C short arithmetic),
+ *                               magnitudes (m0 +sat m1) >> 1, the combined symbol mulhi(., 1/sqrt2) << 1
+ *   dlsch_qpsk / 16qam / 64qam_llr of the combined stream (mode1_flag 0 lengths)
+ * rxdataF[a] = [nsymb][N]; est[p * 2 + a] = dl_ch_estimates[(p << 1) + a]. */
+int orc_rx_pdsch_tm2(const orc_frame_t *fp, int nb_rx, const int32_t *const *rxdataF, const int32_t *const *est,
+                     const uint32_t rb_alloc[4], uint8_t Qm, uint8_t num_pdcch_symbols, uint8_t subframe,
+                     int16_t *llr, uint8_t *log2_maxh_out)
+{
+  if (nb_rx < 1 || nb_rx > 2 || (Qm != 2 && Qm != 4 && Qm != 6)) return -1;
+  const int N = fp->ofdm_symbol_size, nsymb = fp->Ncp == 0 ? 14 : 12;
+  const size_t X = 12 * 110 + 64;
+  int32_t *rx_ext = (int32_t *)calloc(2 * X, 4), *hx = (int32_t *)calloc(4 * X, 4);   /* hx[(p * 2 + a) X + e] */
+  int16_t *comp = (int16_t *)calloc(4 * X * 2, 2), *mag = (int16_t *)calloc(4 * X, 2), *magb = (int16_t *)calloc(4 * X, 2);
+  int16_t *out = llr;
+  uint8_t log2_maxh = 0;
+  const int16_t a1 = Qm == 4 ? QAM16_n1 : (Qm == 6 ? QAM64_n1 : 0), a2 = Qm == 6 ? QAM64_n2 : 0;
+  for (int symbol = num_pdcch_symbols; symbol < nsymb && out; symbol++) {
+    int nb_rb = 0, hw[2] = {0, 0};
+    for (int a = 0; a < nb_rx; a++)
+      (void)extract_dual(fp, rxdataF[a] + symbol * N, est[a] + symbol * N, est[2 + a] + symbol * N, rb_alloc,
+                         (uint8_t)symbol, subframe, rx_ext + a * X, hx + a * X, hx + (2 + a) * X, &nb_rb, &hw[a]);
+    const int symbol_mod = symbol >= 7 - fp->Ncp ? symbol - (7 - fp->Ncp) : symbol;
+    const int pil = symbol_mod == 0 || symbol_mod == 4 - fp->Ncp;
+    const int nre_rb = pil ? 8 : 12;
+    if (nb_rb == 0) { out = NULL; break; }
+    if (symbol == num_pdcch_symbols) {
+      const int nre = symbol_mod == 0 ? 8 : 12;
+      if (hw[0] < nb_rb * nre) { out = NULL; break; }      /* would read unwritten ext slots */
+      int32_t avgs = 0;
+      for (int pa = 0; pa < 4; pa++) {
+        if ((pa & 1) >= nb_rx) continue;
+        uint32_t tot = 0;
+        for (int e = 0; e < nb_rb * nre; e++) {
+          int16_t h[2];
+          memcpy(h, &hx[pa * X + e], 4);
+          tot += (uint32_t)((int32_t)h[0] * h[0]) + (uint32_t)((int32_t)h[1] * h[1]);
+        }
+        const int32_t avg = (int32_t)tot / (nb_rb * nre);
+        avgs = avg > avgs ? avg : avgs;                     /* cmax, starting from 0 */
+      }
+      log2_maxh = (uint8_t)(orc_log2_approx((uint32_t)avgs) / 2);
+    }
+    const int n = nb_rb * nre_rb;
+    if (n > hw[0]) { out = NULL; break; }
+    for (int pa = 0; pa < 4; pa++) {                        /* compensation per (port, RX antenna) */
+      const int a = pa & 1;
+      if (a >= nb_rx) continue;
+      for (int e = 0; e < n; e++) {
+        int16_t h[2], y[2];
+        memcpy(h, &hx[pa * X + e], 4);
+        memcpy(y, &rx_ext[a * X + e], 4);
+        const int16_t m = sat16((int32_t)((uint32_t)((int32_t)h[0] * h[0]) + (uint32_t)((int32_t)h[1] * h[1])) >> log2_maxh);
+        mag[pa * X + e] = mulhi2(m, a1);
+        magb[pa * X + e] = mulhi2(m, a2);
+        const int16_t nhi = (int16_t)-h[1];
+        comp[(pa * X + e) * 2] = sat16((int32_t)((uint32_t)((int32_t)h[0] * y[0]) + (uint32_t)((int32_t)h[1] * y[1])) >> log2_maxh);
+        comp[(pa * X + e) * 2 + 1] = sat16((int32_t)((uint32_t)((int32_t)nhi * y[0]) + (uint32_t)((int32_t)h[0] * y[1])) >> log2_maxh);
+      }
+    }
+    if (nb_rx > 1)                                           /* dlsch_detection_mrc, per port */
+      for (int p = 0; p < 2; p++) {
+        const size_t o0 = (size_t)(2 * p) * X, o1 = o0 + X;
+        for (int e = 0; e < n; e++) {
+          for (int c = 0; c < 2; c++)
+            comp[(o0 + e) * 2 + c] = sat16((comp[(o0 + e) * 2 + c] >> 1) + (comp[(o1 + e) * 2 + c] >> 1));
+          mag[o0 + e] = sat16((mag[o0 + e] >> 1) + (mag[o1 + e] >> 1));
+          magb[o0 + e] = sat16((magb[o0 + e] >> 1) + (magb[o1 + e] >> 1));
+        }
+      }
+    /* dlsch_alamouti: rxF0 = port 0 (slot 0), rxF1 = port 1 (slot 2) */
+    int16_t *c0 = comp, *c1 = comp + 2 * 2 * X;
+    for (int e = 0; e + 1 < n; e += 2) {
+      c0[2 * e] = (int16_t)(c0[2 * e] + c1[2 * e + 2]);
+      c0[2 * e + 1] = (int16_t)(c0[2 * e + 1] - c1[2 * e + 3]);
+      c0[2 * e + 2] = (int16_t)(c0[2 * e + 2] - c1[2 * e]);
+      c0[2 * e + 3] = (int16_t)(c0[2 * e + 3] + c1[2 * e + 1]);
+    }
+    for (int e = 0; e < n; e++) {
+      mag[e] = (int16_t)(sat16((int32_t)mag[e] + mag[2 * X + e]) >> 1);
+      magb[e] = (int16_t)(sat16((int32_t)magb[e] + magb[2 * X + e]) >> 1);
+      for (int c = 0; c < 2; c++) c0[2 * e + c] = (int16_t)(mulhi2(c0[2 * e + c], 23170));
+    }
+    const int adj = Qm == 2 ? 0 : orc_adjust_G2(fp, rb_alloc, subframe, (uint8_t)symbol);
+    const int len = pil ? nb_rb * 8 - 2 * adj / 3 : nb_rb * 12 - adj;
+    if (((len + 1) & ~1) > hw[0]) { out = NULL; break; }
+    for (int j = 0; j < len; j++) {
+      const int16_t cr = c0[2 * j], ci = c0[2 * j + 1];
+      *out++ = cr;
+      *out++ = ci;
+      if (Qm > 2) {
+        const int16_t x1r = sat16((int32_t)mag[j] - abs16(cr)), x1i = sat16((int32_t)mag[j] - abs16(ci));
+        *out++ = x1r;
+        *out++ = x1i;
+        if (Qm == 6) {
+          *out++ = sat16((int32_t)magb[j] - abs16(x1r));
+          *out++ = sat16((int32_t)magb[j] - abs16(x1i));
+        }
+      }
+    }
+  }
+  free(rx_ext);
+  free(hx);
+  free(comp);
+  free(mag);
+  free(magb);
+  if (!out) return -1;
+  if (log2_maxh_out) *log2_maxh_out = log2_maxh;
+  return (int)(out - llr);
+}

@@ -605,3 +605,24 @@ def rx_pdsch_tm3(fp, rxF, est, rb_alloc, Qm0, Qm1, mcs0, num_pdcch, subframe):
                                ctypes.byref(sh))
     assert n >= 0
     return out[:n], sh.value
+
+
+def rx_pdsch_tm2(fp, rxF, est, rb_alloc, Qm, num_pdcch, subframe, check=True):
+    """orc_rx_pdsch_tm2 (ALAMOUTI): rxF = [nb_rx][nsymb*N], est[(p, a)] = [nsymb*N] estimates of port p
+    at RX a.  Returns (LLRs, log2_maxh); with check=False a refusal returns (None, 0)."""
+    nb_rx = len(rxF)
+    rx = [np.ascontiguousarray(r, dtype=np.int32) for r in rxF]
+    keep = {k: np.ascontiguousarray(v, dtype=np.int32) for k, v in est.items()}
+    ep = (ctypes.c_void_p * 4)()
+    for (p_, a), arr in keep.items():
+        if a < nb_rx:
+            ep[2 * p_ + a] = arr.ctypes.data
+    rp = (ctypes.c_void_p * 2)(*[r.ctypes.data for r in rx] + [None] * (2 - nb_rx))
+    out = np.zeros(14 * 1200 * 6 + 64, dtype=np.int16)
+    sh = ctypes.c_uint8()
+    ra = (ctypes.c_uint32 * 4)(*rb_alloc)
+    n = orc().orc_rx_pdsch_tm2(ctypes.byref(fp), nb_rx, rp, ep, ra, Qm, num_pdcch, subframe, P(out), ctypes.byref(sh))
+    if not check and n < 0:
+        return None, 0
+    assert n >= 0
+    return out[:n], sh.value
