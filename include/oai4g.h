@@ -282,6 +282,18 @@ oai4g_rx_config_t *oai4g_rx_config_create_tm3(const oai4g_frame_parms_t *frame_p
 int oai4g_rx_batch_tm3(oai4g_rx_config_t *cfg, int n_sf, const int32_t *d_rxdataF, const int32_t *d_est, int16_t *d_llr,
                        int unscramble, void *stream);
 
+/* TM3 with both codewords QPSK (rx_pdsch, dlsch_demodulation.c:643-669): both precoded streams'
+ * matched filters, dlsch_dual_stream_correlation (rho, rho2), the MRC of stream 0 and rho, and the
+ * interference-aware dlsch_qpsk_qpsk_llr of each stream: codeword 0's LLRs in llr0, codeword 1's in
+ * llr1 (same length, returned; -1 on error). */
+int oai4g_rx_pdsch_tm3_2cw(const oai4g_frame_parms_t *frame_parms, int nb_rx, const int32_t *const *rxdataF,
+                           const int32_t *const *dl_ch_estimates, const uint32_t rb_alloc[4], uint8_t mcs0,
+                           uint8_t num_pdcch_symbols, uint8_t subframe, int16_t *llr0, int16_t *llr1,
+                           uint8_t *log2_maxh);
+/* batch of the same (configuration from oai4g_rx_config_create_tm3 with Qm0 = Qm1 = 2) */
+int oai4g_rx_batch_tm3_2cw(oai4g_rx_config_t *cfg, int n_sf, const int32_t *d_rxdataF, const int32_t *d_est,
+                           int16_t *d_llr0, int16_t *d_llr1, int unscramble, void *stream);
+
 /* TM2 (ALAMOUTI, two TX ports, mode1_flag 0) with dlsim's UE (rx_pdsch, dlsch_demodulation.c:82-800):
  * dlsch_extract_rbs_dual, dlsch_channel_level over both ports (log2_maxh = log2_approx(max avg) / 2),
  * dlsch_channel_compensation per (port, RX antenna), dlsch_detection_mrc over nb_rx (1-2),

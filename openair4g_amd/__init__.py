@@ -228,6 +228,11 @@ _SIGS = {
                                                      ctypes.c_uint8, ctypes.c_uint8, ctypes.c_uint8]),
     "oai4g_rx_batch_tm3": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p,
                                           ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p]),
+    "oai4g_rx_pdsch_tm3_2cw": (ctypes.c_int, [ctypes.POINTER(FrameParms), ctypes.c_int, ctypes.c_void_p,
+                                              ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint8, ctypes.c_uint8,
+                                              ctypes.c_uint8, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]),
+    "oai4g_rx_batch_tm3_2cw": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p,
+                                              ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p]),
     "oai4g_rx_pdsch_tm2": (ctypes.c_int, [ctypes.POINTER(FrameParms), ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p,
                                           ctypes.c_void_p, ctypes.c_uint8, ctypes.c_uint8, ctypes.c_uint8,
                                           ctypes.c_void_p, ctypes.c_void_p]),
@@ -540,6 +545,28 @@ def rx_pdsch_tm3(fp, rxF, est, rb_alloc, Qm0, Qm1, mcs0, num_pdcch, subframe):
     return out[:n], sh.value
 
 
+def rx_pdsch_tm3_2cw(fp, rxF, est, rb_alloc, mcs0, num_pdcch, subframe):
+    """rx_pdsch for TM3 with both codewords QPSK: rxF = [nb_rx][nsymb*N], est[(p, a)] = [nsymb*N].
+    Returns (codeword-0 LLRs, codeword-1 LLRs, log2_maxh)."""
+    init()
+    nb_rx = len(rxF)
+    rx = [np.ascontiguousarray(r, dtype=np.int32) for r in rxF]
+    keep = {k: np.ascontiguousarray(v, dtype=np.int32) for k, v in est.items()}
+    ep = (ctypes.c_void_p * 4)()
+    for (p_, a), arr in keep.items():
+        if a < nb_rx:
+            ep[2 * p_ + a] = arr.ctypes.data
+    rp = (ctypes.c_void_p * 2)(*[r.ctypes.data for r in rx] + [None] * (2 - nb_rx))
+    o0 = np.zeros(14 * 1200 * 2 + 64, dtype=np.int16)
+    o1 = np.zeros_like(o0)
+    sh = ctypes.c_uint8()
+    ra = (ctypes.c_uint32 * 4)(*rb_alloc)
+    n = lib().oai4g_rx_pdsch_tm3_2cw(ctypes.byref(fp), nb_rx, rp, ep, ra, mcs0, num_pdcch, subframe, _ptr(o0),
+                                     _ptr(o1), ctypes.byref(sh))
+    _check(n >= 0)
+    return o0[:n], o1[:n], sh.value
+
+
 def rx_pdsch_tm2(fp, rxF, est, rb_alloc, Qm, num_pdcch, subframe):
     """rx_pdsch for TM2 (ALAMOUTI): rxF = [nb_rx][nsymb*N], est[(p, a)] = [nsymb*N].
     Returns (LLRs, log2_maxh)."""
@@ -616,6 +643,20 @@ class RxBatchTM3:
     def launch(self, d_rxF, unscramble=1, stream=None):
         _check(self.L.oai4g_rx_batch_tm3(self.cfg, self.n_sf, d_rxF, self.d_est, self.d_llr, unscramble, stream) == 0)
 
+    def launch_2cw(self, d_rxF, unscramble=1, stream=None):
+        """both codewords QPSK: codeword 0 into d_llr, codeword 1 into d_llr1 (llrs1())"""
+        if not getattr(self, "d_llr1", None):
+            self.d_llr1 = self.L.oai4g_dev_alloc(self.n_sf * self.stride * 2)
+            _check(bool(self.d_llr1))
+        _check(self.L.oai4g_rx_batch_tm3_2cw(self.cfg, self.n_sf, d_rxF, self.d_est, self.d_llr, self.d_llr1,
+                                             unscramble, stream) == 0)
+
+    def llrs1(self):
+        _check(self.L.oai4g_sync() == 0)
+        out = np.empty((self.n_sf, self.stride), dtype=np.int16)
+        _check(self.L.oai4g_memcpy_d2h(_ptr(out), self.d_llr1, out.nbytes) == 0)
+        return out
+
     def llrs(self):
         _check(self.L.oai4g_sync() == 0)
         out = np.empty((self.n_sf, self.stride), dtype=np.int16)
@@ -636,6 +677,9 @@ class RxBatchTM3:
         self._chest = {}
         self.L.oai4g_dev_free(self.d_est)
         self.L.oai4g_dev_free(self.d_llr)
+        if getattr(self, "d_llr1", None):
+            self.L.oai4g_dev_free(self.d_llr1)
+            self.d_llr1 = None
         self.L.oai4g_rx_config_destroy(self.cfg)
 
 class RxBatchTM2(RxBatchTM3):

@@ -3429,10 +3429,11 @@ static oai4g_rx_config_t *rx_config_build(const oai4g_frame_parms_t *fp, const u
     set_err("rx_config: TM1 (one TX port), Qm 2/4/6, 1..3 PDCCH symbols only");
     return nullptr;
   }
-  if (tm3 && (fp->nb_antennas_tx != 2 || fp->mode1_flag != 0 || (Qm != 4 && Qm != 6) ||
+  if (tm3 && (fp->nb_antennas_tx != 2 || fp->mode1_flag != 0 || (Qm != 4 && Qm != 6 && !(Qm == 2 && Qm1 == 2)) ||
               (Qm1 != 2 && Qm1 != 4 && Qm1 != 6) || mcs0 > 28 || nb_rx < 1 || nb_rx > 2 || num_pdcch_symbols < 1 ||
               num_pdcch_symbols > 3)) {
-    set_err("rx_config_tm3: two TX ports, Qm0 4/6 (Qm0 = 2 needs the interference-aware LLRs), Qm1 2/4/6, "
+    set_err("rx_config_tm3: two TX ports, Qm0 4/6 with Qm1 2/4/6 or Qm0 = Qm1 = 2 (Qm0 = 2 with a 16/64-QAM "
+            "codeword 1 needs the qpsk_16qam / qpsk_64qam LLRs), "
             "1-2 RX antennas, 1..3 PDCCH symbols");
     return nullptr;
   }
@@ -3617,6 +3618,7 @@ extern "C" int oai4g_rx_batch_tm3(oai4g_rx_config_t *cfg, int n_sf, const int32_
 {
   NEED_INIT(-1);
   if (!cfg || !cfg->h.tm3) { set_err("rx_batch_tm3: not a TM3 configuration (oai4g_rx_config_create_tm3)"); return -1; }
+  if (cfg->h.Qm == 2) { set_err("rx_batch_tm3: both codewords QPSK: oai4g_rx_batch_tm3_2cw"); return -1; }
   if (n_sf <= 0) return 0;
   if (rx_check_batch(cfg, n_sf) != 0) return -1;
   if (n_sf > cfg->shift_cap) {
@@ -3627,6 +3629,27 @@ extern "C" int oai4g_rx_batch_tm3(oai4g_rx_config_t *cfg, int n_sf, const int32_
   const size_t plane = (size_t)n_sf * cfg->h.nsymb * cfg->h.N;
   HCK(oai4g_launch_rx_tm3(cfg->d, &cfg->h, n_sf, d_rxdataF, d_est, plane, d_llr, cfg->d_shift, unscramble,
                           (hipStream_t)stream), -1);
+  return 0;
+}
+
+extern "C" int oai4g_rx_batch_tm3_2cw(oai4g_rx_config_t *cfg, int n_sf, const int32_t *d_rxdataF, const int32_t *d_est,
+                                      int16_t *d_llr0, int16_t *d_llr1, int unscramble, void *stream)
+{
+  NEED_INIT(-1);
+  if (!cfg || !cfg->h.tm3 || cfg->h.Qm != 2) {
+    set_err("rx_batch_tm3_2cw: not a TM3 configuration with both codewords QPSK");
+    return -1;
+  }
+  if (n_sf <= 0) return 0;
+  if (rx_check_batch(cfg, n_sf) != 0) return -1;
+  if (n_sf > cfg->shift_cap) {
+    if (cfg->d_shift) hipFree(cfg->d_shift);
+    HCK(hipMalloc(&cfg->d_shift, (size_t)n_sf), -1);
+    cfg->shift_cap = n_sf;
+  }
+  const size_t plane = (size_t)n_sf * cfg->h.nsymb * cfg->h.N;
+  HCK(oai4g_launch_rx_tm3qq(cfg->d, &cfg->h, n_sf, d_rxdataF, d_est, plane, d_llr0, d_llr1, cfg->d_shift, unscramble,
+                            (hipStream_t)stream), -1);
   return 0;
 }
 
@@ -3724,6 +3747,38 @@ extern "C" int oai4g_rx_pdsch_tm3(const oai4g_frame_parms_t *fp, int nb_rx, cons
     rc = n;
   else
     set_err("rx_pdsch_tm3: HIP error");
+  return rc;
+}
+
+extern "C" int oai4g_rx_pdsch_tm3_2cw(const oai4g_frame_parms_t *fp, int nb_rx, const int32_t *const *rxdataF,
+                                      const int32_t *const *dl_ch_estimates, const uint32_t rb_alloc[4], uint8_t mcs0,
+                                      uint8_t num_pdcch_symbols, uint8_t subframe, int16_t *llr0, int16_t *llr1,
+                                      uint8_t *log2_maxh)
+{
+  NEED_INIT(-1);
+  oai4g_rx_config_t *cfg = rx_cached(fp, rb_alloc, 2, 2, mcs0, num_pdcch_symbols, subframe, 1, nb_rx);
+  if (!cfg) return -1;
+  if (rx_check_batch(cfg, 1) != 0) return -1;
+  const size_t gb = (size_t)cfg->h.nsymb * cfg->h.N * 4, gs = (gb + 255) & ~(size_t)255;
+  const int n = (int)cfg->llr_count[subframe % 10];
+  uint8_t *buf = scratch(6 * gs + (size_t)cfg->h.llr_stride * 4 + 256);
+  if (!buf) return -1;
+  int32_t *dy = (int32_t *)buf, *de = (int32_t *)(buf + 2 * gs);   /* [nb_rx][grid], planes [p * 2 + a] */
+  int16_t *dl = (int16_t *)(buf + 6 * gs), *dl1 = dl + cfg->h.llr_stride;
+  bool ok = true;
+  for (int a = 0; a < nb_rx && ok; a++) ok = hipMemcpyAsync((uint8_t *)dy + a * gb, rxdataF[a], gb, hipMemcpyHostToDevice, g_scr.s) == hipSuccess;
+  for (int pa = 0; pa < 4 && ok; pa++)
+    if ((pa & 1) < nb_rx)
+      ok = hipMemcpyAsync((uint8_t *)de + pa * gb, dl_ch_estimates[pa], gb, hipMemcpyHostToDevice, g_scr.s) == hipSuccess;
+  int rc = -1;
+  if (ok && oai4g_rx_batch_tm3_2cw(cfg, 1, dy, de, dl, dl1, 0, g_scr.s) == 0 &&
+      hipMemcpyAsync(llr0, dl, (size_t)n * 2, hipMemcpyDeviceToHost, g_scr.s) == hipSuccess &&
+      hipMemcpyAsync(llr1, dl1, (size_t)n * 2, hipMemcpyDeviceToHost, g_scr.s) == hipSuccess &&
+      (!log2_maxh || hipMemcpyAsync(log2_maxh, cfg->d_shift, 1, hipMemcpyDeviceToHost, g_scr.s) == hipSuccess) &&
+      hipStreamSynchronize(g_scr.s) == hipSuccess)
+    rc = n;
+  else
+    set_err("rx_pdsch_tm3_2cw: HIP error");
   return rc;
 }
 

@@ -188,6 +188,64 @@ __global__ void __launch_bounds__(256) k_rx_llr_tm3(const rx_dev_t *__restrict__
   }
 }
 
+/* TM3 with both codewords QPSK (dlsch_demodulation.c:643-669): the compensation keeps both precoded
+ * streams, dlsch_dual_stream_correlation gives rho = conj(h0') h1' and rho2 = conj(h1') h0', the MRC
+ * averages stream 0 and rho over the RX antennas (stream 1 and rho2 stay antenna 0's with
+ * dual_stream_flag 0), and dlsch_qpsk_qpsk_llr yields codeword 0 (comp0, comp1, rho) and codeword 1
+ * (comp1, comp0, rho2); both scrambled with q = 0 as dlsim transmits them */
+__global__ void __launch_bounds__(256) k_rx_llr_tm3qq(const rx_dev_t *__restrict__ c, const int32_t *__restrict__ rxF,
+                                                      const int32_t *__restrict__ est, size_t plane,
+                                                      int16_t *__restrict__ llr0, int16_t *__restrict__ llr1,
+                                                      const uint8_t *__restrict__ shift, int unscramble)
+{
+  const uint32_t sf = blockIdx.y, k = blockIdx.x, sfi = (c->first_sf + sf * c->sf_step) % 10;
+  const uint32_t l = c->npdcch + k, len = c->len[sfi][k], nb_rx = c->nb_rx, NS = c->nsymb * c->N;
+  rg32_t *map = (rg32_t *)(c->map + c->map_off[sfi][k]);
+  const size_t eo = ((size_t)sf * c->nsymb + l) * c->N, oo = (size_t)sf * c->llr_stride + c->llr_off[sfi][k];
+  const uint32_t sh = shift[sf], base = c->llr_off[sfi][k];
+  rg32_t *gold = (rg32_t *)(c->gold + (size_t)sfi * c->gold_words);
+  for (uint32_t j = threadIdx.x; j < len; j += blockDim.x) {
+    const uint32_t mw = map[j];
+    const bool neg = (j & 1u) != 0;
+    int16_t c0r[2], c0i[2], r0r[2], r0i[2], c1r = 0, c1i = 0, q2r = 0, q2i = 0;
+#pragma unroll
+    for (uint32_t a = 0; a < 2; a++) {
+      const uint32_t aa = a < nb_rx ? a : 0u;
+      const uint32_t yv = (uint32_t)rxF[((size_t)sf * nb_rx + aa) * NS + (size_t)l * c->N + (mw & 0xFFFFu)];
+      const uint32_t h0 = (uint32_t)est[aa * plane + eo + (mw >> 16)], h1 = (uint32_t)est[(2 + aa) * plane + eo + (mw >> 16)];
+      const uint32_t p0 = rx_prec_tm3(h0, h1, neg), p1 = rx_prec_tm3_s1(h0, h1, neg);
+      rx_conj_mul(p0, yv, sh, c0r[a], c0i[a]);
+      rx_conj_mul(p0, p1, sh, r0r[a], r0i[a]);
+      if (a == 0) {
+        rx_conj_mul(p1, yv, sh, c1r, c1i);
+        rx_conj_mul(p1, p0, sh, q2r, q2i);
+      }
+    }
+    if (nb_rx > 1) {                                            /* dlsch_detection_mrc: stream 0, rho */
+      c0r[0] = rx_sat16((c0r[0] >> 1) + (c0r[1] >> 1));
+      c0i[0] = rx_sat16((c0i[0] >> 1) + (c0i[1] >> 1));
+      r0r[0] = rx_sat16((r0r[0] >> 1) + (r0r[1] >> 1));
+      r0i[0] = rx_sat16((r0i[0] >> 1) + (r0i[1] >> 1));
+    }
+    int16_t v[6];
+    rx_qq_llr(c0r[0], c0i[0], c1r, c1i, r0r[0], r0i[0], v);
+    rx_llr_store<2>(v, unscramble ? gold : nullptr, base + 2 * j, llr0 + oo + 2 * j);
+    rx_qq_llr(c1r, c1i, c0r[0], c0i[0], q2r, q2i, v);
+    rx_llr_store<2>(v, unscramble ? gold : nullptr, base + 2 * j, llr1 + oo + 2 * j);
+  }
+}
+
+hipError_t oai4g_launch_rx_tm3qq(const rx_dev_t *d_cfg, const rx_dev_t *h_cfg, int n_sf, const int32_t *d_rxF,
+                                 const int32_t *d_est, size_t plane, int16_t *d_llr0, int16_t *d_llr1,
+                                 uint8_t *d_shift, int unscramble, hipStream_t s)
+{
+  if (n_sf <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_rx_level_tm3, dim3(n_sf), dim3(256), 0, s, d_cfg, d_est, plane, d_shift);
+  hipLaunchKernelGGL(k_rx_llr_tm3qq, dim3(h_cfg->n_sym, n_sf), dim3(256), 0, s, d_cfg, d_rxF, d_est, plane, d_llr0,
+                     d_llr1, d_shift, unscramble);
+  return hipGetLastError();
+}
+
 hipError_t oai4g_launch_rx_tm3(const rx_dev_t *d_cfg, const rx_dev_t *h_cfg, int n_sf, const int32_t *d_rxF,
                                const int32_t *d_est, size_t plane, int16_t *d_llr, uint8_t *d_shift, int unscramble,
                                hipStream_t s)

@@ -99,6 +99,45 @@ static __device__ __forceinline__ uint32_t rx_prec_tm3(uint32_t h0, uint32_t h1,
   return (uint32_t)(uint16_t)r | ((uint32_t)(uint16_t)i << 16);
 }
 
+/* the stream-1 channel of prec2A_TM3_128: (h0 - s h1) >> 1 per component (subs_epi16, srai) */
+static __device__ __forceinline__ uint32_t rx_prec_tm3_s1(uint32_t h0, uint32_t h1, bool neg)
+{
+  const int16_t b0 = neg ? (int16_t)(-(int32_t)(int16_t)h1) : (int16_t)h1;
+  const int16_t b1 = neg ? (int16_t)(-(int32_t)(int16_t)(h1 >> 16)) : (int16_t)(h1 >> 16);
+  const int16_t r = (int16_t)(rx_sat16((int32_t)(int16_t)h0 - b0) >> 1);
+  const int16_t i = (int16_t)(rx_sat16((int32_t)(int16_t)(h0 >> 16) - b1) >> 1);
+  return (uint32_t)(uint16_t)r | ((uint32_t)(uint16_t)i << 16);
+}
+
+/* conj(a) b >> sh, saturated per component (the madd / sign_epi16 / packs of the compensation and
+ * of dlsch_dual_stream_correlation) */
+static __device__ __forceinline__ void rx_conj_mul(uint32_t a, uint32_t b, uint32_t sh, int16_t &re, int16_t &im)
+{
+  const int16_t ar = (int16_t)a, ai = (int16_t)(a >> 16), br = (int16_t)b, bi = (int16_t)(b >> 16);
+  re = rx_sat16(rx_madd(ar, br, ai, bi) >> sh);
+  im = rx_sat16(rx_madd((int16_t)(-(int32_t)ai), br, ar, bi) >> sh);
+}
+
+/* qpsk_qpsk (dlsch_llr_computation.c:1041-1230) on one RE: the interference-aware max-log LLRs of
+ * QPSK stream y0 with QPSK interference y1 of correlation rho (int16 saturating throughout) */
+static __device__ __forceinline__ void rx_qq_llr(int16_t y0r, int16_t y0i, int16_t y1r, int16_t y1i, int16_t rr,
+                                                 int16_t ri, int16_t *v)
+{
+  auto S = [](int32_t a, int32_t b) { return rx_sat16(a + b); };
+  auto D = [](int32_t a, int32_t b) { return rx_sat16(a - b); };
+  auto M = [](int16_t a, int16_t b) { return a > b ? a : b; };
+  const int16_t rpi = (int16_t)(((int32_t)S(rr, ri) * 23170) >> 16), rmi = (int16_t)(((int32_t)D(rr, ri) * 23170) >> 16);
+  const int16_t y0r2 = (int16_t)(y0r >> 1), y0i2 = (int16_t)(y0i >> 1), y1r2 = (int16_t)(y1r >> 1), y1i2 = (int16_t)(y1i >> 1);
+  const int16_t A = rx_abs16(D(y1r2, rpi)), B = rx_abs16(D(y1i2, rmi)), C = rx_abs16(D(y1r2, rmi)), Dd = rx_abs16(S(y1i2, rpi));
+  const int16_t E = rx_abs16(S(y1r2, rmi)), F = rx_abs16(D(y1i2, rpi)), G = rx_abs16(S(y1r2, rpi)), H = rx_abs16(S(y1i2, rmi));
+  const int16_t num_re = M(S(B, S(A, y0i2)), S(D(C, y0i2), Dd));
+  const int16_t den_re = M(S(F, S(E, y0i2)), S(D(G, y0i2), H));
+  const int16_t num_im = M(S(B, S(A, y0r2)), S(D(E, y0r2), F));
+  const int16_t den_im = M(S(Dd, S(C, y0r2)), S(D(G, y0r2), H));
+  v[0] = D(S(y0r, num_re), den_re);
+  v[1] = D(S(y0i, num_im), den_im);
+}
+
 /* log2_approx(avg) / 2 of dlsch_channel_level (log2_approx: bits 0..30) */
 static __device__ __forceinline__ uint8_t rx_shift_of(int32_t acc, uint32_t div)
 {

@@ -229,6 +229,9 @@ void orc_dlsch_unscrambling(int16_t *llr, int G, uint32_t c_init);
 int orc_rx_pdsch_tm3(const orc_frame_t *fp, int nb_rx, const int32_t *const *rxdataF, const int32_t *const *est,
                      const uint32_t rb_alloc[4], uint8_t Qm0, uint8_t Qm1, uint8_t mcs0, uint8_t num_pdcch_symbols,
                      uint8_t subframe, int16_t *llr, uint8_t *log2_maxh_out);
+int orc_rx_pdsch_tm3_qq(const orc_frame_t *fp, int nb_rx, const int32_t *const *rxdataF, const int32_t *const *est,
+                        const uint32_t rb_alloc[4], uint8_t mcs0, uint8_t num_pdcch_symbols, uint8_t subframe,
+                        int16_t *llr0, int16_t *llr1, uint8_t *log2_maxh_out);
 int orc_rx_pdsch_tm2(const orc_frame_t *fp, int nb_rx, const int32_t *const *rxdataF, const int32_t *const *est,
                      const uint32_t rb_alloc[4], uint8_t Qm, uint8_t num_pdcch_symbols, uint8_t subframe,
                      int16_t *llr, uint8_t *log2_maxh_out);

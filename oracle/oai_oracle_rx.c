@@ -472,6 +472,129 @@ int orc_rx_pdsch_tm3(const orc_frame_t *fp, int nb_rx, const int32_t *const *rxd
   return (int)(out - llr);
 }
 
+/* qpsk_qpsk (dlsch_llr_computation.c:1041-1230) on one RE: the interference-aware max-log LLRs of a
+ * QPSK stream y0 in presence of a QPSK stream y1 with correlation rho, all int16 saturating */
+static void qq_llr(const int16_t y0[2], const int16_t y1[2], const int16_t rho[2], int16_t out[2])
+{
+  const int16_t rpi = (int16_t)(((int32_t)sat16((int32_t)rho[0] + rho[1]) * 23170) >> 16);   /* mulhi, 1/sqrt8 */
+  const int16_t rmi = (int16_t)(((int32_t)sat16((int32_t)rho[0] - rho[1]) * 23170) >> 16);
+  const int16_t y0r2 = (int16_t)(y0[0] >> 1), y0i2 = (int16_t)(y0[1] >> 1);
+  const int16_t y1r2 = (int16_t)(y1[0] >> 1), y1i2 = (int16_t)(y1[1] >> 1);
+#define S_(a, b) sat16((int32_t)(a) + (b))
+#define D_(a, b) sat16((int32_t)(a) - (b))
+#define M_(a, b) ((a) > (b) ? (a) : (b))
+  const int16_t A = abs16(D_(y1r2, rpi)), B = abs16(D_(y1i2, rmi)), C = abs16(D_(y1r2, rmi)), D = abs16(S_(y1i2, rpi));
+  const int16_t E = abs16(S_(y1r2, rmi)), F = abs16(D_(y1i2, rpi)), G = abs16(S_(y1r2, rpi)), H = abs16(S_(y1i2, rmi));
+  const int16_t num_re = M_(S_(B, S_(A, y0i2)), S_(D_(C, y0i2), D));
+  const int16_t den_re = M_(S_(F, S_(E, y0i2)), S_(D_(G, y0i2), H));
+  const int16_t num_im = M_(S_(B, S_(A, y0r2)), S_(D_(E, y0r2), F));
+  const int16_t den_im = M_(S_(D, S_(C, y0r2)), S_(D_(G, y0r2), H));
+  out[0] = D_(S_(y0[0], num_re), den_re);
+  out[1] = D_(S_(y0[1], num_im), den_im);
+#undef S_
+#undef D_
+#undef M_
+}
+
+/* rx_pdsch for TM3 with both codewords QPSK (dlsch_demodulation.c:373-413, 537-552, 643-669):
+ * dlsch_channel_compensation_TM3 keeps both precoded channels h0' = (h0 +sat s h1) >> 1,
+ * h1' = (h0 -sat s h1) >> 1 and both matched-filter outputs; dlsch_dual_stream_correlation gives
+ * rho = conj(h0') h1' and rho2 = conj(h1') h0' (>> log2_maxh, packs); dlsch_detection_mrc averages
+ * stream 0 and rho over the RX antennas (with dual_stream_flag 0 stream 1 and rho2 stay antenna 0's);
+ * dlsch_qpsk_qpsk_llr then gives codeword 0 from (comp0, comp1, rho) and codeword 1 from (comp1,
+ * comp0, rho2).  Writes both LLR streams (same length); returns it or -1. */
+int orc_rx_pdsch_tm3_qq(const orc_frame_t *fp, int nb_rx, const int32_t *const *rxdataF, const int32_t *const *est,
+                        const uint32_t rb_alloc[4], uint8_t mcs0, uint8_t num_pdcch_symbols, uint8_t subframe,
+                        int16_t *llr0, int16_t *llr1, uint8_t *log2_maxh_out)
+{
+  if (nb_rx < 1 || nb_rx > 2 || mcs0 > 28) return -1;
+  const int N = fp->ofdm_symbol_size, nsymb = fp->Ncp == 0 ? 14 : 12;
+  const size_t X = 12 * 110 + 64;
+  int32_t *rx_ext = (int32_t *)calloc(2 * X, 4), *c0 = (int32_t *)calloc(2 * X, 4), *c1 = (int32_t *)calloc(2 * X, 4);
+  int16_t *cp0 = (int16_t *)calloc(2 * X * 2, 2), *cp1 = (int16_t *)calloc(2 * X * 2, 2);
+  int16_t *rho = (int16_t *)calloc(2 * X * 2, 2), *rho2 = (int16_t *)calloc(2 * X * 2, 2);
+  int16_t *o0 = llr0, *o1 = llr1;
+  int ok = 1;
+  uint8_t log2_maxh = 0;
+  for (int symbol = num_pdcch_symbols; symbol < nsymb && ok; symbol++) {
+    int nb_rb = 0, hw[2] = {0, 0};
+    for (int a = 0; a < nb_rx; a++)
+      (void)extract_dual(fp, rxdataF[a] + symbol * N, est[a] + symbol * N, est[2 + a] + symbol * N, rb_alloc,
+                         (uint8_t)symbol, subframe, rx_ext + a * X, c0 + a * X, c1 + a * X, &nb_rb, &hw[a]);
+    const int symbol_mod = symbol >= 7 - fp->Ncp ? symbol - (7 - fp->Ncp) : symbol;
+    const int pil = symbol_mod == 0 || symbol_mod == 4 - fp->Ncp;
+    if (nb_rb == 0) { ok = 0; break; }
+    if (symbol == num_pdcch_symbols) {              /* dlsch_channel_level_TM3, as orc_rx_pdsch_tm3 */
+      const int nre = symbol_mod == 0 ? 8 : 12;
+      if (hw[0] < nb_rb * nre) { ok = 0; break; }
+      uint32_t lane[4] = {0, 0, 0, 0};
+      int32_t avg[2] = {0, 0};
+      for (int a = 0; a < nb_rx; a++) {
+        for (int rb = 0; rb < nb_rb; rb++)
+          for (int r = 0; r < (nre == 8 ? 2 : 3); r++)
+            for (int k = 0; k < 4; k++) {
+              const int e = rb * nre + 4 * r + k;
+              int16_t h0[2], h1[2];
+              memcpy(h0, &c0[a * X + e], 4);
+              memcpy(h1, &c1[a * X + e], 4);
+              const int s = (k & 1) ? -1 : 1;
+              int16_t p0[2];
+              for (int c = 0; c < 2; c++) p0[c] = (int16_t)(sat16((int32_t)h0[c] + sgn16(h1[c], s)) >> 1);
+              lane[k] += (uint32_t)((int32_t)p0[0] * p0[0]) + (uint32_t)((int32_t)p0[1] * p0[1]);
+            }
+        const int div = nb_rb * nre;
+        avg[a] = (int32_t)lane[0] / div + (int32_t)lane[1] / div + (int32_t)lane[2] / div + (int32_t)lane[3] / div;
+      }
+      const int32_t avg0 = nb_rx > 1 ? (avg[0] > avg[1] ? avg[0] : avg[1]) : (avg[0] > 0 ? avg[0] : 0);
+      const int v = (int)orc_log2_approx((uint32_t)avg0) - 13 + mumimo_off[mcs0][0];
+      log2_maxh = (uint8_t)(v > 0 ? v : 0);
+    }
+    const int n = nb_rb * (pil ? 8 : 12);
+    for (int a = 0; a < nb_rx; a++)
+      for (int e = 0; e < n; e++) {
+        int16_t h0[2], h1[2], y[2], p0[2], p1[2];
+        memcpy(h0, &c0[a * X + e], 4);
+        memcpy(h1, &c1[a * X + e], 4);
+        memcpy(y, &rx_ext[a * X + e], 4);
+        const int s = (e & 1) ? -1 : 1;
+        for (int c = 0; c < 2; c++) {
+          const int16_t t = sgn16(h1[c], s);
+          p0[c] = (int16_t)(sat16((int32_t)h0[c] + t) >> 1);
+          p1[c] = (int16_t)(sat16((int32_t)h0[c] - t) >> 1);
+        }
+        const size_t o = (a * X + e) * 2;
+        const int16_t n0 = (int16_t)-p0[1], n1 = (int16_t)-p1[1];        /* sign_epi16 by the conjugate mask */
+        cp0[o] = sat16((int32_t)((uint32_t)((int32_t)p0[0] * y[0]) + (uint32_t)((int32_t)p0[1] * y[1])) >> log2_maxh);
+        cp0[o + 1] = sat16((int32_t)((uint32_t)((int32_t)n0 * y[0]) + (uint32_t)((int32_t)p0[0] * y[1])) >> log2_maxh);
+        cp1[o] = sat16((int32_t)((uint32_t)((int32_t)p1[0] * y[0]) + (uint32_t)((int32_t)p1[1] * y[1])) >> log2_maxh);
+        cp1[o + 1] = sat16((int32_t)((uint32_t)((int32_t)n1 * y[0]) + (uint32_t)((int32_t)p1[0] * y[1])) >> log2_maxh);
+        rho[o] = sat16((int32_t)((uint32_t)((int32_t)p0[0] * p1[0]) + (uint32_t)((int32_t)p0[1] * p1[1])) >> log2_maxh);
+        rho[o + 1] = sat16((int32_t)((uint32_t)((int32_t)n0 * p1[0]) + (uint32_t)((int32_t)p0[0] * p1[1])) >> log2_maxh);
+        rho2[o] = sat16((int32_t)((uint32_t)((int32_t)p1[0] * p0[0]) + (uint32_t)((int32_t)p1[1] * p0[1])) >> log2_maxh);
+        rho2[o + 1] = sat16((int32_t)((uint32_t)((int32_t)n1 * p0[0]) + (uint32_t)((int32_t)p1[0] * p0[1])) >> log2_maxh);
+      }
+    if (nb_rx > 1)                                  /* dlsch_detection_mrc: stream 0 and rho only */
+      for (int e = 0; e < n; e++)
+        for (int c = 0; c < 2; c++) {
+          cp0[e * 2 + c] = sat16((cp0[e * 2 + c] >> 1) + (cp0[(X + e) * 2 + c] >> 1));
+          rho[e * 2 + c] = sat16((rho[e * 2 + c] >> 1) + (rho[(X + e) * 2 + c] >> 1));
+        }
+    const int len = pil ? nb_rb * 8 - 2 * orc_adjust_G2(fp, rb_alloc, subframe, (uint8_t)symbol) / 3
+                        : nb_rb * 12 - orc_adjust_G2(fp, rb_alloc, subframe, (uint8_t)symbol);
+    if (len > hw[0]) { ok = 0; break; }
+    for (int j = 0; j < len; j++) {
+      qq_llr(&cp0[2 * j], &cp1[2 * j], &rho[2 * j], o0);
+      qq_llr(&cp1[2 * j], &cp0[2 * j], &rho2[2 * j], o1);
+      o0 += 2;
+      o1 += 2;
+    }
+  }
+  free(rx_ext); free(c0); free(c1); free(cp0); free(cp1); free(rho); free(rho2);
+  if (!ok) return -1;
+  if (log2_maxh_out) *log2_maxh_out = log2_maxh;
+  return (int)(o0 - llr0);
+}
+
 /* rx_pdsch for TM2 (ALAMOUTI, two TX ports) with dlsim's UE (dual_stream_flag 0,
  * dlsch_demodulation.c:82-800):
  *   dlsch_extract_rbs_dual      as for TM3 (extract_dual above)

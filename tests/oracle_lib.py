@@ -626,3 +626,26 @@ def rx_pdsch_tm2(fp, rxF, est, rb_alloc, Qm, num_pdcch, subframe, check=True):
         return None, 0
     assert n >= 0
     return out[:n], sh.value
+
+
+def rx_pdsch_tm3_qq(fp, rxF, est, rb_alloc, mcs0, num_pdcch, subframe, check=True):
+    """orc_rx_pdsch_tm3_qq: TM3 with both codewords QPSK (the interference-aware qpsk_qpsk LLRs of
+    both streams).  Returns (LLRs of codeword 0, LLRs of codeword 1, log2_maxh)."""
+    nb_rx = len(rxF)
+    rx = [np.ascontiguousarray(r, dtype=np.int32) for r in rxF]
+    keep = {k: np.ascontiguousarray(v, dtype=np.int32) for k, v in est.items()}
+    ep = (ctypes.c_void_p * 4)()
+    for (p_, a), arr in keep.items():
+        if a < nb_rx:
+            ep[2 * p_ + a] = arr.ctypes.data
+    rp = (ctypes.c_void_p * 2)(*[r.ctypes.data for r in rx] + [None] * (2 - nb_rx))
+    o0 = np.zeros(14 * 1200 * 2 + 64, dtype=np.int16)
+    o1 = np.zeros_like(o0)
+    sh = ctypes.c_uint8()
+    ra = (ctypes.c_uint32 * 4)(*rb_alloc)
+    n = orc().orc_rx_pdsch_tm3_qq(ctypes.byref(fp), nb_rx, rp, ep, ra, mcs0, num_pdcch, subframe, P(o0), P(o1),
+                                  ctypes.byref(sh))
+    if not check and n < 0:
+        return None, None, 0
+    assert n >= 0
+    return o0[:n], o1[:n], sh.value

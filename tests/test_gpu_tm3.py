@@ -86,3 +86,72 @@ def test_gpu_tm3_receive_loop(gpu, N_RB, mcs, npd, sf):
     rx.close()
     fep.close()
     pipe.close()
+
+
+QQ_RAND = [(100, 9, 1, 7, 2, None), (50, 5, 2, 3, 1, None), (25, 7, 1, 6, 2, None), (15, 3, 2, 4, 2, None),
+           (100, 8, 3, 8, 2, [0xF0F0F0F0, 0x0000FFFF, 0, 0x3])]
+
+
+@pytest.mark.parametrize("N_RB,mcs,npd,sf,nb_rx,ra", QQ_RAND)
+def test_gpu_tm3_qpsk_two_codewords_random_inputs(gpu, N_RB, mcs, npd, sf, nb_rx, ra):
+    """Both codewords QPSK: the dual-stream correlation and the interference-aware qpsk_qpsk LLRs of
+    both streams, bit-exact against the oracle on full-range random grids and estimates."""
+    ra = ra or alloc(N_RB)
+    fo = O.frame(N_RB, Nid_cell=N_RB + sf, nb_antennas_tx=2, mode1_flag=0)
+    fg = gpu.frame_parms(N_RB, Nid_cell=N_RB + sf, nb_antennas_tx=2, mode1_flag=0)
+    n = fo.symbols_per_tti * fo.ofdm_symbol_size
+    rng = np.random.default_rng(N_RB * 5 + mcs + sf)
+    for scale in (2 ** 31 - 1, 3000):
+        rx = [rng.integers(-scale, scale, n, dtype=np.int64).astype(np.int32) for _ in range(nb_rx)]
+        est = {(p, a): rng.integers(-scale, scale, n, dtype=np.int64).astype(np.int32) for p in (0, 1)
+               for a in range(nb_rx)}
+        a0, a1, so = O.rx_pdsch_tm3_qq(fo, rx, est, ra, mcs, npd, sf)
+        g0, g1, sg = gpu.rx_pdsch_tm3_2cw(fg, rx, est, ra, mcs, npd, sf)
+        assert sg == so and np.array_equal(g0, a0) and np.array_equal(g1, a1), (scale, so, sg)
+
+
+@pytest.mark.parametrize("N_RB,mcs,npd,sf,nb_rx", [(100, 9, 1, 7, 2), (50, 6, 2, 3, 1)])
+def test_gpu_tm3_qpsk_receive_loop_both_codewords(gpu, N_RB, mcs, npd, sf, nb_rx):
+    """C3-shaped TM3 with both codewords QPSK through the GPU: TxPipeline -> channel H = [[2, 1],
+    [1, 2]] -> FepBatch -> 4 estimations -> RxBatchTM3.launch_2cw -> both transport blocks decode."""
+    n_tx, n_sf = 3, 2
+    p = c3_params(N_RB, mcs, npd, sf)
+    p.subframe_step = 1
+    pipe = gpu.TxPipeline(p, n_tx)
+    rng = np.random.default_rng(mcs + N_RB + 3)
+    pay = rng.integers(0, 256, size=(n_tx, 2, p.payload_stride), dtype=np.uint8)
+    pipe.upload_payload(pay)
+    pipe.run()
+    pipe.sync()
+    t16 = pipe.iq().view(np.int16).astype(np.int64)              # [n_tx][2][spt * 2]
+    H = [[2, 1], [1, 2]][:nb_rx]
+    rxs = [np.clip(H[a][0] * t16[:, 0] + H[a][1] * t16[:, 1], -32768, 32767).astype(np.int16).view(np.int32)
+           for a in range(nb_rx)]
+    iq = np.ascontiguousarray(np.stack(rxs, axis=1))
+    fg = gpu.frame_parms(N_RB, nb_antennas_tx=2, mode1_flag=0)
+    fep = gpu.FepBatch(fg, n_tx, nb_rx)
+    fep.upload(iq)
+    fep.run()
+    rx = gpu.RxBatchTM3(fg, alloc(N_RB), 2, 2, mcs, npd, p.rnti, n_sf, nb_rx=nb_rx, first_subframe=sf)
+    rx.estimate(fep.d_rxF, first_subframe=sf)
+    rx.launch_2cw(fep.d_rxF, unscramble=1)
+    l0, l1 = rx.llrs(), rx.llrs1()
+    rxF = fep.result()
+    fo = O.frame(N_RB, nb_antennas_tx=2, mode1_flag=0)
+    for i in range(n_sf):
+        s_ = (sf + i) % 10
+        est = {(pp, a): O.chest_subframe(fo, rxF[i, a].ravel(), rxF[i + 1, a, 0], s_, p=pp) for pp in (0, 1)
+               for a in range(nb_rx)}
+        a0, a1, _ = O.rx_pdsch_tm3_qq(fo, [rxF[i, a].ravel() for a in range(nb_rx)], est, alloc(N_RB), mcs, npd, s_)
+        G = rx.llr_count(s_)
+        for cw, (gl, ol) in enumerate(((l0, a0), (l1, a1))):
+            u = np.zeros(32 * (1 + G // 32), np.int16)
+            u[:G] = ol
+            O.dlsch_unscrambling(u, G, (p.rnti << 14) + (s_ << 9) + fo.Nid_cell)
+            assert len(ol) == G and np.array_equal(gl[i, :G], u[:G]), (s_, cw)
+            res, tb = decode_tb(gl[i, :G], G, p.TBS[cw], 2)
+            assert all(it <= 4 for it, _ in res), (s_, cw, [it for it, _ in res])
+            assert np.array_equal(tb, pay[i, cw, :p.TBS[cw] // 8]), (s_, cw)
+    rx.close()
+    fep.close()
+    pipe.close()

@@ -92,3 +92,29 @@ def test_tm3_rejects_qpsk_and_reports_garbage_free_lengths():
     for sf in (0, 5, 7):
         llr, _ = O.rx_pdsch_tm3(fp, rx, est, alloc(50), 4, 4, 14, 2, sf)
         assert len(llr) % 4 == 0 and len(llr) > 0
+
+
+# Both codewords QPSK: rx_pdsch runs the interference-aware dlsch_qpsk_qpsk_llr for each stream
+# (dlsch_demodulation.c:643-669), so dlsim decodes codeword 1 too.  Stream 1 is demodulated from
+# receive antenna 0 alone (dlsch_detection_mrc leaves it uncombined with dual_stream_flag 0), so the
+# channel's first row must keep the precoded streams apart: H = [[2, 1], [1, 2]].
+QQ = [(100, 9, 1, 7, 2), (50, 5, 2, 3, 2), (25, 7, 1, 6, 2), (100, 4, 3, 8, 1)]
+
+
+@pytest.mark.parametrize("N_RB,mcs,npdcch,sf,nb_rx", QQ)
+def test_tm3_qpsk_loop_decodes_both_codewords(N_RB, mcs, npdcch, sf, nb_rx):
+    p = c3_params(N_RB, mcs, npdcch, sf)
+    rng = np.random.default_rng(N_RB * mcs + sf + 1)
+    pays = [[rng.integers(0, 256, p.payload_stride, dtype=np.uint8) for _ in range(2)] for _ in range(2)]
+    H = [[2, 1], [1, 2]][:nb_rx]
+    fp, rxF, est = tm3_loop(p, sf, pays, H, nb_rx)
+    l0, l1, sh = O.rx_pdsch_tm3_qq(fp, rxF[:nb_rx], est, alloc(N_RB), mcs, npdcch, sf)
+    G = O.get_G(N_RB, 0, 0, 0, N_RB, alloc(N_RB), 2, 1, npdcch, sf)
+    assert len(l0) == G and len(l1) == G
+    for cw, llr in enumerate((l0, l1)):
+        u = np.zeros(32 * (1 + G // 32), np.int16)
+        u[:G] = llr
+        O.dlsch_unscrambling(u, G, (p.rnti << 14) + (sf << 9) + fp.Nid_cell)   # q = 0 for both (dlsim.c:2642-2647)
+        res, tb = decode_tb(u[:G], G, p.TBS[cw], 2)
+        assert all(it <= 4 for it, _ in res), (cw, [it for it, _ in res])
+        assert np.array_equal(tb, pays[0][cw][:p.TBS[cw] // 8]), cw
