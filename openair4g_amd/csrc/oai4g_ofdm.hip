@@ -611,7 +611,8 @@ struct modofdm_geom {
 };
 
 #ifndef OAI4G_DIAG_MODOFDM
-#define OAI4G_DIAG_MODOFDM 0   /* timing diagnostics only: 1 = no IQ stores, 2 = no e-bit staging, 3 = no QAM lookups */
+#define OAI4G_DIAG_MODOFDM 0   /* timing diagnostics only: 1 = no IQ stores, 2 = no e-bit staging, 3 = no QAM lookups,
+                                  4 = QAM table reads without bank conflicts */
 #endif
 #ifndef OAI4G_MODOFDM_WAVES
 #define OAI4G_MODOFDM_WAVES 3   /* measured: 3 waves/SIMD (<=168 VGPRs) beats 2 (no cap) and 4 (spills) */
@@ -772,6 +773,12 @@ __global__ void __launch_bounds__(128) MODOFDM_ATTR k_modofdm(const cfg_dev_t *_
             }
 #pragma unroll
             for (int n = 0; n < GR; n++) { lo[n] = e0[p[n] >> 5]; hi[n] = e0[(p[n] >> 5) + 1]; }
+#if OAI4G_DIAG_MODOFDM == 4   /* timing diagnostic: QAM table reads at lane-unique words (no bank conflicts) */
+            const uint32_t dkeep = c->with_crs ? 0xFFFFFFFFu : 0u, dlane = (uint32_t)threadIdx.x & 31u;
+#define QIDX(x) (((x) & dkeep) | (dlane & ~dkeep))
+#else
+#define QIDX(x) (x)
+#endif
             if constexpr (MODE == 1) {
 #pragma unroll
               for (int n = 0; n < GR; n++) {
@@ -781,7 +788,7 @@ __global__ void __launch_bounds__(128) MODOFDM_ATTR k_modofdm(const cfg_dev_t *_
               }
             } else {
 #pragma unroll
-              for (int n = 0; n < GR; n++) v0[n] = q0[__builtin_amdgcn_alignbit(hi[n], lo[n], p[n] & 31) & mask0];
+              for (int n = 0; n < GR; n++) v0[n] = q0[QIDX(__builtin_amdgcn_alignbit(hi[n], lo[n], p[n] & 31) & mask0)];
             }
             if constexpr (CW2) {
 #pragma unroll
@@ -791,7 +798,7 @@ __global__ void __launch_bounds__(128) MODOFDM_ATTR k_modofdm(const cfg_dev_t *_
                 hi[n] = e1[(p[n] >> 5) + 1];
               }
 #pragma unroll
-              for (int n = 0; n < GR; n++) v1[n] = q1[__builtin_amdgcn_alignbit(hi[n], lo[n], p[n] & 31) & mask1];
+              for (int n = 0; n < GR; n++) v1[n] = q1[QIDX(__builtin_amdgcn_alignbit(hi[n], lo[n], p[n] & 31) & mask1)];
             }
 #pragma unroll
             for (int n = 0; n < GR; n++) {
