@@ -1068,11 +1068,24 @@ static int upload_remap(oai4g_tx_config *cfg)
   if (!cfg->h_remap.empty()) {
     /* natural layout followed by the thread-major copy the fused kernel reads */
     const size_t n = cfg->h_remap.size(), N = cfg->h.N, T = N >> 4;
+#if OAI4G_MOD_STAGE
+    /* k_modofdm stages 4 entries per quad of data REs below a sentinel at 3N/4 */
+    for (int sf = 0; sf < 10; sf++)
+      for (int l = 0; l < 14; l++)
+        if (cfg->h.symnre[sf][l] + 3u > (3u * N) / 4u) { set_err("too many data REs per symbol for the modulator"); return -1; }
+#endif
     std::vector<uint16_t> both(2 * n);
     std::copy(cfg->h_remap.begin(), cfg->h_remap.end(), both.begin());
     for (size_t sl = 0; sl < n / N; sl++)
       for (size_t t = 0; t < T; t++)
-        for (size_t k = 0; k < 16; k++) both[n + sl * N + t * 16 + k] = cfg->h_remap[sl * N + t + T * k];
+        for (size_t k = 0; k < 16; k++) {
+          uint16_t code = cfg->h_remap[sl * N + t + T * k];
+#if OAI4G_MOD_STAGE
+          /* data RE (idx | parity << 15, idx < 3N/4): the byte offset 2 idx of its staged entry */
+          if (code < OAI4G_CTL_CODE) code = (uint16_t)((code & 0x8000u) | ((code & 0x3FFFu) << 1));
+#endif
+          both[n + sl * N + t * 16 + k] = code;
+        }
     HCK(hipMalloc(&cfg->d_remap, both.size() * 2), -1);
     HCK(hipMemcpy(cfg->d_remap, both.data(), both.size() * 2, hipMemcpyHostToDevice), -1);
     cfg->h.remap_tm = cfg->d_remap + n;

@@ -24,6 +24,10 @@
 #define OAI4G_CRS_CODE 0xE000u               /* remap codes >= this (and != 0xFFFF) are CRS REs:
                                                 CRS_CODE | pilot entry i << 9 | port & 1 << 8 | m */
 #define OAI4G_CTL_CODE 0xC000u               /* remap code of a control-region RE (generate_dci_top) */
+#ifndef OAI4G_MOD_STAGE
+#define OAI4G_MOD_STAGE 1   /* k_modofdm stages a QAM-table address per data RE (remap_tm data codes
+                               2 idx | parity << 15); 0 = per-RE bit extraction from staged e words */
+#endif
 #define OAI4G_ENC_CRC_TABLE_WORDS (256 + 256) /* byte tables A/B (the combine multipliers stay in global memory;
                                                   slice-by-4 tables, 2048 words, cost one workgroup per CU: slower) */
 #define OAI4G_GOLD_LANES 256

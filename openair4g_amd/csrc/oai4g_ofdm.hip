@@ -608,7 +608,17 @@ struct modofdm_geom {
   static constexpr int N = 1 << LOG2N, T = N >> 4, UNITS = 128 / T, LDSW = idft_sel<LOG2N>::XW;
   /* staged e-bit words per codeword: up to 12 N_RB <= 0.71 N data REs (15 PRB in 256) of 6 bits */
   static constexpr int EW = (6 * ((N * 3) / 4)) / 32 + 4;
+  /* OAI4G_MOD_STAGE: per codeword one 16-bit QAM-table address per data RE (12 N_RB + 3 <= 3N/4
+   * entries, host-checked), two sentinel entries at SENT; quad q = 4 REs, QPT quads per thread */
+  static constexpr int SENT = (N * 3) / 4, SW = SENT + 4, QPT = 3, QROW = 65;
 };
+
+/* 4 bytes from any byte address of global memory (unaligned dword load) */
+typedef uint32_t __attribute__((aligned(1))) u32_a1_t;
+static __device__ __forceinline__ uint32_t ld_u32_any(const uint8_t *p)
+{
+  return *(const __attribute__((address_space(1))) u32_a1_t *)p;
+}
 
 #ifndef OAI4G_DIAG_MODOFDM
 #define OAI4G_DIAG_MODOFDM 0   /* timing diagnostics only: 1 = no IQ stores, 2 = no e-bit staging, 3 = no QAM lookups,
@@ -635,13 +645,39 @@ __global__ void __launch_bounds__(128) MODOFDM_ATTR k_modofdm(const cfg_dev_t *_
   constexpr bool CW2 = MODE == 2 || MODE == 3;
   constexpr uint32_t IPS = MODE == 3 ? 2u : 1u;   /* items per (subframe, symbol) */
   __shared__ uint32_t lds_data[UNITS * NA * LDSW];
+#if OAI4G_MOD_STAGE
+  /* per codeword, the qtab byte address of every data RE's QAM word: entries 4q..4q+3 staged from
+   * quad q's 4 Qm bits; entries SENT, SENT + 1 address the zero word that non-data REs read */
+  constexpr int SW = G::SW, SENT = G::SENT, QPT = G::QPT, QROW = G::QROW;
+  constexpr uint32_t QZERO = 4u * 64u;          /* byte address of qtab[0][64] = 0 */
+  __shared__ __attribute__((aligned(16))) uint16_t lds_s[UNITS][2][SW];
+  __shared__ uint32_t qtab[4][QROW];            /* row cw * 2 + pilot symbol: 64 packed IQ words + 0 */
+#else
   __shared__ uint32_t lds_e[UNITS][2][EW];
   __shared__ uint32_t qtab[2][2][64];          /* [cw][pilot symbol][Qm bits] -> packed IQ */
+#endif
   const int unit = threadIdx.x / T, t = threadIdx.x % T;
   typename idft_sel<LOG2N>::tw_t twr;
   twr.load(c->tw, t);
   const uint32_t n_ant = c->n_ant, nsymb = c->nsymb;
   constexpr uint32_t sps = ECP ? 6 : 7;
+#if OAI4G_MOD_STAGE
+  for (uint32_t i = threadIdx.x; i < 4 * QROW; i += blockDim.x) {
+    const uint32_t row = i / QROW, bits = i - row * QROW, cw = row >> 1, pil = row & 1;
+    uint32_t v = 0;
+    if (bits < 64) {
+      if constexpr (MODE == 1) {        /* one codeword: rows 0/1 = TA, rows 2/3 = TB */
+        const cw_dev_t &w = c->cw[0];
+        v = c2u(cw ? alm_tb(bits, w, pil) : alm_ta(bits, w, pil));
+      } else {
+        const cw_dev_t &w = c->cw[cw];
+        v = c2u(qam_map(bits, w.Qm, pil ? w.qam_b : w.qam_a, pil ? w.qpsk_b : w.qpsk_a));
+      }
+    }
+    qtab[row][bits] = v;
+  }
+  for (uint32_t i = threadIdx.x; i < UNITS * 4; i += blockDim.x) lds_s[i >> 2][(i >> 1) & 1][SENT + (i & 1)] = QZERO;
+#else
   for (uint32_t i = threadIdx.x; i < 256; i += blockDim.x) {
     const uint32_t cw = i >> 7, pil = (i >> 6) & 1, bits = i & 63;
     if constexpr (MODE == 1) {          /* one codeword: [0] = TA, [1] = TB */
@@ -652,6 +688,7 @@ __global__ void __launch_bounds__(128) MODOFDM_ATTR k_modofdm(const cfg_dev_t *_
       qtab[cw][pil][bits] = c2u(qam_map(bits, w.Qm, pil ? w.qam_b : w.qam_a, pil ? w.qpsk_b : w.qpsk_a));
     }
   }
+#endif
   const uint32_t Qm0 = c->cw[0].Qm, Qm1 = c->cw[1].Qm;
   const uint32_t mask0 = (1u << Qm0) - 1u, mask1 = (1u << Qm1) - 1u;
   __syncthreads();
@@ -662,18 +699,37 @@ __global__ void __launch_bounds__(128) MODOFDM_ATTR k_modofdm(const cfg_dev_t *_
   const int stride = gridDim.x * UNITS;
   struct pf_t {
     u32x4_t ra, rb;
+#if OAI4G_MOD_STAGE
+    uint32_t x0[QPT], x1[QPT];   /* quad q = t + k T: the 4 bytes holding its 4 Qm bits */
+#else
     uint32_t e0[EPT], e1[EPT];
+#endif
   } pf;
   auto fetch = [&](int bse) {
     const int item = bse + unit;
     const bool act = item < n_items;
-    const uint32_t it = (act ? (uint32_t)item : 0u) / IPS;
+    /* one unit per workgroup: the item is wave-uniform, so its table reads become scalar loads and
+     * the next item's vector loads need no wait before their use */
+    const uint32_t it0 = (act ? (uint32_t)item : 0u) / IPS;
+    const uint32_t it = UNITS == 1 ? __builtin_amdgcn_readfirstlane(it0) : it0;
     const uint32_t sf = it / nsymb, l = it - sf * nsymb;
     const uint32_t sfi = (c->first_sf + (sf0 + sf) * c->sf_step) % 10;
     const uint32_t nre = act ? c->symnre[sfi][l] : 0u, re0 = c->symbase[sfi][l];
     const gu128_t *rsrc = (const gu128_t *)(c->remap_tm + ((size_t)sfi * 14 + l) * N + (size_t)t * 16);
     pf.ra = rsrc[0];
     pf.rb = rsrc[1];
+#if OAI4G_MOD_STAGE
+    if (act && nre) {
+      const uint8_t *esf = (const uint8_t *)(ebits + (size_t)(sf * c->n_cw) * c->ebits_words);
+      const uint32_t nq = (nre + 3) >> 2;
+#pragma unroll
+      for (int k = 0; k < QPT; k++) {   /* unconditional (quads past nq re-read the last one): no branch */
+        const uint32_t q = min((uint32_t)t + (uint32_t)(k * T), nq - 1);
+        pf.x0[k] = ld_u32_any(esf + (((re0 + 4 * q) * Qm0) >> 3));
+        if constexpr (CW2) pf.x1[k] = ld_u32_any(esf + (size_t)4 * c->ebits_words + (((re0 + 4 * q) * Qm1) >> 3));
+      }
+    }
+#else
     if (act && nre && OAI4G_DIAG_MODOFDM != 2) {
       gu32_t *esf = (gu32_t *)(ebits + (size_t)(sf * c->n_cw) * c->ebits_words);
       const uint32_t wlo0 = (re0 * Qm0) >> 5, cnt0 = min((uint32_t)EW, (((re0 + nre) * Qm0 + 31) >> 5) - wlo0 + 1);
@@ -687,13 +743,15 @@ __global__ void __launch_bounds__(128) MODOFDM_ATTR k_modofdm(const cfg_dev_t *_
           if (t + k * T < (int)cnt1) pf.e1[k] = esf[c->ebits_words + wlo1 + t + k * T];
       }
     }
+#endif
   };
   fetch(blockIdx.x * UNITS);
 
   for (int base = blockIdx.x * UNITS; base < n_items; base += stride) {
     const int item = base + unit;
     const bool active = item < n_items;
-    const uint32_t it = (active ? (uint32_t)item : 0u) / IPS, pair = (uint32_t)item % IPS;
+    const uint32_t it0 = (active ? (uint32_t)item : 0u) / IPS, pair = (uint32_t)item % IPS;
+    const uint32_t it = UNITS == 1 ? __builtin_amdgcn_readfirstlane(it0) : it0;
     const uint32_t sf = it / nsymb, l = it - sf * nsymb;
     const uint32_t sfi = (c->first_sf + (sf0 + sf) * c->sf_step) % 10;
     const uint32_t nre = active ? c->symnre[sfi][l] : 0u, re0 = c->symbase[sfi][l];
@@ -720,6 +778,29 @@ __global__ void __launch_bounds__(128) MODOFDM_ATTR k_modofdm(const cfg_dev_t *_
 
     /* this thread's 16 RE codes (thread-major copy, prefetched) */
     const uint32_t rw[8] = {pf.ra.x, pf.ra.y, pf.ra.z, pf.ra.w, pf.rb.x, pf.rb.y, pf.rb.z, pf.rb.w};
+#if OAI4G_MOD_STAGE
+    /* stage, per codeword, the QAM-table address of every data RE of this symbol: quad q's 4 Qm
+     * bits from its prefetched bytes -> 4 entries (ALAMOUTI: even entries TA rows, odd TB rows) */
+    if (active && nre) {
+      const uint32_t nq = (nre + 3) >> 2;
+      auto stage = [&](uint32_t xw, uint32_t q, uint32_t Qm, uint32_t mask, uint32_t ra, uint32_t rb, uint16_t *dst) {
+        const uint32_t x = xw >> (((re0 + 4 * q) * Qm) & 7u);
+        const uint32_t s0 = ra + 4 * (x & mask), s1 = rb + 4 * ((x >> Qm) & mask);
+        const uint32_t s2 = ra + 4 * ((x >> (2 * Qm)) & mask), s3 = rb + 4 * ((x >> (3 * Qm)) & mask);
+        *(u32x2_t *)(dst + 4 * q) = (u32x2_t){s0 | (s1 << 16), s2 | (s3 << 16)};
+      };
+      constexpr uint32_t RB = 4u * QROW;   /* bytes per qtab row */
+#pragma unroll
+      for (int k = 0; k < QPT; k++) {
+        const uint32_t q = (uint32_t)t + (uint32_t)(k * T);
+        if (q < nq) {
+          if constexpr (MODE == 1) stage(pf.x0[k], q, Qm0, mask0, pil * RB, (2 + pil) * RB, lds_s[unit][0]);
+          else stage(pf.x0[k], q, Qm0, mask0, pil * RB, pil * RB, lds_s[unit][0]);
+          if constexpr (CW2) stage(pf.x1[k], q, Qm1, mask1, (2 + pil) * RB, (2 + pil) * RB, lds_s[unit][1]);
+        }
+      }
+    }
+#else
     /* stage this symbol's e bits of each codeword (prefetched words, coalesced) */
     const uint32_t wlo0 = (re0 * Qm0) >> 5, wlo1 = (re0 * Qm1) >> 5;
     if (active && nre && OAI4G_DIAG_MODOFDM != 2) {
@@ -734,16 +815,21 @@ __global__ void __launch_bounds__(128) MODOFDM_ATTR k_modofdm(const cfg_dev_t *_
           if (t + k * T < (int)cnt1) lds_e[unit][1][t + k * T] = pf.e1[k];
       }
     }
+#endif
     __syncthreads();
     fetch(base + stride);
 
     gu32_t *crs_tab = (gu32_t *)c->crs_tab;
     const bool crs = CRS && stat_sym;
     gu32_t *ctl_tab = (gu32_t *)c->ctl_tab;
+#if OAI4G_MOD_STAGE
+    const char *sb0 = (const char *)lds_s[unit][0], *sb1 = (const char *)lds_s[unit][1], *qb = (const char *)qtab;
+#else
     const uint32_t *e0 = lds_e[unit][0], *e1 = lds_e[unit][1];
     const uint32_t *q0 = qtab[0][pil], *q1 = qtab[1][pil];
     /* bit position of data RE idx within the staged words: idx * Qm + (re0 * Qm - 32 wlo) */
     const uint32_t b0 = re0 * Qm0 - 32 * wlo0, b1 = re0 * Qm1 - 32 * wlo1;
+#endif
     idft_any<LOG2N, NA>(
         lds_data + unit * NA * LDSW, t, active, twr,
         [&](s16x2 (*x)[16]) {
@@ -754,6 +840,45 @@ __global__ void __launch_bounds__(128) MODOFDM_ATTR k_modofdm(const cfg_dev_t *_
 #define OAI4G_MOD_GROUP 4   /* REs whose LDS round trips are issued together (register budget) */
 #endif
           constexpr int GR = OAI4G_MOD_GROUP;
+#if OAI4G_MOD_STAGE
+          /* remap_tm data codes are 2 idx | parity << 15 (ALAMOUTI: 2 (2i + role)): the byte
+           * offset of entry idx; any non-data code (>= 0xC000) clamps to the zero sentinel */
+          constexpr uint32_t AM = MODE == 1 ? 0x7FFCu : 0x7FFEu;
+#pragma unroll
+          for (int g = 0; g < 16; g += GR) {
+            uint32_t code[GR], v0[GR], v1[GR];
+#pragma unroll
+            for (int n = 0; n < GR; n++) {
+              code[n] = (rw[(g + n) >> 1] >> (16 * ((g + n) & 1))) & 0xFFFFu;
+              const uint32_t a = min(code[n] & AM, 2u * SENT);
+              v0[n] = *(const uint16_t *)(sb0 + a);
+              if constexpr (MODE == 1) v1[n] = *(const uint16_t *)(sb0 + a + 2);
+              if constexpr (CW2) v1[n] = *(const uint16_t *)(sb1 + a);
+            }
+#pragma unroll
+            for (int n = 0; n < GR; n++) {
+              v0[n] = *(const uint32_t *)(qb + v0[n]);
+              if constexpr (MODE == 1 || CW2) v1[n] = *(const uint32_t *)(qb + v1[n]);
+            }
+#pragma unroll
+            for (int n = 0; n < GR; n++) {
+              const s16x2 x0 = u2c(v0[n]);
+              if constexpr (MODE == 1) {
+                alm_pair(x0, u2c(v1[n]), (code[n] >> 1) & 1u, x[0][g + n], x[1][g + n]);
+              } else if constexpr (MODE == 3) {
+                const s16x2 x1 = u2c(v1[n]);
+                const uint32_t sel = ((re0 + ((code[n] & 0x7FFFu) >> 1)) & 7u) * 4u + 2u * pair;   /* (i mod 8, p) */
+#pragma unroll
+                for (int a = 0; a < 2; a++)
+                  x[a][g + n] = half_signed(((CDD4_QSEL >> (sel + a)) & 1u) ? x1 : x0, (CDD4_NEG >> (sel + a)) & 1u);
+              } else if constexpr (NA == 2) {
+                cdd_pair(x0, u2c(v1[n]), code[n] >> 15 & 1u, x[0][g + n], x[1][g + n]);
+              } else {
+                x[0][g + n] = x0;                                   /* TM1: SISO precoder */
+              }
+            }
+          }
+#else
 #if OAI4G_DIAG_MODOFDM == 3
 #pragma unroll
           for (int n = 0; n < 16; n++)
@@ -820,6 +945,7 @@ __global__ void __launch_bounds__(128) MODOFDM_ATTR k_modofdm(const cfg_dev_t *_
               }
             }
           }
+#endif
           if constexpr (CRS) {
             if (crs) {
               /* cell-specific RS (pilots.c:43-168): overwrite the antenna carrying port p */
