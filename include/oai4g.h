@@ -266,8 +266,11 @@ int oai4g_rx_batch(oai4g_rx_config_t *cfg, int n_sf, const int32_t *d_rxdataF, c
 /* TM3 (LARGE_CDD, two TX ports) with dlsim's UE (rx_pdsch with dual_stream_flag = 0,
  * dlsch_demodulation.c:82-800): dlsch_extract_rbs_dual, dlsch_channel_level_TM3 + log2_maxh,
  * dlsch_channel_compensation_TM3 (prec2A_TM3), dlsch_detection_mrc over nb_rx (1-2) receive
- * antennas, then the single-stream 16 / 64-QAM LLRs of codeword 0 (Qm0 4 / 6; the reference
- * computes no codeword-1 LLRs there).  Drop-in on host buffers: rxdataF[a] = [nsymb][N] per receive
+ * antennas, then codeword 0's LLRs: the single-stream 16 / 64-QAM LLRs for Qm0 4 / 6 (the reference
+ * computes no codeword-1 LLRs there); for Qm0 = 2 the interference-aware dlsch_qpsk_qpsk_llr /
+ * dlsch_qpsk_16qam_llr / dlsch_qpsk_64qam_llr against codeword 1 of modulation order Qm1
+ * (dlsch_demodulation.c:643-690, dlsch_llr_computation.c:983, :1232, :1516).  Drop-in on host
+ * buffers: rxdataF[a] = [nsymb][N] per receive
  * antenna, dl_ch_estimates[p * 2 + a] = [nsymb][N] (the reference's dl_ch_estimates[(p << 1) + a]).
  * Returns the LLR count (not unscrambled) or -1. */
 int oai4g_rx_pdsch_tm3(const oai4g_frame_parms_t *frame_parms, int nb_rx, const int32_t *const *rxdataF,

@@ -3442,12 +3442,10 @@ static oai4g_rx_config_t *rx_config_build(const oai4g_frame_parms_t *fp, const u
     set_err("rx_config: TM1 (one TX port), Qm 2/4/6, 1..3 PDCCH symbols only");
     return nullptr;
   }
-  if (tm3 && (fp->nb_antennas_tx != 2 || fp->mode1_flag != 0 || (Qm != 4 && Qm != 6 && !(Qm == 2 && Qm1 == 2)) ||
+  if (tm3 && (fp->nb_antennas_tx != 2 || fp->mode1_flag != 0 || (Qm != 2 && Qm != 4 && Qm != 6) ||
               (Qm1 != 2 && Qm1 != 4 && Qm1 != 6) || mcs0 > 28 || nb_rx < 1 || nb_rx > 2 || num_pdcch_symbols < 1 ||
               num_pdcch_symbols > 3)) {
-    set_err("rx_config_tm3: two TX ports, Qm0 4/6 with Qm1 2/4/6 or Qm0 = Qm1 = 2 (Qm0 = 2 with a 16/64-QAM "
-            "codeword 1 needs the qpsk_16qam / qpsk_64qam LLRs), "
-            "1-2 RX antennas, 1..3 PDCCH symbols");
+    set_err("rx_config_tm3: two TX ports, Qm0 and Qm1 2/4/6, 1-2 RX antennas, 1..3 PDCCH symbols");
     return nullptr;
   }
   const uint32_t nsymb = fp->Ncp == 0 ? 14 : 12, N = fp->ofdm_symbol_size;
@@ -3473,6 +3471,7 @@ static oai4g_rx_config_t *rx_config_build(const oai4g_frame_parms_t *fp, const u
   h.tm2 = tm2 ? 1u : 0u;
   h.nb_rx = dual ? nb_rx : 1u;
   h.mu_off = tm3 ? k_mumimo_off[mcs0][(Qm1 >> 1) - 1] : 0;
+  h.qm1 = tm3 ? Qm1 : 0u;
   std::vector<uint32_t> map;
   uint32_t max_llr = 0;
   for (uint32_t sf = 0; sf < 10; sf++) {
@@ -3631,7 +3630,6 @@ extern "C" int oai4g_rx_batch_tm3(oai4g_rx_config_t *cfg, int n_sf, const int32_
 {
   NEED_INIT(-1);
   if (!cfg || !cfg->h.tm3) { set_err("rx_batch_tm3: not a TM3 configuration (oai4g_rx_config_create_tm3)"); return -1; }
-  if (cfg->h.Qm == 2) { set_err("rx_batch_tm3: both codewords QPSK: oai4g_rx_batch_tm3_2cw"); return -1; }
   if (n_sf <= 0) return 0;
   if (rx_check_batch(cfg, n_sf) != 0) return -1;
   if (n_sf > cfg->shift_cap) {
@@ -3640,8 +3638,12 @@ extern "C" int oai4g_rx_batch_tm3(oai4g_rx_config_t *cfg, int n_sf, const int32_
     cfg->shift_cap = n_sf;
   }
   const size_t plane = (size_t)n_sf * cfg->h.nsymb * cfg->h.N;
-  HCK(oai4g_launch_rx_tm3(cfg->d, &cfg->h, n_sf, d_rxdataF, d_est, plane, d_llr, cfg->d_shift, unscramble,
-                          (hipStream_t)stream), -1);
+  if (cfg->h.Qm == 2)   /* codeword 0 QPSK: the interference-aware qpsk_qpsk / qpsk_16qam / qpsk_64qam LLRs */
+    HCK(oai4g_launch_rx_tm3qq(cfg->d, &cfg->h, n_sf, d_rxdataF, d_est, plane, d_llr, nullptr, cfg->d_shift, unscramble,
+                              (hipStream_t)stream), -1);
+  else
+    HCK(oai4g_launch_rx_tm3(cfg->d, &cfg->h, n_sf, d_rxdataF, d_est, plane, d_llr, cfg->d_shift, unscramble,
+                            (hipStream_t)stream), -1);
   return 0;
 }
 
@@ -3649,7 +3651,7 @@ extern "C" int oai4g_rx_batch_tm3_2cw(oai4g_rx_config_t *cfg, int n_sf, const in
                                       int16_t *d_llr0, int16_t *d_llr1, int unscramble, void *stream)
 {
   NEED_INIT(-1);
-  if (!cfg || !cfg->h.tm3 || cfg->h.Qm != 2) {
+  if (!cfg || !cfg->h.tm3 || cfg->h.Qm != 2 || cfg->h.qm1 != 2) {
     set_err("rx_batch_tm3_2cw: not a TM3 configuration with both codewords QPSK");
     return -1;
   }

@@ -381,12 +381,14 @@ struct rx_dev_t {
   int32_t mu_off;
   /* TM2 (ALAMOUTI, dual extraction): dlsch_channel_level over both ports, dlsch_alamouti */
   uint32_t tm2;
+  uint32_t qm1;                   /* TM3: codeword 1's modulation order (Qm = 2 picks qpsk_qpsk / _qam16 / _qam64) */
 };
 hipError_t oai4g_launch_rx_chest(const chest_dev_t *d_ce, const rx_dev_t *d_rx, const rx_dev_t *h_rx, int n_sf,
                                  const int32_t *d_rxF, int16_t *d_llr, uint8_t *d_shift, int unscramble, hipStream_t s);
 hipError_t oai4g_launch_rx_tm3(const rx_dev_t *d_cfg, const rx_dev_t *h_cfg, int n_sf, const int32_t *d_rxF,
                                const int32_t *d_est, size_t plane, int16_t *d_llr, uint8_t *d_shift, int unscramble,
                                hipStream_t s);
+/* TM3 with codeword 0 QPSK: Qm1 = 2 both codewords (d_llr1 may be null), Qm1 = 4 / 6 codeword 0 */
 hipError_t oai4g_launch_rx_tm3qq(const rx_dev_t *d_cfg, const rx_dev_t *h_cfg, int n_sf, const int32_t *d_rxF,
                                  const int32_t *d_est, size_t plane, int16_t *d_llr0, int16_t *d_llr1,
                                  uint8_t *d_shift, int unscramble, hipStream_t s);

@@ -695,7 +695,9 @@ __global__ void __launch_bounds__(128) MODOFDM_ATTR k_modofdm(const cfg_dev_t *_
 
   /* software pipeline: the RE codes and e-bit words of a unit's next item are loaded while the
    * current item is transformed, so no item starts with an exposed HBM round trip */
+#if !OAI4G_MOD_STAGE
   constexpr int EPT = (EW + T - 1) / T;          /* staged e words per thread and codeword */
+#endif
   const int stride = gridDim.x * UNITS;
   struct pf_t {
     u32x4_t ra, rb;

@@ -188,11 +188,14 @@ __global__ void __launch_bounds__(256) k_rx_llr_tm3(const rx_dev_t *__restrict__
   }
 }
 
-/* TM3 with both codewords QPSK (dlsch_demodulation.c:643-669): the compensation keeps both precoded
+/* TM3 with codeword 0 QPSK (dlsch_demodulation.c:643-690): the compensation keeps both precoded
  * streams, dlsch_dual_stream_correlation gives rho = conj(h0') h1' and rho2 = conj(h1') h0', the MRC
- * averages stream 0 and rho over the RX antennas (stream 1 and rho2 stay antenna 0's with
- * dual_stream_flag 0), and dlsch_qpsk_qpsk_llr yields codeword 0 (comp0, comp1, rho) and codeword 1
- * (comp1, comp0, rho2); both scrambled with q = 0 as dlsim transmits them */
+ * averages stream 0 and rho over the RX antennas (stream 1, rho2 and dl_ch_mag1 stay antenna 0's with
+ * dual_stream_flag 0).  QM1 = 2: dlsch_qpsk_qpsk_llr yields codeword 0 (comp0, comp1, rho) and, when
+ * llr1 is given, codeword 1 (comp1, comp0, rho2), both scrambled with q = 0 as dlsim transmits them;
+ * QM1 = 4 / 6: dlsch_qpsk_16qam_llr / dlsch_qpsk_64qam_llr yield codeword 0 from (comp0, comp1,
+ * dl_ch_mag1, rho) */
+template <int QM1>
 __global__ void __launch_bounds__(256) k_rx_llr_tm3qq(const rx_dev_t *__restrict__ c, const int32_t *__restrict__ rxF,
                                                       const int32_t *__restrict__ est, size_t plane,
                                                       int16_t *__restrict__ llr0, int16_t *__restrict__ llr1,
@@ -207,7 +210,7 @@ __global__ void __launch_bounds__(256) k_rx_llr_tm3qq(const rx_dev_t *__restrict
   for (uint32_t j = threadIdx.x; j < len; j += blockDim.x) {
     const uint32_t mw = map[j];
     const bool neg = (j & 1u) != 0;
-    int16_t c0r[2], c0i[2], r0r[2], r0i[2], c1r = 0, c1i = 0, q2r = 0, q2i = 0;
+    int16_t c0r[2], c0i[2], r0r[2], r0i[2], c1r = 0, c1i = 0, q2r = 0, q2i = 0, m1 = 0;
 #pragma unroll
     for (uint32_t a = 0; a < 2; a++) {
       const uint32_t aa = a < nb_rx ? a : 0u;
@@ -218,7 +221,12 @@ __global__ void __launch_bounds__(256) k_rx_llr_tm3qq(const rx_dev_t *__restrict
       rx_conj_mul(p0, p1, sh, r0r[a], r0i[a]);
       if (a == 0) {
         rx_conj_mul(p1, yv, sh, c1r, c1i);
-        rx_conj_mul(p1, p0, sh, q2r, q2i);
+        if (QM1 == 2) rx_conj_mul(p1, p0, sh, q2r, q2i);
+        if (QM1 > 2) {                                              /* dl_ch_mag1 of antenna 0 */
+          const int16_t hr = (int16_t)p1, hi = (int16_t)(p1 >> 16);
+          const int16_t m = rx_sat16(rx_madd(hr, hr, hi, hi) >> sh);
+          m1 = (int16_t)((((int32_t)m * (QM1 == 4 ? 20724 : 20225)) >> 16) << 1);   /* QAM16_n1 / QAM64_n1 */
+        }
       }
     }
     if (nb_rx > 1) {                                            /* dlsch_detection_mrc: stream 0, rho */
@@ -228,10 +236,13 @@ __global__ void __launch_bounds__(256) k_rx_llr_tm3qq(const rx_dev_t *__restrict
       r0i[0] = rx_sat16((r0i[0] >> 1) + (r0i[1] >> 1));
     }
     int16_t v[6];
-    rx_qq_llr(c0r[0], c0i[0], c1r, c1i, r0r[0], r0i[0], v);
+    if (QM1 == 2) rx_qq_llr(c0r[0], c0i[0], c1r, c1i, r0r[0], r0i[0], v);
+    else rx_qx_llr<QM1>(c0r[0], c0i[0], c1r, c1i, m1, r0r[0], r0i[0], v);
     rx_llr_store<2>(v, unscramble ? gold : nullptr, base + 2 * j, llr0 + oo + 2 * j);
-    rx_qq_llr(c1r, c1i, c0r[0], c0i[0], q2r, q2i, v);
-    rx_llr_store<2>(v, unscramble ? gold : nullptr, base + 2 * j, llr1 + oo + 2 * j);
+    if (QM1 == 2 && llr1) {
+      rx_qq_llr(c1r, c1i, c0r[0], c0i[0], q2r, q2i, v);
+      rx_llr_store<2>(v, unscramble ? gold : nullptr, base + 2 * j, llr1 + oo + 2 * j);
+    }
   }
 }
 
@@ -241,8 +252,13 @@ hipError_t oai4g_launch_rx_tm3qq(const rx_dev_t *d_cfg, const rx_dev_t *h_cfg, i
 {
   if (n_sf <= 0) return hipSuccess;
   hipLaunchKernelGGL(k_rx_level_tm3, dim3(n_sf), dim3(256), 0, s, d_cfg, d_est, plane, d_shift);
-  hipLaunchKernelGGL(k_rx_llr_tm3qq, dim3(h_cfg->n_sym, n_sf), dim3(256), 0, s, d_cfg, d_rxF, d_est, plane, d_llr0,
-                     d_llr1, d_shift, unscramble);
+  const dim3 g(h_cfg->n_sym, n_sf), b(256);
+  if (h_cfg->qm1 == 4)
+    hipLaunchKernelGGL(k_rx_llr_tm3qq<4>, g, b, 0, s, d_cfg, d_rxF, d_est, plane, d_llr0, nullptr, d_shift, unscramble);
+  else if (h_cfg->qm1 == 6)
+    hipLaunchKernelGGL(k_rx_llr_tm3qq<6>, g, b, 0, s, d_cfg, d_rxF, d_est, plane, d_llr0, nullptr, d_shift, unscramble);
+  else
+    hipLaunchKernelGGL(k_rx_llr_tm3qq<2>, g, b, 0, s, d_cfg, d_rxF, d_est, plane, d_llr0, d_llr1, d_shift, unscramble);
   return hipGetLastError();
 }
 

@@ -138,6 +138,51 @@ static __device__ __forceinline__ void rx_qq_llr(int16_t y0r, int16_t y0i, int16
   v[1] = D(S(y0i, num_im), den_im);
 }
 
+static __device__ __forceinline__ int16_t rx_mh(int16_t a, int16_t b) { return (int16_t)(((int32_t)a * b) >> 16); }
+static __device__ __forceinline__ int16_t rx_shl(int16_t a, int n) { return (int16_t)(uint16_t)((uint32_t)(uint16_t)a << n); }
+
+/* qpsk_qam16 (dlsch_llr_computation.c:1300-1514) / qpsk_qam64 (:1584-1814) on one RE: LLRs of the QPSK
+ * stream y0 with a 16 / 64-QAM interferer y1 of magnitude mag and correlation rho.  As written: y0's
+ * mulhi by 1/sqrt2 is overwritten by y0 << 1, interference_abs(_64qam)_epi16 picks the interferer
+ * amplitude from compare masks (OR of the masked constants), the 64-QAM psi_a is mulhi(., 23170) << 2 */
+template <int QM1>
+static __device__ __forceinline__ void rx_qx_llr(int16_t y0r, int16_t y0i, int16_t y1r, int16_t y1i, int16_t mag,
+                                                 int16_t rr, int16_t ri, int16_t *v)
+{
+  auto S = [](int32_t a, int32_t b) { return rx_sat16(a + b); };
+  auto D = [](int32_t a, int32_t b) { return rx_sat16(a - b); };
+  auto M = [](int16_t a, int16_t b) { return a > b ? a : b; };
+  const int16_t rpi = rx_shl(rx_mh(S(rr, ri), 23170), 1), rmi = rx_shl(rx_mh(D(rr, ri), 23170), 1);
+  const int16_t y0a = rx_shl(y0r, 1), y0b = rx_shl(y0i, 1);
+  const int16_t yp = S(y0a, y0b), ym = D(y0a, y0b);
+  const int16_t psi[8] = {rx_abs16(D(y1r, rpi)), rx_abs16(D(y1i, rmi)), rx_abs16(D(y1r, rmi)), rx_abs16(S(y1i, rpi)),
+                          rx_abs16(S(y1r, rmi)), rx_abs16(D(y1i, rpi)), rx_abs16(S(y1r, rpi)), rx_abs16(S(y1i, rmi))};
+  const int16_t c1x = (int16_t)(mag >> 1), c3x = S(c1x, mag);
+  int16_t met[4];
+#pragma unroll
+  for (int h = 0; h < 4; h++) {
+    int16_t a[2], sq[2];
+#pragma unroll
+    for (int c = 0; c < 2; c++) {
+      const int16_t x = psi[2 * h + c];
+      if (QM1 == 4) {
+        a[c] = x < mag ? (int16_t)10362 : (int16_t)31086;
+      } else {
+        const bool lt2 = x < mag, lt1 = x < c1x, gt3 = x > c3x;
+        a[c] = (int16_t)(((lt2 != lt1) ? 10726 : 0) | (lt1 ? 3575 : 0) | ((!lt2) != gt3 ? 17876 : 0) | (gt3 ? 25027 : 0));
+      }
+      const int16_t t = rx_shl(rx_mh(a[c], a[c]), 1);
+      sq[c] = QM1 == 4 ? rx_shl(rx_mh(rx_shl(rx_mh(t, 25905), 1), mag), 1) : rx_shl(rx_mh(rx_shl(rx_mh(t, 13272), 3), mag), 1);
+    }
+    int16_t pa = S(rx_shl(rx_mh(psi[2 * h], a[0]), 1), rx_shl(rx_mh(psi[2 * h + 1], a[1]), 1));
+    if (QM1 == 6) pa = rx_shl(rx_mh(pa, 23170), 2);
+    const int16_t d = D(pa, S(sq[0], sq[1]));
+    met[h] = h == 0 ? S(d, yp) : h == 1 ? S(d, ym) : h == 2 ? D(d, ym) : D(d, yp);
+  }
+  v[0] = D(M(met[0], met[1]), M(met[2], met[3]));
+  v[1] = D(M(met[0], met[2]), M(met[1], met[3]));
+}
+
 /* log2_approx(avg) / 2 of dlsch_channel_level (log2_approx: bits 0..30) */
 static __device__ __forceinline__ uint8_t rx_shift_of(int32_t acc, uint32_t div)
 {

@@ -224,11 +224,17 @@ int orc_rx_pdsch_siso(const orc_frame_t *fp, const int32_t *rxdataF, const int32
                       const uint32_t rb_alloc[4], uint8_t Qm, uint8_t num_pdcch_symbols, uint8_t subframe,
                       int16_t *llr, uint8_t *log2_maxh_out);
 void orc_dlsch_unscrambling(int16_t *llr, int G, uint32_t c_init);
-/* rx_pdsch for TM3 (LARGE_CDD, 2 ports), dual_stream_flag = 0: codeword 0's LLRs (Qm0 4 / 6).
+/* rx_pdsch for TM3 (LARGE_CDD, 2 ports), dual_stream_flag = 0: codeword 0's LLRs (Qm0 4 / 6; Qm0 2
+ * runs orc_rx_pdsch_tm3_q2 for codeword 0).
  * rxdataF[a] = [nsymb][N] per receive antenna, est[p * 2 + a] = [nsymb][N] estimates of port p. */
 int orc_rx_pdsch_tm3(const orc_frame_t *fp, int nb_rx, const int32_t *const *rxdataF, const int32_t *const *est,
                      const uint32_t rb_alloc[4], uint8_t Qm0, uint8_t Qm1, uint8_t mcs0, uint8_t num_pdcch_symbols,
                      uint8_t subframe, int16_t *llr, uint8_t *log2_maxh_out);
+/* TM3 with codeword 0 QPSK: Qm1 = 2 both codewords (qpsk_qpsk; llr1 may be NULL), Qm1 = 4 / 6 codeword 0
+ * (qpsk_qam16 / qpsk_qam64) */
+int orc_rx_pdsch_tm3_q2(const orc_frame_t *fp, int nb_rx, const int32_t *const *rxdataF, const int32_t *const *est,
+                        const uint32_t rb_alloc[4], uint8_t Qm1, uint8_t mcs0, uint8_t num_pdcch_symbols,
+                        uint8_t subframe, int16_t *llr0, int16_t *llr1, uint8_t *log2_maxh_out);
 int orc_rx_pdsch_tm3_qq(const orc_frame_t *fp, int nb_rx, const int32_t *const *rxdataF, const int32_t *const *est,
                         const uint32_t rb_alloc[4], uint8_t mcs0, uint8_t num_pdcch_symbols, uint8_t subframe,
                         int16_t *llr0, int16_t *llr1, uint8_t *log2_maxh_out);

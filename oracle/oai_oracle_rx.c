@@ -376,6 +376,9 @@ int orc_rx_pdsch_tm3(const orc_frame_t *fp, int nb_rx, const int32_t *const *rxd
                      uint8_t subframe, int16_t *llr, uint8_t *log2_maxh_out)
 {
   /* rxdataF[a] = [nsymb][N] of receive antenna a; est[p * 2 + a] = dl_ch_estimates[(p << 1) + a] */
+  if (Qm0 == 2)   /* codeword 0 QPSK: the interference-aware qpsk_qpsk / qpsk_qam16 / qpsk_qam64 LLRs */
+    return orc_rx_pdsch_tm3_q2(fp, nb_rx, rxdataF, est, rb_alloc, Qm1, mcs0, num_pdcch_symbols, subframe, llr,
+                               NULL, log2_maxh_out);
   if (nb_rx < 1 || nb_rx > 2 || (Qm0 != 4 && Qm0 != 6) || (Qm1 != 2 && Qm1 != 4 && Qm1 != 6) || mcs0 > 28) return -1;
   const int N = fp->ofdm_symbol_size, nsymb = fp->Ncp == 0 ? 14 : 12;
   const size_t X = 12 * 110 + 64;
@@ -496,6 +499,57 @@ static void qq_llr(const int16_t y0[2], const int16_t y1[2], const int16_t rho[2
 #undef M_
 }
 
+static int16_t mh16(int16_t a, int16_t b) { return (int16_t)(((int32_t)a * b) >> 16); }   /* mulhi_epi16 */
+static int16_t shl16(int16_t a, int n) { return (int16_t)(uint16_t)((uint32_t)(uint16_t)a << n); }   /* slli_epi16 */
+
+/* interference_abs_64qam_epi16 (dlsch_llr_computation.c:616): the amplitude of the 64-QAM
+ * interferer closest to psi, from the masks (psi < 2m) ^ (psi < m), psi < m, (psi >= 2m) ^ (psi > 3m),
+ * psi > 3m with m = mag >> 1, 2m = mag, 3m = m +sat mag; the masked constants are OR-ed */
+static int16_t ia64(int16_t psi, int16_t mag)
+{
+  const int16_t c1x = (int16_t)(mag >> 1), c2x = mag, c3x = sat16((int32_t)c1x + c2x);
+  const int lt2 = psi < c2x, lt1 = psi < c1x, gt3 = psi > c3x;
+  const int t = lt2 ^ lt1, t3 = (!lt2) ^ gt3;
+  return (int16_t)((t ? 10726 : 0) | (lt1 ? 3575 : 0) | (t3 ? 17876 : 0) | (gt3 ? 25027 : 0));
+}
+
+/* qpsk_qam16 (dlsch_llr_computation.c:1300-1514) / qpsk_qam64 (:1584-1814) on one RE: the LLRs of the
+ * QPSK stream y0 in presence of a 16 / 64-QAM stream y1 of magnitude mag (dl_ch_mag1) and correlation
+ * rho.  Kept as written: y0's mulhi by 1/sqrt2 is overwritten by y0 << 1 (:1397-1400); the 64-QAM
+ * branch scales psi_a by mulhi(., 23170) << 2 (:1761-1768) and its a^2 by sqrt(42)/4 << 3 (:622) */
+static void qx_llr(int qm1, const int16_t y0[2], const int16_t y1[2], int16_t mag, const int16_t rho[2], int16_t out[2])
+{
+  const int16_t rpi = shl16(mh16(sat16((int32_t)rho[0] + rho[1]), 23170), 1);
+  const int16_t rmi = shl16(mh16(sat16((int32_t)rho[0] - rho[1]), 23170), 1);
+  const int16_t y0r = shl16(y0[0], 1), y0i = shl16(y0[1], 1);
+  const int16_t yp = sat16((int32_t)y0r + y0i), ym = sat16((int32_t)y0r - y0i);
+  const int16_t y1r = y1[0], y1i = y1[1];
+  /* psi (r, i) for the interferer hypotheses (+1 +1), (+1 -1), (-1 +1), (-1 -1) */
+  const int16_t psi[8] = {abs16(sat16((int32_t)y1r - rpi)), abs16(sat16((int32_t)y1i - rmi)),
+                          abs16(sat16((int32_t)y1r - rmi)), abs16(sat16((int32_t)y1i + rpi)),
+                          abs16(sat16((int32_t)y1r + rmi)), abs16(sat16((int32_t)y1i - rpi)),
+                          abs16(sat16((int32_t)y1r + rpi)), abs16(sat16((int32_t)y1i + rmi))};
+  int16_t met[4];
+  for (int h = 0; h < 4; h++) {
+    int16_t a[2], sq[2];
+    for (int c = 0; c < 2; c++) {
+      const int16_t x = psi[2 * h + c];
+      a[c] = qm1 == 4 ? (int16_t)(x < mag ? 10362 : 31086) : ia64(x, mag);   /* interference_abs_epi16 (:612) */
+      const int16_t t = shl16(mh16(a[c], a[c]), 1);                          /* square_a(_64qam)_epi16 (:619, :622) */
+      sq[c] = qm1 == 4 ? shl16(mh16(shl16(mh16(t, 25905), 1), mag), 1) : shl16(mh16(shl16(mh16(t, 13272), 3), mag), 1);
+    }
+    int16_t pa = sat16((int32_t)shl16(mh16(psi[2 * h], a[0]), 1) + shl16(mh16(psi[2 * h + 1], a[1]), 1));   /* prodsum (:609) */
+    if (qm1 == 6) pa = shl16(mh16(pa, 23170), 2);
+    const int16_t d = sat16((int32_t)pa - sat16((int32_t)sq[0] + sq[1]));
+    met[h] = h == 0 ? sat16((int32_t)d + yp) : h == 1 ? sat16((int32_t)d + ym) : h == 2 ? sat16((int32_t)d - ym)
+                                                                                          : sat16((int32_t)d - yp);
+  }
+#define M_(a, b) ((a) > (b) ? (a) : (b))
+  out[0] = sat16((int32_t)M_(met[0], met[1]) - M_(met[2], met[3]));
+  out[1] = sat16((int32_t)M_(met[0], met[2]) - M_(met[1], met[3]));
+#undef M_
+}
+
 /* rx_pdsch for TM3 with both codewords QPSK (dlsch_demodulation.c:373-413, 537-552, 643-669):
  * dlsch_channel_compensation_TM3 keeps both precoded channels h0' = (h0 +sat s h1) >> 1,
  * h1' = (h0 -sat s h1) >> 1 and both matched-filter outputs; dlsch_dual_stream_correlation gives
@@ -503,16 +557,22 @@ static void qq_llr(const int16_t y0[2], const int16_t y1[2], const int16_t rho[2
  * stream 0 and rho over the RX antennas (with dual_stream_flag 0 stream 1 and rho2 stay antenna 0's);
  * dlsch_qpsk_qpsk_llr then gives codeword 0 from (comp0, comp1, rho) and codeword 1 from (comp1,
  * comp0, rho2).  Writes both LLR streams (same length); returns it or -1. */
-int orc_rx_pdsch_tm3_qq(const orc_frame_t *fp, int nb_rx, const int32_t *const *rxdataF, const int32_t *const *est,
-                        const uint32_t rb_alloc[4], uint8_t mcs0, uint8_t num_pdcch_symbols, uint8_t subframe,
-                        int16_t *llr0, int16_t *llr1, uint8_t *log2_maxh_out)
+/* Codeword 0 QPSK, codeword 1 of modulation order Qm1: Qm1 = 2 is the QPSK-QPSK case above (both
+ * codewords); Qm1 = 4 / 6 run dlsch_qpsk_16qam_llr / dlsch_qpsk_64qam_llr (:670-690) for codeword 0
+ * only, with dl_ch_mag1 = |h1'|^2 >> log2_maxh (packs) times QAM16_n1 / QAM64_n1 (mulhi << 1) of
+ * antenna 0 (the MRC leaves it alone with dual_stream_flag 0); llr1 is not written. */
+int orc_rx_pdsch_tm3_q2(const orc_frame_t *fp, int nb_rx, const int32_t *const *rxdataF, const int32_t *const *est,
+                        const uint32_t rb_alloc[4], uint8_t Qm1, uint8_t mcs0, uint8_t num_pdcch_symbols,
+                        uint8_t subframe, int16_t *llr0, int16_t *llr1, uint8_t *log2_maxh_out)
 {
-  if (nb_rx < 1 || nb_rx > 2 || mcs0 > 28) return -1;
+  if (nb_rx < 1 || nb_rx > 2 || mcs0 > 28 || (Qm1 != 2 && Qm1 != 4 && Qm1 != 6)) return -1;
   const int N = fp->ofdm_symbol_size, nsymb = fp->Ncp == 0 ? 14 : 12;
   const size_t X = 12 * 110 + 64;
   int32_t *rx_ext = (int32_t *)calloc(2 * X, 4), *c0 = (int32_t *)calloc(2 * X, 4), *c1 = (int32_t *)calloc(2 * X, 4);
   int16_t *cp0 = (int16_t *)calloc(2 * X * 2, 2), *cp1 = (int16_t *)calloc(2 * X * 2, 2);
   int16_t *rho = (int16_t *)calloc(2 * X * 2, 2), *rho2 = (int16_t *)calloc(2 * X * 2, 2);
+  int16_t *mag1 = (int16_t *)calloc(2 * X, 2);
+  const int16_t a1 = Qm1 == 4 ? QAM16_n1 : QAM64_n1;
   int16_t *o0 = llr0, *o1 = llr1;
   int ok = 1;
   uint8_t log2_maxh = 0;
@@ -546,7 +606,7 @@ int orc_rx_pdsch_tm3_qq(const orc_frame_t *fp, int nb_rx, const int32_t *const *
         avg[a] = (int32_t)lane[0] / div + (int32_t)lane[1] / div + (int32_t)lane[2] / div + (int32_t)lane[3] / div;
       }
       const int32_t avg0 = nb_rx > 1 ? (avg[0] > avg[1] ? avg[0] : avg[1]) : (avg[0] > 0 ? avg[0] : 0);
-      const int v = (int)orc_log2_approx((uint32_t)avg0) - 13 + mumimo_off[mcs0][0];
+      const int v = (int)orc_log2_approx((uint32_t)avg0) - 13 + mumimo_off[mcs0][(Qm1 >> 1) - 1];
       log2_maxh = (uint8_t)(v > 0 ? v : 0);
     }
     const int n = nb_rb * (pil ? 8 : 12);
@@ -572,6 +632,8 @@ int orc_rx_pdsch_tm3_qq(const orc_frame_t *fp, int nb_rx, const int32_t *const *
         rho[o + 1] = sat16((int32_t)((uint32_t)((int32_t)n0 * p1[0]) + (uint32_t)((int32_t)p0[0] * p1[1])) >> log2_maxh);
         rho2[o] = sat16((int32_t)((uint32_t)((int32_t)p1[0] * p0[0]) + (uint32_t)((int32_t)p1[1] * p0[1])) >> log2_maxh);
         rho2[o + 1] = sat16((int32_t)((uint32_t)((int32_t)n1 * p0[0]) + (uint32_t)((int32_t)p1[0] * p0[1])) >> log2_maxh);
+        const int16_t m1 = sat16((int32_t)((uint32_t)((int32_t)p1[0] * p1[0]) + (uint32_t)((int32_t)p1[1] * p1[1])) >> log2_maxh);
+        mag1[a * X + e] = mulhi2(m1, a1);
       }
     if (nb_rx > 1)                                  /* dlsch_detection_mrc: stream 0 and rho only */
       for (int e = 0; e < n; e++)
@@ -583,16 +645,28 @@ int orc_rx_pdsch_tm3_qq(const orc_frame_t *fp, int nb_rx, const int32_t *const *
                         : nb_rb * 12 - orc_adjust_G2(fp, rb_alloc, subframe, (uint8_t)symbol);
     if (len > hw[0]) { ok = 0; break; }
     for (int j = 0; j < len; j++) {
-      qq_llr(&cp0[2 * j], &cp1[2 * j], &rho[2 * j], o0);
-      qq_llr(&cp1[2 * j], &cp0[2 * j], &rho2[2 * j], o1);
+      if (Qm1 == 2) {
+        qq_llr(&cp0[2 * j], &cp1[2 * j], &rho[2 * j], o0);
+        if (o1) { qq_llr(&cp1[2 * j], &cp0[2 * j], &rho2[2 * j], o1); o1 += 2; }
+      } else {
+        qx_llr(Qm1, &cp0[2 * j], &cp1[2 * j], mag1[j], &rho[2 * j], o0);
+      }
       o0 += 2;
-      o1 += 2;
     }
   }
-  free(rx_ext); free(c0); free(c1); free(cp0); free(cp1); free(rho); free(rho2);
+  free(rx_ext); free(c0); free(c1); free(cp0); free(cp1); free(rho); free(rho2); free(mag1);
   if (!ok) return -1;
   if (log2_maxh_out) *log2_maxh_out = log2_maxh;
   return (int)(o0 - llr0);
+}
+
+int orc_rx_pdsch_tm3_qq(const orc_frame_t *fp, int nb_rx, const int32_t *const *rxdataF, const int32_t *const *est,
+                        const uint32_t rb_alloc[4], uint8_t mcs0, uint8_t num_pdcch_symbols, uint8_t subframe,
+                        int16_t *llr0, int16_t *llr1, uint8_t *log2_maxh_out)
+{
+  if (!llr1) return -1;
+  return orc_rx_pdsch_tm3_q2(fp, nb_rx, rxdataF, est, rb_alloc, 2, mcs0, num_pdcch_symbols, subframe, llr0, llr1,
+                             log2_maxh_out);
 }
 
 /* rx_pdsch for TM2 (ALAMOUTI, two TX ports) with dlsim's UE (dual_stream_flag 0,

@@ -155,3 +155,77 @@ def test_gpu_tm3_qpsk_receive_loop_both_codewords(gpu, N_RB, mcs, npd, sf, nb_rx
     rx.close()
     fep.close()
     pipe.close()
+
+
+QX_RAND = [(100, 4, 9, 1, 7, 2, None), (50, 6, 5, 2, 3, 1, None), (25, 4, 7, 1, 6, 2, None),
+           (15, 6, 3, 2, 4, 2, None), (100, 6, 8, 3, 8, 2, [0xF0F0F0F0, 0x0000FFFF, 0, 0x3]),
+           (50, 2, 6, 1, 2, 2, None)]
+
+
+@pytest.mark.parametrize("N_RB,Qm1,mcs,npd,sf,nb_rx,ra", QX_RAND)
+def test_gpu_tm3_qpsk_codeword0_random_inputs(gpu, N_RB, Qm1, mcs, npd, sf, nb_rx, ra):
+    """Codeword 0 QPSK through the drop-in rx_pdsch_tm3: qpsk_qam16 / qpsk_qam64 against a 16 / 64-QAM
+    codeword 1 (interferer magnitude dl_ch_mag1 of antenna 0), qpsk_qpsk's codeword 0 when both are
+    QPSK; bit-exact against the oracle on full-range random grids and estimates."""
+    ra = ra or alloc(N_RB)
+    fo = O.frame(N_RB, Nid_cell=N_RB + sf, nb_antennas_tx=2, mode1_flag=0)
+    fg = gpu.frame_parms(N_RB, Nid_cell=N_RB + sf, nb_antennas_tx=2, mode1_flag=0)
+    n = fo.symbols_per_tti * fo.ofdm_symbol_size
+    rng = np.random.default_rng(N_RB * 3 + Qm1 + mcs + sf)
+    for scale in (2 ** 31 - 1, 3000, 300):
+        rx = [rng.integers(-scale, scale, n, dtype=np.int64).astype(np.int32) for _ in range(nb_rx)]
+        est = {(p, a): rng.integers(-scale, scale, n, dtype=np.int64).astype(np.int32) for p in (0, 1)
+               for a in range(nb_rx)}
+        lo, so = O.rx_pdsch_tm3(fo, rx, est, ra, 2, Qm1, mcs, npd, sf)
+        lg, sg = gpu.rx_pdsch_tm3(fg, rx, est, ra, 2, Qm1, mcs, npd, sf)
+        assert sg == so and np.array_equal(lg, lo), (scale, so, sg)
+
+
+@pytest.mark.parametrize("N_RB,mcs0,mcs1,npd,sf", [(100, 9, 19, 1, 7), (50, 7, 14, 2, 3)])
+def test_gpu_tm3_qpsk_with_qam_interferer_receive_loop(gpu, N_RB, mcs0, mcs1, npd, sf):
+    """TM3 with codeword 0 QPSK and codeword 1 16 / 64-QAM through the GPU: TxPipeline -> H = [[2, 1],
+    [1, 2]] -> FepBatch -> 4 estimations -> RxBatchTM3 (qpsk_qam16 / qpsk_qam64) -> codeword 0 decodes,
+    LLRs bit-exact against the oracle's loop."""
+    import openair4g_amd as oai
+    n_tx, n_sf = 3, 2
+    p = oai.make_params("C3", subframe=sf, N_RB_DL=N_RB, nb_rb=N_RB, rb_alloc=alloc(N_RB), mcs=[mcs0, mcs1], TBS=None,
+                        num_pdcch_symbols=npd, with_crs=1, Nid_cell=0)
+    p.subframe_step = 1
+    pipe = gpu.TxPipeline(p, n_tx)
+    rng = np.random.default_rng(mcs0 + mcs1 + N_RB)
+    pay = rng.integers(0, 256, size=(n_tx, 2, p.payload_stride), dtype=np.uint8)
+    pipe.upload_payload(pay)
+    pipe.run()
+    pipe.sync()
+    t16 = pipe.iq().view(np.int16).astype(np.int64)
+    H = [[2, 1], [1, 2]]
+    rxs = [np.clip(H[a][0] * t16[:, 0] + H[a][1] * t16[:, 1], -32768, 32767).astype(np.int16).view(np.int32)
+           for a in range(2)]
+    iq = np.ascontiguousarray(np.stack(rxs, axis=1))
+    fg = gpu.frame_parms(N_RB, nb_antennas_tx=2, mode1_flag=0)
+    fep = gpu.FepBatch(fg, n_tx, 2)
+    fep.upload(iq)
+    fep.run()
+    Qm1 = 4 if mcs1 < 17 else 6
+    rx = gpu.RxBatchTM3(fg, alloc(N_RB), 2, Qm1, mcs0, npd, p.rnti, n_sf, nb_rx=2, first_subframe=sf)
+    rx.estimate(fep.d_rxF, first_subframe=sf)
+    rx.launch(fep.d_rxF, unscramble=1)
+    llr = rx.llrs()
+    rxF = fep.result()
+    fo = O.frame(N_RB, nb_antennas_tx=2, mode1_flag=0)
+    for i in range(n_sf):
+        s_ = (sf + i) % 10
+        est = {(pp, a): O.chest_subframe(fo, rxF[i, a].ravel(), rxF[i + 1, a, 0], s_, p=pp) for pp in (0, 1)
+               for a in range(2)}
+        lo, _ = O.rx_pdsch_tm3(fo, [rxF[i, 0].ravel(), rxF[i, 1].ravel()], est, alloc(N_RB), 2, Qm1, mcs0, npd, s_)
+        G = rx.llr_count(s_)
+        u = np.zeros(32 * (1 + G // 32), np.int16)
+        u[:G] = lo
+        O.dlsch_unscrambling(u, G, (p.rnti << 14) + (s_ << 9) + fo.Nid_cell)
+        assert len(lo) == G and np.array_equal(llr[i, :G], u[:G]), s_
+        res, tb = decode_tb(llr[i, :G], G, p.TBS[0], 2)
+        assert all(it <= 4 for it, _ in res), (s_, [it for it, _ in res])
+        assert np.array_equal(tb, pay[i, 0, :p.TBS[0] // 8]), s_
+    rx.close()
+    fep.close()
+    pipe.close()

@@ -74,19 +74,16 @@ def test_tm3_loop_decodes_codeword0(N_RB, mcs, npdcch, sf, nb_rx):
     assert np.array_equal(tb, pays[0][0][:p.TBS[0] // 8])
 
 
-def test_tm3_rejects_qpsk_and_reports_garbage_free_lengths():
+def test_tm3_qpsk_codeword0_and_garbage_free_lengths():
     fp = O.frame(50, nb_antennas_tx=2, mode1_flag=0)
     N = fp.ofdm_symbol_size
     rng = np.random.default_rng(1)
     rx = [rng.integers(-3000, 3000, 14 * N).astype(np.int32) for _ in range(2)]
     est = {(pp, a): rng.integers(-3000, 3000, 14 * N).astype(np.int32) for pp in (0, 1) for a in (0, 1)}
-    import ctypes
-    out = np.zeros(14 * 1200 * 6, np.int16)
-    rp = (ctypes.c_void_p * 2)(*[r.ctypes.data for r in rx])
-    ep = (ctypes.c_void_p * 4)(*[est[(pp, a)].ctypes.data for pp in (0, 1) for a in (0, 1)])
-    ra = (ctypes.c_uint32 * 4)(*alloc(50))
-    # Qm0 = 2 needs the interference-aware qpsk_qpsk / qpsk_qam LLRs: not restated
-    assert O.orc().orc_rx_pdsch_tm3(ctypes.byref(fp), 2, rp, ep, ra, 2, 2, 5, 1, 7, O.P(out), None) == -1
+    # Qm0 = 2: codeword 0 of the interference-aware path (qpsk_qpsk with Qm1 = 2)
+    l0, sh0 = O.rx_pdsch_tm3(fp, rx, est, alloc(50), 2, 2, 5, 1, 7)
+    q0, _, shq = O.rx_pdsch_tm3_qq(fp, rx, est, alloc(50), 5, 1, 7)
+    assert np.array_equal(l0, q0) and sh0 == shq
     # subframes 0 / 5 drop the PBCH / sync RBs (unlike the single-antenna extraction) and shorten by
     # adjust_G2 (16-QAM: pilot symbols by 2/3 of it)
     for sf in (0, 5, 7):
@@ -118,3 +115,29 @@ def test_tm3_qpsk_loop_decodes_both_codewords(N_RB, mcs, npdcch, sf, nb_rx):
         res, tb = decode_tb(u[:G], G, p.TBS[cw], 2)
         assert all(it <= 4 for it, _ in res), (cw, [it for it, _ in res])
         assert np.array_equal(tb, pays[0][cw][:p.TBS[cw] // 8]), cw
+
+
+# Codeword 0 QPSK, codeword 1 16 / 64-QAM: rx_pdsch runs dlsch_qpsk_16qam_llr / dlsch_qpsk_64qam_llr
+# for codeword 0 only (dlsch_demodulation.c:670-690), stream 1 and dl_ch_mag1 from receive antenna 0.
+QX = [(50, 9, 16, 1, 7), (50, 9, 22, 1, 7), (25, 5, 12, 2, 3), (100, 7, 19, 1, 8)]
+
+
+@pytest.mark.parametrize("N_RB,mcs0,mcs1,npdcch,sf", QX)
+def test_tm3_qpsk_with_qam_interferer_decodes_codeword0(N_RB, mcs0, mcs1, npdcch, sf):
+    import openair4g_amd as oai
+    p = oai.make_params("C3", subframe=sf, N_RB_DL=N_RB, nb_rb=N_RB, rb_alloc=alloc(N_RB), mcs=[mcs0, mcs1], TBS=None,
+                        num_pdcch_symbols=npdcch, with_crs=1, Nid_cell=0)
+    rng = np.random.default_rng(N_RB + mcs0 + mcs1)
+    pays = [[rng.integers(0, 256, p.payload_stride, dtype=np.uint8) for _ in range(2)] for _ in range(2)]
+    Qm1 = 4 if mcs1 < 17 else 6
+    for H in ([[1, 0], [0, 1]], [[2, 1], [1, 2]]):
+        fp, rxF, est = tm3_loop(p, sf, pays, H, 2)
+        llr, sh = O.rx_pdsch_tm3(fp, rxF, est, alloc(N_RB), 2, Qm1, mcs0, npdcch, sf)
+        G = O.get_G(N_RB, 0, 0, 0, N_RB, alloc(N_RB), 2, 1, npdcch, sf)
+        assert len(llr) == G
+        u = np.zeros(32 * (1 + G // 32), np.int16)
+        u[:G] = llr
+        O.dlsch_unscrambling(u, G, (p.rnti << 14) + (sf << 9) + fp.Nid_cell)
+        res, tb = decode_tb(u[:G], G, p.TBS[0], 2)
+        assert all(it <= 4 for it, _ in res), (H, [it for it, _ in res])
+        assert np.array_equal(tb, pays[0][0][:p.TBS[0] // 8]), H
