@@ -624,6 +624,11 @@ static __device__ __forceinline__ uint32_t ld_u32_any(const uint8_t *p)
 #define OAI4G_DIAG_MODOFDM 0   /* timing diagnostics only: 1 = no IQ stores, 2 = no e-bit staging, 3 = no QAM lookups,
                                   4 = QAM table reads without bank conflicts */
 #endif
+#ifndef OAI4G_MOD_ENDSYNC
+/* the barrier at the end of an item is not needed: the next item's LDS writes (staging, then the
+ * leaves) are separated from this item's last reads (prologue, pass C) by the staging barrier */
+#define OAI4G_MOD_ENDSYNC 0
+#endif
 #ifndef OAI4G_MODOFDM_WAVES
 #define OAI4G_MODOFDM_WAVES 3   /* measured: 3 waves/SIMD (<=168 VGPRs) beats 2 (no cap) and 4 (spills) */
 #endif
@@ -641,6 +646,7 @@ __global__ void __launch_bounds__(128) MODOFDM_ATTR k_modofdm(const cfg_dev_t *_
 {
   using G = modofdm_geom<LOG2N>;
   constexpr int N = G::N, T = G::T, UNITS = G::UNITS, LDSW = G::LDSW, EW = G::EW;
+  (void)EW;
   constexpr int NA = MODE == 0 ? 1 : 2;
   constexpr bool CW2 = MODE == 2 || MODE == 3;
   constexpr uint32_t IPS = MODE == 3 ? 2u : 1u;   /* items per (subframe, symbol) */
@@ -995,7 +1001,9 @@ __global__ void __launch_bounds__(128) MODOFDM_ATTR k_modofdm(const cfg_dev_t *_
           }
         },
         1);
+#if OAI4G_MOD_ENDSYNC
     __syncthreads();
+#endif
   }
 }
 
