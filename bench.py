@@ -525,12 +525,21 @@ def bench_ue(args, world, rank, dist, torch):
                             p.num_pdcch_symbols, p.rnti, n_sf, nb_rx=2, first_subframe=0)
         cb = None
 
-        def step(stream):
-            fb.run(stream=stream)
-            rb.estimate(fb.d_rxF, stream=stream)
-            rb.launch(fb.d_rxF, 1, stream=stream)
-        stages = {"k_fep": lambda: fb.run(stream=sid), "k_chest x4": lambda: rb.estimate(fb.d_rxF, stream=sid),
-                  "k_rx_level_tm3+k_rx_llr_tm3": lambda: rb.launch(fb.d_rxF, 1, stream=sid)}
+        if args.ue_unfused:   # the four 14-row estimate planes through memory
+            def step(stream):
+                fb.run(stream=stream)
+                rb.estimate(fb.d_rxF, stream=stream)
+                rb.launch(fb.d_rxF, 1, stream=stream)
+            stages = {"k_fep": lambda: fb.run(stream=sid), "k_chest x4": lambda: rb.estimate(fb.d_rxF, stream=sid),
+                      "k_rx_level_tm3+k_rx_llr_tm3": lambda: rb.launch(fb.d_rxF, 1, stream=sid)}
+        else:                 # the 5 pilot rows only; the demodulator interpolates the other rows
+            def step(stream):
+                fb.run(stream=stream)
+                rb.estimate_pilots(fb.d_rxF, stream=stream)
+                rb.launch_pilots(fb.d_rxF, 1, stream=stream)
+            stages = {"k_fep": lambda: fb.run(stream=sid),
+                      "k_chest pilots x4": lambda: rb.estimate_pilots(fb.d_rxF, stream=sid),
+                      "k_rx_level_tm3+k_rx_llr_tm3 (pilot rows)": lambda: rb.launch_pilots(fb.d_rxF, 1, stream=sid)}
     else:
         cb = oai.ChestBatch(fp, n_sf, first_subframe=0)
         rb = oai.RxBatch(fp, list(p.rb_alloc), Qm, p.num_pdcch_symbols, p.rnti, n_sf, first_subframe=0,
@@ -586,7 +595,10 @@ def bench_ue(args, world, rank, dist, torch):
            "k_rx_level+k_rx_llr": n_re * 8 + n_llr * 2 + n_sf * 1200 * 4,  # y + h per RE, LLRs, level row
            "k_rx_chest": n_re * 4 + n_llr * 2 + n_sf * 5 * 1200 * 4,       # y per RE, LLRs, 5 pilot rows
            # 2 y + 4 h per RE, LLRs, the level symbol's 4 estimate rows
-           "k_rx_level_tm3+k_rx_llr_tm3": n_re * 24 + n_llr * 2 + n_sf * 4 * 1200 * 4}
+           "k_rx_level_tm3+k_rx_llr_tm3": n_re * 24 + n_llr * 2 + n_sf * 4 * 1200 * 4,
+           # 4 pilot-row pairs (1216 columns) written, 5 pilot rows of the grid read
+           "k_chest pilots x4": 4 * n_sf * (8 * 1216 * 4 + 5 * N * 4),
+           "k_rx_level_tm3+k_rx_llr_tm3 (pilot rows)": n_re * 8 + n_llr * 2 + n_sf * 4 * 8 * 1216 * 4}
     alg = {k: v for k, v in alg.items() if k in stages}
     fb.close()
     if cb is not None:
@@ -601,7 +613,9 @@ def bench_ue(args, world, rank, dist, torch):
     if tm3:
         metric = "UE PDSCH RX subframes/sec (20 MHz TM3 2x2 64-QAM, estimated channel)"
         wl = ("slot_fep x2 + lte_dl_channel_estimation (2 ports x 2 RX) + rx_pdsch TM3 (dual extraction, "
-              "level_TM3, prec2A/compensation_TM3, MRC, codeword-0 LLRs) + dlsch_unscrambling, C3 20 MHz")
+              "level_TM3, prec2A/compensation_TM3, MRC, codeword-0 LLRs) + dlsch_unscrambling, C3 20 MHz"
+              + (" (14-row estimate planes through memory)" if args.ue_unfused else
+                 " (pilot rows only; the demodulator interpolates the estimate rows)"))
     else:
         metric = "UE PDSCH RX subframes/sec (20 MHz TM1 16-QAM, 1 RX, estimated channel)"
         wl = ("slot_fep + lte_dl_channel_estimation + rx_pdsch + dlsch_unscrambling, C2 20 MHz"

@@ -296,6 +296,15 @@ int oai4g_rx_pdsch_tm3_2cw(const oai4g_frame_parms_t *frame_parms, int nb_rx, co
 /* batch of the same (configuration from oai4g_rx_config_create_tm3 with Qm0 = Qm1 = 2) */
 int oai4g_rx_batch_tm3_2cw(oai4g_rx_config_t *cfg, int n_sf, const int32_t *d_rxdataF, const int32_t *d_est,
                            int16_t *d_llr0, int16_t *d_llr1, int unscramble, void *stream);
+/* The same two TM3 batches from the pilot rows only: d_pil = four planes [p * 2 + a][n_sf][4][N][2]
+ * written by oai4g_chest_batch_pilots (plane p * 2 + a from a port-p configuration over receive
+ * antenna a). Every other estimate row is formed in the demodulator with
+ * lte_dl_channel_estimation's temporal interpolation (lte_dl_channel_estimation.c:639-698), so the
+ * 14-row estimate planes never reach memory. The LLRs are bit-identical. */
+int oai4g_rx_batch_tm3_pilots(oai4g_rx_config_t *cfg, int n_sf, const int32_t *d_rxdataF, const int32_t *d_pil,
+                              int16_t *d_llr, int unscramble, void *stream);
+int oai4g_rx_batch_tm3_2cw_pilots(oai4g_rx_config_t *cfg, int n_sf, const int32_t *d_rxdataF, const int32_t *d_pil,
+                                  int16_t *d_llr0, int16_t *d_llr1, int unscramble, void *stream);
 
 /* TM2 (ALAMOUTI, two TX ports, mode1_flag 0) with dlsim's UE (rx_pdsch, dlsch_demodulation.c:82-800):
  * dlsch_extract_rbs_dual, dlsch_channel_level over both ports (log2_maxh = log2_approx(max avg) / 2),
@@ -343,6 +352,12 @@ void oai4g_chest_config_destroy(oai4g_chest_config_t *cfg);
  * batch: n / n (pass d_rxdataF + a nsymb N). */
 int oai4g_chest_config_set_stride(oai4g_chest_config_t *cfg, uint32_t subframes_per_element, uint32_t next_subframes);
 int oai4g_chest_batch(oai4g_chest_config_t *cfg, int n_sf, const int32_t *d_rxdataF, int32_t *d_est, void *stream);
+/* The pilot rows only: per subframe the 5 frequency-interpolated rows P0..P4 of symbols 0, p1, p2,
+ * p3 and the next subframe's symbol 0, stored as the pairs of consecutive rows: d_pil =
+ * [n_sf][4][N][2] words, pair k at column j = (P_k[j], P_k+1[j]); columns below 12 N_RB + 16 (the
+ * others are not written). They feed oai4g_rx_batch_tm3_pilots. */
+int oai4g_chest_batch_pilots(oai4g_chest_config_t *cfg, int n_sf, const int32_t *d_rxdataF, int32_t *d_pil,
+                             void *stream);
 /* The batch chain without the estimate buffer: oai4g_chest_batch followed by oai4g_rx_batch, fused
  * (the estimate of each PDSCH RE is formed in LDS from the pilot rows), same LLRs; d_rxdataF as
  * for oai4g_chest_batch (n_sf subframes + the next symbol 0).  rx and ce describe the same frame

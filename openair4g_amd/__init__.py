@@ -255,6 +255,12 @@ _SIGS = {
                                                 ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p]),
     "oai4g_chest_batch": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p,
                                          ctypes.c_void_p]),
+    "oai4g_chest_batch_pilots": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p,
+                                                ctypes.c_void_p]),
+    "oai4g_rx_batch_tm3_pilots": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p,
+                                                 ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p]),
+    "oai4g_rx_batch_tm3_2cw_pilots": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p,
+                                                     ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p]),
     "oai4g_phy_threegpplte_turbo_decoder8": (ctypes.c_uint8, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint16,
                                                               ctypes.c_uint16, ctypes.c_uint16, ctypes.c_uint8,
                                                               ctypes.c_uint8, ctypes.c_uint8]),
@@ -643,6 +649,35 @@ class RxBatchTM3:
     def launch(self, d_rxF, unscramble=1, stream=None):
         _check(self.L.oai4g_rx_batch_tm3(self.cfg, self.n_sf, d_rxF, self.d_est, self.d_llr, unscramble, stream) == 0)
 
+    def _pil(self):
+        if not getattr(self, "d_pil", None):
+            self.pil_plane = self.n_sf * 4 * self.fp.ofdm_symbol_size * 2
+            self.d_pil = self.L.oai4g_dev_alloc(4 * self.pil_plane * 4)
+            _check(bool(self.d_pil))
+        return self.d_pil
+
+    def estimate_pilots(self, d_rxF, first_subframe=0, subframe_step=1, stream=None):
+        """The four pilot-row estimations (oai4g_chest_batch_pilots): 5 rows per subframe instead of 14."""
+        N, nsymb = self.fp.ofdm_symbol_size, self.fp.symbols_per_tti
+        d_pil = self._pil()
+        for p, cfg in enumerate(self._chest_cfgs(first_subframe, subframe_step)):
+            for a in range(self.nb_rx):
+                _check(self.L.oai4g_chest_batch_pilots(cfg, self.n_sf, ctypes.c_void_p(d_rxF + a * nsymb * N * 4),
+                                                       ctypes.c_void_p(d_pil + (2 * p + a) * self.pil_plane * 4),
+                                                       stream) == 0)
+
+    def launch_pilots(self, d_rxF, unscramble=1, stream=None):
+        """oai4g_rx_batch_tm3_pilots: the demodulation from the pilot rows (estimate_pilots)"""
+        _check(self.L.oai4g_rx_batch_tm3_pilots(self.cfg, self.n_sf, d_rxF, self._pil(), self.d_llr, unscramble,
+                                                stream) == 0)
+
+    def launch_2cw_pilots(self, d_rxF, unscramble=1, stream=None):
+        if not getattr(self, "d_llr1", None):
+            self.d_llr1 = self.L.oai4g_dev_alloc(self.n_sf * self.stride * 2)
+            _check(bool(self.d_llr1))
+        _check(self.L.oai4g_rx_batch_tm3_2cw_pilots(self.cfg, self.n_sf, d_rxF, self._pil(), self.d_llr, self.d_llr1,
+                                                    unscramble, stream) == 0)
+
     def launch_2cw(self, d_rxF, unscramble=1, stream=None):
         """both codewords QPSK: codeword 0 into d_llr, codeword 1 into d_llr1 (llrs1())"""
         if not getattr(self, "d_llr1", None):
@@ -680,6 +715,9 @@ class RxBatchTM3:
         if getattr(self, "d_llr1", None):
             self.L.oai4g_dev_free(self.d_llr1)
             self.d_llr1 = None
+        if getattr(self, "d_pil", None):
+            self.L.oai4g_dev_free(self.d_pil)
+            self.d_pil = None
         self.L.oai4g_rx_config_destroy(self.cfg)
 
 class RxBatchTM2(RxBatchTM3):

@@ -126,7 +126,13 @@ __device__ __forceinline__ void ce_window(uint32_t N_RB, uint32_t j0, uint32_t j
 }  // namespace
 
 /* batch: grid (ceil(N / 256), n_sf); rxF = n_sf subframes of nsymb x N words followed by the
- * symbol 0 of the subframe after the batch; est = n_sf x nsymb x N */
+ * symbol 0 of the subframe after the batch; est = n_sf x nsymb x N.  PIL: only the 5 frequency-
+ * interpolated pilot rows (symbols 0, p1, p2, p3 and the next subframe's 0), stored as the 4 pairs
+ * of consecutive pilot rows, est = n_sf x 4 x N x 2 words (pair k at column j = (P_k, P_k+1)): every
+ * estimate row is one 8-byte load of a pair, coalesced across the columns.  Only the columns a
+ * pilot reaches are written (the grid stops at 12 N_RB + 16); the demodulator forms the rows itself
+ * (rx_est, the same temporal interpolation) */
+template <bool PIL>
 __global__ void __launch_bounds__(CE_WG) k_chest(const chest_dev_t *__restrict__ c, const int32_t *__restrict__ rxF,
                                                  int32_t *__restrict__ est)
 {
@@ -153,6 +159,13 @@ __global__ void __launch_bounds__(CE_WG) k_chest(const chest_dev_t *__restrict__
   uint32_t P[5] = {0, 0, 0, 0, 0};
   if (c->branch)
     for (uint32_t in = 0; in < 5; in++) P[in] = ce_column(N_RB, flt[in & 1u], chl[in], m_base, j);
+  if constexpr (PIL) {
+    typedef uint32_t u32x2_t __attribute__((ext_vector_type(2)));
+    u32x2_t *E2 = (u32x2_t *)est + (size_t)sf * 4 * N + j;
+#pragma unroll
+    for (uint32_t k = 0; k < 4; k++) E2[k * N] = (u32x2_t){P[k], P[k + 1]};
+    return;
+  }
   int32_t *E = est + (size_t)sf * nsymb * N + j;
   E[0] = (int32_t)P[0];
   E[p1 * N] = (int32_t)P[1];
@@ -342,7 +355,16 @@ hipError_t oai4g_launch_chest(const chest_dev_t *d_cfg, const chest_dev_t *h_cfg
                               int32_t *d_est, hipStream_t s)
 {
   if (n_sf <= 0) return hipSuccess;
-  hipLaunchKernelGGL(k_chest, dim3((h_cfg->N + CE_WG - 1) / CE_WG, n_sf), dim3(CE_WG), 0, s, d_cfg, d_rxF, d_est);
+  hipLaunchKernelGGL(k_chest<false>, dim3((h_cfg->N + CE_WG - 1) / CE_WG, n_sf), dim3(CE_WG), 0, s, d_cfg, d_rxF, d_est);
+  return hipGetLastError();
+}
+
+hipError_t oai4g_launch_chest_pilots(const chest_dev_t *d_cfg, const chest_dev_t *h_cfg, int n_sf, const int32_t *d_rxF,
+                                     int32_t *d_pil, hipStream_t s)
+{
+  if (n_sf <= 0) return hipSuccess;
+  const uint32_t span = min(h_cfg->N, 12 * h_cfg->N_RB + 16);   /* columns a pilot window reaches */
+  hipLaunchKernelGGL(k_chest<true>, dim3((span + CE_WG - 1) / CE_WG, n_sf), dim3(CE_WG), 0, s, d_cfg, d_rxF, d_pil);
   return hipGetLastError();
 }
 

@@ -3472,6 +3472,24 @@ static oai4g_rx_config_t *rx_config_build(const oai4g_frame_parms_t *fp, const u
   h.nb_rx = dual ? nb_rx : 1u;
   h.mu_off = tm3 ? k_mumimo_off[mcs0][(Qm1 >> 1) - 1] : 0;
   h.qm1 = tm3 ? Qm1 : 0u;
+  /* estimate rows from the 5 pilot rows (P0 .. P3 = symbols 0, p1, p2, p3; P4 = the next subframe's
+   * symbol 0): lte_dl_channel_estimation.c:639-698 as k_chest's ce_interp applies it */
+  {
+    const uint32_t p1 = fp->Ncp ? 3 : 4, p2 = fp->Ncp ? 6 : 7, p3 = fp->Ncp ? 9 : 11;
+    auto row = [&](uint32_t l, uint8_t a, int16_t wa, uint8_t b, int16_t wb) {
+      h.ea[l] = a; h.ewa[l] = wa; h.eb[l] = b; h.ewb[l] = wb;
+    };
+    row(0, 0, 0, 0, 0); row(p1, 1, 0, 0, 0); row(p2, 2, 0, 0, 0); row(p3, 3, 0, 0, 0);
+    row(p3 + 1, 3, 21845, 4, 10923); row(p3 + 2, 3, 10923, 4, 21845);
+    row(p1 + 1, 1, 21845, 2, 10923); row(p1 + 2, 1, 10923, 2, 21845);
+    if (fp->Ncp == 0) {
+      row(1, 0, 24576, 1, 8192); row(2, 0, 16384, 1, 16384); row(3, 0, 8192, 1, 24576);
+      row(p2 + 1, 2, 24576, 3, 8192); row(p2 + 2, 2, 16384, 3, 16384); row(p2 + 3, 2, 8192, 3, 24576);
+    } else {                                                 /* the reference's 1/3, 2/3 order, as written */
+      row(1, 0, 10923, 1, 21845); row(2, 0, 21845, 1, 10923);
+      row(p2 + 1, 2, 10923, 3, 21845); row(p2 + 2, 2, 21845, 3, 10923);
+    }
+  }
   std::vector<uint32_t> map;
   uint32_t max_llr = 0;
   for (uint32_t sf = 0; sf < 10; sf++) {
@@ -3645,6 +3663,47 @@ extern "C" int oai4g_rx_batch_tm3(oai4g_rx_config_t *cfg, int n_sf, const int32_
     HCK(oai4g_launch_rx_tm3(cfg->d, &cfg->h, n_sf, d_rxdataF, d_est, plane, d_llr, cfg->d_shift, unscramble,
                             (hipStream_t)stream), -1);
   return 0;
+}
+
+/* The TM3 batch from the pilot rows only: oai4g_chest_batch_pilots wrote [p * 2 + a][n_sf][5][N]
+ * (the 5 frequency-interpolated pilot rows per subframe); the demodulator forms every other row
+ * with the estimator's temporal interpolation, so the 14-row estimate planes never reach HBM.
+ * LLRs bit-identical to oai4g_chest_batch x 4 + oai4g_rx_batch_tm3 / _tm3_2cw. */
+static int rx_batch_tm3_pil(oai4g_rx_config_t *cfg, int n_sf, const int32_t *d_rxdataF, const int32_t *d_pil,
+                            int16_t *d_llr0, int16_t *d_llr1, int unscramble, void *stream, bool two_cw)
+{
+  NEED_INIT(-1);
+  if (!cfg || !cfg->h.tm3) { set_err("rx_batch_tm3_pilots: not a TM3 configuration"); return -1; }
+  if (two_cw && (cfg->h.Qm != 2 || cfg->h.qm1 != 2)) {
+    set_err("rx_batch_tm3_2cw_pilots: not a TM3 configuration with both codewords QPSK");
+    return -1;
+  }
+  if (n_sf <= 0) return 0;
+  if (rx_check_batch(cfg, n_sf) != 0) return -1;
+  if (n_sf > cfg->shift_cap) {
+    if (cfg->d_shift) hipFree(cfg->d_shift);
+    HCK(hipMalloc(&cfg->d_shift, (size_t)n_sf), -1);
+    cfg->shift_cap = n_sf;
+  }
+  const size_t plane = (size_t)n_sf * 4 * cfg->h.N * 2;        /* words: 4 pilot-row pairs per subframe */
+  if (cfg->h.Qm == 2)
+    HCK(oai4g_launch_rx_tm3qq(cfg->d, &cfg->h, n_sf, d_rxdataF, d_pil, plane, d_llr0, two_cw ? d_llr1 : nullptr,
+                              cfg->d_shift, unscramble, (hipStream_t)stream, 1), -1);
+  else
+    HCK(oai4g_launch_rx_tm3(cfg->d, &cfg->h, n_sf, d_rxdataF, d_pil, plane, d_llr0, cfg->d_shift, unscramble,
+                            (hipStream_t)stream, 1), -1);
+  return 0;
+}
+extern "C" int oai4g_rx_batch_tm3_pilots(oai4g_rx_config_t *cfg, int n_sf, const int32_t *d_rxdataF, const int32_t *d_pil,
+                                         int16_t *d_llr, int unscramble, void *stream)
+{
+  return rx_batch_tm3_pil(cfg, n_sf, d_rxdataF, d_pil, d_llr, nullptr, unscramble, stream, false);
+}
+extern "C" int oai4g_rx_batch_tm3_2cw_pilots(oai4g_rx_config_t *cfg, int n_sf, const int32_t *d_rxdataF,
+                                             const int32_t *d_pil, int16_t *d_llr0, int16_t *d_llr1, int unscramble,
+                                             void *stream)
+{
+  return rx_batch_tm3_pil(cfg, n_sf, d_rxdataF, d_pil, d_llr0, d_llr1, unscramble, stream, true);
 }
 
 extern "C" int oai4g_rx_batch_tm3_2cw(oai4g_rx_config_t *cfg, int n_sf, const int32_t *d_rxdataF, const int32_t *d_est,
@@ -4022,6 +4081,15 @@ extern "C" int oai4g_chest_batch(oai4g_chest_config_t *cfg, int n_sf, const int3
   NEED_INIT(-1);
   if (!cfg || n_sf < 0) { set_err("chest_batch: bad arguments"); return -1; }
   HCK(oai4g_launch_chest(cfg->d, &cfg->h, n_sf, d_rxdataF, d_est, (hipStream_t)stream), -1);
+  return 0;
+}
+
+extern "C" int oai4g_chest_batch_pilots(oai4g_chest_config_t *cfg, int n_sf, const int32_t *d_rxdataF, int32_t *d_pil,
+                                        void *stream)
+{
+  NEED_INIT(-1);
+  if (!cfg || n_sf < 0) { set_err("chest_batch_pilots: bad arguments"); return -1; }
+  HCK(oai4g_launch_chest_pilots(cfg->d, &cfg->h, n_sf, d_rxdataF, d_pil, (hipStream_t)stream), -1);
   return 0;
 }
 

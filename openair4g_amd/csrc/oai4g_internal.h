@@ -359,6 +359,9 @@ hipError_t oai4g_launch_awgn(const int32_t *d_tx, size_t tx_stride, uint32_t tx_
 hipError_t oai4g_launch_unscramble(int16_t *d_llr, const uint32_t *d_c, int n, hipStream_t s);
 hipError_t oai4g_launch_chest(const chest_dev_t *d_cfg, const chest_dev_t *h_cfg, int n_sf, const int32_t *d_rxF,
                               int32_t *d_est, hipStream_t s);
+/* the 5 pilot rows per subframe only ([n_sf][5][N], columns < 12 N_RB + 16) */
+hipError_t oai4g_launch_chest_pilots(const chest_dev_t *d_cfg, const chest_dev_t *h_cfg, int n_sf, const int32_t *d_rxF,
+                                     int32_t *d_pil, hipStream_t s);
 hipError_t oai4g_launch_chest_symbol(const chest_dev_t *d_cfg, const chest_dev_t *h_cfg, const int32_t *d_rxF_sym,
                                      int32_t *d_est, int Ns, int l, int symbol, hipStream_t s);
 
@@ -382,16 +385,20 @@ struct rx_dev_t {
   /* TM2 (ALAMOUTI, dual extraction): dlsch_channel_level over both ports, dlsch_alamouti */
   uint32_t tm2;
   uint32_t qm1;                   /* TM3: codeword 1's modulation order (Qm = 2 picks qpsk_qpsk / _qam16 / _qam64) */
+  /* estimate row l from the 5 pilot rows (lte_dl_channel_estimation.c:639-698): pilot row ea[l]
+   * when ewa[l] == 0, else mulhi(P[ea], ewa) << 1 +sat mulhi(P[eb], ewb) << 1 */
+  uint8_t ea[14], eb[14];
+  int16_t ewa[14], ewb[14];
 };
 hipError_t oai4g_launch_rx_chest(const chest_dev_t *d_ce, const rx_dev_t *d_rx, const rx_dev_t *h_rx, int n_sf,
                                  const int32_t *d_rxF, int16_t *d_llr, uint8_t *d_shift, int unscramble, hipStream_t s);
 hipError_t oai4g_launch_rx_tm3(const rx_dev_t *d_cfg, const rx_dev_t *h_cfg, int n_sf, const int32_t *d_rxF,
                                const int32_t *d_est, size_t plane, int16_t *d_llr, uint8_t *d_shift, int unscramble,
-                               hipStream_t s);
+                               hipStream_t s, int pil = 0);
 /* TM3 with codeword 0 QPSK: Qm1 = 2 both codewords (d_llr1 may be null), Qm1 = 4 / 6 codeword 0 */
 hipError_t oai4g_launch_rx_tm3qq(const rx_dev_t *d_cfg, const rx_dev_t *h_cfg, int n_sf, const int32_t *d_rxF,
                                  const int32_t *d_est, size_t plane, int16_t *d_llr0, int16_t *d_llr1,
-                                 uint8_t *d_shift, int unscramble, hipStream_t s);
+                                 uint8_t *d_shift, int unscramble, hipStream_t s, int pil = 0);
 hipError_t oai4g_launch_rx_tm2(const rx_dev_t *d_cfg, const rx_dev_t *h_cfg, int n_sf, const int32_t *d_rxF,
                                const int32_t *d_est, size_t plane, int16_t *d_llr, uint8_t *d_shift, int unscramble,
                                hipStream_t s);

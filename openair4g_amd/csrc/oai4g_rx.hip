@@ -16,6 +16,29 @@
  */
 #include "oai4g_rx_prims.h"
 
+/* estimate entry of plane pa (= p * 2 + a), subframe sf, symbol l, estimate column col: from the
+ * estimate planes [pa][n_sf][nsymb][N] (plane words each), or (PIL) from the pilot-row pairs
+ * [pa][n_sf][4][N] x (P_k, P_k+1) with lte_dl_channel_estimation's temporal interpolation
+ * (:639-698: mulhi(P_a, w_a) << 1 +sat mulhi(P_a+1, w_b) << 1, per component; one 8-byte load) */
+template <bool PIL>
+static __device__ __forceinline__ uint32_t rx_est(const rx_dev_t *__restrict__ c, const int32_t *__restrict__ est,
+                                                  size_t plane, uint32_t pa, uint32_t sf, uint32_t l, uint32_t col)
+{
+  if constexpr (!PIL) {
+    return (uint32_t)est[pa * plane + ((size_t)sf * c->nsymb + l) * c->N + col];
+  } else {
+    typedef uint32_t u32x2p_t __attribute__((ext_vector_type(2)));
+    const u32x2p_t v = *((const u32x2p_t *)(est + pa * plane) + ((size_t)sf * 4 + c->ea[l]) * c->N + col);
+    const int16_t wa = c->ewa[l];
+    const uint32_t x = v.x, y = v.y;                              /* P_a, P_a+1 (eb = ea + 1) */
+    if (wa == 0) return x;
+    const int16_t wb = c->ewb[l];
+    const int16_t r = rx_sat16((int32_t)rx_shl(rx_mh((int16_t)x, wa), 1) + rx_shl(rx_mh((int16_t)y, wb), 1));
+    const int16_t i = rx_sat16((int32_t)rx_shl(rx_mh((int16_t)(x >> 16), wa), 1) + rx_shl(rx_mh((int16_t)(y >> 16), wb), 1));
+    return (uint32_t)(uint16_t)r | ((uint32_t)(uint16_t)i << 16);
+  }
+}
+
 /* dlsch_channel_level over the first PDSCH symbol -> log2_maxh = log2_approx(avg) / 2, per subframe */
 __global__ void __launch_bounds__(256) k_rx_level(const rx_dev_t *__restrict__ c, const int32_t *__restrict__ ch,
                                                   uint8_t *__restrict__ shift)
@@ -84,9 +107,11 @@ __global__ void __launch_bounds__(256) k_rx_llr(const rx_dev_t *__restrict__ c, 
  *   dlsch_channel_compensation_TM3 :1846-2120 with prec2A_TM3_128 (s alternates per slot)
  *   dlsch_detection_mrc         :2583-2718 (stream 0: (a >> 1) +sat (b >> 1))
  *   dlsch_16qam / 64qam_llr     of stream 0, unscrambled
- * d_est holds the estimate planes [p * 2 + a][n_sf][nsymb][N] (plane = n_sf nsymb N words), d_rxF
- * the FEP output [n_sf][nb_rx][nsymb][N].
+ * d_est holds the estimate planes [p * 2 + a][n_sf][nsymb][N] (plane = n_sf nsymb N words), or with
+ * PIL the pilot rows [p * 2 + a][n_sf][5][N] (plane = n_sf 5 N words); d_rxF the FEP output
+ * [n_sf][nb_rx][nsymb][N].
  * ==================================================================================== */
+template <bool PIL>
 __global__ void __launch_bounds__(256) k_rx_level_tm3(const rx_dev_t *__restrict__ c, const int32_t *__restrict__ est,
                                                       size_t plane, uint8_t *__restrict__ shift)
 {
@@ -95,12 +120,11 @@ __global__ void __launch_bounds__(256) k_rx_level_tm3(const rx_dev_t *__restrict
   if (threadIdx.x < 8) lane[threadIdx.x >> 2][threadIdx.x & 3] = 0;
   __syncthreads();
   rg32_t *map = (rg32_t *)(c->map + c->map_off[sfi][0]);
-  const size_t so = ((size_t)sf * c->nsymb + l) * c->N;
   uint32_t part[2][4] = {{0, 0, 0, 0}, {0, 0, 0, 0}};
   for (uint32_t j = threadIdx.x; j < c->lvl_n[sfi]; j += blockDim.x) {
     const uint32_t col = map[j] >> 16;
     for (uint32_t a = 0; a < c->nb_rx; a++) {
-      const uint32_t h0 = (uint32_t)est[a * plane + so + col], h1 = (uint32_t)est[(2 + a) * plane + so + col];
+      const uint32_t h0 = rx_est<PIL>(c, est, plane, a, sf, l, col), h1 = rx_est<PIL>(c, est, plane, 2 + a, sf, l, col);
       const uint32_t v = rx_h2(rx_prec_tm3(h0, h1, (j & 1u) != 0));
 #pragma unroll
       for (int q = 0; q < 4; q++)
@@ -129,7 +153,7 @@ __global__ void __launch_bounds__(256) k_rx_level_tm3(const rx_dev_t *__restrict
   }
 }
 
-template <int QM>
+template <int QM, bool PIL>
 __global__ void __launch_bounds__(256) k_rx_llr_tm3(const rx_dev_t *__restrict__ c, const int32_t *__restrict__ rxF,
                                                     const int32_t *__restrict__ est, size_t plane,
                                                     int16_t *__restrict__ llr, const uint8_t *__restrict__ shift,
@@ -138,7 +162,6 @@ __global__ void __launch_bounds__(256) k_rx_llr_tm3(const rx_dev_t *__restrict__
   const uint32_t sf = blockIdx.y, k = blockIdx.x, sfi = (c->first_sf + sf * c->sf_step) % 10;
   const uint32_t l = c->npdcch + k, len = c->len[sfi][k], nb_rx = c->nb_rx, NS = c->nsymb * c->N;
   rg32_t *map = (rg32_t *)(c->map + c->map_off[sfi][k]);
-  const size_t eo = ((size_t)sf * c->nsymb + l) * c->N;
   int16_t *out = llr + (size_t)sf * c->llr_stride + c->llr_off[sfi][k];
   const uint32_t sh = shift[sf], base = c->llr_off[sfi][k];
   rg32_t *gold = (rg32_t *)(c->gold + (size_t)sfi * c->gold_words);
@@ -157,8 +180,8 @@ __global__ void __launch_bounds__(256) k_rx_llr_tm3(const rx_dev_t *__restrict__
       const uint32_t aa = a < nb_rx ? a : 0u;
       const size_t yo = ((size_t)sf * nb_rx + aa) * NS + (size_t)l * c->N;
       yv[a][r] = (uint32_t)rxF[yo + (mw[r] & 0xFFFFu)];
-      h0[a][r] = (uint32_t)est[aa * plane + eo + (mw[r] >> 16)];
-      h1[a][r] = (uint32_t)est[(2 + aa) * plane + eo + (mw[r] >> 16)];
+      h0[a][r] = rx_est<PIL>(c, est, plane, aa, sf, l, mw[r] >> 16);
+      h1[a][r] = rx_est<PIL>(c, est, plane, 2 + aa, sf, l, mw[r] >> 16);
     }
 #pragma unroll
   for (int r = 0; r < RX_R; r++) {
@@ -195,7 +218,7 @@ __global__ void __launch_bounds__(256) k_rx_llr_tm3(const rx_dev_t *__restrict__
  * llr1 is given, codeword 1 (comp1, comp0, rho2), both scrambled with q = 0 as dlsim transmits them;
  * QM1 = 4 / 6: dlsch_qpsk_16qam_llr / dlsch_qpsk_64qam_llr yield codeword 0 from (comp0, comp1,
  * dl_ch_mag1, rho) */
-template <int QM1>
+template <int QM1, bool PIL>
 __global__ void __launch_bounds__(256) k_rx_llr_tm3qq(const rx_dev_t *__restrict__ c, const int32_t *__restrict__ rxF,
                                                       const int32_t *__restrict__ est, size_t plane,
                                                       int16_t *__restrict__ llr0, int16_t *__restrict__ llr1,
@@ -204,7 +227,7 @@ __global__ void __launch_bounds__(256) k_rx_llr_tm3qq(const rx_dev_t *__restrict
   const uint32_t sf = blockIdx.y, k = blockIdx.x, sfi = (c->first_sf + sf * c->sf_step) % 10;
   const uint32_t l = c->npdcch + k, len = c->len[sfi][k], nb_rx = c->nb_rx, NS = c->nsymb * c->N;
   rg32_t *map = (rg32_t *)(c->map + c->map_off[sfi][k]);
-  const size_t eo = ((size_t)sf * c->nsymb + l) * c->N, oo = (size_t)sf * c->llr_stride + c->llr_off[sfi][k];
+  const size_t oo = (size_t)sf * c->llr_stride + c->llr_off[sfi][k];
   const uint32_t sh = shift[sf], base = c->llr_off[sfi][k];
   rg32_t *gold = (rg32_t *)(c->gold + (size_t)sfi * c->gold_words);
   for (uint32_t j = threadIdx.x; j < len; j += blockDim.x) {
@@ -215,7 +238,7 @@ __global__ void __launch_bounds__(256) k_rx_llr_tm3qq(const rx_dev_t *__restrict
     for (uint32_t a = 0; a < 2; a++) {
       const uint32_t aa = a < nb_rx ? a : 0u;
       const uint32_t yv = (uint32_t)rxF[((size_t)sf * nb_rx + aa) * NS + (size_t)l * c->N + (mw & 0xFFFFu)];
-      const uint32_t h0 = (uint32_t)est[aa * plane + eo + (mw >> 16)], h1 = (uint32_t)est[(2 + aa) * plane + eo + (mw >> 16)];
+      const uint32_t h0 = rx_est<PIL>(c, est, plane, aa, sf, l, mw >> 16), h1 = rx_est<PIL>(c, est, plane, 2 + aa, sf, l, mw >> 16);
       const uint32_t p0 = rx_prec_tm3(h0, h1, neg), p1 = rx_prec_tm3_s1(h0, h1, neg);
       rx_conj_mul(p0, yv, sh, c0r[a], c0i[a]);
       rx_conj_mul(p0, p1, sh, r0r[a], r0i[a]);
@@ -246,34 +269,52 @@ __global__ void __launch_bounds__(256) k_rx_llr_tm3qq(const rx_dev_t *__restrict
   }
 }
 
-hipError_t oai4g_launch_rx_tm3qq(const rx_dev_t *d_cfg, const rx_dev_t *h_cfg, int n_sf, const int32_t *d_rxF,
-                                 const int32_t *d_est, size_t plane, int16_t *d_llr0, int16_t *d_llr1,
-                                 uint8_t *d_shift, int unscramble, hipStream_t s)
+template <bool PIL>
+static hipError_t launch_rx_tm3qq(const rx_dev_t *d_cfg, const rx_dev_t *h_cfg, int n_sf, const int32_t *d_rxF,
+                                  const int32_t *d_est, size_t plane, int16_t *d_llr0, int16_t *d_llr1, uint8_t *d_shift,
+                                  int unscramble, hipStream_t s)
 {
-  if (n_sf <= 0) return hipSuccess;
-  hipLaunchKernelGGL(k_rx_level_tm3, dim3(n_sf), dim3(256), 0, s, d_cfg, d_est, plane, d_shift);
+  hipLaunchKernelGGL(k_rx_level_tm3<PIL>, dim3(n_sf), dim3(256), 0, s, d_cfg, d_est, plane, d_shift);
   const dim3 g(h_cfg->n_sym, n_sf), b(256);
   if (h_cfg->qm1 == 4)
-    hipLaunchKernelGGL(k_rx_llr_tm3qq<4>, g, b, 0, s, d_cfg, d_rxF, d_est, plane, d_llr0, nullptr, d_shift, unscramble);
+    hipLaunchKernelGGL((k_rx_llr_tm3qq<4, PIL>), g, b, 0, s, d_cfg, d_rxF, d_est, plane, d_llr0, nullptr, d_shift, unscramble);
   else if (h_cfg->qm1 == 6)
-    hipLaunchKernelGGL(k_rx_llr_tm3qq<6>, g, b, 0, s, d_cfg, d_rxF, d_est, plane, d_llr0, nullptr, d_shift, unscramble);
+    hipLaunchKernelGGL((k_rx_llr_tm3qq<6, PIL>), g, b, 0, s, d_cfg, d_rxF, d_est, plane, d_llr0, nullptr, d_shift, unscramble);
   else
-    hipLaunchKernelGGL(k_rx_llr_tm3qq<2>, g, b, 0, s, d_cfg, d_rxF, d_est, plane, d_llr0, d_llr1, d_shift, unscramble);
+    hipLaunchKernelGGL((k_rx_llr_tm3qq<2, PIL>), g, b, 0, s, d_cfg, d_rxF, d_est, plane, d_llr0, d_llr1, d_shift, unscramble);
+  return hipGetLastError();
+}
+
+hipError_t oai4g_launch_rx_tm3qq(const rx_dev_t *d_cfg, const rx_dev_t *h_cfg, int n_sf, const int32_t *d_rxF,
+                                 const int32_t *d_est, size_t plane, int16_t *d_llr0, int16_t *d_llr1,
+                                 uint8_t *d_shift, int unscramble, hipStream_t s, int pil)
+{
+  if (n_sf <= 0) return hipSuccess;
+  return pil ? launch_rx_tm3qq<true>(d_cfg, h_cfg, n_sf, d_rxF, d_est, plane, d_llr0, d_llr1, d_shift, unscramble, s)
+             : launch_rx_tm3qq<false>(d_cfg, h_cfg, n_sf, d_rxF, d_est, plane, d_llr0, d_llr1, d_shift, unscramble, s);
+}
+
+template <bool PIL>
+static hipError_t launch_rx_tm3(const rx_dev_t *d_cfg, const rx_dev_t *h_cfg, int n_sf, const int32_t *d_rxF,
+                                const int32_t *d_est, size_t plane, int16_t *d_llr, uint8_t *d_shift, int unscramble,
+                                hipStream_t s)
+{
+  hipLaunchKernelGGL(k_rx_level_tm3<PIL>, dim3(n_sf), dim3(256), 0, s, d_cfg, d_est, plane, d_shift);
+  const dim3 g(h_cfg->n_sym, n_sf), b(256);
+  if (h_cfg->Qm == 4)
+    hipLaunchKernelGGL((k_rx_llr_tm3<4, PIL>), g, b, 0, s, d_cfg, d_rxF, d_est, plane, d_llr, d_shift, unscramble);
+  else
+    hipLaunchKernelGGL((k_rx_llr_tm3<6, PIL>), g, b, 0, s, d_cfg, d_rxF, d_est, plane, d_llr, d_shift, unscramble);
   return hipGetLastError();
 }
 
 hipError_t oai4g_launch_rx_tm3(const rx_dev_t *d_cfg, const rx_dev_t *h_cfg, int n_sf, const int32_t *d_rxF,
                                const int32_t *d_est, size_t plane, int16_t *d_llr, uint8_t *d_shift, int unscramble,
-                               hipStream_t s)
+                               hipStream_t s, int pil)
 {
   if (n_sf <= 0) return hipSuccess;
-  hipLaunchKernelGGL(k_rx_level_tm3, dim3(n_sf), dim3(256), 0, s, d_cfg, d_est, plane, d_shift);
-  const dim3 g(h_cfg->n_sym, n_sf), b(256);
-  if (h_cfg->Qm == 4)
-    hipLaunchKernelGGL(k_rx_llr_tm3<4>, g, b, 0, s, d_cfg, d_rxF, d_est, plane, d_llr, d_shift, unscramble);
-  else
-    hipLaunchKernelGGL(k_rx_llr_tm3<6>, g, b, 0, s, d_cfg, d_rxF, d_est, plane, d_llr, d_shift, unscramble);
-  return hipGetLastError();
+  return pil ? launch_rx_tm3<true>(d_cfg, h_cfg, n_sf, d_rxF, d_est, plane, d_llr, d_shift, unscramble, s)
+             : launch_rx_tm3<false>(d_cfg, h_cfg, n_sf, d_rxF, d_est, plane, d_llr, d_shift, unscramble, s);
 }
 
 /* ======================================================================================

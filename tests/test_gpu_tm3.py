@@ -229,3 +229,36 @@ def test_gpu_tm3_qpsk_with_qam_interferer_receive_loop(gpu, N_RB, mcs0, mcs1, np
     rx.close()
     fep.close()
     pipe.close()
+
+
+@pytest.mark.parametrize("N_RB,Qm0,Qm1,mcs,npd,sf,nb_rx,ecp", [(100, 6, 6, 19, 1, 7, 2, 0), (50, 4, 2, 12, 2, 3, 1, 0),
+                                                               (25, 2, 6, 7, 1, 6, 2, 0), (100, 2, 2, 9, 3, 8, 2, 0),
+                                                               (50, 6, 4, 20, 1, 2, 2, 1), (15, 4, 4, 12, 2, 6, 2, 1)])
+def test_gpu_tm3_from_pilot_rows_equals_estimate_planes(gpu, N_RB, Qm0, Qm1, mcs, npd, sf, nb_rx, ecp):
+    """oai4g_chest_batch_pilots + oai4g_rx_batch_tm3_pilots (the demodulator forms the estimate rows
+    from the 5 pilot rows with the estimator's temporal interpolation) against the four 14-row
+    estimate planes + oai4g_rx_batch_tm3: bit-identical LLRs on random FEP outputs, both CP types,
+    every codeword-0 LLR family (both codewords too when both are QPSK)."""
+    import ctypes
+    fg = gpu.frame_parms(N_RB, Nid_cell=N_RB + sf, nb_antennas_tx=2, mode1_flag=0, Ncp=ecp)
+    n_sf, N, nsymb = 3, fg.ofdm_symbol_size, fg.symbols_per_tti
+    rng = np.random.default_rng(N_RB + mcs + 17 * ecp)
+    for scale in (3000, 2 ** 31 - 1):
+        rxF = rng.integers(-scale, scale, (n_sf + 1) * nb_rx * nsymb * N, dtype=np.int64).astype(np.int32)
+        L = gpu.lib()
+        d = L.oai4g_dev_alloc(rxF.nbytes)
+        assert d and L.oai4g_memcpy_h2d(d, rxF.ctypes.data, rxF.nbytes) == 0
+        rx = gpu.RxBatchTM3(fg, alloc(N_RB), Qm0, Qm1, mcs, npd, 0x1234, n_sf, nb_rx=nb_rx, first_subframe=sf)
+        two = Qm0 == 2 and Qm1 == 2
+        rx.estimate(d, first_subframe=sf)
+        rx.launch_2cw(d) if two else rx.launch(d)
+        a0 = rx.llrs()
+        a1 = rx.llrs1() if two else None
+        rx.estimate_pilots(d, first_subframe=sf)
+        rx.launch_2cw_pilots(d) if two else rx.launch_pilots(d)
+        b0 = rx.llrs()
+        assert np.array_equal(a0, b0), scale
+        if two:
+            assert np.array_equal(a1, rx.llrs1()), scale
+        rx.close()
+        L.oai4g_dev_free(ctypes.c_void_p(d))
