@@ -329,9 +329,40 @@ int oai4g_rx_batch_tm2(oai4g_rx_config_t *cfg, int n_sf, const int32_t *d_rxdata
  * 12 / 13 of the previous subframe's pilot 11).  rxdataF / dl_ch_estimates = [nsymb][N] host
  * buffers of the subframe; N_RB_DL 6 / 15 / 25 / 50 / 100 (other sizes: the reference's "not
  * implemented" row of zeros; 15 PRB with its second-half start 1 + nushift + 3 p, :582).  The idft of the estimate into
- * dl_ch_estimates_time (:704-738, the UE's timing tracker) is not produced.  Returns 0 / -1. */
+ * dl_ch_estimates_time (:704-738) is the separate entry oai4g_dl_ch_estimates_time below, which the
+ * shim calls after this one.  Returns 0 / -1. */
 int oai4g_lte_dl_channel_estimation(const oai4g_frame_parms_t *frame_parms, const int32_t *rxdataF,
                                     int32_t *dl_ch_estimates, uint8_t Ns, uint8_t p, uint8_t l, uint8_t symbol);
+/* The tail of lte_dl_channel_estimation (lte_dl_channel_estimation.c:704-738): for every RX antenna
+ * aarx < nb_antennas_rx and port p < nb_antennas_tx_eNB (nb_antennas_tx when 0) whose plane
+ * dl_ch_estimates[(p << 1) + aarx] is not NULL, dl_ch_estimates_time[(p << 1) + aarx] =
+ * idft_N(plane from word 8, scale 1): words 8 .. N + 7 (row 0 then the first 8 words of row 1),
+ * N = ofdm_symbol_size (log2_symbol_size outside 7..11: idft512, the switch's default).  The
+ * input of the UE timing tracker (lte_adjust_sync.c:60-70).  Returns 0 / -1. */
+int oai4g_dl_ch_estimates_time(const oai4g_frame_parms_t *frame_parms, int nb_antennas_rx,
+                               const int32_t *const *dl_ch_estimates, int32_t *const *dl_ch_estimates_time);
+/* Batched form: job j transforms d_est[j * est_stride + 8 ...] into d_time[j * time_stride ...]
+ * (est_stride >= N + 8, time_stride >= N words); device pointers, async on `stream`. */
+int oai4g_chest_time_batch(const oai4g_frame_parms_t *frame_parms, int n_jobs, const int32_t *d_est,
+                           size_t est_stride, int32_t *d_time, size_t time_stride, void *stream);
+
+/* lte_est_freq_offset (PHY/LTE_ESTIMATION/lte_est_freq_offset.c:104-193, called by slot_fep.c:211-217
+ * at l = 4 - Ncp): antenna 0's plane dl_ch_estimates[0]; dl_ch_shift = 6 + log2_approx(
+ * dl_channel_level(row l from RE 12)) / 2; omega = dot_product (cdot_prod.c:40) of row l against the
+ * other pilot row (row 4 - Ncp when l = 0, else row 0) over (N_RB_DL / 2 - 1) * 12 REs from RE 12 plus
+ * the same from RE (N_RB_DL / 2 + 1) * 12; freq_offset_est = (int)(atan2(omega) / 2 pi / 285.8 us
+ * (normal CP) or 250 us); the first call (or one with reset != 0) stores it, later calls filter
+ * (est * 2^10 + f * (32767 - 2^10)) >> 15.  The filter state is process-wide, as the reference's
+ * static first_run.  The dot products run on the GPU; atan2 and the filter are the host's scalar
+ * tail, as in the reference.  Returns 0, or -1 for l other than 0 / 4 - Ncp (freq_offset untouched). */
+int oai4g_lte_est_freq_offset(int32_t *const *dl_ch_estimates, const oai4g_frame_parms_t *frame_parms, int l,
+                              int *freq_offset, int reset);
+/* Batched integer part: omega (re | im << 16) of n_jobs estimate planes d_est[j * est_stride ...]
+ * (rows 0 .. 4 - Ncp present) into d_omega[j]; then oai4g_freq_offset_update applies the scalar
+ * tail of one call per omega with a caller-held first_run (1 = the reference's first run). */
+int oai4g_freq_offset_omega_batch(const oai4g_frame_parms_t *frame_parms, int n_jobs, const int32_t *d_est,
+                                  size_t est_stride, int l, int32_t *d_omega, void *stream);
+int oai4g_freq_offset_update(const oai4g_frame_parms_t *frame_parms, int32_t omega, int *freq_offset, int *first_run);
 /* The six interpolation filters of pilot offset k = (nu + nushift) % 6 as the estimator uses them
  * (lte_dl_channel_estimation.c:105-180): fl, f2l2, f, f2, fr, f2r2 (filt96_32.h by formula). */
 void oai4g_chest_filters(uint8_t k, int16_t out[6][24]);

@@ -142,8 +142,8 @@ int slot_fep(PHY_VARS_UE *ue, unsigned char l, unsigned char Ns, int sample_offs
   int ret = oai4g_slot_fep((int32_t **)ue->lte_ue_common_vars.rxdata, (int32_t **)ue->lte_ue_common_vars.rxdataF,
                            &fp, ue->lte_frame_parms.nb_antennas_rx, l, Ns, sample_offset, no_prefix);
   if (ret != 0) return ret;
-  /* channel estimation: lte_dl_channel_estimation below (GPU); the frequency-offset estimator
-   * stays on the reference's CPU code (slot_fep.c:179-222) */
+  /* channel estimation and the frequency-offset estimator (slot_fep.c:179-222): the GPU bindings
+   * lte_dl_channel_estimation / lte_est_freq_offset below */
   if (ue->perfect_ce == 0 && (l == 0 || l == 4 - ue->lte_frame_parms.Ncp)) {
     const unsigned char symbol = l + (7 - ue->lte_frame_parms.Ncp) * (Ns & 1);
     for (int aa = 0; aa < ue->lte_frame_parms.nb_antennas_tx_eNB; aa++) {
@@ -247,7 +247,17 @@ int lte_dl_channel_estimation(PHY_VARS_UE *ue, uint8_t eNB_id, uint8_t eNB_offse
                                         (int32_t *)ue->lte_ue_common_vars.dl_ch_estimates[0][(p << 1) + a], Ns, p, l,
                                         symbol) != 0)
       return -1;
-  return 0;
+  /* :704-738: the idft of every (port, RX antenna) plane into dl_ch_estimates_time */
+  return oai4g_dl_ch_estimates_time(&fp, nrx, (const int32_t *const *)ue->lte_ue_common_vars.dl_ch_estimates[0],
+                                    (int32_t *const *)ue->lte_ue_common_vars.dl_ch_estimates_time[0]);
+}
+
+/* lte_est_freq_offset.c:104 (dot products on the GPU, atan2 + filter on the host as in the reference) */
+int lte_est_freq_offset(int **dl_ch_estimates, LTE_DL_FRAME_PARMS *frame_parms, int l, int *freq_offset, int reset)
+{
+  oai4g_frame_parms_t fp;
+  fp_to(frame_parms, &fp);
+  return oai4g_lte_est_freq_offset((int32_t *const *)dl_ch_estimates, &fp, l, freq_offset, reset);
 }
 
 /* rx_pdsch (dlsch_demodulation.c:82) for TM1 (one TX port, one RX antenna), TM2 (ALAMOUTI) and TM3

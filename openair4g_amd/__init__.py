@@ -241,6 +241,16 @@ _SIGS = {
                                                      ctypes.c_uint8]),
     "oai4g_rx_batch_tm2": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p,
                                           ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p]),
+    "oai4g_dl_ch_estimates_time": (ctypes.c_int, [ctypes.POINTER(FrameParms), ctypes.c_int, ctypes.c_void_p,
+                                                  ctypes.c_void_p]),
+    "oai4g_chest_time_batch": (ctypes.c_int, [ctypes.POINTER(FrameParms), ctypes.c_int, ctypes.c_void_p,
+                                              ctypes.c_size_t, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p]),
+    "oai4g_lte_est_freq_offset": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(FrameParms), ctypes.c_int,
+                                                 ctypes.POINTER(ctypes.c_int), ctypes.c_int]),
+    "oai4g_freq_offset_omega_batch": (ctypes.c_int, [ctypes.POINTER(FrameParms), ctypes.c_int, ctypes.c_void_p,
+                                                     ctypes.c_size_t, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p]),
+    "oai4g_freq_offset_update": (ctypes.c_int, [ctypes.POINTER(FrameParms), ctypes.c_int32,
+                                                ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int)]),
     "oai4g_signal_energy": (ctypes.c_int32, [ctypes.c_void_p, ctypes.c_uint32]),
     "oai4g_signal_energy_batch": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_size_t, ctypes.c_uint32,
                                                  ctypes.c_void_p, ctypes.c_void_p]),
@@ -753,6 +763,40 @@ def lte_dl_channel_estimation(fp, rxdataF, est, Ns, p, l, symbol):
     return est
 
 
+def _plane_ptrs(planes):
+    arr = (ctypes.c_void_p * 8)()
+    for i, a in enumerate(planes):
+        if a is not None:
+            assert a.dtype == np.int32 and a.flags.c_contiguous
+            arr[i] = a.ctypes.data
+    return arr
+
+
+def dl_ch_estimates_time(fp, nb_antennas_rx, planes, out_planes):
+    """lte_dl_channel_estimation's idft tail (:704-738): out_planes[(p << 1) + aarx] = idft_N of the
+    estimate plane from word 8 (scale 1), for every non-None plane; lists of 8 int32 arrays / None."""
+    init()
+    _check(lib().oai4g_dl_ch_estimates_time(ctypes.byref(fp), nb_antennas_rx, _plane_ptrs(planes),
+                                             _plane_ptrs(out_planes)) == 0)
+    return out_planes
+
+
+def lte_est_freq_offset(planes, fp, l, freq_offset, reset=0):
+    """lte_est_freq_offset drop-in: planes[0] = antenna 0's estimate plane (int32 [nsymb*N]);
+    freq_offset = a ctypes.c_int updated in place (process-wide first_run, as the reference's static)."""
+    init()
+    _check(lib().oai4g_lte_est_freq_offset(_plane_ptrs(planes), ctypes.byref(fp), l, ctypes.byref(freq_offset),
+                                            reset) == 0)
+    return freq_offset.value
+
+
+def freq_offset_update(fp, omega, freq_offset, first_run):
+    """The scalar tail of one lte_est_freq_offset call (ctypes.c_int state in place)."""
+    _check(lib().oai4g_freq_offset_update(ctypes.byref(fp), int(np.int32(omega)), ctypes.byref(freq_offset),
+                                           ctypes.byref(first_run)) == 0)
+    return freq_offset.value
+
+
 def chest_dc_filters(k):
     """The 25-PRB DC-pair filters (filt24_k_dcr, filt24_(k+2)_dcl) of pilot offset k."""
     out = np.zeros((2, 24), dtype=np.int16)
@@ -797,6 +841,35 @@ class ChestBatch:
     def launch(self, d_rxdataF, stream=None):
         """Device-only: estimates of d_rxdataF (n_sf grids + the next symbol 0) into self.d_est."""
         _check(self.L.oai4g_chest_batch(self.cfg, self.n_sf, d_rxdataF, self.d_est, stream) == 0)
+
+    def time_estimates(self, stream=None):
+        """dl_ch_estimates_time of every subframe's estimate plane in self.d_est: [n_sf][N] int32."""
+        N, stride = self.fp.ofdm_symbol_size, self.n_grid // self.n_sf
+        d_t = self.L.oai4g_dev_alloc(self.n_sf * N * 4)
+        _check(bool(d_t))
+        try:
+            _check(self.L.oai4g_chest_time_batch(ctypes.byref(self.fp), self.n_sf, self.d_est, stride, d_t, N,
+                                                 stream) == 0)
+            _check(self.L.oai4g_sync() == 0)
+            out = np.empty((self.n_sf, N), dtype=np.int32)
+            _check(self.L.oai4g_memcpy_d2h(_ptr(out), d_t, out.nbytes) == 0)
+        finally:
+            self.L.oai4g_dev_free(d_t)
+        return out
+
+    def freq_offset_omegas(self, l, stream=None):
+        """lte_est_freq_offset's integer part (omega, re | im << 16) of every subframe's plane."""
+        d_o = self.L.oai4g_dev_alloc(max(4, self.n_sf * 4))
+        _check(bool(d_o))
+        try:
+            _check(self.L.oai4g_freq_offset_omega_batch(ctypes.byref(self.fp), self.n_sf, self.d_est,
+                                                        self.n_grid // self.n_sf, l, d_o, stream) == 0)
+            _check(self.L.oai4g_sync() == 0)
+            out = np.empty(self.n_sf, dtype=np.int32)
+            _check(self.L.oai4g_memcpy_d2h(_ptr(out), d_o, out.nbytes) == 0)
+        finally:
+            self.L.oai4g_dev_free(d_o)
+        return out
 
     def close(self):
         self.L.oai4g_dev_free(self.d_rx)

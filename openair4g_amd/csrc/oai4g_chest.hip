@@ -375,3 +375,72 @@ hipError_t oai4g_launch_chest_symbol(const chest_dev_t *d_cfg, const chest_dev_t
                      (uint32_t)Ns, (uint32_t)(l == 0 ? 0 : 1), (uint32_t)symbol);
   return hipGetLastError();
 }
+
+/* ======================================================================================
+ * lte_est_freq_offset's integer part (PHY/LTE_ESTIMATION/lte_est_freq_offset.c:45-166, antenna 0):
+ * one wave per estimate plane.  dl_channel_level of row l from RE 12 (re^2 + im^2 over N_RB * 12
+ * REs, wrapping 32-bit sums, C int division), dl_ch_shift = 6 + log2_approx(level) / 2, then
+ * dot_product (PHY/TOOLS/cdot_prod.c:40-118: per RE (xr yr + xi yi) >> shift and
+ * (xr yi - xi yr) >> shift, wrapping sums, packs to int16) of row l against the previous pilot
+ * row over the lower half (from RE 12) and the upper half (from RE (N_RB / 2 + 1) * 12),
+ * (N_RB / 2 - 1) * 12 REs each; omega = the int16 component sums (wrap) as re | im << 16.
+ * Sums are mod 2^32, so the wave's reduction order gives the reference's lane sums exactly.
+ * ==================================================================================== */
+static __device__ __forceinline__ uint32_t wave_sum_u32(uint32_t v)
+{
+#pragma unroll
+  for (int m = 32; m >= 1; m >>= 1) v += (uint32_t)__shfl_xor((int)v, m, 64);
+  return v;
+}
+
+static __device__ __forceinline__ int16_t fo_sat16(int32_t v) { return (int16_t)max(-32768, min(32767, v)); }
+
+__global__ void __launch_bounds__(64) k_freq_offset(const int32_t *__restrict__ est, size_t est_stride, int n_jobs,
+                                                    int N_RB, uint32_t row_off, uint32_t prev_off,
+                                                    int32_t *__restrict__ omega)
+{
+  const int j = blockIdx.x;
+  if (j >= n_jobs) return;
+  const int lane = threadIdx.x;
+  const uint32_t *p = (const uint32_t *)est + (size_t)j * est_stride;
+  const int nre = N_RB * 12;
+  uint32_t acc = 0;
+  for (int i = lane; i < nre; i += 64) {
+    const uint32_t w = p[row_off + 12 + i];
+    const int32_t re = (int16_t)(w & 0xFFFF), im = (int16_t)(w >> 16);
+    acc += (uint32_t)(re * re) + (uint32_t)(im * im);
+  }
+  acc = wave_sum_u32(acc);
+  const int32_t avg = (int32_t)acc / nre;
+  const uint32_t x = (uint32_t)avg & 0x7FFFFFFFu;      /* log2_approx: bits 0..30 */
+  const uint32_t shift = 6 + (x ? 32u - __clz(x) : 0u) / 2;
+  const int n = (N_RB / 2 - 1) * 12, hi = (N_RB / 2 + 1) * 12;
+  int16_t out_re = 0, out_im = 0;
+#pragma unroll
+  for (int half = 0; half < 2; half++) {
+    const int base = half ? hi : 12;
+    uint32_t sre = 0, sim = 0;
+    for (int i = lane; i < n; i += 64) {
+      const uint32_t a = p[row_off + base + i], b = p[prev_off + base + i];
+      const int32_t xr = (int16_t)(a & 0xFFFF), xi = (int16_t)(a >> 16);
+      const int32_t yr = (int16_t)(b & 0xFFFF), yi = (int16_t)(b >> 16);
+      const int32_t nyr = (int16_t)(-yr);                 /* _mm_sign_epi16: -(-32768) = -32768 */
+      sre += (uint32_t)((int32_t)((uint32_t)(xr * yr) + (uint32_t)(xi * yi)) >> shift);
+      sim += (uint32_t)((int32_t)((uint32_t)(xr * yi) + (uint32_t)(xi * nyr)) >> shift);
+    }
+    sre = wave_sum_u32(sre);
+    sim = wave_sum_u32(sim);
+    out_re = (int16_t)(out_re + fo_sat16((int32_t)sre));
+    out_im = (int16_t)(out_im + fo_sat16((int32_t)sim));
+  }
+  if (lane == 0) omega[j] = (int32_t)((uint32_t)(uint16_t)out_re | ((uint32_t)(uint16_t)out_im << 16));
+}
+
+hipError_t oai4g_launch_freq_offset(const int32_t *d_est, size_t est_stride, int n_jobs, int N_RB, uint32_t row_off,
+                                    uint32_t prev_off, int32_t *d_omega, hipStream_t s)
+{
+  if (n_jobs <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_freq_offset, dim3(n_jobs), dim3(64), 0, s, d_est, est_stride, n_jobs, N_RB, row_off, prev_off,
+                     d_omega);
+  return hipGetLastError();
+}

@@ -4156,3 +4156,121 @@ extern "C" int oai4g_lte_dl_channel_estimation(const oai4g_frame_parms_t *fp, co
   }
   return 0;
 }
+
+/* ------------------------------------------------------------------------------------------
+ * lte_est_freq_offset (PHY/LTE_ESTIMATION/lte_est_freq_offset.c:104-193) and dl_ch_estimates_time
+ * (lte_dl_channel_estimation.c:704-738)
+ * ---------------------------------------------------------------------------------------- */
+static int fo_rows(const oai4g_frame_parms_t *fp, int l, uint32_t *row_off, uint32_t *prev_off)
+{
+  const int lp = 4 - fp->Ncp;
+  if (l != 0 && l != lp) {
+    set_err("lte_est_freq_offset: l (%d) must be 0 or %d", l, lp);   /* :127-130 */
+    return -1;
+  }
+  if (fp->N_RB_DL < 4 || (size_t)fp->N_RB_DL * 12 + 12 > fp->ofdm_symbol_size) {
+    set_err("lte_est_freq_offset: N_RB_DL %d not supported", fp->N_RB_DL);
+    return -1;
+  }
+  *row_off = (uint32_t)l * fp->ofdm_symbol_size;
+  *prev_off = (uint32_t)(l == 0 ? lp : 0) * fp->ofdm_symbol_size;
+  return 0;
+}
+
+extern "C" int oai4g_freq_offset_omega_batch(const oai4g_frame_parms_t *fp, int n_jobs, const int32_t *d_est,
+                                             size_t est_stride, int l, int32_t *d_omega, void *stream)
+{
+  NEED_INIT(-1);
+  uint32_t ro, po;
+  if (fo_rows(fp, l, &ro, &po) != 0) return -1;
+  if (n_jobs < 0 || (n_jobs > 0 && (!d_est || !d_omega))) { set_err("freq_offset_omega_batch: bad arguments"); return -1; }
+  HCK(oai4g_launch_freq_offset(d_est, est_stride, n_jobs, fp->N_RB_DL, ro, po, d_omega, (hipStream_t)stream), -1);
+  return 0;
+}
+
+extern "C" int oai4g_freq_offset_update(const oai4g_frame_parms_t *fp, int32_t omega, int *freq_offset, int *first_run)
+{
+  if (!fp || !freq_offset || !first_run) { set_err("freq_offset_update: bad arguments"); return -1; }
+  const double phase = atan2((double)(int16_t)((uint32_t)omega >> 16), (double)(int16_t)omega);   /* :168 */
+  const int est = (int)(phase / (2 * M_PI) / (fp->Ncp == 0 ? 285.8e-6 : 2.5e-4));              /* :174 */
+  if (*first_run == 1) {                                                                          /* :178-182 */
+    *freq_offset = est;
+    *first_run = 0;
+  } else
+    *freq_offset = (est * (1 << 10) + *freq_offset * (32767 - (1 << 10))) >> 15;
+  return 0;
+}
+
+/* the reference's function-static first_run (:117), shared by every caller as there */
+static int g_fo_first_run = 1;
+static std::mutex g_fo_mu;
+
+extern "C" int oai4g_lte_est_freq_offset(int32_t *const *dl_ch_estimates, const oai4g_frame_parms_t *fp, int l,
+                                         int *freq_offset, int reset)
+{
+  NEED_INIT(-1);
+  if (!dl_ch_estimates || !dl_ch_estimates[0] || !fp || !freq_offset) { set_err("lte_est_freq_offset: bad arguments"); return -1; }
+  std::lock_guard<std::mutex> lk(g_fo_mu);
+  if (reset != 0) g_fo_first_run = 1;                                                             /* :122-123 */
+  uint32_t ro, po;
+  if (fo_rows(fp, l, &ro, &po) != 0) return -1;
+  const size_t words = (size_t)(4 - fp->Ncp + 1) * fp->ofdm_symbol_size;   /* rows 0 .. 4 - Ncp */
+  uint8_t *buf = scratch(words * 4 + 256);
+  if (!buf) return -1;
+  int32_t *d_est = (int32_t *)buf, *d_om = (int32_t *)(buf + ((words * 4 + 255) & ~(size_t)255));
+  int32_t om = 0;
+  HCK(hipMemcpyAsync(d_est, dl_ch_estimates[0], words * 4, hipMemcpyHostToDevice, g_scr.s), -1);
+  HCK(oai4g_launch_freq_offset(d_est, 0, 1, fp->N_RB_DL, ro, po, d_om, g_scr.s), -1);
+  HCK(hipMemcpyAsync(&om, d_om, 4, hipMemcpyDeviceToHost, g_scr.s), -1);
+  HCK(hipStreamSynchronize(g_scr.s), -1);
+  return oai4g_freq_offset_update(fp, om, freq_offset, &g_fo_first_run);
+}
+
+static int chest_time_log2n(const oai4g_frame_parms_t *fp)
+{
+  const int l2 = fp->log2_symbol_size;
+  return (l2 >= 7 && l2 <= 11) ? l2 : 9;   /* the switch's default: idft512 (:713-735) */
+}
+
+extern "C" int oai4g_chest_time_batch(const oai4g_frame_parms_t *fp, int n_jobs, const int32_t *d_est,
+                                      size_t est_stride, int32_t *d_time, size_t time_stride, void *stream)
+{
+  NEED_INIT(-1);
+  const int l2 = chest_time_log2n(fp);
+  if (!fp || n_jobs < 0 || (n_jobs > 0 && (!d_est || !d_time)) || est_stride < ((size_t)1 << l2) + 8 ||
+      time_stride < ((size_t)1 << l2)) {
+    set_err("chest_time_batch: bad arguments (an estimate plane must hold N + 8 words)");
+    return -1;
+  }
+  HCK(oai4g_launch_idft_strided(d_est, d_time, l2, n_jobs, est_stride, 8, time_stride, 1, g_tw, (hipStream_t)stream), -1);
+  return 0;
+}
+
+extern "C" int oai4g_dl_ch_estimates_time(const oai4g_frame_parms_t *fp, int nb_antennas_rx,
+                                          const int32_t *const *dl_ch_estimates, int32_t *const *dl_ch_estimates_time)
+{
+  NEED_INIT(-1);
+  if (!fp || !dl_ch_estimates || !dl_ch_estimates_time || nb_antennas_rx < 1 || nb_antennas_rx > 2) {
+    set_err("dl_ch_estimates_time: bad arguments");
+    return -1;
+  }
+  const int l2 = chest_time_log2n(fp);
+  const size_t n = (size_t)1 << l2, in_w = n + 8;
+  const int ntx = fp->nb_antennas_tx_eNB ? fp->nb_antennas_tx_eNB : fp->nb_antennas_tx;
+  int planes[8], np = 0;
+  for (int aarx = 0; aarx < nb_antennas_rx; aarx++)        /* :731-737, NULL planes skipped */
+    for (int p = 0; p < ntx && p < 4; p++)
+      if (dl_ch_estimates[(p << 1) + aarx]) planes[np++] = (p << 1) + aarx;
+  if (np == 0) return 0;
+  const size_t ib = (size_t)np * in_w * 4, ob = (size_t)np * n * 4;
+  uint8_t *buf = scratch(ib + ob + 256);
+  if (!buf) return -1;
+  int32_t *d_in = (int32_t *)buf, *d_out = (int32_t *)(buf + ((ib + 255) & ~(size_t)255));
+  for (int i = 0; i < np; i++)
+    HCK(hipMemcpyAsync(d_in + i * in_w, dl_ch_estimates[planes[i]], in_w * 4, hipMemcpyHostToDevice, g_scr.s), -1);
+  HCK(oai4g_launch_idft_strided(d_in, d_out, l2, np, in_w, 8, n, 1, g_tw, g_scr.s), -1);   /* words 8 .. N + 7 */
+  for (int i = 0; i < np; i++)
+    HCK(hipMemcpyAsync(dl_ch_estimates_time[planes[i]], d_out + i * n, n * 4, hipMemcpyDeviceToHost, g_scr.s), -1);
+  HCK(hipStreamSynchronize(g_scr.s), -1);
+  return 0;
+}

@@ -241,6 +241,11 @@ struct ofdm_sym_t {
 };
 hipError_t oai4g_launch_ofdm(const int32_t *d_in, int32_t *d_out, int log2n, int nsym, const ofdm_sym_t *syms,
                              int scale, const uint32_t *d_tw, hipStream_t s);
+hipError_t oai4g_launch_idft_strided(const int32_t *d_in, int32_t *d_out, int log2n, int n_jobs, size_t in_stride,
+                                     uint32_t in_off, size_t out_stride, int scale, const uint32_t *d_tw, hipStream_t s);
+/* lte_est_freq_offset's integer part (oai4g_chest.hip) */
+hipError_t oai4g_launch_freq_offset(const int32_t *d_est, size_t est_stride, int n_jobs, int N_RB, uint32_t row_off,
+                                    uint32_t prev_off, int32_t *d_omega, hipStream_t s);
 /* control region (oai4g_ctrl.hip): PCFICH */
 struct pcfich_args_t {
   uint32_t c_init;      /* pcfich_scrambling x2 (pcfich.c:97) */

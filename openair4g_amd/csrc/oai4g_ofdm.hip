@@ -495,6 +495,51 @@ hipError_t oai4g_launch_ofdm(const int32_t *d_in, int32_t *d_out, int log2n, int
   return hipGetLastError();
 }
 
+/* Strided IDFT batch: job j transforms in[j * in_stride + in_off ...] (N words) into
+ * out[j * out_stride ...] with the reference's idft decomposition (no prefix).  Used for
+ * dl_ch_estimates_time (lte_dl_channel_estimation.c:704-738: idft of each estimate plane from
+ * word 8, scale 1). */
+template <int LOG2N>
+__global__ void __launch_bounds__(128) k_idft_strided(const int32_t *__restrict__ in, int32_t *__restrict__ out,
+                                                      int n_jobs, size_t in_stride, uint32_t in_off,
+                                                      size_t out_stride, int scale, const uint32_t *__restrict__ tw)
+{
+  constexpr int N = 1 << LOG2N, T = N >> 4, UNITS = 128 / T, LDSW = idft_sel<LOG2N>::XW;
+  __shared__ uint32_t lds_all[UNITS * LDSW];
+  const int unit = threadIdx.x / T, t = threadIdx.x % T;
+  const int j = blockIdx.x * UNITS + unit;
+  const bool active = j < n_jobs;
+  typename idft_sel<LOG2N>::tw_t twr;
+  twr.load(tw, t);
+  const size_t jj = active ? (size_t)j : 0;
+  const uint32_t *src = (const uint32_t *)in + jj * in_stride + in_off;
+  uint32_t *dst = (uint32_t *)out + jj * out_stride;
+  idft_any<LOG2N, 1>(
+      lds_all + unit * LDSW, t, active, twr, [&](s16x2 (*x)[16]) {
+#pragma unroll
+        for (int n = 0; n < 16; n++) x[0][n] = u2c(src[t + T * n]);
+      },
+      [&](int, int tt, int off, s16x2 y) { dst[tt + off] = c2u(y); }, scale);
+}
+
+hipError_t oai4g_launch_idft_strided(const int32_t *d_in, int32_t *d_out, int log2n, int n_jobs, size_t in_stride,
+                                     uint32_t in_off, size_t out_stride, int scale, const uint32_t *d_tw, hipStream_t s)
+{
+  if (n_jobs <= 0) return hipSuccess;
+  const int units = 128 / ((1 << log2n) >> 4);
+  const dim3 grid((n_jobs + units - 1) / units), blk(128);
+  switch (log2n) {
+  case 6: hipLaunchKernelGGL(k_idft_strided<6>, grid, blk, 0, s, d_in, d_out, n_jobs, in_stride, in_off, out_stride, scale, d_tw); break;
+  case 7: hipLaunchKernelGGL(k_idft_strided<7>, grid, blk, 0, s, d_in, d_out, n_jobs, in_stride, in_off, out_stride, scale, d_tw); break;
+  case 8: hipLaunchKernelGGL(k_idft_strided<8>, grid, blk, 0, s, d_in, d_out, n_jobs, in_stride, in_off, out_stride, scale, d_tw); break;
+  case 9: hipLaunchKernelGGL(k_idft_strided<9>, grid, blk, 0, s, d_in, d_out, n_jobs, in_stride, in_off, out_stride, scale, d_tw); break;
+  case 10: hipLaunchKernelGGL(k_idft_strided<10>, grid, blk, 0, s, d_in, d_out, n_jobs, in_stride, in_off, out_stride, scale, d_tw); break;
+  case 11: hipLaunchKernelGGL(k_idft_strided<11>, grid, blk, 0, s, d_in, d_out, n_jobs, in_stride, in_off, out_stride, scale, d_tw); break;
+  default: return hipErrorInvalidValue;
+  }
+  return hipGetLastError();
+}
+
 /* ======================================================================================
  * Modulation helpers shared by the fused kernel and the drop-in grid kernel.
  * ==================================================================================== */

@@ -254,6 +254,12 @@ void orc_chest_dc_filters(uint8_t k, int16_t out[2][24]);      /* filt24_k_dcr, 
 const int16_t *orc_chest_pilot_filter(const int16_t f[6][24], const int16_t fdc[2][24], int N_RB, int m);
 int  orc_lte_dl_channel_estimation(const orc_frame_t *fp, const uint32_t gold[20][2][14], const int32_t *rxdataF,
                                    int32_t *dl_ch_estimates, uint8_t Ns, uint8_t p, uint8_t l, uint8_t symbol);
+/* lte_est_freq_offset.c:45-193, cdot_prod.c:40-118, lte_dl_channel_estimation.c:704-738 */
+int32_t orc_fo_channel_level(const int16_t *dl_ch, int N_RB);
+int32_t orc_dot_product(const int16_t *x, const int16_t *y, uint32_t N, uint8_t shift);
+int32_t orc_fo_omega(const orc_frame_t *fp, const int32_t *dl_ch_estimates0, int l);
+void    orc_fo_update(int Ncp, int32_t omega, int *freq_offset, int *first_run);
+void    orc_chest_time(const orc_frame_t *fp, const int32_t *dl_ch_estimates_plane, int32_t *time_out);
 
 /* ---- dlsim's channel stage (PHY/TOOLS/signal_energy.c:66-110, SIMULATION/TOOLS/rangen_double.c:47-118,
  *      SIMULATION/LTE_PHY/dlsim.c:2852-2866) ---- */

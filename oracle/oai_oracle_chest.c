@@ -7,7 +7,12 @@
  *                              (N_RB_DL 6 / 50 / 100, 25 and 15 branches; high_speed_flag = 1, dlsim.c:2057 and
  *                              lte_init.c:1212; perfect_ce = 0; eNB_offset 0; one RX antenna).
  *                              The final idft of the estimate into dl_ch_estimates_time (:704-738,
- *                              consumed only by the UE's timing tracker) is not restated.
+ *                              the UE timing tracker's input): orc_chest_time.
+ *   lte_est_freq_offset        PHY/LTE_ESTIMATION/lte_est_freq_offset.c:45-193 (dl_channel_level, the
+ *                              two half-band dot products, atan2 and the moving-average filter):
+ *                              orc_fo_channel_level / orc_fo_omega / orc_fo_update
+ *   dot_product                PHY/TOOLS/cdot_prod.c:40-118 (pinned to the reference TU compiled
+ *                              into oracle/_ref/libref_tools.so)
  *   lte_dl_cell_spec_rx        PHY/LTE_REFSIG/lte_dl_cell_spec.c:205-260 (conjugated QPSK pilots,
  *                              amplitude ONE_OVER_SQRT2_Q15)
  *   multadd_real_vector_complex_scalar  PHY/TOOLS/cmult_sv.c:81-122 (mulhi << 2, adds)
@@ -20,6 +25,7 @@
  * (high_speed_flag = 1: ch_offset = symbol * ofdm_symbol_size), subcarrier i of RB rb at
  * 5 + 12 rb + i, the layout dlsch_extract_rbs_single reads.
  */
+#include <math.h>
 #include <stdlib.h>
 #include <string.h>
 
@@ -215,4 +221,86 @@ int orc_lte_dl_channel_estimation(const orc_frame_t *fp, const uint32_t gold[20]
   }
 #undef ROW
   return 0;
+}
+
+/* ---- frequency-offset estimation (PHY/LTE_ESTIMATION/lte_est_freq_offset.c:45-193) and the
+ *      time-domain estimate (lte_dl_channel_estimation.c:704-738) ----
+ * All 32-bit sums wrap (the reference's epi32 lanes); they are taken mod 2^32 here, so the
+ * order of the additions does not matter. */
+
+/* dl_channel_level (lte_est_freq_offset.c:45-102): sum of re^2 + im^2 (madd_epi16, wrapping
+ * epi32 lanes) over N_RB_DL * 12 REs, divided by N_RB_DL * 12 (C int division). */
+int32_t orc_fo_channel_level(const int16_t *dl_ch, int N_RB)
+{
+  uint32_t acc = 0;
+  for (int i = 0; i < N_RB * 12; i++) {
+    const int32_t re = dl_ch[2 * i], im = dl_ch[2 * i + 1];
+    acc += (uint32_t)(re * re) + (uint32_t)(im * im);     /* madd_epi16: the pair sum wraps */
+  }
+  return (int32_t)acc / (N_RB * 12);
+}
+
+/* dot_product (PHY/TOOLS/cdot_prod.c:40-118): sum over N complex of
+ *   re: (xr yr + xi yi) >> shift,  im: (xr yi - xi yr) >> shift   (each madd wraps, srai per RE)
+ * then packs_pi32: both sums saturated to int16; result = re | im << 16. */
+int32_t orc_dot_product(const int16_t *x, const int16_t *y, uint32_t N, uint8_t shift)
+{
+  uint32_t sre = 0, sim = 0;
+  for (uint32_t i = 0; i < (N & ~3u); i++) {
+    const int32_t xr = x[2 * i], xi = x[2 * i + 1], yr = y[2 * i], yi = y[2 * i + 1];
+    /* _mm_sign_epi16(y_swapped, (1, -1)): -yr, with -(-32768) = -32768 */
+    const int32_t nyr = (int16_t)(-yr);
+    const int32_t re = (int32_t)((uint32_t)(xr * yr) + (uint32_t)(xi * yi));
+    const int32_t im = (int32_t)((uint32_t)(xr * yi) + (uint32_t)(xi * nyr));
+    sre += (uint32_t)(re >> shift);
+    sim += (uint32_t)(im >> shift);
+  }
+  return (int32_t)(((uint32_t)(uint16_t)sat16((int32_t)sre)) | ((uint32_t)(uint16_t)sat16((int32_t)sim) << 16));
+}
+
+/* lte_est_freq_offset's integer part (:125-166), antenna 0 only (:135): dl_ch_shift from the
+ * channel level of row l at offset 12, then omega = dot(row l, previous pilot row) over the
+ * lower half (from RE 12) plus the upper half (from RE (N_RB/2 + 1) * 12), (N_RB/2 - 1) * 12 REs
+ * each, added as int16 components (wrap).  Returns omega (re | im << 16), or -1 << 31 for an l
+ * other than 0 or 4 - Ncp (the reference prints and returns -1 without touching freq_offset). */
+int32_t orc_fo_omega(const orc_frame_t *fp, const int32_t *dl_ch_estimates0, int l)
+{
+  const int N = fp->ofdm_symbol_size, N_RB = fp->N_RB_DL, lp = 4 - fp->Ncp;
+  if (l != 0 && l != lp) return INT32_MIN;
+  const int ch_offset = l * N;
+  const int16_t *dl_ch = (const int16_t *)&dl_ch_estimates0[12 + ch_offset];
+  const uint8_t shift = (uint8_t)(6 + orc_log2_approx((uint32_t)orc_fo_channel_level(dl_ch, N_RB)) / 2);
+  const int16_t *prev = (const int16_t *)&dl_ch_estimates0[12 + (ch_offset == 0 ? lp * N : 0)];
+  const uint32_t n = (uint32_t)((N_RB / 2 - 1) * 12);
+  const int32_t o1 = orc_dot_product(dl_ch, prev, n, shift);
+  const int hi = (N_RB / 2 + 1) * 12;
+  dl_ch = (const int16_t *)&dl_ch_estimates0[hi + ch_offset];
+  prev = (const int16_t *)&dl_ch_estimates0[hi + (ch_offset == 0 ? lp * N : 0)];
+  const int32_t o2 = orc_dot_product(dl_ch, prev, n, shift);
+  const int16_t re = (int16_t)((int16_t)o1 + (int16_t)o2), im = (int16_t)((int16_t)(o1 >> 16) + (int16_t)(o2 >> 16));
+  return (int32_t)((uint32_t)(uint16_t)re | ((uint32_t)(uint16_t)im << 16));
+}
+
+/* lte_est_freq_offset's scalar tail (:168-182): phase = atan2(im, re); estimate =
+ * (int)(phase / 2 pi / 285.8e-6 (normal CP) or 2.5e-4); first call (or after a reset) takes the
+ * estimate, later calls filter with coef 2^10: (est * 1024 + f * 31743) >> 15.  *first_run plays
+ * the reference's static first_run. */
+void orc_fo_update(int Ncp, int32_t omega, int *freq_offset, int *first_run)
+{
+  const double phase = atan2((double)(int16_t)(omega >> 16), (double)(int16_t)omega);
+  const int est = (int)(phase / (2 * M_PI) / (Ncp == 0 ? 285.8e-6 : 2.5e-4));
+  if (*first_run == 1) {
+    *freq_offset = est;
+    *first_run = 0;
+  } else
+    *freq_offset = (est * (1 << 10) + *freq_offset * (32767 - (1 << 10))) >> 15;
+}
+
+/* dl_ch_estimates_time (lte_dl_channel_estimation.c:704-738): idft(log2_symbol_size; other sizes:
+ * idft512) of the plane from word 8 (row 0 words 8..N-1, then row 1 words 0..7), scale 1. */
+void orc_chest_time(const orc_frame_t *fp, const int32_t *dl_ch_estimates_plane, int32_t *time_out)
+{
+  int l2 = fp->log2_symbol_size;
+  if (l2 < 7 || l2 > 11) l2 = 9;
+  orc_idft(l2, (const int16_t *)(dl_ch_estimates_plane + 8), (int16_t *)time_out, 1);
 }

@@ -649,3 +649,59 @@ def rx_pdsch_tm3_qq(fp, rxF, est, rb_alloc, mcs0, num_pdcch, subframe, check=Tru
         return None, None, 0
     assert n >= 0
     return o0[:n], o1[:n], sh.value
+
+
+# ---- lte_est_freq_offset (lte_est_freq_offset.c:45-193), dot_product (cdot_prod.c:40-118),
+#      dl_ch_estimates_time (lte_dl_channel_estimation.c:704-738) ----
+REF_TOOLS_SO = os.path.join(ORACLE_DIR, "_ref", "libref_tools.so")
+
+
+def ref_tools():
+    """The reference's PHY/TOOLS signal_energy.c / cdot_prod.c / log2_approx.c compiled unmodified
+    (oracle/_ref/libref_tools.so), or None when it was not built here."""
+    if not os.path.exists(REF_TOOLS_SO):
+        return None
+    L = ctypes.CDLL(REF_TOOLS_SO)
+    if hasattr(L, "dot_product"):
+        L.dot_product.restype = ctypes.c_int32
+        L.dot_product.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint8]
+        L.log2_approx.restype = ctypes.c_uint8
+        L.log2_approx.argtypes = [ctypes.c_uint32]
+    return L
+
+
+def dot_product(x, y, N, shift):
+    L = orc()
+    L.orc_dot_product.restype = ctypes.c_int32
+    L.orc_dot_product.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint8]
+    return L.orc_dot_product(P(np.ascontiguousarray(x, np.int16)), P(np.ascontiguousarray(y, np.int16)), N, shift)
+
+
+def fo_omega(fp, plane0, l):
+    L = orc()
+    L.orc_fo_omega.restype = ctypes.c_int32
+    return L.orc_fo_omega(ctypes.byref(fp), P(np.ascontiguousarray(plane0, np.int32)), l)
+
+
+class FreqOffsetState:
+    """The reference's *freq_offset and static first_run for a sequence of lte_est_freq_offset calls."""
+
+    def __init__(self):
+        self.f = ctypes.c_int(0)
+        self.first = ctypes.c_int(1)
+
+    def call(self, fp, plane0, l, reset=0):
+        if reset:
+            self.first.value = 1
+        om = fo_omega(fp, plane0, l)
+        orc().orc_fo_update(fp.Ncp, ctypes.c_int32(om), ctypes.byref(self.f), ctypes.byref(self.first))
+        return self.f.value
+
+
+def chest_time(fp, plane):
+    """dl_ch_estimates_time of one estimate plane (int32 [>= N + 8])."""
+    out = np.zeros(fp.ofdm_symbol_size if 7 <= fp.log2_symbol_size <= 11 else 512, np.int32)
+    a = _aligned(plane.size, np.int32)
+    a[:] = plane
+    orc().orc_chest_time(ctypes.byref(fp), P(a), P(out))
+    return out
