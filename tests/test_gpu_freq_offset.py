@@ -14,7 +14,7 @@ from test_freq_offset_cpu import _rotated_planes
 
 pytestmark = pytest.mark.gpu
 
-SIZES = [(6, 0), (15, 0), (25, 0), (25, 1), (50, 0), (50, 1), (75, 0), (100, 0), (100, 1)]
+SIZES = [(6, 0), (15, 0), (25, 0), (25, 1), (50, 0), (50, 1), (100, 0), (100, 1)]
 
 
 @pytest.mark.parametrize("N_RB,Ncp", SIZES)
