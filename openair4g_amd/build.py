@@ -74,9 +74,9 @@ def build_oracle(verbose=False):
 
 
 if __name__ == "__main__":
-    if "--variant" in sys.argv:   # build.py --variant NAME -DFOO=1 ... -> variants/NAME/libopenair4g_amd.so
+    if "--variant" in sys.argv:   # build.py --variant NAME -DFOO=1 [-mllvm X] ... -> variants/NAME/libopenair4g_amd.so
         i = sys.argv.index("--variant")
-        name, defs = sys.argv[i + 1], [a for a in sys.argv[i + 2:] if a.startswith("-D")]
+        name, defs = sys.argv[i + 1], [a for a in sys.argv[i + 2:] if a != "--force"]
         print("built", build_lib(force=True, out=os.path.join(ROOT, "variants", name, "libopenair4g_amd.so"),
                                  defines=defs))
         sys.exit(0)

@@ -255,6 +255,8 @@ const int16_t *orc_chest_pilot_filter(const int16_t f[6][24], const int16_t fdc[
 int  orc_lte_dl_channel_estimation(const orc_frame_t *fp, const uint32_t gold[20][2][14], const int32_t *rxdataF,
                                    int32_t *dl_ch_estimates, uint8_t Ns, uint8_t p, uint8_t l, uint8_t symbol);
 /* lte_est_freq_offset.c:45-193, cdot_prod.c:40-118, lte_dl_channel_estimation.c:704-738 */
+void    orc_multadd_complex_vector_real_scalar(const int16_t *x, int16_t alpha, int16_t *y, uint8_t zero_flag, uint32_t N);
+void    orc_multadd_real_vector_complex_scalar(const int16_t *x, const int16_t *alpha, int16_t *y, uint32_t N);
 int32_t orc_fo_channel_level(const int16_t *dl_ch, int N_RB);
 int32_t orc_dot_product(const int16_t *x, const int16_t *y, uint32_t N, uint8_t shift);
 int32_t orc_fo_omega(const orc_frame_t *fp, const int32_t *dl_ch_estimates0, int l);

@@ -16,7 +16,8 @@
  *   lte_dl_cell_spec_rx        PHY/LTE_REFSIG/lte_dl_cell_spec.c:205-260 (conjugated QPSK pilots,
  *                              amplitude ONE_OVER_SQRT2_Q15)
  *   multadd_real_vector_complex_scalar  PHY/TOOLS/cmult_sv.c:81-122 (mulhi << 2, adds)
- *   multadd_complex_vector_real_scalar  cmult_sv.c:55-80 (mulhi << 1, optional adds)
+ *   multadd_complex_vector_real_scalar  cmult_sv.c:55-80 (mulhi << 1, optional adds); both pinned to the
+ *                              reference TU compiled into oracle/_ref/libref_tools.so
  *   filt24_* interpolation filters      PHY/LTE_ESTIMATION/filt96_32.h, restated by formula in
  *                              orc_chest_filters (tests/test_chest_cpu.py checks them entry by
  *                              entry against the header when the reference tree is present).
@@ -112,19 +113,30 @@ const int16_t *orc_chest_pilot_filter(const int16_t f[6][24], const int16_t fdc[
   return (m & 1) ? f[3] : f[2];
 }
 
-/* multadd_complex_vector_real_scalar over one row of N complex entries */
+/* multadd_complex_vector_real_scalar (cmult_sv.c:55-80): y = mulhi(x, alpha) << 1 (zero_flag 1)
+ * or y +sat= that, per int16 of N complex entries */
+void orc_multadd_complex_vector_real_scalar(const int16_t *x, int16_t alpha, int16_t *y, uint8_t zero_flag, uint32_t N)
+{
+  for (uint32_t n = 0; n < 2 * (N & ~3u); n++) {
+    const int16_t m = (int16_t)(uint16_t)((uint32_t)(((int32_t)x[n] * alpha) >> 16) << 1);
+    y[n] = zero_flag == 1 ? m : sat16((int32_t)y[n] + m);
+  }
+}
+
+/* multadd_real_vector_complex_scalar (cmult_sv.c:81-122): for each real x[i], y[i] +sat=
+ * (mulhi(alpha.re, x[i]) << 2, mulhi(alpha.im, x[i]) << 2), N (a multiple of 8) entries */
+void orc_multadd_real_vector_complex_scalar(const int16_t *x, const int16_t *alpha, int16_t *y, uint32_t N)
+{
+  for (uint32_t i = 0; i < (N & ~7u); i++)
+    for (int c = 0; c < 2; c++) {
+      const int16_t v = (int16_t)(uint16_t)((uint32_t)(((int32_t)alpha[c] * x[i]) >> 16) << 2);
+      y[2 * i + c] = sat16((int32_t)y[2 * i + c] + v);
+    }
+}
+
 static void multadd_row(const int32_t *x, int16_t alpha, int32_t *y, int zero_flag, int N)
 {
-  for (int n = 0; n < N; n++) {
-    int16_t v[2], o[2];
-    memcpy(v, &x[n], 4);
-    memcpy(o, &y[n], 4);
-    for (int c = 0; c < 2; c++) {
-      const int16_t m = (int16_t)(uint16_t)((uint32_t)(((int32_t)v[c] * alpha) >> 16) << 1);
-      o[c] = zero_flag ? m : sat16((int32_t)o[c] + m);
-    }
-    memcpy(&y[n], o, 4);
-  }
+  orc_multadd_complex_vector_real_scalar((const int16_t *)x, alpha, (int16_t *)y, (uint8_t)zero_flag, (uint32_t)N);
 }
 
 int orc_lte_dl_channel_estimation(const orc_frame_t *fp, const uint32_t gold[20][2][14], const int32_t *rxdataF,
@@ -166,15 +178,7 @@ int orc_lte_dl_channel_estimation(const orc_frame_t *fp, const uint32_t gold[20]
       /* dl_ch advances 4 entries after an even pilot and 8 after an odd one (also across the DC
        * pair of 15 / 25 PRB, :431-457, :573-592) */
       int32_t *y = dl_ch + 12 * (m >> 1) + 4 * (m & 1);
-      for (int i = 0; i < 24; i++) {                         /* multadd_real_vector_complex_scalar */
-        int16_t o[2];
-        memcpy(o, &y[i], 4);
-        for (int c = 0; c < 2; c++) {
-          const int16_t v = (int16_t)(uint16_t)((uint32_t)(((int32_t)ch[c] * flt[i]) >> 16) << 2);
-          o[c] = sat16((int32_t)o[c] + v);
-        }
-        memcpy(&y[i], o, 4);
-      }
+      orc_multadd_real_vector_complex_scalar(flt, ch, (int16_t *)y, 24);
     }
   }                                                          /* other N_RB: "not implemented", row stays 0 */
   /* temporal interpolation (high_speed_flag = 1, :639-698) */

@@ -8,6 +8,7 @@ high_speed_flag = 1, the 6 / 50 / 100, 25 and 15 PRB branches).  Pinned
     turbo decoder recovers the transport block, also at 6 PRB where slot_fep's 4-sample alignment
     shifts the window (the estimate absorbs the phase ramp that a constant estimate cannot).
 No GPU needed."""
+import ctypes
 import os
 import re
 
@@ -127,3 +128,53 @@ def test_constant_channel_interior_is_flat():
     O.dl_channel_estimation(fp, g, grid, est, 6, 0, 0, 0)
     row = est[:N].view(np.int16).reshape(-1, 2)[5 + 24:5 + 12 * 50 - 24]
     assert np.all(np.abs(row[:, 0].astype(int) - 1024) <= 8) and np.all(np.abs(row[:, 1]) <= 8), row[:4]
+
+
+# ---- the estimator's vector primitives pinned to the reference's own PHY/TOOLS/cmult_sv.c ----
+@pytest.mark.parametrize("zero_flag", [0, 1])
+@pytest.mark.parametrize("N", [4, 128, 2048])
+def test_multadd_complex_vector_real_scalar_equals_reference(zero_flag, N):
+    R = O.ref_tools()
+    if R is None or not hasattr(R, "multadd_complex_vector_real_scalar"):
+        pytest.skip("reference tree absent (oracle/_ref/libref_tools.so not built)")
+    R.multadd_complex_vector_real_scalar.argtypes = [ctypes.c_void_p, ctypes.c_int16, ctypes.c_void_p, ctypes.c_uint8,
+                                                     ctypes.c_uint32]
+    L = O.orc()
+    L.orc_multadd_complex_vector_real_scalar.argtypes = [ctypes.c_void_p, ctypes.c_int16, ctypes.c_void_p,
+                                                         ctypes.c_uint8, ctypes.c_uint32]
+    rng = np.random.default_rng(N + zero_flag)
+    for alpha in (21845, 10923, 24576, 8192, 16384, 32767, -32768, 1):
+        x = O._aligned(2 * N, np.int16)
+        x[:] = rng.integers(-2**15, 2**15, 2 * N)
+        x[:8] = [-32768, 32767, -32768, -1, 0, 1, 32767, -32767][:min(8, 2 * N)]
+        y0 = rng.integers(-2**15, 2**15, 2 * N).astype(np.int16)
+        yr, yo = O._aligned(2 * N, np.int16), O._aligned(2 * N, np.int16)
+        yr[:] = y0
+        yo[:] = y0
+        R.multadd_complex_vector_real_scalar(O.P(x), alpha, O.P(yr), zero_flag, N)
+        L.orc_multadd_complex_vector_real_scalar(O.P(x), alpha, O.P(yo), zero_flag, N)
+        assert np.array_equal(yr, yo), alpha
+
+
+def test_multadd_real_vector_complex_scalar_equals_reference():
+    R = O.ref_tools()
+    if R is None or not hasattr(R, "multadd_real_vector_complex_scalar"):
+        pytest.skip("reference tree absent")
+    R.multadd_real_vector_complex_scalar.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32]
+    L = O.orc()
+    L.orc_multadd_real_vector_complex_scalar.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                                         ctypes.c_uint32]
+    rng = np.random.default_rng(9)
+    for trial in range(200):
+        N = 24 if trial % 2 else 8 * int(rng.integers(1, 40))
+        x = O._aligned(N, np.int16)
+        x[:] = rng.integers(-2**15, 2**15, N) if trial % 3 else rng.choice([-32768, 32767, 0, 16384, -16384], N)
+        a = O._aligned(2, np.int16)
+        a[:] = rng.integers(-2**15, 2**15, 2)
+        y0 = rng.integers(-2**15, 2**15, 2 * N).astype(np.int16)
+        yr, yo = O._aligned(2 * N, np.int16), O._aligned(2 * N, np.int16)
+        yr[:] = y0
+        yo[:] = y0
+        R.multadd_real_vector_complex_scalar(O.P(x), O.P(a), O.P(yr), N)
+        L.orc_multadd_real_vector_complex_scalar(O.P(x), O.P(a), O.P(yo), N)
+        assert np.array_equal(yr, yo), trial
