@@ -656,6 +656,10 @@ struct modofdm_geom {
   /* OAI4G_MOD_STAGE: per codeword one 16-bit QAM-table address per data RE (12 N_RB + 3 <= 3N/4
    * entries, host-checked), two sentinel entries at SENT; quad q = 4 REs, QPT quads per thread */
   static constexpr int SENT = (N * 3) / 4, SW = SENT + 4, QPT = 3, QROW = 65;
+  /* guard band: leaf inputs t + T n with n in [ZLO, ZHI] fall between subcarrier 6 N_RB_DL and
+   * first_carrier_offset = N - 6 N_RB_DL for every thread t (N_RB_DL 6/25/50/100: n = 5..10;
+   * 15: n = 6..9; host-checked), where the reference's grid is zero */
+  static constexpr int ZLO = LOG2N == 8 ? 6 : 5, ZHI = LOG2N == 8 ? 9 : 10;
 };
 
 /* 4 bytes from any byte address of global memory (unaligned dword load) */
@@ -673,6 +677,9 @@ static __device__ __forceinline__ uint32_t ld_u32_any(const uint8_t *p)
 /* the barrier at the end of an item is not needed: the next item's LDS writes (staging, then the
  * leaves) are separated from this item's last reads (prologue, pass C) by the staging barrier */
 #define OAI4G_MOD_ENDSYNC 0
+#endif
+#ifndef OAI4G_MOD_ZBAND
+#define OAI4G_MOD_ZBAND 1   /* the guard-band leaf inputs are the constant 0: no code, LDS or QAM work for them */
 #endif
 #ifndef OAI4G_MODOFDM_WAVES
 #define OAI4G_MODOFDM_WAVES 3   /* measured: 3 waves/SIMD (<=168 VGPRs) beats 2 (no cap) and 4 (spills) */
@@ -897,11 +904,13 @@ __global__ void __launch_bounds__(128) MODOFDM_ATTR k_modofdm(const cfg_dev_t *_
           /* remap_tm data codes are 2 idx | parity << 15 (ALAMOUTI: 2 (2i + role)): the byte
            * offset of entry idx; any non-data code (>= 0xC000) clamps to the zero sentinel */
           constexpr uint32_t AM = MODE == 1 ? 0x7FFCu : 0x7FFEu;
+          auto zb = [&](int n) { return OAI4G_MOD_ZBAND && n >= G::ZLO && n <= G::ZHI; };   /* constant after unrolling */
 #pragma unroll
           for (int g = 0; g < 16; g += GR) {
             uint32_t code[GR], v0[GR], v1[GR];
 #pragma unroll
             for (int n = 0; n < GR; n++) {
+              if (zb(g + n)) continue;
               code[n] = (rw[(g + n) >> 1] >> (16 * ((g + n) & 1))) & 0xFFFFu;
               const uint32_t a = min(code[n] & AM, 2u * SENT);
               v0[n] = *(const uint16_t *)(sb0 + a);
@@ -910,11 +919,17 @@ __global__ void __launch_bounds__(128) MODOFDM_ATTR k_modofdm(const cfg_dev_t *_
             }
 #pragma unroll
             for (int n = 0; n < GR; n++) {
+              if (zb(g + n)) continue;
               v0[n] = *(const uint32_t *)(qb + v0[n]);
               if constexpr (MODE == 1 || CW2) v1[n] = *(const uint32_t *)(qb + v1[n]);
             }
 #pragma unroll
             for (int n = 0; n < GR; n++) {
+              if (zb(g + n)) {
+#pragma unroll
+                for (int a = 0; a < NA; a++) x[a][g + n] = (s16x2){0, 0};
+                continue;
+              }
               const s16x2 x0 = u2c(v0[n]);
               if constexpr (MODE == 1) {
                 alm_pair(x0, u2c(v1[n]), (code[n] >> 1) & 1u, x[0][g + n], x[1][g + n]);
@@ -1004,6 +1019,9 @@ __global__ void __launch_bounds__(128) MODOFDM_ATTR k_modofdm(const cfg_dev_t *_
               /* cell-specific RS (pilots.c:43-168): overwrite the antenna carrying port p */
 #pragma unroll
               for (int n = 0; n < 16; n++) {
+#if OAI4G_MOD_STAGE
+                if (zb(n)) continue;   /* no CRS or control RE in the guard band */
+#endif
                 const uint32_t cd = (rw[n >> 1] >> (16 * (n & 1))) & 0xFFFFu;
                 const bool pil_re = cd >= OAI4G_CRS_CODE && cd != 0xFFFFu;
                 const uint32_t ci = (cd >> 9) & 7u, m = cd & 0xFFu, port = ((cd >> 8) & 1u) | (ci >= 4 ? 2u : 0u);
@@ -1121,6 +1139,13 @@ hipError_t oai4g_launch_modofdm(const cfg_dev_t *d_cfg, const cfg_dev_t *h_cfg, 
   if (h_cfg->mimo_mode != OAI4G_SISO && h_cfg->n_ant != 2 && !(h_cfg->mimo_mode == OAI4G_LARGE_CDD && h_cfg->n_ant == 4))
     return hipErrorInvalidValue;
   if (h_cfg->mimo_mode == OAI4G_LARGE_CDD && h_cfg->n_cw != 2) return hipErrorInvalidValue;
+  if (OAI4G_MOD_ZBAND && h_cfg->log2N >= 7 && h_cfg->log2N <= 11) {
+    /* the guard-band leaf inputs must be zero subcarriers: T ZLO > 6 N_RB_DL, T (ZHI + 1) <= first_carrier */
+    const uint32_t T = h_cfg->N >> 4, zlo = h_cfg->log2N == 8 ? 6u : 5u, zhi = h_cfg->log2N == 8 ? 9u : 10u;
+    if (h_cfg->first_carrier != h_cfg->N - 6 * h_cfg->N_RB_DL || T * zlo <= 6 * h_cfg->N_RB_DL ||
+        T * (zhi + 1) > h_cfg->first_carrier)
+      return hipErrorInvalidValue;
+  }
   switch (h_cfg->log2N) {
   case 7: return launch_modofdm_n<7>(d_cfg, h_cfg, sf0, n_items, d_ebits, d_iq, s);
   case 8: return launch_modofdm_n<8>(d_cfg, h_cfg, sf0, n_items, d_ebits, d_iq, s);
