@@ -679,7 +679,10 @@ static __device__ __forceinline__ uint32_t ld_u32_any(const uint8_t *p)
 #define OAI4G_MOD_ENDSYNC 0
 #endif
 #ifndef OAI4G_MOD_ZBAND
-#define OAI4G_MOD_ZBAND 1   /* the guard-band leaf inputs are the constant 0: no code, LDS or QAM work for them */
+/* the guard-band leaf inputs are the constant 0: no code, LDS or QAM work for them.  1 = in every
+ * kernel but the plain LARGE_CDD one (C3 without CRS / control: measured 1.7 % slower with it, while
+ * the full grid gains 0.9 % and C4 4-6 %, profiles/mod_ab_r03_zband.txt); 2 = everywhere; 0 = off */
+#define OAI4G_MOD_ZBAND 1
 #endif
 #ifndef OAI4G_MODOFDM_WAVES
 #define OAI4G_MODOFDM_WAVES 3   /* measured: 3 waves/SIMD (<=168 VGPRs) beats 2 (no cap) and 4 (spills) */
@@ -904,45 +907,54 @@ __global__ void __launch_bounds__(128) MODOFDM_ATTR k_modofdm(const cfg_dev_t *_
           /* remap_tm data codes are 2 idx | parity << 15 (ALAMOUTI: 2 (2i + role)): the byte
            * offset of entry idx; any non-data code (>= 0xC000) clamps to the zero sentinel */
           constexpr uint32_t AM = MODE == 1 ? 0x7FFCu : 0x7FFEu;
-          auto zb = [&](int n) { return OAI4G_MOD_ZBAND && n >= G::ZLO && n <= G::ZHI; };   /* constant after unrolling */
+          constexpr bool ZB = OAI4G_MOD_ZBAND == 2 || (OAI4G_MOD_ZBAND == 1 && (CRS || MODE != 2));
+          auto zb = [&](int n) { return ZB && n >= G::ZLO && n <= G::ZHI; };   /* constant after unrolling */
+          /* the NZ leaf inputs outside the guard band, visited in groups of GZ (the i-th is act(i)) */
+          constexpr int NZ = ZB ? 16 - (G::ZHI - G::ZLO + 1) : 16;
+#ifndef OAI4G_MOD_GROUPZ
+#define OAI4G_MOD_GROUPZ 5
+#endif
+          constexpr int GZ = ZB ? (NZ % OAI4G_MOD_GROUPZ == 0 ? OAI4G_MOD_GROUPZ : 4) : GR;
+          auto act = [&](int i) { return (ZB && i >= G::ZLO) ? i + (G::ZHI - G::ZLO + 1) : i; };
 #pragma unroll
-          for (int g = 0; g < 16; g += GR) {
-            uint32_t code[GR], v0[GR], v1[GR];
+          for (int n = 0; n < 16; n++)
+            if (zb(n)) {
 #pragma unroll
-            for (int n = 0; n < GR; n++) {
-              if (zb(g + n)) continue;
-              code[n] = (rw[(g + n) >> 1] >> (16 * ((g + n) & 1))) & 0xFFFFu;
+              for (int a = 0; a < NA; a++) x[a][n] = (s16x2){0, 0};
+            }
+#pragma unroll
+          for (int g = 0; g < NZ; g += GZ) {
+            uint32_t code[GZ], v0[GZ], v1[GZ];
+#pragma unroll
+            for (int n = 0; n < GZ; n++) {
+              const int i = act(g + n);
+              code[n] = (rw[i >> 1] >> (16 * (i & 1))) & 0xFFFFu;
               const uint32_t a = min(code[n] & AM, 2u * SENT);
               v0[n] = *(const uint16_t *)(sb0 + a);
               if constexpr (MODE == 1) v1[n] = *(const uint16_t *)(sb0 + a + 2);
               if constexpr (CW2) v1[n] = *(const uint16_t *)(sb1 + a);
             }
 #pragma unroll
-            for (int n = 0; n < GR; n++) {
-              if (zb(g + n)) continue;
+            for (int n = 0; n < GZ; n++) {
               v0[n] = *(const uint32_t *)(qb + v0[n]);
               if constexpr (MODE == 1 || CW2) v1[n] = *(const uint32_t *)(qb + v1[n]);
             }
 #pragma unroll
-            for (int n = 0; n < GR; n++) {
-              if (zb(g + n)) {
-#pragma unroll
-                for (int a = 0; a < NA; a++) x[a][g + n] = (s16x2){0, 0};
-                continue;
-              }
+            for (int n = 0; n < GZ; n++) {
+              const int i = act(g + n);
               const s16x2 x0 = u2c(v0[n]);
               if constexpr (MODE == 1) {
-                alm_pair(x0, u2c(v1[n]), (code[n] >> 1) & 1u, x[0][g + n], x[1][g + n]);
+                alm_pair(x0, u2c(v1[n]), (code[n] >> 1) & 1u, x[0][i], x[1][i]);
               } else if constexpr (MODE == 3) {
                 const s16x2 x1 = u2c(v1[n]);
                 const uint32_t sel = ((re0 + ((code[n] & 0x7FFFu) >> 1)) & 7u) * 4u + 2u * pair;   /* (i mod 8, p) */
 #pragma unroll
                 for (int a = 0; a < 2; a++)
-                  x[a][g + n] = half_signed(((CDD4_QSEL >> (sel + a)) & 1u) ? x1 : x0, (CDD4_NEG >> (sel + a)) & 1u);
+                  x[a][i] = half_signed(((CDD4_QSEL >> (sel + a)) & 1u) ? x1 : x0, (CDD4_NEG >> (sel + a)) & 1u);
               } else if constexpr (NA == 2) {
-                cdd_pair(x0, u2c(v1[n]), code[n] >> 15 & 1u, x[0][g + n], x[1][g + n]);
+                cdd_pair(x0, u2c(v1[n]), code[n] >> 15 & 1u, x[0][i], x[1][i]);
               } else {
-                x[0][g + n] = x0;                                   /* TM1: SISO precoder */
+                x[0][i] = x0;                                   /* TM1: SISO precoder */
               }
             }
           }
