@@ -916,11 +916,16 @@ __global__ void __launch_bounds__(128) MODOFDM_ATTR k_modofdm(const cfg_dev_t *_
 #endif
           constexpr int GZ = ZB ? (NZ % OAI4G_MOD_GROUPZ == 0 ? OAI4G_MOD_GROUPZ : 4) : GR;
           auto act = [&](int i) { return (ZB && i >= G::ZLO) ? i + (G::ZHI - G::ZLO + 1) : i; };
+#ifndef OAI4G_MOD_ZB_OPAQUE
+#define OAI4G_MOD_ZB_OPAQUE 0   /* 1: the guard-band zeros come from a v_mov the compiler cannot fold (A/B of the leaf folding) */
+#endif
 #pragma unroll
           for (int n = 0; n < 16; n++)
             if (zb(n)) {
+              uint32_t z = 0;
+              if (OAI4G_MOD_ZB_OPAQUE) asm("v_mov_b32 %0, 0" : "=v"(z));
 #pragma unroll
-              for (int a = 0; a < NA; a++) x[a][n] = (s16x2){0, 0};
+              for (int a = 0; a < NA; a++) x[a][n] = u2c(z);
             }
 #pragma unroll
           for (int g = 0; g < NZ; g += GZ) {
