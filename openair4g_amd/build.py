@@ -54,18 +54,22 @@ def build_lib(force=False, verbose=False, out=None, defines=()):
 
 
 def build_host_tools(verbose=False):
-    """gcc-built C host programs over the C ABI (tools/dlsim_tx.c -> tools/bin/dlsim_tx)."""
-    out = os.path.join(ROOT, "tools", "bin", "dlsim_tx")
-    src = os.path.join(ROOT, "tools", "dlsim_tx.c")
-    if not _newer(out, [src, LIB, os.path.join(ROOT, "include", "oai4g.h")]):
-        return out
-    os.makedirs(os.path.dirname(out), exist_ok=True)
-    cmd = ["gcc", "-O2", "-std=gnu11", "-Wall", "-I", os.path.join(ROOT, "include"), src, "-L", LIBDIR,
-           "-lopenair4g_amd", "-Wl,-rpath,$ORIGIN/../../openair4g_amd/lib", "-o", out]
-    if verbose:
-        print(" ".join(cmd))
-    subprocess.run(cmd, check=True)
-    return out
+    """gcc-built C host programs over the C ABI: tools/dlsim_tx.c (dlsim's transmit loop) and
+    tools/dlsim_rx.c (the whole downlink loop, eNB to decoded transport blocks) -> tools/bin/."""
+    outs = []
+    for name in ("dlsim_tx", "dlsim_rx"):
+        out = os.path.join(ROOT, "tools", "bin", name)
+        src = os.path.join(ROOT, "tools", name + ".c")
+        outs.append(out)
+        if not _newer(out, [src, LIB, os.path.join(ROOT, "include", "oai4g.h")]):
+            continue
+        os.makedirs(os.path.dirname(out), exist_ok=True)
+        cmd = ["gcc", "-O2", "-std=gnu11", "-Wall", "-I", os.path.join(ROOT, "include"), src, "-L", LIBDIR,
+               "-lopenair4g_amd", "-Wl,-rpath,$ORIGIN/../../openair4g_amd/lib", "-o", out]
+        if verbose:
+            print(" ".join(cmd))
+        subprocess.run(cmd, check=True)
+    return outs[0]
 
 
 def build_oracle(verbose=False):

@@ -45,7 +45,7 @@ def _calls(src):
 DECL = {k: v for k, v in _calls(_strip_comments(HDR)).items() if not k.endswith("_t")}
 
 
-@pytest.mark.parametrize("path", ["integration/oai4g_shim.c", "tools/dlsim_tx.c"])
+@pytest.mark.parametrize("path", ["integration/oai4g_shim.c", "tools/dlsim_tx.c", "tools/dlsim_rx.c"])
 def test_callers_match_header(path):
     calls = _calls(_strip_comments(open(os.path.join(ROOT, path)).read()))
     assert calls
@@ -63,7 +63,8 @@ def test_shim_entry_points_exported():
         assert "oai4g_" + name in exported, name
 
 
-def test_dlsim_tx_compiles_warning_free(tmp_path):
+@pytest.mark.parametrize("name", ["dlsim_tx", "dlsim_rx"])
+def test_c_drivers_compile_warning_free(tmp_path, name):
     subprocess.run(["gcc", "-O2", "-std=gnu11", "-Wall", "-Wextra", "-Werror", "-Wno-unused-parameter",
-                    "-I", os.path.join(ROOT, "include"), "-c", os.path.join(ROOT, "tools", "dlsim_tx.c"),
+                    "-I", os.path.join(ROOT, "include"), "-c", os.path.join(ROOT, "tools", name + ".c"),
                     "-o", str(tmp_path / "d.o")], check=True)
