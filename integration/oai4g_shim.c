@@ -120,6 +120,7 @@ void do_OFDM_mod(mod_sym_t **txdataF, int32_t **txdata, uint32_t frame, uint16_t
 
 void idft2048(int16_t *x, int16_t *y, int scale) { oai4g_idft2048(x, y, scale); }
 void idft1024(int16_t *x, int16_t *y, int scale) { oai4g_idft1024(x, y, scale); }
+void idft512(int16_t *x, int16_t *y, int scale)  { oai4g_idft512(x, y, scale); }
 void idft256(int16_t *x, int16_t *y, int scale)  { oai4g_idft256(x, y, scale); }
 void idft128(int16_t *x, int16_t *y, int scale)  { oai4g_idft128(x, y, scale); }
 void idft64(int16_t *x, int16_t *y, int scale)   { oai4g_idft64(x, y, scale); }
@@ -156,6 +157,14 @@ int slot_fep(PHY_VARS_UE *ue, unsigned char l, unsigned char Ns, int sample_offs
                           &ue->lte_ue_common_vars.freq_offset, reset_freq_est);
   }
   return 0;
+}
+
+/* cell-specific reference signals: pilots.c:43 (all antennas of the eNB, N subframes) */
+void generate_pilots(PHY_VARS_eNB *phy_vars_eNB, mod_sym_t **txdataF, int16_t amp, uint16_t N)
+{
+  oai4g_frame_parms_t fp;
+  fp_to(&phy_vars_eNB->lte_frame_parms, &fp);
+  oai4g_generate_pilots((int32_t **)txdataF, amp, &fp, N);
 }
 
 /* control region: pcfich.c:48 / :144 (frame_parms->pcfich_reg is derived inside the library) */
