@@ -627,6 +627,8 @@ int oai4g_tx_encode(const oai4g_tx_config_t *cfg, int n_sf, const uint8_t *d_pay
  * (0 load+Gold, 1 CRC, 2 segmentation, 3 turbo, 4 w build, 99 = complete).  Outputs invalid. */
 int oai4g_diag_encode_phase_ms(const oai4g_tx_config_t *cfg, int n_sf, const uint8_t *d_payload, void *d_work,
                                int stop_phase, int reps, float *ms);
+/* Diagnostics: resident k_encode workgroups per CU and the dynamic LDS bytes per workgroup. */
+int oai4g_diag_encode_occupancy(const oai4g_tx_config_t *cfg, int *blocks_per_cu, size_t *lds_bytes);
 /* PMC calibration: stream `bytes` through HBM at 4 B per lane (mode 0 read, 1 write) */
 int oai4g_diag_stream(const void *d_src, void *d_dst, size_t bytes, int mode, void *stream);
 

@@ -315,6 +315,8 @@ _SIGS = {
                                        ctypes.c_void_p]),
     "oai4g_diag_encode_phase_ms": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p,
                                                   ctypes.c_int, ctypes.c_int, ctypes.POINTER(ctypes.c_float)]),
+    "oai4g_diag_encode_occupancy": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(ctypes.c_int),
+                                                   ctypes.POINTER(ctypes.c_size_t)]),
     "oai4g_diag_stream": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int,
                                          ctypes.c_void_p]),
     "oai4g_dev_alloc": (ctypes.c_void_p, [ctypes.c_size_t]),

@@ -1123,6 +1123,14 @@ static hipError_t launch_encode_impl(const cfg_dev_t *d_cfg, const cfg_dev_t *h_
   return hipGetLastError();
 }
 
+/* resident k_encode workgroups per CU at this configuration's dynamic LDS (diagnostic) */
+hipError_t oai4g_encode_occupancy(const cfg_dev_t *h_cfg, int *blocks_per_cu, size_t *lds_bytes)
+{
+  *lds_bytes = enc_lds_bytes(h_cfg);
+  (void)hipFuncSetAttribute((const void *)k_encode, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+  return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, k_encode, 256, *lds_bytes);
+}
+
 hipError_t oai4g_launch_encode_debug(const cfg_dev_t *d_cfg, const cfg_dev_t *h_cfg, int cw, int sf,
                                      const uint8_t *d_payload, enc_debug_t dbg, hipStream_t s)
 {

@@ -1295,6 +1295,15 @@ extern "C" int oai4g_diag_encode_phase_ms(const oai4g_tx_config_t *cfg, int n_sf
   return 0;
 }
 
+/* Diagnostics: resident encoder workgroups per CU and the dynamic LDS bytes of one workgroup */
+extern "C" int oai4g_diag_encode_occupancy(const oai4g_tx_config_t *cfg, int *blocks_per_cu, size_t *lds_bytes)
+{
+  NEED_INIT(-1);
+  if (!cfg || !blocks_per_cu || !lds_bytes) { set_err("diag_encode_occupancy: bad arguments"); return -1; }
+  HCK(oai4g_encode_occupancy(&cfg->h, blocks_per_cu, lds_bytes), -1);
+  return 0;
+}
+
 /* PMC calibration: stream `bytes` at 4 B per lane (mode 0 read from src, 1 write to dst) */
 extern "C" int oai4g_diag_stream(const void *d_src, void *d_dst, size_t bytes, int mode, void *stream)
 {

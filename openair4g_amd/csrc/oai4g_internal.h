@@ -171,6 +171,7 @@ struct cfg_dev_t {
 /* encoder path */
 hipError_t oai4g_launch_encode(const cfg_dev_t *d_cfg, const cfg_dev_t *h_cfg, int sf0, int n_sf,
                                const uint8_t *d_payload, uint32_t *d_ebits, hipStream_t s);
+hipError_t oai4g_encode_occupancy(const cfg_dev_t *h_cfg, int *blocks_per_cu, size_t *lds_bytes);
 hipError_t oai4g_launch_encode_phase(const cfg_dev_t *d_cfg, const cfg_dev_t *h_cfg, int n_sf,
                                      const uint8_t *d_payload, uint32_t *d_ebits, int stop_phase, hipStream_t s);
 struct enc_debug_t {
