@@ -151,57 +151,65 @@ int main(int argc, char **argv)
     if (e > best) { best = e; peak = (int)j; }
   }
 
-  /* dlsch_decoding per subframe: G differs between subframe indices (control / CRS REs) */
+  /* dlsch_decoding: one oai4g_ul_decode_batch per run of consecutive subframes with the same G
+   * (G differs between subframe indices with the control / CRS REs) */
   uint32_t C, Cp, Cm, Kp, Km, F;
   const uint32_t B = p.TBS[0] + 24;
   CHECK(oai4g_lte_segmentation(NULL, NULL, B, &C, &Cp, &Cm, &Kp, &Km, &F) == 0, "lte_segmentation");
   uint8_t *pay = (uint8_t *)malloc((size_t)n_tx * p.payload_stride);
-  int16_t *llr = (int16_t *)malloc(llr_stride * 2);
   const size_t c_stride = 6144 / 8 + 8;
-  uint8_t *cb = (uint8_t *)malloc(C * c_stride), its[OAI4G_MAX_SEGMENTS];
-  CHECK(pay && llr && cb, "host allocation");
+  uint8_t *cb = (uint8_t *)malloc((size_t)n_sf * C * c_stride), *its = (uint8_t *)malloc((size_t)n_sf * C);
+  uint8_t *d_c = (uint8_t *)oai4g_dev_alloc((size_t)n_sf * C * c_stride), *d_it = (uint8_t *)oai4g_dev_alloc(256 + (size_t)n_sf * C);
+  CHECK(pay && cb && its && d_c && d_it, "allocation (decoder)");
   CHECK(oai4g_memcpy_d2h(pay, d_pay, (size_t)n_tx * p.payload_stride) == 0, "copy payload");
-  int ok = 1, max_it = 0;
+  int ok = 1, max_it = 0, launches = 0;
   double t_dec = 0;
-  for (int i = 0; i < n_sf; i++) {
-    const int sf = (sf0 + i) % 10, G = oai4g_rx_llr_count(rx, sf);
+  for (int i0 = 0; i0 < n_sf;) {
+    const int G = oai4g_rx_llr_count(rx, (sf0 + i0) % 10);
     CHECK(G > 0, "rx_llr_count");
+    int n = 1;
+    while (i0 + n < n_sf && oai4g_rx_llr_count(rx, (sf0 + i0 + n) % 10) == G) n++;
     oai4g_ul_config_t *ul = oai4g_ul_config_create(B, (uint32_t)G, Qm, 0, 8, OAI4G_NSOFT, 4);
     CHECK(ul && oai4g_ul_config_C(ul) == (int)C, "ul_config_create");
-    uint8_t *d_c = (uint8_t *)oai4g_dev_alloc(C * c_stride), *d_it = (uint8_t *)oai4g_dev_alloc(256);
-    CHECK(d_c && d_it, "device allocation (decoder)");
     const double d0 = now_us();
-    CHECK(oai4g_ul_decode_batch(ul, 1, d_llr + (size_t)i * llr_stride, llr_stride, d_c, c_stride, d_it, NULL) == 0 &&
-              oai4g_sync() == 0, "ul_decode_batch");
+    CHECK(oai4g_ul_decode_batch(ul, n, d_llr + (size_t)i0 * llr_stride, llr_stride, d_c + (size_t)i0 * C * c_stride,
+                                c_stride, d_it + (size_t)i0 * C, NULL) == 0 && oai4g_sync() == 0, "ul_decode_batch");
     t_dec += now_us() - d0;
-    CHECK(oai4g_memcpy_d2h(cb, d_c, C * c_stride) == 0 && oai4g_memcpy_d2h(its, d_it, C) == 0, "copy blocks");
+    launches++;
+    oai4g_ul_config_destroy(ul);
+    i0 += n;
+  }
+  CHECK(oai4g_memcpy_d2h(cb, d_c, (size_t)n_sf * C * c_stride) == 0 && oai4g_memcpy_d2h(its, d_it, (size_t)n_sf * C) == 0,
+        "copy blocks");
+  for (int i = 0; i < n_sf; i++) {
+    const int sf = (sf0 + i) % 10;
     /* the TB from the blocks: skip block 0's F fillers, drop each block's CRC24B when C > 1 */
     uint32_t pos = 0;
     int tb_ok = 1;
     for (uint32_t r = 0; r < C; r++) {
       const uint32_t K = r < Cm ? Km : Kp, lo = r == 0 ? F : 0, hi = K - (C > 1 ? 24 : 0);
-      if (its[r] > max_it) max_it = its[r];
-      if (its[r] > 4) tb_ok = 0;
+      const uint8_t it = its[(size_t)i * C + r], *blk = cb + ((size_t)i * C + r) * c_stride;
+      if (it > max_it) max_it = it;
+      if (it > 4) tb_ok = 0;
       for (uint32_t k = lo; k < hi && pos < p.TBS[0]; k++, pos++)
-        if (get_bit(cb + r * c_stride, k) != get_bit(pay + (size_t)i * p.payload_stride, pos)) tb_ok = 0;
+        if (get_bit(blk, k) != get_bit(pay + (size_t)i * p.payload_stride, pos)) tb_ok = 0;
     }
     if (pos != p.TBS[0]) tb_ok = 0;
-    printf("subframe %d: G %d, %u blocks, TB %s\n", sf, G, C, tb_ok ? "ok" : "FAILED");
+    printf("subframe %d: G %d, %u blocks, TB %s\n", sf, oai4g_rx_llr_count(rx, sf), C, tb_ok ? "ok" : "FAILED");
     ok &= tb_ok;
-    oai4g_dev_free(d_c);
-    oai4g_dev_free(d_it);
-    oai4g_ul_config_destroy(ul);
   }
+  oai4g_dev_free(d_c);
+  oai4g_dev_free(d_it);
   printf("N_RB %d mcs %d TBS %u: %d subframes, %s; max turbo iterations %d; freq_offset %d Hz; timing peak %d\n", nrb,
          mcs, p.TBS[0], n_sf, ok ? "all transport blocks recovered" : "DECODING FAILED", max_it, freq_offset, peak);
   if (timing)
-    printf("tx %.1f us, fep %.1f us, chest %.1f us, freq/time %.1f us, rx %.1f us, decode %.1f us (first pass, "
-           "includes launch setup)\n",
-           t[1] - t[0], t[2] - t[1], t[3] - t[2], t[4] - t[3], t[5] - t[4], t_dec);
+    printf("tx %.1f us, fep %.1f us, chest %.1f us, freq/time %.1f us, rx %.1f us, decode %.1f us in %d launch(es) "
+           "(first pass, includes launch setup)\n",
+           t[1] - t[0], t[2] - t[1], t[3] - t[2], t[4] - t[3], t[5] - t[4], t_dec, launches);
   free(om);
   free(tim);
   free(pay);
-  free(llr);
   free(cb);
+  free(its);
   return ok ? 0 : 1;
 }
