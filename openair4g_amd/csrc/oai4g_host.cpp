@@ -3335,8 +3335,13 @@ static void rx_extract_map(const oai4g_frame_parms_t *fp, const uint32_t rb_allo
 /* dlsch_extract_rbs_dual (dlsch_demodulation.c:3683-4056) of one symbol as an extraction map of
  * the slots one receive antenna's call leaves written (every antenna and both ports share it): the
  * PBCH / PSS / SSS RBs are dropped; 8 REs per RB in pilot symbols; odd N_RB_DL as written there —
- * the RB around DC reads bins 0..5 for its upper half in non-pilot symbols, and the skip_half = 2
- * pilot branch advances the pointers inside its RE loop. */
+ * the RB around DC reads bins 0..5 for its upper half in non-pilot symbols, the skip_half = 2
+ * pilot branch advances the pointers inside its RE loop, and the full-RB non-pilot branch
+ * (:3932-3936) is `for (i=0;i<12;i++) dl_ch0_ext+=12;` (its loop body was a printf, now commented
+ * out), so the port-0 estimate pointer moves 144 slots per RB while rxF_ext / dl_ch1_ext move 12.
+ * The port-0 writes are tracked with that drift; n = the prefix of slots where the received RE and
+ * both estimates come from the same column (past it the reference reads stale or unwritten port-0
+ * slots, and its writes run past dl_ch_estimates_ext: a stream reaching there is refused). */
 static void rx_extract_map_dual(const oai4g_frame_parms_t *fp, const uint32_t rb_alloc[4], uint32_t subframe, uint32_t l,
                                 std::vector<uint32_t> &map, uint32_t &nb_rb, uint32_t &n)
 {
@@ -3348,11 +3353,14 @@ static void rx_extract_map_dual(const oai4g_frame_parms_t *fp, const uint32_t rb
   const int pss_symb = fp->frame_type == 1 ? 2 : (nsymb >> 1) - 1;
   std::vector<uint32_t> slot(12 * 110 + 256, 0);
   std::vector<uint8_t> wr(12 * 110 + 256, 0);
-  uint32_t p = 0, hw = 0;
+  std::vector<int32_t> col_rx(12 * 110 + 256, -1), col_c0(12 * 110 + 256, -1);
+  uint32_t p = 0, hw = 0, drift = 0;                         /* drift = dl_ch0_ext - rxF_ext (slots) */
   nb_rb = 0;
   auto put = [&](uint32_t pos, uint32_t bin, uint32_t col) {
     slot[pos] = bin | ((5 + col) << 16);
     wr[pos] = 1;
+    col_rx[pos] = (int32_t)col;
+    if (pos + drift < col_c0.size()) col_c0[pos + drift] = (int32_t)col;
     hw = pos + 1 > hw ? pos + 1 : hw;
   };
   auto data_re = [&](uint32_t i) { return i != ns && i != ns + 3 && i != ns + 6 && i != (ns + 9) % 12; };
@@ -3387,6 +3395,7 @@ static void rx_extract_map_dual(const oai4g_frame_parms_t *fp, const uint32_t rb
         const uint32_t o = skip_half == 2 ? 6 : 0, cnt = skip_half ? 6 : 12;
         for (uint32_t i = 0; i < cnt; i++) put(p + i, b0 + o + i, col0 + o + i);
         p += cnt;
+        if (!skip_half) drift += 132;                        /* dl_ch0_ext += 144 (:3932-3934) */
       } else if (skip_half == 1) {
         uint32_t j = 0;
         for (uint32_t i = 0; i < 6; i++)
@@ -3423,7 +3432,7 @@ static void rx_extract_map_dual(const oai4g_frame_parms_t *fp, const uint32_t rb
   /* n = the written prefix: the skip_half = 2 pilot branch leaves holes, which the reference would
    * fill from earlier symbols' ext data (a stream reaching one is refused) */
   n = 0;
-  while (n < hw && wr[n]) n++;
+  while (n < hw && wr[n] && col_c0[n] == col_rx[n]) n++;
   map.insert(map.end(), slot.begin(), slot.begin() + hw);
 }
 

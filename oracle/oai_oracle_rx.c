@@ -278,16 +278,25 @@ static int extract_dual(const orc_frame_t *fp, const int32_t *rxF_sym, const int
   const int sss_symb = fp->frame_type == 1 ? nsymb - 1 : (nsymb >> 1) - 2;
   const int pss_symb = fp->frame_type == 1 ? 2 : (nsymb >> 1) - 1;
   int p = 0;                                                   /* the ext pointer (slot index) */
-  uint8_t wr[12 * 110 + 256];
+  int drift = 0;                                               /* dl_ch0_ext - rxF_ext, in slots */
+  enum { XS = 12 * 110 + 256 };
+  uint8_t wr[XS];
+  int colrx[XS], colc0[XS];
   memset(wr, 0, sizeof(wr));
+  for (int i = 0; i < XS; i++) colrx[i] = colc0[i] = -1;
   *nb_rb = 0;
   *hw = 0;
+  /* the port-0 estimate lands `drift` slots after the others (see the odd full-RB branch below);
+   * writes past the caller's ext plane (the reference overruns dl_ch_estimates_ext there) are
+   * dropped, and the slots they would leave stale are refused through *hw */
 #define PUT(pos, bin, col)                                                              \
   do {                                                                                  \
     rx_ext[pos] = rxF_sym[bin];                                                         \
-    c0_ext[pos] = ch0_sym[5 + (col)];                                                   \
+    if ((pos) + drift < 12 * 110 + 64) c0_ext[(pos) + drift] = ch0_sym[5 + (col)];      \
+    if ((pos) + drift < XS) colc0[(pos) + drift] = (col);                               \
     c1_ext[pos] = ch1_sym[5 + (col)];                                                   \
     wr[pos] = 1;                                                                        \
+    colrx[pos] = (col);                                                                 \
     if ((pos) + 1 > *hw) *hw = (pos) + 1;                                               \
   } while (0)
   for (int prb = 0; prb < fp->N_RB_DL; prb++) {
@@ -327,6 +336,9 @@ static int extract_dual(const orc_frame_t *fp, const int32_t *rxF_sym, const int
         const int o = skip_half == 2 ? 6 : 0, n = skip_half ? 6 : 12;
         for (int i = 0; i < n; i++) PUT(p + i, b0 + o + i, col0 + o + i);
         p += n;
+        /* skip_half == 0 (:3929-3936): `for (i=0;i<12;i++) dl_ch0_ext+=12;` — the loop body was a
+         * printf, now commented out — then dl_ch1_ext += 12, rxF_ext += 12 */
+        if (!skip_half) drift += 132;
       } else if (skip_half == 1) {
         int j = 0;
         for (int i = 0; i < 6; i++)
@@ -364,7 +376,7 @@ static int extract_dual(const orc_frame_t *fp, const int32_t *rxF_sym, const int
   /* *hw = the written prefix (the skip_half = 2 pilot branch leaves holes that the reference fills
    * from earlier symbols' ext data: a stream reaching one is refused) */
   int n = 0;
-  while (n < *hw && wr[n]) n++;
+  while (n < *hw && wr[n] && colc0[n] == colrx[n]) n++;
   *hw = n;
   return p;
 }

@@ -705,3 +705,127 @@ def chest_time(fp, plane):
     a[:] = plane
     orc().orc_chest_time(ctypes.byref(fp), P(a), P(out))
     return out
+
+
+# ---- the reference's own rate matcher and Gold generator (oracle/_ref/libref_rm.so: PHY/CODING/
+#      lte_rate_matching.c, oracle/_ref/libref_gold.so: PHY/LTE_REFSIG/lte_gold.c, both compiled
+#      unmodified; present only in the build container) ----
+REF_RM_SO = os.path.join(ORACLE_DIR, "_ref", "libref_rm.so")
+REF_GOLD_SO = os.path.join(ORACLE_DIR, "_ref", "libref_gold.so")
+_refrm = None
+_refgold = None
+U8, U16, U32 = ctypes.c_uint8, ctypes.c_uint16, ctypes.c_uint32
+VP = ctypes.c_void_p
+
+
+def ref_rm():
+    """lte_rate_matching.c compiled unmodified, or None when it was not built here."""
+    global _refrm
+    if _refrm is None:
+        if not os.path.exists(REF_RM_SO):
+            return None
+        L = ctypes.CDLL(REF_RM_SO)
+        L.sub_block_interleaving_turbo.restype = U32
+        L.sub_block_interleaving_turbo.argtypes = [U32, VP, VP]
+        L.sub_block_deinterleaving_turbo.restype = None
+        L.sub_block_deinterleaving_turbo.argtypes = [U32, VP, VP]
+        L.generate_dummy_w.restype = U32
+        L.generate_dummy_w.argtypes = [U32, VP, U8]
+        L.lte_rate_matching_turbo.restype = U32
+        L.lte_rate_matching_turbo.argtypes = [U32, U32, VP, VP, U8, U32, U8, U8, U8, U8, U8, U8, U8, U8]
+        L.lte_rate_matching_turbo_rx.restype = ctypes.c_int
+        L.lte_rate_matching_turbo_rx.argtypes = [U32, U32, VP, VP, VP, U8, U32, U8, U8, U8, U8, U8, U8, U8,
+                                                 ctypes.POINTER(U32)]
+        L.sub_block_interleaving_cc.restype = U32
+        L.sub_block_interleaving_cc.argtypes = [U32, VP, VP]
+        L.lte_rate_matching_cc.restype = U32
+        L.lte_rate_matching_cc.argtypes = [U32, U16, VP, VP]
+        _refrm = L
+    return _refrm
+
+
+def ref_gold():
+    """lte_gold.c compiled unmodified (+ the ctypes glue ref_glue_gold.c), or None."""
+    global _refgold
+    if _refgold is None:
+        if not os.path.exists(REF_GOLD_SO):
+            return None
+        L = ctypes.CDLL(REF_GOLD_SO)
+        L.lte_gold_generic.restype = U32
+        L.lte_gold_generic.argtypes = [ctypes.POINTER(U32), ctypes.POINTER(U32), U8]
+        L.ref_glue_lte_gold.argtypes = [ctypes.c_int, U16, VP]
+        _refgold = L
+    return _refgold
+
+
+def _dbuf(d, D, prefix=96):
+    """d (3D stream entries, no prefix) behind a `prefix`-byte LTE_NULL prefix, as new_eNB_dlsch lays
+    out harq->d (dlsch_coding.c:202-206), with slack after it for the d[3D+2] side effect."""
+    buf = _aligned(prefix + 3 * D + 64, np.uint8)
+    buf[:] = 2
+    buf[prefix:prefix + len(d)] = d
+    return buf
+
+
+def ref_subblock(d, D):
+    """sub_block_interleaving_turbo on d (3D entries).  Returns (R, w, d buffer after the call)."""
+    buf = _dbuf(d, D)
+    R = (D + 31) >> 5
+    w = _aligned(3 * 32 * R + 64, np.uint8)
+    rtc = ref_rm().sub_block_interleaving_turbo(D, VP(buf.ctypes.data + 96), P(w))
+    return rtc, w[:3 * 32 * R].copy(), buf
+
+
+def ref_rate_match(RTC, G, w, C, r, Qm, rvidx=0, Nl=1, Kmimo=1, Mdlharq=8, Nsoft=1827072):
+    wa = _aligned(len(w) + 64, np.uint8)
+    wa[:len(w)] = w
+    e = _aligned(G + 64, np.uint8)
+    E = ref_rm().lte_rate_matching_turbo(RTC, G, P(wa), P(e), C, Nsoft, Mdlharq, Kmimo, rvidx, Qm, Nl, r, 0, 0)
+    return e[:E].copy()
+
+
+def ref_dummy_w(D, F=0):
+    R = (D + 31) >> 5
+    w = _aligned(3 * 32 * R + 64, np.uint8)
+    rtc = ref_rm().generate_dummy_w(D, P(w), F)
+    return rtc, w[:3 * 32 * R].copy()
+
+
+def ref_rate_match_rx(RTC, G, w, dummy_w, soft, C, r, Qm, rvidx=0, clear=1, Nl=1, Kmimo=1, Mdlharq=8,
+                      Nsoft=1827072):
+    """lte_rate_matching_turbo_rx: w (int16, modified copy returned), returns (ret, E, w)."""
+    wa = _aligned(len(w) + 32, np.int16)
+    wa[:len(w)] = w
+    dw = _aligned(len(dummy_w) + 64, np.uint8)
+    dw[:len(dummy_w)] = dummy_w
+    sa = _aligned(len(soft) + 32, np.int16)
+    sa[:len(soft)] = soft
+    E = U32()
+    ret = ref_rm().lte_rate_matching_turbo_rx(RTC, G, P(wa), P(dw), P(sa), C, Nsoft, Mdlharq, Kmimo, rvidx, clear,
+                                              Qm, Nl, r, ctypes.byref(E))
+    return ret, E.value, wa[:len(w)].copy()
+
+
+def ref_deinterleave(D, w, pad=96):
+    """sub_block_deinterleaving_turbo: writes d - 3 ND .. (the caller's d has room in front)."""
+    d = _aligned(pad + 3 * D + 64, np.int16)
+    wa = _aligned(len(w) + 32, np.int16)
+    wa[:len(w)] = w
+    ref_rm().sub_block_deinterleaving_turbo(D, VP(d.ctypes.data + 2 * pad), P(wa))
+    return d
+
+
+def ref_gold_words(c_init, n):
+    """n words of lte_gold_generic from c_init (reset on the first call, as dlsch_scrambling does)."""
+    L = ref_gold()
+    x1, x2 = U32(0), U32(c_init)
+    out = np.empty(n, np.uint32)
+    for i in range(n):
+        out[i] = L.lte_gold_generic(ctypes.byref(x1), ctypes.byref(x2), 1 if i == 0 else 0)
+    return out
+
+
+def ref_gold_table(Ncp, Nid_cell):
+    t = np.zeros((20, 2, 14), np.uint32)
+    ref_gold().ref_glue_lte_gold(Ncp, Nid_cell, P(t))
+    return t

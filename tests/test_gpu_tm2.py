@@ -10,7 +10,7 @@ import numpy as np
 import pytest
 
 import oracle_lib as O
-from test_rx_cpu import alloc, decode_tb
+from test_rx_cpu import alloc, decode_tb, dual_alloc
 from test_rx_tm2_cpu import qm_of, tm2_params
 
 pytestmark = pytest.mark.gpu
@@ -22,7 +22,7 @@ RAND = [(100, 2, 1, 7, 2, None), (50, 4, 2, 3, 2, None), (100, 6, 3, 1, 1, None)
 
 @pytest.mark.parametrize("N_RB,Qm,npd,sf,nb_rx,ra", RAND)
 def test_gpu_tm2_random_inputs(gpu, N_RB, Qm, npd, sf, nb_rx, ra):
-    ra = ra or alloc(N_RB)
+    ra = ra or dual_alloc(N_RB)
     fo = O.frame(N_RB, Nid_cell=N_RB + sf, nb_antennas_tx=2, mode1_flag=0)
     fg = gpu.frame_parms(N_RB, Nid_cell=N_RB + sf, nb_antennas_tx=2, mode1_flag=0)
     n = fo.symbols_per_tti * fo.ofdm_symbol_size
@@ -57,7 +57,7 @@ def test_gpu_tm2_receive_loop(gpu, N_RB, mcs, npd, sf, nb_rx):
     fep.upload(iq)
     fep.run()
     Qm = qm_of(mcs)
-    rx = gpu.RxBatchTM2(fg, alloc(N_RB), Qm, npd, p.rnti, n_sf, nb_rx=nb_rx, first_subframe=sf)
+    rx = gpu.RxBatchTM2(fg, dual_alloc(N_RB), Qm, npd, p.rnti, n_sf, nb_rx=nb_rx, first_subframe=sf)
     rx.estimate(fep.d_rxF, first_subframe=sf)
     rx.launch(fep.d_rxF, unscramble=1)
     llr = rx.llrs()

@@ -10,19 +10,20 @@ import numpy as np
 import pytest
 
 import oracle_lib as O
-from test_rx_cpu import alloc, decode_tb
+from test_rx_cpu import alloc, decode_tb, dual_alloc
 from test_rx_tm3_cpu import c3_params
 
 pytestmark = pytest.mark.gpu
 
 RAND = [(100, 6, 6, 19, 1, 7, 2, None), (50, 4, 2, 12, 2, 3, 2, None), (100, 6, 4, 22, 3, 0, 2, None),
-        (25, 6, 6, 19, 1, 5, 2, None), (25, 4, 4, 14, 2, 5, 1, None), (15, 6, 6, 20, 1, 5, 2, None),
+        (25, 6, 6, 19, 1, 6, 2, None), (25, 4, 4, 14, 2, 4, 1, None), (15, 6, 6, 20, 1, 3, 2, None),
+        (50, 6, 6, 19, 1, 5, 2, None),
         (100, 4, 6, 10, 2, 8, 1, [0xF0F0F0F0, 0x0000FFFF, 0, 0x3])]
 
 
 @pytest.mark.parametrize("N_RB,Qm0,Qm1,mcs,npd,sf,nb_rx,ra", RAND)
 def test_gpu_tm3_random_inputs(gpu, N_RB, Qm0, Qm1, mcs, npd, sf, nb_rx, ra):
-    ra = ra or alloc(N_RB)
+    ra = ra or dual_alloc(N_RB)
     fo = O.frame(N_RB, Nid_cell=N_RB + sf, nb_antennas_tx=2, mode1_flag=0)
     fg = gpu.frame_parms(N_RB, Nid_cell=N_RB + sf, nb_antennas_tx=2, mode1_flag=0)
     n = fo.symbols_per_tti * fo.ofdm_symbol_size
@@ -34,6 +35,23 @@ def test_gpu_tm3_random_inputs(gpu, N_RB, Qm0, Qm1, mcs, npd, sf, nb_rx, ra):
         lo, so = O.rx_pdsch_tm3(fo, rx, est, ra, Qm0, Qm1, mcs, npd, sf)
         lg, sg = gpu.rx_pdsch_tm3(fg, rx, est, ra, Qm0, Qm1, mcs, npd, sf)
         assert sg == so and np.array_equal(lg, lo), (scale, so, sg)
+
+
+@pytest.mark.parametrize("N_RB,sf", [(25, 7), (15, 3)])
+def test_gpu_dual_extraction_odd_full_allocation_refused(gpu, N_RB, sf):
+    """Odd N_RB_DL, every RB allocated: the reference's dl_ch0_ext moves 144 slots per full RB in
+    non-pilot symbols (dlsch_demodulation.c:3932-3936), so its port-0 estimates go stale from the
+    second full RB on — refused by the TM3 and TM2 drop-ins, as by the oracle."""
+    fg = gpu.frame_parms(N_RB, nb_antennas_tx=2, mode1_flag=0)
+    fo = O.frame(N_RB, nb_antennas_tx=2, mode1_flag=0)
+    n = fg.symbols_per_tti * fg.ofdm_symbol_size
+    z = np.ones(n, np.int32)
+    est = {(p, a): z for p in (0, 1) for a in (0, 1)}
+    with pytest.raises(gpu.OAI4GError):
+        gpu.rx_pdsch_tm3(fg, [z, z], est, alloc(N_RB), 6, 6, 19, 1, sf)
+    with pytest.raises(gpu.OAI4GError):
+        gpu.rx_pdsch_tm2(fg, [z, z], est, alloc(N_RB), 4, 1, sf)
+    assert O.rx_pdsch_tm2(fo, [z, z], est, alloc(N_RB), 4, 1, sf, check=False)[0] is None
 
 
 def test_gpu_tm3_refuses_holes(gpu):
@@ -63,7 +81,7 @@ def test_gpu_tm3_receive_loop(gpu, N_RB, mcs, npd, sf):
     fep.upload(iq)
     fep.run()
     Qm = 4 if mcs < 17 else 6
-    rx = gpu.RxBatchTM3(fg, alloc(N_RB), Qm, Qm, mcs, npd, p.rnti, n_sf, nb_rx=2, first_subframe=sf)
+    rx = gpu.RxBatchTM3(fg, dual_alloc(N_RB), Qm, Qm, mcs, npd, p.rnti, n_sf, nb_rx=2, first_subframe=sf)
     rx.estimate(fep.d_rxF, first_subframe=sf)
     rx.launch(fep.d_rxF, unscramble=1)
     llr = rx.llrs()
@@ -96,7 +114,7 @@ QQ_RAND = [(100, 9, 1, 7, 2, None), (50, 5, 2, 3, 1, None), (25, 7, 1, 6, 2, Non
 def test_gpu_tm3_qpsk_two_codewords_random_inputs(gpu, N_RB, mcs, npd, sf, nb_rx, ra):
     """Both codewords QPSK: the dual-stream correlation and the interference-aware qpsk_qpsk LLRs of
     both streams, bit-exact against the oracle on full-range random grids and estimates."""
-    ra = ra or alloc(N_RB)
+    ra = ra or dual_alloc(N_RB)
     fo = O.frame(N_RB, Nid_cell=N_RB + sf, nb_antennas_tx=2, mode1_flag=0)
     fg = gpu.frame_parms(N_RB, Nid_cell=N_RB + sf, nb_antennas_tx=2, mode1_flag=0)
     n = fo.symbols_per_tti * fo.ofdm_symbol_size
@@ -132,7 +150,7 @@ def test_gpu_tm3_qpsk_receive_loop_both_codewords(gpu, N_RB, mcs, npd, sf, nb_rx
     fep = gpu.FepBatch(fg, n_tx, nb_rx)
     fep.upload(iq)
     fep.run()
-    rx = gpu.RxBatchTM3(fg, alloc(N_RB), 2, 2, mcs, npd, p.rnti, n_sf, nb_rx=nb_rx, first_subframe=sf)
+    rx = gpu.RxBatchTM3(fg, dual_alloc(N_RB), 2, 2, mcs, npd, p.rnti, n_sf, nb_rx=nb_rx, first_subframe=sf)
     rx.estimate(fep.d_rxF, first_subframe=sf)
     rx.launch_2cw(fep.d_rxF, unscramble=1)
     l0, l1 = rx.llrs(), rx.llrs1()
@@ -167,7 +185,7 @@ def test_gpu_tm3_qpsk_codeword0_random_inputs(gpu, N_RB, Qm1, mcs, npd, sf, nb_r
     """Codeword 0 QPSK through the drop-in rx_pdsch_tm3: qpsk_qam16 / qpsk_qam64 against a 16 / 64-QAM
     codeword 1 (interferer magnitude dl_ch_mag1 of antenna 0), qpsk_qpsk's codeword 0 when both are
     QPSK; bit-exact against the oracle on full-range random grids and estimates."""
-    ra = ra or alloc(N_RB)
+    ra = ra or dual_alloc(N_RB)
     fo = O.frame(N_RB, Nid_cell=N_RB + sf, nb_antennas_tx=2, mode1_flag=0)
     fg = gpu.frame_parms(N_RB, Nid_cell=N_RB + sf, nb_antennas_tx=2, mode1_flag=0)
     n = fo.symbols_per_tti * fo.ofdm_symbol_size
@@ -207,7 +225,7 @@ def test_gpu_tm3_qpsk_with_qam_interferer_receive_loop(gpu, N_RB, mcs0, mcs1, np
     fep.upload(iq)
     fep.run()
     Qm1 = 4 if mcs1 < 17 else 6
-    rx = gpu.RxBatchTM3(fg, alloc(N_RB), 2, Qm1, mcs0, npd, p.rnti, n_sf, nb_rx=2, first_subframe=sf)
+    rx = gpu.RxBatchTM3(fg, dual_alloc(N_RB), 2, Qm1, mcs0, npd, p.rnti, n_sf, nb_rx=2, first_subframe=sf)
     rx.estimate(fep.d_rxF, first_subframe=sf)
     rx.launch(fep.d_rxF, unscramble=1)
     llr = rx.llrs()
@@ -248,7 +266,7 @@ def test_gpu_tm3_from_pilot_rows_equals_estimate_planes(gpu, N_RB, Qm0, Qm1, mcs
         L = gpu.lib()
         d = L.oai4g_dev_alloc(rxF.nbytes)
         assert d and L.oai4g_memcpy_h2d(d, rxF.ctypes.data, rxF.nbytes) == 0
-        rx = gpu.RxBatchTM3(fg, alloc(N_RB), Qm0, Qm1, mcs, npd, 0x1234, n_sf, nb_rx=nb_rx, first_subframe=sf)
+        rx = gpu.RxBatchTM3(fg, dual_alloc(N_RB), Qm0, Qm1, mcs, npd, 0x1234, n_sf, nb_rx=nb_rx, first_subframe=sf)
         two = Qm0 == 2 and Qm1 == 2
         rx.estimate(d, first_subframe=sf)
         rx.launch_2cw(d) if two else rx.launch(d)

@@ -21,6 +21,24 @@ def alloc(N_RB):
     return [((1 << min(32, max(0, N_RB - 32 * i))) - 1) & 0xFFFFFFFF for i in range(4)]
 
 
+def dual_alloc(N_RB, dc=True):
+    """The allocation the two-port (TM2 / TM3) tests use: every RB for even N_RB_DL; for odd N_RB_DL
+    the RB around DC and the one after it (dc = False: the one after it alone — the receive loops,
+    since the dual extraction reads the DC RB's upper half from bins 0..5, :4003-4007, which no
+    transmitter fills: a two-RB codeword does not survive that).  dlsch_extract_rbs_dual's odd full-RB non-pilot branch
+    moves dl_ch0_ext 144 slots per RB (dlsch_demodulation.c:3932-3936), so from the second full RB
+    on the port-0 estimates of a symbol are stale (the reference also writes past its buffer);
+    only allocations whose full RBs end the symbol stay defined, the others are refused."""
+    if N_RB % 2 == 0:
+        return alloc(N_RB)
+    half = N_RB >> 1
+    return [((1 << half) if dc else 0) | (1 << (half + 1)), 0, 0, 0]
+
+
+def n_alloc(ra):
+    return sum(bin(x).count("1") for x in ra)
+
+
 def params(name, N_RB, mcs, npdcch, sf, **kw):
     return oai.make_params(name, subframe=sf, N_RB_DL=N_RB, nb_rb=N_RB, rb_alloc=alloc(N_RB), mcs=[mcs], TBS=None,
                            num_pdcch_symbols=npdcch, with_crs=1, **kw)

@@ -10,12 +10,13 @@ import numpy as np
 import pytest
 
 import oracle_lib as O
-from test_rx_cpu import alloc, decode_tb
+from test_rx_cpu import alloc, decode_tb, dual_alloc, n_alloc
 
 
 def tm2_params(N_RB, mcs, npdcch, sf, Nid=0):
     import openair4g_amd as oai
-    return oai.make_params("TM2", subframe=sf, N_RB_DL=N_RB, nb_rb=N_RB, rb_alloc=alloc(N_RB), mcs=[mcs, 0], TBS=None,
+    ra = dual_alloc(N_RB, dc=False)
+    return oai.make_params("TM2", subframe=sf, N_RB_DL=N_RB, nb_rb=n_alloc(ra), rb_alloc=ra, mcs=[mcs, 0], TBS=None,
                            num_pdcch_symbols=npdcch, with_crs=1, Nid_cell=Nid)
 
 
@@ -62,8 +63,8 @@ def test_tm2_loop_decodes(N_RB, mcs, npdcch, sf, nb_rx):
     H = [[1, 0], [0, 1]] if nb_rx == 2 else [[1, 1]]
     fp, rxF, est = tm2_loop(p, sf, pays, H, nb_rx)
     Qm = qm_of(mcs)
-    llr, sh = O.rx_pdsch_tm2(fp, rxF[:nb_rx], est, alloc(N_RB), Qm, npdcch, sf)
-    G = O.get_G(N_RB, 0, 0, 0, N_RB, alloc(N_RB), Qm, 1, npdcch, sf)
+    llr, sh = O.rx_pdsch_tm2(fp, rxF[:nb_rx], est, dual_alloc(N_RB, dc=False), Qm, npdcch, sf)
+    G = O.get_G(N_RB, 0, 0, 0, n_alloc(dual_alloc(N_RB, dc=False)), dual_alloc(N_RB, dc=False), Qm, 1, npdcch, sf)
     assert len(llr) == Qm * (G // Qm) and len(llr) == G
     u = np.zeros(32 * (1 + G // 32), np.int16)
     u[:G] = llr

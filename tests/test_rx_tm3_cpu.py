@@ -12,12 +12,13 @@ import numpy as np
 import pytest
 
 import oracle_lib as O
-from test_rx_cpu import alloc, decode_tb
+from test_rx_cpu import alloc, decode_tb, dual_alloc, n_alloc
 
 
 def c3_params(N_RB, mcs, npdcch, sf, Nid=0):
     import openair4g_amd as oai
-    return oai.make_params("C3", subframe=sf, N_RB_DL=N_RB, nb_rb=N_RB, rb_alloc=alloc(N_RB), mcs=[mcs, mcs], TBS=None,
+    ra = dual_alloc(N_RB, dc=False)
+    return oai.make_params("C3", subframe=sf, N_RB_DL=N_RB, nb_rb=n_alloc(ra), rb_alloc=ra, mcs=[mcs, mcs], TBS=None,
                            num_pdcch_symbols=npdcch, with_crs=1, Nid_cell=Nid)
 
 
@@ -63,8 +64,8 @@ def test_tm3_loop_decodes_codeword0(N_RB, mcs, npdcch, sf, nb_rx):
     H = [[1, 0], [0, 1]] if nb_rx == 2 else [[1, 1]]
     fp, rxF, est = tm3_loop(p, sf, pays, H, nb_rx)
     Qm = 4 if mcs < 17 else 6
-    llr, sh = O.rx_pdsch_tm3(fp, rxF[:nb_rx], est, alloc(N_RB), Qm, Qm, mcs, npdcch, sf)
-    G = O.get_G(N_RB, 0, 0, 0, N_RB, alloc(N_RB), Qm, 1, npdcch, sf)
+    llr, sh = O.rx_pdsch_tm3(fp, rxF[:nb_rx], est, dual_alloc(N_RB, dc=False), Qm, Qm, mcs, npdcch, sf)
+    G = O.get_G(N_RB, 0, 0, 0, n_alloc(dual_alloc(N_RB, dc=False)), dual_alloc(N_RB, dc=False), Qm, 1, npdcch, sf)
     assert len(llr) == G
     u = np.zeros(32 * (1 + G // 32), np.int16)
     u[:G] = llr
@@ -105,8 +106,8 @@ def test_tm3_qpsk_loop_decodes_both_codewords(N_RB, mcs, npdcch, sf, nb_rx):
     pays = [[rng.integers(0, 256, p.payload_stride, dtype=np.uint8) for _ in range(2)] for _ in range(2)]
     H = [[2, 1], [1, 2]][:nb_rx]
     fp, rxF, est = tm3_loop(p, sf, pays, H, nb_rx)
-    l0, l1, sh = O.rx_pdsch_tm3_qq(fp, rxF[:nb_rx], est, alloc(N_RB), mcs, npdcch, sf)
-    G = O.get_G(N_RB, 0, 0, 0, N_RB, alloc(N_RB), 2, 1, npdcch, sf)
+    l0, l1, sh = O.rx_pdsch_tm3_qq(fp, rxF[:nb_rx], est, dual_alloc(N_RB, dc=False), mcs, npdcch, sf)
+    G = O.get_G(N_RB, 0, 0, 0, n_alloc(dual_alloc(N_RB, dc=False)), dual_alloc(N_RB, dc=False), 2, 1, npdcch, sf)
     assert len(l0) == G and len(l1) == G
     for cw, llr in enumerate((l0, l1)):
         u = np.zeros(32 * (1 + G // 32), np.int16)
@@ -125,15 +126,16 @@ QX = [(50, 9, 16, 1, 7), (50, 9, 22, 1, 7), (25, 5, 12, 2, 3), (100, 7, 19, 1, 8
 @pytest.mark.parametrize("N_RB,mcs0,mcs1,npdcch,sf", QX)
 def test_tm3_qpsk_with_qam_interferer_decodes_codeword0(N_RB, mcs0, mcs1, npdcch, sf):
     import openair4g_amd as oai
-    p = oai.make_params("C3", subframe=sf, N_RB_DL=N_RB, nb_rb=N_RB, rb_alloc=alloc(N_RB), mcs=[mcs0, mcs1], TBS=None,
+    ra = dual_alloc(N_RB, dc=False)
+    p = oai.make_params("C3", subframe=sf, N_RB_DL=N_RB, nb_rb=n_alloc(ra), rb_alloc=ra, mcs=[mcs0, mcs1], TBS=None,
                         num_pdcch_symbols=npdcch, with_crs=1, Nid_cell=0)
     rng = np.random.default_rng(N_RB + mcs0 + mcs1)
     pays = [[rng.integers(0, 256, p.payload_stride, dtype=np.uint8) for _ in range(2)] for _ in range(2)]
     Qm1 = 4 if mcs1 < 17 else 6
     for H in ([[1, 0], [0, 1]], [[2, 1], [1, 2]]):
         fp, rxF, est = tm3_loop(p, sf, pays, H, 2)
-        llr, sh = O.rx_pdsch_tm3(fp, rxF, est, alloc(N_RB), 2, Qm1, mcs0, npdcch, sf)
-        G = O.get_G(N_RB, 0, 0, 0, N_RB, alloc(N_RB), 2, 1, npdcch, sf)
+        llr, sh = O.rx_pdsch_tm3(fp, rxF, est, ra, 2, Qm1, mcs0, npdcch, sf)
+        G = O.get_G(N_RB, 0, 0, 0, n_alloc(dual_alloc(N_RB, dc=False)), dual_alloc(N_RB, dc=False), 2, 1, npdcch, sf)
         assert len(llr) == G
         u = np.zeros(32 * (1 + G // 32), np.int16)
         u[:G] = llr
@@ -141,3 +143,26 @@ def test_tm3_qpsk_with_qam_interferer_decodes_codeword0(N_RB, mcs0, mcs1, npdcch
         res, tb = decode_tb(u[:G], G, p.TBS[0], 2)
         assert all(it <= 4 for it, _ in res), (H, [it for it, _ in res])
         assert np.array_equal(tb, pays[0][0][:p.TBS[0] // 8]), H
+
+
+@pytest.mark.parametrize("N_RB", [15, 25])
+def test_tm3_odd_nrb_full_allocation_refused(N_RB):
+    """Odd N_RB_DL, every RB allocated: from the second full RB of a non-pilot symbol on, the
+    reference's dl_ch0_ext has moved 144 slots per RB (dlsch_demodulation.c:3932-3936) and the
+    port-0 estimates it reads are stale, so the oracle refuses (as the library does)."""
+    fp = O.frame(N_RB, nb_antennas_tx=2, mode1_flag=0)
+    N = fp.ofdm_symbol_size
+    rng = np.random.default_rng(N_RB)
+    rx = [rng.integers(-3000, 3000, 14 * N).astype(np.int32) for _ in range(2)]
+    est = {(pp, a): rng.integers(-3000, 3000, 14 * N).astype(np.int32) for pp in (0, 1) for a in (0, 1)}
+    import ctypes
+    out = np.zeros(14 * 1200 * 6 + 64, dtype=np.int16)
+    rp = (ctypes.c_void_p * 2)(*[r.ctypes.data for r in rx])
+    ep = (ctypes.c_void_p * 4)(*[est[(p_, a)].ctypes.data for p_ in (0, 1) for a in (0, 1)])
+    sh = ctypes.c_uint8()
+    ra = (ctypes.c_uint32 * 4)(*alloc(N_RB))
+    for sf in (3, 7):
+        assert O.orc().orc_rx_pdsch_tm3(ctypes.byref(fp), 2, rp, ep, ra, 6, 6, 19, 1, sf, O.P(out), ctypes.byref(sh)) < 0
+    # the DC RB and the next one stay defined
+    llr, _ = O.rx_pdsch_tm3(fp, rx, est, dual_alloc(N_RB), 6, 6, 19, 1, 7)
+    assert len(llr) > 0

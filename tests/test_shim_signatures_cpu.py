@@ -3,7 +3,7 @@ own name with the reference's own parameter types, so a dlsim linked with it res
 to the GPU binding with no other change.  Checked here against the prototypes in the reference's
 headers (PHY/**/*.h, or the defining .c file when no header declares it; read as text, when the
 reference tree is present): the
-return type and every parameter type, after normalising whitespace, parameter names and the
+return type (exactly) and every parameter type, after normalising whitespace, parameter names and the
 `const` the reference omits.  (The shim's bodies need the asn1c-generated headers to compile, so
 this is the check of the boundary that runs here; test_integration_cpu.py checks the oai4g_ side.)"""
 import glob
@@ -19,7 +19,8 @@ SHIM = os.path.join(ROOT, "integration", "oai4g_shim.c")
 # other spellings of the same types (module_id_t: openair2/COMMON/platform_types.h:70; the header
 # declares lte_dl_channel_estimation's eNB_id as module_id_t, its definition as uint8_t)
 TYPE_ALIASES = {"module_id_t": "uint8_t", "short": "int16_t", "unsigned short": "uint16_t", "unsigned char": "uint8_t", "int": "int32_t",
-                "unsigned int": "uint32_t", "signed char": "int8_t", "char": "int8_t"}
+                "unsigned int": "uint32_t", "signed char": "int8_t"}
+# plain `char` is a distinct C type (neither int8_t nor uint8_t): it is deliberately not aliased
 
 
 def _strip(s):
@@ -101,6 +102,17 @@ def test_shim_signatures_equal_reference_prototypes():
     bad = []
     for name, (ret, params) in shim.items():
         rret, rparams, where = ref[name]
-        if params != rparams or (ret != rret and not (ret.startswith("int") and rret.startswith("int"))):
+        if params != rparams or ret != rret:
             bad.append((name, where, (ret, params), (rret, rparams)))
     assert not bad, "\n".join(map(str, bad))
+
+
+def test_normaliser_keeps_distinct_types_distinct():
+    """The comparison would catch the prototype mismatches a lenient check lets through."""
+    assert _norm_type("char *") != _norm_type("int8_t *")
+    assert _norm_type("char") != _norm_type("uint8_t")
+    assert _norm_type("int") != _norm_type("uint32_t")
+    assert _norm_type("int32_t") != _norm_type("int16_t")
+    assert _norm_type("unsigned char") == _norm_type("uint8_t")
+    assert _norm_type("const short *") == _norm_type("int16_t*")
+    assert _params("uint8_t *a, int b[2], LTE_DL_FRAME_PARMS *fp") == ["uint8_t*", "int32_t*", "LTE_DL_FRAME_PARMS*"]
