@@ -888,7 +888,8 @@ def bench_tx(args, world, rank, host):
     from openair4g_amd import dist as odist
     dist = host.dist
     if not host.stub:
-        oai.lib().oai4g_set_device(host.local_rank)
+        if oai.lib().oai4g_set_device(host.local_rank) != 0:
+            raise oai.OAI4GError(oai.lib().oai4g_last_error().decode())
         oai.init()
     # ---- parameter block: built on rank 0, broadcast over RCCL (the only collective): the C ABI's
     # oai4g_dist_broadcast_params on the GPU, torch.distributed (gloo) under --cpu-stub ----

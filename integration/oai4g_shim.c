@@ -315,22 +315,22 @@ int rx_pdsch(PHY_VARS_UE *ue, PDSCH_t type, unsigned char eNB_id, unsigned char 
       est[2 + a] = (const int32_t *)ue->lte_ue_common_vars.dl_ch_estimates[eNB_id][2 + a];
     }
     if (tm2) {
-      n = oai4g_rx_pdsch_tm2(&fp, f->nb_antennas_rx, rxF, est, h->rb_alloc_even, get_Qm(h->mcs), npdcch, subframe,
+      n = oai4g_rx_pdsch_tm2(&fp, f->nb_antennas_rx, rxF, est, h->rb_alloc_even, h->Qm, npdcch, subframe,
                              ue->lte_ue_pdsch_vars[eNB_id]->llr[0], &log2_maxh);
     } else {
       LTE_DL_UE_HARQ_t *h1 = ue->dlsch_ue[eNB_id][1]->harq_processes[harq_pid];
-      if (get_Qm(h->mcs) == 2 && get_Qm(h1->mcs) == 2)   /* both QPSK: dlsch_qpsk_qpsk_llr fills llr[0] and llr[1] */
+      if (h->Qm == 2 && h1->Qm == 2)   /* both QPSK: dlsch_qpsk_qpsk_llr fills llr[0] and llr[1] */
         n = oai4g_rx_pdsch_tm3_2cw(&fp, f->nb_antennas_rx, rxF, est, h->rb_alloc_even, h->mcs, npdcch, subframe,
                                    ue->lte_ue_pdsch_vars[eNB_id]->llr[0], ue->lte_ue_pdsch_vars[eNB_id]->llr[1],
                                    &log2_maxh);
       else
-        n = oai4g_rx_pdsch_tm3(&fp, f->nb_antennas_rx, rxF, est, h->rb_alloc_even, get_Qm(h->mcs), get_Qm(h1->mcs),
+        n = oai4g_rx_pdsch_tm3(&fp, f->nb_antennas_rx, rxF, est, h->rb_alloc_even, h->Qm, h1->Qm,
                                h->mcs, npdcch, subframe, ue->lte_ue_pdsch_vars[eNB_id]->llr[0], &log2_maxh);
     }
   } else {
     n = oai4g_rx_pdsch_siso(&fp, (const int32_t *)ue->lte_ue_common_vars.rxdataF[0],
                             (const int32_t *)ue->lte_ue_common_vars.dl_ch_estimates[eNB_id][0], h->rb_alloc_even,
-                            get_Qm(h->mcs), npdcch, subframe, ue->lte_ue_pdsch_vars[eNB_id]->llr[0], &log2_maxh);
+                            h->Qm, npdcch, subframe, ue->lte_ue_pdsch_vars[eNB_id]->llr[0], &log2_maxh);
   }
   if (n < 0) return -1;
   ue->lte_ue_pdsch_vars[eNB_id]->log2_maxh = log2_maxh;

@@ -81,14 +81,21 @@ extern "C" int oai4g_dist_init(int rank, int world, const uint8_t id[OAI4G_DIST_
 {
   if (world < 1 || rank < 0 || rank >= world) { oai4g_set_error("dist_init: rank %d of world %d", rank, world); return -1; }
   if (g_dist.comm) { oai4g_set_error("dist_init: already initialised"); return -1; }
-  if (oai4g_init() != 0) return -1;                  /* the rank's device: oai4g_set_device before */
+  if (oai4g_init() != 0 || oai4g_bind_thread() != 0) return -1;   /* the rank's device: oai4g_set_device before */
   ncclUniqueId u;
   memcpy(&u, id, sizeof(u));
   if (hipStreamCreateWithFlags(&g_dist.s, hipStreamNonBlocking) != hipSuccess) {
     oai4g_set_error("dist_init: stream creation failed");
     return -1;
   }
-  NCK(ncclCommInitRank(&g_dist.comm, world, u, rank), "dist_init (ncclCommInitRank)");
+  ncclResult_t r = ncclCommInitRank(&g_dist.comm, world, u, rank);
+  if (r != ncclSuccess) {                              /* leave g_dist as before: a retry starts clean */
+    oai4g_set_error("dist_init (ncclCommInitRank): %s", ncclGetErrorString(r));
+    hipStreamDestroy(g_dist.s);
+    g_dist.s = nullptr;
+    g_dist.comm = nullptr;
+    return -1;
+  }
   g_dist.rank = rank;
   g_dist.world = world;
   return 0;

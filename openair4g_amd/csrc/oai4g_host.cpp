@@ -145,6 +145,7 @@ static uint32_t crs_qpsk(int16_t amp, uint32_t idx)
 }
 
 static bool g_init_done = false;
+static int g_device = 0;                           /* the device the tables live on (do_init) */
 static void do_init(void)
 {
   g_init_done = true;
@@ -158,6 +159,7 @@ static void do_init(void)
   }
   int dev = 0;
   hipGetDevice(&dev);
+  g_device = dev;                                  /* every later thread binds to this device */
   hipDeviceProp_t prop;
   if (hipGetDeviceProperties(&prop, dev) != hipSuccess || strncmp(prop.gcnArchName, "gfx950", 6) != 0) {
     snprintf(g_init_err, sizeof(g_init_err), "device %d is not gfx950 (%s)", dev, prop.gcnArchName);
@@ -229,14 +231,31 @@ extern "C" int oai4g_set_device(int device)
     set_err("set_device: device %d of %d", device, n);
     return -1;
   }
-  int cur = -1;
-  if (g_init_done && (hipGetDevice(&cur) != hipSuccess || cur != device)) {
-    set_err("set_device: the library is already initialised on device %d", cur);
+  if (g_init_done && g_device != device) {
+    set_err("set_device: the library is already initialised on device %d", g_device);
     return -1;
   }
   HCK(hipSetDevice(device), -1);
   return 0;
 }
+
+/* hipSetDevice is per thread: a thread that calls in after another initialised the library binds
+ * itself to the library's device before it creates streams, buffers or launches (the device tables
+ * live there).  Called by NEED_INIT. */
+static thread_local bool t_bound = false;
+static int bind_thread_device(void)
+{
+  if (t_bound) return 0;
+  int cur = -1;
+  if (hipGetDevice(&cur) != hipSuccess) return -1;
+  if (cur != g_device && hipSetDevice(g_device) != hipSuccess) {
+    set_err("thread bind: hipSetDevice(%d) failed", g_device);
+    return -1;
+  }
+  t_bound = true;
+  return 0;
+}
+int oai4g_bind_thread(void) { return bind_thread_device(); }
 
 extern "C" int oai4g_init(void)
 {
@@ -285,9 +304,9 @@ static uint8_t *scratch(size_t bytes)
   return g_scr.buf;
 }
 
-#define NEED_INIT(ret)                    \
-  do {                                    \
-    if (oai4g_init() != 0) return ret;    \
+#define NEED_INIT(ret)                                          \
+  do {                                                          \
+    if (oai4g_init() != 0 || bind_thread_device() != 0) return ret; \
   } while (0)
 
 /* ------------------------------------------------------------------------------------------

@@ -357,6 +357,8 @@ struct chest_dev_t {
   uint32_t gold[20][2][14];       /* lte_gold_table */
 };
 void oai4g_set_error(const char *fmt, ...);
+/* binds the calling thread to the device the library was initialised on (hipSetDevice is per thread) */
+int oai4g_bind_thread(void);
 hipError_t oai4g_launch_signal_energy(const int32_t *d_x, int n, size_t stride, uint32_t length, int32_t *d_out,
                                       hipStream_t s);
 hipError_t oai4g_launch_awgn(const int32_t *d_tx, size_t tx_stride, uint32_t tx_len, const int32_t *d_tail,

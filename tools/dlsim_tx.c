@@ -205,9 +205,19 @@ int main(int argc, char **argv)
       pids[r] = fork();
       CHECK(pids[r] >= 0, "fork");
       if (pids[r] == 0) {
+        /* keep only this rank's end of the id pipes: a rank 0 that fails before writing the id
+         * then closes the last write end, and the other ranks read EOF and exit non-zero */
         rank = r;
+        for (int q = 1; q < world; q++) {
+          if (r != 0) close(fds[q][1]);
+          if (q != r) close(fds[q][0]);
+        }
         goto rank_main;
       }
+    }
+    for (int q = 1; q < world; q++) {
+      close(fds[q][0]);
+      close(fds[q][1]);
     }
     int rc_all = 0;
     for (int r = 0; r < world; r++) {
