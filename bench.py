@@ -125,33 +125,61 @@ def _port_rate(name, subframe, seconds, procs, full=False):
     return tot, n_all
 
 
+def _harness_args(p, seconds, seed):
+    """argv of oracle/cpu_baseline for an openair4g_amd.TxParams (same configuration)."""
+    return [os.path.join(ROOT, "oracle", "cpu_baseline"), f"{seconds}", str(seed), str(p.N_RB_DL),
+            str(p.nb_antennas_tx), str(p.mode1_flag), str(p.n_cw), str(p.mimo_mode), str(p.num_pdcch_symbols),
+            str(p.first_subframe), str(p.Kmimo), str(p.mcs[0]), str(p.mcs[1] if p.n_cw > 1 else 0), str(p.TBS[0]),
+            str(p.TBS[1] if p.n_cw > 1 else 0)] + [hex(p.rb_alloc[i]) for i in range(4)] + [str(p.nb_rb),
+                                                                                          str(p.rnti)]
+
+
+def _harness_rate(p, seconds, procs):
+    """oracle/cpu_baseline in `procs` independent processes: (aggregate subframes/s, subframes, the
+    per-process JSON lines)."""
+    import subprocess
+    ps = [subprocess.Popen(_harness_args(p, seconds, 0x5EED + i), stdout=subprocess.PIPE, text=True)
+          for i in range(procs)]
+    outs = []
+    for q in ps:
+        out, _ = q.communicate()
+        if q.returncode != 0:
+            raise RuntimeError(f"oracle/cpu_baseline failed ({q.returncode})")
+        outs.append(json.loads(out))
+    return sum(o["rate"] for o in outs), sum(o["subframes"] for o in outs), outs
+
+
 def cpu_baseline(name, seconds, subframe, full=False):
-    """The oracle ("port") on the host cores over a bounded sample of the same workload: one core,
-    then every core of this process's share (independent processes, as N dlsim instances would
-    run), plus the reference-equivalent rate through BASELINE.md section 3's calibration
-    (profiles/cpu_calibration.json: the reference TUs' 870 subframes/s/core measured by the survey
-    in the build container vs the port's rate measured in the same container)."""
-    one, n1 = _port_rate(name, subframe, seconds, 1, full)
+    """The CPU transmit path on the host cores over a bounded sample of the same workload, one core
+    and then every core of this process's share (independent processes, as N dlsim instances would
+    run).  PDSCH configurations run oracle/cpu_baseline: the reference's own crc24a,
+    sub_block_interleaving_turbo, lte_rate_matching_turbo, lte_gold_generic and idft2048 compiled
+    unmodified (oracle/_ref), the oracle's restatement for the stages whose reference TU does not
+    build here (segmentation, turbo encoder, the scrambling loop, modulation, the CP copy); its
+    first subframe is checked bit-exactly against the oracle's whole chain.  The rate is over the
+    stages' summed time, as dlsim's phy_proc_tx timer covers them (DCI / pilots excluded).
+    --full-grid keeps the oracle port over subframes 0..9 with CRS + PCFICH/PDCCH."""
+    import openair4g_amd as oai
     cores = host_cores()
-    allc, nall = _port_rate(name, subframe, max(2.0, seconds / 2), cores, full) if cores > 1 else (one, n1)
-    cal = None
-    try:
-        cal = json.load(open(os.path.join(ROOT, "profiles", "cpu_calibration.json"))).get(name)
-    except Exception:
-        pass
-    out = {"value": one, "unit": "subframes/s", "cores": 1, "kind": "port", "cpu_model": cpu_model(),
-           "value_all_cores": allc, "cores_all": cores,
-           "sample": f"{n1} subframes of {name} "
-                     + ("(subframes 0..9 with CRS + PCFICH/PDCCH; the common signals, < 1 % of the REs, not in the "
-                        "CPU sample)" if full else f"(sf {subframe})")
-                     + f" through the C oracle on 1 core in {seconds:.0f} s; "
-                     f"{nall} on {cores} cores (independent processes)"}
-    if cal and not full:
-        r = cal["ref_per_core"] / cal["port_per_core"]
-        out["ref_equiv_per_core"] = one * r
-        out["ref_equiv_all_cores"] = allc * r
-        out["calibration"] = cal
-    return out
+    if full:
+        one, n1 = _port_rate(name, subframe, seconds, 1, full)
+        allc, nall = _port_rate(name, subframe, max(2.0, seconds / 2), cores, full) if cores > 1 else (one, n1)
+        return {"value": one, "unit": "subframes/s", "cores": 1, "kind": "port", "cpu_model": cpu_model(),
+                "value_all_cores": allc, "cores_all": cores,
+                "sample": f"{n1} subframes of {name} (subframes 0..9 with CRS + PCFICH/PDCCH; the common signals, "
+                          f"< 1 % of the REs, not in the CPU sample) through the C oracle on 1 core in {seconds:.0f} s; "
+                          f"{nall} on {cores} cores (independent processes)"}
+    p = oai.make_params(name, subframe=subframe)
+    one, n1, o1 = _harness_rate(p, seconds, 1)
+    allc, nall, _ = _harness_rate(p, max(2.0, seconds / 2), cores) if cores > 1 else (one, n1, o1)
+    kinds = set(o1[0]["impl"].values())
+    return {"value": one, "unit": "subframes/s", "cores": 1,
+            "kind": "reference+port" if any(k != "port" for k in kinds) else "port",
+            "cpu_model": cpu_model(), "value_all_cores": allc, "cores_all": cores,
+            "stage_us_per_subframe": o1[0]["stage_us"], "stage_impl": o1[0]["impl"],
+            "sample": f"{n1} {name} subframes (sf {subframe}) on 1 core in {seconds:.0f} s, {nall} on {cores} cores "
+                      f"(independent processes); oracle/cpu_baseline: reference TUs where they build, port "
+                      f"elsewhere (stage_impl); first subframe bit-exact vs the oracle chain"}
 
 
 C5_K, C5_CB = 5504, 8          # UL 100 PRB MCS 20: TBS 43816 -> C = 8 blocks of K = 5504 (SURVEY 8d)
@@ -884,6 +912,7 @@ def full_grid_setup(pipe, params, name):
 
 def bench_tx(args, world, rank, host):
     """Transmit path (C1-C4): a step = one pass of encode + modulate/IDFT/CP over the batch."""
+    import numpy as np
     import openair4g_amd as oai
     from openair4g_amd import dist as odist
     dist = host.dist
@@ -930,11 +959,11 @@ def bench_tx(args, world, rank, host):
 
     # per-kernel launch durations for the roofline: the same batch run serially, HIP events on the
     # launch stream around each kernel (outside the timed region)
-    kern = [0.0, 0.0]
+    kern = [[], []]
     for _ in range(args.kernel_reps):
         a, b = pipe.run_timed()
-        kern[0] += a
-        kern[1] += b
+        kern[0].append(a)
+        kern[1].append(b)
     elapsed = host.max_over_ranks(elapsed)
     units = host.sum_over_ranks(args.batch * args.steps)      # subframes all ranks processed
 
@@ -945,16 +974,20 @@ def bench_tx(args, world, rank, host):
     sfs = range(10) if args.full_grid else [args.subframe]
     G = [sum(pipe.G(cw, sf) for sf in sfs) / len(sfs) for cw in range(params.n_cw)]      # mean over the batch
     ebits_b = sum((g + 7) / 8 for g in G)
-    enc_ms = kern[0] / args.kernel_reps
-    mod_ms = kern[1] / args.kernel_reps
-    per_kernel = {
+    enc_ms = float(np.median(kern[0]))
+    mod_ms = float(np.median(kern[1]))
+    per_kernel = {            # bytes = the kernel's own boundary (payload -> e words -> IQ), a diagnostic
         "encode_rm_scramble": {"ms": enc_ms, "bytes": args.batch * (payload_b + ebits_b)},
         "modulate_idft_cp": {"ms": mod_ms, "bytes": args.batch * (ebits_b + iq_b)},
     }
     dom = max(per_kernel, key=lambda k: per_kernel[k]["ms"])
-    ach = per_kernel[dom]["bytes"] / (per_kernel[dom]["ms"] * 1e-3) / 1e9
+    # roofline.achieved: SURVEY 8(d)'s algorithmic bytes per subframe (payload read + IQ written)
+    # x the subframes one launch processes, over the dominant kernel's launch time (HIP events)
+    alg_launch = args.batch * (payload_b + iq_b)
+    ach = alg_launch / (per_kernel[dom]["ms"] * 1e-3) / 1e9
     ptag = args.config + ("_full" if args.full_grid else "")     # profiles/traffic_<tag>.json
     traffic = _traffic(ptag, dom, args.batch)
+    prof_ms = _traffic(ptag + "_ms", dom, args.batch)           # rocprofv3 average of the same command
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
@@ -990,9 +1023,18 @@ def bench_tx(args, world, rank, host):
                        "parallelism": f"subframe-sharded x{world}"},
             "roofline": {"bound": "hbm", "kernel": dom, "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": ach / HBM_PEAK_GBS, "traffic": traffic,
-                         "valu_issue_frac": _valu_busy(ptag, args.batch),
+                         "algorithmic_bytes_per_launch": alg_launch,
+                         "bytes_basis": f"SURVEY 8(d): payload + IQ = {payload_b + iq_b} B per subframe x "
+                                        f"{args.batch} subframes per launch",
+                         "timing": f"HIP events around each kernel on its launch stream, median of "
+                                   f"{args.kernel_reps} serial runs of the batch (outside the timed region)",
                          "kernel_ms": {k: v["ms"] for k, v in per_kernel.items()},
-                         "algorithmic_bytes_per_launch": {k: v["bytes"] for k, v in per_kernel.items()}},
+                         "profiler_ms": prof_ms,
+                         "frac_profiler": (alg_launch / (prof_ms * 1e-3) / 1e9 / HBM_PEAK_GBS) if prof_ms else None,
+                         "valu_issue_frac": _valu_busy(ptag, args.batch),
+                         "kernel_boundary_bytes_per_launch": {k: v["bytes"] for k, v in per_kernel.items()},
+                         "kernel_boundary_frac": {k: v["bytes"] / (v["ms"] * 1e-3) / 1e9 / HBM_PEAK_GBS
+                                                  for k, v in per_kernel.items()}},
             "end_to_end_algorithmic_GBps": value * (payload_b + iq_b) / 1e9,
             "cpu_baseline": cpu,
         }

@@ -520,7 +520,7 @@ uint32_t oai4g_generate_dummy_w(uint32_t D, uint8_t *w, uint8_t F);
 
 /* Batched UL receive chain of ulsch_decoding (PHY/LTE_TRANSPORT/ulsch_decoding.c:1208-1350) for
  * n_tb transport blocks of one configuration (B = TBS + 24 bits, G soft bits, Qm, rvidx, first
- * round: clear = 1, Nl = 1, Kmimo = 1): per code block r, lte_rate_matching_turbo_rx of the
+ * round: clear = 1, Nl = 1, Kmimo = 1; later rounds: oai4g_ul_decode_batch_harq below): per code block r, lte_rate_matching_turbo_rx of the
  * E_r soft bits at offset r_offset(r) of the TB's e stream, sub_block_deinterleaving_turbo and
  * phy_threegpplte_turbo_decoder16 (CRC24_B when C > 1, else CRC24_A with the filler F).  Device
  * pointers: d_e [n_tb][e_stride] int16, d_c [n_tb][C][c_stride] bytes (the reference's c[r],
@@ -537,6 +537,15 @@ uint32_t oai4g_ul_config_E(const oai4g_ul_config_t *cfg, int r);
 uint32_t oai4g_ul_config_G_offset(const oai4g_ul_config_t *cfg, int r);
 int oai4g_ul_decode_batch(oai4g_ul_config_t *cfg, int n_tb, const int16_t *d_e, size_t e_stride, uint8_t *d_c,
                           size_t c_stride, uint8_t *d_iters, void *stream);
+/* The same chain with HARQ soft combining across rounds, as dlsch_decoding / ulsch_decoding run it
+ * (dlsch_decoding.c:348-383: lte_rate_matching_turbo_rx with clear = (round == 0), the round's
+ * rvidx; dlsim's round loop, dlsim.c:2141): d_w [n_tb][C][w_stride] int16 device soft buffers, the
+ * reference's harq->w[r], updated in place (w_stride >= oai4g_ul_config_w_entries(cfg); zero them
+ * once before round 0 so entries past Ncb read 0).  rvidx 0..3 overrides the configuration's. */
+size_t oai4g_ul_config_w_entries(const oai4g_ul_config_t *cfg);
+int oai4g_ul_decode_batch_harq(oai4g_ul_config_t *cfg, int n_tb, const int16_t *d_e, size_t e_stride, int16_t *d_w,
+                               size_t w_stride, uint8_t rvidx, uint8_t clear, uint8_t *d_c, size_t c_stride,
+                               uint8_t *d_iters, void *stream);
 
 /* ---------------- batched device-resident transmit path ---------------- */
 /* Plain-old-data parameter block: what rank 0 broadcasts (RCCL) to the other ranks. */

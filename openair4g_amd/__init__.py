@@ -287,6 +287,10 @@ _SIGS = {
     "oai4g_ul_config_G_offset": (ctypes.c_uint32, [ctypes.c_void_p, ctypes.c_int]),
     "oai4g_ul_decode_batch": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_size_t,
                                              ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p, ctypes.c_void_p]),
+    "oai4g_ul_config_w_entries": (ctypes.c_size_t, [ctypes.c_void_p]),
+    "oai4g_ul_decode_batch_harq": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_size_t,
+                                                  ctypes.c_void_p, ctypes.c_size_t, ctypes.c_uint8, ctypes.c_uint8,
+                                                  ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p, ctypes.c_void_p]),
     "oai4g_dft": (ctypes.c_int, [ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int]),
     "oai4g_dft2048": (None, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int]),
     "oai4g_dft1024": (None, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int]),
@@ -1110,6 +1114,26 @@ class UlDecodeBatch:
         _check(self.L.oai4g_ul_decode_batch(self.cfg, self.n_tb, self.d_e, self.e_stride, self.d_c, self.c_stride,
                                             self.d_it, stream) == 0)
 
+    def launch_harq(self, rvidx, clear, stream=None):
+        """One HARQ round (oai4g_ul_decode_batch_harq) on the uploaded soft bits: the per-block soft
+        buffers (allocated zeroed on first use) combine this round's rvidx; clear = 1 on round 0."""
+        if getattr(self, "d_w", None) is None:
+            self.w_stride = (self.L.oai4g_ul_config_w_entries(self.cfg) + 63) & ~63
+            nbytes = self.n_tb * self.C * self.w_stride * 2
+            self.d_w = self.L.oai4g_dev_alloc(nbytes)
+            _check(bool(self.d_w))
+            z = np.zeros(nbytes // 2, np.int16)
+            _check(self.L.oai4g_memcpy_h2d(self.d_w, _ptr(z), nbytes) == 0)
+        _check(self.L.oai4g_ul_decode_batch_harq(self.cfg, self.n_tb, self.d_e, self.e_stride, self.d_w, self.w_stride,
+                                                 rvidx, clear, self.d_c, self.c_stride, self.d_it, stream) == 0)
+
+    def soft_buffers(self):
+        """[n_tb][C][w_stride] int16 HARQ soft buffers (after launch_harq)."""
+        _check(self.L.oai4g_sync() == 0)
+        w = np.empty((self.n_tb, self.C, self.w_stride), dtype=np.int16)
+        _check(self.L.oai4g_memcpy_d2h(_ptr(w), self.d_w, w.nbytes) == 0)
+        return w
+
     def results(self):
         _check(self.L.oai4g_sync() == 0)
         c = np.empty((self.n_tb, self.C, self.c_stride), dtype=np.uint8)
@@ -1119,8 +1143,9 @@ class UlDecodeBatch:
         return it, c
 
     def close(self):
-        for p in (self.d_e, self.d_c, self.d_it):
-            self.L.oai4g_dev_free(p)
+        for p in (self.d_e, self.d_c, self.d_it, getattr(self, "d_w", None)):
+            if p:
+                self.L.oai4g_dev_free(p)
         self.L.oai4g_ul_config_destroy(self.cfg)
 
 

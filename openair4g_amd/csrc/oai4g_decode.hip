@@ -599,6 +599,66 @@ hipError_t oai4g_launch_ul_rm_deint(const ul_dev_t *d_cfg, const ul_dev_t *h_cfg
   return hipSuccess;
 }
 
+/* lte_rate_matching_turbo_rx (lte_rate_matching.c:688-831) of every block into its HARQ soft buffer
+ * w, one thread per circular-buffer position p < Ncb (rows j = (tb, r) on blockIdx.y): clear = 1
+ * (round 0) starts from 0 (the reference's memset of w[0..Ncb)), clear = 0 from the stored value;
+ * the soft inputs the circular selection of this round's k0 maps to p are added with int16
+ * wrap-around, in the reference's order (the sum is associative mod 2^16). */
+__global__ void __launch_bounds__(256) k_ul_rm_harq(const ul_dev_t *__restrict__ c, const int16_t *__restrict__ e,
+                                                    size_t e_stride, int16_t *__restrict__ w, size_t w_stride,
+                                                    uint32_t rv, int clear, uint32_t j0)
+{
+  const uint32_t j = j0 + blockIdx.y, tb = j / c->C, r = j - tb * c->C;
+  const ul_pat_t &P = c->pat[c->pat_of[r]];
+  const uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= P.Ncb) return;
+  int16_t *wp = w + (size_t)j * w_stride + p;
+  int16_t acc = clear ? (int16_t)0 : *wp;
+  if (P.dummy[p] != OAI4G_LTE_NULL) {
+    const int16_t *soft = e + tb * e_stride + c->off[r];
+    const uint32_t ci = P.cidx[p], E = c->E[r], k0c = P.k0cr[rv];
+    for (uint32_t q = ci >= k0c ? ci - k0c : ci + P.Nnn - k0c; q < E; q += P.Nnn) acc = (int16_t)(acc + soft[q]);
+  }
+  *wp = acc;
+}
+
+/* sub_block_deinterleaving_turbo (lte_rate_matching.c:193-243) of every block's soft buffer into
+ * its decoder row, one thread per d entry (the inverse map of k_ul_rm_deint); positions past Ncb
+ * read 0, as a zero-initialised buffer the RX rate matcher never writes there gives */
+__global__ void __launch_bounds__(256) k_ul_deint_w(const ul_dev_t *__restrict__ c, const int16_t *__restrict__ w,
+                                                    size_t w_stride, int16_t *__restrict__ dfull, size_t d_stride,
+                                                    uint32_t j0)
+{
+  const uint32_t j = j0 + blockIdx.y, r = j % c->C;
+  const ul_pat_t &P = c->pat[c->pat_of[r]];
+  const uint32_t R = P.R, Kpi = R << 5, i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= 3 * Kpi + 3 || i == 2) return;
+  const uint32_t sft = i % 3, base = sft == 2 ? i - 5 : i, row = base / 96, cp = (base % 96) / 3;
+  if (row >= R) return;
+  const uint32_t k = (__builtin_bitreverse32(cp) >> 27) * R + row;
+  const uint32_t p = sft == 0 ? k : Kpi + 2 * k + (sft == 2 ? 1 : 0);
+  dfull[(size_t)j * d_stride + 96 - 3 * (Kpi - P.D) + i] = p < P.Ncb ? w[(size_t)j * w_stride + p] : (int16_t)0;
+}
+
+hipError_t oai4g_launch_ul_rm_harq(const ul_dev_t *d_cfg, const ul_dev_t *h_cfg, int n_tb, const int16_t *d_e,
+                                   size_t e_stride, int16_t *d_w, size_t w_stride, uint32_t rv, int clear,
+                                   int16_t *d_dfull, size_t d_stride, hipStream_t s)
+{
+  if (n_tb <= 0) return hipSuccess;
+  const uint32_t rows = (uint32_t)n_tb * h_cfg->C, gw = (3 * (h_cfg->Rmax << 5) + 255) / 256,
+                 gd = (3 * (h_cfg->Rmax << 5) + 3 + 255) / 256;
+  for (uint32_t j0 = 0; j0 < rows; j0 += 65535u) {
+    const uint32_t n = rows - j0 < 65535u ? rows - j0 : 65535u;
+    hipLaunchKernelGGL(k_ul_rm_harq, dim3(gw, n), dim3(256), 0, s, d_cfg, d_e, e_stride, d_w, w_stride, rv, clear, j0);
+    hipError_t err = hipGetLastError();
+    if (err != hipSuccess) return err;
+    hipLaunchKernelGGL(k_ul_deint_w, dim3(gd, n), dim3(256), 0, s, d_cfg, d_w, w_stride, d_dfull, d_stride, j0);
+    err = hipGetLastError();
+    if (err != hipSuccess) return err;
+  }
+  return hipSuccess;
+}
+
 hipError_t oai4g_launch_rm_rx(const int16_t *d_soft, uint32_t E, int16_t *d_w, const uint8_t *d_dummy,
                               const uint32_t *d_cidx, uint32_t Ncb, uint32_t Nnn, uint32_t k0c, int clear, hipStream_t s)
 {

@@ -2140,6 +2140,12 @@ extern "C" oai4g_ul_config_t *oai4g_ul_config_create(uint32_t B, uint32_t G, uin
       if (k0 >= P.Ncb) k0c = 0;
       P.Nnn = nn;
       P.k0c = k0c;
+      for (uint32_t rv = 0; rv < 4; rv++) {        /* every round's k0 (lte_rate_matching.c:743-745) */
+        const uint32_t k0r = P.R * (2 + (rv * (((Ncbmod == 0) ? 0 : 1) + (P.Ncb / (P.R << 3))) * 2));
+        uint32_t c = 0;
+        for (uint32_t q = 0; q < P.Ncb && q < k0r; q++) c += dw[q] != OAI4G_LTE_NULL;
+        P.k0cr[rv] = k0r >= P.Ncb ? 0 : c;
+      }
       if (P.R > h.Rmax) h.Rmax = P.R;
       uint8_t *dd = nullptr;
       uint32_t *dc = nullptr;
@@ -2193,29 +2199,29 @@ extern "C" int oai4g_ul_config_C(const oai4g_ul_config_t *cfg) { return (int)cfg
 extern "C" uint32_t oai4g_ul_config_G_offset(const oai4g_ul_config_t *cfg, int r) { return cfg->h.off[r]; }
 extern "C" uint32_t oai4g_ul_config_E(const oai4g_ul_config_t *cfg, int r) { return cfg->h.E[r]; }
 
-extern "C" int oai4g_ul_decode_batch(oai4g_ul_config_t *cfg, int n_tb, const int16_t *d_e, size_t e_stride,
-                                     uint8_t *d_c, size_t c_stride, uint8_t *d_iters, void *stream)
+static int ul_scratch(oai4g_ul_config_t *cfg, int n_tb)
 {
-  NEED_INIT(-1);
-  if (n_tb <= 0) return 0;
-  if (c_stride < cfg->Kplus / 8 || e_stride < cfg->G) { set_err("ul_decode_batch: strides too small"); return -1; }
-  if (n_tb > cfg->cap) {
-    if (cfg->d_dfull) hipFree(cfg->d_dfull);
-    if (cfg->d_td) hipFree(cfg->d_td);
-    cfg->d_dfull = nullptr;
-    cfg->d_td = nullptr;
-    const size_t nb = (size_t)n_tb * cfg->C;
-    const size_t td = cfg->bits == 8 ? oai4g_td8_scratch_bytes((uint16_t)cfg->Kplus, (int)nb)
-                                     : oai4g_td_scratch_bytes((uint16_t)cfg->Kplus, (int)nb);
-    if (hipMalloc(&cfg->d_dfull, nb * cfg->d_stride * 2) != hipSuccess || hipMalloc(&cfg->d_td, td) != hipSuccess) {
-      set_err("ul_decode_batch: device allocation failed");
-      cfg->cap = 0;
-      return -1;
-    }
-    cfg->cap = n_tb;
+  if (n_tb <= cfg->cap) return 0;
+  if (cfg->d_dfull) hipFree(cfg->d_dfull);
+  if (cfg->d_td) hipFree(cfg->d_td);
+  cfg->d_dfull = nullptr;
+  cfg->d_td = nullptr;
+  const size_t nb = (size_t)n_tb * cfg->C;
+  const size_t td = cfg->bits == 8 ? oai4g_td8_scratch_bytes((uint16_t)cfg->Kplus, (int)nb)
+                                   : oai4g_td_scratch_bytes((uint16_t)cfg->Kplus, (int)nb);
+  if (hipMalloc(&cfg->d_dfull, nb * cfg->d_stride * 2) != hipSuccess || hipMalloc(&cfg->d_td, td) != hipSuccess) {
+    set_err("ul_decode_batch: device allocation failed");
+    cfg->cap = 0;
+    return -1;
   }
-  hipStream_t s = (hipStream_t)stream;
-  HCK(oai4g_launch_ul_rm_deint(cfg->d, &cfg->h, n_tb, d_e, e_stride, cfg->d_dfull, cfg->d_stride, s), -1);
+  cfg->cap = n_tb;
+  return 0;
+}
+
+/* the decoders over the deinterleaved rows (one launch per block size) */
+static int ul_decode_rows(oai4g_ul_config_t *cfg, int n_tb, uint8_t *d_c, size_t c_stride, uint8_t *d_iters,
+                          hipStream_t s)
+{
   const uint32_t crc = cfg->C == 1 ? OAI4G_CRC24_A : OAI4G_CRC24_B, F = cfg->C == 1 ? cfg->F : 0;
   const int16_t *y = cfg->d_dfull + 96;
   if (cfg->bits == 8) {
@@ -2233,6 +2239,40 @@ extern "C" int oai4g_ul_decode_batch(oai4g_ul_config_t *cfg, int n_tb, const int
                         cfg->max_it, crc, F, td_tables(cfg->Kplus), cfg->d_td, s, cfg->C - cfg->Cminus, cfg->C,
                         cfg->Cminus), -1);
   return 0;
+}
+
+extern "C" int oai4g_ul_decode_batch(oai4g_ul_config_t *cfg, int n_tb, const int16_t *d_e, size_t e_stride,
+                                     uint8_t *d_c, size_t c_stride, uint8_t *d_iters, void *stream)
+{
+  NEED_INIT(-1);
+  if (n_tb <= 0) return 0;
+  if (c_stride < cfg->Kplus / 8 || e_stride < cfg->G) { set_err("ul_decode_batch: strides too small"); return -1; }
+  if (ul_scratch(cfg, n_tb) != 0) return -1;
+  hipStream_t s = (hipStream_t)stream;
+  HCK(oai4g_launch_ul_rm_deint(cfg->d, &cfg->h, n_tb, d_e, e_stride, cfg->d_dfull, cfg->d_stride, s), -1);
+  return ul_decode_rows(cfg, n_tb, d_c, c_stride, d_iters, s);
+}
+
+extern "C" size_t oai4g_ul_config_w_entries(const oai4g_ul_config_t *cfg) { return 3 * ((size_t)cfg->h.Rmax << 5); }
+
+/* the batch with HARQ soft combining: the decoders' input comes from the caller's per-block soft
+ * buffers d_w, updated in place by this round (dlsch_decoding.c:348-383, ulsch_decoding.c:1262-1294) */
+extern "C" int oai4g_ul_decode_batch_harq(oai4g_ul_config_t *cfg, int n_tb, const int16_t *d_e, size_t e_stride,
+                                          int16_t *d_w, size_t w_stride, uint8_t rvidx, uint8_t clear, uint8_t *d_c,
+                                          size_t c_stride, uint8_t *d_iters, void *stream)
+{
+  NEED_INIT(-1);
+  if (n_tb <= 0) return 0;
+  if (rvidx > 3 || clear > 1) { set_err("ul_decode_batch_harq: rvidx 0..3, clear 0 / 1"); return -1; }
+  if (c_stride < cfg->Kplus / 8 || e_stride < cfg->G || w_stride < oai4g_ul_config_w_entries(cfg)) {
+    set_err("ul_decode_batch_harq: strides too small");
+    return -1;
+  }
+  if (ul_scratch(cfg, n_tb) != 0) return -1;
+  hipStream_t s = (hipStream_t)stream;
+  HCK(oai4g_launch_ul_rm_harq(cfg->d, &cfg->h, n_tb, d_e, e_stride, d_w, w_stride, rvidx, clear, cfg->d_dfull,
+                              cfg->d_stride, s), -1);
+  return ul_decode_rows(cfg, n_tb, d_c, c_stride, d_iters, s);
 }
 
 extern "C" uint8_t oai4g_phy_threegpplte_turbo_decoder16(const int16_t *y, uint8_t *decoded_bytes, uint16_t n,

@@ -218,6 +218,7 @@ hipError_t oai4g_launch_td8(int n_cb, uint32_t K, const int16_t *d_llr, size_t l
 #define OAI4G_UL_MAX_C 16
 struct ul_pat_t {
   uint32_t D, R, Ncb, Nnn, k0c;
+  uint32_t k0cr[4];                /* k0c of rvidx 0..3 (the HARQ rounds) */
   const uint8_t *dummy;            /* [3 R 32] LTE_NULL marks */
   const uint32_t *cidx;            /* [Ncb] compact index */
 };
@@ -228,6 +229,11 @@ struct ul_dev_t {
 };
 hipError_t oai4g_launch_ul_rm_deint(const ul_dev_t *d_cfg, const ul_dev_t *h_cfg, int n_tb, const int16_t *d_e,
                                     size_t e_stride, int16_t *d_dfull, size_t d_stride, hipStream_t s);
+/* HARQ form: w [rows][w_stride] int16 circular soft buffers kept across rounds; the round's rv and
+ * clear (round 0) select k0 and the reset; then w -> the decoder's d buffers */
+hipError_t oai4g_launch_ul_rm_harq(const ul_dev_t *d_cfg, const ul_dev_t *h_cfg, int n_tb, const int16_t *d_e,
+                                   size_t e_stride, int16_t *d_w, size_t w_stride, uint32_t rv, int clear,
+                                   int16_t *d_dfull, size_t d_stride, hipStream_t s);
 hipError_t oai4g_launch_rm_rx(const int16_t *d_soft, uint32_t E, int16_t *d_w, const uint8_t *d_dummy,
                               const uint32_t *d_cidx, uint32_t Ncb, uint32_t Nnn, uint32_t k0c, int clear, hipStream_t s);
 hipError_t oai4g_launch_subblock_deint(uint32_t D, int16_t *d_dfull, const int16_t *d_w, hipStream_t s);

@@ -1,0 +1,273 @@
+/* cpu_baseline — TEST INFRASTRUCTURE ONLY (bench.py's cpu_baseline leg).
+ *
+ * Times the transmit path of one configuration on the host CPU, one subframe after another, the
+ * way dlsim's phy_proc_tx timer covers it (dlsim.c:2167-2699, generate_dci_top / generate_pilots
+ * excluded), with every stage that has a buildable reference translation unit running the
+ * REFERENCE's own code, compiled unmodified into oracle/_ref (oracle/Makefile), and the others the
+ * oracle's restatement (oracle/liboracle.so):
+ *
+ *   stage                  runs                                   reference
+ *   crc24a                 ref  crc24a                           crc_byte.c:117 (libref_coding.so)
+ *   segmentation           port orc_segmentation (+ CRC24B)      lte_segmentation.c:39 (PHY/defs.h: unbuildable)
+ *   turbo_encoder          port orc_turbo_encode                 3gpplte_sse.c:380 (lte_interleaver.h blob missing)
+ *   subblock_interleaving  ref  sub_block_interleaving_turbo     lte_rate_matching.c:51 (libref_rm.so)
+ *   rate_matching          ref  lte_rate_matching_turbo          lte_rate_matching.c:464 (libref_rm.so)
+ *   scrambling             ref  lte_gold_generic + the XOR loop  lte_gold.c:151 (libref_gold.so); the loop of
+ *                               of dlsch_scrambling (port)       dlsch_scrambling.c:78-92 (unbuildable)
+ *   modulation             port orc_modulation                   dlsch_modulation.c:1181 (unbuildable)
+ *   idft                   ref  idft2048 / idft1024 / ...        lte_dfts.c:2779 (libref_dfts.so)
+ *   cyclic_prefix          port the CP copy of PHY_ofdm_mod      ofdm_mod.c:139-171 (unbuildable)
+ *
+ * A stage whose reference library is absent falls back to the port and says so.  The first
+ * subframe's IQ is checked bit-exactly against orc_tx_subframe (the oracle's whole chain), so the
+ * composition does the same work.  Output: one JSON line with the per-stage microseconds per
+ * subframe, the subframes done and the rate from the stage-time sum.
+ *
+ *   cpu_baseline SECONDS SEED N_RB n_ant mode1 n_cw mimo_mode npdcch subframe Kmimo mcs0 mcs1 TBS0 TBS1
+ *                ra0 ra1 ra2 ra3 nb_rb rnti
+ */
+#define _GNU_SOURCE
+#include <dlfcn.h>
+#include <libgen.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+#include <time.h>
+#include <unistd.h>
+
+#include "../include/oai4g_qpp.h"
+#include "oai_oracle.h"
+
+enum { S_CRC, S_SEG, S_TURBO, S_SBI, S_RM, S_SCR, S_MOD, S_IDFT, S_CP, S_N };
+static const char *S_NAME[S_N] = {"crc24a", "segmentation", "turbo_encoder", "subblock_interleaving",
+                                  "rate_matching", "scrambling", "modulation", "idft", "cyclic_prefix"};
+
+static uint32_t (*ref_crc24a)(uint8_t *, uint32_t);
+static void (*ref_crcTableInit)(void);
+static uint32_t (*ref_sbi)(uint32_t, uint8_t *, uint8_t *);
+static uint32_t (*ref_rm)(uint32_t, uint32_t, uint8_t *, uint8_t *, uint8_t, uint32_t, uint8_t, uint8_t, uint8_t,
+                          uint8_t, uint8_t, uint8_t, uint8_t, uint8_t);
+static uint32_t (*ref_gold)(uint32_t *, uint32_t *, uint8_t);
+static void (*ref_idft)(int16_t *, int16_t *, int);
+
+static double now(void)
+{
+  struct timespec t;
+  clock_gettime(CLOCK_MONOTONIC, &t);
+  return t.tv_sec + 1e-9 * t.tv_nsec;
+}
+
+static void *ref_open(const char *dir, const char *name)
+{
+  char p[4096];
+  snprintf(p, sizeof(p), "%s/_ref/%s", dir, name);
+  return dlopen(p, RTLD_NOW | RTLD_LOCAL);
+}
+
+static uint64_t splitmix64(uint64_t *s)
+{
+  uint64_t z = (*s += 0x9E3779B97F4A7C15ull);
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
+
+/* the CP copy of PHY_ofdm_mod (ofdm_mod.c:139-171) after one symbol's IDFT */
+static void cp_copy(int32_t *out, int N, int cp)
+{
+  for (int k = 1; k <= cp; k++) out[-k] = out[N - k];
+}
+
+int main(int argc, char **argv)
+{
+  if (argc < 21) {
+    fprintf(stderr, "usage: see the header of oracle/cpu_baseline.c\n");
+    return 2;
+  }
+  char exe[4096];
+  ssize_t n_exe = readlink("/proc/self/exe", exe, sizeof(exe) - 1);
+  if (n_exe <= 0) return 2;
+  exe[n_exe] = 0;
+  const char *dir = dirname(exe);
+
+  const double seconds = atof(argv[1]);
+  uint64_t seed = strtoull(argv[2], NULL, 0);
+  orc_tx_cfg_t cfg;
+  memset(&cfg, 0, sizeof(cfg));
+  const int N_RB = atoi(argv[3]), n_ant = atoi(argv[4]), mode1 = atoi(argv[5]);
+  cfg.n_cw = (uint8_t)atoi(argv[6]);
+  cfg.mimo_mode = (uint8_t)atoi(argv[7]);
+  cfg.num_pdcch_symbols = (uint8_t)atoi(argv[8]);
+  cfg.subframe = (uint8_t)atoi(argv[9]);
+  cfg.Kmimo = (uint8_t)atoi(argv[10]);
+  cfg.mcs[0] = (uint8_t)atoi(argv[11]);
+  cfg.mcs[1] = (uint8_t)atoi(argv[12]);
+  cfg.TBS[0] = (uint32_t)atoi(argv[13]);
+  cfg.TBS[1] = (uint32_t)atoi(argv[14]);
+  for (int i = 0; i < 4; i++) cfg.rb_alloc[i] = (uint32_t)strtoul(argv[15 + i], NULL, 0);
+  cfg.nb_rb = (uint16_t)atoi(argv[19]);
+  cfg.rnti = (uint16_t)atoi(argv[20]);
+  cfg.amp = 512;
+  cfg.sqrt_rho_a = cfg.sqrt_rho_b = 8192;
+  cfg.Mdlharq = 8;
+  if (orc_init_frame(&cfg.fp, (uint16_t)N_RB, 0, 0, (uint8_t)n_ant, (uint8_t)mode1, 0) != 0) return 2;
+  const orc_frame_t *fp = &cfg.fp;
+  const int N = fp->ofdm_symbol_size, nsymb = fp->symbols_per_tti, spt = (int)fp->samples_per_tti;
+
+  /* the reference's own code where it builds (oracle/_ref); the port otherwise */
+  void *hc = ref_open(dir, "libref_coding.so"), *hr = ref_open(dir, "libref_rm.so");
+  void *hg = ref_open(dir, "libref_gold.so"), *hd = ref_open(dir, "libref_dfts.so");
+  if (hc) {
+    ref_crc24a = (uint32_t(*)(uint8_t *, uint32_t))dlsym(hc, "crc24a");
+    ref_crcTableInit = (void (*)(void))dlsym(hc, "crcTableInit");
+    if (ref_crcTableInit) ref_crcTableInit();
+    if (!ref_crcTableInit) ref_crc24a = NULL;
+  }
+  if (hr) {
+    ref_sbi = (uint32_t(*)(uint32_t, uint8_t *, uint8_t *))dlsym(hr, "sub_block_interleaving_turbo");
+    ref_rm = (uint32_t(*)(uint32_t, uint32_t, uint8_t *, uint8_t *, uint8_t, uint32_t, uint8_t, uint8_t, uint8_t, uint8_t,
+                          uint8_t, uint8_t, uint8_t, uint8_t))dlsym(hr, "lte_rate_matching_turbo");
+  }
+  if (hg) ref_gold = (uint32_t(*)(uint32_t *, uint32_t *, uint8_t))dlsym(hg, "lte_gold_generic");
+  if (hd) {
+    char nm[32];
+    snprintf(nm, sizeof(nm), "idft%d", N);
+    ref_idft = (void (*)(int16_t *, int16_t *, int))dlsym(hd, nm);
+  }
+  const int use_ref[S_N] = {ref_crc24a != NULL, 0, 0, ref_sbi != NULL, ref_rm != NULL, ref_gold != NULL, 0,
+                            ref_idft != NULL, 0};
+
+  int G[2] = {0, 0};
+  uint8_t Qm[2];
+  for (int cw = 0; cw < cfg.n_cw; cw++) {
+    Qm[cw] = orc_get_Qm(cfg.mcs[cw]);
+    G[cw] = n_ant == 4 ? orc_count_pdsch_res(fp, cfg.rb_alloc, cfg.num_pdcch_symbols, cfg.subframe) * Qm[cw]
+                       : orc_get_G(fp->N_RB_DL, fp->Ncp, fp->mode1_flag, fp->frame_type, cfg.nb_rb, cfg.rb_alloc, Qm[cw],
+                                   1, cfg.num_pdcch_symbols, cfg.subframe);
+  }
+  /* buffers: 16-byte aligned as the reference's malloc16 gives them */
+  uint8_t *pay[2], *a[2], *e[2];
+  for (int cw = 0; cw < 2; cw++) {
+    pay[cw] = aligned_alloc(64, 6200);
+    a[cw] = aligned_alloc(64, 6200);
+    e[cw] = aligned_alloc(64, (size_t)((1 + (G[cw] >> 5)) * 32 + 128));
+    for (int i = 0; i < 6200; i++) pay[cw][i] = (uint8_t)splitmix64(&seed);
+  }
+  static uint8_t cbuf[16][8 + 3 + 768];
+  uint8_t *dbuf = aligned_alloc(64, 96 + 12 + 3 + 3 * 6144 + 128), *wbuf = aligned_alloc(64, 3 * 6176 + 128);
+  int32_t *txF[4], *txd[4], *chk[4], *chkF[4];
+  for (int aa = 0; aa < n_ant; aa++) {
+    txF[aa] = aligned_alloc(64, (size_t)10 * nsymb * N * 4);
+    txd[aa] = aligned_alloc(64, (size_t)spt * 4 + 64);
+    chk[aa] = aligned_alloc(64, (size_t)spt * 4 + 64);
+    chkF[aa] = aligned_alloc(64, (size_t)nsymb * N * 4);
+    memset(txF[aa], 0, (size_t)10 * nsymb * N * 4);
+  }
+
+  int32_t *tmp128 = aligned_alloc(64, 128 * 4 * 4);
+  double st[S_N];
+  memset(st, 0, sizeof(st));
+  long done = 0;
+  const double t_start = now();
+  for (;;) {
+    double t0, t1;
+    for (int cw = 0; cw < cfg.n_cw; cw++) {
+      const uint32_t A = cfg.TBS[cw];
+      memcpy(a[cw], pay[cw], A / 8);
+      t0 = now();
+      uint32_t crc = (use_ref[S_CRC] ? ref_crc24a(a[cw], A) : orc_crc24a(a[cw], (int)A)) >> 8;   /* dlsch_coding.c:296 */
+      a[cw][A >> 3] = (uint8_t)(crc >> 16);
+      a[cw][1 + (A >> 3)] = (uint8_t)(crc >> 8);
+      a[cw][2 + (A >> 3)] = (uint8_t)crc;
+      t1 = now(); st[S_CRC] += t1 - t0; t0 = t1;
+      uint32_t C, Cp, Cm, Kp, Km, F;
+      uint8_t *cptr[16];
+      for (int r = 0; r < 16; r++) cptr[r] = cbuf[r];
+      if (orc_segmentation(a[cw], cptr, A + 24, &C, &Cp, &Cm, &Kp, &Km, &F) < 0) return 3;
+      t1 = now(); st[S_SEG] += t1 - t0;
+      uint32_t r_off = 0;
+      for (uint32_t r = 0; r < C; r++) {
+        const uint32_t Kr = r < Cm ? Km : Kp;
+        const int qi = oai4g_qpp_index(Kr);
+        t0 = now();
+        memset(dbuf, ORC_LTE_NULL, 96);
+        orc_turbo_encode(cptr[r], (uint16_t)(Kr >> 3), dbuf + 96, oai4g_qpp_table[qi].f1, oai4g_qpp_table[qi].f2);
+        t1 = now(); st[S_TURBO] += t1 - t0; t0 = t1;
+        uint32_t RTC = use_ref[S_SBI] ? ref_sbi(Kr + 4, dbuf + 96, wbuf) : orc_subblock_interleave(Kr + 4, dbuf + 96, wbuf);
+        t1 = now(); st[S_SBI] += t1 - t0; t0 = t1;
+        r_off += use_ref[S_RM] ? ref_rm(RTC, (uint32_t)G[cw], wbuf, e[cw] + r_off, (uint8_t)C, ORC_NSOFT, cfg.Mdlharq,
+                                        cfg.Kmimo, 0, Qm[cw], 1, (uint8_t)r, 0, 0)
+                               : orc_rate_match(RTC, (uint32_t)G[cw], wbuf, e[cw] + r_off, (uint8_t)C, ORC_NSOFT,
+                                                cfg.Mdlharq, cfg.Kmimo, 0, Qm[cw], 1, (uint8_t)r);
+        t1 = now(); st[S_RM] += t1 - t0;
+      }
+      /* dlsch_scrambling (dlsch_scrambling.c:51-97) around the reference's lte_gold_generic */
+      t0 = now();
+      uint32_t x1 = 0, x2 = ((uint32_t)cfg.rnti << 14) + ((uint32_t)cfg.subframe << 9) + fp->Nid_cell;
+      uint32_t (*gold)(uint32_t *, uint32_t *, uint8_t) = use_ref[S_SCR] ? ref_gold : orc_gold_generic;
+      uint32_t s = gold(&x1, &x2, 1);
+      uint8_t *ep = e[cw];
+      for (int i = 0, k = 0; i < 1 + (G[cw] >> 5); i++) {
+        for (int j = 0; j < 32; j++, k++) ep[k] = (ep[k] & 1) ^ ((s >> j) & 1);
+        s = gold(&x1, &x2, 0);
+      }
+      t1 = now(); st[S_SCR] += t1 - t0;
+    }
+    /* dlsch_modulation into the frame grid (dlsim zeroes txdataF before its timer, dlsim.c:2161) */
+    for (int aa = 0; aa < n_ant; aa++) memset(txF[aa] + (size_t)cfg.subframe * nsymb * N, 0, (size_t)nsymb * N * 4);
+    t0 = now();
+    orc_cw_t c0 = {e[0], cfg.mcs[0], cfg.mimo_mode, 1, {0}}, c1 = {e[1], cfg.mcs[1], cfg.mimo_mode, 1, {0}};
+    memcpy(c0.rb_alloc, cfg.rb_alloc, sizeof(c0.rb_alloc));
+    memcpy(c1.rb_alloc, cfg.rb_alloc, sizeof(c1.rb_alloc));
+    if (orc_modulation(txF, cfg.amp, cfg.subframe, fp, cfg.num_pdcch_symbols, &c0, cfg.n_cw > 1 ? &c1 : NULL,
+                       cfg.sqrt_rho_a, cfg.sqrt_rho_b) < 0)
+      return 3;
+    t1 = now(); st[S_MOD] += t1 - t0;
+    /* do_OFDM_mod_l x 2 slots -> normal_prefix_mod -> PHY_ofdm_mod (ofdm_mod.c:47-229), normal CP */
+    for (int aa = 0; aa < n_ant; aa++) {
+      const int32_t *in = txF[aa] + (size_t)cfg.subframe * nsymb * N;
+      for (int slot = 0; slot < 2; slot++)
+        for (int l = 0; l < 7; l++) {
+          const int cp = l == 0 ? fp->nb_prefix_samples0 : fp->nb_prefix_samples;
+          const int off = slot * (spt >> 1) + l * N + fp->nb_prefix_samples0 + (l > 0 ? l * fp->nb_prefix_samples : 0);
+          int32_t *out = txd[aa] + off;
+          t0 = now();
+          if (use_ref[S_IDFT] && N == 128) {        /* PHY_ofdm_mod's static temp (ofdm_mod.c:94, 142-156) */
+            ref_idft((int16_t *)(in + (slot * 7 + l) * N), (int16_t *)tmp128, 1);
+            memcpy(out, tmp128, 128 * 4);
+          } else if (use_ref[S_IDFT])
+            ref_idft((int16_t *)(in + (slot * 7 + l) * N), (int16_t *)out, 1);
+          else
+            orc_idft(fp->log2_symbol_size, (const int16_t *)(in + (slot * 7 + l) * N), (int16_t *)out, 1);
+          t1 = now(); st[S_IDFT] += t1 - t0; t0 = t1;
+          cp_copy(out, N, cp);
+          t1 = now(); st[S_CP] += t1 - t0;
+        }
+    }
+    if (done == 0) {
+      /* the composition against the oracle's whole chain, bit for bit */
+      uint8_t *pp[2] = {a[0], a[1]};
+      for (int cw = 0; cw < cfg.n_cw; cw++) memcpy(a[cw], pay[cw], cfg.TBS[cw] / 8);
+      if (orc_tx_subframe(&cfg, pp, chkF, chk, NULL) != 0) return 4;
+      for (int aa = 0; aa < n_ant; aa++)
+        if (memcmp(chk[aa], txd[aa], (size_t)spt * 4) != 0) {
+          fprintf(stderr, "cpu_baseline: composed IQ differs from orc_tx_subframe (antenna %d)\n", aa);
+          return 5;
+        }
+    }
+    done++;
+    if (now() - t_start >= seconds) break;
+  }
+  double tot = 0;
+  for (int k = 0; k < S_N; k++) tot += st[k];
+  printf("{\"subframes\": %ld, \"wall_s\": %.6f, \"stage_s\": %.6f, \"rate\": %.3f, \"validated\": true, \"stage_us\": {",
+         done, now() - t_start, tot, done / tot);
+  for (int k = 0; k < S_N; k++) printf("%s\"%s\": %.3f", k ? ", " : "", S_NAME[k], 1e6 * st[k] / done);
+  printf("}, \"impl\": {");
+  for (int k = 0; k < S_N; k++)
+    printf("%s\"%s\": \"%s\"", k ? ", " : "", S_NAME[k],
+           use_ref[k] ? (k == S_SCR ? "reference generator + port loop" : "reference") : "port");
+  printf("}}\n");
+  return 0;
+}

@@ -575,6 +575,25 @@ def ulsch_decode(e, B, G, Qm, rvidx=0, max_it=8, Mdlharq=8):
     return out
 
 
+def ulsch_decode_harq(e, B, G, Qm, rvidx, clear, w_state, max_it=8, Mdlharq=8):
+    """One HARQ round of the per-block chain (dlsch_decoding.c:348-383): lte_rate_matching_turbo_rx
+    into the kept soft buffers w_state[r] (int16 arrays, updated in place; clear = 1 on round 0),
+    sub-block deinterleaving, turbo decoding.  Returns [(iterations, bytes)] per block."""
+    import spec_model as S
+    blocks, F = S.segment([0] * B)
+    C = len(blocks)
+    e = np.ascontiguousarray(e, dtype=np.int16)
+    off, out = 0, []
+    for r, blk in enumerate(blocks):
+        K = len(blk)
+        dw = dummy_w_F(K + 4, F if r == 0 else 0)
+        w, E = rate_match_rx(e[off:], K, G, C, r, Qm, rvidx=rvidx, Mdlharq=Mdlharq, dw=dw, w=w_state[r], clear=clear)
+        off += E
+        d = subblock_deinterleave(w, K)
+        out.append(turbo_decode(d, K, max_it=max_it, crc_type=1 if C > 1 else 0, F=(F if C == 1 else 0)))
+    return out
+
+
 def turbo_decode8(y, K, max_it=8, crc_type=0, F=0):
     """phy_threegpplte_turbo_decoder8 (oracle/oai_oracle_td8.c): y = 3K+12 int16 LLRs (4 more
     entries are read, zero here).  Returns (iterations, decoded bytes)."""

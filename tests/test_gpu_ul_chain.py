@@ -75,3 +75,35 @@ def test_gpu_ul_chain_rows_beyond_grid_y_limit(gpu):
         for r, (it, d) in enumerate(ref):
             assert its[t, r] == it and np.array_equal(c[t, r, :len(d)], d), (t, r)
     ub.close()
+
+
+@pytest.mark.parametrize("tbs,G,Qm", UL)
+def test_gpu_ul_chain_harq_rounds_match_oracle(gpu, tbs, G, Qm):
+    """oai4g_ul_decode_batch_harq over dlsim's four-round sequence rv 0, 2, 3, 1 (clear = 1 on round
+    0, then soft combining in the kept buffers; dlsch_decoding.c:348-383, dlsim.c:2141): iteration
+    counts, decoded blocks and the soft buffers bit-exact per round against the oracle chain,
+    whose lte_rate_matching_turbo_rx is pinned to the reference's own (tests/test_ref_pin_rm_cpu.py).
+    Large soft values make the int16 sums wrap."""
+    import spec_model as S
+    from test_ul_chain_cpu import ul_e
+    n_tb, rng = 4, np.random.default_rng(tbs)
+    pays = [rng.integers(0, 256, tbs // 8 + 8, dtype=np.uint8) for _ in range(n_tb)]
+    blocks, _ = S.segment([0] * (tbs + 24))
+    w_o = [[np.zeros(3 * 32 * ((len(b) + 4 + 31) // 32) + 64, np.int16) for b in blocks] for _ in range(n_tb)]
+    ub = gpu.UlDecodeBatch(tbs + 24, G, Qm, n_tb, max_iterations=4)
+    for rnd, rv in enumerate((0, 2, 3, 1)):
+        amp = 12000 if rnd == 3 else 20
+        e = np.stack([np.clip(np.round((2 * np.array(ul_e(pays[t], tbs, G, Qm, rv=rv), np.float64) - 1) * amp
+                                       + rng.normal(0, 30, G)), -32768, 32767).astype(np.int16) for t in range(n_tb)])
+        ub.upload(e)
+        ub.launch_harq(rv, 1 if rnd == 0 else 0)
+        its, c = ub.results()
+        wg = ub.soft_buffers()
+        for t in range(n_tb):
+            ref = O.ulsch_decode_harq(e[t], tbs + 24, G, Qm, rv, 1 if rnd == 0 else 0, w_o[t], max_it=4)
+            for r, (it, d) in enumerate(ref):
+                Ncb = 3 * 32 * ((len(blocks[r]) + 4 + 31) // 32)
+                assert np.array_equal(wg[t, r, :Ncb], w_o[t][r][:Ncb]), (rnd, t, r)
+                assert its[t, r] == it, (rnd, t, r, its[t, r], it)
+                assert np.array_equal(c[t, r, :len(d)], d), (rnd, t, r)
+    ub.close()

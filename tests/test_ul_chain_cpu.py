@@ -39,7 +39,7 @@ def test_dummy_w_matches_36212_null_positions():
         assert np.array_equal(got, want), (K, F, np.nonzero(got != want)[0][:5])
 
 
-def ul_e(payload, tbs, G, Qm):
+def ul_e(payload, tbs, G, Qm, rv=0):
     """36.212 coding of one UL TB with the filler bits as <NULL> (5.1.3.2.1: d0 / d1 of the first
     block's F filler positions are <NULL>, so rate matching skips them) -- what the reference's RX
     (generate_dummy_w with F) expects.  The reference's own encoder transmits them as 0 bits
@@ -56,7 +56,7 @@ def ul_e(payload, tbs, G, Qm):
             for k in range(F):
                 st[0][k] = st[1][k] = S.NULL
         R, w = S.subblock(st)
-        e += S.rate_match(w, R, G, len(blocks), r, Qm)
+        e += S.rate_match(w, R, G, len(blocks), r, Qm, rv=rv)
     return e
 
 
@@ -81,3 +81,21 @@ def test_ul_chain_recovers_tb(tbs, G, Qm):
     blocks, F = S.segment(S.bytes_to_bits(pay, tbs) + S.crc24(S.bytes_to_bits(pay, tbs), S.CRC24A))
     for (it, c), blk in zip(res, blocks):
         assert np.array_equal(np.unpackbits(c)[:len(blk)], np.array(blk, np.uint8))
+
+
+def test_harq_rounds_combine_on_the_oracle():
+    """dlsim's round loop on the oracle: a TB too noisy for one round decodes after soft-combining
+    the rv 0, 2, 3, 1 retransmissions in the kept buffers (the combined soft buffer of round n is
+    the int16 sum of every round's contribution, checked against separately combined rounds)."""
+    tbs, G, Qm = 7000, 14400, 4
+    rng = np.random.default_rng(41)
+    pay = rng.integers(0, 256, tbs // 8 + 8, dtype=np.uint8)
+    blocks, _ = S.segment([0] * (tbs + 24))
+    w = [np.zeros(3 * 32 * ((len(b) + 4 + 31) // 32) + 64, np.int16) for b in blocks]
+    ok = []
+    for rnd, rv in enumerate((0, 2, 3, 1)):
+        e = np.array(ul_e(pay, tbs, G, Qm, rv=rv), dtype=np.float64)
+        y = np.clip(np.round((2 * e - 1) * 20 + rng.normal(0, 30, G)), -32768, 32767).astype(np.int16)
+        res = O.ulsch_decode_harq(y, tbs + 24, G, Qm, rv, 1 if rnd == 0 else 0, w, max_it=4)
+        ok.append(all(it <= 4 for it, _ in res))
+    assert not ok[0] and ok[-1], ok

@@ -65,14 +65,34 @@ def main(prof_dir, tag, config, out_dir):
         b = (f * cal["FETCH_SIZE"] + w * cal["WRITE_SIZE"]) * 1024
         traffic[k] = b
         lines.append(f"| {k} | {f:.0f} | {w:.0f} | {b/1e6:.1f} MB | {res.get(k)} |")
+    # per-dispatch durations from the kernel trace: the median over the launches of each kernel is
+    # what bench.py reports beside its HIP-event time (roofline.profiler_ms)
+    kt = os.path.join(prof_dir, f"trace_{tag}", "run_kernel_trace.csv")
+    prof_ms = {}
+    if os.path.exists(kt):
+        durs = collections.defaultdict(list)
+        for r in csv.DictReader(open(kt)):
+            k = short(r["Kernel_Name"])
+            if k:
+                durs[k].append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6)
+        lines += ["", "Per-dispatch durations (kernel trace):", "",
+                  "| kernel | dispatches | median ms | mean ms | min ms |", "|---|---|---|---|---|"]
+        for k, v in sorted(durs.items()):
+            v = sorted(v)
+            med = v[len(v) // 2] if len(v) % 2 else 0.5 * (v[len(v) // 2 - 1] + v[len(v) // 2])
+            prof_ms[k] = med
+            lines.append(f"| {k} | {len(v)} | {med:.4f} | {sum(v) / len(v):.4f} | {v[0]:.4f} |")
     os.makedirs(out_dir, exist_ok=True)
     open(os.path.join(out_dir, f"rocprof_{tag}_{config}.md"), "w").write("\n".join(lines) + "\n")
     traffic["batch"] = int(os.environ.get("BATCH", {"C3": 8192, "C4": 1024, "C5": 2048, "FEP": 8192, "UE": 4096}.get(config, 0)))
     json.dump(traffic, open(os.path.join(out_dir, f"traffic_{config}.json"), "w"), indent=1)
+    if prof_ms:
+        prof_ms["batch"] = traffic["batch"]
+        json.dump(prof_ms, open(os.path.join(out_dir, f"traffic_{config}_ms.json"), "w"), indent=1)
     for s in ("trace", "fetch", "write", "calfetch", "calwrite"):
         d = os.path.join(prof_dir, f"{s}_{tag}")
         for fn in os.listdir(d):
-            if fn.endswith("stats.csv") or fn.endswith("counter_collection.csv"):
+            if fn.endswith("stats.csv") or fn.endswith("counter_collection.csv") or fn.endswith("kernel_trace.csv"):
                 src = os.path.join(d, fn)
                 dst = os.path.join(out_dir, f"{tag}_{config}_{s}_{fn}")
                 open(dst, "w").write(open(src).read())

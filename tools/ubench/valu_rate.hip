@@ -1,5 +1,6 @@
 // Microbenchmark: wave-instruction throughput of the VALU forms the IDFT / decoder use (gfx950).
-// Every CU runs 8 waves per SIMD of a loop of 16 independent chains x ITER of one instruction.
+// Every CU runs 1, 2, 4 and 8 waves per SIMD of a loop of 16 independent chains x ITER of one
+// instruction, plus encoding-size controls (the same op as VOP2 / VOP3).
 #include <hip/hip_runtime.h>
 #include <cstdio>
 #define ITER 2048
@@ -71,6 +72,17 @@ KERNEL(k_cndmask, "v_cndmask_b32 %0, %0, %1, vcc")
 KERNEL(k_lshlor2, "v_lshl_or_b32 %0, %0, 1, %1")
 KERNEL(k_dot2u, "v_dot2_u32_u16 %0, %0, %1, %0")
 KERNEL(k_mulu24, "v_mul_u32_u24 %0, %0, %1")
+// encoding-size controls: the full-rate VOP2 ops forced into the 8-byte VOP3 encoding, and
+// half-rate ops that have a 4-byte VOP2 / VOP1 encoding (is the rate the op or the fetch?)
+KERNEL(k_add_e64, "v_add_u32_e64 %0, %0, %1")
+KERNEL(k_and_e64, "v_and_b32_e64 %0, %0, %1")
+KERNEL(k_xor_e64, "v_xor_b32_e64 %0, %0, %1")
+KERNEL(k_mov_e64, "v_mov_b32_e64 %0, %1")
+KERNEL(k_max_e32, "v_max_i32_e32 %0, %0, %1")
+KERNEL(k_lshl_e32v, "v_lshlrev_b32_e32 %0, %1, %0")
+KERNEL(k_mul24_e32, "v_mul_i32_i24_e32 %0, %0, %1")
+KERNEL(k_maxu16_e32, "v_max_u16_e32 %0, %0, %1")
+KERNEL(k_addf32_e32, "v_add_f32_e32 %0, %0, %1")
 
 typedef void (*kfn)(unsigned *, unsigned);
 int main() {
@@ -80,7 +92,10 @@ int main() {
       {"v_pk_max_i16", k_pkmax}, {"v_ashrrev_i32", k_ashr}, {"v_pk_ashrrev_i16", k_pkashr},
       {"v_alignbit_b32", k_alignbit}, {"v_perm_b32", k_perm}, {"v_mad_u32_u24", k_mad24},
       {"v_mul_lo_u32", k_mullo}, {"v_max3_i32", k_max3}, {"v_bitop3_b32", k_bitop3}, {"v_mov_b32_dpp", k_dpp},
-      {"v_add_u16_sdwa", k_addsdwa}, {"v_max_i16_sdwa", k_pkmaxsdwa}, {"v_lshlrev_b32", k_lshl}, {"v_and_b32", k_and}, {"v_or_b32", k_or}, {"v_xor_b32", k_xor}, {"v_sub_u32", k_sub}, {"v_mul_i32_i24", k_mul24}, {"v_mul_hi_i32_i24", k_mulhi24}, {"v_add3_u32", k_add3}, {"v_lshl_add_u32", k_lshladd}, {"v_lshl_or_b32", k_lshlor}, {"v_and_or_b32", k_andor}, {"v_or3_b32", k_or3}, {"v_bfe_i32", k_bfei}, {"v_med3_i32", k_med3}, {"v_pk_mul_lo_u16 sel", k_pkmullo}, {"v_mov_b32", k_mov}, {"v_sub_u16", k_sub16}, {"v_add_i32", k_addi32c}, {"v_mad_i32_i24", k_madi24}, {"v_alignbyte_b32", k_alignbyte}, {"v_max_i32", k_max}, {"v_pk_lshlrev_b16", k_pklshl}, {"v_lshrrev_b16", k_lshr16}, {"v_not_b32", k_not}, {"v_bfi_b32", k_bfi}, {"v_add_co_u32", k_addco}, {"v_pk_sub_i16", k_pksubsat}, {"v_pk_sub_i16 sel", k_pksubsel}, {"v_xad_u32", k_xad}, {"v_add_u32_sdwa sdwa", k_addsdwa32}, {"v_ashrrev_i32_sdwa sdwa", k_ashrsdwa}, {"v_cndmask_b32", k_cndmask}, {"v_lshl_or_b32", k_lshlor2}, {"v_dot2_u32_u16", k_dot2u}, {"v_mul_u32_u24", k_mulu24}};
+      {"v_add_u16_sdwa", k_addsdwa}, {"v_max_i16_sdwa", k_pkmaxsdwa}, {"v_lshlrev_b32", k_lshl}, {"v_and_b32", k_and}, {"v_or_b32", k_or}, {"v_xor_b32", k_xor}, {"v_sub_u32", k_sub}, {"v_mul_i32_i24", k_mul24}, {"v_mul_hi_i32_i24", k_mulhi24}, {"v_add3_u32", k_add3}, {"v_lshl_add_u32", k_lshladd}, {"v_lshl_or_b32", k_lshlor}, {"v_and_or_b32", k_andor}, {"v_or3_b32", k_or3}, {"v_bfe_i32", k_bfei}, {"v_med3_i32", k_med3}, {"v_pk_mul_lo_u16 sel", k_pkmullo}, {"v_mov_b32", k_mov}, {"v_sub_u16", k_sub16}, {"v_add_i32", k_addi32c}, {"v_mad_i32_i24", k_madi24}, {"v_alignbyte_b32", k_alignbyte}, {"v_max_i32", k_max}, {"v_pk_lshlrev_b16", k_pklshl}, {"v_lshrrev_b16", k_lshr16}, {"v_not_b32", k_not}, {"v_bfi_b32", k_bfi}, {"v_add_co_u32", k_addco}, {"v_pk_sub_i16", k_pksubsat}, {"v_pk_sub_i16 sel", k_pksubsel}, {"v_xad_u32", k_xad}, {"v_add_u32_sdwa sdwa", k_addsdwa32}, {"v_ashrrev_i32_sdwa sdwa", k_ashrsdwa}, {"v_cndmask_b32", k_cndmask}, {"v_lshl_or_b32", k_lshlor2}, {"v_dot2_u32_u16", k_dot2u}, {"v_mul_u32_u24", k_mulu24},
+      {"v_add_u32_e64 (VOP3)", k_add_e64}, {"v_and_b32_e64 (VOP3)", k_and_e64}, {"v_xor_b32_e64 (VOP3)", k_xor_e64},
+      {"v_mov_b32_e64 (VOP3)", k_mov_e64}, {"v_max_i32_e32 (VOP2)", k_max_e32}, {"v_lshlrev_b32_e32 vv", k_lshl_e32v},
+      {"v_mul_i32_i24_e32", k_mul24_e32}, {"v_max_u16_e32 (VOP2)", k_maxu16_e32}, {"v_add_f32_e32 (VOP2)", k_addf32_e32}};
   unsigned *d;
   hipMalloc(&d, 64);
   hipDeviceProp_t p;
@@ -89,7 +104,7 @@ int main() {
   hipEvent_t a, b;
   hipEventCreate(&a);
   hipEventCreate(&b);
-  for (int wps : {2, 8}) {
+  for (int wps : {1, 2, 4, 8}) {
   int blocks = cus * wps;   // 256-thread blocks: wps per CU = wps waves per SIMD
   printf("--- %d wave(s) per SIMD\n", wps);
   for (auto &k : ks) {
