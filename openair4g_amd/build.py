@@ -25,8 +25,10 @@ def _newer(target, deps):
     return any(os.path.getmtime(d) > t for d in deps)
 
 
-def build_lib(force=False, verbose=False, out=None, defines=()):
-    """Compile the library; `out`/`defines` build a variant (e.g. -DOAI4G_MODOFDM_WAVES=3)."""
+def build_lib(force=False, verbose=False, out=None, defines=(), only=None):
+    """Compile the library; `out`/`defines` build a variant (e.g. -DOAI4G_MODOFDM_WAVES=3); with
+    `only` (source basenames) a variant recompiles just those and links the in-tree objects of
+    the others."""
     lib = out or LIB
     libdir = os.path.dirname(lib)
     os.makedirs(libdir, exist_ok=True)
@@ -35,8 +37,16 @@ def build_lib(force=False, verbose=False, out=None, defines=()):
     if not force and not _newer(lib, deps):
         return lib
     objs = []
+    hdrs = deps[len(srcs) + len(EXTRA):] + [os.path.join(ROOT, "include", "oai4g_qpp.h"),
+                                             os.path.join(ROOT, "include", "oai4g_tbs.h")]
     for src in srcs + EXTRA:
         obj = os.path.join(libdir, os.path.basename(src) + ".o")
+        if only is not None and os.path.basename(src) not in only:
+            objs.append(os.path.join(LIBDIR, os.path.basename(src) + ".o"))
+            continue
+        if not force and not defines and not _newer(obj, [src] + hdrs):   # incremental: unchanged objects stay
+            objs.append(obj)
+            continue
         lang = ["-x", "hip"] if src.endswith((".hip", ".cpp")) else ["-x", "c"]
         cmd = [HIPCC, f"--offload-arch={ARCH}", "-O3", "-fPIC", "-Wall", "-Wno-unused-result", "-Wno-unused-value",
                "-I", os.path.join(ROOT, "include")] + list(defines) + (["-std=c++17"] if lang[1] == "hip" else []) + lang + \
@@ -80,9 +90,11 @@ def build_oracle(verbose=False):
 if __name__ == "__main__":
     if "--variant" in sys.argv:   # build.py --variant NAME -DFOO=1 [-mllvm X] ... -> variants/NAME/libopenair4g_amd.so
         i = sys.argv.index("--variant")
-        name, defs = sys.argv[i + 1], [a for a in sys.argv[i + 2:] if a != "--force"]
+        rest = [a for a in sys.argv[i + 2:] if a != "--force"]
+        only = [a[len("--only="):] for a in rest if a.startswith("--only=")] or None
+        name, defs = sys.argv[i + 1], [a for a in rest if not a.startswith("--only=")]
         print("built", build_lib(force=True, out=os.path.join(ROOT, "variants", name, "libopenair4g_amd.so"),
-                                 defines=defs))
+                                 defines=defs, only=only))
         sys.exit(0)
     build_lib(force="--force" in sys.argv, verbose=True)
     build_host_tools(verbose=True)

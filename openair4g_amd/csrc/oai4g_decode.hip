@@ -188,6 +188,10 @@ static __device__ __attribute__((noinline)) void log_map(short *sys, const short
   /* Every global operand of a step is loaded one chunk ahead into registers: the loads are
    * independent of the recursions, but the compiler cannot hoist them across the (possibly
    * aliasing) ext / checkpoint stores, so without this each step waits a full memory latency. */
+  /* a noinline function receives its arguments in VGPRs: re-establish that K and tf are wave-uniform,
+   * so the per-step bounds tests become scalar branches instead of exec-mask juggling */
+  K = __builtin_amdgcn_readfirstlane(K);
+  tf = __builtin_amdgcn_readfirstlane(tf);
   const uint32_t K1 = K >> 3, nseg = (K1 + TD_SEG - 1) / TD_SEG, lane = threadIdx.x & 63;
   uint4 *A5 = A + 64 * (nseg + 1);             /* first-run alpha(5) */
   short g11, g10;

@@ -322,7 +322,10 @@ static __device__ __forceinline__ void idft2048_unit(uint32_t *lds, int t, bool 
   /* pass A: leaves */
   if (active) {
     prod(x);
-    const uint32_t wo = 2u * (t & 31) + ((t >> 5) & 1) + 64u * (t >> 6);
+#ifndef OAI4G_DIAG_PASSA
+#define OAI4G_DIAG_PASSA 0   /* timing diagnostic only: 1 = pass-A stores at bank-distinct (wrong) words */
+#endif
+    const uint32_t wo = OAI4G_DIAG_PASSA ? (uint32_t)t : 2u * (t & 31) + ((t >> 5) & 1) + 64u * (t >> 6);
 #pragma unroll
     for (int a = 0; a < NA; a++) {
       idft16_reg(x[a], tw.l16);
@@ -939,11 +942,21 @@ __global__ void __launch_bounds__(128) MODOFDM_ATTR k_modofdm(const cfg_dev_t *_
               if constexpr (MODE == 1) v1[n] = *(const uint16_t *)(sb0 + a + 2);
               if constexpr (CW2) v1[n] = *(const uint16_t *)(sb1 + a);
             }
+#ifndef OAI4G_DIAG_QTAB
+#define OAI4G_DIAG_QTAB 0    /* timing diagnostic only: 1 = QAM-table reads at lane-distinct banks (wrong values) */
+#endif
+#if OAI4G_DIAG_QTAB
+            const uint32_t qkeep = c->with_crs ? 0xFFFFFFFFu : 0u, qlane = ((uint32_t)threadIdx.x & 31u) << 2;
+#define QADDR(x) (((x) & qkeep) | (qlane & ~qkeep))
+#else
+#define QADDR(x) (x)
+#endif
 #pragma unroll
             for (int n = 0; n < GZ; n++) {
-              v0[n] = *(const uint32_t *)(qb + v0[n]);
-              if constexpr (MODE == 1 || CW2) v1[n] = *(const uint32_t *)(qb + v1[n]);
+              v0[n] = *(const uint32_t *)(qb + QADDR(v0[n]));
+              if constexpr (MODE == 1 || CW2) v1[n] = *(const uint32_t *)(qb + QADDR(v1[n]));
             }
+#undef QADDR
 #pragma unroll
             for (int n = 0; n < GZ; n++) {
               const int i = act(g + n);
