@@ -22,6 +22,8 @@
  */
 #include "oai4g_internal.h"
 
+#include <type_traits>
+
 typedef const __attribute__((address_space(1))) int16_t gs16_t;
 
 static __device__ __forceinline__ short sadd(short a, short b) { return __builtin_elementwise_add_sat(a, b); }
@@ -29,17 +31,34 @@ static __device__ __forceinline__ short ssub(short a, short b) { return __builti
 
 #define TD_MAXH 128    /* MAX / 2 */
 #ifndef TD_FS
-#define TD_FS 16             /* forward chunk (steps whose operands are loaded one chunk ahead) */
+#define TD_FS 12             /* forward chunk (steps whose operands are loaded one chunk ahead); a multiple of 3
+                                (the metric layouts rotate with period 3) */
 #endif
 #ifndef TD_FSG
-#define TD_FSG 4             /* forward chunk of the gathered forms (two loads deep: pi, then the gather;
-                                measured best of 2 / 4 / 6 / 8 / 12 / 16 at C5) */
+#define TD_FSG 3             /* forward chunk of the gathered forms (two loads deep: pi, then the gather);
+                                round 2 measured 4 best of 2 / 4 / 6 / 8 / 12 / 16 with the fixed layout */
 #endif
 #ifndef TD_XR
 #define TD_XR 32      /* steps per round of the exchange gathers (index loads, then gathers, in flight) */
 #endif
 #ifndef TD_SEG
-#define TD_SEG 4      /* alpha checkpoint interval (steps); measured best of 2/4/8/16 at C5 (with TD_FS = 16) */
+#define TD_SEG 6      /* alpha checkpoint interval (steps), a multiple of 3 so every checkpoint holds layout EO
+                         (round 2 measured 4 best of 2/4/8/16 with the fixed layout) */
+#endif
+static_assert(TD_FS % 3 == 0 && TD_FSG % 3 == 0, "layout period");
+/* TD_SEG == 6: every checkpoint holds layout EO, and the re-run's alpha(0..5) fill exactly segment 0
+ * (alpha(6) onward continue the first run); 12 spills */
+static_assert(TD_SEG == 6, "checkpoint interval");
+
+/* log_map is not inlined: explicit address spaces keep its scratch accesses global_* / ds_* (a flat
+ * access counts on both vmcnt and lgkmcnt and returns out of order, so every wait on one would drain
+ * all loads in flight, the one-segment-ahead operand loads included) */
+#ifdef TD_NOAS
+#define TD_G
+#define TD_L
+#else
+#define TD_G __attribute__((address_space(1)))
+#define TD_L __attribute__((address_space(3)))
 #endif
 
 struct td_blk_t {      /* one wave's scratch: the 8 blocks interleaved, element i of block g at
@@ -89,6 +108,22 @@ static __device__ __forceinline__ uint4 tm_pack(const tm_t &t)
 {
   return make_uint4(__builtin_bit_cast(uint32_t, t.v[0]), __builtin_bit_cast(uint32_t, t.v[1]),
                     __builtin_bit_cast(uint32_t, t.v[2]), __builtin_bit_cast(uint32_t, t.v[3]));
+}
+typedef uint32_t u4v __attribute__((ext_vector_type(4)));   /* checkpoint word in log_map's global / LDS arrays */
+static __device__ __forceinline__ u4v tm_packv(const tm_t &t)
+{
+  return (u4v){__builtin_bit_cast(uint32_t, t.v[0]), __builtin_bit_cast(uint32_t, t.v[1]),
+               __builtin_bit_cast(uint32_t, t.v[2]), __builtin_bit_cast(uint32_t, t.v[3])};
+}
+static __device__ __forceinline__ tm_t tm_unpack(u4v u)
+{
+  /* the elements go through scalars: clang's __builtin_bit_cast of an ext-vector element lvalue
+   * (u.y, u[1]) reads the vector's first element (measured on this toolchain) */
+  const uint32_t w0 = u.x, w1 = u.y, w2 = u.z, w3 = u.w;
+  tm_t t;
+  t.v[0] = __builtin_bit_cast(s2v, w0); t.v[1] = __builtin_bit_cast(s2v, w1);
+  t.v[2] = __builtin_bit_cast(s2v, w2); t.v[3] = __builtin_bit_cast(s2v, w3);
+  return t;
 }
 static __device__ __forceinline__ tm_t tm_unpack(uint4 u)
 {
@@ -152,11 +187,179 @@ static __device__ __forceinline__ short ext_of(const tm_t &a, const tm_t &b, sho
   return __builtin_elementwise_sub_sat(V.y, V.x);
 }
 
-static __device__ __forceinline__ void gamma_of(const short *sys, const short *par, uint32_t e, short &g11, short &g10)
+template <typename P, typename Q>
+static __device__ __forceinline__ void gamma_of(P sys, Q par, uint32_t e, short &g11, short &g10)
 {
   const short s = sys[e], p = par[e];
   g11 = (short)(sadd(s, p) >> 1);
   g10 = (short)(ssub(s, p) >> 1);
+}
+
+/* ======================================================================================
+ * Rotating metric layouts (round 4).  The 8 state metrics live in 4 packed int16 pairs; a
+ * step reads its operands as pairs of one register (the same register's halves, swapped or
+ * broadcast, cost nothing: VOP3P op_sel) only if the input layout matches the pairs the step
+ * forms.  No single layout does for every step, but three do in rotation:
+ *   EO = (0,2)(1,3)(4,6)(5,7),  N = (0,1)(2,3)(4,5)(6,7),  L2 = (0,4)(1,5)(2,6)(3,7).
+ * alpha (compute_alpha16): EO -> N -> L2 -> EO; beta (compute_beta16): L2 -> N -> EO -> L2;
+ * with alpha(k) in layout k mod 3 and beta(k) in layout k mod 3 (EO, N, L2) every extrinsic
+ * (compute_ext16) combines alpha(k) and beta(k + 1) in one of the pairs (EO, N), (N, L2),
+ * (L2, EO), each of which also has a register-local pairing.  What is left of the per-step
+ * permutes are the gamma constants with mixed signs: (g11, -g10) / (g10, -g11) or
+ * (g11, -g11) / (g10, -g10) on two steps of three, shared by the alpha, beta and extrinsic of
+ * the step.  Every saturating add / sub / max is still the reference's own, state by state.
+ * ==================================================================================== */
+enum { LY_EO = 0, LY_N = 1, LY_L2 = 2 };
+__host__ __device__ constexpr int ly_reg(int L, int s) { return L == LY_N ? s >> 1 : L == LY_EO ? (((s >> 2) << 1) | (s & 1)) : (s & 3); }
+__host__ __device__ constexpr int ly_half(int L, int s) { return L == LY_N ? (s & 1) : L == LY_EO ? ((s >> 1) & 1) : (s >> 2); }
+__host__ __device__ constexpr int ly_state(int L, int r, int h)
+{
+  return L == LY_N ? 2 * r + h : L == LY_EO ? (((r >> 1) << 2) | (h << 1) | (r & 1)) : r + 4 * h;
+}
+
+/* (x_I, x_J) of a metric vector held in layout L */
+template <int L, int I, int J>
+static __device__ __forceinline__ s2v ly_pair(const tm_t &t)
+{
+  constexpr int ri = ly_reg(L, I), rj = ly_reg(L, J), hi = ly_half(L, I), hj = ly_half(L, J);
+  if constexpr (ri == rj) return SHUF2(t.v[ri], t.v[ri], hi, hj);
+  else return SHUF2(t.v[ri], t.v[rj], hi, 2 + hj);
+}
+
+template <int LF, int LT>
+static __device__ __forceinline__ tm_t ly_conv(const tm_t &t)
+{
+  if constexpr (LF == LT) return t;
+  else {
+    tm_t o;
+    o.v[0] = ly_pair<LF, ly_state(LT, 0, 0), ly_state(LT, 0, 1)>(t);
+    o.v[1] = ly_pair<LF, ly_state(LT, 1, 0), ly_state(LT, 1, 1)>(t);
+    o.v[2] = ly_pair<LF, ly_state(LT, 2, 0), ly_state(LT, 2, 1)>(t);
+    o.v[3] = ly_pair<LF, ly_state(LT, 3, 0), ly_state(LT, 3, 1)>(t);
+    return o;
+  }
+}
+/* layout change with a run-time (wave-uniform) source layout */
+template <int LT>
+static __device__ __forceinline__ tm_t ly_conv_from(const tm_t &t, int lf)
+{
+  return lf == LY_EO ? ly_conv<LY_EO, LT>(t) : lf == LY_N ? ly_conv<LY_N, LT>(t) : ly_conv<LY_L2, LT>(t);
+}
+template <int LF>
+static __device__ __forceinline__ tm_t ly_conv_to(const tm_t &t, int lt)
+{
+  return lt == LY_EO ? ly_conv<LF, LY_EO>(t) : lt == LY_N ? ly_conv<LF, LY_N>(t) : ly_conv<LF, LY_L2>(t);
+}
+
+struct gk_t { s2v gg, ng; };    /* (g11, g10) and (-g11, -g10) (int16 wrap; |g| <= 16384) */
+static __device__ __forceinline__ gk_t gk_of(uint32_t ggw)
+{
+  const s2v g = __builtin_bit_cast(s2v, ggw);
+  return {g, (s2v){0, 0} - g};
+}
+static __device__ __forceinline__ uint32_t gg_of(short sy, short pa)   /* compute_gamma16: (s + p) >> 1, (s - p) >> 1 */
+{
+  const short g11 = (short)(sadd(sy, pa) >> 1), g10 = (short)(ssub(sy, pa) >> 1);
+  return (uint32_t)(uint16_t)g11 | ((uint32_t)(uint16_t)g10 << 16);
+}
+/* the constant pair (g_A, SB g_B), A / B = 11 or 10 */
+template <int GA, int GB, int SB>
+static __device__ __forceinline__ s2v kpair(const gk_t &k)
+{
+  constexpr int ha = GA == 11 ? 0 : 1, hb = GB == 11 ? 0 : 1;
+  if constexpr (SB > 0) return SHUF2(k.gg, k.gg, ha, hb);
+  else return SHUF2(k.gg, k.ng, ha, 2 + hb);
+}
+
+/* the recursions as r_s = max(x[U_s] + S_s g_s, x[W_s] - S_s g_s):
+ *   alpha (compute_alpha16 :286-367): U = 1 3 5 7 1 3 5 7, W = U - 1, S = + - + - - + - +, g = 11 10 10 11 11 10 10 11
+ *   beta (compute_beta16 :588-685):   U = 4 4 5 5 6 6 7 7, W = U - 4, S = + - - + + - - +, g = 11 11 10 10 10 10 11 11 */
+__host__ __device__ constexpr int tr_u(bool beta, int s) { return beta ? 4 + (s >> 1) : 2 * (s & 3) + 1; }
+__host__ __device__ constexpr int tr_w(bool beta, int s) { return beta ? (s >> 1) : 2 * (s & 3); }
+__host__ __device__ constexpr int tr_s(bool beta, int s) { return (beta ? ((s ^ (s >> 1)) & 1) : ((s & 1) ^ (s >> 2))) ? -1 : 1; }
+__host__ __device__ constexpr int tr_g(bool beta, int s) { return beta ? (((s + 2) & 7) < 4 ? 11 : 10) : (((s & 3) == 0 || (s & 3) == 3) ? 11 : 10); }
+
+/* output register O of a step: the constant is taken with a positive first lane, the adds / subs
+ * swapped when S is negative there (x - c == x + (-c) under saturation for |c| <= 16384) */
+template <bool BETA, int LIN, int LOUT, int O>
+static __device__ __forceinline__ s2v tpair(const tm_t &x, const gk_t &k)
+{
+  constexpr int sa = ly_state(LOUT, O, 0), sb = ly_state(LOUT, O, 1);
+  constexpr int sga = tr_s(BETA, sa), sgb = tr_s(BETA, sb);
+  const s2v U = ly_pair<LIN, tr_u(BETA, sa), tr_u(BETA, sb)>(x);
+  const s2v W = ly_pair<LIN, tr_w(BETA, sa), tr_w(BETA, sb)>(x);
+  const s2v C = kpair<tr_g(BETA, sa), tr_g(BETA, sb), sga * sgb>(k);
+  if constexpr (sga > 0) return max2(adds2(U, C), subs2(W, C));
+  else return max2(subs2(U, C), adds2(W, C));
+}
+/* one recursion step LIN -> LOUT, normalised by the maximum (the reference's minus max) */
+template <bool BETA, int LIN, int LOUT>
+static __device__ __forceinline__ void tstep(tm_t &x, const gk_t &k)
+{
+  const s2v r0 = tpair<BETA, LIN, LOUT, 0>(x, k), r1 = tpair<BETA, LIN, LOUT, 1>(x, k);
+  const s2v r2 = tpair<BETA, LIN, LOUT, 2>(x, k), r3 = tpair<BETA, LIN, LOUT, 3>(x, k);
+  const s2v m = max2(max2(r0, r1), max2(r2, r3)), mm = max2(m, SHUF2(m, m, 1, 0));
+  x.v[0] = subs2(r0, mm); x.v[1] = subs2(r1, mm); x.v[2] = subs2(r2, mm); x.v[3] = subs2(r3, mm);
+}
+template <int P> static __device__ __forceinline__ void alpha_ph(tm_t &a, const gk_t &k) { tstep<false, P, (P + 1) % 3>(a, k); }
+template <int P> static __device__ __forceinline__ void beta_ph(tm_t &b, const gk_t &k) { tstep<true, P, (P + 2) % 3>(b, k); }
+
+/* one packed term pair (a_I + b_J, a_I2 + b_J2) */
+template <int LA, int LB, int I, int J, int I2, int J2>
+static __device__ __forceinline__ s2v eterm(const tm_t &a, const tm_t &b)
+{
+  return adds2(ly_pair<LA, I, I2>(a), ly_pair<LB, J, J2>(b));
+}
+/* compute_ext16 (:733-875) from alpha(k) in layout P and beta(k + 1) in layout (P + 1) mod 3:
+ * m00 = max(a0+b0, a1+b4, a6+b7, a7+b3) - g11, m11 = max(a0+b4, a1+b0, a6+b3, a7+b7) + g11,
+ * m01 = max(a2+b5, a3+b1, a4+b2, a5+b6) - g10, m10 = max(a2+b1, a3+b5, a4+b6, a5+b2) + g10,
+ * ext = max(m10, m11) - max(m01, m00); each packed term takes both its operands from one
+ * register of its layout (pairings searched once for the three layout pairs) */
+template <int P>
+static __device__ __forceinline__ short ext_ph(const tm_t &a, const tm_t &b, const gk_t &k)
+{
+  constexpr int LA = P, LB = (P + 1) % 3;
+  if constexpr (P == LY_EO) {             /* (m00, m10) and (m01, m11) */
+    const s2v X = max2(max2(eterm<LA, LB, 0, 0, 2, 1>(a, b), eterm<LA, LB, 1, 4, 3, 5>(a, b)),
+                       max2(eterm<LA, LB, 6, 7, 4, 6>(a, b), eterm<LA, LB, 7, 3, 5, 2>(a, b)));
+    const s2v Y = max2(max2(eterm<LA, LB, 2, 5, 0, 4>(a, b), eterm<LA, LB, 3, 1, 1, 0>(a, b)),
+                       max2(eterm<LA, LB, 4, 2, 6, 3>(a, b), eterm<LA, LB, 5, 6, 7, 7>(a, b)));
+    const s2v V = max2(subs2(X, kpair<11, 10, -1>(k)), subs2(Y, kpair<10, 11, -1>(k)));   /* (max(m00, m01), max(m10, m11)) */
+    return __builtin_elementwise_sub_sat(V.y, V.x);
+  } else if constexpr (P == LY_N) {       /* (m00, m11) and (m01, m10) */
+    const s2v X = max2(max2(eterm<LA, LB, 0, 0, 0, 4>(a, b), eterm<LA, LB, 1, 4, 1, 0>(a, b)),
+                       max2(eterm<LA, LB, 6, 7, 6, 3>(a, b), eterm<LA, LB, 7, 3, 7, 7>(a, b)));
+    const s2v Y = max2(max2(eterm<LA, LB, 2, 5, 2, 1>(a, b), eterm<LA, LB, 3, 1, 3, 5>(a, b)),
+                       max2(eterm<LA, LB, 4, 2, 4, 6>(a, b), eterm<LA, LB, 5, 6, 5, 2>(a, b)));
+    const s2v V = max2(subs2(X, kpair<11, 11, -1>(k)), subs2(Y, kpair<10, 10, -1>(k)));   /* (max(m00, m01), max(m11, m10)) */
+    return __builtin_elementwise_sub_sat(V.y, V.x);
+  } else {                                /* (m00, m01) and (m10, m11) */
+    const s2v X = max2(max2(eterm<LA, LB, 0, 0, 4, 2>(a, b), eterm<LA, LB, 1, 4, 5, 6>(a, b)),
+                       max2(eterm<LA, LB, 6, 7, 2, 5>(a, b), eterm<LA, LB, 7, 3, 3, 1>(a, b)));
+    const s2v Y = max2(max2(eterm<LA, LB, 2, 1, 6, 3>(a, b), eterm<LA, LB, 3, 5, 7, 7>(a, b)),
+                       max2(eterm<LA, LB, 4, 6, 0, 4>(a, b), eterm<LA, LB, 5, 2, 1, 0>(a, b)));
+    const s2v Xg = subs2(X, kpair<11, 10, 1>(k)), Yg = adds2(Y, kpair<10, 11, 1>(k));
+    const s2v Xm = max2(Xg, SHUF2(Xg, Xg, 1, 0)), Ym = max2(Yg, SHUF2(Yg, Yg, 1, 0));
+    return __builtin_elementwise_sub_sat(Ym.x, Xm.x);
+  }
+}
+
+/* compile-time loop (the layout phase of step J is J mod 3) */
+template <int B, int E, class F>
+static __device__ __forceinline__ void sfor(F &&f)
+{
+  if constexpr (B < E) {
+    f(std::integral_constant<int, B>{});
+    sfor<B + 1, E>(f);
+  }
+}
+template <int B, int E, class F>      /* E - 1 down to B */
+static __device__ __forceinline__ void sfor_down(F &&f)
+{
+  if constexpr (B < E) {
+    f(std::integral_constant<int, E - 1>{});
+    sfor_down<B, E - 1>(f);
+  }
 }
 
 /*
@@ -181,32 +384,35 @@ static __device__ __forceinline__ void gamma_of(const short *sys, const short *p
  * exchange passes and their re-reads of the exchanged stream disappear. */
 enum { TD_SRC_SYS = 0, TD_SRC_INTL = 1, TD_SRC_DINT = 2 };
 template <bool POST, int SRC>
-static __device__ __attribute__((noinline)) void log_map(short *sys, const short *par, short *ext, uint4 *A, uint32_t K,
-                                               uint32_t q, int tf, uint4 *asave /* [6][64] */, const short *s0,
-                                               const short *gsrc, const uint16_t *pi)
+static __device__ __attribute__((noinline)) void log_map(TD_G short *sys, TD_G const short *par, TD_G short *ext,
+                                               TD_G u4v *A, uint32_t K, uint32_t q, int tf,
+                                               TD_L u4v *asave /* [6][64] */, TD_G const short *s0,
+                                               TD_G const short *gsrc, TD_G const uint16_t *pi)
 {
-  /* Every global operand of a step is loaded one chunk ahead into registers: the loads are
-   * independent of the recursions, but the compiler cannot hoist them across the (possibly
-   * aliasing) ext / checkpoint stores, so without this each step waits a full memory latency. */
   /* a noinline function receives its arguments in VGPRs: re-establish that K and tf are wave-uniform,
    * so the per-step bounds tests become scalar branches instead of exec-mask juggling */
   K = __builtin_amdgcn_readfirstlane(K);
   tf = __builtin_amdgcn_readfirstlane(tf);
+  /* Every global operand of a step is loaded one chunk ahead into registers: the loads are
+   * independent of the recursions, but the compiler cannot hoist them across the (possibly
+   * aliasing) ext / checkpoint stores, so without this each step waits a full memory latency. */
   const uint32_t K1 = K >> 3, nseg = (K1 + TD_SEG - 1) / TD_SEG, lane = threadIdx.x & 63;
-  uint4 *A5 = A + 64 * (nseg + 1);             /* first-run alpha(5) */
-  short g11, g10;
-  /* forward, first run, in chunks of FS steps (operands of the next chunk in flight) */
+  const int pK = (int)(K1 % 3);                /* layout of alpha(K1) and beta(K1) */
+  /* forward, first run, in chunks of FS steps (operands of the next chunk in flight); alpha(k) is
+   * in layout k mod 3 (alpha(0) EO: tm_init puts state 0 at register 0's low half in every layout) */
   constexpr int FS = SRC == TD_SRC_SYS ? TD_FS : TD_FSG;
   const uint32_t nfc = (K1 + FS - 1) / FS;
   tm_t a = tm_init(q == 0);
   {
-    s2v nsp[FS];                                /* (sys, par) of the next chunk */
+    /* operands stay one 16-bit value per register until their step: packing two loads into one
+     * register right after they are issued would wait on them there, a memory latency per chunk */
+    short nsy[FS], npa[FS];                     /* sys, par of the next chunk */
     uint32_t nix[FS];                           /* gathered forms: pi of the chunk after next */
-    s2v nez[FS];                                /* TD_SRC_DINT: (ext, s0) of the next chunk */
+    short nex[FS], nzs[FS];                     /* TD_SRC_DINT: ext, s0 of the next chunk */
     auto pix = [&](uint32_t k) { return (uint32_t)pi[8 * (k < K1 ? k : K1 - 1) + q]; };
     if constexpr (SRC == TD_SRC_SYS) {
 #pragma unroll
-      for (int j = 0; j < FS; j++) nsp[j] = (s2v){sys[64 * j + q], par[64 * j + q]};
+      for (int j = 0; j < FS; j++) { nsy[j] = sys[64 * j + q]; npa[j] = par[64 * j + q]; }
     } else {
       uint32_t ix0[FS];
 #pragma unroll
@@ -214,26 +420,25 @@ static __device__ __attribute__((noinline)) void log_map(short *sys, const short
 #pragma unroll
       for (int j = 0; j < FS; j++) nix[j] = pix(FS + j);
 #pragma unroll
-      for (int j = 0; j < FS; j++) nsp[j] = (s2v){gsrc[td_ix(ix0[j])], par[64 * j + q]};
+      for (int j = 0; j < FS; j++) { nsy[j] = gsrc[td_ix(ix0[j])]; npa[j] = par[64 * j + q]; }
       if constexpr (SRC == TD_SRC_DINT) {
 #pragma unroll
-        for (int j = 0; j < FS; j++) nez[j] = (s2v){ext[64 * j + q], s0[64 * j + q]};
+        for (int j = 0; j < FS; j++) { nex[j] = ext[64 * j + q]; nzs[j] = s0[64 * j + q]; }
       }
     }
     for (uint32_t c = 0; c < nfc; c++) {
-      s2v csp[FS];
-      s2v cez[FS];
+      short csy[FS], cpa[FS], cex[FS], czs[FS];
 #pragma unroll
-      for (int j = 0; j < FS; j++) csp[j] = nsp[j];
+      for (int j = 0; j < FS; j++) { csy[j] = nsy[j]; cpa[j] = npa[j]; }
       if constexpr (SRC == TD_SRC_DINT) {
 #pragma unroll
-        for (int j = 0; j < FS; j++) cez[j] = nez[j];
+        for (int j = 0; j < FS; j++) { cex[j] = nex[j]; czs[j] = nzs[j]; }
       }
       if (c + 1 < nfc) {
         const uint32_t b = 64 * FS * (c + 1) + q;
         if constexpr (SRC == TD_SRC_SYS) {
 #pragma unroll
-          for (int j = 0; j < FS; j++) nsp[j] = (s2v){sys[b + 64 * j], par[b + 64 * j]};
+          for (int j = 0; j < FS; j++) { nsy[j] = sys[b + 64 * j]; npa[j] = par[b + 64 * j]; }
         } else {
           uint32_t ix[FS];
 #pragma unroll
@@ -241,29 +446,29 @@ static __device__ __attribute__((noinline)) void log_map(short *sys, const short
 #pragma unroll
           for (int j = 0; j < FS; j++) nix[j] = pix(FS * (c + 2) + j);
 #pragma unroll
-          for (int j = 0; j < FS; j++) nsp[j] = (s2v){gsrc[td_ix(ix[j])], par[b + 64 * j]};
+          for (int j = 0; j < FS; j++) { nsy[j] = gsrc[td_ix(ix[j])]; npa[j] = par[b + 64 * j]; }
           if constexpr (SRC == TD_SRC_DINT) {
 #pragma unroll
-            for (int j = 0; j < FS; j++) nez[j] = (s2v){ext[b + 64 * j], s0[b + 64 * j]};
+            for (int j = 0; j < FS; j++) { nex[j] = ext[b + 64 * j]; nzs[j] = s0[b + 64 * j]; }
           }
         }
       }
-#pragma unroll
-      for (int j = 0; j < FS; j++) {
+      const bool full = c * FS + FS <= K1;     /* uniform: only the last chunk may be partial */
+      sfor<0, FS>([&](auto J) {
+        constexpr int j = decltype(J)::value;
         const uint32_t k = c * FS + j;
-        if (k < K1) {
-          if constexpr (SRC == TD_SRC_DINT) csp[j].x = sadd(ssub(csp[j].x, cez[j].x), cez[j].y);
-          if constexpr (SRC != TD_SRC_SYS) sys[64 * k + q] = csp[j].x;
-          alpha_step(a, (short)(sadd(csp[j].x, csp[j].y) >> 1), (short)(ssub(csp[j].x, csp[j].y) >> 1));
-          if (k + 1 == 5) A5[q] = tm_pack(a);
-          if (((k + 1) & (TD_SEG - 1)) == 0) A[64 * ((k + 1) / TD_SEG) + q] = tm_pack(a);
+        if (full || k < K1) {
+          if constexpr (SRC == TD_SRC_DINT) csy[j] = sadd(ssub(csy[j], cex[j]), czs[j]);
+          if constexpr (SRC != TD_SRC_SYS) sys[64 * k + q] = csy[j];
+          alpha_ph<j % 3>(a, gk_of(gg_of(csy[j], cpa[j])));
+          if ((k + 1) % TD_SEG == 0) A[64 * ((k + 1) / TD_SEG) + q] = tm_packv(a);   /* layout EO */
         }
-      }
+      });
     }
   }
   /* forward re-run over L/8 steps from the previous window's final alpha; its alpha(0) is
-   * checkpoint 0, alpha(1..5) are recomputed from it */
-  const tm_t fin = a;
+   * checkpoint 0, alpha(1..5) are recomputed from it (TD_SEG > 5: no checkpoint inside) */
+  const tm_t fin = a;                          /* alpha(K1), layout pK */
   {
     const tm_t z = tm_init(true);
 #pragma unroll
@@ -271,15 +476,14 @@ static __device__ __attribute__((noinline)) void log_map(short *sys, const short
       const uint32_t up = (uint32_t)__shfl_up((int)__builtin_bit_cast(uint32_t, a.v[v]), 1, 8);
       a.v[v] = q == 0 ? z.v[v] : __builtin_bit_cast(s2v, up);
     }
+    a = ly_conv_from<LY_EO>(a, pK);            /* (z is the same in every layout) */
   }
-  A[q] = tm_pack(a);
-  for (uint32_t k = 0; k < 5; k++) {
-    gamma_of(sys, par, 64 * k + q, g11, g10);
-    alpha_step(a, g11, g10);
-    /* checkpoints inside the re-run range hold re-run values (alpha(1..5) of the reference) */
-    if (((k + 1) & (TD_SEG - 1)) == 0 && k + 1 <= K1) A[64 * ((k + 1) / TD_SEG) + q] = tm_pack(a);
-  }
-  /* termination betas of the last window (compute_beta16 :467-521, int16 wrap arithmetic) */
+  A[q] = tm_packv(a);
+  sfor<0, 5>([&](auto J) {
+    constexpr int k = decltype(J)::value;
+    alpha_ph<k % 3>(a, gk_of(gg_of(sys[64 * k + q], par[64 * k + q])));
+  });
+  /* termination betas of the last window (compute_beta16 :467-521, int16 wrap arithmetic), layout N */
   tm_t t;
   {
     short m[3], mm[3], tv[8];
@@ -298,84 +502,129 @@ static __device__ __attribute__((noinline)) void log_map(short *sys, const short
   }
   /* backward, first run: seeded with the lane's own final alpha as the reference stores it
    * after the re-run (the re-run reaches step K1 when K1 == 5); extrinsic of steps whose beta
-   * the re-run does not touch.  Segment operands (sys, par, s0, checkpoint) one segment ahead. */
-  tm_t b = q == 7 ? t : (K1 == 5 ? a : fin);
+   * the re-run does not touch.  beta(k) is in layout k mod 3, so beta(K1) shares alpha(K1)'s.
+   * Segment operands (sys, par, s0, checkpoint) one segment ahead. */
+  tm_t b = q == 7 ? ly_conv_to<LY_N>(t, pK) : (K1 == 5 ? a : fin);
   const int kr = (int)K1 - 6;                 /* steps >= kr take their extrinsic from the re-run */
-  const uint4 a5v = A5[q];
-  s2v nsp[TD_SEG], nzz[TD_SEG / 2];            /* (sys, par) and (POST) s0 pairs of the next segment */
-  uint4 nA;
+  const int nfast = kr > 0 ? kr / TD_SEG : 0;  /* segments [0, nfast) lie wholly below kr */
+  short nsy[TD_SEG], npa[TD_SEG], nzs[TD_SEG]; /* sys, par and (POST) s0 of the next segment */
+  u4v nA;
   auto fetch = [&](int seg) {
     const uint32_t b0 = 64u * (uint32_t)(seg * TD_SEG) + q;
 #pragma unroll
-    for (int j = 0; j < TD_SEG; j++) nsp[j] = (s2v){sys[b0 + 64 * j], par[b0 + 64 * j]};
+    for (int j = 0; j < TD_SEG; j++) { nsy[j] = sys[b0 + 64 * j]; npa[j] = par[b0 + 64 * j]; }
     if constexpr (POST) {
 #pragma unroll
-      for (int i = 0; i < TD_SEG / 2; i++) nzz[i] = (s2v){s0[b0 + 128 * i], s0[b0 + 128 * i + 64]};
+      for (int j = 0; j < TD_SEG; j++) nzs[j] = s0[b0 + 64 * j];
     }
     nA = A[64 * seg + q];
   };
+  /* a segment's operands in registers: gammas, and (POST) its sys and s0 */
+  struct segops_t {
+    uint32_t gg[TD_SEG];                       /* g11 | g10 << 16 */
+    short ss[TD_SEG], zz[TD_SEG];
+  };
+  auto take = [&](segops_t &o) {
+#pragma unroll
+    for (int j = 0; j < TD_SEG; j++) {
+      o.gg[j] = gg_of(nsy[j], npa[j]);
+      o.ss[j] = nsy[j];
+      o.zz[j] = nzs[j];
+    }
+  };
+  /* extrinsic of step k0 + j from alpha (layout j mod 3) and beta(k0 + j + 1) */
+  auto emit = [&](auto J, const segops_t &o, const u4v &al, int k0) {
+    constexpr int j = decltype(J)::value;
+    short v = ext_ph<j % 3>(tm_unpack(al), b, gk_of(o.gg[j]));
+    if constexpr (POST) {
+      v = __builtin_elementwise_add_sat(__builtin_elementwise_sub_sat(v, o.ss[j]), o.zz[j]);
+    }
+    ext[64 * (k0 + j) + q] = v;
+  };
   fetch((int)nseg - 1);
-  for (int seg = (int)nseg - 1; seg >= 0; seg--) {
+  /* top segments (partial, or holding steps >= kr): guarded steps, alpha recompute then beta */
+  for (int seg = (int)nseg - 1; seg >= nfast; seg--) {
     const int k0 = seg * TD_SEG, n = min((int)TD_SEG, (int)K1 - k0);
     /* a partial last segment reads padding past K1 (the arrays have TD_SEG steps of slack) and
      * leaves beta untouched for those steps */
-    s2v css[TD_SEG / 2], czz[TD_SEG / 2];      /* sys and s0 of the segment's steps, pairwise */
-    uint4 al[TD_SEG];
-    uint32_t gg[TD_SEG];                       /* g11 | g10 << 16 */
-    tm_t c = tm_unpack(nA);
-#pragma unroll
-    for (int j = 0; j < TD_SEG; j++) {
-      const short x11 = (short)(sadd(nsp[j].x, nsp[j].y) >> 1), x10 = (short)(ssub(nsp[j].x, nsp[j].y) >> 1);
-      gg[j] = (uint16_t)x11 | ((uint32_t)(uint16_t)x10 << 16);
-    }
-#pragma unroll
-    for (int i = 0; i < TD_SEG / 2; i++) {
-      css[i] = (s2v){nsp[2 * i].x, nsp[2 * i + 1].x};
-      czz[i] = nzz[i];
-    }
+    segops_t o;
+    u4v al[TD_SEG];
+    tm_t c = tm_unpack(nA);                    /* alpha(k0), layout EO */
+    take(o);
     if (seg > 0) fetch(seg - 1);
-#pragma unroll
-    for (int j = 0; j < TD_SEG; j++) {
-      const short x11 = (short)gg[j], x10 = (short)(gg[j] >> 16);
-      al[j] = tm_pack(c);
-      if (k0 + j == 5) c = tm_unpack(a5v);               /* alpha(6) continues the first run */
-      alpha_step(c, x11, x10);
-    }
-#pragma unroll
-    for (int j = TD_SEG - 1; j >= 0; j--) {
-      const int k = k0 + j;
-      const short x11 = (short)gg[j], x10 = (short)(gg[j] >> 16);
+    sfor<0, TD_SEG>([&](auto J) {
+      constexpr int j = decltype(J)::value;
+      al[j] = tm_packv(c);
+      alpha_ph<j % 3>(c, gk_of(o.gg[j]));
+    });
+    sfor_down<0, TD_SEG>([&](auto J) {
+      constexpr int j = decltype(J)::value;
       if (j < n) {
-        if (k < kr) {
-          short v = ext_of(tm_unpack(al[j]), b, x11, x10);
-          if constexpr (POST) {
-            const short sv = (j & 1) ? css[j >> 1].y : css[j >> 1].x, zv = (j & 1) ? czz[j >> 1].y : czz[j >> 1].x;
-            v = __builtin_elementwise_add_sat(__builtin_elementwise_sub_sat(v, sv), zv);
-          }
-          ext[64 * k + q] = v;
-        } else {
-          asave[(k - kr) * 64 + lane] = al[j];
-        }
+        const int k = k0 + j;
+        if (k < kr) emit(J, o, al[j], k0);
+        else asave[(k - kr) * 64 + lane] = al[j];   /* layout k mod 3 */
+        beta_ph<(j + 1) % 3>(b, gk_of(o.gg[j]));      /* beta(k + 1) -> beta(k) */
       }
-      tm_t nb = b;
-      beta_step(nb, x11, x10);
-#pragma unroll
-      for (int v = 0; v < 4; v++) b.v[v] = j < n ? nb.v[v] : b.v[v];
-    }
+    });
   }
-  /* backward re-run over the last L/8 steps from the next window's beta[0] */
+  /* full segments below kr, software-pipelined: the beta / extrinsic steps of segment seg
+   * interleave with the alpha recompute of segment seg - 1 (two independent dependency chains
+   * per lane); operands two segments ahead */
+  if (nfast > 0) {
+    segops_t cur, nx;
+    u4v alc[TD_SEG], aln[TD_SEG];
+    {
+      tm_t c = tm_unpack(nA);
+      take(cur);
+      if (nfast > 1) fetch(nfast - 2);
+      sfor<0, TD_SEG>([&](auto J) {
+        constexpr int j = decltype(J)::value;
+        alc[j] = tm_packv(c);
+        alpha_ph<j % 3>(c, gk_of(cur.gg[j]));
+      });
+    }
+    for (int seg = nfast - 1; seg >= 1; seg--) {
+      const int k0 = seg * TD_SEG;
+      tm_t c = tm_unpack(nA);                  /* alpha((seg - 1) TD_SEG) */
+      take(nx);
+      if (seg > 1) fetch(seg - 2);
+      sfor<0, TD_SEG>([&](auto J) {
+        constexpr int j = decltype(J)::value;
+        constexpr int jj = TD_SEG - 1 - j;
+        aln[j] = tm_packv(c);
+        alpha_ph<j % 3>(c, gk_of(nx.gg[j]));
+        emit(std::integral_constant<int, jj>{}, cur, alc[jj], k0);
+        beta_ph<(jj + 1) % 3>(b, gk_of(cur.gg[jj]));
+      });
+      cur = nx;
+#pragma unroll
+      for (int j = 0; j < TD_SEG; j++) alc[j] = aln[j];
+    }
+    sfor_down<0, TD_SEG>([&](auto J) {
+      constexpr int j = decltype(J)::value;
+      emit(J, cur, alc[j], 0);
+      beta_ph<(j + 1) % 3>(b, gk_of(cur.gg[j]));
+    });
+  }
+  /* backward re-run over the last L/8 steps from the next window's beta[0] (layout EO), in the
+   * fixed layout N (alpha_step / beta_step / ext_of): 6 steps per call */
+  tm_t bn;
 #pragma unroll
   for (int v = 0; v < 4; v++) {
     const uint32_t dn = (uint32_t)__shfl_down((int)__builtin_bit_cast(uint32_t, b.v[v]), 1, 8);
-    b.v[v] = q == 7 ? t.v[v] : __builtin_bit_cast(s2v, dn);
+    bn.v[v] = __builtin_bit_cast(s2v, dn);
   }
+  bn = ly_conv<LY_EO, LY_N>(bn);
+  if (q == 7) bn = t;
   for (int k = (int)K1 - 1; k >= kr && k >= 0; k--) {
     const uint32_t e = 64 * k + q;
+    short g11, g10;
     gamma_of(sys, par, e, g11, g10);
-    short v = ext_of(tm_unpack(asave[(k - kr) * 64 + lane]), b, g11, g10);
+    const tm_t av = ly_conv_from<LY_N>(tm_unpack(asave[(k - kr) * 64 + lane]), k % 3);
+    short v = ext_of(av, bn, g11, g10);
     if constexpr (POST) v = __builtin_elementwise_add_sat(__builtin_elementwise_sub_sat(v, sys[e]), s0[e]);
     ext[e] = v;
-    if (k >= (int)K1 - 5) beta_step(b, g11, g10);
+    if (k >= (int)K1 - 5) beta_step(bn, g11, g10);
   }
 }
 
@@ -459,12 +708,15 @@ __global__ void __launch_bounds__(64) k_td16(int n_cb, uint32_t K, const int16_t
   }
   __syncthreads();
   bool active = valid && max_it > 0;
-  if (valid) log_map<false, TD_SRC_SYS>(B.s0, B.yp1, B.ext, B.A, K, q, 0, asave, B.s0, nullptr, nullptr);
+  if (valid) log_map<false, TD_SRC_SYS>((TD_G short *)B.s0, (TD_G short *)B.yp1, (TD_G short *)B.ext, (TD_G u4v *)B.A, K, q, 0,
+                                        (TD_L u4v *)asave, (TD_G short *)B.s0, nullptr, nullptr);
   __syncthreads();
   uint32_t it = 0;
   for (it = 1; it <= max_it; it++) {
     /* decoder 2 takes ext[pi4] straight from decoder 1's output (interleave exchange fused) */
-    if (active) log_map<false, TD_SRC_INTL>(B.s2, B.yp2, B.ext2, B.A, K, q, 1, asave, B.s0, B.ext, pi4);
+    if (active) log_map<false, TD_SRC_INTL>((TD_G short *)B.s2, (TD_G short *)B.yp2, (TD_G short *)B.ext2, (TD_G u4v *)B.A, K, q,
+                                                  1, (TD_L u4v *)asave, (TD_G short *)B.s0, (TD_G short *)B.ext,
+                                                  (TD_G const uint16_t *)pi4);
     __syncthreads();
     if (active && it > 1) {
       for (uint32_t i0 = q; i0 < Kb; i0 += 8 * (TD_XR / 8)) {   /* hard decisions (:1267-1283), MSB first */
@@ -504,7 +756,9 @@ __global__ void __launch_bounds__(64) k_td16(int n_cb, uint32_t K, const int16_t
     __syncthreads();
     if (active && done_it[g]) active = false;
     /* decoder 1 takes ext2[pi5] - ext + s0 (deinterleave + update fused) */
-    if (active && it < max_it) log_map<true, TD_SRC_DINT>(B.s1, B.yp1, B.ext, B.A, K, q, 0, asave, B.s0, B.ext2, pi5);
+    if (active && it < max_it) log_map<true, TD_SRC_DINT>((TD_G short *)B.s1, (TD_G short *)B.yp1, (TD_G short *)B.ext, (TD_G u4v *)B.A,
+                                                            K, q, 0, (TD_L u4v *)asave, (TD_G short *)B.s0,
+                                                            (TD_G short *)B.ext2, (TD_G const uint16_t *)pi5);
     __syncthreads();
     if (!__any(active)) break;
   }

@@ -240,6 +240,51 @@ static __device__ __forceinline__ uint32_t crc_chunk_w(const uint32_t *base32, u
   return reg >> 8;
 }
 
+/* crc_chunk_w for both generator polynomials at once (two independent table chains over the same
+ * word reads): ra over P_A (tab8a), rb over P_B (tab8b) */
+static __device__ __forceinline__ void crc_chunk_w2(const uint32_t *base32, uint32_t start, uint32_t nbytes,
+                                                    uint32_t per, uint32_t pos, uint32_t nl, const uint32_t *tab8a,
+                                                    const uint32_t *tab8b, uint32_t &ra, uint32_t &rb)
+{
+  const int vstart = (int)(pos * per) - (int)(per * nl - nbytes);
+  uint32_t a = 0, b = 0;
+  for (uint32_t i = 0; i < per; i += 4) {
+    const int o = vstart + (int)i;
+    const uint32_t ad = start + (uint32_t)(o > 0 ? o : 0), wi = ad >> 2;
+    uint32_t w = __builtin_amdgcn_alignbit(base32[wi + 1], base32[wi], (ad & 3u) * 8u);
+    if (o < 0) w = o <= -4 ? 0u : w << (8 * (uint32_t)(-o));   /* bytes before the block are zero */
+#pragma unroll
+    for (int q = 0; q < 4; q++) {
+      const uint32_t by = (w >> (8 * q)) & 0xffu;
+      a = (a << 8) ^ tab8a[(a >> 24) ^ by];
+      b = (b << 8) ^ tab8b[(b >> 24) ^ by];
+    }
+  }
+  ra = a >> 8;
+  rb = b >> 8;
+}
+
+/* crc_wave_tree2 over aligned groups of lpb lanes (16, 32 or 64; pos = lane within the group), both
+ * polynomials; the results are in every lane of the group */
+static __device__ __forceinline__ void crc_group_tree2(uint32_t &ra, uint32_t &rb, uint32_t pos, uint32_t lpb,
+                                                       const uint32_t (*ma)[8][96], const uint32_t (*mb)[8][96])
+{
+  const uint32_t j0 = 7 - (pos & 7), j1 = (lpb >> 3) - 1 - (pos >> 3);
+  ra = crc_mul_tab(ra, ma[0][j0]);
+  rb = crc_mul_tab(rb, mb[0][j0]);
+#pragma unroll
+  for (int m = 1; m < 8; m <<= 1) {
+    ra ^= __shfl_xor(ra, m, 64);
+    rb ^= __shfl_xor(rb, m, 64);
+  }
+  ra = crc_mul_tab(ra, ma[1][j1]);
+  rb = crc_mul_tab(rb, mb[1][j1]);
+  for (uint32_t m = 8; m < lpb; m <<= 1) {
+    ra ^= __shfl_xor(ra, (int)m, 64);
+    rb ^= __shfl_xor(rb, (int)m, 64);
+  }
+}
+
 /* 6-level in-wave tree; mul = [6][6][16] tables; result valid in lane 0 */
 [[maybe_unused]] static __device__ __forceinline__ uint32_t crc_wave_tree(uint32_t reg, const uint32_t *mul)
 {
@@ -564,6 +609,7 @@ static __device__ void encode_codeword(const cfg_dev_t *__restrict__ c, uint32_t
       const uint32_t w = ((cw.K[r] + 31) >> 5) + (i & 3u);
       if (w < sw) strm[slot * sw + w] = 0u;
     }
+    if (ct == 0) crcs[0] = 0u;                    /* phase 1's XOR accumulator (C > 1) */
     for (uint32_t v = ct; v < 256; v += cn) {     /* the register-in-the-top-24-bits form */
       crctab_a[v] = c->crctab[0][v] << 8;
       crctab_b[v] = c->crctab[1][v] << 8;
@@ -578,8 +624,39 @@ static __device__ void encode_codeword(const cfg_dev_t *__restrict__ c, uint32_t
   __syncthreads();
   if (stop_phase <= 0) return;
 
-  /* ---- phase 1: CRC-24A over the TB (dlsch_coding.c:296-300), 256 lanes ---- */
-  {
+  /* ---- phase 1: CRC-24A over the TB (dlsch_coding.c:296-300) and CRC-24B of every block's data
+   * bytes (lte_segmentation.c:156-166) ---- */
+  if (C > 1) {
+    /* one pass for both: crc_lpb lanes per block, each lane a chunk of one block through both byte
+     * tables; the groups combine their chunks per block (-> CRC-24B) and multiply the block's
+     * CRC-24A part into place (crcmul_blk), LDS XOR atomics sum the TB's */
+    const uint32_t lpb = __builtin_amdgcn_readfirstlane(cw.crc_lpb), per = __builtin_amdgcn_readfirstlane(cw.crc_per_cb);
+    const uint32_t pos = tid & (lpb - 1);
+    for (uint32_t r = tid / lpb; r < C; r += nth / lpb) {
+      uint32_t s0 = cw.src[r], n = cw.ncopy[r];
+      if (s0 + n > Ab) n = Ab > s0 ? Ab - s0 : 0;
+      uint32_t ra, rb;
+      crc_chunk_w2(tbw, s0, n, per, pos, lpb, crctab_a, crctab_b, ra, rb);
+      crc_group_tree2(ra, rb, pos, lpb, cw.crc2_cb[0], cw.crc2_cb[1]);
+      if (pos == 0) {
+        crcs[1 + r] = rb;
+        atomicXor(&crcs[0], crc_mul_tab(ra, cw.crcmul_blk[r]));
+      }
+    }
+    __syncthreads();
+    if (tid == 0) {
+      const uint32_t crc = crcs[0];
+      tbb[Ab] = (uint8_t)(crc >> 16);
+      tbb[Ab + 1] = (uint8_t)(crc >> 8);
+      tbb[Ab + 2] = (uint8_t)crc;
+      /* the TB-CRC bytes inside the last block, folded into its CRC-24B */
+      for (uint32_t r = 0; r < C; r++) {
+        uint32_t s0 = cw.src[r], e0 = s0 + cw.ncopy[r], reg = crcs[1 + r];
+        for (uint32_t i = (s0 > Ab ? s0 : Ab); i < e0; i++) reg = ((reg << 8) & 0xffffffu) ^ (crctab_b[((reg >> 16) ^ tbb[i]) & 0xffu] >> 8);
+        crcs[1 + r] = reg;
+      }
+    }
+  } else {
     uint32_t reg = crc_chunk_w(tbw, 0, Ab, cw.crc_per_tb, tid, nth, crctab_a);
     reg = crc_wave_tree2(reg, cw.crc2_tb);
     if (lane == 0) red[wave] = reg;
@@ -591,25 +668,6 @@ static __device__ void encode_codeword(const cfg_dev_t *__restrict__ c, uint32_t
       tbb[Ab] = (uint8_t)(crc >> 16);
       tbb[Ab + 1] = (uint8_t)(crc >> 8);
       tbb[Ab + 2] = (uint8_t)crc;
-    }
-  }
-  /* CRC-24B of every block's data bytes (lte_segmentation.c:156-166), one wave per block;
-   * the TB-CRC bytes inside the last block are folded in once they exist */
-  if (C > 1) {
-    for (uint32_t r = wave; r < C; r += nwaves) {
-      uint32_t s0 = cw.src[r], n = cw.ncopy[r];
-      if (s0 + n > Ab) n = Ab > s0 ? Ab - s0 : 0;
-      uint32_t reg = crc_chunk_w(tbw, s0, n, cw.crc_per_cb, lane, 64, crctab_b);
-      reg = crc_wave_tree2(reg, cw.crc2_cb);
-      if (lane == 0) crcs[1 + r] = reg;
-    }
-  }
-  __syncthreads();
-  if (C > 1 && tid == 0) {
-    for (uint32_t r = 0; r < C; r++) {
-      uint32_t s0 = cw.src[r], e0 = s0 + cw.ncopy[r], reg = crcs[1 + r];
-      for (uint32_t i = (s0 > Ab ? s0 : Ab); i < e0; i++) reg = ((reg << 8) & 0xffffffu) ^ (crctab_b[((reg >> 16) ^ tbb[i]) & 0xffu] >> 8);
-      crcs[1 + r] = reg;
     }
   }
   __syncthreads();

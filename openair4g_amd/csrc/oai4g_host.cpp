@@ -895,9 +895,18 @@ static int derive_cfg(oai4g_tx_config *cfg, const oai4g_tx_params_t *p, const ui
       if (c.src[r] + n > c.A_bytes) n = c.A_bytes > c.src[r] ? c.A_bytes - c.src[r] : 0;
       ncb_max = n > ncb_max ? n : ncb_max;
     }
-    c.crc_per_cb = (((ncb_max + 63) / 64) + 3) & ~3u;
-    crc_mul_tables(c.crc_per_cb ? c.crc_per_cb : 1, 6, 0x800063u, c.crcmul_cb);
-    crc_mul_tables2(c.crc_per_cb ? c.crc_per_cb : 1, 0x800063u, c.crc2_cb);
+    /* C > 1: the CRC-24A and every CRC-24B in one pass, crc_lpb lanes per block (k_encode phase 1) */
+    c.crc_lpb = C <= 4 ? 64u : (C <= 8 ? 32u : 16u);
+    c.crc_per_cb = (((ncb_max + c.crc_lpb - 1) / c.crc_lpb) + 3) & ~3u;
+    crc_mul_tables2(c.crc_per_cb ? c.crc_per_cb : 1, 0x864cfbu, c.crc2_cb[0]);
+    crc_mul_tables2(c.crc_per_cb ? c.crc_per_cb : 1, 0x800063u, c.crc2_cb[1]);
+    for (uint32_t r = 0; r < C; r++) {
+      uint32_t end = c.src[r] + c.ncopy[r];
+      if (end > c.A_bytes) end = c.A_bytes;
+      const uint32_t m = crc_xpow8_h(c.A_bytes - (end > c.src[r] ? end : c.src[r]), 0x864cfbu);
+      for (int k = 0; k < 6; k++)
+        for (uint32_t v = 0; v < 16; v++) c.crcmul_blk[r][16 * k + v] = crc_mulmod_h((v << (4 * k)) & 0xffffffu, m, 0x864cfbu);
+    }
     for (int ki = 0; ki < 2; ki++) {
       uint32_t K = ki == 0 ? (Km ? Km : Kp) : Kp;
       int n = null_positions(K, c.nullpos[ki], OAI4G_MAX_NULLS);

@@ -111,14 +111,18 @@ struct cw_dev_t {
   int16_t alm_qpsk[2][2];
   uint32_t stream_words;        /* LDS words per stream per block (padded) */
   /* CRC tree combine (x^(8*per*2^d) mod P as 6 nibble tables of 16 entries per level) */
-  uint32_t crc_per_tb;          /* bytes per lane, 256 lanes, CRC-24A over the TB */
-  uint32_t crc_per_cb;          /* bytes per lane, 64 lanes, CRC-24B per block */
+  uint32_t crc_per_tb;          /* bytes per lane, 256 lanes, CRC-24A over the TB (C == 1) */
+  uint32_t crc_per_cb;          /* C > 1: bytes per lane, crc_lpb lanes per block, CRC-24A and -24B together */
+  uint32_t crc_lpb;             /* lanes per block (16, 32 or 64) */
   uint32_t crcmul_tb[8][6][16];
-  uint32_t crcmul_cb[6][6][16];
+  /* C > 1: block r's CRC-24A contribution to the TB's, x^(8 (A_bytes - end_r)) mod P_A (end_r = the
+   * block's last TB byte + 1), as 6 nibble tables */
+  uint32_t crcmul_blk[OAI4G_MAX_CB][96];
   /* two-level in-wave combine: lane l's chunk CRC times x^(8 per (7 - l mod 8)) ([0][j] = power
-   * j), XOR over the 8 lanes of its group, times x^(64 per (7 - l / 8)) ([1][j]), XOR over the wave */
+   * j), XOR over the 8 lanes of its group, times x^(64 per (g - 1 - l / 8)) ([1][j], g groups of 8),
+   * XOR over the g groups */
   uint32_t crc2_tb[2][8][96];
-  uint32_t crc2_cb[2][8][96];
+  uint32_t crc2_cb[2][2][8][96];   /* [P_A, P_B] at crc_per_cb */
   /* sub-block interleaver + rate matcher plan per block size (k_encode phase 4), tile t of a
    * block (v0 tiles of 32 rows, then interlaced tiles of 16 y1 / y2 row pairs), half-wave lane L:
    *   rm_src: before the 32x32 transpose, the stream bits lane L loads: bit shift (0..4) and LDS

@@ -1,7 +1,9 @@
 """dlsim's BLER loop on the GPU (openair1/SIMULATION/LTE_PHY/dlsim.c:2065-3545), batched over trials.
 
-One trial of the reference, TM1 / SISO / one receive antenna / AWGN (`-gL`, channel model 18), as the
-reference's AWGN_results/bler_tx1_chan18_nrx1_mcs*.csv were produced:
+One trial of the reference, TM1 / SISO / one receive antenna / AWGN (`-gN`: channel_model = AWGN, value
+18 of SCM_t in SIMULATION/TOOLS/defs.h:158-178, applied through multipath_channel, a single unit tap at
+Ricean factor 0 -- `-gL` would be Rice8 = 14), as the reference's
+AWGN_results/bler_tx1_chan18_nrx1_mcs*.csv were produced:
   - transmit (:2553-2704): generate_dci_top's PCFICH + PDCCH for one format-1 DCI (L = 1, RNTI
     0x1234; dlsim.c:1154-1157), dlsch_encoding / dlsch_scrambling / dlsch_modulation of a random
     transport block, generate_pilots, do_OFDM_mod_l of the subframe's two slots, and of the next
