@@ -35,8 +35,8 @@ static __device__ __forceinline__ short ssub(short a, short b) { return __builti
                                 (the metric layouts rotate with period 3) */
 #endif
 #ifndef TD_FSG
-#define TD_FSG 3             /* forward chunk of the gathered forms (two loads deep: pi, then the gather);
-                                round 2 measured 4 best of 2 / 4 / 6 / 8 / 12 / 16 with the fixed layout */
+#define TD_FSG 12            /* forward chunk of the gathered forms (two loads deep: pi, then the gather);
+                                round 4, loads held unpacked: C5 3 -> 192 k, 6 -> 222 k, 9 -> 223 k, 12 -> 229 k */
 #endif
 #ifndef TD_XR
 #define TD_XR 32      /* steps per round of the exchange gathers (index loads, then gathers, in flight) */
