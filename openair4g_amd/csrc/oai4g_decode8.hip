@@ -24,8 +24,12 @@
 
 typedef short s2v8 __attribute__((ext_vector_type(2)));
 
+#ifndef TD8_FS
 #define TD8_FS 16
+#endif
+#ifndef TD8_SEG
 #define TD8_SEG 4
+#endif
 #define TD8_XR 32
 #define TD8_L 16
 
@@ -53,6 +57,24 @@ __device__ __forceinline__ tm8_t up8(uint4 u)
   tm8_t t;
   t.v[0] = __builtin_bit_cast(s2v8, u.x); t.v[1] = __builtin_bit_cast(s2v8, u.y);
   t.v[2] = __builtin_bit_cast(s2v8, u.z); t.v[3] = __builtin_bit_cast(s2v8, u.w);
+  return t;
+}
+/* log_map8_lane is not inlined: explicit address spaces keep its scratch accesses global_* / ds_*
+ * (see oai4g_decode.hip, TD_G); checkpoint words as an ext vector, unpacked through scalars */
+#define TD8_GAS __attribute__((address_space(1)))
+#define TD8_LAS __attribute__((address_space(3)))
+typedef uint32_t u4v8 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ u4v8 pk8v(const tm8_t &t)
+{
+  return (u4v8){__builtin_bit_cast(uint32_t, t.v[0]), __builtin_bit_cast(uint32_t, t.v[1]),
+                __builtin_bit_cast(uint32_t, t.v[2]), __builtin_bit_cast(uint32_t, t.v[3])};
+}
+__device__ __forceinline__ tm8_t up8(u4v8 u)
+{
+  const uint32_t w0 = u.x, w1 = u.y, w2 = u.z, w3 = u.w;
+  tm8_t t;
+  t.v[0] = __builtin_bit_cast(s2v8, w0); t.v[1] = __builtin_bit_cast(s2v8, w1);
+  t.v[2] = __builtin_bit_cast(s2v8, w2); t.v[3] = __builtin_bit_cast(s2v8, w3);
   return t;
 }
 __device__ __forceinline__ tm8_t init8(bool zero_first)
@@ -139,34 +161,37 @@ __device__ __forceinline__ td8_blk_t t8_layout(uint8_t *base, uint32_t K)
 
 /* log_map8 for the calling lane (window q of its block) */
 template <bool POST>
-__device__ __attribute__((noinline)) void log_map8_lane(const short *sys, const short *par, short *ext, uint4 *A, uint32_t K,
-                                                        uint32_t q, uint4 *asave /* [17][64] */, const short *s0)
+__device__ __attribute__((noinline)) void log_map8_lane(TD8_GAS const short *sys, TD8_GAS const short *par, TD8_GAS short *ext,
+                                                        TD8_GAS u4v8 *A, uint32_t K, uint32_t q,
+                                                        TD8_LAS u4v8 *asave /* [17][64] */, TD8_GAS const short *s0)
 {
+  K = __builtin_amdgcn_readfirstlane(K);
   const uint32_t K1 = K >> 4, nseg = (K1 + TD8_SEG - 1) / TD8_SEG, lane = threadIdx.x & 63;
-  uint4 *A16 = A + 64 * (nseg + 1);              /* first-run alpha(16) */
+  TD8_GAS u4v8 *A16 = A + 64 * (nseg + 1);         /* first-run alpha(16) */
   constexpr int FS = TD8_FS;
   const uint32_t nfc = (K1 + FS - 1) / FS;
   tm8_t a = init8(q == 0);
   {
-    s2v8 nsp[FS];
+    short nsy[FS], npa[FS];                     /* one value per register until its step (no wait at issue) */
 #pragma unroll
-    for (int j = 0; j < FS; j++) nsp[j] = (s2v8){sys[64 * j + q], par[64 * j + q]};
+    for (int j = 0; j < FS; j++) { nsy[j] = sys[64 * j + q]; npa[j] = par[64 * j + q]; }
     for (uint32_t c = 0; c < nfc; c++) {
-      s2v8 csp[FS];
+      short csy[FS], cpa[FS];
 #pragma unroll
-      for (int j = 0; j < FS; j++) csp[j] = nsp[j];
+      for (int j = 0; j < FS; j++) { csy[j] = nsy[j]; cpa[j] = npa[j]; }
       if (c + 1 < nfc) {
         const uint32_t b = 64 * FS * (c + 1) + q;
 #pragma unroll
-        for (int j = 0; j < FS; j++) nsp[j] = (s2v8){sys[b + 64 * j], par[b + 64 * j]};
+        for (int j = 0; j < FS; j++) { nsy[j] = sys[b + 64 * j]; npa[j] = par[b + 64 * j]; }
       }
+      const bool full = c * FS + FS <= K1;     /* uniform: only the last chunk may be partial */
 #pragma unroll
       for (int j = 0; j < FS; j++) {
         const uint32_t k = c * FS + j;
-        if (k < K1) {
-          alpha8_step(a, (short)(((int)csp[j].x + csp[j].y) >> 1), (short)(((int)csp[j].x - csp[j].y) >> 1));
-          if (k + 1 == TD8_L) A16[q] = pk8(a);
-          if (((k + 1) & (TD8_SEG - 1)) == 0) A[64 * ((k + 1) / TD8_SEG) + q] = pk8(a);
+        if (full || k < K1) {
+          alpha8_step(a, (short)(((int)csy[j] + cpa[j]) >> 1), (short)(((int)csy[j] - cpa[j]) >> 1));
+          if (k + 1 == TD8_L) A16[q] = pk8v(a);
+          if (((k + 1) & (TD8_SEG - 1)) == 0) A[64 * ((k + 1) / TD8_SEG) + q] = pk8v(a);
         }
       }
     }
@@ -180,49 +205,46 @@ __device__ __attribute__((noinline)) void log_map8_lane(const short *sys, const 
       a.v[v] = q == 0 ? z.v[v] : __builtin_bit_cast(s2v8, up);
     }
   }
-  A[q] = pk8(a);
+  A[q] = pk8v(a);
   for (uint32_t k = 0; k < TD8_L; k++) {
     const short s = sys[64 * k + q], p = par[64 * k + q];
     alpha8_step(a, (short)(((int)s + p) >> 1), (short)(((int)s - p) >> 1));
-    if (((k + 1) & (TD8_SEG - 1)) == 0) A[64 * ((k + 1) / TD8_SEG) + q] = pk8(a);
+    if (((k + 1) & (TD8_SEG - 1)) == 0) A[64 * ((k + 1) / TD8_SEG) + q] = pk8v(a);
   }
   /* backward first run from the final alpha, window 15 from the zeroed termination */
   tm8_t b = q == 15 ? zero8() : fin;
   const int kr = (int)K1 - (TD8_L + 1);          /* steps >= kr take their extrinsic from the re-run */
-  const uint4 a16v = A16[q];
-  s2v8 nsp[TD8_SEG], nzz[TD8_SEG / 2];
-  uint4 nA;
+  const u4v8 a16v = A16[q];
+  short nsy[TD8_SEG], npa[TD8_SEG], nzs[TD8_SEG];
+  u4v8 nA;
   auto fetch = [&](int seg) {
     const uint32_t b0 = 64u * (uint32_t)(seg * TD8_SEG) + q;
 #pragma unroll
-    for (int j = 0; j < TD8_SEG; j++) nsp[j] = (s2v8){sys[b0 + 64 * j], par[b0 + 64 * j]};
+    for (int j = 0; j < TD8_SEG; j++) { nsy[j] = sys[b0 + 64 * j]; npa[j] = par[b0 + 64 * j]; }
     if constexpr (POST) {
 #pragma unroll
-      for (int i = 0; i < TD8_SEG / 2; i++) nzz[i] = (s2v8){s0[b0 + 128 * i], s0[b0 + 128 * i + 64]};
+      for (int j = 0; j < TD8_SEG; j++) nzs[j] = s0[b0 + 64 * j];
     }
     nA = A[64 * seg + q];
   };
   fetch((int)nseg - 1);
   for (int seg = (int)nseg - 1; seg >= 0; seg--) {
     const int k0 = seg * TD8_SEG, n = min((int)TD8_SEG, (int)K1 - k0);
-    s2v8 css[TD8_SEG / 2], czz[TD8_SEG / 2];
-    uint4 al[TD8_SEG];
+    short css[TD8_SEG], czz[TD8_SEG];
+    u4v8 al[TD8_SEG];
     uint32_t gg[TD8_SEG];
     tm8_t c = up8(nA);
 #pragma unroll
     for (int j = 0; j < TD8_SEG; j++) {
-      const short x11 = (short)(((int)nsp[j].x + nsp[j].y) >> 1), x10 = (short)(((int)nsp[j].x - nsp[j].y) >> 1);
+      const short x11 = (short)(((int)nsy[j] + npa[j]) >> 1), x10 = (short)(((int)nsy[j] - npa[j]) >> 1);
       gg[j] = (uint16_t)x11 | ((uint32_t)(uint16_t)x10 << 16);
-    }
-#pragma unroll
-    for (int i = 0; i < TD8_SEG / 2; i++) {
-      css[i] = (s2v8){nsp[2 * i].x, nsp[2 * i + 1].x};
-      czz[i] = nzz[i];
+      css[j] = nsy[j];
+      czz[j] = nzs[j];
     }
     if (seg > 0) fetch(seg - 1);
 #pragma unroll
     for (int j = 0; j < TD8_SEG; j++) {
-      al[j] = pk8(c);
+      al[j] = pk8v(c);
       if (k0 + j == TD8_L) c = up8(a16v);        /* alpha(17) continues the first run */
       alpha8_step(c, (short)gg[j], (short)(gg[j] >> 16));
     }
@@ -234,8 +256,7 @@ __device__ __attribute__((noinline)) void log_map8_lane(const short *sys, const 
         if (k < kr) {
           short v = ext8_of(up8(al[j]), b, x11, x10);
           if constexpr (POST) {
-            const short sv = (j & 1) ? css[j >> 1].y : css[j >> 1].x, zv = (j & 1) ? czz[j >> 1].y : czz[j >> 1].x;
-            v = sa8((int)sa8((int)v - sv) + zv);
+            v = sa8((int)sa8((int)v - css[j]) + czz[j]);
           }
           ext[64 * k + q] = v;
         } else {
@@ -344,7 +365,8 @@ __global__ void __launch_bounds__(64) k_td8(int n_cb, uint32_t K, const int16_t 
   }
   __syncthreads();
   bool active = valid && max_it > 0;
-  if (valid) log_map8_lane<false>(B.s0, B.yp1, B.ext, B.A, K, q, asave, B.s0);
+  if (valid) log_map8_lane<false>((TD8_GAS short *)B.s0, (TD8_GAS short *)B.yp1, (TD8_GAS short *)B.ext, (TD8_GAS u4v8 *)B.A, K, q,
+                                   (TD8_LAS u4v8 *)asave, (TD8_GAS short *)B.s0);
   __syncthreads();
   uint32_t it = 0;
   for (it = 1; it <= max_it; it++) {
@@ -362,7 +384,8 @@ __global__ void __launch_bounds__(64) k_td8(int n_cb, uint32_t K, const int16_t 
       }
     }
     __syncthreads();
-    if (active) log_map8_lane<false>(B.s2, B.yp2, B.ext2, B.A, K, q, asave, B.s0);
+    if (active) log_map8_lane<false>((TD8_GAS short *)B.s2, (TD8_GAS short *)B.yp2, (TD8_GAS short *)B.ext2, (TD8_GAS u4v8 *)B.A, K,
+                                      q, (TD8_LAS u4v8 *)asave, (TD8_GAS short *)B.s0);
     __syncthreads();
     if (active) {
       for (uint32_t v0 = 0; v0 < K1; v0 += TD8_XR) {   /* deinterleave (pi5) + update */
@@ -415,7 +438,8 @@ __global__ void __launch_bounds__(64) k_td8(int n_cb, uint32_t K, const int16_t 
     }
     __syncthreads();
     if (active && done_it[g]) active = false;
-    if (active && it < max_it) log_map8_lane<true>(B.s1, B.yp1, B.ext, B.A, K, q, asave, B.s0);
+    if (active && it < max_it) log_map8_lane<true>((TD8_GAS short *)B.s1, (TD8_GAS short *)B.yp1, (TD8_GAS short *)B.ext,
+                                                    (TD8_GAS u4v8 *)B.A, K, q, (TD8_LAS u4v8 *)asave, (TD8_GAS short *)B.s0);
     __syncthreads();
     if (!__any(active)) break;
   }
