@@ -30,7 +30,9 @@ typedef short s2v8 __attribute__((ext_vector_type(2)));
 #ifndef TD8_SEG
 #define TD8_SEG 4
 #endif
-#define TD8_XR 32
+#ifndef TD8_XR
+#define TD8_XR 16
+#endif
 #define TD8_L 16
 
 namespace {
@@ -163,7 +165,7 @@ __device__ __forceinline__ td8_blk_t t8_layout(uint8_t *base, uint32_t K)
 template <bool POST>
 __device__ __attribute__((noinline)) void log_map8_lane(TD8_GAS const short *sys, TD8_GAS const short *par, TD8_GAS short *ext,
                                                         TD8_GAS u4v8 *A, uint32_t K, uint32_t q,
-                                                        TD8_LAS u4v8 *asave /* [17][64] */, TD8_GAS const short *s0)
+                                                        TD8_GAS u4v8 *asave /* [17][64] */, TD8_GAS const short *s0)
 {
   K = __builtin_amdgcn_readfirstlane(K);
   const uint32_t K1 = K >> 4, nseg = (K1 + TD8_SEG - 1) / TD8_SEG, lane = threadIdx.x & 63;
@@ -290,12 +292,18 @@ __device__ __attribute__((noinline)) void log_map8_lane(TD8_GAS const short *sys
 size_t oai4g_td8_wave_bytes(uint32_t K)
 {
   const size_t K1 = K >> 4, nseg = (K1 + TD8_SEG - 1) / TD8_SEG;
-  return ((7 * 4 * t8_n16(K) * 2 + 15) & ~(size_t)15) + (nseg + 2) * 64 * 16 + 256;
+  return ((7 * 4 * t8_n16(K) * 2 + 15) & ~(size_t)15) + (nseg + 2 + TD8_L + 1) * 64 * 16 + 256;
 }
 
 /* blockIdx.x decodes blocks 4 blockIdx.x .. +3 (one 64-lane wave).  llr: [n_cb][llr_stride] int16
  * (3K + 12, 4 more readable), out: [n_cb][out_stride] bytes, iters: [n_cb]. */
-__global__ void __launch_bounds__(64) k_td8(int n_cb, uint32_t K, const int16_t *__restrict__ llr, size_t llr_stride,
+/* 4 waves per SIMD (the launch has 4096 one-wave workgroups at C5): the register cap costs a few
+ * spilled words in log_map8 and buys the fourth wave (C5 8-bit: 3 waves 132 k, 4 waves 146 k) */
+#ifndef TD8_WAVES
+#define TD8_WAVES 4
+#endif
+#define TD8_WAVES_ATTR __attribute__((amdgpu_waves_per_eu(TD8_WAVES, TD8_WAVES)))
+__global__ void __launch_bounds__(64) TD8_WAVES_ATTR k_td8(int n_cb, uint32_t K, const int16_t *__restrict__ llr, size_t llr_stride,
                                             uint8_t *__restrict__ out, size_t out_stride, uint8_t *__restrict__ iters,
                                             uint32_t max_it, uint32_t crc_type, uint32_t F,
                                             const uint16_t *__restrict__ pi4, const uint16_t *__restrict__ pi5,
@@ -305,7 +313,6 @@ __global__ void __launch_bounds__(64) k_td8(int n_cb, uint32_t K, const int16_t 
   __shared__ uint32_t crctab[256];
   __shared__ uint8_t dec[4][6144 / 8 + 8];
   __shared__ uint32_t done_it[4];
-  __shared__ uint4 asave[(TD8_L + 1) * 64];
   const uint32_t lane = threadIdx.x, g = lane >> 4, q = lane & 15;
   const int cb = (int)(blockIdx.x * 4 + g);
   const bool valid = cb < n_cb;
@@ -326,6 +333,9 @@ __global__ void __launch_bounds__(64) k_td8(int n_cb, uint32_t K, const int16_t 
   td8_blk_t B;
   B.s0 = Wv.s0 + 16 * g; B.s1 = Wv.s1 + 16 * g; B.s2 = Wv.s2 + 16 * g; B.yp1 = Wv.yp1 + 16 * g;
   B.yp2 = Wv.yp2 + 16 * g; B.ext = Wv.ext + 16 * g; B.ext2 = Wv.ext2 + 16 * g; B.A = Wv.A + 16 * g;
+  /* the re-run's saved alphas, [17][64] per wave behind the checkpoints (global: 17 KB of LDS per
+   * one-wave workgroup would cap residency below 2 waves per SIMD) */
+  TD8_GAS u4v8 *asave = (TD8_GAS u4v8 *)(Wv.A + 64 * ((K1 + TD8_SEG - 1) / TD8_SEG + 2));
   const int16_t *y = llr + (size_t)(valid ? cb : 0) * llr_stride;
   /* input scaling (:1001-1031): mean of |w0|+|w1|+|w2|+|w3|+2|w4|+2|w5| over 3 (K/16) + 1
    * vectors of 8 (abs_epi16 keeps -32768), reduced over the block's 16 lanes */
@@ -366,7 +376,7 @@ __global__ void __launch_bounds__(64) k_td8(int n_cb, uint32_t K, const int16_t 
   __syncthreads();
   bool active = valid && max_it > 0;
   if (valid) log_map8_lane<false>((TD8_GAS short *)B.s0, (TD8_GAS short *)B.yp1, (TD8_GAS short *)B.ext, (TD8_GAS u4v8 *)B.A, K, q,
-                                   (TD8_LAS u4v8 *)asave, (TD8_GAS short *)B.s0);
+                                   asave, (TD8_GAS short *)B.s0);
   __syncthreads();
   uint32_t it = 0;
   for (it = 1; it <= max_it; it++) {
@@ -385,7 +395,7 @@ __global__ void __launch_bounds__(64) k_td8(int n_cb, uint32_t K, const int16_t 
     }
     __syncthreads();
     if (active) log_map8_lane<false>((TD8_GAS short *)B.s2, (TD8_GAS short *)B.yp2, (TD8_GAS short *)B.ext2, (TD8_GAS u4v8 *)B.A, K,
-                                      q, (TD8_LAS u4v8 *)asave, (TD8_GAS short *)B.s0);
+                                      q, asave, (TD8_GAS short *)B.s0);
     __syncthreads();
     if (active) {
       for (uint32_t v0 = 0; v0 < K1; v0 += TD8_XR) {   /* deinterleave (pi5) + update */
@@ -439,7 +449,7 @@ __global__ void __launch_bounds__(64) k_td8(int n_cb, uint32_t K, const int16_t 
     __syncthreads();
     if (active && done_it[g]) active = false;
     if (active && it < max_it) log_map8_lane<true>((TD8_GAS short *)B.s1, (TD8_GAS short *)B.yp1, (TD8_GAS short *)B.ext,
-                                                    (TD8_GAS u4v8 *)B.A, K, q, (TD8_LAS u4v8 *)asave, (TD8_GAS short *)B.s0);
+                                                    (TD8_GAS u4v8 *)B.A, K, q, asave, (TD8_GAS short *)B.s0);
     __syncthreads();
     if (!__any(active)) break;
   }
