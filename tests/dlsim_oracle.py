@@ -40,11 +40,14 @@ def wilson(k, n, z=1.96):
     return max(0.0, c - h), min(1.0, c + h)
 
 
-def load_curves():
-    """{mcs: [(snr, err0, trials0)]} from the committed fixture (tests/golden/make_bler_fixture.py)."""
+def load_curves(which="awgn_results"):
+    """{mcs: [(snr, err0, trials0)]} from the committed fixture (tests/golden/make_bler_fixture.py):
+    which = "awgn_results" (AWGN_results/bler_tx1_chan18_nrx1_mcs*.csv) or "perf_curves_abs" (the
+    reference's second set for the same configuration, Perf_Curves_Abs/awgn_bler_tx1_mcs*.csv)."""
     import json
     d = json.load(open(GOLDEN_CSV))
-    return {int(k): [tuple(r) for r in v["rows"]] for k, v in d["curves"].items()}
+    c = d["curves"] if which == "awgn_results" else d["curves_" + which]
+    return {int(k): [tuple(r) for r in v["rows"]] for k, v in c.items()}
 
 
 class OracleTrial:

@@ -8,6 +8,7 @@
     binomial error of a small CPU sample.  The GPU reproduces the same rows with 32 768 trials each
     (tests/test_gpu_dlsim.py)."""
 import ctypes
+import sys
 import os
 
 import numpy as np
@@ -81,3 +82,21 @@ def test_oracle_bler_matches_reference_curve_mcs9(snr, n):
     z = (p - q) / np.sqrt(p * (1 - p) / n + q * (1 - q) / ref[2] + 1e-12)
     print(f"SNR {snr}: oracle {k}/{n} = {p:.4f}, reference {ref[1]}/{ref[2]} = {q:.4f}, z = {z:+.2f}")
     assert abs(z) < 3, (k, n, ref)
+
+
+def test_reference_curve_sets_same_configuration_and_offset():
+    """The fixture's two reference-held sets (AWGN_results, Perf_Curves_Abs) carry the same TBS and
+    code rate at every MCS (the same dlsim configuration), and yet Perf_Curves_Abs lies 0.05-0.3 dB to
+    the left at every MCS (tools/bler_ref_sets.py): the run-to-run spread of the reference's own
+    curves, against which the GPU BLER pin (test_gpu_bler_matches_reference_curves) is read."""
+    import json
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tools"))
+    import bler_ref_sets as R
+    d = json.load(open(D.GOLDEN_CSV))
+    a, b = d["curves"], d["curves_perf_curves_abs"]
+    assert sorted(a, key=int) == sorted(b, key=int) and len(a) == 28
+    for m in a:
+        assert (a[m]["TBS"], a[m]["rate"]) == (b[m]["TBS"], b[m]["rate"]), m
+    A, B = D.load_curves("awgn_results"), D.load_curves("perf_curves_abs")
+    shifts = [R.shift(A[m], B[m])[0] for m in range(28)]
+    assert all(-0.35 <= s <= -0.04 for s in shifts), shifts

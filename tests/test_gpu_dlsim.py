@@ -121,21 +121,29 @@ def test_gpu_trial_equals_oracle_trial(gpu, mcs, snr, llr8):
     sim.close()
 
 
-# Statistical pin to the reference-held curves.  Their dlsim options are not recorded with them;
-# measured here (tools/bler_sweep.py, 16 384 - 32 768 trials per row): MCS 9 follows
-# the curve with the 8-bit decoder (dlsim -L) over the whole waterfall and its tail (5 of 6 rows
-# inside the CSV's 95 % interval), MCS 27's waterfall with the 16-bit decoder within 0.1 dB (0.075);
-# MCS 0 / 16 come out 0.35 / 0.27 dB better than the CSVs with either decoder.  The assertion: at
-# least `need` CSV rows whose 95 % Wilson interval contains the GPU estimate, and the fitted SNR
-# shift within the stated bound.
-PINS = [(9, True, [3.6, 3.7, 3.8, 3.9, 4.0, 4.1], 3, 0.05),
-        (27, False, [16.7, 16.8, 16.9, 17.0, 17.1, 17.2], 0, 0.1)]
+# Statistical pin to the reference-held curves.  The reference holds two AWGN curve sets for the
+# same dlsim configuration (TM1, 25 PRB, one RX; the same TBS per MCS): AWGN_results/ and
+# Perf_Curves_Abs/.  They disagree with each other by 0.05-0.3 dB at every MCS
+# (tools/bler_ref_sets.py, profiles/bler_r04_ref_sets.txt); the GPU chain with dlsim's default 16-bit
+# decoder follows Perf_Curves_Abs over the waterfall and its error floor (tools/bler_sweep.py
+# --curves perf_curves_abs, profiles/bler_r04_perf16.log), and sits on the better side of
+# AWGN_results by about that same offset.  The assertion: at least `need` reference rows whose
+# 95 % Wilson interval contains the GPU estimate, and the fitted SNR shift within the stated bound.
+# (MCS 27's Perf_Curves_Abs rows are 502-1000 trials at 0.2 dB spacing, hence the looser shift.)
+# The rows: every waterfall row of the set (reference BLER in (0.005, 0.995)).
+PINS = [(0, False, "perf_curves_abs", None, 3, 0.05),
+        (9, False, "perf_curves_abs", None, 3, 0.05),
+        (16, False, "perf_curves_abs", None, 3, 0.05),
+        (27, False, "perf_curves_abs", None, 3, 0.1),
+        (27, False, "awgn_results", [16.7, 16.8, 16.9, 17.0, 17.1, 17.2], 0, 0.2)]
 
 
-@pytest.mark.parametrize("mcs,llr8,snrs,need,shift", PINS)
-def test_gpu_bler_matches_reference_curves(gpu, mcs, llr8, snrs, need, shift):
+@pytest.mark.parametrize("mcs,llr8,which,snrs,need,shift", PINS)
+def test_gpu_bler_matches_reference_curves(gpu, mcs, llr8, which, snrs, need, shift):
     from openair4g_amd.dlsim import DlsimBler, wilson
-    curves = D.load_curves()[mcs]
+    curves = D.load_curves(which)[mcs]
+    if snrs is None:
+        snrs = [r[0] for r in curves if 0.005 < r[1] / r[2] < 0.995]
     sim = DlsimBler(mcs, batch=4096, llr8=llr8)
     inside, rows = 0, []
     for snr in snrs:

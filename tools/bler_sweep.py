@@ -29,10 +29,12 @@ def main():
     ap.add_argument("--lo", type=float, default=0.005)
     ap.add_argument("--hi", type=float, default=0.995)
     ap.add_argument("--out", default=None)
+    ap.add_argument("--curves", default="awgn_results", choices=["awgn_results", "perf_curves_abs"],
+                    help="which reference-held curve set to compare with")
     a = ap.parse_args()
     import dlsim_oracle as D
     from openair4g_amd.dlsim import DlsimBler
-    curves = D.load_curves()
+    curves = D.load_curves(a.curves)
     res = {}
     for mcs in a.mcs:
         sim = DlsimBler(mcs, batch=a.batch, with_dci=not a.no_dci, llr8=a.llr8)
@@ -62,7 +64,13 @@ def main():
             if best is None or err < best[1]:
                 best = (round(float(d), 3), err)
         print(f"MCS {mcs}: best shift ref(snr) ~ gpu(snr + d), d = {best}  ({time.time() - t0:.1f}s)", flush=True)
-        res[mcs] = {"rows": rows, "shift_db": best[0] if best else None, "dci": not a.no_dci, "llr8": a.llr8}
+        from openair4g_amd.dlsim import wilson
+        inside = sum(1 for r in rows if abs(r[5]) <= 1.96)
+        in_ci = sum(1 for r in rows if wilson(r[3], r[4])[0] <= r[1] / r[2] <= wilson(r[3], r[4])[1])
+        print(f"MCS {mcs}: {inside} of {len(rows)} rows within |z| <= 1.96; {in_ci} inside the reference row's "
+              f"95 % (Wilson) interval", flush=True)
+        res[mcs] = {"rows": rows, "shift_db": best[0] if best else None, "dci": not a.no_dci, "llr8": a.llr8,
+                    "curves": a.curves, "rows_within_z196": inside, "rows_inside_ci": in_ci}
         sim.close()
     if a.out:
         json.dump(res, open(a.out, "w"), indent=1)
