@@ -41,6 +41,9 @@ static __device__ __forceinline__ short ssub(short a, short b) { return __builti
 #ifndef TD_XR
 #define TD_XR 32      /* steps per round of the exchange gathers (index loads, then gathers, in flight) */
 #endif
+#ifndef TD_BPF
+#define TD_BPF 1      /* backward pass: segments between an operand fetch and its alpha recompute (1 or 2) */
+#endif
 #ifndef TD_SEG
 #define TD_SEG 6      /* alpha checkpoint interval (steps), a multiple of 3 so every checkpoint holds layout EO
                          (round 2 measured 4 best of 2/4/8/16 with the fixed layout) */
@@ -507,29 +510,33 @@ static __device__ __attribute__((noinline)) void log_map(TD_G short *sys, TD_G c
   tm_t b = q == 7 ? ly_conv_to<LY_N>(t, pK) : (K1 == 5 ? a : fin);
   const int kr = (int)K1 - 6;                 /* steps >= kr take their extrinsic from the re-run */
   const int nfast = kr > 0 ? kr / TD_SEG : 0;  /* segments [0, nfast) lie wholly below kr */
-  short nsy[TD_SEG], npa[TD_SEG], nzs[TD_SEG]; /* sys, par and (POST) s0 of the next segment */
-  u4v nA;
-  auto fetch = [&](int seg) {
+  /* a segment's operands as loaded: sys, par, (POST) s0 and its alpha checkpoint, one 16-bit value
+   * per register until they are taken */
+  struct bundle_t {
+    short sy[TD_SEG], pa[TD_SEG], zs[TD_SEG];
+    u4v A;
+  };
+  auto fetch = [&](bundle_t &d, int seg) {
     const uint32_t b0 = 64u * (uint32_t)(seg * TD_SEG) + q;
 #pragma unroll
-    for (int j = 0; j < TD_SEG; j++) { nsy[j] = sys[b0 + 64 * j]; npa[j] = par[b0 + 64 * j]; }
+    for (int j = 0; j < TD_SEG; j++) { d.sy[j] = sys[b0 + 64 * j]; d.pa[j] = par[b0 + 64 * j]; }
     if constexpr (POST) {
 #pragma unroll
-      for (int j = 0; j < TD_SEG; j++) nzs[j] = s0[b0 + 64 * j];
+      for (int j = 0; j < TD_SEG; j++) d.zs[j] = s0[b0 + 64 * j];
     }
-    nA = A[64 * seg + q];
+    d.A = A[64 * seg + q];
   };
   /* a segment's operands in registers: gammas, and (POST) its sys and s0 */
   struct segops_t {
     uint32_t gg[TD_SEG];                       /* g11 | g10 << 16 */
     short ss[TD_SEG], zz[TD_SEG];
   };
-  auto take = [&](segops_t &o) {
+  auto take = [&](segops_t &o, const bundle_t &d) {
 #pragma unroll
     for (int j = 0; j < TD_SEG; j++) {
-      o.gg[j] = gg_of(nsy[j], npa[j]);
-      o.ss[j] = nsy[j];
-      o.zz[j] = nzs[j];
+      o.gg[j] = gg_of(d.sy[j], d.pa[j]);
+      o.ss[j] = d.sy[j];
+      o.zz[j] = d.zs[j];
     }
   };
   /* extrinsic of step k0 + j from alpha (layout j mod 3) and beta(k0 + j + 1) */
@@ -541,7 +548,8 @@ static __device__ __attribute__((noinline)) void log_map(TD_G short *sys, TD_G c
     }
     ext[64 * (k0 + j) + q] = v;
   };
-  fetch((int)nseg - 1);
+  bundle_t bx, by;                             /* operands in flight (bx: the next segment) */
+  fetch(bx, (int)nseg - 1);
   /* top segments (partial, or holding steps >= kr): guarded steps, alpha recompute then beta */
   for (int seg = (int)nseg - 1; seg >= nfast; seg--) {
     const int k0 = seg * TD_SEG, n = min((int)TD_SEG, (int)K1 - k0);
@@ -549,9 +557,9 @@ static __device__ __attribute__((noinline)) void log_map(TD_G short *sys, TD_G c
      * leaves beta untouched for those steps */
     segops_t o;
     u4v al[TD_SEG];
-    tm_t c = tm_unpack(nA);                    /* alpha(k0), layout EO */
-    take(o);
-    if (seg > 0) fetch(seg - 1);
+    tm_t c = tm_unpack(bx.A);                  /* alpha(k0), layout EO */
+    take(o, bx);
+    if (seg > 0) fetch(bx, seg - 1);
     sfor<0, TD_SEG>([&](auto J) {
       constexpr int j = decltype(J)::value;
       al[j] = tm_packv(c);
@@ -569,25 +577,29 @@ static __device__ __attribute__((noinline)) void log_map(TD_G short *sys, TD_G c
   }
   /* full segments below kr, software-pipelined: the beta / extrinsic steps of segment seg
    * interleave with the alpha recompute of segment seg - 1 (two independent dependency chains
-   * per lane); operands two segments ahead */
+   * per lane); operands TD_BPF segments ahead of their alpha recompute, in alternating bundles */
   if (nfast > 0) {
     segops_t cur, nx;
     u4v alc[TD_SEG], aln[TD_SEG];
     {
-      tm_t c = tm_unpack(nA);
-      take(cur);
-      if (nfast > 1) fetch(nfast - 2);
+      tm_t c = tm_unpack(bx.A);
+      take(cur, bx);
+      if (nfast > 1) fetch(bx, nfast - 2);
+#if TD_BPF > 1
+      if (nfast > 2) fetch(by, nfast - 3);
+#endif
       sfor<0, TD_SEG>([&](auto J) {
         constexpr int j = decltype(J)::value;
         alc[j] = tm_packv(c);
         alpha_ph<j % 3>(c, gk_of(cur.gg[j]));
       });
     }
-    for (int seg = nfast - 1; seg >= 1; seg--) {
+    /* one segment: bt holds segment seg - 1's operands; it is refilled TD_BPF + 1 segments down */
+    auto step_seg = [&](int seg, bundle_t &bt) {
       const int k0 = seg * TD_SEG;
-      tm_t c = tm_unpack(nA);                  /* alpha((seg - 1) TD_SEG) */
-      take(nx);
-      if (seg > 1) fetch(seg - 2);
+      tm_t c = tm_unpack(bt.A);                /* alpha((seg - 1) TD_SEG) */
+      take(nx, bt);
+      if (seg > TD_BPF) fetch(bt, seg - 1 - TD_BPF);
       sfor<0, TD_SEG>([&](auto J) {
         constexpr int j = decltype(J)::value;
         constexpr int jj = TD_SEG - 1 - j;
@@ -599,7 +611,17 @@ static __device__ __attribute__((noinline)) void log_map(TD_G short *sys, TD_G c
       cur = nx;
 #pragma unroll
       for (int j = 0; j < TD_SEG; j++) alc[j] = aln[j];
+    };
+    int seg = nfast - 1;
+#if TD_BPF > 1
+    for (; seg >= 2; seg -= 2) {
+      step_seg(seg, bx);
+      step_seg(seg - 1, by);
     }
+    if (seg == 1) step_seg(1, bx);
+#else
+    for (; seg >= 1; seg--) step_seg(seg, bx);
+#endif
     sfor_down<0, TD_SEG>([&](auto J) {
       constexpr int j = decltype(J)::value;
       emit(J, cur, alc[j], 0);
