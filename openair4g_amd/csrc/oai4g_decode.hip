@@ -650,6 +650,18 @@ static __device__ __attribute__((noinline)) void log_map(TD_G short *sys, TD_G c
   }
 }
 
+/* a * b mod P over GF(2) for the 24-bit CRC generators (P without its x^24 term) */
+__device__ static __forceinline__ uint32_t td_mulmod(uint32_t a, uint32_t b, uint32_t poly)
+{
+  uint32_t r = 0;
+  for (int i = 23; i >= 0; i--) {
+    r <<= 1;
+    if (r & 0x1000000u) r ^= 0x1000000u | poly;
+    if ((b >> i) & 1u) r ^= a;
+  }
+  return r;
+}
+
 __device__ static const uint32_t *td_crc_tab(uint32_t *lds, uint32_t poly)
 {
   for (uint32_t v = threadIdx.x; v < 256; v += blockDim.x) {
@@ -684,6 +696,21 @@ __global__ void __launch_bounds__(64) k_td16(int n_cb, uint32_t K, const int16_t
   const size_t cb = (size_t)(cbl / (int)cg) * c_per + r0 + (uint32_t)cbl % cg;   /* slot in llr / out / iters */
   const uint32_t K1 = K >> 3, Kb = K >> 3;
   td_crc_tab(crctab, crc_type == 0 ? 0x864cfbu : 0x800063u);
+  /* CRC early stop split over the block's 8 lanes: chunk length, and lane q's multiplier
+   * x^(8 cl (7 - q)) mod P (square and multiply, once per launch) */
+  const uint32_t crc_poly = crc_type == 0 ? 0x864cfbu : 0x800063u;
+  const uint32_t crc_s0 = crc_type == 0 ? (F >> 3) : 0;
+  const uint32_t crc_nb = crc_type == 0 ? (K - 24 - F) >> 3 : (K - 24) >> 3;
+  const uint32_t crc_cl = (crc_nb + 7) >> 3;
+  uint32_t crc_mq = 1;
+  {
+    uint32_t base = 0x100u, n = crc_cl * (7 - (threadIdx.x & 7));
+    while (n) {
+      if (n & 1u) crc_mq = td_mulmod(crc_mq, base, crc_poly);
+      base = td_mulmod(base, base, crc_poly);
+      n >>= 1;
+    }
+  }
   if (lane < 8) done_it[lane] = 0;
 #ifdef TD_DIAG_L2
   /* DIAGNOSTIC ONLY (wrong results): the waves of a launch share TD_DIAG_L2 scratch regions, so the
@@ -765,15 +792,28 @@ __global__ void __launch_bounds__(64) k_td16(int n_cb, uint32_t K, const int16_t
       }
     }
     __syncthreads();
-    if (active && it > 1 && q == 0) {            /* CRC early stop (:1304-1351) */
-      const uint32_t clen = 3, s0b = crc_type == 0 ? (F >> 3) : 0;
-      const uint32_t nbytes = crc_type == 0 ? (K - 24 - F) >> 3 : (K - 24) >> 3;
+    if (active && it > 1) {                      /* CRC early stop (:1304-1351) */
+      /* the block's 8 lanes each run the byte table over one chunk (chunks aligned to the end, the
+       * zero bytes in front of the first leave the zero register unchanged), multiply it into
+       * place by x^(8 cl (7 - q)) and XOR-reduce: a chain of nbytes / 8 table reads, not nbytes */
+      const uint32_t clen = 3;
+      const int st = (int)(q * crc_cl) - (int)(8 * crc_cl - crc_nb);
       uint32_t reg = 0;
-      for (uint32_t i = 0; i < nbytes; i++) reg = ((reg << 8) & 0xffffffu) ^ crctab[((reg >> 16) ^ dec[g][s0b + i]) & 0xffu];
-      const uint32_t oldcrc = (uint32_t)dec[g][Kb - clen] | ((uint32_t)dec[g][Kb - clen + 1] << 8) |
-                              ((uint32_t)dec[g][Kb - clen + 2] << 16);
-      const uint32_t crc = ((reg & 0xffu) << 16) | (reg & 0xff00u) | ((reg >> 16) & 0xffu);
-      if (crc == oldcrc && crc != 0) done_it[g] = it;
+      for (uint32_t i = 0; i < crc_cl; i++) {
+        const int ix = st + (int)i;
+        const uint32_t by = ix >= 0 ? dec[g][crc_s0 + (uint32_t)ix] : 0u;
+        reg = ((reg << 8) & 0xffffffu) ^ crctab[((reg >> 16) ^ by) & 0xffu];
+      }
+      reg = td_mulmod(reg, crc_mq, crc_poly);
+      reg ^= (uint32_t)__shfl_xor((int)reg, 1, 8);
+      reg ^= (uint32_t)__shfl_xor((int)reg, 2, 8);
+      reg ^= (uint32_t)__shfl_xor((int)reg, 4, 8);
+      if (q == 0) {
+        const uint32_t oldcrc = (uint32_t)dec[g][Kb - clen] | ((uint32_t)dec[g][Kb - clen + 1] << 8) |
+                                ((uint32_t)dec[g][Kb - clen + 2] << 16);
+        const uint32_t crc = ((reg & 0xffu) << 16) | (reg & 0xff00u) | ((reg >> 16) & 0xffu);
+        if (crc == oldcrc && crc != 0) done_it[g] = it;
+      }
     }
     __syncthreads();
     if (active && done_it[g]) active = false;
