@@ -107,11 +107,6 @@ static __device__ __forceinline__ s2v max2(s2v a, s2v b) { return __builtin_elem
 
 struct tm_t { s2v v[4]; };
 
-static __device__ __forceinline__ uint4 tm_pack(const tm_t &t)
-{
-  return make_uint4(__builtin_bit_cast(uint32_t, t.v[0]), __builtin_bit_cast(uint32_t, t.v[1]),
-                    __builtin_bit_cast(uint32_t, t.v[2]), __builtin_bit_cast(uint32_t, t.v[3]));
-}
 typedef uint32_t u4v __attribute__((ext_vector_type(4)));   /* checkpoint word in log_map's global / LDS arrays */
 static __device__ __forceinline__ u4v tm_packv(const tm_t &t)
 {
@@ -128,13 +123,6 @@ static __device__ __forceinline__ tm_t tm_unpack(u4v u)
   t.v[2] = __builtin_bit_cast(s2v, w2); t.v[3] = __builtin_bit_cast(s2v, w3);
   return t;
 }
-static __device__ __forceinline__ tm_t tm_unpack(uint4 u)
-{
-  tm_t t;
-  t.v[0] = __builtin_bit_cast(s2v, u.x); t.v[1] = __builtin_bit_cast(s2v, u.y);
-  t.v[2] = __builtin_bit_cast(s2v, u.z); t.v[3] = __builtin_bit_cast(s2v, u.w);
-  return t;
-}
 static __device__ __forceinline__ tm_t tm_init(bool zero_first)
 {
   tm_t t;
@@ -144,8 +132,11 @@ static __device__ __forceinline__ tm_t tm_init(bool zero_first)
 }
 
 /* forward step (compute_alpha16 :286-367): r0 = max(a1+g11, a0-g11), r1 = max(a3-g10, a2+g10),
- * r2 = max(a5+g10, a4-g10), r3 = max(a7-g11, a6+g11), r4..r7 the opposite signs; minus max */
-static __device__ __forceinline__ void alpha_step(tm_t &a, short g11, short g10)
+ * r2 = max(a5+g10, a4-g10), r3 = max(a7-g11, a6+g11), r4..r7 the opposite signs; minus max.
+ * The reference form in the fixed layout N; log_map runs alpha_ph, its layout-rotating restatement
+ * (kept as the specification alpha_ph is checked against in review; beta_step / ext_of below still
+ * run the backward re-run) */
+[[maybe_unused]] static __device__ __forceinline__ void alpha_step(tm_t &a, short g11, short g10)
 {
   const s2v G = {g11, (short)-g10}, H = {g10, (short)-g11};
   const s2v x13 = SHUF2(a.v[0], a.v[1], 1, 3), x02 = SHUF2(a.v[0], a.v[1], 0, 2);
@@ -548,7 +539,10 @@ static __device__ __attribute__((noinline)) void log_map(TD_G short *sys, TD_G c
     }
     ext[64 * (k0 + j) + q] = v;
   };
-  bundle_t bx, by;                             /* operands in flight (bx: the next segment) */
+  bundle_t bx;                                 /* operands in flight: the next segment */
+#if TD_BPF > 1
+  bundle_t by;                                 /* and the one after (TD_BPF = 2) */
+#endif
   fetch(bx, (int)nseg - 1);
   /* top segments (partial, or holding steps >= kr): guarded steps, alpha recompute then beta */
   for (int seg = (int)nseg - 1; seg >= nfast; seg--) {

@@ -49,18 +49,6 @@ __device__ __forceinline__ short sa8(int v) { return (short)max(-128, min(127, v
 
 struct tm8_t { s2v8 v[4]; };
 
-__device__ __forceinline__ uint4 pk8(const tm8_t &t)
-{
-  return make_uint4(__builtin_bit_cast(uint32_t, t.v[0]), __builtin_bit_cast(uint32_t, t.v[1]),
-                    __builtin_bit_cast(uint32_t, t.v[2]), __builtin_bit_cast(uint32_t, t.v[3]));
-}
-__device__ __forceinline__ tm8_t up8(uint4 u)
-{
-  tm8_t t;
-  t.v[0] = __builtin_bit_cast(s2v8, u.x); t.v[1] = __builtin_bit_cast(s2v8, u.y);
-  t.v[2] = __builtin_bit_cast(s2v8, u.z); t.v[3] = __builtin_bit_cast(s2v8, u.w);
-  return t;
-}
 /* log_map8_lane is not inlined: explicit address spaces keep its scratch accesses global_* / ds_*
  * (see oai4g_decode.hip, TD_G); checkpoint words as an ext vector, unpacked through scalars */
 #define TD8_GAS __attribute__((address_space(1)))
@@ -140,6 +128,18 @@ struct td8_blk_t {   /* one wave's scratch: 4 blocks interleaved, element e of b
   short *s0, *s1, *s2, *yp1, *yp2, *ext, *ext2;
   uint4 *A;
 };
+
+/* a * b mod P over GF(2) for the 24-bit CRC generators (P without its x^24 term) */
+__device__ __forceinline__ uint32_t t8_mulmod(uint32_t a, uint32_t b, uint32_t poly)
+{
+  uint32_t r = 0;
+  for (int i = 23; i >= 0; i--) {
+    r <<= 1;
+    if (r & 0x1000000u) r ^= 0x1000000u | poly;
+    if ((b >> i) & 1u) r ^= a;
+  }
+  return r;
+}
 
 __device__ __forceinline__ uint32_t t8_ix(uint32_t e) { return ((e >> 4) << 6) | (e & 15); }
 
@@ -324,6 +324,19 @@ __global__ void __launch_bounds__(64) TD8_WAVES_ATTR k_td8(int n_cb, uint32_t K,
     crctab[v] = r;
   }
   if (lane < 4) done_it[lane] = 0;
+  const uint32_t crc_poly = crc_type == 0 ? 0x864cfbu : 0x800063u;
+  const uint32_t crc_s0 = crc_type == 0 ? (F >> 3) : 0;
+  const uint32_t crc_nb = crc_type == 0 ? (K - 24 - F) >> 3 : (K - 24) >> 3;
+  const uint32_t crc_cl = (crc_nb + 15) >> 4;
+  uint32_t crc_mq = 1;                           /* x^(8 cl (15 - q)) mod P */
+  {
+    uint32_t base = 0x100u, n = crc_cl * (15 - (lane & 15));
+    while (n) {
+      if (n & 1u) crc_mq = t8_mulmod(crc_mq, base, crc_poly);
+      base = t8_mulmod(base, base, crc_poly);
+      n >>= 1;
+    }
+  }
 #ifdef TD_DIAG_L2
   /* DIAGNOSTIC ONLY (wrong results): shared scratch regions, the working set stays in the L2s */
   const td8_blk_t Wv = t8_layout(scratch + (size_t)(blockIdx.x % TD_DIAG_L2) * wave_bytes, K);
@@ -437,14 +450,24 @@ __global__ void __launch_bounds__(64) TD8_WAVES_ATTR k_td8(int n_cb, uint32_t K,
       }
     }
     __syncthreads();
-    if (active && it > 1 && q == 0) {            /* CRC early stop (:1583-1628) */
-      const uint32_t s0b = crc_type == 0 ? (F >> 3) : 0;
-      const uint32_t nbytes = crc_type == 0 ? (K - 24 - F) >> 3 : (K - 24) >> 3;
+    if (active && it > 1) {                      /* CRC early stop (:1583-1628) */
+      /* split over the block's 16 lanes as in k_td16: chunks aligned to the end, each multiplied
+       * into place by x^(8 cl (15 - q)), XOR-reduced */
+      const int st = (int)(q * crc_cl) - (int)(16 * crc_cl - crc_nb);
       uint32_t reg = 0;
-      for (uint32_t i = 0; i < nbytes; i++) reg = ((reg << 8) & 0xffffffu) ^ crctab[((reg >> 16) ^ dec[g][s0b + i]) & 0xffu];
-      const uint32_t oldcrc = (uint32_t)dec[g][Kb - 3] | ((uint32_t)dec[g][Kb - 2] << 8) | ((uint32_t)dec[g][Kb - 1] << 16);
-      const uint32_t crc = ((reg & 0xffu) << 16) | (reg & 0xff00u) | ((reg >> 16) & 0xffu);
-      if (crc == oldcrc && crc != 0) done_it[g] = it;
+      for (uint32_t i = 0; i < crc_cl; i++) {
+        const int ix = st + (int)i;
+        const uint32_t by = ix >= 0 ? dec[g][crc_s0 + (uint32_t)ix] : 0u;
+        reg = ((reg << 8) & 0xffffffu) ^ crctab[((reg >> 16) ^ by) & 0xffu];
+      }
+      reg = t8_mulmod(reg, crc_mq, crc_poly);
+#pragma unroll
+      for (int m = 1; m < 16; m <<= 1) reg ^= (uint32_t)__shfl_xor((int)reg, m, 16);
+      if (q == 0) {
+        const uint32_t oldcrc = (uint32_t)dec[g][Kb - 3] | ((uint32_t)dec[g][Kb - 2] << 8) | ((uint32_t)dec[g][Kb - 1] << 16);
+        const uint32_t crc = ((reg & 0xffu) << 16) | (reg & 0xff00u) | ((reg >> 16) & 0xffu);
+        if (crc == oldcrc && crc != 0) done_it[g] = it;
+      }
     }
     __syncthreads();
     if (active && done_it[g]) active = false;
