@@ -38,17 +38,20 @@ static __device__ __forceinline__ short ssub(short a, short b) { return __builti
 #define TD_FSG 12            /* forward chunk of the gathered forms (two loads deep: pi, then the gather);
                                 round 4, loads held unpacked: C5 3 -> 192 k, 6 -> 222 k, 9 -> 223 k, 12 -> 229 k */
 #endif
+#ifndef TD_FSGD
+#define TD_FSGD TD_FSG       /* the same for decoder 1's deinterleave + update form (two more streams per step) */
+#endif
 #ifndef TD_XR
 #define TD_XR 32      /* steps per round of the exchange gathers (index loads, then gathers, in flight) */
 #endif
 #ifndef TD_BPF
-#define TD_BPF 1      /* backward pass: segments between an operand fetch and its alpha recompute (1 or 2) */
+#define TD_BPF 2      /* backward pass: segments between an operand fetch and its alpha recompute (1 or 2; decoder 1's form stays at 1) */
 #endif
 #ifndef TD_SEG
 #define TD_SEG 6      /* alpha checkpoint interval (steps), a multiple of 3 so every checkpoint holds layout EO
                          (round 2 measured 4 best of 2/4/8/16 with the fixed layout) */
 #endif
-static_assert(TD_FS % 3 == 0 && TD_FSG % 3 == 0, "layout period");
+static_assert(TD_FS % 3 == 0 && TD_FSG % 3 == 0 && TD_FSGD % 3 == 0, "layout period");
 /* TD_SEG == 6: every checkpoint holds layout EO, and the re-run's alpha(0..5) fill exactly segment 0
  * (alpha(6) onward continue the first run); 12 spills */
 static_assert(TD_SEG == 6, "checkpoint interval");
@@ -394,7 +397,7 @@ static __device__ __attribute__((noinline)) void log_map(TD_G short *sys, TD_G c
   const int pK = (int)(K1 % 3);                /* layout of alpha(K1) and beta(K1) */
   /* forward, first run, in chunks of FS steps (operands of the next chunk in flight); alpha(k) is
    * in layout k mod 3 (alpha(0) EO: tm_init puts state 0 at register 0's low half in every layout) */
-  constexpr int FS = SRC == TD_SRC_SYS ? TD_FS : TD_FSG;
+  constexpr int FS = SRC == TD_SRC_SYS ? TD_FS : (SRC == TD_SRC_INTL ? TD_FSG : TD_FSGD);
   const uint32_t nfc = (K1 + FS - 1) / FS;
   tm_t a = tm_init(q == 0);
   {
@@ -520,14 +523,13 @@ static __device__ __attribute__((noinline)) void log_map(TD_G short *sys, TD_G c
   /* a segment's operands in registers: gammas, and (POST) its sys and s0 */
   struct segops_t {
     uint32_t gg[TD_SEG];                       /* g11 | g10 << 16 */
-    short ss[TD_SEG], zz[TD_SEG];
+    s2v sz[TD_SEG];                            /* (POST) (sys, s0), packed once the loads have landed */
   };
   auto take = [&](segops_t &o, const bundle_t &d) {
 #pragma unroll
     for (int j = 0; j < TD_SEG; j++) {
       o.gg[j] = gg_of(d.sy[j], d.pa[j]);
-      o.ss[j] = d.sy[j];
-      o.zz[j] = d.zs[j];
+      if constexpr (POST) o.sz[j] = (s2v){d.sy[j], d.zs[j]};
     }
   };
   /* extrinsic of step k0 + j from alpha (layout j mod 3) and beta(k0 + j + 1) */
@@ -535,14 +537,14 @@ static __device__ __attribute__((noinline)) void log_map(TD_G short *sys, TD_G c
     constexpr int j = decltype(J)::value;
     short v = ext_ph<j % 3>(tm_unpack(al), b, gk_of(o.gg[j]));
     if constexpr (POST) {
-      v = __builtin_elementwise_add_sat(__builtin_elementwise_sub_sat(v, o.ss[j]), o.zz[j]);
+      v = __builtin_elementwise_add_sat(__builtin_elementwise_sub_sat(v, o.sz[j].x), o.sz[j].y);
     }
     ext[64 * (k0 + j) + q] = v;
   };
-  bundle_t bx;                                 /* operands in flight: the next segment */
-#if TD_BPF > 1
-  bundle_t by;                                 /* and the one after (TD_BPF = 2) */
-#endif
+  /* backward prefetch distance: decoder 1's form (POST) holds two more operand streams and has no
+   * registers left for a second bundle */
+  constexpr int BPF = POST ? 1 : TD_BPF;
+  bundle_t bx, by;                             /* operands in flight: the next segment (and, BPF = 2, the one after) */
   fetch(bx, (int)nseg - 1);
   /* top segments (partial, or holding steps >= kr): guarded steps, alpha recompute then beta */
   for (int seg = (int)nseg - 1; seg >= nfast; seg--) {
@@ -579,21 +581,21 @@ static __device__ __attribute__((noinline)) void log_map(TD_G short *sys, TD_G c
       tm_t c = tm_unpack(bx.A);
       take(cur, bx);
       if (nfast > 1) fetch(bx, nfast - 2);
-#if TD_BPF > 1
-      if (nfast > 2) fetch(by, nfast - 3);
-#endif
+      if constexpr (BPF > 1) {
+        if (nfast > 2) fetch(by, nfast - 3);
+      }
       sfor<0, TD_SEG>([&](auto J) {
         constexpr int j = decltype(J)::value;
         alc[j] = tm_packv(c);
         alpha_ph<j % 3>(c, gk_of(cur.gg[j]));
       });
     }
-    /* one segment: bt holds segment seg - 1's operands; it is refilled TD_BPF + 1 segments down */
+    /* one segment: bt holds segment seg - 1's operands; it is refilled BPF + 1 segments down */
     auto step_seg = [&](int seg, bundle_t &bt) {
       const int k0 = seg * TD_SEG;
       tm_t c = tm_unpack(bt.A);                /* alpha((seg - 1) TD_SEG) */
       take(nx, bt);
-      if (seg > TD_BPF) fetch(bt, seg - 1 - TD_BPF);
+      if (seg > BPF) fetch(bt, seg - 1 - BPF);
       sfor<0, TD_SEG>([&](auto J) {
         constexpr int j = decltype(J)::value;
         constexpr int jj = TD_SEG - 1 - j;
@@ -607,15 +609,15 @@ static __device__ __attribute__((noinline)) void log_map(TD_G short *sys, TD_G c
       for (int j = 0; j < TD_SEG; j++) alc[j] = aln[j];
     };
     int seg = nfast - 1;
-#if TD_BPF > 1
-    for (; seg >= 2; seg -= 2) {
-      step_seg(seg, bx);
-      step_seg(seg - 1, by);
+    if constexpr (BPF > 1) {
+      for (; seg >= 2; seg -= 2) {
+        step_seg(seg, bx);
+        step_seg(seg - 1, by);
+      }
+      if (seg == 1) step_seg(1, bx);
+    } else {
+      for (; seg >= 1; seg--) step_seg(seg, bx);
     }
-    if (seg == 1) step_seg(1, bx);
-#else
-    for (; seg >= 1; seg--) step_seg(seg, bx);
-#endif
     sfor_down<0, TD_SEG>([&](auto J) {
       constexpr int j = decltype(J)::value;
       emit(J, cur, alc[j], 0);
