@@ -89,3 +89,21 @@ def test_rate_matching_rx_and_deinterleave(gpu, K, C, r, G, Qm, rv, clear):
     d_o = O.subblock_deinterleave(w_o, K)
     d_g = gpu.sub_block_deinterleaving_turbo(D, w_o)
     assert np.array_equal(d_g[96:96 + 3 * K + 12], d_o)
+
+
+# every K up to 320 (K1 = K / 8 steps per window): the backward pass's segment schedule changes
+# with K1 -- no full segment below the re-run (K1 <= 11), one to six of them with the two-bundle
+# operand prefetch taking both its odd and even branches, a partial top segment or none
+SMALL_K = [K for K in sorted(QPP) if K <= 320]
+
+
+def test_drop_in_decoder_every_small_K(gpu):
+    rng = np.random.default_rng(320)
+    for K in SMALL_K:
+        for amp, sigma, crc, max_it in ((32, 24, "a", 8), (32, 40, "b", 5)):
+            y = noisy_llr(rng, K, amp, sigma, crc)
+            ct = 0 if crc == "a" else 1
+            it_o, dec_o = O.turbo_decode(y, K, max_it=max_it, crc_type=ct)
+            it_g, dec_g = gpu.turbo_decoder16(y, K, max_iterations=max_it, crc_type=ct)
+            assert it_g == it_o, (K, sigma)
+            assert np.array_equal(dec_g[:K // 8], dec_o), (K, sigma)
