@@ -575,18 +575,21 @@ static __device__ void encode_codeword(const cfg_dev_t *__restrict__ c, uint32_t
   const uint32_t tid = threadIdx.x, nth = blockDim.x, wave = tid >> 6, lane = tid & 63, nwaves = nth >> 6;
   const uint32_t sfi = DEBUG ? sf : (c->first_sf + (sf0 + sf) * c->sf_step) % 10;
   const uint32_t C = cw.C, sw = cw.stream_words;
-  /* LDS carve-up.  Region A: TB || CRC and the CRC tables (phases 0-2), the QPP-interleaved
-   * words (phase 3), packed w (phase 4).  Region B: the constituent streams. */
+  /* LDS carve-up.  Region A: TB || CRC (phases 0-2), the QPP-interleaved words (phase 3), one half
+   * of the e words (phase 4).  Region B: the CRC byte tables (phases 0-1), then the constituent
+   * streams (the QPP planes in the parity slots during phase 3a). */
   uint32_t *tbw = lds_base;
-  uint32_t *crctab_a = tbw + c->lds_tb_words;
-  uint32_t *crctab_b = crctab_a + 256;
   uint32_t *strm = lds_base + c->lds_a_words;
+  /* the CRC byte tables live in region B until segmentation writes the streams (phases 0-1) */
+  uint32_t *crctab_a = strm;
+  uint32_t *crctab_b = crctab_a + 256;
   uint32_t *tails = strm + c->lds_b_words;
   uint32_t *crcs = tails + 2 * OAI4G_MAX_CB;             /* [0] = CRC24A, [1+r] = CRC24B of block r */
   uint32_t *red = crcs + OAI4G_MAX_CB + 2;               /* 4 per-wave partials */
   enc_tabs_t *tabs = (enc_tabs_t *)(red + 4);
+  uint32_t *dbg_ebuf = (uint32_t *)(tabs + 1);          /* k_encode_debug only: the whole codeword's e words */
   uint8_t *tbb = (uint8_t *)tbw;
-  const uint32_t G = cw.G[sfi], Gw = (G + 31) >> 5;
+  const uint32_t G = cw.G[sfi];
 
   /* ---- phase 0: TB bytes, stream words past each block's data, tables ---- */
   const uint8_t *src = payload + (size_t)(DEBUG ? 0 : (sf * c->n_cw + cwi)) * c->payload_stride;
@@ -601,13 +604,6 @@ static __device__ void encode_codeword(const cfg_dev_t *__restrict__ c, uint32_t
         if (valid < 4) v &= (1u << (8 * valid)) - 1u;
       }
       tbw[i] = v;
-    }
-    /* stream words past the data of each block (tail bits, read-ahead); the data words are
-     * fully written by segmentation (systematic) and the phase-3 planes / turbo (parity) */
-    for (uint32_t i = ct; i < C * 3 * 4; i += cn) {
-      const uint32_t slot = i >> 2, r = slot / 3;
-      const uint32_t w = ((cw.K[r] + 31) >> 5) + (i & 3u);
-      if (w < sw) strm[slot * sw + w] = 0u;
     }
     if (ct == 0) crcs[0] = 0u;                    /* phase 1's XOR accumulator (C > 1) */
     for (uint32_t v = ct; v < 256; v += cn) {     /* the register-in-the-top-24-bits form */
@@ -675,6 +671,14 @@ static __device__ void encode_codeword(const cfg_dev_t *__restrict__ c, uint32_t
     for (uint32_t i = tid; i < Ab + 3; i += nth) dbg.b[i] = tbb[i];
   if (stop_phase <= 1) return;
 
+  /* stream words past the data of each block (tail bits, read-ahead; region B held the CRC tables
+   * until here); the data words are fully written by segmentation (systematic) and the phase-3
+   * planes / turbo (parity) */
+  for (uint32_t i = tid; i < C * 3 * 4; i += nth) {
+    const uint32_t slot = i >> 2, r = slot / 3;
+    const uint32_t w = ((cw.K[r] + 31) >> 5) + (i & 3u);
+    if (w < sw) strm[slot * sw + w] = 0u;
+  }
   /* ---- phase 2: segmentation -> systematic streams (LSB-first words), one word per thread over
    * the words of all blocks; a word inside the copied bytes is one unaligned 4-byte read ---- */
   const uint32_t nw = cw.ilv_off[C], u0 = cw.u0, n0 = cw.n0;
@@ -725,13 +729,12 @@ static __device__ void encode_codeword(const cfg_dev_t *__restrict__ c, uint32_t
    * Plane 0 is the systematic stream, planes 1 / 2 are staged in the (not yet written) parity
    * stream slots of the block, plane 3 in region A behind the interleaved words. ---- */
   uint32_t *ilv = lds_base;
-  [[maybe_unused]] uint32_t *pl3 = lds_base + nw;
-#ifndef OAI4G_ENC_QPP_WALK
   /* byte-interleaved planes of every block, over x' < Q only: word w holds positions x' = 8w..8w+7,
    * byte q = plane q (c[x' + qQ]); plane p at x = x' + uQ is byte (p + u) mod 4 there, so one
    * rotate by 8u + (x' & 7) aligns all four bits of position x.  Built from four 32-bit plane words
-   * per 32 positions with byte permutes. */
-  uint32_t *bi = lds_base + nw;
+   * per 32 positions with byte permutes.  A block's planes (K / 32 words) live in its first parity
+   * stream's slot, which the turbo encoder writes only in phase 3b: region A holds just the
+   * interleaved words. */
   for (uint32_t r = 0; r < C; r++) {
     const uint32_t K = r < n0 ? kk0 : kk1, Kw = (K + 31) >> 5, Q = K >> 2, io = r < n0 ? r * kw0 : u0 + (r - n0) * kw1;
     const uint32_t *sys = strm + r * 3 * sw;
@@ -751,7 +754,7 @@ static __device__ void encode_codeword(const cfg_dev_t *__restrict__ c, uint32_t
       for (uint32_t jb = 0; jb < 4; jb++) {
         const uint32_t t01 = __builtin_amdgcn_perm(P[1], P[0], 0x0c0c0000u | jb | ((4 + jb) << 8));
         const uint32_t t23 = __builtin_amdgcn_perm(P[3], P[2], 0x00000c0cu | (jb << 16) | ((4 + jb) << 24));
-        if (4 * g + jb < nbw) bi[io + 4 * g + jb] = t01 | t23;
+        if (4 * g + jb < nbw) strm[(r * 3 + 1) * sw + 4 * g + jb] = t01 | t23;
       }
     }
   }
@@ -763,11 +766,10 @@ static __device__ void encode_codeword(const cfg_dev_t *__restrict__ c, uint32_t
     for (uint32_t i = tid; i < nw; i += nth) {
       uint32_t r, j, K, ki;
       unit_of(i, r, j, K, ki);
-      (void)r;
       const uint32_t Q = K >> 2;
       const uint4 e4 = *(const uint4 *)&cw.qpp_tab[ki][4 * j];
       const uint32_t ew[4] = {e4.x, e4.y, e4.z, e4.w};
-      const uint32_t *b8 = bi + (i - j);
+      const uint32_t *b8 = strm + (r * 3 + 1) * sw;     /* block r's planes */
       uint32_t acc = 0;
 #pragma unroll
       for (int b = 0; b < 8; b++) {
@@ -797,72 +799,6 @@ static __device__ void encode_codeword(const cfg_dev_t *__restrict__ c, uint32_t
       }
     }
   }
-#else
-  /* rotated planes 1..3 of every block: uniform loops over (block, plane), a word per lane */
-  for (uint32_t r = 0; r < C; r++) {
-    const uint32_t K = r < n0 ? kk0 : kk1, Kw = (K + 31) >> 5, Q = K >> 2, io = r < n0 ? r * kw0 : u0 + (r - n0) * kw1;
-    const uint32_t *sys = strm + r * 3 * sw;
-    for (uint32_t w = tid; w < Kw; w += nth) ilv[io + w] = 0u;
-#pragma unroll
-    for (uint32_t pr = 1; pr <= 3; pr++) {
-      uint32_t *dst = pr < 3 ? strm + (r * 3 + pr) * sw : pl3 + io;
-      for (uint32_t w = tid; w < Kw; w += nth) {
-        uint32_t src = 32 * w + pr * Q;
-        src = src >= K ? src - K : src;
-        const uint32_t wi = src >> 5;
-        const uint32_t lo = sys[wi], hi = wi + 1 < Kw ? sys[wi + 1] : 0u;   /* bits >= K are zero */
-        uint32_t v = __builtin_amdgcn_alignbit(hi, lo, src);
-        if (src + 32 > K) v |= sys[0] << (K - src);                          /* wrap to c_0.. */
-        dst[w] = v;
-      }
-    }
-  }
-  __syncthreads();
-  {
-    /* 8-step units: unit j of block r walks k = 8j .. 8j+7 (< Q) and yields one byte of each
-     * quarter; there are ceil(K/32) units per block, indexed like the interleaved words */
-    const uint32_t d2a = __builtin_amdgcn_readfirstlane(cw.qpp_d2[0]), d2b = __builtin_amdgcn_readfirstlane(cw.qpp_d2[1]);
-    const bool s3a = __builtin_amdgcn_readfirstlane(cw.qpp_s3[0]) != 0, s3b = __builtin_amdgcn_readfirstlane(cw.qpp_s3[1]) != 0;
-    for (uint32_t i = tid; i < nw; i += nth) {
-      uint32_t r, j, K, ki;
-      unit_of(i, r, j, K, ki);
-      const uint32_t Q = K >> 2, start = cw.qpp0[ki][j], d2 = ki ? d2b : d2a;
-      const uint32_t *p0 = strm + r * 3 * sw, *p3 = pl3 + (i - j);
-      uint32_t pi = start & 0xffffu, dl = start >> 16, a0 = 0, a1 = 0, a2 = 0, a3 = 0;
-#pragma unroll
-      for (int b = 0; b < 8; b++) {
-        const uint32_t wi = pi >> 5;
-        a0 |= __builtin_amdgcn_ubfe(p0[wi], pi, 1u) << b;
-        a1 |= __builtin_amdgcn_ubfe(p0[wi + sw], pi, 1u) << b;
-        a2 |= __builtin_amdgcn_ubfe(p0[wi + 2 * sw], pi, 1u) << b;
-        a3 |= __builtin_amdgcn_ubfe(p3[wi], pi, 1u) << b;
-        pi += dl;
-        pi = min(pi, pi - K);
-        dl += d2;
-        dl = min(dl, dl - K);
-      }
-      const uint32_t n = Q - 8 * j;
-      if (n < 8) {
-        const uint32_t m = (1u << n) - 1u;
-        a0 &= m; a1 &= m; a2 &= m; a3 &= m;
-      }
-      /* output quarter q reads plane (q c4 / Q) mod 4 */
-      const bool s3 = ki ? s3b : s3a;
-      const uint32_t q1 = s3 ? a3 : a1, q3 = s3 ? a1 : a3;
-      uint32_t *o = ilv + (i - j);
-      if ((Q & 7u) == 0) {                                  /* byte-aligned quarters (32 | K) */
-        uint8_t *ob = (uint8_t *)o + j;
-        const uint32_t qb = Q >> 3;
-        ob[0] = (uint8_t)a0; ob[qb] = (uint8_t)q1; ob[2 * qb] = (uint8_t)a2; ob[3 * qb] = (uint8_t)q3;
-      } else {
-        or_bits(o, 8 * j, a0);
-        or_bits(o, Q + 8 * j, q1);
-        or_bits(o, 2 * Q + 8 * j, a2);
-        or_bits(o, 3 * Q + 8 * j, q3);
-      }
-    }
-  }
-#endif
   __syncthreads();
   if (stop_phase == 23) return;   /* diagnostics: QPP interleaving only */
 
@@ -931,12 +867,11 @@ static __device__ void encode_codeword(const cfg_dev_t *__restrict__ c, uint32_t
    * position among the non-NULL entries of w is closed-form, and the run goes straight to its
    * place(s) in the circular-buffer output: e index (ci - k0c) mod Nnn (+ j Nnn while < E),
    * positions >= Ncb excluded.  Region A (the interleaved words are dead) holds the output. ---- */
-  uint32_t *ebuf = lds_base;
-  for (uint32_t i = tid; i < Gw + 1; i += nth) ebuf[i] = 0u;
-  __syncthreads();
-#ifndef OAI4G_ENC_RM_GENERIC
-  /* the host-built plan (cw.rm_src / rm_dst, oai4g_host.cpp rm_plan): per (block size, tile, lane)
-   * the stream bits to load and, after the transpose, where the column run goes */
+  /* The e words are staged per half of the blocks: blocks [0, hb) then [hb, C), each half's words
+   * (its first word may be shared with the previous half: carried over) zeroed, ORed into, then
+   * scrambled and stored.  Region A holds one half (the host sizes it, lds_a_words), so the
+   * three streams and the output are never resident in full together.  The debug kernel stages
+   * the whole codeword in one pass behind the tables (dbg.ebuf). */
   {
     const uint32_t lane32 = tid & 31;
     const uint32_t nt0 = __builtin_amdgcn_readfirstlane(cw.ntk[0]), nt1 = __builtin_amdgcn_readfirstlane(cw.ntk[1]);
@@ -947,8 +882,10 @@ static __device__ void encode_codeword(const cfg_dev_t *__restrict__ c, uint32_t
     /* no repetition (E <= Nnn for every block): a run lands once at most */
     const bool once = Ehi <= min(Nnn0, Nnn1) && Elo <= min(Nnn0, Nnn1);
     const uint32_t pp0 = (nt0 + 1) >> 1, pp1 = (nt1 + 1) >> 1;            /* tile pairs per block */
-    const uint32_t psplit = n0 * pp0, ptot = psplit + (C - n0) * pp1;
+    const uint32_t psplit = n0 * pp0;
     const uint32_t pm0 = ((1u << 20) + pp0 - 1) / pp0, pm1 = ((1u << 20) + pp1 - 1) / pp1;
+    auto ro_of = [&](uint32_t r) { return r >= es ? es * Elo + (r - es) * Ehi : r * Elo; };   /* e bit offset of block r */
+    auto pair0 = [&](uint32_t r) { return r < n0 ? r * pp0 : psplit + (r - n0) * pp1; };      /* first tile pair of block r */
     /* tile pair P -> (block size, block, first tile); the pair's plan rows are contiguous, so a
      * lane's plan words sit at a wave-uniform base + 4 lane.  Loaded one pair ahead. */
     auto decode = [&](uint32_t P, uint32_t &ki, uint32_t &r, uint32_t &t0) {
@@ -958,169 +895,90 @@ static __device__ void encode_codeword(const cfg_dev_t *__restrict__ c, uint32_t
       r = ki ? n0 + rr : rr;
       t0 = 2 * rem;
     };
-    uint32_t nsrc = 1u << 5, ndst = 0;
-    if (wave < ptot) {
-      uint32_t ki, r, t0;
-      decode(__builtin_amdgcn_readfirstlane(wave), ki, r, t0);
-      nsrc = (&cw.rm_src[ki][t0][0])[lane];
-      ndst = (&cw.rm_dst[ki][t0][0])[lane];
-    }
-    for (uint32_t pw = wave; pw < ptot; pw += nwaves) {
-      const uint32_t P = __builtin_amdgcn_readfirstlane(pw);
-      uint32_t ki, r, t0;
-      decode(P, ki, r, t0);
-      const uint32_t ND = ki ? ND1 : ND0;
-      const uint32_t src = nsrc, dst = ndst;
-      if (P + nwaves < ptot) {
-        uint32_t k2, r2, t2;
-        decode(P + nwaves, k2, r2, t2);
-        (void)r2;
-        nsrc = (&cw.rm_src[k2][t2][0])[lane];
-        ndst = (&cw.rm_dst[k2][t2][0])[lane];
+    gu32_t *gold = (gu32_t *)(c->gold_tab + (size_t)(sfi * c->n_cw + cwi) * c->ebits_words);
+    uint32_t *eout = DEBUG ? nullptr : ebits + (size_t)(sf * c->n_cw + cwi) * c->ebits_words;
+    uint32_t *ebuf = DEBUG ? dbg_ebuf : lds_base;
+    const uint32_t hb = DEBUG ? C : (C + 1) >> 1, nhalf = DEBUG ? 1u : 2u;
+    uint32_t carry = 0;                          /* the boundary word of the first half */
+    for (uint32_t h = 0; h < nhalf; h++) {
+      const uint32_t rb0 = h ? hb : 0, rb1 = h ? C : hb;
+      const uint32_t eb0 = ro_of(rb0), eb1 = rb1 < C ? ro_of(rb1) : G;   /* e bits [eb0, eb1) */
+      const uint32_t w0 = eb0 >> 5, nwh = ((eb1 + 31) >> 5) - w0;       /* staged words */
+      for (uint32_t i = tid; i < nwh + 1; i += nth) ebuf[i] = (i == 0 && h) ? carry : 0u;
+      __syncthreads();
+      const uint32_t pb = pair0(rb0), pe = pair0(rb1), bit0 = 32 * w0;
+      uint32_t nsrc = 1u << 5, ndst = 0;
+      if (pb + wave < pe) {
+        uint32_t ki, r, t0;
+        decode(__builtin_amdgcn_readfirstlane(pb + wave), ki, r, t0);
+        nsrc = (&cw.rm_src[ki][t0][0])[lane];
+        ndst = (&cw.rm_dst[ki][t0][0])[lane];
       }
-      const uint32_t *bb = strm + r * 3 * sw - 1;                           /* block streams - 1 word */
-      const uint32_t *wp = bb + ((src >> 5) & 0x7fffu);
-      uint32_t y = __builtin_amdgcn_alignbit(wp[1], wp[0], src);            /* bits before 0 are NULLs */
-      if (src & OAI4G_RM_SRC_LAST) {
-        y &= 0x7fffffffu;                       /* j = Kpi-1 reads y^(2)_0: NULL if ND > 0 */
-        if (ND == 0) y |= (bb[1 + 2 * sw] & 1u) << 31;
-      }
-      y = transpose32(y, lane32);
-      const uint32_t m = (dst >> 21) & 63u;
-      if (m) {
-        const uint32_t z = (dst >> 16) & 31u, o = dst & 0xffffu;
-        y = (y >> z) & (0xffffffffu >> (32 - m));
-        const bool eh = r >= es;
-        const uint32_t E = eh ? Ehi : Elo, ro = eh ? es * Elo + (r - es) * Ehi : r * Elo;
-        if (once && !(dst & OAI4G_RM_DST_WRAP)) {
-          if (o < E) or_bits(ebuf, ro + o, y & (0xffffffffu >> (32 - min(m, E - o))));
-        } else {
-          /* the run may straddle the wrap back to k0c; E > Nnn repeats the buffer */
-          const uint32_t Nnn = ki ? Nnn1 : Nnn0, ma = min(m, Nnn - o);
-          for (uint32_t part = 0; part < 2; part++) {
-            const uint32_t len = part ? m - ma : ma, os = part ? 0u : o;
-            const uint32_t v = part ? (ma < 32 ? y >> ma : 0u) : (ma < 32 ? y & ((1u << ma) - 1u) : y);
-            for (uint32_t x = os; len && x < E; x += Nnn) {                     /* repetition rounds */
-              const uint32_t l = min(len, E - x);
-              or_bits(ebuf, ro + x, v & (0xffffffffu >> (32 - l)));
-            }
-          }
+      for (uint32_t pw = pb + wave; pw < pe; pw += nwaves) {
+        const uint32_t P = __builtin_amdgcn_readfirstlane(pw);
+        uint32_t ki, r, t0;
+        decode(P, ki, r, t0);
+        const uint32_t ND = ki ? ND1 : ND0;
+        const uint32_t src = nsrc, dst = ndst;
+        if (P + nwaves < pe) {
+          uint32_t k2, r2, t2;
+          decode(P + nwaves, k2, r2, t2);
+          (void)r2;
+          nsrc = (&cw.rm_src[k2][t2][0])[lane];
+          ndst = (&cw.rm_dst[k2][t2][0])[lane];
         }
-      }
-    }
-  }
-#else
-  {
-    const uint32_t R0 = __builtin_amdgcn_readfirstlane(cw.Rk[0]), R1 = __builtin_amdgcn_readfirstlane(cw.Rk[1]);
-    const uint32_t ND0 = __builtin_amdgcn_readfirstlane(cw.NDk[0]), ND1 = __builtin_amdgcn_readfirstlane(cw.NDk[1]);
-    const uint32_t nt0 = __builtin_amdgcn_readfirstlane(cw.ntk[0]), nt1 = __builtin_amdgcn_readfirstlane(cw.ntk[1]);
-    const uint32_t tz0 = __builtin_amdgcn_readfirstlane(cw.t0k[0]), tz1 = __builtin_amdgcn_readfirstlane(cw.t0k[1]);
-    const uint32_t nm0 = __builtin_amdgcn_readfirstlane(cw.ntmag[0]), nm1 = __builtin_amdgcn_readfirstlane(cw.ntmag[1]);
-    const uint32_t Ncb0 = __builtin_amdgcn_readfirstlane(cw.Ncbk[0]), Ncb1 = __builtin_amdgcn_readfirstlane(cw.Ncbk[1]);
-    const uint32_t Nnn0 = __builtin_amdgcn_readfirstlane(cw.Nnnk[0]), Nnn1 = __builtin_amdgcn_readfirstlane(cw.Nnnk[1]);
-    const uint32_t k0c0 = __builtin_amdgcn_readfirstlane(cw.k0ck[0]), k0c1 = __builtin_amdgcn_readfirstlane(cw.k0ck[1]);
-    const uint32_t nc00 = __builtin_amdgcn_readfirstlane(cw.nullcol[0][0]), nc01 = __builtin_amdgcn_readfirstlane(cw.nullcol[0][1]);
-    const uint32_t nc10 = __builtin_amdgcn_readfirstlane(cw.nullcol[1][0]), nc11 = __builtin_amdgcn_readfirstlane(cw.nullcol[1][1]);
-    /* blocks r < es carry E_lo bits, the rest E_hi (36.212 5.1.4.1.2) */
-    const uint32_t es = __builtin_amdgcn_readfirstlane(cw.esplit[sfi]);
-    const uint32_t Elo = __builtin_amdgcn_readfirstlane(cw.E[sfi][0]), Ehi = __builtin_amdgcn_readfirstlane(cw.E[sfi][C - 1]);
-    const uint32_t tsplit = n0 * nt0, ntot = tsplit + (C - n0) * nt1;
-    const uint32_t lane32 = tid & 31, wcol = colperm(lane32), below = (1u << wcol) - 1u;
-    /* per-lane column constants for (block size ki, region il): compact index of the column's
-     * first non-NULL entry, its row-0 NULL count, w position of the column start */
-    uint32_t csv[2][2], zcv[2][2], pcv[2][2];
-#pragma unroll
-    for (int ki = 0; ki < 2; ki++) {
-      const uint32_t R = ki ? R1 : R0, ND = ki ? ND1 : ND0;
-      const uint32_t b0 = __builtin_popcount((ki ? nc10 : nc00) & below), b1 = __builtin_popcount((ki ? nc11 : nc01) & below);
-      const uint32_t wr = __umul24(wcol, R);
-      csv[ki][0] = wr - b0;
-      csv[ki][1] = 32 * R - ND + 2 * wr - b0 - b1;
-      zcv[ki][0] = lane32 < ND ? 1u : 0u;
-      zcv[ki][1] = zcv[ki][0] + (lane32 + 1 < ND ? 1u : 0u);
-      pcv[ki][0] = wr;
-      pcv[ki][1] = 32 * R + 2 * wr;
-    }
-    /* a wave takes tiles rb = 2 rbp and 2 rbp + 1 of one (block, region): every block quantity is
-     * wave-uniform (scalar); pairs of block r: ceil(t0/2) v0 pairs, then ceil((nt - t0)/2) */
-    const uint32_t pv0 = (tz0 + 1) >> 1, pv1 = (tz1 + 1) >> 1;
-    const uint32_t pp0 = pv0 + ((nt0 - tz0 + 1) >> 1), pp1 = pv1 + ((nt1 - tz1 + 1) >> 1);
-    const uint32_t psplit = n0 * pp0, ptot = psplit + (C - n0) * pp1, half = lane >> 5;
-    const uint32_t pm0 = ((1u << 20) + pp0 - 1) / pp0, pm1 = ((1u << 20) + pp1 - 1) / pp1;   /* once, scalar */
-    (void)ntot; (void)nm0; (void)nm1;
-    for (uint32_t pw = wave; pw < ptot; pw += nwaves) {
-      const uint32_t P = __builtin_amdgcn_readfirstlane(pw);
-      const uint32_t ki = P >= psplit ? 1u : 0u, PP = ki ? P - psplit : P, pp = ki ? pp1 : pp0;
-      const uint32_t rr = (PP * (ki ? pm1 : pm0)) >> 20, rem = PP - rr * pp;
-      const uint32_t r = ki ? n0 + rr : rr, R = ki ? R1 : R0, ND = ki ? ND1 : ND0, tz = ki ? tz1 : tz0;
-      const uint32_t pvz = ki ? pv1 : pv0, il = rem >= pvz ? 1u : 0u;
-      const uint32_t rb = 2 * (il ? rem - pvz : rem) + half;
-      const bool tile_ok = rb < (il ? (ki ? nt1 : nt0) - tz : tz);
-      const uint32_t row = il ? 16 * rb + (lane32 >> 1) : 32 * rb + lane32, s = il ? 1 + (lane32 & 1) : 0;
-      const uint32_t *st = strm + __umul24(r * 3 + s, sw);
-      uint32_t y = 0;
-      if (row < R) {
-        y = sx32(st, (int)(32 * row) - (int)ND + (s == 2 ? 1 : 0));
-        if (s == 2 && row == R - 1) {
+        const uint32_t *bb = strm + r * 3 * sw - 1;                           /* block streams - 1 word */
+        const uint32_t *wp = bb + ((src >> 5) & 0x7fffu);
+        uint32_t y = __builtin_amdgcn_alignbit(wp[1], wp[0], src);            /* bits before 0 are NULLs */
+        if (src & OAI4G_RM_SRC_LAST) {
           y &= 0x7fffffffu;                       /* j = Kpi-1 reads y^(2)_0: NULL if ND > 0 */
-          if (ND == 0) y |= (st[0] & 1u) << 31;
+          if (ND == 0) y |= (bb[1 + 2 * sw] & 1u) << 31;
         }
-      }
-      y = transpose32(y, lane32);
-      /* lane c = lane32 now holds w bits [p0, p0 + n) of column wcol, rows from 32 rb (v0) or
-       * 16 rb (interlaced); the column's row-0 entries are NULL for c < ND (and y^(2): c + 1 < ND) */
-      const int left = il ? 2 * ((int)R - 16 * (int)rb) : (int)R - 32 * (int)rb; /* w bits left in the column */
-      uint32_t n = tile_ok ? (uint32_t)min(32, left) : 0u;
-      if (il && lane32 == 31 && ND > 0 && left <= 32 && n) n--;               /* w[3Kpi-1] is NULL */
-      const uint32_t zc = ki ? (il ? zcv[1][1] : zcv[1][0]) : (il ? zcv[0][1] : zcv[0][0]);
-      const uint32_t cs = ki ? (il ? csv[1][1] : csv[1][0]) : (il ? csv[0][1] : csv[0][0]);
-      const uint32_t p0 = (ki ? (il ? pcv[1][1] : pcv[1][0]) : (il ? pcv[0][1] : pcv[0][0])) + 32 * rb;
-      const uint32_t z = rb ? 0u : zc, ci0 = rb ? cs + 32 * rb - zc : cs;
-      const uint32_t Ncb = ki ? Ncb1 : Ncb0, Nnn = ki ? Nnn1 : Nnn0, k0c = ki ? k0c1 : k0c0;
-      const int m = p0 + n > Ncb ? (int)Ncb - (int)(p0 + z) : (int)n - (int)z;  /* limited buffer */
-      if (m > 0) {
-        y = (y >> z) & (0xffffffffu >> (32 - m));
-        const bool eh = r >= es;
-        const uint32_t E = eh ? Ehi : Elo, ro = eh ? es * Elo + (r - es) * Ehi : r * Elo;
-        /* circular read from compact index k0c */
-        uint32_t o = ci0 + Nnn - k0c;
-        o = o >= Nnn ? o - Nnn : o;
-        if (E <= Nnn && o + (uint32_t)m <= Nnn) {
-          /* one placement at most (no repetition, no wrap inside the run) */
-          if (o < E) or_bits(ebuf, ro + o, y & (0xffffffffu >> (32 - min((uint32_t)m, E - o))));
-        } else {
-          /* the run may straddle the wrap back to k0c; E > Nnn repeats the buffer */
-          const uint32_t ma = min((uint32_t)m, Nnn - o);
-          for (uint32_t part = 0; part < 2; part++) {
-            const uint32_t len = part ? (uint32_t)m - ma : ma, os = part ? 0u : o;
-            const uint32_t v = part ? (ma < 32 ? y >> ma : 0u) : (ma < 32 ? y & ((1u << ma) - 1u) : y);
-            for (uint32_t x = os; len && x < E; x += Nnn) {                     /* repetition rounds */
-              const uint32_t l = min(len, E - x);
-              or_bits(ebuf, ro + x, v & (0xffffffffu >> (32 - l)));
+        y = transpose32(y, lane32);
+        const uint32_t m = (dst >> 21) & 63u;
+        if (m) {
+          const uint32_t z = (dst >> 16) & 31u, o = dst & 0xffffu;
+          y = (y >> z) & (0xffffffffu >> (32 - m));
+          const bool eh = r >= es;
+          const uint32_t E = eh ? Ehi : Elo, ro = ro_of(r) - bit0;           /* relative to the staged words */
+          if (once && !(dst & OAI4G_RM_DST_WRAP)) {
+            if (o < E) or_bits(ebuf, ro + o, y & (0xffffffffu >> (32 - min(m, E - o))));
+          } else {
+            /* the run may straddle the wrap back to k0c; E > Nnn repeats the buffer */
+            const uint32_t Nnn = ki ? Nnn1 : Nnn0, ma = min(m, Nnn - o);
+            for (uint32_t part = 0; part < 2; part++) {
+              const uint32_t len = part ? m - ma : ma, os = part ? 0u : o;
+              const uint32_t v = part ? (ma < 32 ? y >> ma : 0u) : (ma < 32 ? y & ((1u << ma) - 1u) : y);
+              for (uint32_t x = os; len && x < E; x += Nnn) {                     /* repetition rounds */
+                const uint32_t l = min(len, E - x);
+                or_bits(ebuf, ro + x, v & (0xffffffffu >> (32 - l)));
+              }
             }
           }
         }
       }
+      __syncthreads();
+      if (DEBUG) {
+        for (uint32_t k = tid; k < G; k += nth) dbg.e[k] = (uint8_t)((ebuf[k >> 5] >> (k & 31)) & 1u);
+        return;
+      }
+      /* scrambling (dlsch_scrambling.c:51-97): c_init = rnti 2^14 + q 2^13 + subframe 2^9 + Nid_cell
+       * depends only on (subframe index, codeword), so the Gold words come from the configuration's
+       * table (L2-resident) and are XORed into the RM output on the way out.  A first half that ends
+       * inside a word leaves that word to the second. */
+      const uint32_t nst = stop_phase <= 4 ? 0u : ((h + 1 < nhalf && (eb1 & 31u)) ? nwh - 1 : nwh);
+      for (uint32_t i = tid; i < nst; i += nth) {
+        const uint32_t wi = w0 + i;
+        uint32_t v = ebuf[i] ^ gold[wi];
+        const uint32_t nb = min(32u, G - 32 * wi);
+        if (nb < 32) v &= (1u << nb) - 1u;
+        eout[wi] = v;
+      }
+      if (h + 1 < nhalf) {
+        carry = (eb1 & 31u) ? ebuf[nwh - 1] : 0u;
+        __syncthreads();
+      }
     }
-  }
-#endif
-  __syncthreads();
-  if (stop_phase <= 4) return;
-
-  if (DEBUG) {
-    for (uint32_t k = tid; k < G; k += nth) dbg.e[k] = (uint8_t)((ebuf[k >> 5] >> (k & 31)) & 1u);
-    return;
-  }
-  /* scrambling (dlsch_scrambling.c:51-97): c_init = rnti 2^14 + q 2^13 + subframe 2^9 + Nid_cell
-   * depends only on (subframe index, codeword), so the Gold words come from the configuration's
-   * table (L2-resident) and are XORed into the RM output on the way out */
-  gu32_t *gold = (gu32_t *)(c->gold_tab + (size_t)(sfi * c->n_cw + cwi) * c->ebits_words);
-  uint32_t *eout = ebits + (size_t)(sf * c->n_cw + cwi) * c->ebits_words;
-  for (uint32_t i = tid; i < Gw; i += nth) {
-    uint32_t v = ebuf[i] ^ gold[i];
-    uint32_t nb = min(32u, G - 32 * i);
-    if (nb < 32) v &= (1u << nb) - 1u;
-    eout[i] = v;
   }
 }
 
@@ -1144,6 +1002,9 @@ static size_t enc_lds_bytes(const cfg_dev_t *h)
 {
   size_t words = (size_t)h->lds_a_words + h->lds_b_words + 2 * OAI4G_MAX_CB + OAI4G_MAX_CB + 2 + 4;
   size_t bytes = words * 4 + sizeof(enc_tabs_t);
+#ifdef OAI4G_ENC_LDS_PAD
+  bytes += OAI4G_ENC_LDS_PAD;   /* DIAGNOSTIC: unused LDS, fewer resident workgroups per CU */
+#endif
   return (bytes + 15) & ~(size_t)15;
 }
 
@@ -1192,7 +1053,7 @@ hipError_t oai4g_encode_occupancy(const cfg_dev_t *h_cfg, int *blocks_per_cu, si
 hipError_t oai4g_launch_encode_debug(const cfg_dev_t *d_cfg, const cfg_dev_t *h_cfg, int cw, int sf,
                                      const uint8_t *d_payload, enc_debug_t dbg, hipStream_t s)
 {
-  size_t lds = enc_lds_bytes(h_cfg);
+  size_t lds = enc_lds_bytes(h_cfg) + 4 * ((size_t)h_cfg->lds_gold_words + 1);   /* + dbg_ebuf */
   (void)hipFuncSetAttribute((const void *)k_encode_debug, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
   hipLaunchKernelGGL(k_encode_debug, dim3(1), dim3(256), lds, s, d_cfg, (uint32_t)sf, (uint32_t)cw, d_payload, dbg);
   return hipGetLastError();

@@ -1016,14 +1016,24 @@ static int derive_cfg(oai4g_tx_config *cfg, const oai4g_tx_params_t *p, const ui
   h.lds_w_words = max_w;
   (void)max_inw;
   /* encoder LDS regions with phase-disjoint lifetimes (see oai4g_encode.hip) */
-  h.lds_a_words = max_tb_words + OAI4G_ENC_CRC_TABLE_WORDS;
-  for (int cw = 0; cw < p->n_cw; cw++)   /* region A also holds the interleaved words and plane 3 in phase 3 */
-    if (2 * h.cw[cw].ilv_off[h.cw[cw].C] > h.lds_a_words) h.lds_a_words = 2 * h.cw[cw].ilv_off[h.cw[cw].C];
+  h.lds_a_words = max_tb_words;
+  for (int cw = 0; cw < p->n_cw; cw++) {
+    const cw_dev_t &c = h.cw[cw];
+    /* region A also holds the interleaved words in phase 3 (the planes sit in the parity slots) */
+    if (c.ilv_off[c.C] > h.lds_a_words) h.lds_a_words = c.ilv_off[c.C];
+    /* and, in phase 4, the e words of one half of the blocks at a time (k_encode): blocks [0, hb)
+     * then [hb, C), each half from the word holding its first bit, + 1 word for or_bits */
+    const uint32_t hb = (c.C + 1) / 2;
+    for (int sf = 0; sf < 10; sf++) {
+      const uint32_t G = c.G[sf], eb = hb < c.C ? c.roff[sf][hb] : G;
+      const uint32_t w1 = (eb + 31) / 32 + 1, w2 = (G + 31) / 32 - eb / 32 + 1;
+      if (w1 > h.lds_a_words) h.lds_a_words = w1;
+      if (w2 > h.lds_a_words) h.lds_a_words = w2;
+    }
+  }
   h.lds_b_words = max_stream_words;
-  /* region A holds the rate-matcher output words once the interleaved words are dead; region B
-   * the Gold words once the streams are dead */
-  if (h.lds_gold_words > h.lds_b_words) h.lds_b_words = h.lds_gold_words;
-  if (h.lds_gold_words > h.lds_a_words) h.lds_a_words = h.lds_gold_words;
+  if (h.lds_b_words < OAI4G_ENC_CRC_TABLE_WORDS) h.lds_b_words = OAI4G_ENC_CRC_TABLE_WORDS;   /* the CRC tables, phases 0-1 */
+
   /* RE maps */
   if (need_remap) {
     uint32_t N = h.N;
