@@ -241,10 +241,16 @@ static __device__ __forceinline__ uint32_t crc_chunk_w(const uint32_t *base32, u
 }
 
 /* crc_chunk_w for both generator polynomials at once (two independent table chains over the same
- * word reads): ra over P_A (tab8a), rb over P_B (tab8b) */
-static __device__ __forceinline__ void crc_chunk_w2(const uint32_t *base32, uint32_t start, uint32_t nbytes,
-                                                    uint32_t per, uint32_t pos, uint32_t nl, const uint32_t *tab8a,
-                                                    const uint32_t *tab8b, uint32_t &ra, uint32_t &rb)
+ * word reads: ra over P_A, rb over P_B), in reflected form: with r = bitrev32(reg) the MSB-first step
+ * reg' = (reg << 8) ^ T8[(reg >> 24) ^ b] becomes r' = (r >> 8) ^ R[(r ^ bitrev8(b)) & 0xff],
+ * R[x] = bitrev32(T8[bitrev8(x)]).  Registers and tables are kept shifted left by 2 (r2 = r << 2,
+ * R2 = R << 2), so (r2 ^ x2) & 0x3fc is the entry's byte offset (one bitop3; bits 0-1 of r2 pick up
+ * bits that the next mask and shift drop): a byte step is bitop3, base add, ds_read, shift, xor --
+ * four fast VALU ops against five (two of them slow: lshl, lshl_add) in crc_chunk_w's form.  Bytes of a
+ * word enter in order: bitrev32 puts byte q reversed at bits 31-8q..24-8q. */
+static __device__ __forceinline__ void crc_chunk_w2r(const uint32_t *base32, uint32_t start, uint32_t nbytes,
+                                                     uint32_t per, uint32_t pos, uint32_t nl, const uint8_t *r2a,
+                                                     const uint8_t *r2b, uint32_t &ra, uint32_t &rb)
 {
   const int vstart = (int)(pos * per) - (int)(per * nl - nbytes);
   uint32_t a = 0, b = 0;
@@ -253,15 +259,16 @@ static __device__ __forceinline__ void crc_chunk_w2(const uint32_t *base32, uint
     const uint32_t ad = start + (uint32_t)(o > 0 ? o : 0), wi = ad >> 2;
     uint32_t w = __builtin_amdgcn_alignbit(base32[wi + 1], base32[wi], (ad & 3u) * 8u);
     if (o < 0) w = o <= -4 ? 0u : w << (8 * (uint32_t)(-o));   /* bytes before the block are zero */
+    const uint32_t wr = __builtin_bitreverse32(w);
+    const uint32_t x[4] = {wr >> 22, wr >> 14, wr >> 6, wr << 2};
 #pragma unroll
     for (int q = 0; q < 4; q++) {
-      const uint32_t by = (w >> (8 * q)) & 0xffu;
-      a = (a << 8) ^ tab8a[(a >> 24) ^ by];
-      b = (b << 8) ^ tab8b[(b >> 24) ^ by];
+      a = (a >> 8) ^ *(const uint32_t *)(r2a + ((a ^ x[q]) & 0x3fcu));
+      b = (b >> 8) ^ *(const uint32_t *)(r2b + ((b ^ x[q]) & 0x3fcu));
     }
   }
-  ra = a >> 8;
-  rb = b >> 8;
+  ra = __builtin_bitreverse32(a >> 2) >> 8;
+  rb = __builtin_bitreverse32(b >> 2) >> 8;
 }
 
 /* crc_wave_tree2 over aligned groups of lpb lanes (16, 32 or 64; pos = lane within the group), both
@@ -606,9 +613,15 @@ static __device__ void encode_codeword(const cfg_dev_t *__restrict__ c, uint32_t
       tbw[i] = v;
     }
     if (ct == 0) crcs[0] = 0u;                    /* phase 1's XOR accumulator (C > 1) */
-    for (uint32_t v = ct; v < 256; v += cn) {     /* the register-in-the-top-24-bits form */
-      crctab_a[v] = c->crctab[0][v] << 8;
-      crctab_b[v] = c->crctab[1][v] << 8;
+    if (C > 1) {
+      for (uint32_t v = ct; v < 256; v += cn) {   /* reflected, << 2 (crc_chunk_w2r) */
+        const uint32_t iv = __builtin_bitreverse32(v) >> 24;
+        crctab_a[v] = __builtin_bitreverse32(c->crctab[0][iv] << 8) << 2;
+        crctab_b[v] = __builtin_bitreverse32(c->crctab[1][iv] << 8) << 2;
+      }
+    } else {
+      for (uint32_t v = ct; v < 256; v += cn)     /* the register-in-the-top-24-bits form */
+        crctab_a[v] = c->crctab[0][v] << 8;
     }
     for (uint32_t i = ct; i < 128; i += cn) {
       (&tabs->next[0][0])[i] = (&c_rsc.next[0][0])[i];
@@ -632,7 +645,7 @@ static __device__ void encode_codeword(const cfg_dev_t *__restrict__ c, uint32_t
       uint32_t s0 = cw.src[r], n = cw.ncopy[r];
       if (s0 + n > Ab) n = Ab > s0 ? Ab - s0 : 0;
       uint32_t ra, rb;
-      crc_chunk_w2(tbw, s0, n, per, pos, lpb, crctab_a, crctab_b, ra, rb);
+      crc_chunk_w2r(tbw, s0, n, per, pos, lpb, (const uint8_t *)crctab_a, (const uint8_t *)crctab_b, ra, rb);
       crc_group_tree2(ra, rb, pos, lpb, cw.crc2_cb[0], cw.crc2_cb[1]);
       if (pos == 0) {
         crcs[1 + r] = rb;
@@ -648,7 +661,7 @@ static __device__ void encode_codeword(const cfg_dev_t *__restrict__ c, uint32_t
       /* the TB-CRC bytes inside the last block, folded into its CRC-24B */
       for (uint32_t r = 0; r < C; r++) {
         uint32_t s0 = cw.src[r], e0 = s0 + cw.ncopy[r], reg = crcs[1 + r];
-        for (uint32_t i = (s0 > Ab ? s0 : Ab); i < e0; i++) reg = ((reg << 8) & 0xffffffu) ^ (crctab_b[((reg >> 16) ^ tbb[i]) & 0xffu] >> 8);
+        for (uint32_t i = (s0 > Ab ? s0 : Ab); i < e0; i++) reg = ((reg << 8) & 0xffffffu) ^ c->crctab[1][((reg >> 16) ^ tbb[i]) & 0xffu];
         crcs[1 + r] = reg;
       }
     }
