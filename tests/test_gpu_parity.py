@@ -298,3 +298,12 @@ def test_generate_pilots_drop_in(gpu, N_RB, nid, n_ant, mode1):
     gpu.lte_dl_cell_spec(sym, 512, fp, 3, 1, 0)
     N = fp.ofdm_symbol_size
     assert np.array_equal(sym, ref[0][(1 * 14 + 11) * N:(1 * 14 + 12) * N])   # slot 3 = subframe 1, symbol 11
+
+
+# k_encode stages the e words per half of the code blocks (blocks [0, ceil(C/2)) then the rest,
+# a word shared by the halves carried over): every MCS at 100 PRB TM1 covers C = 1..13, odd and
+# even C, half boundaries inside and on word edges, and circular-buffer repetition (E > Nnn at
+# low MCS with C > 1); each subframe index varies G and the per-block E split
+@pytest.mark.parametrize("mcs", [0, 3, 5, 7, 9, 12, 16, 20, 24, 27])
+def test_pipeline_every_block_count(gpu, mcs):
+    _pipeline_check(gpu, "C2", 10, 0, 1, mcs=[mcs], TBS=None)
