@@ -900,10 +900,47 @@ __global__ void __launch_bounds__(256) k_ul_rm_deint(const ul_dev_t *__restrict_
   dfull[(size_t)j * d_stride + 96 - 3 * (Kpi - P.D) + i] = acc;
 }
 
+/* k_ul_rm_deint with the block's E soft inputs staged in LDS first (one coalesced pass; the
+ * deinterleaved order gathers them at stride ~R otherwise, one 128-byte line per few useful bytes):
+ * one workgroup per row j = (tb, r) */
+__global__ void __launch_bounds__(256) k_ul_rm_deint_lds(const ul_dev_t *__restrict__ c, const int16_t *__restrict__ e,
+                                                         size_t e_stride, int16_t *__restrict__ dfull, size_t d_stride)
+{
+  extern __shared__ int16_t sb[];
+  const uint32_t j = blockIdx.x, tb = j / c->C, r = j - tb * c->C;
+  const ul_pat_t &P = c->pat[c->pat_of[r]];
+  const uint32_t R = P.R, Kpi = R << 5, E = c->E[r];
+  const int16_t *soft = e + tb * e_stride + c->off[r];
+  for (uint32_t q = threadIdx.x; q < E; q += blockDim.x) sb[q] = soft[q];
+  __syncthreads();
+  int16_t *d = dfull + (size_t)j * d_stride + 96 - 3 * (Kpi - P.D);
+  for (uint32_t i = threadIdx.x; i < 3 * Kpi + 3; i += blockDim.x) {
+    if (i == 2) continue;
+    const uint32_t sft = i % 3, base = sft == 2 ? i - 5 : i, row = base / 96, cp = (base % 96) / 3;
+    if (row >= R) continue;
+    const uint32_t k = (__builtin_bitreverse32(cp) >> 27) * R + row;
+    const uint32_t p = sft == 0 ? k : Kpi + 2 * k + (sft == 2 ? 1 : 0);
+    int16_t acc = 0;
+    if (p < P.Ncb && P.dummy[p] != OAI4G_LTE_NULL) {
+      const uint32_t ci = P.cidx[p];
+      for (uint32_t q = ci >= P.k0c ? ci - P.k0c : ci + P.Nnn - P.k0c; q < E; q += P.Nnn) acc = (int16_t)(acc + sb[q]);
+    }
+    d[i] = acc;
+  }
+}
+
 hipError_t oai4g_launch_ul_rm_deint(const ul_dev_t *d_cfg, const ul_dev_t *h_cfg, int n_tb, const int16_t *d_e,
                                     size_t e_stride, int16_t *d_dfull, size_t d_stride, hipStream_t s)
 {
   if (n_tb <= 0) return hipSuccess;
+  uint32_t emax = 0;
+  for (uint32_t r = 0; r < h_cfg->C; r++) emax = h_cfg->E[r] > emax ? h_cfg->E[r] : emax;
+  if (2 * (size_t)emax <= 64 * 1024) {         /* the staged form while a block's inputs fit 64 KB of LDS */
+    const uint32_t rows = (uint32_t)n_tb * h_cfg->C;
+    hipLaunchKernelGGL(k_ul_rm_deint_lds, dim3(rows), dim3(256), 2 * (size_t)emax, s, d_cfg, d_e, e_stride, d_dfull,
+                       d_stride);
+    return hipGetLastError();
+  }
   /* (tb, r) rows in chunks within the 65535 limit of gridDim.y */
   const uint32_t rows = (uint32_t)n_tb * h_cfg->C, gx = (3 * (h_cfg->Rmax << 5) + 3 + 255) / 256;
   for (uint32_t j0 = 0; j0 < rows; j0 += 65535u) {
