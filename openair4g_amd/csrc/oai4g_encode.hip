@@ -788,7 +788,7 @@ static __device__ void encode_codeword(const cfg_dev_t *__restrict__ c, uint32_t
       for (int b = 0; b < 8; b++) {
         const uint32_t e = (ew[b >> 1] >> (16 * (b & 1))) & 0xffffu;
         const uint32_t D = b8[e & 0x7ffu];
-        acc |= (__builtin_amdgcn_alignbit(D, D, e >> 11) & 0x01010101u) << b;
+        acc |= __builtin_amdgcn_alignbit(D, D, e >> 11) & (0x01010101u << b);
       }
       uint32_t a0 = acc & 0xffu, a1 = (acc >> 8) & 0xffu, a2 = (acc >> 16) & 0xffu, a3 = acc >> 24;
       const uint32_t n = Q - 8 * j;
