@@ -313,7 +313,9 @@ typedef uint32_t u32x2_t __attribute__((ext_vector_type(2)));
 #define IDFT_SYNC() __syncthreads()
 #endif
 
-template <int NA, class Prod, class Cons>
+/* PSYNC: the producer reads LDS that the exchange aliases (k_modofdm's staged QAM addresses), so
+ * the leaf stores wait for every thread's producer */
+template <int NA, bool PSYNC, class Prod, class Cons>
 static __device__ __forceinline__ void idft2048_unit(uint32_t *lds, int t, bool active, const idft2048_tw_t &tw,
                                                      Prod prod, Cons cons, int scale)
 {
@@ -322,13 +324,19 @@ static __device__ __forceinline__ void idft2048_unit(uint32_t *lds, int t, bool 
   /* pass A: leaves */
   if (active) {
     prod(x);
+    if constexpr (PSYNC)
+#pragma unroll
+      for (int a = 0; a < NA; a++) idft16_reg(x[a], tw.l16);
+  }
+  if constexpr (PSYNC) IDFT_SYNC();
+  if (active) {
 #ifndef OAI4G_DIAG_PASSA
 #define OAI4G_DIAG_PASSA 0   /* timing diagnostic only: 1 = pass-A stores at bank-distinct (wrong) words */
 #endif
     const uint32_t wo = OAI4G_DIAG_PASSA ? (uint32_t)t : 2u * (t & 31) + ((t >> 5) & 1) + 64u * (t >> 6);
 #pragma unroll
     for (int a = 0; a < NA; a++) {
-      idft16_reg(x[a], tw.l16);
+      if constexpr (!PSYNC) idft16_reg(x[a], tw.l16);
 #pragma unroll
       for (int k = 0; k < 16; k++) lds[a * X1W + k * 144 + wo] = c2u(x[a][k]);
     }
@@ -428,12 +436,12 @@ struct idft_sel<11> {
   using tw_t = idft2048_tw_t;
   static constexpr int XW = idft2048_tw_t::X1W;
 };
-template <int LOG2N, int NA, class Prod, class Cons>
+template <int LOG2N, int NA, bool PSYNC = false, class Prod, class Cons>
 static __device__ __forceinline__ void idft_any(uint32_t *lds, int t, bool active,
                                                 const typename idft_sel<LOG2N>::tw_t &tw, Prod prod, Cons cons,
                                                 int scale)
 {
-  if constexpr (LOG2N == 11) idft2048_unit<NA>(lds, t, active, tw, prod, cons, scale);
+  if constexpr (LOG2N == 11) idft2048_unit<NA, PSYNC>(lds, t, active, tw, prod, cons, scale);
   else idft_unit<LOG2N, NA>(lds, t, active, tw, prod, cons, scale);
 }
 
@@ -690,6 +698,11 @@ static __device__ __forceinline__ uint32_t ld_u32_any(const uint8_t *p)
 #ifndef OAI4G_MODOFDM_WAVES
 #define OAI4G_MODOFDM_WAVES 3   /* measured: 3 waves/SIMD (<=168 VGPRs) beats 2 (no cap) and 4 (spills) */
 #endif
+#ifndef OAI4G_MOD_ALIAS
+/* 2048-point symbols: the staged QAM addresses share LDS with the IDFT exchange (two more barriers
+ * per item), 19.0 KB per workgroup instead of 25.0 KB */
+#define OAI4G_MOD_ALIAS 0
+#endif
 #if OAI4G_MODOFDM_WAVES > 0
 #define MODOFDM_ATTR __attribute__((amdgpu_waves_per_eu(OAI4G_MODOFDM_WAVES)))
 #else
@@ -708,13 +721,16 @@ __global__ void __launch_bounds__(128) MODOFDM_ATTR k_modofdm(const cfg_dev_t *_
   constexpr int NA = MODE == 0 ? 1 : 2;
   constexpr bool CW2 = MODE == 2 || MODE == 3;
   constexpr uint32_t IPS = MODE == 3 ? 2u : 1u;   /* items per (subframe, symbol) */
-  __shared__ uint32_t lds_data[UNITS * NA * LDSW];
+  __shared__ __attribute__((aligned(16))) uint32_t lds_data[UNITS * NA * LDSW];
 #if OAI4G_MOD_STAGE
   /* per codeword, the qtab byte address of every data RE's QAM word: entries 4q..4q+3 staged from
    * quad q's 4 Qm bits; entries SENT, SENT + 1 address the zero word that non-data REs read */
   constexpr int SW = G::SW, SENT = G::SENT, QPT = G::QPT, QROW = G::QROW;
   constexpr uint32_t QZERO = 4u * 64u;          /* byte address of qtab[0][64] = 0 */
-  __shared__ __attribute__((aligned(16))) uint16_t lds_s[UNITS][2][SW];
+  constexpr bool ALIAS = OAI4G_MOD_ALIAS && LOG2N == 11;
+  static_assert(!ALIAS || (UNITS == 1 && 2 * SW <= 2 * NA * LDSW), "staged addresses must fit the exchange");
+  __shared__ __attribute__((aligned(16))) uint16_t lds_s_own[ALIAS ? 1 : UNITS][2][SW];
+  uint16_t(*lds_s)[2][SW] = ALIAS ? (uint16_t(*)[2][SW])lds_data : lds_s_own;
   __shared__ uint32_t qtab[4][QROW];            /* row cw * 2 + pilot symbol: 64 packed IQ words + 0 */
 #else
   __shared__ uint32_t lds_e[UNITS][2][EW];
@@ -740,7 +756,8 @@ __global__ void __launch_bounds__(128) MODOFDM_ATTR k_modofdm(const cfg_dev_t *_
     }
     qtab[row][bits] = v;
   }
-  for (uint32_t i = threadIdx.x; i < UNITS * 4; i += blockDim.x) lds_s[i >> 2][(i >> 1) & 1][SENT + (i & 1)] = QZERO;
+  if (!ALIAS)
+    for (uint32_t i = threadIdx.x; i < UNITS * 4; i += blockDim.x) lds_s[i >> 2][(i >> 1) & 1][SENT + (i & 1)] = QZERO;
 #else
   for (uint32_t i = threadIdx.x; i < 256; i += blockDim.x) {
     const uint32_t cw = i >> 7, pil = (i >> 6) & 1, bits = i & 63;
@@ -847,6 +864,7 @@ __global__ void __launch_bounds__(128) MODOFDM_ATTR k_modofdm(const cfg_dev_t *_
 #if OAI4G_MOD_STAGE
     /* stage, per codeword, the QAM-table address of every data RE of this symbol: quad q's 4 Qm
      * bits from its prefetched bytes -> 4 entries (ALAMOUTI: even entries TA rows, odd TB rows) */
+    if (ALIAS && active && t < 4) lds_s[0][t >> 1][SENT + (t & 1)] = QZERO;   /* the exchange overwrote them */
     if (active && nre) {
       const uint32_t nq = (nre + 3) >> 2;
       auto stage = [&](uint32_t xw, uint32_t q, uint32_t Qm, uint32_t mask, uint32_t ra, uint32_t rb, uint16_t *dst) {
@@ -896,7 +914,12 @@ __global__ void __launch_bounds__(128) MODOFDM_ATTR k_modofdm(const cfg_dev_t *_
     /* bit position of data RE idx within the staged words: idx * Qm + (re0 * Qm - 32 wlo) */
     const uint32_t b0 = re0 * Qm0 - 32 * wlo0, b1 = re0 * Qm1 - 32 * wlo1;
 #endif
-    idft_any<LOG2N, NA>(
+#if OAI4G_MOD_STAGE
+    constexpr bool PSYNC = ALIAS;
+#else
+    constexpr bool PSYNC = false;
+#endif
+    idft_any<LOG2N, NA, PSYNC>(
         lds_data + unit * NA * LDSW, t, active, twr,
         [&](s16x2 (*x)[16]) {
           /* branch-free and staged in groups of GR REs so each LDS round trip is issued for the
@@ -1094,9 +1117,7 @@ __global__ void __launch_bounds__(128) MODOFDM_ATTR k_modofdm(const cfg_dev_t *_
           }
         },
         1);
-#if OAI4G_MOD_ENDSYNC
-    __syncthreads();
-#endif
+    if (OAI4G_MOD_ENDSYNC || PSYNC) __syncthreads();   /* PSYNC: the next item stages into the exchange */
   }
 }
 
