@@ -15,3 +15,5 @@ run OAI4G_PIPE_CHUNK=4096 OAI4G_MODOFDM_OCC=5
 run OAI4G_PIPE_CHUNK=2048 OAI4G_MODOFDM_OCC=5
 run OAI4G_PIPE_CHUNK=2048 OAI4G_MODOFDM_OCC=4
 run OAI4G_PIPE_CHUNK=1024 OAI4G_MODOFDM_OCC=4
+run OAI4G_PIPE_CHUNK=4096 OAI4G_MODOFDM_OCC=4
+run X=serial_again
