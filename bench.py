@@ -153,11 +153,14 @@ def cpu_baseline(name, seconds, subframe, full=False):
     """The CPU transmit path on the host cores over a bounded sample of the same workload, one core
     and then every core of this process's share (independent processes, as N dlsim instances would
     run).  PDSCH configurations run oracle/cpu_baseline: the reference's own crc24a,
-    sub_block_interleaving_turbo, lte_rate_matching_turbo, lte_gold_generic and idft2048 compiled
-    unmodified (oracle/_ref), the oracle's restatement for the stages whose reference TU does not
-    build here (segmentation, turbo encoder, the scrambling loop, modulation, the CP copy); its
-    first subframe is checked bit-exactly against the oracle's whole chain.  The rate is over the
-    stages' summed time, as dlsim's phy_proc_tx timer covers them (DCI / pilots excluded).
+    lte_segmentation, sub_block_interleaving_turbo, lte_rate_matching_turbo, lte_gold_generic and
+    do_OFDM_mod (-> normal_prefix_mod -> PHY_ofdm_mod -> idft2048) compiled unmodified
+    (oracle/_ref), the oracle's restatement for the stages whose reference TU does not build here
+    (turbo encoder, the scrambling loop, modulation); its first subframe is checked bit-exactly
+    against the oracle's whole chain.  The rate is over the stages' summed time, as dlsim's
+    phy_proc_tx timer covers them (DCI / pilots excluded).  `port_share` is the fraction of that
+    time spent in ported stages: the reference's SSE modulation / turbo encoder may run faster than
+    the scalar ports, so the CPU rate is a lower bound on the reference's by up to that share.
     --full-grid keeps the oracle port over subframes 0..9 with CRS + PCFICH/PDCCH."""
     import openair4g_amd as oai
     cores = host_cores()
@@ -177,9 +180,11 @@ def cpu_baseline(name, seconds, subframe, full=False):
             "kind": "reference+port" if any(k != "port" for k in kinds) else "port",
             "cpu_model": cpu_model(), "value_all_cores": allc, "cores_all": cores,
             "stage_us_per_subframe": o1[0]["stage_us"], "stage_impl": o1[0]["impl"],
+            "port_share": o1[0].get("port_share"),
             "sample": f"{n1} {name} subframes (sf {subframe}) on 1 core in {seconds:.0f} s, {nall} on {cores} cores "
                       f"(independent processes); oracle/cpu_baseline: reference TUs where they build, port "
-                      f"elsewhere (stage_impl); first subframe bit-exact vs the oracle chain"}
+                      f"elsewhere (stage_impl; port_share of the time in ported stages, which may understate the "
+                      f"reference's SSE code there); first subframe bit-exact vs the oracle chain"}
 
 
 C5_K, C5_CB = 5504, 8          # UL 100 PRB MCS 20: TBS 43816 -> C = 8 blocks of K = 5504
@@ -257,6 +262,7 @@ def bench_c5_chain(args, world, rank, dist, torch):
             n += 1
         dt = time.perf_counter() - t1
         cpu = {"value": n / dt, "unit": "subframes/s", "cores": 1, "kind": "port",
+               "caveat": "scalar C restatement of the reference's 8-lane SSE decoder (3gpplte_turbo_decoder_sse_16bit.c; its TU needs il_tb/f1f2mat from the missing lte_interleaver.h blob, so it cannot be built here): it may understate the reference CPU by up to ~8x (the SIMD width)", "port_share": 1.0,
                "sample": f"{n} transport blocks (8 x K={C5_K}) through the C oracle chain (RM-rx, deinterleave, "
                          f"decoder16), single thread, {dt:.1f} s"}
     if rank == 0:
@@ -363,6 +369,7 @@ def bench_c5(args, world, rank, dist, torch):
         allc, nall = _c5_port_rate(args.c5_bits, args.c5_mode, max(2.0, args.cpu_seconds / 2), cores) \
             if cores > 1 else (n / dt, n)
         cpu = {"value": n / C5_CB / dt, "unit": "subframes/s", "cores": 1, "kind": "port",
+               "caveat": "scalar C restatement of the reference's 8-lane SSE decoder (3gpplte_turbo_decoder_sse_16bit.c; its TU needs il_tb/f1f2mat from the missing lte_interleaver.h blob, so it cannot be built here): it may understate the reference CPU by up to ~8x (the SIMD width)", "port_share": 1.0,
                "cpu_model": cpu_model(), "value_all_cores": allc / C5_CB, "cores_all": cores,
                "sample": f"{n} code blocks (K={C5_K}, mode {args.c5_mode}) through the C oracle decoder, "
                          f"single thread, {dt:.1f} s; {nall} on {cores} cores (independent processes)"}

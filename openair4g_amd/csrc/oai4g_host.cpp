@@ -1785,6 +1785,9 @@ static int run_ofdm(const int32_t *input, size_t in_n, int32_t *output, size_t o
 }
 
 static bool log2n_ok(int l) { return l >= 6 && l <= 11; }
+/* PHY_ofdm_mod's switch (ofdm_mod.c:103-127) names idft128..idft2048; any other size falls to its
+ * default (idft512 over a 2^log2 stride, overlapping symbols), which the drop-in refuses instead */
+static bool ofdm_log2_ok(int l) { return l >= 7 && l <= 11; }
 
 extern "C" void oai4g_PHY_ofdm_mod(const int32_t *input, int32_t *output, uint8_t log2fftsize, uint8_t nb_symbols,
                                    uint16_t nb_prefix_samples, int etype)
@@ -1793,12 +1796,16 @@ extern "C" void oai4g_PHY_ofdm_mod(const int32_t *input, int32_t *output, uint8_
     set_err("PHY_ofdm_mod: only CYCLIC_PREFIX is supported");
     return;
   }
-  if (!log2n_ok(log2fftsize) || nb_symbols == 0 || nb_symbols > 28) {
+  if (!ofdm_log2_ok(log2fftsize) || nb_symbols == 0 || nb_symbols > 28) {
     set_err("PHY_ofdm_mod: unsupported size 2^%u or symbol count %u", log2fftsize, nb_symbols);
     return;
   }
   ofdm_sym_t syms[28];
   uint32_t N = 1u << log2fftsize;
+  if (nb_prefix_samples > N) { /* the CP loop (ofdm_mod.c:167-171) would read in front of the symbol */
+    set_err("PHY_ofdm_mod: prefix %u longer than the symbol", nb_prefix_samples);
+    return;
+  }
   for (int i = 0; i < nb_symbols; i++) {
     syms[i].in_off = (uint32_t)i * N;
     syms[i].out_off = (uint32_t)i * N + (uint32_t)(1 + i) * nb_prefix_samples;
@@ -1826,7 +1833,7 @@ static void slot_syms(const oai4g_frame_parms_t *fp, uint32_t in_base, uint32_t 
 extern "C" void oai4g_normal_prefix_mod(const int32_t *txdataF, int32_t *txdata, uint8_t nsymb,
                                         const oai4g_frame_parms_t *fp)
 {
-  if (!log2n_ok(fp->log2_symbol_size)) { set_err("normal_prefix_mod: unsupported FFT size"); return; }
+  if (!ofdm_log2_ok(fp->log2_symbol_size)) { set_err("normal_prefix_mod: unsupported FFT size"); return; }
   uint32_t N = fp->ofdm_symbol_size;
   int short_offset = (2 * nsymb) < fp->symbols_per_tti;
   int nslots = short_offset + 2 * nsymb / fp->symbols_per_tti;

@@ -8,15 +8,16 @@
  *
  *   stage                  runs                                   reference
  *   crc24a                 ref  crc24a                           crc_byte.c:117 (libref_coding.so)
- *   segmentation           port orc_segmentation (+ CRC24B)      lte_segmentation.c:39 (PHY/defs.h: unbuildable)
+ *   segmentation           ref  lte_segmentation (+ its crc24b)  lte_segmentation.c:39 (libref_seg.so)
  *   turbo_encoder          port orc_turbo_encode                 3gpplte_sse.c:380 (lte_interleaver.h blob missing)
  *   subblock_interleaving  ref  sub_block_interleaving_turbo     lte_rate_matching.c:51 (libref_rm.so)
  *   rate_matching          ref  lte_rate_matching_turbo          lte_rate_matching.c:464 (libref_rm.so)
  *   scrambling             ref  lte_gold_generic + the XOR loop  lte_gold.c:151 (libref_gold.so); the loop of
- *                               of dlsch_scrambling (port)       dlsch_scrambling.c:78-92 (unbuildable)
- *   modulation             port orc_modulation                   dlsch_modulation.c:1181 (unbuildable)
- *   idft                   ref  idft2048 / idft1024 / ...        lte_dfts.c:2779 (libref_dfts.so)
- *   cyclic_prefix          port the CP copy of PHY_ofdm_mod      ofdm_mod.c:139-171 (unbuildable)
+ *                               of dlsch_scrambling (port)       dlsch_scrambling.c:78-92 (asn1c headers)
+ *   modulation             port orc_modulation                   dlsch_modulation.c:1181 (asn1c headers)
+ *   ofdm_mod               ref  do_OFDM_mod x 2 slots            ofdm_mod.c:233 -> normal_prefix_mod :47 ->
+ *                               (IDFT + CP + slot layout)        PHY_ofdm_mod :85 -> idft2048 (libref_ofdm.so,
+ *                                                                libref_dfts.so)
  *
  * A stage whose reference library is absent falls back to the port and says so.  The first
  * subframe's IQ is checked bit-exactly against orc_tx_subframe (the oracle's whole chain), so the
@@ -39,9 +40,9 @@
 #include "../include/oai4g_qpp.h"
 #include "oai_oracle.h"
 
-enum { S_CRC, S_SEG, S_TURBO, S_SBI, S_RM, S_SCR, S_MOD, S_IDFT, S_CP, S_N };
+enum { S_CRC, S_SEG, S_TURBO, S_SBI, S_RM, S_SCR, S_MOD, S_OFDM, S_N };
 static const char *S_NAME[S_N] = {"crc24a", "segmentation", "turbo_encoder", "subblock_interleaving",
-                                  "rate_matching", "scrambling", "modulation", "idft", "cyclic_prefix"};
+                                  "rate_matching", "scrambling", "modulation", "ofdm_mod"};
 
 static uint32_t (*ref_crc24a)(uint8_t *, uint32_t);
 static void (*ref_crcTableInit)(void);
@@ -49,7 +50,9 @@ static uint32_t (*ref_sbi)(uint32_t, uint8_t *, uint8_t *);
 static uint32_t (*ref_rm)(uint32_t, uint32_t, uint8_t *, uint8_t *, uint8_t, uint32_t, uint8_t, uint8_t, uint8_t,
                           uint8_t, uint8_t, uint8_t, uint8_t, uint8_t);
 static uint32_t (*ref_gold)(uint32_t *, uint32_t *, uint8_t);
-static void (*ref_idft)(int16_t *, int16_t *, int);
+static int (*ref_seg)(uint8_t *, uint8_t **, unsigned, unsigned *, unsigned *, unsigned *, unsigned *, unsigned *,
+                      unsigned *);
+static void (*ref_do_ofdm)(int32_t **, int32_t **, uint32_t, uint16_t, const int32_t *);
 
 static double now(void)
 {
@@ -58,11 +61,11 @@ static double now(void)
   return t.tv_sec + 1e-9 * t.tv_nsec;
 }
 
-static void *ref_open(const char *dir, const char *name)
+static void *ref_open(const char *dir, const char *name, int mode)
 {
   char p[4096];
   snprintf(p, sizeof(p), "%s/_ref/%s", dir, name);
-  return dlopen(p, RTLD_NOW | RTLD_LOCAL);
+  return dlopen(p, mode | RTLD_LOCAL);
 }
 
 static uint64_t splitmix64(uint64_t *s)
@@ -71,12 +74,6 @@ static uint64_t splitmix64(uint64_t *s)
   z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
   z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
   return z ^ (z >> 31);
-}
-
-/* the CP copy of PHY_ofdm_mod (ofdm_mod.c:139-171) after one symbol's IDFT */
-static void cp_copy(int32_t *out, int N, int cp)
-{
-  for (int k = 1; k <= cp; k++) out[-k] = out[N - k];
 }
 
 int main(int argc, char **argv)
@@ -116,8 +113,10 @@ int main(int argc, char **argv)
   const int N = fp->ofdm_symbol_size, nsymb = fp->symbols_per_tti, spt = (int)fp->samples_per_tti;
 
   /* the reference's own code where it builds (oracle/_ref); the port otherwise */
-  void *hc = ref_open(dir, "libref_coding.so"), *hr = ref_open(dir, "libref_rm.so");
-  void *hg = ref_open(dir, "libref_gold.so"), *hd = ref_open(dir, "libref_dfts.so");
+  void *hc = ref_open(dir, "libref_coding.so", RTLD_NOW), *hr = ref_open(dir, "libref_rm.so", RTLD_NOW);
+  void *hg = ref_open(dir, "libref_gold.so", RTLD_NOW), *hs = ref_open(dir, "libref_seg.so", RTLD_NOW);
+  /* RTLD_LAZY: ofdm_mod.c's LOG_D (logRecord) sits on the PMCH branch only (oracle/ref_glue_ofdm.c) */
+  void *ho = ref_open(dir, "libref_ofdm.so", RTLD_LAZY);
   if (hc) {
     ref_crc24a = (uint32_t(*)(uint8_t *, uint32_t))dlsym(hc, "crc24a");
     ref_crcTableInit = (void (*)(void))dlsym(hc, "crcTableInit");
@@ -130,13 +129,16 @@ int main(int argc, char **argv)
                           uint8_t, uint8_t, uint8_t, uint8_t))dlsym(hr, "lte_rate_matching_turbo");
   }
   if (hg) ref_gold = (uint32_t(*)(uint32_t *, uint32_t *, uint8_t))dlsym(hg, "lte_gold_generic");
-  if (hd) {
-    char nm[32];
-    snprintf(nm, sizeof(nm), "idft%d", N);
-    ref_idft = (void (*)(int16_t *, int16_t *, int))dlsym(hd, nm);
-  }
-  const int use_ref[S_N] = {ref_crc24a != NULL, 0, 0, ref_sbi != NULL, ref_rm != NULL, ref_gold != NULL, 0,
-                            ref_idft != NULL, 0};
+  /* lte_segmentation's crc24b is libref_coding.so's (the same loaded object: DT_NEEDED via $ORIGIN),
+   * whose table crcTableInit filled above */
+  if (hs && ref_crc24a)
+    ref_seg = (int (*)(uint8_t *, uint8_t **, unsigned, unsigned *, unsigned *, unsigned *, unsigned *, unsigned *,
+                       unsigned *))dlsym(hs, "lte_segmentation");
+  if (ho) ref_do_ofdm = (void (*)(int32_t **, int32_t **, uint32_t, uint16_t, const int32_t *))dlsym(ho, "ref_glue_do_OFDM_mod");
+  const int use_ref[S_N] = {ref_crc24a != NULL, ref_seg != NULL, 0, ref_sbi != NULL, ref_rm != NULL, ref_gold != NULL,
+                            0, ref_do_ofdm != NULL};
+  const int32_t geom[9] = {fp->N_RB_DL, fp->Ncp, fp->nb_antennas_tx, N, fp->log2_symbol_size, fp->nb_prefix_samples,
+                           fp->nb_prefix_samples0, nsymb, spt};
 
   int G[2] = {0, 0};
   uint8_t Qm[2];
@@ -146,26 +148,31 @@ int main(int argc, char **argv)
                        : orc_get_G(fp->N_RB_DL, fp->Ncp, fp->mode1_flag, fp->frame_type, cfg.nb_rb, cfg.rb_alloc, Qm[cw],
                                    1, cfg.num_pdcch_symbols, cfg.subframe);
   }
-  /* buffers: 16-byte aligned as the reference's malloc16 gives them */
+  /* buffers: 16-byte aligned as the reference's malloc16 gives them, sized from the TBS (+ CRC) */
+  for (int cw = 0; cw < cfg.n_cw; cw++)
+    if (cfg.TBS[cw] == 0 || cfg.TBS[cw] > 16 * 6120 - 24) {
+      fprintf(stderr, "cpu_baseline: TBS %u outside 1..%d (16 code blocks)\n", cfg.TBS[cw], 16 * 6120 - 24);
+      return 2;
+    }
+  const size_t abytes = (((cfg.TBS[0] > cfg.TBS[1] ? cfg.TBS[0] : cfg.TBS[1]) / 8 + 3 + 63) / 64 + 1) * 64;
   uint8_t *pay[2], *a[2], *e[2];
   for (int cw = 0; cw < 2; cw++) {
-    pay[cw] = aligned_alloc(64, 6200);
-    a[cw] = aligned_alloc(64, 6200);
+    pay[cw] = aligned_alloc(64, abytes);
+    a[cw] = aligned_alloc(64, abytes);
     e[cw] = aligned_alloc(64, (size_t)((1 + (G[cw] >> 5)) * 32 + 128));
-    for (int i = 0; i < 6200; i++) pay[cw][i] = (uint8_t)splitmix64(&seed);
+    for (size_t i = 0; i < abytes; i++) pay[cw][i] = (uint8_t)splitmix64(&seed);
   }
   static uint8_t cbuf[16][8 + 3 + 768];
   uint8_t *dbuf = aligned_alloc(64, 96 + 12 + 3 + 3 * 6144 + 128), *wbuf = aligned_alloc(64, 3 * 6176 + 128);
   int32_t *txF[4], *txd[4], *chk[4], *chkF[4];
   for (int aa = 0; aa < n_ant; aa++) {
     txF[aa] = aligned_alloc(64, (size_t)10 * nsymb * N * 4);
-    txd[aa] = aligned_alloc(64, (size_t)spt * 4 + 64);
+    txd[aa] = aligned_alloc(64, (size_t)10 * spt * 4 + 64);      /* the frame, as do_OFDM_mod indexes it */
     chk[aa] = aligned_alloc(64, (size_t)spt * 4 + 64);
     chkF[aa] = aligned_alloc(64, (size_t)nsymb * N * 4);
     memset(txF[aa], 0, (size_t)10 * nsymb * N * 4);
   }
 
-  int32_t *tmp128 = aligned_alloc(64, 128 * 4 * 4);
   double st[S_N];
   memset(st, 0, sizeof(st));
   long done = 0;
@@ -184,7 +191,9 @@ int main(int argc, char **argv)
       uint32_t C, Cp, Cm, Kp, Km, F;
       uint8_t *cptr[16];
       for (int r = 0; r < 16; r++) cptr[r] = cbuf[r];
-      if (orc_segmentation(a[cw], cptr, A + 24, &C, &Cp, &Cm, &Kp, &Km, &F) < 0) return 3;
+      if ((use_ref[S_SEG] ? ref_seg(a[cw], cptr, A + 24, &C, &Cp, &Cm, &Kp, &Km, &F)
+                          : orc_segmentation(a[cw], cptr, A + 24, &C, &Cp, &Cm, &Kp, &Km, &F)) < 0)
+        return 3;
       t1 = now(); st[S_SEG] += t1 - t0;
       uint32_t r_off = 0;
       for (uint32_t r = 0; r < C; r++) {
@@ -224,34 +233,20 @@ int main(int argc, char **argv)
                        cfg.sqrt_rho_a, cfg.sqrt_rho_b) < 0)
       return 3;
     t1 = now(); st[S_MOD] += t1 - t0;
-    /* do_OFDM_mod_l x 2 slots -> normal_prefix_mod -> PHY_ofdm_mod (ofdm_mod.c:47-229), normal CP */
-    for (int aa = 0; aa < n_ant; aa++) {
-      const int32_t *in = txF[aa] + (size_t)cfg.subframe * nsymb * N;
-      for (int slot = 0; slot < 2; slot++)
-        for (int l = 0; l < 7; l++) {
-          const int cp = l == 0 ? fp->nb_prefix_samples0 : fp->nb_prefix_samples;
-          const int off = slot * (spt >> 1) + l * N + fp->nb_prefix_samples0 + (l > 0 ? l * fp->nb_prefix_samples : 0);
-          int32_t *out = txd[aa] + off;
-          t0 = now();
-          if (use_ref[S_IDFT] && N == 128) {        /* PHY_ofdm_mod's static temp (ofdm_mod.c:94, 142-156) */
-            ref_idft((int16_t *)(in + (slot * 7 + l) * N), (int16_t *)tmp128, 1);
-            memcpy(out, tmp128, 128 * 4);
-          } else if (use_ref[S_IDFT])
-            ref_idft((int16_t *)(in + (slot * 7 + l) * N), (int16_t *)out, 1);
-          else
-            orc_idft(fp->log2_symbol_size, (const int16_t *)(in + (slot * 7 + l) * N), (int16_t *)out, 1);
-          t1 = now(); st[S_IDFT] += t1 - t0; t0 = t1;
-          cp_copy(out, N, cp);
-          t1 = now(); st[S_CP] += t1 - t0;
-        }
+    /* do_OFDM_mod_l x 2 slots (dlsim.c:2680-2699) -> normal_prefix_mod -> PHY_ofdm_mod, normal CP */
+    t0 = now();
+    for (int slot = 2 * cfg.subframe; slot < 2 * cfg.subframe + 2; slot++) {
+      if (use_ref[S_OFDM]) ref_do_ofdm(txF, txd, 0, (uint16_t)slot, geom);
+      else orc_do_OFDM_mod(txF, txd, 0, (uint16_t)slot, fp);
     }
+    t1 = now(); st[S_OFDM] += t1 - t0;
     if (done == 0) {
       /* the composition against the oracle's whole chain, bit for bit */
       uint8_t *pp[2] = {a[0], a[1]};
       for (int cw = 0; cw < cfg.n_cw; cw++) memcpy(a[cw], pay[cw], cfg.TBS[cw] / 8);
       if (orc_tx_subframe(&cfg, pp, chkF, chk, NULL) != 0) return 4;
       for (int aa = 0; aa < n_ant; aa++)
-        if (memcmp(chk[aa], txd[aa], (size_t)spt * 4) != 0) {
+        if (memcmp(chk[aa], txd[aa] + (size_t)cfg.subframe * spt, (size_t)spt * 4) != 0) {
           fprintf(stderr, "cpu_baseline: composed IQ differs from orc_tx_subframe (antenna %d)\n", aa);
           return 5;
         }
@@ -259,10 +254,14 @@ int main(int argc, char **argv)
     done++;
     if (now() - t_start >= seconds) break;
   }
-  double tot = 0;
-  for (int k = 0; k < S_N; k++) tot += st[k];
-  printf("{\"subframes\": %ld, \"wall_s\": %.6f, \"stage_s\": %.6f, \"rate\": %.3f, \"validated\": true, \"stage_us\": {",
-         done, now() - t_start, tot, done / tot);
+  double tot = 0, port = 0;
+  for (int k = 0; k < S_N; k++) {
+    tot += st[k];
+    if (!use_ref[k] || k == S_SCR) port += st[k];      /* the scrambling loop around the ref generator is a port */
+  }
+  printf("{\"subframes\": %ld, \"wall_s\": %.6f, \"stage_s\": %.6f, \"rate\": %.3f, \"validated\": true, "
+         "\"port_share\": %.4f, \"stage_us\": {",
+         done, now() - t_start, tot, done / tot, port / tot);
   for (int k = 0; k < S_N; k++) printf("%s\"%s\": %.3f", k ? ", " : "", S_NAME[k], 1e6 * st[k] / done);
   printf("}, \"impl\": {");
   for (int k = 0; k < S_N; k++)

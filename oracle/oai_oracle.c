@@ -932,6 +932,23 @@ void orc_normal_prefix_mod(const int32_t *txdataF, int32_t *txdata, uint8_t nsym
   }
 }
 
+/* do_OFDM_mod (ofdm_mod.c:233-284): slot next_slot of every antenna's whole-frame grid.  The
+ * frame parameters here carry no MBSFN configuration, so is_pmch_subframe (pmch.c:97-190) is 0
+ * for every subframe and only the non-PMCH branch (:267-281) is reachable. */
+void orc_do_OFDM_mod(int32_t **txdataF, int32_t **txdata, uint32_t frame, uint16_t next_slot, const orc_frame_t *fp)
+{
+  (void)frame;
+  const uint32_t slot_offset_F = (uint32_t)next_slot * fp->ofdm_symbol_size * (fp->Ncp == 1 ? 6 : 7);
+  const uint32_t slot_offset = (uint32_t)next_slot * (fp->samples_per_tti >> 1);
+  for (int aa = 0; aa < fp->nb_antennas_tx; aa++) {
+    if (fp->Ncp == 1)
+      orc_ofdm_mod(&txdataF[aa][slot_offset_F], &txdata[aa][slot_offset], fp->log2_symbol_size, 6,
+                   fp->nb_prefix_samples);
+    else
+      orc_normal_prefix_mod(&txdataF[aa][slot_offset_F], &txdata[aa][slot_offset], 7, fp);
+  }
+}
+
 /* ======================================================================================
  * Whole subframe — dlsim.c:2567-2699 (dlsch_encoding dlsch_coding.c:254-419,
  * dlsch_scrambling, dlsch_modulation, do_OFDM_mod_l x2 slots).  DCI and pilots excluded.

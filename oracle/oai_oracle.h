@@ -117,6 +117,7 @@ int orc_slot_fep(int32_t **rxdata, int32_t **rxdataF, const orc_frame_t *fp, int
 void orc_ofdm_mod(const int32_t *input, int32_t *output, uint8_t log2fftsize, uint8_t nb_symbols,
                   uint16_t nb_prefix_samples);
 void orc_normal_prefix_mod(const int32_t *txdataF, int32_t *txdata, uint8_t nsymb, const orc_frame_t *fp);
+void orc_do_OFDM_mod(int32_t **txdataF, int32_t **txdata, uint32_t frame, uint16_t next_slot, const orc_frame_t *fp);
 
 /* ---- cell-specific reference signals (LTE_REFSIG/lte_gold.c:52-93, lte_dl_cell_spec.c:123-203,
  *      LTE_TRANSPORT/pilots.c:43-168) ---- */

@@ -848,3 +848,73 @@ def ref_gold_table(Ncp, Nid_cell):
     t = np.zeros((20, 2, 14), np.uint32)
     ref_gold().ref_glue_lte_gold(Ncp, Nid_cell, P(t))
     return t
+
+
+# ---- the reference's own segmentation and OFDM modulator (oracle/_ref/libref_seg.so: PHY/CODING/
+#      lte_segmentation.c, oracle/_ref/libref_ofdm.so: PHY/MODULATION/ofdm_mod.c, both compiled
+#      unmodified; present only in the build container) ----
+REF_SEG_SO = os.path.join(ORACLE_DIR, "_ref", "libref_seg.so")
+REF_OFDM_SO = os.path.join(ORACLE_DIR, "_ref", "libref_ofdm.so")
+_refseg = None
+_refofdm = None
+
+
+def ref_seg():
+    """lte_segmentation.c compiled unmodified (its crc24b from libref_coding.so, whose table
+    ref_coding() initialises), or None when it was not built here."""
+    global _refseg
+    if _refseg is None:
+        if not os.path.exists(REF_SEG_SO) or ref_coding() is None:
+            return None
+        L = ctypes.CDLL(REF_SEG_SO)
+        L.lte_segmentation.restype = ctypes.c_int
+        L.lte_segmentation.argtypes = [VP, ctypes.POINTER(VP), U32] + [ctypes.POINTER(U32)] * 6
+        _refseg = L
+    return _refseg
+
+
+def ref_ofdm():
+    """ofdm_mod.c compiled unmodified (+ the ctypes glue ref_glue_ofdm.c), or None."""
+    global _refofdm
+    if _refofdm is None:
+        if not os.path.exists(REF_OFDM_SO):
+            return None
+        # RTLD_LAZY: logRecord (LOG_D on the PMCH branch, ofdm_mod.c:244/260) stays unbound; no
+        # case here reaches that branch (ref_glue_ofdm.c)
+        L = ctypes.CDLL(REF_OFDM_SO, mode=os.RTLD_LAZY | os.RTLD_LOCAL)
+        L.PHY_ofdm_mod.restype = None
+        L.PHY_ofdm_mod.argtypes = [VP, VP, ctypes.c_ubyte, ctypes.c_ubyte, ctypes.c_ushort, ctypes.c_int]
+        L.ref_glue_normal_prefix_mod.argtypes = [VP, VP, U8, VP]
+        L.ref_glue_do_OFDM_mod.argtypes = [ctypes.POINTER(VP), ctypes.POINTER(VP), U32, U16, VP]
+        _refofdm = L
+    return _refofdm
+
+
+def seg_out_buffers(C, fill=0xA5, size=768 + 8 + 3):
+    """output_buffers for lte_segmentation: C (>= 1) byte buffers pre-filled with `fill`, so bytes the
+    function does not write stay visible."""
+    bufs = [_aligned(size, np.uint8) for _ in range(max(C, 1))]
+    for b in bufs:
+        b[:] = fill
+    return bufs
+
+
+def ref_segmentation(B, data=None, C_hint=16):
+    """lte_segmentation(input, outputs, B, ...): (ret, (C, Cplus, Cminus, Kplus, Kminus, F), buffers).
+    Without `data` both pointers are NULL (the parameter-only call of dlsch_coding.c)."""
+    vals = [U32(0) for _ in range(6)]
+    if data is None:
+        ret = ref_seg().lte_segmentation(None, None, B, *[ctypes.byref(v) for v in vals])
+        return ret, tuple(v.value for v in vals), None
+    inp = _aligned(len(data) + 16, np.uint8)
+    inp[:len(data)] = data
+    bufs = seg_out_buffers(C_hint)
+    ptrs = (VP * len(bufs))(*[b.ctypes.data for b in bufs])
+    ret = ref_seg().lte_segmentation(P(inp), ptrs, B, *[ctypes.byref(v) for v in vals])
+    return ret, tuple(v.value for v in vals), bufs
+
+
+def frame_geometry(fp):
+    """The ofdm_mod.c glue's geometry vector from an OrcFrame / FrameParms."""
+    return np.array([fp.N_RB_DL, fp.Ncp, fp.nb_antennas_tx, fp.ofdm_symbol_size, fp.log2_symbol_size,
+                     fp.nb_prefix_samples, fp.nb_prefix_samples0, fp.symbols_per_tti, fp.samples_per_tti], np.int32)

@@ -53,4 +53,6 @@ def test_cpu_baseline_fields():
     # with the reference tree built here, the stages that have a buildable TU run the reference
     if os.path.exists(os.path.join(ROOT, "oracle", "_ref", "libref_rm.so")):
         assert cb["kind"] == "reference+port"
-        assert cb["stage_impl"]["rate_matching"] == "reference" and cb["stage_impl"]["idft"] == "reference"
+        assert cb["stage_impl"]["rate_matching"] == "reference" and cb["stage_impl"]["ofdm_mod"] == "reference"
+        assert cb["stage_impl"]["segmentation"] == "reference"
+        assert 0 < cb["port_share"] < 1
