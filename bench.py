@@ -788,6 +788,14 @@ class Host:
         self.dist.all_reduce(t, op=self.dist.ReduceOp.SUM)
         return float(t.item())
 
+    def gather_over_ranks(self, v):
+        """Every rank's value, in rank order (an all-gather of one float per rank)."""
+        if self.dist is None:
+            return [v]
+        ts = [self.torch.zeros(1, dtype=self.torch.float64, device=self.device) for _ in range(self.world)]
+        self.dist.all_gather(ts, self.torch.tensor([v], dtype=self.torch.float64, device=self.device))
+        return [float(t.item()) for t in ts]
+
     def close(self):
         if not self.stub and self.world > 1:
             import openair4g_amd as oai
@@ -971,6 +979,7 @@ def bench_tx(args, world, rank, host):
         a, b = pipe.run_timed()
         kern[0].append(a)
         kern[1].append(b)
+    rank_elapsed = host.gather_over_ranks(elapsed)           # per-rank wall time (readable SCALE lines)
     elapsed = host.max_over_ranks(elapsed)
     units = host.sum_over_ranks(args.batch * args.steps)      # subframes all ranks processed
 
@@ -1043,6 +1052,10 @@ def bench_tx(args, world, rank, host):
                          "kernel_boundary_frac": {k: v["bytes"] / (v["ms"] * 1e-3) / 1e9 / HBM_PEAK_GBS
                                                   for k, v in per_kernel.items()}},
             "end_to_end_algorithmic_GBps": value * (payload_b + iq_b) / 1e9,
+            "per_rank_subframes_per_s": [args.batch * args.steps / e for e in rank_elapsed],
+            # value over the sum of the ranks' own rates: 1.0 when every shard takes the same time (the
+            # job waits for the slowest); the driver computes scaling efficiency across N itself
+            "rank_efficiency": value / sum(args.batch * args.steps / e for e in rank_elapsed),
             "cpu_baseline": cpu,
         }
         print(json.dumps(out), flush=True)

@@ -107,7 +107,9 @@ typedef struct {
   oai4g_dl_harq_t *harq_processes[8];
 } oai4g_dlsch_t;
 
-/* ---------------- library / device ---------------- */
+/* ---------------- library / device ----------------
+ * The library runs on one device (oai4g_set_device before oai4g_init, else the current one).  Every
+ * compute call makes that device the calling thread's current HIP device and leaves it so. */
 int oai4g_init(void);                       /* idempotent; 0 on success, <0 if no usable GPU */
 const char *oai4g_last_error(void);
 int oai4g_device_name(char *buf, int len);
@@ -540,8 +542,12 @@ int oai4g_ul_decode_batch(oai4g_ul_config_t *cfg, int n_tb, const int16_t *d_e, 
 /* The same chain with HARQ soft combining across rounds, as dlsch_decoding / ulsch_decoding run it
  * (dlsch_decoding.c:348-383: lte_rate_matching_turbo_rx with clear = (round == 0), the round's
  * rvidx; dlsim's round loop, dlsim.c:2141): d_w [n_tb][C][w_stride] int16 device soft buffers, the
- * reference's harq->w[r], updated in place (w_stride >= oai4g_ul_config_w_entries(cfg); zero them
- * once before round 0 so entries past Ncb read 0).  rvidx 0..3 overrides the configuration's. */
+ * reference's harq->w[r], updated in place (w_stride >= oai4g_ul_config_w_entries(cfg)).  clear = 1
+ * writes every entry below Ncb (NULL positions 0, as the reference's memset); entries at or past
+ * Ncb are never read, so no initialisation of d_w is needed.  rvidx 0..3 overrides the
+ * configuration's.  The configuration's soft-buffer split is Kmimo = 1 (the uplink; dlsch_decoding
+ * with one codeword per TB, TM1 / TM2): a DL TM3 transport block (Kmimo = 2) has another Ncb and k0
+ * and is outside this API. */
 size_t oai4g_ul_config_w_entries(const oai4g_ul_config_t *cfg);
 int oai4g_ul_decode_batch_harq(oai4g_ul_config_t *cfg, int n_tb, const int16_t *d_e, size_t e_stride, int16_t *d_w,
                                size_t w_stride, uint8_t rvidx, uint8_t clear, uint8_t *d_c, size_t c_stride,

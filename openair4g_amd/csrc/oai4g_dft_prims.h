@@ -20,12 +20,32 @@ static __device__ __forceinline__ s16x2 csubs(s16x2 a, s16x2 b) { return __built
 static __device__ __forceinline__ s16x2 caddw(s16x2 a, s16x2 b) { return a + b; }
 /* sign_epi16(x,{-1,1}) + pair swap: -j*x with a wrapping negate (lte_dfts.c:1463-1466) */
 static __device__ __forceinline__ s16x2 cflip(s16x2 a) { return (s16x2){a.y, (short)(-(int)a.x)}; }
+/* The same as one v_pk_mul_lo_u16 with swapped operand halves (lo = a.hi * 1, hi = a.lo * 0xFFFF)
+ * instead of the compiler's v_sub_u16 + v_alignbit pair.  Used where it measured a gain (the
+ * two-antenna 2048-point kernels); elsewhere the opaque asm raised register pressure. */
+static __device__ __forceinline__ s16x2 cflip_f(s16x2 a)
+{
+  if (__builtin_constant_p(__builtin_bit_cast(uint32_t, a)))
+    return (s16x2){a.y, (short)(-(int)a.x)};
+  uint32_t r;
+  asm("v_pk_mul_lo_u16 %0, %1, %2 op_sel:[1,0] op_sel_hi:[0,1]" : "=v"(r) : "v"(a), "s"(0xFFFF0001u));
+  return __builtin_bit_cast(s16x2, r);
+}
 /* v_dot2_i32_i16 with an inline-zero accumulator (the compiler otherwise picks the tied
  * v_dot2c form and zeroes its accumulator with an extra v_mov per product) */
 static __device__ __forceinline__ int dot2(s16x2 a, s16x2 b)
 {
   int r;
   asm("v_dot2_i32_i16 %0, %1, %2, 0" : "=v"(r) : "v"(a), "v"(b));
+  return r;
+}
+/* the same with a wave-uniform second operand (twiddles from scalar loads, constants): the "s"
+ * constraint keeps it in an SGPR (VOP3P reads one through the constant bus) instead of a VGPR copy.
+ * Only for values that are uniform by construction. */
+static __device__ __forceinline__ int dot2s(s16x2 a, s16x2 b)
+{
+  int r;
+  asm("v_dot2_i32_i16 %0, %1, %2, 0" : "=v"(r) : "v"(a), "s"(b));
   return r;
 }
 static __device__ __forceinline__ int wadd(int a, int b) { return (int)((unsigned)a + (unsigned)b); }
@@ -53,15 +73,21 @@ static __device__ __forceinline__ s16x2 cmulc16(s16x2 x, const twp_t &w)
   cmulc32(x, w, re, im);
   return cpack32(re, im);
 }
+/* x * conj(w) with a wave-uniform twiddle pair (SGPR operands) */
+static __device__ __forceinline__ s16x2 cmulc16u(s16x2 x, const twp_t &w)
+{
+  return cpack32(dot2s(x, w.t), dot2s(x, w.tn));
+}
 
 /* saturating inverse radix-4 (idft16 stages; ibfly4_16 lte_dfts.c:1049-1090) */
+template <bool FF = false>
 static __device__ __forceinline__ void r4inv(s16x2 p0, s16x2 p1, s16x2 p2, s16x2 p3, s16x2 &o0, s16x2 &o1,
                                              s16x2 &o2, s16x2 &o3)
 {
   s16x2 s02 = cadds(p0, p2), s13 = cadds(p1, p3);
   o0 = cadds(s02, s13);
   o2 = csubs(s02, s13);
-  s16x2 d02 = csubs(p0, p2), d13 = csubs(cflip(p1), cflip(p3));
+  s16x2 d02 = csubs(p0, p2), d13 = FF ? csubs(cflip_f(p1), cflip_f(p3)) : csubs(cflip(p1), cflip(p3));
   o3 = cadds(d02, d13);
   o1 = csubs(d02, d13);
 }
@@ -84,7 +110,7 @@ static __device__ __forceinline__ void ibfly4(s16x2 x0, s16x2 x1, s16x2 x2, s16x
 /* ibfly2 (lte_dfts.c:502-527): x0 * 32767 via the same madd as the twiddled operand */
 static __device__ __forceinline__ void ibfly2(s16x2 x0, s16x2 x1, const twp_t &t, s16x2 &y0, s16x2 &y1)
 {
-  int a0r = dot2(x0, (s16x2){32767, 0}), a0i = dot2(x0, (s16x2){0, 32767}), a1r, a1i;
+  int a0r = dot2s(x0, (s16x2){32767, 0}), a0i = dot2s(x0, (s16x2){0, 32767}), a1r, a1i;
   cmulc32(x1, t, a1r, a1i);
   y0 = cpack32(wadd(a0r, a1r), wadd(a0i, a1i));
   y1 = cpack32(wsub(a0r, a1r), wsub(a0i, a1i));
@@ -95,8 +121,23 @@ static __device__ __forceinline__ s16x2 shr1(s16x2 a) { return (s16x2){(short)(a
 /* mulhi_int16(a, 23170) = slli(mulhi_epi16(a, 23170), 1) (lte_dfts.c:1755); |result| <= 23170 */
 static __device__ __forceinline__ s16x2 mulhi2(s16x2 a)
 {
-  int pr = dot2(a, (s16x2){23170, 0}), pi = dot2(a, (s16x2){0, 23170});
+  int pr = dot2s(a, (s16x2){23170, 0}), pi = dot2s(a, (s16x2){0, 23170});
   return (s16x2){(short)((pr >> 16) << 1), (short)((pi >> 16) << 1)};
+}
+/* The same with the packing as four fast-rate ops: lane = ((p >> 16) << 1) mod 2^16 = bits 16..30
+ * of p moved up by one, so low lane (pr >> 15) & 0xFFFE, high lane (pi << 1) & 0xFFFE0000 (pi + pi
+ * for << 1; the mask also clears bit 16, which holds bit 15 of pi), merged by one v_bitop3 mux
+ * "c ? a : b" (0xe4, c = 0x0000FFFE).  The compiler's own form (v_perm, or v_lshlrev + v_and_or)
+ * issues at the slow rate.  Used in the two-antenna 2048-point kernels; in the TM1 kernel the
+ * opaque asm raised register pressure past 4 waves. */
+static __device__ __forceinline__ s16x2 mulhi2_f(s16x2 a)
+{
+  const uint32_t pr = (uint32_t)dot2s(a, (s16x2){23170, 0}), pi = (uint32_t)dot2s(a, (s16x2){0, 23170});
+  const uint32_t lo = pr >> 15;
+  uint32_t hi, r;
+  asm("v_add_u32_e32 %0, %1, %1\n\tv_and_b32_e32 %0, 0xfffe0000, %0" : "=&v"(hi) : "v"(pi));
+  asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0xe4" : "=v"(r) : "v"(lo), "v"(hi), "s"(0x0000FFFEu));
+  return u2c(r);
 }
 
 static __device__ __forceinline__ uint32_t lphys(uint32_t pos) { return pos + (pos >> 5); }

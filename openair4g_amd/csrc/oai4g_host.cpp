@@ -239,20 +239,19 @@ extern "C" int oai4g_set_device(int device)
   return 0;
 }
 
-/* hipSetDevice is per thread: a thread that calls in after another initialised the library binds
- * itself to the library's device before it creates streams, buffers or launches (the device tables
- * live there).  Called by NEED_INIT. */
-static thread_local bool t_bound = false;
+/* hipSetDevice is per thread: every library call binds the calling thread to the library's device
+ * before it creates streams, buffers or launches (the device tables live there).  Checked on every
+ * call, not cached: the application may switch the thread's device in between (hipSetDevice,
+ * torch.cuda.set_device).  The binding stays in effect after the call (include/oai4g.h).  Called by
+ * NEED_INIT. */
 static int bind_thread_device(void)
 {
-  if (t_bound) return 0;
   int cur = -1;
   if (hipGetDevice(&cur) != hipSuccess) return -1;
   if (cur != g_device && hipSetDevice(g_device) != hipSuccess) {
     set_err("thread bind: hipSetDevice(%d) failed", g_device);
     return -1;
   }
-  t_bound = true;
   return 0;
 }
 int oai4g_bind_thread(void) { return bind_thread_device(); }
@@ -1115,8 +1114,10 @@ static int upload_remap(oai4g_tx_config *cfg)
       for (int l = 0; l < 14; l++)
         if (cfg->h.symnre[sf][l] + 3u > (3u * N) / 4u) { set_err("too many data REs per symbol for the modulator"); return -1; }
 #endif
-    std::vector<uint16_t> both(2 * n);
+    /* natural, thread-major, thread-major with the non-data codes on the zero sentinel */
+    std::vector<uint16_t> both(3 * n);
     std::copy(cfg->h_remap.begin(), cfg->h_remap.end(), both.begin());
+    const uint16_t sentinel = (uint16_t)(2u * ((3u * (uint32_t)N) / 4u));   /* modofdm_geom::SENT, bytes */
     for (size_t sl = 0; sl < n / N; sl++)
       for (size_t t = 0; t < T; t++)
         for (size_t k = 0; k < 16; k++) {
@@ -1126,12 +1127,15 @@ static int upload_remap(oai4g_tx_config *cfg)
           if (code < OAI4G_CTL_CODE) code = (uint16_t)((code & 0x8000u) | ((code & 0x3FFFu) << 1));
 #endif
           both[n + sl * N + t * 16 + k] = code;
+          both[2 * n + sl * N + t * 16 + k] = code < OAI4G_CTL_CODE ? code : sentinel;
         }
     HCK(hipMalloc(&cfg->d_remap, both.size() * 2), -1);
     HCK(hipMemcpy(cfg->d_remap, both.data(), both.size() * 2, hipMemcpyHostToDevice), -1);
     cfg->h.remap_tm = cfg->d_remap + n;
+    cfg->h.remap_tm0 = cfg->d_remap + 2 * n;
   } else {
     cfg->h.remap_tm = nullptr;
+    cfg->h.remap_tm0 = nullptr;
   }
   cfg->h.remap = cfg->d_remap;
   return 0;

@@ -156,6 +156,9 @@ struct cfg_dev_t {
                                    symbol<<9 | port<<8 | m for a CRS RE; 0xFFFF = none */
   const uint16_t *remap_tm;     /* the same codes thread-major: per (sf, l), [t][n] = remap[t + (N/16) n],
                                    so each modofdm thread fetches its 16 codes with two 16-B loads */
+  const uint16_t *remap_tm0;    /* remap_tm with every non-data code replaced by the staged zero
+                                   sentinel's byte offset (2 * 3N/4): the kernels without CRS or control
+                                   REs then address the sentinel without a clamp */
   uint32_t with_crs;
   uint32_t pilmask;             /* bit l: symbol l carries CRS (QAM levels scaled by rho_B) */
   const uint32_t *crs_tab;      /* [10][6][200] packed CRS IQ of pilot symbol i (l = 0, 4, 7, 11; 1, 8 for

@@ -83,20 +83,31 @@ struct idft_tw_t {
 };
 
 static __device__ __forceinline__ twp_t tw_of(s16x2 t) { return {t, (s16x2){(short)(-(int)t.y), t.x}}; }
+/* The same pair with the companion rebuilt by one v_pk_mul_lo_u16 (lo = t.hi * -1, hi = t.lo * 1,
+ * wrapping like (short)-t.y).  `dep` is any per-item value: it is an operand of the asm, so the
+ * companion cannot be hoisted out of a persistent item loop, where the compiler would otherwise
+ * keep a second register per twiddle for the whole kernel (29 VGPRs at 2048 points). */
+static __device__ __forceinline__ twp_t tw_use(s16x2 t, uint32_t dep)
+{
+  uint32_t tn;
+  asm("v_pk_mul_lo_u16 %0, %1, %2 op_sel:[1,0] op_sel_hi:[0,1] ; %3" : "=v"(tn) : "v"(t), "s"(0x0001FFFFu), "s"(dep));
+  return {t, u2c(tn)};
+}
 
-/* leaf IDFT16 in registers (lte_dfts.c:1597-1724) */
+/* leaf IDFT16 in registers (lte_dfts.c:1597-1724); w16 is wave-uniform (scalar loads) */
+template <bool FF = false>
 static __device__ __forceinline__ void idft16_reg(s16x2 *x, const twp_t *w16 /* W^{0,1,2,3,4,6,9} */)
 {
   constexpr int k1[4] = {0, 1, 2, 3}, k2[4] = {0, 2, 4, 5}, k3[4] = {0, 3, 5, 6}; /* slots of k, 2k, 3k */
   s16x2 S[4][4];
 #pragma unroll
-  for (int j = 0; j < 4; j++) r4inv(x[j], x[4 + j], x[8 + j], x[12 + j], S[0][j], S[1][j], S[2][j], S[3][j]);
+  for (int j = 0; j < 4; j++) r4inv<FF>(x[j], x[4 + j], x[8 + j], x[12 + j], S[0][j], S[1][j], S[2][j], S[3][j]);
 #pragma unroll
   for (int k = 0; k < 4; k++) {
-    s16x2 b1 = cmulc16(S[k][1], w16[k1[k]]);
-    s16x2 b2 = cmulc16(S[k][2], w16[k2[k]]);
-    s16x2 b3 = cmulc16(S[k][3], w16[k3[k]]);
-    r4inv(S[k][0], b1, b2, b3, x[k], x[4 + k], x[8 + k], x[12 + k]);
+    s16x2 b1 = cmulc16u(S[k][1], w16[k1[k]]);
+    s16x2 b2 = cmulc16u(S[k][2], w16[k2[k]]);
+    s16x2 b3 = cmulc16u(S[k][3], w16[k3[k]]);
+    r4inv<FF>(S[k][0], b1, b2, b3, x[k], x[4 + k], x[8 + k], x[12 + k]);
   }
 }
 
@@ -317,7 +328,7 @@ typedef uint32_t u32x2_t __attribute__((ext_vector_type(2)));
  * the leaf stores wait for every thread's producer */
 template <int NA, bool PSYNC, class Prod, class Cons>
 static __device__ __forceinline__ void idft2048_unit(uint32_t *lds, int t, bool active, const idft2048_tw_t &tw,
-                                                     Prod prod, Cons cons, int scale)
+                                                     Prod prod, Cons cons, int scale, uint32_t dep)
 {
   constexpr int X1W = idft2048_tw_t::X1W;
   s16x2 x[NA][16];
@@ -326,7 +337,7 @@ static __device__ __forceinline__ void idft2048_unit(uint32_t *lds, int t, bool 
     prod(x);
     if constexpr (PSYNC)
 #pragma unroll
-      for (int a = 0; a < NA; a++) idft16_reg(x[a], tw.l16);
+      for (int a = 0; a < NA; a++) idft16_reg<NA == 2>(x[a], tw.l16);
   }
   if constexpr (PSYNC) IDFT_SYNC();
   if (active) {
@@ -336,7 +347,7 @@ static __device__ __forceinline__ void idft2048_unit(uint32_t *lds, int t, bool 
     const uint32_t wo = OAI4G_DIAG_PASSA ? (uint32_t)t : 2u * (t & 31) + ((t >> 5) & 1) + 64u * (t >> 6);
 #pragma unroll
     for (int a = 0; a < NA; a++) {
-      if constexpr (!PSYNC) idft16_reg(x[a], tw.l16);
+      if constexpr (!PSYNC) idft16_reg<NA == 2>(x[a], tw.l16);
 #pragma unroll
       for (int k = 0; k < 16; k++) lds[a * X1W + k * 144 + wo] = c2u(x[a][k]);
     }
@@ -359,64 +370,69 @@ static __device__ __forceinline__ void idft2048_unit(uint32_t *lds, int t, bool 
   }
   IDFT_SYNC();   /* E2 aliases E1 */
   if (active) {
-    const twp_t w64[3] = {tw_of(tw.b64[0]), tw_of(tw.b64[1]), tw_of(tw.b64[2])};
+    /* E2 word of out256_j[k2] = 8 k2 + j + 2 (k2 >> 3): an affine base plus immediates */
+    const uint32_t wb = 8u * k4 + j + 2u * (k4 >> 3);
+    const twp_t w64[3] = {tw_use(tw.b64[0], dep), tw_use(tw.b64[1], dep), tw_use(tw.b64[2], dep)};
 #pragma unroll
     for (int a = 0; a < NA; a++) {
       s16x2 o[4][4];   /* [r2][m3] */
 #pragma unroll
       for (int r2 = 0; r2 < 4; r2++) {
         const s16x2 *v = &x[a][4 * r2];
-        r4inv(v[0], cmulc16(v[1], w64[0]), cmulc16(v[2], w64[1]), cmulc16(v[3], w64[2]), o[r2][0], o[r2][1],
+        r4inv<NA == 2>(v[0], cmulc16(v[1], w64[0]), cmulc16(v[2], w64[1]), cmulc16(v[3], w64[2]), o[r2][0], o[r2][1],
               o[r2][2], o[r2][3]);
 #pragma unroll
         for (int m = 0; m < 4; m++) o[r2][m] = shr3(o[r2][m]);
       }
 #pragma unroll
       for (int m3 = 0; m3 < 4; m3++) {
+        /* the 12 companions of this level stay in registers (used once per antenna): 124 VGPRs at
+         * 4 waves/SIMD; the other levels' are rebuilt at use */
         const twp_t w[3] = {tw_of(tw.b256[m3][0]), tw_of(tw.b256[m3][1]), tw_of(tw.b256[m3][2])};
         s16x2 y[4];
         ibfly4(o[0][m3], o[1][m3], o[2][m3], o[3][m3], w[0], w[1], w[2], y[0], y[1], y[2], y[3]);
 #pragma unroll
-        for (int m2 = 0; m2 < 4; m2++) {
-          const uint32_t k2 = (uint32_t)k4 + 16u * m3 + 64u * m2;
-          lds[a * X1W + 8u * k2 + j + 2u * (k2 >> 3)] = c2u(shr1(y[m2]));
-        }
+        for (int m2 = 0; m2 < 4; m2++)   /* k2 = k4 + 16 m3 + 64 m2, k4 < 16: k2 >> 3 = (k4 >> 3) + 2 m3 + 8 m2 */
+          lds[a * X1W + wb + 132u * m3 + 528u * m2] = c2u(shr1(y[m2]));
       }
     }
   }
   IDFT_SYNC();
-  /* pass C: 1024- and 2048-levels for k2 = t + 128 h */
+  /* pass C: 1024- and 2048-levels for k2 = t + 128 h (h outer: the twiddle companions of h are
+   * built once for every antenna) */
   if (active) {
 #pragma unroll
-    for (int a = 0; a < NA; a++) {
-      s16x2 v[2][8];
+    for (int h = 0; h < 2; h++) {
+      const twp_t w[3] = {tw_use(tw.c1024[h][0], dep), tw_use(tw.c1024[h][1], dep), tw_use(tw.c1024[h][2], dep)};
+      twp_t w2[4];
 #pragma unroll
-      for (int h = 0; h < 2; h++) {
-        const uint32_t k2 = (uint32_t)t + 128u * h;
-        const uint32_t ro = 8u * k2 + 2u * (k2 >> 3);
+      for (int m1 = 0; m1 < 4; m1++) w2[m1] = tw_use(tw.c2048[h + 2 * m1], dep);
+      /* k2 = t + 128 h: 8 k2 + 2 (k2 >> 3) = 8 t + 2 (t >> 3) + 1056 h */
+      const uint32_t ro = 8u * (uint32_t)t + 2u * ((uint32_t)t >> 3) + 1056u * h;
+#pragma unroll
+      for (int a = 0; a < NA; a++) {
+        s16x2 v[8];
 #pragma unroll
         for (int i = 0; i < 4; i++) {
           const u32x2_t q = *(const u32x2_t *)&lds[a * X1W + ro + 2 * i];
-          v[h][2 * i] = u2c(q.x);
-          v[h][2 * i + 1] = u2c(q.y);
+          v[2 * i] = u2c(q.x);
+          v[2 * i + 1] = u2c(q.y);
         }
-      }
-#pragma unroll
-      for (int h = 0; h < 2; h++) {
-        const twp_t w[3] = {tw_of(tw.c1024[h][0]), tw_of(tw.c1024[h][1]), tw_of(tw.c1024[h][2])};
         s16x2 o[2][4];   /* [e][m1] */
 #pragma unroll
         for (int e = 0; e < 2; e++) {
-          ibfly4(v[h][e], v[h][e + 2], v[h][e + 4], v[h][e + 6], w[0], w[1], w[2], o[e][0], o[e][1], o[e][2],
-                 o[e][3]);
+          ibfly4(v[e], v[e + 2], v[e + 4], v[e + 6], w[0], w[1], w[2], o[e][0], o[e][1], o[e][2], o[e][3]);
 #pragma unroll
           for (int m = 0; m < 4; m++) o[e][m] = shr1(o[e][m]);
         }
 #pragma unroll
         for (int m1 = 0; m1 < 4; m1++) {
           s16x2 y0, y1;
-          ibfly2(o[0][m1], o[1][m1], tw_of(tw.c2048[h + 2 * m1]), y0, y1);
-          if (scale) { y0 = mulhi2(y0); y1 = mulhi2(y1); }
+          ibfly2(o[0][m1], o[1][m1], w2[m1], y0, y1);
+          if (scale) {
+            y0 = NA == 2 ? mulhi2_f(y0) : mulhi2(y0);
+            y1 = NA == 2 ? mulhi2_f(y1) : mulhi2(y1);
+          }
           cons(a, t, 128 * h + 256 * m1, y0);
           cons(a, t, 128 * h + 256 * m1 + 1024, y1);
         }
@@ -436,12 +452,13 @@ struct idft_sel<11> {
   using tw_t = idft2048_tw_t;
   static constexpr int XW = idft2048_tw_t::X1W;
 };
+/* dep: a per-item value in persistent loops (see tw_use), 0 elsewhere */
 template <int LOG2N, int NA, bool PSYNC = false, class Prod, class Cons>
 static __device__ __forceinline__ void idft_any(uint32_t *lds, int t, bool active,
                                                 const typename idft_sel<LOG2N>::tw_t &tw, Prod prod, Cons cons,
-                                                int scale)
+                                                int scale, uint32_t dep = 0)
 {
-  if constexpr (LOG2N == 11) idft2048_unit<NA, PSYNC>(lds, t, active, tw, prod, cons, scale);
+  if constexpr (LOG2N == 11) idft2048_unit<NA, PSYNC>(lds, t, active, tw, prod, cons, scale, dep);
   else idft_unit<LOG2N, NA>(lds, t, active, tw, prod, cons, scale);
 }
 
@@ -595,6 +612,19 @@ static __device__ __forceinline__ void cdd_pair(s16x2 x0, s16x2 x1, uint32_t par
   s16x2 d = h - u2c(~a & b);
   y1 = parity ? (s16x2){0, 0} - d : d;
 }
+/* The same with the sign as a lane mask m (0 or ~0, from the RE code's parity bit): y1 = (d ^ m) - m
+ * per 16-bit lane (wrapping, = -d when m = ~0).  Written as v_xor + v_pk_sub_u16 so the compiler
+ * cannot turn it back into v_cmp + v_cndmask, whose SGPR mask costs an s_nop 1 hazard per RE. */
+static __device__ __forceinline__ void cdd_pair_m(s16x2 x0, s16x2 x1, uint32_t m, s16x2 &y0, s16x2 &y1)
+{
+  const uint32_t a = c2u(x0), b = c2u(x1);
+  const s16x2 h = u2c(a ^ b) >> (s16x2){1, 1};
+  y0 = u2c(a & b) + h;
+  const s16x2 d = h - u2c(~a & b);
+  uint32_t r;
+  asm("v_xor_b32_e32 %0, %1, %2\n\tv_pk_sub_u16 %0, %0, %2" : "=&v"(r) : "v"(c2u(d)), "v"(m));
+  y1 = u2c(r);
+}
 
 /* ALAMOUTI levels (dlsch_modulation.c:362-546): TA = antenna 0 at RE n (x0/sqrt2), TB = antenna
  * 1 at n (-conj(x1)/sqrt2); QPSK signs are applied before the 1/sqrt2 scaling, QAM negation after */
@@ -696,18 +726,18 @@ static __device__ __forceinline__ uint32_t ld_u32_any(const uint8_t *p)
 #define OAI4G_MOD_ZBAND 1
 #endif
 #ifndef OAI4G_MODOFDM_WAVES
-#define OAI4G_MODOFDM_WAVES 3   /* measured: 3 waves/SIMD (<=168 VGPRs) beats 2 (no cap) and 4 (spills) */
+/* waves per SIMD: 2048 points 4 (round 5: SGPR twiddle operands, affine LDS addresses and
+ * companions rebuilt at use bring the kernel to <= 124 VGPRs, and the LDS alias to 19.0 KB per
+ * workgroup: 8 workgroups per CU); smaller transforms 3 (24 KB of LDS per workgroup) */
+#define OAI4G_MODOFDM_WAVES 0
 #endif
 #ifndef OAI4G_MOD_ALIAS
 /* 2048-point symbols: the staged QAM addresses share LDS with the IDFT exchange (two more barriers
  * per item), 19.0 KB per workgroup instead of 25.0 KB */
-#define OAI4G_MOD_ALIAS 0
+#define OAI4G_MOD_ALIAS 1
 #endif
-#if OAI4G_MODOFDM_WAVES > 0
-#define MODOFDM_ATTR __attribute__((amdgpu_waves_per_eu(OAI4G_MODOFDM_WAVES)))
-#else
-#define MODOFDM_ATTR
-#endif
+#define MODOFDM_WAVES_OF(L) (OAI4G_MODOFDM_WAVES > 0 ? OAI4G_MODOFDM_WAVES : ((L) == 11 ? 4 : 3))
+#define MODOFDM_ATTR __attribute__((amdgpu_waves_per_eu(MODOFDM_WAVES_OF(LOG2N))))
 /* MODE: 0 = TM1 (one transform stored to every antenna), 1 = ALAMOUTI, 2 = LARGE_CDD, 3 = 4-port
  * LARGE_CDD (C4: two items per symbol, each transforming one antenna pair) */
 template <int LOG2N, int MODE, bool CRS, bool ECP>
@@ -798,7 +828,7 @@ __global__ void __launch_bounds__(128) MODOFDM_ATTR k_modofdm(const cfg_dev_t *_
     const uint32_t sf = it / nsymb, l = it - sf * nsymb;
     const uint32_t sfi = (c->first_sf + (sf0 + sf) * c->sf_step) % 10;
     const uint32_t nre = act ? c->symnre[sfi][l] : 0u, re0 = c->symbase[sfi][l];
-    const gu128_t *rsrc = (const gu128_t *)(c->remap_tm + ((size_t)sfi * 14 + l) * N + (size_t)t * 16);
+    const gu128_t *rsrc = (const gu128_t *)((CRS ? c->remap_tm : c->remap_tm0) + ((size_t)sfi * 14 + l) * N + (size_t)t * 16);
     pf.ra = rsrc[0];
     pf.rb = rsrc[1];
 #if OAI4G_MOD_STAGE
@@ -931,7 +961,8 @@ __global__ void __launch_bounds__(128) MODOFDM_ATTR k_modofdm(const cfg_dev_t *_
           constexpr int GR = OAI4G_MOD_GROUP;
 #if OAI4G_MOD_STAGE
           /* remap_tm data codes are 2 idx | parity << 15 (ALAMOUTI: 2 (2i + role)): the byte
-           * offset of entry idx; any non-data code (>= 0xC000) clamps to the zero sentinel */
+           * offset of entry idx; any non-data code (>= 0xC000) clamps to the zero sentinel (in
+           * remap_tm0 it already is the sentinel) */
           constexpr uint32_t AM = MODE == 1 ? 0x7FFCu : 0x7FFEu;
           constexpr bool ZB = OAI4G_MOD_ZBAND == 2 || (OAI4G_MOD_ZBAND == 1 && (CRS || MODE != 2));
           auto zb = [&](int n) { return ZB && n >= G::ZLO && n <= G::ZHI; };   /* constant after unrolling */
@@ -960,7 +991,8 @@ __global__ void __launch_bounds__(128) MODOFDM_ATTR k_modofdm(const cfg_dev_t *_
             for (int n = 0; n < GZ; n++) {
               const int i = act(g + n);
               code[n] = (rw[i >> 1] >> (16 * (i & 1))) & 0xFFFFu;
-              const uint32_t a = min(code[n] & AM, 2u * SENT);
+              /* without CRS / control REs every non-data code is already the sentinel (remap_tm0) */
+              const uint32_t a = CRS ? min(code[n] & AM, 2u * SENT) : code[n] & AM;
               v0[n] = *(const uint16_t *)(sb0 + a);
               if constexpr (MODE == 1) v1[n] = *(const uint16_t *)(sb0 + a + 2);
               if constexpr (CW2) v1[n] = *(const uint16_t *)(sb1 + a);
@@ -993,7 +1025,8 @@ __global__ void __launch_bounds__(128) MODOFDM_ATTR k_modofdm(const cfg_dev_t *_
                 for (int a = 0; a < 2; a++)
                   x[a][i] = half_signed(((CDD4_QSEL >> (sel + a)) & 1u) ? x1 : x0, (CDD4_NEG >> (sel + a)) & 1u);
               } else if constexpr (NA == 2) {
-                cdd_pair(x0, u2c(v1[n]), code[n] >> 15 & 1u, x[0][i], x[1][i]);
+                /* parity bit 15 of the code -> lane mask 0 / ~0 */
+                cdd_pair_m(x0, u2c(v1[n]), (uint32_t)((int32_t)(code[n] << 16) >> 31), x[0][i], x[1][i]);
               } else {
                 x[0][i] = x0;                                   /* TM1: SISO precoder */
               }
@@ -1116,7 +1149,7 @@ __global__ void __launch_bounds__(128) MODOFDM_ATTR k_modofdm(const cfg_dev_t *_
             for (uint32_t aa = 0; aa < n_ant; aa++) store(dst0 + aa * c->spt);
           }
         },
-        1);
+        1, it);
     if (OAI4G_MOD_ENDSYNC || PSYNC) __syncthreads();   /* PSYNC: the next item stages into the exchange */
   }
 }

@@ -2,8 +2,10 @@
 
 One trial of the reference, TM1 / SISO / one receive antenna / AWGN (`-gN`: channel_model = AWGN, value
 18 of SCM_t in SIMULATION/TOOLS/defs.h:158-178, applied through multipath_channel, a single unit tap at
-Ricean factor 0 -- `-gL` would be Rice8 = 14), as the reference's
-AWGN_results/bler_tx1_chan18_nrx1_mcs*.csv were produced:
+Ricean factor 0 -- `-gL` would be Rice8 = 14), the configuration the reference's
+AWGN_results/bler_tx1_chan18_nrx1_mcs*.csv name in their file names (the reference also holds a second
+set for it, AWGN/Perf_Curves_Abs/awgn_bler_tx1_mcs*.csv, 0.05-0.3 dB apart; the GPU chain follows that
+one, tests/test_gpu_dlsim.py):
   - transmit (:2553-2704): generate_dci_top's PCFICH + PDCCH for one format-1 DCI (L = 1, RNTI
     0x1234; dlsim.c:1154-1157), dlsch_encoding / dlsch_scrambling / dlsch_modulation of a random
     transport block, generate_pilots, do_OFDM_mod_l of the subframe's two slots, and of the next
@@ -13,7 +15,8 @@ AWGN_results/bler_tx1_chan18_nrx1_mcs*.csv were produced:
     - pa_dB (:2852-2866), pa = 0 dB;
   - the UE (:2907-3260): slot_fep of both slots plus symbol 0 of the next, lte_dl_channel_estimation
     (perfect_ce = 0, high_speed_flag = 1), rx_pdsch, dlsch_unscrambling, dlsch_decoding with the
-    16-bit decoder and MAX_TURBO_ITERATIONS = 4 (PHY/CODING/defs.h:51);
+    16-bit decoder (dlsim's default, llr8_flag = 0 at dlsim.c:339; `-L` selects the 8-bit one, llr8
+    here) and MAX_TURBO_ITERATIONS = 4 (PHY/CODING/defs.h:51);
   - a trial errs when dlsch_decoding returns more than max_turbo_iterations (:3330-3350); one round
     (the CSVs hold no retransmission counts).
 On the GPU: TxPipeline (k_encode + k_modofdm with CRS + control) -> k_signal_energy -> k_awgn ->

@@ -29,6 +29,8 @@ def test_bench_spawns_ranks_gloo_stub():
     assert out["config"]["parallelism"] == "subframe-sharded x2"
     assert out["config"]["G"] == [86400, 86400]  # parameter block broadcast from rank 0 intact
     assert out["value"] > 0 and out["ms_per_step"] > 0
+    assert len(out["per_rank_subframes_per_s"]) == 2 and min(out["per_rank_subframes_per_s"]) > 0
+    assert 0 < out["rank_efficiency"] <= 1.0 + 1e-9
 
 
 def test_bench_failing_rank_fails_the_job():
