@@ -555,7 +555,11 @@ static __device__ __forceinline__ uint32_t transpose32_t(uint32_t x, uint32_t la
     const uint32_t p = xor_lane<J>(x);
     const uint32_t sh = __builtin_amdgcn_alignbit(p, p, hi ? J : 32u - J);
     const uint32_t mm = hi ? ~M : M;
-    return transpose32_t<K + 1>((x & mm) | (sh & ~mm), lane32);
+    /* (x & mm) | (sh & ~mm) as one fast-rate v_bitop3 mux (0xe4: c ? a : b); the compiler's
+     * v_and + v_and_or pair has a slow-rate op */
+    uint32_t r;
+    asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0xe4" : "=v"(r) : "v"(x), "v"(sh), "v"(mm));
+    return transpose32_t<K + 1>(r, lane32);
   }
 }
 static __device__ __forceinline__ uint32_t transpose32(uint32_t x, uint32_t lane32) { return transpose32_t<0>(x, lane32); }
