@@ -604,6 +604,7 @@ size_t oai4g_tx_workspace_bytes(const oai4g_tx_config_t *cfg, int n_sf);
  *   d_payload : [n_sf][n_cw][payload_stride] bytes, TBS/8 valid bytes each (not modified)
  *   d_work    : oai4g_tx_workspace_bytes() bytes (packed scrambled e bits)
  *   d_iq      : [n_sf][nb_antennas_tx][samples_per_tti] int32 (int16 I, int16 Q)
+ *               (8-byte aligned: sample pairs leave as 8-byte stores; -1 otherwise)
  * stream is a hipStream_t (NULL = default stream).  Asynchronous. */
 int oai4g_tx_batch(const oai4g_tx_config_t *cfg, int n_sf, const uint8_t *d_payload, void *d_work,
                    int32_t *d_iq, void *stream);

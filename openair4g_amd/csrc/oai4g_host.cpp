@@ -1266,11 +1266,22 @@ extern "C" int oai4g_tx_encode(const oai4g_tx_config_t *cfg, int n_sf, const uin
   return 0;
 }
 
+/* the 2048-point modulator stores sample pairs as 8-byte words */
+static int iq_aligned(const int32_t *d_iq)
+{
+  if ((uintptr_t)d_iq & 7u) {
+    set_err("iq buffer must be 8-byte aligned");
+    return 0;
+  }
+  return 1;
+}
+
 extern "C" int oai4g_tx_batch(const oai4g_tx_config_t *cfg, int n_sf, const uint8_t *d_payload, void *d_work,
                               int32_t *d_iq, void *stream)
 {
   NEED_INIT(-1);
   if (n_sf <= 0) return 0;
+  if (!iq_aligned(d_iq)) return -1;
   hipStream_t s = (hipStream_t)stream;
   uint32_t *ew = (uint32_t *)d_work;
   int chunk = cfg->pipe_chunk;
@@ -1303,6 +1314,7 @@ extern "C" int oai4g_tx_batch_timed(const oai4g_tx_config_t *cfg, int n_sf, cons
                                     int32_t *d_iq, void *stream, float *kernel_ms)
 {
   NEED_INIT(-1);
+  if (!iq_aligned(d_iq)) return -1;
   hipStream_t s = (hipStream_t)stream;
   hipEvent_t ev[3];
   for (int i = 0; i < 3; i++) HCK(hipEventCreate(&ev[i]), -1);

@@ -279,16 +279,18 @@ static __device__ __forceinline__ void idft_unit(uint32_t *lds, int t, bool acti
  * LDS images (one region of X1W words per transform, the second aliasing the first):
  *   E1: L_t[k4] at k4*144 + 2 (t & 31) + ((t >> 5) & 1) + 64 (t >> 6)  — pass-A b32 stores 2-way
  *       (free), pass-B ds_read_b64 of the (r3, r3 + 1) pair conflict-free;
- *   E2: out256_j[k2] at 8 k2 + j + 2 (k2 >> 3) — pass-B b32 stores consecutive, pass-C
- *       ds_read_b64 of (j, j + 1) conflict-free.
+ *   E2: out256_j[k2] at 264 j + k2 — pass-B b32 stores conflict-free (264 = 8 mod 64), pass-C
+ *       ds_read_b64 of the (k2, k2 + 1) pair conflict-free; pass C takes k2 = 2 t + h, so each
+ *       output pair (2 t, 2 t + 1) leaves as one 8-byte store.
  * ==================================================================================== */
 struct idft2048_tw_t {
   static constexpr int X1W = 16 * 144;
   twp_t l16[7];        /* W16^{0,1,2,3,4,6,9} (wave-uniform) */
   s16x2 b64[3];        /* W64^{r k4}, r = 1..3, k4 = t >> 3 */
   s16x2 b256[4][3];    /* W256^{r (k4 + 16 m3)} */
-  s16x2 c1024[2][3];   /* W1024^{r k2}, k2 = t + 128 h */
-  s16x2 c2048[8];      /* W2048^{k1}, k1 = t + 128 (h + 2 m1) */
+  s16x2 c1024[2][3];   /* W1024^{r k2}, k2 = 2 t + h */
+  s16x2 c2048[8];      /* W2048^{k1}, k1 = 2 t + h + 256 m1 at [h + 2 m1] */
+  static constexpr int E2S = 264;   /* E2 words per 256-point transform j */
 
   __device__ __forceinline__ void load(const uint32_t *tw, int t)
   {
@@ -307,9 +309,9 @@ struct idft2048_tw_t {
 #pragma unroll
     for (int h = 0; h < 2; h++)
 #pragma unroll
-      for (int r = 0; r < 3; r++) c1024[h][r] = u2c(g[oai4g_tw_offset(10) + (r + 1) * (t + 128 * h)]);
+      for (int r = 0; r < 3; r++) c1024[h][r] = u2c(g[oai4g_tw_offset(10) + (r + 1) * (2 * t + h)]);
 #pragma unroll
-    for (int i = 0; i < 8; i++) c2048[i] = u2c(g[oai4g_tw_offset(11) + t + 128 * i]);
+    for (int i = 0; i < 8; i++) c2048[i] = u2c(g[oai4g_tw_offset(11) + 2 * t + (i & 1) + 256 * (i >> 1)]);
   }
 };
 
@@ -326,11 +328,12 @@ typedef uint32_t u32x2_t __attribute__((ext_vector_type(2)));
 
 /* PSYNC: the producer reads LDS that the exchange aliases (k_modofdm's staged QAM addresses), so
  * the leaf stores wait for every thread's producer */
-template <int NA, bool PSYNC, class Prod, class Cons>
+template <int NA, bool PSYNC, class Prod, class Cons2>
 static __device__ __forceinline__ void idft2048_unit(uint32_t *lds, int t, bool active, const idft2048_tw_t &tw,
-                                                     Prod prod, Cons cons, int scale, uint32_t dep)
+                                                     Prod prod, Cons2 cons2, int scale, uint32_t dep)
 {
-  constexpr int X1W = idft2048_tw_t::X1W;
+  constexpr int X1W = idft2048_tw_t::X1W, E2S = idft2048_tw_t::E2S;
+  static_assert(7 * E2S + 256 <= X1W, "E2 must fit the exchange");
   s16x2 x[NA][16];
   /* pass A: leaves */
   if (active) {
@@ -370,8 +373,8 @@ static __device__ __forceinline__ void idft2048_unit(uint32_t *lds, int t, bool 
   }
   IDFT_SYNC();   /* E2 aliases E1 */
   if (active) {
-    /* E2 word of out256_j[k2] = 8 k2 + j + 2 (k2 >> 3): an affine base plus immediates */
-    const uint32_t wb = 8u * k4 + j + 2u * (k4 >> 3);
+    /* E2 word of out256_j[k2] = E2S j + k2, k2 = k4 + 16 m3 + 64 m2: an affine base plus immediates */
+    const uint32_t wb = (uint32_t)E2S * j + k4;
     const twp_t w64[3] = {tw_use(tw.b64[0], dep), tw_use(tw.b64[1], dep), tw_use(tw.b64[2], dep)};
 #pragma unroll
     for (int a = 0; a < NA; a++) {
@@ -392,50 +395,62 @@ static __device__ __forceinline__ void idft2048_unit(uint32_t *lds, int t, bool 
         s16x2 y[4];
         ibfly4(o[0][m3], o[1][m3], o[2][m3], o[3][m3], w[0], w[1], w[2], y[0], y[1], y[2], y[3]);
 #pragma unroll
-        for (int m2 = 0; m2 < 4; m2++)   /* k2 = k4 + 16 m3 + 64 m2, k4 < 16: k2 >> 3 = (k4 >> 3) + 2 m3 + 8 m2 */
-          lds[a * X1W + wb + 132u * m3 + 528u * m2] = c2u(shr1(y[m2]));
+        for (int m2 = 0; m2 < 4; m2++) lds[a * X1W + wb + 16u * m3 + 64u * m2] = c2u(shr1(y[m2]));
       }
     }
   }
   IDFT_SYNC();
-  /* pass C: 1024- and 2048-levels for k2 = t + 128 h (h outer: the twiddle companions of h are
-   * built once for every antenna) */
+  /* pass C: 1024- and 2048-levels for k2 = 2 t + h; outputs k2 + 256 m1 (+ 1024) of h = 0, 1 are
+   * adjacent and leave through cons2 as one pair */
   if (active) {
+#ifndef OAI4G_PASSC_TWONCE
+#define OAI4G_PASSC_TWONCE 1   /* 1: the pass-C companions are built once for both antennas (0: per antenna) */
+#endif
+    twp_t wc[2][3], wc2[2][4];
+    auto build_wc = [&]() {
 #pragma unroll
-    for (int h = 0; h < 2; h++) {
-      const twp_t w[3] = {tw_use(tw.c1024[h][0], dep), tw_use(tw.c1024[h][1], dep), tw_use(tw.c1024[h][2], dep)};
-      twp_t w2[4];
+      for (int h = 0; h < 2; h++) {
 #pragma unroll
-      for (int m1 = 0; m1 < 4; m1++) w2[m1] = tw_use(tw.c2048[h + 2 * m1], dep);
-      /* k2 = t + 128 h: 8 k2 + 2 (k2 >> 3) = 8 t + 2 (t >> 3) + 1056 h */
-      const uint32_t ro = 8u * (uint32_t)t + 2u * ((uint32_t)t >> 3) + 1056u * h;
+        for (int r = 0; r < 3; r++) wc[h][r] = tw_use(tw.c1024[h][r], dep);
 #pragma unroll
-      for (int a = 0; a < NA; a++) {
-        s16x2 v[8];
+        for (int m1 = 0; m1 < 4; m1++) wc2[h][m1] = tw_use(tw.c2048[h + 2 * m1], dep);
+      }
+    };
+    if (OAI4G_PASSC_TWONCE) build_wc();
 #pragma unroll
-        for (int i = 0; i < 4; i++) {
-          const u32x2_t q = *(const u32x2_t *)&lds[a * X1W + ro + 2 * i];
-          v[2 * i] = u2c(q.x);
-          v[2 * i + 1] = u2c(q.y);
-        }
+    for (int a = 0; a < NA; a++) {
+      if (!OAI4G_PASSC_TWONCE) build_wc();
+      s16x2 v[2][8];   /* [h][j] */
+#pragma unroll
+      for (int jj = 0; jj < 8; jj++) {
+        const u32x2_t q = *(const u32x2_t *)&lds[a * X1W + E2S * jj + 2 * t];
+        v[0][jj] = u2c(q.x);
+        v[1][jj] = u2c(q.y);
+      }
+      s16x2 y[2][2][4];   /* [h][e][m1] */
+#pragma unroll
+      for (int h = 0; h < 2; h++) {
+        const twp_t *w = wc[h];
         s16x2 o[2][4];   /* [e][m1] */
 #pragma unroll
         for (int e = 0; e < 2; e++) {
-          ibfly4(v[e], v[e + 2], v[e + 4], v[e + 6], w[0], w[1], w[2], o[e][0], o[e][1], o[e][2], o[e][3]);
+          ibfly4(v[h][e], v[h][e + 2], v[h][e + 4], v[h][e + 6], w[0], w[1], w[2], o[e][0], o[e][1], o[e][2], o[e][3]);
 #pragma unroll
           for (int m = 0; m < 4; m++) o[e][m] = shr1(o[e][m]);
         }
 #pragma unroll
         for (int m1 = 0; m1 < 4; m1++) {
-          s16x2 y0, y1;
-          ibfly2(o[0][m1], o[1][m1], w2[m1], y0, y1);
+          ibfly2(o[0][m1], o[1][m1], wc2[h][m1], y[h][0][m1], y[h][1][m1]);
           if (scale) {
-            y0 = NA == 2 ? mulhi2_f(y0) : mulhi2(y0);
-            y1 = NA == 2 ? mulhi2_f(y1) : mulhi2(y1);
+#pragma unroll
+            for (int e = 0; e < 2; e++) y[h][e][m1] = NA == 2 ? mulhi2_f(y[h][e][m1]) : mulhi2(y[h][e][m1]);
           }
-          cons(a, t, 128 * h + 256 * m1, y0);
-          cons(a, t, 128 * h + 256 * m1 + 1024, y1);
         }
+      }
+#pragma unroll
+      for (int m1 = 0; m1 < 4; m1++) {
+        cons2(a, 2 * t, 256 * m1, y[0][0][m1], y[1][0][m1]);
+        cons2(a, 2 * t, 256 * m1 + 1024, y[0][1][m1], y[1][1][m1]);
       }
     }
   }
@@ -452,14 +467,29 @@ struct idft_sel<11> {
   using tw_t = idft2048_tw_t;
   static constexpr int XW = idft2048_tw_t::X1W;
 };
-/* dep: a per-item value in persistent loops (see tw_use), 0 elsewhere */
+/* dep: a per-item value in persistent loops (see tw_use), 0 elsewhere.  cons(a, t, off, y) takes
+ * output t + off of antenna a; cons2(a, tt, off, y0, y1) the adjacent outputs tt + off, tt + off + 1
+ * (tt + off even) — the 2048-point schedule produces pairs */
+template <int LOG2N, int NA, bool PSYNC = false, class Prod, class Cons, class Cons2>
+static __device__ __forceinline__ void idft_any2(uint32_t *lds, int t, bool active,
+                                                 const typename idft_sel<LOG2N>::tw_t &tw, Prod prod, Cons cons,
+                                                 Cons2 cons2, int scale, uint32_t dep = 0)
+{
+  if constexpr (LOG2N == 11) idft2048_unit<NA, PSYNC>(lds, t, active, tw, prod, cons2, scale, dep);
+  else idft_unit<LOG2N, NA>(lds, t, active, tw, prod, cons, scale);
+}
 template <int LOG2N, int NA, bool PSYNC = false, class Prod, class Cons>
 static __device__ __forceinline__ void idft_any(uint32_t *lds, int t, bool active,
                                                 const typename idft_sel<LOG2N>::tw_t &tw, Prod prod, Cons cons,
                                                 int scale, uint32_t dep = 0)
 {
-  if constexpr (LOG2N == 11) idft2048_unit<NA, PSYNC>(lds, t, active, tw, prod, cons, scale, dep);
-  else idft_unit<LOG2N, NA>(lds, t, active, tw, prod, cons, scale);
+  idft_any2<LOG2N, NA, PSYNC>(
+      lds, t, active, tw, prod, cons,
+      [&](int a, int tt, int off, s16x2 y0, s16x2 y1) {
+        cons(a, tt, off, y0);
+        cons(a, tt, off + 1, y1);
+      },
+      scale, dep);
 }
 
 /* ======================================================================================
@@ -949,7 +979,7 @@ __global__ void __launch_bounds__(128) MODOFDM_ATTR k_modofdm(const cfg_dev_t *_
 #else
     constexpr bool PSYNC = false;
 #endif
-    idft_any<LOG2N, NA, PSYNC>(
+    idft_any2<LOG2N, NA, PSYNC>(
         lds_data + unit * NA * LDSW, t, active, twr,
         [&](s16x2 (*x)[16]) {
           /* branch-free and staged in groups of GR REs so each LDS round trip is issued for the
@@ -1142,6 +1172,28 @@ __global__ void __launch_bounds__(128) MODOFDM_ATTR k_modofdm(const cfg_dev_t *_
 #endif
             d[ro] = c2u(y);
             if (off + T - 1 >= N - CPMAX && tt + off >= N - cp) d[ro - N] = c2u(y);
+          };
+          if constexpr (NA == 2) {
+            store(dst0 + (a + 2 * pair) * c->spt);
+          } else {
+            for (uint32_t aa = 0; aa < n_ant; aa++) store(dst0 + aa * c->spt);
+          }
+        },
+        [&](int a, int tt, int off, s16x2 y0, s16x2 y1) {
+          /* outputs tt + off, tt + off + 1 (even first): one 8-byte store (the symbol bodies, CP
+           * lengths and slot/subframe offsets are even and iq is 8-byte aligned, host-checked); N - cp
+           * is even, so both samples of a pair fall in the CP copy or neither does */
+          constexpr int CPMAX = ECP ? N / 4 : (N * 160) / 2048;
+          const bool hi = off >= N / 2;
+          const int ro = hi ? off - N / 2 : off;
+          const u32x2_t v = {c2u(y0), c2u(y1)};
+          auto store = [&](uint32_t *base) {
+            uint32_t *d = base + tt + (hi ? N / 2 : 0);
+#if OAI4G_DIAG_MODOFDM == 1   /* timing diagnostic: the stores (almost) never happen */
+            if (v.x != 0x12345678u) return;
+#endif
+            *(u32x2_t *)&d[ro] = v;
+            if (off + 2 * T - 2 >= N - CPMAX && tt + off >= N - cp) *(u32x2_t *)&d[ro - N] = v;
           };
           if constexpr (NA == 2) {
             store(dst0 + (a + 2 * pair) * c->spt);
