@@ -229,6 +229,7 @@ def bench_c5_chain(args, world, rank, dist, torch):
     ub = oai.UlDecodeBatch(C5_TBS + 24, C5_G, C5_QM, n_sf, max_iterations=8)
     ub.upload(e)
     sid = torch.cuda.current_stream().cuda_stream
+    settle = clock_settle(ub.launch, ub.results, args.settle_ms)
     for _ in range(args.warmup):
         ub.launch()
     ub.results()
@@ -268,7 +269,7 @@ def bench_c5_chain(args, world, rank, dist, torch):
     if rank == 0:
         print(json.dumps({
             "metric": "UL subframes/sec (C5 RM-rx + deinterleave + turbo decode)", "value": value,
-            "unit": "subframes/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+            "unit": "subframes/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup, "clock_settle": {"ms": args.settle_ms, "runs": settle, "why": SETTLE_WHY},
             "ms_per_step": per_launch_ms, "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
             "dtype": "int16", "data": "synthetic soft bits (unstructured: 8 iterations per block)",
             "config": {"workload": "ulsch_decoding 20 MHz MCS20: G 57600 -> 8 x K=5504, max 8 iterations",
@@ -331,6 +332,7 @@ def bench_c5(args, world, rank, dist, torch):
     llr = c5_llrs(n_cb, args.c5_mode, 0xC5 + rank)
     dec = (oai.TurboDecoder8Batch if args.c5_bits == 8 else oai.TurboDecoderBatch)(C5_K, n_cb)
     dec.upload(llr)
+    settle = clock_settle(lambda: dec.run(max_iterations=8, crc_type=crc_type), dec.results, args.settle_ms)
     for _ in range(args.warmup):
         dec.run(max_iterations=8, crc_type=crc_type)
     dec.results()
@@ -377,7 +379,7 @@ def bench_c5(args, world, rank, dist, torch):
         print(json.dumps({
             "metric": "UL subframes/sec (C5 turbo decode)" + (", 8-bit decoder" if args.c5_bits == 8 else ""),
             "value": value, "unit": "subframes/s", "n_gpus": world,
-            "steps": args.steps, "warmup": args.warmup, "ms_per_step": per_launch_ms, "higher_is_better": True,
+            "steps": args.steps, "warmup": args.warmup, "clock_settle": {"ms": args.settle_ms, "runs": settle, "why": SETTLE_WHY}, "ms_per_step": per_launch_ms, "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None, "dtype": "int8" if args.c5_bits == 8 else "int16",
             "data": f"synthetic LLRs ({args.c5_mode})",
             "config": {"workload": "ulsim 20 MHz MCS20 decode: 8 x K=5504, "
@@ -445,6 +447,7 @@ def bench_fep(args, world, rank, dist, torch):
     rx = rng.integers(-3000, 3000, (n_sf, n_ant, 2 * spt), dtype=np.int16).view(np.int32)
     fb = oai.FepBatch(fp, n_sf, n_ant)
     fb.upload(rx)
+    settle = clock_settle(fb.run, oai.lib().oai4g_sync, args.settle_ms)
     for _ in range(args.warmup):
         fb.run()
     oai.lib().oai4g_sync()
@@ -511,7 +514,7 @@ def bench_fep(args, world, rank, dist, torch):
     if rank == 0:
         print(json.dumps({
             "metric": "UE RX front-end subframes/sec (slot_fep, 20 MHz, 2 RX)", "value": value, "unit": "subframes/s",
-            "n_gpus": world, "steps": args.steps, "warmup": args.warmup, "ms_per_step": per_launch_ms,
+            "n_gpus": world, "steps": args.steps, "warmup": args.warmup, "clock_settle": {"ms": args.settle_ms, "runs": settle, "why": SETTLE_WHY}, "ms_per_step": per_launch_ms,
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "int16",
             "data": "synthetic int16 IQ, resident in HBM",
             "config": {"workload": "slot_fep 20 MHz normal CP, 2 RX antennas, 14 x dft2048 per antenna",
@@ -593,6 +596,7 @@ def bench_ue(args, world, rank, dist, torch):
         else:
             stages = {"k_fep": lambda: fb.run(stream=sid),
                       "k_rx_chest": lambda: rb.launch_estimated(cb, fb.d_rxF, 1, stream=sid)}
+    settle = clock_settle(lambda: step(None), oai.lib().oai4g_sync, args.settle_ms)
     for _ in range(args.warmup):
         step(None)
     oai.lib().oai4g_sync()
@@ -659,7 +663,7 @@ def bench_ue(args, world, rank, dist, torch):
     if rank == 0:
         print(json.dumps({
             "metric": metric, "value": value,
-            "unit": "subframes/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+            "unit": "subframes/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup, "clock_settle": {"ms": args.settle_ms, "runs": settle, "why": SETTLE_WHY},
             "ms_per_step": elapsed * 1000.0 / args.steps, "higher_is_better": True, "scaling": "weak",
             "vs_baseline": None, "dtype": "int16",
             "data": f"GPU-transmitted {'C3' if tm3 else 'C2'} subframes (synthetic payload), resident in HBM",
@@ -711,6 +715,25 @@ def _ue_cpu_baseline(args, p, Qm, tm3):
             "slot_fep + 5 lte_dl_channel_estimation calls + rx_pdsch")
     return {"value": n / dt, "unit": "subframes/s", "cores": 1, "kind": "port",
             "sample": f"{n} subframes through the C oracle ({what} + dlsch_unscrambling), single thread, {dt:.1f} s"}
+
+
+SETTLE_WHY = ("GPU power-management ramp: launched cold, the first ~25 ms of back-to-back batches run "
+              "~4 % slower than steady state (profiles/clock_settle_r05.txt); the settle runs precede the "
+              "warmup steps and are not timed")
+
+
+def clock_settle(run, sync, ms):
+    """Run the step (untimed) until `ms` of wall time has passed, so the timed steps see the GPU's
+    steady-state clocks, as a continuously running eNB does; returns the runs made (0 with ms <= 0)."""
+    n = 0
+    t0 = time.perf_counter()
+    while (time.perf_counter() - t0) * 1e3 < ms:
+        run()
+        n += 1
+        if n % 4 == 0:
+            sync()
+    sync()
+    return n
 
 
 def launch_ranks(n, argv):
@@ -849,6 +872,8 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--settle-ms", type=float, default=250.0,
+                    help="untimed runs for this long before the warmup steps (GPU clock ramp); 0 = cold start")
     ap.add_argument("--config", default="C3")
     ap.add_argument("--batch", type=int, default=None,
                     help="subframes per GPU per step (default: C3 8192, C4 1024 = BASELINE config 4's 8192 over "
@@ -957,6 +982,7 @@ def bench_tx(args, world, rank, host):
     pipe.fill_payload(seed=odist.global_payload_seed(0x5EED0000, first, params))
     pipe.sync()
 
+    settle = clock_settle(pipe.run, pipe.sync, args.settle_ms if not host.stub else 0)
     for _ in range(args.warmup):
         pipe.run()
     pipe.sync()
@@ -1023,7 +1049,7 @@ def bench_tx(args, world, rank, host):
             "unit": "subframes/s",
             "n_gpus": world,
             "steps": args.steps,
-            "warmup": args.warmup,
+            "warmup": args.warmup, "clock_settle": {"ms": args.settle_ms, "runs": settle, "why": SETTLE_WHY},
             "ms_per_step": ms_per_step,
             "higher_is_better": True,
             "scaling": "weak",
