@@ -1089,7 +1089,7 @@ static int derive_cfg(oai4g_tx_config *cfg, const oai4g_tx_params_t *p, const ui
       }
       for (int l = 0; l < 14; l++) {
         uint32_t next = l + 1 < (int)h.nsymb ? h.symbase[sf][l + 1] : (uint32_t)n;
-        h.symnre[sf][l] = (uint16_t)(l < p->num_pdcch_symbols || l >= (int)h.nsymb ? 0 : next - h.symbase[sf][l]);
+        h.symnre[sf][l] = (uint32_t)(l < p->num_pdcch_symbols || l >= (int)h.nsymb ? 0 : next - h.symbase[sf][l]);
       }
       for (int cw = 0; cw < p->n_cw; cw++) {
         uint32_t bits = (uint32_t)n * h.cw[cw].Qm;

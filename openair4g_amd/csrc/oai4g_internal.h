@@ -150,7 +150,7 @@ struct cfg_dev_t {
   uint32_t crctab[2][256];      /* CRC byte tables (crc_byte.c:98-105): [0] CRC-24A, [1] CRC-24B */
   cw_dev_t cw[2];
   uint32_t symbase[10][14];     /* data REs before symbol l */
-  uint16_t symnre[10][14];      /* data REs in symbol l */
+  uint32_t symnre[10][14];      /* data REs in symbol l (32-bit: the modulator reads it with a scalar load) */
   uint32_t n_cu;                /* compute units of the device (persistent grids) */
   const uint16_t *remap;        /* [10][14][N] data-RE index | parity<<15; OAI4G_CRS_CODE | pilot
                                    symbol<<9 | port<<8 | m for a CRS RE; 0xFFFF = none */

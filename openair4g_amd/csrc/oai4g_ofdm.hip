@@ -401,7 +401,11 @@ static __device__ __forceinline__ void idft2048_unit(uint32_t *lds, int t, bool 
   }
   IDFT_SYNC();
   /* pass C: 1024- and 2048-levels for k2 = 2 t + h; outputs k2 + 256 m1 (+ 1024) of h = 0, 1 are
-   * adjacent and leave through cons2 as one pair */
+   * adjacent and leave through cons2 as one pair.
+   * The vector loads still in flight here (a persistent caller's prefetch of its next item, issued
+   * before pass A) are waited for now, before this unit's stores: loads and stores share vmcnt, and a
+   * later wait for the prefetch would otherwise be a vmcnt(0) that also drains the stores. */
+  __builtin_amdgcn_s_waitcnt(0x0F70);   /* vmcnt(0), expcnt / lgkmcnt unconstrained */
   if (active) {
 #ifndef OAI4G_PASSC_TWONCE
 #define OAI4G_PASSC_TWONCE 1   /* 1: the pass-C companions are built once for both antennas (0: per antenna) */
@@ -839,7 +843,9 @@ __global__ void __launch_bounds__(128) MODOFDM_ATTR k_modofdm(const cfg_dev_t *_
 #if !OAI4G_MOD_STAGE
   constexpr int EPT = (EW + T - 1) / T;          /* staged e words per thread and codeword */
 #endif
-  const int stride = gridDim.x * UNITS;
+  /* wave-uniform by construction: an SGPR, so the loop control never waits on the vector load of
+   * the dispatch packet (a VGPR copy made every iteration wait for all the IQ stores in flight) */
+  const int stride = __builtin_amdgcn_readfirstlane(gridDim.x * UNITS);
   struct pf_t {
     u32x4_t ra, rb;
 #if OAI4G_MOD_STAGE
@@ -848,6 +854,10 @@ __global__ void __launch_bounds__(128) MODOFDM_ATTR k_modofdm(const cfg_dev_t *_
     uint32_t e0[EPT], e1[EPT];
 #endif
   } pf;
+  /* the configuration through the constant address space: its uniform fields become scalar loads
+   * (lgkmcnt) instead of vector loads the IQ stores would otherwise order behind (shared vmcnt) */
+  typedef const __attribute__((address_space(4))) cfg_dev_t ccfg_t;
+  const ccfg_t *cc = (const ccfg_t *)c;
   auto fetch = [&](int bse) {
     const int item = bse + unit;
     const bool act = item < n_items;
@@ -856,25 +866,26 @@ __global__ void __launch_bounds__(128) MODOFDM_ATTR k_modofdm(const cfg_dev_t *_
     const uint32_t it0 = (act ? (uint32_t)item : 0u) / IPS;
     const uint32_t it = UNITS == 1 ? __builtin_amdgcn_readfirstlane(it0) : it0;
     const uint32_t sf = it / nsymb, l = it - sf * nsymb;
-    const uint32_t sfi = (c->first_sf + (sf0 + sf) * c->sf_step) % 10;
-    const uint32_t nre = act ? c->symnre[sfi][l] : 0u, re0 = c->symbase[sfi][l];
-    const gu128_t *rsrc = (const gu128_t *)((CRS ? c->remap_tm : c->remap_tm0) + ((size_t)sfi * 14 + l) * N + (size_t)t * 16);
+    const uint32_t sfi = (cc->first_sf + (sf0 + sf) * cc->sf_step) % 10;
+    const uint32_t nre_u = cc->symnre[sfi][l], re0 = cc->symbase[sfi][l];   /* uniform: scalar loads */
+    const uint32_t nre = act ? nre_u : 0u;
+    const gu128_t *rsrc = (const gu128_t *)((CRS ? cc->remap_tm : cc->remap_tm0) + ((size_t)sfi * 14 + l) * N + (size_t)t * 16);
     pf.ra = rsrc[0];
     pf.rb = rsrc[1];
 #if OAI4G_MOD_STAGE
     if (act && nre) {
-      const uint8_t *esf = (const uint8_t *)(ebits + (size_t)(sf * c->n_cw) * c->ebits_words);
+      const uint8_t *esf = (const uint8_t *)(ebits + (size_t)(sf * cc->n_cw) * cc->ebits_words);
       const uint32_t nq = (nre + 3) >> 2;
 #pragma unroll
       for (int k = 0; k < QPT; k++) {   /* unconditional (quads past nq re-read the last one): no branch */
         const uint32_t q = min((uint32_t)t + (uint32_t)(k * T), nq - 1);
         pf.x0[k] = ld_u32_any(esf + (((re0 + 4 * q) * Qm0) >> 3));
-        if constexpr (CW2) pf.x1[k] = ld_u32_any(esf + (size_t)4 * c->ebits_words + (((re0 + 4 * q) * Qm1) >> 3));
+        if constexpr (CW2) pf.x1[k] = ld_u32_any(esf + (size_t)4 * cc->ebits_words + (((re0 + 4 * q) * Qm1) >> 3));
       }
     }
 #else
     if (act && nre && OAI4G_DIAG_MODOFDM != 2) {
-      gu32_t *esf = (gu32_t *)(ebits + (size_t)(sf * c->n_cw) * c->ebits_words);
+      gu32_t *esf = (gu32_t *)(ebits + (size_t)(sf * cc->n_cw) * cc->ebits_words);
       const uint32_t wlo0 = (re0 * Qm0) >> 5, cnt0 = min((uint32_t)EW, (((re0 + nre) * Qm0 + 31) >> 5) - wlo0 + 1);
 #pragma unroll
       for (int k = 0; k < EPT; k++)
@@ -883,12 +894,16 @@ __global__ void __launch_bounds__(128) MODOFDM_ATTR k_modofdm(const cfg_dev_t *_
         const uint32_t wlo1 = (re0 * Qm1) >> 5, cnt1 = min((uint32_t)EW, (((re0 + nre) * Qm1 + 31) >> 5) - wlo1 + 1);
 #pragma unroll
         for (int k = 0; k < EPT; k++)
-          if (t + k * T < (int)cnt1) pf.e1[k] = esf[c->ebits_words + wlo1 + t + k * T];
+          if (t + k * T < (int)cnt1) pf.e1[k] = esf[cc->ebits_words + wlo1 + t + k * T];
       }
     }
 #endif
   };
   fetch(blockIdx.x * UNITS);
+  /* no vector load crosses into the item loop: at the loop header the compiler merges the entry
+   * and back-edge states, and a load pending on entry turns into a vmcnt(0) at the top of every item
+   * (draining the previous item's IQ stores) */
+  __builtin_amdgcn_s_waitcnt(0x0F70);
 
   for (int base = blockIdx.x * UNITS; base < n_items; base += stride) {
     const int item = base + unit;
@@ -896,24 +911,26 @@ __global__ void __launch_bounds__(128) MODOFDM_ATTR k_modofdm(const cfg_dev_t *_
     const uint32_t it0 = (active ? (uint32_t)item : 0u) / IPS, pair = (uint32_t)item % IPS;
     const uint32_t it = UNITS == 1 ? __builtin_amdgcn_readfirstlane(it0) : it0;
     const uint32_t sf = it / nsymb, l = it - sf * nsymb;
-    const uint32_t sfi = (c->first_sf + (sf0 + sf) * c->sf_step) % 10;
-    const uint32_t nre = active ? c->symnre[sfi][l] : 0u, re0 = c->symbase[sfi][l];
-    const bool crs_sym = (c->pilmask >> l) & 1u;    /* CRS-bearing symbol: rho_B QAM levels */
+    const uint32_t sfi = (cc->first_sf + (sf0 + sf) * cc->sf_step) % 10;
+    const uint32_t nre_u = cc->symnre[sfi][l], re0 = cc->symbase[sfi][l];
+    const uint32_t nre = active ? nre_u : 0u;
+    const bool crs_sym = (cc->pilmask >> l) & 1u;    /* CRS-bearing symbol: rho_B QAM levels */
     /* symbol with static REs: CRS (with_crs) or the control region (set_control) */
-    const bool stat_sym = (c->with_crs && crs_sym) || ((c->ctlmask[sfi] >> l) & 1u);
+    const bool stat_sym = (cc->with_crs && crs_sym) || ((cc->ctlmask[sfi] >> l) & 1u);
     const uint32_t pil = crs_sym ? 1u : 0u;
     /* output placement: slot, symbol-in-slot i */
     const uint32_t slot = l >= sps ? 1u : 0u, si = l - slot * sps;
-    const uint32_t body = slot * (c->spt >> 1) + (si == 0 ? c->cp0 : (N + c->cp0) + (si - 1) * (N + c->cp) + c->cp);
-    const int cp = (int)(si == 0 ? c->cp0 : c->cp);
-    uint32_t *dst0 = (uint32_t *)iq + (size_t)sf * n_ant * c->spt + body;
+    const uint32_t body = slot * (cc->spt >> 1) + (si == 0 ? cc->cp0 : (N + cc->cp0) + (si - 1) * (N + cc->cp) + cc->cp);
+    const int cp = (int)(si == 0 ? cc->cp0 : cc->cp);
+    uint32_t *dst0 = (uint32_t *)iq + (size_t)sf * n_ant * cc->spt + body;
 
     if (UNITS == 1 && nre == 0 && !(CRS && stat_sym)) {
       /* control-region symbol: the transform of an all-zero grid is zero */
       fetch(base + stride);
+      __builtin_amdgcn_s_waitcnt(0x0F70);   /* the prefetch lands before the stores (see idft2048_unit pass C) */
       if (active)
         for (uint32_t a = MODE == 3 ? 2 * pair : 0; a < (MODE == 3 ? 2 * pair + 2 : n_ant); a++) {
-          uint32_t *d = dst0 + (size_t)a * c->spt - cp;   /* CP start of antenna a */
+          uint32_t *d = dst0 + (size_t)a * cc->spt - cp;   /* CP start of antenna a */
           for (int f = t; f < N + cp; f += T) d[f] = 0u;
         }
       continue;
@@ -963,9 +980,9 @@ __global__ void __launch_bounds__(128) MODOFDM_ATTR k_modofdm(const cfg_dev_t *_
     __syncthreads();
     fetch(base + stride);
 
-    gu32_t *crs_tab = (gu32_t *)c->crs_tab;
+    gu32_t *crs_tab = (gu32_t *)cc->crs_tab;
     const bool crs = CRS && stat_sym;
-    gu32_t *ctl_tab = (gu32_t *)c->ctl_tab;
+    gu32_t *ctl_tab = (gu32_t *)cc->ctl_tab;
 #if OAI4G_MOD_STAGE
     const char *sb0 = (const char *)lds_s[unit][0], *sb1 = (const char *)lds_s[unit][1], *qb = (const char *)qtab;
 #else
@@ -1031,7 +1048,7 @@ __global__ void __launch_bounds__(128) MODOFDM_ATTR k_modofdm(const cfg_dev_t *_
 #define OAI4G_DIAG_QTAB 0    /* timing diagnostic only: 1 = QAM-table reads at lane-distinct banks (wrong values) */
 #endif
 #if OAI4G_DIAG_QTAB
-            const uint32_t qkeep = c->with_crs ? 0xFFFFFFFFu : 0u, qlane = ((uint32_t)threadIdx.x & 31u) << 2;
+            const uint32_t qkeep = cc->with_crs ? 0xFFFFFFFFu : 0u, qlane = ((uint32_t)threadIdx.x & 31u) << 2;
 #define QADDR(x) (((x) & qkeep) | (qlane & ~qkeep))
 #else
 #define QADDR(x) (x)
@@ -1083,7 +1100,7 @@ __global__ void __launch_bounds__(128) MODOFDM_ATTR k_modofdm(const cfg_dev_t *_
 #pragma unroll
             for (int n = 0; n < GR; n++) { lo[n] = e0[p[n] >> 5]; hi[n] = e0[(p[n] >> 5) + 1]; }
 #if OAI4G_DIAG_MODOFDM == 4   /* timing diagnostic: QAM table reads at lane-unique words (no bank conflicts) */
-            const uint32_t dkeep = c->with_crs ? 0xFFFFFFFFu : 0u, dlane = (uint32_t)threadIdx.x & 31u;
+            const uint32_t dkeep = cc->with_crs ? 0xFFFFFFFFu : 0u, dlane = (uint32_t)threadIdx.x & 31u;
 #define QIDX(x) (((x) & dkeep) | (dlane & ~dkeep))
 #else
 #define QIDX(x) (x)
@@ -1174,9 +1191,9 @@ __global__ void __launch_bounds__(128) MODOFDM_ATTR k_modofdm(const cfg_dev_t *_
             if (off + T - 1 >= N - CPMAX && tt + off >= N - cp) d[ro - N] = c2u(y);
           };
           if constexpr (NA == 2) {
-            store(dst0 + (a + 2 * pair) * c->spt);
+            store(dst0 + (a + 2 * pair) * cc->spt);
           } else {
-            for (uint32_t aa = 0; aa < n_ant; aa++) store(dst0 + aa * c->spt);
+            for (uint32_t aa = 0; aa < n_ant; aa++) store(dst0 + aa * cc->spt);
           }
         },
         [&](int a, int tt, int off, s16x2 y0, s16x2 y1) {
@@ -1196,9 +1213,9 @@ __global__ void __launch_bounds__(128) MODOFDM_ATTR k_modofdm(const cfg_dev_t *_
             if (off + 2 * T - 2 >= N - CPMAX && tt + off >= N - cp) *(u32x2_t *)&d[ro - N] = v;
           };
           if constexpr (NA == 2) {
-            store(dst0 + (a + 2 * pair) * c->spt);
+            store(dst0 + (a + 2 * pair) * cc->spt);
           } else {
-            for (uint32_t aa = 0; aa < n_ant; aa++) store(dst0 + aa * c->spt);
+            for (uint32_t aa = 0; aa < n_ant; aa++) store(dst0 + aa * cc->spt);
           }
         },
         1, it);
