@@ -585,7 +585,8 @@ static __device__ void encode_codeword(const cfg_dev_t *__restrict__ c, uint32_t
   const cw_dev_t &cw = c->cw[cwi];
   const uint32_t tid = threadIdx.x, nth = blockDim.x, wave = tid >> 6, lane = tid & 63, nwaves = nth >> 6;
   const uint32_t sfi = DEBUG ? sf : (c->first_sf + (sf0 + sf) * c->sf_step) % 10;
-  const uint32_t C = cw.C, sw = cw.stream_words;
+  /* wave-uniform: SGPRs, so the per-block stream offsets (r 3 sw) are scalar arithmetic */
+  const uint32_t C = __builtin_amdgcn_readfirstlane(cw.C), sw = __builtin_amdgcn_readfirstlane(cw.stream_words);
   /* LDS carve-up.  Region A: TB || CRC (phases 0-2), the QPP-interleaved words (phase 3), one half
    * of the e words (phase 4).  Region B: the CRC byte tables (phases 0-1), then the constituent
    * streams (the QPP planes in the parity slots during phase 3a). */
@@ -891,6 +892,7 @@ static __device__ void encode_codeword(const cfg_dev_t *__restrict__ c, uint32_t
    * the whole codeword in one pass behind the tables (dbg.ebuf). */
   {
     const uint32_t lane32 = tid & 31;
+    const uint32_t sw3 = __builtin_amdgcn_readfirstlane(3 * sw);
     const uint32_t nt0 = __builtin_amdgcn_readfirstlane(cw.ntk[0]), nt1 = __builtin_amdgcn_readfirstlane(cw.ntk[1]);
     const uint32_t ND0 = __builtin_amdgcn_readfirstlane(cw.NDk[0]), ND1 = __builtin_amdgcn_readfirstlane(cw.NDk[1]);
     const uint32_t Nnn0 = __builtin_amdgcn_readfirstlane(cw.Nnnk[0]), Nnn1 = __builtin_amdgcn_readfirstlane(cw.Nnnk[1]);
@@ -925,11 +927,18 @@ static __device__ void encode_codeword(const cfg_dev_t *__restrict__ c, uint32_t
       __syncthreads();
       const uint32_t pb = pair0(rb0), pe = pair0(rb1), bit0 = 32 * w0;
       uint32_t nsrc = 1u << 5, ndst = 0;
+      /* plan rows of pair (ki, t0): a wave-uniform word offset (scalar) from the plan base, so the
+       * loads take an SGPR base and the lane offset, with no vector address arithmetic */
+      const uint32_t *rsrc0 = &cw.rm_src[0][0][0], *rdst0 = &cw.rm_dst[0][0][0];
+      auto row_of = [&](uint32_t ki, uint32_t t0) {
+        return __builtin_amdgcn_readfirstlane(ki * ((OAI4G_RM_TILES + 1) * 32) + t0 * 32);
+      };
       if (pb + wave < pe) {
         uint32_t ki, r, t0;
         decode(__builtin_amdgcn_readfirstlane(pb + wave), ki, r, t0);
-        nsrc = (&cw.rm_src[ki][t0][0])[lane];
-        ndst = (&cw.rm_dst[ki][t0][0])[lane];
+        const uint32_t ro = row_of(ki, t0);
+        nsrc = (rsrc0 + ro)[lane];
+        ndst = (rdst0 + ro)[lane];
       }
       for (uint32_t pw = pb + wave; pw < pe; pw += nwaves) {
         const uint32_t P = __builtin_amdgcn_readfirstlane(pw);
@@ -941,10 +950,11 @@ static __device__ void encode_codeword(const cfg_dev_t *__restrict__ c, uint32_t
           uint32_t k2, r2, t2;
           decode(P + nwaves, k2, r2, t2);
           (void)r2;
-          nsrc = (&cw.rm_src[k2][t2][0])[lane];
-          ndst = (&cw.rm_dst[k2][t2][0])[lane];
+          const uint32_t ro = row_of(k2, t2);
+          nsrc = (rsrc0 + ro)[lane];
+          ndst = (rdst0 + ro)[lane];
         }
-        const uint32_t *bb = strm + r * 3 * sw - 1;                           /* block streams - 1 word */
+        const uint32_t *bb = strm + __builtin_amdgcn_readfirstlane(r * sw3) - 1;   /* block streams - 1 word (scalar offset) */
         const uint32_t *wp = bb + ((src >> 5) & 0x7fffu);
         uint32_t y = __builtin_amdgcn_alignbit(wp[1], wp[0], src);            /* bits before 0 are NULLs */
         if (src & OAI4G_RM_SRC_LAST) {
