@@ -307,3 +307,16 @@ def test_generate_pilots_drop_in(gpu, N_RB, nid, n_ant, mode1):
 @pytest.mark.parametrize("mcs", [0, 3, 5, 7, 9, 12, 16, 20, 24, 27])
 def test_pipeline_every_block_count(gpu, mcs):
     _pipeline_check(gpu, "C2", 10, 0, 1, mcs=[mcs], TBS=None)
+
+
+def test_tx_batch_refuses_misaligned_iq(gpu):
+    """The 2048-point modulator stores sample pairs as 8-byte words: oai4g_tx_batch refuses an IQ
+    buffer that is not 8-byte aligned (returns -1 with a message) instead of faulting."""
+    pipe = gpu.TxPipeline(gpu.make_params("C3"), 1)
+    L = pipe.L
+    assert L.oai4g_tx_batch(pipe.cfg, 1, pipe.d_payload, pipe.d_work, pipe.d_iq + 4, None) == -1
+    assert b"8-byte aligned" in L.oai4g_last_error()
+    ms = (ctypes.c_float * 2)()
+    assert L.oai4g_tx_batch_timed(pipe.cfg, 1, pipe.d_payload, pipe.d_work, pipe.d_iq + 4, None, ms) == -1
+    pipe.run()   # the aligned buffer still works
+    pipe.sync()
