@@ -668,6 +668,15 @@ __device__ static const uint32_t *td_crc_tab(uint32_t *lds, uint32_t poly)
   return lds;
 }
 
+#ifndef TD16_WAVES
+#define TD16_WAVES 0   /* waves per SIMD asked of the compiler (0: its choice, 2 at <= 256 VGPRs) */
+#endif
+#if TD16_WAVES > 0
+#define TD16_ATTR __attribute__((amdgpu_waves_per_eu(TD16_WAVES, TD16_WAVES)))
+#else
+#define TD16_ATTR
+#endif
+
 /*
  * Batch decoder: blockIdx.x decodes blocks 8 blockIdx.x .. +7 (one 64-lane wave).
  * llr: [..][llr_stride] int16 (3K + 12 each), out: [..][out_stride] bytes, iters: [..].  Block cb
@@ -675,7 +684,7 @@ __device__ static const uint32_t *td_crc_tab(uint32_t *lds, uint32_t poly)
  * cg = c_per = 1, r0 = 0; the code blocks r0 .. r0 + cg - 1 of every transport block of a
  * [tb][C] batch otherwise (one launch per block size).
  */
-__global__ void __launch_bounds__(64) k_td16(int n_cb, uint32_t K, const int16_t *__restrict__ llr, size_t llr_stride,
+__global__ void __launch_bounds__(64) TD16_ATTR k_td16(int n_cb, uint32_t K, const int16_t *__restrict__ llr, size_t llr_stride,
                                              uint8_t *__restrict__ out, size_t out_stride, uint8_t *__restrict__ iters,
                                              uint32_t max_it, uint32_t crc_type, uint32_t F,
                                              const uint16_t *__restrict__ pi4, const uint16_t *__restrict__ pi5,
