@@ -12,9 +12,9 @@
  *   turbo_encoder          port orc_turbo_encode                 3gpplte_sse.c:380 (lte_interleaver.h blob missing)
  *   subblock_interleaving  ref  sub_block_interleaving_turbo     lte_rate_matching.c:51 (libref_rm.so)
  *   rate_matching          ref  lte_rate_matching_turbo          lte_rate_matching.c:464 (libref_rm.so)
- *   scrambling             ref  lte_gold_generic + the XOR loop  lte_gold.c:151 (libref_gold.so); the loop of
- *                               of dlsch_scrambling (port)       dlsch_scrambling.c:78-92 (asn1c headers)
- *   modulation             port orc_modulation                   dlsch_modulation.c:1181 (asn1c headers)
+ *   scrambling             ref  dlsch_scrambling                 dlsch_scrambling.c:51 (libref_mod.so, over
+ *                                                                lte_gold.c's lte_gold_generic, libref_gold.so)
+ *   modulation             ref  dlsch_modulation                 dlsch_modulation.c:1181 (libref_mod.so)
  *   ofdm_mod               ref  do_OFDM_mod x 2 slots            ofdm_mod.c:233 -> normal_prefix_mod :47 ->
  *                               (IDFT + CP + slot layout)        PHY_ofdm_mod :85 -> idft2048 (libref_ofdm.so,
  *                                                                libref_dfts.so)
@@ -53,6 +53,18 @@ static uint32_t (*ref_gold)(uint32_t *, uint32_t *, uint8_t);
 static int (*ref_seg)(uint8_t *, uint8_t **, unsigned, unsigned *, unsigned *, unsigned *, unsigned *, unsigned *,
                       unsigned *);
 static void (*ref_do_ofdm)(int32_t **, int32_t **, uint32_t, uint16_t, const int32_t *);
+/* oracle/ref_glue_mod.c over dlsch_modulation.c / dlsch_scrambling.c (libref_mod.so) */
+typedef struct {
+  const uint8_t *e;
+  int32_t G;
+  uint8_t mcs, mimo_mode, Nlayers, first_layer;
+  uint32_t rb_alloc[4];
+  uint16_t nb_rb, pmi_alloc;
+} ref_cw_t;
+static uint8_t *(*ref_harq_e)(int);
+static void (*ref_set_cw)(int, const ref_cw_t *, uint16_t, int16_t, int16_t);
+static void (*ref_scramble_cw)(int, const int32_t *, int, uint8_t, uint8_t);
+static int (*ref_modulate)(int32_t **, int16_t, uint32_t, const int32_t *, uint8_t, int);
 
 static double now(void)
 {
@@ -117,6 +129,8 @@ int main(int argc, char **argv)
   void *hg = ref_open(dir, "libref_gold.so", RTLD_NOW), *hs = ref_open(dir, "libref_seg.so", RTLD_NOW);
   /* RTLD_LAZY: ofdm_mod.c's LOG_D (logRecord) sits on the PMCH branch only (oracle/ref_glue_ofdm.c) */
   void *ho = ref_open(dir, "libref_ofdm.so", RTLD_LAZY);
+  /* RTLD_LAZY: logRecord (LOG_E / LOG_W) sits on dlsch_modulation's unsupported-mode branches only */
+  void *hm = ref_open(dir, "libref_mod.so", RTLD_LAZY);
   if (hc) {
     ref_crc24a = (uint32_t(*)(uint8_t *, uint32_t))dlsym(hc, "crc24a");
     ref_crcTableInit = (void (*)(void))dlsym(hc, "crcTableInit");
@@ -135,10 +149,22 @@ int main(int argc, char **argv)
     ref_seg = (int (*)(uint8_t *, uint8_t **, unsigned, unsigned *, unsigned *, unsigned *, unsigned *, unsigned *,
                        unsigned *))dlsym(hs, "lte_segmentation");
   if (ho) ref_do_ofdm = (void (*)(int32_t **, int32_t **, uint32_t, uint16_t, const int32_t *))dlsym(ho, "ref_glue_do_OFDM_mod");
-  const int use_ref[S_N] = {ref_crc24a != NULL, ref_seg != NULL, 0, ref_sbi != NULL, ref_rm != NULL, ref_gold != NULL,
-                            0, ref_do_ofdm != NULL};
+  if (hm) {
+    ref_harq_e = (uint8_t * (*)(int)) dlsym(hm, "ref_glue_harq_e");
+    ref_set_cw = (void (*)(int, const ref_cw_t *, uint16_t, int16_t, int16_t))dlsym(hm, "ref_glue_set_cw");
+    ref_scramble_cw = (void (*)(int, const int32_t *, int, uint8_t, uint8_t))dlsym(hm, "ref_glue_scramble_cw");
+    ref_modulate = (int (*)(int32_t **, int16_t, uint32_t, const int32_t *, uint8_t, int))dlsym(hm, "ref_glue_modulate");
+    if (!ref_harq_e || !ref_set_cw || !ref_scramble_cw || !ref_modulate) ref_modulate = NULL;
+  }
+  /* the reference modulation reads the e bits from its own HARQ structure, which the reference
+   * scrambling writes: both or neither */
+  const int ref_mod_ok = ref_modulate != NULL && n_ant <= 2;
+  const int use_ref[S_N] = {ref_crc24a != NULL, ref_seg != NULL, 0, ref_sbi != NULL, ref_rm != NULL,
+                            ref_mod_ok || ref_gold != NULL, ref_mod_ok, ref_do_ofdm != NULL};
   const int32_t geom[9] = {fp->N_RB_DL, fp->Ncp, fp->nb_antennas_tx, N, fp->log2_symbol_size, fp->nb_prefix_samples,
                            fp->nb_prefix_samples0, nsymb, spt};
+  const int32_t fmod[9] = {fp->N_RB_DL, fp->Ncp, fp->nb_antennas_tx, N, fp->first_carrier_offset, fp->nushift,
+                           fp->mode1_flag, fp->frame_type, fp->Nid_cell};
 
   int G[2] = {0, 0};
   uint8_t Qm[2];
@@ -160,6 +186,19 @@ int main(int argc, char **argv)
     pay[cw] = aligned_alloc(64, abytes);
     a[cw] = aligned_alloc(64, abytes);
     e[cw] = aligned_alloc(64, (size_t)((1 + (G[cw] >> 5)) * 32 + 128));
+    if (cw < cfg.n_cw && ref_mod_ok) {
+      /* rate matching writes into the reference HARQ structure's e, as dlsch_encoding does */
+      free(e[cw]);
+      e[cw] = ref_harq_e(cw);
+      ref_cw_t rc;
+      memset(&rc, 0, sizeof(rc));
+      rc.mcs = cfg.mcs[cw];
+      rc.mimo_mode = cfg.mimo_mode;
+      rc.Nlayers = 1;
+      memcpy(rc.rb_alloc, cfg.rb_alloc, sizeof(rc.rb_alloc));
+      rc.nb_rb = cfg.nb_rb;
+      ref_set_cw(cw, &rc, cfg.rnti, cfg.sqrt_rho_a, cfg.sqrt_rho_b);
+    }
     for (size_t i = 0; i < abytes; i++) pay[cw][i] = (uint8_t)splitmix64(&seed);
   }
   static uint8_t cbuf[16][8 + 3 + 768];
@@ -211,27 +250,35 @@ int main(int argc, char **argv)
                                                 cfg.Mdlharq, cfg.Kmimo, 0, Qm[cw], 1, (uint8_t)r);
         t1 = now(); st[S_RM] += t1 - t0;
       }
-      /* dlsch_scrambling (dlsch_scrambling.c:51-97) around the reference's lte_gold_generic */
+      /* dlsch_scrambling (dlsch_scrambling.c:51-97; dlsim passes q = 0, Ns = 2 subframe) */
       t0 = now();
-      uint32_t x1 = 0, x2 = ((uint32_t)cfg.rnti << 14) + ((uint32_t)cfg.subframe << 9) + fp->Nid_cell;
-      uint32_t (*gold)(uint32_t *, uint32_t *, uint8_t) = use_ref[S_SCR] ? ref_gold : orc_gold_generic;
-      uint32_t s = gold(&x1, &x2, 1);
-      uint8_t *ep = e[cw];
-      for (int i = 0, k = 0; i < 1 + (G[cw] >> 5); i++) {
-        for (int j = 0; j < 32; j++, k++) ep[k] = (ep[k] & 1) ^ ((s >> j) & 1);
-        s = gold(&x1, &x2, 0);
+      if (ref_mod_ok) {
+        ref_scramble_cw(cw, fmod, G[cw], 0, (uint8_t)(2 * cfg.subframe));
+      } else {       /* the loop restated around the reference's (or the oracle's) Gold generator */
+        uint32_t x1 = 0, x2 = ((uint32_t)cfg.rnti << 14) + ((uint32_t)cfg.subframe << 9) + fp->Nid_cell;
+        uint32_t (*gold)(uint32_t *, uint32_t *, uint8_t) = ref_gold ? ref_gold : orc_gold_generic;
+        uint32_t s = gold(&x1, &x2, 1);
+        uint8_t *ep = e[cw];
+        for (int i = 0, k = 0; i < 1 + (G[cw] >> 5); i++) {
+          for (int j = 0; j < 32; j++, k++) ep[k] = (ep[k] & 1) ^ ((s >> j) & 1);
+          s = gold(&x1, &x2, 0);
+        }
       }
       t1 = now(); st[S_SCR] += t1 - t0;
     }
     /* dlsch_modulation into the frame grid (dlsim zeroes txdataF before its timer, dlsim.c:2161) */
     for (int aa = 0; aa < n_ant; aa++) memset(txF[aa] + (size_t)cfg.subframe * nsymb * N, 0, (size_t)nsymb * N * 4);
     t0 = now();
-    orc_cw_t c0 = {e[0], cfg.mcs[0], cfg.mimo_mode, 1, {0}}, c1 = {e[1], cfg.mcs[1], cfg.mimo_mode, 1, {0}};
-    memcpy(c0.rb_alloc, cfg.rb_alloc, sizeof(c0.rb_alloc));
-    memcpy(c1.rb_alloc, cfg.rb_alloc, sizeof(c1.rb_alloc));
-    if (orc_modulation(txF, cfg.amp, cfg.subframe, fp, cfg.num_pdcch_symbols, &c0, cfg.n_cw > 1 ? &c1 : NULL,
-                       cfg.sqrt_rho_a, cfg.sqrt_rho_b) < 0)
-      return 3;
+    if (ref_mod_ok) {
+      if (ref_modulate(txF, cfg.amp, cfg.subframe, fmod, cfg.num_pdcch_symbols, cfg.n_cw) < 0) return 3;
+    } else {
+      orc_cw_t c0 = {e[0], cfg.mcs[0], cfg.mimo_mode, 1, {0}}, c1 = {e[1], cfg.mcs[1], cfg.mimo_mode, 1, {0}};
+      memcpy(c0.rb_alloc, cfg.rb_alloc, sizeof(c0.rb_alloc));
+      memcpy(c1.rb_alloc, cfg.rb_alloc, sizeof(c1.rb_alloc));
+      if (orc_modulation(txF, cfg.amp, cfg.subframe, fp, cfg.num_pdcch_symbols, &c0, cfg.n_cw > 1 ? &c1 : NULL,
+                         cfg.sqrt_rho_a, cfg.sqrt_rho_b) < 0)
+        return 3;
+    }
     t1 = now(); st[S_MOD] += t1 - t0;
     /* do_OFDM_mod_l x 2 slots (dlsim.c:2680-2699) -> normal_prefix_mod -> PHY_ofdm_mod, normal CP */
     t0 = now();
@@ -257,7 +304,7 @@ int main(int argc, char **argv)
   double tot = 0, port = 0;
   for (int k = 0; k < S_N; k++) {
     tot += st[k];
-    if (!use_ref[k] || k == S_SCR) port += st[k];      /* the scrambling loop around the ref generator is a port */
+    if (!use_ref[k] || (k == S_SCR && !ref_mod_ok)) port += st[k];   /* a restated loop around the ref generator is a port */
   }
   printf("{\"subframes\": %ld, \"wall_s\": %.6f, \"stage_s\": %.6f, \"rate\": %.3f, \"validated\": true, "
          "\"port_share\": %.4f, \"stage_us\": {",
@@ -266,7 +313,7 @@ int main(int argc, char **argv)
   printf("}, \"impl\": {");
   for (int k = 0; k < S_N; k++)
     printf("%s\"%s\": \"%s\"", k ? ", " : "", S_NAME[k],
-           use_ref[k] ? (k == S_SCR ? "reference generator + port loop" : "reference") : "port");
+           use_ref[k] ? (k == S_SCR && !ref_mod_ok ? "reference generator + port loop" : "reference") : "port");
   printf("}}\n");
   return 0;
 }

@@ -63,6 +63,10 @@ def main():
         for slot in SC.DO_OFDM_SLOTS:
             out["do_ofdm"]["%d,%d,%d,%d" % (n_rb, ncp, na, slot)] = SC.digest(SC.run_do_ofdm(ref, fp, 3, slot))
     out["bench_C3"] = {str(i): SC.bench_c3_digests(ref, O, i) for i in SC.BENCH_C3_SAMPLES}
+    # the chain behind the bench digests: e bits from the oracle (RM / Gold pinned to the reference),
+    # then the reference's dlsch_modulation.c (when built) and do_OFDM_mod
+    out["bench_C3_chain"] = ("e (oracle, RM/Gold reference-pinned) -> dlsch_modulation.c -> do_OFDM_mod (ofdm_mod.c)"
+                             if "mod" in ref else "oracle grid -> do_OFDM_mod (ofdm_mod.c)")
     with open(os.path.join(HERE, "seg_ofdm_ref.json"), "w") as f:
         json.dump(out, f, indent=0, sort_keys=True)
     np.savez_compressed(os.path.join(HERE, "seg_ofdm_ref.npz"), seg_B=Bs.astype(np.int32),

@@ -918,3 +918,95 @@ def frame_geometry(fp):
     """The ofdm_mod.c glue's geometry vector from an OrcFrame / FrameParms."""
     return np.array([fp.N_RB_DL, fp.Ncp, fp.nb_antennas_tx, fp.ofdm_symbol_size, fp.log2_symbol_size,
                      fp.nb_prefix_samples, fp.nb_prefix_samples0, fp.symbols_per_tti, fp.samples_per_tti], np.int32)
+
+
+# ---- dlsch_modulation.c / dlsch_scrambling.c compiled unmodified (oracle/_ref/libref_mod.so) ----
+REF_MOD_SO = os.path.join(ORACLE_DIR, "_ref", "libref_mod.so")
+_refmod = None
+
+
+class RefCw(ctypes.Structure):
+    """ref_cw_t of oracle/ref_glue_mod.c"""
+    _fields_ = [("e", VP), ("G", ctypes.c_int32), ("mcs", U8), ("mimo_mode", U8), ("Nlayers", U8),
+                ("first_layer", U8), ("rb_alloc", U32 * 4), ("nb_rb", U16), ("pmi_alloc", U16)]
+
+
+def ref_mod():
+    """dlsch_modulation.c + dlsch_scrambling.c compiled unmodified (+ the ctypes glue ref_glue_mod.c),
+    or None when they were not built here."""
+    global _refmod
+    if _refmod is None:
+        if not os.path.exists(REF_MOD_SO) or ref_gold() is None:
+            return None
+        # RTLD_LAZY: logRecord (LOG_E / LOG_W on the unsupported-mode branches) stays unbound
+        L = ctypes.CDLL(REF_MOD_SO, mode=os.RTLD_LAZY | os.RTLD_LOCAL)
+        L.ref_glue_dlsch_modulation.restype = ctypes.c_int
+        L.ref_glue_dlsch_modulation.argtypes = [ctypes.POINTER(VP), ctypes.c_int16, U32, VP, U8,
+                                                ctypes.POINTER(RefCw), ctypes.POINTER(RefCw), ctypes.c_int16,
+                                                ctypes.c_int16]
+        L.ref_glue_dlsch_scrambling.argtypes = [VP, ctypes.c_int, U16, U16, U8, U8]
+        L.ref_glue_qam_tables.argtypes = [VP, VP]
+        _refmod = L
+    return _refmod
+
+
+def mod_frame_words(fp):
+    """ref_glue_mod.c's frame vector from an OrcFrame"""
+    return np.array([fp.N_RB_DL, fp.Ncp, fp.nb_antennas_tx, fp.ofdm_symbol_size, fp.first_carrier_offset,
+                     fp.nushift, fp.mode1_flag, fp.frame_type, fp.Nid_cell], dtype=np.int32)
+
+
+def _grids(fp):
+    n = 10 * fp.symbols_per_tti * fp.ofdm_symbol_size
+    grids = [np.zeros(n, dtype=np.int32) for _ in range(fp.nb_antennas_tx)]
+    ptrs = (VP * max(2, len(grids)))(*([g.ctypes.data for g in grids] + [None] * max(0, 2 - len(grids))))
+    return grids, ptrs
+
+
+def ref_modulation(fp, amp, subframe, num_pdcch, cws, sqrt_rho_a=8192, sqrt_rho_b=8192):
+    """The reference's dlsch_modulation over frame grids: (return value, [grid per TX antenna]).
+    cws: 1 or 2 dicts {e (uint8 0/1, >= the bits consumed), mcs, mimo_mode, rb_alloc (4 words)}."""
+    grids, ptrs = _grids(fp)
+    keep = []
+    rc = []
+    for cw in cws:
+        e = np.ascontiguousarray(cw["e"][:14 * 1200 * 6], dtype=np.uint8)   # MAX_NUM_CHANNEL_BITS
+        keep.append(e)
+        ra = cw["rb_alloc"]
+        c = RefCw(e=e.ctypes.data, G=len(e), mcs=cw["mcs"], mimo_mode=cw["mimo_mode"], Nlayers=cw.get("Nlayers", 1),
+                  first_layer=0, nb_rb=sum(bin(int(w)).count("1") for w in ra), pmi_alloc=0)
+        for i in range(4):
+            c.rb_alloc[i] = int(ra[i])
+        rc.append(c)
+    f = mod_frame_words(fp)
+    ret = ref_mod().ref_glue_dlsch_modulation(ptrs, amp, subframe, f.ctypes.data, num_pdcch, ctypes.byref(rc[0]),
+                                              ctypes.byref(rc[1]) if len(rc) > 1 else None, sqrt_rho_a,
+                                              sqrt_rho_b)
+    return ret, grids
+
+
+def orc_modulation_grids(fp, amp, subframe, num_pdcch, cws, sqrt_rho_a=8192, sqrt_rho_b=8192):
+    """The oracle's orc_modulation with the same arguments as ref_modulation."""
+    grids, ptrs = _grids(fp)
+    keep = []
+    oc = []
+    for cw in cws:
+        e = np.ascontiguousarray(cw["e"], dtype=np.uint8)
+        keep.append(e)
+        c = OrcCw(e=e.ctypes.data, mcs=cw["mcs"], mimo_mode=cw["mimo_mode"], Nlayers=cw.get("Nlayers", 1))
+        for i in range(4):
+            c.rb_alloc[i] = int(cw["rb_alloc"][i])
+        oc.append(c)
+    ret = orc().orc_modulation(ptrs, amp, subframe, ctypes.byref(fp), num_pdcch, ctypes.byref(oc[0]),
+                               ctypes.byref(oc[1]) if len(oc) > 1 else None, sqrt_rho_a, sqrt_rho_b)
+    return ret, grids
+
+
+def ref_scrambling(e, G, rnti, Nid_cell, q, Ns):
+    """The reference's dlsch_scrambling of e[0 .. G) (returns the 32 (1 + G / 32) entries it writes)."""
+    n = 32 * (1 + (G >> 5))
+    buf = np.zeros(n, dtype=np.uint8)
+    src = np.asarray(e, dtype=np.uint8)
+    buf[:min(n, len(src))] = src[:n]
+    ref_mod().ref_glue_dlsch_scrambling(buf.ctypes.data, G, rnti, Nid_cell, q, Ns)
+    return buf

@@ -148,17 +148,26 @@ def bench_c3_params():
 
 
 def bench_c3_digests(impl, O, i):
-    """Per-antenna digests of subframe i of the C3 bench batch: the oracle's grid of that subframe
-    through impl["do_ofdm"] for slots 14 and 15 of a frame grid (subframe 7)."""
+    """Per-antenna digests of subframe i of the C3 bench batch: the scrambled e bits of that
+    subframe (the oracle's encoder + rate matching + scrambling, RM / Gold pinned to the reference,
+    tests/golden/rm_ref.json) through impl["mod"] (dlsch_modulation, when impl has it; else the
+    oracle's grid) and impl["do_ofdm"] for slots 14 and 15 of a frame grid (subframe 7)."""
     p = bench_c3_params()
     pay = bench_payload(BENCH_SEED, BENCH_N_SF, p.n_cw, p.payload_stride)[i]
     cfg = O.tx_cfg_from_params(p, 7)
-    _, txF, _ = O.tx_subframe(cfg, [pay[cw] for cw in range(p.n_cw)])
+    _, txF, es = O.tx_subframe(cfg, [pay[cw] for cw in range(p.n_cw)], want_e=True)
     fp = cfg.fp
     N, spt, na = fp.ofdm_symbol_size, fp.samples_per_tti, fp.nb_antennas_tx
-    grids = [np.zeros(10 * 14 * N, np.int32) for _ in range(na)]
-    for a in range(na):
-        grids[a][7 * 14 * N:8 * 14 * N] = txF[a]
+    if "mod" in impl:
+        assert not cfg.with_crs                  # the bench batch is the PDSCH alone
+        cws = [dict(e=es[cw], mcs=cfg.mcs[cw], mimo_mode=cfg.mimo_mode, rb_alloc=list(cfg.rb_alloc))
+               for cw in range(cfg.n_cw)]
+        ret, grids = impl["mod"](fp, cfg.amp, 7, cfg.num_pdcch_symbols, cws, cfg.sqrt_rho_a, cfg.sqrt_rho_b)
+        assert ret > 0
+    else:
+        grids = [np.zeros(10 * 14 * N, np.int32) for _ in range(na)]
+        for a in range(na):
+            grids[a][7 * 14 * N:8 * 14 * N] = txF[a]
     outs = [np.zeros(10 * spt + 64, np.int32) for _ in range(na)]
     for slot in (14, 15):
         frame = impl["do_ofdm"](grids, outs, 0, slot, fp).reshape(na, -1)
@@ -193,7 +202,10 @@ def ref_impl(O):
         O.ref_ofdm().ref_glue_do_OFDM_mod(_ptrs(gs), _ptrs(os_), frame, slot, O.P(O.frame_geometry(fp)))
         return np.concatenate(os_)
 
-    return {"seg": seg, "ofdm_mod": ofdm_mod, "npm": npm, "do_ofdm": do_ofdm}
+    impl = {"seg": seg, "ofdm_mod": ofdm_mod, "npm": npm, "do_ofdm": do_ofdm}
+    if O.ref_mod() is not None:                  # dlsch_modulation.c (oracle/_ref/libref_mod.so)
+        impl["mod"] = O.ref_modulation
+    return impl
 
 
 def oracle_impl(O):
