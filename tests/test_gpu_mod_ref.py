@@ -25,6 +25,8 @@ def _dlsch(gpu, c, cw, rnti=0):
         h.rb_alloc[i] = c["rb_alloc"][i]
     h.nb_rb = sum(bin(int(w)).count("1") for w in c["rb_alloc"])
     h.Nl = 1
+    h.Nlayers = 1
+    h.TBS = 1024         # the drop-in derives a coding geometry it does not use for the grid
     dl.d.rnti = rnti
     return dl
 
