@@ -153,14 +153,15 @@ def cpu_baseline(name, seconds, subframe, full=False):
     """The CPU transmit path on the host cores over a bounded sample of the same workload, one core
     and then every core of this process's share (independent processes, as N dlsim instances would
     run).  PDSCH configurations run oracle/cpu_baseline: the reference's own crc24a,
-    lte_segmentation, sub_block_interleaving_turbo, lte_rate_matching_turbo, lte_gold_generic and
-    do_OFDM_mod (-> normal_prefix_mod -> PHY_ofdm_mod -> idft2048) compiled unmodified
-    (oracle/_ref), the oracle's restatement for the stages whose reference TU does not build here
-    (turbo encoder, the scrambling loop, modulation); its first subframe is checked bit-exactly
-    against the oracle's whole chain.  The rate is over the stages' summed time, as dlsim's
-    phy_proc_tx timer covers them (DCI / pilots excluded).  `port_share` is the fraction of that
-    time spent in ported stages: the reference's SSE modulation / turbo encoder may run faster than
-    the scalar ports, so the CPU rate is a lower bound on the reference's by up to that share.
+    lte_segmentation, sub_block_interleaving_turbo, lte_rate_matching_turbo, dlsch_scrambling,
+    dlsch_modulation (1-2 TX ports) and do_OFDM_mod (-> normal_prefix_mod -> PHY_ofdm_mod ->
+    idft2048) compiled unmodified (oracle/_ref), the oracle's restatement where the reference TU
+    does not build here (the turbo encoder; the 4-port modulation of C4, which the reference lacks);
+    its first subframe is checked bit-exactly against the oracle's whole chain.  The rate is over
+    the stages' summed time, as dlsim's phy_proc_tx timer covers them (DCI / pilots excluded).
+    `port_share` is the fraction of that time spent in ported stages: the reference's SSE turbo
+    encoder may run faster than the scalar port, so the CPU rate is a lower bound on the
+    reference's by up to that share.
     --full-grid keeps the oracle port over subframes 0..9 with CRS + PCFICH/PDCCH."""
     import openair4g_amd as oai
     cores = host_cores()
