@@ -57,4 +57,8 @@ def test_cpu_baseline_fields():
         assert cb["kind"] == "reference+port"
         assert cb["stage_impl"]["rate_matching"] == "reference" and cb["stage_impl"]["ofdm_mod"] == "reference"
         assert cb["stage_impl"]["segmentation"] == "reference"
+        if os.path.exists(os.path.join(ROOT, "oracle", "_ref", "libref_mod.so")):
+            # dlsch_modulation.c / dlsch_scrambling.c: only the turbo encoder stays a port
+            assert cb["stage_impl"]["modulation"] == "reference" and cb["stage_impl"]["scrambling"] == "reference"
+            assert cb["stage_impl"]["turbo_encoder"] == "port" and cb["port_share"] < 0.5
         assert 0 < cb["port_share"] < 1
