@@ -540,29 +540,50 @@ static __device__ __forceinline__ uint32_t xor_lane(uint32_t x)
 
 /* 32x32 bit transpose across the 32 lanes of a half-wave: lane c ends with bit i = bit c of
  * lane i's input.  Branch-free butterfly: stage j exchanges the j-bit blocks that differ between
- * partners l and l^j; the partner's word is rotated into place (right by j in the upper lane,
- * left by j in the lower) and merged with a bit-field insert whose mask flips with the lane. */
+ * partners l and l^j.  The byte-granular stages (16, 8) are one v_perm each: the lane's selector
+ * (sel[0] / sel[1], per lane) takes its kept blocks from x and the partner's from p.  The finer
+ * stages rotate the partner's word into place (right by j in the upper lane, left by j in the
+ * lower) and merge with a bit-field mux whose mask flips with the lane. */
+struct tp_lane_t {
+  uint32_t sel16, sel8;        /* v_perm selectors of stages 16 and 8 */
+  uint32_t rot[3], mm[3];      /* stages 4, 2, 1: rotate amount and kept-bit mask */
+};
+
+static __device__ __forceinline__ tp_lane_t tp_lane(uint32_t lane32)
+{
+  tp_lane_t t;
+  /* v_perm bytes 0-3 = second operand (x), 4-7 = first (partner p) */
+  t.sel16 = (lane32 & 16u) ? 0x03020706u : 0x05040100u;   /* hi: [p2 p3 x2 x3], lo: [x0 x1 p0 p1] */
+  t.sel8 = (lane32 & 8u) ? 0x03070105u : 0x06020400u;     /* hi: [p1 x1 p3 x3], lo: [x0 p0 x2 p2] */
+  const uint32_t M[3] = {0x0f0f0f0fu, 0x33333333u, 0x55555555u};
+#pragma unroll
+  for (int k = 0; k < 3; k++) {
+    const uint32_t J = 4u >> k;
+    const bool hi = (lane32 & J) != 0;
+    t.rot[k] = hi ? J : 32u - J;
+    t.mm[k] = hi ? ~M[k] : M[k];
+  }
+  return t;
+}
+
 template <int K = 0>
-static __device__ __forceinline__ uint32_t transpose32_t(uint32_t x, uint32_t lane32)
+static __device__ __forceinline__ uint32_t transpose32_t(uint32_t x, const tp_lane_t &t)
 {
   if constexpr (K == 5) {
     return x;
+  } else if constexpr (K < 2) {
+    const uint32_t p = xor_lane<(16u >> K)>(x);
+    return transpose32_t<K + 1>(__builtin_amdgcn_perm(p, x, K == 0 ? t.sel16 : t.sel8), t);
   } else {
-    constexpr uint32_t J = 16u >> K;
-    constexpr uint32_t M = K == 0 ? 0x0000ffffu : K == 1 ? 0x00ff00ffu : K == 2 ? 0x0f0f0f0fu : K == 3 ? 0x33333333u
-                                                                                                 : 0x55555555u;
-    const bool hi = (lane32 & J) != 0;
-    const uint32_t p = xor_lane<J>(x);
-    const uint32_t sh = __builtin_amdgcn_alignbit(p, p, hi ? J : 32u - J);
-    const uint32_t mm = hi ? ~M : M;
+    const uint32_t p = xor_lane<(16u >> K)>(x);
+    const uint32_t sh = __builtin_amdgcn_alignbit(p, p, t.rot[K - 2]);
     /* (x & mm) | (sh & ~mm) as one fast-rate v_bitop3 mux (0xe4: c ? a : b); the compiler's
      * v_and + v_and_or pair has a slow-rate op */
     uint32_t r;
-    asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0xe4" : "=v"(r) : "v"(x), "v"(sh), "v"(mm));
-    return transpose32_t<K + 1>(r, lane32);
+    asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0xe4" : "=v"(r) : "v"(x), "v"(sh), "v"(t.mm[K - 2]));
+    return transpose32_t<K + 1>(r, t);
   }
 }
-static __device__ __forceinline__ uint32_t transpose32(uint32_t x, uint32_t lane32) { return transpose32_t<0>(x, lane32); }
 
 /* OR 32 bits into an LDS bit array at bit offset `bit` (LDS atomics: tiles of neighbouring
  * columns share boundary words) */
@@ -574,6 +595,16 @@ static __device__ __forceinline__ void or_bits(uint32_t *w, uint32_t bit, uint32
   if (sh && (v >> (32 - sh))) atomicOr(&w[wi + 1], v >> (32 - sh));
 }
 
+/* the same without the tests: both words always (an OR of zero into the second is harmless; the
+ * caller guarantees word bit / 32 + 1 is inside the array), the pair from one 64-bit shift */
+static __device__ __forceinline__ void or_bits2(uint32_t *w, uint32_t bit, uint32_t v)
+{
+  const uint64_t s = (uint64_t)v << (bit & 31u);
+  uint32_t *p = w + (bit >> 5);
+  atomicOr(p, (uint32_t)s);
+  atomicOr(p + 1, (uint32_t)(s >> 32));
+}
+
 /* ---------------------------------------------------------------------------------------
  * The fused encoder.
  * ------------------------------------------------------------------------------------- */
@@ -583,7 +614,9 @@ static __device__ void encode_codeword(const cfg_dev_t *__restrict__ c, uint32_t
                                        enc_debug_t dbg, uint32_t *lds_base, int stop_phase = 99, uint32_t sf0 = 0)
 {
   const cw_dev_t &cw = c->cw[cwi];
-  const uint32_t tid = threadIdx.x, nth = blockDim.x, wave = tid >> 6, lane = tid & 63, nwaves = nth >> 6;
+  const uint32_t tid = threadIdx.x, nth = blockDim.x, lane = tid & 63, nwaves = nth >> 6;
+  /* the wave index as an SGPR: every loop over waves (phases 3b, 4) is then a scalar loop */
+  const uint32_t wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const uint32_t sfi = DEBUG ? sf : (c->first_sf + (sf0 + sf) * c->sf_step) % 10;
   /* wave-uniform: SGPRs, so the per-block stream offsets (r 3 sw) are scalar arithmetic */
   const uint32_t C = __builtin_amdgcn_readfirstlane(cw.C), sw = __builtin_amdgcn_readfirstlane(cw.stream_words);
@@ -872,6 +905,9 @@ static __device__ void encode_codeword(const cfg_dev_t *__restrict__ c, uint32_t
       blk[s * sw + w0] |= t4 << off;
       if (off > 28) blk[s * sw + (w0 + 1)] |= t4 >> (32 - off);
     }
+    /* phase 4's RM_SRC_LAST lane reads y^(2)_0 = d^(2)_0 at stream-2 position Kpi - ND = K + 4
+     * when ND = 0: the reference's own d[3D + 2] = d[2] copy (lte_rate_matching.c:74-75) in stream form */
+    if (cw.ND[r] == 0) blk[2 * sw + ((K + 4) >> 5)] |= (blk[2 * sw] & 1u) << ((K + 4) & 31u);
   }
   __syncthreads();
 
@@ -891,15 +927,16 @@ static __device__ void encode_codeword(const cfg_dev_t *__restrict__ c, uint32_t
    * three streams and the output are never resident in full together.  The debug kernel stages
    * the whole codeword in one pass behind the tables (dbg.ebuf). */
   {
-    const uint32_t lane32 = tid & 31;
+    const tp_lane_t tpl = tp_lane(tid & 31);
     const uint32_t sw3 = __builtin_amdgcn_readfirstlane(3 * sw);
     const uint32_t nt0 = __builtin_amdgcn_readfirstlane(cw.ntk[0]), nt1 = __builtin_amdgcn_readfirstlane(cw.ntk[1]);
     const uint32_t ND0 = __builtin_amdgcn_readfirstlane(cw.NDk[0]), ND1 = __builtin_amdgcn_readfirstlane(cw.NDk[1]);
     const uint32_t Nnn0 = __builtin_amdgcn_readfirstlane(cw.Nnnk[0]), Nnn1 = __builtin_amdgcn_readfirstlane(cw.Nnnk[1]);
     const uint32_t es = __builtin_amdgcn_readfirstlane(cw.esplit[sfi]);
     const uint32_t Elo = __builtin_amdgcn_readfirstlane(cw.E[sfi][0]), Ehi = __builtin_amdgcn_readfirstlane(cw.E[sfi][C - 1]);
+    const uint32_t wrapt0 = __builtin_amdgcn_readfirstlane(cw.rm_wrapt[0]), wrapt1 = __builtin_amdgcn_readfirstlane(cw.rm_wrapt[1]);
     /* no repetition (E <= Nnn for every block): a run lands once at most */
-    const bool once = Ehi <= min(Nnn0, Nnn1) && Elo <= min(Nnn0, Nnn1);
+    const bool once = Ehi <= min(Nnn0, Nnn1) && Elo <= min(Nnn0, Nnn1) && wrapt0 != ~1u && wrapt1 != ~1u;
     const uint32_t pp0 = (nt0 + 1) >> 1, pp1 = (nt1 + 1) >> 1;            /* tile pairs per block */
     const uint32_t psplit = n0 * pp0;
     const uint32_t pm0 = ((1u << 20) + pp0 - 1) / pp0, pm1 = ((1u << 20) + pp1 - 1) / pp1;
@@ -935,16 +972,14 @@ static __device__ void encode_codeword(const cfg_dev_t *__restrict__ c, uint32_t
       };
       if (pb + wave < pe) {
         uint32_t ki, r, t0;
-        decode(__builtin_amdgcn_readfirstlane(pb + wave), ki, r, t0);
+        decode(pb + wave, ki, r, t0);
         const uint32_t ro = row_of(ki, t0);
         nsrc = (rsrc0 + ro)[lane];
         ndst = (rdst0 + ro)[lane];
       }
-      for (uint32_t pw = pb + wave; pw < pe; pw += nwaves) {
-        const uint32_t P = __builtin_amdgcn_readfirstlane(pw);
+      for (uint32_t P = pb + wave; P < pe; P += nwaves) {    /* scalar loop: wave is an SGPR */
         uint32_t ki, r, t0;
         decode(P, ki, r, t0);
-        const uint32_t ND = ki ? ND1 : ND0;
         const uint32_t src = nsrc, dst = ndst;
         if (P + nwaves < pe) {
           uint32_t k2, r2, t2;
@@ -957,29 +992,37 @@ static __device__ void encode_codeword(const cfg_dev_t *__restrict__ c, uint32_t
         const uint32_t *bb = strm + __builtin_amdgcn_readfirstlane(r * sw3) - 1;   /* block streams - 1 word (scalar offset) */
         const uint32_t *wp = bb + ((src >> 5) & 0x7fffu);
         uint32_t y = __builtin_amdgcn_alignbit(wp[1], wp[0], src);            /* bits before 0 are NULLs */
-        if (src & OAI4G_RM_SRC_LAST) {
-          y &= 0x7fffffffu;                       /* j = Kpi-1 reads y^(2)_0: NULL if ND > 0 */
-          if (ND == 0) y |= (bb[1 + 2 * sw] & 1u) << 31;
-        }
-        y = transpose32(y, lane32);
-        const uint32_t m = (dst >> 21) & 63u;
-        if (m) {
-          const uint32_t z = (dst >> 16) & 31u, o = dst & 0xffffu;
-          y = (y >> z) & (0xffffffffu >> (32 - m));
-          const bool eh = r >= es;
-          const uint32_t E = eh ? Ehi : Elo, ro = ro_of(r) - bit0;           /* relative to the staged words */
-          if (once && !(dst & OAI4G_RM_DST_WRAP)) {
-            if (o < E) or_bits(ebuf, ro + o, y & (0xffffffffu >> (32 - min(m, E - o))));
-          } else {
-            /* the run may straddle the wrap back to k0c; E > Nnn repeats the buffer */
-            const uint32_t Nnn = ki ? Nnn1 : Nnn0, ma = min(m, Nnn - o);
-            for (uint32_t part = 0; part < 2; part++) {
-              const uint32_t len = part ? m - ma : ma, os = part ? 0u : o;
-              const uint32_t v = part ? (ma < 32 ? y >> ma : 0u) : (ma < 32 ? y & ((1u << ma) - 1u) : y);
-              for (uint32_t x = os; len && x < E; x += Nnn) {                     /* repetition rounds */
-                const uint32_t l = min(len, E - x);
-                or_bits(ebuf, ro + x, v & (0xffffffffu >> (32 - l)));
-              }
+        /* the RM_SRC_LAST lane (row R - 1 of y2, j = Kpi - 1 reads y^(2)_0 at bit 31) needs no
+         * test: its bit 31 is stream-2 position Kpi - ND, which holds d^(2)_0 when ND = 0 (copied
+         * there with the tail bits) and is past the run (a NULL, m excludes it) when ND > 0 */
+        y = transpose32_t<0>(y, tpl);
+        y >>= (dst >> 16) & 31u;                                             /* leading NULLs z */
+        const uint32_t o = dst & 0xffffu, m = __builtin_amdgcn_ubfe(dst, 21, 6);
+        const uint32_t E = r >= es ? Ehi : Elo, ro = ro_of(r) - bit0;        /* relative to the staged words */
+        if (once) {
+          /* no repetition (E <= Nnn): the run's part below E, then (the one run that straddles the
+           * circular buffer's end: a block's wrap tile, scalar test first) its wrapped part at 0 */
+          const int l = min((int)m, (int)E - (int)o);
+          if (l > 0) or_bits2(ebuf, ro + o, y & (0xffffffffu >> (32 - l)));
+          const uint32_t wt = ki ? wrapt1 : wrapt0;
+          if (t0 == wt || t0 + 1 == wt) {
+            asm volatile("" ::: "memory");   /* keeps the lane test below behind the scalar one */
+            if (dst & OAI4G_RM_DST_WRAP) {
+            const uint32_t Nnn = ki ? Nnn1 : Nnn0, ma = Nnn - o;                /* 1 .. m - 1 */
+            const uint32_t l2 = min(m - ma, E);
+            or_bits2(ebuf, ro, (y >> ma) & (0xffffffffu >> (32 - l2)));
+            }
+          }
+        } else if (m) {
+          y &= 0xffffffffu >> (32 - m);
+          /* the run may straddle the wrap back to k0c; E > Nnn repeats the buffer */
+          const uint32_t Nnn = ki ? Nnn1 : Nnn0, ma = min(m, Nnn - o);
+          for (uint32_t part = 0; part < 2; part++) {
+            const uint32_t len = part ? m - ma : ma, os = part ? 0u : o;
+            const uint32_t v = part ? (ma < 32 ? y >> ma : 0u) : (ma < 32 ? y & ((1u << ma) - 1u) : y);
+            for (uint32_t x = os; len && x < E; x += Nnn) {                     /* repetition rounds */
+              const uint32_t l = min(len, E - x);
+              or_bits(ebuf, ro + x, v & (0xffffffffu >> (32 - l)));
             }
           }
         }

@@ -711,6 +711,7 @@ static void rm_plan(cw_dev_t &c, int ki)
   const uint32_t R = c.Rk[ki], ND = c.NDk[ki], Ncb = c.Ncbk[ki], Nnn = c.Nnnk[ki], k0c = c.k0ck[ki];
   const uint32_t tz = c.t0k[ki], nt = c.ntk[ki], sw = c.stream_words;
   memset(c.rm_dst[ki], 0, sizeof(c.rm_dst[ki]));
+  c.rm_wrapt[ki] = ~0u;
   for (uint32_t t = 0; t <= OAI4G_RM_TILES; t++)
     for (uint32_t L = 0; L < 32; L++) c.rm_src[ki][t][L] = 1u << 5;   /* idle: word 0 of stream 0 */
   for (uint32_t t = 0; t < nt; t++) {
@@ -747,6 +748,9 @@ static void rm_plan(cw_dev_t &c, int ki)
       uint32_t o = ci0 + Nnn - k0c;
       o = o >= Nnn ? o - Nnn : o;
       c.rm_dst[ki][t][L] = o | (z << 16) | ((uint32_t)m << 21) | (o + (uint32_t)m > Nnn ? OAI4G_RM_DST_WRAP : 0u);
+      /* runs are disjoint intervals of the circular buffer, so at most one straddles its end; ~1
+       * (never expected) sends the encoder down its general placement path */
+      if (o + (uint32_t)m > Nnn) c.rm_wrapt[ki] = c.rm_wrapt[ki] == ~0u || c.rm_wrapt[ki] == t ? t : ~1u;
     }
   }
 }

@@ -92,6 +92,7 @@ struct cw_dev_t {
    * derives block metadata from wave-uniform scalars instead of per-lane table loads */
   uint32_t Rk[2], NDk[2], Ncbk[2], Nnnk[2], k0ck[2];
   uint32_t ntk[2], t0k[2], ntmag[2];   /* tiles per block, v0 tiles per block, ceil(2^20 / ntk) */
+  uint32_t rm_wrapt[2];                /* the tile whose run straddles the circular buffer's end (RM_DST_WRAP), or ~0 */
   /* NULL columns of w per block size: bit w' of [0] = row 0 of v0 / v1 column w' is NULL
    * (bitrev5(w') < ND), of [1] = row 0 of v2 column w' is NULL (bitrev5(w') + 1 < ND) */
   uint32_t nullcol[2][2];
