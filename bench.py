@@ -189,6 +189,12 @@ def cpu_baseline(name, seconds, subframe, full=False):
 
 
 C5_K, C5_CB = 5504, 8          # UL 100 PRB MCS 20: TBS 43816 -> C = 8 blocks of K = 5504
+# C5 subframes per step: the decoder runs one wave per 8 code blocks (8 windows each, the reference's
+# layout), so 2048 subframes are exactly 2 waves per SIMD and leave the serial recursions' latency
+# exposed; throughput rises with the number of rounds a launch holds (k_td16 at 3 waves per SIMD,
+# profiles/c5_batch_r05.txt): 2048 -> 236 k, 8192 -> 246 k, 16384 -> 266 k, 24576 -> 275 k,
+# 32768 -> 280 k, 49152 -> 283 k subframes/s.  49152 subframes = 393 216 code blocks, 13 GB of LLRs.
+C5_BATCH = 49152
 
 
 def c5_llrs(n_cb, mode, seed):
@@ -198,7 +204,7 @@ def c5_llrs(n_cb, mode, seed):
     import numpy as np
     rng = np.random.default_rng(seed)
     if mode == "8it":
-        return rng.integers(-40, 41, size=(n_cb, 3 * C5_K + 12)).astype(np.int16)
+        return rng.integers(-40, 41, size=(n_cb, 3 * C5_K + 12), dtype=np.int16)
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     import oracle_lib as O
     import re
@@ -226,7 +232,7 @@ def bench_c5_chain(args, world, rank, dist, torch):
     import openair4g_amd as oai
     n_sf = args.batch
     rng = np.random.default_rng(0xC5E + rank)
-    e = rng.integers(-40, 41, size=(n_sf, C5_G)).astype(np.int16)
+    e = rng.integers(-40, 41, size=(n_sf, C5_G), dtype=np.int16)
     ub = oai.UlDecodeBatch(C5_TBS + 24, C5_G, C5_QM, n_sf, max_iterations=8)
     ub.upload(e)
     sid = torch.cuda.current_stream().cuda_stream
@@ -878,7 +884,7 @@ def main():
     ap.add_argument("--config", default="C3")
     ap.add_argument("--batch", type=int, default=None,
                     help="subframes per GPU per step (default: C3 8192, C4 1024 = BASELINE config 4's 8192 over "
-                         "8 GPUs, FEP 8192, C5 2048); measured on C3: 2048 -> 4.20M, 5120 -> 4.56M, 10240 -> 4.67M "
+                         "8 GPUs, FEP 8192, C5 C5_BATCH = 49152); measured on C3: 2048 -> 4.20M, 5120 -> 4.56M, 10240 -> 4.67M "
                          "subframes/s (launch tails amortised)")
     ap.add_argument("--subframe", type=int, default=7)
     ap.add_argument("--full-grid", action="store_true",
@@ -896,7 +902,7 @@ def main():
                     help="harness test on CPU: gloo, StubPipeline, no GPU (exercises ranks/broadcast/timing)")
     args = ap.parse_args()
     if args.batch is None:
-        args.batch = {"C3": 8192, "C4": 1024, "FEP": 8192, "UE": 4096, "UE3": 2048}.get(args.config, 2048)
+        args.batch = {"C3": 8192, "C4": 1024, "FEP": 8192, "UE": 4096, "UE3": 2048, "C5": C5_BATCH}.get(args.config, 2048)
     if args.cpu_stub:
         args.backend = "gloo"
 

@@ -669,7 +669,11 @@ __device__ static const uint32_t *td_crc_tab(uint32_t *lds, uint32_t poly)
 }
 
 #ifndef TD16_WAVES
-#define TD16_WAVES 0   /* waves per SIMD asked of the compiler (0: its choice, 2 at <= 256 VGPRs) */
+/* waves per SIMD asked of the compiler (0: its choice, 2 at <= 256 VGPRs).  3 (168 VGPRs; log_map
+ * spills 14 / 14 / 36 dwords): the same at 2048 subframes per launch (2048 waves, 2 per SIMD either
+ * way), slower at 4096-8192 subframes, faster once the launch holds many rounds: 12288 -> +1.7 %,
+ * 16384 -> +3.5 %, 24576 -> +5.6 % (profiles/c5_batch_r05.txt) */
+#define TD16_WAVES 3
 #endif
 #if TD16_WAVES > 0
 #define TD16_ATTR __attribute__((amdgpu_waves_per_eu(TD16_WAVES, TD16_WAVES)))

@@ -71,10 +71,12 @@ def test_fep_bench_batch_8192(gpu):
             assert np.array_equal(out[s, a], _oracle_fep_subframe(fp_o, rx[s, a])), (s, a)
 
 
-@pytest.mark.parametrize("mode", ["8it", "snr"])
-def test_c5_bench_batch_16384_blocks(gpu, mode):
+@pytest.mark.parametrize("mode,n_sf", [("8it", 2048), ("snr", 2048), ("8it", None)])
+def test_c5_bench_batch(gpu, mode, n_sf):
+    """2048 subframes (16 384 code blocks, 2 waves per SIMD) and the bench's default batch
+    (bench.C5_BATCH subframes: 393 216 blocks, many rounds of 3-wave residency)."""
     import bench
-    n_cb = 2048 * bench.C5_CB
+    n_cb = (n_sf or bench.C5_BATCH) * bench.C5_CB
     llr = bench.c5_llrs(n_cb, mode, 0xC5)
     dec = gpu.TurboDecoderBatch(bench.C5_K, n_cb)
     dec.upload(llr)
