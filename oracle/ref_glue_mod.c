@@ -12,6 +12,10 @@
  *     asn1c-generated headers.  It is restated here from lte_mcs.c:45-55 (three comparisons); the
  *     modulation order it returns is also what the tests pass explicitly to the oracle.
  *
+ * PHY/LTE_TRANSPORT/pcfich.c is in the same library, also unmodified (its MAC_INTERFACE/extern.h, which
+ * reaches the asn1c chain too, skipped by its guard: the TU uses nothing from it); ref_glue_pcfich()
+ * fills the frame for generate_pcfich_reg_mapping / generate_pcfich.
+ *
  * The other symbol the two TUs leave undefined, logRecord (UTIL/LOG/log.h, LOG_E / LOG_W), is only
  * reached on their error branches (an unsupported MIMO mode or layer count), which no test case
  * takes; the library is opened with RTLD_LAZY (tests/oracle_lib.py ref_mod, oracle/cpu_baseline.c),
@@ -24,6 +28,9 @@ void dlsch_scrambling(LTE_DL_FRAME_PARMS *frame_parms, int mbsfn_flag, LTE_eNB_D
                       uint8_t Ns);
 void generate_64qam_table(void);
 void generate_16qam_table(void);
+void generate_pcfich_reg_mapping(LTE_DL_FRAME_PARMS *frame_parms);
+void generate_pcfich(uint8_t num_pdcch_symbols, int16_t amp, LTE_DL_FRAME_PARMS *frame_parms, mod_sym_t **txdataF,
+                     uint8_t subframe);
 
 unsigned char get_Qm(unsigned char I_MCS)
 {
@@ -185,4 +192,19 @@ void ref_glue_qam_tables(int32_t q16[4], int32_t q64[8])
   ref_glue_init();
   for (int i = 0; i < 4; i++) q16[i] = qam16_table[i];
   for (int i = 0; i < 8; i++) q64[i] = qam64_table[i];
+}
+
+/* generate_pcfich_reg_mapping then generate_pcfich (pcfich.c:48-84, 144-228) into txdataF[ant] (frame
+ * grids); nb_antennas_tx_eNB (the field generate_pcfich tests) = f[2].  reg / first_idx: the mapping. */
+void ref_glue_pcfich(uint8_t num_pdcch_symbols, int16_t amp, const int32_t f[9], int32_t **txdataF, uint8_t subframe,
+                     uint16_t reg[4], uint8_t *first_idx)
+{
+  LTE_DL_FRAME_PARMS fp;
+  ref_glue_frame(&fp, f);
+  fp.nb_antennas_tx_eNB = (uint8_t)f[2];
+  generate_pcfich_reg_mapping(&fp);
+  for (int i = 0; i < 4; i++) reg[i] = fp.pcfich_reg[i];
+  *first_idx = fp.pcfich_first_reg_idx;
+  generate_pcfich(num_pdcch_symbols, amp, &fp, (mod_sym_t **)txdataF, subframe);
+  fflush(stdout);   /* the mapping's own printf (pcfich.c:80-82) leaves while a test's capture is on */
 }

@@ -3,6 +3,9 @@ made by tests/golden/gen_mod_ref.py with the reference's own dlsch_modulation.c 
 dlsch_scrambling.c compiled here, oracle/_ref/libref_mod.so).  Inputs are generated, not stored: e
 bits from splitmix64 (rm_ref_cases), so the GPU box rebuilds them from the case list alone.
 
+PCFICH cases (pcfich.c, the same library): a frame, CFI 1-3, subframe index and amp; expected: the
+REG mapping and the digest of symbol 0 of that subframe per antenna.
+
 Each modulation case: a frame (N_RB_DL, Ncp, TX antennas, mode1_flag, Nid_cell), a transmission
 mode (SISO / ALAMOUTI / LARGE_CDD, one or two codewords), the subframe index, PDCCH symbols, an RB
 bitmap, amp and rho_A / rho_B; expected: dlsch_modulation's return value and the digest of each
@@ -76,3 +79,24 @@ def cws_of(c):
 def frame_of(O, c):
     return O.frame(c["N_RB_DL"], Nid_cell=c["Nid_cell"], Ncp=c["Ncp"], nb_antennas_tx=c["n_ant"],
                    mode1_flag=c["mode1_flag"])
+
+
+def pcfich_cases():
+    """every bandwidth, both prefixes, 1 TX antenna (SISO), 2 (SISO and ALAMOUTI), CFI 1-3"""
+    cases = []
+    k = 0
+    for n_rb in (6, 15, 25, 50, 100):
+        for n_ant, mode1 in ((1, 1), (2, 1), (2, 0)):
+            for cfi in (1, 2, 3):
+                k += 1
+                cases.append(dict(N_RB_DL=n_rb, Ncp=1 if k % 4 == 0 else 0, n_ant=n_ant, mode1_flag=mode1,
+                                  Nid_cell=(97 * k + 11) % 504, cfi=cfi, subframe=(3 * k) % 10,
+                                  amp=(512, 1024, 4096, 32767)[k % 4]))
+    return cases
+
+
+def symbol0_digests(grids, c, N):
+    """per-antenna digests of symbol 0 of subframe c["subframe"] of frame grids"""
+    nsymb = 12 if c["Ncp"] else 14
+    o = c["subframe"] * nsymb * N
+    return [digest(g[o:o + N]) for g in grids]

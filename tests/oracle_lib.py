@@ -946,6 +946,7 @@ def ref_mod():
                                                 ctypes.c_int16]
         L.ref_glue_dlsch_scrambling.argtypes = [VP, ctypes.c_int, U16, U16, U8, U8]
         L.ref_glue_qam_tables.argtypes = [VP, VP]
+        L.ref_glue_pcfich.argtypes = [U8, ctypes.c_int16, VP, ctypes.POINTER(VP), U8, VP, VP]
         _refmod = L
     return _refmod
 
@@ -1010,3 +1011,14 @@ def ref_scrambling(e, G, rnti, Nid_cell, q, Ns):
     buf[:min(n, len(src))] = src[:n]
     ref_mod().ref_glue_dlsch_scrambling(buf.ctypes.data, G, rnti, Nid_cell, q, Ns)
     return buf
+
+
+def ref_pcfich(cfi, amp, fp, subframe):
+    """The reference's generate_pcfich_reg_mapping + generate_pcfich (pcfich.c, compiled unmodified into
+    libref_mod.so) over zeroed frame grids: (grids, reg[4], first_idx)."""
+    grids, ptrs = _grids(fp)
+    reg = np.zeros(4, np.uint16)
+    first = np.zeros(1, np.uint8)
+    f = mod_frame_words(fp)
+    ref_mod().ref_glue_pcfich(cfi, amp, f.ctypes.data, ptrs, subframe, reg.ctypes.data, first.ctypes.data)
+    return grids, [int(r) for r in reg], int(first[0])

@@ -1,14 +1,16 @@
-"""The library's drop-in dlsch_modulation and dlsch_scrambling (C ABI oai4g_dlsch_modulation /
-oai4g_dlsch_scrambling, HIP kernels) against the fixtures the reference's own dlsch_modulation.c and
-dlsch_scrambling.c produced here (tests/golden/mod_ref.json): frame grids digest for digest, the
-return value (re_allocated) equal, scrambled e bits equal."""
+"""The library's drop-in dlsch_modulation, dlsch_scrambling and generate_pcfich (C ABI
+oai4g_dlsch_modulation / oai4g_dlsch_scrambling / oai4g_generate_pcfich, HIP kernels) against the
+fixtures the reference's own dlsch_modulation.c, dlsch_scrambling.c and pcfich.c produced here
+(tests/golden/mod_ref.json): frame grids digest for digest, the return value (re_allocated) equal,
+scrambled e bits equal, the PCFICH REG mapping equal."""
+import ctypes
 import json
 import os
 
 import numpy as np
 import pytest
 
-from mod_ref_cases import NBITS, e_bits, grid_digests
+from mod_ref_cases import NBITS, e_bits, grid_digests, symbol0_digests
 from rm_ref_cases import digest
 
 pytestmark = pytest.mark.gpu
@@ -62,3 +64,18 @@ def test_dlsch_scrambling_equals_reference(gpu, i):
     e[:] = e_bits(c["seed"])
     gpu.dlsch_scrambling(fp, dl, G, c["q"], c["Ns"])
     assert digest(dl.view("e", G)) == s["digest"]
+
+
+@pytest.mark.parametrize("i", range(len(FIX["pcfich"])))
+def test_generate_pcfich_equals_reference(gpu, i):
+    p = FIX["pcfich"][i]
+    c = p["case"]
+    fp = gpu.frame_parms(c["N_RB_DL"], c["Nid_cell"], c["Ncp"], c["n_ant"], c["mode1_flag"], 0)
+    reg = (ctypes.c_uint16 * 4)()
+    first = ctypes.c_uint8()
+    gpu.lib().oai4g_generate_pcfich_reg_mapping(fp, reg, ctypes.byref(first))
+    assert (list(reg), first.value) == (p["reg"], p["first"])
+    nsymb = 12 if c["Ncp"] else 14
+    grids = [np.zeros(10 * nsymb * fp.ofdm_symbol_size, dtype=np.int32) for _ in range(c["n_ant"])]
+    assert gpu.generate_pcfich(c["cfi"], c["amp"], fp, grids, c["subframe"]) == 0
+    assert symbol0_digests(grids, c, fp.ofdm_symbol_size) == p["digests"]

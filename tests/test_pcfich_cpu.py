@@ -1,7 +1,7 @@
 """PCFICH: the oracle restatement of generate_pcfich (oracle/oai_oracle.c,
-pcfich.c:48-228) pinned to an independent 36.211 / 36.212 model (tests/spec_model.py: pcfich).
-The reference TU is unbuildable here (PHY/defs.h -> asn1c headers), so this row is pinned to the
-spec, like the other LTE_TRANSPORT stages."""
+pcfich.c:48-228) against an independent 36.211 / 36.212 model (tests/spec_model.py: pcfich).  The
+reference TU itself is pinned too: pcfich.c builds unmodified (oracle/_ref/libref_mod.so) and
+tests/test_ref_pin_mod_cpu.py / test_mod_fixture_cpu.py / test_gpu_mod_ref.py compare against it."""
 import numpy as np
 import pytest
 

@@ -1,7 +1,7 @@
-"""The oracle's modulation / RE mapping / precoding and scrambling against the reference's own
-PHY/LTE_TRANSPORT/dlsch_modulation.c (:1181-1493, with allocate_REs_in_RB :139-982) and
-dlsch_scrambling.c (:51-97), both compiled unmodified into oracle/_ref/libref_mod.so (oracle/Makefile,
-glue oracle/ref_glue_mod.c).  Frame grids must be identical word for word, and dlsch_modulation's
+"""The oracle's modulation / RE mapping / precoding, scrambling and PCFICH against the reference's own
+PHY/LTE_TRANSPORT/dlsch_modulation.c (:1181-1493, with allocate_REs_in_RB :139-982),
+dlsch_scrambling.c (:51-97) and pcfich.c (:48-228), compiled unmodified into oracle/_ref/libref_mod.so
+(oracle/Makefile, glue oracle/ref_glue_mod.c).  Frame grids must be identical word for word, and dlsch_modulation's
 return value (re_allocated) equal.  Skipped where the reference tree was not built here (the GPU box);
 tests/test_mod_fixture_cpu.py covers the committed fixtures there."""
 import itertools
@@ -129,3 +129,33 @@ def test_scrambling_equals_reference(G):
         ref = O.ref_scrambling(e, G, rnti, Nid, q, Ns)
         orc = O.scramble(e, G, (rnti << 14) + (q << 13) + ((Ns >> 1) << 9) + Nid) if G else e
         assert np.array_equal(ref[:G], orc[:G])
+
+
+@pytest.mark.parametrize("n_rb", [6, 15, 25, 50, 100])
+def test_pcfich_reg_mapping_every_cell(n_rb):
+    """generate_pcfich_reg_mapping (pcfich.c:48-84): the four REGs and the first-REG index for all 504
+    cell ids."""
+    for nid in range(504):
+        fp = O.frame(n_rb, Nid_cell=nid)
+        _, reg, first = O.ref_pcfich(1, 512, fp, 0)
+        assert O.pcfich_reg_mapping(fp) == (reg, first), nid
+
+
+@pytest.mark.parametrize("n_rb", [6, 15, 25, 50, 100])
+@pytest.mark.parametrize("Ncp", [0, 1])
+def test_pcfich_equals_reference(n_rb, Ncp):
+    """generate_pcfich (pcfich.c:144-228): CFI 1-3 codewords, the c_init of 36.211 6.7.1, QPSK at
+    amp / sqrt2 (SISO) or amp / 2 (ALAMOUTI pairs), the nushift holes, 1 or 2 TX antennas; whole
+    frame grids word for word."""
+    rng = np.random.default_rng(7000 + 10 * n_rb + Ncp)
+    for n_ant, mode1 in ((1, 1), (2, 1), (2, 0)):
+        for cfi in (1, 2, 3):
+            for sf in range(10):
+                nid = int(rng.integers(0, 504))
+                amp = int(rng.choice([512, 1024, 4096, 32767]))
+                fp = O.frame(n_rb, Nid_cell=nid, Ncp=Ncp, nb_antennas_tx=n_ant, mode1_flag=mode1)
+                ref, _, _ = O.ref_pcfich(cfi, amp, fp, sf)
+                orc = [np.zeros_like(g) for g in ref]
+                assert O.generate_pcfich(cfi, amp, fp, orc, sf) == 0
+                for a in range(n_ant):
+                    assert np.array_equal(orc[a], ref[a]), (n_ant, mode1, cfi, sf, nid, amp, a)
