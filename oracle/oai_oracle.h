@@ -225,6 +225,12 @@ int orc_rx_pdsch_siso(const orc_frame_t *fp, const int32_t *rxdataF, const int32
                       const uint32_t rb_alloc[4], uint8_t Qm, uint8_t num_pdcch_symbols, uint8_t subframe,
                       int16_t *llr, uint8_t *log2_maxh_out);
 void orc_dlsch_unscrambling(int16_t *llr, int G, uint32_t c_init);
+/* the LLR stages alone over flat streams (dlsch_llr_computation.c: dlsch_qpsk / 16qam / 64qam_llr :636-930,
+ * qpsk_qpsk :1041, qpsk_qam16 :1300, qpsk_qam64 :1584), as the receivers above use them per RE */
+int orc_llr_qam(int Qm, const int16_t *comp, const int16_t *mag, const int16_t *magb, int len, int16_t *llr);
+void orc_llr_qpsk_qpsk(const int16_t *s0, const int16_t *s1, const int16_t *rho, int len, int16_t *llr);
+void orc_llr_qpsk_qamx(int qm1, const int16_t *s0, const int16_t *s1, const int16_t *mag1, const int16_t *rho, int len,
+                       int16_t *llr);
 /* rx_pdsch for TM3 (LARGE_CDD, 2 ports), dual_stream_flag = 0: codeword 0's LLRs (Qm0 4 / 6; Qm0 2
  * runs orc_rx_pdsch_tm3_q2 for codeword 0).
  * rxdataF[a] = [nsymb][N] per receive antenna, est[p * 2 + a] = [nsymb][N] estimates of port p. */

@@ -34,6 +34,23 @@ static int16_t sat16(int32_t v) { return (int16_t)(v > 32767 ? 32767 : (v < -327
 static int16_t abs16(int16_t v) { return (int16_t)(v < 0 ? -v : v); }      /* _mm_abs_epi16: -32768 stays */
 static int16_t mulhi2(int16_t a, int16_t b) { return (int16_t)((((int32_t)a * b) >> 16) << 1); }
 
+/* one RE of dlsch_qpsk_llr / dlsch_16qam_llr / dlsch_64qam_llr (dlsch_llr_computation.c:636-930): the
+ * compensated (cr, ci) pass through; 16-QAM appends mag -sat |y| (abs_epi16 keeps -32768), 64-QAM
+ * also magb -sat |that|.  Returns the LLRs written. */
+static int llr_qam_re(int Qm, int16_t cr, int16_t ci, int16_t mag, int16_t magb, int16_t *out)
+{
+  out[0] = cr;
+  out[1] = ci;
+  if (Qm == 2) return 2;
+  const int16_t x1r = sat16((int32_t)mag - abs16(cr)), x1i = sat16((int32_t)mag - abs16(ci));
+  out[2] = x1r;
+  out[3] = x1i;
+  if (Qm == 4) return 4;
+  out[4] = sat16((int32_t)magb - abs16(x1r));
+  out[5] = sat16((int32_t)magb - abs16(x1i));
+  return 6;
+}
+
 static int alloc_bit(const uint32_t rb_alloc[4], int rb)
 {
   if (rb < 32) return (rb_alloc[0] >> rb) & 1;
@@ -204,21 +221,11 @@ int orc_rx_pdsch_siso(const orc_frame_t *fp, const int32_t *rxdataF, const int32
       const int16_t cr = sat16((int32_t)((uint32_t)((int32_t)hr * yr) + (uint32_t)((int32_t)hi * yi)) >> log2_maxh);
       const int16_t ci = sat16((int32_t)((uint32_t)((int32_t)nhi * yr) + (uint32_t)((int32_t)hr * yi)) >> log2_maxh);
       if (Qm == 2) {
-        *out++ = cr;
-        *out++ = ci;
+        out += llr_qam_re(2, cr, ci, 0, 0, out);
         continue;
       }
       const int16_t m = sat16((int32_t)((uint32_t)((int32_t)hr * hr) + (uint32_t)((int32_t)hi * hi)) >> log2_maxh);
-      const int16_t mag = mulhi2(m, a1), magb = mulhi2(m, a2);
-      const int16_t x1r = sat16((int32_t)mag - abs16(cr)), x1i = sat16((int32_t)mag - abs16(ci));
-      *out++ = cr;
-      *out++ = ci;
-      *out++ = x1r;
-      *out++ = x1i;
-      if (Qm == 6) {
-        *out++ = sat16((int32_t)magb - abs16(x1r));
-        *out++ = sat16((int32_t)magb - abs16(x1i));
-      }
+      out += llr_qam_re(Qm, cr, ci, mulhi2(m, a1), mulhi2(m, a2), out);
     }
   }
   free(rx_ext);
@@ -463,18 +470,7 @@ int orc_rx_pdsch_tm3(const orc_frame_t *fp, int nb_rx, const int32_t *const *rxd
     const int len = pil ? nb_rb * 8 - 2 * orc_adjust_G2(fp, rb_alloc, subframe, (uint8_t)symbol) / 3
                         : nb_rb * 12 - orc_adjust_G2(fp, rb_alloc, subframe, (uint8_t)symbol);
     if (len > hw[0]) { out = NULL; break; }
-    for (int j = 0; j < len; j++) {
-      const int16_t cr = comp[j * 2], ci = comp[j * 2 + 1];
-      const int16_t x1r = sat16((int32_t)mag[j] - abs16(cr)), x1i = sat16((int32_t)mag[j] - abs16(ci));
-      *out++ = cr;
-      *out++ = ci;
-      *out++ = x1r;
-      *out++ = x1i;
-      if (Qm0 == 6) {
-        *out++ = sat16((int32_t)magb[j] - abs16(x1r));
-        *out++ = sat16((int32_t)magb[j] - abs16(x1i));
-      }
-    }
+    for (int j = 0; j < len; j++) out += llr_qam_re(Qm0, comp[j * 2], comp[j * 2 + 1], mag[j], magb[j], out);
   }
   free(rx_ext);
   free(c0);
@@ -560,6 +556,28 @@ static void qx_llr(int qm1, const int16_t y0[2], const int16_t y1[2], int16_t ma
   out[0] = sat16((int32_t)M_(met[0], met[1]) - M_(met[2], met[3]));
   out[1] = sat16((int32_t)M_(met[0], met[2]) - M_(met[1], met[3]));
 #undef M_
+}
+
+/* The per-RE LLR stages above over flat streams of len REs, for the reference pin
+ * (tests/test_ref_pin_llr_cpu.py against dlsch_llr_computation.c compiled unmodified): comp / s0 / s1 /
+ * rho are (re, im) int16 pairs; mag / magb / mag1 one int16 per RE, which the reference's packed
+ * magnitudes carry in both halves. */
+int orc_llr_qam(int Qm, const int16_t *comp, const int16_t *mag, const int16_t *magb, int len, int16_t *llr)
+{
+  int16_t *o = llr;
+  for (int j = 0; j < len; j++) o += llr_qam_re(Qm, comp[2 * j], comp[2 * j + 1], mag ? mag[j] : 0, magb ? magb[j] : 0, o);
+  return (int)(o - llr);
+}
+
+void orc_llr_qpsk_qpsk(const int16_t *s0, const int16_t *s1, const int16_t *rho, int len, int16_t *llr)
+{
+  for (int j = 0; j < len; j++) qq_llr(&s0[2 * j], &s1[2 * j], &rho[2 * j], &llr[2 * j]);
+}
+
+void orc_llr_qpsk_qamx(int qm1, const int16_t *s0, const int16_t *s1, const int16_t *mag1, const int16_t *rho, int len,
+                       int16_t *llr)
+{
+  for (int j = 0; j < len; j++) qx_llr(qm1, &s0[2 * j], &s1[2 * j], mag1[j], &rho[2 * j], &llr[2 * j]);
 }
 
 /* rx_pdsch for TM3 with both codewords QPSK (dlsch_demodulation.c:373-413, 537-552, 643-669):
@@ -778,20 +796,7 @@ int orc_rx_pdsch_tm2(const orc_frame_t *fp, int nb_rx, const int32_t *const *rxd
     const int adj = Qm == 2 ? 0 : orc_adjust_G2(fp, rb_alloc, subframe, (uint8_t)symbol);
     const int len = pil ? nb_rb * 8 - 2 * adj / 3 : nb_rb * 12 - adj;
     if (((len + 1) & ~1) > hw[0]) { out = NULL; break; }
-    for (int j = 0; j < len; j++) {
-      const int16_t cr = c0[2 * j], ci = c0[2 * j + 1];
-      *out++ = cr;
-      *out++ = ci;
-      if (Qm > 2) {
-        const int16_t x1r = sat16((int32_t)mag[j] - abs16(cr)), x1i = sat16((int32_t)mag[j] - abs16(ci));
-        *out++ = x1r;
-        *out++ = x1i;
-        if (Qm == 6) {
-          *out++ = sat16((int32_t)magb[j] - abs16(x1r));
-          *out++ = sat16((int32_t)magb[j] - abs16(x1i));
-        }
-      }
-    }
+    for (int j = 0; j < len; j++) out += llr_qam_re(Qm, c0[2 * j], c0[2 * j + 1], mag[j], magb[j], out);
   }
   free(rx_ext);
   free(hx);

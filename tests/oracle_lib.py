@@ -1022,3 +1022,74 @@ def ref_pcfich(cfi, amp, fp, subframe):
     f = mod_frame_words(fp)
     ref_mod().ref_glue_pcfich(cfi, amp, f.ctypes.data, ptrs, subframe, reg.ctypes.data, first.ctypes.data)
     return grids, [int(r) for r in reg], int(first[0])
+
+
+# ---- dlsch_llr_computation.c compiled unmodified (oracle/_ref/libref_llr.so) ----
+REF_LLR_SO = os.path.join(ORACLE_DIR, "_ref", "libref_llr.so")
+_refllr = None
+
+
+def ref_llr():
+    """dlsch_llr_computation.c compiled unmodified (+ ref_glue_llr.c), or None when not built here."""
+    global _refllr
+    if _refllr is None:
+        if not os.path.exists(REF_LLR_SO):
+            return None
+        L = ctypes.CDLL(REF_LLR_SO, mode=os.RTLD_LAZY | os.RTLD_LOCAL)
+        L.ref_glue_qam_llr.restype = ctypes.c_int
+        L.ref_glue_qam_llr.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, VP, VP, VP, VP, U8, U16,
+                                       U16]
+        for f in ("qpsk_qpsk", "qpsk_qam16", "qpsk_qam64"):
+            getattr(L, f).restype = None
+        L.qpsk_qpsk.argtypes = [VP, VP, VP, VP, ctypes.c_int]
+        L.qpsk_qam16.argtypes = [VP, VP, VP, VP, VP, ctypes.c_int32]
+        L.qpsk_qam64.argtypes = [VP, VP, VP, VP, VP, ctypes.c_int32]
+        _refllr = L
+    return _refllr
+
+
+def aligned(a, align=64):
+    """a copy of array a whose data starts on an `align`-byte boundary (the reference's SSE loads are
+    aligned ones)"""
+    a = np.ascontiguousarray(a)
+    raw = np.zeros(a.nbytes + align, np.uint8)
+    off = (-raw.ctypes.data) % align
+    out = raw[off:off + a.nbytes].view(a.dtype).reshape(a.shape)
+    out[...] = a
+    return out
+
+
+def _orc_llr_types():
+    L = orc()
+    if not getattr(L, "_llr_typed", False):
+        L.orc_llr_qam.argtypes = [ctypes.c_int, VP, VP, VP, ctypes.c_int, VP]
+        L.orc_llr_qpsk_qpsk.argtypes = [VP, VP, VP, ctypes.c_int, VP]
+        L.orc_llr_qpsk_qamx.argtypes = [ctypes.c_int, VP, VP, VP, VP, ctypes.c_int, VP]
+        L.orc_llr_qpsk_qpsk.restype = L.orc_llr_qpsk_qamx.restype = None
+        L._llr_typed = True
+    return L
+
+
+def orc_llr_qam(Qm, comp, mag, magb, n):
+    """the oracle's per-RE LLR stage (orc_llr_qam) over n REs of flat int16 streams"""
+    _orc_llr_types()
+    out = np.zeros(6 * n + 8, np.int16)
+    comp = np.ascontiguousarray(comp, np.int16)
+    mag = np.ascontiguousarray(mag, np.int16)
+    magb = np.ascontiguousarray(magb, np.int16)
+    orc().orc_llr_qam(Qm, comp.ctypes.data, mag.ctypes.data, magb.ctypes.data, n, out.ctypes.data)
+    return out[:Qm * n]
+
+
+def orc_llr_ia(qm1, s0, s1, mag1, rho, n):
+    """the oracle's interference-aware LLRs of stream 0 (orc_llr_qpsk_qpsk / orc_llr_qpsk_qamx)"""
+    _orc_llr_types()
+    out = np.zeros(2 * n, np.int16)
+    s0, s1, rho = (np.ascontiguousarray(x, np.int16) for x in (s0, s1, rho))
+    if qm1 == 2:
+        orc().orc_llr_qpsk_qpsk(s0.ctypes.data, s1.ctypes.data, rho.ctypes.data, n, out.ctypes.data)
+    else:
+        mag1 = np.ascontiguousarray(mag1, np.int16)
+        orc().orc_llr_qpsk_qamx(qm1, s0.ctypes.data, s1.ctypes.data, mag1.ctypes.data, rho.ctypes.data, n,
+                                out.ctypes.data)
+    return out
