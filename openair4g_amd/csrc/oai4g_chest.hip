@@ -382,8 +382,10 @@ hipError_t oai4g_launch_chest_symbol(const chest_dev_t *d_cfg, const chest_dev_t
  * REs, wrapping 32-bit sums, C int division), dl_ch_shift = 6 + log2_approx(level) / 2, then
  * dot_product (PHY/TOOLS/cdot_prod.c:40-118: per RE (xr yr + xi yi) >> shift and
  * (xr yi - xi yr) >> shift, wrapping sums, packs to int16) of row l against the previous pilot
- * row over the lower half (from RE 12) and the upper half (from RE (N_RB / 2 + 1) * 12),
- * (N_RB / 2 - 1) * 12 REs each; omega = the int16 component sums (wrap) as re | im << 16.
+ * row over the upper half (from RE (N_RB / 2 + 1) * 12, (N_RB / 2 - 1) * 12 REs); omega = twice it,
+ * int16 wrap per component, as re | im << 16: the reference's omega_cpx points at omega itself
+ * (:152), so its upper-half dot product (:164) overwrites the lower half's (:150) before
+ * omega_cpx->r += omega.r (:165-166) — the lower half never counts (tests/test_ref_pin_fo_cpu.py).
  * Sums are mod 2^32, so the wave's reduction order gives the reference's lane sums exactly.
  * ==================================================================================== */
 static __device__ __forceinline__ uint32_t wave_sum_u32(uint32_t v)
@@ -416,9 +418,8 @@ __global__ void __launch_bounds__(64) k_freq_offset(const int32_t *__restrict__ 
   const uint32_t shift = 6 + (x ? 32u - __clz(x) : 0u) / 2;
   const int n = (N_RB / 2 - 1) * 12, hi = (N_RB / 2 + 1) * 12;
   int16_t out_re = 0, out_im = 0;
-#pragma unroll
-  for (int half = 0; half < 2; half++) {
-    const int base = half ? hi : 12;
+  {
+    const int base = hi;
     uint32_t sre = 0, sim = 0;
     for (int i = lane; i < n; i += 64) {
       const uint32_t a = p[row_off + base + i], b = p[prev_off + base + i];
@@ -430,8 +431,10 @@ __global__ void __launch_bounds__(64) k_freq_offset(const int32_t *__restrict__ 
     }
     sre = wave_sum_u32(sre);
     sim = wave_sum_u32(sim);
-    out_re = (int16_t)(out_re + fo_sat16((int32_t)sre));
-    out_im = (int16_t)(out_im + fo_sat16((int32_t)sim));
+    out_re = fo_sat16((int32_t)sre);
+    out_im = fo_sat16((int32_t)sim);
+    out_re = (int16_t)(out_re + out_re);
+    out_im = (int16_t)(out_im + out_im);
   }
   if (lane == 0) omega[j] = (int32_t)((uint32_t)(uint16_t)out_re | ((uint32_t)(uint16_t)out_im << 16));
 }

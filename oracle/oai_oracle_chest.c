@@ -263,10 +263,14 @@ int32_t orc_dot_product(const int16_t *x, const int16_t *y, uint32_t N, uint8_t 
 }
 
 /* lte_est_freq_offset's integer part (:125-166), antenna 0 only (:135): dl_ch_shift from the
- * channel level of row l at offset 12, then omega = dot(row l, previous pilot row) over the
- * lower half (from RE 12) plus the upper half (from RE (N_RB/2 + 1) * 12), (N_RB/2 - 1) * 12 REs
- * each, added as int16 components (wrap).  Returns omega (re | im << 16), or -1 << 31 for an l
- * other than 0 or 4 - Ncp (the reference prints and returns -1 without touching freq_offset). */
+ * channel level of row l at offset 12, then omega from dot(row l, previous pilot row) over the
+ * lower half (from RE 12) and the upper half (from RE (N_RB/2 + 1) * 12), (N_RB/2 - 1) * 12 REs
+ * each.  The intended sum of the two is not what the reference computes: omega_cpx points at omega
+ * itself (:152), so the upper half's dot product overwrites the lower's (:164) before
+ * omega_cpx->r += omega.r (:165-166) doubles it — omega = 2 x the upper half, int16 wrap per
+ * component (checked against the TU compiled here, tests/test_ref_pin_fo_cpu.py).  Returns omega
+ * (re | im << 16), or -1 << 31 for an l other than 0 or 4 - Ncp (the reference prints and returns -1
+ * without touching freq_offset). */
 int32_t orc_fo_omega(const orc_frame_t *fp, const int32_t *dl_ch_estimates0, int l)
 {
   const int N = fp->ofdm_symbol_size, N_RB = fp->N_RB_DL, lp = 4 - fp->Ncp;
@@ -276,12 +280,12 @@ int32_t orc_fo_omega(const orc_frame_t *fp, const int32_t *dl_ch_estimates0, int
   const uint8_t shift = (uint8_t)(6 + orc_log2_approx((uint32_t)orc_fo_channel_level(dl_ch, N_RB)) / 2);
   const int16_t *prev = (const int16_t *)&dl_ch_estimates0[12 + (ch_offset == 0 ? lp * N : 0)];
   const uint32_t n = (uint32_t)((N_RB / 2 - 1) * 12);
-  const int32_t o1 = orc_dot_product(dl_ch, prev, n, shift);
+  (void)prev;                                   /* the lower half's dot product (:150) is overwritten */
   const int hi = (N_RB / 2 + 1) * 12;
   dl_ch = (const int16_t *)&dl_ch_estimates0[hi + ch_offset];
   prev = (const int16_t *)&dl_ch_estimates0[hi + (ch_offset == 0 ? lp * N : 0)];
   const int32_t o2 = orc_dot_product(dl_ch, prev, n, shift);
-  const int16_t re = (int16_t)((int16_t)o1 + (int16_t)o2), im = (int16_t)((int16_t)(o1 >> 16) + (int16_t)(o2 >> 16));
+  const int16_t re = (int16_t)((int16_t)o2 + (int16_t)o2), im = (int16_t)((int16_t)(o2 >> 16) + (int16_t)(o2 >> 16));
   return (int32_t)((uint32_t)(uint16_t)re | ((uint32_t)(uint16_t)im << 16));
 }
 

@@ -1093,3 +1093,22 @@ def orc_llr_ia(qm1, s0, s1, mag1, rho, n):
         orc().orc_llr_qpsk_qamx(qm1, s0.ctypes.data, s1.ctypes.data, mag1.ctypes.data, rho.ctypes.data, n,
                                 out.ctypes.data)
     return out
+
+
+# ---- lte_est_freq_offset.c compiled unmodified (oracle/_ref/libref_fo.so) ----
+REF_FO_SO = os.path.join(ORACLE_DIR, "_ref", "libref_fo.so")
+_reffo = None
+
+
+def ref_fo():
+    """lte_est_freq_offset.c compiled unmodified (+ ref_glue_fo.c over libref_tools.so), or None."""
+    global _reffo
+    if _reffo is None:
+        if not os.path.exists(REF_FO_SO) or ref_tools() is None:
+            return None
+        L = ctypes.CDLL(REF_FO_SO, mode=os.RTLD_LAZY | os.RTLD_LOCAL)
+        L.ref_glue_est_freq_offset.restype = ctypes.c_int
+        L.ref_glue_est_freq_offset.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, VP, ctypes.c_int,
+                                               ctypes.POINTER(ctypes.c_int), ctypes.c_int]
+        _reffo = L
+    return _reffo

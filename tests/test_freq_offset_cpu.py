@@ -10,9 +10,10 @@ item 3, the UE front end's remaining pieces):
     (est 2^10 + f (32767 - 2^10)) >> 15 after the first call;
   - dl_ch_estimates_time of the restatement is the reference idft (oracle pinned to lte_dfts.c)
     of the plane from word 8.
-dl_channel_level and the atan2 / filter tail live in lte_est_freq_offset.c, whose PHY/defs.h
-include chain (asn1c headers) is unbuildable here: those lines are restated and pinned by the
-rotation test only."""
+The whole of lte_est_freq_offset is also pinned to the TU itself, which builds unmodified here once
+PHY/defs.h is skipped by its guard (tests/test_ref_pin_fo_cpu.py, tests/test_fo_fixture_cpu.py).  That
+pin showed the reference's omega alias: omega = twice the upper-half dot product, not the sum of the
+two halves; the rotation test below holds either way (both halves carry the same rotation)."""
 import ctypes
 import math
 
