@@ -350,9 +350,11 @@ int oai4g_chest_time_batch(const oai4g_frame_parms_t *frame_parms, int n_jobs, c
 
 /* lte_est_freq_offset (PHY/LTE_ESTIMATION/lte_est_freq_offset.c:104-193, called by slot_fep.c:211-217
  * at l = 4 - Ncp): antenna 0's plane dl_ch_estimates[0]; dl_ch_shift = 6 + log2_approx(
- * dl_channel_level(row l from RE 12)) / 2; omega = dot_product (cdot_prod.c:40) of row l against the
- * other pilot row (row 4 - Ncp when l = 0, else row 0) over (N_RB_DL / 2 - 1) * 12 REs from RE 12 plus
- * the same from RE (N_RB_DL / 2 + 1) * 12; freq_offset_est = (int)(atan2(omega) / 2 pi / 285.8 us
+ * dl_channel_level(row l from RE 12)) / 2; omega as the reference computes it: its dot_product
+ * (cdot_prod.c:40) of row l against the other pilot row (row 4 - Ncp when l = 0, else row 0) over
+ * (N_RB_DL / 2 - 1) * 12 REs from RE (N_RB_DL / 2 + 1) * 12, doubled (int16 wrap per component) — the
+ * lower-half product from RE 12 is overwritten through the omega_cpx alias (:150-166) and never
+ * counts; freq_offset_est = (int)(atan2(omega) / 2 pi / 285.8 us
  * (normal CP) or 250 us); the first call (or one with reset != 0) stores it, later calls filter
  * (est * 2^10 + f * (32767 - 2^10)) >> 15.  The filter state is process-wide, as the reference's
  * static first_run.  The dot products run on the GPU; atan2 and the filter are the host's scalar
