@@ -970,26 +970,33 @@ static __device__ void encode_codeword(const cfg_dev_t *__restrict__ c, uint32_t
       auto row_of = [&](uint32_t ki, uint32_t t0) {
         return __builtin_amdgcn_readfirstlane(ki * ((OAI4G_RM_TILES + 1) * 32) + t0 * 32);
       };
-      if (pb + wave < pe) {
-        uint32_t ki, r, t0;
-        decode(pb + wave, ki, r, t0);
+      /* round-robin pairs P = pb + wave + k nwaves, stepped rather than decoded: the next pair is
+       * nwaves pairs on (2 nwaves tiles), carried over block ends; a block's scalars change only
+       * there.  Plan words loaded one pair ahead. */
+      uint32_t P = pb + wave;
+      uint32_t ki = 0, r = 0, t0 = 0;
+      if (P < pe) {
+        decode(P, ki, r, t0);
         const uint32_t ro = row_of(ki, t0);
         nsrc = (rsrc0 + ro)[lane];
         ndst = (rdst0 + ro)[lane];
       }
-      for (uint32_t P = pb + wave; P < pe; P += nwaves) {    /* scalar loop: wave is an SGPR */
-        uint32_t ki, r, t0;
-        decode(P, ki, r, t0);
+      uint32_t bbo = __builtin_amdgcn_readfirstlane(r * sw3), E = r >= es ? Ehi : Elo, rob = ro_of(r) - bit0;
+      for (; P < pe; P += nwaves) {    /* scalar loop: wave is an SGPR */
         const uint32_t src = nsrc, dst = ndst;
+        /* the next pair of this wave */
+        uint32_t k2 = ki, r2 = r, t2 = t0 + 2 * nwaves;
+        while (t2 >= 2 * (k2 ? pp1 : pp0)) {
+          t2 -= 2 * (k2 ? pp1 : pp0);
+          r2++;
+          k2 = r2 >= n0 ? 1u : 0u;
+        }
         if (P + nwaves < pe) {
-          uint32_t k2, r2, t2;
-          decode(P + nwaves, k2, r2, t2);
-          (void)r2;
           const uint32_t ro = row_of(k2, t2);
           nsrc = (rsrc0 + ro)[lane];
           ndst = (rdst0 + ro)[lane];
         }
-        const uint32_t *bb = strm + __builtin_amdgcn_readfirstlane(r * sw3) - 1;   /* block streams - 1 word (scalar offset) */
+        const uint32_t *bb = strm + bbo - 1;                                 /* block streams - 1 word (scalar offset) */
         const uint32_t *wp = bb + ((src >> 5) & 0x7fffu);
         uint32_t y = __builtin_amdgcn_alignbit(wp[1], wp[0], src);            /* bits before 0 are NULLs */
         /* the RM_SRC_LAST lane (row R - 1 of y2, j = Kpi - 1 reads y^(2)_0 at bit 31) needs no
@@ -998,7 +1005,7 @@ static __device__ void encode_codeword(const cfg_dev_t *__restrict__ c, uint32_t
         y = transpose32_t<0>(y, tpl);
         y >>= (dst >> 16) & 31u;                                             /* leading NULLs z */
         const uint32_t o = dst & 0xffffu, m = __builtin_amdgcn_ubfe(dst, 21, 6);
-        const uint32_t E = r >= es ? Ehi : Elo, ro = ro_of(r) - bit0;        /* relative to the staged words */
+        const uint32_t ro = rob;                                             /* relative to the staged words */
         if (once) {
           /* no repetition (E <= Nnn): the run's part below E, then (the one run that straddles the
            * circular buffer's end: a block's wrap tile, scalar test first) its wrapped part at 0 */
@@ -1026,6 +1033,14 @@ static __device__ void encode_codeword(const cfg_dev_t *__restrict__ c, uint32_t
             }
           }
         }
+        if (r2 != r) {
+          bbo = __builtin_amdgcn_readfirstlane(r2 * sw3);
+          E = r2 >= es ? Ehi : Elo;
+          rob = ro_of(r2) - bit0;
+        }
+        ki = k2;
+        r = r2;
+        t0 = t2;
       }
       __syncthreads();
       if (DEBUG) {
