@@ -930,7 +930,6 @@ static __device__ void encode_codeword(const cfg_dev_t *__restrict__ c, uint32_t
     const tp_lane_t tpl = tp_lane(tid & 31);
     const uint32_t sw3 = __builtin_amdgcn_readfirstlane(3 * sw);
     const uint32_t nt0 = __builtin_amdgcn_readfirstlane(cw.ntk[0]), nt1 = __builtin_amdgcn_readfirstlane(cw.ntk[1]);
-    const uint32_t ND0 = __builtin_amdgcn_readfirstlane(cw.NDk[0]), ND1 = __builtin_amdgcn_readfirstlane(cw.NDk[1]);
     const uint32_t Nnn0 = __builtin_amdgcn_readfirstlane(cw.Nnnk[0]), Nnn1 = __builtin_amdgcn_readfirstlane(cw.Nnnk[1]);
     const uint32_t es = __builtin_amdgcn_readfirstlane(cw.esplit[sfi]);
     const uint32_t Elo = __builtin_amdgcn_readfirstlane(cw.E[sfi][0]), Ehi = __builtin_amdgcn_readfirstlane(cw.E[sfi][C - 1]);
@@ -963,7 +962,6 @@ static __device__ void encode_codeword(const cfg_dev_t *__restrict__ c, uint32_t
       for (uint32_t i = tid; i < nwh + 1; i += nth) ebuf[i] = (i == 0 && h) ? carry : 0u;
       __syncthreads();
       const uint32_t pb = pair0(rb0), pe = pair0(rb1), bit0 = 32 * w0;
-      uint32_t nsrc = 1u << 5, ndst = 0;
       /* plan rows of pair (ki, t0): a wave-uniform word offset (scalar) from the plan base, so the
        * loads take an SGPR base and the lane offset, with no vector address arithmetic */
       const uint32_t *rsrc0 = &cw.rm_src[0][0][0], *rdst0 = &cw.rm_dst[0][0][0];
@@ -973,75 +971,86 @@ static __device__ void encode_codeword(const cfg_dev_t *__restrict__ c, uint32_t
       /* round-robin pairs P = pb + wave + k nwaves, stepped rather than decoded: the next pair is
        * nwaves pairs on (2 nwaves tiles), carried over block ends; a block's scalars change only
        * there.  Plan words loaded one pair ahead. */
-      uint32_t P = pb + wave;
-      uint32_t ki = 0, r = 0, t0 = 0;
-      if (P < pe) {
-        decode(P, ki, r, t0);
-        const uint32_t ro = row_of(ki, t0);
-        nsrc = (rsrc0 + ro)[lane];
-        ndst = (rdst0 + ro)[lane];
-      }
-      uint32_t bbo = __builtin_amdgcn_readfirstlane(r * sw3), E = r >= es ? Ehi : Elo, rob = ro_of(r) - bit0;
-      for (; P < pe; P += nwaves) {    /* scalar loop: wave is an SGPR */
-        const uint32_t src = nsrc, dst = ndst;
-        /* the next pair of this wave */
-        uint32_t k2 = ki, r2 = r, t2 = t0 + 2 * nwaves;
-        while (t2 >= 2 * (k2 ? pp1 : pp0)) {
-          t2 -= 2 * (k2 ? pp1 : pp0);
-          r2++;
-          k2 = r2 >= n0 ? 1u : 0u;
-        }
-        if (P + nwaves < pe) {
-          const uint32_t ro = row_of(k2, t2);
+      /* The pair loop, versioned on `once` (wave-uniform, loop-invariant) so that neither version
+       * tests it per pair; a block's scalars (stream offset, E, e offset, Nnn, wrap tile) are
+       * refreshed only when the walk enters the next block. */
+      auto pair_loop = [&](auto ONCE) {
+        uint32_t P = pb + wave;
+        uint32_t ki = 0, r = 0, t0 = 0;
+        uint32_t nsrc = 1u << 5, ndst = 0;
+        if (P < pe) {
+          decode(P, ki, r, t0);
+          const uint32_t ro = row_of(ki, t0);
           nsrc = (rsrc0 + ro)[lane];
           ndst = (rdst0 + ro)[lane];
         }
-        const uint32_t *bb = strm + bbo - 1;                                 /* block streams - 1 word (scalar offset) */
-        const uint32_t *wp = bb + ((src >> 5) & 0x7fffu);
-        uint32_t y = __builtin_amdgcn_alignbit(wp[1], wp[0], src);            /* bits before 0 are NULLs */
-        /* the RM_SRC_LAST lane (row R - 1 of y2, j = Kpi - 1 reads y^(2)_0 at bit 31) needs no
-         * test: its bit 31 is stream-2 position Kpi - ND, which holds d^(2)_0 when ND = 0 (copied
-         * there with the tail bits) and is past the run (a NULL, m excludes it) when ND > 0 */
-        y = transpose32_t<0>(y, tpl);
-        y >>= (dst >> 16) & 31u;                                             /* leading NULLs z */
-        const uint32_t o = dst & 0xffffu, m = __builtin_amdgcn_ubfe(dst, 21, 6);
-        const uint32_t ro = rob;                                             /* relative to the staged words */
-        if (once) {
-          /* no repetition (E <= Nnn): the run's part below E, then (the one run that straddles the
-           * circular buffer's end: a block's wrap tile, scalar test first) its wrapped part at 0 */
-          const int l = min((int)m, (int)E - (int)o);
-          if (l > 0) or_bits2(ebuf, ro + o, y & (0xffffffffu >> (32 - l)));
-          const uint32_t wt = ki ? wrapt1 : wrapt0;
-          if (t0 == wt || t0 + 1 == wt) {
-            asm volatile("" ::: "memory");   /* keeps the lane test below behind the scalar one */
-            if (dst & OAI4G_RM_DST_WRAP) {
-            const uint32_t Nnn = ki ? Nnn1 : Nnn0, ma = Nnn - o;                /* 1 .. m - 1 */
-            const uint32_t l2 = min(m - ma, E);
-            or_bits2(ebuf, ro, (y >> ma) & (0xffffffffu >> (32 - l2)));
+        uint32_t bbo = 0, E = 0, rob = 0, Nnn = 0, wtc = 0;
+        auto enter = [&](uint32_t rr, uint32_t kk) {
+          bbo = __builtin_amdgcn_readfirstlane(rr * sw3);
+          E = rr >= es ? Ehi : Elo;
+          rob = ro_of(rr) - bit0;
+          Nnn = kk ? Nnn1 : Nnn0;
+          wtc = kk ? wrapt1 : wrapt0;
+        };
+        enter(r, ki);
+        for (; P < pe; P += nwaves) {    /* scalar loop: wave is an SGPR */
+          const uint32_t src = nsrc, dst = ndst;
+          /* the next pair of this wave */
+          uint32_t k2 = ki, r2 = r, t2 = t0 + 2 * nwaves;
+          while (t2 >= 2 * (k2 ? pp1 : pp0)) {
+            t2 -= 2 * (k2 ? pp1 : pp0);
+            r2++;
+            k2 = r2 >= n0 ? 1u : 0u;
+          }
+          if (P + nwaves < pe) {
+            const uint32_t ro = row_of(k2, t2);
+            nsrc = (rsrc0 + ro)[lane];
+            ndst = (rdst0 + ro)[lane];
+          }
+          const uint32_t *bb = strm + bbo - 1;                               /* block streams - 1 word (scalar offset) */
+          const uint32_t *wp = bb + ((src >> 5) & 0x7fffu);
+          uint32_t y = __builtin_amdgcn_alignbit(wp[1], wp[0], src);          /* bits before 0 are NULLs */
+          /* the RM_SRC_LAST lane (row R - 1 of y2, j = Kpi - 1 reads y^(2)_0 at bit 31) needs no
+           * test: its bit 31 is stream-2 position Kpi - ND, which holds d^(2)_0 when ND = 0 (copied
+           * there with the tail bits) and is past the run (a NULL, m excludes it) when ND > 0 */
+          y = transpose32_t<0>(y, tpl);
+          y >>= (dst >> 16) & 31u;                                           /* leading NULLs z */
+          const uint32_t o = dst & 0xffffu, m = __builtin_amdgcn_ubfe(dst, 21, 6);
+          const uint32_t ro = rob;                                           /* relative to the staged words */
+          if constexpr (decltype(ONCE)::value) {
+            /* no repetition (E <= Nnn): the run's part below E, then (the one run that straddles
+             * the circular buffer's end: a block's wrap tile, scalar test first) its wrapped part at 0 */
+            const int l = min((int)m, (int)E - (int)o);
+            if (l > 0) or_bits2(ebuf, ro + o, y & (0xffffffffu >> (32 - l)));
+            if (wtc - t0 < 2u) {                                             /* t0 or t0 + 1 is the wrap tile */
+              asm volatile("" ::: "memory");   /* keeps the lane test below behind the scalar one */
+              if (dst & OAI4G_RM_DST_WRAP) {
+                const uint32_t ma = Nnn - o;                                 /* 1 .. m - 1 */
+                const uint32_t l2 = min(m - ma, E);
+                or_bits2(ebuf, ro, (y >> ma) & (0xffffffffu >> (32 - l2)));
+              }
+            }
+          } else if (m) {
+            y &= 0xffffffffu >> (32 - m);
+            /* the run may straddle the wrap back to k0c; E > Nnn repeats the buffer */
+            const uint32_t ma = min(m, Nnn - o);
+            for (uint32_t part = 0; part < 2; part++) {
+              const uint32_t len = part ? m - ma : ma, os = part ? 0u : o;
+              const uint32_t v = part ? (ma < 32 ? y >> ma : 0u) : (ma < 32 ? y & ((1u << ma) - 1u) : y);
+              for (uint32_t x = os; len && x < E; x += Nnn) {                   /* repetition rounds */
+                const uint32_t l = min(len, E - x);
+                or_bits(ebuf, ro + x, v & (0xffffffffu >> (32 - l)));
+              }
             }
           }
-        } else if (m) {
-          y &= 0xffffffffu >> (32 - m);
-          /* the run may straddle the wrap back to k0c; E > Nnn repeats the buffer */
-          const uint32_t Nnn = ki ? Nnn1 : Nnn0, ma = min(m, Nnn - o);
-          for (uint32_t part = 0; part < 2; part++) {
-            const uint32_t len = part ? m - ma : ma, os = part ? 0u : o;
-            const uint32_t v = part ? (ma < 32 ? y >> ma : 0u) : (ma < 32 ? y & ((1u << ma) - 1u) : y);
-            for (uint32_t x = os; len && x < E; x += Nnn) {                     /* repetition rounds */
-              const uint32_t l = min(len, E - x);
-              or_bits(ebuf, ro + x, v & (0xffffffffu >> (32 - l)));
-            }
-          }
+          if (r2 != r) enter(r2, k2);
+          ki = k2;
+          r = r2;
+          t0 = t2;
         }
-        if (r2 != r) {
-          bbo = __builtin_amdgcn_readfirstlane(r2 * sw3);
-          E = r2 >= es ? Ehi : Elo;
-          rob = ro_of(r2) - bit0;
-        }
-        ki = k2;
-        r = r2;
-        t0 = t2;
-      }
+      };
+      if (once) pair_loop(std::true_type{});
+      else pair_loop(std::false_type{});
       __syncthreads();
       if (DEBUG) {
         for (uint32_t k = tid; k < G; k += nth) dbg.e[k] = (uint8_t)((ebuf[k >> 5] >> (k & 31)) & 1u);
