@@ -984,26 +984,33 @@ static __device__ void encode_codeword(const cfg_dev_t *__restrict__ c, uint32_t
           nsrc = (rsrc0 + ro)[lane];
           ndst = (rdst0 + ro)[lane];
         }
-        uint32_t bbo = 0, E = 0, rob = 0, Nnn = 0, wtc = 0;
+        uint32_t bbo = 0, E = 0, rob = 0, Nnn = 0, wtc = 0, tpb = 0, rowb = 0;
         auto enter = [&](uint32_t rr, uint32_t kk) {
           bbo = __builtin_amdgcn_readfirstlane(rr * sw3);
           E = rr >= es ? Ehi : Elo;
           rob = ro_of(rr) - bit0;
           Nnn = kk ? Nnn1 : Nnn0;
           wtc = kk ? wrapt1 : wrapt0;
+          tpb = 2 * (kk ? pp1 : pp0);                                        /* tiles per block (pairs x 2) */
+          rowb = kk * ((OAI4G_RM_TILES + 1) * 32);                           /* the block size's plan rows */
         };
         enter(r, ki);
         for (; P < pe; P += nwaves) {    /* scalar loop: wave is an SGPR */
           const uint32_t src = nsrc, dst = ndst;
-          /* the next pair of this wave */
-          uint32_t k2 = ki, r2 = r, t2 = t0 + 2 * nwaves;
-          while (t2 >= 2 * (k2 ? pp1 : pp0)) {
-            t2 -= 2 * (k2 ? pp1 : pp0);
-            r2++;
-            k2 = r2 >= n0 ? 1u : 0u;
+          /* the next pair of this wave (crossing into later blocks only at a block end) */
+          uint32_t k2 = ki, r2 = r, t2 = t0 + 2 * nwaves, rowb2 = rowb;
+          if (t2 >= tpb) {
+            uint32_t tpb2 = tpb;
+            do {
+              t2 -= tpb2;
+              r2++;
+              k2 = r2 >= n0 ? 1u : 0u;
+              tpb2 = 2 * (k2 ? pp1 : pp0);
+            } while (t2 >= tpb2);
+            rowb2 = k2 * ((OAI4G_RM_TILES + 1) * 32);
           }
           if (P + nwaves < pe) {
-            const uint32_t ro = row_of(k2, t2);
+            const uint32_t ro = __builtin_amdgcn_readfirstlane(rowb2 + t2 * 32);
             nsrc = (rsrc0 + ro)[lane];
             ndst = (rdst0 + ro)[lane];
           }
