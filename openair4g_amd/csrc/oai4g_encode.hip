@@ -746,11 +746,16 @@ static __device__ void encode_codeword(const cfg_dev_t *__restrict__ c, uint32_t
     r = ki ? n0 + rr : rr;
     K = ki ? kk1 : kk0;
   };
+  /* the block's filler bytes, copied bytes and TB offset in closed form (lte_segmentation.c:52-166:
+   * fill F / 8 in block 0 only; every block copies K / 8 - L / 8 bytes less its fill; offsets are
+   * the running sum), so the loop issues no per-lane loads of cw.fill / ncopy / src */
+  const uint32_t L8 = __builtin_amdgcn_readfirstlane(cw.L) >> 3, F8 = __builtin_amdgcn_readfirstlane(cw.F) >> 3;
+  const uint32_t cb0 = (kk0 >> 3) - L8, cb1 = (kk1 >> 3) - L8;
   for (uint32_t i = tid; i < nw; i += nth) {
     uint32_t r, j, K, ki;
     unit_of(i, r, j, K, ki);
-    (void)ki;
-    const uint32_t fill = cw.fill[r], ncopy = cw.ncopy[r], s0 = cw.src[r], i0 = 4 * j;
+    const uint32_t fill = r == 0 ? F8 : 0u, ncopy = (ki ? cb1 : cb0) - fill;
+    const uint32_t s0 = r == 0 ? 0u : (ki ? n0 * cb0 + (r - n0) * cb1 : r * cb0) - F8, i0 = 4 * j;
     uint32_t le;
     if (i0 >= fill && i0 + 4 <= fill + ncopy) {
       const uint32_t a = s0 + i0 - fill, wi = a >> 2;
