@@ -829,9 +829,11 @@ static __device__ void encode_codeword(const cfg_dev_t *__restrict__ c, uint32_t
       uint32_t acc = 0;
 #pragma unroll
       for (int b = 0; b < 8; b++) {
-        const uint32_t e = (ew[b >> 1] >> (16 * (b & 1))) & 0xffffu;
-        const uint32_t D = b8[e & 0x7ffu];
-        acc |= __builtin_amdgcn_alignbit(D, D, e >> 11) & (0x01010101u << b);
+        /* entry: rotate in bits 0-4 (alignbit reads only those), plane word in bits 7-14, so the
+         * word's byte offset is one field extract of bits 5-14 (bits 5-6 are zero) */
+        const uint32_t e = (b & 1) ? ew[b >> 1] >> 16 : ew[b >> 1];
+        const uint32_t D = *(const uint32_t *)((const uint8_t *)b8 + __builtin_amdgcn_ubfe(e, 5, 10));
+        acc |= __builtin_amdgcn_alignbit(D, D, e) & (0x01010101u << b);
       }
       uint32_t a0 = acc & 0xffu, a1 = (acc >> 8) & 0xffu, a2 = (acc >> 16) & 0xffu, a3 = acc >> 24;
       const uint32_t n = Q - 8 * j;

@@ -867,12 +867,13 @@ static int derive_cfg(oai4g_tx_config *cfg, const oai4g_tx_params_t *p, const ui
       }
       c.qpp_d2[ki] = (uint32_t)((2 * f2) % K);
       memset(c.qpp_tab[ki], 0, sizeof(c.qpp_tab[ki]));
-      /* entry k: plane word xp/8 and the rotate that lands bit (8u + xp%8) of it at bit k%8 of
-       * each byte (the walk's step index is folded into the rotate, so the kernel needs no shift) */
+      /* entry k: plane word xp/8 (bits 7-14) and the rotate (bits 0-4) that lands bit (8u + xp%8) of
+       * it at bit k%8 of each byte (the walk's step index is folded into the rotate, so the kernel
+       * needs no shift) */
       for (uint64_t k = 0; k < K / 4; k++) {
         const uint32_t x = (uint32_t)((f1 * k + f2 * k * k) % K), Q = K / 4, xp = x % Q, u = x / Q;
         const uint32_t rot = (8 * u + (xp & 7) + 32 - (uint32_t)(k & 7)) & 31u;
-        c.qpp_tab[ki][k >> 1] |= ((xp >> 3) | (rot << 11)) << (16 * (k & 1));
+        c.qpp_tab[ki][k >> 1] |= (((xp >> 3) << 7) | rot) << (16 * (k & 1));
       }
       c.qpp_s3[ki] = (uint32_t)((f1 * (K / 4)) % K) == K / 4 ? 0u : 1u;
     }
