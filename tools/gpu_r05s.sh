@@ -1,5 +1,5 @@
 #!/bin/bash
-# round 5: QPP gather table entries repacked (rotate bits 0-4, word bits 7-14) — encoder parity subset + C3 A/B vs abvar/base (previous commit)
+# round 5: segmentation loop block-uniform (scalar block parameters) — encoder parity subset + C3 A/B vs abvar/base (previous commit)
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
 mkdir -p gpurun_out
