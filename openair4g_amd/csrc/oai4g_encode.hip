@@ -757,9 +757,18 @@ static __device__ void encode_codeword(const cfg_dev_t *__restrict__ c, uint32_t
     const uint32_t fill = r == 0 ? F8 : 0u, ncopy = (ki ? cb1 : cb0) - fill;
     const uint32_t s0 = r == 0 ? 0u : (ki ? n0 * cb0 + (r - n0) * cb1 : r * cb0) - F8, i0 = 4 * j;
     uint32_t le;
-    if (i0 >= fill && i0 + 4 <= fill + ncopy) {
+    if (i0 >= fill) {
+      /* the data bytes as one unaligned read; a block's last word (or two) also takes the CRC-24B
+       * bytes from byte sh = fill + ncopy - i0 on, spliced in without a byte loop (bytes past the
+       * block are masked off below) */
       const uint32_t a = s0 + i0 - fill, wi = a >> 2;
       le = __builtin_amdgcn_alignbit(tbw[wi + 1], tbw[wi], (a & 3u) * 8u);
+      const int sh = (int)(fill + ncopy) - (int)i0;
+      if (C > 1 && sh < 4) {                                   /* sh in [-2, 3] */
+        const uint32_t crcle = __builtin_bswap32(crcs[1 + r] << 8);   /* CRC bytes MSB first */
+        const uint32_t cw32 = (uint32_t)(((uint64_t)crcle << (8 * (sh + 4))) >> 32);
+        le = (sh > 0 ? le & (0xffffffffu >> (32 - 8 * sh)) : 0u) | cw32;
+      }
     } else {
       const uint32_t crcb = C > 1 ? crcs[1 + r] : 0;
       le = 0;
