@@ -696,12 +696,15 @@ static __device__ void encode_codeword(const cfg_dev_t *__restrict__ c, uint32_t
       tbb[Ab] = (uint8_t)(crc >> 16);
       tbb[Ab + 1] = (uint8_t)(crc >> 8);
       tbb[Ab + 2] = (uint8_t)crc;
-      /* the TB-CRC bytes inside the last block, folded into its CRC-24B */
-      for (uint32_t r = 0; r < C; r++) {
-        uint32_t s0 = cw.src[r], e0 = s0 + cw.ncopy[r], reg = crcs[1 + r];
-        for (uint32_t i = (s0 > Ab ? s0 : Ab); i < e0; i++) reg = ((reg << 8) & 0xffffffu) ^ c->crctab[1][((reg >> 16) ^ tbb[i]) & 0xffu];
-        crcs[1 + r] = reg;
-      }
+      /* the TB-CRC bytes end the last block's data (lte_segmentation.c: the last block copies the
+       * TB through its CRC-24A), folded into its CRC-24B through the reflected LDS table
+       * (crc_chunk_w2r's register form) */
+      uint32_t a = __builtin_bitreverse32(crcs[C] << 8) << 2;
+      const uint8_t *r2b = (const uint8_t *)crctab_b;
+      a = (a >> 8) ^ *(const uint32_t *)(r2b + ((a ^ (__builtin_bitreverse32(crc >> 16) >> 22)) & 0x3fcu));
+      a = (a >> 8) ^ *(const uint32_t *)(r2b + ((a ^ (__builtin_bitreverse32((crc >> 8) & 0xffu) >> 22)) & 0x3fcu));
+      a = (a >> 8) ^ *(const uint32_t *)(r2b + ((a ^ (__builtin_bitreverse32(crc & 0xffu) >> 22)) & 0x3fcu));
+      crcs[C] = __builtin_bitreverse32(a >> 2) >> 8;
     }
   } else {
     uint32_t reg = crc_chunk_w(tbw, 0, Ab, cw.crc_per_tb, tid, nth, crctab_a);
@@ -725,11 +728,6 @@ static __device__ void encode_codeword(const cfg_dev_t *__restrict__ c, uint32_t
   /* stream words past the data of each block (tail bits, read-ahead; region B held the CRC tables
    * until here); the data words are fully written by segmentation (systematic) and the phase-3
    * planes / turbo (parity) */
-  for (uint32_t i = tid; i < C * 3 * 4; i += nth) {
-    const uint32_t slot = i >> 2, r = slot / 3;
-    const uint32_t w = ((cw.K[r] + 31) >> 5) + (i & 3u);
-    if (w < sw) strm[slot * sw + w] = 0u;
-  }
   /* ---- phase 2: segmentation -> systematic streams (LSB-first words), one word per thread over
    * the words of all blocks; a word inside the copied bytes is one unaligned 4-byte read ---- */
   const uint32_t nw = cw.ilv_off[C], u0 = cw.u0, n0 = cw.n0;
@@ -738,6 +736,11 @@ static __device__ void encode_codeword(const cfg_dev_t *__restrict__ c, uint32_t
   const uint32_t kw0 = __builtin_amdgcn_readfirstlane(cw.kw[0]), kw1 = __builtin_amdgcn_readfirstlane(cw.kw[1]);
   const uint32_t km0 = __builtin_amdgcn_readfirstlane(cw.kmag[0]), km1 = __builtin_amdgcn_readfirstlane(cw.kmag[1]);
   const uint32_t kk0 = __builtin_amdgcn_readfirstlane(cw.kk[0]), kk1 = __builtin_amdgcn_readfirstlane(cw.kk[1]);
+  for (uint32_t i = tid; i < C * 3 * 4; i += nth) {
+    const uint32_t slot = i >> 2, r = slot / 3;
+    const uint32_t w = (r < n0 ? kw0 : kw1) + (i & 3u);
+    if (w < sw) strm[slot * sw + w] = 0u;
+  }
   auto unit_of = [&](uint32_t i, uint32_t &r, uint32_t &j, uint32_t &K, uint32_t &ki) {
     ki = i >= u0 ? 1u : 0u;
     const uint32_t ii = ki ? i - u0 : i, kw = ki ? kw1 : kw0;
@@ -911,8 +914,9 @@ static __device__ void encode_codeword(const cfg_dev_t *__restrict__ c, uint32_t
   }
 
   /* append the 4 tail bits of each constituent stream at bit K (d^(s)_K..K+3) */
+  const uint32_t nd0 = __builtin_amdgcn_readfirstlane(cw.NDk[0]), nd1 = __builtin_amdgcn_readfirstlane(cw.NDk[1]);
   for (uint32_t r = tid; r < C; r += nth) {
-    uint32_t K = cw.K[r];
+    const uint32_t K = r < n0 ? kk0 : kk1, ND = r < n0 ? nd0 : nd1;
     uint32_t *blk = strm + r * 3 * sw;
     for (uint32_t s = 0; s < 3; s++) {
       uint32_t t4 = tail_bit(tails, r, s) | (tail_bit(tails, r, 3 + s) << 1) | (tail_bit(tails, r, 6 + s) << 2) |
@@ -923,7 +927,7 @@ static __device__ void encode_codeword(const cfg_dev_t *__restrict__ c, uint32_t
     }
     /* phase 4's RM_SRC_LAST lane reads y^(2)_0 = d^(2)_0 at stream-2 position Kpi - ND = K + 4
      * when ND = 0: the reference's own d[3D + 2] = d[2] copy (lte_rate_matching.c:74-75) in stream form */
-    if (cw.ND[r] == 0) blk[2 * sw + ((K + 4) >> 5)] |= (blk[2 * sw] & 1u) << ((K + 4) & 31u);
+    if (ND == 0) blk[2 * sw + ((K + 4) >> 5)] |= (blk[2 * sw] & 1u) << ((K + 4) & 31u);
   }
   __syncthreads();
 

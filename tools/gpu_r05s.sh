@@ -1,5 +1,5 @@
 #!/bin/bash
-# round 5: CRC-24B bytes spliced into the block-end words (no byte loop) — encoder parity subset + C3 A/B vs abvar/base (previous commit)
+# round 5: closed-form K / ND in the stream-zeroing and tail loops, CRC fold through the LDS table — encoder parity subset + C3 A/B vs abvar/base (previous commit)
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
 mkdir -p gpurun_out
