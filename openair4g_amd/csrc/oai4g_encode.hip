@@ -636,6 +636,25 @@ static __device__ void encode_codeword(const cfg_dev_t *__restrict__ c, uint32_t
   uint8_t *tbb = (uint8_t *)tbw;
   const uint32_t G = cw.G[sfi];
 
+  /* block geometry as wave-uniform scalars: n0 blocks of size kk0 (kw0 words) then blocks of size
+   * kk1; word i of the interleaved space -> block r, word j, block size K without per-lane table
+   * walks */
+  const uint32_t nw = cw.ilv_off[C], u0 = cw.u0, n0 = cw.n0;
+  const uint32_t kw0 = __builtin_amdgcn_readfirstlane(cw.kw[0]), kw1 = __builtin_amdgcn_readfirstlane(cw.kw[1]);
+  const uint32_t km0 = __builtin_amdgcn_readfirstlane(cw.kmag[0]), km1 = __builtin_amdgcn_readfirstlane(cw.kmag[1]);
+  const uint32_t kk0 = __builtin_amdgcn_readfirstlane(cw.kk[0]), kk1 = __builtin_amdgcn_readfirstlane(cw.kk[1]);
+  /* the block's filler bytes, copied bytes and TB offset in closed form (lte_segmentation.c:52-166:
+   * fill F / 8 in block 0 only; every block copies K / 8 - L / 8 bytes less its fill; offsets are
+   * the running sum): no per-lane loads of cw.fill / ncopy / src ahead of a barrier */
+  const uint32_t L8 = __builtin_amdgcn_readfirstlane(cw.L) >> 3, F8 = __builtin_amdgcn_readfirstlane(cw.F) >> 3;
+  const uint32_t cb0 = (kk0 >> 3) - L8, cb1 = (kk1 >> 3) - L8;
+  auto seg_of = [&](uint32_t r, uint32_t &fill, uint32_t &ncopy, uint32_t &s0) {
+    const uint32_t ki = r >= n0 ? 1u : 0u;
+    fill = r == 0 ? F8 : 0u;
+    ncopy = (ki ? cb1 : cb0) - fill;
+    s0 = r == 0 ? 0u : (ki ? n0 * cb0 + (r - n0) * cb1 : r * cb0) - F8;
+  };
+
   /* ---- phase 0: TB bytes, stream words past each block's data, tables ---- */
   const uint8_t *src = payload + (size_t)(DEBUG ? 0 : (sf * c->n_cw + cwi)) * c->payload_stride;
   const uint32_t Ab = cw.A_bytes;
@@ -680,7 +699,8 @@ static __device__ void encode_codeword(const cfg_dev_t *__restrict__ c, uint32_t
     const uint32_t lpb = __builtin_amdgcn_readfirstlane(cw.crc_lpb), per = __builtin_amdgcn_readfirstlane(cw.crc_per_cb);
     const uint32_t pos = tid & (lpb - 1);
     for (uint32_t r = tid / lpb; r < C; r += nth / lpb) {
-      uint32_t s0 = cw.src[r], n = cw.ncopy[r];
+      uint32_t fill, n, s0;
+      seg_of(r, fill, n, s0);
       if (s0 + n > Ab) n = Ab > s0 ? Ab - s0 : 0;
       uint32_t ra, rb;
       crc_chunk_w2r(tbw, s0, n, per, pos, lpb, (const uint8_t *)crctab_a, (const uint8_t *)crctab_b, ra, rb);
@@ -730,12 +750,6 @@ static __device__ void encode_codeword(const cfg_dev_t *__restrict__ c, uint32_t
    * planes / turbo (parity) */
   /* ---- phase 2: segmentation -> systematic streams (LSB-first words), one word per thread over
    * the words of all blocks; a word inside the copied bytes is one unaligned 4-byte read ---- */
-  const uint32_t nw = cw.ilv_off[C], u0 = cw.u0, n0 = cw.n0;
-  /* word i of the interleaved space -> block r, word j, block size K (no per-lane table walks;
-   * the two block sizes are read once as wave-uniform values, selects stay in registers) */
-  const uint32_t kw0 = __builtin_amdgcn_readfirstlane(cw.kw[0]), kw1 = __builtin_amdgcn_readfirstlane(cw.kw[1]);
-  const uint32_t km0 = __builtin_amdgcn_readfirstlane(cw.kmag[0]), km1 = __builtin_amdgcn_readfirstlane(cw.kmag[1]);
-  const uint32_t kk0 = __builtin_amdgcn_readfirstlane(cw.kk[0]), kk1 = __builtin_amdgcn_readfirstlane(cw.kk[1]);
   for (uint32_t i = tid; i < C * 3 * 4; i += nth) {
     const uint32_t slot = i >> 2, r = slot / 3;
     const uint32_t w = (r < n0 ? kw0 : kw1) + (i & 3u);
@@ -749,16 +763,12 @@ static __device__ void encode_codeword(const cfg_dev_t *__restrict__ c, uint32_t
     r = ki ? n0 + rr : rr;
     K = ki ? kk1 : kk0;
   };
-  /* the block's filler bytes, copied bytes and TB offset in closed form (lte_segmentation.c:52-166:
-   * fill F / 8 in block 0 only; every block copies K / 8 - L / 8 bytes less its fill; offsets are
-   * the running sum), so the loop issues no per-lane loads of cw.fill / ncopy / src */
-  const uint32_t L8 = __builtin_amdgcn_readfirstlane(cw.L) >> 3, F8 = __builtin_amdgcn_readfirstlane(cw.F) >> 3;
-  const uint32_t cb0 = (kk0 >> 3) - L8, cb1 = (kk1 >> 3) - L8;
   for (uint32_t i = tid; i < nw; i += nth) {
     uint32_t r, j, K, ki;
     unit_of(i, r, j, K, ki);
-    const uint32_t fill = r == 0 ? F8 : 0u, ncopy = (ki ? cb1 : cb0) - fill;
-    const uint32_t s0 = r == 0 ? 0u : (ki ? n0 * cb0 + (r - n0) * cb1 : r * cb0) - F8, i0 = 4 * j;
+    uint32_t fill, ncopy, s0;
+    seg_of(r, fill, ncopy, s0);
+    const uint32_t i0 = 4 * j;
     uint32_t le;
     if (i0 >= fill) {
       /* the data bytes as one unaligned read; a block's last word (or two) also takes the CRC-24B
@@ -876,7 +886,8 @@ static __device__ void encode_codeword(const cfg_dev_t *__restrict__ c, uint32_t
   for (uint32_t seg = wave; seg < 2 * C; seg += nwaves) {
     const uint32_t r = seg >> 1, e = seg & 1u;
     uint32_t *blk = strm + r * 3 * sw;
-    turbo_segment(e ? ilv + cw.ilv_off[r] : blk, blk + (1 + e) * sw, cw.K[r], &tails[2 * r + e], tabs);
+    const uint32_t io = r < n0 ? r * kw0 : u0 + (r - n0) * kw1;
+    turbo_segment(e ? ilv + io : blk, blk + (1 + e) * sw, r < n0 ? kk0 : kk1, &tails[2 * r + e], tabs);
   }
   __syncthreads();
   if (stop_phase <= 3) return;
