@@ -1,5 +1,5 @@
 #!/bin/bash
-# round 5: first plan words loaded ahead of the RM zeroing barrier — encoder parity subset + C3 A/B vs abvar/base (previous commit)
+# round 5: LDS-only barriers + first QPP gather entries loaded ahead of the plane build — encoder parity subset + C3 A/B vs abvar/base (previous commit)
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
 mkdir -p gpurun_out
