@@ -87,6 +87,13 @@ def build_oracle(verbose=False):
                    stdout=None if verbose else subprocess.DEVNULL)
 
 
+def build_shim(verbose=False):
+    """integration/liboai4g_shim.so: the reference-side boundary compiled against the reference's own
+    headers (only where /root/reference exists; the built .so travels with the tree)."""
+    subprocess.run(["make", "-s", "-C", os.path.join(ROOT, "integration")], check=True,
+                   stdout=None if verbose else subprocess.DEVNULL)
+
+
 if __name__ == "__main__":
     if "--variant" in sys.argv:   # build.py --variant NAME -DFOO=1 [-mllvm X] ... -> variants/NAME/libopenair4g_amd.so
         i = sys.argv.index("--variant")
@@ -99,4 +106,5 @@ if __name__ == "__main__":
     build_lib(force="--force" in sys.argv, verbose=True)
     build_host_tools(verbose=True)
     build_oracle(verbose=True)
+    build_shim(verbose=True)
     print("built", LIB)

@@ -1112,3 +1112,35 @@ def ref_fo():
                                                ctypes.POINTER(ctypes.c_int), ctypes.c_int]
         _reffo = L
     return _reffo
+
+
+REF_TD_SO = os.path.join(ORACLE_DIR, "_ref", "libref_td.so")
+_reftd = None
+
+
+def ref_td():
+    """PHY/CODING/3gpplte_turbo_decoder.c compiled unmodified (the reference's scalar max-log-MAP
+    decoder, phy_threegpplte_turbo_decoder_scalar :883), its CRCs from libref_coding.so (initialised
+    by ref_coding()), or None when it was not built here."""
+    global _reftd
+    if _reftd is None:
+        if not os.path.exists(REF_TD_SO) or ref_coding() is None:
+            return None
+        L = ctypes.CDLL(REF_TD_SO)
+        L.phy_threegpplte_turbo_decoder_scalar.restype = U8
+        L.phy_threegpplte_turbo_decoder_scalar.argtypes = [VP, VP, U16, U16, U16, U8, U8, U8, U8]
+        _reftd = L
+    return _reftd
+
+
+def ref_turbo_decode_scalar(y, K, f1, f2, max_it=8, crc_type=1, F=0):
+    """phy_threegpplte_turbo_decoder_scalar(y, decoded, n = K, f1, f2, max_it, crc_type, F, 0).
+    y: int16 LLRs in the order the decoder reads them (:929-960): (x, z, z') for k < K, then (x, z) x 3
+    and (x', z') x 3 -- the d[96 ...] layout, positive = bit 1 (:1019).  Returns (iterations, K/8 bytes);
+    iterations = max_it + 1 means the CRC never matched (:1075)."""
+    n = 3 * K + 12
+    ya = _aligned(n + 64, np.int16)
+    ya[:n] = np.asarray(y, np.int16)[:n]
+    out = _aligned(K // 8 + 16, np.uint8)       # the CRC test reads an unsigned int at K/8 - 3 (:1028)
+    it = ref_td().phy_threegpplte_turbo_decoder_scalar(P(ya), P(out), K, f1, f2, max_it, crc_type, F, 0)
+    return int(it), out[:K // 8].copy()

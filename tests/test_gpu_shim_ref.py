@@ -1,0 +1,161 @@
+"""The reference-side boundary, compiled and run: integration/liboai4g_shim.so (integration/oai4g_shim.c
+built against the reference's own headers by integration/Makefile, linked to libopenair4g_amd.so) is
+called under the reference's names with the reference's own LTE_DL_FRAME_PARMS / LTE_eNB_DLSCH_t /
+LTE_DL_eNB_HARQ_t (laid out by oracle/ref_glue_shim.c, allocated as new_eNB_dlsch does), in dlsim's
+order (dlsim.c:2567-2696): dlsch_encoding -> dlsch_scrambling -> dlsch_modulation -> do_OFDM_mod.
+Everything it writes into those structs is checked against the reference's own TUs, live:
+
+  - dlsch_encoding (proto.h:110): the CRC24_A appended into the caller's `a` (crc_byte.c), harq->{B, C,
+    Cplus, Cminus, Kplus, Kminus, F} and every c[r] (lte_segmentation.c), RTC[r] and w[r]
+    (sub_block_interleaving_turbo on the shim's own d[r]), e (lte_rate_matching_turbo on that w, per
+    block), and -- for multi-block transport blocks -- d[r] decoded by the reference's scalar turbo
+    decoder with the systematic stream removed (tests/td_ref_cases.py);
+  - dlsch_scrambling (proto.h:1600): e against dlsch_scrambling.c on the pre-scrambling e;
+  - dlsch_modulation (proto.h:197): the return value and every frame grid against dlsch_modulation.c;
+  - do_OFDM_mod (MODULATION/defs.h:90): both slots' IQ against ofdm_mod.c + lte_dfts.c on that grid.
+Configurations C1 / C2 / C3 / TM2 at subframes 0, 5 and 7 (PBCH / PSS / SSS exclusions at 0 and 5)."""
+import ctypes
+import os
+
+import numpy as np
+import pytest
+
+import oracle_lib as O
+import seg_ofdm_ref_cases as SC
+import td_ref_cases as TC
+from ref_cases import QPP
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+SHIM_SO = os.path.join(ROOT, "integration", "liboai4g_shim.so")
+GLUE_SO = os.path.join(O.ORACLE_DIR, "_ref", "libref_shimglue.so")
+LIVE = (os.path.exists(SHIM_SO) and os.path.exists(GLUE_SO) and O.ref_seg() is not None and O.ref_rm() is not None
+        and O.ref_mod() is not None and O.ref_ofdm() is not None and O.ref_td() is not None)
+pytestmark = [pytest.mark.gpu, pytest.mark.skipif(not LIVE, reason="integration/liboai4g_shim.so or oracle/_ref "
+                                                                   "not built (needs the reference tree)")]
+VP, U8, U16, U32, I32 = ctypes.c_void_p, ctypes.c_uint8, ctypes.c_uint16, ctypes.c_uint32, ctypes.c_int32
+
+
+@pytest.fixture(scope="module")
+def shim(gpu):
+    S = ctypes.CDLL(SHIM_SO, mode=os.RTLD_LOCAL)
+    S.dlsch_encoding.restype = I32
+    S.dlsch_encoding.argtypes = [VP, VP, U8, VP, ctypes.c_int, U8, VP, VP, VP]
+    S.dlsch_scrambling.restype = None
+    S.dlsch_scrambling.argtypes = [VP, ctypes.c_int, VP, ctypes.c_int, U8, U8]
+    S.dlsch_modulation.restype = I32
+    S.dlsch_modulation.argtypes = [ctypes.POINTER(VP), ctypes.c_int16, U32, VP, U8, VP, VP]
+    S.do_OFDM_mod.restype = None
+    S.do_OFDM_mod.argtypes = [ctypes.POINTER(VP), ctypes.POINTER(VP), U32, U16, VP]
+    G = ctypes.CDLL(GLUE_SO, mode=os.RTLD_LOCAL)
+    G.ref_shim_frame.restype = VP
+    G.ref_shim_frame.argtypes = [VP]
+    G.ref_shim_free.argtypes = [VP]
+    G.ref_shim_new_dlsch.restype = VP
+    G.ref_shim_new_dlsch.argtypes = [U8, U8, U8]
+    G.ref_shim_free_dlsch.argtypes = [VP]
+    G.ref_shim_set.argtypes = [VP, VP]
+    G.ref_shim_get.argtypes = [VP, VP]
+    G.ref_shim_buf.restype = VP
+    G.ref_shim_buf.argtypes = [VP, ctypes.c_int, ctypes.c_int]
+    G.ref_shim_sizes.restype = U32
+    return S, G
+
+
+def _view(G, dl, which, n, r=0, dtype=np.uint8):
+    p = G.ref_shim_buf(dl, which, r)
+    return np.ctypeslib.as_array(ctypes.cast(p, ctypes.POINTER(ctypes.c_uint8)), shape=(n,)).view(dtype)
+
+
+def _ptrs(arrs):
+    return (VP * len(arrs))(*[a.ctypes.data for a in arrs])
+
+
+CASES = [(n, sf) for n in ("C1", "C2", "C3", "TM2") for sf in (0, 5, 7)]
+
+
+@pytest.mark.parametrize("name,subframe", CASES)
+def test_reference_boundary_in_dlsim_order(gpu, shim, name, subframe):
+    S, G = shim
+    p = gpu.make_params(name, subframe=subframe)
+    ofp = gpu.frame_parms(p.N_RB_DL, p.Nid_cell, p.Ncp, p.nb_antennas_tx, p.mode1_flag, 0)
+    f = np.array([ofp.N_RB_DL, ofp.Nid_cell, ofp.Ncp, ofp.nushift, ofp.mode1_flag, ofp.nb_antennas_tx,
+                  ofp.nb_antennas_tx_eNB or ofp.nb_antennas_tx, ofp.frame_type, ofp.tdd_config, ofp.symbols_per_tti,
+                  ofp.log2_symbol_size, ofp.ofdm_symbol_size, ofp.first_carrier_offset, ofp.nb_prefix_samples,
+                  ofp.nb_prefix_samples0, ofp.samples_per_tti, ofp.phich_resource, ofp.phich_duration,
+                  ofp.Nid_cell_mbsfn, 1], np.int32)
+    rfp = G.ref_shim_frame(f.ctypes.data)
+    orc_fp = O.frame(p.N_RB_DL, p.Nid_cell, p.Ncp, p.nb_antennas_tx, p.mode1_flag, 0)
+    pay = SC.bench_payload(0xB0D1 + subframe, 1, p.n_cw, p.payload_stride)[0]
+    dls, es, cws = [], [], []
+    try:
+        for cw in range(p.n_cw):
+            dl = G.ref_shim_new_dlsch(p.Kmimo, 8, p.N_RB_DL)
+            dls.append(dl)
+            TBS, mcs = p.TBS[cw], p.mcs[cw]
+            Qm = 2 if mcs < 10 else 4 if mcs < 17 else 6
+            v = np.array([p.rnti, TBS, mcs, 0, 0, p.mimo_mode, 1, p.nb_rb, *[p.rb_alloc[i] for i in range(4)],
+                          p.sqrt_rho_a, p.sqrt_rho_b, 1, 0], np.int32)
+            G.ref_shim_set(dl, v.ctypes.data)
+            a = np.zeros(TBS // 8 + 16, np.uint8)
+            a[:TBS // 8] = pay[cw][:TBS // 8]
+            assert S.dlsch_encoding(a.ctypes.data, rfp, p.num_pdcch_symbols, dl, 0, subframe, None, None, None) == 0
+            # CRC24_A appended into the caller's buffer (dlsch_coding.c:296-300)
+            crc = O.ref_crc(pay[cw][:TBS // 8], TBS, "24a") >> 8
+            assert list(a[TBS // 8:TBS // 8 + 3]) == [crc >> 16, (crc >> 8) & 255, crc & 255]
+            # segmentation fields and c[r] (lte_segmentation.c)
+            out = np.zeros(23, np.uint32)
+            G.ref_shim_get(dl, out.ctypes.data)
+            B = TBS + 24
+            ret, seg, bufs = O.ref_segmentation(B, a[:B // 8])
+            assert ret == 0 and out[0] == B and tuple(int(x) for x in out[1:7]) == seg, (out[:7], seg)
+            C, Cplus, Cminus, Kplus, Kminus, F = seg
+            assert F == 0
+            Gbits = gpu.get_G(ofp, p.nb_rb, [p.rb_alloc[i] for i in range(4)], Qm, 1, p.num_pdcch_symbols, subframe)
+            e = _view(G, dl, 4, Gbits).copy()
+            e_ref = []
+            for r in range(C):
+                K = Kminus if r < Cminus else Kplus
+                D = K + 4
+                assert np.array_equal(_view(G, dl, 1, K // 8, r), bufs[r][:K // 8]), (name, cw, r)
+                d = _view(G, dl, 2, 96 + 3 * D, r)
+                R, w_ref = O.ref_subblock(d[96:].copy(), D)[:2]
+                assert out[7 + r] == R
+                assert np.array_equal(_view(G, dl, 3, 3 * 32 * R, r), w_ref), (name, cw, r)
+                e_ref.append(O.ref_rate_match(R, Gbits, w_ref, C, r, Qm, Nl=1, Kmimo=p.Kmimo))
+                if C > 1:    # CRC24_B blocks: the reference's scalar decoder, systematic stream removed
+                    c = _view(G, dl, 1, K // 8, r).copy()
+                    for var in ("z_only", "zp_only"):
+                        it, dec = TC.decode(TC.variant(d[96:], K, var), K, 1)
+                        assert it <= TC.MAX_IT and np.array_equal(dec, c), (name, cw, r, var)
+            assert np.array_equal(e, np.concatenate(e_ref)), (name, cw)
+            # dlsch_scrambling (dlsch_scrambling.c:51) in place on harq->e
+            n = 32 * (1 + (Gbits >> 5))
+            want = O.ref_scrambling(_view(G, dl, 4, n).copy(), Gbits, p.rnti, p.Nid_cell, p.q[cw], 2 * subframe)
+            S.dlsch_scrambling(rfp, 0, dl, Gbits, p.q[cw], 2 * subframe)
+            got = _view(G, dl, 4, n).copy()
+            assert np.array_equal(got, want), (name, cw)
+            es.append(got)
+            cws.append(dict(e=np.concatenate([got, np.zeros(14 * 1200 * 6, np.uint8)]), mcs=mcs,
+                            mimo_mode=p.mimo_mode, rb_alloc=[p.rb_alloc[i] for i in range(4)]))
+        # dlsch_modulation over frame grids (+= into the caller's zeroed txdataF)
+        N, spt, na = ofp.ofdm_symbol_size, ofp.samples_per_tti, ofp.nb_antennas_tx
+        grids = [np.zeros(10 * 14 * N, np.int32) for _ in range(na)]
+        ret = S.dlsch_modulation(_ptrs(grids), p.amp, subframe, rfp, p.num_pdcch_symbols, dls[0],
+                                 dls[1] if len(dls) > 1 else None)
+        ret_ref, grids_ref = O.ref_modulation(orc_fp, p.amp, subframe, p.num_pdcch_symbols, cws)
+        assert ret == ret_ref and ret > 0
+        for a in range(na):
+            assert np.array_equal(grids[a], grids_ref[a]), (name, a)
+        # do_OFDM_mod, both slots of the subframe, into frame buffers
+        outs = [np.zeros(10 * spt + 64, np.int32) for _ in range(na)]
+        outs_ref = [o.copy() for o in outs]
+        for slot in (2 * subframe, 2 * subframe + 1):
+            S.do_OFDM_mod(_ptrs(grids), _ptrs(outs), 0, slot, rfp)
+            outs_ref = list(SC.ref_impl(O)["do_ofdm"](grids, outs_ref, 0, slot, orc_fp).reshape(na, -1))
+        for a in range(na):
+            assert np.array_equal(outs[a][:10 * spt], outs_ref[a][:10 * spt]), (name, a)
+            assert np.any(outs[a][subframe * spt:(subframe + 1) * spt])
+    finally:
+        for dl in dls:
+            G.ref_shim_free_dlsch(dl)
+        G.ref_shim_free(rfp)

@@ -4,7 +4,8 @@ to the GPU binding with no other change.  Checked here against the prototypes in
 headers (PHY/**/*.h, or the defining .c file when no header declares it; read as text, when the
 reference tree is present): the
 return type (exactly) and every parameter type, after normalising whitespace, parameter names and the
-`const` the reference omits.  (The shim's bodies need the asn1c-generated headers to compile, so
+`const` the reference omits.  (oai4g_shim.c also compiles and runs against the reference's headers: tests/test_gpu_shim_ref.py; the
+PHY_VARS_* bindings of oai4g_shim_ue.c need the asn1c-generated headers to compile, so
 this is the check of the boundary that runs here; test_integration_cpu.py checks the oai4g_ side.)"""
 import glob
 import os
@@ -15,6 +16,7 @@ import pytest
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 REF = "/root/reference/openair1"
 SHIM = os.path.join(ROOT, "integration", "oai4g_shim.c")
+SHIM_UE = os.path.join(ROOT, "integration", "oai4g_shim_ue.c")    # the PHY_VARS_* bindings
 
 # other spellings of the same types (module_id_t: openair2/COMMON/platform_types.h:70; the header
 # declares lte_dl_channel_estimation's eNB_id as module_id_t, its definition as uint8_t)
@@ -52,7 +54,7 @@ def _params(args):
 
 
 def _shim_functions():
-    s = _strip(open(SHIM).read())
+    s = _strip(open(SHIM).read() + "\n" + open(SHIM_UE).read())
     fns = {}
     for ret, name, args in re.findall(r"^(?!static)([A-Za-z_][\w \*]*?)\b(\w+)\(([^;{]*?)\)\s*\{", s, flags=re.M):
         fns[name] = (_norm_type(ret), _params(args))
