@@ -1132,7 +1132,13 @@ static int upload_remap(oai4g_tx_config *cfg)
           if (code < OAI4G_CTL_CODE) code = (uint16_t)((code & 0x8000u) | ((code & 0x3FFFu) << 1));
 #endif
           both[n + sl * N + t * 16 + k] = code;
+#if OAI4G_MOD_STAGE
           both[2 * n + sl * N + t * 16 + k] = code < OAI4G_CTL_CODE ? code : sentinel;
+#else
+          /* the unstaged modulator tests code < OAI4G_CTL_CODE itself: keep the non-data codes */
+          (void)sentinel;
+          both[2 * n + sl * N + t * 16 + k] = code;
+#endif
         }
     HCK(hipMalloc(&cfg->d_remap, both.size() * 2), -1);
     HCK(hipMemcpy(cfg->d_remap, both.data(), both.size() * 2, hipMemcpyHostToDevice), -1);
