@@ -193,32 +193,37 @@ C5_K, C5_CB = 5504, 8          # UL 100 PRB MCS 20: TBS 43816 -> C = 8 blocks of
 # layout), so 2048 subframes are exactly 2 waves per SIMD and leave the serial recursions' latency
 # exposed; throughput rises with the number of rounds a launch holds (k_td16 at 3 waves per SIMD,
 # profiles/c5_batch_r05.txt): 2048 -> 236 k, 8192 -> 246 k, 16384 -> 266 k, 24576 -> 275 k,
-# 32768 -> 280 k, 49152 -> 283 k subframes/s.  49152 subframes = 393 216 code blocks, 13 GB of LLRs.
+# 32768 -> 280 k, 49152 -> 283 k subframes/s.  49152 subframes = 393 216 code blocks, 13 GB of LLRs on
+# the device, tiled from C5_BASE host rows (c5_llrs, upload_tiled).
 C5_BATCH = 49152
 
 
-def c5_llrs(n_cb, mode, seed):
-    """Decoder inputs (3K+12 int16 per block): "8it" = unstructured LLRs, every CRC check fails,
-    the full 8 iterations run (SURVEY 8d C5 "8 iterations fixed"); "snr" = CRC-terminated
-    codewords, BPSK amplitude 32 + Gaussian noise sigma 28 (early stop)."""
+C5_BASE = 64                   # distinct code blocks per batch, tiled (no full host copy: ADVICE r05)
+
+
+def c5_llrs(mode, seed, n=C5_BASE):
+    """n distinct decoder inputs (3K+12 int16 each); a batch tiles them (block i = row i % n,
+    TurboDecoderBatch.upload_tiled).  "8it" = unstructured LLRs, every CRC check fails, the full 8
+    iterations run (SURVEY 8d C5 "8 iterations fixed"); "snr" = CRC-terminated codewords, BPSK
+    amplitude 32 + Gaussian noise sigma 28 (early stop)."""
     import numpy as np
     rng = np.random.default_rng(seed)
     if mode == "8it":
-        return rng.integers(-40, 41, size=(n_cb, 3 * C5_K + 12), dtype=np.int16)
+        return rng.integers(-40, 41, size=(n, 3 * C5_K + 12), dtype=np.int16)
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     import oracle_lib as O
     import re
     src = open(os.path.join(ROOT, "include", "oai4g_qpp.c")).read()
     f = {int(a): (int(b), int(c)) for a, b, c in re.findall(r"\{\s*(\d+)\s*,\s*(\d+)\s*,\s*(\d+)\s*\}", src)}
     base = []
-    for _ in range(64):                    # 64 distinct codewords, tiled
+    for _ in range(n):
         c = np.zeros(C5_K // 8 + 4, dtype=np.uint8)
         c[:(C5_K - 24) // 8] = rng.integers(0, 256, (C5_K - 24) // 8, dtype=np.uint8)
         v = O.crc24b(c, C5_K - 24) >> 8
         c[(C5_K - 24) // 8:(C5_K - 24) // 8 + 3] = [v >> 16, (v >> 8) & 255, v & 255]
         d = O.turbo_encode(c[:C5_K // 8], *f[C5_K]).astype(np.float64)
         base.append(np.clip(np.round((2 * d - 1) * 32 + rng.normal(0, 28, d.size)), -32768, 32767).astype(np.int16))
-    return np.stack([base[i % 64] for i in range(n_cb)])
+    return np.stack(base)
 
 
 C5_TBS, C5_G, C5_QM = 43816, 57600, 4   # UL 100 PRB MCS 20: 12 data symbols x 1200 REs x 16-QAM
@@ -293,7 +298,7 @@ _C5_WORKER = r"""
 import sys, time
 sys.path.insert(0, sys.argv[1]); sys.path.insert(0, sys.argv[1] + '/tests')
 import bench, oracle_lib as O
-llr = bench.c5_llrs(64, sys.argv[3], 0xC5 + int(sys.argv[5]))
+llr = bench.c5_llrs(sys.argv[3], 0xC5 + int(sys.argv[5]))
 fn = O.turbo_decode8 if sys.argv[2] == "8" else O.turbo_decode
 n, t0 = 0, time.perf_counter()
 while time.perf_counter() - t0 < float(sys.argv[4]):
@@ -336,9 +341,9 @@ def bench_c5(args, world, rank, dist, torch):
     crc_type = 1                           # C > 1: per-block CRC24_B (ulsch_decoding.c)
     if args.c5_mode == "chain":
         return bench_c5_chain(args, world, rank, dist, torch)
-    llr = c5_llrs(n_cb, args.c5_mode, 0xC5 + rank)
+    llr = c5_llrs(args.c5_mode, 0xC5 + rank)
     dec = (oai.TurboDecoder8Batch if args.c5_bits == 8 else oai.TurboDecoderBatch)(C5_K, n_cb)
-    dec.upload(llr)
+    dec.upload_tiled(llr)
     settle = clock_settle(lambda: dec.run(max_iterations=8, crc_type=crc_type), dec.results, args.settle_ms)
     for _ in range(args.warmup):
         dec.run(max_iterations=8, crc_type=crc_type)
@@ -362,6 +367,20 @@ def bench_c5(args, world, rank, dist, torch):
     dec.close()
     value = n_sf * args.steps * world / elapsed
     per_launch_ms = elapsed * 1000.0 / args.steps
+    small = None
+    if n_sf != 2048 and rank == 0 and world == 1:
+        # the figure at 2048 subframes per launch (2 waves per SIMD, one round), comparable with the
+        # rounds before the batch grew: the same kernel on a smaller launch, 5 timed runs
+        d2 = (oai.TurboDecoder8Batch if args.c5_bits == 8 else oai.TurboDecoderBatch)(C5_K, 2048 * C5_CB)
+        d2.upload_tiled(llr)
+        d2.run(max_iterations=8, crc_type=crc_type)
+        d2.results()
+        t2 = time.perf_counter()
+        for _ in range(5):
+            d2.run(max_iterations=8, crc_type=crc_type)
+        oai.lib().oai4g_sync()
+        small = {"subframes_per_step": 2048, "value": 2048 * 5 / (time.perf_counter() - t2), "unit": "subframes/s"}
+        d2.close()
     alg = n_cb * (2 * (3 * C5_K + 12) + C5_K // 8)          # LLR read + bits written
     ach = alg / (per_launch_ms * 1e-3) / 1e9
     cpu = None
@@ -393,6 +412,7 @@ def bench_c5(args, world, rank, dist, torch):
                                    + ("8-bit (16-window)" if args.c5_bits == 8 else "16-bit") + " max-log-MAP, max 8 iterations",
                        "config_id": "C5", "subframes_per_gpu_per_step": n_sf, "code_blocks_per_step": n_cb,
                        "mean_iterations": float(np.mean(its)), "parallelism": f"block-sharded x{world}"},
+            "at_2048_subframes": small,
             "roofline": {"bound": "hbm", "kernel": "k_td8" if args.c5_bits == 8 else "k_td16", "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": ach / HBM_PEAK_GBS, "traffic": None if args.c5_bits == 8 else _traffic("C5", "k_td16", n_sf),
                          "valu_issue_frac": None if args.c5_bits == 8 or args.c5_mode != "8it" else _c5_valu(n_sf),

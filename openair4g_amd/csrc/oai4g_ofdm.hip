@@ -334,14 +334,35 @@ static __device__ __forceinline__ void idft2048_unit(uint32_t *lds, int t, bool 
 {
   constexpr int X1W = idft2048_tw_t::X1W, E2S = idft2048_tw_t::E2S;
   static_assert(7 * E2S + 256 <= X1W, "E2 must fit the exchange");
+#ifndef OAI4G_DIAG_MODCUT
+#define OAI4G_DIAG_MODCUT 0   /* timing diagnostic only (wrong output): the unit stops after phase 1 = prologue
+                                 (QAM / RE map / precoding), 2 = leaf IDFT16, 3 = pass A + B (the 64- and 256-levels
+                                 and the E2 stores), 4 = pass C without its IQ stores; the cut values are kept
+                                 alive by empty asm operands (no instruction), so the earlier phases still run */
+#endif
+  auto sink = [&](const s16x2 (&v)[16]) {
+#pragma unroll
+    for (int k = 0; k < 16; k++) asm volatile("" ::"v"(c2u(v[k])));
+  };
   s16x2 x[NA][16];
   /* pass A: leaves */
   if (active) {
     prod(x);
+    if constexpr (OAI4G_DIAG_MODCUT == 1) {
+#pragma unroll
+      for (int a = 0; a < NA; a++) sink(x[a]);
+      return;
+    }
     if constexpr (PSYNC)
 #pragma unroll
       for (int a = 0; a < NA; a++) idft16_reg<NA == 2>(x[a], tw.l16);
+    if constexpr (OAI4G_DIAG_MODCUT == 2) {
+#pragma unroll
+      for (int a = 0; a < NA; a++) sink(x[a]);
+      return;
+    }
   }
+  if constexpr (OAI4G_DIAG_MODCUT == 1 || OAI4G_DIAG_MODCUT == 2) return;
   if constexpr (PSYNC) IDFT_SYNC();
   if (active) {
 #ifndef OAI4G_DIAG_PASSA
@@ -400,6 +421,7 @@ static __device__ __forceinline__ void idft2048_unit(uint32_t *lds, int t, bool 
     }
   }
   IDFT_SYNC();
+  if constexpr (OAI4G_DIAG_MODCUT == 3) return;   /* the E2 stores are the cut point's live values */
   /* pass C: 1024- and 2048-levels for k2 = 2 t + h; outputs k2 + 256 m1 (+ 1024) of h = 0, 1 are
    * adjacent and leave through cons2 as one pair.
    * The vector loads still in flight here (a persistent caller's prefetch of its next item, issued
@@ -453,6 +475,10 @@ static __device__ __forceinline__ void idft2048_unit(uint32_t *lds, int t, bool 
       }
 #pragma unroll
       for (int m1 = 0; m1 < 4; m1++) {
+        if constexpr (OAI4G_DIAG_MODCUT == 4) {
+          asm volatile("" ::"v"(c2u(y[0][0][m1])), "v"(c2u(y[1][0][m1])), "v"(c2u(y[0][1][m1])), "v"(c2u(y[1][1][m1])));
+          continue;
+        }
         cons2(a, 2 * t, 256 * m1, y[0][0][m1], y[1][0][m1]);
         cons2(a, 2 * t, 256 * m1 + 1024, y[0][1][m1], y[1][1][m1]);
       }

@@ -77,14 +77,14 @@ def test_c5_bench_batch(gpu, mode, n_sf):
     (bench.C5_BATCH subframes: 393 216 blocks, many rounds of 3-wave residency)."""
     import bench
     n_cb = (n_sf or bench.C5_BATCH) * bench.C5_CB
-    llr = bench.c5_llrs(n_cb, mode, 0xC5)
+    llr = bench.c5_llrs(mode, 0xC5)           # block i = llr[i % 64], as the bench tiles them
     dec = gpu.TurboDecoderBatch(bench.C5_K, n_cb)
-    dec.upload(llr)
+    dec.upload_tiled(llr)
     dec.run(max_iterations=8, crc_type=1)
     its, outs = dec.results()
     dec.close()
     for i in _samples(n_cb, 4, 7):
-        it, d = O.turbo_decode(llr[i], bench.C5_K, max_it=8, crc_type=1)
+        it, d = O.turbo_decode(llr[i % len(llr)], bench.C5_K, max_it=8, crc_type=1)
         assert its[i] == it and np.array_equal(outs[i], d), i
     if mode == "8it":
         assert np.all(its == 9)                 # unstructured LLRs: every CRC check fails
