@@ -380,7 +380,9 @@ static __device__ __forceinline__ void sfor_down(F &&f)
  * The gathered forms are written to sys[] as they are consumed, for the backward pass: the
  * exchange passes and their re-reads of the exchanged stream disappear. */
 enum { TD_SRC_SYS = 0, TD_SRC_INTL = 1, TD_SRC_DINT = 2 };
-template <bool POST, int SRC>
+/* W: the residency of the kernel that calls it (one noinline copy per kernel, so each gets its
+ * caller's register budget) */
+template <int WV, bool POST, int SRC>
 static __device__ __attribute__((noinline)) void log_map(TD_G short *sys, TD_G const short *par, TD_G short *ext,
                                                TD_G u4v *A, uint32_t K, uint32_t q, int tf,
                                                TD_L u4v *asave /* [6][64] */, TD_G const short *s0,
@@ -668,17 +670,13 @@ __device__ static const uint32_t *td_crc_tab(uint32_t *lds, uint32_t poly)
   return lds;
 }
 
-#ifndef TD16_WAVES
-/* waves per SIMD asked of the compiler (0: its choice, 2 at <= 256 VGPRs).  3 (168 VGPRs; log_map
- * spills 14 / 14 / 36 dwords): the same at 2048 subframes per launch (2048 waves, 2 per SIMD either
- * way), slower at 4096-8192 subframes, faster once the launch holds many rounds: 12288 -> +1.7 %,
- * 16384 -> +3.5 %, 24576 -> +5.6 % (profiles/c5_batch_r05.txt) */
-#define TD16_WAVES 3
-#endif
-#if TD16_WAVES > 0
-#define TD16_ATTR __attribute__((amdgpu_waves_per_eu(TD16_WAVES, TD16_WAVES)))
-#else
-#define TD16_ATTR
+#ifndef TD16_W3_MIN_CB
+/* Residency per launch size.  k_td16_w3 asks for 3 waves per SIMD (168 VGPRs; the
+ * scratch of log_map's copies is its callee-saved VGPRs, saved once per call in the prologue, not
+ * spills in the step loops); k_td16 leaves the choice to the compiler (2 waves, 252 VGPRs).  3 waves
+ * lose at 4096-8192 subframes per launch and win from 12288 on (profiles/c5_batch_r05.txt), so the
+ * 3-wave kernel runs from 12288 subframes = 98 304 blocks. */
+#define TD16_W3_MIN_CB 98304
 #endif
 
 /*
@@ -688,12 +686,13 @@ __device__ static const uint32_t *td_crc_tab(uint32_t *lds, uint32_t poly)
  * cg = c_per = 1, r0 = 0; the code blocks r0 .. r0 + cg - 1 of every transport block of a
  * [tb][C] batch otherwise (one launch per block size).
  */
-__global__ void __launch_bounds__(64) TD16_ATTR k_td16(int n_cb, uint32_t K, const int16_t *__restrict__ llr, size_t llr_stride,
-                                             uint8_t *__restrict__ out, size_t out_stride, uint8_t *__restrict__ iters,
-                                             uint32_t max_it, uint32_t crc_type, uint32_t F,
-                                             const uint16_t *__restrict__ pi4, const uint16_t *__restrict__ pi5,
-                                             const uint16_t *__restrict__ pi6, uint8_t *__restrict__ scratch,
-                                             size_t blk_bytes, uint32_t cg, uint32_t c_per, uint32_t r0)
+template <int WV>
+static __device__ __forceinline__ void td16_body(int n_cb, uint32_t K, const int16_t *__restrict__ llr, size_t llr_stride,
+                                                 uint8_t *__restrict__ out, size_t out_stride, uint8_t *__restrict__ iters,
+                                                 uint32_t max_it, uint32_t crc_type, uint32_t F,
+                                                 const uint16_t *__restrict__ pi4, const uint16_t *__restrict__ pi5,
+                                                 const uint16_t *__restrict__ pi6, uint8_t *__restrict__ scratch,
+                                                 size_t blk_bytes, uint32_t cg, uint32_t c_per, uint32_t r0)
 {
   __shared__ uint32_t crctab[256];
   __shared__ uint8_t dec[8][6144 / 8 + 8];
@@ -766,13 +765,13 @@ __global__ void __launch_bounds__(64) TD16_ATTR k_td16(int n_cb, uint32_t K, con
   }
   __syncthreads();
   bool active = valid && max_it > 0;
-  if (valid) log_map<false, TD_SRC_SYS>((TD_G short *)B.s0, (TD_G short *)B.yp1, (TD_G short *)B.ext, (TD_G u4v *)B.A, K, q, 0,
+  if (valid) log_map<WV, false, TD_SRC_SYS>((TD_G short *)B.s0, (TD_G short *)B.yp1, (TD_G short *)B.ext, (TD_G u4v *)B.A, K, q, 0,
                                         (TD_L u4v *)asave, (TD_G short *)B.s0, nullptr, nullptr);
   __syncthreads();
   uint32_t it = 0;
   for (it = 1; it <= max_it; it++) {
     /* decoder 2 takes ext[pi4] straight from decoder 1's output (interleave exchange fused) */
-    if (active) log_map<false, TD_SRC_INTL>((TD_G short *)B.s2, (TD_G short *)B.yp2, (TD_G short *)B.ext2, (TD_G u4v *)B.A, K, q,
+    if (active) log_map<WV, false, TD_SRC_INTL>((TD_G short *)B.s2, (TD_G short *)B.yp2, (TD_G short *)B.ext2, (TD_G u4v *)B.A, K, q,
                                                   1, (TD_L u4v *)asave, (TD_G short *)B.s0, (TD_G short *)B.ext,
                                                   (TD_G const uint16_t *)pi4);
     __syncthreads();
@@ -827,7 +826,7 @@ __global__ void __launch_bounds__(64) TD16_ATTR k_td16(int n_cb, uint32_t K, con
     __syncthreads();
     if (active && done_it[g]) active = false;
     /* decoder 1 takes ext2[pi5] - ext + s0 (deinterleave + update fused) */
-    if (active && it < max_it) log_map<true, TD_SRC_DINT>((TD_G short *)B.s1, (TD_G short *)B.yp1, (TD_G short *)B.ext, (TD_G u4v *)B.A,
+    if (active && it < max_it) log_map<WV, true, TD_SRC_DINT>((TD_G short *)B.s1, (TD_G short *)B.yp1, (TD_G short *)B.ext, (TD_G u4v *)B.A,
                                                             K, q, 0, (TD_L u4v *)asave, (TD_G short *)B.s0,
                                                             (TD_G short *)B.ext2, (TD_G const uint16_t *)pi5);
     __syncthreads();
@@ -836,15 +835,32 @@ __global__ void __launch_bounds__(64) TD16_ATTR k_td16(int n_cb, uint32_t K, con
   if (valid && q == 0) iters[cb] = (uint8_t)(done_it[g] ? done_it[g] : max_it + 1);
 }
 
+#define TD16_PARAMS                                                                                                 \
+  int n_cb, uint32_t K, const int16_t *__restrict__ llr, size_t llr_stride, uint8_t *__restrict__ out, size_t out_stride, \
+      uint8_t *__restrict__ iters, uint32_t max_it, uint32_t crc_type, uint32_t F, const uint16_t *__restrict__ pi4,   \
+      const uint16_t *__restrict__ pi5, const uint16_t *__restrict__ pi6, uint8_t *__restrict__ scratch, size_t blk_bytes, \
+      uint32_t cg, uint32_t c_per, uint32_t r0
+#define TD16_ARGS n_cb, K, llr, llr_stride, out, out_stride, iters, max_it, crc_type, F, pi4, pi5, pi6, scratch, blk_bytes, cg, c_per, r0
+__global__ void __launch_bounds__(64) k_td16(TD16_PARAMS) { td16_body<0>(TD16_ARGS); }
+__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3, 3))) k_td16_w3(TD16_PARAMS)
+{
+  td16_body<3>(TD16_ARGS);
+}
+
 hipError_t oai4g_launch_td16(int n_cb, uint32_t K, const int16_t *d_llr, size_t llr_stride, uint8_t *d_out,
                              size_t out_stride, uint8_t *d_iters, uint32_t max_it, uint32_t crc_type, uint32_t F,
                              const uint16_t *d_pi, uint8_t *d_scratch, hipStream_t s, uint32_t cg, uint32_t c_per,
                              uint32_t r0)
 {
   if (n_cb <= 0) return hipSuccess;
-  hipLaunchKernelGGL(k_td16, dim3((n_cb + 7) / 8), dim3(64), 0, s, n_cb, K, d_llr, llr_stride, d_out, out_stride,
-                     d_iters, max_it, crc_type, F, d_pi, d_pi + K, d_pi + 2 * K, d_scratch, oai4g_td_block_bytes(K), cg,
-                     c_per, r0);
+  if (n_cb >= TD16_W3_MIN_CB)
+    hipLaunchKernelGGL(k_td16_w3, dim3((n_cb + 7) / 8), dim3(64), 0, s, n_cb, K, d_llr, llr_stride, d_out, out_stride,
+                       d_iters, max_it, crc_type, F, d_pi, d_pi + K, d_pi + 2 * K, d_scratch, oai4g_td_block_bytes(K), cg,
+                       c_per, r0);
+  else
+    hipLaunchKernelGGL(k_td16, dim3((n_cb + 7) / 8), dim3(64), 0, s, n_cb, K, d_llr, llr_stride, d_out, out_stride,
+                       d_iters, max_it, crc_type, F, d_pi, d_pi + K, d_pi + 2 * K, d_scratch, oai4g_td_block_bytes(K), cg,
+                       c_per, r0);
   return hipGetLastError();
 }
 

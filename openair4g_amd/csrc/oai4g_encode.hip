@@ -990,6 +990,9 @@ static __device__ void encode_codeword(const cfg_dev_t *__restrict__ c, uint32_t
       const uint32_t rb0 = h ? hb : 0, rb1 = h ? C : hb;
       const uint32_t eb0 = ro_of(rb0), eb1 = rb1 < C ? ro_of(rb1) : G;   /* e bits [eb0, eb1) */
       const uint32_t w0 = eb0 >> 5, nwh = ((eb1 + 31) >> 5) - w0;       /* staged words */
+      /* nwh + 1 words: or_bits2 always writes word bit / 32 + 1 as well, so the word past the half's last
+       * is zeroed too; the host reserves it (derive_cfg: lds_a_words >= w1, w2 = staged words + 1; the
+       * debug kernel's dbg_ebuf holds the whole codeword + 1) */
       for (uint32_t i = tid; i < nwh + 1; i += nth) ebuf[i] = (i == 0 && h) ? carry : 0u;
       __syncthreads();
       const uint32_t pb = pair0(rb0), pe = pair0(rb1), bit0 = 32 * w0;

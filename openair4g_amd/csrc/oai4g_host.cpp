@@ -753,6 +753,9 @@ static void rm_plan(cw_dev_t &c, int ki)
       if (o + (uint32_t)m > Nnn) c.rm_wrapt[ki] = c.rm_wrapt[ki] == ~0u || c.rm_wrapt[ki] == t ? t : ~1u;
     }
   }
+  /* test hook: OAI4G_ENC_GENERAL_RM set sends every block size down the encoder's general placement
+   * path (the ~1 plan), which no LTE geometry reaches by itself (tests/test_gpu_rm_paths.py) */
+  if (getenv("OAI4G_ENC_GENERAL_RM")) c.rm_wrapt[ki] = ~1u;
 }
 
 static int derive_cfg(oai4g_tx_config *cfg, const oai4g_tx_params_t *p, const uint8_t Nl[2], bool need_remap,

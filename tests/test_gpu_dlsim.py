@@ -136,17 +136,20 @@ def test_gpu_trial_equals_oracle_trial(gpu, mcs, snr, llr8):
 # (llr8_flag = 0, dlsim.c:339).  The 8-bit decoder (dlsim -L, llr8) has no reference curve of its
 # own; its row pins it to the 16-bit Perf_Curves_Abs set through the fitted shift alone: it runs
 # 0.135 dB behind at MCS 9 (profiles/bler_r04_perf8.log), the int8 quantisation's cost, bounded here
-# at 0.2 dB.
-PINS = [(0, False, "perf_curves_abs", None, 3, 0.05),
-        (9, False, "perf_curves_abs", None, 3, 0.05),
-        (16, False, "perf_curves_abs", None, 3, 0.05),
-        (27, False, "perf_curves_abs", None, 3, 0.1),
-        (27, False, "awgn_results", [16.7, 16.8, 16.9, 17.0, 17.1, 17.2], 0, 0.2),
-        (9, True, "perf_curves_abs", None, 0, 0.2)]
+# at 0.2 dB; and once moved by that fitted shift, at least `need_shifted` of its rows must fall inside
+# the reference's 95 % intervals (the curve's shape, not only its position, is pinned).
+# The AWGN_results row of MCS 27 is the other curve set, offset from the one this chain follows: a
+# shift bound only.
+PINS = [(0, False, "perf_curves_abs", None, 3, 0.05, 0),
+        (9, False, "perf_curves_abs", None, 3, 0.05, 0),
+        (16, False, "perf_curves_abs", None, 3, 0.05, 0),
+        (27, False, "perf_curves_abs", None, 3, 0.1, 0),
+        (27, False, "awgn_results", [16.7, 16.8, 16.9, 17.0, 17.1, 17.2], 0, 0.2, 0),
+        (9, True, "perf_curves_abs", None, 0, 0.2, 1)]
 
 
-@pytest.mark.parametrize("mcs,llr8,which,snrs,need,shift", PINS)
-def test_gpu_bler_matches_reference_curves(gpu, mcs, llr8, which, snrs, need, shift):
+@pytest.mark.parametrize("mcs,llr8,which,snrs,need,shift,need_shifted", PINS)
+def test_gpu_bler_matches_reference_curves(gpu, mcs, llr8, which, snrs, need, shift, need_shifted):
     from openair4g_amd.dlsim import DlsimBler, wilson
     curves = D.load_curves(which)[mcs]
     if snrs is None:
@@ -168,4 +171,11 @@ def test_gpu_bler_matches_reference_curves(gpu, mcs, llr8, which, snrs, need, sh
     g, q = np.log(np.array([r[1] for r in rows])), np.log(np.array([r[2] for r in rows]))
     ds = np.arange(-0.3, 0.3001, 0.005)
     errs = [np.nanmean((np.interp(s + d, s, g, left=np.nan, right=np.nan) - q) ** 2) for d in ds]
-    assert abs(ds[int(np.nanargmin(errs))]) <= shift, ds[int(np.nanargmin(errs))]
+    best = ds[int(np.nanargmin(errs))]
+    assert abs(best) <= shift, best
+    # rows inside the reference's intervals once the GPU curve is moved by the fitted shift
+    moved = np.exp(np.interp(s + best, s, g, left=np.nan, right=np.nan))
+    refs = [r for snr in s for r in curves if abs(r[0] - snr) < 1e-6]
+    inside_shifted = sum(1 for m, r in zip(moved, refs) if np.isfinite(m) and wilson(r[1], r[2])[0] <= m <= wilson(r[1], r[2])[1])
+    print(f"fitted shift {best:+.3f} dB, rows inside after the shift: {inside_shifted}/{len(rows)}")
+    assert inside_shifted >= need_shifted, (best, inside_shifted, rows)
