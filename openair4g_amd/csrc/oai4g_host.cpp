@@ -1125,14 +1125,19 @@ static int upload_remap(oai4g_tx_config *cfg)
     /* natural, thread-major, thread-major with the non-data codes on the zero sentinel */
     std::vector<uint16_t> both(3 * n);
     std::copy(cfg->h_remap.begin(), cfg->h_remap.end(), both.begin());
-    const uint16_t sentinel = (uint16_t)(2u * ((3u * (uint32_t)N) / 4u));   /* modofdm_geom::SENT, bytes */
+    /* staged entries: 2-byte QAM-table addresses, or (OAI4G_MOD_PRE, C3's kernel) 8-byte (y0, d) pairs */
+    const bool pre = OAI4G_MOD_STAGE && OAI4G_MOD_PRE && cfg->h.mimo_mode == OAI4G_LARGE_CDD && cfg->h.n_ant == 2 &&
+                     cfg->h.log2N == 11;
+    const uint32_t esh = pre ? 3u : 1u;
+    const uint16_t sentinel = (uint16_t)(((3u * (uint32_t)N) / 4u) << esh);   /* modofdm_geom::SENT, bytes */
     for (size_t sl = 0; sl < n / N; sl++)
       for (size_t t = 0; t < T; t++)
         for (size_t k = 0; k < 16; k++) {
           uint16_t code = cfg->h_remap[sl * N + t + T * k];
 #if OAI4G_MOD_STAGE
-          /* data RE (idx | parity << 15, idx < 3N/4): the byte offset 2 idx of its staged entry */
-          if (code < OAI4G_CTL_CODE) code = (uint16_t)((code & 0x8000u) | ((code & 0x3FFFu) << 1));
+          /* data RE (idx | parity << 15, idx < 3N/4): the byte offset of its staged entry (2 idx, or 8 idx
+           * for the precoded pairs: < 8 * 1536 < 2^15) */
+          if (code < OAI4G_CTL_CODE) code = (uint16_t)((code & 0x8000u) | ((code & 0x3FFFu) << esh));
 #endif
           both[n + sl * N + t * 16 + k] = code;
 #if OAI4G_MOD_STAGE

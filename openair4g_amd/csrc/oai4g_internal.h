@@ -28,6 +28,11 @@
 #define OAI4G_MOD_STAGE 1   /* k_modofdm stages a QAM-table address per data RE (remap_tm data codes
                                2 idx | parity << 15); 0 = per-RE bit extraction from staged e words */
 #endif
+#ifndef OAI4G_MOD_PRE
+#define OAI4G_MOD_PRE 1     /* 2048-point LARGE_CDD (C3): the staging step also does the QAM lookups and the
+                               CDD sums of both codewords, one (y0, d) pair of words per data RE; the RE
+                               codes of that kernel are 8 idx | parity << 15 (oai4g_mod_pre) */
+#endif
 #define OAI4G_ENC_CRC_TABLE_WORDS (256 + 256) /* byte tables A/B (the combine multipliers stay in global memory;
                                                   slice-by-4 tables, 2048 words, cost one workgroup per CU: slower) */
 #define OAI4G_GOLD_LANES 256

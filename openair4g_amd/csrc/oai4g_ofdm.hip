@@ -822,6 +822,13 @@ __global__ void __launch_bounds__(128) MODOFDM_ATTR k_modofdm(const cfg_dev_t *_
   __shared__ __attribute__((aligned(16))) uint16_t lds_s_own[ALIAS ? 1 : UNITS][2][SW];
   uint16_t(*lds_s)[2][SW] = ALIAS ? (uint16_t(*)[2][SW])lds_data : lds_s_own;
   __shared__ uint32_t qtab[4][QROW];            /* row cw * 2 + pilot symbol: 64 packed IQ words + 0 */
+  /* OAI4G_MOD_PRE (C3's kernel): the staging step looks the QAM words of both codewords up and stores
+   * their CDD sums per data RE, (y0, d) = ((x0 + x1) >> 1, (x0 - x1) >> 1) lane by lane: the RE step is
+   * then one 8-byte LDS read and the sign of y1 = s d, instead of two dependent LDS round trips per
+   * codeword and the sums */
+  constexpr bool PRE = OAI4G_MOD_PRE && MODE == 2 && ALIAS;
+  static_assert(!PRE || SW * 8 <= NA * LDSW * 4, "the precoded pairs must fit the exchange");
+  u32x2_t *lds_p = (u32x2_t *)lds_data;
 #else
   __shared__ uint32_t lds_e[UNITS][2][EW];
   __shared__ uint32_t qtab[2][2][64];          /* [cw][pilot symbol][Qm bits] -> packed IQ */
@@ -967,7 +974,9 @@ __global__ void __launch_bounds__(128) MODOFDM_ATTR k_modofdm(const cfg_dev_t *_
 #if OAI4G_MOD_STAGE
     /* stage, per codeword, the QAM-table address of every data RE of this symbol: quad q's 4 Qm
      * bits from its prefetched bytes -> 4 entries (ALAMOUTI: even entries TA rows, odd TB rows) */
-    if (ALIAS && active && t < 4) lds_s[0][t >> 1][SENT + (t & 1)] = QZERO;   /* the exchange overwrote them */
+    if (PRE) {
+      if (active && t < 2) lds_p[SENT + t] = (u32x2_t){0u, 0u};                 /* the exchange overwrote them */
+    } else if (ALIAS && active && t < 4) lds_s[0][t >> 1][SENT + (t & 1)] = QZERO;
     if (active && nre) {
       const uint32_t nq = (nre + 3) >> 2;
       auto stage = [&](uint32_t xw, uint32_t q, uint32_t Qm, uint32_t mask, uint32_t ra, uint32_t rb, uint16_t *dst) {
@@ -977,13 +986,40 @@ __global__ void __launch_bounds__(128) MODOFDM_ATTR k_modofdm(const cfg_dev_t *_
         *(u32x2_t *)(dst + 4 * q) = (u32x2_t){s0 | (s1 << 16), s2 | (s3 << 16)};
       };
       constexpr uint32_t RB = 4u * QROW;   /* bytes per qtab row */
+      const char *qbs = (const char *)qtab;
+      /* PRE: quad q's 4 QAM words of each codeword (8 independent LDS reads), their CDD sums, and the
+       * 4 (y0, d) pairs as two 16-byte stores */
+      auto stage_pre = [&](uint32_t xw0, uint32_t xw1, uint32_t q) {
+        const uint32_t x0 = xw0 >> (((re0 + 4 * q) * Qm0) & 7u), x1 = xw1 >> (((re0 + 4 * q) * Qm1) & 7u);
+        uint32_t v0[4], v1[4];
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+          v0[j] = *(const uint32_t *)(qbs + pil * RB + 4 * ((x0 >> (j * Qm0)) & mask0));
+          v1[j] = *(const uint32_t *)(qbs + (2 + pil) * RB + 4 * ((x1 >> (j * Qm1)) & mask1));
+        }
+        uint32_t o[8];
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+          const uint32_t a = v0[j], b = v1[j];
+          const s16x2 h = u2c(a ^ b) >> (s16x2){1, 1};
+          o[2 * j] = c2u(u2c(a & b) + h);           /* y0 = floor((x0 + x1) / 2) per int16 lane */
+          o[2 * j + 1] = c2u(h - u2c(~a & b));      /* d  = floor((x0 - x1) / 2) */
+        }
+        u32x4_t *dst = (u32x4_t *)(lds_p + 4 * q);
+        dst[0] = (u32x4_t){o[0], o[1], o[2], o[3]};
+        dst[1] = (u32x4_t){o[4], o[5], o[6], o[7]};
+      };
 #pragma unroll
       for (int k = 0; k < QPT; k++) {
         const uint32_t q = (uint32_t)t + (uint32_t)(k * T);
         if (q < nq) {
-          if constexpr (MODE == 1) stage(pf.x0[k], q, Qm0, mask0, pil * RB, (2 + pil) * RB, lds_s[unit][0]);
-          else stage(pf.x0[k], q, Qm0, mask0, pil * RB, pil * RB, lds_s[unit][0]);
-          if constexpr (CW2) stage(pf.x1[k], q, Qm1, mask1, (2 + pil) * RB, (2 + pil) * RB, lds_s[unit][1]);
+          if constexpr (PRE) {
+            stage_pre(pf.x0[k], pf.x1[k], q);
+          } else {
+            if constexpr (MODE == 1) stage(pf.x0[k], q, Qm0, mask0, pil * RB, (2 + pil) * RB, lds_s[unit][0]);
+            else stage(pf.x0[k], q, Qm0, mask0, pil * RB, pil * RB, lds_s[unit][0]);
+            if constexpr (CW2) stage(pf.x1[k], q, Qm1, mask1, (2 + pil) * RB, (2 + pil) * RB, lds_s[unit][1]);
+          }
         }
       }
     }
@@ -1057,6 +1093,33 @@ __global__ void __launch_bounds__(128) MODOFDM_ATTR k_modofdm(const cfg_dev_t *_
 #pragma unroll
               for (int a = 0; a < NA; a++) x[a][n] = u2c(z);
             }
+          if constexpr (PRE) {
+            /* one 8-byte read per RE: the pair staged for its data index (codes 8 idx | parity << 15;
+             * every non-data code addresses the zero pair, clamped when CRS / control codes occur) */
+            const char *pb = (const char *)lds_p;
+#pragma unroll
+            for (int g = 0; g < NZ; g += GZ) {
+              uint32_t code[GZ];
+              u32x2_t v[GZ];
+#pragma unroll
+              for (int n = 0; n < GZ; n++) {
+                const int i = act(g + n);
+                code[n] = (rw[i >> 1] >> (16 * (i & 1))) & 0xFFFFu;
+                const uint32_t a = CRS ? min(code[n] & 0x7FF8u, 8u * SENT) : code[n] & 0x7FF8u;
+                v[n] = *(const u32x2_t *)(pb + a);
+              }
+#pragma unroll
+              for (int n = 0; n < GZ; n++) {
+                /* y1 = s d: the parity bit 15 of the code -> lane mask m, (d ^ m) - m per int16 lane */
+                const int i = act(g + n);
+                const uint32_t m = (uint32_t)((int32_t)(code[n] << 16) >> 31);
+                uint32_t r;
+                asm("v_xor_b32_e32 %0, %1, %2\n\tv_pk_sub_u16 %0, %0, %2" : "=&v"(r) : "v"(v[n].y), "v"(m));
+                x[0][i] = u2c(v[n].x);
+                x[1][i] = u2c(r);
+              }
+            }
+          } else
 #pragma unroll
           for (int g = 0; g < NZ; g += GZ) {
             uint32_t code[GZ], v0[GZ], v1[GZ];
