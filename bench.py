@@ -322,12 +322,14 @@ def _c5_port_rate(bits, mode, seconds, procs):
 
 
 def _c5_valu(batch):
-    """k_td16's VALU-busy fraction from the committed pass (profiles/valu_C5.json) at this batch."""
+    """The decoder's VALU-busy fraction from the committed pass (profiles/valu_C5.json) at this batch:
+    the build the per-size dispatch runs for 8 blocks per subframe (k_td16_w3 from 98304 blocks)."""
     try:
         t = json.load(open(os.path.join(ROOT, "profiles", "valu_C5.json")))
     except Exception:
         return None
-    return round(t["k_td16"]["valu_busy"], 4) if t.get("batch") == batch and "k_td16" in t else None
+    k = "k_td16_w3" if 8 * batch >= 98304 else "k_td16"
+    return round(t[k]["valu_busy"], 4) if t.get("batch") == batch and k in t else None
 
 
 def bench_c5(args, world, rank, dist, torch):

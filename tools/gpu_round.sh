@@ -38,7 +38,7 @@ for step in "$@"; do
            bench_line C5 --config C5; bench_line C5_snr --config C5 --c5-mode snr; bench_line C5_chain --config C5 --c5-mode chain
            bench_line C5_8bit --config C5 --c5-bits 8; bench_line FEP --config FEP; bench_line UE --config UE
            bench_line UE3 --config UE3 ;;
-    profile) c=${arg:-C3}; TAG=${TAG}_$c CONFIG=$c bash tools/gpu_profile.sh > gpurun_out/prof_${TAG}_$c.log 2>&1 \
+    profile) c=${arg:-C3}; TAG=$TAG CONFIG=$c bash tools/gpu_profile.sh > gpurun_out/prof_${TAG}_$c.log 2>&1 \
                || { tail -20 gpurun_out/prof_${TAG}_$c.log; fail "profile $c"; }
              rm -rf gpurun_out/prof_$c && mv gpurun_out/prof gpurun_out/prof_$c
              tail -8 gpurun_out/prof_${TAG}_$c.log ;;

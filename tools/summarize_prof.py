@@ -40,13 +40,22 @@ def main(prof_dir, tag, config, out_dir):
     cal = calibration(prof_dir, tag)
     pmc = collections.defaultdict(list)
     res = {}
-    for sub, ctr in (("fetch", "FETCH_SIZE"), ("write", "WRITE_SIZE")):
+    # only the batch launches count: bench.py also times smaller side runs (C5's 2048-subframe rate, on
+    # the k_td16 build the per-size dispatch picks below 98304 blocks), so per key keep the largest grid
+    grid = collections.defaultdict(int)
+    for sub in ("fetch", "write"):
         for r in csv.DictReader(open(os.path.join(prof_dir, f"{sub}_{tag}", "run_counter_collection.csv"))):
             k = short(r["Kernel_Name"])
             if k:
+                grid[k] = max(grid[k], int(r["Grid_Size"]))
+    for sub, ctr in (("fetch", "FETCH_SIZE"), ("write", "WRITE_SIZE")):
+        for r in csv.DictReader(open(os.path.join(prof_dir, f"{sub}_{tag}", "run_counter_collection.csv"))):
+            k = short(r["Kernel_Name"])
+            if k and int(r["Grid_Size"]) == grid[k]:
+                res[k] = dict(res.get(k, {}), kernel=r["Kernel_Name"].split("(")[0])
                 pmc[(k, ctr)].append(float(r["Counter_Value"]))
-                res[k] = {x: r[x] for x in ("Grid_Size", "Workgroup_Size", "LDS_Block_Size", "Scratch_Size",
-                                            "VGPR_Count", "SGPR_Count")}
+                res[k].update({x: r[x] for x in ("Grid_Size", "Workgroup_Size", "LDS_Block_Size", "Scratch_Size",
+                                            "VGPR_Count", "SGPR_Count")})
     traffic = {}
     lines = [f"# rocprofv3 summary {tag} — config {config}", "",
              "Command: `rocprofv3 --kernel-trace --stats -- python3 bench.py --steps 5 --warmup 1 --no-cpu-baseline`"
@@ -73,9 +82,9 @@ def main(prof_dir, tag, config, out_dir):
         durs = collections.defaultdict(list)
         for r in csv.DictReader(open(kt)):
             k = short(r["Kernel_Name"])
-            if k:
+            if k and (k not in grid or int(r["Grid_Size_X"]) * int(r["Grid_Size_Y"]) * int(r["Grid_Size_Z"]) == grid[k]):
                 durs[k].append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6)
-        lines += ["", "Per-dispatch durations (kernel trace):", "",
+        lines += ["", "Per-dispatch durations (kernel trace; batch-size launches only):", "",
                   "| kernel | dispatches | median ms | mean ms | min ms |", "|---|---|---|---|---|"]
         for k, v in sorted(durs.items()):
             v = sorted(v)
