@@ -640,6 +640,13 @@ typedef struct {
 int oai4g_tx_config_set_common(oai4g_tx_config_t *cfg, const oai4g_common_sig_t *common);
 /* Stage entry for parity tests: run only the encoder kernel (payload -> packed e bits). */
 int oai4g_tx_encode(const oai4g_tx_config_t *cfg, int n_sf, const uint8_t *d_payload, void *d_work, void *stream);
+/* Stage entry: run only the modulator kernel (packed scrambled e bits in d_work, as oai4g_tx_encode
+ * leaves them -> QAM / RE map / precoding / IDFT / CP -> d_iq). */
+int oai4g_tx_modulate(const oai4g_tx_config_t *cfg, int n_sf, const void *d_work, int32_t *d_iq, void *stream);
+/* 1 when the configuration's range check admits the modulator's fused IDFT levels (2048-point
+ * two-antenna LARGE_CDD whose largest QAM level keeps every 256- / 1024-level value inside int16;
+ * DESIGN.md), 0 otherwise. */
+int oai4g_tx_mod_nosat(const oai4g_tx_config_t *cfg);
 
 /* Diagnostics: average ms of the encoder kernel stopped after phase `stop_phase`
  * (0 load+Gold, 1 CRC, 2 segmentation, 3 turbo, 4 w build, 99 = complete).  Outputs invalid. */

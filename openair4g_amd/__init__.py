@@ -317,6 +317,9 @@ _SIGS = {
                                             ctypes.c_void_p, ctypes.c_void_p, ctypes.POINTER(ctypes.c_float)]),
     "oai4g_tx_encode": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p,
                                        ctypes.c_void_p]),
+    "oai4g_tx_modulate": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p,
+                                         ctypes.c_void_p]),
+    "oai4g_tx_mod_nosat": (ctypes.c_int, [ctypes.c_void_p]),
     "oai4g_diag_encode_phase_ms": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p,
                                                   ctypes.c_int, ctypes.c_int, ctypes.POINTER(ctypes.c_float)]),
     "oai4g_diag_encode_occupancy": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(ctypes.c_int),
@@ -1441,6 +1444,20 @@ class TxPipeline:
         _check(self.L.oai4g_diag_encode_phase_ms(self.cfg, self.n_sf, self.d_payload, self.d_work, stop_phase, reps,
                                                  ctypes.byref(ms)) == 0)
         return ms.value
+
+    def modulate_only(self, stream=None):
+        """oai4g_tx_modulate: the modulator kernel alone, from the e-bit words in the workspace."""
+        _check(self.L.oai4g_tx_modulate(self.cfg, self.n_sf, self.d_work, self.d_iq, stream) == 0)
+
+    def upload_ebits(self, words):
+        """Packed scrambled e-bit words [n_sf][n_cw][ebits_words] into the workspace."""
+        words = np.ascontiguousarray(words, dtype=np.uint32)
+        assert words.nbytes <= self.work_bytes
+        _check(self.L.oai4g_memcpy_h2d(self.d_work, _ptr(words), words.nbytes) == 0)
+
+    @property
+    def mod_nosat(self):
+        return bool(self.L.oai4g_tx_mod_nosat(self.cfg))
 
     def sync(self):
         _check(self.L.oai4g_sync() == 0)

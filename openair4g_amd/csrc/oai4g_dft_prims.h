@@ -79,15 +79,18 @@ static __device__ __forceinline__ s16x2 cmulc16u(s16x2 x, const twp_t &w)
   return cpack32(dot2s(x, w.t), dot2s(x, w.tn));
 }
 
-/* saturating inverse radix-4 (idft16 stages; ibfly4_16 lte_dfts.c:1049-1090) */
-template <bool FF = false>
+/* saturating inverse radix-4 (idft16 stages; ibfly4_16 lte_dfts.c:1049-1090).  NS: the caller's range
+ * check guarantees no operand is -32768 and no difference saturates, so cflip(p1) - cflip(p3) =
+ * cflip(p1 - p3) (one rotation instead of two) */
+template <bool FF = false, bool NS = false>
 static __device__ __forceinline__ void r4inv(s16x2 p0, s16x2 p1, s16x2 p2, s16x2 p3, s16x2 &o0, s16x2 &o1,
                                              s16x2 &o2, s16x2 &o3)
 {
   s16x2 s02 = cadds(p0, p2), s13 = cadds(p1, p3);
   o0 = cadds(s02, s13);
   o2 = csubs(s02, s13);
-  s16x2 d02 = csubs(p0, p2), d13 = FF ? csubs(cflip_f(p1), cflip_f(p3)) : csubs(cflip(p1), cflip(p3));
+  s16x2 d02 = csubs(p0, p2),
+        d13 = NS ? cflip_f(csubs(p1, p3)) : FF ? csubs(cflip_f(p1), cflip_f(p3)) : csubs(cflip(p1), cflip(p3));
   o3 = cadds(d02, d13);
   o1 = csubs(d02, d13);
 }
@@ -105,6 +108,49 @@ static __device__ __forceinline__ void ibfly4(s16x2 x0, s16x2 x1, s16x2 x2, s16x
   y3 = caddw(x0, cpack32(wsub(a1i, wadd(a2r, a3i)), wsub(wsub(a3r, a2i), a1r)));
   y2 = caddw(x0, cpack32(wsub(wsub(a2r, a3r), a1r), wsub(wsub(a2i, a3i), a1i)));
   y1 = caddw(x0, cpack32(wsub(wsub(a3i, a2r), a1i), wsub(a1r, wadd(a2i, a3r))));
+}
+
+/* v_dot2_i32_i16 with a VGPR accumulator */
+static __device__ __forceinline__ int dot2acc(s16x2 a, s16x2 b, int c)
+{
+  int r;
+  asm("v_dot2_i32_i16 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+  return r;
+}
+/* lanes (R >> 16, I >> 16): bits 16..31 of each, one v_perm_b32 */
+static __device__ __forceinline__ s16x2 hi16_pair(int R, int I)
+{
+  return u2c(__builtin_amdgcn_perm((uint32_t)I, (uint32_t)R, 0x07060302u));
+}
+
+/*
+ * ibfly4 followed by shr1 when no value of the level can leave int16 (the caller's range check,
+ * oai4g_host.cpp mod_nosat_ok): then packs_epi32 never clamps and the wrapping add of x0 never
+ * wraps, and per lane
+ *     (x0 + (S >> 15)) >> 1  ==  (x0 2^15 + S) >> 16          (floor division nests)
+ * with S the lane's three-product sum.  So x0 2^15 joins the 32-bit sums, and the cpack, the add
+ * and the shift become one v_perm of bits 16..31.  The sums share their terms pairwise:
+ *   re: y0 / y2 = (X + a2r) +- (a1r + a3r),  y3 / y1 = (X - a2r) +- (a1i - a3i)
+ *   im: y0 / y2 = (X + a2i) +- (a1i + a3i),  y3 / y1 = (X - a2i) +- (a3r - a1r)
+ * (the terms of ibfly4 above regrouped), X + a2 from the dot2 accumulator and X - a2 = 2X - (X + a2).
+ * Intermediate sums may wrap in 32 bits; each final sum is x0 2^15 + S, inside int32 under the check.
+ */
+static __device__ __forceinline__ void ibfly4_shr1_ns(s16x2 x0, s16x2 x1, s16x2 x2, s16x2 x3, const twp_t &t1,
+                                                      const twp_t &t2, const twp_t &t3, s16x2 &y0, s16x2 &y1,
+                                                      s16x2 &y2, s16x2 &y3)
+{
+  const uint32_t xu = c2u(x0);
+  const int x2lo = (int)(xu << 16), x2hi = (int)(xu & 0xFFFF0000u);   /* 2X per lane */
+  int a1r, a1i, a3r, a3i;
+  cmulc32(x1, t1, a1r, a1i);
+  cmulc32(x3, t3, a3r, a3i);
+  const int ur = dot2acc(x2, t2.t, x2lo >> 1), ui = dot2acc(x2, t2.tn, x2hi >> 1);
+  const int vr = wsub(x2lo, ur), vi = wsub(x2hi, ui);
+  const int pr = wadd(a1r, a3r), pi = wadd(a1i, a3i), qr = wsub(a1i, a3i), qi = wsub(a3r, a1r);
+  y0 = hi16_pair(wadd(ur, pr), wadd(ui, pi));
+  y2 = hi16_pair(wsub(ur, pr), wsub(ui, pi));
+  y3 = hi16_pair(wadd(vr, qr), wadd(vi, qi));
+  y1 = hi16_pair(wsub(vr, qr), wsub(vi, qi));
 }
 
 /* ibfly2 (lte_dfts.c:502-527): x0 * 32767 via the same madd as the twiddled operand */

@@ -13,6 +13,8 @@
 #include <string.h>
 
 #include <algorithm>
+#include <cmath>
+#include <cstdlib>
 #include <vector>
 #include <map>
 #include <mutex>
@@ -565,6 +567,37 @@ static void qam_tables_scaled(int Qm, int16_t amp, int16_t srho_a, int16_t srho_
 }
 
 /* ------------------------------------------------------------------------------------------
+ * Range check for k_modofdm's no-saturation IDFT forms (ibfly4_shr1_ns and r4inv<NS>,
+ * oai4g_dft_prims.h).  The 2048-point transform is DIT: a 64-level value (before its >> 3) is part
+ * of a 64-point DFT over the subcarriers of one residue class mod 32, a 256-level value one of a
+ * 256-point DFT over a class mod 8 scaled by 1/8 (the 64-level's shift), a 1024-level value one over
+ * a class mod 2 scaled by 1/16; the leaf's are parts of 16-point DFTs, inside the 64-level's classes.
+ * Every twiddle has modulus < 1 (Q15, |t| <= 32767.7), so a value's modulus is at most (occupied
+ * subcarriers of its class) x (largest input modulus) x scale, plus the truncations of the levels
+ * below (< 64 in modulus).  Inputs of C3's kernel are the CDD pairs (floor((x0 + x1) / 2),
+ * +-floor((x0 - x1) / 2)) of two QAM words, components <= the largest QAM level V, modulus <=
+ * sqrt(2) V, and only 12 N_RB_DL subcarriers carry anything.  When the three bounds stay inside
+ * int16 with a margin of 128, no add of those levels saturates or wraps, packs_epi32 never clamps
+ * and no operand is -32768, whatever the bits: the no-saturation forms are then the reference's
+ * arithmetic.  (C3: V = 553, R = 782.1; 39 R + 128 = 30629, 151 R / 8 + 128 = 14890, 601 R / 16 +
+ * 128 = 29505.)  OAI4G_MOD_SAT (test hook) keeps the saturating forms.
+ * ---------------------------------------------------------------------------------------- */
+static uint32_t mod_nosat_ok(const cfg_dev_t &h)
+{
+  if (h.log2N != 11 || h.mimo_mode != OAI4G_LARGE_CDD || h.n_ant != 2 || h.n_cw != 2 || getenv("OAI4G_MOD_SAT"))
+    return 0;
+  int v = 0;
+  for (uint32_t cw = 0; cw < h.n_cw; cw++) {
+    const cw_dev_t &c = h.cw[cw];
+    for (int i = 0; i < 8; i++) v = std::max(v, std::max(std::abs((int)c.qam_a[i]), std::abs((int)c.qam_b[i])));
+    v = std::max(v, std::max(std::abs((int)c.qpsk_a), std::abs((int)c.qpsk_b)));
+  }
+  const double R = std::sqrt(2.0) * v, band = 12.0 * h.N_RB_DL;
+  const double c32 = std::ceil(band / 32) + 1, c8 = std::ceil(band / 8) + 1, c2 = std::ceil(band / 2) + 1;
+  return (c32 * R + 128 <= 32767 && c8 * R / 8 + 128 <= 32767 && c2 * R / 16 + 128 <= 32767) ? 1u : 0u;
+}
+
+/* ------------------------------------------------------------------------------------------
  * RE map: restatement of dlsch_modulation's control flow (dlsch_modulation.c:1258-1493 and
  * allocate_REs_in_RB :139-249, 745-748) producing, per symbol, the data-RE order.
  * Returns REs allocated, or -1 for an unsupported mode.
@@ -1019,6 +1052,7 @@ static int derive_cfg(oai4g_tx_config *cfg, const oai4g_tx_params_t *p, const ui
     }
     qam_tables_scaled((int)c.Qm, p->amp, p->sqrt_rho_a, p->sqrt_rho_b, p->mimo_mode == OAI4G_ALAMOUTI, c);
   }
+  h.mod_nosat = mod_nosat_ok(h);
   if (max_gw > OAI4G_MAX_GOLD_WORDS) { set_err("G too large"); return -1; }
   h.lds_tb_words = max_tb_words;
   h.lds_stream_words = max_stream_words;
@@ -1348,6 +1382,17 @@ extern "C" int oai4g_tx_batch_timed(const oai4g_tx_config_t *cfg, int n_sf, cons
   for (int i = 0; i < 3; i++) hipEventDestroy(ev[i]);
   return 0;
 }
+
+extern "C" int oai4g_tx_modulate(const oai4g_tx_config_t *cfg, int n_sf, const void *d_work, int32_t *d_iq,
+                                 void *stream)
+{
+  NEED_INIT(-1);
+  if (!cfg || !iq_aligned(d_iq)) return -1;
+  HCK(oai4g_launch_modofdm(cfg->d, &cfg->h, 0, n_sf, (const uint32_t *)d_work, d_iq, (hipStream_t)stream), -1);
+  return 0;
+}
+
+extern "C" int oai4g_tx_mod_nosat(const oai4g_tx_config_t *cfg) { return cfg ? (int)cfg->h.mod_nosat : 0; }
 
 /* Diagnostics: time the encoder with an early exit after phase `stop_phase`
  * (0 load/Gold, 1 CRC, 2 segmentation, 3 turbo, 4 w build, 99 full). Outputs are invalid. */

@@ -152,7 +152,8 @@ struct cfg_dev_t {
   uint32_t lds_w_words;         /* packed sub-block interleaver output of every block */
   uint32_t lds_a_words;         /* region A: TB + CRC tables (0-2) | interleaved words (3) | packed w (4) */
   uint32_t lds_b_words;         /* region B: constituent streams */
-  uint32_t pad[2];
+  uint32_t mod_nosat;            /* 1: k_modofdm may take the fused IDFT levels (oai4g_host.cpp mod_nosat_ok) */
+  uint32_t pad;
   uint32_t crctab[2][256];      /* CRC byte tables (crc_byte.c:98-105): [0] CRC-24A, [1] CRC-24B */
   cw_dev_t cw[2];
   uint32_t symbase[10][14];     /* data REs before symbol l */

@@ -95,19 +95,19 @@ static __device__ __forceinline__ twp_t tw_use(s16x2 t, uint32_t dep)
 }
 
 /* leaf IDFT16 in registers (lte_dfts.c:1597-1724); w16 is wave-uniform (scalar loads) */
-template <bool FF = false>
+template <bool FF = false, bool NS = false>
 static __device__ __forceinline__ void idft16_reg(s16x2 *x, const twp_t *w16 /* W^{0,1,2,3,4,6,9} */)
 {
   constexpr int k1[4] = {0, 1, 2, 3}, k2[4] = {0, 2, 4, 5}, k3[4] = {0, 3, 5, 6}; /* slots of k, 2k, 3k */
   s16x2 S[4][4];
 #pragma unroll
-  for (int j = 0; j < 4; j++) r4inv<FF>(x[j], x[4 + j], x[8 + j], x[12 + j], S[0][j], S[1][j], S[2][j], S[3][j]);
+  for (int j = 0; j < 4; j++) r4inv<FF, NS>(x[j], x[4 + j], x[8 + j], x[12 + j], S[0][j], S[1][j], S[2][j], S[3][j]);
 #pragma unroll
   for (int k = 0; k < 4; k++) {
     s16x2 b1 = cmulc16u(S[k][1], w16[k1[k]]);
     s16x2 b2 = cmulc16u(S[k][2], w16[k2[k]]);
     s16x2 b3 = cmulc16u(S[k][3], w16[k3[k]]);
-    r4inv<FF>(S[k][0], b1, b2, b3, x[k], x[4 + k], x[8 + k], x[12 + k]);
+    r4inv<FF, NS>(S[k][0], b1, b2, b3, x[k], x[4 + k], x[8 + k], x[12 + k]);
   }
 }
 
@@ -328,7 +328,10 @@ typedef uint32_t u32x2_t __attribute__((ext_vector_type(2)));
 
 /* PSYNC: the producer reads LDS that the exchange aliases (k_modofdm's staged QAM addresses), so
  * the leaf stores wait for every thread's producer */
-template <int NA, bool PSYNC, class Prod, class Cons2>
+/* NS: the caller's configuration passed the range check (oai4g_host.cpp mod_nosat_ok: no value of the
+ * leaf, 64-, 256- or 1024-level leaves int16), so the 256- and 1024-levels take the fused form
+ * (ibfly4_shr1_ns) and the radix-4 adds rotate once (r4inv NS) */
+template <int NA, bool PSYNC, bool NS, class Prod, class Cons2>
 static __device__ __forceinline__ void idft2048_unit(uint32_t *lds, int t, bool active, const idft2048_tw_t &tw,
                                                      Prod prod, Cons2 cons2, int scale, uint32_t dep)
 {
@@ -355,7 +358,7 @@ static __device__ __forceinline__ void idft2048_unit(uint32_t *lds, int t, bool 
     }
     if constexpr (PSYNC)
 #pragma unroll
-      for (int a = 0; a < NA; a++) idft16_reg<NA == 2>(x[a], tw.l16);
+      for (int a = 0; a < NA; a++) idft16_reg<NA == 2, NS>(x[a], tw.l16);
     if constexpr (OAI4G_DIAG_MODCUT == 2) {
 #pragma unroll
       for (int a = 0; a < NA; a++) sink(x[a]);
@@ -371,7 +374,7 @@ static __device__ __forceinline__ void idft2048_unit(uint32_t *lds, int t, bool 
     const uint32_t wo = OAI4G_DIAG_PASSA ? (uint32_t)t : 2u * (t & 31) + ((t >> 5) & 1) + 64u * (t >> 6);
 #pragma unroll
     for (int a = 0; a < NA; a++) {
-      if constexpr (!PSYNC) idft16_reg<NA == 2>(x[a], tw.l16);
+      if constexpr (!PSYNC) idft16_reg<NA == 2, NS>(x[a], tw.l16);
 #pragma unroll
       for (int k = 0; k < 16; k++) lds[a * X1W + k * 144 + wo] = c2u(x[a][k]);
     }
@@ -403,7 +406,7 @@ static __device__ __forceinline__ void idft2048_unit(uint32_t *lds, int t, bool 
 #pragma unroll
       for (int r2 = 0; r2 < 4; r2++) {
         const s16x2 *v = &x[a][4 * r2];
-        r4inv<NA == 2>(v[0], cmulc16(v[1], w64[0]), cmulc16(v[2], w64[1]), cmulc16(v[3], w64[2]), o[r2][0], o[r2][1],
+        r4inv<NA == 2, NS>(v[0], cmulc16(v[1], w64[0]), cmulc16(v[2], w64[1]), cmulc16(v[3], w64[2]), o[r2][0], o[r2][1],
               o[r2][2], o[r2][3]);
 #pragma unroll
         for (int m = 0; m < 4; m++) o[r2][m] = shr3(o[r2][m]);
@@ -414,9 +417,15 @@ static __device__ __forceinline__ void idft2048_unit(uint32_t *lds, int t, bool 
          * 4 waves/SIMD; the other levels' are rebuilt at use */
         const twp_t w[3] = {tw_of(tw.b256[m3][0]), tw_of(tw.b256[m3][1]), tw_of(tw.b256[m3][2])};
         s16x2 y[4];
-        ibfly4(o[0][m3], o[1][m3], o[2][m3], o[3][m3], w[0], w[1], w[2], y[0], y[1], y[2], y[3]);
+        if constexpr (NS) {
+          ibfly4_shr1_ns(o[0][m3], o[1][m3], o[2][m3], o[3][m3], w[0], w[1], w[2], y[0], y[1], y[2], y[3]);
+        } else {
+          ibfly4(o[0][m3], o[1][m3], o[2][m3], o[3][m3], w[0], w[1], w[2], y[0], y[1], y[2], y[3]);
 #pragma unroll
-        for (int m2 = 0; m2 < 4; m2++) lds[a * X1W + wb + 16u * m3 + 64u * m2] = c2u(shr1(y[m2]));
+          for (int m2 = 0; m2 < 4; m2++) y[m2] = shr1(y[m2]);
+        }
+#pragma unroll
+        for (int m2 = 0; m2 < 4; m2++) lds[a * X1W + wb + 16u * m3 + 64u * m2] = c2u(y[m2]);
       }
     }
   }
@@ -460,9 +469,14 @@ static __device__ __forceinline__ void idft2048_unit(uint32_t *lds, int t, bool 
         s16x2 o[2][4];   /* [e][m1] */
 #pragma unroll
         for (int e = 0; e < 2; e++) {
-          ibfly4(v[h][e], v[h][e + 2], v[h][e + 4], v[h][e + 6], w[0], w[1], w[2], o[e][0], o[e][1], o[e][2], o[e][3]);
+          if constexpr (NS) {
+            ibfly4_shr1_ns(v[h][e], v[h][e + 2], v[h][e + 4], v[h][e + 6], w[0], w[1], w[2], o[e][0], o[e][1], o[e][2],
+                           o[e][3]);
+          } else {
+            ibfly4(v[h][e], v[h][e + 2], v[h][e + 4], v[h][e + 6], w[0], w[1], w[2], o[e][0], o[e][1], o[e][2], o[e][3]);
 #pragma unroll
-          for (int m = 0; m < 4; m++) o[e][m] = shr1(o[e][m]);
+            for (int m = 0; m < 4; m++) o[e][m] = shr1(o[e][m]);
+          }
         }
 #pragma unroll
         for (int m1 = 0; m1 < 4; m1++) {
@@ -500,12 +514,12 @@ struct idft_sel<11> {
 /* dep: a per-item value in persistent loops (see tw_use), 0 elsewhere.  cons(a, t, off, y) takes
  * output t + off of antenna a; cons2(a, tt, off, y0, y1) the adjacent outputs tt + off, tt + off + 1
  * (tt + off even) — the 2048-point schedule produces pairs */
-template <int LOG2N, int NA, bool PSYNC = false, class Prod, class Cons, class Cons2>
+template <int LOG2N, int NA, bool PSYNC = false, bool NS = false, class Prod, class Cons, class Cons2>
 static __device__ __forceinline__ void idft_any2(uint32_t *lds, int t, bool active,
                                                  const typename idft_sel<LOG2N>::tw_t &tw, Prod prod, Cons cons,
                                                  Cons2 cons2, int scale, uint32_t dep = 0)
 {
-  if constexpr (LOG2N == 11) idft2048_unit<NA, PSYNC>(lds, t, active, tw, prod, cons2, scale, dep);
+  if constexpr (LOG2N == 11) idft2048_unit<NA, PSYNC, NS>(lds, t, active, tw, prod, cons2, scale, dep);
   else idft_unit<LOG2N, NA>(lds, t, active, tw, prod, cons, scale);
 }
 template <int LOG2N, int NA, bool PSYNC = false, class Prod, class Cons>
@@ -800,7 +814,9 @@ static __device__ __forceinline__ uint32_t ld_u32_any(const uint8_t *p)
 #define MODOFDM_ATTR __attribute__((amdgpu_waves_per_eu(MODOFDM_WAVES_OF(LOG2N))))
 /* MODE: 0 = TM1 (one transform stored to every antenna), 1 = ALAMOUTI, 2 = LARGE_CDD, 3 = 4-port
  * LARGE_CDD (C4: two items per symbol, each transforming one antenna pair) */
-template <int LOG2N, int MODE, bool CRS, bool ECP>
+/* NS: the fused ibfly4 + shr1 levels (ibfly4_shr1_ns); the host sets it only for configurations whose
+ * range check passed (mod_nosat_ok) */
+template <int LOG2N, int MODE, bool CRS, bool ECP, bool NS = false>
 __global__ void __launch_bounds__(128) MODOFDM_ATTR k_modofdm(const cfg_dev_t *__restrict__ c, int n_items,
                                                  const uint32_t *__restrict__ ebits, int32_t *__restrict__ iq,
                                                  uint32_t sf0)
@@ -1058,7 +1074,7 @@ __global__ void __launch_bounds__(128) MODOFDM_ATTR k_modofdm(const cfg_dev_t *_
 #else
     constexpr bool PSYNC = false;
 #endif
-    idft_any2<LOG2N, NA, PSYNC>(
+    idft_any2<LOG2N, NA, PSYNC, NS>(
         lds_data + unit * NA * LDSW, t, active, twr,
         [&](s16x2 (*x)[16]) {
           /* branch-free and staged in groups of GR REs so each LDS round trip is issued for the
@@ -1312,13 +1328,13 @@ __global__ void __launch_bounds__(128) MODOFDM_ATTR k_modofdm(const cfg_dev_t *_
   }
 }
 
-template <int LOG2N, int MODE, bool CRS, bool ECP>
+template <int LOG2N, int MODE, bool CRS, bool ECP, bool NS = false>
 static hipError_t launch_modofdm_t(const cfg_dev_t *d_cfg, const cfg_dev_t *h_cfg, int sf0, int n_items,
                                    const uint32_t *d_ebits, int32_t *d_iq, hipStream_t s)
 {
   static int occ = 0;
   if (!occ) {
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, k_modofdm<LOG2N, MODE, CRS, ECP>, 128, 0) != hipSuccess ||
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, k_modofdm<LOG2N, MODE, CRS, ECP, NS>, 128, 0) != hipSuccess ||
         occ < 1)
       occ = 1;
     /* OAI4G_MODOFDM_OCC=n caps the persistent grid at n workgroups per CU (diagnostic: leaves
@@ -1332,7 +1348,7 @@ static hipError_t launch_modofdm_t(const cfg_dev_t *d_cfg, const cfg_dev_t *h_cf
   int want = (n_items + units - 1) / units, cap = occ * (int)h_cfg->n_cu;
   int grid = want < cap ? want : cap;
   if (grid < 1) grid = 1;
-  hipLaunchKernelGGL((k_modofdm<LOG2N, MODE, CRS, ECP>), dim3(grid), dim3(128), 0, s, d_cfg, n_items, d_ebits, d_iq,
+  hipLaunchKernelGGL((k_modofdm<LOG2N, MODE, CRS, ECP, NS>), dim3(grid), dim3(128), 0, s, d_cfg, n_items, d_ebits, d_iq,
                      (uint32_t)sf0);
   return hipGetLastError();
 }
@@ -1341,8 +1357,12 @@ template <int LOG2N, int MODE, bool ECP>
 static hipError_t launch_modofdm_c(const cfg_dev_t *d_cfg, const cfg_dev_t *h_cfg, int sf0, int n_items,
                                    const uint32_t *d_ebits, int32_t *d_iq, hipStream_t s)
 {
-  return (h_cfg->with_crs || h_cfg->ctl_on) ? launch_modofdm_t<LOG2N, MODE, true, ECP>(d_cfg, h_cfg, sf0, n_items, d_ebits, d_iq, s)
-                         : launch_modofdm_t<LOG2N, MODE, false, ECP>(d_cfg, h_cfg, sf0, n_items, d_ebits, d_iq, s);
+  if (h_cfg->with_crs || h_cfg->ctl_on)
+    return launch_modofdm_t<LOG2N, MODE, true, ECP>(d_cfg, h_cfg, sf0, n_items, d_ebits, d_iq, s);
+  /* the fused levels: C3's kernel (2048 points, two-antenna LARGE_CDD) when the range check passed */
+  if constexpr (LOG2N == 11 && MODE == 2 && !ECP)
+    if (h_cfg->mod_nosat) return launch_modofdm_t<LOG2N, MODE, false, ECP, true>(d_cfg, h_cfg, sf0, n_items, d_ebits, d_iq, s);
+  return launch_modofdm_t<LOG2N, MODE, false, ECP>(d_cfg, h_cfg, sf0, n_items, d_ebits, d_iq, s);
 }
 
 template <int LOG2N, bool ECP>
