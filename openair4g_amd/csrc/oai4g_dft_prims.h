@@ -162,6 +162,28 @@ static __device__ __forceinline__ void ibfly2(s16x2 x0, s16x2 x1, const twp_t &t
   y1 = cpack32(wsub(a0r, a1r), wsub(a0i, a1i));
 }
 
+/* ibfly2 then mulhi2_f on both outputs when neither sum can leave int16 (the caller's range check):
+ * packs_epi32 then never clamps, so each lane of y is the 32-bit sum >> 15 as it stands and the
+ * x 23170 product takes it from the VGPR (v_mul_i32_i24) instead of from a packed pair (dot2): the
+ * v_cvt_pk of each output disappears.  Lane extraction as mulhi2_f. */
+static __device__ __forceinline__ s16x2 mulhi2_lanes(int yr, int yi)
+{
+  uint32_t pr, pi, hi, r;
+  asm("v_mul_i32_i24_e32 %0, 0x5a82, %1" : "=v"(pr) : "v"(yr));    /* yr, yi within 17 bits: exact */
+  asm("v_mul_i32_i24_e32 %0, 0x5a82, %1" : "=v"(pi) : "v"(yi));
+  const uint32_t lo = pr >> 15;
+  asm("v_add_u32_e32 %0, %1, %1\n\tv_and_b32_e32 %0, 0xfffe0000, %0" : "=&v"(hi) : "v"(pi));
+  asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0xe4" : "=v"(r) : "v"(lo), "v"(hi), "s"(0x0000FFFEu));
+  return u2c(r);
+}
+static __device__ __forceinline__ void ibfly2_mulhi_ns(s16x2 x0, s16x2 x1, const twp_t &t, s16x2 &y0, s16x2 &y1)
+{
+  int a0r = dot2s(x0, (s16x2){32767, 0}), a0i = dot2s(x0, (s16x2){0, 32767}), a1r, a1i;
+  cmulc32(x1, t, a1r, a1i);
+  y0 = mulhi2_lanes(wadd(a0r, a1r) >> 15, wadd(a0i, a1i) >> 15);
+  y1 = mulhi2_lanes(wsub(a0r, a1r) >> 15, wsub(a0i, a1i) >> 15);
+}
+
 static __device__ __forceinline__ s16x2 shr3(s16x2 a) { return (s16x2){(short)(a.x >> 3), (short)(a.y >> 3)}; }
 static __device__ __forceinline__ s16x2 shr1(s16x2 a) { return (s16x2){(short)(a.x >> 1), (short)(a.y >> 1)}; }
 /* mulhi_int16(a, 23170) = slli(mulhi_epi16(a, 23170), 1) (lte_dfts.c:1755); |result| <= 23170 */

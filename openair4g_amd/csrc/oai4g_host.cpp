@@ -571,16 +571,17 @@ static void qam_tables_scaled(int Qm, int16_t amp, int16_t srho_a, int16_t srho_
  * oai4g_dft_prims.h).  The 2048-point transform is DIT: a 64-level value (before its >> 3) is part
  * of a 64-point DFT over the subcarriers of one residue class mod 32, a 256-level value one of a
  * 256-point DFT over a class mod 8 scaled by 1/8 (the 64-level's shift), a 1024-level value one over
- * a class mod 2 scaled by 1/16; the leaf's are parts of 16-point DFTs, inside the 64-level's classes.
+ * a class mod 2 scaled by 1/16, a 2048-level sum (before mulhi) one over every subcarrier scaled by
+ * 1/32; the leaf's are parts of 16-point DFTs, inside the 64-level's classes.
  * Every twiddle has modulus < 1 (Q15, |t| <= 32767.7), so a value's modulus is at most (occupied
  * subcarriers of its class) x (largest input modulus) x scale, plus the truncations of the levels
  * below (< 64 in modulus).  Inputs of C3's kernel are the CDD pairs (floor((x0 + x1) / 2),
  * +-floor((x0 - x1) / 2)) of two QAM words, components <= the largest QAM level V, modulus <=
- * sqrt(2) V, and only 12 N_RB_DL subcarriers carry anything.  When the three bounds stay inside
+ * sqrt(2) V, and only 12 N_RB_DL subcarriers carry anything.  When the four bounds stay inside
  * int16 with a margin of 128, no add of those levels saturates or wraps, packs_epi32 never clamps
  * and no operand is -32768, whatever the bits: the no-saturation forms are then the reference's
  * arithmetic.  (C3: V = 553, R = 782.1; 39 R + 128 = 30629, 151 R / 8 + 128 = 14890, 601 R / 16 +
- * 128 = 29505.)  OAI4G_MOD_SAT (test hook) keeps the saturating forms.
+ * 128 = 29505, 1201 R / 32 + 128 = 29480.)  OAI4G_MOD_SAT (test hook) keeps the saturating forms.
  * ---------------------------------------------------------------------------------------- */
 static uint32_t mod_nosat_ok(const cfg_dev_t &h)
 {
@@ -594,7 +595,8 @@ static uint32_t mod_nosat_ok(const cfg_dev_t &h)
   }
   const double R = std::sqrt(2.0) * v, band = 12.0 * h.N_RB_DL;
   const double c32 = std::ceil(band / 32) + 1, c8 = std::ceil(band / 8) + 1, c2 = std::ceil(band / 2) + 1;
-  return (c32 * R + 128 <= 32767 && c8 * R / 8 + 128 <= 32767 && c2 * R / 16 + 128 <= 32767) ? 1u : 0u;
+  return (c32 * R + 128 <= 32767 && c8 * R / 8 + 128 <= 32767 && c2 * R / 16 + 128 <= 32767 &&
+          (band + 1) * R / 32 + 128 <= 32767) ? 1u : 0u;
 }
 
 /* ------------------------------------------------------------------------------------------

@@ -329,8 +329,9 @@ typedef uint32_t u32x2_t __attribute__((ext_vector_type(2)));
 /* PSYNC: the producer reads LDS that the exchange aliases (k_modofdm's staged QAM addresses), so
  * the leaf stores wait for every thread's producer */
 /* NS: the caller's configuration passed the range check (oai4g_host.cpp mod_nosat_ok: no value of the
- * leaf, 64-, 256- or 1024-level leaves int16), so the 256- and 1024-levels take the fused form
- * (ibfly4_shr1_ns) and the radix-4 adds rotate once (r4inv NS) */
+ * leaf, 64-, 256-, 1024- or 2048-level leaves int16), so the 256- and 1024-levels take the fused form
+ * (ibfly4_shr1_ns), the radix-4 adds rotate once (r4inv NS) and the 2048-level's scale multiplies
+ * the unpacked sums (ibfly2_mulhi_ns) */
 template <int NA, bool PSYNC, bool NS, class Prod, class Cons2>
 static __device__ __forceinline__ void idft2048_unit(uint32_t *lds, int t, bool active, const idft2048_tw_t &tw,
                                                      Prod prod, Cons2 cons2, int scale, uint32_t dep)
@@ -480,6 +481,10 @@ static __device__ __forceinline__ void idft2048_unit(uint32_t *lds, int t, bool 
         }
 #pragma unroll
         for (int m1 = 0; m1 < 4; m1++) {
+          if (NS && scale) {
+            ibfly2_mulhi_ns(o[0][m1], o[1][m1], wc2[h][m1], y[h][0][m1], y[h][1][m1]);
+            continue;
+          }
           ibfly2(o[0][m1], o[1][m1], wc2[h][m1], y[h][0][m1], y[h][1][m1]);
           if (scale) {
 #pragma unroll
