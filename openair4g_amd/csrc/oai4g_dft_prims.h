@@ -168,11 +168,13 @@ static __device__ __forceinline__ void ibfly2(s16x2 x0, s16x2 x1, const twp_t &t
  * v_cvt_pk of each output disappears.  Lane extraction as mulhi2_f. */
 static __device__ __forceinline__ s16x2 mulhi2_lanes(int yr, int yi)
 {
-  uint32_t pr, pi, hi, r;
-  asm("v_mul_i32_i24_e32 %0, 0x5a82, %1" : "=v"(pr) : "v"(yr));    /* yr, yi within 17 bits: exact */
-  asm("v_mul_i32_i24_e32 %0, 0x5a82, %1" : "=v"(pi) : "v"(yi));
+  uint32_t pr, pi2, hi, r;
+  /* yr, yi are int16 values in 32-bit lanes: exact 24-bit products; the imaginary one doubled (46340 =
+   * 2 x 23170) is mulhi2_f's pi + pi */
+  asm("v_mul_i32_i24_e32 %0, 0x5a82, %1" : "=v"(pr) : "v"(yr));
+  asm("v_mul_i32_i24_e32 %0, 0xb504, %1" : "=v"(pi2) : "v"(yi));
   const uint32_t lo = pr >> 15;
-  asm("v_add_u32_e32 %0, %1, %1\n\tv_and_b32_e32 %0, 0xfffe0000, %0" : "=&v"(hi) : "v"(pi));
+  asm("v_and_b32_e32 %0, 0xfffe0000, %1" : "=v"(hi) : "v"(pi2));
   asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0xe4" : "=v"(r) : "v"(lo), "v"(hi), "s"(0x0000FFFEu));
   return u2c(r);
 }

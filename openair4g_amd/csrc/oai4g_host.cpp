@@ -581,13 +581,16 @@ static void qam_tables_scaled(int Qm, int16_t amp, int16_t srho_a, int16_t srho_
  * int16 with a margin of 128, no add of those levels saturates or wraps, packs_epi32 never clamps
  * and no operand is -32768, whatever the bits: the no-saturation forms are then the reference's
  * arithmetic.  (C3: V = 553, R = 782.1; 39 R + 128 = 30629, 151 R / 8 + 128 = 14890, 601 R / 16 +
- * 128 = 29505, 1201 R / 32 + 128 = 29480.)  OAI4G_MOD_SAT (test hook) keeps the saturating forms.
+ * 128 = 29505, 1201 R / 32 + 128 = 29480.)  With CRS or static REs (PCFICH, PDCCH, PHICH, PSS, SSS,
+ * PBCH) in the grid, V also covers their components (v_static: the largest over the CRS table and the
+ * static-RE table, re-checked whenever oai4g_tx_config_set_control / _set_common rebuild it).
+ * OAI4G_MOD_SAT (test hook) keeps the saturating forms.
  * ---------------------------------------------------------------------------------------- */
-static uint32_t mod_nosat_ok(const cfg_dev_t &h)
+static uint32_t mod_nosat_ok(const cfg_dev_t &h, int v_static)
 {
   if (h.log2N != 11 || h.mimo_mode != OAI4G_LARGE_CDD || h.n_ant != 2 || h.n_cw != 2 || getenv("OAI4G_MOD_SAT"))
     return 0;
-  int v = 0;
+  int v = v_static;
   for (uint32_t cw = 0; cw < h.n_cw; cw++) {
     const cw_dev_t &c = h.cw[cw];
     for (int i = 0; i < 8; i++) v = std::max(v, std::max(std::abs((int)c.qam_a[i]), std::abs((int)c.qam_b[i])));
@@ -597,6 +600,13 @@ static uint32_t mod_nosat_ok(const cfg_dev_t &h)
   const double c32 = std::ceil(band / 32) + 1, c8 = std::ceil(band / 8) + 1, c2 = std::ceil(band / 2) + 1;
   return (c32 * R + 128 <= 32767 && c8 * R / 8 + 128 <= 32767 && c2 * R / 16 + 128 <= 32767 &&
           (band + 1) * R / 32 + 128 <= 32767) ? 1u : 0u;
+}
+
+static int packed_iq_max(const std::vector<uint32_t> &t)
+{
+  int v = 0;
+  for (uint32_t w : t) v = std::max(v, std::max(std::abs((int)(int16_t)(w & 0xFFFFu)), std::abs((int)(int16_t)(w >> 16))));
+  return v;
 }
 
 /* ------------------------------------------------------------------------------------------
@@ -720,6 +730,7 @@ struct oai4g_tx_config {
   uint32_t *d_gold = nullptr;           /* [10][n_cw][ebits_words] scrambling words */
   std::vector<uint32_t> h_crs;          /* [10][4][200] packed CRS IQ */
   uint32_t *d_ctl = nullptr;            /* static RE values [10][14][2][N] (set_control / set_common) */
+  int ctl_vmax = 0;                     /* largest I / Q magnitude in the static-RE table (mod_nosat_ok) */
   std::vector<oai4g_dci_alloc_t> dci;   /* oai4g_tx_config_set_control's DCI set */
   uint8_t n_ue_dci = 0, n_common_dci = 0;
   bool common_on = false;
@@ -1054,7 +1065,6 @@ static int derive_cfg(oai4g_tx_config *cfg, const oai4g_tx_params_t *p, const ui
     }
     qam_tables_scaled((int)c.Qm, p->amp, p->sqrt_rho_a, p->sqrt_rho_b, p->mimo_mode == OAI4G_ALAMOUTI, c);
   }
-  h.mod_nosat = mod_nosat_ok(h);
   if (max_gw > OAI4G_MAX_GOLD_WORDS) { set_err("G too large"); return -1; }
   h.lds_tb_words = max_tb_words;
   h.lds_stream_words = max_stream_words;
@@ -1239,6 +1249,7 @@ static int upload_cfg(oai4g_tx_config *cfg)
   }
   cfg->h.crs_tab = cfg->d_crs;
   cfg->h.with_crs = cfg->d_crs ? 1u : 0u;
+  cfg->h.mod_nosat = mod_nosat_ok(cfg->h, std::max(packed_iq_max(cfg->h_crs), cfg->ctl_vmax));
   cfg->h.n_cu = (uint32_t)g_n_cu;
   cfg->h.gold_x1 = g_gx1;
   cfg->h.gold_x2j = g_gx2j;
@@ -3002,6 +3013,7 @@ static int rebuild_static(oai4g_tx_config_t *cfg)
   if (cfg->d_ctl) hipFree(cfg->d_ctl);
   cfg->d_ctl = nullptr;
   cfg->h.ctl_tab = nullptr;
+  cfg->ctl_vmax = 0;
   const bool dci_on = (uint32_t)cfg->n_ue_dci + cfg->n_common_dci > 0;
   if (dci_on || cfg->common_on) {
     if (cfg->h_remap.empty()) { set_err("static REs: configuration has no RE map"); return -1; }
@@ -3118,7 +3130,9 @@ static int rebuild_static(oai4g_tx_config_t *cfg)
     HCK(hipMemcpy(cfg->d_ctl, tab.data(), tab.size() * 4, hipMemcpyHostToDevice), -1);
     cfg->h.ctl_tab = cfg->d_ctl;
     cfg->h.ctl_on = 1;
+    cfg->ctl_vmax = packed_iq_max(tab);
   }
+  cfg->h.mod_nosat = mod_nosat_ok(cfg->h, std::max(packed_iq_max(cfg->h_crs), cfg->ctl_vmax));
   if (upload_remap(cfg) != 0) return -1;
   HCK(hipMemcpy(cfg->d, &cfg->h, sizeof(cfg_dev_t), hipMemcpyHostToDevice), -1);
   return 0;

@@ -163,3 +163,38 @@ def test_fused_levels_equal_reference_chain_on_adversarial_bits(gpu, subframe):
             out = np.zeros(fp.samples_per_tti + 64, dtype=np.int32)
             O.ref_ofdm().ref_glue_normal_prefix_mod(O.P(g), O.P(out), nsymb, O.P(O.frame_geometry(fp)))
             assert np.array_equal(iq[i, a], out[:fp.samples_per_tti]), (subframe, i, a)
+
+
+def test_full_grid_fused_levels_equal_saturating_levels(gpu):
+    """The CRS kernel (CRS + PCFICH / PDCCH + PSS / SSS / PBCH / PHICH in the grid, bench --full-grid):
+    the range check covers the static REs' values too; adversarial e bits over subframe indices 0..9
+    give identical IQ on the fused and the saturating kernels."""
+    import bench
+    p = gpu.make_params("C3", subframe=0, subframe_step=1, with_crs=1)
+    probe = gpu.TxPipeline(p, 10, alloc=False)
+    G = [[probe.G(cw, sf) for cw in range(2)] for sf in range(10)]
+    ew = probe.ebits_words
+    probe.close()
+    rng = np.random.default_rng(0xF6)
+    words = np.zeros((10, 2, ew), dtype=np.uint32)
+    for sf in range(10):
+        syms = _patterns(G[sf][0] // 6, rng)[sf % N_SF]
+        for cw in range(2):
+            words[sf, cw], _ = _words(syms[cw], G[sf][cw], ew)
+    out = []
+    for sat in (False, True):
+        if sat:
+            os.environ["OAI4G_MOD_SAT"] = "1"
+        try:
+            pipe = gpu.TxPipeline(p, 10)
+            bench.full_grid_setup(pipe, p, "C3")
+        finally:
+            os.environ.pop("OAI4G_MOD_SAT", None)
+        assert pipe.mod_nosat == (not sat)
+        pipe.upload_ebits(words)
+        pipe.modulate_only()
+        pipe.sync()
+        out.append(pipe.iq())
+        pipe.close()
+    for sf in range(10):
+        assert np.array_equal(out[0][sf], out[1][sf]), sf
