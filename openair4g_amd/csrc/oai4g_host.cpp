@@ -575,9 +575,10 @@ static void qam_tables_scaled(int Qm, int16_t amp, int16_t srho_a, int16_t srho_
  * 1/32; the leaf's are parts of 16-point DFTs, inside the 64-level's classes.
  * Every twiddle has modulus < 1 (Q15, |t| <= 32767.7), so a value's modulus is at most (occupied
  * subcarriers of its class) x (largest input modulus) x scale, plus the truncations of the levels
- * below (< 64 in modulus).  Inputs of C3's kernel are the CDD pairs (floor((x0 + x1) / 2),
- * +-floor((x0 - x1) / 2)) of two QAM words, components <= the largest QAM level V, modulus <=
- * sqrt(2) V, and only 12 N_RB_DL subcarriers carry anything.  When the four bounds stay inside
+ * below (< 64 in modulus).  Every transform input is a QAM word (TM1), a sign-flipped / swapped one
+ * (ALAMOUTI), a CDD pair (floor((x0 + x1) / 2), +-floor((x0 - x1) / 2)) of two (LARGE_CDD) or a halved
+ * one (4-port CDD): components <= the largest level V of the configuration's QAM / QPSK tables,
+ * modulus <= sqrt(2) V, and only 12 N_RB_DL subcarriers carry anything.  When the four bounds stay inside
  * int16 with a margin of 128, no add of those levels saturates or wraps, packs_epi32 never clamps
  * and no operand is -32768, whatever the bits: the no-saturation forms are then the reference's
  * arithmetic.  (C3: V = 553, R = 782.1; 39 R + 128 = 30629, 151 R / 8 + 128 = 14890, 601 R / 16 +
@@ -588,13 +589,14 @@ static void qam_tables_scaled(int Qm, int16_t amp, int16_t srho_a, int16_t srho_
  * ---------------------------------------------------------------------------------------- */
 static uint32_t mod_nosat_ok(const cfg_dev_t &h, int v_static)
 {
-  if (h.log2N != 11 || h.mimo_mode != OAI4G_LARGE_CDD || h.n_ant != 2 || h.n_cw != 2 || getenv("OAI4G_MOD_SAT"))
-    return 0;
+  if (h.log2N != 11 || h.nsymb != 14 || getenv("OAI4G_MOD_SAT")) return 0;
   int v = v_static;
   for (uint32_t cw = 0; cw < h.n_cw; cw++) {
     const cw_dev_t &c = h.cw[cw];
     for (int i = 0; i < 8; i++) v = std::max(v, std::max(std::abs((int)c.qam_a[i]), std::abs((int)c.qam_b[i])));
     v = std::max(v, std::max(std::abs((int)c.qpsk_a), std::abs((int)c.qpsk_b)));
+    for (int i = 0; i < 2; i++)
+      v = std::max(v, std::max(std::abs((int)c.alm_qpsk[i][0]), std::abs((int)c.alm_qpsk[i][1])));
   }
   const double R = std::sqrt(2.0) * v, band = 12.0 * h.N_RB_DL;
   const double c32 = std::ceil(band / 32) + 1, c8 = std::ceil(band / 8) + 1, c2 = std::ceil(band / 2) + 1;

@@ -1362,13 +1362,13 @@ template <int LOG2N, int MODE, bool ECP>
 static hipError_t launch_modofdm_c(const cfg_dev_t *d_cfg, const cfg_dev_t *h_cfg, int sf0, int n_items,
                                    const uint32_t *d_ebits, int32_t *d_iq, hipStream_t s)
 {
-  /* the no-saturation forms: C3's kernels (2048 points, two-antenna LARGE_CDD) when the range check passed */
+  /* the no-saturation forms (2048 points, normal prefix) when the range check passed */
   if (h_cfg->with_crs || h_cfg->ctl_on) {
-    if constexpr (LOG2N == 11 && MODE == 2 && !ECP)
+    if constexpr (LOG2N == 11 && !ECP)
       if (h_cfg->mod_nosat) return launch_modofdm_t<LOG2N, MODE, true, ECP, true>(d_cfg, h_cfg, sf0, n_items, d_ebits, d_iq, s);
     return launch_modofdm_t<LOG2N, MODE, true, ECP>(d_cfg, h_cfg, sf0, n_items, d_ebits, d_iq, s);
   }
-  if constexpr (LOG2N == 11 && MODE == 2 && !ECP)
+  if constexpr (LOG2N == 11 && !ECP)
     if (h_cfg->mod_nosat) return launch_modofdm_t<LOG2N, MODE, false, ECP, true>(d_cfg, h_cfg, sf0, n_items, d_ebits, d_iq, s);
   return launch_modofdm_t<LOG2N, MODE, false, ECP>(d_cfg, h_cfg, sf0, n_items, d_ebits, d_iq, s);
 }

@@ -26,32 +26,36 @@ import oracle_lib as O
 pytestmark = pytest.mark.gpu
 
 N_SF = 8
-Q64 = [15169, 5057, 25281, 35393, -15169, -5057, -25281, -35393]   # raw 64-QAM levels by index (sign only matters)
+LEVELS = {2: None, 4: [10362, 31086, -10362, -31086], 6: [15169, 5057, 25281, 35393, -15169, -5057, -25281, -35393]}
 
 
-def _level_index(v):
-    """qam_map's 64-QAM (I, Q) level indices of symbol value v (bit j = the RE's j-th e bit)."""
-    ir = ((v & 1) << 2) | (((v >> 2) & 1) << 1) | ((v >> 4) & 1)
-    ii = (((v >> 1) & 1) << 2) | (((v >> 3) & 1) << 1) | ((v >> 5) & 1)
-    return ir, ii
+def _level(v, Qm):
+    """qam_map's (I, Q) levels of symbol value v (bit j = the RE's j-th e bit), raw table values;
+    QPSK: bit 0 / 1 set = negative I / Q"""
+    if Qm == 2:
+        return (-1 if v & 1 else 1), (-1 if v & 2 else 1)
+    if Qm == 4:
+        ir, ii = ((v & 1) << 1) | ((v >> 2) & 1), (v & 2) | ((v >> 3) & 1)
+    else:
+        ir = ((v & 1) << 2) | (((v >> 2) & 1) << 1) | ((v >> 4) & 1)
+        ii = (((v >> 1) & 1) << 2) | (((v >> 3) & 1) << 1) | ((v >> 5) & 1)
+    return LEVELS[Qm][ir], LEVELS[Qm][ii]
 
 
-def _corner(si, sq):
-    """the symbol value whose (I, Q) is the outer corner with signs (si, sq)"""
-    for v in range(64):
-        ir, ii = _level_index(v)
-        if abs(Q64[ir]) == 35393 and abs(Q64[ii]) == 35393 and np.sign(Q64[ir]) == si and np.sign(Q64[ii]) == sq:
-            return v
-    raise AssertionError
+def _corners(Qm):
+    """symbol values of the outer corners (+,+), (-,+), (-,-), (+,-)"""
+    top = 1 if Qm == 2 else max(LEVELS[Qm])
+    out = []
+    for si, sq in ((1, 1), (-1, 1), (-1, -1), (1, -1)):
+        out.append(next(v for v in range(1 << Qm) if _level(v, Qm) == (si * top, sq * top)))
+    return np.array(out)
 
 
-PP, MP, MM, PM = _corner(1, 1), _corner(-1, 1), _corner(-1, -1), _corner(1, -1)
-
-
-def _patterns(n_re, rng):
+def _patterns(n_re, Qm, rng):
     """(cw0 symbols, cw1 symbols) per subframe of the batch"""
     idx = np.arange(n_re)
-    rot = np.array([PP, MP, MM, PM])
+    rot = _corners(Qm)
+    PP, MM, PM = rot[0], rot[2], rot[3]
     out = [
         (np.full(n_re, PP), np.full(n_re, PP)),                         # all REs one corner: class DC bins
         (np.full(n_re, PP), np.full(n_re, MM)),                         # opposed codewords: y0 ~ 0, |d| max
@@ -59,15 +63,15 @@ def _patterns(n_re, rng):
         (rot[idx & 3], rot[idx & 3]),                                   # quarter turn per RE
         (rot[(idx >> 1) & 3], rot[3 - ((idx >> 1) & 3)]),              # both codewords, opposite turns
         (rot[rng.integers(0, 4, n_re)], rot[rng.integers(0, 4, n_re)]),   # random corners
-        (rng.integers(0, 64, n_re), rng.integers(0, 64, n_re)),         # random symbols
+        (rng.integers(0, 1 << Qm, n_re), rng.integers(0, 1 << Qm, n_re)),   # random symbols
         (np.full(n_re, MM), np.full(n_re, PM)),
     ]
     assert len(out) == N_SF
     return out
 
 
-def _words(sym, G, n_words):
-    bits = ((np.asarray(sym, dtype=np.uint32)[:, None] >> np.arange(6, dtype=np.uint32)) & 1).astype(np.uint8).ravel()
+def _words(sym, Qm, G, n_words):
+    bits = ((np.asarray(sym, dtype=np.uint32)[:, None] >> np.arange(Qm, dtype=np.uint32)) & 1).astype(np.uint8).ravel()
     assert bits.size == G
     buf = np.zeros(n_words * 4, dtype=np.uint8)
     packed = np.packbits(bits, bitorder="little")
@@ -75,11 +79,13 @@ def _words(sym, G, n_words):
     return buf.view(np.uint32), bits
 
 
-def _run(gpu, p, words, sat):
+def _run(gpu, p, words, sat, n_sf=N_SF, setup=None):
     if sat:
         os.environ["OAI4G_MOD_SAT"] = "1"
     try:
-        pipe = gpu.TxPipeline(p, N_SF)
+        pipe = gpu.TxPipeline(p, n_sf)
+        if setup:
+            setup(pipe)
     finally:
         os.environ.pop("OAI4G_MOD_SAT", None)
     nosat = pipe.mod_nosat
@@ -91,19 +97,24 @@ def _run(gpu, p, words, sat):
     return nosat, iq
 
 
-def _case(gpu, subframe):
-    p = gpu.make_params("C3", subframe=subframe, subframe_step=0)
-    probe = gpu.TxPipeline(p, N_SF, alloc=False)
-    G = [probe.G(cw, subframe) for cw in range(2)]
+def _case(gpu, subframe, name="C3", step=0, n_sf=N_SF, **over):
+    """adversarial packed e-bit words: batch element i (subframe index subframe + i step) carries
+    pattern i mod N_SF on every codeword"""
+    p = gpu.make_params(name, subframe=subframe, subframe_step=step, **over)
+    probe = gpu.TxPipeline(p, n_sf, alloc=False)
+    sfs = [(subframe + i * step) % 10 for i in range(n_sf)]
+    G = [[probe.G(cw, sf) for cw in range(p.n_cw)] for sf in sfs]
     ew = probe.ebits_words
     probe.close()
-    rng = np.random.default_rng(0xC3 + subframe)
-    words = np.zeros((N_SF, 2, ew), dtype=np.uint32)
+    Qm = [gpu.lib().oai4g_get_Qm(p.mcs[cw]) for cw in range(p.n_cw)]
+    rng = np.random.default_rng(0xC3 + subframe + 101 * len(name))
+    words = np.zeros((n_sf, p.n_cw, ew), dtype=np.uint32)
     bits = []
-    for i, syms in enumerate(_patterns(G[0] // 6, rng)):
+    for i in range(n_sf):
         row = []
-        for cw in range(2):
-            words[i, cw], b = _words(syms[cw], G[cw], ew)
+        for cw in range(p.n_cw):
+            syms = _patterns(G[i][cw] // Qm[cw], Qm[cw], rng)[i % N_SF][cw]
+            words[i, cw], b = _words(syms, Qm[cw], G[i][cw], ew)
             row.append(b)
         bits.append(row)
     return p, words, bits
@@ -121,15 +132,19 @@ def test_range_check_admits_c3_and_refuses_large_amplitudes(gpu):
         pipe = gpu.TxPipeline(p, 1, alloc=False)
         assert pipe.mod_nosat == ok, amp
         pipe.close()
-    p = gpu.make_params("C2")                              # TM1: no fused kernel
-    pipe = gpu.TxPipeline(p, 1, alloc=False)
+    for name in ("C2", "TM2", "C4"):                       # every 2048-point transmit mode
+        pipe = gpu.TxPipeline(gpu.make_params(name), 1, alloc=False)
+        assert pipe.mod_nosat, name
+        pipe.close()
+    pipe = gpu.TxPipeline(gpu.make_params("C1"), 1, alloc=False)   # 128 points: no fused kernel
     assert not pipe.mod_nosat
     pipe.close()
 
 
-@pytest.mark.parametrize("subframe", [7, 0, 5])
-def test_fused_levels_equal_saturating_levels_on_adversarial_bits(gpu, subframe):
-    p, words, _ = _case(gpu, subframe)
+@pytest.mark.parametrize("name,subframe", [("C3", 7), ("C3", 0), ("C3", 5), ("C2", 7), ("TM2", 7), ("TM2", 0),
+                                            ("C4", 7), ("C4", 5)])
+def test_fused_levels_equal_saturating_levels_on_adversarial_bits(gpu, name, subframe):
+    p, words, _ = _case(gpu, subframe, name)
     ns, iq_ns = _run(gpu, p, words, sat=False)
     s, iq_sat = _run(gpu, p, words, sat=True)
     assert ns and not s
@@ -139,7 +154,8 @@ def test_fused_levels_equal_saturating_levels_on_adversarial_bits(gpu, subframe)
     # the adversarial subframes do reach large sample values (the bound is not vacuous)
     pk = np.abs(iq_ns.view(np.int16).reshape(N_SF, -1).astype(np.int32)).max(axis=1)
     print("peak |sample| per pattern:", pk.tolist())
-    assert pk[0] > 8000, pk
+    if name in ("C3", "C2"):
+        assert pk[0] > 8000, pk
 
 
 @pytest.mark.parametrize("subframe", [7, 0])
@@ -165,36 +181,16 @@ def test_fused_levels_equal_reference_chain_on_adversarial_bits(gpu, subframe):
             assert np.array_equal(iq[i, a], out[:fp.samples_per_tti]), (subframe, i, a)
 
 
-def test_full_grid_fused_levels_equal_saturating_levels(gpu):
-    """The CRS kernel (CRS + PCFICH / PDCCH + PSS / SSS / PBCH / PHICH in the grid, bench --full-grid):
+@pytest.mark.parametrize("name", ["C3", "C2", "C4"])
+def test_full_grid_fused_levels_equal_saturating_levels(gpu, name):
+    """The CRS kernels (CRS + PCFICH / PDCCH + PSS / SSS / PBCH / PHICH in the grid, bench --full-grid):
     the range check covers the static REs' values too; adversarial e bits over subframe indices 0..9
     give identical IQ on the fused and the saturating kernels."""
     import bench
-    p = gpu.make_params("C3", subframe=0, subframe_step=1, with_crs=1)
-    probe = gpu.TxPipeline(p, 10, alloc=False)
-    G = [[probe.G(cw, sf) for cw in range(2)] for sf in range(10)]
-    ew = probe.ebits_words
-    probe.close()
-    rng = np.random.default_rng(0xF6)
-    words = np.zeros((10, 2, ew), dtype=np.uint32)
+    p, words, _ = _case(gpu, 0, name, step=1, n_sf=10, with_crs=1)
+    setup = lambda pipe: bench.full_grid_setup(pipe, p, name)   # noqa: E731
+    ns, iq_ns = _run(gpu, p, words, False, n_sf=10, setup=setup)
+    s, iq_sat = _run(gpu, p, words, True, n_sf=10, setup=setup)
+    assert ns and not s
     for sf in range(10):
-        syms = _patterns(G[sf][0] // 6, rng)[sf % N_SF]
-        for cw in range(2):
-            words[sf, cw], _ = _words(syms[cw], G[sf][cw], ew)
-    out = []
-    for sat in (False, True):
-        if sat:
-            os.environ["OAI4G_MOD_SAT"] = "1"
-        try:
-            pipe = gpu.TxPipeline(p, 10)
-            bench.full_grid_setup(pipe, p, "C3")
-        finally:
-            os.environ.pop("OAI4G_MOD_SAT", None)
-        assert pipe.mod_nosat == (not sat)
-        pipe.upload_ebits(words)
-        pipe.modulate_only()
-        pipe.sync()
-        out.append(pipe.iq())
-        pipe.close()
-    for sf in range(10):
-        assert np.array_equal(out[0][sf], out[1][sf]), sf
+        assert np.array_equal(iq_ns[sf], iq_sat[sf]), (name, sf)
