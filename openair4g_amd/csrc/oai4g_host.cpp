@@ -1185,7 +1185,16 @@ static int upload_remap(oai4g_tx_config *cfg)
 #if OAI4G_MOD_STAGE
           /* data RE (idx | parity << 15, idx < 3N/4): the byte offset of its staged entry (2 idx, or 8 idx
            * for the precoded pairs: < 8 * 1536 < 2^15) */
-          if (code < OAI4G_CTL_CODE) code = (uint16_t)((code & 0x8000u) | ((code & 0x3FFFu) << esh));
+          if (code < OAI4G_CTL_CODE) {
+            /* the precoded pairs carry the CDD sign already: the staging step stores -d for an odd
+             * data index.  The reference alternates the sign per RE within each RB
+             * (dlsch_modulation.c:733-749) and every RB of a two-port grid holds an even number of
+             * data REs (12, 8 beside the 4 CRS REs, 6 / 4 in a half RB), so the parity is the index's;
+             * checked here for every RE */
+            const uint32_t idx = code & 0x3FFFu, par = code >> 15;
+            if (pre && par != (idx & 1u)) { set_err("LARGE_CDD: CDD parity differs from the RE index parity"); return -1; }
+            code = (uint16_t)(((pre ? 0u : par) << 15) | (idx << esh));
+          }
 #endif
           both[n + sl * N + t * 16 + k] = code;
 #if OAI4G_MOD_STAGE

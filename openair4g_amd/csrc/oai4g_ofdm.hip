@@ -1024,7 +1024,9 @@ __global__ void __launch_bounds__(128) MODOFDM_ATTR k_modofdm(const cfg_dev_t *_
           const uint32_t a = v0[j], b = v1[j];
           const s16x2 h = u2c(a ^ b) >> (s16x2){1, 1};
           o[2 * j] = c2u(u2c(a & b) + h);           /* y0 = floor((x0 + x1) / 2) per int16 lane */
-          o[2 * j + 1] = c2u(h - u2c(~a & b));      /* d  = floor((x0 - x1) / 2) */
+          /* d = floor((x0 - x1) / 2); RE 4q + j of odd index stores -d (wrapping): its CDD sign
+           * (dlsch_modulation.c's per-RB alternation equals the index parity, host-checked) */
+          o[2 * j + 1] = (j & 1) ? c2u(u2c(~a & b) - h) : c2u(h - u2c(~a & b));
         }
         u32x4_t *dst = (u32x4_t *)(lds_p + 4 * q);
         dst[0] = (u32x4_t){o[0], o[1], o[2], o[3]};
@@ -1115,8 +1117,8 @@ __global__ void __launch_bounds__(128) MODOFDM_ATTR k_modofdm(const cfg_dev_t *_
               for (int a = 0; a < NA; a++) x[a][n] = u2c(z);
             }
           if constexpr (PRE) {
-            /* one 8-byte read per RE: the pair staged for its data index (codes 8 idx | parity << 15;
-             * every non-data code addresses the zero pair, clamped when CRS / control codes occur) */
+            /* one 8-byte read per RE: the pair staged for its data index, CDD sign included (codes
+             * 8 idx; every non-data code addresses the zero pair, clamped when CRS / control codes occur) */
             const char *pb = (const char *)lds_p;
 #pragma unroll
             for (int g = 0; g < NZ; g += GZ) {
@@ -1131,13 +1133,9 @@ __global__ void __launch_bounds__(128) MODOFDM_ATTR k_modofdm(const cfg_dev_t *_
               }
 #pragma unroll
               for (int n = 0; n < GZ; n++) {
-                /* y1 = s d: the parity bit 15 of the code -> lane mask m, (d ^ m) - m per int16 lane */
                 const int i = act(g + n);
-                const uint32_t m = (uint32_t)((int32_t)(code[n] << 16) >> 31);
-                uint32_t r;
-                asm("v_xor_b32_e32 %0, %1, %2\n\tv_pk_sub_u16 %0, %0, %2" : "=&v"(r) : "v"(v[n].y), "v"(m));
                 x[0][i] = u2c(v[n].x);
-                x[1][i] = u2c(r);
+                x[1][i] = u2c(v[n].y);
               }
             }
           } else
