@@ -375,13 +375,15 @@ def bench_c5(args, world, rank, dist, torch):
         # rounds before the batch grew: the same kernel on a smaller launch, 5 timed runs
         d2 = (oai.TurboDecoder8Batch if args.c5_bits == 8 else oai.TurboDecoderBatch)(C5_K, 2048 * C5_CB)
         d2.upload_tiled(llr)
+        # the upload leaves the GPU idle long enough for its clocks to drop: settle them again first
+        clock_settle(lambda: d2.run(max_iterations=8, crc_type=crc_type), d2.results, args.settle_ms)
         d2.run(max_iterations=8, crc_type=crc_type)
         d2.results()
         t2 = time.perf_counter()
-        for _ in range(5):
+        for _ in range(10):
             d2.run(max_iterations=8, crc_type=crc_type)
         oai.lib().oai4g_sync()
-        small = {"subframes_per_step": 2048, "value": 2048 * 5 / (time.perf_counter() - t2), "unit": "subframes/s"}
+        small = {"subframes_per_step": 2048, "value": 2048 * 10 / (time.perf_counter() - t2), "unit": "subframes/s"}
         d2.close()
     alg = n_cb * (2 * (3 * C5_K + 12) + C5_K // 8)          # LLR read + bits written
     ach = alg / (per_launch_ms * 1e-3) / 1e9
