@@ -775,7 +775,7 @@ struct modofdm_geom {
   static constexpr int EW = (6 * ((N * 3) / 4)) / 32 + 4;
   /* OAI4G_MOD_STAGE: per codeword one 16-bit QAM-table address per data RE (12 N_RB + 3 <= 3N/4
    * entries, host-checked), two sentinel entries at SENT; quad q = 4 REs, QPT quads per thread */
-  static constexpr int SENT = (N * 3) / 4, SW = SENT + 4, QPT = 3, QROW = 65;
+  static constexpr int SENT = (N * 3) / 4, SW = SENT + 4, QPT = 3, QROW = 64;
   /* guard band: leaf inputs t + T n with n in [ZLO, ZHI] fall between subcarrier 6 N_RB_DL and
    * first_carrier_offset = N - 6 N_RB_DL for every thread t (N_RB_DL 6/25/50/100: n = 5..10;
    * 15: n = 6..9; host-checked), where the reference's grid is zero */
@@ -837,12 +837,14 @@ __global__ void __launch_bounds__(128) MODOFDM_ATTR k_modofdm(const cfg_dev_t *_
   /* per codeword, the qtab byte address of every data RE's QAM word: entries 4q..4q+3 staged from
    * quad q's 4 Qm bits; entries SENT, SENT + 1 address the zero word that non-data REs read */
   constexpr int SW = G::SW, SENT = G::SENT, QPT = G::QPT, QROW = G::QROW;
-  constexpr uint32_t QZERO = 4u * 64u;          /* byte address of qtab[0][64] = 0 */
+  constexpr uint32_t QZERO = 4u * 4u * QROW;     /* byte address of the zero word behind the 4 rows */
   constexpr bool ALIAS = OAI4G_MOD_ALIAS && LOG2N == 11;
   static_assert(!ALIAS || (UNITS == 1 && 2 * SW <= 2 * NA * LDSW), "staged addresses must fit the exchange");
   __shared__ __attribute__((aligned(16))) uint16_t lds_s_own[ALIAS ? 1 : UNITS][2][SW];
   uint16_t(*lds_s)[2][SW] = ALIAS ? (uint16_t(*)[2][SW])lds_data : lds_s_own;
-  __shared__ uint32_t qtab[4][QROW];            /* row cw * 2 + pilot symbol: 64 packed IQ words + 0 */
+  /* row cw * 2 + pilot symbol: 64 packed IQ words, 256 bytes, so a row base ORs into an entry's byte
+   * offset (bits 8-9 against 2-7); then the zero word */
+  __shared__ uint32_t qtab[4 * QROW + 1];
   /* OAI4G_MOD_PRE (C3's kernel): the staging step looks the QAM words of both codewords up and stores
    * their CDD sums per data RE, (y0, d) = ((x0 + x1) >> 1, (x0 - x1) >> 1) lane by lane: the RE step is
    * then one 8-byte LDS read and the sign of y1 = s d, instead of two dependent LDS round trips per
@@ -860,10 +862,10 @@ __global__ void __launch_bounds__(128) MODOFDM_ATTR k_modofdm(const cfg_dev_t *_
   const uint32_t n_ant = c->n_ant, nsymb = c->nsymb;
   constexpr uint32_t sps = ECP ? 6 : 7;
 #if OAI4G_MOD_STAGE
-  for (uint32_t i = threadIdx.x; i < 4 * QROW; i += blockDim.x) {
+  for (uint32_t i = threadIdx.x; i < 4 * QROW + 1; i += blockDim.x) {
     const uint32_t row = i / QROW, bits = i - row * QROW, cw = row >> 1, pil = row & 1;
     uint32_t v = 0;
-    if (bits < 64) {
+    if (row < 4) {
       if constexpr (MODE == 1) {        /* one codeword: rows 0/1 = TA, rows 2/3 = TB */
         const cw_dev_t &w = c->cw[0];
         v = c2u(cw ? alm_tb(bits, w, pil) : alm_ta(bits, w, pil));
@@ -872,7 +874,7 @@ __global__ void __launch_bounds__(128) MODOFDM_ATTR k_modofdm(const cfg_dev_t *_
         v = c2u(qam_map(bits, w.Qm, pil ? w.qam_b : w.qam_a, pil ? w.qpsk_b : w.qpsk_a));
       }
     }
-    qtab[row][bits] = v;
+    qtab[i] = v;
   }
   if (!ALIAS)
     for (uint32_t i = threadIdx.x; i < UNITS * 4; i += blockDim.x) lds_s[i >> 2][(i >> 1) & 1][SENT + (i & 1)] = QZERO;
@@ -890,6 +892,10 @@ __global__ void __launch_bounds__(128) MODOFDM_ATTR k_modofdm(const cfg_dev_t *_
 #endif
   const uint32_t Qm0 = c->cw[0].Qm, Qm1 = c->cw[1].Qm;
   const uint32_t mask0 = (1u << Qm0) - 1u, mask1 = (1u << Qm1) - 1u;
+  /* 4 Qm t: the lane part of a quad's bit offset (loop-invariant) */
+  const uint32_t qt0 = 4u * Qm0 * (uint32_t)t, qt1 = 4u * Qm1 * (uint32_t)t;
+  (void)qt0;
+  (void)qt1;
   __syncthreads();
 
   /* software pipeline: the RE codes and e-bit words of a unit's next item are loaded while the
@@ -930,11 +936,14 @@ __global__ void __launch_bounds__(128) MODOFDM_ATTR k_modofdm(const cfg_dev_t *_
     if (act && nre) {
       const uint8_t *esf = (const uint8_t *)(ebits + (size_t)(sf * cc->n_cw) * cc->ebits_words);
       const uint32_t nq = (nre + 3) >> 2;
+      /* bit (re0 + 4 q) Qm of quad q = t + k T as re0 Qm + min(4 Qm t + 4 Qm T k, 4 Qm (nq - 1)): uniform
+       * terms and the loop-invariant 4 Qm t, no per-lane multiply */
+      const uint32_t b0 = re0 * Qm0, lim0 = 4 * Qm0 * (nq - 1), b1 = re0 * Qm1, lim1 = 4 * Qm1 * (nq - 1);
 #pragma unroll
       for (int k = 0; k < QPT; k++) {   /* unconditional (quads past nq re-read the last one): no branch */
-        const uint32_t q = min((uint32_t)t + (uint32_t)(k * T), nq - 1);
-        pf.x0[k] = ld_u32_any(esf + (((re0 + 4 * q) * Qm0) >> 3));
-        if constexpr (CW2) pf.x1[k] = ld_u32_any(esf + (size_t)4 * cc->ebits_words + (((re0 + 4 * q) * Qm1) >> 3));
+        pf.x0[k] = ld_u32_any(esf + ((b0 + min(qt0 + (uint32_t)(4 * T * k) * Qm0, lim0)) >> 3));
+        if constexpr (CW2)
+          pf.x1[k] = ld_u32_any(esf + (size_t)4 * cc->ebits_words + ((b1 + min(qt1 + (uint32_t)(4 * T * k) * Qm1, lim1)) >> 3));
       }
     }
 #else
@@ -1000,10 +1009,21 @@ __global__ void __launch_bounds__(128) MODOFDM_ATTR k_modofdm(const cfg_dev_t *_
     } else if (ALIAS && active && t < 4) lds_s[0][t >> 1][SENT + (t & 1)] = QZERO;
     if (active && nre) {
       const uint32_t nq = (nre + 3) >> 2;
-      auto stage = [&](uint32_t xw, uint32_t q, uint32_t Qm, uint32_t mask, uint32_t ra, uint32_t rb, uint16_t *dst) {
-        const uint32_t x = xw >> (((re0 + 4 * q) * Qm) & 7u);
-        const uint32_t s0 = ra + 4 * (x & mask), s1 = rb + 4 * ((x >> Qm) & mask);
-        const uint32_t s2 = ra + 4 * ((x >> (2 * Qm)) & mask), s3 = rb + 4 * ((x >> (3 * Qm)) & mask);
+      /* quad q = t + k T starts at bit (re0 + 4 q) Qm of the codeword, (re0 Qm + 4 Qm t) mod 8 into its
+       * prefetched bytes for every k (4 Qm T is a multiple of 8); x << 2 puts entry j's table offset at
+       * bits j Qm + 2.., so an entry is one shift and one v_bitop3 (offset & (mask << 2)) | row base */
+      const uint32_t sh0 = (re0 * Qm0 + qt0) & 7u, sh1 = (re0 * Qm1 + qt1) & 7u;
+      const uint32_t m40 = mask0 << 2, m41 = mask1 << 2;
+      auto ent = [&](uint32_t x4, uint32_t shift, uint32_t m4, uint32_t row) {
+        uint32_t r;
+        /* (a & b) | c; one SGPR operand at most (gfx9 constant bus) */
+        asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0xea" : "=v"(r) : "v"(x4 >> shift), "s"(m4), "v"(row));
+        return r;
+      };
+      auto stage = [&](uint32_t xw, uint32_t q, uint32_t sh, uint32_t Qm, uint32_t m4, uint32_t ra, uint32_t rb, uint16_t *dst) {
+        const uint32_t x4 = (xw >> sh) << 2;
+        const uint32_t s0 = ent(x4, 0, m4, ra), s1 = ent(x4, Qm, m4, rb);
+        const uint32_t s2 = ent(x4, 2 * Qm, m4, ra), s3 = ent(x4, 3 * Qm, m4, rb);
         *(u32x2_t *)(dst + 4 * q) = (u32x2_t){s0 | (s1 << 16), s2 | (s3 << 16)};
       };
       constexpr uint32_t RB = 4u * QROW;   /* bytes per qtab row */
@@ -1011,12 +1031,12 @@ __global__ void __launch_bounds__(128) MODOFDM_ATTR k_modofdm(const cfg_dev_t *_
       /* PRE: quad q's 4 QAM words of each codeword (8 independent LDS reads), their CDD sums, and the
        * 4 (y0, d) pairs as two 16-byte stores */
       auto stage_pre = [&](uint32_t xw0, uint32_t xw1, uint32_t q) {
-        const uint32_t x0 = xw0 >> (((re0 + 4 * q) * Qm0) & 7u), x1 = xw1 >> (((re0 + 4 * q) * Qm1) & 7u);
+        const uint32_t x0 = (xw0 >> sh0) << 2, x1 = (xw1 >> sh1) << 2;
         uint32_t v0[4], v1[4];
 #pragma unroll
         for (int j = 0; j < 4; j++) {
-          v0[j] = *(const uint32_t *)(qbs + pil * RB + 4 * ((x0 >> (j * Qm0)) & mask0));
-          v1[j] = *(const uint32_t *)(qbs + (2 + pil) * RB + 4 * ((x1 >> (j * Qm1)) & mask1));
+          v0[j] = *(const uint32_t *)(qbs + ent(x0, j * Qm0, m40, pil * RB));
+          v1[j] = *(const uint32_t *)(qbs + ent(x1, j * Qm1, m41, (2 + pil) * RB));
         }
         uint32_t o[8];
 #pragma unroll
@@ -1039,9 +1059,9 @@ __global__ void __launch_bounds__(128) MODOFDM_ATTR k_modofdm(const cfg_dev_t *_
           if constexpr (PRE) {
             stage_pre(pf.x0[k], pf.x1[k], q);
           } else {
-            if constexpr (MODE == 1) stage(pf.x0[k], q, Qm0, mask0, pil * RB, (2 + pil) * RB, lds_s[unit][0]);
-            else stage(pf.x0[k], q, Qm0, mask0, pil * RB, pil * RB, lds_s[unit][0]);
-            if constexpr (CW2) stage(pf.x1[k], q, Qm1, mask1, (2 + pil) * RB, (2 + pil) * RB, lds_s[unit][1]);
+            if constexpr (MODE == 1) stage(pf.x0[k], q, sh0, Qm0, m40, pil * RB, (2 + pil) * RB, lds_s[unit][0]);
+            else stage(pf.x0[k], q, sh0, Qm0, m40, pil * RB, pil * RB, lds_s[unit][0]);
+            if constexpr (CW2) stage(pf.x1[k], q, sh1, Qm1, m41, (2 + pil) * RB, (2 + pil) * RB, lds_s[unit][1]);
           }
         }
       }
