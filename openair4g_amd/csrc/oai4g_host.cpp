@@ -1173,10 +1173,12 @@ static int upload_remap(oai4g_tx_config *cfg)
     /* natural, thread-major, thread-major with the non-data codes on the zero sentinel */
     std::vector<uint16_t> both(3 * n);
     std::copy(cfg->h_remap.begin(), cfg->h_remap.end(), both.begin());
-    /* staged entries: 2-byte QAM-table addresses, or (OAI4G_MOD_PRE, C3's kernel) 8-byte (y0, d) pairs */
+    /* staged entries: 2-byte QAM-table addresses, or (OAI4G_MOD_PRE, the 2048-point kernels) 8-byte
+     * (y0, d) pairs of two-antenna LARGE_CDD / 4-byte QAM words of TM1 */
     const bool pre = OAI4G_MOD_STAGE && OAI4G_MOD_PRE && cfg->h.mimo_mode == OAI4G_LARGE_CDD && cfg->h.n_ant == 2 &&
                      cfg->h.log2N == 11;
-    const uint32_t esh = pre ? 3u : 1u;
+    const bool pre1 = OAI4G_MOD_STAGE && OAI4G_MOD_PRE && cfg->h.mimo_mode == OAI4G_SISO && cfg->h.log2N == 11;
+    const uint32_t esh = pre ? 3u : pre1 ? 2u : 1u;
     const uint16_t sentinel = (uint16_t)(((3u * (uint32_t)N) / 4u) << esh);   /* modofdm_geom::SENT, bytes */
     for (size_t sl = 0; sl < n / N; sl++)
       for (size_t t = 0; t < T; t++)
@@ -1193,7 +1195,7 @@ static int upload_remap(oai4g_tx_config *cfg)
              * checked here for every RE */
             const uint32_t idx = code & 0x3FFFu, par = code >> 15;
             if (pre && par != (idx & 1u)) { set_err("LARGE_CDD: CDD parity differs from the RE index parity"); return -1; }
-            code = (uint16_t)(((pre ? 0u : par) << 15) | (idx << esh));
+            code = (uint16_t)(((pre || pre1 ? 0u : par) << 15) | (idx << esh));
           }
 #endif
           both[n + sl * N + t * 16 + k] = code;

@@ -852,6 +852,11 @@ __global__ void __launch_bounds__(128) MODOFDM_ATTR k_modofdm(const cfg_dev_t *_
   constexpr bool PRE = OAI4G_MOD_PRE && MODE == 2 && ALIAS;
   static_assert(!PRE || SW * 8 <= NA * LDSW * 4, "the precoded pairs must fit the exchange");
   u32x2_t *lds_p = (u32x2_t *)lds_data;
+  /* the same for TM1 (one codeword, one transform): the staging step stores each data RE's QAM word,
+   * the RE step reads it with one 4-byte LDS read (codes 4 idx) */
+  constexpr bool PRE1 = OAI4G_MOD_PRE && MODE == 0 && ALIAS;
+  static_assert(!PRE1 || SW * 4 <= NA * LDSW * 4, "the staged QAM words must fit the exchange");
+  uint32_t *lds_w = (uint32_t *)lds_data;
 #else
   __shared__ uint32_t lds_e[UNITS][2][EW];
   __shared__ uint32_t qtab[2][2][64];          /* [cw][pilot symbol][Qm bits] -> packed IQ */
@@ -1006,6 +1011,8 @@ __global__ void __launch_bounds__(128) MODOFDM_ATTR k_modofdm(const cfg_dev_t *_
      * bits from its prefetched bytes -> 4 entries (ALAMOUTI: even entries TA rows, odd TB rows) */
     if (PRE) {
       if (active && t < 2) lds_p[SENT + t] = (u32x2_t){0u, 0u};                 /* the exchange overwrote them */
+    } else if (PRE1) {
+      if (active && t < 2) lds_w[SENT + t] = 0u;
     } else if (ALIAS && active && t < 4) lds_s[0][t >> 1][SENT + (t & 1)] = QZERO;
     if (active && nre) {
       const uint32_t nq = (nre + 3) >> 2;
@@ -1052,12 +1059,22 @@ __global__ void __launch_bounds__(128) MODOFDM_ATTR k_modofdm(const cfg_dev_t *_
         dst[0] = (u32x4_t){o[0], o[1], o[2], o[3]};
         dst[1] = (u32x4_t){o[4], o[5], o[6], o[7]};
       };
+      /* PRE1: quad q's 4 QAM words (4 independent LDS reads) as one 16-byte store */
+      auto stage_pre1 = [&](uint32_t xw0, uint32_t q) {
+        const uint32_t x0 = (xw0 >> sh0) << 2;
+        uint32_t v0[4];
+#pragma unroll
+        for (int j = 0; j < 4; j++) v0[j] = *(const uint32_t *)(qbs + ent(x0, j * Qm0, m40, pil * RB));
+        *(u32x4_t *)(lds_w + 4 * q) = (u32x4_t){v0[0], v0[1], v0[2], v0[3]};
+      };
 #pragma unroll
       for (int k = 0; k < QPT; k++) {
         const uint32_t q = (uint32_t)t + (uint32_t)(k * T);
         if (q < nq) {
           if constexpr (PRE) {
             stage_pre(pf.x0[k], pf.x1[k], q);
+          } else if constexpr (PRE1) {
+            stage_pre1(pf.x0[k], q);
           } else {
             if constexpr (MODE == 1) stage(pf.x0[k], q, sh0, Qm0, m40, pil * RB, (2 + pil) * RB, lds_s[unit][0]);
             else stage(pf.x0[k], q, sh0, Qm0, m40, pil * RB, pil * RB, lds_s[unit][0]);
@@ -1157,6 +1174,22 @@ __global__ void __launch_bounds__(128) MODOFDM_ATTR k_modofdm(const cfg_dev_t *_
                 x[0][i] = u2c(v[n].x);
                 x[1][i] = u2c(v[n].y);
               }
+            }
+          } else if constexpr (PRE1) {
+            /* one 4-byte read per RE: the QAM word staged for its data index (codes 4 idx) */
+            const char *pb = (const char *)lds_w;
+#pragma unroll
+            for (int g = 0; g < NZ; g += GZ) {
+              uint32_t v[GZ];
+#pragma unroll
+              for (int n = 0; n < GZ; n++) {
+                const int i = act(g + n);
+                const uint32_t code = (rw[i >> 1] >> (16 * (i & 1))) & 0xFFFFu;
+                const uint32_t a = CRS ? min(code & 0x7FFCu, 4u * SENT) : code & 0x7FFCu;
+                v[n] = *(const uint32_t *)(pb + a);
+              }
+#pragma unroll
+              for (int n = 0; n < GZ; n++) x[0][act(g + n)] = u2c(v[n]);
             }
           } else
 #pragma unroll
