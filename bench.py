@@ -405,6 +405,23 @@ def bench_c5(args, world, rank, dist, torch):
                "cpu_model": cpu_model(), "value_all_cores": allc / C5_CB, "cores_all": cores,
                "sample": f"{n} code blocks (K={C5_K}, mode {args.c5_mode}) through the C oracle decoder, "
                          f"single thread, {dt:.1f} s; {nall} on {cores} cores (independent processes)"}
+        if args.c5_bits == 16 and O.ref_td() is not None:
+            # the reference's own CPU decoder where it builds: phy_threegpplte_turbo_decoder_scalar
+            # (3gpplte_turbo_decoder.c:883, compiled unmodified into oracle/_ref/libref_td.so), same
+            # blocks, same iteration cap, CRC24_B (the K = 5504 blocks fit its buffers)
+            from ref_cases import QPP
+            f1, f2 = QPP[C5_K]
+            nr, t2 = 0, time.perf_counter()
+            while time.perf_counter() - t2 < max(2.0, args.cpu_seconds / 2):
+                O.ref_turbo_decode_scalar(llr[nr % len(llr)], C5_K, f1, f2, max_it=8, crc_type=crc_type)
+                nr += 1
+            dr = time.perf_counter() - t2
+            cpu["reference_scalar"] = {
+                "value": nr / C5_CB / dr, "unit": "subframes/s", "cores": 1, "kind": "reference",
+                "sample": f"{nr} code blocks (K={C5_K}) through phy_threegpplte_turbo_decoder_scalar "
+                          f"(3gpplte_turbo_decoder.c:883, the reference compiled unmodified), max 8 iterations, "
+                          f"single thread, {dr:.1f} s",
+                "note": "the reference's scalar decoder; its default SSE 16-bit decoder cannot be built here"}
     if rank == 0:
         print(json.dumps({
             "metric": "UL subframes/sec (C5 turbo decode)" + (", 8-bit decoder" if args.c5_bits == 8 else ""),
