@@ -352,6 +352,13 @@ static __device__ __forceinline__ void idft2048_unit(uint32_t *lds, int t, bool 
   /* pass A: leaves */
   if (active) {
     prod(x);
+#ifndef OAI4G_MOD_PRIO
+/* 1: the item's staging and RE-lookup phase (LDS round trips, little VALU) runs at wave priority 2, the
+ * transform at 0, so the arbiter issues a wave's latency-bound phase ahead of the other waves' VALU
+ * streams (-1.5 %, profiles/mod_prio_r06.txt); 2: also the pass-B / pass-C loads at 1; 3: priority 3 */
+#define OAI4G_MOD_PRIO 1
+#endif
+    if constexpr (OAI4G_MOD_PRIO >= 1) __builtin_amdgcn_s_setprio(0);
     if constexpr (OAI4G_DIAG_MODCUT == 1) {
 #pragma unroll
       for (int a = 0; a < NA; a++) sink(x[a]);
@@ -383,6 +390,7 @@ static __device__ __forceinline__ void idft2048_unit(uint32_t *lds, int t, bool 
   IDFT_SYNC();
   /* pass B: 64- and 256-levels of the 256-point transform j = t & 7 at k4 = t >> 3 */
   const int j = t & 7, k4 = t >> 3;
+  if constexpr (OAI4G_MOD_PRIO == 2) __builtin_amdgcn_s_setprio(1);
   if (active) {
     const uint32_t ro = (uint32_t)k4 * 144u + 2u * j;
 #pragma unroll
@@ -397,6 +405,7 @@ static __device__ __forceinline__ void idft2048_unit(uint32_t *lds, int t, bool 
         }
   }
   IDFT_SYNC();   /* E2 aliases E1 */
+  if constexpr (OAI4G_MOD_PRIO == 2) __builtin_amdgcn_s_setprio(0);
   if (active) {
     /* E2 word of out256_j[k2] = E2S j + k2, k2 = k4 + 16 m3 + 64 m2: an affine base plus immediates */
     const uint32_t wb = (uint32_t)E2S * j + k4;
@@ -438,6 +447,7 @@ static __device__ __forceinline__ void idft2048_unit(uint32_t *lds, int t, bool 
    * before pass A) are waited for now, before this unit's stores: loads and stores share vmcnt, and a
    * later wait for the prefetch would otherwise be a vmcnt(0) that also drains the stores. */
   __builtin_amdgcn_s_waitcnt(0x0F70);   /* vmcnt(0), expcnt / lgkmcnt unconstrained */
+  if constexpr (OAI4G_MOD_PRIO == 2) __builtin_amdgcn_s_setprio(1);
   if (active) {
 #ifndef OAI4G_PASSC_TWONCE
 #define OAI4G_PASSC_TWONCE 1   /* 1: the pass-C companions are built once for both antennas (0: per antenna) */
@@ -463,6 +473,7 @@ static __device__ __forceinline__ void idft2048_unit(uint32_t *lds, int t, bool 
         v[0][jj] = u2c(q.x);
         v[1][jj] = u2c(q.y);
       }
+      if constexpr (OAI4G_MOD_PRIO == 2) __builtin_amdgcn_s_setprio(0);
       s16x2 y[2][2][4];   /* [h][e][m1] */
 #pragma unroll
       for (int h = 0; h < 2; h++) {
@@ -1006,6 +1017,7 @@ __global__ void __launch_bounds__(128) MODOFDM_ATTR k_modofdm(const cfg_dev_t *_
 
     /* this thread's 16 RE codes (thread-major copy, prefetched) */
     const uint32_t rw[8] = {pf.ra.x, pf.ra.y, pf.ra.z, pf.ra.w, pf.rb.x, pf.rb.y, pf.rb.z, pf.rb.w};
+    if constexpr (OAI4G_MOD_PRIO >= 1) __builtin_amdgcn_s_setprio(OAI4G_MOD_PRIO == 3 ? 3 : 2);
 #if OAI4G_MOD_STAGE
     /* stage, per codeword, the QAM-table address of every data RE of this symbol: quad q's 4 Qm
      * bits from its prefetched bytes -> 4 entries (ALAMOUTI: even entries TA rows, odd TB rows) */
