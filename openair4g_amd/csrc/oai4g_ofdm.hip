@@ -353,12 +353,16 @@ static __device__ __forceinline__ void idft2048_unit(uint32_t *lds, int t, bool 
   if (active) {
     prod(x);
 #ifndef OAI4G_MOD_PRIO
-/* 1: the item's staging and RE-lookup phase (LDS round trips, little VALU) runs at wave priority 2, the
- * transform at 0, so the arbiter issues a wave's latency-bound phase ahead of the other waves' VALU
- * streams (-1.5 %, profiles/mod_prio_r06.txt); 2: also the pass-B / pass-C loads at 1; 3: priority 3 */
-#define OAI4G_MOD_PRIO 1
+/* wave priority 2 from the item's start to a point of the transform, 0 after it: the arbiter issues
+ * the latency-bound staging / RE lookups (LDS round trips, little VALU) and the passes that follow
+ * ahead of the other waves' pass-C VALU streams (profiles/mod_prio_r06.txt).  Lowered: 1 after the RE
+ * lookups (-1.2 %), 5 after the radix-16 leaf (-2.5 %), 6 after the pass-B loads, 7 at pass C, 9 after
+ * the first pass-C loads (kept: -4 %), 4 after the staging barrier (slower); 8 = 7 with the leaf and
+ * pass B at 1; 2: 1 + the pass-B / pass-C loads at 1; 3: 1 at priority 3 */
+#define OAI4G_MOD_PRIO 9
 #endif
-    if constexpr (OAI4G_MOD_PRIO >= 1) __builtin_amdgcn_s_setprio(0);
+    if constexpr (OAI4G_MOD_PRIO >= 1 && OAI4G_MOD_PRIO <= 3) __builtin_amdgcn_s_setprio(0);
+    if constexpr (OAI4G_MOD_PRIO == 8) __builtin_amdgcn_s_setprio(1);
     if constexpr (OAI4G_DIAG_MODCUT == 1) {
 #pragma unroll
       for (int a = 0; a < NA; a++) sink(x[a]);
@@ -367,6 +371,7 @@ static __device__ __forceinline__ void idft2048_unit(uint32_t *lds, int t, bool 
     if constexpr (PSYNC)
 #pragma unroll
       for (int a = 0; a < NA; a++) idft16_reg<NA == 2, NS>(x[a], tw.l16);
+    if constexpr (OAI4G_MOD_PRIO == 5) __builtin_amdgcn_s_setprio(0);
     if constexpr (OAI4G_DIAG_MODCUT == 2) {
 #pragma unroll
       for (int a = 0; a < NA; a++) sink(x[a]);
@@ -405,7 +410,7 @@ static __device__ __forceinline__ void idft2048_unit(uint32_t *lds, int t, bool 
         }
   }
   IDFT_SYNC();   /* E2 aliases E1 */
-  if constexpr (OAI4G_MOD_PRIO == 2) __builtin_amdgcn_s_setprio(0);
+  if constexpr (OAI4G_MOD_PRIO == 2 || OAI4G_MOD_PRIO == 6) __builtin_amdgcn_s_setprio(0);
   if (active) {
     /* E2 word of out256_j[k2] = E2S j + k2, k2 = k4 + 16 m3 + 64 m2: an affine base plus immediates */
     const uint32_t wb = (uint32_t)E2S * j + k4;
@@ -448,6 +453,7 @@ static __device__ __forceinline__ void idft2048_unit(uint32_t *lds, int t, bool 
    * later wait for the prefetch would otherwise be a vmcnt(0) that also drains the stores. */
   __builtin_amdgcn_s_waitcnt(0x0F70);   /* vmcnt(0), expcnt / lgkmcnt unconstrained */
   if constexpr (OAI4G_MOD_PRIO == 2) __builtin_amdgcn_s_setprio(1);
+  if constexpr (OAI4G_MOD_PRIO == 7 || OAI4G_MOD_PRIO == 8) __builtin_amdgcn_s_setprio(0);
   if (active) {
 #ifndef OAI4G_PASSC_TWONCE
 #define OAI4G_PASSC_TWONCE 1   /* 1: the pass-C companions are built once for both antennas (0: per antenna) */
@@ -473,7 +479,7 @@ static __device__ __forceinline__ void idft2048_unit(uint32_t *lds, int t, bool 
         v[0][jj] = u2c(q.x);
         v[1][jj] = u2c(q.y);
       }
-      if constexpr (OAI4G_MOD_PRIO == 2) __builtin_amdgcn_s_setprio(0);
+      if constexpr (OAI4G_MOD_PRIO == 2 || OAI4G_MOD_PRIO == 9) __builtin_amdgcn_s_setprio(0);
       s16x2 y[2][2][4];   /* [h][e][m1] */
 #pragma unroll
       for (int h = 0; h < 2; h++) {
@@ -1112,6 +1118,7 @@ __global__ void __launch_bounds__(128) MODOFDM_ATTR k_modofdm(const cfg_dev_t *_
     }
 #endif
     __syncthreads();
+    if constexpr (OAI4G_MOD_PRIO == 4) __builtin_amdgcn_s_setprio(0);
     fetch(base + stride);
 
     gu32_t *crs_tab = (gu32_t *)cc->crs_tab;
