@@ -94,6 +94,21 @@ static __device__ __forceinline__ twp_t tw_use(s16x2 t, uint32_t dep)
   return {t, u2c(tn)};
 }
 
+#ifndef OAI4G_MOD_W0
+#define OAI4G_MOD_W0 1   /* NS leaf: the W^0 products as x - (x > 0) (0: the dot2 form) */
+#endif
+/* x * conj(W^0) with W^0 = (32767, 0), packed like cmulc16: each lane floor(32767 x / 2^15), which is
+ * x - 1 for x > 0 and x for x <= 0 when |x| < 2^15 (NS: no leaf value is -32768).  The lane's x > 0 is
+ * the sign bit of -x; the 32-bit subtraction of the two 0/1 flags cannot borrow across lanes (the low
+ * flag is 1 only where the low lane is >= 1).  One packed op and three fast ones instead of two dot2,
+ * two shifts and a cvt_pk. */
+static __device__ __forceinline__ s16x2 w0mul_ns(s16x2 x)
+{
+  uint32_t n;
+  asm("v_pk_sub_u16 %0, 0, %1" : "=v"(n) : "v"(x));
+  return u2c(c2u(x) - ((n >> 15) & 0x00010001u));
+}
+
 /* leaf IDFT16 in registers (lte_dfts.c:1597-1724); w16 is wave-uniform (scalar loads) */
 template <bool FF = false, bool NS = false>
 static __device__ __forceinline__ void idft16_reg(s16x2 *x, const twp_t *w16 /* W^{0,1,2,3,4,6,9} */)
@@ -104,9 +119,12 @@ static __device__ __forceinline__ void idft16_reg(s16x2 *x, const twp_t *w16 /* 
   for (int j = 0; j < 4; j++) r4inv<FF, NS>(x[j], x[4 + j], x[8 + j], x[12 + j], S[0][j], S[1][j], S[2][j], S[3][j]);
 #pragma unroll
   for (int k = 0; k < 4; k++) {
-    s16x2 b1 = cmulc16u(S[k][1], w16[k1[k]]);
-    s16x2 b2 = cmulc16u(S[k][2], w16[k2[k]]);
-    s16x2 b3 = cmulc16u(S[k][3], w16[k3[k]]);
+    /* NS: row 0 multiplies by W^0 = (32767, 0) (companion (0, 32767)), lane by lane floor(32767 x / 2^15)
+     * = x - (x > 0) for |x| < 2^15 (w0mul_ns) */
+    const bool w0 = NS && OAI4G_MOD_W0 && k == 0;
+    s16x2 b1 = w0 ? w0mul_ns(S[k][1]) : cmulc16u(S[k][1], w16[k1[k]]);
+    s16x2 b2 = w0 ? w0mul_ns(S[k][2]) : cmulc16u(S[k][2], w16[k2[k]]);
+    s16x2 b3 = w0 ? w0mul_ns(S[k][3]) : cmulc16u(S[k][3], w16[k3[k]]);
     r4inv<FF, NS>(S[k][0], b1, b2, b3, x[k], x[4 + k], x[8 + k], x[12 + k]);
   }
 }
@@ -881,7 +899,10 @@ __global__ void __launch_bounds__(128) MODOFDM_ATTR k_modofdm(const cfg_dev_t *_
   const int unit = threadIdx.x / T, t = threadIdx.x % T;
   typename idft_sel<LOG2N>::tw_t twr;
   twr.load(c->tw, t);
-  const uint32_t n_ant = c->n_ant, nsymb = c->nsymb;
+  /* symbols per subframe as a constant (the launch checks cfg nsymb): the item -> (subframe, symbol)
+   * split is a multiply-high, not a run-time division per item */
+  const uint32_t n_ant = c->n_ant;
+  constexpr uint32_t nsymb = ECP ? 12u : 14u;
   constexpr uint32_t sps = ECP ? 6 : 7;
 #if OAI4G_MOD_STAGE
   for (uint32_t i = threadIdx.x; i < 4 * QROW + 1; i += blockDim.x) {
@@ -941,7 +962,9 @@ __global__ void __launch_bounds__(128) MODOFDM_ATTR k_modofdm(const cfg_dev_t *_
   typedef const __attribute__((address_space(4))) cfg_dev_t ccfg_t;
   const ccfg_t *cc = (const ccfg_t *)c;
   auto fetch = [&](int bse) {
-    const int item = bse + unit;
+    /* one unit per workgroup: unit is 0, and the item is a scalar from the start (act, nre and the
+     * staging offsets become scalar too) */
+    const int item = bse + (UNITS == 1 ? 0 : unit);
     const bool act = item < n_items;
     /* one unit per workgroup: the item is wave-uniform, so its table reads become scalar loads and
      * the next item's vector loads need no wait before their use */
@@ -991,7 +1014,7 @@ __global__ void __launch_bounds__(128) MODOFDM_ATTR k_modofdm(const cfg_dev_t *_
   __builtin_amdgcn_s_waitcnt(0x0F70);
 
   for (int base = blockIdx.x * UNITS; base < n_items; base += stride) {
-    const int item = base + unit;
+    const int item = base + (UNITS == 1 ? 0 : unit);
     const bool active = item < n_items;
     const uint32_t it0 = (active ? (uint32_t)item : 0u) / IPS, pair = (uint32_t)item % IPS;
     const uint32_t it = UNITS == 1 ? __builtin_amdgcn_readfirstlane(it0) : it0;
@@ -1471,6 +1494,7 @@ hipError_t oai4g_launch_modofdm(const cfg_dev_t *d_cfg, const cfg_dev_t *h_cfg, 
                                 const uint32_t *d_ebits, int32_t *d_iq, hipStream_t s)
 {
   if (n_sf <= 0) return hipSuccess;
+  if (h_cfg->nsymb != 12 && h_cfg->nsymb != 14) return hipErrorInvalidValue;   /* k_modofdm: 12 <=> ECP */
   const int n_items = n_sf * (int)h_cfg->nsymb;
   d_ebits += (size_t)sf0 * h_cfg->n_cw * h_cfg->ebits_words;
   d_iq += (size_t)sf0 * h_cfg->n_ant * h_cfg->spt;
