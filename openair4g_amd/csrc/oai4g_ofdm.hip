@@ -718,7 +718,7 @@ static __device__ __forceinline__ s16x2 precode(const cfg_dev_t *__restrict__ c,
 }
 
 /* LARGE_CDD on packed lanes: floor((a+b)/2) = (a&b) + ((a^b)>>1), floor((a-b)/2) = ((a^b)>>1) - (~a&b) */
-static __device__ __forceinline__ void cdd_pair(s16x2 x0, s16x2 x1, uint32_t parity, s16x2 &y0, s16x2 &y1)
+[[maybe_unused]] static __device__ __forceinline__ void cdd_pair(s16x2 x0, s16x2 x1, uint32_t parity, s16x2 &y0, s16x2 &y1)
 {
   const uint32_t a = c2u(x0), b = c2u(x1);
   const s16x2 h = u2c(a ^ b) >> (s16x2){1, 1};
