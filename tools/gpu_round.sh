@@ -42,7 +42,7 @@ for step in "$@"; do
                || { tail -20 gpurun_out/prof_${TAG}_$c.log; fail "profile $c"; }
              rm -rf gpurun_out/prof_$c && mv gpurun_out/prof gpurun_out/prof_$c
              tail -8 gpurun_out/prof_${TAG}_$c.log ;;
-    valu) c=${arg:-C3}; b=${BATCH:-$([ "$c" = C5 ] && echo 49152 || echo 8192)}
+    valu) c=${arg:-C3}; b=${BATCH:-$(case $c in C5) echo 49152 ;; C2) echo 2048 ;; C4) echo 1024 ;; *) echo 8192 ;; esac)}
           TAG=$TAG CONFIG=$c NAME=$c BATCH=$b bash tools/gpu_pmc_valu.sh > gpurun_out/valu_${TAG}_$c.log 2>&1 \
             || { tail -20 gpurun_out/valu_${TAG}_$c.log; fail "valu $c"; }
           tail -6 gpurun_out/valu_${TAG}_$c.log ;;

@@ -93,7 +93,7 @@ def main(prof_dir, tag, config, out_dir):
             lines.append(f"| {k} | {len(v)} | {med:.4f} | {sum(v) / len(v):.4f} | {v[0]:.4f} |")
     os.makedirs(out_dir, exist_ok=True)
     open(os.path.join(out_dir, f"rocprof_{tag}_{config}.md"), "w").write("\n".join(lines) + "\n")
-    traffic["batch"] = int(os.environ.get("BATCH", {"C3": 8192, "C4": 1024, "C5": 49152, "FEP": 8192, "UE": 4096}.get(config, 0)))
+    traffic["batch"] = int(os.environ.get("BATCH", {"C3": 8192, "C2": 2048, "C4": 1024, "C5": 49152, "FEP": 8192, "UE": 4096}.get(config, 0)))
     json.dump(traffic, open(os.path.join(out_dir, f"traffic_{config}.json"), "w"), indent=1)
     if prof_ms:
         prof_ms["batch"] = traffic["batch"]
