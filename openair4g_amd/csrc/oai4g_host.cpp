@@ -732,6 +732,8 @@ struct oai4g_tx_config {
   uint32_t *d_gold = nullptr;           /* [10][n_cw][ebits_words] scrambling words */
   std::vector<uint32_t> h_crs;          /* [10][4][200] packed CRS IQ */
   uint32_t *d_ctl = nullptr;            /* static RE values [10][14][2][N] (set_control / set_common) */
+  std::vector<uint32_t> h_ctl;          /* host copy of d_ctl's table (empty when no control REs) */
+  uint32_t *d_stat = nullptr;           /* cfg_dev_t::stat_tm */
   int ctl_vmax = 0;                     /* largest I / Q magnitude in the static-RE table (mod_nosat_ok) */
   std::vector<oai4g_dci_alloc_t> dci;   /* oai4g_tx_config_set_control's DCI set */
   uint8_t n_ue_dci = 0, n_common_dci = 0;
@@ -1157,6 +1159,44 @@ static int derive_cfg(oai4g_tx_config *cfg, const oai4g_tx_params_t *p, const ui
   return rm_fail ? -2 : 0;
 }
 
+/* cfg_dev_t::stat_tm from the RE map, the CRS values and the control table: for kernel antenna `ant`
+ * (TM1: the one transform) the value the modulator's static-RE step used to produce per RE
+ * (pilots.c:43-168: port p's pilot on antenna p, every port's in the single TM1 transform; the
+ * control REs of generate_dci_top on antennas 0 / 1 only), in remap_tm's thread-major order */
+static int build_stat_tm(oai4g_tx_config *cfg)
+{
+  if (cfg->d_stat) hipFree(cfg->d_stat);
+  cfg->d_stat = nullptr;
+  cfg->h.stat_tm = nullptr;
+  cfg->h.stat_planes = 0;
+  if (cfg->h_remap.empty() || (cfg->h_crs.empty() && cfg->h_ctl.empty())) return 0;
+  const size_t N = cfg->h.N, T = N >> 4, nsl = cfg->h_remap.size() / N;
+  const uint32_t planes = cfg->h.mimo_mode == OAI4G_SISO ? 1u : cfg->h.n_ant;
+  std::vector<uint32_t> st(nsl * planes * N, 0u);
+  for (size_t sl = 0; sl < nsl; sl++) {
+    const size_t sf = sl / 14;
+    for (size_t pos = 0; pos < N; pos++) {
+      const uint32_t cd = cfg->h_remap[sl * N + pos];
+      const size_t t = pos % T, k = pos / T;
+      for (uint32_t ant = 0; ant < planes; ant++) {
+        uint32_t v = 0;
+        if (cd != 0xFFFFu && (cd & 0xE000u) == OAI4G_CRS_CODE) {
+          const uint32_t ci = (cd >> 9) & 7u, m = cd & 0xFFu, port = ((cd >> 8) & 1u) | (ci >= 4 ? 2u : 0u);
+          if (!cfg->h_crs.empty() && (planes == 1 || ant == port)) v = cfg->h_crs[(sf * 6 + ci) * 200 + m];
+        } else if ((cd & 0xE000u) == OAI4G_CTL_CODE) {
+          if (!cfg->h_ctl.empty() && ant < 2) v = cfg->h_ctl[(sl * 2 + ant) * N + pos];
+        }
+        st[(sl * planes + ant) * N + t * 16 + k] = v;
+      }
+    }
+  }
+  HCK(hipMalloc(&cfg->d_stat, st.size() * 4), -1);
+  HCK(hipMemcpy(cfg->d_stat, st.data(), st.size() * 4, hipMemcpyHostToDevice), -1);
+  cfg->h.stat_tm = cfg->d_stat;
+  cfg->h.stat_planes = planes;
+  return 0;
+}
+
 static int upload_remap(oai4g_tx_config *cfg)
 {
   if (cfg->d_remap) hipFree(cfg->d_remap);
@@ -1215,6 +1255,7 @@ static int upload_remap(oai4g_tx_config *cfg)
     cfg->h.remap_tm = nullptr;
     cfg->h.remap_tm0 = nullptr;
   }
+  if (build_stat_tm(cfg) != 0) return -1;
   cfg->h.remap = cfg->d_remap;
   return 0;
 }
@@ -1284,7 +1325,9 @@ static void release_cfg(oai4g_tx_config *cfg)
   if (cfg->d_remap) hipFree(cfg->d_remap);
   if (cfg->d_crs) hipFree(cfg->d_crs);
   if (cfg->d_ctl) hipFree(cfg->d_ctl);
+  if (cfg->d_stat) hipFree(cfg->d_stat);
   if (cfg->d_gold) hipFree(cfg->d_gold);
+  cfg->d_stat = nullptr;
   cfg->d_gold = nullptr;
   cfg->d_crs = nullptr;
   cfg->d_ctl = nullptr;
@@ -3026,6 +3069,7 @@ static int rebuild_static(oai4g_tx_config_t *cfg)
   if (cfg->d_ctl) hipFree(cfg->d_ctl);
   cfg->d_ctl = nullptr;
   cfg->h.ctl_tab = nullptr;
+  cfg->h_ctl.clear();
   cfg->ctl_vmax = 0;
   const bool dci_on = (uint32_t)cfg->n_ue_dci + cfg->n_common_dci > 0;
   if (dci_on || cfg->common_on) {
@@ -3143,6 +3187,7 @@ static int rebuild_static(oai4g_tx_config_t *cfg)
     HCK(hipMemcpy(cfg->d_ctl, tab.data(), tab.size() * 4, hipMemcpyHostToDevice), -1);
     cfg->h.ctl_tab = cfg->d_ctl;
     cfg->h.ctl_on = 1;
+    cfg->h_ctl = tab;
     cfg->ctl_vmax = packed_iq_max(tab);
   }
   cfg->h.mod_nosat = mod_nosat_ok(cfg->h, std::max(packed_iq_max(cfg->h_crs), cfg->ctl_vmax));

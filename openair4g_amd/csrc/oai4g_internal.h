@@ -179,6 +179,12 @@ struct cfg_dev_t {
   const uint32_t *gold_x1;      /* [256]     x1 state after 50+16l word steps */
   const uint32_t *gold_x2j;     /* [256][32] columns of M2^(50+16l) */
   const uint32_t *tw;           /* 2 x OAI4G_TW_TOTAL packed twiddles t, then (-t.im, t.re) */
+  const uint32_t *stat_tm;      /* [10][14][stat_planes][N] thread-major like remap_tm: the packed IQ each
+                                   kernel antenna takes at a CRS or control RE, 0 elsewhere (CRS / control
+                                   configurations; k_modofdm ORs it over the data path, which reads the
+                                   zero sentinel there) */
+  uint32_t stat_planes;         /* 1 (TM1: one transform) or the TX antennas */
+  uint32_t pad2;
 };
 
 /* ---------------- launch helpers implemented in the .hip files ---------------- */

@@ -868,6 +868,11 @@ __global__ void __launch_bounds__(128) MODOFDM_ATTR k_modofdm(const cfg_dev_t *_
   constexpr bool CW2 = MODE == 2 || MODE == 3;
   constexpr uint32_t IPS = MODE == 3 ? 2u : 1u;   /* items per (subframe, symbol) */
   __shared__ __attribute__((aligned(16))) uint32_t lds_data[UNITS * NA * LDSW];
+#ifndef OAI4G_MOD_STATTM
+#define OAI4G_MOD_STATTM 1   /* CRS / control kernels (staged builds): the static REs come from cfg stat_tm, ORed
+                                over a data path that reads the zero sentinel there (0: per-RE code tests) */
+#endif
+  constexpr bool STATTM = OAI4G_MOD_STATTM && OAI4G_MOD_STAGE && CRS;
 #if OAI4G_MOD_STAGE
   /* per codeword, the qtab byte address of every data RE's QAM word: entries 4q..4q+3 staged from
    * quad q's 4 Qm bits; entries SENT, SENT + 1 address the zero word that non-data REs read */
@@ -974,7 +979,7 @@ __global__ void __launch_bounds__(128) MODOFDM_ATTR k_modofdm(const cfg_dev_t *_
     const uint32_t sfi = (cc->first_sf + (sf0 + sf) * cc->sf_step) % 10;
     const uint32_t nre_u = cc->symnre[sfi][l], re0 = cc->symbase[sfi][l];   /* uniform: scalar loads */
     const uint32_t nre = act ? nre_u : 0u;
-    const gu128_t *rsrc = (const gu128_t *)((CRS ? cc->remap_tm : cc->remap_tm0) + ((size_t)sfi * 14 + l) * N + (size_t)t * 16);
+    const gu128_t *rsrc = (const gu128_t *)((CRS && !STATTM ? cc->remap_tm : cc->remap_tm0) + ((size_t)sfi * 14 + l) * N + (size_t)t * 16);
     pf.ra = rsrc[0];
     pf.rb = rsrc[1];
 #if OAI4G_MOD_STAGE
@@ -1207,7 +1212,7 @@ __global__ void __launch_bounds__(128) MODOFDM_ATTR k_modofdm(const cfg_dev_t *_
               for (int n = 0; n < GZ; n++) {
                 const int i = act(g + n);
                 code[n] = (rw[i >> 1] >> (16 * (i & 1))) & 0xFFFFu;
-                const uint32_t a = CRS ? min(code[n] & 0x7FF8u, 8u * SENT) : code[n] & 0x7FF8u;
+                const uint32_t a = CRS && !STATTM ? min(code[n] & 0x7FF8u, 8u * SENT) : code[n] & 0x7FF8u;
                 v[n] = *(const u32x2_t *)(pb + a);
               }
 #pragma unroll
@@ -1227,7 +1232,7 @@ __global__ void __launch_bounds__(128) MODOFDM_ATTR k_modofdm(const cfg_dev_t *_
               for (int n = 0; n < GZ; n++) {
                 const int i = act(g + n);
                 const uint32_t code = (rw[i >> 1] >> (16 * (i & 1))) & 0xFFFFu;
-                const uint32_t a = CRS ? min(code & 0x7FFCu, 4u * SENT) : code & 0x7FFCu;
+                const uint32_t a = CRS && !STATTM ? min(code & 0x7FFCu, 4u * SENT) : code & 0x7FFCu;
                 v[n] = *(const uint32_t *)(pb + a);
               }
 #pragma unroll
@@ -1242,7 +1247,7 @@ __global__ void __launch_bounds__(128) MODOFDM_ATTR k_modofdm(const cfg_dev_t *_
               const int i = act(g + n);
               code[n] = (rw[i >> 1] >> (16 * (i & 1))) & 0xFFFFu;
               /* without CRS / control REs every non-data code is already the sentinel (remap_tm0) */
-              const uint32_t a = CRS ? min(code[n] & AM, 2u * SENT) : code[n] & AM;
+              const uint32_t a = CRS && !STATTM ? min(code[n] & AM, 2u * SENT) : code[n] & AM;
               v0[n] = *(const uint16_t *)(sb0 + a);
               if constexpr (MODE == 1) v1[n] = *(const uint16_t *)(sb0 + a + 2);
               if constexpr (CW2) v1[n] = *(const uint16_t *)(sb1 + a);
@@ -1350,7 +1355,27 @@ __global__ void __launch_bounds__(128) MODOFDM_ATTR k_modofdm(const cfg_dev_t *_
             }
           }
 #endif
-          if constexpr (CRS) {
+          if constexpr (CRS && STATTM) {
+            if (crs) {
+              /* CRS / control symbol: the data path read the zero sentinel at every static RE (remap_tm0),
+               * so the antenna's static values (0 at data REs) are ORed over it: 16 consecutive words per
+               * thread and antenna, four 16-byte loads, no per-RE tests */
+#pragma unroll
+              for (int a = 0; a < NA; a++) {
+                const uint32_t ant = NA == 1 ? 0u : (uint32_t)a + 2u * pair;
+                const gu128_t *sp = (const gu128_t *)(cc->stat_tm + ((sfi * 14u + l) * cc->stat_planes + ant) * (uint32_t)N +
+                                                      (uint32_t)t * 16u);
+                u32x4_t w[4];
+#pragma unroll
+                for (int q = 0; q < 4; q++) w[q] = sp[q];
+#pragma unroll
+                for (int n = 0; n < 16; n++) {
+                  if (zb(n)) continue;   /* no CRS or control RE in the guard band */
+                  x[a][n] = u2c(c2u(x[a][n]) | w[n >> 2][n & 3]);
+                }
+              }
+            }
+          } else if constexpr (CRS) {
             if (crs) {
               /* cell-specific RS (pilots.c:43-168): overwrite the antenna carrying port p */
 #pragma unroll
