@@ -873,6 +873,11 @@ __global__ void __launch_bounds__(128) MODOFDM_ATTR k_modofdm(const cfg_dev_t *_
                                 over a data path that reads the zero sentinel there (0: per-RE code tests) */
 #endif
   constexpr bool STATTM = OAI4G_MOD_STATTM && OAI4G_MOD_STAGE && CRS;
+#ifndef OAI4G_MOD_STATEARLY
+#define OAI4G_MOD_STATEARLY 1   /* STATTM: the static words are read before the staging barrier (0: in the prologue) */
+#endif
+  /* not in the two-antenna 2048-point kernels: 32 more live VGPRs there spill (20-100 bytes per lane) */
+  constexpr bool SEARLY = STATTM && OAI4G_MOD_STATEARLY && (NA == 1 || LOG2N < 11);
 #if OAI4G_MOD_STAGE
   /* per codeword, the qtab byte address of every data RE's QAM word: entries 4q..4q+3 staged from
    * quad q's 4 Qm bits; entries SENT, SENT + 1 address the zero word that non-data REs read */
@@ -1145,6 +1150,21 @@ __global__ void __launch_bounds__(128) MODOFDM_ATTR k_modofdm(const cfg_dev_t *_
       }
     }
 #endif
+    /* a CRS / control symbol's static words (STATTM) are read here, ahead of the staging barrier: their L2
+     * round trip overlaps the barrier and the next item's prefetch instead of stalling the prologue */
+    u32x4_t stw[NA][4];
+    if constexpr (SEARLY) {
+      if (stat_sym) {
+#pragma unroll
+        for (int a = 0; a < NA; a++) {
+          const uint32_t ant = NA == 1 ? 0u : (uint32_t)a + 2u * pair;
+          const gu128_t *sp =
+              (const gu128_t *)(cc->stat_tm + ((sfi * 14u + l) * cc->stat_planes + ant) * (uint32_t)N + (uint32_t)t * 16u);
+#pragma unroll
+          for (int q = 0; q < 4; q++) stw[a][q] = sp[q];
+        }
+      }
+    }
     __syncthreads();
     if constexpr (OAI4G_MOD_PRIO == 4) __builtin_amdgcn_s_setprio(0);
     fetch(base + stride);
@@ -1362,12 +1382,17 @@ __global__ void __launch_bounds__(128) MODOFDM_ATTR k_modofdm(const cfg_dev_t *_
                * thread and antenna, four 16-byte loads, no per-RE tests */
 #pragma unroll
               for (int a = 0; a < NA; a++) {
-                const uint32_t ant = NA == 1 ? 0u : (uint32_t)a + 2u * pair;
-                const gu128_t *sp = (const gu128_t *)(cc->stat_tm + ((sfi * 14u + l) * cc->stat_planes + ant) * (uint32_t)N +
-                                                      (uint32_t)t * 16u);
                 u32x4_t w[4];
+                if constexpr (SEARLY) {
 #pragma unroll
-                for (int q = 0; q < 4; q++) w[q] = sp[q];
+                  for (int q = 0; q < 4; q++) w[q] = stw[a][q];
+                } else {
+                  const uint32_t ant = NA == 1 ? 0u : (uint32_t)a + 2u * pair;
+                  const gu128_t *sp = (const gu128_t *)(cc->stat_tm + ((sfi * 14u + l) * cc->stat_planes + ant) * (uint32_t)N +
+                                                        (uint32_t)t * 16u);
+#pragma unroll
+                  for (int q = 0; q < 4; q++) w[q] = sp[q];
+                }
 #pragma unroll
                 for (int n = 0; n < 16; n++) {
                   if (zb(n)) continue;   /* no CRS or control RE in the guard band */
